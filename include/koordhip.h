@@ -1,0 +1,225 @@
+/*
+ * koordhip.h -- C-ABI of libkoordhip.so, the MI355X batched placement engine
+ * for koord-scheduler's Filter/Score hot path (NodeResourcesFit,
+ * LoadAwareScheduling, NodeNUMAResource) plus argmax and the Reserve delta.
+ *
+ * Plain C, no torch / HIP types in any signature: a Go host binds it with cgo
+ * (see INTEGRATION.md), Python with ctypes.  Every function returns 0 on
+ * success and a negative KOORDHIP_E* code on error; the message of the last
+ * error on the calling thread is returned by koordhip_last_error().
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * koordinator tree, "(upstream)" = k8s.io/kubernetes v1.24.15):
+ *   koordhip_create         <- loadaware.New            pkg/scheduler/plugins/loadaware/load_aware.go:76-110
+ *                              nodenumaresource.New     pkg/scheduler/plugins/nodenumaresource/plugin.go:101-151
+ *                              (upstream) noderesources.NewFit + args from config/manager/scheduler-config.yaml:17-46
+ *   koordhip_load_snapshot  <- the per-cycle NodeInfo snapshot + NodeMetric lister reads
+ *                              load_aware.go:133,270-278; (upstream) Snapshot.NodeInfos()
+ *   koordhip_update_nodes   <- informer deltas: podAssignCache.OnAdd/OnUpdate/OnDelete pod_assign_cache.go:82-117,
+ *                              NodeMetric informer (load_aware.go:114-121)
+ *   koordhip_eval           <- Filter  load_aware.go:123-171, (upstream) fit.go Filter/fitsRequest,
+ *                              Score   load_aware.go:269-335, (upstream) resource_allocation.go score,
+ *                              called per (pod,node) by frameworkext/framework_extender.go:192-238
+ *   koordhip_place_stream   <- (upstream) schedule_one.go scheduleOne: findNodesThatFitPod ->
+ *                              prioritizeNodes -> selectHost (tie -> lowest node index) -> Reserve
+ *   koordhip_commit         <- Reserve  load_aware.go:260-263 (podAssignCache.assign, pod_assign_cache.go:53-68),
+ *                              (upstream) cache.AssumePod -> NodeInfo.AddPod
+ *   koordhip_uncommit       <- Unreserve load_aware.go:265-267 (pod_assign_cache.go:70-80)
+ */
+#ifndef KOORDHIP_H
+#define KOORDHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KOORDHIP_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define KOORDHIP_OK 0
+#define KOORDHIP_EINVAL (-1)   /* bad argument / config (validation_pluginargs.go:31-95 analogue) */
+#define KOORDHIP_EDEVICE (-2)  /* HIP runtime error */
+#define KOORDHIP_ESTATE (-3)   /* call out of order (e.g. eval before load_snapshot) */
+#define KOORDHIP_ENOMEM (-4)
+#define KOORDHIP_ECOMM (-5)    /* RCCL error */
+
+/* ---- plugins ------------------------------------------------------------ */
+#define KOORDHIP_PLUGIN_FIT 1u        /* NodeResourcesFit (upstream) */
+#define KOORDHIP_PLUGIN_LOADAWARE 2u  /* LoadAwareScheduling */
+#define KOORDHIP_PLUGIN_NUMA 4u       /* NodeNUMAResource */
+#define KOORDHIP_NPLUGINS 3
+
+/* Fit resource slots (ResourceSpec names in scheduler-config.yaml:21-31). */
+#define KOORDHIP_RES_CPU 0   /* "cpu", milli-CPU */
+#define KOORDHIP_RES_MEM 1   /* "memory", bytes */
+#define KOORDHIP_RES_EPH 2   /* "ephemeral-storage", bytes */
+#define KOORDHIP_RES_BCPU 3  /* "kubernetes.io/batch-cpu", Value() */
+#define KOORDHIP_RES_BMEM 4  /* "kubernetes.io/batch-memory", bytes */
+#define KOORDHIP_NRES 5
+
+/* Per-node LoadAware snapshot flags (koordhip_node_soa.la_flags), resolved by the
+ * marshaller at snapshot time T0 (wall-clock predicates are never re-read). */
+#define KOORDHIP_LA_HAS_METRIC 1u        /* nodeMetricLister.Get found (load_aware.go:133-142,278-286) */
+#define KOORDHIP_LA_FILTER_SKIP 2u       /* FilterExpiredNodeMetrics && expired (load_aware.go:144-147) */
+#define KOORDHIP_LA_SCORE_EXPIRED 4u     /* isNodeMetricExpired(NodeMetricExpirationSeconds) (load_aware.go:287-289) */
+#define KOORDHIP_LA_FILTER_USAGE 8u      /* Status.NodeMetric != nil and the filter's usage source non-nil (load_aware.go:174-211) */
+#define KOORDHIP_LA_PROD_MODE 16u        /* len(ProdUsageThresholds) > 0 (load_aware.go:150) */
+#define KOORDHIP_LA_HAS_PODS_METRIC 32u  /* len(Status.PodsMetric) > 0 (load_aware.go:227-229) */
+#define KOORDHIP_LA_AGGREGATED 64u       /* filter uses aggregated usage (status reason only) */
+
+/* Per-pod flags (koordhip_pod.flags), computed once per pod by the host
+ * (PreFilter analogue). */
+#define KOORDHIP_POD_PROD 1u          /* GetPodPriorityClassWithDefault == koord-prod (priority_utils.go:26-34) */
+#define KOORDHIP_POD_DAEMONSET 2u     /* isDaemonSetPod (helper.go:188-196) */
+#define KOORDHIP_POD_HAS_REQ 4u       /* request not all-zero / scalar map non-empty (upstream fitsRequest) */
+#define KOORDHIP_POD_REQ_BCPU 8u      /* batch-cpu key present in the pod request map */
+#define KOORDHIP_POD_REQ_BMEM 16u     /* batch-memory key present in the pod request map */
+#define KOORDHIP_POD_CPUSET 32u       /* NUMA: requestCPUBind (plugin.go:230-245) */
+#define KOORDHIP_POD_NUMA_SKIP 64u    /* NUMA: PreFilter skip (zero request) (plugin.go:218-226) */
+
+/* Per-(pod,node) status bits written by koordhip_eval (no short-circuit, one
+ * bit per plugin that returned non-Success from Filter). */
+#define KOORDHIP_ST_FIT_FAIL 1u
+#define KOORDHIP_ST_LA_FAIL 2u
+#define KOORDHIP_ST_NUMA_FAIL 4u
+
+/* place_stream out_node values */
+#define KOORDHIP_UNSCHEDULABLE (-1)
+#define KOORDHIP_RESERVE_FAILED (-2)
+
+typedef struct koordhip_ctx koordhip_ctx;
+
+/* Plugin arguments (pkg/scheduler/apis/config/types.go:29-108, defaults
+ * v1beta2/defaults.go:32-121, weights scheduler-config.yaml:82-91). */
+typedef struct koordhip_config {
+  int32_t abi_version;      /* must be KOORDHIP_ABI_VERSION */
+  uint32_t filter_plugins;  /* KOORDHIP_PLUGIN_* bits enabled at Filter */
+  uint32_t score_plugins;   /* KOORDHIP_PLUGIN_* bits enabled at Score */
+  int32_t device;           /* HIP device ordinal; -1 = current device */
+  int64_t plugin_weight[KOORDHIP_NPLUGINS]; /* score weight: Fit, LoadAware, NUMA (1..100) */
+  int64_t fit_weight[KOORDHIP_NRES];        /* NodeResourcesFitArgs LeastAllocated weights, 0 = resource not listed */
+  int64_t la_weight_cpu;                    /* LoadAwareSchedulingArgs.ResourceWeights[cpu] (1..100) */
+  int64_t la_weight_mem;                    /* LoadAwareSchedulingArgs.ResourceWeights[memory] (1..100) */
+  int32_t la_score_according_prod_usage;    /* LoadAwareSchedulingArgs.ScoreAccordingProdUsage */
+  int32_t batch_pods;       /* pods per speculative round of place_stream (0 = default 32; max 64) */
+  int32_t numa_weight_cpu;  /* NodeNUMAResourceArgs.ScoringStrategy LeastAllocated weights */
+  int32_t numa_weight_mem;
+  int32_t profile_kernels;  /* 1 = time every stream eval launch with HIP events (koordhip_last_stats) */
+  int32_t reserved[7];
+} koordhip_config;
+
+/* Columnar node snapshot, all arrays of length n, little-endian, caller-owned
+ * and copied by koordhip_load_snapshot.  Units: CPU in milli-cores, memory /
+ * ephemeral storage in bytes, batch-cpu as Quantity.Value().  Mutable columns
+ * (requested / nz / npods / la_used*) are advanced on device by commits. */
+typedef struct koordhip_node_soa {
+  /* NodeResourcesFit: NodeInfo.Allocatable (upstream framework/types.go) */
+  const int64_t *alloc[KOORDHIP_NRES];
+  const int32_t *alloc_pods;               /* Allocatable.AllowedPodNumber */
+  /* NodeResourcesFit: NodeInfo.Requested, .NonZeroRequested, len(.Pods) */
+  const int64_t *requested[KOORDHIP_NRES];
+  const int64_t *nz_cpu_m;
+  const int64_t *nz_mem;
+  const int32_t *npods;
+  /* LoadAwareScheduling Score (load_aware.go:269-335) */
+  const int64_t *la_alloc_cpu_m;           /* EstimateNode(node)[cpu].MilliValue() (default_estimator.go:110-129) */
+  const int64_t *la_alloc_mem;             /* EstimateNode(node)[memory].Value() */
+  const int64_t *la_used_cpu_m;            /* assigned-pod estimates + nodeUsage (cond. minus estimated pods' actual) */
+  const int64_t *la_used_mem;
+  const int64_t *la_used_prod_cpu_m;       /* prod-pod variant (ScoreAccordingProdUsage); may be NULL otherwise */
+  const int64_t *la_used_prod_mem;
+  /* LoadAwareScheduling Filter inputs (load_aware.go:173-254), milli values */
+  const int64_t *laf_used_m[2];            /* nodeUsage (or target aggregated usage) cpu, memory: MilliValue() */
+  const int64_t *laf_total_m[2];           /* EstimateNode allocatable cpu, memory: MilliValue() */
+  const int64_t *laf_prod_used_m[2];       /* sum of prod pods' usage (buildPodMetricMap+sumPodUsages) */
+  const int64_t *laf_thr[2];               /* resolved usage thresholds cpu, memory (0 = disabled) */
+  const int64_t *laf_prod_thr[2];          /* resolved prod usage thresholds (0 = disabled) */
+  const uint8_t *la_flags;                 /* KOORDHIP_LA_* */
+} koordhip_node_soa;
+
+/* One pod of the stream, the host-side PreFilter product (96 bytes). */
+typedef struct koordhip_pod {
+  int64_t req[KOORDHIP_NRES]; /* computePodResourceRequest (upstream fit.go): max(sum containers, init) + overhead */
+  int64_t nz_cpu_m;           /* non-zero request: GetNonzeroRequests defaults 100m / 200Mi (upstream) */
+  int64_t nz_mem;
+  int64_t est_cpu;            /* EstimatePod(pod)[cpu]    (default_estimator.go:57-108) */
+  int64_t est_mem;            /* EstimatePod(pod)[memory] */
+  uint32_t flags;             /* KOORDHIP_POD_* */
+  int32_t numa_cpus;          /* NUMA numCPUsNeeded (plugin.go:247) */
+  int64_t reserved[2];
+} koordhip_pod;
+
+/* One top-k record of koordhip_eval. */
+typedef struct koordhip_topk {
+  int32_t node;   /* node index, -1 = none */
+  int32_t score;  /* total weighted score */
+} koordhip_topk;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+const char *koordhip_last_error(void);
+int koordhip_abi_version(void);
+int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out);
+int koordhip_destroy(koordhip_ctx *ctx);
+
+/* Copy a full snapshot of n nodes to device (replaces any previous one) and
+ * run the on-device LoadAware threshold-mask kernel. */
+int koordhip_load_snapshot(koordhip_ctx *ctx, const koordhip_node_soa *soa, int32_t n);
+
+/* Replace rows idx[0..m) with rows 0..m of `rows` (informer deltas) and
+ * recompute their masks. */
+int koordhip_update_nodes(koordhip_ctx *ctx, const int32_t *idx, const koordhip_node_soa *rows, int32_t m);
+
+/* Copy the current (committed) mutable columns back to host arrays; any
+ * pointer may be NULL.  Used by tests and the Go shim's debug service. */
+int koordhip_read_nodes(koordhip_ctx *ctx, int64_t *requested /* [NRES][n] */, int64_t *nz /* [2][n] */,
+                        int32_t *npods, int64_t *la_used /* [2][n] */, int64_t *la_used_prod /* [2][n] */);
+
+/* Parity/debug mode, no commit: for n_pods pods against the current state.
+ *   status : optional, [n_pods][n] KOORDHIP_ST_* bits (every plugin evaluated)
+ *   scores : optional, [n_pods][KOORDHIP_NPLUGINS][n] per-plugin scores (0 where the plugin is disabled)
+ *   topk   : optional, [n_pods][k] best feasible nodes by (total desc, index asc), node = -1 past the end */
+int koordhip_eval(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, uint8_t *status, int32_t *scores,
+                  koordhip_topk *topk, int32_t k);
+
+/* Greedy stream: pods attempted once, in order, each against the state left
+ * by all earlier commits; winner = lowest-index max total score; the Reserve
+ * delta is applied on device.  out_node[i] = node, -1 unschedulable. */
+int koordhip_place_stream(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, int32_t *out_node);
+
+/* The same split in two so a caller can time the device part alone: stage
+ * (host -> HBM copy) then place (HBM-resident pods, result kept on device
+ * until koordhip_fetch_placements). */
+int koordhip_stage_pods(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods);
+int koordhip_place_staged(koordhip_ctx *ctx);
+int koordhip_fetch_placements(koordhip_ctx *ctx, int32_t *out_node, int32_t n_pods);
+int koordhip_synchronize(koordhip_ctx *ctx);
+
+/* Device-side checkpoint of the mutable columns (requested / nz / npods /
+ * la_used* / flags) and its restore: rolls a whole speculative cycle back
+ * (bulk Unreserve) without re-uploading the snapshot. */
+int koordhip_checkpoint(koordhip_ctx *ctx);
+int koordhip_restore(koordhip_ctx *ctx);
+
+/* Reserve / Unreserve of one pod on one node (state delta only). */
+int koordhip_commit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node);
+int koordhip_uncommit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node);
+
+/* Device-time of the last place call's eval kernels, split for roofline
+ * accounting: total ms of eval kernels, launches, evals processed. */
+int koordhip_last_stats(koordhip_ctx *ctx, double *eval_ms, int64_t *eval_launches, int64_t *evals,
+                        double *total_ms);
+
+/* ---- multi-GPU (node-index sharding, RCCL all-gather of per-shard top-k) -- */
+#define KOORDHIP_UNIQUE_ID_BYTES 128
+int koordhip_comm_unique_id(uint8_t *id_out /* KOORDHIP_UNIQUE_ID_BYTES */);
+/* Attach an RCCL communicator: this context then evaluates only node shard
+ * [rank*n/world, (rank+1)*n/world) and merges per-shard top-k over xGMI. */
+int koordhip_comm_init(koordhip_ctx *ctx, const uint8_t *id, int32_t world, int32_t rank);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KOORDHIP_H */

@@ -1,0 +1,170 @@
+"""ctypes mirror of include/koordhip.h and the loader for libkoordhip.so.
+
+The library is built in-tree by __graft_entry__.build() into
+koordinator_amd/lib/libkoordhip.so.  There is no fallback: if the library is
+missing, importing the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+KOORDHIP_ABI_VERSION = 1
+NRES = 5
+NPLUGINS = 3
+
+PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA = 1, 2, 4
+PLUGIN_BITS = {"NodeResourcesFit": PLUGIN_FIT, "LoadAwareScheduling": PLUGIN_LOADAWARE,
+               "NodeNUMAResource": PLUGIN_NUMA}
+RES_CPU, RES_MEM, RES_EPH, RES_BCPU, RES_BMEM = range(5)
+
+LA_HAS_METRIC, LA_FILTER_SKIP, LA_SCORE_EXPIRED, LA_FILTER_USAGE = 1, 2, 4, 8
+LA_PROD_MODE, LA_HAS_PODS_METRIC, LA_AGGREGATED = 16, 32, 64
+
+POD_PROD, POD_DAEMONSET, POD_HAS_REQ, POD_REQ_BCPU, POD_REQ_BMEM = 1, 2, 4, 8, 16
+POD_CPUSET, POD_NUMA_SKIP = 32, 64
+
+ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL = 1, 2, 4
+UNSCHEDULABLE, RESERVE_FAILED = -1, -2
+UNIQUE_ID_BYTES = 128
+
+_i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class KoordhipConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32),
+        ("filter_plugins", C.c_uint32),
+        ("score_plugins", C.c_uint32),
+        ("device", C.c_int32),
+        ("plugin_weight", C.c_int64 * NPLUGINS),
+        ("fit_weight", C.c_int64 * NRES),
+        ("la_weight_cpu", C.c_int64),
+        ("la_weight_mem", C.c_int64),
+        ("la_score_according_prod_usage", C.c_int32),
+        ("batch_pods", C.c_int32),
+        ("numa_weight_cpu", C.c_int32),
+        ("numa_weight_mem", C.c_int32),
+        ("profile_kernels", C.c_int32),
+        ("reserved", C.c_int32 * 7),
+    ]
+
+
+class KoordhipNodeSoa(C.Structure):
+    _fields_ = [
+        ("alloc", _i64p * NRES),
+        ("alloc_pods", _i32p),
+        ("requested", _i64p * NRES),
+        ("nz_cpu_m", _i64p),
+        ("nz_mem", _i64p),
+        ("npods", _i32p),
+        ("la_alloc_cpu_m", _i64p),
+        ("la_alloc_mem", _i64p),
+        ("la_used_cpu_m", _i64p),
+        ("la_used_mem", _i64p),
+        ("la_used_prod_cpu_m", _i64p),
+        ("la_used_prod_mem", _i64p),
+        ("laf_used_m", _i64p * 2),
+        ("laf_total_m", _i64p * 2),
+        ("laf_prod_used_m", _i64p * 2),
+        ("laf_thr", _i64p * 2),
+        ("laf_prod_thr", _i64p * 2),
+        ("la_flags", _u8p),
+    ]
+
+
+class KoordhipTopk(C.Structure):
+    _fields_ = [("node", C.c_int32), ("score", C.c_int32)]
+
+
+# numpy twin of koordhip_pod (96 bytes)
+POD_DTYPE = np.dtype([
+    ("req", "<i8", (NRES,)),
+    ("nz_cpu_m", "<i8"),
+    ("nz_mem", "<i8"),
+    ("est_cpu", "<i8"),
+    ("est_mem", "<i8"),
+    ("flags", "<u4"),
+    ("numa_cpus", "<i4"),
+    ("reserved", "<i8", (2,)),
+], align=True)
+assert POD_DTYPE.itemsize == 96
+TOPK_DTYPE = np.dtype([("node", "<i4"), ("score", "<i4")])
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkoordhip.so")
+
+
+class KoordhipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"koordhip error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libkoordhip.so.  Fails loudly when it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                           " (there is no CPU fallback)")
+    lib = C.CDLL(path)
+    vp = C.c_void_p
+    sig = {
+        "koordhip_last_error": (C.c_char_p, []),
+        "koordhip_abi_version": (C.c_int, []),
+        "koordhip_create": (C.c_int, [C.POINTER(KoordhipConfig), C.POINTER(vp)]),
+        "koordhip_destroy": (C.c_int, [vp]),
+        "koordhip_load_snapshot": (C.c_int, [vp, C.POINTER(KoordhipNodeSoa), C.c_int32]),
+        "koordhip_update_nodes": (C.c_int, [vp, _i32p, C.POINTER(KoordhipNodeSoa), C.c_int32]),
+        "koordhip_read_nodes": (C.c_int, [vp, _i64p, _i64p, _i32p, _i64p, _i64p]),
+        "koordhip_eval": (C.c_int, [vp, vp, C.c_int32, _u8p, _i32p, vp, C.c_int32]),
+        "koordhip_place_stream": (C.c_int, [vp, vp, C.c_int32, _i32p]),
+        "koordhip_stage_pods": (C.c_int, [vp, vp, C.c_int32]),
+        "koordhip_place_staged": (C.c_int, [vp]),
+        "koordhip_fetch_placements": (C.c_int, [vp, _i32p, C.c_int32]),
+        "koordhip_synchronize": (C.c_int, [vp]),
+        "koordhip_checkpoint": (C.c_int, [vp]),
+        "koordhip_restore": (C.c_int, [vp]),
+        "koordhip_commit": (C.c_int, [vp, vp, C.c_int32]),
+        "koordhip_uncommit": (C.c_int, [vp, vp, C.c_int32]),
+        "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                          C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+        "koordhip_comm_unique_id": (C.c_int, [C.c_char_p]),
+        "koordhip_comm_init": (C.c_int, [vp, C.c_char_p, C.c_int32, C.c_int32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.koordhip_abi_version() != KOORDHIP_ABI_VERSION:
+        raise RuntimeError("libkoordhip.so ABI version mismatch; rebuild")
+    _lib = lib
+    return lib
+
+
+EXPORTED_SYMBOLS = [
+    "koordhip_last_error", "koordhip_abi_version", "koordhip_create", "koordhip_destroy",
+    "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
+    "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
+    "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit", "koordhip_last_stats",
+    "koordhip_comm_unique_id", "koordhip_comm_init",
+]
+
+
+def check(lib, rc: int):
+    if rc != 0:
+        raise KoordhipError(rc, (lib.koordhip_last_error() or b"").decode())
+    return rc
+
+
+def ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype)) if a is not None else None

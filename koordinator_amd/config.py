@@ -1,0 +1,175 @@
+"""Plugin arguments for the three hot-path plugins, with the reference's
+defaults and validation, and their lowering to the C-ABI koordhip_config.
+
+  LoadAwareSchedulingArgs  pkg/scheduler/apis/config/types.go:29-74
+                           defaults v1beta2/defaults.go:32-96
+                           validation validation/validation_pluginargs.go:31-95
+  NodeNUMAResourceArgs     types.go:102-108, defaults v1beta2/defaults.go:98-121
+  NodeResourcesFitArgs     (upstream) + config/manager/scheduler-config.yaml:17-31
+  plugin score weights     config/manager/scheduler-config.yaml:82-91
+"""
+from __future__ import annotations
+
+import copy
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+from . import k8s
+
+FIT_RESOURCES = [k8s.CPU, k8s.MEMORY, k8s.EPHEMERAL, k8s.BATCH_CPU, k8s.BATCH_MEMORY]
+
+PLUGIN_FIT = "NodeResourcesFit"
+PLUGIN_LOADAWARE = "LoadAwareScheduling"
+PLUGIN_NUMA = "NodeNUMAResource"
+
+
+class ArgsError(ValueError):
+    """field.ErrorList.ToAggregate() analogue."""
+
+
+@dataclass
+class LoadAwareSchedulingAggregatedArgs:
+    usage_thresholds: Dict[str, int] = field(default_factory=dict)
+    usage_aggregation_type: str = ""
+    usage_aggregated_duration_s: float = 0.0
+    score_aggregation_type: str = ""
+    score_aggregated_duration_s: float = 0.0
+
+
+@dataclass
+class LoadAwareSchedulingArgs:
+    filter_expired_node_metrics: Optional[bool] = None
+    node_metric_expiration_seconds: Optional[int] = None
+    resource_weights: Dict[str, int] = field(default_factory=dict)
+    usage_thresholds: Dict[str, int] = field(default_factory=dict)
+    prod_usage_thresholds: Dict[str, int] = field(default_factory=dict)
+    score_according_prod_usage: bool = False
+    estimated_scaling_factors: Optional[Dict[str, int]] = None
+    aggregated: Optional[LoadAwareSchedulingAggregatedArgs] = None
+
+    def with_defaults(self) -> "LoadAwareSchedulingArgs":
+        """SetDefaults_LoadAwareSchedulingArgs, v1beta2/defaults.go:75-96."""
+        a = copy.deepcopy(self)
+        if a.filter_expired_node_metrics is None:
+            a.filter_expired_node_metrics = True
+        if a.node_metric_expiration_seconds is None:
+            a.node_metric_expiration_seconds = 180
+        if not a.resource_weights:
+            a.resource_weights = {k8s.CPU: 1, k8s.MEMORY: 1}
+        if not a.usage_thresholds:
+            a.usage_thresholds = {k8s.CPU: 65, k8s.MEMORY: 95}
+        if a.estimated_scaling_factors is None:
+            a.estimated_scaling_factors = {k8s.CPU: 85, k8s.MEMORY: 70}
+        else:
+            for k, v in {k8s.CPU: 85, k8s.MEMORY: 70}.items():
+                a.estimated_scaling_factors.setdefault(k, v)
+        return a
+
+    def validate(self):
+        """ValidateLoadAwareSchedulingArgs, validation_pluginargs.go:31-95."""
+        errs = []
+        if self.node_metric_expiration_seconds is not None and self.node_metric_expiration_seconds <= 0:
+            errs.append("nodeMetricExpiredSeconds should be a positive value")
+        for r, w in self.resource_weights.items():
+            if w <= 0 or w > 100:
+                errs.append(f"resourceWeights: resource Weight of {r} out of range, got {w}")
+                break
+        for r, t in self.usage_thresholds.items():
+            if t < 0 or t > 100:
+                errs.append(f"usageThresholds: resource Threshold of {r} out of range, got {t}")
+                break
+        for r, f in (self.estimated_scaling_factors or {}).items():
+            if f <= 0 or f > 100:
+                errs.append(f"estimatedScalingFactors: estimated resource Threshold of {r} out of range, got {f}")
+                break
+        for r in self.resource_weights:
+            if r not in (self.estimated_scaling_factors or {}):
+                errs.append(f"estimatedScalingFactors: Not found: {r!r}")
+                break
+        # Engine restriction (documented in DESIGN.md): weighted resources are cpu/memory.
+        for r in self.resource_weights:
+            if r not in (k8s.CPU, k8s.MEMORY):
+                errs.append(f"resourceWeights: {r!r} is not supported by the engine (cpu, memory only)")
+        if errs:
+            raise ArgsError("; ".join(errs))
+
+
+@dataclass
+class NodeResourcesFitArgs:
+    """LeastAllocated scoring strategy only (the shipped profile)."""
+    scoring_type: str = "LeastAllocated"
+    resources: Dict[str, int] = field(default_factory=lambda: {k8s.CPU: 1, k8s.MEMORY: 1})
+
+    def validate(self):
+        if self.scoring_type != "LeastAllocated":
+            raise ArgsError(f"scoringStrategy.type {self.scoring_type!r} not supported (LeastAllocated)")
+        for r, w in self.resources.items():
+            if r not in FIT_RESOURCES:
+                raise ArgsError(f"scoringStrategy.resources: {r!r} not supported by the engine")
+            if w < 1 or w > 100:
+                raise ArgsError(f"scoringStrategy.resources: weight of {r} out of range, got {w}")
+
+
+@dataclass
+class NodeNUMAResourceArgs:
+    default_cpu_bind_policy: str = "FullPCPUs"
+    scoring_type: str = "LeastAllocated"
+    resources: Dict[str, int] = field(default_factory=lambda: {k8s.CPU: 1, k8s.MEMORY: 1})
+
+
+@dataclass
+class Profile:
+    """The scheduling profile restricted to the hot-path plugins."""
+    filters: tuple = (PLUGIN_FIT, PLUGIN_LOADAWARE)
+    scores: Dict[str, int] = field(default_factory=lambda: {PLUGIN_FIT: 1, PLUGIN_LOADAWARE: 1})
+    fit: NodeResourcesFitArgs = field(default_factory=NodeResourcesFitArgs)
+    loadaware: LoadAwareSchedulingArgs = field(default_factory=LoadAwareSchedulingArgs)
+    numa: NodeNUMAResourceArgs = field(default_factory=NodeNUMAResourceArgs)
+    batch_pods: int = 0
+
+    def resolved(self) -> "Profile":
+        p = copy.deepcopy(self)
+        p.loadaware = p.loadaware.with_defaults()
+        return p
+
+
+def shipped_profile() -> Profile:
+    """config/manager/scheduler-config.yaml:17-46,82-91 restricted to Fit + LoadAware."""
+    la = LoadAwareSchedulingArgs(
+        filter_expired_node_metrics=False,
+        node_metric_expiration_seconds=300,
+        resource_weights={k8s.CPU: 1, k8s.MEMORY: 1},
+        usage_thresholds={k8s.CPU: 65, k8s.MEMORY: 95},
+        estimated_scaling_factors={k8s.CPU: 85, k8s.MEMORY: 70},
+    )
+    fit = NodeResourcesFitArgs(resources={k8s.CPU: 1, k8s.MEMORY: 1, k8s.BATCH_CPU: 1, k8s.BATCH_MEMORY: 1})
+    return Profile(fit=fit, loadaware=la)
+
+
+def to_c_config(profile: Profile, device: int = -1):
+    """Lower a resolved profile to the koordhip_config ctypes struct."""
+    from .abi import (KOORDHIP_ABI_VERSION, PLUGIN_BITS, KoordhipConfig)
+
+    p = profile.resolved()
+    p.loadaware.validate()
+    p.fit.validate()
+    cfg = KoordhipConfig()
+    cfg.abi_version = KOORDHIP_ABI_VERSION
+    cfg.filter_plugins = sum(PLUGIN_BITS[x] for x in set(p.filters))
+    cfg.score_plugins = sum(PLUGIN_BITS[x] for x in p.scores)
+    cfg.device = device
+    order = [PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA]
+    for i, name in enumerate(order):
+        w = p.scores.get(name, 0)
+        if name in p.scores and not (1 <= w <= 100):
+            raise ArgsError(f"score weight of {name} out of range, got {w}")
+        cfg.plugin_weight[i] = w
+    for i, r in enumerate(FIT_RESOURCES):
+        cfg.fit_weight[i] = p.fit.resources.get(r, 0)
+    cfg.la_weight_cpu = p.loadaware.resource_weights.get(k8s.CPU, 0)
+    cfg.la_weight_mem = p.loadaware.resource_weights.get(k8s.MEMORY, 0)
+    cfg.la_score_according_prod_usage = 1 if p.loadaware.score_according_prod_usage else 0
+    cfg.batch_pods = p.batch_pods
+    cfg.numa_weight_cpu = p.numa.resources.get(k8s.CPU, 0)
+    cfg.numa_weight_mem = p.numa.resources.get(k8s.MEMORY, 0)
+    return cfg

@@ -1,0 +1,684 @@
+// api.hip -- the C-ABI of libkoordhip.so (include/koordhip.h): context,
+// HBM-resident columnar snapshot, the round loop of the greedy stream and the
+// RCCL all-gather of per-shard top-k for node-sharded multi-GPU runs.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/koordhip.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return fail(KOORDHIP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                        \
+  do {                                                                                        \
+    ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess) return fail(KOORDHIP_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+constexpr int kDefaultBatch = 32;
+constexpr int kMaxBatch = 64;
+
+}  // namespace
+
+struct koordhip_ctx {
+  koordhip_config cfg{};
+  kh::DevCfg dc{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int32_t n = 0;
+  bool loaded = false;
+  int32_t batch = kDefaultBatch;
+  int32_t monotone = 1;
+
+  std::vector<void *> cols;  // every device column allocation
+  kh::DevNodes d{};
+  kh::PrepIn prep{};
+
+  // stream buffers
+  koordhip_pod *d_pods = nullptr;
+  int32_t pods_cap = 0, n_staged = 0;
+  int32_t *d_out = nullptr;
+  int32_t out_cap = 0;
+  uint64_t *d_partial = nullptr;
+  size_t partial_cap = 0;
+  uint64_t *d_lists = nullptr;   // [batch][k]
+  uint64_t *d_gather = nullptr;  // [world][batch][k]
+  uint64_t *d_final = nullptr;   // [batch][k]
+  koordhip_pod *d_tmp_pod = nullptr;
+
+  // checkpoint of the mutable columns
+  std::vector<void *> ckpt;
+
+  // sharding
+  ncclComm_t comm = nullptr;
+  int32_t world = 1, rank = 0;
+
+  // stats
+  std::vector<hipEvent_t> ev;  // pairs around eval launches (profile_kernels)
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  int32_t ev_used = 0;
+  double last_eval_ms = 0, last_total_ms = 0;
+  int64_t last_launches = 0, last_evals = 0;
+};
+
+namespace {
+
+template <typename T>
+int dev_alloc(koordhip_ctx *c, T **p, size_t count) {
+  void *q = nullptr;
+  HIP_TRY(hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)));
+  c->cols.push_back(q);
+  *p = static_cast<T *>(q);
+  return 0;
+}
+
+void free_cols(koordhip_ctx *c) {
+  for (void *p : c->cols) (void)hipFree(p);
+  c->cols.clear();
+  c->d = kh::DevNodes{};
+  c->prep = kh::PrepIn{};
+  c->loaded = false;
+  c->n = 0;
+}
+
+template <typename T>
+int upload(koordhip_ctx *c, T *dst, const T *src, size_t count) {
+  if (count == 0) return 0;
+  if (src) {
+    HIP_TRY(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  } else {
+    HIP_TRY(hipMemsetAsync(dst, 0, count * sizeof(T), c->stream));
+  }
+  return 0;
+}
+
+int validate_soa(const koordhip_node_soa *s) {
+  if (!s) return fail(KOORDHIP_EINVAL, "soa is NULL");
+  for (int r = 0; r < KOORDHIP_NRES; r++)
+    if (!s->alloc[r] || !s->requested[r]) return fail(KOORDHIP_EINVAL, "alloc/requested column missing");
+  if (!s->alloc_pods || !s->npods || !s->nz_cpu_m || !s->nz_mem || !s->la_alloc_cpu_m || !s->la_alloc_mem ||
+      !s->la_used_cpu_m || !s->la_used_mem || !s->la_flags)
+    return fail(KOORDHIP_EINVAL, "required column missing");
+  for (int r = 0; r < 2; r++)
+    if (!s->laf_used_m[r] || !s->laf_total_m[r] || !s->laf_prod_used_m[r] || !s->laf_thr[r] || !s->laf_prod_thr[r])
+      return fail(KOORDHIP_EINVAL, "LoadAware filter column missing");
+  return 0;
+}
+
+int ensure(koordhip_ctx *c, void **p, size_t *cap, size_t bytes) {
+  if (*cap >= bytes && *p) return 0;
+  if (*p) HIP_TRY(hipFree(*p));
+  *p = nullptr;
+  HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 64)));
+  *cap = bytes;
+  return 0;
+}
+
+// Work decomposition of one eval launch over node range [lo, hi):
+// chunks of `chunk` nodes (a multiple of 64); enough waves to fill 256 CUs.
+void chunking(int32_t lo, int32_t hi, int32_t pods, int32_t *chunk, int32_t *nchunks) {
+  const int64_t span = std::max<int64_t>(hi - lo, 1);
+  const int64_t target_waves = 256 * 4 * 6;  // ~6 waves per SIMD
+  int64_t nc = std::max<int64_t>(1, target_waves / std::max(pods, 1));
+  int64_t ch = (span + nc - 1) / nc;
+  ch = std::max<int64_t>(256, ((ch + 63) / 64) * 64);
+  *chunk = (int32_t)ch;
+  *nchunks = (int32_t)((span + ch - 1) / ch);
+}
+
+int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
+               uint64_t *out, bool timed) {
+  int32_t chunk, nchunks;
+  chunking(lo, hi, np, &chunk, &nchunks);
+  size_t need = (size_t)np * nchunks * k * sizeof(uint64_t);
+  if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial), &c->partial_cap, need)) return e;
+  hipEvent_t *e0 = nullptr, *e1 = nullptr;
+  if (timed && c->cfg.profile_kernels) {
+    if (c->ev_used + 2 > (int32_t)c->ev.size()) {
+      for (int i = 0; i < 1024; i++) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->ev.push_back(e);
+      }
+    }
+    e0 = &c->ev[c->ev_used];
+    e1 = &c->ev[c->ev_used + 1];
+    c->ev_used += 2;
+    HIP_TRY(hipEventRecord(*e0, c->stream));
+  }
+  HIP_TRY(kh::launch_topk_partial(c->dc, c->d, d_pods, np, lo, hi, chunk, nchunks, k, c->d_partial, c->stream));
+  if (e1) HIP_TRY(hipEventRecord(*e1, c->stream));
+  c->last_launches++;
+  c->last_evals += (int64_t)np * (hi - lo);
+  HIP_TRY(kh::launch_topk_merge(c->d_partial, (int64_t)nchunks * k, k, np, nchunks, k, out, c->stream));
+  return 0;
+}
+
+void shard(const koordhip_ctx *c, int32_t *lo, int32_t *hi) {
+  *lo = (int32_t)((int64_t)c->n * c->rank / c->world);
+  *hi = (int32_t)((int64_t)c->n * (c->rank + 1) / c->world);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *koordhip_last_error(void) { return g_err.c_str(); }
+int koordhip_abi_version(void) { return KOORDHIP_ABI_VERSION; }
+
+int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
+  if (!cfg || !out) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (cfg->abi_version != KOORDHIP_ABI_VERSION) return fail(KOORDHIP_EINVAL, "abi_version mismatch");
+  const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE;
+  if ((cfg->filter_plugins | cfg->score_plugins) & ~known)
+    return fail(KOORDHIP_EINVAL, "unsupported plugin bit (NodeNUMAResource is not built into this library version)");
+  for (int p = 0; p < 2; p++) {
+    const uint32_t bit = 1u << p;
+    if ((cfg->score_plugins & bit) && (cfg->plugin_weight[p] < 1 || cfg->plugin_weight[p] > 100))
+      return fail(KOORDHIP_EINVAL, "plugin score weight must be in [1, 100]");
+  }
+  for (int r = 0; r < KOORDHIP_NRES; r++)
+    if (cfg->fit_weight[r] < 0 || cfg->fit_weight[r] > 100) return fail(KOORDHIP_EINVAL, "fit weight out of range");
+  if (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) {
+    if (cfg->la_weight_cpu < 0 || cfg->la_weight_cpu > 100 || cfg->la_weight_mem < 0 || cfg->la_weight_mem > 100 ||
+        cfg->la_weight_cpu + cfg->la_weight_mem == 0)
+      return fail(KOORDHIP_EINVAL, "LoadAware resource weights must be in [1, 100]");
+  }
+  if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return fail(KOORDHIP_EINVAL, "batch_pods must be in [0, 64]");
+  auto *c = new koordhip_ctx();
+  c->cfg = *cfg;
+  c->batch = cfg->batch_pods ? cfg->batch_pods : kDefaultBatch;
+  c->dc.filt = cfg->filter_plugins;
+  c->dc.score = cfg->score_plugins;
+  c->dc.w_fit = (int32_t)cfg->plugin_weight[0];
+  c->dc.w_la = (int32_t)cfg->plugin_weight[1];
+  c->dc.w_numa = (int32_t)cfg->plugin_weight[2];
+  for (int r = 0; r < KOORDHIP_NRES; r++) c->dc.fit_w[r] = (int32_t)cfg->fit_weight[r];
+  c->dc.la_w_cpu = (int32_t)cfg->la_weight_cpu;
+  c->dc.la_w_mem = (int32_t)cfg->la_weight_mem;
+  c->dc.according = cfg->la_score_according_prod_usage ? 1 : 0;
+  c->monotone = 1;  // Fit LeastAllocated + LoadAware least-used: a commit never raises a key
+  int dev = cfg->device;
+  if (dev < 0) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  }
+  c->device = dev;
+  hipError_t e = hipSetDevice(dev);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->t0);
+  if (e == hipSuccess) e = hipEventCreate(&c->t1);
+  if (e == hipSuccess) e = hipMalloc(&c->d_tmp_pod, sizeof(koordhip_pod));
+  if (e != hipSuccess) {
+    std::string m = std::string("device init: ") + hipGetErrorString(e);
+    delete c;
+    return fail(KOORDHIP_EDEVICE, m);
+  }
+  *out = c;
+  return 0;
+}
+
+int koordhip_destroy(koordhip_ctx *c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_cols(c);
+  for (void *p : c->ckpt) (void)hipFree(p);
+  for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
+                  (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod})
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->t0) (void)hipEventDestroy(c->t0);
+  if (c->t1) (void)hipEventDestroy(c->t1);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (n < 0) return fail(KOORDHIP_EINVAL, "n < 0");
+  if (int e = validate_soa(s)) return e;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  free_cols(c);
+  for (void *p : c->ckpt) (void)hipFree(p);
+  c->ckpt.clear();
+  kh::DevNodes &d = c->d;
+  d.n = n;
+  int e = 0;
+  for (int r = 0; r < KOORDHIP_NRES && !e; r++) {
+    int64_t *a = nullptr, *q = nullptr;
+    e = dev_alloc(c, &a, n);
+    if (!e) e = dev_alloc(c, &q, n);
+    if (!e) e = upload(c, a, s->alloc[r], n);
+    if (!e) e = upload(c, q, s->requested[r], n);
+    d.alloc[r] = a;
+    d.requested[r] = q;
+  }
+  auto col64 = [&](int64_t **dst, const int64_t *src) {
+    if (!e) e = dev_alloc(c, dst, n);
+    if (!e) e = upload(c, *dst, src, n);
+  };
+  int32_t *ap = nullptr, *np = nullptr;
+  if (!e) e = dev_alloc(c, &ap, n);
+  if (!e) e = upload(c, ap, s->alloc_pods, n);
+  if (!e) e = dev_alloc(c, &np, n);
+  if (!e) e = upload(c, np, s->npods, n);
+  d.alloc_pods = ap;
+  d.npods = np;
+  col64(&d.nz_cpu, s->nz_cpu_m);
+  col64(&d.nz_mem, s->nz_mem);
+  int64_t *lac = nullptr, *lam = nullptr;
+  col64(&lac, s->la_alloc_cpu_m);
+  col64(&lam, s->la_alloc_mem);
+  d.la_alloc_cpu = lac;
+  d.la_alloc_mem = lam;
+  col64(&d.la_used_cpu, s->la_used_cpu_m);
+  col64(&d.la_used_mem, s->la_used_mem);
+  col64(&d.la_used_prod_cpu, s->la_used_prod_cpu_m);  // NULL -> zeros
+  col64(&d.la_used_prod_mem, s->la_used_prod_mem);
+  if (!e) e = dev_alloc(c, &d.flags, n);
+  // LoadAware Filter inputs
+  kh::PrepIn &pi = c->prep;
+  for (int r = 0; r < 2 && !e; r++) {
+    int64_t *a = nullptr, *b = nullptr, *cc = nullptr, *t = nullptr, *pt = nullptr;
+    col64(&a, s->laf_used_m[r]);
+    col64(&b, s->laf_total_m[r]);
+    col64(&cc, s->laf_prod_used_m[r]);
+    col64(&t, s->laf_thr[r]);
+    col64(&pt, s->laf_prod_thr[r]);
+    pi.used_m[r] = a;
+    pi.total_m[r] = b;
+    pi.prod_used_m[r] = cc;
+    pi.thr[r] = t;
+    pi.prod_thr[r] = pt;
+  }
+  uint8_t *lf = nullptr;
+  if (!e) e = dev_alloc(c, &lf, n);
+  if (!e) e = upload(c, lf, s->la_flags, n);
+  pi.la_flags = lf;
+  if (e) {
+    free_cols(c);
+    return e;
+  }
+  // la_alloc == alloc for cpu and memory? then the eval kernels read them once
+  c->dc.la_alias = (n == 0) || (std::memcmp(s->la_alloc_cpu_m, s->alloc[KOORDHIP_RES_CPU], n * sizeof(int64_t)) == 0 &&
+                                std::memcmp(s->la_alloc_mem, s->alloc[KOORDHIP_RES_MEM], n * sizeof(int64_t)) == 0);
+  HIP_TRY(kh::launch_prep_flags(pi, d, nullptr, n, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->n = n;
+  c->loaded = true;
+  return 0;
+}
+
+int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_node_soa *rows, int32_t m) {
+  if (!c || !idx) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (m <= 0) return 0;
+  if (int e = validate_soa(rows)) return e;
+  for (int32_t j = 0; j < m; j++)
+    if (idx[j] < 0 || idx[j] >= c->n) return fail(KOORDHIP_EINVAL, "row index out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  int32_t *d_idx = nullptr;
+  void *stage = nullptr;
+  HIP_TRY(hipMalloc(&d_idx, m * sizeof(int32_t)));
+  HIP_TRY(hipMalloc(&stage, (size_t)m * sizeof(int64_t)));
+  int e = 0;
+  auto put64 = [&](int64_t *dst, const int64_t *src) {
+    if (e) return;
+    e = upload(c, (int64_t *)stage, src, m);
+    if (!e && kh::launch_scatter<int64_t>(dst, (const int64_t *)stage, d_idx, m, c->stream) != hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "scatter");
+    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
+  };
+  auto put32 = [&](int32_t *dst, const int32_t *src) {
+    if (e) return;
+    e = upload(c, (int32_t *)stage, src, m);
+    if (!e && kh::launch_scatter<int32_t>(dst, (const int32_t *)stage, d_idx, m, c->stream) != hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "scatter");
+    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
+  };
+  auto put8 = [&](uint8_t *dst, const uint8_t *src) {
+    if (e) return;
+    e = upload(c, (uint8_t *)stage, src, m);
+    if (!e && kh::launch_scatter<uint8_t>(dst, (const uint8_t *)stage, d_idx, m, c->stream) != hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "scatter");
+    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
+  };
+  e = upload(c, d_idx, idx, m);
+  kh::DevNodes &d = c->d;
+  kh::PrepIn &pi = c->prep;
+  for (int r = 0; r < KOORDHIP_NRES; r++) {
+    put64(const_cast<int64_t *>(d.alloc[r]), rows->alloc[r]);
+    put64(d.requested[r], rows->requested[r]);
+  }
+  put32(const_cast<int32_t *>(d.alloc_pods), rows->alloc_pods);
+  put32(d.npods, rows->npods);
+  put64(d.nz_cpu, rows->nz_cpu_m);
+  put64(d.nz_mem, rows->nz_mem);
+  put64(const_cast<int64_t *>(d.la_alloc_cpu), rows->la_alloc_cpu_m);
+  put64(const_cast<int64_t *>(d.la_alloc_mem), rows->la_alloc_mem);
+  put64(d.la_used_cpu, rows->la_used_cpu_m);
+  put64(d.la_used_mem, rows->la_used_mem);
+  put64(d.la_used_prod_cpu, rows->la_used_prod_cpu_m);
+  put64(d.la_used_prod_mem, rows->la_used_prod_mem);
+  for (int r = 0; r < 2; r++) {
+    put64(const_cast<int64_t *>(pi.used_m[r]), rows->laf_used_m[r]);
+    put64(const_cast<int64_t *>(pi.total_m[r]), rows->laf_total_m[r]);
+    put64(const_cast<int64_t *>(pi.prod_used_m[r]), rows->laf_prod_used_m[r]);
+    put64(const_cast<int64_t *>(pi.thr[r]), rows->laf_thr[r]);
+    put64(const_cast<int64_t *>(pi.prod_thr[r]), rows->laf_prod_thr[r]);
+  }
+  put8(const_cast<uint8_t *>(pi.la_flags), rows->la_flags);
+  if (!e && c->dc.la_alias) {
+    for (int32_t j = 0; j < m && c->dc.la_alias; j++)
+      if (rows->la_alloc_cpu_m[j] != rows->alloc[KOORDHIP_RES_CPU][j] ||
+          rows->la_alloc_mem[j] != rows->alloc[KOORDHIP_RES_MEM][j])
+        c->dc.la_alias = 0;
+  }
+  if (!e && kh::launch_prep_flags(pi, d, d_idx, m, c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "prep");
+  if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
+  (void)hipFree(d_idx);
+  (void)hipFree(stage);
+  return e;
+}
+
+int koordhip_read_nodes(koordhip_ctx *c, int64_t *requested, int64_t *nz, int32_t *npods, int64_t *la_used,
+                        int64_t *la_used_prod) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t n = c->n, b = n * sizeof(int64_t);
+  if (n == 0) return 0;
+  if (requested)
+    for (int r = 0; r < KOORDHIP_NRES; r++) HIP_TRY(hipMemcpy(requested + r * n, c->d.requested[r], b, hipMemcpyDeviceToHost));
+  if (nz) {
+    HIP_TRY(hipMemcpy(nz, c->d.nz_cpu, b, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(nz + n, c->d.nz_mem, b, hipMemcpyDeviceToHost));
+  }
+  if (npods) HIP_TRY(hipMemcpy(npods, c->d.npods, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (la_used) {
+    HIP_TRY(hipMemcpy(la_used, c->d.la_used_cpu, b, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(la_used + n, c->d.la_used_mem, b, hipMemcpyDeviceToHost));
+  }
+  if (la_used_prod) {
+    HIP_TRY(hipMemcpy(la_used_prod, c->d.la_used_prod_cpu, b, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(la_used_prod + n, c->d.la_used_prod_mem, b, hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uint8_t *status, int32_t *scores,
+                  koordhip_topk *topk, int32_t k) {
+  if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
+  if (topk && (k < 1 || k > kMaxBatch)) return fail(KOORDHIP_EINVAL, "k must be in [1, 64]");
+  if (n_pods == 0) return 0;
+  HIP_TRY(hipSetDevice(c->device));
+  const int32_t n = c->n;
+  // parity mode works in slices of pods so the status/score buffers stay bounded
+  const int32_t per = std::max<int32_t>(1, std::min<int32_t>(kMaxBatch, (int32_t)((256ll << 20) / (16ll * std::max(n, 1)))));
+  koordhip_pod *dp = nullptr;
+  uint8_t *dst = nullptr;
+  int32_t *dsc = nullptr;
+  uint64_t *dk = nullptr;
+  int e = 0;
+  auto cleanup = [&]() {
+    for (void *p : {(void *)dp, (void *)dst, (void *)dsc, (void *)dk})
+      if (p) (void)hipFree(p);
+  };
+  if (hipMalloc(&dp, (size_t)per * sizeof(koordhip_pod)) != hipSuccess ||
+      (status && hipMalloc(&dst, (size_t)per * n) != hipSuccess) ||
+      (scores && hipMalloc(&dsc, (size_t)per * KOORDHIP_NPLUGINS * n * sizeof(int32_t)) != hipSuccess) ||
+      (topk && hipMalloc(&dk, (size_t)per * k * sizeof(uint64_t)) != hipSuccess)) {
+    cleanup();
+    return fail(KOORDHIP_ENOMEM, "eval buffers");
+  }
+  std::vector<uint64_t> hk(topk ? (size_t)per * k : 0);
+  for (int32_t p0 = 0; p0 < n_pods && !e; p0 += per) {
+    const int32_t np = std::min(per, n_pods - p0);
+    if (hipMemcpyAsync(dp, pods + p0, np * sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+      e = fail(KOORDHIP_EDEVICE, "copy pods");
+      break;
+    }
+    if ((status || scores) && kh::launch_eval_full(c->dc, c->d, dp, np, dst, dsc, c->stream) != hipSuccess) {
+      e = fail(KOORDHIP_EDEVICE, "eval_full launch");
+      break;
+    }
+    if (topk) e = topk_batch(c, dp, np, k, 0, n, dk, false);
+    if (e) break;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) {
+      e = fail(KOORDHIP_EDEVICE, "eval sync");
+      break;
+    }
+    if (status && hipMemcpy(status + (size_t)p0 * n, dst, (size_t)np * n, hipMemcpyDeviceToHost) != hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "copy status");
+    if (!e && scores &&
+        hipMemcpy(scores + (size_t)p0 * KOORDHIP_NPLUGINS * n, dsc, (size_t)np * KOORDHIP_NPLUGINS * n * sizeof(int32_t),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "copy scores");
+    if (!e && topk) {
+      if (hipMemcpy(hk.data(), dk, (size_t)np * k * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        e = fail(KOORDHIP_EDEVICE, "copy topk");
+        break;
+      }
+      for (size_t j = 0; j < (size_t)np * k; j++) {
+        koordhip_topk &o = topk[(size_t)p0 * k + j];
+        const uint64_t x = hk[j];
+        o.node = x ? (int32_t)(0xFFFFFFFFu - (uint32_t)x) : -1;
+        o.score = x ? (int32_t)(x >> 32) - 1 : 0;
+      }
+    }
+  }
+  cleanup();
+  return e;
+}
+
+int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods) {
+  if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
+  HIP_TRY(hipSetDevice(c->device));
+  if (n_pods > c->pods_cap) {
+    if (c->d_pods) HIP_TRY(hipFree(c->d_pods));
+    if (c->d_out) HIP_TRY(hipFree(c->d_out));
+    c->d_pods = nullptr;
+    c->d_out = nullptr;
+    HIP_TRY(hipMalloc(&c->d_pods, (size_t)n_pods * sizeof(koordhip_pod)));
+    HIP_TRY(hipMalloc(&c->d_out, (size_t)n_pods * sizeof(int32_t)));
+    c->pods_cap = n_pods;
+  }
+  if (n_pods) HIP_TRY(hipMemcpyAsync(c->d_pods, pods, (size_t)n_pods * sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->n_staged = n_pods;
+  return 0;
+}
+
+int koordhip_place_staged(koordhip_ctx *c) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  const int32_t P = c->batch, K = c->batch;
+  size_t cap = 0;
+  if (!c->d_lists) {
+    HIP_TRY(hipMalloc(&c->d_lists, (size_t)kMaxBatch * kMaxBatch * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_final, (size_t)kMaxBatch * kMaxBatch * sizeof(uint64_t)));
+  }
+  if (c->world > 1 && !c->d_gather)
+    HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * kMaxBatch * kMaxBatch * sizeof(uint64_t)));
+  (void)cap;
+  int32_t lo = 0, hi = c->n;
+  shard(c, &lo, &hi);
+  c->ev_used = 0;
+  c->last_launches = 0;
+  c->last_evals = 0;
+  HIP_TRY(hipEventRecord(c->t0, c->stream));
+  const int32_t total = c->n_staged;
+  for (int32_t p0 = 0; p0 < total; p0 += P) {
+    const int32_t np = std::min(P, total - p0);
+    const koordhip_pod *pods = c->d_pods + p0;
+    if (c->world > 1) {
+      if (np < P) HIP_TRY(hipMemsetAsync(c->d_lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
+      if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
+      NCCL_TRY(ncclAllGather(c->d_lists, c->d_gather, (size_t)P * K, ncclUint64, c->comm, c->stream));
+      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->d_final, c->stream));
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0, c->stream));
+    } else {
+      if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_lists, c->monotone, c->d_out + p0, c->stream));
+    }
+  }
+  HIP_TRY(hipEventRecord(c->t1, c->stream));
+  return 0;
+}
+
+int koordhip_synchronize(koordhip_ctx *c) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int koordhip_fetch_placements(koordhip_ctx *c, int32_t *out_node, int32_t n_pods) {
+  if (!c || (!out_node && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (n_pods > c->n_staged) return fail(KOORDHIP_EINVAL, "n_pods exceeds the staged stream");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (n_pods) HIP_TRY(hipMemcpy(out_node, c->d_out, (size_t)n_pods * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int koordhip_place_stream(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, int32_t *out_node) {
+  if (int e = koordhip_stage_pods(c, pods, n_pods)) return e;
+  if (int e = koordhip_place_staged(c)) return e;
+  return koordhip_fetch_placements(c, out_node, n_pods);
+}
+
+// mutable columns: (device pointer, bytes)
+static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
+  const size_t n = c->n, b = n * sizeof(int64_t);
+  std::vector<std::pair<void *, size_t>> v;
+  for (int r = 0; r < KOORDHIP_NRES; r++) v.push_back({c->d.requested[r], b});
+  v.push_back({c->d.nz_cpu, b});
+  v.push_back({c->d.nz_mem, b});
+  v.push_back({c->d.npods, n * sizeof(int32_t)});
+  v.push_back({c->d.la_used_cpu, b});
+  v.push_back({c->d.la_used_mem, b});
+  v.push_back({c->d.la_used_prod_cpu, b});
+  v.push_back({c->d.la_used_prod_mem, b});
+  v.push_back({c->d.flags, n});
+  return v;
+}
+
+int koordhip_checkpoint(koordhip_ctx *c) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  auto cols = mutable_cols(c);
+  if (c->ckpt.size() != cols.size()) {
+    for (void *p : c->ckpt) (void)hipFree(p);
+    c->ckpt.assign(cols.size(), nullptr);
+    for (size_t i = 0; i < cols.size(); i++) HIP_TRY(hipMalloc(&c->ckpt[i], std::max<size_t>(cols[i].second, 1)));
+  }
+  for (size_t i = 0; i < cols.size(); i++)
+    if (cols[i].second) HIP_TRY(hipMemcpyAsync(c->ckpt[i], cols[i].first, cols[i].second, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int koordhip_restore(koordhip_ctx *c) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  auto cols = mutable_cols(c);
+  if (c->ckpt.size() != cols.size()) return fail(KOORDHIP_ESTATE, "no checkpoint");
+  HIP_TRY(hipSetDevice(c->device));
+  for (size_t i = 0; i < cols.size(); i++)
+    if (cols[i].second) HIP_TRY(hipMemcpyAsync(cols[i].first, c->ckpt[i], cols[i].second, hipMemcpyDeviceToDevice, c->stream));
+  return 0;
+}
+
+static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, int sign) {
+  if (!c || !pod) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (node < 0 || node >= c->n) return fail(KOORDHIP_EINVAL, "node index out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(c->d_tmp_pod, pod, sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(kh::launch_commit(c->d, c->d_tmp_pod, node, sign, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int koordhip_commit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node) { return commit_impl(c, pod, node, +1); }
+int koordhip_uncommit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node) { return commit_impl(c, pod, node, -1); }
+
+int koordhip_last_stats(koordhip_ctx *c, double *eval_ms, int64_t *eval_launches, int64_t *evals, double *total_ms) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, c->t0, c->t1));
+  double em = 0;
+  for (int32_t i = 0; i + 1 < c->ev_used; i += 2) {
+    float x = 0;
+    HIP_TRY(hipEventElapsedTime(&x, c->ev[i], c->ev[i + 1]));
+    em += x;
+  }
+  if (eval_ms) *eval_ms = em;
+  if (eval_launches) *eval_launches = c->last_launches;
+  if (evals) *evals = c->last_evals;
+  if (total_ms) *total_ms = ms;
+  return 0;
+}
+
+int koordhip_comm_unique_id(uint8_t *id_out) {
+  if (!id_out) return fail(KOORDHIP_EINVAL, "NULL argument");
+  static_assert(sizeof(ncclUniqueId) <= KOORDHIP_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  std::memset(id_out, 0, KOORDHIP_UNIQUE_ID_BYTES);
+  std::memcpy(id_out, &id, sizeof(id));
+  return 0;
+}
+
+int koordhip_comm_init(koordhip_ctx *c, const uint8_t *id, int32_t world, int32_t rank) {
+  if (!c || !id) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (world < 1 || rank < 0 || rank >= world) return fail(KOORDHIP_EINVAL, "bad world/rank");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->comm) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  if (world > 1) {
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
+  }
+  c->world = world;
+  c->rank = rank;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,302 @@
+// eval.hpp -- the per-(pod,node) Filter+Score arithmetic on CDNA4, shared by
+// every kernel of libkoordhip.so (stream top-k, resolve, parity eval).
+//
+// Exactness: all plugin arithmetic is int64 as in the reference; the only
+// divisions are quotients known to lie in [0, 101] (leastRequestedScore and the
+// weighted averages), computed as an f64 reciprocal estimate followed by an
+// exact int64 remainder fix-up, so the result equals Go's truncating int64
+// division bit for bit (see lrs_div below).  The LoadAware threshold mask uses
+// IEEE f64 division + round-half-away exactly like math.Round in
+// load_aware.go:214,248 (compiled with -ffp-contract=off).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/koordhip.h"
+
+namespace kh {
+
+// device-side node flag bits (flags column, maintained on device)
+enum : uint32_t {
+  NF_LA_OK_NONPROD = 1u,  // LoadAware Filter passes for non-prod pods
+  NF_LA_OK_PROD = 2u,     // ... for prod pods
+  NF_LA_SCORE_ZERO = 4u,  // LoadAware Score is 0 (missing / expired NodeMetric)
+  NF_OVER_CPU = 8u,       // Requested.cpu > Allocatable.cpu (fitsRequest with a 0 request fails)
+  NF_OVER_MEM = 16u,
+  NF_OVER_EPH = 32u,
+};
+
+struct DevCfg {
+  uint32_t filt, score;
+  int32_t w_fit, w_la, w_numa;
+  int32_t fit_w[KOORDHIP_NRES];
+  int32_t la_w_cpu, la_w_mem;
+  int32_t according;  // ScoreAccordingProdUsage
+  int32_t la_alias;   // la_alloc columns equal alloc cpu/mem columns (loaded once)
+};
+
+// Columnar node state in HBM.  Static columns are const; the mutable ones are
+// advanced by the resolve kernel (Reserve delta) and by commit/uncommit.
+struct DevNodes {
+  const int64_t *alloc[KOORDHIP_NRES];
+  const int32_t *alloc_pods;
+  int64_t *requested[KOORDHIP_NRES];
+  int64_t *nz_cpu, *nz_mem;
+  int32_t *npods;
+  const int64_t *la_alloc_cpu, *la_alloc_mem;
+  int64_t *la_used_cpu, *la_used_mem, *la_used_prod_cpu, *la_used_prod_mem;
+  uint8_t *flags;
+  int32_t n;
+};
+
+// One node's values as the evaluation consumes them (registers or an LDS row).
+struct NV {
+  int64_t a[KOORDHIP_NRES];
+  int64_t r[KOORDHIP_NRES];
+  int64_t nz_cpu, nz_mem;
+  int64_t la_a_cpu, la_a_mem, la_u_cpu, la_u_mem, la_up_cpu, la_up_mem;
+  int32_t a_pods, npods;
+  uint32_t flags;
+};
+
+// What one pod's evaluation needs from the node columns (wave-uniform).
+struct Need {
+  bool pods, r_cpu, r_mem, eph, bcpu, bmem, a_cpu, a_mem, nz_cpu, nz_mem, la, la_prod;
+};
+
+__device__ __forceinline__ Need pod_needs(const koordhip_pod &p, const DevCfg &c) {
+  Need n{};
+  const bool ff = c.filt & KOORDHIP_PLUGIN_FIT;
+  const bool fs = c.score & KOORDHIP_PLUGIN_FIT;
+  const bool hr = p.flags & KOORDHIP_POD_HAS_REQ;
+  n.pods = ff;
+  n.r_cpu = ff && hr && p.req[KOORDHIP_RES_CPU] != 0;
+  n.r_mem = ff && hr && p.req[KOORDHIP_RES_MEM] != 0;
+  n.eph = (ff && hr && p.req[KOORDHIP_RES_EPH] != 0) || (fs && c.fit_w[KOORDHIP_RES_EPH] != 0);
+  n.bcpu = (ff && (p.flags & KOORDHIP_POD_REQ_BCPU)) ||
+           (fs && c.fit_w[KOORDHIP_RES_BCPU] != 0 && p.req[KOORDHIP_RES_BCPU] != 0);
+  n.bmem = (ff && (p.flags & KOORDHIP_POD_REQ_BMEM)) ||
+           (fs && c.fit_w[KOORDHIP_RES_BMEM] != 0 && p.req[KOORDHIP_RES_BMEM] != 0);
+  n.nz_cpu = fs && c.fit_w[KOORDHIP_RES_CPU] != 0;
+  n.nz_mem = fs && c.fit_w[KOORDHIP_RES_MEM] != 0;
+  n.la = c.score & KOORDHIP_PLUGIN_LOADAWARE;
+  n.la_prod = n.la && c.according && (p.flags & KOORDHIP_POD_PROD);
+  n.a_cpu = n.r_cpu || n.nz_cpu || (n.la && c.la_alias);
+  n.a_mem = n.r_mem || n.nz_mem || (n.la && c.la_alias);
+  return n;
+}
+
+__device__ __forceinline__ Need need_all(const DevCfg &c) {
+  Need n;
+  n.pods = n.r_cpu = n.r_mem = n.eph = n.bcpu = n.bmem = n.a_cpu = n.a_mem = n.nz_cpu = n.nz_mem = true;
+  n.la = true;
+  n.la_prod = c.according != 0;
+  return n;
+}
+
+// Load node i's columns the evaluation needs (coalesced across lanes).
+__device__ __forceinline__ void load_node(NV &v, const DevNodes &d, int32_t i, const Need &n, const DevCfg &c) {
+  v.flags = d.flags[i];
+  if (n.pods) {
+    v.a_pods = d.alloc_pods[i];
+    v.npods = d.npods[i];
+  }
+  if (n.a_cpu) v.a[KOORDHIP_RES_CPU] = d.alloc[KOORDHIP_RES_CPU][i];
+  if (n.a_mem) v.a[KOORDHIP_RES_MEM] = d.alloc[KOORDHIP_RES_MEM][i];
+  if (n.r_cpu) v.r[KOORDHIP_RES_CPU] = d.requested[KOORDHIP_RES_CPU][i];
+  if (n.r_mem) v.r[KOORDHIP_RES_MEM] = d.requested[KOORDHIP_RES_MEM][i];
+  if (n.eph) {
+    v.a[KOORDHIP_RES_EPH] = d.alloc[KOORDHIP_RES_EPH][i];
+    v.r[KOORDHIP_RES_EPH] = d.requested[KOORDHIP_RES_EPH][i];
+  }
+  if (n.bcpu) {
+    v.a[KOORDHIP_RES_BCPU] = d.alloc[KOORDHIP_RES_BCPU][i];
+    v.r[KOORDHIP_RES_BCPU] = d.requested[KOORDHIP_RES_BCPU][i];
+  }
+  if (n.bmem) {
+    v.a[KOORDHIP_RES_BMEM] = d.alloc[KOORDHIP_RES_BMEM][i];
+    v.r[KOORDHIP_RES_BMEM] = d.requested[KOORDHIP_RES_BMEM][i];
+  }
+  if (n.nz_cpu) v.nz_cpu = d.nz_cpu[i];
+  if (n.nz_mem) v.nz_mem = d.nz_mem[i];
+  if (n.la) {
+    if (c.la_alias) {
+      v.la_a_cpu = v.a[KOORDHIP_RES_CPU];
+      v.la_a_mem = v.a[KOORDHIP_RES_MEM];
+    } else {
+      v.la_a_cpu = d.la_alloc_cpu[i];
+      v.la_a_mem = d.la_alloc_mem[i];
+    }
+    if (n.la_prod) {
+      v.la_up_cpu = d.la_used_prod_cpu[i];
+      v.la_up_mem = d.la_used_prod_mem[i];
+    } else {
+      v.la_u_cpu = d.la_used_cpu[i];
+      v.la_u_mem = d.la_used_mem[i];
+    }
+  }
+}
+
+// floor(a / b) for 0 <= a/b < 2^20, b > 0: f64 reciprocal estimate (|err| << 1)
+// then one exact int64 correction step in each direction.
+__device__ __forceinline__ int32_t div_small(int64_t a, int64_t b) {
+  double qd = (double)a * __builtin_amdgcn_rcp((double)b);
+  int32_t q = (int32_t)qd;
+  int64_t r = a - (int64_t)q * b;
+  q -= (r < 0);
+  q += (r >= b);
+  return q;
+}
+
+// leastRequestedScore, load_aware.go:388-397 / least_allocated.go:49-58.
+__device__ __forceinline__ int32_t lrs(int64_t req, int64_t cap) {
+  if (cap == 0 || req > cap) return 0;
+  return div_small((cap - req) * 100, cap);
+}
+
+// Fit LeastAllocated score (upstream resource_allocation.go + least_allocated.go;
+// koord copy nodenumaresource/scoring.go:191-246).
+__device__ __forceinline__ int32_t fit_score(const koordhip_pod &p, const NV &v, const DevCfg &c) {
+  int64_t num = 0, ws = 0;
+  if (c.fit_w[KOORDHIP_RES_CPU] && v.a[KOORDHIP_RES_CPU] != 0) {
+    num += (int64_t)lrs(v.nz_cpu + p.nz_cpu_m, v.a[KOORDHIP_RES_CPU]) * c.fit_w[KOORDHIP_RES_CPU];
+    ws += c.fit_w[KOORDHIP_RES_CPU];
+  }
+  if (c.fit_w[KOORDHIP_RES_MEM] && v.a[KOORDHIP_RES_MEM] != 0) {
+    num += (int64_t)lrs(v.nz_mem + p.nz_mem, v.a[KOORDHIP_RES_MEM]) * c.fit_w[KOORDHIP_RES_MEM];
+    ws += c.fit_w[KOORDHIP_RES_MEM];
+  }
+  if (c.fit_w[KOORDHIP_RES_EPH] && v.a[KOORDHIP_RES_EPH] != 0) {
+    num += (int64_t)lrs(v.r[KOORDHIP_RES_EPH] + p.req[KOORDHIP_RES_EPH], v.a[KOORDHIP_RES_EPH]) *
+           c.fit_w[KOORDHIP_RES_EPH];
+    ws += c.fit_w[KOORDHIP_RES_EPH];
+  }
+#pragma unroll
+  for (int r = KOORDHIP_RES_BCPU; r <= KOORDHIP_RES_BMEM; r++) {
+    if (c.fit_w[r] && p.req[r] != 0 && v.a[r] != 0) {
+      num += (int64_t)lrs(v.r[r] + p.req[r], v.a[r]) * c.fit_w[r];
+      ws += c.fit_w[r];
+    }
+  }
+  if (ws == 0) return 0;
+  return div_small(num, ws);
+}
+
+// fitsRequest (upstream fit.go; mirror reservation/plugin.go:445-494).  A zero
+// request on cpu/memory/ephemeral reduces to "Requested > Allocatable", kept
+// as the NF_OVER_* bits so such pods need not read those columns.
+__device__ __forceinline__ bool fit_filter(const koordhip_pod &p, const NV &v) {
+  if ((int64_t)v.npods + 1 > (int64_t)v.a_pods) return false;
+  if (!(p.flags & KOORDHIP_POD_HAS_REQ)) return true;
+  if (p.req[KOORDHIP_RES_CPU] != 0) {
+    if (p.req[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU] - v.r[KOORDHIP_RES_CPU]) return false;
+  } else if (v.flags & NF_OVER_CPU) {
+    return false;
+  }
+  if (p.req[KOORDHIP_RES_MEM] != 0) {
+    if (p.req[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM] - v.r[KOORDHIP_RES_MEM]) return false;
+  } else if (v.flags & NF_OVER_MEM) {
+    return false;
+  }
+  if (p.req[KOORDHIP_RES_EPH] != 0) {
+    if (p.req[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH] - v.r[KOORDHIP_RES_EPH]) return false;
+  } else if (v.flags & NF_OVER_EPH) {
+    return false;
+  }
+  if ((p.flags & KOORDHIP_POD_REQ_BCPU) &&
+      p.req[KOORDHIP_RES_BCPU] > v.a[KOORDHIP_RES_BCPU] - v.r[KOORDHIP_RES_BCPU])
+    return false;
+  if ((p.flags & KOORDHIP_POD_REQ_BMEM) &&
+      p.req[KOORDHIP_RES_BMEM] > v.a[KOORDHIP_RES_BMEM] - v.r[KOORDHIP_RES_BMEM])
+    return false;
+  return true;
+}
+
+// LoadAware Filter (load_aware.go:123-171): static mask + DaemonSet bypass.
+__device__ __forceinline__ bool la_filter(const koordhip_pod &p, const NV &v) {
+  if (p.flags & KOORDHIP_POD_DAEMONSET) return true;
+  return v.flags & ((p.flags & KOORDHIP_POD_PROD) ? NF_LA_OK_PROD : NF_LA_OK_NONPROD);
+}
+
+// LoadAware Score (load_aware.go:269-335, scorer :378-386).
+__device__ __forceinline__ int32_t la_score(const koordhip_pod &p, const NV &v, const DevCfg &c) {
+  if (v.flags & NF_LA_SCORE_ZERO) return 0;
+  const bool prod = c.according && (p.flags & KOORDHIP_POD_PROD);
+  const int64_t ucpu = p.est_cpu + (prod ? v.la_up_cpu : v.la_u_cpu);
+  const int64_t umem = p.est_mem + (prod ? v.la_up_mem : v.la_u_mem);
+  const int64_t num = (int64_t)lrs(ucpu, v.la_a_cpu) * c.la_w_cpu + (int64_t)lrs(umem, v.la_a_mem) * c.la_w_mem;
+  return div_small(num, (int64_t)(c.la_w_cpu + c.la_w_mem));
+}
+
+// Total weighted score, or -1 when any enabled Filter fails (short-circuit).
+__device__ __forceinline__ int32_t eval_total(const koordhip_pod &p, const NV &v, const DevCfg &c) {
+  if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(p, v)) return -1;
+  if ((c.filt & KOORDHIP_PLUGIN_LOADAWARE) && !la_filter(p, v)) return -1;
+  int32_t t = 0;
+  if (c.score & KOORDHIP_PLUGIN_FIT) t += c.w_fit * fit_score(p, v, c);
+  if (c.score & KOORDHIP_PLUGIN_LOADAWARE) t += c.w_la * la_score(p, v, c);
+  return t;
+}
+
+// Ranking key: larger is better; equal totals -> lower node index wins
+// (replaces selectHost's reservoir-random tie-break).  0 = infeasible.
+__device__ __forceinline__ uint64_t make_key(int32_t total, int32_t node) {
+  return total < 0 ? 0ull : (((uint64_t)(uint32_t)(total + 1)) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)node);
+}
+__device__ __forceinline__ int32_t key_node(uint64_t k) { return (int32_t)(0xFFFFFFFFu - (uint32_t)k); }
+__device__ __forceinline__ int32_t key_score(uint64_t k) { return (int32_t)(k >> 32) - 1; }
+
+// Reserve delta (podAssignCache.assign + NodeInfo.AddPod), sign = +1 / -1.
+__device__ __forceinline__ void apply_delta(NV &v, const koordhip_pod &p, int sign) {
+#pragma unroll
+  for (int r = 0; r < KOORDHIP_NRES; r++) v.r[r] += sign * p.req[r];
+  v.nz_cpu += sign * p.nz_cpu_m;
+  v.nz_mem += sign * p.nz_mem;
+  v.npods += sign;
+  v.la_u_cpu += sign * p.est_cpu;
+  v.la_u_mem += sign * p.est_mem;
+  if (p.flags & KOORDHIP_POD_PROD) {
+    v.la_up_cpu += sign * p.est_cpu;
+    v.la_up_mem += sign * p.est_mem;
+  }
+  uint32_t f = v.flags & ~(NF_OVER_CPU | NF_OVER_MEM | NF_OVER_EPH);
+  if (v.r[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU]) f |= NF_OVER_CPU;
+  if (v.r[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM]) f |= NF_OVER_MEM;
+  if (v.r[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH]) f |= NF_OVER_EPH;
+  v.flags = f;
+}
+
+// Full row load / store (resolve and commit paths).
+__device__ __forceinline__ void load_row(NV &v, const DevNodes &d, int32_t i) {
+#pragma unroll
+  for (int r = 0; r < KOORDHIP_NRES; r++) {
+    v.a[r] = d.alloc[r][i];
+    v.r[r] = d.requested[r][i];
+  }
+  v.a_pods = d.alloc_pods[i];
+  v.npods = d.npods[i];
+  v.nz_cpu = d.nz_cpu[i];
+  v.nz_mem = d.nz_mem[i];
+  v.la_a_cpu = d.la_alloc_cpu[i];
+  v.la_a_mem = d.la_alloc_mem[i];
+  v.la_u_cpu = d.la_used_cpu[i];
+  v.la_u_mem = d.la_used_mem[i];
+  v.la_up_cpu = d.la_used_prod_cpu[i];
+  v.la_up_mem = d.la_used_prod_mem[i];
+  v.flags = d.flags[i];
+}
+
+__device__ __forceinline__ void store_row(const NV &v, const DevNodes &d, int32_t i) {
+#pragma unroll
+  for (int r = 0; r < KOORDHIP_NRES; r++) d.requested[r][i] = v.r[r];
+  d.npods[i] = v.npods;
+  d.nz_cpu[i] = v.nz_cpu;
+  d.nz_mem[i] = v.nz_mem;
+  d.la_used_cpu[i] = v.la_u_cpu;
+  d.la_used_mem[i] = v.la_u_mem;
+  d.la_used_prod_cpu[i] = v.la_up_cpu;
+  d.la_used_prod_mem[i] = v.la_up_mem;
+  d.flags[i] = (uint8_t)v.flags;
+}
+
+}  // namespace kh

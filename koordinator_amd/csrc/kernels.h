@@ -1,0 +1,33 @@
+// kernels.h -- launch wrappers of kernels.hip (host side).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "eval.hpp"
+
+namespace kh {
+
+// LoadAware Filter inputs (device copies of koordhip_node_soa.laf_* / la_flags).
+struct PrepIn {
+  const int64_t *used_m[2];
+  const int64_t *total_m[2];
+  const int64_t *prod_used_m[2];
+  const int64_t *thr[2];
+  const int64_t *prod_thr[2];
+  const uint8_t *la_flags;
+};
+
+hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t *rows, int32_t m, hipStream_t s);
+hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
+                            uint8_t *status, int32_t *scores, hipStream_t s);
+hipError_t launch_topk_partial(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
+                               int32_t lo, int32_t hi, int32_t chunk, int32_t nchunks, int32_t k, uint64_t *out,
+                               hipStream_t s);
+hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
+                             int32_t k, uint64_t *out, hipStream_t s);
+template <typename T>
+hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
+hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods, int32_t k,
+                          const uint64_t *lists, int32_t monotone, int32_t *out_node, hipStream_t s);
+hipError_t launch_commit(const DevNodes &d, const koordhip_pod *pod, int32_t node, int32_t sign, hipStream_t s);
+
+}  // namespace kh

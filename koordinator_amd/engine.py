@@ -1,0 +1,132 @@
+"""PlacementEngine: the Python face of libkoordhip.so (what the Go shim binds
+through cgo).  Thin: every call goes straight to the C-ABI,
+there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+from .config import Profile, to_c_config
+from .snapshot import NodeTable
+
+
+class PlacementEngine:
+    def __init__(self, profile: Profile, device: int = -1, profile_kernels: bool = False):
+        self.lib = abi.load_library()
+        self.cfg = to_c_config(profile, device)
+        self.cfg.profile_kernels = 1 if profile_kernels else 0
+        self._ctx = C.c_void_p()
+        abi.check(self.lib, self.lib.koordhip_create(C.byref(self.cfg), C.byref(self._ctx)))
+        self.n = 0
+        self._table: Optional[NodeTable] = None
+
+    def close(self):
+        if self._ctx:
+            self.lib.koordhip_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- snapshot -----------------------------------------------------------
+    def load_snapshot(self, table: NodeTable):
+        soa = table.as_soa()
+        abi.check(self.lib, self.lib.koordhip_load_snapshot(self._ctx, C.byref(soa), table.n))
+        self.n = table.n
+        self._table = table
+
+    def update_nodes(self, idx, rows: NodeTable):
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        soa = rows.as_soa()
+        abi.check(self.lib, self.lib.koordhip_update_nodes(self._ctx, abi.ptr(idx, C.c_int32), C.byref(soa), len(idx)))
+
+    def read_nodes(self) -> dict:
+        n = self.n
+        req = np.zeros((abi.NRES, n), np.int64)
+        nz = np.zeros((2, n), np.int64)
+        npods = np.zeros(n, np.int32)
+        la = np.zeros((2, n), np.int64)
+        lap = np.zeros((2, n), np.int64)
+        abi.check(self.lib, self.lib.koordhip_read_nodes(self._ctx, abi.ptr(req, C.c_int64), abi.ptr(nz, C.c_int64),
+                                                         abi.ptr(npods, C.c_int32), abi.ptr(la, C.c_int64),
+                                                         abi.ptr(lap, C.c_int64)))
+        return {"requested": req, "nz": nz, "npods": npods, "la_used": la, "la_used_prod": lap}
+
+    # ---- evaluation ---------------------------------------------------------
+    def eval(self, pods: np.ndarray, status: bool = True, scores: bool = True, k: int = 0) -> dict:
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        p, n = len(pods), self.n
+        st = np.zeros((p, n), np.uint8) if status else None
+        sc = np.zeros((p, abi.NPLUGINS, n), np.int32) if scores else None
+        tk = np.zeros((p, k), abi.TOPK_DTYPE) if k else None
+        abi.check(self.lib, self.lib.koordhip_eval(
+            self._ctx, pods.ctypes.data, p, abi.ptr(st, C.c_uint8), abi.ptr(sc, C.c_int32),
+            tk.ctypes.data if tk is not None else None, k))
+        return {"status": st, "scores": sc, "topk": tk}
+
+    def place_stream(self, pods: np.ndarray) -> np.ndarray:
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        out = np.zeros(len(pods), np.int32)
+        abi.check(self.lib, self.lib.koordhip_place_stream(self._ctx, pods.ctypes.data, len(pods),
+                                                           abi.ptr(out, C.c_int32)))
+        return out
+
+    def stage_pods(self, pods: np.ndarray):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        self._staged = pods
+        abi.check(self.lib, self.lib.koordhip_stage_pods(self._ctx, pods.ctypes.data, len(pods)))
+
+    def place_staged(self):
+        abi.check(self.lib, self.lib.koordhip_place_staged(self._ctx))
+
+    def synchronize(self):
+        abi.check(self.lib, self.lib.koordhip_synchronize(self._ctx))
+
+    def fetch_placements(self, n: int) -> np.ndarray:
+        out = np.zeros(n, np.int32)
+        abi.check(self.lib, self.lib.koordhip_fetch_placements(self._ctx, abi.ptr(out, C.c_int32), n))
+        return out
+
+    def checkpoint(self):
+        abi.check(self.lib, self.lib.koordhip_checkpoint(self._ctx))
+
+    def restore(self):
+        abi.check(self.lib, self.lib.koordhip_restore(self._ctx))
+
+    def commit(self, pod, node: int):
+        pod = np.ascontiguousarray(np.atleast_1d(pod), dtype=abi.POD_DTYPE)
+        abi.check(self.lib, self.lib.koordhip_commit(self._ctx, pod.ctypes.data, int(node)))
+
+    def uncommit(self, pod, node: int):
+        pod = np.ascontiguousarray(np.atleast_1d(pod), dtype=abi.POD_DTYPE)
+        abi.check(self.lib, self.lib.koordhip_uncommit(self._ctx, pod.ctypes.data, int(node)))
+
+    def last_stats(self) -> dict:
+        em, tm = C.c_double(), C.c_double()
+        nl, ne = C.c_int64(), C.c_int64()
+        abi.check(self.lib, self.lib.koordhip_last_stats(self._ctx, C.byref(em), C.byref(nl), C.byref(ne), C.byref(tm)))
+        return {"eval_ms": em.value, "eval_launches": nl.value, "evals": ne.value, "total_ms": tm.value}
+
+    # ---- multi-GPU ----------------------------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        lib = abi.load_library()
+        buf = C.create_string_buffer(abi.UNIQUE_ID_BYTES)
+        abi.check(lib, lib.koordhip_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, uid: bytes, world: int, rank: int):
+        abi.check(self.lib, self.lib.koordhip_comm_init(self._ctx, uid, world, rank))

@@ -1,0 +1,467 @@
+"""Snapshot marshaller: Kubernetes objects -> koordhip SoA rows and pod records.
+
+This is the host half of the drop-in boundary (what the Go shim does before
+crossing cgo).  Everything that depends on wall-clock time, listers or JSON
+annotations is resolved here ONCE per snapshot at time `now`; the device only
+sees integers.  Each rule cites the reference line it restates.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Set, Tuple
+
+import numpy as np
+
+from . import abi, k8s
+from .config import LoadAwareSchedulingArgs, Profile
+from .snapshot import NodeTable, pod_array
+
+DEFAULT_MILLI_CPU_REQUEST = 250                 # estimator/default_estimator.go:35-38
+DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024
+NONZERO_DEFAULT_MILLI_CPU = 100                 # (upstream) scheduler/util/pod_resources.go
+NONZERO_DEFAULT_MEMORY = 200 * 1024 * 1024
+DEFAULT_REPORT_INTERVAL_S = 60.0                # load_aware.go:56
+
+
+class MarshalError(ValueError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+# Pod side (PreFilter products)
+
+def estimated_used_by_resource(requests, limits, name: str, factor: int) -> int:
+    """estimatedUsedByResource, estimator/default_estimator.go:73-108."""
+    lim = limits.get(name, k8s.Quantity(0))
+    req = requests.get(name, k8s.Quantity(0))
+    if lim.cmp(req) > 0:
+        factor, q = 100, lim
+    else:
+        q = req
+    if q.is_zero():
+        if name in (k8s.CPU, k8s.BATCH_CPU):
+            return DEFAULT_MILLI_CPU_REQUEST
+        if name in (k8s.MEMORY, k8s.BATCH_MEMORY):
+            return DEFAULT_MEMORY_REQUEST
+        return 0
+    if name == k8s.CPU:
+        est = k8s.round_half_away(float(q.milli_value()) * float(factor) / 100)
+        limit = lim.milli_value()
+    else:
+        est = k8s.round_half_away(float(q.value()) * float(factor) / 100)
+        limit = lim.value()
+    if limit > 0 and est > limit:
+        est = limit
+    return est
+
+
+def estimate_pod(pod: k8s.Pod, args: LoadAwareSchedulingArgs) -> Dict[str, int]:
+    """DefaultEstimator.EstimatePod, default_estimator.go:57-70."""
+    requests, limits = k8s.pod_requests_and_limits(pod)
+    pc = k8s.priority_class(pod)
+    out = {}
+    for name in args.resource_weights:
+        real = k8s.translate_resource(pc, name)
+        out[name] = estimated_used_by_resource(requests, limits, real, args.estimated_scaling_factors.get(name, 0))
+    return out
+
+
+_NATIVE_FIT = {k8s.CPU: abi.RES_CPU, k8s.MEMORY: abi.RES_MEM, k8s.EPHEMERAL: abi.RES_EPH}
+_SCALAR_FIT = {k8s.BATCH_CPU: abi.RES_BCPU, k8s.BATCH_MEMORY: abi.RES_BMEM}
+
+
+def _is_scalar(name: str) -> bool:
+    """(upstream) schedutil.IsScalarResourceName: extended, hugepages, prefixed-native, attachable."""
+    return name not in (k8s.CPU, k8s.MEMORY, k8s.EPHEMERAL, k8s.PODS)
+
+
+def _resource_add(acc: List[int], present: Set[str], rlist: k8s.ResourceList):
+    """(upstream) framework.Resource.Add."""
+    for n, q in rlist.items():
+        if n == k8s.CPU:
+            acc[abi.RES_CPU] += q.milli_value()
+        elif n == k8s.MEMORY:
+            acc[abi.RES_MEM] += q.value()
+        elif n == k8s.EPHEMERAL:
+            acc[abi.RES_EPH] += q.value()
+        elif n == k8s.PODS:
+            pass
+        elif _is_scalar(n):
+            if n not in _SCALAR_FIT:
+                raise MarshalError(f"scalar resource {n!r} is not supported by the engine")
+            acc[_SCALAR_FIT[n]] += q.value()
+            present.add(n)
+
+
+def _resource_setmax(acc: List[int], present: Set[str], rlist: k8s.ResourceList):
+    """(upstream) framework.Resource.SetMaxResource."""
+    for n, q in rlist.items():
+        if n == k8s.CPU:
+            acc[abi.RES_CPU] = max(acc[abi.RES_CPU], q.milli_value())
+        elif n == k8s.MEMORY:
+            acc[abi.RES_MEM] = max(acc[abi.RES_MEM], q.value())
+        elif n == k8s.EPHEMERAL:
+            acc[abi.RES_EPH] = max(acc[abi.RES_EPH], q.value())
+        elif n == k8s.PODS:
+            pass
+        elif _is_scalar(n):
+            if n not in _SCALAR_FIT:
+                raise MarshalError(f"scalar resource {n!r} is not supported by the engine")
+            i = _SCALAR_FIT[n]
+            acc[i] = max(acc[i], q.value())
+            present.add(n)
+
+
+def fit_request(pod: k8s.Pod) -> Tuple[List[int], Set[str]]:
+    """(upstream) noderesources computePodResourceRequest: max(sum containers, each init) + overhead.
+    UPSTREAM-ASSUMED."""
+    acc = [0] * abi.NRES
+    present: Set[str] = set()
+    for c in pod.containers:
+        _resource_add(acc, present, c.requests)
+    for c in pod.init_containers:
+        _resource_setmax(acc, present, c.requests)
+    if pod.overhead:
+        _resource_add(acc, present, pod.overhead)
+    return acc, present
+
+
+def _nonzero(rlist: k8s.ResourceList) -> Tuple[int, int]:
+    """(upstream) schedutil.GetNonzeroRequests: unset cpu/memory -> 100m / 200MiB."""
+    cpu = rlist[k8s.CPU].milli_value() if k8s.CPU in rlist else NONZERO_DEFAULT_MILLI_CPU
+    mem = rlist[k8s.MEMORY].value() if k8s.MEMORY in rlist else NONZERO_DEFAULT_MEMORY
+    return cpu, mem
+
+
+def nonzero_request(pod: k8s.Pod) -> Tuple[int, int]:
+    """(upstream) framework calculateResource non0CPU/non0Mem (== resource_allocation
+    calculatePodResourceRequest with nonZero=true for cpu/memory). UPSTREAM-ASSUMED."""
+    cpu = mem = 0
+    for c in pod.containers:
+        a, b = _nonzero(c.requests)
+        cpu += a
+        mem += b
+    for c in pod.init_containers:
+        a, b = _nonzero(c.requests)
+        cpu, mem = max(cpu, a), max(mem, b)
+    if pod.overhead:
+        if k8s.CPU in pod.overhead:
+            cpu += pod.overhead[k8s.CPU].milli_value()
+        if k8s.MEMORY in pod.overhead:
+            mem += pod.overhead[k8s.MEMORY].value()
+    return cpu, mem
+
+
+def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """One koordhip_pod record for `pod` (the per-pod PreFilter products)."""
+    p = profile.resolved()
+    rec = out if out is not None else pod_array(1)[0]
+    req, present = fit_request(pod)
+    rec["req"][:] = req
+    nzc, nzm = nonzero_request(pod)
+    rec["nz_cpu_m"], rec["nz_mem"] = nzc, nzm
+    est = estimate_pod(pod, p.loadaware)
+    rec["est_cpu"] = est.get(k8s.CPU, 0)
+    rec["est_mem"] = est.get(k8s.MEMORY, 0)
+    flags = 0
+    if k8s.priority_class(pod) == k8s.PRIORITY_PROD:
+        flags |= abi.POD_PROD
+    if k8s.is_daemonset_pod(pod):
+        flags |= abi.POD_DAEMONSET
+    if req[abi.RES_CPU] or req[abi.RES_MEM] or req[abi.RES_EPH] or present:
+        flags |= abi.POD_HAS_REQ
+    if k8s.BATCH_CPU in present:
+        flags |= abi.POD_REQ_BCPU
+    if k8s.BATCH_MEMORY in present:
+        flags |= abi.POD_REQ_BMEM
+    rec["flags"] = flags
+    return rec
+
+
+def pod_records(pods: Iterable[k8s.Pod], profile: Profile) -> np.ndarray:
+    pods = list(pods)
+    arr = pod_array(len(pods))
+    for i, p in enumerate(pods):
+        pod_record(p, profile, arr[i])
+    return arr
+
+
+# ---------------------------------------------------------------------------
+# Node side
+
+@dataclass
+class AssignedPod:
+    """podAssignCache entry (pod_assign_cache.go:40-43)."""
+    pod: k8s.Pod
+    timestamp: float
+
+
+@dataclass
+class ClusterState:
+    """What the plugins read at a scheduling cycle: nodes, NodeMetrics, the pod
+    lister, the NodeInfo pods and the LoadAware podAssignCache."""
+    nodes: List[k8s.Node] = field(default_factory=list)
+    node_metrics: Dict[str, k8s.NodeMetric] = field(default_factory=dict)
+    pods: Dict[str, k8s.Pod] = field(default_factory=dict)            # lister, key ns/name
+    node_pods: Dict[str, List[k8s.Pod]] = field(default_factory=dict)  # NodeInfo.Pods per node
+    assigned: Dict[str, List[AssignedPod]] = field(default_factory=dict)
+
+
+def estimate_node(node: k8s.Node) -> k8s.ResourceList:
+    """EstimateNode, default_estimator.go:110-129 (raw-allocatable override)."""
+    raw = node.annotations.get(k8s.ANNOTATION_NODE_RAW_ALLOCATABLE)
+    if raw is None:
+        return node.allocatable
+    try:
+        parsed = {k: k8s.Quantity(v) for k, v in json.loads(raw).items()}
+    except Exception:  # json error -> Allocatable
+        return node.allocatable
+    if not parsed:
+        return node.allocatable
+    out = dict(node.allocatable)
+    out.update(parsed)
+    return out
+
+
+def is_node_metric_expired(nm: Optional[k8s.NodeMetric], expiration_s: int, now: float) -> bool:
+    """isNodeMetricExpired, helper.go:36-41."""
+    return nm is None or nm.update_time is None or (expiration_s > 0 and now - nm.update_time >= expiration_s)
+
+
+def get_target_aggregated_usage(nm: k8s.NodeMetric, duration_s: Optional[float], agg_type: str):
+    """getTargetAggregatedUsage, helper.go:58-90."""
+    if not nm.node_metric_present or not nm.aggregated:
+        return None
+    if not duration_s:
+        max_d, max_i = 0.0, 0
+        for i, v in enumerate(nm.aggregated):
+            if v.duration_s > max_d:
+                max_d, max_i = v.duration_s, i
+        usage = nm.aggregated[max_i].usage.get(agg_type)
+        return usage if usage else None
+    for v in nm.aggregated:
+        if v.duration_s == duration_s:
+            usage = v.usage.get(agg_type)
+            if usage:
+                return usage
+    return None
+
+
+@dataclass
+class _FilterProfile:
+    usage_thresholds: Dict[str, int]
+    prod_usage_thresholds: Dict[str, int]
+    aggregated: Optional[Tuple[Dict[str, int], str, float]]  # (thresholds, type, duration)
+
+
+def usage_thresholds_filter_profile(node: k8s.Node, args: LoadAwareSchedulingArgs) -> _FilterProfile:
+    """generateUsageThresholdsFilterProfile, helper.go:102-140 (+ GetCustomUsageThresholds load_aware.go:51-62)."""
+    agg_args = args.aggregated
+    filter_with_agg = agg_args is not None and len(agg_args.usage_thresholds) > 0 and agg_args.usage_aggregation_type != ""
+    default_agg = ((dict(agg_args.usage_thresholds), agg_args.usage_aggregation_type,
+                    agg_args.usage_aggregated_duration_s) if filter_with_agg else None)
+    data = node.annotations.get(k8s.ANNOTATION_CUSTOM_USAGE_THRESHOLDS)
+    custom = None
+    if data is not None:
+        try:
+            custom = json.loads(data)
+            if not isinstance(custom, dict):
+                custom = None
+        except Exception:
+            custom = None
+    if data is not None and custom is None:  # unmarshal error
+        return _FilterProfile(dict(args.usage_thresholds), dict(args.prod_usage_thresholds), default_agg)
+    custom = custom or {}
+    ut = custom.get("usageThresholds") or {}
+    pt = custom.get("prodUsageThresholds") or {}
+    ag = custom.get("aggregatedUsage")
+    if not ut:
+        ut = dict(args.usage_thresholds)
+    if not pt:
+        pt = dict(args.prod_usage_thresholds)
+    agg = None
+    if ag is not None:
+        at = ag.get("usageThresholds") or {}
+        typ = ag.get("usageAggregationType") or ""
+        if at and typ:
+            agg = (dict(at), typ, _parse_duration(ag.get("usageAggregatedDuration")))
+    if agg is None and filter_with_agg:
+        agg = default_agg
+    return _FilterProfile({k: int(v) for k, v in ut.items()}, {k: int(v) for k, v in pt.items()}, agg)
+
+
+def _parse_duration(v) -> float:
+    if v is None:
+        return 0.0
+    if isinstance(v, (int, float)):
+        return float(v)
+    import re
+    total = 0.0
+    for num, unit in re.findall(r"([0-9.]+)(ns|us|ms|s|m|h)", v):
+        total += float(num) * {"ns": 1e-9, "us": 1e-6, "ms": 1e-3, "s": 1, "m": 60, "h": 3600}[unit]
+    return total
+
+
+def build_pod_metric_map(cluster: ClusterState, nm: k8s.NodeMetric, filter_prod: bool) -> Dict[str, k8s.ResourceList]:
+    """buildPodMetricMap, helper.go:153-170."""
+    out = {}
+    for pm in nm.pods_metric:
+        pod = cluster.pods.get(f"{pm.namespace}/{pm.name}")
+        if pod is None:
+            continue
+        if filter_prod and k8s.priority_class(pod) != k8s.PRIORITY_PROD:
+            continue
+        out[f"{pm.namespace}/{pm.name}"] = pm.usage
+    return out
+
+
+def _sum_rl(dst: Dict[str, k8s.Quantity], src: k8s.ResourceList):
+    for n, q in src.items():
+        dst[n] = dst.get(n, k8s.Quantity(0)) + q
+
+
+def estimated_assigned_pod_used(cluster: ClusterState, node_name: str, nm: k8s.NodeMetric, pod_metrics,
+                                filter_prod: bool, args: LoadAwareSchedulingArgs, score_agg_nil: bool):
+    """estimatedAssignedPodUsed, load_aware.go:337-376."""
+    est_used: Dict[str, int] = {}
+    est_pods: Set[str] = set()
+    update_t = nm.update_time if nm.update_time is not None else float("-inf")
+    interval = nm.report_interval_s if nm.report_interval_s is not None else DEFAULT_REPORT_INTERVAL_S
+    for info in cluster.assigned.get(node_name, []):
+        if filter_prod and k8s.priority_class(info.pod) != k8s.PRIORITY_PROD:
+            continue
+        name = info.pod.key
+        usage = pod_metrics.get(name) or {}
+        missed = info.timestamp > update_t                                         # helper.go:50-52
+        in_interval = info.timestamp < update_t and (update_t - info.timestamp) < interval  # helper.go:54-56
+        if not usage or missed or in_interval or score_agg_nil:
+            est = estimate_pod(info.pod, args)
+            for r, v in est.items():
+                if r in usage:
+                    u = k8s.resource_value(r, usage[r])
+                    if u > v:
+                        v = u
+                est_used[r] = est_used.get(r, 0) + v
+            est_pods.add(name)
+    return est_used, est_pods
+
+
+def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, profile: Profile, now: float):
+    """Fill row i of `table` from the objects (Fit accounting + LoadAware state)."""
+    p = profile.resolved()
+    args = p.loadaware
+    t = table.cols
+    # ---- Fit: Allocatable / Requested / NonZeroRequested / len(Pods)
+    alloc = node.allocatable
+    t["alloc0"][i] = alloc[k8s.CPU].milli_value() if k8s.CPU in alloc else 0
+    t["alloc1"][i] = alloc[k8s.MEMORY].value() if k8s.MEMORY in alloc else 0
+    t["alloc2"][i] = alloc[k8s.EPHEMERAL].value() if k8s.EPHEMERAL in alloc else 0
+    t["alloc3"][i] = alloc[k8s.BATCH_CPU].value() if k8s.BATCH_CPU in alloc else 0
+    t["alloc4"][i] = alloc[k8s.BATCH_MEMORY].value() if k8s.BATCH_MEMORY in alloc else 0
+    t["alloc_pods"][i] = alloc[k8s.PODS].value() if k8s.PODS in alloc else 0
+    req = [0] * abi.NRES
+    nzc = nzm = 0
+    pods_on_node = cluster.node_pods.get(node.name, [])
+    for pod in pods_on_node:
+        r, _ = fit_request(pod)
+        for k in range(abi.NRES):
+            req[k] += r[k]
+        a, b = nonzero_request(pod)
+        nzc += a
+        nzm += b
+    for k in range(abi.NRES):
+        t[f"requested{k}"][i] = req[k]
+    t["nz_cpu_m"][i], t["nz_mem"][i] = nzc, nzm
+    t["npods"][i] = len(pods_on_node)
+    # ---- LoadAware
+    est_alloc = estimate_node(node)
+    t["la_alloc_cpu_m"][i] = est_alloc[k8s.CPU].milli_value() if k8s.CPU in est_alloc else 0
+    t["la_alloc_mem"][i] = est_alloc[k8s.MEMORY].value() if k8s.MEMORY in est_alloc else 0
+    t["laf_total_m0"][i] = t["la_alloc_cpu_m"][i]
+    t["laf_total_m1"][i] = est_alloc[k8s.MEMORY].milli_value() if k8s.MEMORY in est_alloc else 0
+    nm = cluster.node_metrics.get(node.name)
+    flags = 0
+    for c in ("la_used_cpu_m", "la_used_mem", "la_used_prod_cpu_m", "la_used_prod_mem", "laf_used_m0",
+              "laf_used_m1", "laf_prod_used_m0", "laf_prod_used_m1", "laf_thr0", "laf_thr1",
+              "laf_prod_thr0", "laf_prod_thr1"):
+        t[c][i] = 0
+    if nm is not None:
+        flags |= abi.LA_HAS_METRIC
+        expired = is_node_metric_expired(nm, args.node_metric_expiration_seconds, now)
+        if args.filter_expired_node_metrics and args.node_metric_expiration_seconds is not None and expired:
+            flags |= abi.LA_FILTER_SKIP
+        if args.node_metric_expiration_seconds is not None and expired:
+            flags |= abi.LA_SCORE_EXPIRED
+        fp = usage_thresholds_filter_profile(node, args)
+        thresholds = fp.aggregated[0] if fp.aggregated else fp.usage_thresholds
+        _check_thr_keys(thresholds)
+        _check_thr_keys(fp.prod_usage_thresholds)
+        t["laf_thr0"][i] = thresholds.get(k8s.CPU, 0)
+        t["laf_thr1"][i] = thresholds.get(k8s.MEMORY, 0)
+        t["laf_prod_thr0"][i] = fp.prod_usage_thresholds.get(k8s.CPU, 0)
+        t["laf_prod_thr1"][i] = fp.prod_usage_thresholds.get(k8s.MEMORY, 0)
+        if fp.prod_usage_thresholds:
+            flags |= abi.LA_PROD_MODE
+        if nm.pods_metric:
+            flags |= abi.LA_HAS_PODS_METRIC
+        if nm.node_metric_present:
+            if fp.aggregated:
+                flags |= abi.LA_AGGREGATED
+                usage = get_target_aggregated_usage(nm, fp.aggregated[2], fp.aggregated[1])
+            else:
+                usage = nm.node_usage if nm.node_usage is not None else {}
+            if usage is not None:
+                flags |= abi.LA_FILTER_USAGE
+                t["laf_used_m0"][i] = usage[k8s.CPU].milli_value() if k8s.CPU in usage else 0
+                t["laf_used_m1"][i] = usage[k8s.MEMORY].milli_value() if k8s.MEMORY in usage else 0
+        # prod pods' usage for filterProdUsage (load_aware.go:232-233)
+        prod_metrics = build_pod_metric_map(cluster, nm, True)
+        prod_sum: Dict[str, k8s.Quantity] = {}
+        for u in prod_metrics.values():
+            _sum_rl(prod_sum, u)
+        t["laf_prod_used_m0"][i] = prod_sum[k8s.CPU].milli_value() if k8s.CPU in prod_sum else 0
+        t["laf_prod_used_m1"][i] = prod_sum[k8s.MEMORY].milli_value() if k8s.MEMORY in prod_sum else 0
+        # ---- Score base, non-prod path (load_aware.go:292-327)
+        agg = args.aggregated
+        score_with_agg = agg is not None and agg.score_aggregation_type != ""
+        score_usage = None
+        if nm.node_metric_present:
+            score_usage = (get_target_aggregated_usage(nm, agg.score_aggregated_duration_s, agg.score_aggregation_type)
+                           if score_with_agg else (nm.node_usage if nm.node_usage is not None else {}))
+        score_agg_nil = score_with_agg and score_usage is None
+        for prod_path in (False, True):
+            pm = build_pod_metric_map(cluster, nm, prod_path)
+            est_used, est_pods = estimated_assigned_pod_used(cluster, node.name, nm, pm, prod_path, args, score_agg_nil)
+            pod_usages: Dict[str, k8s.Quantity] = {}
+            est_usages: Dict[str, k8s.Quantity] = {}
+            for name, u in pm.items():
+                _sum_rl(est_usages if name in est_pods else pod_usages, u)
+            base = dict(est_used)
+            if prod_path:
+                for r, q in pod_usages.items():
+                    base[r] = base.get(r, 0) + k8s.resource_value(r, q)
+            elif nm.node_metric_present and score_usage is not None:
+                for r, q in score_usage.items():
+                    e = est_usages.get(r)
+                    if e is not None and not e.is_zero() and q.cmp(e) >= 0:
+                        q = q - e
+                    base[r] = base.get(r, 0) + k8s.resource_value(r, q)
+            pre = "la_used_prod_" if prod_path else "la_used_"
+            t[pre + "cpu_m"][i] = base.get(k8s.CPU, 0)
+            t[pre + "mem"][i] = base.get(k8s.MEMORY, 0)
+    t["la_flags"][i] = flags
+
+
+def _check_thr_keys(th: Dict[str, int]):
+    for k in th:
+        if k not in (k8s.CPU, k8s.MEMORY):
+            raise MarshalError(f"usage threshold on {k!r} is not supported by the engine (cpu, memory only)")
+
+
+def build_table(cluster: ClusterState, profile: Profile, now: float) -> NodeTable:
+    t = NodeTable.empty(len(cluster.nodes))
+    t.names = [n.name for n in cluster.nodes]
+    for i, node in enumerate(cluster.nodes):
+        node_row(t, i, node, cluster, profile, now)
+    return t

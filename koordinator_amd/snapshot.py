@@ -1,0 +1,107 @@
+"""Columnar node snapshot (SoA) and pod records, in the exact byte layout of
+include/koordhip.h.  Both the HIP engine and the test oracle consume these
+arrays, so a snapshot is marshalled once and evaluated by both.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List
+
+import numpy as np
+
+from . import abi
+
+I64_COLS = (
+    [f"alloc{r}" for r in range(abi.NRES)]
+    + [f"requested{r}" for r in range(abi.NRES)]
+    + ["nz_cpu_m", "nz_mem", "la_alloc_cpu_m", "la_alloc_mem", "la_used_cpu_m", "la_used_mem",
+       "la_used_prod_cpu_m", "la_used_prod_mem",
+       "laf_used_m0", "laf_used_m1", "laf_total_m0", "laf_total_m1", "laf_prod_used_m0", "laf_prod_used_m1",
+       "laf_thr0", "laf_thr1", "laf_prod_thr0", "laf_prod_thr1"]
+)
+I32_COLS = ["alloc_pods", "npods"]
+U8_COLS = ["la_flags"]
+ALL_COLS = I64_COLS + I32_COLS + U8_COLS
+
+
+def _dtype(col: str):
+    if col in I32_COLS:
+        return np.int32
+    if col in U8_COLS:
+        return np.uint8
+    return np.int64
+
+
+@dataclass
+class NodeTable:
+    """n rows of the koordhip_node_soa columns (numpy, C-contiguous)."""
+    n: int
+    cols: Dict[str, np.ndarray] = field(default_factory=dict)
+    names: List[str] = field(default_factory=list)
+
+    @classmethod
+    def empty(cls, n: int) -> "NodeTable":
+        t = cls(n=n)
+        for c in ALL_COLS:
+            t.cols[c] = np.zeros(n, dtype=_dtype(c))
+        t.names = [f"node-{i}" for i in range(n)]
+        return t
+
+    def __getitem__(self, c: str) -> np.ndarray:
+        return self.cols[c]
+
+    def rows(self, idx) -> "NodeTable":
+        idx = np.asarray(idx, dtype=np.int64)
+        t = NodeTable(n=len(idx))
+        for c in ALL_COLS:
+            t.cols[c] = np.ascontiguousarray(self.cols[c][idx])
+        t.names = [self.names[i] for i in idx] if self.names else []
+        return t
+
+    def copy(self) -> "NodeTable":
+        t = NodeTable(n=self.n)
+        t.cols = {k: v.copy() for k, v in self.cols.items()}
+        t.names = list(self.names)
+        return t
+
+    def as_soa(self) -> abi.KoordhipNodeSoa:
+        """Build a koordhip_node_soa pointing at this table's arrays (keep `self` alive)."""
+        for c in ALL_COLS:
+            a = self.cols[c]
+            if not a.flags.c_contiguous or a.dtype != _dtype(c) or a.shape != (self.n,):
+                self.cols[c] = np.ascontiguousarray(a, dtype=_dtype(c))
+        s = abi.KoordhipNodeSoa()
+        p64 = lambda c: self.cols[c].ctypes.data_as(C.POINTER(C.c_int64))
+        p32 = lambda c: self.cols[c].ctypes.data_as(C.POINTER(C.c_int32))
+        for r in range(abi.NRES):
+            s.alloc[r] = p64(f"alloc{r}")
+            s.requested[r] = p64(f"requested{r}")
+        s.alloc_pods = p32("alloc_pods")
+        s.npods = p32("npods")
+        for c in ["nz_cpu_m", "nz_mem", "la_alloc_cpu_m", "la_alloc_mem", "la_used_cpu_m", "la_used_mem",
+                  "la_used_prod_cpu_m", "la_used_prod_mem"]:
+            setattr(s, c, p64(c))
+        for k in range(2):
+            s.laf_used_m[k] = p64(f"laf_used_m{k}")
+            s.laf_total_m[k] = p64(f"laf_total_m{k}")
+            s.laf_prod_used_m[k] = p64(f"laf_prod_used_m{k}")
+            s.laf_thr[k] = p64(f"laf_thr{k}")
+            s.laf_prod_thr[k] = p64(f"laf_prod_thr{k}")
+        s.la_flags = self.cols["la_flags"].ctypes.data_as(C.POINTER(C.c_uint8))
+        return s
+
+    def nbytes(self) -> int:
+        return sum(v.nbytes for v in self.cols.values())
+
+
+def concat(tables: List[NodeTable]) -> NodeTable:
+    t = NodeTable(n=sum(x.n for x in tables))
+    for c in ALL_COLS:
+        t.cols[c] = np.concatenate([x.cols[c] for x in tables])
+    t.names = [nm for x in tables for nm in x.names]
+    return t
+
+
+def pod_array(n: int) -> np.ndarray:
+    return np.zeros(n, dtype=abi.POD_DTYPE)

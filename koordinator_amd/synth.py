@@ -1,0 +1,199 @@
+"""Seeded synthetic clusters and pod streams.
+
+One generator, shared by the HIP engine and the oracle: it emits the SoA node
+table and koordhip_pod records directly (vectorised, so 200k-node snapshots
+build in well under a second).  All randomness is splitmix64 with the seed
+0x6B6F6F7264 ("koord") by default, so every run of every config sees the same
+bytes.  `cluster_objects` / `pod_objects` rebuild the same rows as Kubernetes
+objects for the marshaller cross-check (tests/test_synth.py).
+
+Units: cpu milli-cores, memory bytes, batch-cpu Value() (milli-core count).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Tuple
+
+import numpy as np
+
+from . import abi, k8s
+from .config import Profile
+from .snapshot import NodeTable, pod_array
+
+SEED = 0x6B6F6F7264
+GI = 1 << 30
+MI = 1 << 20
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(seed: int, n: int, stream: int) -> np.ndarray:
+    """n splitmix64 outputs of the sequence seeded by (seed, stream)."""
+    with np.errstate(over="ignore"):
+        base = np.uint64((seed ^ (stream * 0x9E3779B97F4A7C15)) & 0xFFFFFFFFFFFFFFFF)
+        z = base + (np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def uniform(seed: int, n: int, stream: int) -> np.ndarray:
+    """U[0,1) doubles from the top 53 bits."""
+    return (splitmix64(seed, n, stream) >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def choice(seed: int, n: int, stream: int, values) -> np.ndarray:
+    v = np.asarray(values)
+    idx = (splitmix64(seed, n, stream) % np.uint64(len(v))).astype(np.int64)
+    return v[idx]
+
+
+@dataclass
+class ClusterSpec:
+    n_nodes: int
+    seed: int = SEED
+    metric_missing_frac: float = 0.02
+    pods_allocatable: int = 110
+
+
+def make_cluster(spec: ClusterSpec, profile: Profile) -> NodeTable:
+    """Node shapes / NodeMetric / Requested per SURVEY.md §8(d)."""
+    n, s = spec.n_nodes, spec.seed
+    la = profile.resolved().loadaware
+    t = NodeTable.empty(n)
+    cpu = choice(s, n, 1, [32, 64, 96, 128]).astype(np.int64) * 1000
+    mem = choice(s, n, 2, [128, 256, 512, 1024]).astype(np.int64) * GI
+    bcpu = np.floor(cpu * (0.2 + 0.4 * uniform(s, n, 3))).astype(np.int64)
+    bmem = np.floor(mem * (0.2 + 0.4 * uniform(s, n, 4))).astype(np.int64)
+    t["alloc0"][:] = cpu
+    t["alloc1"][:] = mem
+    t["alloc2"][:] = 0
+    t["alloc3"][:] = bcpu
+    t["alloc4"][:] = bmem
+    t["alloc_pods"][:] = spec.pods_allocatable
+    rc = np.floor(cpu * 0.5 * uniform(s, n, 5)).astype(np.int64)
+    rm = np.floor(mem * 0.5 * uniform(s, n, 6)).astype(np.int64)
+    t["requested0"][:] = rc
+    t["requested1"][:] = rm
+    t["requested3"][:] = np.floor(bcpu * 0.5 * uniform(s, n, 7)).astype(np.int64)
+    t["requested4"][:] = np.floor(bmem * 0.5 * uniform(s, n, 8)).astype(np.int64)
+    t["nz_cpu_m"][:] = rc
+    t["nz_mem"][:] = rm
+    t["npods"][:] = (splitmix64(s, n, 9) % np.uint64(41)).astype(np.int32)
+    # NodeMetric: usage cpu U[0,0.8]*alloc, mem U[0.1,0.9]*alloc, never expired, 2% missing
+    ucpu = np.floor(cpu * 0.8 * uniform(s, n, 10)).astype(np.int64)
+    umem = np.floor(mem * (0.1 + 0.8 * uniform(s, n, 11))).astype(np.int64)
+    has = uniform(s, n, 12) >= spec.metric_missing_frac
+    t["la_alloc_cpu_m"][:] = cpu
+    t["la_alloc_mem"][:] = mem
+    t["la_used_cpu_m"][:] = np.where(has, ucpu, 0)
+    t["la_used_mem"][:] = np.where(has, umem, 0)
+    t["la_used_prod_cpu_m"][:] = 0
+    t["la_used_prod_mem"][:] = 0
+    t["laf_used_m0"][:] = np.where(has, ucpu, 0)          # cpu MilliValue
+    t["laf_used_m1"][:] = np.where(has, umem * 1000, 0)   # memory MilliValue
+    t["laf_total_m0"][:] = cpu
+    t["laf_total_m1"][:] = mem * 1000
+    t["laf_thr0"][:] = np.where(has, la.usage_thresholds.get(k8s.CPU, 0), 0)
+    t["laf_thr1"][:] = np.where(has, la.usage_thresholds.get(k8s.MEMORY, 0), 0)
+    flags = np.where(has, abi.LA_HAS_METRIC | abi.LA_FILTER_USAGE, 0)
+    if la.prod_usage_thresholds:
+        flags = flags | np.where(has, abi.LA_PROD_MODE, 0)
+        t["laf_prod_thr0"][:] = np.where(has, la.prod_usage_thresholds.get(k8s.CPU, 0), 0)
+        t["laf_prod_thr1"][:] = np.where(has, la.prod_usage_thresholds.get(k8s.MEMORY, 0), 0)
+    t["la_flags"][:] = flags.astype(np.uint8)
+    return t
+
+
+@dataclass
+class StreamSpec:
+    n_pods: int
+    be_frac: float = 0.0
+    seed: int = SEED
+
+
+LS_CPU = [250, 500, 1000, 2000, 4000]
+LS_MEM = [256 * MI, 512 * MI, 1 * GI, 2 * GI, 4 * GI, 8 * GI]
+BE_CPU = [500, 1000, 2000, 4000]
+BE_MEM = [512 * MI, 1 * GI, 2 * GI, 4 * GI, 8 * GI]
+
+
+def _round_half_away(x: np.ndarray) -> np.ndarray:
+    f = np.floor(x)
+    return (f + ((x - f) >= 0.5)).astype(np.int64)
+
+
+def make_pods(spec: StreamSpec, profile: Profile) -> np.ndarray:
+    """LS: prod, Burstable, 50% with limit = 2x request; BE: koord.sh/qosClass=BE,
+    priority 5000, batch-cpu/batch-memory with limit = request."""
+    n, s = spec.n_pods, spec.seed + 1
+    la = profile.resolved().loadaware
+    fc = la.estimated_scaling_factors.get(k8s.CPU, 85)
+    fm = la.estimated_scaling_factors.get(k8s.MEMORY, 70)
+    pods = pod_array(n)
+    be = uniform(s, n, 20) < spec.be_frac
+    burst = uniform(s, n, 21) < 0.5
+    ls_cpu = choice(s, n, 22, LS_CPU).astype(np.int64)
+    ls_mem = choice(s, n, 23, LS_MEM).astype(np.int64)
+    be_cpu = choice(s, n, 24, BE_CPU).astype(np.int64)
+    be_mem = choice(s, n, 25, BE_MEM).astype(np.int64)
+    # LS (prod): requests cpu/mem; limit = 2x request when bursting else = request
+    lim_mult = np.where(burst, 2, 1)
+    ls_est_cpu = np.where(burst, ls_cpu * 2, _round_half_away(ls_cpu.astype(np.float64) * fc / 100))
+    ls_est_cpu = np.minimum(ls_est_cpu, ls_cpu * lim_mult)
+    ls_est_mem = np.where(burst, ls_mem * 2, _round_half_away(ls_mem.astype(np.float64) * fm / 100))
+    ls_est_mem = np.minimum(ls_est_mem, ls_mem * lim_mult)
+    be_est_cpu = np.minimum(_round_half_away(be_cpu.astype(np.float64) * fc / 100), be_cpu)
+    be_est_mem = np.minimum(_round_half_away(be_mem.astype(np.float64) * fm / 100), be_mem)
+    req = pods["req"]
+    req[:, abi.RES_CPU] = np.where(be, 0, ls_cpu)
+    req[:, abi.RES_MEM] = np.where(be, 0, ls_mem)
+    req[:, abi.RES_BCPU] = np.where(be, be_cpu, 0)
+    req[:, abi.RES_BMEM] = np.where(be, be_mem, 0)
+    # BE pods request no cpu/memory -> non-zero defaults 100m / 200MiB
+    pods["nz_cpu_m"] = np.where(be, 100, ls_cpu)
+    pods["nz_mem"] = np.where(be, 200 * MI, ls_mem)
+    pods["est_cpu"] = np.where(be, be_est_cpu, ls_est_cpu)
+    pods["est_mem"] = np.where(be, be_est_mem, ls_est_mem)
+    pods["flags"] = np.where(be, abi.POD_HAS_REQ | abi.POD_REQ_BCPU | abi.POD_REQ_BMEM,
+                             abi.POD_PROD | abi.POD_HAS_REQ).astype(np.uint32)
+    return pods
+
+
+def pod_objects(spec: StreamSpec, limit: int = None) -> List[k8s.Pod]:
+    """The same stream as Kubernetes objects (for the marshaller cross-check)."""
+    n, s = spec.n_pods, spec.seed + 1
+    be = uniform(s, n, 20) < spec.be_frac
+    burst = uniform(s, n, 21) < 0.5
+    ls_cpu = choice(s, n, 22, LS_CPU)
+    ls_mem = choice(s, n, 23, LS_MEM)
+    be_cpu = choice(s, n, 24, BE_CPU)
+    be_mem = choice(s, n, 25, BE_MEM)
+    out = []
+    for i in range(n if limit is None else min(n, limit)):
+        if be[i]:
+            r = {k8s.BATCH_CPU: k8s.Q(int(be_cpu[i])), k8s.BATCH_MEMORY: k8s.Q(int(be_mem[i]))}
+            out.append(k8s.Pod(name=f"be-{i}", labels={k8s.LABEL_POD_QOS: k8s.QOS_BE}, priority=5000,
+                               containers=[k8s.Container(requests=dict(r), limits=dict(r))]))
+        else:
+            m = 2 if burst[i] else 1
+            r = {k8s.CPU: k8s.Q(f"{int(ls_cpu[i])}m"), k8s.MEMORY: k8s.Q(int(ls_mem[i]))}
+            lim = {k8s.CPU: k8s.Q(f"{int(ls_cpu[i]) * m}m"), k8s.MEMORY: k8s.Q(int(ls_mem[i]) * m)}
+            out.append(k8s.Pod(name=f"ls-{i}", priority=9500, containers=[k8s.Container(requests=r, limits=lim)]))
+    return out
+
+
+# Benchmark / parity configurations (BASELINE.json "configs")
+CONFIGS = {
+    1: dict(nodes=500, pods=1000, be_frac=0.0),
+    2: dict(nodes=5000, pods=10000, be_frac=0.0),
+    4: dict(nodes=50000, pods=100000, be_frac=0.3),
+    5: dict(nodes=200000, pods=100000, be_frac=0.3),
+}
+
+
+def config_workload(cfg_id: int, profile: Profile, n_nodes: int = None, n_pods: int = None) -> Tuple[NodeTable, np.ndarray]:
+    c = CONFIGS[cfg_id]
+    table = make_cluster(ClusterSpec(n_nodes or c["nodes"]), profile)
+    pods = make_pods(StreamSpec(n_pods or c["pods"], be_frac=c["be_frac"]), profile)
+    return table, pods

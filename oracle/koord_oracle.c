@@ -1,0 +1,470 @@
+/*
+ * koord_oracle.c -- TEST INFRASTRUCTURE (see koord_oracle.h).  A plain-C
+ * restatement of the reference algorithm, one function per reference rule,
+ * each citing the koordinator file:line it follows.  It is the checker for the
+ * HIP path and the timed `cpu_baseline` of bench.py; it is never linked into
+ * the product.
+ *
+ * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math, so the
+ * f64 usage arithmetic matches Go's IEEE float64 exactly).
+ */
+#define _GNU_SOURCE
+#include "koord_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Scalar rules                                                              */
+/* ------------------------------------------------------------------------ */
+
+/* load_aware.go:214 and :248:
+ *   usage := int64(math.Round(float64(used.MilliValue()) / float64(total.MilliValue()) * 100))
+ * math.Round is half-away-from-zero == C round(). */
+int64_t orc_usage_percent(int64_t used_milli, int64_t total_milli) {
+  double u = (double)used_milli / (double)total_milli;
+  u = u * 100.0;
+  return (int64_t)round(u);
+}
+
+/* load_aware.go:388-397 leastRequestedScore; identical rule in (upstream)
+ * noderesources/least_allocated.go and nodenumaresource/least_allocated.go:49-58. */
+int64_t orc_least_requested(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * 100) / capacity; /* framework.MaxNodeScore = 100 */
+}
+
+/* ------------------------------------------------------------------------ */
+/* LoadAware Filter (static per snapshot)                                    */
+/* ------------------------------------------------------------------------ */
+
+/* filterNodeUsage, load_aware.go:173-224: per resource, skip threshold 0
+ * (:186-188), skip zero total (:194-197), skip absent usage source (:209-211),
+ * fail when usage >= threshold (:215). */
+static int la_usage_ok(const koordhip_node_soa *s, int32_t i) {
+  if (!(s->la_flags[i] & KOORDHIP_LA_FILTER_USAGE)) return 1; /* :174-176 / :209-211 */
+  for (int r = 0; r < 2; r++) {
+    int64_t thr = s->laf_thr[r][i];
+    if (thr == 0) continue;
+    int64_t total = s->laf_total_m[r][i];
+    if (total == 0) continue;
+    if (orc_usage_percent(s->laf_used_m[r][i], total) >= thr) return 0;
+  }
+  return 1;
+}
+
+/* filterProdUsage, load_aware.go:226-254. */
+static int la_prod_ok(const koordhip_node_soa *s, int32_t i) {
+  if (!(s->la_flags[i] & KOORDHIP_LA_HAS_PODS_METRIC)) return 1; /* :227-229 */
+  for (int r = 0; r < 2; r++) {
+    int64_t thr = s->laf_prod_thr[r][i];
+    if (thr == 0) continue;
+    int64_t total = s->laf_total_m[r][i];
+    if (total == 0) continue;
+    if (orc_usage_percent(s->laf_prod_used_m[r][i], total) >= thr) return 0;
+  }
+  return 1;
+}
+
+/* Filter, load_aware.go:123-171, resolved per node for {non-prod, prod} pods
+ * (the DaemonSet bypass :129-131 is per pod, applied in orc_la_filter). */
+void orc_la_flags(const koordhip_node_soa *s, int32_t n, uint8_t *out) {
+  for (int32_t i = 0; i < n; i++) {
+    uint8_t f = s->la_flags[i];
+    uint8_t o = 0;
+    if (!(f & KOORDHIP_LA_HAS_METRIC) || (f & KOORDHIP_LA_FILTER_SKIP)) {
+      o |= ORC_LA_OK_NONPROD | ORC_LA_OK_PROD; /* :138-140, :144-147 */
+    } else {
+      int np = la_usage_ok(s, i);              /* :155-168 */
+      int p = (f & KOORDHIP_LA_PROD_MODE) ? la_prod_ok(s, i) : np; /* :150-154 */
+      if (np) o |= ORC_LA_OK_NONPROD;
+      if (p) o |= ORC_LA_OK_PROD;
+    }
+    /* Score returns 0 for a missing or expired NodeMetric, load_aware.go:278-289 */
+    if (!(f & KOORDHIP_LA_HAS_METRIC) || (f & KOORDHIP_LA_SCORE_EXPIRED)) o |= ORC_LA_SCORE_ZERO;
+    out[i] = o;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* State                                                                     */
+/* ------------------------------------------------------------------------ */
+
+static int64_t *dup64(const int64_t *src, int32_t n) {
+  int64_t *d = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  if (!d) return NULL;
+  if (src) memcpy(d, src, sizeof(int64_t) * (size_t)n);
+  else memset(d, 0, sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  return d;
+}
+
+int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
+  memset(st, 0, sizeof(*st));
+  st->n = n;
+  st->soa = soa;
+  st->flags = (uint8_t *)malloc((size_t)(n > 0 ? n : 1));
+  for (int r = 0; r < KOORDHIP_NRES; r++) st->requested[r] = dup64(soa->requested[r], n);
+  st->nz_cpu_m = dup64(soa->nz_cpu_m, n);
+  st->nz_mem = dup64(soa->nz_mem, n);
+  st->npods = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  if (soa->npods) memcpy(st->npods, soa->npods, sizeof(int32_t) * (size_t)n);
+  else memset(st->npods, 0, sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  st->la_used_cpu_m = dup64(soa->la_used_cpu_m, n);
+  st->la_used_mem = dup64(soa->la_used_mem, n);
+  st->la_used_prod_cpu_m = dup64(soa->la_used_prod_cpu_m, n);
+  st->la_used_prod_mem = dup64(soa->la_used_prod_mem, n);
+  if (!st->flags || !st->npods) return -1;
+  orc_la_flags(soa, n, st->flags);
+  return 0;
+}
+
+void orc_state_free(orc_state *st) {
+  free(st->flags);
+  for (int r = 0; r < KOORDHIP_NRES; r++) free(st->requested[r]);
+  free(st->nz_cpu_m);
+  free(st->nz_mem);
+  free(st->npods);
+  free(st->la_used_cpu_m);
+  free(st->la_used_mem);
+  free(st->la_used_prod_cpu_m);
+  free(st->la_used_prod_mem);
+  memset(st, 0, sizeof(*st));
+}
+
+/* ------------------------------------------------------------------------ */
+/* Per-(pod,node) plugin rules                                               */
+/* ------------------------------------------------------------------------ */
+
+/* UPSTREAM-ASSUMED: (upstream) noderesources/fit.go fitsRequest (k8s v1.24.15).
+ * In-reference mirror: pkg/scheduler/plugins/reservation/plugin.go:445-494
+ * (fitsNode with rInfo=nil).  1 = fits. */
+int orc_fit_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  (void)cfg;
+  const koordhip_node_soa *s = st->soa;
+  if ((int64_t)st->npods[i] + 1 > (int64_t)s->alloc_pods[i]) return 0; /* Too many pods */
+  if (!(pod->flags & KOORDHIP_POD_HAS_REQ)) return 1;                   /* all-zero request */
+  for (int r = KOORDHIP_RES_CPU; r <= KOORDHIP_RES_EPH; r++)            /* cpu, memory, ephemeral-storage */
+    if (pod->req[r] > s->alloc[r][i] - st->requested[r][i]) return 0;
+  if ((pod->flags & KOORDHIP_POD_REQ_BCPU) &&
+      pod->req[KOORDHIP_RES_BCPU] > s->alloc[KOORDHIP_RES_BCPU][i] - st->requested[KOORDHIP_RES_BCPU][i])
+    return 0;
+  if ((pod->flags & KOORDHIP_POD_REQ_BMEM) &&
+      pod->req[KOORDHIP_RES_BMEM] > s->alloc[KOORDHIP_RES_BMEM][i] - st->requested[KOORDHIP_RES_BMEM][i])
+    return 0;
+  return 1;
+}
+
+/* UPSTREAM-ASSUMED: (upstream) noderesources/resource_allocation.go score +
+ * calculateResourceAllocatableRequest + least_allocated.go leastResourceScorer.
+ * Koord copy of the same rules: nodenumaresource/scoring.go:191-246 (skip a
+ * scalar the pod does not request :211-215, skip alloc == 0) and
+ * least_allocated.go:30-58.  cpu/memory use NonZeroRequested + the pod's
+ * non-zero request; other resources use Requested + the pod request. */
+int64_t orc_fit_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  const koordhip_node_soa *s = st->soa;
+  int64_t num = 0, wsum = 0;
+  for (int r = 0; r < KOORDHIP_NRES; r++) {
+    int64_t w = cfg->fit_weight[r];
+    if (w == 0) continue; /* not in scoringStrategy.resources */
+    int64_t podreq, nodereq;
+    if (r == KOORDHIP_RES_CPU) {
+      podreq = pod->nz_cpu_m;
+      nodereq = st->nz_cpu_m[i];
+    } else if (r == KOORDHIP_RES_MEM) {
+      podreq = pod->nz_mem;
+      nodereq = st->nz_mem[i];
+    } else {
+      podreq = pod->req[r];
+      nodereq = st->requested[r][i];
+      if (r != KOORDHIP_RES_EPH && podreq == 0) continue; /* scalar not requested -> (0,0) */
+    }
+    int64_t alloc = s->alloc[r][i];
+    if (alloc == 0) continue; /* "Only fill the extended resource entry when it's non-zero" */
+    num += orc_least_requested(nodereq + podreq, alloc) * w;
+    wsum += w;
+  }
+  if (wsum == 0) return 0;
+  return num / wsum;
+}
+
+/* load_aware.go:123-171 (static part resolved by orc_la_flags); 1 = passes. */
+int orc_la_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  (void)cfg;
+  if (pod->flags & KOORDHIP_POD_DAEMONSET) return 1; /* :129-131 */
+  uint8_t bit = (pod->flags & KOORDHIP_POD_PROD) ? ORC_LA_OK_PROD : ORC_LA_OK_NONPROD;
+  return (st->flags[i] & bit) ? 1 : 0;
+}
+
+/* load_aware.go:269-335 with loadAwareSchedulingScorer :378-386.  The
+ * per-node usage base (nodeUsage minus estimated pods' actual usage when
+ * larger :316-324, plus assigned-pod estimates :298-301) is marshalled into
+ * la_used; pods committed during the stream add EstimatePod (L10). */
+int64_t orc_la_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  const koordhip_node_soa *s = st->soa;
+  if (st->flags[i] & ORC_LA_SCORE_ZERO) return 0; /* :278-289 */
+  int prod = (pod->flags & KOORDHIP_POD_PROD) && cfg->la_score_according_prod_usage; /* :291 */
+  int64_t used_cpu = pod->est_cpu + (prod ? st->la_used_prod_cpu_m[i] : st->la_used_cpu_m[i]);
+  int64_t used_mem = pod->est_mem + (prod ? st->la_used_prod_mem[i] : st->la_used_mem[i]);
+  int64_t num = orc_least_requested(used_cpu, s->la_alloc_cpu_m[i]) * cfg->la_weight_cpu +
+                orc_least_requested(used_mem, s->la_alloc_mem[i]) * cfg->la_weight_mem;
+  int64_t wsum = cfg->la_weight_cpu + cfg->la_weight_mem; /* every weight counts, :380-384 */
+  return num / wsum;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Combined evaluation                                                       */
+/* ------------------------------------------------------------------------ */
+
+static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
+  return 1;
+}
+
+static int64_t orc_total(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  int64_t t = 0;
+  if (cfg->score_plugins & KOORDHIP_PLUGIN_FIT) t += cfg->plugin_weight[0] * orc_fit_score(cfg, st, pod, i);
+  if (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) t += cfg->plugin_weight[1] * orc_la_score(cfg, st, pod, i);
+  return t;
+}
+
+/* key = (total+1) << 32 | (0xFFFFFFFF - node): larger is better, ties -> lower index. */
+static inline uint64_t mkkey(int64_t total, int32_t node) {
+  return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)node);
+}
+
+static int cmp_key_desc(const void *a, const void *b) {
+  uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+  return x < y ? 1 : (x > y ? -1 : 0);
+}
+
+int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, int32_t n_pods,
+             uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
+  const int32_t n = st->n;
+  uint64_t *keys = (topk && k > 0) ? (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1)) : NULL;
+  for (int32_t p = 0; p < n_pods; p++) {
+    const koordhip_pod *pod = &pods[p];
+    int32_t nk = 0;
+    for (int32_t i = 0; i < n; i++) {
+      int fit_ok = orc_fit_filter(cfg, st, pod, i);
+      int la_ok = orc_la_filter(cfg, st, pod, i);
+      if (status) {
+        uint8_t b = 0;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !fit_ok) b |= KOORDHIP_ST_FIT_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !la_ok) b |= KOORDHIP_ST_LA_FAIL;
+        status[(size_t)p * n + i] = b;
+      }
+      if (scores) {
+        int32_t *row = scores + (size_t)p * KOORDHIP_NPLUGINS * n;
+        row[0 * (size_t)n + i] = (cfg->score_plugins & KOORDHIP_PLUGIN_FIT) ? (int32_t)orc_fit_score(cfg, st, pod, i) : 0;
+        row[1 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) ? (int32_t)orc_la_score(cfg, st, pod, i) : 0;
+        row[2 * (size_t)n + i] = 0;
+      }
+      if (keys && orc_feasible(cfg, st, pod, i)) keys[nk++] = mkkey(orc_total(cfg, st, pod, i), i);
+    }
+    if (keys) {
+      qsort(keys, (size_t)nk, sizeof(uint64_t), cmp_key_desc);
+      for (int32_t j = 0; j < k; j++) {
+        koordhip_topk *o = &topk[(size_t)p * k + j];
+        if (j < nk) {
+          o->node = (int32_t)(0xFFFFFFFFu - (uint32_t)(keys[j] & 0xFFFFFFFFu));
+          o->score = (int32_t)((keys[j] >> 32) - 1);
+        } else {
+          o->node = -1;
+          o->score = 0;
+        }
+      }
+    }
+  }
+  free(keys);
+  return 0;
+}
+
+/* Reserve: podAssignCache.assign (pod_assign_cache.go:53-68) makes the pod an
+ * estimated assigned pod on the node (load_aware.go:353-372: no metric ->
+ * EstimatePod); (upstream) NodeInfo.AddPod adds Requested/NonZeroRequested and
+ * one pod (mirror: reservation/transformer.go:280-333).  sign = -1: Unreserve. */
+void orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t i, int sign) {
+  for (int r = 0; r < KOORDHIP_NRES; r++) st->requested[r][i] += sign * pod->req[r];
+  st->nz_cpu_m[i] += sign * pod->nz_cpu_m;
+  st->nz_mem[i] += sign * pod->nz_mem;
+  st->npods[i] += sign;
+  st->la_used_cpu_m[i] += sign * pod->est_cpu;
+  st->la_used_mem[i] += sign * pod->est_mem;
+  if (pod->flags & KOORDHIP_POD_PROD) { /* prod-only walk, load_aware.go:349-351 */
+    st->la_used_prod_cpu_m[i] += sign * pod->est_cpu;
+    st->la_used_prod_mem[i] += sign * pod->est_mem;
+  }
+  (void)cfg;
+}
+
+/* ------------------------------------------------------------------------ */
+/* parallelize.Until (pkg/util/parallelize/parallelism.go:28-49)            */
+/* ------------------------------------------------------------------------ */
+
+typedef void (*piece_fn)(void *arg, int32_t lo, int32_t hi);
+
+typedef struct pool {
+  int32_t nthreads;
+  pthread_t *tid;
+  _Atomic int64_t gen;      /* job generation */
+  _Atomic int32_t done;     /* workers finished this generation */
+  _Atomic int32_t next;     /* next piece */
+  _Atomic int32_t quit;
+  int32_t pieces, chunk;
+  piece_fn fn;
+  void *arg;
+} pool;
+
+/* chunkSizeFor: max(1, min(sqrt(n), n/parallelism + 1)), parallelism.go:33-44 */
+static int32_t chunk_size_for(int32_t n, int32_t parallelism) {
+  int32_t s = (int32_t)sqrt((double)n);
+  int32_t r = n / parallelism + 1;
+  if (s > r) s = r;
+  else if (s < 1) s = 1;
+  return s;
+}
+
+static void run_pieces(pool *p) {
+  for (;;) {
+    int32_t lo = atomic_fetch_add(&p->next, p->chunk);
+    if (lo >= p->pieces) break;
+    int32_t hi = lo + p->chunk;
+    if (hi > p->pieces) hi = p->pieces;
+    p->fn(p->arg, lo, hi);
+  }
+}
+
+static void *worker(void *a) {
+  pool *p = (pool *)a;
+  int64_t seen = 0;
+  for (;;) {
+    int64_t g;
+    int spins = 0;
+    while ((g = atomic_load(&p->gen)) == seen && !atomic_load(&p->quit)) {
+      if (++spins > 64) sched_yield();
+    }
+    if (atomic_load(&p->quit)) return NULL;
+    seen = g;
+    run_pieces(p);
+    atomic_fetch_add(&p->done, 1);
+  }
+}
+
+static int pool_init(pool *p, int32_t nthreads) {
+  memset(p, 0, sizeof(*p));
+  p->nthreads = nthreads;
+  if (nthreads <= 1) return 0;
+  p->tid = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int32_t t = 0; t < nthreads - 1; t++) /* the caller is the last worker */
+    if (pthread_create(&p->tid[t], NULL, worker, p)) return -1;
+  return 0;
+}
+
+static void pool_free(pool *p) {
+  if (p->nthreads > 1) {
+    atomic_store(&p->quit, 1);
+    for (int32_t t = 0; t < p->nthreads - 1; t++) pthread_join(p->tid[t], NULL);
+    free(p->tid);
+  }
+}
+
+/* Until(ctx, pieces, f) with `nthreads` workers and the reference chunking. */
+static void pool_until(pool *p, int32_t pieces, piece_fn fn, void *arg) {
+  if (pieces <= 0) return;
+  if (p->nthreads <= 1) {
+    fn(arg, 0, pieces);
+    return;
+  }
+  p->pieces = pieces;
+  p->chunk = chunk_size_for(pieces, 16);
+  p->fn = fn;
+  p->arg = arg;
+  atomic_store(&p->next, 0);
+  atomic_store(&p->done, 0);
+  atomic_fetch_add(&p->gen, 1);
+  run_pieces(p);
+  int spins = 0;
+  while (atomic_load(&p->done) < p->nthreads - 1)
+    if (++spins > 64) sched_yield();
+}
+
+/* ------------------------------------------------------------------------ */
+/* Greedy stream with the reference loop structure                           */
+/* ------------------------------------------------------------------------ */
+
+typedef struct stream_ctx {
+  const koordhip_config *cfg;
+  const orc_state *st;
+  const koordhip_pod *pod;
+  _Atomic int32_t nfeasible;
+  int32_t *feasible;      /* node ids (unordered, like upstream's atomic append) */
+  int64_t *plugin_scores; /* [2][nfeasible] */
+} stream_ctx;
+
+/* (upstream) findNodesThatPassFilters checkNode: RunFilterPlugins, append on success. */
+static void filter_piece(void *a, int32_t lo, int32_t hi) {
+  stream_ctx *c = (stream_ctx *)a;
+  for (int32_t i = lo; i < hi; i++)
+    if (orc_feasible(c->cfg, c->st, c->pod, i)) c->feasible[atomic_fetch_add(&c->nfeasible, 1)] = i;
+}
+
+/* (upstream) framework.RunScorePlugins: one Until over nodes, every score plugin per node. */
+static void score_piece(void *a, int32_t lo, int32_t hi) {
+  stream_ctx *c = (stream_ctx *)a;
+  int32_t nf = atomic_load(&c->nfeasible);
+  for (int32_t j = lo; j < hi; j++) {
+    int32_t i = c->feasible[j];
+    c->plugin_scores[j] =
+        (c->cfg->score_plugins & KOORDHIP_PLUGIN_FIT) ? orc_fit_score(c->cfg, c->st, c->pod, i) : 0;
+    c->plugin_scores[(size_t)nf + j] =
+        (c->cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) ? orc_la_score(c->cfg, c->st, c->pod, i) : 0;
+  }
+}
+
+int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods, int32_t n_pods,
+                     int32_t *out_node, int32_t threads) {
+  const int32_t n = st->n;
+  pool pl;
+  if (pool_init(&pl, threads)) return -1;
+  stream_ctx c;
+  c.cfg = cfg;
+  c.st = st;
+  c.feasible = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(n > 0 ? n : 1));
+  for (int32_t p = 0; p < n_pods; p++) {
+    c.pod = &pods[p];
+    atomic_store(&c.nfeasible, 0);
+    pool_until(&pl, n, filter_piece, &c);
+    int32_t nf = atomic_load(&c.nfeasible);
+    if (nf == 0) {
+      out_node[p] = KOORDHIP_UNSCHEDULABLE;
+      continue;
+    }
+    pool_until(&pl, nf, score_piece, &c);
+    /* (upstream) prioritizeNodes: sum of score x weight; selectHost: max,
+     * reservoir-random tie-break REPLACED by lowest node index (BASELINE.json). */
+    int64_t best = -1;
+    int32_t best_node = -1;
+    for (int32_t j = 0; j < nf; j++) {
+      int32_t i = c.feasible[j];
+      int64_t t = cfg->plugin_weight[0] * c.plugin_scores[j] + cfg->plugin_weight[1] * c.plugin_scores[(size_t)nf + j];
+      if (t > best || (t == best && i < best_node)) {
+        best = t;
+        best_node = i;
+      }
+    }
+    out_node[p] = best_node;
+    orc_commit(cfg, st, &pods[p], best_node, +1); /* Reserve + AssumePod */
+  }
+  free(c.feasible);
+  free(c.plugin_scores);
+  pool_free(&pl);
+  return 0;
+}

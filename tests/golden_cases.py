@@ -1,0 +1,96 @@
+"""Turns the golden fixture JSON (tests/golden/*.json) into objects, snapshots
+and pod records, the way the reference tests build their fakes
+(load_aware_test.go:804-910, :1754-1851)."""
+from __future__ import annotations
+
+import json
+import os
+
+from koordinator_amd import k8s, marshal
+from koordinator_amd.config import (LoadAwareSchedulingAggregatedArgs, LoadAwareSchedulingArgs, Profile,
+                                    PLUGIN_LOADAWARE)
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NOW = 1_000_000.0
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def rlist(d):
+    return {k: k8s.Quantity(v) for k, v in (d or {}).items()}
+
+
+def make_pod(d):
+    return k8s.Pod(namespace=d["ns"], name=d["name"], priority=d.get("priority"), labels=dict(d.get("labels") or {}),
+                   owner_kinds=list(d.get("owner_kinds") or []),
+                   containers=[k8s.Container(requests=rlist(c["requests"]), limits=rlist(c["limits"]))
+                               for c in d.get("containers", [])])
+
+
+def make_node_metric(d, node_name):
+    if d is None:
+        return None
+    aggregated = [k8s.AggregatedUsage(a["duration_s"], {t: rlist(u) for t, u in a["usage"].items()})
+                  for a in d.get("aggregated", [])]
+    return k8s.NodeMetric(
+        name=node_name,
+        update_time=None if d["update_dt"] is None else NOW + d["update_dt"],
+        report_interval_s=d.get("report_interval_s"),
+        node_usage=rlist(d["node_usage"]) if d.get("node_usage") is not None else None,
+        aggregated=aggregated,
+        pods_metric=[k8s.PodMetric(p["ns"], p["name"], rlist(p["usage"])) for p in d.get("pods_metric", [])],
+        has_node_metric=d.get("has_node_metric"),
+    )
+
+
+def make_args(d) -> LoadAwareSchedulingArgs:
+    a = LoadAwareSchedulingArgs()
+    for k, v in (d or {}).items():
+        if k == "aggregated":
+            a.aggregated = LoadAwareSchedulingAggregatedArgs(**v)
+        else:
+            setattr(a, k, v)
+    return a
+
+
+def la_profile(args_d) -> Profile:
+    return Profile(filters=(PLUGIN_LOADAWARE,), scores={PLUGIN_LOADAWARE: 1}, loadaware=make_args(args_d))
+
+
+def build_case(case, node_d, *, test_pod_key="pod"):
+    """-> (profile, NodeTable(1 row), pod record array(1))"""
+    node = k8s.Node(name=node_d["name"], allocatable=rlist(node_d["allocatable"]))
+    if case.get("annotation") is not None:
+        node.annotations[k8s.ANNOTATION_CUSTOM_USAGE_THRESHOLDS] = json.dumps(case["annotation"])
+    profile = la_profile(case.get("args"))
+    cluster = marshal.ClusterState(nodes=[node])
+    nmd = make_node_metric(case.get("node_metric"), node.name)
+    if nmd is not None:
+        cluster.node_metrics[node.name] = nmd
+    for p in case.get("pods", []):
+        pp = make_pod(p)
+        cluster.pods[pp.key] = pp
+    tp = make_pod(case[test_pod_key])
+    if case[test_pod_key]["name"]:
+        cluster.pods[tp.key] = tp
+    for a in case.get("assigned", []):
+        ap = make_pod(a["pod"])
+        ap.node_name = node.name
+        cluster.pods[ap.key] = ap
+        cluster.assigned.setdefault(node.name, []).append(marshal.AssignedPod(ap, NOW + a["dt"]))
+    table = marshal.build_table(cluster, profile, NOW)
+    rec = marshal.pod_records([tp], profile)
+    return profile, table, rec
+
+
+def score_cases():
+    d = load("loadaware_score.json")
+    return [(c["name"], c, d["node"]) for c in d["cases"]]
+
+
+def filter_cases():
+    d = load("loadaware_filter.json")
+    return [(c["name"], c, c.get("node", d["node"])) for c in d["cases"]]
