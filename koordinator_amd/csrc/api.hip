@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -37,6 +38,7 @@ int fail(int code, const std::string &msg) {
   } while (0)
 
 constexpr int kDefaultBatch = 32;
+constexpr int32_t kMaxNodes = 700000;  // resolve keeps a per-node bit in LDS
 constexpr int kMaxBatch = 64;
 
 }  // namespace
@@ -50,6 +52,8 @@ struct koordhip_ctx {
   bool loaded = false;
   int32_t batch = kDefaultBatch;
   int32_t monotone = 1;
+  int32_t score_bits = 16;  // bits of (max total score + 1)
+  int32_t partial_r = 4;    // nodes per lane of k_topk_partial (tuning knob KOORDHIP_TOPK_R)
 
   std::vector<void *> cols;  // every device column allocation
   kh::DevNodes d{};
@@ -135,22 +139,16 @@ int ensure(koordhip_ctx *c, void **p, size_t *cap, size_t bytes) {
   return 0;
 }
 
-// Work decomposition of one eval launch over node range [lo, hi):
-// chunks of `chunk` nodes (a multiple of 64); enough waves to fill 256 CUs.
-void chunking(int32_t lo, int32_t hi, int32_t pods, int32_t *chunk, int32_t *nchunks) {
-  const int64_t span = std::max<int64_t>(hi - lo, 1);
-  const int64_t target_waves = 256 * 4 * 6;  // ~6 waves per SIMD
-  int64_t nc = std::max<int64_t>(1, target_waves / std::max(pods, 1));
-  int64_t ch = (span + nc - 1) / nc;
-  ch = std::max<int64_t>(256, ((ch + 63) / 64) * 64);
-  *chunk = (int32_t)ch;
-  *nchunks = (int32_t)((span + ch - 1) / ch);
+// Work decomposition of one eval launch over node range [lo, hi): one wave
+// per (pod, chunk of 64 x R nodes).
+int32_t nchunks_for(const koordhip_ctx *c, int32_t lo, int32_t hi) {
+  const int32_t w = 64 * c->partial_r;
+  return std::max<int32_t>(1, (hi - lo + w - 1) / w);
 }
 
 int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
                uint64_t *out, bool timed) {
-  int32_t chunk, nchunks;
-  chunking(lo, hi, np, &chunk, &nchunks);
+  const int32_t nchunks = nchunks_for(c, lo, hi);
   size_t need = (size_t)np * nchunks * k * sizeof(uint64_t);
   if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial), &c->partial_cap, need)) return e;
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
@@ -167,7 +165,8 @@ int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t 
     c->ev_used += 2;
     HIP_TRY(hipEventRecord(*e0, c->stream));
   }
-  HIP_TRY(kh::launch_topk_partial(c->dc, c->d, d_pods, np, lo, hi, chunk, nchunks, k, c->d_partial, c->stream));
+  HIP_TRY(kh::launch_topk_partial(c->partial_r, c->dc, c->d, d_pods, np, lo, hi, nchunks, k, c->score_bits, c->d_partial,
+                                  c->stream));
   if (e1) HIP_TRY(hipEventRecord(*e1, c->stream));
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
@@ -218,7 +217,19 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.la_w_cpu = (int32_t)cfg->la_weight_cpu;
   c->dc.la_w_mem = (int32_t)cfg->la_weight_mem;
   c->dc.according = cfg->la_score_according_prod_usage ? 1 : 0;
+  if (const char *r = std::getenv("KOORDHIP_TOPK_R")) {
+    const int v = std::atoi(r);
+    if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
+  }
   c->monotone = 1;  // Fit LeastAllocated + LoadAware least-used: a commit never raises a key
+  {
+    int64_t max_total = 0;  // every plugin score is in [0, 100]
+    for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
+      if (cfg->score_plugins & (1u << p)) max_total += 100 * cfg->plugin_weight[p];
+    int bits = 1;
+    while ((1ll << bits) <= max_total + 1) bits++;
+    c->score_bits = bits;
+  }
   int dev = cfg->device;
   if (dev < 0) {
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
@@ -259,6 +270,7 @@ int koordhip_destroy(koordhip_ctx *c) {
 int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
   if (n < 0) return fail(KOORDHIP_EINVAL, "n < 0");
+  if (n > kMaxNodes) return fail(KOORDHIP_EINVAL, "more than 700000 nodes in one snapshot");
   if (int e = validate_soa(s)) return e;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));

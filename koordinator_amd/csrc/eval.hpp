@@ -61,7 +61,7 @@ struct NV {
 
 // What one pod's evaluation needs from the node columns (wave-uniform).
 struct Need {
-  bool pods, r_cpu, r_mem, eph, bcpu, bmem, a_cpu, a_mem, nz_cpu, nz_mem, la, la_prod;
+  bool pods, r_cpu, r_mem, eph, bcpu, bmem, a_cpu, a_mem, nz_cpu, nz_mem, la, la_nonprod, la_prod;
 };
 
 __device__ __forceinline__ Need pod_needs(const koordhip_pod &p, const DevCfg &c) {
@@ -81,6 +81,7 @@ __device__ __forceinline__ Need pod_needs(const koordhip_pod &p, const DevCfg &c
   n.nz_mem = fs && c.fit_w[KOORDHIP_RES_MEM] != 0;
   n.la = c.score & KOORDHIP_PLUGIN_LOADAWARE;
   n.la_prod = n.la && c.according && (p.flags & KOORDHIP_POD_PROD);
+  n.la_nonprod = n.la && !n.la_prod;
   n.a_cpu = n.r_cpu || n.nz_cpu || (n.la && c.la_alias);
   n.a_mem = n.r_mem || n.nz_mem || (n.la && c.la_alias);
   return n;
@@ -90,6 +91,7 @@ __device__ __forceinline__ Need need_all(const DevCfg &c) {
   Need n;
   n.pods = n.r_cpu = n.r_mem = n.eph = n.bcpu = n.bmem = n.a_cpu = n.a_mem = n.nz_cpu = n.nz_mem = true;
   n.la = true;
+  n.la_nonprod = true;
   n.la_prod = c.according != 0;
   return n;
 }
@@ -130,7 +132,8 @@ __device__ __forceinline__ void load_node(NV &v, const DevNodes &d, int32_t i, c
     if (n.la_prod) {
       v.la_up_cpu = d.la_used_prod_cpu[i];
       v.la_up_mem = d.la_used_prod_mem[i];
-    } else {
+    }
+    if (n.la_nonprod) {
       v.la_u_cpu = d.la_used_cpu[i];
       v.la_u_mem = d.la_used_mem[i];
     }

@@ -19,9 +19,10 @@ struct PrepIn {
 hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t *rows, int32_t m, hipStream_t s);
 hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
                             uint8_t *status, int32_t *scores, hipStream_t s);
-hipError_t launch_topk_partial(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
-                               int32_t lo, int32_t hi, int32_t chunk, int32_t nchunks, int32_t k, uint64_t *out,
-                               hipStream_t s);
+// k_topk_partial: one wave evaluates 64 x R nodes (R in {1, 2, 4, 8})
+hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
+                               int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
+                               uint64_t *out, hipStream_t s);
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
                              int32_t k, uint64_t *out, hipStream_t s);
 template <typename T>

@@ -51,6 +51,33 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// uniform-source lane read (v_readlane: SALU-visible, no LDS crossbar)
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW_MASK, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Wave max of a u64 with DPP row shifts + row broadcasts (GFX9 DPP), result
+// uniform.  Max is idempotent, so shifted prefix-max steps are a reduction.
+__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
+  uint64_t o;
+  o = dpp_u64<0x111>(v); v = o > v ? o : v;        // row_shr:1
+  o = dpp_u64<0x112>(v); v = o > v ? o : v;        // row_shr:2
+  o = dpp_u64<0x114>(v); v = o > v ? o : v;        // row_shr:4
+  o = dpp_u64<0x118>(v); v = o > v ? o : v;        // row_shr:8
+  o = dpp_u64<0x142, 0xa>(v); v = o > v ? o : v;   // row_bcast:15
+  o = dpp_u64<0x143, 0xc>(v); v = o > v ? o : v;   // row_bcast:31
+  return readlane_u64(v, 63);
+}
+
 // ---------------------------------------------------------------------------
 // k_prep_flags: load_aware.go:123-254 resolved per node, plus the Fit
 // over-commit bits.  usage = int64(math.Round(float64(used)/float64(total)*100)).
@@ -124,51 +151,89 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const koordhip_pod *__restrict
 }
 
 // ---------------------------------------------------------------------------
-// k_topk_partial
+// k_topk_partial: one wave = one pod x one chunk of 64*R nodes.
+//
+// Lane l evaluates nodes c0 + r*64 + l (r < R): every column load is a
+// coalesced 512-B (i64) or 256-B (i32) wave access, the R evaluations are
+// independent so their loads overlap.  The chunk's exact top-k is then found
+// without sorting: a radix select over the (small) total-score values with
+// wave ballots finds the k-th largest score T; every key with score > T is
+// taken and, for score == T, the lowest node indexes (r-major, lane-minor =
+// index order) up to k.  Output: k keys per (pod, chunk), unsorted, 0-padded.
 
+template <int R>
 __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
-                                                      int32_t n_pods, int32_t lo, int32_t hi, int32_t chunk,
-                                                      int32_t k, uint64_t *__restrict__ out) {
+                                                      int32_t n_pods, int32_t lo, int32_t hi, int32_t k,
+                                                      int32_t score_bits, uint64_t *__restrict__ out) {
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const int32_t p = blockIdx.y * (blockDim.x >> 6) + wave;
   if (p >= n_pods) return;  // wave-uniform
-  const int32_t c0 = lo + blockIdx.x * chunk;
-  const int32_t c1 = min(hi, c0 + chunk);
+  const int32_t c0 = lo + blockIdx.x * (64 * R);
   const koordhip_pod pod = pods[p];
   const Need need = pod_needs(pod, c);
-  uint64_t list = 0;  // rank `lane` of this chunk's running top-k (0 = empty)
-  uint64_t thr = 0;   // current k-th key
-  for (int32_t base = c0; base < c1; base += 64) {
-    const int32_t i = base + lane;
-    uint64_t key = 0;
-    if (i < c1) {
+  int32_t s[R];  // total score + 1, 0 = infeasible / past the end
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int32_t i = c0 + r * 64 + lane;
+    s[r] = 0;
+    if (i < hi) {
       NV v;
       load_node(v, d, i, need, c);
-      key = make_key(eval_total(pod, v, c), i);
-    }
-    uint64_t cand = __ballot(key > thr);
-    while (cand) {  // rank-insert every key that beats the k-th
-      const int src = __builtin_ctzll(cand);
-      cand &= cand - 1;
-      const uint64_t x = shfl_u64(key, src);
-      if (x <= thr) continue;  // wave-uniform
-      const int pos = __popcll(__ballot(list > x));
-      const uint64_t up = shfl_up_u64(list, 1);
-      if (lane > pos) list = up;
-      if (lane == pos) list = x;
-      if (lane >= k) list = 0;
-      thr = shfl_u64(list, k - 1);
+      s[r] = eval_total(pod, v, c) + 1;
     }
   }
-  if (lane < k) out[((size_t)p * gridDim.x + blockIdx.x) * k + lane] = list;
+  // k-th largest score value T (radix select, MSB first)
+  int32_t feasible = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) feasible += __popcll(__ballot(s[r] > 0));
+  int32_t T = 1;
+  if (feasible > k) {
+    T = 0;
+    for (int b = score_bits - 1; b >= 0; b--) {
+      const int32_t cand = T | (1 << b);
+      int32_t cnt = 0;
+#pragma unroll
+      for (int r = 0; r < R; r++) cnt += __popcll(__ballot(s[r] >= cand));
+      if (cnt >= k) T = cand;
+    }
+  }
+  // selection in node-index order
+  int32_t gt = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) gt += __popcll(__ballot(s[r] > T));
+  int32_t eq_left = k - gt;  // ties at T still to take (lowest index first)
+  int32_t base = 0;
+  uint64_t *o = out + ((size_t)p * gridDim.x + blockIdx.x) * k;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const bool eq = s[r] == T && s[r] > 0;
+    const uint64_t me = __ballot(eq);
+    const int32_t eq_rank = __popcll(me & lt);
+    const bool sel = s[r] > T || (eq && eq_rank < eq_left);
+    eq_left -= min(__popcll(me), max(eq_left, 0));
+    const uint64_t ms = __ballot(sel);
+    if (sel) {
+      const int32_t i = c0 + r * 64 + lane;
+      o[base + __popcll(ms & lt)] = (((uint64_t)(uint32_t)s[r]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+    }
+    base += __popcll(ms);
+  }
+  for (int32_t j = base + lane; j < k; j += 64) o[j] = 0;
 }
 
 // ---------------------------------------------------------------------------
-// k_topk_merge: per pod, exact top-k of L sorted lists of k keys.
+// k_topk_merge: per pod, exact top-k of L lists of k keys (each the exact
+// top-k of its node range, unsorted, 0-padded).
+//
+// A lower bound tau on the pod's k-th key prunes the candidates: the k-th
+// largest of the list heads and the largest tail of a full list both are.
+// Keys >= tau are gathered in LDS and rank-sorted (keys are unique).
 
 constexpr int MERGE_THREADS = 256;
 constexpr int MERGE_CAP = 2048;
+constexpr int MERGE_MAXL = 2048;
 
 __device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t *red) {
   v = wave_max_u64(v);
@@ -185,33 +250,53 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
                                                               int64_t list_stride, int32_t L, int32_t k,
                                                               uint64_t *__restrict__ out) {
   __shared__ uint64_t buf[MERGE_CAP];
+  __shared__ uint64_t heads[MERGE_MAXL];
   __shared__ uint64_t red[MERGE_THREADS / 64];
   __shared__ int32_t cnt;
   const int32_t p = blockIdx.x;
   const uint64_t *lists = in + (size_t)p * pod_stride;
-  // 1. tau = max over lists of the k-th key: the global k-th key is >= tau.
-  uint64_t t = 0;
+  const int32_t Lh = min(L, MERGE_MAXL);
+  // 1. per-list head and (full lists) tail
+  uint64_t tail = 0;
   for (int32_t l = threadIdx.x; l < L; l += blockDim.x) {
-    uint64_t x = lists[(size_t)l * list_stride + (k - 1)];
-    t = x > t ? x : t;
+    const uint64_t *x = lists + (size_t)l * list_stride;
+    uint64_t mx = 0, mn = ~0ull;
+    for (int32_t j = 0; j < k; j++) {
+      const uint64_t y = x[j];
+      mx = y > mx ? y : mx;
+      mn = y < mn ? y : mn;
+    }
+    if (mn != 0) tail = mn > tail ? mn : tail;  // full list: k keys >= mn
+    if (l < Lh) heads[l] = mx;
   }
-  const uint64_t tau = block_max_u64(t, red);
+  __syncthreads();
+  // k-th largest head (distinct keys; 0s are empty lists)
+  uint64_t th = 0;
+  if (Lh >= k) {
+    for (int32_t l = threadIdx.x; l < Lh; l += blockDim.x) {
+      const uint64_t h = heads[l];
+      int32_t rank = 0;
+      for (int32_t q = 0; q < Lh; q++) rank += heads[q] > h;
+      if (rank == k - 1) th = h;
+    }
+  }
+  const uint64_t tau = block_max_u64(th > tail ? th : tail, red);
   if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
-  // 2. collect every key >= tau (and > 0)
+  // 2. gather every key >= tau
   const int32_t total = L * k;
-  for (int32_t j = threadIdx.x; j < total; j += blockDim.x) {
-    uint64_t x = lists[(size_t)(j / k) * list_stride + (j % k)];
-    if (x != 0 && x >= tau) {
-      int32_t s = atomicAdd(&cnt, 1);
-      if (s < MERGE_CAP) buf[s] = x;
+  for (int32_t t = threadIdx.x; t < total; t += blockDim.x) {
+    const int32_t l = t / k, j = t - l * k;
+    const uint64_t y = lists[(size_t)l * list_stride + j];
+    if (y != 0 && y >= tau) {
+      const int32_t slot = atomicAdd(&cnt, 1);
+      if (slot < MERGE_CAP) buf[slot] = y;
     }
   }
   __syncthreads();
   const int32_t m = cnt;
   uint64_t *o = out + (size_t)p * k;
   if (m <= MERGE_CAP) {
-    // 3. rank sort (keys are unique): rank = #keys greater
     for (int32_t j = threadIdx.x; j < m; j += blockDim.x) {
       const uint64_t x = buf[j];
       int32_t rank = 0;
@@ -220,12 +305,13 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
     }
     for (int32_t j = m + threadIdx.x; j < k; j += blockDim.x) o[j] = 0;
   } else {
-    // overflow: k rounds of "largest key below the previous one" over all keys
+    // overflow: k rounds of "largest key below the previous one"
     uint64_t prev = ~0ull;
     for (int32_t r = 0; r < k; r++) {
       uint64_t b = 0;
-      for (int32_t j = threadIdx.x; j < total; j += blockDim.x) {
-        uint64_t x = lists[(size_t)(j / k) * list_stride + (j % k)];
+      for (int32_t t = threadIdx.x; t < total; t += blockDim.x) {
+        const int32_t l = t / k, j = t - l * k;
+        const uint64_t x = lists[(size_t)l * list_stride + j];
         if (x < prev && x > b) b = x;
       }
       b = block_max_u64(b, red);
@@ -249,47 +335,58 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 // skipped when no list prefix entry is modified.
 
 constexpr int RES_MAXP = 64;
-constexpr int RES_HASH = 256;
-
-__device__ __forceinline__ int hash_find(const int32_t *ht_node, const int8_t *ht_row, int32_t node) {
-  uint32_t h = ((uint32_t)node * 2654435761u) >> 24;  // 256 slots
-  for (int probe = 0; probe < RES_HASH; probe++) {
-    const int32_t x = ht_node[h];
-    if (x == node) return ht_row[h];
-    if (x < 0) return -1;
-    h = (h + 1) & (RES_HASH - 1);
-  }
-  return -1;
+__device__ __forceinline__ void copy_row(NV *dst, const NV *src, int lane) {
+  constexpr int W = (int)(sizeof(NV) / 8);
+  static_assert(sizeof(NV) % 8 == 0 && W <= 64, "NV must be a whole number of 8-byte words");
+  if (lane < W) reinterpret_cast<uint64_t *>(dst)[lane] = reinterpret_cast<const uint64_t *>(src)[lane];
 }
 
 __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
                                                 int32_t n_pods, int32_t k, const uint64_t *__restrict__ lists,
                                                 int32_t monotone, int32_t *__restrict__ out_node) {
+  constexpr int PRE = 2;  // list entries per pod whose rows are prefetched
   __shared__ NV rows[RES_MAXP];
+  __shared__ NV pre[PRE * RES_MAXP];
   __shared__ int32_t row_node[RES_MAXP];
   __shared__ uint64_t lk[RES_MAXP * RES_MAXP];
   __shared__ koordhip_pod lp[RES_MAXP];
-  __shared__ int32_t ht_node[RES_HASH];
-  __shared__ int8_t ht_row[RES_HASH];
+  extern __shared__ uint32_t modmap[];  // one bit per node: committed this round
   const int lane = lane_id();
+  const int32_t words = (d.n + 31) >> 5;
+  for (int32_t j = lane; j < words; j += 64) modmap[j] = 0;
   for (int32_t j = lane; j < n_pods * k; j += 64) lk[j] = lists[j];
   {
     const uint64_t *src = reinterpret_cast<const uint64_t *>(pods);
     uint64_t *dst = reinterpret_cast<uint64_t *>(lp);
-    const int32_t words = n_pods * (int32_t)(sizeof(koordhip_pod) / 8);
-    for (int32_t j = lane; j < words; j += 64) dst[j] = src[j];
+    const int32_t pw = n_pods * (int32_t)(sizeof(koordhip_pod) / 8);
+    for (int32_t j = lane; j < pw; j += 64) dst[j] = src[j];
   }
-  for (int32_t j = lane; j < RES_HASH; j += 64) ht_node[j] = -1;
+  // Prefetch the snapshot rows of every pod's first PRE list entries: the
+  // winner is either already modified this round (LDS) or the first
+  // unmodified entry of its list, which is almost always one of these.
+  for (int32_t t = lane; t < PRE * n_pods; t += 64) {
+    const int32_t j = t / PRE, q = t - j * PRE;
+    const uint64_t e = q < k ? lists[j * k + q] : 0;
+    if (e != 0) {
+      NV v;
+      load_row(v, d, key_node(e));
+      pre[t] = v;
+    }
+  }
   __syncthreads();
   int32_t nm = 0;  // modified rows this round (wave-uniform)
   for (int32_t j = 0; j < n_pods; j++) {
     const koordhip_pod pod = lp[j];
     const uint64_t e = lane < k ? lk[j * k + lane] : 0;
     bool mod = false;
-    if (e != 0 && nm > 0) mod = hash_find(ht_node, ht_row, key_node(e)) >= 0;
+    if (e != 0) {
+      const int32_t nd = key_node(e);
+      mod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+    }
     const uint64_t free_mask = __ballot(e != 0 && !mod);
     const int first = free_mask ? __builtin_ctzll(free_mask) : 64;
-    uint64_t best = free_mask ? shfl_u64(e, first) : 0;
+    const uint64_t cand = free_mask ? readlane_u64(e, first) : 0;
+    uint64_t best = cand;
     const bool prefix_modified = __ballot(e != 0 && mod && lane < first) != 0;
     if (nm > 0 && (!monotone || prefix_modified)) {
       uint64_t key = 0;
@@ -297,7 +394,7 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
         const NV v = rows[lane];
         key = make_key(eval_total(pod, v, c), row_node[lane]);
       }
-      key = wave_max_u64(key);
+      key = wave_max_u64_dpp(key);
       best = key > best ? key : best;
     }
     if (best == 0) {
@@ -306,19 +403,25 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
     }
     const int32_t w = key_node(best);
     if (lane == 0) out_node[j] = w;
-    int32_t r = nm > 0 ? hash_find(ht_node, ht_row, w) : -1;  // uniform
-    if (r < 0) {
+    const uint64_t hit = __ballot(lane < nm && row_node[lane] == w);
+    int32_t r;
+    if (hit) {
+      r = __builtin_ctzll(hit);
+    } else {
+      // w is new this round, hence pod j's first unmodified list entry
       r = nm++;
-      if (lane == 0) {
+      if (first < PRE && best == cand) {
+        copy_row(&rows[r], &pre[j * PRE + first], lane);
+      } else if (lane == 0) {
         NV v;
         load_row(v, d, w);
         rows[r] = v;
-        row_node[r] = w;
-        uint32_t h = ((uint32_t)w * 2654435761u) >> 24;
-        while (ht_node[h] >= 0) h = (h + 1) & (RES_HASH - 1);
-        ht_node[h] = w;
-        ht_row[h] = (int8_t)r;
       }
+      if (lane == 0) {
+        row_node[r] = w;
+        modmap[w >> 5] |= 1u << (w & 31);
+      }
+      __syncthreads();
     }
     if (lane == 0) {
       NV v = rows[r];
@@ -377,11 +480,24 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_p
   return hipGetLastError();
 }
 
-hipError_t launch_topk_partial(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
-                               int32_t lo, int32_t hi, int32_t chunk, int32_t nchunks, int32_t k, uint64_t *out,
-                               hipStream_t s) {
+hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
+                               int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
+                               uint64_t *out, hipStream_t s) {
   dim3 grid(nchunks, (n_pods + 3) / 4);
-  hipLaunchKernelGGL(k_topk_partial, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, chunk, k, out);
+  switch (R) {
+    case 1:
+      hipLaunchKernelGGL(k_topk_partial<1>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_topk_partial<2>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      break;
+    case 4:
+      hipLaunchKernelGGL(k_topk_partial<4>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      break;
+    default:
+      hipLaunchKernelGGL(k_topk_partial<8>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      break;
+  }
   return hipGetLastError();
 }
 
@@ -393,7 +509,8 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
 
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods, int32_t k,
                           const uint64_t *lists, int32_t monotone, int32_t *out_node, hipStream_t s) {
-  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), 0, s, c, d, pods, n_pods, k, lists, monotone, out_node);
+  const size_t bitmap = (size_t)((d.n + 31) >> 5) * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone, out_node);
   return hipGetLastError();
 }
 

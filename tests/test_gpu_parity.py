@@ -173,13 +173,16 @@ def test_commit_uncommit_and_update_nodes(Engine):
         idx = np.arange(0, 400, 8, dtype=np.int32)
         rows = table.rows(idx)
         rows["laf_used_m0"][:] = rows["laf_total_m0"] * 9 // 10   # now above the 65% cpu threshold
-        rows["requested0"][:] = s["requested"][0][idx]
-        rows["requested1"][:] = s["requested"][1][idx]
+        for r in range(abi.NRES):   # the informer row carries the current NodeInfo accounting
+            rows[f"requested{r}"][:] = s["requested"][r][idx]
+        rows["nz_cpu_m"][:], rows["nz_mem"][:] = s["nz"][0][idx], s["nz"][1][idx]
+        rows["npods"][:] = s["npods"][idx]
+        rows["la_used_cpu_m"][:], rows["la_used_mem"][:] = s["la_used"][0][idx], s["la_used"][1][idx]
+        rows["la_used_prod_cpu_m"][:] = s["la_used_prod"][0][idx]
+        rows["la_used_prod_mem"][:] = s["la_used_prod"][1][idx]
         e.update_nodes(idx, rows)
         got = e.eval(pods[:16], k=8)
     t2 = table.copy()
-    for c in rows.cols:
-        t2[c][idx] = rows[c]
     st = o.state()
     for r in range(abi.NRES):
         t2[f"requested{r}"][:] = st["requested"][r]
@@ -187,10 +190,13 @@ def test_commit_uncommit_and_update_nodes(Engine):
     t2["npods"][:] = st["npods"]
     t2["la_used_cpu_m"][:], t2["la_used_mem"][:] = st["la_used"]
     t2["la_used_prod_cpu_m"][:], t2["la_used_prod_mem"][:] = st["la_used_prod"]
+    for c in rows.cols:
+        t2[c][idx] = rows[c]
     ref = oracle.Oracle(cfg, t2).eval(pods[:16], k=8)
     for key in ("status", "scores", "topk"):
         assert np.array_equal(got[key], ref[key]), key
-    assert (got["status"][:, idx] & abi.ST_LA_FAIL).all()
+    has_metric = (rows["la_flags"] & abi.LA_HAS_METRIC) != 0   # missing NodeMetric -> Filter passes
+    assert (got["status"][:, idx[has_metric]] & abi.ST_LA_FAIL).all()
 
 
 def test_plugin_subsets(Engine):
