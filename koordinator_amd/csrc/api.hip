@@ -70,6 +70,7 @@ struct koordhip_ctx {
   uint64_t *d_gather = nullptr;  // [world][batch][k]
   uint64_t *d_final = nullptr;   // [batch][k]
   koordhip_pod *d_tmp_pod = nullptr;
+  uint64_t *d_dbg = nullptr;  // KOORDHIP_STAMPS diagnostic counters (resolve segments)
 
   // checkpoint of the mutable columns
   std::vector<void *> ckpt;
@@ -149,8 +150,10 @@ int32_t nchunks_for(const koordhip_ctx *c, int32_t lo, int32_t hi) {
 int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
                uint64_t *out, bool timed) {
   const int32_t nchunks = nchunks_for(c, lo, hi);
-  size_t need = (size_t)np * nchunks * k * sizeof(uint64_t);
+  const size_t lists_bytes = (size_t)np * nchunks * k * sizeof(uint64_t);
+  size_t need = lists_bytes + (size_t)np * nchunks * 2 * sizeof(uint64_t);
   if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial), &c->partial_cap, need)) return e;
+  uint64_t *ht = c->d_partial + lists_bytes / sizeof(uint64_t);
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   if (timed && c->cfg.profile_kernels) {
     if (c->ev_used + 2 > (int32_t)c->ev.size()) {
@@ -165,12 +168,12 @@ int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t 
     c->ev_used += 2;
     HIP_TRY(hipEventRecord(*e0, c->stream));
   }
-  HIP_TRY(kh::launch_topk_partial(c->partial_r, c->dc, c->d, d_pods, np, lo, hi, nchunks, k, c->score_bits, c->d_partial,
+  HIP_TRY(kh::launch_topk_partial(c->partial_r, c->dc, c->d, d_pods, np, lo, hi, nchunks, k, c->score_bits, c->d_partial, ht,
                                   c->stream));
   if (e1) HIP_TRY(hipEventRecord(*e1, c->stream));
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
-  HIP_TRY(kh::launch_topk_merge(c->d_partial, (int64_t)nchunks * k, k, np, nchunks, k, out, c->stream));
+  HIP_TRY(kh::launch_topk_merge(c->d_partial, (int64_t)nchunks * k, k, np, nchunks, k, ht, out, c->stream));
   return 0;
 }
 
@@ -256,7 +259,7 @@ int koordhip_destroy(koordhip_ctx *c) {
   free_cols(c);
   for (void *p : c->ckpt) (void)hipFree(p);
   for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
-                  (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod})
+                  (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
@@ -519,7 +522,8 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
     if (c->d_out) HIP_TRY(hipFree(c->d_out));
     c->d_pods = nullptr;
     c->d_out = nullptr;
-    HIP_TRY(hipMalloc(&c->d_pods, (size_t)n_pods * sizeof(koordhip_pod)));
+    // +16 records of padding: the resolve kernel DMA-copies pod records in 1 KiB pieces
+    HIP_TRY(hipMalloc(&c->d_pods, (size_t)(n_pods + 16) * sizeof(koordhip_pod)));
     HIP_TRY(hipMalloc(&c->d_out, (size_t)n_pods * sizeof(int32_t)));
     c->pods_cap = n_pods;
   }
@@ -547,6 +551,10 @@ int koordhip_place_staged(koordhip_ctx *c) {
   c->ev_used = 0;
   c->last_launches = 0;
   c->last_evals = 0;
+  if (std::getenv("KOORDHIP_STAMPS")) {
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 8 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 8 * sizeof(uint64_t), c->stream));
+  }
   HIP_TRY(hipEventRecord(c->t0, c->stream));
   const int32_t total = c->n_staged;
   for (int32_t p0 = 0; p0 < total; p0 += P) {
@@ -556,14 +564,24 @@ int koordhip_place_staged(koordhip_ctx *c) {
       if (np < P) HIP_TRY(hipMemsetAsync(c->d_lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
       NCCL_TRY(ncclAllGather(c->d_lists, c->d_gather, (size_t)P * K, ncclUint64, c->comm, c->stream));
-      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->d_final, c->stream));
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0, c->stream));
+      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, nullptr, c->d_final, c->stream));
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0, c->d_dbg, c->stream));
     } else {
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_lists, c->monotone, c->d_out + p0, c->stream));
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_lists, c->monotone, c->d_out + p0, c->d_dbg, c->stream));
     }
   }
   HIP_TRY(hipEventRecord(c->t1, c->stream));
+  if (c->d_dbg) {
+    uint64_t h[8];
+    HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::fprintf(stderr,
+                 "[koordhip stamps] rounds-total cycles: prologue %llu  list %llu  eval %llu  commit %llu  kernel %llu"
+                 "  | evals %llu prefetch-misses %llu pods %llu\n",
+                 (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
+                 (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7]);
+  }
   return 0;
 }
 

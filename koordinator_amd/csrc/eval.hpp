@@ -151,6 +151,13 @@ __device__ __forceinline__ int32_t div_small(int64_t a, int64_t b) {
   return q;
 }
 
+// num / ws for the weighted averages: ws is a small weight sum, very often a
+// power of two (the shipped profile: 2 and 4), then a shift is exact.
+__device__ __forceinline__ int32_t div_weights(int64_t num, int64_t ws) {
+  if ((ws & (ws - 1)) == 0) return (int32_t)(num >> __builtin_ctzll((uint64_t)ws));
+  return div_small(num, ws);
+}
+
 // leastRequestedScore, load_aware.go:388-397 / least_allocated.go:49-58.
 __device__ __forceinline__ int32_t lrs(int64_t req, int64_t cap) {
   if (cap == 0 || req > cap) return 0;
@@ -182,7 +189,7 @@ __device__ __forceinline__ int32_t fit_score(const koordhip_pod &p, const NV &v,
     }
   }
   if (ws == 0) return 0;
-  return div_small(num, ws);
+  return div_weights(num, ws);
 }
 
 // fitsRequest (upstream fit.go; mirror reservation/plugin.go:445-494).  A zero
@@ -228,7 +235,7 @@ __device__ __forceinline__ int32_t la_score(const koordhip_pod &p, const NV &v, 
   const int64_t ucpu = p.est_cpu + (prod ? v.la_up_cpu : v.la_u_cpu);
   const int64_t umem = p.est_mem + (prod ? v.la_up_mem : v.la_u_mem);
   const int64_t num = (int64_t)lrs(ucpu, v.la_a_cpu) * c.la_w_cpu + (int64_t)lrs(umem, v.la_a_mem) * c.la_w_mem;
-  return div_small(num, (int64_t)(c.la_w_cpu + c.la_w_mem));
+  return div_weights(num, (int64_t)(c.la_w_cpu + c.la_w_mem));
 }
 
 // Total weighted score, or -1 when any enabled Filter fails (short-circuit).

@@ -164,7 +164,8 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const koordhip_pod *__restrict
 template <int R>
 __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
                                                       int32_t n_pods, int32_t lo, int32_t hi, int32_t k,
-                                                      int32_t score_bits, uint64_t *__restrict__ out) {
+                                                      int32_t score_bits, uint64_t *__restrict__ out,
+                                                      uint64_t *__restrict__ out_ht) {
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const int32_t p = blockIdx.y * (blockDim.x >> 6) + wave;
@@ -204,8 +205,10 @@ __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, cons
   for (int r = 0; r < R; r++) gt += __popcll(__ballot(s[r] > T));
   int32_t eq_left = k - gt;  // ties at T still to take (lowest index first)
   int32_t base = 0;
-  uint64_t *o = out + ((size_t)p * gridDim.x + blockIdx.x) * k;
+  const size_t list = (size_t)p * gridDim.x + blockIdx.x;
+  uint64_t *o = out + list * k;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint64_t hmax = 0, nmin = 0;  // max selected key, max of ~key (= ~min key)
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const bool eq = s[r] == T && s[r] > 0;
@@ -216,11 +219,21 @@ __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, cons
     const uint64_t ms = __ballot(sel);
     if (sel) {
       const int32_t i = c0 + r * 64 + lane;
-      o[base + __popcll(ms & lt)] = (((uint64_t)(uint32_t)s[r]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+      const uint64_t key = (((uint64_t)(uint32_t)s[r]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+      o[base + __popcll(ms & lt)] = key;
+      hmax = key > hmax ? key : hmax;
+      nmin = ~key > nmin ? ~key : nmin;
     }
     base += __popcll(ms);
   }
   for (int32_t j = base + lane; j < k; j += 64) o[j] = 0;
+  // list head and (full list) tail for the merge's pruning bound
+  hmax = wave_max_u64_dpp(hmax);
+  nmin = wave_max_u64_dpp(nmin);
+  if (lane == 0) {
+    out_ht[2 * list] = hmax;
+    out_ht[2 * list + 1] = base >= k ? ~nmin : 0;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -248,6 +261,7 @@ __device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t *red) {
 
 __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__restrict__ in, int64_t pod_stride,
                                                               int64_t list_stride, int32_t L, int32_t k,
+                                                              const uint64_t *__restrict__ ht,
                                                               uint64_t *__restrict__ out) {
   __shared__ uint64_t buf[MERGE_CAP];
   __shared__ uint64_t heads[MERGE_MAXL];
@@ -256,17 +270,24 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
   const int32_t p = blockIdx.x;
   const uint64_t *lists = in + (size_t)p * pod_stride;
   const int32_t Lh = min(L, MERGE_MAXL);
-  // 1. per-list head and (full lists) tail
+  // 1. per-list head and (full lists) tail: from the partial kernel when it
+  //    wrote them (ht != nullptr), else by scanning the lists
   uint64_t tail = 0;
   for (int32_t l = threadIdx.x; l < L; l += blockDim.x) {
-    const uint64_t *x = lists + (size_t)l * list_stride;
-    uint64_t mx = 0, mn = ~0ull;
-    for (int32_t j = 0; j < k; j++) {
-      const uint64_t y = x[j];
-      mx = y > mx ? y : mx;
-      mn = y < mn ? y : mn;
+    uint64_t mx = 0, mn = 0;
+    if (ht) {
+      mx = ht[2 * ((size_t)p * L + l)];
+      mn = ht[2 * ((size_t)p * L + l) + 1];
+    } else {
+      const uint64_t *x = lists + (size_t)l * list_stride;
+      mn = ~0ull;
+      for (int32_t j = 0; j < k; j++) {
+        const uint64_t y = x[j];
+        mx = y > mx ? y : mx;
+        mn = y < mn ? y : mn;
+      }
     }
-    if (mn != 0) tail = mn > tail ? mn : tail;  // full list: k keys >= mn
+    tail = mn > tail ? mn : tail;  // full list: k keys >= its min (0 when not full)
     if (l < Lh) heads[l] = mx;
   }
   __syncthreads();
@@ -341,96 +362,156 @@ __device__ __forceinline__ void copy_row(NV *dst, const NV *src, int lane) {
   if (lane < W) reinterpret_cast<uint64_t *>(dst)[lane] = reinterpret_cast<const uint64_t *>(src)[lane];
 }
 
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// Copy `bytes` (a multiple of 1 KiB) global -> LDS with LDS-DMA, 16 B per lane
+// per instruction, all in flight at once; the caller waits (vmcnt) + barriers.
+__device__ __forceinline__ void dma_to_lds(void *lds, const void *src, int32_t bytes, int lane) {
+  const char *g = static_cast<const char *>(src);
+  char *l = static_cast<char *>(lds);
+  for (int32_t off = 0; off < bytes; off += 1024)
+    __builtin_amdgcn_global_load_lds((gvoid_t *)(g + off + lane * 16), (lvoid_t *)(l + off), 16, 0, 0);
+}
+
+constexpr int RES_PRE = 128;  // prefetched snapshot rows per round
+
 __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
                                                 int32_t n_pods, int32_t k, const uint64_t *__restrict__ lists,
-                                                int32_t monotone, int32_t *__restrict__ out_node) {
-  constexpr int PRE = 2;  // list entries per pod whose rows are prefetched
-  __shared__ NV rows[RES_MAXP];
-  __shared__ NV pre[PRE * RES_MAXP];
-  __shared__ int32_t row_node[RES_MAXP];
-  __shared__ uint64_t lk[RES_MAXP * RES_MAXP];
-  __shared__ koordhip_pod lp[RES_MAXP];
+                                                int32_t monotone, int32_t *__restrict__ out_node,
+                                                uint64_t *__restrict__ dbg) {
+  // dbg (diagnostic builds only, KOORDHIP_STAMPS): s_memtime segment sums
+  uint64_t t_entry = dbg ? stamp() : 0, t_a = 0, t_b = 0, t_c = 0, t_mark = 0, n_eval = 0, n_miss = 0;
+  __shared__ __attribute__((aligned(16))) uint64_t lk[RES_MAXP * RES_MAXP];
+  __shared__ __attribute__((aligned(16))) koordhip_pod lp[RES_MAXP + 16];
+  // Prefetched snapshot rows: slot t holds pod (t % n_pods)'s list entry at
+  // position t / n_pods.  A round's winner is either a node already modified
+  // in the round (kept in registers) or its pod's first unmodified list
+  // entry, which is nearly always among the first few positions.
+  __shared__ NV pre[RES_PRE];
+  __shared__ int32_t pre_node[RES_PRE];
   extern __shared__ uint32_t modmap[];  // one bit per node: committed this round
   const int lane = lane_id();
+  // LDS-DMA the round's lists and pod records (buffers are padded to 1 KiB)
+  dma_to_lds(lk, lists, ((n_pods * k * 8) + 1023) & ~1023, lane);
+  dma_to_lds(lp, pods, ((n_pods * (int32_t)sizeof(koordhip_pod)) + 1023) & ~1023, lane);
   const int32_t words = (d.n + 31) >> 5;
   for (int32_t j = lane; j < words; j += 64) modmap[j] = 0;
-  for (int32_t j = lane; j < n_pods * k; j += 64) lk[j] = lists[j];
-  {
-    const uint64_t *src = reinterpret_cast<const uint64_t *>(pods);
-    uint64_t *dst = reinterpret_cast<uint64_t *>(lp);
-    const int32_t pw = n_pods * (int32_t)(sizeof(koordhip_pod) / 8);
-    for (int32_t j = lane; j < pw; j += 64) dst[j] = src[j];
-  }
-  // Prefetch the snapshot rows of every pod's first PRE list entries: the
-  // winner is either already modified this round (LDS) or the first
-  // unmodified entry of its list, which is almost always one of these.
-  for (int32_t t = lane; t < PRE * n_pods; t += 64) {
-    const int32_t j = t / PRE, q = t - j * PRE;
-    const uint64_t e = q < k ? lists[j * k + q] : 0;
-    if (e != 0) {
+  for (int32_t t = lane; t < RES_PRE; t += 64) {
+    const int32_t j = t % n_pods, q = t / n_pods;
+    int32_t nd = -1;
+    if (q < k) {
+      const uint64_t e = lists[(size_t)j * k + q];
+      if (e != 0) nd = key_node(e);
+    }
+    if (nd >= 0) {
       NV v;
-      load_row(v, d, key_node(e));
+      load_row(v, d, nd);
       pre[t] = v;
     }
+    pre_node[t] = nd;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  const uint64_t t_pro = dbg ? stamp() : 0;
+  // Lane r owns modified row r in registers (evaluated and committed in place).
+  NV my{};
+  int32_t my_node = -1;
   int32_t nm = 0;  // modified rows this round (wave-uniform)
+  uint64_t e = lane < k ? lk[lane] : 0;
+  bool mod = false;
   for (int32_t j = 0; j < n_pods; j++) {
+    if (dbg) t_mark = stamp();
     const koordhip_pod pod = lp[j];
-    const uint64_t e = lane < k ? lk[j * k + lane] : 0;
-    bool mod = false;
-    if (e != 0) {
-      const int32_t nd = key_node(e);
-      mod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-    }
     const uint64_t free_mask = __ballot(e != 0 && !mod);
     const int first = free_mask ? __builtin_ctzll(free_mask) : 64;
     const uint64_t cand = free_mask ? readlane_u64(e, first) : 0;
     uint64_t best = cand;
     const bool prefix_modified = __ballot(e != 0 && mod && lane < first) != 0;
+    // Speculatively stage the row of `cand` (the winner whenever the winner is
+    // not an already-modified node) into lane nm, the owner such a new row
+    // gets; the LDS/global latency overlaps the re-evaluation below.
+    int32_t staged = -1;
+    if (cand != 0) {
+      const int32_t cn = key_node(cand);
+      const uint64_t pm0 = __ballot(pre_node[lane] == cn);
+      const uint64_t pm1 = __ballot(pre_node[lane + 64] == cn);
+      const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
+      if (src >= 0) {
+        if (lane == nm) my = pre[src];
+      } else {
+        n_miss++;
+        if (lane == nm) load_row(my, d, cn);
+      }
+      staged = cn;
+    }
+    if (dbg) {
+      const uint64_t t = stamp();
+      t_a += t - t_mark;
+      t_mark = t;
+    }
     if (nm > 0 && (!monotone || prefix_modified)) {
       uint64_t key = 0;
-      if (lane < nm) {
-        const NV v = rows[lane];
-        key = make_key(eval_total(pod, v, c), row_node[lane]);
-      }
+      if (lane < nm) key = make_key(eval_total(pod, my, c), my_node);
       key = wave_max_u64_dpp(key);
       best = key > best ? key : best;
+      n_eval++;
+    }
+    if (dbg) {
+      const uint64_t t = stamp();
+      t_b += t - t_mark;
+      t_mark = t;
     }
     if (best == 0) {
       if (lane == 0) out_node[j] = KOORDHIP_UNSCHEDULABLE;
-      continue;
-    }
-    const int32_t w = key_node(best);
-    if (lane == 0) out_node[j] = w;
-    const uint64_t hit = __ballot(lane < nm && row_node[lane] == w);
-    int32_t r;
-    if (hit) {
-      r = __builtin_ctzll(hit);
     } else {
-      // w is new this round, hence pod j's first unmodified list entry
-      r = nm++;
-      if (first < PRE && best == cand) {
-        copy_row(&rows[r], &pre[j * PRE + first], lane);
-      } else if (lane == 0) {
-        NV v;
-        load_row(v, d, w);
-        rows[r] = v;
+      const int32_t w = key_node(best);
+      if (lane == 0) out_node[j] = w;
+      const uint64_t hit = __ballot(lane < nm && my_node == w);
+      int32_t r;
+      if (hit) {
+        r = __builtin_ctzll(hit);
+      } else {
+        // w is new this round, hence pod j's first unmodified list entry,
+        // whose row lane nm already staged
+        r = nm++;
+        if (staged != w && lane == r) load_row(my, d, w);  // unreachable by construction; kept for safety
+        if (lane == r) {
+          my_node = w;
+          modmap[w >> 5] |= 1u << (w & 31);
+        }
       }
-      if (lane == 0) {
-        row_node[r] = w;
-        modmap[w >> 5] |= 1u << (w & 31);
+      if (lane == r) apply_delta(my, pod, +1);
+    }
+    // next pod's list against the state after pod j's commit
+    if (j + 1 < n_pods) {
+      e = lane < k ? lk[(j + 1) * k + lane] : 0;
+      mod = false;
+      if (e != 0) {
+        const int32_t nd = key_node(e);
+        mod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
       }
-      __syncthreads();
     }
-    if (lane == 0) {
-      NV v = rows[r];
-      apply_delta(v, pod, +1);
-      rows[r] = v;
-    }
-    __syncthreads();
+    if (dbg) t_c += stamp() - t_mark;
   }
-  if (lane < nm) store_row(rows[lane], d, row_node[lane]);
+  if (lane < nm) store_row(my, d, my_node);
+  if (dbg && lane == 0) {
+    const uint64_t t_end = stamp();
+    atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)(t_pro - t_entry));
+    atomicAdd((unsigned long long *)&dbg[1], (unsigned long long)t_a);
+    atomicAdd((unsigned long long *)&dbg[2], (unsigned long long)t_b);
+    atomicAdd((unsigned long long *)&dbg[3], (unsigned long long)t_c);
+    atomicAdd((unsigned long long *)&dbg[4], (unsigned long long)(t_end - t_entry));
+    atomicAdd((unsigned long long *)&dbg[5], (unsigned long long)n_eval);
+    atomicAdd((unsigned long long *)&dbg[6], (unsigned long long)n_miss);
+    atomicAdd((unsigned long long *)&dbg[7], (unsigned long long)n_pods);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -482,35 +563,35 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_p
 
 hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
                                int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
-                               uint64_t *out, hipStream_t s) {
+                               uint64_t *out, uint64_t *ht, hipStream_t s) {
   dim3 grid(nchunks, (n_pods + 3) / 4);
   switch (R) {
     case 1:
-      hipLaunchKernelGGL(k_topk_partial<1>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      hipLaunchKernelGGL(k_topk_partial<1>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
       break;
     case 2:
-      hipLaunchKernelGGL(k_topk_partial<2>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      hipLaunchKernelGGL(k_topk_partial<2>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
       break;
     case 4:
-      hipLaunchKernelGGL(k_topk_partial<4>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      hipLaunchKernelGGL(k_topk_partial<4>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
       break;
     default:
-      hipLaunchKernelGGL(k_topk_partial<8>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
+      hipLaunchKernelGGL(k_topk_partial<8>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
       break;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
-                             int32_t k, uint64_t *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_topk_merge, dim3(n_pods), dim3(MERGE_THREADS), 0, s, in, pod_stride, list_stride, L, k, out);
+                             int32_t k, const uint64_t *ht, uint64_t *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_topk_merge, dim3(n_pods), dim3(MERGE_THREADS), 0, s, in, pod_stride, list_stride, L, k, ht, out);
   return hipGetLastError();
 }
 
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods, int32_t k,
-                          const uint64_t *lists, int32_t monotone, int32_t *out_node, hipStream_t s) {
+                          const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *dbg, hipStream_t s) {
   const size_t bitmap = (size_t)((d.n + 31) >> 5) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone, out_node);
+  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone, out_node, dbg);
   return hipGetLastError();
 }
 
