@@ -37,7 +37,7 @@ int fail(int code, const std::string &msg) {
     if (_r != ncclSuccess) return fail(KOORDHIP_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
   } while (0)
 
-constexpr int kDefaultBatch = 32;
+constexpr int kDefaultBatch = 64;
 constexpr int32_t kMaxNodes = 700000;  // resolve keeps a per-node bit in LDS
 constexpr int kMaxBatch = 64;
 
@@ -53,7 +53,7 @@ struct koordhip_ctx {
   int32_t batch = kDefaultBatch;
   int32_t monotone = 1;
   int32_t score_bits = 16;  // bits of (max total score + 1)
-  int32_t partial_r = 4;    // nodes per lane of k_topk_partial (tuning knob KOORDHIP_TOPK_R)
+  int32_t partial_r = 8;    // nodes per lane of k_topk_partial (tuning knob KOORDHIP_TOPK_R)
 
   std::vector<void *> cols;  // every device column allocation
   kh::DevNodes d{};
@@ -150,10 +150,8 @@ int32_t nchunks_for(const koordhip_ctx *c, int32_t lo, int32_t hi) {
 int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
                uint64_t *out, bool timed) {
   const int32_t nchunks = nchunks_for(c, lo, hi);
-  const size_t lists_bytes = (size_t)np * nchunks * k * sizeof(uint64_t);
-  size_t need = lists_bytes + (size_t)np * nchunks * 2 * sizeof(uint64_t);
+  const size_t need = (size_t)np * nchunks * k * sizeof(uint64_t) + 1024;  // +1 KiB: merge DMA padding
   if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial), &c->partial_cap, need)) return e;
-  uint64_t *ht = c->d_partial + lists_bytes / sizeof(uint64_t);
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   if (timed && c->cfg.profile_kernels) {
     if (c->ev_used + 2 > (int32_t)c->ev.size()) {
@@ -168,12 +166,12 @@ int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t 
     c->ev_used += 2;
     HIP_TRY(hipEventRecord(*e0, c->stream));
   }
-  HIP_TRY(kh::launch_topk_partial(c->partial_r, c->dc, c->d, d_pods, np, lo, hi, nchunks, k, c->score_bits, c->d_partial, ht,
+  HIP_TRY(kh::launch_topk_partial(c->partial_r, c->dc, c->d, d_pods, np, lo, hi, nchunks, k, c->score_bits, c->d_partial,
                                   c->stream));
   if (e1) HIP_TRY(hipEventRecord(*e1, c->stream));
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
-  HIP_TRY(kh::launch_topk_merge(c->d_partial, (int64_t)nchunks * k, k, np, nchunks, k, ht, out, c->stream));
+  HIP_TRY(kh::launch_topk_merge(c->d_partial, (int64_t)nchunks * k, k, np, nchunks, k, c->score_bits, out, c->stream));
   return 0;
 }
 
@@ -564,7 +562,7 @@ int koordhip_place_staged(koordhip_ctx *c) {
       if (np < P) HIP_TRY(hipMemsetAsync(c->d_lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
       NCCL_TRY(ncclAllGather(c->d_lists, c->d_gather, (size_t)P * K, ncclUint64, c->comm, c->stream));
-      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, nullptr, c->d_final, c->stream));
+      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits, c->d_final, c->stream));
       HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0, c->d_dbg, c->stream));
     } else {
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;

@@ -22,10 +22,10 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_p
 // k_topk_partial: one wave evaluates 64 x R nodes (R in {1, 2, 4, 8})
 hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
                                int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
-                               uint64_t *out, uint64_t *ht, hipStream_t s);
-// ht: optional [n_pods][L][2] (head, tail-if-full) written by the partial kernel
+                               uint64_t *out, hipStream_t s);
+// lists: ranges ascending with l, equal-score keys in ascending node order
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
-                             int32_t k, const uint64_t *ht, uint64_t *out, hipStream_t s);
+                             int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s);
 template <typename T>
 hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods, int32_t k,

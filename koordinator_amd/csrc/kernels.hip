@@ -164,8 +164,7 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const koordhip_pod *__restrict
 template <int R>
 __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
                                                       int32_t n_pods, int32_t lo, int32_t hi, int32_t k,
-                                                      int32_t score_bits, uint64_t *__restrict__ out,
-                                                      uint64_t *__restrict__ out_ht) {
+                                                      int32_t score_bits, uint64_t *__restrict__ out) {
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const int32_t p = blockIdx.y * (blockDim.x >> 6) + wave;
@@ -208,7 +207,6 @@ __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, cons
   const size_t list = (size_t)p * gridDim.x + blockIdx.x;
   uint64_t *o = out + list * k;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint64_t hmax = 0, nmin = 0;  // max selected key, max of ~key (= ~min key)
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const bool eq = s[r] == T && s[r] > 0;
@@ -221,125 +219,197 @@ __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, cons
       const int32_t i = c0 + r * 64 + lane;
       const uint64_t key = (((uint64_t)(uint32_t)s[r]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
       o[base + __popcll(ms & lt)] = key;
-      hmax = key > hmax ? key : hmax;
-      nmin = ~key > nmin ? ~key : nmin;
     }
     base += __popcll(ms);
   }
   for (int32_t j = base + lane; j < k; j += 64) o[j] = 0;
-  // list head and (full list) tail for the merge's pruning bound
-  hmax = wave_max_u64_dpp(hmax);
-  nmin = wave_max_u64_dpp(nmin);
-  if (lane == 0) {
-    out_ht[2 * list] = hmax;
-    out_ht[2 * list + 1] = base >= k ? ~nmin : 0;
-  }
 }
 
 // ---------------------------------------------------------------------------
-// k_topk_merge: per pod, exact top-k of L lists of k keys (each the exact
-// top-k of its node range, unsorted, 0-padded).
+// k_topk_merge: per pod, the exact top-k of L lists of k keys.
 //
-// A lower bound tau on the pod's k-th key prunes the candidates: the k-th
-// largest of the list heads and the largest tail of a full list both are.
-// Keys >= tau are gathered in LDS and rank-sorted (keys are unique).
+// Input contract: list l holds the exact top-k of a contiguous node range,
+// the ranges ascend with l, and inside a list keys of equal score appear in
+// ascending node order (0 = empty slot).  Then the pod's k-th largest score
+// S over the union of the lists is the global one; every key scoring > S is
+// in some list (fewer than k of them), and the lowest-index ties at S are the
+// first ties of the first lists.  So: radix-select S on the score (two 8-bit
+// digits, LDS histograms), gather the > S keys, and take the ties list by
+// list in order with a block prefix sum -- no comparison sort of candidates.
+
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// Copy `bytes` (a multiple of 1 KiB) global -> LDS with LDS-DMA, 16 B per lane
+// per instruction, all in flight at once; the caller waits (vmcnt) + barriers.
+__device__ __forceinline__ void dma_to_lds(void *lds, const void *src, int32_t bytes, int lane) {
+  const char *g = static_cast<const char *>(src);
+  char *l = static_cast<char *>(lds);
+  for (int32_t off = 0; off < bytes; off += 1024)
+    __builtin_amdgcn_global_load_lds((gvoid_t *)(g + off + lane * 16), (lvoid_t *)(l + off), 16, 0, 0);
+}
+
+// The same across a whole workgroup (each wave takes every 4th KiB).
+__device__ __forceinline__ void dma_to_lds_block(void *lds, const void *src, int32_t bytes) {
+  const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const char *g = static_cast<const char *>(src);
+  char *l = static_cast<char *>(lds);
+  for (int32_t off = w * 1024; off < bytes; off += nw * 1024)
+    __builtin_amdgcn_global_load_lds((gvoid_t *)(g + off + lane * 16), (lvoid_t *)(l + off), 16, 0, 0);
+}
 
 constexpr int MERGE_THREADS = 256;
-constexpr int MERGE_CAP = 2048;
-constexpr int MERGE_MAXL = 2048;
+constexpr int RES_MAXP = 64;         // max pods per round = max k
+constexpr int MERGE_STAGE = 8192;    // keys staged in LDS (64 KiB)
+constexpr int MERGE_MAXL = 4096;     // lists per pod
 
-__device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t *red) {
-  v = wave_max_u64(v);
-  const int w = threadIdx.x >> 6;
-  if (lane_id() == 0) red[w] = v;
+__device__ __forceinline__ int32_t key_sc(uint64_t k) { return (int32_t)(k >> 32); }  // score + 1
+
+// Block-wide exclusive prefix sum of one value per thread (wave shuffles + one
+// LDS exchange of the 4 wave totals).
+__device__ __forceinline__ int32_t block_exclusive_scan(int32_t v, int32_t *wsum, int32_t *total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  int32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
   __syncthreads();
-  uint64_t r = 0;
-  for (int j = 0; j < (int)(blockDim.x >> 6); j++) r = red[j] > r ? red[j] : r;
+  int32_t base = 0, tot = 0;
+  for (int q = 0; q < MERGE_THREADS / 64; q++) {
+    if (q < w) base += wsum[q];
+    tot += wsum[q];
+  }
   __syncthreads();
-  return r;
+  *total = tot;
+  return base + x - v;
 }
 
 __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__restrict__ in, int64_t pod_stride,
                                                               int64_t list_stride, int32_t L, int32_t k,
-                                                              const uint64_t *__restrict__ ht,
-                                                              uint64_t *__restrict__ out) {
-  __shared__ uint64_t buf[MERGE_CAP];
-  __shared__ uint64_t heads[MERGE_MAXL];
-  __shared__ uint64_t red[MERGE_THREADS / 64];
-  __shared__ int32_t cnt;
+                                                              int32_t score_bits, uint64_t *__restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint64_t stage[MERGE_STAGE + 128];
+  __shared__ int32_t tie_pre[MERGE_MAXL];
+  __shared__ uint64_t gtbuf[RES_MAXP];
+  __shared__ int32_t wsum[MERGE_THREADS / 64];
+  __shared__ int32_t cnt_gt;
+  const int t = threadIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
   const int32_t p = blockIdx.x;
   const uint64_t *lists = in + (size_t)p * pod_stride;
-  const int32_t Lh = min(L, MERGE_MAXL);
-  // 1. per-list head and (full lists) tail: from the partial kernel when it
-  //    wrote them (ht != nullptr), else by scanning the lists
-  uint64_t tail = 0;
-  for (int32_t l = threadIdx.x; l < L; l += blockDim.x) {
-    uint64_t mx = 0, mn = 0;
-    if (ht) {
-      mx = ht[2 * ((size_t)p * L + l)];
-      mn = ht[2 * ((size_t)p * L + l) + 1];
-    } else {
-      const uint64_t *x = lists + (size_t)l * list_stride;
-      mn = ~0ull;
-      for (int32_t j = 0; j < k; j++) {
-        const uint64_t y = x[j];
-        mx = y > mx ? y : mx;
-        mn = y < mn ? y : mn;
-      }
-    }
-    tail = mn > tail ? mn : tail;  // full list: k keys >= its min (0 when not full)
-    if (l < Lh) heads[l] = mx;
-  }
-  __syncthreads();
-  // k-th largest head (distinct keys; 0s are empty lists)
-  uint64_t th = 0;
-  if (Lh >= k) {
-    for (int32_t l = threadIdx.x; l < Lh; l += blockDim.x) {
-      const uint64_t h = heads[l];
-      int32_t rank = 0;
-      for (int32_t q = 0; q < Lh; q++) rank += heads[q] > h;
-      if (rank == k - 1) th = h;
-    }
-  }
-  const uint64_t tau = block_max_u64(th > tail ? th : tail, red);
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
-  // 2. gather every key >= tau
   const int32_t total = L * k;
-  for (int32_t t = threadIdx.x; t < total; t += blockDim.x) {
-    const int32_t l = t / k, j = t - l * k;
-    const uint64_t y = lists[(size_t)l * list_stride + j];
-    if (y != 0 && y >= tau) {
-      const int32_t slot = atomicAdd(&cnt, 1);
-      if (slot < MERGE_CAP) buf[slot] = y;
-    }
+  const bool staged = total <= MERGE_STAGE && L <= MERGE_MAXL;
+  auto gkey = [&](int32_t l, int32_t j) -> uint64_t { return lists[(size_t)l * list_stride + j]; };
+  auto key = [&](int32_t l, int32_t j) -> uint64_t { return staged ? stage[l * k + j] : gkey(l, j); };
+  // ---- 1. stage the lists in LDS
+  if (t == 0) {
+
+    cnt_gt = 0;
+  }
+  if (staged && list_stride == k) {
+    // contiguous lists: one LDS-DMA burst (the buffer is padded to 1 KiB)
+    dma_to_lds_block(stage, lists, (total * 8 + 1023) & ~1023);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (staged) {
+    for (int32_t l = w; l < L; l += MERGE_THREADS / 64)
+      for (int32_t j = lane; j < k; j += 64) stage[l * k + j] = gkey(l, j);
   }
   __syncthreads();
-  const int32_t m = cnt;
-  uint64_t *o = out + (size_t)p * k;
-  if (m <= MERGE_CAP) {
-    for (int32_t j = threadIdx.x; j < m; j += blockDim.x) {
-      const uint64_t x = buf[j];
-      int32_t rank = 0;
-      for (int32_t q = 0; q < m; q++) rank += buf[q] > x;
-      if (rank < k) o[rank] = x;
+  // ---- 2. k-th largest score S: bitwise search on counts, keys' scores held
+  //         in registers (up to MERGE_STAGE / MERGE_THREADS per thread)
+  constexpr int PER = MERGE_STAGE / MERGE_THREADS;
+  int32_t sc[PER];
+  int32_t mine = 0;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int32_t q = t + i * MERGE_THREADS;
+    if (staged) {
+      sc[i] = q < total ? key_sc(stage[q]) : 0;
+    } else {
+      sc[i] = 0;
     }
-    for (int32_t j = m + threadIdx.x; j < k; j += blockDim.x) o[j] = 0;
-  } else {
-    // overflow: k rounds of "largest key below the previous one"
-    uint64_t prev = ~0ull;
-    for (int32_t r = 0; r < k; r++) {
-      uint64_t b = 0;
-      for (int32_t t = threadIdx.x; t < total; t += blockDim.x) {
-        const int32_t l = t / k, j = t - l * k;
-        const uint64_t x = lists[(size_t)l * list_stride + j];
-        if (x < prev && x > b) b = x;
+    mine += sc[i] > 0;
+  }
+  if (!staged)  // large inputs: count from global memory
+    for (int32_t q = t; q < total; q += MERGE_THREADS) {
+      const int32_t l = q / k;
+      mine += key_sc(gkey(l, q - l * k)) > 0;
+    }
+  int32_t n_keys;
+  (void)block_exclusive_scan(mine, wsum, &n_keys);
+  int32_t S = 1;
+  if (n_keys > k) {
+    S = 0;
+    for (int b = score_bits; b >= 0; b--) {
+      const int32_t cand = S | (1 << b);
+      int32_t c = 0;
+      if (staged) {
+#pragma unroll
+        for (int i = 0; i < PER; i++) c += sc[i] >= cand;
+      } else {
+        for (int32_t q = t; q < total; q += MERGE_THREADS) {
+          const int32_t l = q / k;
+          c += key_sc(gkey(l, q - l * k)) >= cand;
+        }
       }
-      b = block_max_u64(b, red);
-      if (threadIdx.x == 0) o[r] = b;
-      prev = b;
+      int32_t cnt;
+      (void)block_exclusive_scan(c, wsum, &cnt);
+      if (cnt >= k) S = cand;
     }
   }
+  // ---- 3. keys above S (fewer than k) and tie counts per list
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int32_t l = w; l < L; l += MERGE_THREADS / 64) {
+    int32_t ties = 0;
+    for (int32_t j0 = 0; j0 < k; j0 += 64) {
+      const int32_t j = j0 + lane;
+      const uint64_t x = j < k ? key(l, j) : 0;
+      const int32_t sc = key_sc(x);
+      if (sc > S) gtbuf[atomicAdd(&cnt_gt, 1)] = x;
+      ties += __popcll(__ballot(sc == S));
+    }
+    if (lane == 0 && l < MERGE_MAXL) tie_pre[l] = ties;
+  }
+  __syncthreads();
+  // per-list exclusive prefix of the tie counts (lists in node order)
+  const int32_t per = (L + MERGE_THREADS - 1) / MERGE_THREADS;
+  const int32_t l0 = min(L, t * per), l1 = min(L, l0 + per);
+  int32_t seg = 0;
+  for (int32_t l = l0; l < l1; l++) seg += tie_pre[l];
+  int32_t all_ties;
+  int32_t run = block_exclusive_scan(seg, wsum, &all_ties);
+  for (int32_t l = l0; l < l1; l++) {
+    const int32_t c = tie_pre[l];
+    tie_pre[l] = run;
+    run += c;
+  }
+  __syncthreads();
+  // ---- 4. output: sorted keys above S, then the lowest-index ties
+  const int32_t gt = cnt_gt;
+  const int32_t need = k - gt;
+  uint64_t *o = out + (size_t)p * k;
+  for (int32_t j = t; j < gt; j += MERGE_THREADS) {
+    const uint64_t x = gtbuf[j];
+    int32_t rank = 0;
+    for (int32_t q = 0; q < gt; q++) rank += gtbuf[q] > x;
+    o[rank] = x;
+  }
+  for (int32_t l = w; l < L; l += MERGE_THREADS / 64) {
+    int32_t base = tie_pre[l];
+    if (base >= need) continue;  // wave-uniform
+    for (int32_t j0 = 0; j0 < k; j0 += 64) {
+      const int32_t j = j0 + lane;
+      const uint64_t x = j < k ? key(l, j) : 0;
+      const bool tie = key_sc(x) == S;
+      const uint64_t tb = __ballot(tie);
+      const int32_t pos = base + __popcll(tb & lt);
+      if (tie && pos < need) o[gt + pos] = x;
+      base += __popcll(tb);
+    }
+  }
+  const int32_t filled = gt + min(need, all_ties);
+  for (int32_t j = filled + t; j < k; j += MERGE_THREADS) o[j] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -355,7 +425,6 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 // can only win if it ranks above that first entry, so the re-evaluation is
 // skipped when no list prefix entry is modified.
 
-constexpr int RES_MAXP = 64;
 __device__ __forceinline__ void copy_row(NV *dst, const NV *src, int lane) {
   constexpr int W = (int)(sizeof(NV) / 8);
   static_assert(sizeof(NV) % 8 == 0 && W <= 64, "NV must be a whole number of 8-byte words");
@@ -366,18 +435,6 @@ __device__ __forceinline__ uint64_t stamp() {
   uint64_t t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
-}
-
-typedef __attribute__((address_space(1))) void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-
-// Copy `bytes` (a multiple of 1 KiB) global -> LDS with LDS-DMA, 16 B per lane
-// per instruction, all in flight at once; the caller waits (vmcnt) + barriers.
-__device__ __forceinline__ void dma_to_lds(void *lds, const void *src, int32_t bytes, int lane) {
-  const char *g = static_cast<const char *>(src);
-  char *l = static_cast<char *>(lds);
-  for (int32_t off = 0; off < bytes; off += 1024)
-    __builtin_amdgcn_global_load_lds((gvoid_t *)(g + off + lane * 16), (lvoid_t *)(l + off), 16, 0, 0);
 }
 
 constexpr int RES_PRE = 128;  // prefetched snapshot rows per round
@@ -563,28 +620,30 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_p
 
 hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
                                int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
-                               uint64_t *out, uint64_t *ht, hipStream_t s) {
+                               uint64_t *out, hipStream_t s) {
   dim3 grid(nchunks, (n_pods + 3) / 4);
   switch (R) {
     case 1:
-      hipLaunchKernelGGL(k_topk_partial<1>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
+      hipLaunchKernelGGL(k_topk_partial<1>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
       break;
     case 2:
-      hipLaunchKernelGGL(k_topk_partial<2>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
+      hipLaunchKernelGGL(k_topk_partial<2>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
       break;
     case 4:
-      hipLaunchKernelGGL(k_topk_partial<4>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
+      hipLaunchKernelGGL(k_topk_partial<4>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
       break;
     default:
-      hipLaunchKernelGGL(k_topk_partial<8>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out, ht);
+      hipLaunchKernelGGL(k_topk_partial<8>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
       break;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
-                             int32_t k, const uint64_t *ht, uint64_t *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_topk_merge, dim3(n_pods), dim3(MERGE_THREADS), 0, s, in, pod_stride, list_stride, L, k, ht, out);
+                             int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s) {
+  if (score_bits > 16 || L > MERGE_MAXL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_topk_merge, dim3(n_pods), dim3(MERGE_THREADS), 0, s, in, pod_stride, list_stride, L, k,
+                     score_bits, out);
   return hipGetLastError();
 }
 
