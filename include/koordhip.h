@@ -217,6 +217,13 @@ int koordhip_comm_unique_id(uint8_t *id_out /* KOORDHIP_UNIQUE_ID_BYTES */);
 /* Attach an RCCL communicator: this context then evaluates only node shard
  * [rank*n/world, (rank+1)*n/world) and merges per-shard top-k over xGMI. */
 int koordhip_comm_init(koordhip_ctx *ctx, const uint8_t *id, int32_t world, int32_t rank);
+/* The same sharding for `world` contexts driven by ONE process (one host
+ * thread per context, e.g. one scheduler process owning several GPUs, or
+ * several contexts on one GPU): ctxs[r] becomes rank r and the per-round
+ * exchange is a device-to-device copy instead of RCCL.  The contexts'
+ * place_staged / place_stream calls must then run concurrently with the same
+ * pod stream, as collective calls. */
+int koordhip_comm_init_local(koordhip_ctx **ctxs, int32_t world);
 
 #ifdef __cplusplus
 }

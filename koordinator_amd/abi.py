@@ -140,6 +140,7 @@ def load_library(path: str = LIB_PATH):
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_comm_unique_id": (C.c_int, [C.c_char_p]),
         "koordhip_comm_init": (C.c_int, [vp, C.c_char_p, C.c_int32, C.c_int32]),
+        "koordhip_comm_init_local": (C.c_int, [C.POINTER(vp), C.c_int32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -156,7 +157,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit", "koordhip_last_stats",
-    "koordhip_comm_unique_id", "koordhip_comm_init",
+    "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]
 
 

@@ -6,6 +6,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -41,6 +44,39 @@ constexpr int kDefaultBatch = 64;
 constexpr int32_t kMaxNodes = 700000;  // resolve keeps a per-node bit in LDS
 constexpr int kMaxBatch = 64;
 
+// Contexts of one process sharing node shards without RCCL
+// (koordhip_comm_init_local): a generation barrier per exchange step; a
+// failing member aborts the group so its peers return instead of waiting.
+struct LocalGroup {
+  int32_t world = 0;
+  std::vector<koordhip_ctx *> ctx;
+  std::vector<int64_t> keys;
+  std::mutex mu;
+  std::condition_variable cv;
+  int32_t arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+
+  bool barrier() {
+    std::unique_lock<std::mutex> l(mu);
+    if (aborted) return false;
+    const uint64_t g = gen;
+    if (++arrived == world) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+      return true;
+    }
+    cv.wait(l, [&] { return gen != g || aborted; });
+    return gen != g;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> l(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+};
+
 }  // namespace
 
 struct koordhip_ctx {
@@ -68,6 +104,7 @@ struct koordhip_ctx {
   size_t partial_cap = 0;
   uint64_t *d_lists = nullptr;   // [batch][k]
   uint64_t *d_gather = nullptr;  // [world][batch][k]
+  int32_t gather_world = 1;
   uint64_t *d_final = nullptr;   // [batch][k]
   koordhip_pod *d_tmp_pod = nullptr;
   uint64_t *d_dbg = nullptr;  // KOORDHIP_STAMPS diagnostic counters (resolve segments)
@@ -77,6 +114,8 @@ struct koordhip_ctx {
 
   // sharding
   ncclComm_t comm = nullptr;
+  std::shared_ptr<LocalGroup> group;       // koordhip_comm_init_local
+  hipEvent_t ev_part = nullptr, ev_copy = nullptr;
   int32_t world = 1, rank = 0;
 
   // stats
@@ -263,6 +302,9 @@ int koordhip_destroy(koordhip_ctx *c) {
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->group) c->group->abort();
+  for (hipEvent_t e : {c->ev_part, c->ev_copy})
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -531,8 +573,65 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
   return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+// All-gather of the per-shard lists of one round: RCCL, or for a local group
+// a device-to-device pull of every member's list after its eval finished
+// (events + host barrier), then a second barrier so no member overwrites its
+// list before every peer has copied it.
+int exchange(koordhip_ctx *c, size_t count) {
+  if (c->comm) {
+    NCCL_TRY(ncclAllGather(c->d_lists, c->d_gather, count, ncclUint64, c->comm, c->stream));
+    return 0;
+  }
+  LocalGroup &g = *c->group;
+  HIP_TRY(hipEventRecord(c->ev_part, c->stream));
+  if (!g.barrier()) return fail(KOORDHIP_ECOMM, "local group aborted by a peer");
+  for (int32_t j = 0; j < g.world; j++) {
+    koordhip_ctx *p = g.ctx[j];
+    if (p != c) HIP_TRY(hipStreamWaitEvent(c->stream, p->ev_part, 0));
+    HIP_TRY(hipMemcpyAsync(c->d_gather + (size_t)j * count, p->d_lists, count * sizeof(uint64_t), hipMemcpyDefault,
+                           c->stream));
+  }
+  HIP_TRY(hipEventRecord(c->ev_copy, c->stream));
+  if (!g.barrier()) return fail(KOORDHIP_ECOMM, "local group aborted by a peer");
+  for (int32_t j = 0; j < g.world; j++)
+    if (g.ctx[j] != c) HIP_TRY(hipStreamWaitEvent(c->stream, g.ctx[j]->ev_copy, 0));
+  return 0;
+}
+
+// Members of a local group must agree on the stream before the first round,
+// or the per-round barriers would never match up.
+int group_agree(koordhip_ctx *c) {
+  LocalGroup &g = *c->group;
+  const int64_t key = ((int64_t)c->n << 40) ^ ((int64_t)c->n_staged << 8) ^ c->batch;
+  g.keys[c->rank] = key;
+  if (!g.barrier()) return fail(KOORDHIP_ECOMM, "local group aborted by a peer");
+  for (int32_t j = 0; j < g.world; j++)
+    if (g.keys[j] != key) return fail(KOORDHIP_EINVAL, "local group members disagree on snapshot size, stream or batch");
+  return 0;
+}
+
+int place_staged_impl(koordhip_ctx *c);
+
+}  // namespace
+
+extern "C" {
+
 int koordhip_place_staged(koordhip_ctx *c) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  const int e = place_staged_impl(c);
+  if (e && c->group) c->group->abort();
+  return e;
+}
+
+}  // extern "C"
+
+namespace {
+
+int place_staged_impl(koordhip_ctx *c) {
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   HIP_TRY(hipSetDevice(c->device));
   const int32_t P = c->batch, K = c->batch;
@@ -541,9 +640,15 @@ int koordhip_place_staged(koordhip_ctx *c) {
     HIP_TRY(hipMalloc(&c->d_lists, (size_t)kMaxBatch * kMaxBatch * sizeof(uint64_t)));
     HIP_TRY(hipMalloc(&c->d_final, (size_t)kMaxBatch * kMaxBatch * sizeof(uint64_t)));
   }
-  if (c->world > 1 && !c->d_gather)
+  if (c->world > c->gather_world) {
+    if (c->d_gather) HIP_TRY(hipFree(c->d_gather));
+    c->d_gather = nullptr;
     HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * kMaxBatch * kMaxBatch * sizeof(uint64_t)));
+    c->gather_world = c->world;
+  }
   (void)cap;
+  if (c->group)
+    if (int e = group_agree(c)) return e;
   int32_t lo = 0, hi = c->n;
   shard(c, &lo, &hi);
   c->ev_used = 0;
@@ -561,7 +666,7 @@ int koordhip_place_staged(koordhip_ctx *c) {
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(c->d_lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
-      NCCL_TRY(ncclAllGather(c->d_lists, c->d_gather, (size_t)P * K, ncclUint64, c->comm, c->stream));
+      if (int e = exchange(c, (size_t)P * K)) return e;
       HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits, c->d_final, c->stream));
       HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0, c->d_dbg, c->stream));
     } else {
@@ -582,6 +687,10 @@ int koordhip_place_staged(koordhip_ctx *c) {
   }
   return 0;
 }
+
+}  // namespace
+
+extern "C" {
 
 int koordhip_synchronize(koordhip_ctx *c) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
@@ -699,6 +808,7 @@ int koordhip_comm_init(koordhip_ctx *c, const uint8_t *id, int32_t world, int32_
     (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
   }
+  c->group.reset();
   if (world > 1) {
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
@@ -706,6 +816,34 @@ int koordhip_comm_init(koordhip_ctx *c, const uint8_t *id, int32_t world, int32_
   }
   c->world = world;
   c->rank = rank;
+  return 0;
+}
+
+int koordhip_comm_init_local(koordhip_ctx **ctxs, int32_t world) {
+  if (!ctxs) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (world < 1 || world > 64) return fail(KOORDHIP_EINVAL, "world must be in [1, 64]");
+  for (int32_t r = 0; r < world; r++) {
+    if (!ctxs[r]) return fail(KOORDHIP_EINVAL, "NULL context in group");
+    for (int32_t q = 0; q < r; q++)
+      if (ctxs[q] == ctxs[r]) return fail(KOORDHIP_EINVAL, "context listed twice in group");
+  }
+  auto g = std::make_shared<LocalGroup>();
+  g->world = world;
+  g->ctx.assign(ctxs, ctxs + world);
+  g->keys.assign(world, 0);
+  for (int32_t r = 0; r < world; r++) {
+    koordhip_ctx *c = ctxs[r];
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->comm) {
+      (void)ncclCommDestroy(c->comm);
+      c->comm = nullptr;
+    }
+    for (hipEvent_t *e : {&c->ev_part, &c->ev_copy})
+      if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    c->group = world > 1 ? g : nullptr;
+    c->world = world;
+    c->rank = r;
+  }
   return 0;
 }
 

@@ -130,3 +130,35 @@ class PlacementEngine:
 
     def comm_init(self, uid: bytes, world: int, rank: int):
         abi.check(self.lib, self.lib.koordhip_comm_init(self._ctx, uid, world, rank))
+
+    @staticmethod
+    def comm_init_local(engines):
+        """One process, several contexts (GPUs, or contexts sharing one GPU):
+        engines[r] becomes rank r of a node-sharded group (koordhip_comm_init_local)."""
+        lib = abi.load_library()
+        arr = (C.c_void_p * len(engines))(*[e._ctx.value for e in engines])
+        abi.check(lib, lib.koordhip_comm_init_local(arr, len(engines)))
+
+
+def place_stream_group(engines, pods: np.ndarray) -> list:
+    """Collective place_stream over a local group: one host thread per context
+    (ctypes releases the GIL for the duration of each call)."""
+    import threading
+    out = [None] * len(engines)
+    err = [None] * len(engines)
+
+    def run(r):
+        try:
+            out[r] = engines[r].place_stream(pods)
+        except Exception as e:  # noqa: BLE001 - re-raised below
+            err[r] = e
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(len(engines))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    return out

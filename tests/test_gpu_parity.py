@@ -212,3 +212,38 @@ def test_plugin_subsets(Engine):
             got = e.place_stream(pods)
         ref = oracle.Oracle(cfg, table).place_stream(pods)
         assert np.array_equal(got, ref), (filters, scores)
+
+
+# ------------------------------------------------- node-sharded groups (§8(e))
+@pytest.mark.parametrize("world,n_nodes,n_pods,be,batch", [
+    (2, 3000, 1500, 0.3, 0),
+    (3, 1001, 800, 0.3, 32),
+    (4, 77, 500, 0.5, 17),     # tiny shards, pile-ups, unschedulable tail
+    (4, 3, 40, 0.3, 8),        # a shard with no nodes
+])
+def test_sharded_group_bit_exact(Engine, world, n_nodes, n_pods, be, batch):
+    """Node-index shards evaluated by `world` contexts on one GPU, per-shard
+    top-k exchanged by the local group (the RCCL path's layout and merge), then
+    the replicated resolve: every rank must return the unsharded placements."""
+    from koordinator_amd.engine import place_stream_group
+    prof, table, pods = workload(n_nodes, n_pods, be)
+    prof.batch_pods = batch
+    cfg = to_c_config(prof)
+    engines = [Engine(prof, device=0) for _ in range(world)]
+    try:
+        for e in engines:
+            e.load_snapshot(table)
+        Engine.comm_init_local(engines)
+        outs = place_stream_group(engines, pods)
+        states = [e.read_nodes() for e in engines]
+    finally:
+        for e in engines:
+            e.close()
+    o = oracle.Oracle(cfg, table)
+    ref = o.place_stream(pods)
+    for r in range(world):
+        assert np.array_equal(outs[r], ref), (r, int(np.flatnonzero(outs[r] != ref)[0]))
+    rs = o.state()
+    for s in states:
+        for k in ("requested", "npods", "la_used"):
+            assert np.array_equal(s[k], rs[k]), k
