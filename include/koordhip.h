@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 1
+#define KOORDHIP_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -44,6 +44,7 @@ extern "C" {
 #define KOORDHIP_ESTATE (-3)   /* call out of order (e.g. eval before load_snapshot) */
 #define KOORDHIP_ENOMEM (-4)
 #define KOORDHIP_ECOMM (-5)    /* RCCL error */
+#define KOORDHIP_ERESERVE (-6) /* a Reserve plugin failed (NodeNUMAResource Allocate, plugin.go:398-401) */
 
 /* ---- plugins ------------------------------------------------------------ */
 #define KOORDHIP_PLUGIN_FIT 1u        /* NodeResourcesFit (upstream) */
@@ -78,6 +79,43 @@ extern "C" {
 #define KOORDHIP_POD_REQ_BMEM 16u     /* batch-memory key present in the pod request map */
 #define KOORDHIP_POD_CPUSET 32u       /* NUMA: requestCPUBind (plugin.go:230-245) */
 #define KOORDHIP_POD_NUMA_SKIP 64u    /* NUMA: PreFilter skip (zero request) (plugin.go:218-226) */
+#define KOORDHIP_POD_NUMA_ERROR 128u  /* NUMA: PreFilter error (non-integral cpuset request, plugin.go:242-245) */
+
+/* koordhip_pod.numa_policy, the NUMA PreFilter state (plugin.go:227-255):
+ * bits 0-1 requiredCPUBindPolicy, 2-3 preferredCPUBindPolicy (= required when
+ * set), 4-5 preferredCPUExclusivePolicy. */
+#define KOORDHIP_CPUBIND_NONE 0u
+#define KOORDHIP_CPUBIND_FULL_PCPUS 1u
+#define KOORDHIP_CPUBIND_SPREAD_BY_PCPUS 2u
+#define KOORDHIP_CPUEXCL_NONE 0u
+#define KOORDHIP_CPUEXCL_PCPU 1u
+#define KOORDHIP_CPUEXCL_NUMA 2u
+#define KOORDHIP_NUMA_REQUIRED(p) ((p) & 3u)
+#define KOORDHIP_NUMA_PREFERRED(p) (((p) >> 2) & 3u)
+#define KOORDHIP_NUMA_EXCLUSIVE(p) (((p) >> 4) & 3u)
+
+/* koordhip_node_soa.numa_flags: node CPU bind policy (GetNodeCPUBindPolicy,
+ * apis/extension/numa_aware.go:314-325) and NUMA allocate strategy
+ * (GetNUMAAllocateStrategy, nodenumaresource/util.go:34-40). */
+#define KOORDHIP_NODE_CPUBIND_MASK 3u   /* 0 None, 1 FullPCPUsOnly, 2 SpreadByPCPUs */
+#define KOORDHIP_NODE_NUMA_MOST_ALLOCATED 4u
+
+/* CPU topology of a node (cpu_topology.go:25-103), shared by every node of
+ * the same shape.  CPU "positions" are core-major: pos = core_rank *
+ * cpus_per_core + t, cores in ascending CoreID, t in ascending CPU id, so one
+ * bit per position in a 4 x 64-bit mask.  NUMA nodes and sockets are ranked
+ * by ascending id.  Every core must hold exactly cpus_per_core CPUs. */
+#define KOORDHIP_NUMA_MAX_CPUS 256
+#define KOORDHIP_NUMA_MAX_NODES 8
+#define KOORDHIP_NUMA_WORDS 4
+typedef struct koordhip_numa_class {
+  int32_t num_cpus, num_cores, num_nodes, num_sockets; /* CPUTopology counters (builder semantics) */
+  int32_t cpus_per_core;
+  int32_t reserved0;
+  int32_t cpu_id[KOORDHIP_NUMA_MAX_CPUS];       /* pos -> logical CPU id */
+  uint8_t node_of[KOORDHIP_NUMA_MAX_CPUS];      /* pos -> NUMA node rank */
+  uint8_t socket_of[KOORDHIP_NUMA_MAX_CPUS];    /* pos -> socket rank */
+} koordhip_numa_class;
 
 /* Per-(pod,node) status bits written by koordhip_eval (no short-circuit, one
  * bit per plugin that returned non-Success from Filter). */
@@ -137,6 +175,17 @@ typedef struct koordhip_node_soa {
   const int64_t *laf_thr[2];               /* resolved usage thresholds cpu, memory (0 = disabled) */
   const int64_t *laf_prod_thr[2];          /* resolved prod usage thresholds (0 = disabled) */
   const uint8_t *la_flags;                 /* KOORDHIP_LA_* */
+  /* NodeNUMAResource (TopologyOptions + NodeAllocation, topology_options.go:40-48,
+   * node_allocation.go:32-38); all NULL / n_numa_classes = 0 when unused */
+  const koordhip_numa_class *numa_classes;
+  int32_t n_numa_classes;
+  int32_t reserved0;
+  const int32_t *numa_class;               /* class index, -1 = no (valid) CPU topology */
+  const uint64_t *numa_free[KOORDHIP_NUMA_WORDS];      /* available CPUs: all - refcount>=1 - ReservedCPUs (node_allocation.go:133-153) */
+  const uint64_t *numa_excl_pcpu[KOORDHIP_NUMA_WORDS]; /* allocated CPUs whose ExclusivePolicy is PCPULevel */
+  const uint64_t *numa_excl_numa[KOORDHIP_NUMA_WORDS]; /* allocated CPUs whose ExclusivePolicy is NUMANodeLevel */
+  const int32_t *numa_alloc_cnt;           /* |allocatedCPUs| (scoring.go:161-166) */
+  const uint8_t *numa_flags;               /* KOORDHIP_NODE_* */
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -147,8 +196,10 @@ typedef struct koordhip_pod {
   int64_t est_cpu;            /* EstimatePod(pod)[cpu]    (default_estimator.go:57-108) */
   int64_t est_mem;            /* EstimatePod(pod)[memory] */
   uint32_t flags;             /* KOORDHIP_POD_* */
-  int32_t numa_cpus;          /* NUMA numCPUsNeeded (plugin.go:247) */
-  int64_t reserved[2];
+  int32_t numa_cpus;          /* NUMA numCPUsNeeded (plugin.go:252) */
+  uint32_t numa_policy;       /* KOORDHIP_NUMA_* packed policies */
+  int32_t reserved0;
+  int64_t reserved1;
 } koordhip_pod;
 
 /* One top-k record of koordhip_eval. */
@@ -175,17 +226,24 @@ int koordhip_update_nodes(koordhip_ctx *ctx, const int32_t *idx, const koordhip_
  * pointer may be NULL.  Used by tests and the Go shim's debug service. */
 int koordhip_read_nodes(koordhip_ctx *ctx, int64_t *requested /* [NRES][n] */, int64_t *nz /* [2][n] */,
                         int32_t *npods, int64_t *la_used /* [2][n] */, int64_t *la_used_prod /* [2][n] */);
+/* NodeNUMAResource mutable state: free / exclusive masks [WORDS][n], allocated CPU counts [n]. */
+int koordhip_read_numa(koordhip_ctx *ctx, uint64_t *free_mask, uint64_t *excl_pcpu, uint64_t *excl_numa,
+                       int32_t *alloc_cnt);
 
 /* Parity/debug mode, no commit: for n_pods pods against the current state.
  *   status : optional, [n_pods][n] KOORDHIP_ST_* bits (every plugin evaluated)
- *   scores : optional, [n_pods][KOORDHIP_NPLUGINS][n] per-plugin scores (0 where the plugin is disabled)
+ *   scores : optional, [n_pods][KOORDHIP_NPLUGINS][n] per-plugin scores (0 where the plugin is disabled;
+ *            the NodeNUMAResource score of a pair failing the NUMA Filter is unspecified, as the
+ *            framework never scores such a node)
  *   topk   : optional, [n_pods][k] best feasible nodes by (total desc, index asc), node = -1 past the end */
 int koordhip_eval(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, uint8_t *status, int32_t *scores,
                   koordhip_topk *topk, int32_t k);
 
 /* Greedy stream: pods attempted once, in order, each against the state left
  * by all earlier commits; winner = lowest-index max total score; the Reserve
- * delta is applied on device.  out_node[i] = node, -1 unschedulable. */
+ * delta is applied on device.  out_node[i] = node, -1 unschedulable, -2 the
+ * winner's Reserve failed (NodeNUMAResource Allocate; nothing committed, no
+ * retry). */
 int koordhip_place_stream(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, int32_t *out_node);
 
 /* The same split in two so a caller can time the device part alone: stage
@@ -202,9 +260,19 @@ int koordhip_synchronize(koordhip_ctx *ctx);
 int koordhip_checkpoint(koordhip_ctx *ctx);
 int koordhip_restore(koordhip_ctx *ctx);
 
-/* Reserve / Unreserve of one pod on one node (state delta only). */
-int koordhip_commit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node);
-int koordhip_uncommit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node);
+/* Reserve / Unreserve of one pod on one node (state delta only).  For a
+ * cpuset pod the NodeNUMAResource Reserve allocates CPUs (the exact
+ * cpuAccumulator choice, cpu_accumulator.go:87-232); cpus_out (optional,
+ * KOORDHIP_NUMA_WORDS words, core-major positions) receives them, and
+ * KOORDHIP_ERESERVE means Allocate failed and nothing was committed.
+ * Unreserve of a cpuset pod takes the CPUs it was given. */
+int koordhip_commit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
+int koordhip_uncommit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node, const uint64_t *cpus);
+
+/* CPUs allocated to each pod of the last place call ([n_pods][KOORDHIP_NUMA_WORDS],
+ * zero for non-cpuset pods): what PreBind writes into the resource-status
+ * annotation (plugin.go:425-453). */
+int koordhip_fetch_cpusets(koordhip_ctx *ctx, uint64_t *cpus, int32_t n_pods);
 
 /* Device-time of the last place call's eval kernels, split for roofline
  * accounting: total ms of eval kernels, launches, evals processed. */

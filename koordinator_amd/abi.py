@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 1
+KOORDHIP_ABI_VERSION = 2
 NRES = 5
 NPLUGINS = 3
 
@@ -24,15 +24,27 @@ LA_HAS_METRIC, LA_FILTER_SKIP, LA_SCORE_EXPIRED, LA_FILTER_USAGE = 1, 2, 4, 8
 LA_PROD_MODE, LA_HAS_PODS_METRIC, LA_AGGREGATED = 16, 32, 64
 
 POD_PROD, POD_DAEMONSET, POD_HAS_REQ, POD_REQ_BCPU, POD_REQ_BMEM = 1, 2, 4, 8, 16
-POD_CPUSET, POD_NUMA_SKIP = 32, 64
+POD_CPUSET, POD_NUMA_SKIP, POD_NUMA_ERROR = 32, 64, 128
+
+CPUBIND_NONE, CPUBIND_FULL_PCPUS, CPUBIND_SPREAD_BY_PCPUS = 0, 1, 2
+CPUEXCL_NONE, CPUEXCL_PCPU, CPUEXCL_NUMA = 0, 1, 2
+NODE_CPUBIND_NONE, NODE_CPUBIND_FULL_PCPUS_ONLY, NODE_CPUBIND_SPREAD_BY_PCPUS = 0, 1, 2
+NODE_NUMA_MOST_ALLOCATED = 4
+NUMA_MAX_CPUS, NUMA_MAX_NODES, NUMA_WORDS = 256, 8, 4
+
+
+def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> int:
+    return (required & 3) | ((preferred & 3) << 2) | ((exclusive & 3) << 4)
 
 ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL = 1, 2, 4
 UNSCHEDULABLE, RESERVE_FAILED = -1, -2
+E_RESERVE = -6
 UNIQUE_ID_BYTES = 128
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
 _u8p = C.POINTER(C.c_uint8)
+_u64p = C.POINTER(C.c_uint64)
 
 
 class KoordhipConfig(C.Structure):
@@ -74,7 +86,27 @@ class KoordhipNodeSoa(C.Structure):
         ("laf_thr", _i64p * 2),
         ("laf_prod_thr", _i64p * 2),
         ("la_flags", _u8p),
+        ("numa_classes", C.c_void_p),
+        ("n_numa_classes", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("numa_class", _i32p),
+        ("numa_free", _u64p * NUMA_WORDS),
+        ("numa_excl_pcpu", _u64p * NUMA_WORDS),
+        ("numa_excl_numa", _u64p * NUMA_WORDS),
+        ("numa_alloc_cnt", _i32p),
+        ("numa_flags", _u8p),
     ]
+
+
+# numpy twin of koordhip_numa_class
+NUMA_CLASS_DTYPE = np.dtype([
+    ("num_cpus", "<i4"), ("num_cores", "<i4"), ("num_nodes", "<i4"), ("num_sockets", "<i4"),
+    ("cpus_per_core", "<i4"), ("reserved0", "<i4"),
+    ("cpu_id", "<i4", (NUMA_MAX_CPUS,)),
+    ("node_of", "u1", (NUMA_MAX_CPUS,)),
+    ("socket_of", "u1", (NUMA_MAX_CPUS,)),
+], align=True)
+assert NUMA_CLASS_DTYPE.itemsize == 24 + 4 * 256 + 512
 
 
 class KoordhipTopk(C.Structure):
@@ -90,7 +122,9 @@ POD_DTYPE = np.dtype([
     ("est_mem", "<i8"),
     ("flags", "<u4"),
     ("numa_cpus", "<i4"),
-    ("reserved", "<i8", (2,)),
+    ("numa_policy", "<u4"),
+    ("reserved0", "<i4"),
+    ("reserved1", "<i8"),
 ], align=True)
 assert POD_DTYPE.itemsize == 96
 TOPK_DTYPE = np.dtype([("node", "<i4"), ("score", "<i4")])
@@ -134,8 +168,10 @@ def load_library(path: str = LIB_PATH):
         "koordhip_synchronize": (C.c_int, [vp]),
         "koordhip_checkpoint": (C.c_int, [vp]),
         "koordhip_restore": (C.c_int, [vp]),
-        "koordhip_commit": (C.c_int, [vp, vp, C.c_int32]),
-        "koordhip_uncommit": (C.c_int, [vp, vp, C.c_int32]),
+        "koordhip_commit": (C.c_int, [vp, vp, C.c_int32, _u64p]),
+        "koordhip_uncommit": (C.c_int, [vp, vp, C.c_int32, _u64p]),
+        "koordhip_fetch_cpusets": (C.c_int, [vp, _u64p, C.c_int32]),
+        "koordhip_read_numa": (C.c_int, [vp, _u64p, _u64p, _u64p, _i32p]),
         "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_comm_unique_id": (C.c_int, [C.c_char_p]),
@@ -156,7 +192,8 @@ EXPORTED_SYMBOLS = [
     "koordhip_last_error", "koordhip_abi_version", "koordhip_create", "koordhip_destroy",
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
-    "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit", "koordhip_last_stats",
+    "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
+    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_last_stats",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]
 

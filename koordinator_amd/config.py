@@ -116,6 +116,23 @@ class NodeNUMAResourceArgs:
     scoring_type: str = "LeastAllocated"
     resources: Dict[str, int] = field(default_factory=lambda: {k8s.CPU: 1, k8s.MEMORY: 1})
 
+    @property
+    def default_most_allocated(self) -> bool:
+        """GetDefaultNUMAAllocateStrategy (nodenumaresource/util.go:25-32)."""
+        return self.scoring_type != "LeastAllocated"
+
+    def validate(self):
+        """ValidateNodeNUMAResourceArgs + the engine's scope (LeastAllocated over cpu/memory)."""
+        if self.default_cpu_bind_policy not in ("", "Default", "FullPCPUs", "SpreadByPCPUs", "ConstrainedBurst"):
+            raise ArgsError(f"defaultCPUBindPolicy: unsupported value {self.default_cpu_bind_policy!r}")
+        if self.scoring_type != "LeastAllocated":
+            raise ArgsError("NodeNUMAResource scoringStrategy: only LeastAllocated is built into this engine")
+        for r, w in self.resources.items():
+            if r not in (k8s.CPU, k8s.MEMORY):
+                raise ArgsError(f"NodeNUMAResource scoringStrategy.resources: {r} is not supported by this engine")
+            if not (0 <= w <= 100):
+                raise ArgsError(f"NodeNUMAResource scoringStrategy.resources: weight of {r} out of range, got {w}")
+
 
 @dataclass
 class Profile:
@@ -133,8 +150,9 @@ class Profile:
         return p
 
 
-def shipped_profile() -> Profile:
-    """config/manager/scheduler-config.yaml:17-46,82-91 restricted to Fit + LoadAware."""
+def shipped_profile(numa: bool = False) -> Profile:
+    """config/manager/scheduler-config.yaml:17-46,82-91 restricted to Fit + LoadAware
+    (+ NodeNUMAResource with default args and score weight 1 when `numa`)."""
     la = LoadAwareSchedulingArgs(
         filter_expired_node_metrics=False,
         node_metric_expiration_seconds=300,
@@ -143,6 +161,9 @@ def shipped_profile() -> Profile:
         estimated_scaling_factors={k8s.CPU: 85, k8s.MEMORY: 70},
     )
     fit = NodeResourcesFitArgs(resources={k8s.CPU: 1, k8s.MEMORY: 1, k8s.BATCH_CPU: 1, k8s.BATCH_MEMORY: 1})
+    if numa:
+        return Profile(filters=(PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA),
+                       scores={PLUGIN_FIT: 1, PLUGIN_LOADAWARE: 1, PLUGIN_NUMA: 1}, fit=fit, loadaware=la)
     return Profile(fit=fit, loadaware=la)
 
 
@@ -153,6 +174,8 @@ def to_c_config(profile: Profile, device: int = -1):
     p = profile.resolved()
     p.loadaware.validate()
     p.fit.validate()
+    if PLUGIN_NUMA in p.filters or PLUGIN_NUMA in p.scores:
+        p.numa.validate()
     cfg = KoordhipConfig()
     cfg.abi_version = KOORDHIP_ABI_VERSION
     cfg.filter_plugins = sum(PLUGIN_BITS[x] for x in set(p.filters))

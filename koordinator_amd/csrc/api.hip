@@ -99,7 +99,12 @@ struct koordhip_ctx {
   koordhip_pod *d_pods = nullptr;
   int32_t pods_cap = 0, n_staged = 0;
   int32_t *d_out = nullptr;
+  uint64_t *d_cpus = nullptr;  // [pods_cap][KOORDHIP_NUMA_WORDS] cpusets of the last place call (NUMA)
   int32_t out_cap = 0;
+  bool numa = false;           // NodeNUMAResource enabled (Filter or Score)
+  int32_t n_classes = 0;
+  kh::DevNumaClass *d_classes = nullptr;
+  int32_t *d_rc = nullptr;     // k_commit status
   uint64_t *d_partial = nullptr;
   size_t partial_cap = 0;
   uint64_t *d_lists = nullptr;   // [batch][k]
@@ -214,6 +219,102 @@ int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t 
   return 0;
 }
 
+// NodeNUMAResource topology classes -> device tables (numa.hpp DevNumaClass).
+int build_numa_class(const koordhip_numa_class &t, kh::DevNumaClass &o) {
+  std::memset(&o, 0, sizeof(o));
+  if (t.num_cpus <= 0 || t.num_cpus > KOORDHIP_NUMA_MAX_CPUS || t.num_cores <= 0 || t.num_nodes <= 0 ||
+      t.num_sockets <= 0)
+    return fail(KOORDHIP_EINVAL, "invalid NUMA topology class");
+  const int cpc = t.num_cpus / t.num_cores;
+  if (cpc != t.cpus_per_core || (cpc != 1 && cpc != 2) || cpc * t.num_cores != t.num_cpus)
+    return fail(KOORDHIP_EINVAL, "NUMA topology class: cpus_per_core must be 1 or 2 with uniform cores");
+  o.ncpu = t.num_cpus;
+  o.cpc = cpc;
+  o.cpn = t.num_cpus / t.num_nodes;
+  o.cps = t.num_cpus / t.num_sockets;
+  int nn = 0, ns = 0;
+  for (int p = 0; p < t.num_cpus; p++) {
+    const int k = t.node_of[p], sck = t.socket_of[p];
+    if (k >= KOORDHIP_NUMA_MAX_NODES || sck >= KOORDHIP_NUMA_MAX_NODES)
+      return fail(KOORDHIP_EINVAL, "NUMA topology class: more than 8 NUMA nodes / sockets");
+    if (p % cpc != 0 && (t.node_of[p - 1] != k || t.socket_of[p - 1] != sck))
+      return fail(KOORDHIP_EINVAL, "NUMA topology class: a core spans NUMA nodes");
+    nn = std::max(nn, k + 1);
+    ns = std::max(ns, sck + 1);
+    o.nm[k][p >> 6] |= 1ull << (p & 63);
+    o.sm[sck][p >> 6] |= 1ull << (p & 63);
+    o.sock_of_node[k] = (uint8_t)sck;
+  }
+  o.nnuma = nn;
+  o.nsock = ns;
+  std::vector<int> order(t.num_cpus);
+  for (int p = 0; p < t.num_cpus; p++) order[p] = p;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return t.cpu_id[a] < t.cpu_id[b]; });
+  for (int i = 0; i < t.num_cpus; i++) o.pos_by_id[i] = (uint8_t)order[i];
+  return 0;
+}
+
+int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
+  kh::DevNuma &nu = c->d.nu;
+  nu = kh::DevNuma{};
+  if (c->d_classes) {
+    (void)hipFree(c->d_classes);
+    c->d_classes = nullptr;
+  }
+  if (!c->numa) return 0;
+  const bool have = s->numa_class != nullptr;
+  if (have && s->n_numa_classes > 0 && !s->numa_classes) return fail(KOORDHIP_EINVAL, "numa_classes is NULL");
+  if (have)
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
+      if (!s->numa_free[w] || !s->numa_excl_pcpu[w] || !s->numa_excl_numa[w])
+        return fail(KOORDHIP_EINVAL, "NUMA mask column missing");
+  if (have && (!s->numa_alloc_cnt || !s->numa_flags)) return fail(KOORDHIP_EINVAL, "NUMA column missing");
+  std::vector<kh::DevNumaClass> cls(std::max(1, have ? s->n_numa_classes : 0));
+  for (int q = 0; have && q < s->n_numa_classes; q++)
+    if (int e = build_numa_class(s->numa_classes[q], cls[q])) return e;
+  if (have)
+    for (int32_t i = 0; i < n; i++)
+      if (s->numa_class[i] >= s->n_numa_classes) return fail(KOORDHIP_EINVAL, "numa_class index out of range");
+  c->n_classes = have ? s->n_numa_classes : 0;
+  HIP_TRY(hipMalloc(&c->d_classes, cls.size() * sizeof(kh::DevNumaClass)));
+  HIP_TRY(hipMemcpyAsync(c->d_classes, cls.data(), cls.size() * sizeof(kh::DevNumaClass), hipMemcpyHostToDevice,
+                         c->stream));
+  nu.cls = c->d_classes;
+  int e = 0;
+  int32_t *nc = nullptr, *cnt = nullptr;
+  uint8_t *nf = nullptr;
+  e = dev_alloc(c, &nc, n);
+  if (!e) {
+    if (have) {
+      e = upload(c, nc, s->numa_class, n);
+    } else if (n) {
+      std::vector<int32_t> none(n, -1);  // no NodeResourceTopology anywhere
+      HIP_TRY(hipMemcpyAsync(nc, none.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+  }
+  if (!e) e = dev_alloc(c, &cnt, n);
+  if (!e) e = upload(c, cnt, have ? s->numa_alloc_cnt : nullptr, n);
+  if (!e) e = dev_alloc(c, &nf, n);
+  if (!e) e = upload(c, nf, have ? s->numa_flags : nullptr, n);
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS && !e; w++) {
+    uint64_t *a = nullptr, *b = nullptr, *d = nullptr;
+    e = dev_alloc(c, &a, n);
+    if (!e) e = upload(c, a, have ? s->numa_free[w] : nullptr, n);
+    if (!e) e = dev_alloc(c, &b, n);
+    if (!e) e = upload(c, b, have ? s->numa_excl_pcpu[w] : nullptr, n);
+    if (!e) e = dev_alloc(c, &d, n);
+    if (!e) e = upload(c, d, have ? s->numa_excl_numa[w] : nullptr, n);
+    nu.fr[w] = a;
+    nu.ep[w] = b;
+    nu.en[w] = d;
+  }
+  nu.node_cls = nc;
+  nu.cnt = cnt;
+  nu.nflags = nf;
+  return e;
+}
+
 void shard(const koordhip_ctx *c, int32_t *lo, int32_t *hi) {
   *lo = (int32_t)((int64_t)c->n * c->rank / c->world);
   *hi = (int32_t)((int64_t)c->n * (c->rank + 1) / c->world);
@@ -229,10 +330,13 @@ int koordhip_abi_version(void) { return KOORDHIP_ABI_VERSION; }
 int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (!cfg || !out) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (cfg->abi_version != KOORDHIP_ABI_VERSION) return fail(KOORDHIP_EINVAL, "abi_version mismatch");
-  const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE;
-  if ((cfg->filter_plugins | cfg->score_plugins) & ~known)
-    return fail(KOORDHIP_EINVAL, "unsupported plugin bit (NodeNUMAResource is not built into this library version)");
-  for (int p = 0; p < 2; p++) {
+  const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA;
+  if ((cfg->filter_plugins | cfg->score_plugins) & ~known) return fail(KOORDHIP_EINVAL, "unknown plugin bit");
+  if (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) {
+    if (cfg->numa_weight_cpu < 0 || cfg->numa_weight_cpu > 100 || cfg->numa_weight_mem < 0 || cfg->numa_weight_mem > 100)
+      return fail(KOORDHIP_EINVAL, "NodeNUMAResource resource weights must be in [0, 100]");
+  }
+  for (int p = 0; p < KOORDHIP_NPLUGINS; p++) {
     const uint32_t bit = 1u << p;
     if ((cfg->score_plugins & bit) && (cfg->plugin_weight[p] < 1 || cfg->plugin_weight[p] > 100))
       return fail(KOORDHIP_EINVAL, "plugin score weight must be in [1, 100]");
@@ -257,10 +361,14 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.la_w_cpu = (int32_t)cfg->la_weight_cpu;
   c->dc.la_w_mem = (int32_t)cfg->la_weight_mem;
   c->dc.according = cfg->la_score_according_prod_usage ? 1 : 0;
+  c->dc.numa_w_cpu = cfg->numa_weight_cpu;
+  c->dc.numa_w_mem = cfg->numa_weight_mem;
+  c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   if (const char *r = std::getenv("KOORDHIP_TOPK_R")) {
     const int v = std::atoi(r);
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
   }
+  if (c->numa && c->partial_r > 4) c->partial_r = 4;  // the NUMA eval kernel is built for R <= 4
   c->monotone = 1;  // Fit LeastAllocated + LoadAware least-used: a commit never raises a key
   {
     int64_t max_total = 0;  // every plugin score is in [0, 100]
@@ -280,6 +388,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (e == hipSuccess) e = hipEventCreate(&c->t0);
   if (e == hipSuccess) e = hipEventCreate(&c->t1);
   if (e == hipSuccess) e = hipMalloc(&c->d_tmp_pod, sizeof(koordhip_pod));
+  if (e == hipSuccess) e = hipMalloc(&c->d_rc, 64);  // int32 status + (at byte 8) the commit cpuset
   if (e != hipSuccess) {
     std::string m = std::string("device init: ") + hipGetErrorString(e);
     delete c;
@@ -296,7 +405,8 @@ int koordhip_destroy(koordhip_ctx *c) {
   free_cols(c);
   for (void *p : c->ckpt) (void)hipFree(p);
   for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
-                  (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg})
+                  (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
+                  (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
@@ -374,6 +484,7 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   if (!e) e = dev_alloc(c, &lf, n);
   if (!e) e = upload(c, lf, s->la_flags, n);
   pi.la_flags = lf;
+  if (!e) e = load_numa_columns(c, s, n);
   if (e) {
     free_cols(c);
     return e;
@@ -447,6 +558,20 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     put64(const_cast<int64_t *>(pi.prod_thr[r]), rows->laf_prod_thr[r]);
   }
   put8(const_cast<uint8_t *>(pi.la_flags), rows->la_flags);
+  if (!e && c->numa && rows->numa_class) {
+    for (int32_t j = 0; j < m && !e; j++)
+      if (rows->numa_class[j] >= 0 && c->n_classes >= 0 && rows->numa_class[j] >= c->n_classes)
+        e = fail(KOORDHIP_EINVAL, "numa_class index out of range (classes are fixed at load_snapshot)");
+    kh::DevNuma &nu = c->d.nu;
+    put32(const_cast<int32_t *>(nu.node_cls), rows->numa_class);
+    put32(nu.cnt, rows->numa_alloc_cnt);
+    put8(const_cast<uint8_t *>(nu.nflags), rows->numa_flags);
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+      put64((int64_t *)nu.fr[w], (const int64_t *)rows->numa_free[w]);
+      put64((int64_t *)nu.ep[w], (const int64_t *)rows->numa_excl_pcpu[w]);
+      put64((int64_t *)nu.en[w], (const int64_t *)rows->numa_excl_numa[w]);
+    }
+  }
   if (!e && c->dc.la_alias) {
     for (int32_t j = 0; j < m && c->dc.la_alias; j++)
       if (rows->la_alloc_cpu_m[j] != rows->alloc[KOORDHIP_RES_CPU][j] ||
@@ -483,6 +608,25 @@ int koordhip_read_nodes(koordhip_ctx *c, int64_t *requested, int64_t *nz, int32_
     HIP_TRY(hipMemcpy(la_used_prod, c->d.la_used_prod_cpu, b, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(la_used_prod + n, c->d.la_used_prod_mem, b, hipMemcpyDeviceToHost));
   }
+  return 0;
+}
+
+int koordhip_read_numa(koordhip_ctx *c, uint64_t *free_mask, uint64_t *excl_pcpu, uint64_t *excl_numa,
+                       int32_t *alloc_cnt) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (!c->numa) return fail(KOORDHIP_ESTATE, "NodeNUMAResource is not enabled");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t n = c->n, b = n * sizeof(uint64_t);
+  if (n == 0) return 0;
+  const kh::DevNuma &nu = c->d.nu;
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    if (free_mask) HIP_TRY(hipMemcpy(free_mask + w * n, nu.fr[w], b, hipMemcpyDeviceToHost));
+    if (excl_pcpu) HIP_TRY(hipMemcpy(excl_pcpu + w * n, nu.ep[w], b, hipMemcpyDeviceToHost));
+    if (excl_numa) HIP_TRY(hipMemcpy(excl_numa + w * n, nu.en[w], b, hipMemcpyDeviceToHost));
+  }
+  if (alloc_cnt) HIP_TRY(hipMemcpy(alloc_cnt, nu.cnt, n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -560,11 +704,14 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
   if (n_pods > c->pods_cap) {
     if (c->d_pods) HIP_TRY(hipFree(c->d_pods));
     if (c->d_out) HIP_TRY(hipFree(c->d_out));
+    if (c->d_cpus) HIP_TRY(hipFree(c->d_cpus));
     c->d_pods = nullptr;
     c->d_out = nullptr;
+    c->d_cpus = nullptr;
     // +16 records of padding: the resolve kernel DMA-copies pod records in 1 KiB pieces
     HIP_TRY(hipMalloc(&c->d_pods, (size_t)(n_pods + 16) * sizeof(koordhip_pod)));
     HIP_TRY(hipMalloc(&c->d_out, (size_t)n_pods * sizeof(int32_t)));
+    if (c->numa) HIP_TRY(hipMalloc(&c->d_cpus, (size_t)std::max(n_pods, 1) * KOORDHIP_NUMA_WORDS * sizeof(uint64_t)));
     c->pods_cap = n_pods;
   }
   if (n_pods) HIP_TRY(hipMemcpyAsync(c->d_pods, pods, (size_t)n_pods * sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream));
@@ -668,10 +815,14 @@ int place_staged_impl(koordhip_ctx *c) {
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
       if (int e = exchange(c, (size_t)P * K)) return e;
       HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits, c->d_final, c->stream));
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0, c->d_dbg, c->stream));
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0,
+                                 c->d_cpus ? c->d_cpus + (size_t)p0 * KOORDHIP_NUMA_WORDS : nullptr, c->d_dbg,
+                                 c->stream));
     } else {
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_lists, c->monotone, c->d_out + p0, c->d_dbg, c->stream));
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_lists, c->monotone, c->d_out + p0,
+                                 c->d_cpus ? c->d_cpus + (size_t)p0 * KOORDHIP_NUMA_WORDS : nullptr, c->d_dbg,
+                                 c->stream));
     }
   }
   HIP_TRY(hipEventRecord(c->t1, c->stream));
@@ -708,6 +859,20 @@ int koordhip_fetch_placements(koordhip_ctx *c, int32_t *out_node, int32_t n_pods
   return 0;
 }
 
+int koordhip_fetch_cpusets(koordhip_ctx *c, uint64_t *cpus, int32_t n_pods) {
+  if (!c || (!cpus && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (n_pods > c->n_staged) return fail(KOORDHIP_EINVAL, "n_pods exceeds the staged stream");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t b = (size_t)n_pods * KOORDHIP_NUMA_WORDS * sizeof(uint64_t);
+  if (!c->d_cpus) {
+    if (b) std::memset(cpus, 0, b);
+    return 0;
+  }
+  if (b) HIP_TRY(hipMemcpy(cpus, c->d_cpus, b, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int koordhip_place_stream(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, int32_t *out_node) {
   if (int e = koordhip_stage_pods(c, pods, n_pods)) return e;
   if (int e = koordhip_place_staged(c)) return e;
@@ -727,6 +892,15 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
   v.push_back({c->d.la_used_prod_cpu, b});
   v.push_back({c->d.la_used_prod_mem, b});
   v.push_back({c->d.flags, n});
+  if (c->numa) {
+    const kh::DevNuma &nu = c->d.nu;
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+      v.push_back({nu.fr[w], n * sizeof(uint64_t)});
+      v.push_back({nu.ep[w], n * sizeof(uint64_t)});
+      v.push_back({nu.en[w], n * sizeof(uint64_t)});
+    }
+    v.push_back({nu.cnt, n * sizeof(int32_t)});
+  }
   return v;
 }
 
@@ -757,19 +931,35 @@ int koordhip_restore(koordhip_ctx *c) {
   return 0;
 }
 
-static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, int sign) {
+static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, int sign, uint64_t *cpus_io) {
   if (!c || !pod) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   if (node < 0 || node >= c->n) return fail(KOORDHIP_EINVAL, "node index out of range");
+  const bool cpuset = c->numa && (pod->flags & KOORDHIP_POD_CPUSET) &&
+                      !(pod->flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+  if (sign < 0 && cpuset && !cpus_io) return fail(KOORDHIP_EINVAL, "Unreserve of a cpuset pod needs its cpus");
   HIP_TRY(hipSetDevice(c->device));
+  uint64_t *d_cpus = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(c->d_rc) + sizeof(uint64_t));
   HIP_TRY(hipMemcpyAsync(c->d_tmp_pod, pod, sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(kh::launch_commit(c->d, c->d_tmp_pod, node, sign, c->stream));
+  if (sign < 0 && cpus_io)
+    HIP_TRY(hipMemcpyAsync(d_cpus, cpus_io, KOORDHIP_NUMA_WORDS * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(kh::launch_commit(c->dc, c->d, c->d_tmp_pod, node, sign, d_cpus, c->d_rc, c->stream));
+  int32_t rc = 0;
+  uint64_t got[KOORDHIP_NUMA_WORDS];
+  HIP_TRY(hipMemcpyAsync(&rc, c->d_rc, sizeof(rc), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(got, d_cpus, sizeof(got), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (rc) return fail(rc, "Reserve failed: NodeNUMAResource could not allocate the cpuset");
+  if (sign > 0 && cpus_io) std::memcpy(cpus_io, got, sizeof(got));
   return 0;
 }
 
-int koordhip_commit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node) { return commit_impl(c, pod, node, +1); }
-int koordhip_uncommit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node) { return commit_impl(c, pod, node, -1); }
+int koordhip_commit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out) {
+  return commit_impl(c, pod, node, +1, cpus_out);
+}
+int koordhip_uncommit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, const uint64_t *cpus) {
+  return commit_impl(c, pod, node, -1, const_cast<uint64_t *>(cpus));
+}
 
 int koordhip_last_stats(koordhip_ctx *c, double *eval_ms, int64_t *eval_launches, int64_t *evals, double *total_ms) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");

@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include "../../include/koordhip.h"
+#include "numa.hpp"
 
 namespace kh {
 
@@ -33,6 +34,7 @@ struct DevCfg {
   int32_t la_w_cpu, la_w_mem;
   int32_t according;  // ScoreAccordingProdUsage
   int32_t la_alias;   // la_alloc columns equal alloc cpu/mem columns (loaded once)
+  int32_t numa_w_cpu, numa_w_mem;  // NodeNUMAResourceArgs LeastAllocated weights
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -47,6 +49,7 @@ struct DevNodes {
   int64_t *la_used_cpu, *la_used_mem, *la_used_prod_cpu, *la_used_prod_mem;
   uint8_t *flags;
   int32_t n;
+  DevNuma nu;  // NodeNUMAResource columns (unused unless the plugin is enabled)
 };
 
 // One node's values as the evaluation consumes them (registers or an LDS row).
@@ -62,7 +65,15 @@ struct NV {
 // What one pod's evaluation needs from the node columns (wave-uniform).
 struct Need {
   bool pods, r_cpu, r_mem, eph, bcpu, bmem, a_cpu, a_mem, nz_cpu, nz_mem, la, la_nonprod, la_prod;
+  bool numa, numa_masks;  // NUMA class (+ the cpuset masks for a cpuset pod)
 };
+
+__device__ __forceinline__ bool numa_on(const DevCfg &c) {
+  return ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
+}
+__device__ __forceinline__ bool is_cpuset(const koordhip_pod &p) {
+  return (p.flags & KOORDHIP_POD_CPUSET) && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+}
 
 __device__ __forceinline__ Need pod_needs(const koordhip_pod &p, const DevCfg &c) {
   Need n{};
@@ -82,8 +93,17 @@ __device__ __forceinline__ Need pod_needs(const koordhip_pod &p, const DevCfg &c
   n.la = c.score & KOORDHIP_PLUGIN_LOADAWARE;
   n.la_prod = n.la && c.according && (p.flags & KOORDHIP_POD_PROD);
   n.la_nonprod = n.la && !n.la_prod;
-  n.a_cpu = n.r_cpu || n.nz_cpu || (n.la && c.la_alias);
-  n.a_mem = n.r_mem || n.nz_mem || (n.la && c.la_alias);
+  // NodeNUMAResource: Score reads Requested cpu/memory + Allocatable (scoring.go:104-106, :161-166)
+  const bool ns = (c.score & KOORDHIP_PLUGIN_NUMA) && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+  n.numa = ns || ((c.filt & KOORDHIP_PLUGIN_NUMA) && is_cpuset(p));
+  n.numa_masks = numa_on(c) && is_cpuset(p);
+  if (ns) {
+    n.r_cpu |= !is_cpuset(p);
+    n.r_mem = true;
+    n.a_cpu = n.a_mem = true;
+  }
+  n.a_cpu = n.a_cpu || n.r_cpu || n.nz_cpu || (n.la && c.la_alias);
+  n.a_mem = n.a_mem || n.r_mem || n.nz_mem || (n.la && c.la_alias);
   return n;
 }
 
@@ -93,7 +113,25 @@ __device__ __forceinline__ Need need_all(const DevCfg &c) {
   n.la = true;
   n.la_nonprod = true;
   n.la_prod = c.according != 0;
+  n.numa = n.numa_masks = numa_on(c);
   return n;
+}
+
+// NodeNUMAResource columns of node i.
+__device__ __forceinline__ void load_numa(NumaRow &r, const DevNodes &d, int32_t i, const Need &n) {
+  r.cls = -1;
+  if (!n.numa) return;
+  r.cls = d.nu.node_cls[i];
+  if (n.numa_masks) {
+    r.nflags = d.nu.nflags[i];
+    r.cnt = d.nu.cnt[i];
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      r.fr[w] = d.nu.fr[w][i];
+      r.ep[w] = d.nu.ep[w][i];
+      r.en[w] = d.nu.en[w][i];
+    }
+  }
 }
 
 // Load node i's columns the evaluation needs (coalesced across lanes).
@@ -238,6 +276,23 @@ __device__ __forceinline__ int32_t la_score(const koordhip_pod &p, const NV &v, 
   return div_weights(num, (int64_t)(c.la_w_cpu + c.la_w_mem));
 }
 
+// NodeNUMAResource Score (scoring.go:55-168).
+__device__ __forceinline__ int32_t numa_score(const koordhip_pod &p, const NV &v, const NumaRow &r,
+                                              const DevNumaClass *classes, const DevCfg &c) {
+  if (p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0;
+  if (r.cls < 0) return 0;  // no CPU topology: getResourceOptions / Allocate error -> 0
+  auto lr = [](int64_t a, int64_t b) { return lrs(a, b); };
+  auto dw = [](int64_t a, int64_t b) { return div_weights(a, b); };
+  if (!(p.flags & KOORDHIP_POD_CPUSET))
+    return numa_la(v.r[KOORDHIP_RES_CPU] + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
+                   v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM], v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem,
+                   lr, dw);
+  if (!numa_alloc_ok(classes[r.cls], r, p)) return 0;
+  return numa_la((int64_t)r.cnt * 1000 + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
+                 v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM], v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem,
+                 lr, dw);
+}
+
 // Total weighted score, or -1 when any enabled Filter fails (short-circuit).
 __device__ __forceinline__ int32_t eval_total(const koordhip_pod &p, const NV &v, const DevCfg &c) {
   if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(p, v)) return -1;
@@ -245,6 +300,16 @@ __device__ __forceinline__ int32_t eval_total(const koordhip_pod &p, const NV &v
   int32_t t = 0;
   if (c.score & KOORDHIP_PLUGIN_FIT) t += c.w_fit * fit_score(p, v, c);
   if (c.score & KOORDHIP_PLUGIN_LOADAWARE) t += c.w_la * la_score(p, v, c);
+  return t;
+}
+
+// ... with NodeNUMAResource
+__device__ __forceinline__ int32_t eval_total_numa(const koordhip_pod &p, const NV &v, const NumaRow &r,
+                                                   const DevNumaClass *classes, const DevCfg &c) {
+  int32_t t = eval_total(p, v, c);
+  if (t < 0) return t;
+  if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter(p, r, classes)) return -1;
+  if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score(p, v, r, classes, c);
   return t;
 }
 
@@ -294,6 +359,49 @@ __device__ __forceinline__ void load_row(NV &v, const DevNodes &d, int32_t i) {
   v.la_up_cpu = d.la_used_prod_cpu[i];
   v.la_up_mem = d.la_used_prod_mem[i];
   v.flags = d.flags[i];
+}
+
+__device__ __forceinline__ void load_numa_row(NumaRow &r, const DevNodes &d, int32_t i) {
+  r.cls = d.nu.node_cls[i];
+  r.nflags = d.nu.nflags[i];
+  r.cnt = d.nu.cnt[i];
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    r.fr[w] = d.nu.fr[w][i];
+    r.ep[w] = d.nu.ep[w][i];
+    r.en[w] = d.nu.en[w][i];
+  }
+}
+
+__device__ __forceinline__ void store_numa_row(const NumaRow &r, const DevNodes &d, int32_t i) {
+  d.nu.cnt[i] = r.cnt;
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    d.nu.fr[w][i] = r.fr[w];
+    d.nu.ep[w][i] = r.ep[w];
+    d.nu.en[w][i] = r.en[w];
+  }
+}
+
+// NodeNUMAResource Reserve / Release on a row (resourceManager.Update / Release,
+// node_allocation.go:76-131).
+__device__ __forceinline__ void numa_apply(NumaRow &r, const koordhip_pod &p, const uint64_t *cpus, int sign) {
+  const int ex = (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy);
+  int n = 0;
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    n += __popcll(cpus[w]);
+    if (sign > 0) {
+      r.fr[w] &= ~cpus[w];
+      if (ex == (int)KOORDHIP_CPUEXCL_PCPU) r.ep[w] |= cpus[w];
+      if (ex == (int)KOORDHIP_CPUEXCL_NUMA) r.en[w] |= cpus[w];
+    } else {
+      r.fr[w] |= cpus[w];
+      r.ep[w] &= ~cpus[w];
+      r.en[w] &= ~cpus[w];
+    }
+  }
+  r.cnt += sign * n;
 }
 
 __device__ __forceinline__ void store_row(const NV &v, const DevNodes &d, int32_t i) {

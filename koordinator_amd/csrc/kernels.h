@@ -29,7 +29,10 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
 template <typename T>
 hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods, int32_t k,
-                          const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *dbg, hipStream_t s);
-hipError_t launch_commit(const DevNodes &d, const koordhip_pod *pod, int32_t node, int32_t sign, hipStream_t s);
+                          const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *out_cpus,
+                          uint64_t *dbg, hipStream_t s);
+// single Reserve (sign +1, cpus <- allocated CPUs, *rc = KOORDHIP_ERESERVE on failure) / Unreserve (cpus given)
+hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const koordhip_pod *pod, int32_t node, int32_t sign,
+                         uint64_t *cpus, int32_t *rc, hipStream_t s);
 
 }  // namespace kh

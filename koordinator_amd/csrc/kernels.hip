@@ -135,18 +135,22 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const koordhip_pod *__restrict
   if (i >= d.n || p >= n_pods) return;
   const koordhip_pod pod = pods[p];
   NV v{};
-  load_node(v, d, i, need_all(c), c);
+  const Need all = need_all(c);
+  load_node(v, d, i, all, c);
+  NumaRow nr{};
+  load_numa(nr, d, i, all);
   if (status) {
     uint8_t b = 0;
     if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(pod, v)) b |= KOORDHIP_ST_FIT_FAIL;
     if ((c.filt & KOORDHIP_PLUGIN_LOADAWARE) && !la_filter(pod, v)) b |= KOORDHIP_ST_LA_FAIL;
+    if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter(pod, nr, d.nu.cls)) b |= KOORDHIP_ST_NUMA_FAIL;
     status[(size_t)p * d.n + i] = b;
   }
   if (scores) {
     int32_t *row = scores + (size_t)p * KOORDHIP_NPLUGINS * d.n;
     row[i] = (c.score & KOORDHIP_PLUGIN_FIT) ? fit_score(pod, v, c) : 0;
     row[(size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_LOADAWARE) ? la_score(pod, v, c) : 0;
-    row[2 * (size_t)d.n + i] = 0;
+    row[2 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_NUMA) ? numa_score(pod, v, nr, d.nu.cls, c) : 0;
   }
 }
 
@@ -161,7 +165,7 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const koordhip_pod *__restrict
 // taken and, for score == T, the lowest node indexes (r-major, lane-minor =
 // index order) up to k.  Output: k keys per (pod, chunk), unsorted, 0-padded.
 
-template <int R>
+template <int R, bool NUMA>
 __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
                                                       int32_t n_pods, int32_t lo, int32_t hi, int32_t k,
                                                       int32_t score_bits, uint64_t *__restrict__ out) {
@@ -180,7 +184,13 @@ __global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, cons
     if (i < hi) {
       NV v;
       load_node(v, d, i, need, c);
-      s[r] = eval_total(pod, v, c) + 1;
+      if constexpr (NUMA) {
+        NumaRow nr;
+        load_numa(nr, d, i, need);
+        s[r] = eval_total_numa(pod, v, nr, d.nu.cls, c) + 1;
+      } else {
+        s[r] = eval_total(pod, v, c) + 1;
+      }
     }
   }
   // k-th largest score value T (radix select, MSB first)
@@ -439,10 +449,11 @@ __device__ __forceinline__ uint64_t stamp() {
 
 constexpr int RES_PRE = 128;  // prefetched snapshot rows per round
 
+template <bool NUMA>
 __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
                                                 int32_t n_pods, int32_t k, const uint64_t *__restrict__ lists,
                                                 int32_t monotone, int32_t *__restrict__ out_node,
-                                                uint64_t *__restrict__ dbg) {
+                                                uint64_t *__restrict__ out_cpus, uint64_t *__restrict__ dbg) {
   // dbg (diagnostic builds only, KOORDHIP_STAMPS): s_memtime segment sums
   uint64_t t_entry = dbg ? stamp() : 0, t_a = 0, t_b = 0, t_c = 0, t_mark = 0, n_eval = 0, n_miss = 0;
   __shared__ __attribute__((aligned(16))) uint64_t lk[RES_MAXP * RES_MAXP];
@@ -479,6 +490,7 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
   const uint64_t t_pro = dbg ? stamp() : 0;
   // Lane r owns modified row r in registers (evaluated and committed in place).
   NV my{};
+  NumaRow mynr{};  // ... and its NodeNUMAResource state (NUMA builds)
   int32_t my_node = -1;
   int32_t nm = 0;  // modified rows this round (wave-uniform)
   uint64_t e = lane < k ? lk[lane] : 0;
@@ -506,6 +518,9 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
         n_miss++;
         if (lane == nm) load_row(my, d, cn);
       }
+      if constexpr (NUMA) {
+        if (lane == nm) load_numa_row(mynr, d, cn);
+      }
       staged = cn;
     }
     if (dbg) {
@@ -513,9 +528,16 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
       t_a += t - t_mark;
       t_mark = t;
     }
-    if (nm > 0 && (!monotone || prefix_modified)) {
+    // a required-policy cpuset pod's NUMA feasibility is not monotone in the
+    // node's free CPUs (numa_spread_ok): re-evaluate the modified rows for it
+    const bool nonmono = NUMA && is_cpuset(pod) && KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE;
+    if (nm > 0 && (!monotone || prefix_modified || nonmono)) {
       uint64_t key = 0;
-      if (lane < nm) key = make_key(eval_total(pod, my, c), my_node);
+      if constexpr (NUMA) {
+        if (lane < nm) key = make_key(eval_total_numa(pod, my, mynr, d.nu.cls, c), my_node);
+      } else {
+        if (lane < nm) key = make_key(eval_total(pod, my, c), my_node);
+      }
       key = wave_max_u64_dpp(key);
       best = key > best ? key : best;
       n_eval++;
@@ -525,27 +547,56 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
       t_b += t - t_mark;
       t_mark = t;
     }
+    uint64_t cpus[NW] = {0, 0, 0, 0};
     if (best == 0) {
       if (lane == 0) out_node[j] = KOORDHIP_UNSCHEDULABLE;
     } else {
       const int32_t w = key_node(best);
-      if (lane == 0) out_node[j] = w;
       const uint64_t hit = __ballot(lane < nm && my_node == w);
-      int32_t r;
-      if (hit) {
-        r = __builtin_ctzll(hit);
-      } else {
-        // w is new this round, hence pod j's first unmodified list entry,
-        // whose row lane nm already staged
-        r = nm++;
-        if (staged != w && lane == r) load_row(my, d, w);  // unreachable by construction; kept for safety
-        if (lane == r) {
-          my_node = w;
-          modmap[w >> 5] |= 1u << (w & 31);
+      // w is either a modified row (lane `hit`) or new this round, hence pod j's
+      // first unmodified list entry, whose row lane nm already staged
+      const int32_t r = hit ? __builtin_ctzll(hit) : nm;
+      if (!hit && staged != w && lane == r) {  // unreachable by construction; kept for safety
+        load_row(my, d, w);
+        if constexpr (NUMA) load_numa_row(mynr, d, w);
+      }
+      bool ok = true;
+      if constexpr (NUMA) {
+        if (numa_on(c) && is_cpuset(pod)) {
+          // NodeNUMAResource Reserve: every lane replays the accumulator on row r
+          NumaRow br;
+          br.cls = __builtin_amdgcn_readlane(mynr.cls, r);
+          br.nflags = (uint32_t)__builtin_amdgcn_readlane((int)mynr.nflags, r);
+          br.cnt = __builtin_amdgcn_readlane(mynr.cnt, r);
+          for (int q = 0; q < NW; q++) {
+            br.fr[q] = readlane_u64(mynr.fr[q], r);
+            br.ep[q] = readlane_u64(mynr.ep[q], r);
+            br.en[q] = readlane_u64(mynr.en[q], r);
+          }
+          ok = br.cls >= 0 && numa_allocate(d.nu.cls[br.cls], br, pod, cpus);
         }
       }
-      if (lane == r) apply_delta(my, pod, +1);
+      if (!ok) {
+        if (lane == 0) out_node[j] = KOORDHIP_RESERVE_FAILED;  // every Reserve is rolled back
+      } else {
+        if (lane == 0) out_node[j] = w;
+        if (!hit) {
+          nm++;
+          if (lane == r) {
+            my_node = w;
+            modmap[w >> 5] |= 1u << (w & 31);
+          }
+        }
+        if (lane == r) {
+          apply_delta(my, pod, +1);
+          if constexpr (NUMA) {
+            if (numa_on(c) && is_cpuset(pod)) numa_apply(mynr, pod, cpus, +1);
+          }
+        }
+      }
     }
+    if (out_cpus && lane < NW)
+      out_cpus[(size_t)j * NW + lane] = lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
     // next pod's list against the state after pod j's commit
     if (j + 1 < n_pods) {
       e = lane < k ? lk[(j + 1) * k + lane] : 0;
@@ -557,7 +608,10 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
     }
     if (dbg) t_c += stamp() - t_mark;
   }
-  if (lane < nm) store_row(my, d, my_node);
+  if (lane < nm) {
+    store_row(my, d, my_node);
+    if constexpr (NUMA) store_numa_row(mynr, d, my_node);
+  }
   if (dbg && lane == 0) {
     const uint64_t t_end = stamp();
     atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)(t_pro - t_entry));
@@ -574,11 +628,33 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
 // ---------------------------------------------------------------------------
 // single-pod commit / uncommit (Reserve / Unreserve from the host)
 
-__global__ void k_commit(DevNodes d, const koordhip_pod *__restrict__ pod, int32_t node, int32_t sign) {
+__global__ void k_commit(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pod, int32_t node, int32_t sign,
+                         uint64_t *__restrict__ cpus, int32_t *__restrict__ rc) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const koordhip_pod p = *pod;
+  *rc = 0;
+  if (numa_on(c) && is_cpuset(p)) {
+    NumaRow r;
+    load_numa_row(r, d, node);
+    uint64_t m[NW];
+    if (sign > 0) {
+      if (r.cls < 0 || !numa_allocate(d.nu.cls[r.cls], r, p, m)) {
+        *rc = KOORDHIP_ERESERVE;  // Reserve fails: nothing is committed
+        return;
+      }
+    } else {
+      for (int w = 0; w < NW; w++) m[w] = cpus[w];
+    }
+    numa_apply(r, p, m, sign);
+    store_numa_row(r, d, node);
+    if (sign > 0)
+      for (int w = 0; w < NW; w++) cpus[w] = m[w];
+  } else if (sign > 0) {
+    for (int w = 0; w < NW; w++) cpus[w] = 0;
+  }
   NV v;
   load_row(v, d, node);
-  apply_delta(v, *pod, sign);
+  apply_delta(v, p, sign);
   store_row(v, d, node);
 }
 
@@ -622,20 +698,24 @@ hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const 
                                int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
                                uint64_t *out, hipStream_t s) {
   dim3 grid(nchunks, (n_pods + 3) / 4);
-  switch (R) {
-    case 1:
-      hipLaunchKernelGGL(k_topk_partial<1>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
-      break;
-    case 2:
-      hipLaunchKernelGGL(k_topk_partial<2>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
-      break;
-    case 4:
-      hipLaunchKernelGGL(k_topk_partial<4>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
-      break;
-    default:
-      hipLaunchKernelGGL(k_topk_partial<8>, grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out);
-      break;
+  const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
+#define KH_PARTIAL(RR, NN) \
+  hipLaunchKernelGGL((k_topk_partial<RR, NN>), grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out)
+  if (numa) {
+    switch (R) {
+      case 1: KH_PARTIAL(1, true); break;
+      case 2: KH_PARTIAL(2, true); break;
+      default: KH_PARTIAL(4, true); break;
+    }
+  } else {
+    switch (R) {
+      case 1: KH_PARTIAL(1, false); break;
+      case 2: KH_PARTIAL(2, false); break;
+      case 4: KH_PARTIAL(4, false); break;
+      default: KH_PARTIAL(8, false); break;
+    }
   }
+#undef KH_PARTIAL
   return hipGetLastError();
 }
 
@@ -648,14 +728,21 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
 }
 
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods, int32_t k,
-                          const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *dbg, hipStream_t s) {
+                          const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *out_cpus,
+                          uint64_t *dbg, hipStream_t s) {
   const size_t bitmap = (size_t)((d.n + 31) >> 5) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone, out_node, dbg);
+  if ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA)
+    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone, out_node,
+                       out_cpus, dbg);
+  else
+    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone,
+                       out_node, out_cpus, dbg);
   return hipGetLastError();
 }
 
-hipError_t launch_commit(const DevNodes &d, const koordhip_pod *pod, int32_t node, int32_t sign, hipStream_t s) {
-  hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, d, pod, node, sign);
+hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const koordhip_pod *pod, int32_t node, int32_t sign,
+                         uint64_t *cpus, int32_t *rc, hipStream_t s) {
+  hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, c, d, pod, node, sign, cpus, rc);
   return hipGetLastError();
 }
 

@@ -1,0 +1,599 @@
+// numa.hpp -- NodeNUMAResource on CDNA4 (NUMA topology policy None,
+// maxRefCount 1, no reservation-preferred CPUs, cpus_per_core 1 or 2).
+//
+// Node state is a handful of 4 x 64-bit masks over core-major CPU positions
+// (pos = core_rank * cpc + t), so a core is an aligned group of cpc bits:
+// "any CPU of the core" / "every CPU of the core" are one shift + OR / AND
+// and NUMA-node / socket membership is an AND with a per-class mask.
+//
+// Filter/Score need only whether resourceManager.Allocate would succeed
+// (scoring.go:86-91 uses the allocated size of the NODE, not of the choice),
+// which has a closed form per bind policy (derived from the accumulator's
+// control flow, cpu_accumulator.go:87-232; checked against the oracle's
+// literal accumulator in tests):
+//   preferred only      : |free| >= need                           (:257-259)
+//   required FullPCPUs  : cpc * #fully-free cores >= need          (:105-177 take whole cores first)
+//   required Spread     : the first NUMA node / socket the accumulator
+//                         would pick decides; see numa_spread_ok.
+// Reserve needs the exact CPUs: acc_take_cpus replays the accumulator on the
+// masks (wave-uniform: every lane computes the same result).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/koordhip.h"
+
+namespace kh {
+
+constexpr int NW = KOORDHIP_NUMA_WORDS;
+constexpr int NMAX = KOORDHIP_NUMA_MAX_NODES;
+
+struct DevNumaClass {
+  int32_t ncpu, cpc, cpn, cps, nnuma, nsock;
+  uint8_t sock_of_node[NMAX];
+  uint64_t nm[NMAX][NW];  // CPUs of NUMA node k
+  uint64_t sm[NMAX][NW];  // CPUs of socket s
+  uint8_t pos_by_id[KOORDHIP_NUMA_MAX_CPUS];  // positions in ascending CPU id
+};
+
+struct NumaRow {
+  int32_t cls;     // -1: no CPU topology
+  uint32_t nflags; // KOORDHIP_NODE_*
+  int32_t cnt;     // allocated CPUs
+  int32_t pad;
+  uint64_t fr[NW], ep[NW], en[NW];
+};
+
+struct DevNuma {
+  const DevNumaClass *cls;
+  const int32_t *node_cls;
+  const uint8_t *nflags;
+  uint64_t *fr[NW], *ep[NW], *en[NW];
+  int32_t *cnt;
+};
+
+__device__ __forceinline__ int popc4(const uint64_t *m) {
+  return __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
+}
+
+// lead bit of every core with any / every CPU set in m
+__device__ __forceinline__ uint64_t fold_or(uint64_t m, int cpc) {
+  return cpc == 1 ? m : ((m | (m >> 1)) & 0x5555555555555555ull);
+}
+__device__ __forceinline__ uint64_t fold_and(uint64_t m, int cpc) {
+  return cpc == 1 ? m : ((m & (m >> 1)) & 0x5555555555555555ull);
+}
+__device__ __forceinline__ uint64_t expand(uint64_t lead, int cpc) { return cpc == 1 ? lead : (lead | (lead << 1)); }
+
+__device__ __forceinline__ int popc_and(const uint64_t *a, const uint64_t *b) {
+  return __popcll(a[0] & b[0]) + __popcll(a[1] & b[1]) + __popcll(a[2] & b[2]) + __popcll(a[3] & b[3]);
+}
+
+// strategy direction of a free-score comparison: MostAllocated -> ascending
+__device__ __forceinline__ bool free_before(bool most, int x, int y) { return most ? x < y : x > y; }
+
+__device__ __forceinline__ int node_policy(uint32_t nflags, int preferred) {
+  const uint32_t p = nflags & KOORDHIP_NODE_CPUBIND_MASK;  // getPreferredCPUBindPolicy, plugin.go:546-566
+  return p == 1 ? (int)KOORDHIP_CPUBIND_FULL_PCPUS : (p == 2 ? (int)KOORDHIP_CPUBIND_SPREAD_BY_PCPUS : preferred);
+}
+
+// CPUs excluded by the pod's exclusive policy (isCPUExclusivePCPULevel /
+// isCPUExclusiveNUMANodeLevel, cpu_accumulator.go:318-330): whole cores holding a
+// PCPULevel-allocated CPU, or whole NUMA nodes holding a NUMANodeLevel one.
+__device__ __forceinline__ void excluded_set(const DevNumaClass &C, const NumaRow &r, int excl, bool pcpu_only,
+                                             uint64_t *X) {
+  for (int w = 0; w < NW; w++) X[w] = 0;
+  if (excl == (int)KOORDHIP_CPUEXCL_PCPU) {
+    for (int w = 0; w < NW; w++) X[w] = expand(fold_or(r.ep[w], C.cpc), C.cpc);
+  } else if (excl == (int)KOORDHIP_CPUEXCL_NUMA && !pcpu_only) {
+    for (int k = 0; k < C.nnuma; k++)
+      if (popc_and(r.en, C.nm[k]))
+        for (int w = 0; w < NW; w++) X[w] |= C.nm[k][w];
+  }
+}
+
+// distinct cores among m & g
+__device__ __forceinline__ int cores_in(const uint64_t *m, const uint64_t *g, int cpc) {
+  int c = 0;
+  for (int w = 0; w < NW; w++) c += __popcll(fold_or(m[w] & g[w], cpc));
+  return c;
+}
+
+// Required SpreadByPCPUs with cpc == 2: whether takeCPUs' choice is one CPU
+// per core.  Stages follow cpu_accumulator.go:184-229; a stage that finds a
+// group big enough returns immediately, with distinct cores iff the group has
+// that many distinct cores (spreadCPUs takes one CPU per core first).
+__device__ bool numa_spread_ok(const DevNumaClass &C, const NumaRow &r, int need, int excl, bool most) {
+  const int cpc = C.cpc;
+  uint64_t X[NW], Xp[NW], F[NW];
+  excluded_set(C, r, excl, false, X);
+  excluded_set(C, r, excl, true, Xp);
+  if (need <= C.cpn) {
+    // pass filterExclusive=true: extracted lists (distinct cores) -> any big enough node succeeds
+    for (int w = 0; w < NW; w++) F[w] = r.fr[w] & ~X[w];
+    for (int k = 0; k < C.nnuma; k++)
+      if (cores_in(F, C.nm[k], cpc) >= need) return true;
+    // pass false: the first node in (free, socket free, id) order with >= need CPUs decides
+    int best = -1, bf = 0, bs = 0;
+    for (int k = 0; k < C.nnuma; k++) {
+      const int f = popc_and(r.fr, C.nm[k]);
+      if (f < need) continue;
+      const int sf = popc_and(r.fr, C.sm[C.sock_of_node[k]]);
+      if (best < 0 || (f != bf ? free_before(most, f, bf) : (sf != bs ? free_before(most, sf, bs) : false))) {
+        best = k;
+        bf = f;
+        bs = sf;
+      }
+    }
+    if (best >= 0) return cores_in(r.fr, C.nm[best], cpc) >= need;
+  }
+  if (need <= C.cps) {
+    for (int w = 0; w < NW; w++) F[w] = r.fr[w] & ~Xp[w];  // socket pass true filters PCPULevel only (:612)
+    for (int s = 0; s < C.nsock; s++)
+      if (cores_in(F, C.sm[s], cpc) >= need) return true;
+    int best = -1, bf = 0;
+    for (int s = 0; s < C.nsock; s++) {
+      const int f = popc_and(r.fr, C.sm[s]);
+      if (f < need) continue;
+      if (best < 0 || (f != bf && free_before(most, f, bf))) {
+        best = s;
+        bf = f;
+      }
+    }
+    if (best >= 0) return cores_in(r.fr, C.sm[best], cpc) >= need;
+  }
+  // freeCPUs(true) spread, then freeCPUs(false) over what is left (:218-229)
+  uint64_t allm[NW], FX[NW];
+  for (int w = 0; w < NW; w++) {
+    allm[w] = ~0ull;
+    F[w] = r.fr[w] & ~X[w];
+    FX[w] = r.fr[w] & X[w];
+  }
+  const int cT = popc4(F), dT = cores_in(F, allm, cpc);
+  if (need <= dT) return true;
+  if (cT >= need || cT > dT) return false;
+  return need - cT <= cores_in(FX, allm, cpc);
+}
+
+// resourceManager.Allocate succeeds? (empty hint, no preferred CPUs)
+__device__ __forceinline__ bool numa_alloc_ok(const DevNumaClass &C, const NumaRow &r, const koordhip_pod &p) {
+  const int need = p.numa_cpus;
+  if (popc4(r.fr) < need) return false;  // allocateCPUSet :257-259 (filterAvailableCPUsByRequiredCPUBindPolicy is a no-op)
+  const int req = (int)KOORDHIP_NUMA_REQUIRED(p.numa_policy);
+  if (req == (int)KOORDHIP_CPUBIND_NONE) return true;  // takeCPUs never fails once need <= |available|
+  const int pol = node_policy(r.nflags, (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy));
+  if (pol == (int)KOORDHIP_CPUBIND_FULL_PCPUS) {
+    int full = 0;
+    for (int w = 0; w < NW; w++) full += __popcll(fold_and(r.fr[w], C.cpc));
+    return full * C.cpc >= need;
+  }
+  if (C.cpc == 1) return true;
+  return numa_spread_ok(C, r, need, (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy),
+                        (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0);
+}
+
+// Filter, plugin.go:266-324; true = passes.
+__device__ __forceinline__ bool numa_filter(const koordhip_pod &p, const NumaRow &r, const DevNumaClass *classes) {
+  if (p.flags & KOORDHIP_POD_NUMA_ERROR) return false;
+  if ((p.flags & KOORDHIP_POD_NUMA_SKIP) || !(p.flags & KOORDHIP_POD_CPUSET)) return true;
+  if (r.cls < 0) return false;
+  const DevNumaClass &C = classes[r.cls];
+  const int req = (int)KOORDHIP_NUMA_REQUIRED(p.numa_policy);
+  const bool full_only = (r.nflags & KOORDHIP_NODE_CPUBIND_MASK) == 1u;
+  if (full_only || req == (int)KOORDHIP_CPUBIND_FULL_PCPUS) {
+    if (p.numa_cpus % C.cpc != 0) return false;
+    if (full_only && (req != (int)KOORDHIP_CPUBIND_FULL_PCPUS ||
+                      (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy) != (int)KOORDHIP_CPUBIND_FULL_PCPUS))
+      return false;
+  }
+  if (req != (int)KOORDHIP_CPUBIND_NONE) return numa_alloc_ok(C, r, p);
+  return true;
+}
+
+// leastResourceScorer over {cpu, memory}, alloc 0 left out (scoring.go:191-230)
+template <typename Lrs, typename Div>
+__device__ __forceinline__ int32_t numa_la(int64_t rc, int64_t ac, int64_t rm, int64_t am, int32_t wc, int32_t wm,
+                                           Lrs lrs_fn, Div div_fn) {
+  int64_t num = 0, ws = 0;
+  if (wc && ac != 0) {
+    num += (int64_t)lrs_fn(rc, ac) * wc;
+    ws += wc;
+  }
+  if (wm && am != 0) {
+    num += (int64_t)lrs_fn(rm, am) * wm;
+    ws += wm;
+  }
+  return ws ? div_fn(num, ws) : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Exact accumulator replay for Reserve (cpu_accumulator.go:87-232, mask form).
+
+struct Acc {
+  uint64_t A[NW];   // allocatable
+  uint64_t R[NW];   // result
+  uint64_t XC[NW];  // exclusiveInCores (lead bits)
+  uint32_t XN;      // exclusiveInNUMANodes
+  int need, excl;
+  bool most;
+};
+
+__device__ __forceinline__ bool tbit(const uint64_t *m, int p) { return (m[p >> 6] >> (p & 63)) & 1ull; }
+__device__ __forceinline__ void sbit(uint64_t *m, int p) { m[p >> 6] |= 1ull << (p & 63); }
+
+__device__ __forceinline__ void acc_take1(const DevNumaClass &C, Acc &a, int p) {
+  sbit(a.R, p);
+  a.A[p >> 6] &= ~(1ull << (p & 63));
+  if (a.excl == (int)KOORDHIP_CPUEXCL_PCPU) sbit(a.XC, p - (p % C.cpc));
+  if (a.excl == (int)KOORDHIP_CPUEXCL_NUMA)
+    for (int k = 0; k < C.nnuma; k++)
+      if (tbit(C.nm[k], p)) a.XN |= 1u << k;
+  a.need--;
+}
+
+// take the lowest n positions of m
+__device__ __forceinline__ void acc_take_low(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
+  for (int w = 0; w < NW && n > 0; w++) {
+    uint64_t x = m[w];
+    while (x && n > 0) {
+      const int b = __builtin_ctzll(x);
+      x &= x - 1;
+      acc_take1(C, a, w * 64 + b);
+      n--;
+    }
+  }
+}
+
+// the accumulator's exclusion mask for filterExclusive passes
+__device__ __forceinline__ void acc_excluded(const DevNumaClass &C, const Acc &a, bool pcpu_only, uint64_t *X) {
+  for (int w = 0; w < NW; w++) X[w] = 0;
+  if (a.excl == (int)KOORDHIP_CPUEXCL_PCPU) {
+    for (int w = 0; w < NW; w++) X[w] = expand(a.XC[w], C.cpc);
+  } else if (a.excl == (int)KOORDHIP_CPUEXCL_NUMA && !pcpu_only) {
+    for (int k = 0; k < C.nnuma; k++)
+      if (a.XN & (1u << k))
+        for (int w = 0; w < NW; w++) X[w] |= C.nm[k][w];
+  }
+}
+
+// spread order of the CPUs of m listed in ascending CPU id (freeCPUsInNode /
+// freeCPUsInSocket + spreadCPUs): round t takes each core's t-th CPU by id,
+// rounds in id order; lists of <= cpc CPUs are kept in id order.  Takes n.
+__device__ void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
+  const int len = popc4(m);
+  if (len <= C.cpc) {
+    for (int i = 0; i < C.ncpu && n > 0; i++) {
+      const int p = C.pos_by_id[i];
+      if (tbit(m, p)) {
+        acc_take1(C, a, p);
+        n--;
+      }
+    }
+    return;
+  }
+  uint64_t used[NW] = {0, 0, 0, 0};
+  for (int round = 0; round < C.cpc && n > 0; round++) {
+    uint64_t seen[NW] = {0, 0, 0, 0};  // cores already visited this round
+    for (int i = 0; i < C.ncpu && n > 0; i++) {
+      const int p = C.pos_by_id[i];
+      if (!tbit(m, p) || tbit(used, p)) continue;
+      const int lead = p - (p % C.cpc);
+      if (tbit(seen, lead)) continue;
+      sbit(seen, lead);
+      sbit(used, p);
+      acc_take1(C, a, p);
+      n--;
+    }
+  }
+}
+
+// freeCPUs(filterExclusive) + spreadCPUs + one-by-one take (:218-229).
+__device__ void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
+  uint64_t X[NW], F[NW];
+  if (fe) acc_excluded(C, a, false, X);
+  else
+    for (int w = 0; w < NW; w++) X[w] = 0;
+  for (int w = 0; w < NW; w++) F[w] = a.A[w] & ~X[w];
+  int nfree[NMAX], sfree[NMAX], colo[NMAX];
+  for (int k = 0; k < NMAX; k++) nfree[k] = sfree[k] = colo[k] = 0;
+  for (int k = 0; k < C.nnuma; k++) nfree[k] = popc_and(F, C.nm[k]);
+  for (int s = 0; s < C.nsock; s++) {
+    sfree[s] = popc_and(F, C.sm[s]);
+    colo[s] = popc_and(a.R, C.sm[s]);
+  }
+  // core groups (node k, free CPUs in core cf): every sort key except the core id
+  // is constant inside a group; order groups, merge equal keys, list cores by id.
+  int gk[2 * NMAX], gc[2 * NMAX], ng = 0;
+  for (int k = 0; k < C.nnuma; k++)
+    for (int cf = 1; cf <= C.cpc; cf++) {
+      gk[ng] = k;
+      gc[ng] = cf;
+      ng++;
+    }
+  auto before = [&](int x, int y) -> int {  // 1: x before y, -1: y before x, 0: equal key
+    const int sx = C.sock_of_node[gk[x]], sy = C.sock_of_node[gk[y]];
+    if (colo[sx] != colo[sy]) return colo[sx] > colo[sy] ? 1 : -1;
+    if (sfree[sx] != sfree[sy]) return free_before(a.most, sfree[sx], sfree[sy]) ? 1 : -1;
+    if (nfree[gk[x]] != nfree[gk[y]]) return free_before(a.most, nfree[gk[x]], nfree[gk[y]]) ? 1 : -1;
+    if (gc[x] != gc[y]) return gc[x] < gc[y] ? 1 : -1;
+    if (sx != sy) return sx < sy ? 1 : -1;
+    return 0;
+  };
+  for (int i = 1; i < ng; i++)
+    for (int j = i; j > 0 && before(j, j - 1) > 0; j--) {
+      const int tk = gk[j], tc = gc[j];
+      gk[j] = gk[j - 1];
+      gc[j] = gc[j - 1];
+      gk[j - 1] = tk;
+      gc[j - 1] = tc;
+    }
+  // the list: merged groups in order, cores ascending, CPUs ascending by id (= t order)
+  // collected as positions; then spread (round t = t-th CPU of each listed core)
+  int16_t lst[KOORDHIP_NUMA_MAX_CPUS];
+  int nl = 0;
+  for (int g0 = 0; g0 < ng;) {
+    int g1 = g0 + 1;
+    while (g1 < ng && before(g0, g1) == 0) g1++;
+    uint64_t lead[NW] = {0, 0, 0, 0};
+    for (int g = g0; g < g1; g++)
+      for (int w = 0; w < NW; w++) {
+        const uint64_t nmF = F[w] & C.nm[gk[g]][w];
+        const uint64_t any = fold_or(nmF, C.cpc), all = fold_and(nmF, C.cpc);
+        lead[w] |= (gc[g] == C.cpc) ? all : (any & ~all);  // cpc <= 2: 1 CPU or both
+      }
+    for (int w = 0; w < NW; w++) {
+      uint64_t x = lead[w];
+      while (x) {
+        const int b = __builtin_ctzll(x);
+        x &= x - 1;
+        for (int t = 0; t < C.cpc; t++)
+          if (tbit(F, w * 64 + b + t)) lst[nl++] = (int16_t)(w * 64 + b + t);
+      }
+    }
+    g0 = g1;
+  }
+  if (nl > C.cpc) {
+    // spreadCPUs: stable rounds over the listed order
+    uint64_t done[NW] = {0, 0, 0, 0};
+    for (int round = 0; round < C.cpc && a.need > 0; round++) {
+      uint64_t seen[NW] = {0, 0, 0, 0};
+      for (int i = 0; i < nl && a.need > 0; i++) {
+        const int p = lst[i];
+        if (tbit(done, p)) continue;
+        const int lead = p - (p % C.cpc);
+        if (tbit(seen, lead)) continue;
+        sbit(seen, lead);
+        sbit(done, p);
+        acc_take1(C, a, p);
+      }
+    }
+  } else {
+    for (int i = 0; i < nl && a.need > 0; i++) acc_take1(C, a, lst[i]);
+  }
+}
+
+// takeCPUs; returns true with a.R filled.
+__device__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
+  if (a.need < 1) return true;
+  if (a.need > popc4(a.A)) return false;
+  const int cpc = C.cpc;
+  const bool full = policy == (int)KOORDHIP_CPUBIND_FULL_PCPUS;
+  uint64_t FA[NW], T[NW], X[NW];
+  if (full || cpc == 1) {
+    if (a.need <= C.cpn) {  // :111-121
+      for (int fe = 1; fe >= 0; fe--) {
+        if (fe) acc_excluded(C, a, false, X);
+        for (int w = 0; w < NW; w++) {
+          uint64_t allowed = a.A[w];
+          if (fe && a.excl == (int)KOORDHIP_CPUEXCL_NUMA) allowed &= ~X[w];  // NUMANodeLevel only (:377)
+          FA[w] = expand(fold_and(allowed, cpc), cpc);
+          X[w] = fe ? X[w] : 0;
+        }
+        int best = -1, bc = 0, bs = 0;
+        for (int k = 0; k < C.nnuma; k++) {
+          const int cnt = popc_and(FA, C.nm[k]);
+          if (cnt < a.need) continue;
+          int sf = 0;  // socketFreeScores: allowed CPUs of the node's socket
+          for (int w = 0; w < NW; w++) {
+            uint64_t allowed = a.A[w];
+            if (fe && a.excl == (int)KOORDHIP_CPUEXCL_NUMA) allowed &= ~X[w];
+            sf += __popcll(allowed & C.sm[C.sock_of_node[k]][w]);
+          }
+          if (best < 0 || (cnt != bc ? free_before(a.most, cnt, bc) : (sf != bs && free_before(a.most, sf, bs)))) {
+            best = k;
+            bc = cnt;
+            bs = sf;
+          }
+        }
+        if (best >= 0) {
+          for (int w = 0; w < NW; w++) T[w] = FA[w] & C.nm[best][w];
+          acc_take_low(C, a, T, a.need);
+          return true;
+        }
+      }
+    }
+    for (int w = 0; w < NW; w++) FA[w] = expand(fold_and(a.A[w], cpc), cpc);
+    if (a.need <= C.cps) {  // :126-134
+      int best = -1, bc = 0;
+      for (int s = 0; s < C.nsock; s++) {
+        const int cnt = popc_and(FA, C.sm[s]);
+        if (cnt < a.need) continue;
+        if (best < 0 || (cnt != bc && free_before(a.most, cnt, bc))) {
+          best = s;
+          bc = cnt;
+        }
+      }
+      if (best >= 0) {
+        for (int w = 0; w < NW; w++) T[w] = FA[w] & C.sm[best][w];
+        acc_take_low(C, a, T, a.need);
+        return true;
+      }
+    }
+    // :141-155: sockets (in strategy order, then stably by count desc)
+    int ord[NMAX], cnt[NMAX], no = 0;
+    for (int s = 0; s < C.nsock; s++) {
+      const int c = popc_and(FA, C.sm[s]);
+      if (c == 0) continue;
+      int j = no++;
+      // strategy order: (count per strategy, id)
+      while (j > 0 && free_before(a.most, c, cnt[j - 1])) {
+        ord[j] = ord[j - 1];
+        cnt[j] = cnt[j - 1];
+        j--;
+      }
+      ord[j] = s;
+      cnt[j] = c;
+    }
+    for (int i = 1; i < no; i++)  // stable: count desc
+      for (int j = i; j > 0 && cnt[j] > cnt[j - 1]; j--) {
+        const int to = ord[j], tc = cnt[j];
+        ord[j] = ord[j - 1];
+        cnt[j] = cnt[j - 1];
+        ord[j - 1] = to;
+        cnt[j - 1] = tc;
+      }
+    int uo[NMAX], uc[NMAX], nu = 0;
+    for (int i = 0; i < no; i++) {
+      if (a.need < cnt[i]) {
+        uo[nu] = ord[i];
+        uc[nu] = cnt[i];
+        nu++;
+      } else {
+        for (int w = 0; w < NW; w++) T[w] = FA[w] & C.sm[ord[i]][w];
+        acc_take_low(C, a, T, cnt[i]);
+        if (a.need < 1) return true;
+      }
+    }
+    if (a.need >= cpc) {  // :159-176: deferred sockets by count asc, core by core
+      for (int i = 1; i < nu; i++)
+        for (int j = i; j > 0 && uc[j] < uc[j - 1]; j--) {
+          const int to = uo[j], tc = uc[j];
+          uo[j] = uo[j - 1];
+          uc[j] = uc[j - 1];
+          uo[j - 1] = to;
+          uc[j - 1] = tc;
+        }
+      for (int i = 0; i < nu; i++) {
+        for (int w = 0; w < NW; w++) T[w] = FA[w] & C.sm[uo[i]][w];
+        bool stop = false;
+        for (int w = 0; w < NW && !stop; w++) {
+          uint64_t x = T[w];
+          while (x) {
+            const int b = __builtin_ctzll(x);
+            uint64_t core = (cpc == 1) ? (1ull << b) : (3ull << b);
+            x &= ~core;
+            for (int t = 0; t < cpc; t++) acc_take1(C, a, w * 64 + b + t);
+            if (a.need < 1) return true;
+            if (a.need < cpc) {
+              stop = true;
+              break;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (!full) {
+    if (a.need <= C.cpn) {  // :187-199
+      for (int fe = 1; fe >= 0; fe--) {
+        if (fe) acc_excluded(C, a, false, X);
+        uint64_t Fl[NW];
+        for (int w = 0; w < NW; w++) Fl[w] = a.A[w] & ~(fe ? X[w] : 0ull);
+        int best = -1, bf = 0, bs = 0;
+        for (int k = 0; k < C.nnuma; k++) {
+          const int nf = popc_and(Fl, C.nm[k]);
+          if (nf == 0) continue;
+          const int len = fe ? cores_in(Fl, C.nm[k], cpc) : nf;
+          if (len < a.need) continue;
+          const int sf = popc_and(Fl, C.sm[C.sock_of_node[k]]);
+          if (best < 0 || (nf != bf ? free_before(a.most, nf, bf) : (sf != bs && free_before(a.most, sf, bs)))) {
+            best = k;
+            bf = nf;
+            bs = sf;
+          }
+        }
+        if (best >= 0) {
+          for (int w = 0; w < NW; w++) T[w] = Fl[w] & C.nm[best][w];
+          if (fe) {  // extractCPU: each core's lowest-id allowed CPU
+            uint64_t E[NW];
+            for (int w = 0; w < NW; w++) {
+              const uint64_t any = fold_or(T[w], cpc);
+              E[w] = cpc == 1 ? T[w] : ((T[w] & 0x5555555555555555ull) | ((any & ~T[w]) << 1));
+            }
+            acc_take_spread_by_id(C, a, E, a.need);
+          } else {
+            acc_take_spread_by_id(C, a, T, a.need);
+          }
+          return true;
+        }
+      }
+    }
+    if (a.need <= C.cps) {  // :203-214
+      for (int fe = 1; fe >= 0; fe--) {
+        if (fe) acc_excluded(C, a, true, X);
+        uint64_t Fl[NW];
+        for (int w = 0; w < NW; w++) Fl[w] = a.A[w] & ~(fe ? X[w] : 0ull);
+        int best = -1, bl = 0;
+        for (int s = 0; s < C.nsock; s++) {
+          const int nf = popc_and(Fl, C.sm[s]);
+          if (nf == 0) continue;
+          const int len = fe ? cores_in(Fl, C.sm[s], cpc) : nf;
+          if (len < a.need) continue;
+          if (best < 0 || (len != bl && free_before(a.most, len, bl))) {
+            best = s;
+            bl = len;
+          }
+        }
+        if (best >= 0) {
+          for (int w = 0; w < NW; w++) T[w] = Fl[w] & C.sm[best][w];
+          if (fe) {
+            uint64_t E[NW];
+            for (int w = 0; w < NW; w++) {
+              const uint64_t any = fold_or(T[w], cpc);
+              E[w] = cpc == 1 ? T[w] : ((T[w] & 0x5555555555555555ull) | ((any & ~T[w]) << 1));
+            }
+            acc_take_spread_by_id(C, a, E, a.need);
+          } else {
+            acc_take_spread_by_id(C, a, T, a.need);
+          }
+          return true;
+        }
+      }
+    }
+  }
+  acc_fallback_pass(C, a, true);
+  if (a.need < 1) return true;
+  acc_fallback_pass(C, a, false);
+  return a.need < 1;
+}
+
+// Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
+__device__ bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const koordhip_pod &p, uint64_t *cpus) {
+  for (int w = 0; w < NW; w++) cpus[w] = 0;
+  const int need = p.numa_cpus;
+  if (popc4(r.fr) < need) return false;
+  Acc a;
+  for (int w = 0; w < NW; w++) {
+    a.A[w] = r.fr[w];
+    a.R[w] = 0;
+    a.XC[w] = fold_or(r.ep[w], C.cpc);
+  }
+  a.XN = 0;
+  for (int k = 0; k < C.nnuma; k++)
+    if (popc_and(r.en, C.nm[k])) a.XN |= 1u << k;
+  a.need = need;
+  a.excl = (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy);
+  a.most = (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0;
+  const int pol = node_policy(r.nflags, (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy));
+  if (!acc_take_cpus(C, a, pol)) return false;
+  if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE) {  // satisfiedRequiredCPUBindPolicy
+    int n = popc4(a.R), cores = 0;
+    for (int w = 0; w < NW; w++) cores += __popcll(fold_or(a.R[w], C.cpc));
+    if (pol == (int)KOORDHIP_CPUBIND_FULL_PCPUS && cores * C.cpc != n) return false;
+    if (pol == (int)KOORDHIP_CPUBIND_SPREAD_BY_PCPUS && cores != n) return false;
+  }
+  for (int w = 0; w < NW; w++) cpus[w] = a.R[w];
+  return true;
+}
+
+}  // namespace kh

@@ -106,13 +106,35 @@ class PlacementEngine:
     def restore(self):
         abi.check(self.lib, self.lib.koordhip_restore(self._ctx))
 
-    def commit(self, pod, node: int):
+    def commit(self, pod, node: int) -> np.ndarray:
+        """Reserve; returns the allocated cpuset mask (zeros for a non-cpuset pod).
+        Raises KoordhipError(code=abi.E_RESERVE) when the NUMA Allocate fails."""
         pod = np.ascontiguousarray(np.atleast_1d(pod), dtype=abi.POD_DTYPE)
-        abi.check(self.lib, self.lib.koordhip_commit(self._ctx, pod.ctypes.data, int(node)))
+        cpus = np.zeros(abi.NUMA_WORDS, np.uint64)
+        abi.check(self.lib, self.lib.koordhip_commit(self._ctx, pod.ctypes.data, int(node),
+                                                     abi.ptr(cpus, C.c_uint64)))
+        return cpus
 
-    def uncommit(self, pod, node: int):
+    def uncommit(self, pod, node: int, cpus=None):
         pod = np.ascontiguousarray(np.atleast_1d(pod), dtype=abi.POD_DTYPE)
-        abi.check(self.lib, self.lib.koordhip_uncommit(self._ctx, pod.ctypes.data, int(node)))
+        c = None if cpus is None else np.ascontiguousarray(cpus, dtype=np.uint64)
+        abi.check(self.lib, self.lib.koordhip_uncommit(self._ctx, pod.ctypes.data, int(node),
+                                                       abi.ptr(c, C.c_uint64)))
+
+    def read_numa(self) -> dict:
+        n = self.n
+        fr = np.zeros((abi.NUMA_WORDS, n), np.uint64)
+        ep = np.zeros((abi.NUMA_WORDS, n), np.uint64)
+        en = np.zeros((abi.NUMA_WORDS, n), np.uint64)
+        cnt = np.zeros(n, np.int32)
+        abi.check(self.lib, self.lib.koordhip_read_numa(self._ctx, abi.ptr(fr, C.c_uint64), abi.ptr(ep, C.c_uint64),
+                                                        abi.ptr(en, C.c_uint64), abi.ptr(cnt, C.c_int32)))
+        return {"free": fr, "excl_pcpu": ep, "excl_numa": en, "alloc_cnt": cnt}
+
+    def fetch_cpusets(self, n: int) -> np.ndarray:
+        out = np.zeros((n, abi.NUMA_WORDS), np.uint64)
+        abi.check(self.lib, self.lib.koordhip_fetch_cpusets(self._ctx, abi.ptr(out, C.c_uint64), n))
+        return out
 
     def last_stats(self) -> dict:
         em, tm = C.c_double(), C.c_double()

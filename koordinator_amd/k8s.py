@@ -258,6 +258,12 @@ def kube_qos(pod: Pod) -> str:
     return "Burstable"
 
 
+def qos_class_raw(pod: Pod) -> str:
+    """GetPodQoSClassRaw, qos_utils.go:57-70: the koordinator.sh/qosClass label only."""
+    q = pod.labels.get(LABEL_POD_QOS) if pod.labels else None
+    return q if q in (QOS_LSE, QOS_LSR, QOS_LS, QOS_BE, QOS_SYSTEM) else QOS_NONE
+
+
 def qos_class(pod: Pod) -> str:
     """GetPodQoSClassWithDefault, qos_utils.go:32-62 (Guaranteed -> LSR)."""
     q = pod.labels.get(LABEL_POD_QOS) if pod.labels else None

@@ -13,7 +13,7 @@ from typing import Dict, Iterable, List, Optional, Set, Tuple
 
 import numpy as np
 
-from . import abi, k8s
+from . import abi, numa, k8s
 from .config import LoadAwareSchedulingArgs, Profile
 from .snapshot import NodeTable, pod_array
 
@@ -175,7 +175,17 @@ def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None)
         flags |= abi.POD_REQ_BCPU
     if k8s.BATCH_MEMORY in present:
         flags |= abi.POD_REQ_BMEM
-    rec["flags"] = flags
+    # NodeNUMAResource PreFilter (plugin.go:210-260, AllowUseCPUSet util.go:48-55)
+    allow = k8s.qos_class_raw(pod) in (k8s.QOS_LSE, k8s.QOS_LSR) and k8s.priority_class(pod) == k8s.PRIORITY_PROD
+    zero = not (any(req) or present)
+    try:
+        nf, ncpus, pol = numa.prefilter_state(pod.annotations or {}, allow, int(req[abi.RES_CPU]), zero,
+                                              p.numa.default_cpu_bind_policy)
+    except numa.PreFilterError:
+        nf, ncpus, pol = abi.POD_NUMA_ERROR, 0, 0
+    rec["flags"] = flags | nf
+    rec["numa_cpus"] = ncpus
+    rec["numa_policy"] = pol
     return rec
 
 

@@ -20,9 +20,13 @@ I64_COLS = (
        "laf_used_m0", "laf_used_m1", "laf_total_m0", "laf_total_m1", "laf_prod_used_m0", "laf_prod_used_m1",
        "laf_thr0", "laf_thr1", "laf_prod_thr0", "laf_prod_thr1"]
 )
-I32_COLS = ["alloc_pods", "npods"]
-U8_COLS = ["la_flags"]
-ALL_COLS = I64_COLS + I32_COLS + U8_COLS
+I32_COLS = ["alloc_pods", "npods", "numa_class", "numa_alloc_cnt"]
+U8_COLS = ["la_flags", "numa_flags"]
+U64_COLS = ([f"numa_free{w}" for w in range(abi.NUMA_WORDS)] + [f"numa_excl_pcpu{w}" for w in range(abi.NUMA_WORDS)]
+            + [f"numa_excl_numa{w}" for w in range(abi.NUMA_WORDS)])
+ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS
+# NodeNUMAResource mutable columns (advanced by cpuset Reserves)
+NUMA_MUTABLE = [c for c in U64_COLS] + ["numa_alloc_cnt"]
 
 
 def _dtype(col: str):
@@ -30,6 +34,8 @@ def _dtype(col: str):
         return np.int32
     if col in U8_COLS:
         return np.uint8
+    if col in U64_COLS:
+        return np.uint64
     return np.int64
 
 
@@ -39,12 +45,15 @@ class NodeTable:
     n: int
     cols: Dict[str, np.ndarray] = field(default_factory=dict)
     names: List[str] = field(default_factory=list)
+    # NodeNUMAResource topology classes (abi.NUMA_CLASS_DTYPE), indexed by numa_class
+    numa_classes: np.ndarray = field(default_factory=lambda: np.zeros(0, abi.NUMA_CLASS_DTYPE))
 
     @classmethod
     def empty(cls, n: int) -> "NodeTable":
         t = cls(n=n)
         for c in ALL_COLS:
             t.cols[c] = np.zeros(n, dtype=_dtype(c))
+        t.cols["numa_class"][:] = -1
         t.names = [f"node-{i}" for i in range(n)]
         return t
 
@@ -57,12 +66,14 @@ class NodeTable:
         for c in ALL_COLS:
             t.cols[c] = np.ascontiguousarray(self.cols[c][idx])
         t.names = [self.names[i] for i in idx] if self.names else []
+        t.numa_classes = self.numa_classes
         return t
 
     def copy(self) -> "NodeTable":
         t = NodeTable(n=self.n)
         t.cols = {k: v.copy() for k, v in self.cols.items()}
         t.names = list(self.names)
+        t.numa_classes = self.numa_classes.copy()
         return t
 
     def as_soa(self) -> abi.KoordhipNodeSoa:
@@ -89,6 +100,17 @@ class NodeTable:
             s.laf_thr[k] = p64(f"laf_thr{k}")
             s.laf_prod_thr[k] = p64(f"laf_prod_thr{k}")
         s.la_flags = self.cols["la_flags"].ctypes.data_as(C.POINTER(C.c_uint8))
+        self.numa_classes = np.ascontiguousarray(self.numa_classes, dtype=abi.NUMA_CLASS_DTYPE)
+        s.numa_classes = self.numa_classes.ctypes.data if len(self.numa_classes) else None
+        s.n_numa_classes = len(self.numa_classes)
+        s.numa_class = p32("numa_class")
+        p64u = lambda c: self.cols[c].ctypes.data_as(C.POINTER(C.c_uint64))
+        for w in range(abi.NUMA_WORDS):
+            s.numa_free[w] = p64u(f"numa_free{w}")
+            s.numa_excl_pcpu[w] = p64u(f"numa_excl_pcpu{w}")
+            s.numa_excl_numa[w] = p64u(f"numa_excl_numa{w}")
+        s.numa_alloc_cnt = p32("numa_alloc_cnt")
+        s.numa_flags = self.cols["numa_flags"].ctypes.data_as(C.POINTER(C.c_uint8))
         return s
 
     def nbytes(self) -> int:
@@ -100,6 +122,17 @@ def concat(tables: List[NodeTable]) -> NodeTable:
     for c in ALL_COLS:
         t.cols[c] = np.concatenate([x.cols[c] for x in tables])
     t.names = [nm for x in tables for nm in x.names]
+    # merge topology class tables, re-indexing each part's numa_class
+    classes, off = [], 0
+    pos = 0
+    for x in tables:
+        cls = t.cols["numa_class"][pos:pos + x.n]
+        cls[cls >= 0] += off
+        classes.append(x.numa_classes)
+        off += len(x.numa_classes)
+        pos += x.n
+    t.numa_classes = (np.concatenate(classes) if classes else np.zeros(0, abi.NUMA_CLASS_DTYPE)).astype(
+        abi.NUMA_CLASS_DTYPE)
     return t
 
 

@@ -105,11 +105,95 @@ def make_cluster(spec: ClusterSpec, profile: Profile) -> NodeTable:
     return t
 
 
+# ------------------------------------------------------------------ NUMA (config 3)
+# node cpu -> 2-socket topology (sockets, NUMA nodes per socket, cores per node, threads)
+NUMA_SHAPES = {32000: (2, 1, 8, 2), 64000: (2, 1, 16, 2), 96000: (2, 1, 24, 2), 128000: (2, 2, 16, 2)}
+
+
+@dataclass
+class NumaSpec:
+    no_topology_frac: float = 0.02     # nodes without a (valid) NodeResourceTopology
+    max_prealloc_frac: float = 0.5     # cores already held by cpuset pods: U[0, max] of the cores
+    excl_frac: float = 0.2             # share of pre-allocated cores held with an exclusive policy
+    reserved_frac: float = 0.3         # nodes with kubelet-reserved CPUs (the first core)
+    full_only_frac: float = 0.05       # node label cpu-bind-policy=FullPCPUsOnly
+    spread_frac: float = 0.05          # node label cpu-bind-policy=SpreadByPCPUs
+    most_allocated_frac: float = 0.3   # node label numa-allocate-strategy=MostAllocated
+    linux_numbering: bool = True
+
+
+def add_numa(t: NodeTable, spec: NumaSpec, profile: Profile, seed: int = SEED) -> NodeTable:
+    """NodeNUMAResource columns for a synthetic cluster: a 2-socket topology
+    matching each node's cpu, pre-allocated cpusets (some exclusive), reserved
+    CPUs, node bind-policy / allocate-strategy labels."""
+    from . import numa as nm
+    n, s = t.n, seed + 7
+    classes = nm.ClassTable()
+    cls_of = {}
+    for cpu, shape in NUMA_SHAPES.items():
+        topo = nm.linux_topology(*shape) if spec.linux_numbering else nm.reference_test_topology(*shape)
+        cls_of[cpu] = (classes.add(topo), topo)
+    t.numa_classes = classes.records()
+    no_topo = uniform(s, n, 40) < spec.no_topology_frac
+    frac = uniform(s, n, 41) * spec.max_prealloc_frac
+    reserved = uniform(s, n, 42) < spec.reserved_frac
+    u_pol = uniform(s, n, 43)
+    most = uniform(s, n, 44) < spec.most_allocated_frac
+    default_most = profile.numa.default_most_allocated
+    rnd = splitmix64(s, n * 4, 45)
+    for i in range(n):
+        cpu = int(t["alloc0"][i])
+        if no_topo[i] or cpu not in cls_of:
+            t["numa_class"][i] = -1
+            continue
+        ci, topo = cls_of[cpu]
+        t["numa_class"][i] = ci
+        ncores = topo.num_cores
+        cpc = topo.cpus_per_core
+        rng = np.random.default_rng(int(rnd[i * 4]))
+        k = int(frac[i] * ncores)
+        taken = rng.choice(ncores, size=k, replace=False) if k else np.zeros(0, np.int64)
+        free = np.zeros(abi.NUMA_WORDS, np.uint64)
+        ep = np.zeros(abi.NUMA_WORDS, np.uint64)
+        en = np.zeros(abi.NUMA_WORDS, np.uint64)
+        all_pos = np.arange(topo.num_cpus)
+        used = np.zeros(topo.num_cpus, bool)
+        for c in taken:
+            used[c * cpc:(c + 1) * cpc] = True
+            r = rng.random()
+            if r < spec.excl_frac / 2:
+                for p in range(c * cpc, (c + 1) * cpc):
+                    ep[p >> 6] |= np.uint64(1) << np.uint64(p & 63)
+            elif r < spec.excl_frac:
+                for p in range(c * cpc, (c + 1) * cpc):
+                    en[p >> 6] |= np.uint64(1) << np.uint64(p & 63)
+        res = np.zeros(topo.num_cpus, bool)
+        if reserved[i]:
+            res[0:cpc] = True           # kubelet reserved: the first core
+        for p in all_pos[~used & ~res]:
+            free[p >> 6] |= np.uint64(1) << np.uint64(int(p) & 63)
+        for w in range(abi.NUMA_WORDS):
+            t[f"numa_free{w}"][i] = free[w]
+            t[f"numa_excl_pcpu{w}"][i] = ep[w]
+            t[f"numa_excl_numa{w}"][i] = en[w]
+        t["numa_alloc_cnt"][i] = int(used.sum())
+        f = 0
+        if u_pol[i] < spec.full_only_frac:
+            f = abi.NODE_CPUBIND_FULL_PCPUS_ONLY
+        elif u_pol[i] < spec.full_only_frac + spec.spread_frac:
+            f = abi.NODE_CPUBIND_SPREAD_BY_PCPUS
+        if (most[i] if spec.most_allocated_frac > 0 else default_most):
+            f |= abi.NODE_NUMA_MOST_ALLOCATED
+        t["numa_flags"][i] = f
+    return t
+
+
 @dataclass
 class StreamSpec:
     n_pods: int
     be_frac: float = 0.0
     seed: int = SEED
+    cpuset_frac: float = 0.0   # share of LS pods that are LSR/LSE cpuset pods (NodeNUMAResource)
 
 
 LS_CPU = [250, 500, 1000, 2000, 4000]
@@ -157,7 +241,44 @@ def make_pods(spec: StreamSpec, profile: Profile) -> np.ndarray:
     pods["est_mem"] = np.where(be, be_est_mem, ls_est_mem)
     pods["flags"] = np.where(be, abi.POD_HAS_REQ | abi.POD_REQ_BCPU | abi.POD_REQ_BMEM,
                              abi.POD_PROD | abi.POD_HAS_REQ).astype(np.uint32)
+    if spec.cpuset_frac > 0:
+        _make_cpuset_pods(pods, be, spec, fc, fm)
     return pods
+
+
+CPUSET_CPUS = [1, 2, 4, 8, 16]
+# (required, preferred, exclusive) mixes of LSR/LSE resource-spec annotations
+CPUSET_POLICIES = [
+    (abi.CPUBIND_NONE, abi.CPUBIND_FULL_PCPUS, abi.CPUEXCL_NONE),          # default policy (FullPCPUs)
+    (abi.CPUBIND_NONE, abi.CPUBIND_FULL_PCPUS, abi.CPUEXCL_NONE),
+    (abi.CPUBIND_NONE, abi.CPUBIND_SPREAD_BY_PCPUS, abi.CPUEXCL_NONE),
+    (abi.CPUBIND_FULL_PCPUS, abi.CPUBIND_FULL_PCPUS, abi.CPUEXCL_NONE),
+    (abi.CPUBIND_SPREAD_BY_PCPUS, abi.CPUBIND_SPREAD_BY_PCPUS, abi.CPUEXCL_NONE),
+    (abi.CPUBIND_NONE, abi.CPUBIND_SPREAD_BY_PCPUS, abi.CPUEXCL_PCPU),
+    (abi.CPUBIND_FULL_PCPUS, abi.CPUBIND_FULL_PCPUS, abi.CPUEXCL_NUMA),
+    (abi.CPUBIND_SPREAD_BY_PCPUS, abi.CPUBIND_SPREAD_BY_PCPUS, abi.CPUEXCL_PCPU),
+]
+
+
+def _make_cpuset_pods(pods, be, spec: StreamSpec, fc: int, fm: int):
+    """LSR/LSE prod pods with integral cpu (Guaranteed: limit = request)."""
+    n, s = spec.n_pods, spec.seed + 1
+    cs = (~be) & (uniform(s, n, 30) < spec.cpuset_frac)
+    ncpu = choice(s, n, 31, CPUSET_CPUS).astype(np.int64)
+    pol = (splitmix64(s, n, 32) % np.uint64(len(CPUSET_POLICIES))).astype(np.int64)
+    mem = choice(s, n, 33, LS_MEM).astype(np.int64)
+    req = pods["req"]
+    req[cs, abi.RES_CPU] = ncpu[cs] * 1000
+    req[cs, abi.RES_MEM] = mem[cs]
+    pods["nz_cpu_m"][cs] = ncpu[cs] * 1000
+    pods["nz_mem"][cs] = mem[cs]
+    pods["est_cpu"][cs] = np.minimum(_round_half_away((ncpu[cs] * 1000).astype(np.float64) * fc / 100),
+                                     ncpu[cs] * 1000)
+    pods["est_mem"][cs] = np.minimum(_round_half_away(mem[cs].astype(np.float64) * fm / 100), mem[cs])
+    pods["flags"][cs] |= np.uint32(abi.POD_CPUSET)
+    pods["numa_cpus"][cs] = ncpu[cs].astype(np.int32)
+    codes = np.array([abi.numa_policy(*x) for x in CPUSET_POLICIES], np.uint32)
+    pods["numa_policy"][cs] = codes[pol[cs]]
 
 
 def pod_objects(spec: StreamSpec, limit: int = None) -> List[k8s.Pod]:
@@ -187,6 +308,7 @@ def pod_objects(spec: StreamSpec, limit: int = None) -> List[k8s.Pod]:
 CONFIGS = {
     1: dict(nodes=500, pods=1000, be_frac=0.0),
     2: dict(nodes=5000, pods=10000, be_frac=0.0),
+    3: dict(nodes=5000, pods=10000, be_frac=0.2, cpuset_frac=0.5, numa=True),
     4: dict(nodes=50000, pods=100000, be_frac=0.3),
     5: dict(nodes=200000, pods=100000, be_frac=0.3),
 }
@@ -195,5 +317,8 @@ CONFIGS = {
 def config_workload(cfg_id: int, profile: Profile, n_nodes: int = None, n_pods: int = None) -> Tuple[NodeTable, np.ndarray]:
     c = CONFIGS[cfg_id]
     table = make_cluster(ClusterSpec(n_nodes or c["nodes"]), profile)
-    pods = make_pods(StreamSpec(n_pods or c["pods"], be_frac=c["be_frac"]), profile)
+    if c.get("numa"):
+        add_numa(table, NumaSpec(), profile)
+    pods = make_pods(StreamSpec(n_pods or c["pods"], be_frac=c["be_frac"], cpuset_frac=c.get("cpuset_frac", 0.0)),
+                     profile)
     return table, pods

@@ -33,6 +33,11 @@ class OrcState(C.Structure):
         ("la_used_mem", C.POINTER(C.c_int64)),
         ("la_used_prod_cpu_m", C.POINTER(C.c_int64)),
         ("la_used_prod_mem", C.POINTER(C.c_int64)),
+        ("numa_free", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
+        ("numa_excl_pcpu", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
+        ("numa_excl_numa", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
+        ("numa_alloc_cnt", C.POINTER(C.c_int32)),
+        ("cpuset_out", C.c_void_p),
     ]
 
 
@@ -58,7 +63,13 @@ def lib():
         L.orc_state_free.argtypes = [C.POINTER(OrcState)]
         L.orc_eval.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32,
                                vp, vp, vp, C.c_int32]
-        L.orc_commit.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32, C.c_int]
+        L.orc_commit.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32, C.c_int, vp]
+        L.orc_commit.restype = C.c_int
+        L.orc_take_cpus.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+        L.orc_take_cpus.restype = C.c_int
+        L.orc_spread_order.argtypes = [vp, vp, C.c_int, vp]
+        L.orc_spread_order.restype = C.c_int
+        L.orc_set_cpuset_out.argtypes = [C.POINTER(OrcState), vp]
         L.orc_place_stream.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32,
                                        vp, C.c_int32]
         L.orc_la_flags.argtypes = [C.POINTER(abi.KoordhipNodeSoa), C.c_int32, vp]
@@ -98,18 +109,26 @@ class Oracle:
                        tk.ctypes.data if tk is not None else None, k)
         return {"status": st, "scores": sc, "topk": tk}
 
-    def commit(self, pod: np.ndarray, node: int, sign: int = 1):
+    def commit(self, pod: np.ndarray, node: int, sign: int = 1, cpus=None):
+        """Reserve (sign 1) / Unreserve (sign -1).  Returns (rc, cpus): rc is
+        abi.E_RESERVE when the NUMA Allocate fails; for Unreserve of a cpuset
+        pod pass the cpus it was given."""
         pod = np.ascontiguousarray(np.atleast_1d(pod))
-        lib().orc_commit(C.byref(self.cfg), C.byref(self.st), pod.ctypes.data, node, sign)
+        buf = np.zeros(abi.NUMA_WORDS, np.uint64) if cpus is None else np.ascontiguousarray(cpus, np.uint64).copy()
+        rc = lib().orc_commit(C.byref(self.cfg), C.byref(self.st), pod.ctypes.data, node, sign, buf.ctypes.data)
+        return rc, buf
 
-    def place_stream(self, pods: np.ndarray, threads: int = 1) -> np.ndarray:
+    def place_stream(self, pods: np.ndarray, threads: int = 1, cpusets: bool = False):
         pods = np.ascontiguousarray(pods)
         out = np.zeros(len(pods), np.int32)
+        cs = np.zeros((len(pods), abi.NUMA_WORDS), np.uint64) if cpusets else None
+        lib().orc_set_cpuset_out(C.byref(self.st), cs.ctypes.data if cs is not None else None)
         rc = lib().orc_place_stream(C.byref(self.cfg), C.byref(self.st), pods.ctypes.data, len(pods),
                                     out.ctypes.data, threads)
+        lib().orc_set_cpuset_out(C.byref(self.st), None)
         if rc != 0:
             raise RuntimeError("orc_place_stream failed")
-        return out
+        return (out, cs) if cpusets else out
 
     def flags(self) -> np.ndarray:
         return np.ctypeslib.as_array(self.st.flags, shape=(self.n,)).copy()
@@ -124,6 +143,37 @@ class Oracle:
             "la_used": np.stack([a64(self.st.la_used_cpu_m), a64(self.st.la_used_mem)]),
             "la_used_prod": np.stack([a64(self.st.la_used_prod_cpu_m), a64(self.st.la_used_prod_mem)]),
         }
+
+    def numa_state(self) -> dict:
+        n = self.n
+        a = lambda p, shape=(n,): np.ctypeslib.as_array(p, shape=shape).copy()
+        return {
+            "free": np.stack([a(self.st.numa_free[w]) for w in range(abi.NUMA_WORDS)]),
+            "excl_pcpu": np.stack([a(self.st.numa_excl_pcpu[w]) for w in range(abi.NUMA_WORDS)]),
+            "excl_numa": np.stack([a(self.st.numa_excl_numa[w]) for w in range(abi.NUMA_WORDS)]),
+            "alloc_cnt": a(self.st.numa_alloc_cnt),
+        }
+
+
+def take_cpus(cls: np.ndarray, avail, need: int, bind_policy: int, excl_policy: int = 0, most_allocated: bool = True,
+              excl_pcpu=None, excl_numa=None):
+    """takeCPUs on one topology class (a NUMA_CLASS_DTYPE record); masks are
+    [NUMA_WORDS] uint64 over core-major positions.  Returns the mask or None."""
+    cls = np.ascontiguousarray(cls, dtype=abi.NUMA_CLASS_DTYPE)
+    m = lambda x: np.ascontiguousarray(np.zeros(abi.NUMA_WORDS, np.uint64) if x is None else x, np.uint64)
+    av, ep, en = m(avail), m(excl_pcpu), m(excl_numa)
+    out = np.zeros(abi.NUMA_WORDS, np.uint64)
+    ok = lib().orc_take_cpus(cls.ctypes.data, av.ctypes.data, ep.ctypes.data, en.ctypes.data, need, bind_policy,
+                             excl_policy, int(most_allocated), out.ctypes.data)
+    return out if ok else None
+
+
+def spread_order(cls: np.ndarray, avail, most_allocated: bool = True):
+    cls = np.ascontiguousarray(cls, dtype=abi.NUMA_CLASS_DTYPE)
+    av = np.ascontiguousarray(avail, np.uint64)
+    ids = np.zeros(abi.NUMA_MAX_CPUS, np.int32)
+    n = lib().orc_spread_order(cls.ctypes.data, av.ctypes.data, int(most_allocated), ids.ctypes.data)
+    return ids[:n].tolist()
 
 
 def usage_percent(used_milli: int, total_milli: int) -> int:

@@ -118,7 +118,14 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
   st->la_used_mem = dup64(soa->la_used_mem, n);
   st->la_used_prod_cpu_m = dup64(soa->la_used_prod_cpu_m, n);
   st->la_used_prod_mem = dup64(soa->la_used_prod_mem, n);
-  if (!st->flags || !st->npods) return -1;
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    st->numa_free[w] = (uint64_t *)dup64(soa->numa_class ? (const int64_t *)soa->numa_free[w] : NULL, n);
+    st->numa_excl_pcpu[w] = (uint64_t *)dup64(soa->numa_class ? (const int64_t *)soa->numa_excl_pcpu[w] : NULL, n);
+    st->numa_excl_numa[w] = (uint64_t *)dup64(soa->numa_class ? (const int64_t *)soa->numa_excl_numa[w] : NULL, n);
+  }
+  st->numa_alloc_cnt = (int32_t *)calloc((size_t)(n > 0 ? n : 1), sizeof(int32_t));
+  if (soa->numa_class && soa->numa_alloc_cnt) memcpy(st->numa_alloc_cnt, soa->numa_alloc_cnt, sizeof(int32_t) * (size_t)n);
+  if (!st->flags || !st->npods || !st->numa_alloc_cnt) return -1;
   orc_la_flags(soa, n, st->flags);
   return 0;
 }
@@ -133,6 +140,12 @@ void orc_state_free(orc_state *st) {
   free(st->la_used_mem);
   free(st->la_used_prod_cpu_m);
   free(st->la_used_prod_mem);
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    free(st->numa_free[w]);
+    free(st->numa_excl_pcpu[w]);
+    free(st->numa_excl_numa[w]);
+  }
+  free(st->numa_alloc_cnt);
   memset(st, 0, sizeof(*st));
 }
 
@@ -223,6 +236,7 @@ int64_t orc_la_score(const koordhip_config *cfg, const orc_state *st, const koor
 static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) return 0;
   return 1;
 }
 
@@ -230,6 +244,7 @@ static int64_t orc_total(const koordhip_config *cfg, const orc_state *st, const 
   int64_t t = 0;
   if (cfg->score_plugins & KOORDHIP_PLUGIN_FIT) t += cfg->plugin_weight[0] * orc_fit_score(cfg, st, pod, i);
   if (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) t += cfg->plugin_weight[1] * orc_la_score(cfg, st, pod, i);
+  if (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) t += cfg->plugin_weight[2] * orc_numa_score(cfg, st, pod, i);
   return t;
 }
 
@@ -253,10 +268,12 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
     for (int32_t i = 0; i < n; i++) {
       int fit_ok = orc_fit_filter(cfg, st, pod, i);
       int la_ok = orc_la_filter(cfg, st, pod, i);
+      int numa_ok = (cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) ? orc_numa_filter(cfg, st, pod, i) : 1;
       if (status) {
         uint8_t b = 0;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !fit_ok) b |= KOORDHIP_ST_FIT_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !la_ok) b |= KOORDHIP_ST_LA_FAIL;
+        if (!numa_ok) b |= KOORDHIP_ST_NUMA_FAIL;
         status[(size_t)p * n + i] = b;
       }
       if (scores) {
@@ -264,7 +281,8 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
         row[0 * (size_t)n + i] = (cfg->score_plugins & KOORDHIP_PLUGIN_FIT) ? (int32_t)orc_fit_score(cfg, st, pod, i) : 0;
         row[1 * (size_t)n + i] =
             (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) ? (int32_t)orc_la_score(cfg, st, pod, i) : 0;
-        row[2 * (size_t)n + i] = 0;
+        row[2 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) ? (int32_t)orc_numa_score(cfg, st, pod, i) : 0;
       }
       if (keys && orc_feasible(cfg, st, pod, i)) keys[nk++] = mkkey(orc_total(cfg, st, pod, i), i);
     }
@@ -289,8 +307,25 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
 /* Reserve: podAssignCache.assign (pod_assign_cache.go:53-68) makes the pod an
  * estimated assigned pod on the node (load_aware.go:353-372: no metric ->
  * EstimatePod); (upstream) NodeInfo.AddPod adds Requested/NonZeroRequested and
- * one pod (mirror: reservation/transformer.go:280-333).  sign = -1: Unreserve. */
-void orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t i, int sign) {
+ * one pod (mirror: reservation/transformer.go:280-333).  sign = -1: Unreserve.
+ * NodeNUMAResource Reserve allocates a cpuset for a cpuset pod (plugin.go:365-405);
+ * when it fails the framework unreserves every plugin: nothing is committed. */
+static int numa_reserve_active(const koordhip_config *cfg, const koordhip_pod *pod) {
+  return ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) && (pod->flags & KOORDHIP_POD_CPUSET) &&
+         !(pod->flags & KOORDHIP_POD_NUMA_SKIP);
+}
+
+int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t i, int sign,
+               uint64_t *cpus) {
+  if (numa_reserve_active(cfg, pod)) {
+    if (sign > 0) {
+      if (!orc_numa_reserve(st, pod, i, cpus)) return KOORDHIP_ERESERVE;
+    } else if (cpus) {
+      orc_numa_release(st, i, cpus);
+    }
+  } else if (cpus && sign > 0) {
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
+  }
   for (int r = 0; r < KOORDHIP_NRES; r++) st->requested[r][i] += sign * pod->req[r];
   st->nz_cpu_m[i] += sign * pod->nz_cpu_m;
   st->nz_mem[i] += sign * pod->nz_mem;
@@ -301,8 +336,10 @@ void orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *p
     st->la_used_prod_cpu_m[i] += sign * pod->est_cpu;
     st->la_used_prod_mem[i] += sign * pod->est_mem;
   }
-  (void)cfg;
+  return 0;
 }
+
+void orc_set_cpuset_out(orc_state *st, uint64_t *cpus) { st->cpuset_out = cpus; }
 
 /* ------------------------------------------------------------------------ */
 /* parallelize.Until (pkg/util/parallelize/parallelism.go:28-49)            */
@@ -405,7 +442,7 @@ typedef struct stream_ctx {
   const koordhip_pod *pod;
   _Atomic int32_t nfeasible;
   int32_t *feasible;      /* node ids (unordered, like upstream's atomic append) */
-  int64_t *plugin_scores; /* [2][nfeasible] */
+  int64_t *plugin_scores; /* [3][nfeasible] */
 } stream_ctx;
 
 /* (upstream) findNodesThatPassFilters checkNode: RunFilterPlugins, append on success. */
@@ -425,6 +462,8 @@ static void score_piece(void *a, int32_t lo, int32_t hi) {
         (c->cfg->score_plugins & KOORDHIP_PLUGIN_FIT) ? orc_fit_score(c->cfg, c->st, c->pod, i) : 0;
     c->plugin_scores[(size_t)nf + j] =
         (c->cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) ? orc_la_score(c->cfg, c->st, c->pod, i) : 0;
+    c->plugin_scores[2 * (size_t)nf + j] =
+        (c->cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) ? orc_numa_score(c->cfg, c->st, c->pod, i) : 0;
   }
 }
 
@@ -437,7 +476,7 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
   c.cfg = cfg;
   c.st = st;
   c.feasible = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
-  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(n > 0 ? n : 1));
+  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * 3 * (size_t)(n > 0 ? n : 1));
   for (int32_t p = 0; p < n_pods; p++) {
     c.pod = &pods[p];
     atomic_store(&c.nfeasible, 0);
@@ -445,6 +484,7 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
     int32_t nf = atomic_load(&c.nfeasible);
     if (nf == 0) {
       out_node[p] = KOORDHIP_UNSCHEDULABLE;
+      if (st->cpuset_out) memset(st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS, 0, 8 * KOORDHIP_NUMA_WORDS);
       continue;
     }
     pool_until(&pl, nf, score_piece, &c);
@@ -454,14 +494,16 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
     int32_t best_node = -1;
     for (int32_t j = 0; j < nf; j++) {
       int32_t i = c.feasible[j];
-      int64_t t = cfg->plugin_weight[0] * c.plugin_scores[j] + cfg->plugin_weight[1] * c.plugin_scores[(size_t)nf + j];
+      int64_t t = cfg->plugin_weight[0] * c.plugin_scores[j] + cfg->plugin_weight[1] * c.plugin_scores[(size_t)nf + j] +
+                  cfg->plugin_weight[2] * c.plugin_scores[2 * (size_t)nf + j];
       if (t > best || (t == best && i < best_node)) {
         best = t;
         best_node = i;
       }
     }
-    out_node[p] = best_node;
-    orc_commit(cfg, st, &pods[p], best_node, +1); /* Reserve + AssumePod */
+    uint64_t *cs = st->cpuset_out ? st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS : NULL;
+    /* Reserve (+ AssumePod); a failed Reserve leaves no state and is not retried */
+    out_node[p] = orc_commit(cfg, st, &pods[p], best_node, +1, cs) ? KOORDHIP_RESERVE_FAILED : best_node;
   }
   free(c.feasible);
   free(c.plugin_scores);

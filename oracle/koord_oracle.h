@@ -1,6 +1,6 @@
 /*
  * koord_oracle.h -- TEST INFRASTRUCTURE.  CPU restatement of koord-scheduler's
- * Filter/Score hot path (NodeResourcesFit, LoadAwareScheduling) used ONLY as the
+ * Filter/Score hot path (NodeResourcesFit, LoadAwareScheduling, NodeNUMAResource) used ONLY as the
  * checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
  * Nothing in the product (koordinator_amd/, libkoordhip.so) links or calls it.
  *
@@ -46,6 +46,12 @@ typedef struct orc_state {
   int32_t *npods;
   int64_t *la_used_cpu_m, *la_used_mem;
   int64_t *la_used_prod_cpu_m, *la_used_prod_mem;
+  /* NodeNUMAResource NodeAllocation (maxRefCount 1) */
+  uint64_t *numa_free[KOORDHIP_NUMA_WORDS];
+  uint64_t *numa_excl_pcpu[KOORDHIP_NUMA_WORDS];
+  uint64_t *numa_excl_numa[KOORDHIP_NUMA_WORDS];
+  int32_t *numa_alloc_cnt;
+  uint64_t *cpuset_out; /* optional [n_pods][WORDS] output of orc_place_stream */
 } orc_state;
 
 int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n);
@@ -57,12 +63,26 @@ int64_t orc_fit_score(const koordhip_config *cfg, const orc_state *st, const koo
 int orc_la_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 int64_t orc_la_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 
+/* NodeNUMAResource (numa_oracle.c). */
+int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
+int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
+int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
+int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
+void orc_numa_release(orc_state *st, int32_t node, const uint64_t *cpus);
+/* takeCPUs on one topology (cpu_accumulator.go:87-232), maxRefCount 1; 1 = ok. */
+int orc_take_cpus(const koordhip_numa_class *t, const uint64_t *avail, const uint64_t *excl_pcpu,
+                  const uint64_t *excl_numa, int need, int bind_policy, int excl_policy, int most_allocated,
+                  uint64_t *out);
+int orc_spread_order(const koordhip_numa_class *t, const uint64_t *avail, int most_allocated, int32_t *cpu_ids);
+
 /* Same contract as koordhip_eval (status / scores / topk all optional). */
 int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, int32_t n_pods,
              uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
 
-/* Reserve / Unreserve delta. */
-void orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t node, int sign);
+/* Reserve / Unreserve delta.  Reserve returns KOORDHIP_ERESERVE (nothing
+ * committed) when the NUMA Allocate fails; cpus: the cpuset given / taken back. */
+int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t node, int sign,
+               uint64_t *cpus);
 
 /* Greedy stream with the reference loop structure: per pod a parallel Filter
  * over all nodes, a parallel Score per plugin over the feasible nodes
@@ -70,6 +90,8 @@ void orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *p
  * serial lowest-index argmax, serial Reserve.  threads <= 1 runs serially. */
 int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods, int32_t n_pods,
                      int32_t *out_node, int32_t threads);
+/* cpusets of the last orc_place_stream call are written here when non-NULL ([n_pods][WORDS]). */
+void orc_set_cpuset_out(orc_state *st, uint64_t *cpus);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,620 @@
+/*
+ * numa_oracle.c -- TEST INFRASTRUCTURE (see koord_oracle.h).  Plain-C
+ * restatement of NodeNUMAResource for NUMA topology policy None:
+ *   - the cpuAccumulator (pkg/scheduler/plugins/nodenumaresource/cpu_accumulator.go),
+ *     kept in the reference's own shape: per-call grouping of the allocatable
+ *     CPUs into per-core / per-NUMA-node / per-socket lists, the same sort
+ *     keys, the same passes;
+ *   - Allocate / allocateCPUSet / satisfiedRequiredCPUBindPolicy
+ *     (resource_manager.go:142-164,244-326,442-463);
+ *   - Filter / Score / Reserve (plugin.go:266-324,365-405, scoring.go:55-168).
+ * Go's sort.Slice is not stable; the only comparators without a final id
+ * tie-break are the two len-only socket sorts (cpu_accumulator.go:142-144,
+ * 161-163), which run on <= 8 elements where Go's pdqsort is an insertion sort,
+ * i.e. stable: every sort here is a stable insertion sort.
+ * Pinned by the known-answer tables of cpu_accumulator_test.go (tests/golden/).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "koord_oracle.h"
+
+#define MAXC KOORDHIP_NUMA_MAX_CPUS
+#define MAXG 16
+
+typedef struct acc {
+  const koordhip_numa_class *t;
+  int ncpu, cpc, cpn, cps; /* CPUsPerCore / PerNode / PerSocket (cpu_topology.go:82-103) */
+  uint8_t allocatable[MAXC];
+  int need;
+  int excl_policy; /* pod's preferredCPUExclusivePolicy */
+  int exclusive;
+  uint8_t excl_core[MAXC];               /* exclusiveInCores, by core rank */
+  uint8_t excl_node[KOORDHIP_NUMA_MAX_NODES]; /* exclusiveInNUMANodes */
+  int most_allocated;
+  uint8_t result[MAXC];
+  int nresult;
+} acc;
+
+typedef struct list {
+  int n;
+  int16_t v[MAXC];
+} list;
+
+typedef struct groups {
+  int n;
+  int id[MAXG];
+  list l[MAXG];
+} groups;
+
+static int core_of(const acc *a, int p) { return p / a->cpc; }
+static int node_of(const acc *a, int p) { return a->t->node_of[p]; }
+static int sock_of(const acc *a, int p) { return a->t->socket_of[p]; }
+static int cpuid(const acc *a, int p) { return a->t->cpu_id[p]; }
+
+static int bit(const uint64_t *m, int p) { return (int)((m[p >> 6] >> (p & 63)) & 1u); }
+
+/* newCPUAccumulator, cpu_accumulator.go:247-288 (maxRefCount = 1). */
+static void acc_init(acc *a, const koordhip_numa_class *t, const uint64_t *avail, const uint64_t *excl_pcpu,
+                     const uint64_t *excl_numa, int need, int excl_policy, int most_allocated) {
+  memset(a, 0, sizeof(*a));
+  a->t = t;
+  a->ncpu = t->num_cpus;
+  a->cpc = t->num_cores ? t->num_cpus / t->num_cores : 0;
+  a->cpn = t->num_nodes ? t->num_cpus / t->num_nodes : 0;
+  a->cps = t->num_sockets ? t->num_cpus / t->num_sockets : 0;
+  for (int p = 0; p < a->ncpu; p++) {
+    a->allocatable[p] = (uint8_t)bit(avail, p);
+    if (excl_pcpu && bit(excl_pcpu, p)) a->excl_core[p / a->cpc] = 1; /* :258-261 */
+    if (excl_numa && bit(excl_numa, p)) a->excl_node[t->node_of[p]] = 1;
+  }
+  a->need = need;
+  a->excl_policy = excl_policy;
+  a->exclusive = excl_policy == KOORDHIP_CPUEXCL_PCPU || excl_policy == KOORDHIP_CPUEXCL_NUMA; /* :265-266 */
+  a->most_allocated = most_allocated;
+}
+
+/* take, :290-304 */
+static void acc_take(acc *a, const int16_t *cpus, int n) {
+  for (int i = 0; i < n; i++) {
+    int p = cpus[i];
+    if (!a->result[p]) a->nresult++;
+    a->result[p] = 1;
+    a->allocatable[p] = 0;
+    if (a->exclusive) {
+      if (a->excl_policy == KOORDHIP_CPUEXCL_PCPU) a->excl_core[core_of(a, p)] = 1;
+      else a->excl_node[node_of(a, p)] = 1;
+    }
+  }
+  a->need -= n;
+}
+static int acc_needs(const acc *a, int n) { return a->need >= n; }
+static int acc_satisfied(const acc *a) { return a->need < 1; }
+static int acc_navail(const acc *a) {
+  int c = 0;
+  for (int p = 0; p < a->ncpu; p++) c += a->allocatable[p];
+  return c;
+}
+static int acc_failed(const acc *a) { return a->need > acc_navail(a); }
+
+static int excl_pcpu_level(const acc *a, int p) {
+  return a->excl_policy == KOORDHIP_CPUEXCL_PCPU && a->excl_core[core_of(a, p)]; /* :318-323 */
+}
+static int excl_numa_level(const acc *a, int p) {
+  return a->excl_policy == KOORDHIP_CPUEXCL_NUMA && a->excl_node[node_of(a, p)]; /* :325-330 */
+}
+
+/* sort.Ints on positions by CPU id (insertion sort) */
+static void sort_by_cpuid(const acc *a, int16_t *v, int n) {
+  for (int i = 1; i < n; i++) {
+    int16_t x = v[i];
+    int j = i - 1;
+    while (j >= 0 && cpuid(a, v[j]) > cpuid(a, x)) {
+      v[j + 1] = v[j];
+      j--;
+    }
+    v[j + 1] = x;
+  }
+}
+
+/* extractCPU, :332-343: first CPU of each core, in list order */
+static void extract_cpu(const acc *a, list *l) {
+  uint8_t seen[MAXC];
+  memset(seen, 0, sizeof(seen));
+  int m = 0;
+  for (int i = 0; i < l->n; i++) {
+    int c = core_of(a, l->v[i]);
+    if (!seen[c]) {
+      seen[c] = 1;
+      l->v[m++] = l->v[i];
+    }
+  }
+  l->n = m;
+}
+
+/* spreadCPUs, :798-822 */
+static void spread_cpus(const acc *a, list *l) {
+  if (l->n <= a->cpc) return;
+  list prep = *l, keep;
+  l->n = 0;
+  while (prep.n > 0) {
+    uint8_t seen[MAXC];
+    memset(seen, 0, sizeof(seen));
+    keep.n = 0;
+    for (int i = 0; i < prep.n; i++) {
+      int c = core_of(a, prep.v[i]);
+      if (seen[c]) {
+        keep.v[keep.n++] = prep.v[i];
+        continue;
+      }
+      l->v[l->n++] = prep.v[i];
+      seen[c] = 1;
+    }
+    prep = keep;
+  }
+}
+
+/* strategy comparison of free scores: MostAllocated -> ascending (:434-438) */
+static int free_before(const acc *a, int x, int y) { return a->most_allocated ? x < y : x > y; }
+
+/* Per-core allowed CPUs (ascending CPU id) for a predicate. */
+typedef int (*allow_fn)(const acc *a, int p);
+
+/* freeCoresInNode (by_socket = 0, :371-461) / freeCoresInSocket (by_socket = 1, :464-527) */
+static void free_cores(const acc *a, int by_socket, int filter_full, int filter_excl, groups *out) {
+  int core_cnt[MAXC];
+  int socket_free[KOORDHIP_NUMA_MAX_NODES];
+  memset(core_cnt, 0, sizeof(core_cnt));
+  memset(socket_free, 0, sizeof(socket_free));
+  for (int p = 0; p < a->ncpu; p++) {
+    if (!a->allocatable[p]) continue;
+    if (!by_socket && filter_excl && excl_numa_level(a, p)) continue;
+    core_cnt[core_of(a, p)]++;
+    socket_free[sock_of(a, p)]++;
+  }
+  const int ncores = a->ncpu / a->cpc;
+  /* group -> cores (ascending core id == sortCores order: all counts equal
+   * when filter_full; otherwise count desc then core id, :345-368) */
+  out->n = 0;
+  int gid_of[KOORDHIP_NUMA_MAX_NODES];
+  for (int g = 0; g < KOORDHIP_NUMA_MAX_NODES; g++) gid_of[g] = -1;
+  int core_list[KOORDHIP_NUMA_MAX_NODES][MAXC];
+  int ncl[KOORDHIP_NUMA_MAX_NODES];
+  memset(ncl, 0, sizeof(ncl));
+  for (int c = 0; c < ncores; c++) {
+    if (!core_cnt[c]) continue;
+    if (filter_full && core_cnt[c] != a->cpc) continue;
+    int first = c * a->cpc; /* any CPU of the core carries its node / socket */
+    int g = by_socket ? sock_of(a, first) : node_of(a, first);
+    core_list[g][ncl[g]++] = c;
+  }
+  for (int g = 0; g < KOORDHIP_NUMA_MAX_NODES; g++) {
+    if (!ncl[g]) continue;
+    /* sortCores: cpus count desc, core id asc (insertion) */
+    for (int i = 1; i < ncl[g]; i++) {
+      int x = core_list[g][i], j = i - 1;
+      while (j >= 0 && (core_cnt[core_list[g][j]] < core_cnt[x] ||
+                        (core_cnt[core_list[g][j]] == core_cnt[x] && core_list[g][j] > x))) {
+        core_list[g][j + 1] = core_list[g][j];
+        j--;
+      }
+      core_list[g][j + 1] = x;
+    }
+    list *l = &out->l[out->n];
+    l->n = 0;
+    for (int i = 0; i < ncl[g]; i++) {
+      int c = core_list[g][i];
+      int16_t tmp[8];
+      int nt = 0;
+      for (int t = 0; t < a->cpc; t++) {
+        int p = c * a->cpc + t;
+        if (a->allocatable[p] && !(!by_socket && filter_excl && excl_numa_level(a, p))) tmp[nt++] = (int16_t)p;
+      }
+      sort_by_cpuid(a, tmp, nt);
+      for (int t = 0; t < nt; t++) l->v[l->n++] = tmp[t];
+    }
+    out->id[out->n] = g;
+    gid_of[g] = out->n;
+    out->n++;
+  }
+  /* order groups */
+  for (int i = 1; i < out->n; i++) {
+    int j = i;
+    while (j > 0) {
+      int x = j, y = j - 1; /* is x before y? */
+      int lx = out->l[x].n, ly = out->l[y].n, before;
+      if (lx != ly) {
+        before = free_before(a, lx, ly);
+      } else if (!by_socket) {
+        int sx = socket_free[sock_of(a, out->l[x].v[0])], sy = socket_free[sock_of(a, out->l[y].v[0])];
+        before = sx != sy ? free_before(a, sx, sy) : out->id[x] < out->id[y];
+      } else {
+        before = out->id[x] < out->id[y];
+      }
+      if (!before) break;
+      int tid = out->id[x];
+      out->id[x] = out->id[y];
+      out->id[y] = tid;
+      list tl = out->l[x];
+      out->l[x] = out->l[y];
+      out->l[y] = tl;
+      j--;
+    }
+  }
+  (void)gid_of;
+}
+
+/* freeCPUsInNode (by_socket = 0, :530-605) / freeCPUsInSocket (by_socket = 1, :608-656) */
+static void free_cpus_in(const acc *a, int by_socket, int filter_excl, groups *out) {
+  int gfree[KOORDHIP_NUMA_MAX_NODES], socket_free[KOORDHIP_NUMA_MAX_NODES];
+  memset(gfree, 0, sizeof(gfree));
+  memset(socket_free, 0, sizeof(socket_free));
+  list lists[KOORDHIP_NUMA_MAX_NODES];
+  for (int g = 0; g < KOORDHIP_NUMA_MAX_NODES; g++) lists[g].n = 0;
+  for (int p = 0; p < a->ncpu; p++) {
+    if (!a->allocatable[p]) continue;
+    if (filter_excl) {
+      if (excl_pcpu_level(a, p)) continue;
+      if (!by_socket && excl_numa_level(a, p)) continue;
+    }
+    int g = by_socket ? sock_of(a, p) : node_of(a, p);
+    lists[g].v[lists[g].n++] = (int16_t)p;
+    gfree[g]++;
+    socket_free[sock_of(a, p)]++;
+  }
+  out->n = 0;
+  for (int g = 0; g < KOORDHIP_NUMA_MAX_NODES; g++) {
+    if (!lists[g].n) continue;
+    sort_by_cpuid(a, lists[g].v, lists[g].n);
+    if (filter_excl) extract_cpu(a, &lists[g]);
+    out->id[out->n] = g;
+    out->l[out->n] = lists[g];
+    out->n++;
+  }
+  for (int i = 1; i < out->n; i++) {
+    int j = i;
+    while (j > 0) {
+      int x = j, y = j - 1, before;
+      if (!by_socket) {
+        int gx = out->id[x], gy = out->id[y];
+        int sx = socket_free[sock_of(a, out->l[x].v[0])], sy = socket_free[sock_of(a, out->l[y].v[0])];
+        if (gfree[gx] != gfree[gy]) before = free_before(a, gfree[gx], gfree[gy]);
+        else if (sx != sy) before = free_before(a, sx, sy);
+        else before = gx < gy;
+      } else {
+        int lx = out->l[x].n, ly = out->l[y].n; /* len after extractCPU, :637-646 */
+        before = lx != ly ? free_before(a, lx, ly) : out->id[x] < out->id[y];
+      }
+      if (!before) break;
+      int tid = out->id[x];
+      out->id[x] = out->id[y];
+      out->id[y] = tid;
+      list tl = out->l[x];
+      out->l[x] = out->l[y];
+      out->l[y] = tl;
+      j--;
+    }
+  }
+}
+
+/* freeCPUs, :666-774 */
+static void free_cpus(const acc *a, int filter_excl, list *out) {
+  const int ncores = a->ncpu / a->cpc;
+  int core_cnt[MAXC], node_free[KOORDHIP_NUMA_MAX_NODES], socket_free[KOORDHIP_NUMA_MAX_NODES],
+      colo[KOORDHIP_NUMA_MAX_NODES];
+  memset(core_cnt, 0, sizeof(core_cnt));
+  memset(node_free, 0, sizeof(node_free));
+  memset(socket_free, 0, sizeof(socket_free));
+  memset(colo, 0, sizeof(colo));
+  uint8_t allowed[MAXC];
+  for (int p = 0; p < a->ncpu; p++) {
+    allowed[p] = a->allocatable[p] && !(filter_excl && (excl_pcpu_level(a, p) || excl_numa_level(a, p)));
+    if (!allowed[p]) continue;
+    core_cnt[core_of(a, p)]++;
+    node_free[node_of(a, p)]++;
+    socket_free[sock_of(a, p)]++;
+  }
+  /* socketColoScores: CPUs of the result on each socket (:690-694) */
+  for (int p = 0; p < a->ncpu; p++)
+    if (a->result[p]) colo[sock_of(a, p)]++;
+  int cores[MAXC], nc = 0;
+  for (int c = 0; c < ncores; c++)
+    if (core_cnt[c]) cores[nc++] = c;
+  for (int i = 1; i < nc; i++) {
+    int j = i;
+    while (j > 0) {
+      int x = cores[j], y = cores[j - 1], before;
+      int fx = x * a->cpc, fy = y * a->cpc;
+      int sx = sock_of(a, fx), sy = sock_of(a, fy);
+      int nx = node_of(a, fx), ny = node_of(a, fy);
+      if (colo[sx] != colo[sy]) before = colo[sx] > colo[sy];
+      else if (socket_free[sx] != socket_free[sy]) before = free_before(a, socket_free[sx], socket_free[sy]);
+      else if (node_free[nx] != node_free[ny]) before = free_before(a, node_free[nx], node_free[ny]);
+      else if (core_cnt[x] != core_cnt[y]) before = core_cnt[x] < core_cnt[y];
+      else if (sx != sy) before = sx < sy;
+      else before = x < y;
+      if (!before) break;
+      cores[j] = y;
+      cores[j - 1] = x;
+      j--;
+    }
+  }
+  out->n = 0;
+  for (int i = 0; i < nc; i++) {
+    int16_t tmp[8];
+    int nt = 0;
+    for (int t = 0; t < a->cpc; t++) {
+      int p = cores[i] * a->cpc + t;
+      if (allowed[p]) tmp[nt++] = (int16_t)p;
+    }
+    sort_by_cpuid(a, tmp, nt);
+    for (int t = 0; t < nt; t++) out->v[out->n++] = tmp[t];
+  }
+}
+
+/* stable sort of groups by list length (desc = 1 / asc = 0), :142-144 / :161-163 */
+static void sort_groups_len(groups *g, int desc) {
+  for (int i = 1; i < g->n; i++) {
+    int j = i;
+    while (j > 0) {
+      int lx = g->l[j].n, ly = g->l[j - 1].n;
+      int before = desc ? lx > ly : lx < ly;
+      if (!before) break;
+      list tl = g->l[j];
+      g->l[j] = g->l[j - 1];
+      g->l[j - 1] = tl;
+      int ti = g->id[j];
+      g->id[j] = g->id[j - 1];
+      g->id[j - 1] = ti;
+      j--;
+    }
+  }
+}
+
+/* takeCPUs, cpu_accumulator.go:87-232.  Returns 1 and fills a->result on success. */
+static int take_cpus(acc *a, int bind_policy) {
+  if (acc_satisfied(a)) return 1; /* :98-100 */
+  if (acc_failed(a)) return 0;    /* :101-103 */
+  groups g;
+  const int full = bind_policy == KOORDHIP_CPUBIND_FULL_PCPUS;
+  if (full || a->cpc == 1) {
+    if (a->need <= a->cpn) { /* :111-121 */
+      for (int fe = 1; fe >= 0; fe--) {
+        free_cores(a, 0, 1, fe, &g);
+        for (int i = 0; i < g.n; i++)
+          if (g.l[i].n >= a->need) {
+            acc_take(a, g.l[i].v, a->need);
+            return 1;
+          }
+      }
+    }
+    if (a->need <= a->cps) { /* :126-134 */
+      free_cores(a, 1, 1, 0, &g);
+      for (int i = 0; i < g.n; i++)
+        if (g.l[i].n >= a->need) {
+          acc_take(a, g.l[i].v, a->need);
+          return 1;
+        }
+    }
+    free_cores(a, 1, 1, 0, &g); /* :141-155 */
+    sort_groups_len(&g, 1);
+    groups uns;
+    uns.n = 0;
+    for (int i = 0; i < g.n; i++) {
+      if (!acc_needs(a, g.l[i].n)) {
+        uns.l[uns.n] = g.l[i];
+        uns.id[uns.n] = g.id[i];
+        uns.n++;
+      } else {
+        acc_take(a, g.l[i].v, g.l[i].n);
+        if (acc_satisfied(a)) return 1;
+      }
+    }
+    if (acc_needs(a, a->cpc)) { /* :159-176 */
+      sort_groups_len(&uns, 0);
+      for (int i = 0; i < uns.n; i++) {
+        for (int k = 0; k < uns.l[i].n; k += a->cpc) {
+          acc_take(a, uns.l[i].v + k, a->cpc);
+          if (acc_satisfied(a)) return 1;
+          if (!acc_needs(a, a->cpc)) break;
+        }
+      }
+    }
+  }
+  if (!full) {
+    if (a->need <= a->cpn) { /* :187-199 */
+      for (int fe = 1; fe >= 0; fe--) {
+        free_cpus_in(a, 0, fe, &g);
+        for (int i = 0; i < g.n; i++)
+          if (g.l[i].n >= a->need) {
+            spread_cpus(a, &g.l[i]);
+            acc_take(a, g.l[i].v, a->need);
+            return 1;
+          }
+      }
+    }
+    if (a->need <= a->cps) { /* :203-214 */
+      for (int fe = 1; fe >= 0; fe--) {
+        free_cpus_in(a, 1, fe, &g);
+        for (int i = 0; i < g.n; i++)
+          if (g.l[i].n >= a->need) {
+            spread_cpus(a, &g.l[i]);
+            acc_take(a, g.l[i].v, a->need);
+            return 1;
+          }
+      }
+    }
+  }
+  for (int fe = 1; fe >= 0; fe--) { /* :218-229 */
+    list l;
+    free_cpus(a, fe, &l);
+    spread_cpus(a, &l);
+    for (int i = 0; i < l.n; i++) {
+      if (acc_needs(a, 1)) acc_take(a, &l.v[i], 1);
+      if (acc_satisfied(a)) return 1;
+    }
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+
+int orc_take_cpus(const koordhip_numa_class *t, const uint64_t *avail, const uint64_t *excl_pcpu,
+                  const uint64_t *excl_numa, int need, int bind_policy, int excl_policy, int most_allocated,
+                  uint64_t *out) {
+  acc a;
+  acc_init(&a, t, avail, excl_pcpu, excl_numa, need, excl_policy, most_allocated);
+  int ok = take_cpus(&a, bind_policy);
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) out[w] = 0;
+  if (!ok) return 0;
+  for (int p = 0; p < a.ncpu; p++)
+    if (a.result[p]) out[p >> 6] |= 1ull << (p & 63);
+  return 1;
+}
+
+/* the spread order of freeCPUs(false) on a fresh accumulator (TestCPUSpreadByPCPUs) */
+int orc_spread_order(const koordhip_numa_class *t, const uint64_t *avail, int most_allocated, int32_t *cpu_ids) {
+  acc a;
+  acc_init(&a, t, avail, NULL, NULL, 0, KOORDHIP_CPUEXCL_NONE, most_allocated);
+  list l;
+  free_cpus(&a, 0, &l);
+  spread_cpus(&a, &l);
+  for (int i = 0; i < l.n; i++) cpu_ids[i] = cpuid(&a, l.v[i]);
+  return l.n;
+}
+
+static int popc(const uint64_t *m) {
+  int c = 0;
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) c += __builtin_popcountll(m[w]);
+  return c;
+}
+
+/* getPreferredCPUBindPolicy, plugin.go:546-566 */
+static int effective_bind_policy(uint8_t node_flags, int preferred) {
+  switch (node_flags & KOORDHIP_NODE_CPUBIND_MASK) {
+    case 1: return KOORDHIP_CPUBIND_FULL_PCPUS;       /* FullPCPUsOnly */
+    case 2: return KOORDHIP_CPUBIND_SPREAD_BY_PCPUS;  /* SpreadByPCPUs */
+    default: return preferred;
+  }
+}
+
+/* resourceManager.Allocate for a cpuset pod with an empty hint and no
+ * reservation (resource_manager.go:142-164, allocateCPUSet :244-326). */
+int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *out) {
+  const koordhip_node_soa *s = st->soa;
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) out[w] = 0;
+  int cls = s->numa_class[i];
+  if (cls < 0) return 0; /* GetAvailableCPUs: ErrNotFoundCPUTopology */
+  const koordhip_numa_class *t = &s->numa_classes[cls];
+  uint64_t avail[KOORDHIP_NUMA_WORDS], ep[KOORDHIP_NUMA_WORDS], en[KOORDHIP_NUMA_WORDS];
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    avail[w] = st->numa_free[w][i];
+    ep[w] = st->numa_excl_pcpu[w][i];
+    en[w] = st->numa_excl_numa[w][i];
+  }
+  const int need = pod->numa_cpus;
+  const int required = KOORDHIP_NUMA_REQUIRED(pod->numa_policy) != KOORDHIP_CPUBIND_NONE;
+  const int policy = effective_bind_policy(s->numa_flags[i], (int)KOORDHIP_NUMA_PREFERRED(pod->numa_policy));
+  /* filterAvailableCPUsByRequiredCPUBindPolicy (:430-440) returns a set equal
+   * to availableCPUs on both branches: no-op. */
+  if (popc(avail) < need) return 0; /* :257-259 */
+  if (!orc_take_cpus(t, avail, ep, en, need, policy, (int)KOORDHIP_NUMA_EXCLUSIVE(pod->numa_policy),
+                     (s->numa_flags[i] & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0, out))
+    return 0;
+  if (required) { /* satisfiedRequiredCPUBindPolicy :442-463 */
+    const int cpc = t->num_cpus / t->num_cores;
+    int cores = 0, n = popc(out);
+    for (int c = 0; c < t->num_cpus / cpc; c++) {
+      int any = 0;
+      for (int q = 0; q < cpc; q++) any |= bit(out, c * cpc + q);
+      cores += any;
+    }
+    if (policy == KOORDHIP_CPUBIND_FULL_PCPUS && cores * cpc != n) return 0;
+    if (policy == KOORDHIP_CPUBIND_SPREAD_BY_PCPUS && cores != n) return 0;
+  }
+  return 1;
+}
+
+/* Filter, plugin.go:266-324 (NUMA topology policy None; amplification ratio <= 1). */
+int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  (void)cfg;
+  const koordhip_node_soa *s = st->soa;
+  if (pod->flags & KOORDHIP_POD_NUMA_ERROR) return 0;            /* PreFilter error */
+  if ((pod->flags & KOORDHIP_POD_NUMA_SKIP) || !(pod->flags & KOORDHIP_POD_CPUSET)) return 1; /* skipTheNode :280-282 */
+  if (!s->numa_class || s->numa_class[i] < 0) return 0;          /* :285-294 */
+  const koordhip_numa_class *t = &s->numa_classes[s->numa_class[i]];
+  const int req = (int)KOORDHIP_NUMA_REQUIRED(pod->numa_policy);
+  const int pref = (int)KOORDHIP_NUMA_PREFERRED(pod->numa_policy);
+  const int node_full_only = (s->numa_flags[i] & KOORDHIP_NODE_CPUBIND_MASK) == 1;
+  if (node_full_only || req == KOORDHIP_CPUBIND_FULL_PCPUS) { /* :295-305 */
+    const int cpc = t->num_cpus / t->num_cores;
+    if (pod->numa_cpus % cpc != 0) return 0;
+    if (node_full_only && (req != KOORDHIP_CPUBIND_FULL_PCPUS || pref != KOORDHIP_CPUBIND_FULL_PCPUS)) return 0;
+  }
+  if (req != KOORDHIP_CPUBIND_NONE) { /* :307-316 */
+    uint64_t out[KOORDHIP_NUMA_WORDS];
+    if (!orc_numa_allocate(st, pod, i, out)) return 0;
+  }
+  return 1;
+}
+
+/* leastResourceScorer over {cpu, memory} (nodenumaresource/scoring.go:191-230,
+ * least_allocated.go:30-58): resources with allocatable 0 are left out. */
+static int64_t numa_least_allocated(const koordhip_config *cfg, int64_t req_cpu, int64_t alloc_cpu, int64_t req_mem,
+                                    int64_t alloc_mem) {
+  int64_t num = 0, wsum = 0;
+  if (cfg->numa_weight_cpu && alloc_cpu != 0) {
+    num += orc_least_requested(req_cpu, alloc_cpu) * cfg->numa_weight_cpu;
+    wsum += cfg->numa_weight_cpu;
+  }
+  if (cfg->numa_weight_mem && alloc_mem != 0) {
+    num += orc_least_requested(req_mem, alloc_mem) * cfg->numa_weight_mem;
+    wsum += cfg->numa_weight_mem;
+  }
+  return wsum ? num / wsum : 0;
+}
+
+/* Score, scoring.go:55-120,122-168. */
+int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  const koordhip_node_soa *s = st->soa;
+  if (pod->flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0; /* :70-72 */
+  const int has_topo = s->numa_class && s->numa_class[i] >= 0;
+  const int64_t acpu = s->alloc[KOORDHIP_RES_CPU][i], amem = s->alloc[KOORDHIP_RES_MEM][i];
+  if (!(pod->flags & KOORDHIP_POD_CPUSET)) {
+    if (!has_topo) return 0; /* scoreWithAmplifiedCPUs -> getResourceOptions error :97-100 */
+    return numa_least_allocated(cfg, st->requested[KOORDHIP_RES_CPU][i] + pod->req[KOORDHIP_RES_CPU], acpu,
+                                st->requested[KOORDHIP_RES_MEM][i] + pod->req[KOORDHIP_RES_MEM], amem); /* :104-106 */
+  }
+  if (!has_topo) return 0; /* :76-78 */
+  uint64_t out[KOORDHIP_NUMA_WORDS];
+  if (!orc_numa_allocate(st, pod, i, out)) return 0; /* :86-89 */
+  /* calculateAllocatableAndRequested: requested cpu := allocated cpuset size (:161-166) */
+  return numa_least_allocated(cfg, (int64_t)st->numa_alloc_cnt[i] * 1000 + pod->req[KOORDHIP_RES_CPU], acpu,
+                              st->requested[KOORDHIP_RES_MEM][i] + pod->req[KOORDHIP_RES_MEM], amem);
+}
+
+/* Reserve (plugin.go:365-405) + resourceManager.Update (resource_manager.go:328-339,
+ * node_allocation.go:76-103) for a cpuset pod; returns 0 when Allocate fails. */
+int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *cpus_out) {
+  uint64_t out[KOORDHIP_NUMA_WORDS];
+  if (!orc_numa_allocate(st, pod, i, out)) return 0;
+  const int ex = (int)KOORDHIP_NUMA_EXCLUSIVE(pod->numa_policy);
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    st->numa_free[w][i] &= ~out[w];
+    if (ex == KOORDHIP_CPUEXCL_PCPU) st->numa_excl_pcpu[w][i] |= out[w];
+    if (ex == KOORDHIP_CPUEXCL_NUMA) st->numa_excl_numa[w][i] |= out[w];
+    if (cpus_out) cpus_out[w] = out[w];
+  }
+  st->numa_alloc_cnt[i] += popc(out);
+  return 1;
+}
+
+/* Unreserve -> resourceManager.Release (node_allocation.go:105-131). */
+void orc_numa_release(orc_state *st, int32_t i, const uint64_t *cpus) {
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    st->numa_free[w][i] |= cpus[w];
+    st->numa_excl_pcpu[w][i] &= ~cpus[w];
+    st->numa_excl_numa[w][i] &= ~cpus[w];
+  }
+  st->numa_alloc_cnt[i] -= popc(cpus);
+}

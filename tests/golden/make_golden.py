@@ -206,6 +206,106 @@ for c in estimate_node_cases:
     c["source"] = f"{EST_TEST}:{c.pop('line')}"
 
 
+# --------------------------------------------------------------- cpu_accumulator_test.go
+ACC_TEST = "pkg/scheduler/plugins/nodenumaresource/cpu_accumulator_test.go"
+
+
+def acc(name, line, topo, need, want, allocated="", policy="FullPCPUs", excl="None", strategy="MostAllocated",
+        allocated_excl="", error=False):
+    """One takeCPUs call: topology = buildCPUTopologyForTest(sockets, nodesPerSocket, coresPerNode, cpusPerCore),
+    available = all - allocated, allocatedCPUs = KeepOnly(allocated) with ExclusivePolicy allocated_excl."""
+    return dict(name=name, source=f"{ACC_TEST}:{line}", topology=topo, allocated=allocated, need=need,
+                bind_policy=policy, exclusive_policy=excl, strategy=strategy, allocated_exclusive_policy=allocated_excl,
+                want=want, want_error=error)
+
+
+_full_most = [  # TestTakeFullPCPUs, :59-173 (NUMAMostAllocated)
+    ("allocate on non-NUMA node", 70, [1, 1, 4, 2], "", 2, "0-1"),
+    ("with allocated cpus", 77, [1, 1, 4, 2], "0-1", 2, "2-3"),
+    ("allocate whole socket", 85, [2, 1, 4, 2], "", 8, "0-7"),
+    ("allocate across socket", 92, [2, 1, 4, 2], "", 12, "0-11"),
+    ("allocate whole socket with partially-allocated socket", 99, [2, 1, 4, 2], "0-1", 8, "8-15"),
+    ("allocate in the smallest idle socket", 107, [2, 2, 4, 2], "0-5,16-23", 6, "24-29"),
+    ("allocate the most of CPUs on the same socket", 115, [2, 2, 4, 2], "0-5,16-23", 12, "6-15,24-25"),
+    ("allocate from first socket", 123, [2, 2, 4, 2], "0-3,8-11", 4, "4-7"),
+    ("allocate with less spread cpus", 131, [2, 2, 2, 2], "0,2,4,8,12", 4, "10-11,14-15"),
+    ("allocate with the most spread cpus", 139, [2, 2, 2, 2], "0,2,4,8,10,12", 6, "5-7,13-15"),
+    ("allocate with the most spread cpus on the smallest idle cpus socket", 147, [2, 2, 2, 2], "0,2,4,8-10,12", 6,
+     "6-7,11,13-15"),
+]
+_full_least = [  # TestTakeFullPCPUsWithNUMALeastAllocated, :175-289
+    ("allocate on non-NUMA node", 186, [1, 1, 4, 2], "", 2, "0-1"),
+    ("with allocated cpus", 193, [1, 1, 4, 2], "0-1", 2, "2-3"),
+    ("allocate whole socket", 201, [2, 1, 4, 2], "", 8, "0-7"),
+    ("allocate across socket", 208, [2, 1, 4, 2], "", 12, "0-11"),
+    ("allocate whole socket with partially-allocated socket", 215, [2, 1, 4, 2], "0-1", 8, "8-15"),
+    ("allocate in the most idle socket", 223, [2, 2, 4, 2], "0-5,16-23", 6, "8-13"),
+    ("allocate the most of CPUs on the same socket", 231, [2, 2, 4, 2], "0-5,16-23", 12, "6-15,24-25"),
+    ("allocate from second socket", 239, [2, 2, 4, 2], "0-3,8-11", 4, "16-19"),
+    ("allocate with less spread cpus", 247, [2, 2, 2, 2], "0,2,4,8,12", 4, "10-11,14-15"),
+    ("allocate with the less spread cpus 2", 255, [2, 2, 2, 2], "0,2,4,8,10,12", 6, "1,3,6-7,14-15"),
+    ("allocate with the most spread cpus on the most idle cpus socket 3", 263, [2, 2, 4, 2], "0,2,4,8-10,12", 6,
+     "16-21"),
+]
+_spread_most = [  # TestTakeSpreadByPCPUs, :301-361
+    ("allocate on non-NUMA node", 312, [1, 1, 4, 2], "", 4, "0,2,4,6"),
+    ("allocate satisfied the partially-allocated socket", 319, [2, 1, 4, 2], "0,2", 4, "1,3,4,6"),
+    ("allocate cpus on full-free socket", 327, [2, 1, 4, 2], "0-3", 4, "8,10,12,14"),
+    ("allocate most of CPUs in the same socket and overlapped-cores", 335, [2, 1, 4, 2], "0,2", 6, "1,3-7"),
+]
+_spread_least = [  # TestTakeSpreadByPCPUsWithNUMALeastAllocated, :373-433
+    ("allocate on non-NUMA node", 384, [1, 1, 4, 2], "", 4, "0,2,4,6"),
+    ("allocate satisfied the partially-allocated socket", 391, [2, 1, 4, 2], "0,2", 4, "8,10,12,14"),
+    ("allocate cpus on full-free socket", 399, [2, 1, 4, 2], "0-3", 4, "8,10,12,14"),
+    ("allocate most of CPUs in the same socket and overlapped-cores", 407, [2, 1, 4, 2], "0,2", 6,
+     "8-12,14"),
+]
+acc_cases = []
+for n, l, t, a, k, w in _full_most:
+    acc_cases.append(acc("FullPCPUs/" + n, l, t, k, w, allocated=a))
+for n, l, t, a, k, w in _full_least:
+    acc_cases.append(acc("FullPCPUs-least/" + n, l, t, k, w, allocated=a, strategy="LeastAllocated"))
+for n, l, t, a, k, w in _spread_most:
+    acc_cases.append(acc("Spread/" + n, l, t, k, w, allocated=a, policy="SpreadByPCPUs"))
+for n, l, t, a, k, w in _spread_least:
+    acc_cases.append(acc("Spread-least/" + n, l, t, k, w, allocated=a, policy="SpreadByPCPUs",
+                         strategy="LeastAllocated"))
+# TestTakeCPUsWithExclusivePolicy, :435-558: allocated CPUs carry PCPULevel unless stated, the pod's
+# exclusive policy defaults to PCPULevel and its bind policy to SpreadByPCPUs (:531-540)
+_excl = [
+    ("allocate cpus on full-free socket with PCPULevel", 448, [2, 1, 4, 2], "0,2", "", "PCPULevel", "SpreadByPCPUs",
+     4, "8,10,12,14"),
+    ("allocate overlapped cpus with PCPULevel", 455, [2, 1, 4, 2], "", "", "PCPULevel", "SpreadByPCPUs", 10,
+     "0-4,6,8,10,12,14"),
+    ("allocate cpus on large-size partially-allocated socket with PCPULevel", 461, [2, 1, 8, 2], "0,2", "",
+     "PCPULevel", "SpreadByPCPUs", 4, "4,6,8,10"),
+    ("allocate cpus with none exclusive policy", 468, [2, 1, 8, 2], "0,2", "", "None", "SpreadByPCPUs", 4, "1,3,4,6"),
+    ("allocate cpus on full-free socket with NUMANodeLevel", 476, [2, 1, 4, 2], "0,2", "NUMANodeLevel",
+     "NUMANodeLevel", "SpreadByPCPUs", 4, "8,10,12,14"),
+    ("allocate cpus on partially-allocated socket without NUMANodeLevel", 485, [2, 1, 4, 2], "0,2", "NUMANodeLevel",
+     "None", "SpreadByPCPUs", 4, "1,3,4,6"),
+    ("allocate cpus on full-free socket with NUMANodeLevel with PCPUs", 494, [2, 1, 4, 2], "0,2", "NUMANodeLevel",
+     "NUMANodeLevel", "FullPCPUs", 4, "8-11"),
+    ("allocate cpus on partially-allocated socket without NUMANodeLevel with PCPUs", 504, [2, 1, 4, 2], "0,2",
+     "NUMANodeLevel", "None", "FullPCPUs", 4, "4-7"),
+]
+for n, l, t, a, ae, ex, pol, k, w in _excl:
+    acc_cases.append(acc("Exclusive/" + n, l, t, k, w, allocated=a, policy=pol, excl=ex,
+                         allocated_excl=ae or "PCPULevel"))
+# TestTakePreferredCPUs, :758-777, the two calls without preferred CPUs
+acc_cases.append(acc("Preferred/takeCPUs spread 2", 761, [2, 1, 16, 2], 2, "0,2", policy="SpreadByPCPUs"))
+acc_cases.append(acc("Preferred/empty preferred on the rest", 769, [2, 1, 16, 2], 2, "1,3", allocated="0,2",
+                     policy="SpreadByPCPUs"))
+_SPREAD_ORDER = [0, 2, 4, 6, 8, 10, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30,
+                 1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31]
+spread_order_cases = [
+    dict(name="TestCPUSpreadByPCPUs", source=f"{ACC_TEST}:291-299", topology=[2, 2, 4, 2], strategy="MostAllocated",
+         want=_SPREAD_ORDER),
+    dict(name="TestCPUSpreadByPCPUsWithNUMALeastAllocated", source=f"{ACC_TEST}:363-371", topology=[2, 2, 4, 2],
+         strategy="LeastAllocated", want=_SPREAD_ORDER),
+]
+
+
 def dump(name, obj):
     with open(os.path.join(HERE, name), "w") as f:
         json.dump(obj, f, indent=1, sort_keys=True)
@@ -219,4 +319,9 @@ if __name__ == "__main__":
                                    "harness": f"{LA_TEST}:804-910, :200-258"})
     dump("estimator.json", {"estimate_pod": estimate_cases, "estimate_node": estimate_node_cases,
                             "harness": f"{EST_TEST}:233-250, :314-329"})
+    dump("cpu_accumulator.json", {"take_cpus": acc_cases, "spread_order": spread_order_cases,
+                                  "harness": f"{ACC_TEST}:156-171 (takeCPUs, maxRefCount 1)",
+                                  "not_transcribed": "TestTakeCPUsWithMaxRefCount / TestTakeCPUsSortByRefCount "
+                                                     "(maxRefCount 2) and the preferred-CPU calls of "
+                                                     "TestTakePreferredCPUs (Reservation): out of the engine's scope"})
     print("wrote golden fixtures")
