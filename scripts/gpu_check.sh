@@ -14,7 +14,7 @@ run() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
   return $rc
 }
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench 600 python bench.py --steps ${BENCH_STEPS:-2} --warmup 1 --cpu-budget ${CPU_BUDGET:-8}
 exit 0
