@@ -96,7 +96,7 @@ struct koordhip_ctx {
   kh::PrepIn prep{};
 
   // stream buffers
-  koordhip_pod *d_pods = nullptr;
+  kh::DevPod *d_pods = nullptr;
   int32_t pods_cap = 0, n_staged = 0;
   int32_t *d_out = nullptr;
   uint64_t *d_cpus = nullptr;  // [pods_cap][KOORDHIP_NUMA_WORDS] cpusets of the last place call (NUMA)
@@ -111,7 +111,7 @@ struct koordhip_ctx {
   uint64_t *d_gather = nullptr;  // [world][batch][k]
   int32_t gather_world = 1;
   uint64_t *d_final = nullptr;   // [batch][k]
-  koordhip_pod *d_tmp_pod = nullptr;
+  kh::DevPod *d_tmp_pod = nullptr;
   uint64_t *d_dbg = nullptr;  // KOORDHIP_STAMPS diagnostic counters (resolve segments)
 
   // checkpoint of the mutable columns
@@ -162,6 +162,60 @@ int upload(koordhip_ctx *c, T *dst, const T *src, size_t count) {
   return 0;
 }
 
+// Resource quantities live on device as exact f64 (eval.hpp): |v| < 2^45.
+constexpr int64_t kExact = 1ll << 45;
+
+bool exact_ok(int64_t v) { return v < kExact && v > -kExact; }
+
+// int64 quantity column -> f64 device column (NULL src -> zeros)
+int upload_q(koordhip_ctx *c, double *dst, const int64_t *src, size_t count, const char *what) {
+  if (count == 0) return 0;
+  if (!src) {
+    HIP_TRY(hipMemsetAsync(dst, 0, count * sizeof(double), c->stream));
+    return 0;
+  }
+  std::vector<double> tmp(count);
+  for (size_t i = 0; i < count; i++) {
+    if (!exact_ok(src[i]))
+      return fail(KOORDHIP_EINVAL, std::string(what) + ": quantity magnitude >= 2^45 is outside the engine's exact range");
+    tmp[i] = (double)src[i];
+  }
+  HIP_TRY(hipMemcpyAsync(dst, tmp.data(), count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// f64 device column -> int64 host array
+int download_q(double *src, int64_t *dst, size_t count) {
+  if (count == 0) return 0;
+  std::vector<double> tmp(count);
+  HIP_TRY(hipMemcpy(tmp.data(), src, count * sizeof(double), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < count; i++) dst[i] = (int64_t)tmp[i];
+  return 0;
+}
+
+// koordhip_pod (ABI) -> DevPod (device record)
+int to_dev_pods(const koordhip_pod *src, int32_t n, std::vector<kh::DevPod> &out) {
+  out.resize(std::max(n, 0));
+  for (int32_t j = 0; j < n; j++) {
+    const koordhip_pod &p = src[j];
+    kh::DevPod &o = out[j];
+    std::memset(&o, 0, sizeof(o));
+    const int64_t q[] = {p.req[0], p.req[1], p.req[2], p.req[3], p.req[4], p.nz_cpu_m, p.nz_mem, p.est_cpu, p.est_mem};
+    for (int64_t v : q)
+      if (!exact_ok(v)) return fail(KOORDHIP_EINVAL, "pod quantity magnitude >= 2^45 is outside the engine's exact range");
+    for (int r = 0; r < KOORDHIP_NRES; r++) o.req[r] = (double)p.req[r];
+    o.nz_cpu_m = (double)p.nz_cpu_m;
+    o.nz_mem = (double)p.nz_mem;
+    o.est_cpu = (double)p.est_cpu;
+    o.est_mem = (double)p.est_mem;
+    o.flags = p.flags;
+    o.numa_cpus = p.numa_cpus;
+    o.numa_policy = p.numa_policy;
+  }
+  return 0;
+}
+
 int validate_soa(const koordhip_node_soa *s) {
   if (!s) return fail(KOORDHIP_EINVAL, "soa is NULL");
   for (int r = 0; r < KOORDHIP_NRES; r++)
@@ -191,7 +245,7 @@ int32_t nchunks_for(const koordhip_ctx *c, int32_t lo, int32_t hi) {
   return std::max<int32_t>(1, (hi - lo + w - 1) / w);
 }
 
-int topk_batch(koordhip_ctx *c, const koordhip_pod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
+int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
                uint64_t *out, bool timed) {
   const int32_t nchunks = nchunks_for(c, lo, hi);
   const size_t need = (size_t)np * nchunks * k * sizeof(uint64_t) + 1024;  // +1 KiB: merge DMA padding
@@ -387,7 +441,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->t0);
   if (e == hipSuccess) e = hipEventCreate(&c->t1);
-  if (e == hipSuccess) e = hipMalloc(&c->d_tmp_pod, sizeof(koordhip_pod));
+  if (e == hipSuccess) e = hipMalloc(&c->d_tmp_pod, sizeof(kh::DevPod));
   if (e == hipSuccess) e = hipMalloc(&c->d_rc, 64);  // int32 status + (at byte 8) the commit cpuset
   if (e != hipSuccess) {
     std::string m = std::string("device init: ") + hipGetErrorString(e);
@@ -434,17 +488,21 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   d.n = n;
   int e = 0;
   for (int r = 0; r < KOORDHIP_NRES && !e; r++) {
-    int64_t *a = nullptr, *q = nullptr;
+    double *a = nullptr, *q = nullptr;
     e = dev_alloc(c, &a, n);
     if (!e) e = dev_alloc(c, &q, n);
-    if (!e) e = upload(c, a, s->alloc[r], n);
-    if (!e) e = upload(c, q, s->requested[r], n);
+    if (!e) e = upload_q(c, a, s->alloc[r], n, "alloc");
+    if (!e) e = upload_q(c, q, s->requested[r], n, "requested");
     d.alloc[r] = a;
     d.requested[r] = q;
   }
   auto col64 = [&](int64_t **dst, const int64_t *src) {
     if (!e) e = dev_alloc(c, dst, n);
     if (!e) e = upload(c, *dst, src, n);
+  };
+  auto colq = [&](double **dst, const int64_t *src, const char *what) {
+    if (!e) e = dev_alloc(c, dst, n);
+    if (!e) e = upload_q(c, *dst, src, n, what);
   };
   int32_t *ap = nullptr, *np = nullptr;
   if (!e) e = dev_alloc(c, &ap, n);
@@ -453,17 +511,17 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   if (!e) e = upload(c, np, s->npods, n);
   d.alloc_pods = ap;
   d.npods = np;
-  col64(&d.nz_cpu, s->nz_cpu_m);
-  col64(&d.nz_mem, s->nz_mem);
-  int64_t *lac = nullptr, *lam = nullptr;
-  col64(&lac, s->la_alloc_cpu_m);
-  col64(&lam, s->la_alloc_mem);
+  colq(&d.nz_cpu, s->nz_cpu_m, "nz_cpu_m");
+  colq(&d.nz_mem, s->nz_mem, "nz_mem");
+  double *lac = nullptr, *lam = nullptr;
+  colq(&lac, s->la_alloc_cpu_m, "la_alloc_cpu_m");
+  colq(&lam, s->la_alloc_mem, "la_alloc_mem");
   d.la_alloc_cpu = lac;
   d.la_alloc_mem = lam;
-  col64(&d.la_used_cpu, s->la_used_cpu_m);
-  col64(&d.la_used_mem, s->la_used_mem);
-  col64(&d.la_used_prod_cpu, s->la_used_prod_cpu_m);  // NULL -> zeros
-  col64(&d.la_used_prod_mem, s->la_used_prod_mem);
+  colq(&d.la_used_cpu, s->la_used_cpu_m, "la_used_cpu_m");
+  colq(&d.la_used_mem, s->la_used_mem, "la_used_mem");
+  colq(&d.la_used_prod_cpu, s->la_used_prod_cpu_m, "la_used_prod_cpu_m");  // NULL -> zeros
+  colq(&d.la_used_prod_mem, s->la_used_prod_mem, "la_used_prod_mem");
   if (!e) e = dev_alloc(c, &d.flags, n);
   // LoadAware Filter inputs
   kh::PrepIn &pi = c->prep;
@@ -519,6 +577,13 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       e = fail(KOORDHIP_EDEVICE, "scatter");
     if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
   };
+  auto putq = [&](double *dst, const int64_t *src, const char *what) {
+    if (e) return;
+    e = upload_q(c, (double *)stage, src, m, what);
+    if (!e && kh::launch_scatter<int64_t>((int64_t *)dst, (const int64_t *)stage, d_idx, m, c->stream) != hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "scatter");
+    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
+  };
   auto put32 = [&](int32_t *dst, const int32_t *src) {
     if (e) return;
     e = upload(c, (int32_t *)stage, src, m);
@@ -537,19 +602,19 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   kh::DevNodes &d = c->d;
   kh::PrepIn &pi = c->prep;
   for (int r = 0; r < KOORDHIP_NRES; r++) {
-    put64(const_cast<int64_t *>(d.alloc[r]), rows->alloc[r]);
-    put64(d.requested[r], rows->requested[r]);
+    putq(const_cast<double *>(d.alloc[r]), rows->alloc[r], "alloc");
+    putq(d.requested[r], rows->requested[r], "requested");
   }
   put32(const_cast<int32_t *>(d.alloc_pods), rows->alloc_pods);
   put32(d.npods, rows->npods);
-  put64(d.nz_cpu, rows->nz_cpu_m);
-  put64(d.nz_mem, rows->nz_mem);
-  put64(const_cast<int64_t *>(d.la_alloc_cpu), rows->la_alloc_cpu_m);
-  put64(const_cast<int64_t *>(d.la_alloc_mem), rows->la_alloc_mem);
-  put64(d.la_used_cpu, rows->la_used_cpu_m);
-  put64(d.la_used_mem, rows->la_used_mem);
-  put64(d.la_used_prod_cpu, rows->la_used_prod_cpu_m);
-  put64(d.la_used_prod_mem, rows->la_used_prod_mem);
+  putq(d.nz_cpu, rows->nz_cpu_m, "nz_cpu_m");
+  putq(d.nz_mem, rows->nz_mem, "nz_mem");
+  putq(const_cast<double *>(d.la_alloc_cpu), rows->la_alloc_cpu_m, "la_alloc_cpu_m");
+  putq(const_cast<double *>(d.la_alloc_mem), rows->la_alloc_mem, "la_alloc_mem");
+  putq(d.la_used_cpu, rows->la_used_cpu_m, "la_used_cpu_m");
+  putq(d.la_used_mem, rows->la_used_mem, "la_used_mem");
+  putq(d.la_used_prod_cpu, rows->la_used_prod_cpu_m, "la_used_prod_cpu_m");
+  putq(d.la_used_prod_mem, rows->la_used_prod_mem, "la_used_prod_mem");
   for (int r = 0; r < 2; r++) {
     put64(const_cast<int64_t *>(pi.used_m[r]), rows->laf_used_m[r]);
     put64(const_cast<int64_t *>(pi.total_m[r]), rows->laf_total_m[r]);
@@ -593,22 +658,19 @@ int koordhip_read_nodes(koordhip_ctx *c, int64_t *requested, int64_t *nz, int32_
   HIP_TRY(hipStreamSynchronize(c->stream));
   const size_t n = c->n, b = n * sizeof(int64_t);
   if (n == 0) return 0;
+  (void)b;
+  int e = 0;
   if (requested)
-    for (int r = 0; r < KOORDHIP_NRES; r++) HIP_TRY(hipMemcpy(requested + r * n, c->d.requested[r], b, hipMemcpyDeviceToHost));
-  if (nz) {
-    HIP_TRY(hipMemcpy(nz, c->d.nz_cpu, b, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(nz + n, c->d.nz_mem, b, hipMemcpyDeviceToHost));
-  }
+    for (int r = 0; r < KOORDHIP_NRES && !e; r++) e = download_q(c->d.requested[r], requested + r * n, n);
+  if (nz && !e) e = download_q(c->d.nz_cpu, nz, n);
+  if (nz && !e) e = download_q(c->d.nz_mem, nz + n, n);
+  if (e) return e;
   if (npods) HIP_TRY(hipMemcpy(npods, c->d.npods, n * sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (la_used) {
-    HIP_TRY(hipMemcpy(la_used, c->d.la_used_cpu, b, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(la_used + n, c->d.la_used_mem, b, hipMemcpyDeviceToHost));
-  }
-  if (la_used_prod) {
-    HIP_TRY(hipMemcpy(la_used_prod, c->d.la_used_prod_cpu, b, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(la_used_prod + n, c->d.la_used_prod_mem, b, hipMemcpyDeviceToHost));
-  }
-  return 0;
+  if (la_used && !e) e = download_q(c->d.la_used_cpu, la_used, n);
+  if (la_used && !e) e = download_q(c->d.la_used_mem, la_used + n, n);
+  if (la_used_prod && !e) e = download_q(c->d.la_used_prod_cpu, la_used_prod, n);
+  if (la_used_prod && !e) e = download_q(c->d.la_used_prod_mem, la_used_prod + n, n);
+  return e;
 }
 
 int koordhip_read_numa(koordhip_ctx *c, uint64_t *free_mask, uint64_t *excl_pcpu, uint64_t *excl_numa,
@@ -641,7 +703,7 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
   const int32_t n = c->n;
   // parity mode works in slices of pods so the status/score buffers stay bounded
   const int32_t per = std::max<int32_t>(1, std::min<int32_t>(kMaxBatch, (int32_t)((256ll << 20) / (16ll * std::max(n, 1)))));
-  koordhip_pod *dp = nullptr;
+  kh::DevPod *dp = nullptr;
   uint8_t *dst = nullptr;
   int32_t *dsc = nullptr;
   uint64_t *dk = nullptr;
@@ -650,7 +712,9 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
     for (void *p : {(void *)dp, (void *)dst, (void *)dsc, (void *)dk})
       if (p) (void)hipFree(p);
   };
-  if (hipMalloc(&dp, (size_t)per * sizeof(koordhip_pod)) != hipSuccess ||
+  std::vector<kh::DevPod> hp;
+  if (int ce = to_dev_pods(pods, n_pods, hp)) return ce;
+  if (hipMalloc(&dp, (size_t)per * sizeof(kh::DevPod)) != hipSuccess ||
       (status && hipMalloc(&dst, (size_t)per * n) != hipSuccess) ||
       (scores && hipMalloc(&dsc, (size_t)per * KOORDHIP_NPLUGINS * n * sizeof(int32_t)) != hipSuccess) ||
       (topk && hipMalloc(&dk, (size_t)per * k * sizeof(uint64_t)) != hipSuccess)) {
@@ -660,7 +724,7 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
   std::vector<uint64_t> hk(topk ? (size_t)per * k : 0);
   for (int32_t p0 = 0; p0 < n_pods && !e; p0 += per) {
     const int32_t np = std::min(per, n_pods - p0);
-    if (hipMemcpyAsync(dp, pods + p0, np * sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    if (hipMemcpyAsync(dp, hp.data() + p0, np * sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
       e = fail(KOORDHIP_EDEVICE, "copy pods");
       break;
     }
@@ -700,6 +764,8 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
 int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
+  std::vector<kh::DevPod> hp;
+  if (int e = to_dev_pods(pods, n_pods, hp)) return e;
   HIP_TRY(hipSetDevice(c->device));
   if (n_pods > c->pods_cap) {
     if (c->d_pods) HIP_TRY(hipFree(c->d_pods));
@@ -709,12 +775,12 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
     c->d_out = nullptr;
     c->d_cpus = nullptr;
     // +16 records of padding: the resolve kernel DMA-copies pod records in 1 KiB pieces
-    HIP_TRY(hipMalloc(&c->d_pods, (size_t)(n_pods + 16) * sizeof(koordhip_pod)));
+    HIP_TRY(hipMalloc(&c->d_pods, (size_t)(n_pods + 16) * sizeof(kh::DevPod)));
     HIP_TRY(hipMalloc(&c->d_out, (size_t)n_pods * sizeof(int32_t)));
     if (c->numa) HIP_TRY(hipMalloc(&c->d_cpus, (size_t)std::max(n_pods, 1) * KOORDHIP_NUMA_WORDS * sizeof(uint64_t)));
     c->pods_cap = n_pods;
   }
-  if (n_pods) HIP_TRY(hipMemcpyAsync(c->d_pods, pods, (size_t)n_pods * sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream));
+  if (n_pods) HIP_TRY(hipMemcpyAsync(c->d_pods, hp.data(), (size_t)n_pods * sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->n_staged = n_pods;
   return 0;
@@ -809,7 +875,7 @@ int place_staged_impl(koordhip_ctx *c) {
   const int32_t total = c->n_staged;
   for (int32_t p0 = 0; p0 < total; p0 += P) {
     const int32_t np = std::min(P, total - p0);
-    const koordhip_pod *pods = c->d_pods + p0;
+    const kh::DevPod *pods = c->d_pods + p0;
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(c->d_lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
       if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
@@ -940,7 +1006,9 @@ static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, i
   if (sign < 0 && cpuset && !cpus_io) return fail(KOORDHIP_EINVAL, "Unreserve of a cpuset pod needs its cpus");
   HIP_TRY(hipSetDevice(c->device));
   uint64_t *d_cpus = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(c->d_rc) + sizeof(uint64_t));
-  HIP_TRY(hipMemcpyAsync(c->d_tmp_pod, pod, sizeof(koordhip_pod), hipMemcpyHostToDevice, c->stream));
+  std::vector<kh::DevPod> hp;
+  if (int e = to_dev_pods(pod, 1, hp)) return e;
+  HIP_TRY(hipMemcpyAsync(c->d_tmp_pod, hp.data(), sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
   if (sign < 0 && cpus_io)
     HIP_TRY(hipMemcpyAsync(d_cpus, cpus_io, KOORDHIP_NUMA_WORDS * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(kh::launch_commit(c->dc, c->d, c->d_tmp_pod, node, sign, d_cpus, c->d_rc, c->stream));

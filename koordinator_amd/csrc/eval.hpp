@@ -1,12 +1,17 @@
 // eval.hpp -- the per-(pod,node) Filter+Score arithmetic on CDNA4, shared by
 // every kernel of libkoordhip.so (stream top-k, resolve, parity eval).
 //
-// Exactness: all plugin arithmetic is int64 as in the reference; the only
-// divisions are quotients known to lie in [0, 101] (leastRequestedScore and the
-// weighted averages), computed as an f64 reciprocal estimate followed by an
-// exact int64 remainder fix-up, so the result equals Go's truncating int64
-// division bit for bit (see lrs_div below).  The LoadAware threshold mask uses
-// IEEE f64 division + round-half-away exactly like math.Round in
+// Exactness: the reference computes in int64.  On device every resource
+// quantity (node columns and pod records) is held as an f64 that IS that
+// integer: the host rejects magnitudes >= 2^45 (KH_EXACT_LIMIT), so sums,
+// differences, the x100 of leastRequestedScore and the division remainders
+// below are all integers < 2^53 and therefore exact in binary64.  The only
+// divisions are quotients in [0, 101] (leastRequestedScore, weighted
+// averages): a reciprocal estimate, then one exact remainder fix-up in each
+// direction, equals Go's truncating int64 division bit for bit (lrs,
+// div_weights).  f64 is native on CDNA4's VALU, where int64 multiply/convert
+// are multi-instruction sequences.  The LoadAware threshold mask uses IEEE
+// f64 division + round-half-away exactly like math.Round in
 // load_aware.go:214,248 (compiled with -ffp-contract=off).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -40,13 +45,13 @@ struct DevCfg {
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
 // advanced by the resolve kernel (Reserve delta) and by commit/uncommit.
 struct DevNodes {
-  const int64_t *alloc[KOORDHIP_NRES];
+  const double *alloc[KOORDHIP_NRES];
   const int32_t *alloc_pods;
-  int64_t *requested[KOORDHIP_NRES];
-  int64_t *nz_cpu, *nz_mem;
+  double *requested[KOORDHIP_NRES];
+  double *nz_cpu, *nz_mem;
   int32_t *npods;
-  const int64_t *la_alloc_cpu, *la_alloc_mem;
-  int64_t *la_used_cpu, *la_used_mem, *la_used_prod_cpu, *la_used_prod_mem;
+  const double *la_alloc_cpu, *la_alloc_mem;
+  double *la_used_cpu, *la_used_mem, *la_used_prod_cpu, *la_used_prod_mem;
   uint8_t *flags;
   int32_t n;
   DevNuma nu;  // NodeNUMAResource columns (unused unless the plugin is enabled)
@@ -54,10 +59,10 @@ struct DevNodes {
 
 // One node's values as the evaluation consumes them (registers or an LDS row).
 struct NV {
-  int64_t a[KOORDHIP_NRES];
-  int64_t r[KOORDHIP_NRES];
-  int64_t nz_cpu, nz_mem;
-  int64_t la_a_cpu, la_a_mem, la_u_cpu, la_u_mem, la_up_cpu, la_up_mem;
+  double a[KOORDHIP_NRES];
+  double r[KOORDHIP_NRES];
+  double nz_cpu, nz_mem;
+  double la_a_cpu, la_a_mem, la_u_cpu, la_u_mem, la_up_cpu, la_up_mem;
   int32_t a_pods, npods;
   uint32_t flags;
 };
@@ -71,23 +76,23 @@ struct Need {
 __device__ __forceinline__ bool numa_on(const DevCfg &c) {
   return ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
 }
-__device__ __forceinline__ bool is_cpuset(const koordhip_pod &p) {
+__device__ __forceinline__ bool is_cpuset(const DevPod &p) {
   return (p.flags & KOORDHIP_POD_CPUSET) && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
 }
 
-__device__ __forceinline__ Need pod_needs(const koordhip_pod &p, const DevCfg &c) {
+__device__ __forceinline__ Need pod_needs(const DevPod &p, const DevCfg &c) {
   Need n{};
   const bool ff = c.filt & KOORDHIP_PLUGIN_FIT;
   const bool fs = c.score & KOORDHIP_PLUGIN_FIT;
   const bool hr = p.flags & KOORDHIP_POD_HAS_REQ;
   n.pods = ff;
-  n.r_cpu = ff && hr && p.req[KOORDHIP_RES_CPU] != 0;
-  n.r_mem = ff && hr && p.req[KOORDHIP_RES_MEM] != 0;
-  n.eph = (ff && hr && p.req[KOORDHIP_RES_EPH] != 0) || (fs && c.fit_w[KOORDHIP_RES_EPH] != 0);
+  n.r_cpu = ff && hr && p.req[KOORDHIP_RES_CPU] != 0.0;
+  n.r_mem = ff && hr && p.req[KOORDHIP_RES_MEM] != 0.0;
+  n.eph = (ff && hr && p.req[KOORDHIP_RES_EPH] != 0.0) || (fs && c.fit_w[KOORDHIP_RES_EPH] != 0);
   n.bcpu = (ff && (p.flags & KOORDHIP_POD_REQ_BCPU)) ||
-           (fs && c.fit_w[KOORDHIP_RES_BCPU] != 0 && p.req[KOORDHIP_RES_BCPU] != 0);
+           (fs && c.fit_w[KOORDHIP_RES_BCPU] != 0 && p.req[KOORDHIP_RES_BCPU] != 0.0);
   n.bmem = (ff && (p.flags & KOORDHIP_POD_REQ_BMEM)) ||
-           (fs && c.fit_w[KOORDHIP_RES_BMEM] != 0 && p.req[KOORDHIP_RES_BMEM] != 0);
+           (fs && c.fit_w[KOORDHIP_RES_BMEM] != 0 && p.req[KOORDHIP_RES_BMEM] != 0.0);
   n.nz_cpu = fs && c.fit_w[KOORDHIP_RES_CPU] != 0;
   n.nz_mem = fs && c.fit_w[KOORDHIP_RES_MEM] != 0;
   n.la = c.score & KOORDHIP_PLUGIN_LOADAWARE;
@@ -178,51 +183,53 @@ __device__ __forceinline__ void load_node(NV &v, const DevNodes &d, int32_t i, c
   }
 }
 
-// floor(a / b) for 0 <= a/b < 2^20, b > 0: f64 reciprocal estimate (|err| << 1)
-// then one exact int64 correction step in each direction.
-__device__ __forceinline__ int32_t div_small(int64_t a, int64_t b) {
-  double qd = (double)a * __builtin_amdgcn_rcp((double)b);
-  int32_t q = (int32_t)qd;
-  int64_t r = a - (int64_t)q * b;
+// num / ws for the weighted averages (num <= 100 * sum of weights <= 50000,
+// ws <= 500): a shift when ws is a power of two (the shipped profile: 2 and
+// 4), else an f32 reciprocal estimate (error << 1) + one int32 fix-up.
+__device__ __forceinline__ int32_t div_weights(int32_t num, int32_t ws) {
+  if ((ws & (ws - 1)) == 0) return num >> __builtin_ctz((uint32_t)ws);
+  int32_t q = (int32_t)((float)num * __builtin_amdgcn_rcpf((float)ws));
+  const int32_t r = num - q * ws;
   q -= (r < 0);
-  q += (r >= b);
+  q += (r >= ws);
   return q;
 }
 
-// num / ws for the weighted averages: ws is a small weight sum, very often a
-// power of two (the shipped profile: 2 and 4), then a shift is exact.
-__device__ __forceinline__ int32_t div_weights(int64_t num, int64_t ws) {
-  if ((ws & (ws - 1)) == 0) return (int32_t)(num >> __builtin_ctzll((uint64_t)ws));
-  return div_small(num, ws);
-}
-
-// leastRequestedScore, load_aware.go:388-397 / least_allocated.go:49-58.
-__device__ __forceinline__ int32_t lrs(int64_t req, int64_t cap) {
-  if (cap == 0 || req > cap) return 0;
-  return div_small((cap - req) * 100, cap);
+// leastRequestedScore, load_aware.go:388-397 / least_allocated.go:49-58:
+// (cap - req) * 100 / cap in int64.  f = (cap - req) * 100 < 2^52 is exact, the
+// reciprocal estimate of f / cap <= 100 is within 1 of the quotient, and the
+// remainder f - q * cap (one fma, exact: an integer < 2^53) fixes it up.
+__device__ __forceinline__ int32_t lrs(double req, double cap) {
+  if (cap == 0.0 || req > cap) return 0;
+  const double f = (cap - req) * 100.0;
+  int32_t q = (int32_t)(f * __builtin_amdgcn_rcp(cap));
+  const double r = __builtin_fma(-(double)q, cap, f);
+  q -= (r < 0.0);
+  q += (r >= cap);
+  return q;
 }
 
 // Fit LeastAllocated score (upstream resource_allocation.go + least_allocated.go;
 // koord copy nodenumaresource/scoring.go:191-246).
-__device__ __forceinline__ int32_t fit_score(const koordhip_pod &p, const NV &v, const DevCfg &c) {
-  int64_t num = 0, ws = 0;
-  if (c.fit_w[KOORDHIP_RES_CPU] && v.a[KOORDHIP_RES_CPU] != 0) {
-    num += (int64_t)lrs(v.nz_cpu + p.nz_cpu_m, v.a[KOORDHIP_RES_CPU]) * c.fit_w[KOORDHIP_RES_CPU];
+__device__ __forceinline__ int32_t fit_score(const DevPod &p, const NV &v, const DevCfg &c) {
+  int32_t num = 0, ws = 0;
+  if (c.fit_w[KOORDHIP_RES_CPU] && v.a[KOORDHIP_RES_CPU] != 0.0) {
+    num += lrs(v.nz_cpu + p.nz_cpu_m, v.a[KOORDHIP_RES_CPU]) * c.fit_w[KOORDHIP_RES_CPU];
     ws += c.fit_w[KOORDHIP_RES_CPU];
   }
-  if (c.fit_w[KOORDHIP_RES_MEM] && v.a[KOORDHIP_RES_MEM] != 0) {
-    num += (int64_t)lrs(v.nz_mem + p.nz_mem, v.a[KOORDHIP_RES_MEM]) * c.fit_w[KOORDHIP_RES_MEM];
+  if (c.fit_w[KOORDHIP_RES_MEM] && v.a[KOORDHIP_RES_MEM] != 0.0) {
+    num += lrs(v.nz_mem + p.nz_mem, v.a[KOORDHIP_RES_MEM]) * c.fit_w[KOORDHIP_RES_MEM];
     ws += c.fit_w[KOORDHIP_RES_MEM];
   }
-  if (c.fit_w[KOORDHIP_RES_EPH] && v.a[KOORDHIP_RES_EPH] != 0) {
-    num += (int64_t)lrs(v.r[KOORDHIP_RES_EPH] + p.req[KOORDHIP_RES_EPH], v.a[KOORDHIP_RES_EPH]) *
+  if (c.fit_w[KOORDHIP_RES_EPH] && v.a[KOORDHIP_RES_EPH] != 0.0) {
+    num += lrs(v.r[KOORDHIP_RES_EPH] + p.req[KOORDHIP_RES_EPH], v.a[KOORDHIP_RES_EPH]) *
            c.fit_w[KOORDHIP_RES_EPH];
     ws += c.fit_w[KOORDHIP_RES_EPH];
   }
 #pragma unroll
   for (int r = KOORDHIP_RES_BCPU; r <= KOORDHIP_RES_BMEM; r++) {
-    if (c.fit_w[r] && p.req[r] != 0 && v.a[r] != 0) {
-      num += (int64_t)lrs(v.r[r] + p.req[r], v.a[r]) * c.fit_w[r];
+    if (c.fit_w[r] && p.req[r] != 0.0 && v.a[r] != 0.0) {
+      num += lrs(v.r[r] + p.req[r], v.a[r]) * c.fit_w[r];
       ws += c.fit_w[r];
     }
   }
@@ -233,20 +240,20 @@ __device__ __forceinline__ int32_t fit_score(const koordhip_pod &p, const NV &v,
 // fitsRequest (upstream fit.go; mirror reservation/plugin.go:445-494).  A zero
 // request on cpu/memory/ephemeral reduces to "Requested > Allocatable", kept
 // as the NF_OVER_* bits so such pods need not read those columns.
-__device__ __forceinline__ bool fit_filter(const koordhip_pod &p, const NV &v) {
-  if ((int64_t)v.npods + 1 > (int64_t)v.a_pods) return false;
+__device__ __forceinline__ bool fit_filter(const DevPod &p, const NV &v) {
+  if (v.npods + 1 > v.a_pods) return false;
   if (!(p.flags & KOORDHIP_POD_HAS_REQ)) return true;
-  if (p.req[KOORDHIP_RES_CPU] != 0) {
+  if (p.req[KOORDHIP_RES_CPU] != 0.0) {
     if (p.req[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU] - v.r[KOORDHIP_RES_CPU]) return false;
   } else if (v.flags & NF_OVER_CPU) {
     return false;
   }
-  if (p.req[KOORDHIP_RES_MEM] != 0) {
+  if (p.req[KOORDHIP_RES_MEM] != 0.0) {
     if (p.req[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM] - v.r[KOORDHIP_RES_MEM]) return false;
   } else if (v.flags & NF_OVER_MEM) {
     return false;
   }
-  if (p.req[KOORDHIP_RES_EPH] != 0) {
+  if (p.req[KOORDHIP_RES_EPH] != 0.0) {
     if (p.req[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH] - v.r[KOORDHIP_RES_EPH]) return false;
   } else if (v.flags & NF_OVER_EPH) {
     return false;
@@ -261,40 +268,40 @@ __device__ __forceinline__ bool fit_filter(const koordhip_pod &p, const NV &v) {
 }
 
 // LoadAware Filter (load_aware.go:123-171): static mask + DaemonSet bypass.
-__device__ __forceinline__ bool la_filter(const koordhip_pod &p, const NV &v) {
+__device__ __forceinline__ bool la_filter(const DevPod &p, const NV &v) {
   if (p.flags & KOORDHIP_POD_DAEMONSET) return true;
   return v.flags & ((p.flags & KOORDHIP_POD_PROD) ? NF_LA_OK_PROD : NF_LA_OK_NONPROD);
 }
 
 // LoadAware Score (load_aware.go:269-335, scorer :378-386).
-__device__ __forceinline__ int32_t la_score(const koordhip_pod &p, const NV &v, const DevCfg &c) {
+__device__ __forceinline__ int32_t la_score(const DevPod &p, const NV &v, const DevCfg &c) {
   if (v.flags & NF_LA_SCORE_ZERO) return 0;
   const bool prod = c.according && (p.flags & KOORDHIP_POD_PROD);
-  const int64_t ucpu = p.est_cpu + (prod ? v.la_up_cpu : v.la_u_cpu);
-  const int64_t umem = p.est_mem + (prod ? v.la_up_mem : v.la_u_mem);
-  const int64_t num = (int64_t)lrs(ucpu, v.la_a_cpu) * c.la_w_cpu + (int64_t)lrs(umem, v.la_a_mem) * c.la_w_mem;
-  return div_weights(num, (int64_t)(c.la_w_cpu + c.la_w_mem));
+  const double ucpu = p.est_cpu + (prod ? v.la_up_cpu : v.la_u_cpu);
+  const double umem = p.est_mem + (prod ? v.la_up_mem : v.la_u_mem);
+  const int32_t num = lrs(ucpu, v.la_a_cpu) * c.la_w_cpu + lrs(umem, v.la_a_mem) * c.la_w_mem;
+  return div_weights(num, c.la_w_cpu + c.la_w_mem);
 }
 
 // NodeNUMAResource Score (scoring.go:55-168).
-__device__ __forceinline__ int32_t numa_score(const koordhip_pod &p, const NV &v, const NumaRow &r,
+__device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, const NumaRow &r,
                                               const DevNumaClass *classes, const DevCfg &c) {
   if (p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0;
   if (r.cls < 0) return 0;  // no CPU topology: getResourceOptions / Allocate error -> 0
-  auto lr = [](int64_t a, int64_t b) { return lrs(a, b); };
-  auto dw = [](int64_t a, int64_t b) { return div_weights(a, b); };
+  auto lr = [](double a, double b) { return lrs(a, b); };
+  auto dw = [](int32_t a, int32_t b) { return div_weights(a, b); };
   if (!(p.flags & KOORDHIP_POD_CPUSET))
     return numa_la(v.r[KOORDHIP_RES_CPU] + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
                    v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM], v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem,
                    lr, dw);
   if (!numa_alloc_ok(classes[r.cls], r, p)) return 0;
-  return numa_la((int64_t)r.cnt * 1000 + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
+  return numa_la((double)r.cnt * 1000.0 + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
                  v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM], v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem,
                  lr, dw);
 }
 
 // Total weighted score, or -1 when any enabled Filter fails (short-circuit).
-__device__ __forceinline__ int32_t eval_total(const koordhip_pod &p, const NV &v, const DevCfg &c) {
+__device__ __forceinline__ int32_t eval_total(const DevPod &p, const NV &v, const DevCfg &c) {
   if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(p, v)) return -1;
   if ((c.filt & KOORDHIP_PLUGIN_LOADAWARE) && !la_filter(p, v)) return -1;
   int32_t t = 0;
@@ -304,7 +311,7 @@ __device__ __forceinline__ int32_t eval_total(const koordhip_pod &p, const NV &v
 }
 
 // ... with NodeNUMAResource
-__device__ __forceinline__ int32_t eval_total_numa(const koordhip_pod &p, const NV &v, const NumaRow &r,
+__device__ __forceinline__ int32_t eval_total_numa(const DevPod &p, const NV &v, const NumaRow &r,
                                                    const DevNumaClass *classes, const DevCfg &c) {
   int32_t t = eval_total(p, v, c);
   if (t < 0) return t;
@@ -322,17 +329,18 @@ __device__ __forceinline__ int32_t key_node(uint64_t k) { return (int32_t)(0xFFF
 __device__ __forceinline__ int32_t key_score(uint64_t k) { return (int32_t)(k >> 32) - 1; }
 
 // Reserve delta (podAssignCache.assign + NodeInfo.AddPod), sign = +1 / -1.
-__device__ __forceinline__ void apply_delta(NV &v, const koordhip_pod &p, int sign) {
+__device__ __forceinline__ void apply_delta(NV &v, const DevPod &p, int sign) {
+  const double sg = (double)sign;
 #pragma unroll
-  for (int r = 0; r < KOORDHIP_NRES; r++) v.r[r] += sign * p.req[r];
-  v.nz_cpu += sign * p.nz_cpu_m;
-  v.nz_mem += sign * p.nz_mem;
+  for (int r = 0; r < KOORDHIP_NRES; r++) v.r[r] = __builtin_fma(sg, p.req[r], v.r[r]);
+  v.nz_cpu = __builtin_fma(sg, p.nz_cpu_m, v.nz_cpu);
+  v.nz_mem = __builtin_fma(sg, p.nz_mem, v.nz_mem);
   v.npods += sign;
-  v.la_u_cpu += sign * p.est_cpu;
-  v.la_u_mem += sign * p.est_mem;
+  v.la_u_cpu = __builtin_fma(sg, p.est_cpu, v.la_u_cpu);
+  v.la_u_mem = __builtin_fma(sg, p.est_mem, v.la_u_mem);
   if (p.flags & KOORDHIP_POD_PROD) {
-    v.la_up_cpu += sign * p.est_cpu;
-    v.la_up_mem += sign * p.est_mem;
+    v.la_up_cpu = __builtin_fma(sg, p.est_cpu, v.la_up_cpu);
+    v.la_up_mem = __builtin_fma(sg, p.est_mem, v.la_up_mem);
   }
   uint32_t f = v.flags & ~(NF_OVER_CPU | NF_OVER_MEM | NF_OVER_EPH);
   if (v.r[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU]) f |= NF_OVER_CPU;
@@ -385,7 +393,7 @@ __device__ __forceinline__ void store_numa_row(const NumaRow &r, const DevNodes 
 
 // NodeNUMAResource Reserve / Release on a row (resourceManager.Update / Release,
 // node_allocation.go:76-131).
-__device__ __forceinline__ void numa_apply(NumaRow &r, const koordhip_pod &p, const uint64_t *cpus, int sign) {
+__device__ __forceinline__ void numa_apply(NumaRow &r, const DevPod &p, const uint64_t *cpus, int sign) {
   const int ex = (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy);
   int n = 0;
 #pragma unroll

@@ -128,12 +128,12 @@ __global__ void k_prep_flags(PrepIn in, DevNodes d, const int32_t *__restrict__ 
 // ---------------------------------------------------------------------------
 // k_eval_full: parity mode, no short-circuit.
 
-__global__ void k_eval_full(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods, int32_t n_pods,
+__global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
                             uint8_t *__restrict__ status, int32_t *__restrict__ scores) {
   int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   int32_t p = blockIdx.y;
   if (i >= d.n || p >= n_pods) return;
-  const koordhip_pod pod = pods[p];
+  const DevPod pod = pods[p];
   NV v{};
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
@@ -166,15 +166,15 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const koordhip_pod *__restrict
 // index order) up to k.  Output: k keys per (pod, chunk), unsorted, 0-padded.
 
 template <int R, bool NUMA>
-__global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
+__global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
                                                       int32_t n_pods, int32_t lo, int32_t hi, int32_t k,
                                                       int32_t score_bits, uint64_t *__restrict__ out) {
   const int lane = lane_id();
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: pod fields in SGPRs
   const int32_t p = blockIdx.y * (blockDim.x >> 6) + wave;
   if (p >= n_pods) return;  // wave-uniform
   const int32_t c0 = lo + blockIdx.x * (64 * R);
-  const koordhip_pod pod = pods[p];
+  const DevPod pod = pods[p];
   const Need need = pod_needs(pod, c);
   int32_t s[R];  // total score + 1, 0 = infeasible / past the end
 #pragma unroll
@@ -450,14 +450,14 @@ __device__ __forceinline__ uint64_t stamp() {
 constexpr int RES_PRE = 128;  // prefetched snapshot rows per round
 
 template <bool NUMA>
-__global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pods,
+__global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
                                                 int32_t n_pods, int32_t k, const uint64_t *__restrict__ lists,
                                                 int32_t monotone, int32_t *__restrict__ out_node,
                                                 uint64_t *__restrict__ out_cpus, uint64_t *__restrict__ dbg) {
   // dbg (diagnostic builds only, KOORDHIP_STAMPS): s_memtime segment sums
   uint64_t t_entry = dbg ? stamp() : 0, t_a = 0, t_b = 0, t_c = 0, t_mark = 0, n_eval = 0, n_miss = 0;
   __shared__ __attribute__((aligned(16))) uint64_t lk[RES_MAXP * RES_MAXP];
-  __shared__ __attribute__((aligned(16))) koordhip_pod lp[RES_MAXP + 16];
+  __shared__ __attribute__((aligned(16))) DevPod lp[RES_MAXP + 16];
   // Prefetched snapshot rows: slot t holds pod (t % n_pods)'s list entry at
   // position t / n_pods.  A round's winner is either a node already modified
   // in the round (kept in registers) or its pod's first unmodified list
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
   const int lane = lane_id();
   // LDS-DMA the round's lists and pod records (buffers are padded to 1 KiB)
   dma_to_lds(lk, lists, ((n_pods * k * 8) + 1023) & ~1023, lane);
-  dma_to_lds(lp, pods, ((n_pods * (int32_t)sizeof(koordhip_pod)) + 1023) & ~1023, lane);
+  dma_to_lds(lp, pods, ((n_pods * (int32_t)sizeof(DevPod)) + 1023) & ~1023, lane);
   const int32_t words = (d.n + 31) >> 5;
   for (int32_t j = lane; j < words; j += 64) modmap[j] = 0;
   for (int32_t t = lane; t < RES_PRE; t += 64) {
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
   bool mod = false;
   for (int32_t j = 0; j < n_pods; j++) {
     if (dbg) t_mark = stamp();
-    const koordhip_pod pod = lp[j];
+    const DevPod pod = lp[j];
     const uint64_t free_mask = __ballot(e != 0 && !mod);
     const int first = free_mask ? __builtin_ctzll(free_mask) : 64;
     const uint64_t cand = free_mask ? readlane_u64(e, first) : 0;
@@ -628,10 +628,10 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const koor
 // ---------------------------------------------------------------------------
 // single-pod commit / uncommit (Reserve / Unreserve from the host)
 
-__global__ void k_commit(DevCfg c, DevNodes d, const koordhip_pod *__restrict__ pod, int32_t node, int32_t sign,
+__global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, int32_t node, int32_t sign,
                          uint64_t *__restrict__ cpus, int32_t *__restrict__ rc) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const koordhip_pod p = *pod;
+  const DevPod p = *pod;
   *rc = 0;
   if (numa_on(c) && is_cpuset(p)) {
     NumaRow r;
@@ -686,7 +686,7 @@ hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t 
   return hipGetLastError();
 }
 
-hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
+hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods,
                             uint8_t *status, int32_t *scores, hipStream_t s) {
   if (n_pods <= 0 || d.n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_eval_full, dim3((d.n + 255) / 256, n_pods), dim3(256), 0, s, c, d, pods, n_pods, status,
@@ -694,7 +694,7 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const koordhip_p
   return hipGetLastError();
 }
 
-hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods,
+hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods,
                                int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
                                uint64_t *out, hipStream_t s) {
   dim3 grid(nchunks, (n_pods + 3) / 4);
@@ -727,7 +727,7 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
   return hipGetLastError();
 }
 
-hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod *pods, int32_t n_pods, int32_t k,
+hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t k,
                           const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *out_cpus,
                           uint64_t *dbg, hipStream_t s) {
   const size_t bitmap = (size_t)((d.n + 31) >> 5) * sizeof(uint32_t);
@@ -740,7 +740,7 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const koordhip_pod
   return hipGetLastError();
 }
 
-hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const koordhip_pod *pod, int32_t node, int32_t sign,
+hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const DevPod *pod, int32_t node, int32_t sign,
                          uint64_t *cpus, int32_t *rc, hipStream_t s) {
   hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, c, d, pod, node, sign, cpus, rc);
   return hipGetLastError();

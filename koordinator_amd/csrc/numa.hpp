@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "../../include/koordhip.h"
+#include "pod.hpp"
 
 namespace kh {
 
@@ -156,7 +157,7 @@ __device__ bool numa_spread_ok(const DevNumaClass &C, const NumaRow &r, int need
 }
 
 // resourceManager.Allocate succeeds? (empty hint, no preferred CPUs)
-__device__ __forceinline__ bool numa_alloc_ok(const DevNumaClass &C, const NumaRow &r, const koordhip_pod &p) {
+__device__ __forceinline__ bool numa_alloc_ok(const DevNumaClass &C, const NumaRow &r, const DevPod &p) {
   const int need = p.numa_cpus;
   if (popc4(r.fr) < need) return false;  // allocateCPUSet :257-259 (filterAvailableCPUsByRequiredCPUBindPolicy is a no-op)
   const int req = (int)KOORDHIP_NUMA_REQUIRED(p.numa_policy);
@@ -173,7 +174,7 @@ __device__ __forceinline__ bool numa_alloc_ok(const DevNumaClass &C, const NumaR
 }
 
 // Filter, plugin.go:266-324; true = passes.
-__device__ __forceinline__ bool numa_filter(const koordhip_pod &p, const NumaRow &r, const DevNumaClass *classes) {
+__device__ __forceinline__ bool numa_filter(const DevPod &p, const NumaRow &r, const DevNumaClass *classes) {
   if (p.flags & KOORDHIP_POD_NUMA_ERROR) return false;
   if ((p.flags & KOORDHIP_POD_NUMA_SKIP) || !(p.flags & KOORDHIP_POD_CPUSET)) return true;
   if (r.cls < 0) return false;
@@ -192,15 +193,15 @@ __device__ __forceinline__ bool numa_filter(const koordhip_pod &p, const NumaRow
 
 // leastResourceScorer over {cpu, memory}, alloc 0 left out (scoring.go:191-230)
 template <typename Lrs, typename Div>
-__device__ __forceinline__ int32_t numa_la(int64_t rc, int64_t ac, int64_t rm, int64_t am, int32_t wc, int32_t wm,
+__device__ __forceinline__ int32_t numa_la(double rc, double ac, double rm, double am, int32_t wc, int32_t wm,
                                            Lrs lrs_fn, Div div_fn) {
-  int64_t num = 0, ws = 0;
-  if (wc && ac != 0) {
-    num += (int64_t)lrs_fn(rc, ac) * wc;
+  int32_t num = 0, ws = 0;
+  if (wc && ac != 0.0) {
+    num += lrs_fn(rc, ac) * wc;
     ws += wc;
   }
-  if (wm && am != 0) {
-    num += (int64_t)lrs_fn(rm, am) * wm;
+  if (wm && am != 0.0) {
+    num += lrs_fn(rm, am) * wm;
     ws += wm;
   }
   return ws ? div_fn(num, ws) : 0;
@@ -568,7 +569,7 @@ __device__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
 }
 
 // Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
-__device__ bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const koordhip_pod &p, uint64_t *cpus) {
+__device__ bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
   for (int w = 0; w < NW; w++) cpus[w] = 0;
   const int need = p.numa_cpus;
   if (popc4(r.fr) < need) return false;

@@ -1,0 +1,27 @@
+// pod.hpp -- the device pod record and the exact-f64 quantity range shared by
+// every kernel of libkoordhip.so.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/koordhip.h"
+
+namespace kh {
+
+// Largest quantity magnitude the engine accepts (validated by the host side
+// of api.hip): every quantity is then an exact f64 (see eval.hpp).
+constexpr double KH_EXACT_LIMIT = 35184372088832.0;  // 2^45
+
+// Device copy of one koordhip_pod (same fields, quantities as exact f64).
+struct DevPod {
+  double req[KOORDHIP_NRES];
+  double nz_cpu_m, nz_mem;
+  double est_cpu, est_mem;
+  uint32_t flags;
+  int32_t numa_cpus;
+  uint32_t numa_policy;
+  int32_t reserved0;
+  int64_t reserved1;
+};
+static_assert(sizeof(DevPod) == 96, "DevPod is 96 bytes");
+
+}  // namespace kh
