@@ -41,8 +41,9 @@ int fail(int code, const std::string &msg) {
   } while (0)
 
 constexpr int kDefaultBatch = 64;
-constexpr int32_t kMaxNodes = 700000;  // resolve keeps a per-node bit in LDS
+constexpr int32_t kMaxNodes = 400000;  // the resolve keeps a per-node bit in LDS (next to 2 x 64 x 128 list keys)
 constexpr int kMaxBatch = 64;
+constexpr int kRing = 4;               // per-round events in flight (lag-1 pipeline needs 3)
 
 // Contexts of one process sharing node shards without RCCL
 // (koordhip_comm_init_local): a generation barrier per exchange step; a
@@ -89,7 +90,8 @@ struct koordhip_ctx {
   int32_t batch = kDefaultBatch;
   int32_t monotone = 1;
   int32_t score_bits = 16;  // bits of (max total score + 1)
-  int32_t partial_r = 8;    // nodes per lane of k_topk_partial (tuning knob KOORDHIP_TOPK_R)
+  int32_t nbins = 2;        // score histogram bins of k_select: max total score + 2
+  int32_t partial_r = 2;    // nodes per lane of k_scan (tuning knob KOORDHIP_TOPK_R)
 
   std::vector<void *> cols;  // every device column allocation
   kh::DevNodes d{};
@@ -105,12 +107,16 @@ struct koordhip_ctx {
   int32_t n_classes = 0;
   kh::DevNumaClass *d_classes = nullptr;
   int32_t *d_rc = nullptr;     // k_commit status
-  uint64_t *d_partial = nullptr;
+  uint64_t *d_partial = nullptr;  // score matrix of k_scan (u16 [pods][stride])
   size_t partial_cap = 0;
-  uint64_t *d_lists = nullptr;   // [batch][k]
+  uint64_t *d_lists = nullptr;   // [2][batch][k] (rank-local lists; double buffer: round parity)
   uint64_t *d_gather = nullptr;  // [world][batch][k]
   int32_t gather_world = 1;
-  uint64_t *d_final = nullptr;   // [batch][k]
+  uint64_t *d_final = nullptr;   // [2][batch][k] (merged lists, multi-rank)
+  int32_t *d_mod = nullptr;      // [2][1 + batch]: {count, nodes} committed by a round (ping-pong)
+  const uint64_t *d_cur_lists = nullptr;  // this round's rank-local lists (local-group exchange)
+  hipStream_t rstream = nullptr;  // resolve stream (the eval kernels use `stream`)
+  hipEvent_t ev_sel[kRing] = {}, ev_res[kRing] = {}, ev_start = nullptr;
   kh::DevPod *d_tmp_pod = nullptr;
   uint64_t *d_dbg = nullptr;  // KOORDHIP_STAMPS diagnostic counters (resolve segments)
 
@@ -238,18 +244,19 @@ int ensure(koordhip_ctx *c, void **p, size_t *cap, size_t bytes) {
   return 0;
 }
 
-// Work decomposition of one eval launch over node range [lo, hi): one wave
-// per (pod, chunk of 64 x R nodes).
-int32_t nchunks_for(const koordhip_ctx *c, int32_t lo, int32_t hi) {
-  const int32_t w = 64 * c->partial_r;
-  return std::max<int32_t>(1, (hi - lo + w - 1) / w);
-}
-
+// Exact per-pod top-k over node range [lo, hi) of np pods: k_scan fills the
+// score matrix, k_select reduces each row (best first, 0-padded).
 int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
                uint64_t *out, bool timed) {
-  const int32_t nchunks = nchunks_for(c, lo, hi);
-  const size_t need = (size_t)np * nchunks * k * sizeof(uint64_t) + 1024;  // +1 KiB: merge DMA padding
+  const int R = c->partial_r;
+  const int64_t stride = ((int64_t)(hi - lo) + 63) & ~63ll;
+  const int32_t nchunks = kh::scan_chunks(R, lo, hi);
+  const int32_t mstride = (nchunks + 63) & ~63;
+  const size_t sbytes = (size_t)np * stride * sizeof(uint16_t);
+  const size_t need = sbytes + (size_t)np * mstride * sizeof(uint16_t) + 64;
   if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial), &c->partial_cap, need)) return e;
+  uint16_t *S = reinterpret_cast<uint16_t *>(c->d_partial);
+  uint16_t *Mx = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(c->d_partial) + sbytes);
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   if (timed && c->cfg.profile_kernels) {
     if (c->ev_used + 2 > (int32_t)c->ev.size()) {
@@ -264,12 +271,11 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
     c->ev_used += 2;
     HIP_TRY(hipEventRecord(*e0, c->stream));
   }
-  HIP_TRY(kh::launch_topk_partial(c->partial_r, c->dc, c->d, d_pods, np, lo, hi, nchunks, k, c->score_bits, c->d_partial,
-                                  c->stream));
+  HIP_TRY(kh::launch_scan(R, c->dc, c->d, d_pods, np, lo, hi, S, stride, Mx, mstride, c->stream));
   if (e1) HIP_TRY(hipEventRecord(*e1, c->stream));
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
-  HIP_TRY(kh::launch_topk_merge(c->d_partial, (int64_t)nchunks * k, k, np, nchunks, k, c->score_bits, out, c->stream));
+  HIP_TRY(kh::launch_select(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, out, c->d_dbg, c->stream));
   return 0;
 }
 
@@ -422,7 +428,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     const int v = std::atoi(r);
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
   }
-  if (c->numa && c->partial_r > 4) c->partial_r = 4;  // the NUMA eval kernel is built for R <= 4
+  if (c->numa && c->partial_r > 4) c->partial_r = 4;  // the NUMA scan kernel is built for R <= 4
   c->monotone = 1;  // Fit LeastAllocated + LoadAware least-used: a commit never raises a key
   {
     int64_t max_total = 0;  // every plugin score is in [0, 100]
@@ -431,6 +437,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     int bits = 1;
     while ((1ll << bits) <= max_total + 1) bits++;
     c->score_bits = bits;
+    c->nbins = (int32_t)max_total + 2;
   }
   int dev = cfg->device;
   if (dev < 0) {
@@ -460,8 +467,16 @@ int koordhip_destroy(koordhip_ctx *c) {
   for (void *p : c->ckpt) (void)hipFree(p);
   for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
                   (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
-                  (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc})
+                  (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod})
     if (p) (void)hipFree(p);
+  for (int i = 0; i < kRing; i++)
+    for (hipEvent_t e : {c->ev_sel[i], c->ev_res[i]})
+      if (e) (void)hipEventDestroy(e);
+  if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+  if (c->rstream) {
+    (void)hipStreamSynchronize(c->rstream);
+    (void)hipStreamDestroy(c->rstream);
+  }
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
@@ -477,7 +492,7 @@ int koordhip_destroy(koordhip_ctx *c) {
 int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
   if (n < 0) return fail(KOORDHIP_EINVAL, "n < 0");
-  if (n > kMaxNodes) return fail(KOORDHIP_EINVAL, "more than 700000 nodes in one snapshot");
+  if (n > kMaxNodes) return fail(KOORDHIP_EINVAL, "more than 400000 nodes in one snapshot");
   if (int e = validate_soa(s)) return e;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -794,19 +809,20 @@ namespace {
 // a device-to-device pull of every member's list after its eval finished
 // (events + host barrier), then a second barrier so no member overwrites its
 // list before every peer has copied it.
-int exchange(koordhip_ctx *c, size_t count) {
+int exchange(koordhip_ctx *c, const uint64_t *lists, size_t count) {
   if (c->comm) {
-    NCCL_TRY(ncclAllGather(c->d_lists, c->d_gather, count, ncclUint64, c->comm, c->stream));
+    NCCL_TRY(ncclAllGather(lists, c->d_gather, count, ncclUint64, c->comm, c->stream));
     return 0;
   }
   LocalGroup &g = *c->group;
+  c->d_cur_lists = lists;
   HIP_TRY(hipEventRecord(c->ev_part, c->stream));
   if (!g.barrier()) return fail(KOORDHIP_ECOMM, "local group aborted by a peer");
   for (int32_t j = 0; j < g.world; j++) {
     koordhip_ctx *p = g.ctx[j];
     if (p != c) HIP_TRY(hipStreamWaitEvent(c->stream, p->ev_part, 0));
-    HIP_TRY(hipMemcpyAsync(c->d_gather + (size_t)j * count, p->d_lists, count * sizeof(uint64_t), hipMemcpyDefault,
-                           c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_gather + (size_t)j * count, p->d_cur_lists, count * sizeof(uint64_t),
+                           hipMemcpyDefault, c->stream));
   }
   HIP_TRY(hipEventRecord(c->ev_copy, c->stream));
   if (!g.barrier()) return fail(KOORDHIP_ECOMM, "local group aborted by a peer");
@@ -847,19 +863,27 @@ namespace {
 int place_staged_impl(koordhip_ctx *c) {
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   HIP_TRY(hipSetDevice(c->device));
-  const int32_t P = c->batch, K = c->batch;
-  size_t cap = 0;
+  const int32_t P = c->batch, K = 2 * c->batch;  // lag-1 needs k >= 2 x round size
+  const size_t lbytes = (size_t)kMaxBatch * 2 * kMaxBatch * sizeof(uint64_t);
   if (!c->d_lists) {
-    HIP_TRY(hipMalloc(&c->d_lists, (size_t)kMaxBatch * kMaxBatch * sizeof(uint64_t)));
-    HIP_TRY(hipMalloc(&c->d_final, (size_t)kMaxBatch * kMaxBatch * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_lists, 2 * lbytes));
+    HIP_TRY(hipMalloc(&c->d_final, 2 * lbytes));
+    HIP_TRY(hipMalloc(&c->d_mod, 2 * (1 + kMaxBatch) * sizeof(int32_t)));
+    HIP_TRY(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+    for (int i = 0; i < kRing; i++) {
+      HIP_TRY(hipEventCreateWithFlags(&c->ev_sel[i], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&c->ev_res[i], hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
   }
   if (c->world > c->gather_world) {
     if (c->d_gather) HIP_TRY(hipFree(c->d_gather));
     c->d_gather = nullptr;
-    HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * kMaxBatch * kMaxBatch * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * lbytes));
     c->gather_world = c->world;
   }
-  (void)cap;
+  if (kh::resolve_lds_bytes(P, K, c->n, c->numa) > 159 * 1024)
+    return fail(KOORDHIP_EINVAL, "snapshot too large for the resolve kernel's LDS");
   if (c->group)
     if (int e = group_agree(c)) return e;
   int32_t lo = 0, hi = c->n;
@@ -868,39 +892,61 @@ int place_staged_impl(koordhip_ctx *c) {
   c->last_launches = 0;
   c->last_evals = 0;
   if (std::getenv("KOORDHIP_STAMPS")) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 8 * sizeof(uint64_t)));
-    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 8 * sizeof(uint64_t), c->stream));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 16 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(uint64_t), c->stream));
   }
   HIP_TRY(hipEventRecord(c->t0, c->stream));
+  // round 0 has no predecessor: M' = {}
+  HIP_TRY(hipMemsetAsync(c->d_mod + (1 + kMaxBatch), 0, sizeof(int32_t), c->stream));
+  HIP_TRY(hipEventRecord(c->ev_start, c->stream));
+  HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_start, 0));
+  // Lag-1 pipeline: round r's lists are evaluated (stream) while round r-1 is
+  // resolved (rstream); they wait only for round r-2's commits.
   const int32_t total = c->n_staged;
-  for (int32_t p0 = 0; p0 < total; p0 += P) {
+  const int lag = std::getenv("KOORDHIP_NO_OVERLAP") ? 1 : 2;  // diagnostics: serialise eval after resolve
+  const char *trace_env = std::getenv("KOORDHIP_TRACE_POD");      // diagnostics: printf one pod's resolve step
+  const int32_t trace = trace_env ? std::atoi(trace_env) : -1;
+  int32_t r = 0;
+  for (int32_t p0 = 0; p0 < total; p0 += P, r++) {
     const int32_t np = std::min(P, total - p0);
     const kh::DevPod *pods = c->d_pods + p0;
+    uint64_t *lists = c->d_lists + (size_t)(r & 1) * (lbytes / sizeof(uint64_t));
+    uint64_t *final_lists = lists;
+    if (r >= lag) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[(r - lag) % kRing], 0));
     if (c->world > 1) {
-      if (np < P) HIP_TRY(hipMemsetAsync(c->d_lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
-      if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
-      if (int e = exchange(c, (size_t)P * K)) return e;
-      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits, c->d_final, c->stream));
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_final, c->monotone, c->d_out + p0,
-                                 c->d_cpus ? c->d_cpus + (size_t)p0 * KOORDHIP_NUMA_WORDS : nullptr, c->d_dbg,
-                                 c->stream));
+      if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true)) return e;
+      if (int e = exchange(c, lists, (size_t)P * K)) return e;
+      final_lists = c->d_final + (size_t)(r & 1) * (lbytes / sizeof(uint64_t));
+      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits, final_lists,
+                                    c->stream));
     } else {
-      if (int e = topk_batch(c, pods, np, K, lo, hi, c->d_lists, true)) return e;
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, c->d_lists, c->monotone, c->d_out + p0,
-                                 c->d_cpus ? c->d_cpus + (size_t)p0 * KOORDHIP_NUMA_WORDS : nullptr, c->d_dbg,
-                                 c->stream));
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true)) return e;
     }
+    HIP_TRY(hipEventRecord(c->ev_sel[r % kRing], c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_sel[r % kRing], 0));
+    const int32_t *prev = c->d_mod + (size_t)((r + 1) & 1) * (1 + kMaxBatch);
+    int32_t *next = c->d_mod + (size_t)(r & 1) * (1 + kMaxBatch);
+    HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, final_lists, c->monotone, prev, next, c->d_out + p0,
+                               c->d_cpus ? c->d_cpus + (size_t)p0 * KOORDHIP_NUMA_WORDS : nullptr, c->d_dbg,
+                               trace >= p0 && trace < p0 + np ? trace - p0 : -1, c->rstream));
+    HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->rstream));
   }
+  if (r > 0) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[(r - 1) % kRing], 0));
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   if (c->d_dbg) {
-    uint64_t h[8];
+    uint64_t h[16];
     HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     std::fprintf(stderr,
-                 "[koordhip stamps] rounds-total cycles: prologue %llu  list %llu  eval %llu  commit %llu  kernel %llu"
-                 "  | evals %llu prefetch-misses %llu pods %llu\n",
-                 (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
-                 (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7]);
+                 "[koordhip stamps] select blocks %llu cycles: bound %llu  pass1 %llu  kth %llu  pass2 %llu  out %llu\n",
+                 (unsigned long long)h[8], (unsigned long long)h[9], (unsigned long long)h[10],
+                 (unsigned long long)h[11], (unsigned long long)h[12], (unsigned long long)h[13]);
+    std::fprintf(stderr,
+                 "[koordhip stamps] resolve cycles: prologue %llu  kernel %llu  | re-evals %llu prefetch-misses %llu "
+                 "pods %llu\n",
+                 (unsigned long long)h[0], (unsigned long long)h[4], (unsigned long long)h[5],
+                 (unsigned long long)h[6], (unsigned long long)h[7]);
   }
   return 0;
 }

@@ -139,148 +139,158 @@ __device__ __forceinline__ void load_numa(NumaRow &r, const DevNodes &d, int32_t
   }
 }
 
+// Column element i with a 32-bit byte offset: lets the compiler use the
+// SGPR-base + 32-bit VGPR-offset form of global loads/stores (no 64-bit
+// address arithmetic per column).  Node counts are < 2^26, so offsets fit.
+template <typename T>
+__device__ __forceinline__ const T &col(const T *base, int32_t i) {
+  return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)i * (uint32_t)sizeof(T));
+}
+template <typename T>
+__device__ __forceinline__ T &col(T *base, int32_t i) {
+  return *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t)i * (uint32_t)sizeof(T));
+}
+
 // Load node i's columns the evaluation needs (coalesced across lanes).
 __device__ __forceinline__ void load_node(NV &v, const DevNodes &d, int32_t i, const Need &n, const DevCfg &c) {
-  v.flags = d.flags[i];
+  v.flags = col(d.flags, i);
   if (n.pods) {
-    v.a_pods = d.alloc_pods[i];
-    v.npods = d.npods[i];
+    v.a_pods = col(d.alloc_pods, i);
+    v.npods = col(d.npods, i);
   }
-  if (n.a_cpu) v.a[KOORDHIP_RES_CPU] = d.alloc[KOORDHIP_RES_CPU][i];
-  if (n.a_mem) v.a[KOORDHIP_RES_MEM] = d.alloc[KOORDHIP_RES_MEM][i];
-  if (n.r_cpu) v.r[KOORDHIP_RES_CPU] = d.requested[KOORDHIP_RES_CPU][i];
-  if (n.r_mem) v.r[KOORDHIP_RES_MEM] = d.requested[KOORDHIP_RES_MEM][i];
+  if (n.a_cpu) v.a[KOORDHIP_RES_CPU] = col(d.alloc[KOORDHIP_RES_CPU], i);
+  if (n.a_mem) v.a[KOORDHIP_RES_MEM] = col(d.alloc[KOORDHIP_RES_MEM], i);
+  if (n.r_cpu) v.r[KOORDHIP_RES_CPU] = col(d.requested[KOORDHIP_RES_CPU], i);
+  if (n.r_mem) v.r[KOORDHIP_RES_MEM] = col(d.requested[KOORDHIP_RES_MEM], i);
   if (n.eph) {
-    v.a[KOORDHIP_RES_EPH] = d.alloc[KOORDHIP_RES_EPH][i];
-    v.r[KOORDHIP_RES_EPH] = d.requested[KOORDHIP_RES_EPH][i];
+    v.a[KOORDHIP_RES_EPH] = col(d.alloc[KOORDHIP_RES_EPH], i);
+    v.r[KOORDHIP_RES_EPH] = col(d.requested[KOORDHIP_RES_EPH], i);
   }
   if (n.bcpu) {
-    v.a[KOORDHIP_RES_BCPU] = d.alloc[KOORDHIP_RES_BCPU][i];
-    v.r[KOORDHIP_RES_BCPU] = d.requested[KOORDHIP_RES_BCPU][i];
+    v.a[KOORDHIP_RES_BCPU] = col(d.alloc[KOORDHIP_RES_BCPU], i);
+    v.r[KOORDHIP_RES_BCPU] = col(d.requested[KOORDHIP_RES_BCPU], i);
   }
   if (n.bmem) {
-    v.a[KOORDHIP_RES_BMEM] = d.alloc[KOORDHIP_RES_BMEM][i];
-    v.r[KOORDHIP_RES_BMEM] = d.requested[KOORDHIP_RES_BMEM][i];
+    v.a[KOORDHIP_RES_BMEM] = col(d.alloc[KOORDHIP_RES_BMEM], i);
+    v.r[KOORDHIP_RES_BMEM] = col(d.requested[KOORDHIP_RES_BMEM], i);
   }
-  if (n.nz_cpu) v.nz_cpu = d.nz_cpu[i];
-  if (n.nz_mem) v.nz_mem = d.nz_mem[i];
+  if (n.nz_cpu) v.nz_cpu = col(d.nz_cpu, i);
+  if (n.nz_mem) v.nz_mem = col(d.nz_mem, i);
   if (n.la) {
     if (c.la_alias) {
       v.la_a_cpu = v.a[KOORDHIP_RES_CPU];
       v.la_a_mem = v.a[KOORDHIP_RES_MEM];
     } else {
-      v.la_a_cpu = d.la_alloc_cpu[i];
-      v.la_a_mem = d.la_alloc_mem[i];
+      v.la_a_cpu = col(d.la_alloc_cpu, i);
+      v.la_a_mem = col(d.la_alloc_mem, i);
     }
     if (n.la_prod) {
-      v.la_up_cpu = d.la_used_prod_cpu[i];
-      v.la_up_mem = d.la_used_prod_mem[i];
+      v.la_up_cpu = col(d.la_used_prod_cpu, i);
+      v.la_up_mem = col(d.la_used_prod_mem, i);
     }
     if (n.la_nonprod) {
-      v.la_u_cpu = d.la_used_cpu[i];
-      v.la_u_mem = d.la_used_mem[i];
+      v.la_u_cpu = col(d.la_used_cpu, i);
+      v.la_u_mem = col(d.la_used_mem, i);
     }
   }
 }
 
+// The per-(pod,node) functions below branch only on wave-uniform values (pod
+// record, plugin config); per-node conditions are computed for every lane and
+// combined with selects, so a wave runs one straight-line sequence instead of
+// exec-masked short-circuit paths.
+
 // num / ws for the weighted averages (num <= 100 * sum of weights <= 50000,
-// ws <= 500): a shift when ws is a power of two (the shipped profile: 2 and
-// 4), else an f32 reciprocal estimate (error << 1) + one int32 fix-up.
+// ws <= 500): an f32 reciprocal estimate (relative error ~2^-23, so the
+// absolute error is < 0.01) truncated, then one exact int32 fix-up each way.
 __device__ __forceinline__ int32_t div_weights(int32_t num, int32_t ws) {
-  if ((ws & (ws - 1)) == 0) return num >> __builtin_ctz((uint32_t)ws);
   int32_t q = (int32_t)((float)num * __builtin_amdgcn_rcpf((float)ws));
   const int32_t r = num - q * ws;
   q -= (r < 0);
   q += (r >= ws);
   return q;
 }
+// ... with a wave-uniform power-of-two weight sum: a shift
+__device__ __forceinline__ int32_t div_weights_uniform(int32_t num, int32_t ws) {
+  if ((ws & (ws - 1)) == 0) return num >> __builtin_ctz((uint32_t)ws);
+  return div_weights(num, ws);
+}
 
 // leastRequestedScore, load_aware.go:388-397 / least_allocated.go:49-58:
-// (cap - req) * 100 / cap in int64.  f = (cap - req) * 100 < 2^52 is exact, the
-// reciprocal estimate of f / cap <= 100 is within 1 of the quotient, and the
-// remainder f - q * cap (one fma, exact: an integer < 2^53) fixes it up.
+// (cap - req) * 100 / cap in int64, 0 if cap == 0 or req > cap.
+// f = (cap - req) * 100 < 2^52 is exact, the reciprocal estimate of f / cap
+// (<= 100) is within 1 of the quotient, and the remainder f - q * cap (one
+// fma, exact: an integer < 2^53) fixes it up.
 __device__ __forceinline__ int32_t lrs(double req, double cap) {
-  if (cap == 0.0 || req > cap) return 0;
+  const bool zero = (cap == 0.0) | (req > cap);
   const double f = (cap - req) * 100.0;
   int32_t q = (int32_t)(f * __builtin_amdgcn_rcp(cap));
   const double r = __builtin_fma(-(double)q, cap, f);
   q -= (r < 0.0);
   q += (r >= cap);
-  return q;
+  return zero ? 0 : q;
 }
 
 // Fit LeastAllocated score (upstream resource_allocation.go + least_allocated.go;
-// koord copy nodenumaresource/scoring.go:191-246).
+// koord copy nodenumaresource/scoring.go:191-246): resources with Allocatable 0
+// are left out of both sums; scalar resources only when the pod requests them.
 __device__ __forceinline__ int32_t fit_score(const DevPod &p, const NV &v, const DevCfg &c) {
   int32_t num = 0, ws = 0;
-  if (c.fit_w[KOORDHIP_RES_CPU] && v.a[KOORDHIP_RES_CPU] != 0.0) {
-    num += lrs(v.nz_cpu + p.nz_cpu_m, v.a[KOORDHIP_RES_CPU]) * c.fit_w[KOORDHIP_RES_CPU];
-    ws += c.fit_w[KOORDHIP_RES_CPU];
-  }
-  if (c.fit_w[KOORDHIP_RES_MEM] && v.a[KOORDHIP_RES_MEM] != 0.0) {
-    num += lrs(v.nz_mem + p.nz_mem, v.a[KOORDHIP_RES_MEM]) * c.fit_w[KOORDHIP_RES_MEM];
-    ws += c.fit_w[KOORDHIP_RES_MEM];
-  }
-  if (c.fit_w[KOORDHIP_RES_EPH] && v.a[KOORDHIP_RES_EPH] != 0.0) {
-    num += lrs(v.r[KOORDHIP_RES_EPH] + p.req[KOORDHIP_RES_EPH], v.a[KOORDHIP_RES_EPH]) *
-           c.fit_w[KOORDHIP_RES_EPH];
-    ws += c.fit_w[KOORDHIP_RES_EPH];
-  }
+  auto term = [&](double req, double cap, int32_t w) {
+    const bool on = cap != 0.0;
+    num += on ? lrs(req, cap) * w : 0;
+    ws += on ? w : 0;
+  };
+  if (c.fit_w[KOORDHIP_RES_CPU]) term(v.nz_cpu + p.nz_cpu_m, v.a[KOORDHIP_RES_CPU], c.fit_w[KOORDHIP_RES_CPU]);
+  if (c.fit_w[KOORDHIP_RES_MEM]) term(v.nz_mem + p.nz_mem, v.a[KOORDHIP_RES_MEM], c.fit_w[KOORDHIP_RES_MEM]);
+  if (c.fit_w[KOORDHIP_RES_EPH])
+    term(v.r[KOORDHIP_RES_EPH] + p.req[KOORDHIP_RES_EPH], v.a[KOORDHIP_RES_EPH], c.fit_w[KOORDHIP_RES_EPH]);
 #pragma unroll
-  for (int r = KOORDHIP_RES_BCPU; r <= KOORDHIP_RES_BMEM; r++) {
-    if (c.fit_w[r] && p.req[r] != 0.0 && v.a[r] != 0.0) {
-      num += lrs(v.r[r] + p.req[r], v.a[r]) * c.fit_w[r];
-      ws += c.fit_w[r];
-    }
-  }
-  if (ws == 0) return 0;
-  return div_weights(num, ws);
+  for (int r = KOORDHIP_RES_BCPU; r <= KOORDHIP_RES_BMEM; r++)
+    if (c.fit_w[r] && p.req[r] != 0.0) term(v.r[r] + p.req[r], v.a[r], c.fit_w[r]);
+  return ws == 0 ? 0 : div_weights(num, ws);
 }
 
 // fitsRequest (upstream fit.go; mirror reservation/plugin.go:445-494).  A zero
 // request on cpu/memory/ephemeral reduces to "Requested > Allocatable", kept
 // as the NF_OVER_* bits so such pods need not read those columns.
 __device__ __forceinline__ bool fit_filter(const DevPod &p, const NV &v) {
-  if (v.npods + 1 > v.a_pods) return false;
-  if (!(p.flags & KOORDHIP_POD_HAS_REQ)) return true;
-  if (p.req[KOORDHIP_RES_CPU] != 0.0) {
-    if (p.req[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU] - v.r[KOORDHIP_RES_CPU]) return false;
-  } else if (v.flags & NF_OVER_CPU) {
-    return false;
-  }
-  if (p.req[KOORDHIP_RES_MEM] != 0.0) {
-    if (p.req[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM] - v.r[KOORDHIP_RES_MEM]) return false;
-  } else if (v.flags & NF_OVER_MEM) {
-    return false;
-  }
-  if (p.req[KOORDHIP_RES_EPH] != 0.0) {
-    if (p.req[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH] - v.r[KOORDHIP_RES_EPH]) return false;
-  } else if (v.flags & NF_OVER_EPH) {
-    return false;
-  }
-  if ((p.flags & KOORDHIP_POD_REQ_BCPU) &&
-      p.req[KOORDHIP_RES_BCPU] > v.a[KOORDHIP_RES_BCPU] - v.r[KOORDHIP_RES_BCPU])
-    return false;
-  if ((p.flags & KOORDHIP_POD_REQ_BMEM) &&
-      p.req[KOORDHIP_RES_BMEM] > v.a[KOORDHIP_RES_BMEM] - v.r[KOORDHIP_RES_BMEM])
-    return false;
-  return true;
+  bool ok = v.npods < v.a_pods;  // npods + 1 > allowedPods fails
+  if (!(p.flags & KOORDHIP_POD_HAS_REQ)) return ok;
+  if (p.req[KOORDHIP_RES_CPU] != 0.0)
+    ok &= !(p.req[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU] - v.r[KOORDHIP_RES_CPU]);
+  else
+    ok &= !(v.flags & NF_OVER_CPU);
+  if (p.req[KOORDHIP_RES_MEM] != 0.0)
+    ok &= !(p.req[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM] - v.r[KOORDHIP_RES_MEM]);
+  else
+    ok &= !(v.flags & NF_OVER_MEM);
+  if (p.req[KOORDHIP_RES_EPH] != 0.0)
+    ok &= !(p.req[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH] - v.r[KOORDHIP_RES_EPH]);
+  else
+    ok &= !(v.flags & NF_OVER_EPH);
+  if (p.flags & KOORDHIP_POD_REQ_BCPU)
+    ok &= !(p.req[KOORDHIP_RES_BCPU] > v.a[KOORDHIP_RES_BCPU] - v.r[KOORDHIP_RES_BCPU]);
+  if (p.flags & KOORDHIP_POD_REQ_BMEM)
+    ok &= !(p.req[KOORDHIP_RES_BMEM] > v.a[KOORDHIP_RES_BMEM] - v.r[KOORDHIP_RES_BMEM]);
+  return ok;
 }
 
 // LoadAware Filter (load_aware.go:123-171): static mask + DaemonSet bypass.
 __device__ __forceinline__ bool la_filter(const DevPod &p, const NV &v) {
   if (p.flags & KOORDHIP_POD_DAEMONSET) return true;
-  return v.flags & ((p.flags & KOORDHIP_POD_PROD) ? NF_LA_OK_PROD : NF_LA_OK_NONPROD);
+  return (v.flags & ((p.flags & KOORDHIP_POD_PROD) ? NF_LA_OK_PROD : NF_LA_OK_NONPROD)) != 0;
 }
 
-// LoadAware Score (load_aware.go:269-335, scorer :378-386).
+// LoadAware Score (load_aware.go:269-335, scorer :378-386): every configured
+// weight counts in the denominator.
 __device__ __forceinline__ int32_t la_score(const DevPod &p, const NV &v, const DevCfg &c) {
-  if (v.flags & NF_LA_SCORE_ZERO) return 0;
   const bool prod = c.according && (p.flags & KOORDHIP_POD_PROD);
   const double ucpu = p.est_cpu + (prod ? v.la_up_cpu : v.la_u_cpu);
   const double umem = p.est_mem + (prod ? v.la_up_mem : v.la_u_mem);
   const int32_t num = lrs(ucpu, v.la_a_cpu) * c.la_w_cpu + lrs(umem, v.la_a_mem) * c.la_w_mem;
-  return div_weights(num, c.la_w_cpu + c.la_w_mem);
+  const int32_t s = div_weights_uniform(num, c.la_w_cpu + c.la_w_mem);
+  return (v.flags & NF_LA_SCORE_ZERO) ? 0 : s;
 }
 
 // NodeNUMAResource Score (scoring.go:55-168).
@@ -300,14 +310,15 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
                  lr, dw);
 }
 
-// Total weighted score, or -1 when any enabled Filter fails (short-circuit).
+// Total weighted score, or -1 when any enabled Filter fails.
 __device__ __forceinline__ int32_t eval_total(const DevPod &p, const NV &v, const DevCfg &c) {
-  if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(p, v)) return -1;
-  if ((c.filt & KOORDHIP_PLUGIN_LOADAWARE) && !la_filter(p, v)) return -1;
+  bool ok = true;
+  if (c.filt & KOORDHIP_PLUGIN_FIT) ok &= fit_filter(p, v);
+  if (c.filt & KOORDHIP_PLUGIN_LOADAWARE) ok &= la_filter(p, v);
   int32_t t = 0;
   if (c.score & KOORDHIP_PLUGIN_FIT) t += c.w_fit * fit_score(p, v, c);
   if (c.score & KOORDHIP_PLUGIN_LOADAWARE) t += c.w_la * la_score(p, v, c);
-  return t;
+  return ok ? t : -1;
 }
 
 // ... with NodeNUMAResource

@@ -19,18 +19,28 @@ struct PrepIn {
 hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t *rows, int32_t m, hipStream_t s);
 hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods,
                             uint8_t *status, int32_t *scores, hipStream_t s);
-// k_topk_partial: one wave evaluates 64 x R nodes (R in {1, 2, 4, 8})
-hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods,
-                               int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
-                               uint64_t *out, hipStream_t s);
+// k_scan: score matrix S[p][i - lo] = total score + 1 (0 = infeasible) over the
+// shard [lo, hi), one wave per (pod, 64 x R nodes), XCD-aware grid; Mx[p][chunk]
+// = the chunk's best value.  R in {1, 2, 4, 8} (NUMA: {1, 2, 4}).
+int32_t scan_chunks(int R, int32_t lo, int32_t hi);
+hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t lo,
+                       int32_t hi, uint16_t *S, int64_t s_stride, uint16_t *Mx, int32_t m_stride, hipStream_t s);
+// k_select: per pod the exact top-k keys of its S row (best first, 0-padded);
+// nbins = max total score + 2
+hipError_t launch_select(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,
+                         int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, uint64_t *out,
+                         uint64_t *dbg, hipStream_t s);
 // lists: ranges ascending with l, equal-score keys in ascending node order
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
                              int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s);
 template <typename T>
 hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
+// k_resolve: one round of the greedy, lag-1 (see kernels.hip); prev_mod / next_mod =
+// {count, nodes...} of the previous / this round's committed nodes.  LDS bytes it needs:
+int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t k,
-                          const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *out_cpus,
-                          uint64_t *dbg, hipStream_t s);
+                          const uint64_t *lists, int32_t monotone, const int32_t *prev_mod, int32_t *next_mod,
+                          int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg, int32_t trace_j, hipStream_t s);
 // single Reserve (sign +1, cpus <- allocated CPUs, *rc = KOORDHIP_ERESERVE on failure) / Unreserve (cpus given)
 hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const DevPod *pod, int32_t node, int32_t sign,
                          uint64_t *cpus, int32_t *rc, hipStream_t s);

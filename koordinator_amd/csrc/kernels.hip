@@ -78,6 +78,23 @@ __device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
   return readlane_u64(v, 63);
 }
 
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+// Wave max of an i32 (same DPP pattern), result uniform.
+__device__ __forceinline__ int32_t wave_max_i32_dpp(int32_t v) {
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(INT32_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 // ---------------------------------------------------------------------------
 // k_prep_flags: load_aware.go:123-254 resolved per node, plus the Fit
 // over-commit bits.  usage = int64(math.Round(float64(used)/float64(total)*100)).
@@ -155,87 +172,6 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
 }
 
 // ---------------------------------------------------------------------------
-// k_topk_partial: one wave = one pod x one chunk of 64*R nodes.
-//
-// Lane l evaluates nodes c0 + r*64 + l (r < R): every column load is a
-// coalesced 512-B (i64) or 256-B (i32) wave access, the R evaluations are
-// independent so their loads overlap.  The chunk's exact top-k is then found
-// without sorting: a radix select over the (small) total-score values with
-// wave ballots finds the k-th largest score T; every key with score > T is
-// taken and, for score == T, the lowest node indexes (r-major, lane-minor =
-// index order) up to k.  Output: k keys per (pod, chunk), unsorted, 0-padded.
-
-template <int R, bool NUMA>
-__global__ __launch_bounds__(256) void k_topk_partial(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
-                                                      int32_t n_pods, int32_t lo, int32_t hi, int32_t k,
-                                                      int32_t score_bits, uint64_t *__restrict__ out) {
-  const int lane = lane_id();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: pod fields in SGPRs
-  const int32_t p = blockIdx.y * (blockDim.x >> 6) + wave;
-  if (p >= n_pods) return;  // wave-uniform
-  const int32_t c0 = lo + blockIdx.x * (64 * R);
-  const DevPod pod = pods[p];
-  const Need need = pod_needs(pod, c);
-  int32_t s[R];  // total score + 1, 0 = infeasible / past the end
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int32_t i = c0 + r * 64 + lane;
-    s[r] = 0;
-    if (i < hi) {
-      NV v;
-      load_node(v, d, i, need, c);
-      if constexpr (NUMA) {
-        NumaRow nr;
-        load_numa(nr, d, i, need);
-        s[r] = eval_total_numa(pod, v, nr, d.nu.cls, c) + 1;
-      } else {
-        s[r] = eval_total(pod, v, c) + 1;
-      }
-    }
-  }
-  // k-th largest score value T (radix select, MSB first)
-  int32_t feasible = 0;
-#pragma unroll
-  for (int r = 0; r < R; r++) feasible += __popcll(__ballot(s[r] > 0));
-  int32_t T = 1;
-  if (feasible > k) {
-    T = 0;
-    for (int b = score_bits - 1; b >= 0; b--) {
-      const int32_t cand = T | (1 << b);
-      int32_t cnt = 0;
-#pragma unroll
-      for (int r = 0; r < R; r++) cnt += __popcll(__ballot(s[r] >= cand));
-      if (cnt >= k) T = cand;
-    }
-  }
-  // selection in node-index order
-  int32_t gt = 0;
-#pragma unroll
-  for (int r = 0; r < R; r++) gt += __popcll(__ballot(s[r] > T));
-  int32_t eq_left = k - gt;  // ties at T still to take (lowest index first)
-  int32_t base = 0;
-  const size_t list = (size_t)p * gridDim.x + blockIdx.x;
-  uint64_t *o = out + list * k;
-  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const bool eq = s[r] == T && s[r] > 0;
-    const uint64_t me = __ballot(eq);
-    const int32_t eq_rank = __popcll(me & lt);
-    const bool sel = s[r] > T || (eq && eq_rank < eq_left);
-    eq_left -= min(__popcll(me), max(eq_left, 0));
-    const uint64_t ms = __ballot(sel);
-    if (sel) {
-      const int32_t i = c0 + r * 64 + lane;
-      const uint64_t key = (((uint64_t)(uint32_t)s[r]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
-      o[base + __popcll(ms & lt)] = key;
-    }
-    base += __popcll(ms);
-  }
-  for (int32_t j = base + lane; j < k; j += 64) o[j] = 0;
-}
-
-// ---------------------------------------------------------------------------
 // k_topk_merge: per pod, the exact top-k of L lists of k keys.
 //
 // Input contract: list l holds the exact top-k of a contiguous node range,
@@ -269,7 +205,8 @@ __device__ __forceinline__ void dma_to_lds_block(void *lds, const void *src, int
 }
 
 constexpr int MERGE_THREADS = 256;
-constexpr int RES_MAXP = 64;         // max pods per round = max k
+constexpr int RES_MAXP = 128;        // max k (list length per pod)
+constexpr int RES_MAXP_ROUND = 64;   // max pods per round
 constexpr int MERGE_STAGE = 8192;    // keys staged in LDS (64 KiB)
 constexpr int MERGE_MAXL = 4096;     // lists per pod
 
@@ -423,89 +360,546 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 }
 
 // ---------------------------------------------------------------------------
-// k_resolve: sequential greedy over one round (one wave, 64 lanes).
+// k_scan: one wave = one pod x one chunk of 64*R nodes of the shard [lo, hi).
 //
-// Exactness: within a round only the nodes committed by earlier pods of the
-// round (set M, |M| <= j) differ from the snapshot the lists were built on.
-// For pod j the best unmodified node is the first list entry not in M (its
-// key is exact); the modified nodes are re-evaluated on their current rows.
-// Because |M| < k the list always holds an unmodified entry unless it ran out
-// of feasible nodes.  With monotone scoring (every enabled strategy is
-// LeastAllocated-style: a commit can only lower a node's key) a modified node
-// can only win if it ranks above that first entry, so the re-evaluation is
-// skipped when no list prefix entry is modified.
+// Lane l evaluates nodes c0 + 64r + l (r < R): every column read is a
+// coalesced 512-B (f64) / 256-B (i32) wave access and the R evaluations are
+// independent, so their loads overlap.  The result, score + 1 (0 =
+// infeasible), goes to the pod's row of the score matrix S (u16, a coalesced
+// 128-B store per r).  No selection here: k_select finds the pod's top-k from
+// S afterwards with one LDS histogram, which costs far less than a per-chunk
+// top-k list plus a merge of ~N/512 such lists.
+//
+// XCD-aware grid: workgroup b is dispatched to XCD b % 8, so the chunks are
+// split into 8 contiguous ranges and XCD x only ever touches range x: each
+// XCD's 4 MB L2 then holds its eighth of the node table (50k nodes: ~0.5 MB)
+// and the 4 x (pods/4) re-reads of a row hit L2 instead of the MALL.
 
-__device__ __forceinline__ void copy_row(NV *dst, const NV *src, int lane) {
-  constexpr int W = (int)(sizeof(NV) / 8);
-  static_assert(sizeof(NV) % 8 == 0 && W <= 64, "NV must be a whole number of 8-byte words");
-  if (lane < W) reinterpret_cast<uint64_t *>(dst)[lane] = reinterpret_cast<const uint64_t *>(src)[lane];
+template <int R, bool NUMA>
+__global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
+                                              int32_t lo, int32_t hi, int32_t nchunks, int32_t cpx,
+                                              uint16_t *__restrict__ S, int64_t s_stride,
+                                              uint16_t *__restrict__ Mx, int32_t m_stride) {
+  const int32_t b = blockIdx.x;
+  const int32_t xcd = b & 7, local = b >> 3;
+  const int32_t chunk = xcd * cpx + local % cpx;
+  const int32_t pg = local / cpx;
+  if (chunk >= nchunks) return;  // block-uniform
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: pod fields in SGPRs
+  const int32_t p = pg * 4 + wave;
+  if (p >= n_pods) return;
+  const int32_t c0 = lo + chunk * (64 * R);
+  const DevPod pod = pods[p];
+  const Need need = pod_needs(pod, c);
+  uint16_t *row = S + (size_t)p * s_stride;
+  // evaluate all R nodes first, store afterwards: the u16 stores may alias the
+  // node columns as far as the compiler knows, and a store between two
+  // evaluations would serialise their loads
+  int32_t s[R];
+  const bool full = c0 + 64 * R <= hi;  // wave-uniform
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int32_t i = c0 + r * 64 + lane;
+    s[r] = 0;
+    if (full || i < hi) {
+      NV v;
+      load_node(v, d, i, need, c);
+      if constexpr (NUMA) {
+        NumaRow nr;
+        load_numa(nr, d, i, need);
+        s[r] = eval_total_numa(pod, v, nr, d.nu.cls, c) + 1;
+      } else {
+        s[r] = eval_total(pod, v, c) + 1;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int32_t i = c0 + r * 64 + lane;
+    if (full || i < hi) col(row, i - lo) = (uint16_t)s[r];
+  }
+  // the chunk's best value: k_select's lower bound for the pod's k-th score
+  int32_t mx = s[0];
+#pragma unroll
+  for (int r = 1; r < R; r++) mx = max(mx, s[r]);
+  mx = wave_max_i32_dpp(mx);
+  if (lane == 0) Mx[(size_t)p * m_stride + chunk] = (uint16_t)mx;
 }
 
-__device__ __forceinline__ uint64_t stamp() {
-  uint64_t t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
+// ---------------------------------------------------------------------------
+// k_select: one workgroup per pod, the exact top-k of its score row.
+//
+// Keys order by (score desc, node asc), i.e. the reference's selectHost with
+// the lowest-index tie rule.  A lower bound L <= S* comes first: the k-th
+// largest of the pod's chunk maxima (k_scan), since k distinct chunks each
+// hold a node scoring >= it -- with 128-node chunks L is close to S*.  Pass 1
+// builds the histogram of the row's scores >= L in LDS (one bin per total-
+// score value, <= 30002 bins; few atomics thanks to L); the k-th largest S*
+// follows by a top-down cumulative count, and gt = #(score > S*) < k.  Pass 2
+// walks the row in node order: scores > S* go to a small LDS buffer (rank
+// sorted at the end), ties at S* are numbered by a block prefix sum so the
+// lowest k - gt indexes are taken.  Fewer than k feasible nodes -> all of
+// them (S* = the lowest feasible value).  Output: k keys, best first, 0-padded.
+
+constexpr int SEL_THREADS = 1024;
+constexpr int SEL_WAVES = SEL_THREADS / 64;
+constexpr int SEL_MAXCHUNKS = 8192;  // chunk maxima staged in LDS
+
+// inclusive block prefix sum of one value per thread (SEL_THREADS threads)
+__device__ __forceinline__ int32_t sel_scan(int32_t v, int32_t *wsum, int32_t *total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  int32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int32_t base = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < SEL_WAVES; q++) {
+    const int32_t s = wsum[q];
+    base += q < w ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x;
 }
 
-constexpr int RES_PRE = 128;  // prefetched snapshot rows per round
+// Row layout: tiles of SEL_THREADS x SEL_PER nodes; thread t owns the
+// contiguous nodes [tile + t * SEL_PER, +SEL_PER), read as SEL_ITER 16-B
+// loads issued back to back (the row comes from HBM: latency, not bandwidth,
+// bounds this kernel), so numbering per thread in thread order is node order.  The per-value tests only build bit masks (unrolled, register
+// resident); the few values that pass them are handled in a rolled loop that
+// re-reads them (L2 hits).  A one-tile row (<= 65536 nodes per shard) is
+// loaded once and kept in registers for pass 2.
+constexpr int SEL_ITER = 8;
+constexpr int SEL_PER = SEL_ITER * 8;
+constexpr int32_t SEL_TILE = SEL_THREADS * SEL_PER;
+
+__device__ __forceinline__ int32_t sel_node(int32_t tile, int t, int h) {
+  return tile * SEL_TILE + t * SEL_PER + h;
+}
+
+__device__ __forceinline__ void sel_load(const uint16_t *row, int32_t m, int32_t tile, int t, uint4 *q) {
+#pragma unroll
+  for (int j = 0; j < SEL_ITER; j++) {
+    const int32_t i = sel_node(tile, t, 8 * j);
+    if (i + 8 <= m) {
+      q[j] = *reinterpret_cast<const uint4 *>(row + i);
+    } else {
+      uint32_t w[4];
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const uint32_t a = i + 2 * h < m ? row[i + 2 * h] : 0u, b = i + 2 * h + 1 < m ? row[i + 2 * h + 1] : 0u;
+        w[h] = a | (b << 16);
+      }
+      q[j] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+// bit h of the result: value h of q satisfies (v >= lo_incl) [ge] or (v == x) [eq] / (v > x) [gt]
+__device__ __forceinline__ uint64_t sel_mask_ge(const uint4 *q, uint32_t x) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < SEL_ITER; j++) {
+    const uint32_t w4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      m |= (uint64_t)((w4[h] & 0xFFFFu) >= x) << (8 * j + 2 * h);
+      m |= (uint64_t)((w4[h] >> 16) >= x) << (8 * j + 2 * h + 1);
+    }
+  }
+  return m;
+}
+__device__ __forceinline__ uint64_t sel_mask_eq(const uint4 *q, uint32_t x) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < SEL_ITER; j++) {
+    const uint32_t w4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      m |= (uint64_t)((w4[h] & 0xFFFFu) == x) << (8 * j + 2 * h);
+      m |= (uint64_t)((w4[h] >> 16) == x) << (8 * j + 2 * h + 1);
+    }
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restrict__ S, int64_t s_stride, int32_t lo,
+                                                        int32_t m, int32_t k, int32_t nbins,
+                                                        const uint16_t *__restrict__ Mx, int32_t m_stride,
+                                                        int32_t nchunks, uint64_t *__restrict__ out,
+                                                        uint64_t *__restrict__ dbg) {
+  // dbg (diagnostic builds only, KOORDHIP_STAMPS): per-phase s_memtime sums of thread 0
+  uint64_t ts[6] = {0, 0, 0, 0, 0, 0};
+  if (dbg && threadIdx.x == 0) ts[0] = stamp();
+  extern __shared__ uint32_t hist[];  // nbins
+  __shared__ uint64_t gtbuf[RES_MAXP];
+  __shared__ uint16_t mxs[SEL_MAXCHUNKS];
+  __shared__ int32_t wsum[SEL_WAVES];
+  __shared__ int32_t sh_thr, sh_gt, sh_cnt_gt;
+  const int t = threadIdx.x, lane = lane_id();
+  const int32_t p = blockIdx.x;
+  const uint16_t *row = S + (size_t)p * s_stride;
+  const int32_t ntiles = (m + SEL_TILE - 1) / SEL_TILE;
+  // first tile in flight while the lower bound is computed
+  uint4 q[SEL_ITER];
+  sel_load(row, m, 0, t, q);
+  for (int32_t j = t; j < nbins; j += SEL_THREADS) hist[j] = 0;
+  if (t == 0) sh_cnt_gt = 0;
+  // ---- lower bound L: k-th largest chunk maximum (radix select, MSB first)
+  uint32_t L = 1;
+  if (nchunks >= k) {
+    const uint16_t *mrow = Mx + (size_t)p * m_stride;
+    for (int32_t j = t; j < nchunks; j += SEL_THREADS) mxs[j] = mrow[j];
+    __syncthreads();
+    const int bits = 32 - __builtin_clz((uint32_t)(nbins - 1));
+    uint32_t acc = 0;
+    for (int b = bits - 1; b >= 0; b--) {
+      const uint32_t cand = acc | (1u << b);
+      int32_t cnt = 0;
+      for (int32_t j = t; j < nchunks; j += SEL_THREADS) cnt += (uint32_t)mxs[j] >= cand;
+      int32_t total;
+      (void)sel_scan(cnt, wsum, &total);
+      if (total >= k) acc = cand;
+    }
+    L = acc > 1 ? acc : 1;
+  }
+  __syncthreads();
+  if (dbg && t == 0) ts[1] = stamp();
+  // ---- pass 1: histogram of the scores >= L
+  for (int32_t tile = 0; tile < ntiles; tile++) {
+    if (tile > 0) sel_load(row, m, tile, t, q);
+    uint64_t hit = sel_mask_ge(q, L);
+    while (hit) {
+      const int h = __builtin_ctzll(hit);
+      hit &= hit - 1;
+      atomicAdd(&hist[row[sel_node(tile, t, h)]], 1u);
+    }
+  }
+  __syncthreads();
+  if (dbg && t == 0) ts[2] = stamp();
+  // ---- k-th largest value S*: wave 0 walks the bins top-down, 64 at a time
+  if (t < 64) {
+    int32_t cum = 0, thr = 0, gt = 0;
+    for (int32_t top = nbins - 1; top >= (int32_t)L && thr == 0; top -= 64) {
+      const int32_t v = top - lane;
+      const int32_t c = v >= (int32_t)L ? (int32_t)hist[v] : 0;
+      if (__ballot(c != 0) == 0) continue;  // wave-uniform
+      int32_t x = c;  // inclusive prefix over lanes = bins top, top-1, ...
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      const uint64_t hit = __ballot(c != 0 && cum + x >= k);
+      if (hit) {
+        const int l = __builtin_ctzll(hit);
+        thr = top - l;
+        gt = cum + __shfl(x, l, 64) - __shfl(c, l, 64);
+      } else {
+        cum += __shfl(x, 63, 64);
+      }
+    }
+    if (thr == 0) {  // fewer than k feasible (then L == 1): take every feasible node
+      thr = 1;
+      gt = 0;
+      for (int32_t v = 2 + lane; v < nbins; v += 64) gt += (int32_t)hist[v];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) gt += __shfl_xor(gt, off, 64);
+    }
+    if (lane == 0) {
+      sh_thr = thr;
+      sh_gt = gt;
+    }
+  }
+  __syncthreads();
+  if (dbg && t == 0) ts[3] = stamp();
+  const uint32_t thr = (uint32_t)sh_thr;
+  const int32_t gt = sh_gt, need = k - gt;
+  uint64_t *o = out + (size_t)p * k;
+  // ---- pass 2: scores > S* (fewer than k) and the lowest-index ties at S*
+  int32_t ties = 0;  // ties numbered so far (block-uniform)
+  for (int32_t tile = 0; tile < ntiles; tile++) {
+    if (ntiles > 1) sel_load(row, m, tile, t, q);
+    const uint64_t above = sel_mask_ge(q, thr + 1);
+    uint64_t eq = sel_mask_eq(q, thr);
+    for (uint64_t x = above; x;) {
+      const int h = __builtin_ctzll(x);
+      x &= x - 1;
+      const int32_t i = sel_node(tile, t, h);
+      const int32_t pos = atomicAdd(&sh_cnt_gt, 1);
+      gtbuf[pos] = ((uint64_t)row[i] << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(lo + i));
+    }
+    const int32_t mine = __popcll(eq);
+    int32_t total;
+    int32_t pos = ties + sel_scan(mine, wsum, &total) - mine;
+    while (eq && pos < need) {  // ties in node order: thread-major, then h
+      const int h = __builtin_ctzll(eq);
+      eq &= eq - 1;
+      o[gt + pos] = ((uint64_t)thr << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(lo + sel_node(tile, t, h)));
+      pos++;
+    }
+    ties += total;
+    if (ties >= need && sh_cnt_gt >= gt) break;  // uniform: read after sel_scan's barriers, before any later add
+    __syncthreads();
+  }
+  __syncthreads();
+  if (dbg && t == 0) ts[4] = stamp();
+  // ---- gt keys in descending order, then pad
+  for (int32_t j = t; j < gt; j += SEL_THREADS) {
+    const uint64_t x = gtbuf[j];
+    int32_t rank = 0;
+    for (int32_t q2 = 0; q2 < gt; q2++) rank += gtbuf[q2] > x;
+    o[rank] = x;
+  }
+  const int32_t filled = gt + min(need, ties);
+  for (int32_t j = filled + t; j < k; j += SEL_THREADS) o[j] = 0;
+  if (dbg && t == 0) {
+    ts[5] = stamp();
+    for (int q2 = 1; q2 < 6; q2++) atomicAdd((unsigned long long *)&dbg[8 + q2], (unsigned long long)(ts[q2] - ts[q2 - 1]));
+    atomicAdd((unsigned long long *)&dbg[8], 1ull);
+  }
+  (void)lane;
+}
+
+// ---------------------------------------------------------------------------
+// k_resolve: the sequential greedy over one round of n_pods <= 64 pods,
+// lag-1 pipelined with the evaluation of the next round.
+//
+// The round's lists (k >= 2 * round size keys per pod, the exact top-k of the
+// scanned nodes) were built by k_scan/k_select WHILE the previous round's
+// resolve ran on another stream: they are exact for every node except M' =
+// the nodes that round committed to, whose columns k_scan may even have read
+// half-updated.  A Reserve only raises the columns a key depends on and every
+// enabled score is non-increasing in them (a "monotone" config), so such a
+// stale key is an upper bound of the node's current key.
+//
+// Prologue (16 waves): lists -> LDS; the rows of M' -> LDS (+ node -> slot
+// hash); every list entry on an M' node is re-evaluated on its current row;
+// each list is re-sorted (bitonic).  Every list key is now exact at the start
+// of the round, and a node outside a list scores <= its k-th stale key.
+//
+// Loop (wave 0, s_setprio 3): pod j's candidate is its first list entry not
+// in M = the nodes committed in THIS round (lane-owned rows in registers).
+// Since |M' u M| < k, a full list always has an entry outside M' u M, whose
+// key (exact) bounds every node outside the list, so the candidate beats
+// every node outside M.  A node of M can only win if it ranks above the
+// candidate in the list (its list key bounds its current key), and only then
+// are M's rows re-evaluated (one row per lane, wave max).  Pods whose
+// feasibility is not monotone (NodeNUMAResource required SpreadByPCPUs)
+// re-evaluate M and M' every time.  The winner's Reserve delta is applied to
+// its lane-owned row; rows of M are written back at the end and M is handed
+// to the next round as its M'.
+
+// NUMA builds run the (register-hungry) accumulator replay in wave 0: 4 waves
+// keep 512 VGPRs available to it; otherwise 16 waves for a faster prologue.
+template <bool NUMA>
+constexpr int res_threads() { return NUMA ? 256 : 1024; }
+constexpr int RES_PRE = 128;   // prefetched rows of list heads
+constexpr int RES_HASH = 256;  // node -> M' slot (open addressing)
+constexpr int RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (static LDS: a few flags)
+
+struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
+  int32_t lists, prev_rows, prev_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node, modmap, total;
+};
+
+__host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
+
+__host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, bool numa) {
+  ResLds o;
+  int32_t at = 0;
+  o.lists = at;
+  at += res_align(n_pods_max * kp * 8);
+  o.prev_rows = at;
+  at += res_align(RES_MAXP_ROUND * (int32_t)sizeof(NV));
+  o.prev_numa = at;
+  at += numa ? res_align(RES_MAXP_ROUND * (int32_t)sizeof(NumaRow)) : 0;
+  o.hash_node = at;
+  at += RES_HASH * 4;
+  o.hash_slot = at;
+  at += RES_HASH * 4;
+  o.pre_rows = at;
+  at += res_align(RES_PRE * (int32_t)sizeof(NV));
+  o.pre_numa = at;
+  at += numa ? res_align(RES_PRE * (int32_t)sizeof(NumaRow)) : 0;
+  o.pre_node = at;
+  at += RES_PRE * 4;
+  o.modmap = at;
+  at += res_align(((n_nodes + 31) >> 5) * 4);
+  o.total = at;
+  return o;
+}
+
+__device__ __forceinline__ uint32_t res_hash(int32_t node) { return ((uint32_t)node * 2654435761u) >> 24; }
 
 template <bool NUMA>
-__global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
-                                                int32_t n_pods, int32_t k, const uint64_t *__restrict__ lists,
-                                                int32_t monotone, int32_t *__restrict__ out_node,
-                                                uint64_t *__restrict__ out_cpus, uint64_t *__restrict__ dbg) {
-  // dbg (diagnostic builds only, KOORDHIP_STAMPS): s_memtime segment sums
-  uint64_t t_entry = dbg ? stamp() : 0, t_a = 0, t_b = 0, t_c = 0, t_mark = 0, n_eval = 0, n_miss = 0;
-  __shared__ __attribute__((aligned(16))) uint64_t lk[RES_MAXP * RES_MAXP];
-  __shared__ __attribute__((aligned(16))) DevPod lp[RES_MAXP + 16];
-  // Prefetched snapshot rows: slot t holds pod (t % n_pods)'s list entry at
-  // position t / n_pods.  A round's winner is either a node already modified
-  // in the round (kept in registers) or its pod's first unmodified list
-  // entry, which is nearly always among the first few positions.
-  __shared__ NV pre[RES_PRE];
-  __shared__ int32_t pre_node[RES_PRE];
-  extern __shared__ uint32_t modmap[];  // one bit per node: committed this round
-  const int lane = lane_id();
-  // LDS-DMA the round's lists and pod records (buffers are padded to 1 KiB)
-  dma_to_lds(lk, lists, ((n_pods * k * 8) + 1023) & ~1023, lane);
-  dma_to_lds(lp, pods, ((n_pods * (int32_t)sizeof(DevPod)) + 1023) & ~1023, lane);
+__global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
+                                                         int32_t n_pods, int32_t k, int32_t kp,
+                                                         const uint64_t *__restrict__ lists, int32_t monotone,
+                                                         const int32_t *__restrict__ prev_mod,
+                                                         int32_t *__restrict__ next_mod, ResLds ofs,
+                                                         int32_t *__restrict__ out_node,
+                                                         uint64_t *__restrict__ out_cpus, uint64_t *__restrict__ dbg,
+                                                         int32_t trace_j) {
+  constexpr int RES_THREADS = res_threads<NUMA>();
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  uint64_t *lk = reinterpret_cast<uint64_t *>(lds + ofs.lists);
+  NV *prow = reinterpret_cast<NV *>(lds + ofs.prev_rows);
+  NumaRow *pnr = reinterpret_cast<NumaRow *>(lds + ofs.prev_numa);
+  int32_t *hnode = reinterpret_cast<int32_t *>(lds + ofs.hash_node);
+  int32_t *hslot = reinterpret_cast<int32_t *>(lds + ofs.hash_slot);
+  NV *pre = reinterpret_cast<NV *>(lds + ofs.pre_rows);
+  NumaRow *prenr = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa);
+  int32_t *pre_node = reinterpret_cast<int32_t *>(lds + ofs.pre_node);
+  uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
+  const int t = threadIdx.x, lane = lane_id();
+  const uint64_t t_entry = (dbg && t == 0) ? stamp() : 0;
+  const int32_t mp = min(prev_mod[0], (int32_t)RES_MAXP_ROUND);  // |M'|
+  // ---- 1. lists -> LDS (stride kp, zero padded), M' rows -> LDS, clear maps
+  __shared__ int32_t bad;
+  if (t == 0) bad = 0;
+  __syncthreads();
+  for (int32_t x = t; x < n_pods * kp; x += RES_THREADS) {
+    const int32_t j = x / kp, q = x - j * kp;
+    const uint64_t e = q < k ? lists[(size_t)j * k + q] : 0ull;
+    if (e != 0 && (uint32_t)key_node(e) >= (uint32_t)d.n) bad = 1 + x;
+    lk[x] = e;
+  }
+  if (t <= mp && t > 0 && (uint32_t)prev_mod[t] >= (uint32_t)d.n) bad = -1000 - t;
+  __syncthreads();
+  if (bad) {  // broken input contract: report, touch nothing
+    for (int32_t j = t; j < n_pods; j += RES_THREADS) out_node[j] = -1000000 - bad;
+    if (t == 0) next_mod[0] = 0;
+    return;
+  }
+  for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
   const int32_t words = (d.n + 31) >> 5;
-  for (int32_t j = lane; j < words; j += 64) modmap[j] = 0;
-  for (int32_t t = lane; t < RES_PRE; t += 64) {
+  for (int32_t x = t; x < words; x += RES_THREADS) modmap[x] = 0;
+  if (t < mp) {
+    const int32_t nd = prev_mod[1 + t];
+    NV v;
+    load_row(v, d, nd);
+    prow[t] = v;
+    if constexpr (NUMA) {
+      NumaRow r;
+      load_numa_row(r, d, nd);
+      pnr[t] = r;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {  // M' hash (<= 64 inserts, serial: no insert races)
+    for (int32_t s = 0; s < mp; s++) {
+      const int32_t nd = prev_mod[1 + s];
+      uint32_t h = res_hash(nd);
+      while (hnode[h] >= 0) h = (h + 1) & (RES_HASH - 1);
+      hnode[h] = nd;
+      hslot[h] = s;
+    }
+  }
+  __syncthreads();
+  auto prev_slot = [&](int32_t nd) -> int32_t {
+    uint32_t h = res_hash(nd);
+    for (;;) {
+      const int32_t x = hnode[h];
+      if (x == nd) return hslot[h];
+      if (x < 0) return -1;
+      h = (h + 1) & (RES_HASH - 1);
+    }
+  };
+  // ---- 2. refresh the keys of list entries on M' nodes (exact, current rows)
+  if (mp > 0) {
+    for (int32_t x = t; x < n_pods * kp; x += RES_THREADS) {
+      const uint64_t e = lk[x];
+      if (e == 0) continue;
+      const int32_t nd = key_node(e);
+      const int32_t s = prev_slot(nd);
+      if (s < 0) continue;
+      const int32_t j = x / kp;
+      const DevPod pod = pods[j];
+      int32_t tot;
+      if constexpr (NUMA) {
+        tot = eval_total_numa(pod, prow[s], pnr[s], d.nu.cls, c);
+      } else {
+        tot = eval_total(pod, prow[s], c);
+      }
+      lk[x] = make_key(tot, nd);
+    }
+    __syncthreads();
+    // ---- 3. bitonic sort of every list, descending
+    const int32_t half = n_pods * (kp >> 1);
+    for (int32_t size = 2; size <= kp; size <<= 1) {
+      for (int32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int32_t x = t; x < half; x += RES_THREADS) {
+          const int32_t j = x / (kp >> 1), i = x - j * (kp >> 1);
+          const int32_t a = 2 * stride * (i / stride) + (i % stride), b = a + stride;
+          uint64_t *L = lk + (size_t)j * kp;
+          const uint64_t va = L[a], vb = L[b];
+          const bool desc = (a & size) == 0;
+          if (desc ? va < vb : va > vb) {
+            L[a] = vb;
+            L[b] = va;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  // ---- 4. prefetch the rows of the list heads: slot s = pod s % n, position s / n
+  if (t < RES_PRE) {
     const int32_t j = t % n_pods, q = t / n_pods;
     int32_t nd = -1;
     if (q < k) {
-      const uint64_t e = lists[(size_t)j * k + q];
+      const uint64_t e = lk[(size_t)j * kp + q];
       if (e != 0) nd = key_node(e);
     }
     if (nd >= 0) {
       NV v;
       load_row(v, d, nd);
       pre[t] = v;
+      if constexpr (NUMA) {
+        NumaRow r;
+        load_numa_row(r, d, nd);
+        prenr[t] = r;
+      }
     }
     pre_node[t] = nd;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (t >= 64) return;  // the sequential part is wave 0's
+  __builtin_amdgcn_s_setprio(3);
   const uint64_t t_pro = dbg ? stamp() : 0;
-  // Lane r owns modified row r in registers (evaluated and committed in place).
+  uint64_t n_eval = 0, n_miss = 0;
   NV my{};
-  NumaRow mynr{};  // ... and its NodeNUMAResource state (NUMA builds)
+  NumaRow mynr{};
   int32_t my_node = -1;
-  int32_t nm = 0;  // modified rows this round (wave-uniform)
-  uint64_t e = lane < k ? lk[lane] : 0;
-  bool mod = false;
+  int32_t nm = 0;  // |M| (wave-uniform)
+  const bool two = k > 64;
   for (int32_t j = 0; j < n_pods; j++) {
-    if (dbg) t_mark = stamp();
-    const DevPod pod = lp[j];
-    const uint64_t free_mask = __ballot(e != 0 && !mod);
-    const int first = free_mask ? __builtin_ctzll(free_mask) : 64;
-    const uint64_t cand = free_mask ? readlane_u64(e, first) : 0;
-    uint64_t best = cand;
-    const bool prefix_modified = __ballot(e != 0 && mod && lane < first) != 0;
-    // Speculatively stage the row of `cand` (the winner whenever the winner is
-    // not an already-modified node) into lane nm, the owner such a new row
-    // gets; the LDS/global latency overlaps the re-evaluation below.
+    const DevPod pod = pods[j];  // uniform index: scalar loads
+    const uint64_t *L = lk + (size_t)j * kp;
+    const uint64_t e0 = lane < k ? L[lane] : 0ull;  // lanes past k hold nothing (k may be < 64)
+    const uint64_t e1 = two && 64 + lane < k ? L[64 + lane] : 0ull;
+    bool mod0 = false, mod1 = false;
+    if (e0) {
+      const int32_t nd = key_node(e0);
+      mod0 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+    }
+    if (e1) {
+      const int32_t nd = key_node(e1);
+      mod1 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+    }
+    const uint64_t f0 = __ballot(e0 != 0 && !mod0), f1 = __ballot(e1 != 0 && !mod1);
+    const int first = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
+    const uint64_t cand = first < 64 ? readlane_u64(e0, first) : (first < 128 ? readlane_u64(e1, first - 64) : 0ull);
+    const bool prefix_modified =
+        (__ballot(e0 != 0 && mod0 && lane < first) | __ballot(e1 != 0 && mod1 && lane + 64 < first)) != 0;
+    // stage the candidate's row into lane nm (the owner a new row gets)
     int32_t staged = -1;
     if (cand != 0) {
       const int32_t cn = key_node(cand);
@@ -513,39 +907,60 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const DevP
       const uint64_t pm1 = __ballot(pre_node[lane + 64] == cn);
       const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
       if (src >= 0) {
-        if (lane == nm) my = pre[src];
+        if (lane == nm) {
+          my = pre[src];
+          if constexpr (NUMA) {
+            mynr = prenr[src];
+          }
+        }
       } else {
         n_miss++;
-        if (lane == nm) load_row(my, d, cn);
-      }
-      if constexpr (NUMA) {
-        if (lane == nm) load_numa_row(mynr, d, cn);
+        if (lane == nm) {
+          load_row(my, d, cn);
+          if constexpr (NUMA) load_numa_row(mynr, d, cn);
+        }
       }
       staged = cn;
     }
-    if (dbg) {
-      const uint64_t t = stamp();
-      t_a += t - t_mark;
-      t_mark = t;
-    }
-    // a required-policy cpuset pod's NUMA feasibility is not monotone in the
-    // node's free CPUs (numa_spread_ok): re-evaluate the modified rows for it
-    const bool nonmono = NUMA && is_cpuset(pod) && KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE;
-    if (nm > 0 && (!monotone || prefix_modified || nonmono)) {
+    const bool nonmono = !monotone || (NUMA && is_cpuset(pod) && KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
+    uint64_t best = cand;
+    if (nm > 0 && (prefix_modified || nonmono)) {
       uint64_t key = 0;
-      if constexpr (NUMA) {
-        if (lane < nm) key = make_key(eval_total_numa(pod, my, mynr, d.nu.cls, c), my_node);
-      } else {
-        if (lane < nm) key = make_key(eval_total(pod, my, c), my_node);
+      if (lane < nm) {
+        if constexpr (NUMA) {
+          key = make_key(eval_total_numa(pod, my, mynr, d.nu.cls, c), my_node);
+        } else {
+          key = make_key(eval_total(pod, my, c), my_node);
+        }
       }
       key = wave_max_u64_dpp(key);
       best = key > best ? key : best;
       n_eval++;
     }
-    if (dbg) {
-      const uint64_t t = stamp();
-      t_b += t - t_mark;
-      t_mark = t;
+    if (nonmono && mp > 0) {  // M' nodes outside M: current rows in LDS
+      uint64_t key = 0;
+      if (lane < mp) {
+        const int32_t nd = prev_mod[1 + lane];
+        const bool in_m = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+        if (!in_m) {
+          if constexpr (NUMA) {
+            key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], d.nu.cls, c), nd);
+          } else {
+            key = make_key(eval_total(pod, prow[lane], c), nd);
+          }
+        }
+      }
+      key = wave_max_u64_dpp(key);
+      best = key > best ? key : best;
+    }
+    if (j == trace_j) {  // diagnostics (KOORDHIP_TRACE_POD)
+      if (lane == 0)
+        printf("[trace] j=%d cand=%d/%d first=%d best=%d/%d nm=%d mp=%d nonmono=%d prefix=%d\n", j,
+               cand ? key_node(cand) : -1, cand ? key_score(cand) : -1, first, best ? key_node(best) : -1,
+               best ? key_score(best) : -1, nm, mp, (int)nonmono, (int)prefix_modified);
+      if (lane < nm) printf("[trace] M lane %d node %d\n", lane, my_node);
+      if (lane < mp) printf("[trace] M' lane %d node %d\n", lane, prev_mod[1 + lane]);
+      if (lane < 8) printf("[trace] list %d: %d/%d mod %d\n", lane, e0 ? key_node(e0) : -1, e0 ? key_score(e0) : -1, (int)mod0);
     }
     uint64_t cpus[NW] = {0, 0, 0, 0};
     if (best == 0) {
@@ -553,27 +968,27 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const DevP
     } else {
       const int32_t w = key_node(best);
       const uint64_t hit = __ballot(lane < nm && my_node == w);
-      // w is either a modified row (lane `hit`) or new this round, hence pod j's
-      // first unmodified list entry, whose row lane nm already staged
+      // w is a row of M (lane `hit`) or new this round: then it is the staged
+      // candidate, or (non-monotone pods only) an M' node
       const int32_t r = hit ? __builtin_ctzll(hit) : nm;
-      if (!hit && staged != w && lane == r) {  // unreachable by construction; kept for safety
+      if (!hit && staged != w && lane == r) {
         load_row(my, d, w);
         if constexpr (NUMA) load_numa_row(mynr, d, w);
       }
       bool ok = true;
       if constexpr (NUMA) {
         if (numa_on(c) && is_cpuset(pod)) {
-          // NodeNUMAResource Reserve: every lane replays the accumulator on row r
-          NumaRow br;
-          br.cls = __builtin_amdgcn_readlane(mynr.cls, r);
-          br.nflags = (uint32_t)__builtin_amdgcn_readlane((int)mynr.nflags, r);
-          br.cnt = __builtin_amdgcn_readlane(mynr.cnt, r);
-          for (int q = 0; q < NW; q++) {
-            br.fr[q] = readlane_u64(mynr.fr[q], r);
-            br.ep[q] = readlane_u64(mynr.ep[q], r);
-            br.en[q] = readlane_u64(mynr.en[q], r);
-          }
-          ok = br.cls >= 0 && numa_allocate(d.nu.cls[br.cls], br, pod, cpus);
+          // NodeNUMAResource Reserve: lane r replays the accumulator on its row,
+          // the chosen CPUs are broadcast to the wave
+          uint64_t mc[NW] = {0, 0, 0, 0};
+          int okl = 0;
+          if (lane == r) okl = mynr.cls >= 0 && numa_allocate(d.nu.cls[mynr.cls], mynr, pod, mc);
+          ok = __builtin_amdgcn_readlane(okl, r) != 0;
+#pragma unroll
+          for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], r);
+          if (j == trace_j && lane == 0)
+            printf("[trace] reserve node %d ok %d cpus %llx %llx %llx %llx\n", w, (int)ok, (unsigned long long)cpus[0],
+                   (unsigned long long)cpus[1], (unsigned long long)cpus[2], (unsigned long long)cpus[3]);
         }
       }
       if (!ok) {
@@ -597,27 +1012,16 @@ __global__ __launch_bounds__(64) void k_resolve(DevCfg c, DevNodes d, const DevP
     }
     if (out_cpus && lane < NW)
       out_cpus[(size_t)j * NW + lane] = lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
-    // next pod's list against the state after pod j's commit
-    if (j + 1 < n_pods) {
-      e = lane < k ? lk[(j + 1) * k + lane] : 0;
-      mod = false;
-      if (e != 0) {
-        const int32_t nd = key_node(e);
-        mod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-      }
-    }
-    if (dbg) t_c += stamp() - t_mark;
   }
   if (lane < nm) {
     store_row(my, d, my_node);
     if constexpr (NUMA) store_numa_row(mynr, d, my_node);
+    next_mod[1 + lane] = my_node;
   }
+  if (lane == 0) next_mod[0] = nm;
   if (dbg && lane == 0) {
     const uint64_t t_end = stamp();
     atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)(t_pro - t_entry));
-    atomicAdd((unsigned long long *)&dbg[1], (unsigned long long)t_a);
-    atomicAdd((unsigned long long *)&dbg[2], (unsigned long long)t_b);
-    atomicAdd((unsigned long long *)&dbg[3], (unsigned long long)t_c);
     atomicAdd((unsigned long long *)&dbg[4], (unsigned long long)(t_end - t_entry));
     atomicAdd((unsigned long long *)&dbg[5], (unsigned long long)n_eval);
     atomicAdd((unsigned long long *)&dbg[6], (unsigned long long)n_miss);
@@ -694,28 +1098,53 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const DevPod *po
   return hipGetLastError();
 }
 
-hipError_t launch_topk_partial(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods,
-                               int32_t lo, int32_t hi, int32_t nchunks, int32_t k, int32_t score_bits,
-                               uint64_t *out, hipStream_t s) {
-  dim3 grid(nchunks, (n_pods + 3) / 4);
+int32_t scan_chunks(int R, int32_t lo, int32_t hi) { return hi > lo ? (hi - lo + 64 * R - 1) / (64 * R) : 0; }
+
+hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t lo,
+                       int32_t hi, uint16_t *S, int64_t s_stride, uint16_t *Mx, int32_t m_stride, hipStream_t s) {
+  if (n_pods <= 0 || hi <= lo) return hipSuccess;
   const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
-#define KH_PARTIAL(RR, NN) \
-  hipLaunchKernelGGL((k_topk_partial<RR, NN>), grid, dim3(256), 0, s, c, d, pods, n_pods, lo, hi, k, score_bits, out)
+  const int32_t nchunks = scan_chunks(R, lo, hi);
+  const int32_t cpx = (nchunks + 7) / 8;
+  const int32_t blocks = 8 * cpx * ((n_pods + 3) / 4);
+#define KH_SCAN(RR, NN)                                                                                          \
+  hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), 0, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, S, \
+                     s_stride, Mx, m_stride)
   if (numa) {
     switch (R) {
-      case 1: KH_PARTIAL(1, true); break;
-      case 2: KH_PARTIAL(2, true); break;
-      default: KH_PARTIAL(4, true); break;
+      case 1: KH_SCAN(1, true); break;
+      case 2: KH_SCAN(2, true); break;
+      case 4: KH_SCAN(4, true); break;
+      default: return hipErrorInvalidValue;
     }
   } else {
     switch (R) {
-      case 1: KH_PARTIAL(1, false); break;
-      case 2: KH_PARTIAL(2, false); break;
-      case 4: KH_PARTIAL(4, false); break;
-      default: KH_PARTIAL(8, false); break;
+      case 1: KH_SCAN(1, false); break;
+      case 2: KH_SCAN(2, false); break;
+      case 4: KH_SCAN(4, false); break;
+      case 8: KH_SCAN(8, false); break;
+      default: return hipErrorInvalidValue;
     }
   }
-#undef KH_PARTIAL
+#undef KH_SCAN
+  return hipGetLastError();
+}
+
+hipError_t launch_select(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,
+                         int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, uint64_t *out,
+                         uint64_t *dbg, hipStream_t s) {
+  if (n_pods <= 0) return hipSuccess;
+  if (k < 1 || k > RES_MAXP || nbins < 2 || nbins > 32768) return hipErrorInvalidValue;
+  if (nchunks > SEL_MAXCHUNKS) nchunks = 0;  // no lower bound: histogram the whole row
+  const size_t lds = (size_t)nbins * sizeof(uint32_t);
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void *)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_select, dim3(n_pods), dim3(SEL_THREADS), lds, s, S, s_stride, lo, m, k, nbins, Mx, m_stride,
+                     nchunks, out, dbg);
   return hipGetLastError();
 }
 
@@ -727,16 +1156,35 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
   return hipGetLastError();
 }
 
+int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa) {
+  int32_t kp = 1;
+  while (kp < k) kp <<= 1;
+  return res_lds(n_pods_max, kp, n_nodes, numa).total;
+}
+
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t k,
-                          const uint64_t *lists, int32_t monotone, int32_t *out_node, uint64_t *out_cpus,
-                          uint64_t *dbg, hipStream_t s) {
-  const size_t bitmap = (size_t)((d.n + 31) >> 5) * sizeof(uint32_t);
-  if ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA)
-    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone, out_node,
-                       out_cpus, dbg);
+                          const uint64_t *lists, int32_t monotone, const int32_t *prev_mod, int32_t *next_mod,
+                          int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg, int32_t trace_j, hipStream_t s) {
+  if (n_pods <= 0) return hipSuccess;
+  if (n_pods > RES_MAXP_ROUND || k > RES_MAXP || k < 1) return hipErrorInvalidValue;
+  int32_t kp = 1;
+  while (kp < k) kp <<= 1;
+  const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
+  const ResLds o = res_lds(n_pods, kp, d.n, numa);
+  static bool attr[2] = {false, false};
+  if (!attr[numa]) {
+    const void *f = numa ? (const void *)k_resolve<true> : (const void *)k_resolve<false>;
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS_MAX);
+    if (e != hipSuccess) return e;
+    attr[numa] = true;
+  }
+  if (o.total > RES_LDS_MAX) return hipErrorInvalidValue;
+  if (numa)
+    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(res_threads<true>()), o.total, s, c, d, pods, n_pods, k, kp, lists,
+                       monotone, prev_mod, next_mod, o, out_node, out_cpus, dbg, trace_j);
   else
-    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(64), bitmap, s, c, d, pods, n_pods, k, lists, monotone,
-                       out_node, out_cpus, dbg);
+    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(res_threads<false>()), o.total, s, c, d, pods, n_pods, k, kp, lists,
+                       monotone, prev_mod, next_mod, o, out_node, out_cpus, dbg, trace_j);
   return hipGetLastError();
 }
 

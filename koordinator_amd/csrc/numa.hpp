@@ -71,7 +71,7 @@ __device__ __forceinline__ int popc_and(const uint64_t *a, const uint64_t *b) {
 }
 
 // strategy direction of a free-score comparison: MostAllocated -> ascending
-__device__ __forceinline__ bool free_before(bool most, int x, int y) { return most ? x < y : x > y; }
+__device__ __forceinline__ bool free_before(int most, int x, int y) { return (most ? y - x : x - y) > 0; }
 
 __device__ __forceinline__ int node_policy(uint32_t nflags, int preferred) {
   const uint32_t p = nflags & KOORDHIP_NODE_CPUBIND_MASK;  // getPreferredCPUBindPolicy, plugin.go:546-566
@@ -104,7 +104,7 @@ __device__ __forceinline__ int cores_in(const uint64_t *m, const uint64_t *g, in
 // per core.  Stages follow cpu_accumulator.go:184-229; a stage that finds a
 // group big enough returns immediately, with distinct cores iff the group has
 // that many distinct cores (spreadCPUs takes one CPU per core first).
-__device__ bool numa_spread_ok(const DevNumaClass &C, const NumaRow &r, int need, int excl, bool most) {
+__device__ __attribute__((noinline, optnone)) bool numa_spread_ok(const DevNumaClass &C, const NumaRow &r, int need, int excl, bool most) {
   const int cpc = C.cpc;
   uint64_t X[NW], Xp[NW], F[NW];
   excluded_set(C, r, excl, false, X);
@@ -209,6 +209,15 @@ __device__ __forceinline__ int32_t numa_la(double rc, double ac, double rm, doub
 
 // ---------------------------------------------------------------------------
 // Exact accumulator replay for Reserve (cpu_accumulator.go:87-232, mask form).
+//
+// The non-inline functions of the replay (and numa_spread_ok) are built
+// noinline + optnone: with ROCm 7.2's optimizer (-O2 and -O3 alike) the node /
+// socket selection loops came out wrong once inlined into the 1-wave resolve
+// kernel (a different NUMA node than the reference's order picks; inserting a
+// printf or making the running best volatile "fixed" it, i.e. an optimizer
+// miscompile, not a data race).  These paths run once per cpuset Reserve and
+// for required-SpreadByPCPUs Filters only, so the unoptimized code costs
+// little; tests/test_gpu_numa.py pins every choice bit for bit.
 
 struct Acc {
   uint64_t A[NW];   // allocatable
@@ -216,7 +225,7 @@ struct Acc {
   uint64_t XC[NW];  // exclusiveInCores (lead bits)
   uint32_t XN;      // exclusiveInNUMANodes
   int need, excl;
-  bool most;
+  int most;  // 1: MostAllocated (ascending free), 0: LeastAllocated
 };
 
 __device__ __forceinline__ bool tbit(const uint64_t *m, int p) { return (m[p >> 6] >> (p & 63)) & 1ull; }
@@ -260,7 +269,7 @@ __device__ __forceinline__ void acc_excluded(const DevNumaClass &C, const Acc &a
 // spread order of the CPUs of m listed in ascending CPU id (freeCPUsInNode /
 // freeCPUsInSocket + spreadCPUs): round t takes each core's t-th CPU by id,
 // rounds in id order; lists of <= cpc CPUs are kept in id order.  Takes n.
-__device__ void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
+__device__ __attribute__((noinline, optnone)) void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
   const int len = popc4(m);
   if (len <= C.cpc) {
     for (int i = 0; i < C.ncpu && n > 0; i++) {
@@ -289,7 +298,7 @@ __device__ void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint6
 }
 
 // freeCPUs(filterExclusive) + spreadCPUs + one-by-one take (:218-229).
-__device__ void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
+__device__ __attribute__((noinline, optnone)) void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
   uint64_t X[NW], F[NW];
   if (fe) acc_excluded(C, a, false, X);
   else
@@ -374,7 +383,7 @@ __device__ void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
 }
 
 // takeCPUs; returns true with a.R filled.
-__device__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
+__device__ __attribute__((noinline, optnone)) bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
   if (a.need < 1) return true;
   if (a.need > popc4(a.A)) return false;
   const int cpc = C.cpc;
@@ -569,7 +578,7 @@ __device__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
 }
 
 // Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
-__device__ bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
+__device__ __attribute__((noinline, optnone)) bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
   for (int w = 0; w < NW; w++) cpus[w] = 0;
   const int need = p.numa_cpus;
   if (popc4(r.fr) < need) return false;
@@ -584,7 +593,7 @@ __device__ bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const Dev
     if (popc_and(r.en, C.nm[k])) a.XN |= 1u << k;
   a.need = need;
   a.excl = (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy);
-  a.most = (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0;
+  a.most = (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) ? 1 : 0;
   const int pol = node_policy(r.nflags, (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy));
   if (!acc_take_cpus(C, a, pol)) return false;
   if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE) {  // satisfiedRequiredCPUBindPolicy
