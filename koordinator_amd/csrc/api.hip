@@ -40,7 +40,7 @@ int fail(int code, const std::string &msg) {
     if (_r != ncclSuccess) return fail(KOORDHIP_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
   } while (0)
 
-constexpr int kDefaultBatch = 64;
+constexpr int kDefaultBatch = 32;
 constexpr int32_t kMaxNodes = 400000;  // the resolve keeps a per-node bit in LDS (next to 2 x 64 x 128 list keys)
 constexpr int kMaxBatch = 64;
 constexpr int kRing = 4;               // per-round events in flight (lag-1 pipeline needs 3)
@@ -943,10 +943,12 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[8], (unsigned long long)h[9], (unsigned long long)h[10],
                  (unsigned long long)h[11], (unsigned long long)h[12], (unsigned long long)h[13]);
     std::fprintf(stderr,
-                 "[koordhip stamps] resolve cycles: prologue %llu  kernel %llu  | re-evals %llu prefetch-misses %llu "
-                 "pods %llu\n",
-                 (unsigned long long)h[0], (unsigned long long)h[4], (unsigned long long)h[5],
-                 (unsigned long long)h[6], (unsigned long long)h[7]);
+                 "[koordhip stamps] resolve cycles: prologue %llu (loads %llu refresh %llu)  loop: candidate %llu evals %llu "
+                 "commit %llu  kernel %llu  | re-evals %llu prefetch-misses %llu pods %llu\n",
+                 (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2],
+                 (unsigned long long)h[14], (unsigned long long)h[15], (unsigned long long)h[3],
+                 (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
+                 (unsigned long long)h[7]);
   }
   return 0;
 }

@@ -67,15 +67,24 @@ __device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
 
 // Wave max of a u64 with DPP row shifts + row broadcasts (GFX9 DPP), result
 // uniform.  Max is idempotent, so shifted prefix-max steps are a reduction.
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Wave max of a u64 as two 32-bit DPP max reductions (v_max_u32 takes the DPP
+// operand directly, a 64-bit compare-select does not): the high word first,
+// then the low word among the lanes holding that high word.  Result uniform.
 __device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
-  uint64_t o;
-  o = dpp_u64<0x111>(v); v = o > v ? o : v;        // row_shr:1
-  o = dpp_u64<0x112>(v); v = o > v ? o : v;        // row_shr:2
-  o = dpp_u64<0x114>(v); v = o > v ? o : v;        // row_shr:4
-  o = dpp_u64<0x118>(v); v = o > v ? o : v;        // row_shr:8
-  o = dpp_u64<0x142, 0xa>(v); v = o > v ? o : v;   // row_bcast:15
-  o = dpp_u64<0x143, 0xc>(v); v = o > v ? o : v;   // row_bcast:31
-  return readlane_u64(v, 63);
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  const uint32_t mh = wave_max_u32_dpp(hi);
+  const uint32_t ml = wave_max_u32_dpp(hi == mh ? lo : 0u);
+  return ((uint64_t)mh << 32) | ml;
 }
 
 __device__ __forceinline__ uint64_t stamp() {
@@ -680,33 +689,48 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
 // enabled score is non-increasing in them (a "monotone" config), so such a
 // stale key is an upper bound of the node's current key.
 //
-// Prologue (16 waves): lists -> LDS; the rows of M' -> LDS (+ node -> slot
-// hash); every list entry on an M' node is re-evaluated on its current row;
-// each list is re-sorted (bitonic).  Every list key is now exact at the start
-// of the round, and a node outside a list scores <= its k-th stale key.
+// Prologue (all waves): lists, pod records, the rows of M' and of the list
+// heads -> LDS (+ an M' node -> slot hash); every list entry on an M' node is
+// re-evaluated on its current row (one wave per pod).  Every list key is now
+// exact at the start of the round, and a node outside a list scores <= its
+// k-th stale key.  Lists are not re-sorted: the loop takes maxima.
 //
-// Loop (wave 0, s_setprio 3): pod j's candidate is its first list entry not
+// Loop (wave 0, s_setprio 3): pod j's candidate is its best list entry not
 // in M = the nodes committed in THIS round (lane-owned rows in registers).
 // Since |M' u M| < k, a full list always has an entry outside M' u M, whose
 // key (exact) bounds every node outside the list, so the candidate beats
-// every node outside M.  A node of M can only win if it ranks above the
-// candidate in the list (its list key bounds its current key), and only then
-// are M's rows re-evaluated (one row per lane, wave max).  Pods whose
+// every node outside M.  A node of M can only win if its list key (an upper
+// bound of its current key) beats the candidate, and only then are M's rows
+// re-evaluated (one row per lane, wave max).  Pods whose
 // feasibility is not monotone (NodeNUMAResource required SpreadByPCPUs)
 // re-evaluate M and M' every time.  The winner's Reserve delta is applied to
 // its lane-owned row; rows of M are written back at the end and M is handed
 // to the next round as its M'.
 
-// NUMA builds run the (register-hungry) accumulator replay in wave 0: 4 waves
-// keep 512 VGPRs available to it; otherwise 16 waves for a faster prologue.
+// Wave 0 runs the sequential loop with a lot of state in registers (the M
+// rows, the staged candidate row, NUMA masks and the accumulator replay):
+// 8 waves (4 for NUMA builds) keep 256 (512) VGPRs available to it.
 template <bool NUMA>
-constexpr int res_threads() { return NUMA ? 256 : 1024; }
+constexpr int res_threads() { return NUMA ? 256 : 512; }
+
+// A pod record read from LDS made wave-uniform (SGPRs): every lane read the
+// same record, readfirstlane tells the compiler so.
+__device__ __forceinline__ DevPod uniform_pod(const DevPod &src) {
+  DevPod p;
+  const uint32_t *s = reinterpret_cast<const uint32_t *>(&src);
+  uint32_t *o = reinterpret_cast<uint32_t *>(&p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(DevPod) / 4); i++) o[i] = __builtin_amdgcn_readfirstlane(s[i]);
+  return p;
+}
 constexpr int RES_PRE = 128;   // prefetched rows of list heads
+constexpr int RES_TOP = 8;     // ordered best keys per pod (the loop's fast path)
 constexpr int RES_HASH = 256;  // node -> M' slot (open addressing)
 constexpr int RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (static LDS: a few flags)
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
-  int32_t lists, prev_rows, prev_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node, modmap, total;
+  int32_t lists, pods, prev_rows, prev_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node, want, top, lcnt, modmap,
+      total;
 };
 
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
@@ -716,6 +740,8 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   int32_t at = 0;
   o.lists = at;
   at += res_align(n_pods_max * kp * 8);
+  o.pods = at;
+  at += res_align(n_pods_max * (int32_t)sizeof(DevPod));
   o.prev_rows = at;
   at += res_align(RES_MAXP_ROUND * (int32_t)sizeof(NV));
   o.prev_numa = at;
@@ -730,6 +756,12 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += numa ? res_align(RES_PRE * (int32_t)sizeof(NumaRow)) : 0;
   o.pre_node = at;
   at += RES_PRE * 4;
+  o.want = at;
+  at += RES_PRE * 4;
+  o.top = at;
+  at += RES_MAXP_ROUND * RES_TOP * 8;
+  o.lcnt = at;
+  at += RES_MAXP_ROUND * 4;
   o.modmap = at;
   at += res_align(((n_nodes + 31) >> 5) * 4);
   o.total = at;
@@ -757,11 +789,18 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
   NV *pre = reinterpret_cast<NV *>(lds + ofs.pre_rows);
   NumaRow *prenr = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa);
   int32_t *pre_node = reinterpret_cast<int32_t *>(lds + ofs.pre_node);
+  int32_t *want = reinterpret_cast<int32_t *>(lds + ofs.want);
+  uint64_t *top = reinterpret_cast<uint64_t *>(lds + ofs.top);
+  int32_t *lcnt = reinterpret_cast<int32_t *>(lds + ofs.lcnt);
   uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
   const int t = threadIdx.x, lane = lane_id();
   const uint64_t t_entry = (dbg && t == 0) ? stamp() : 0;
   const int32_t mp = min(prev_mod[0], (int32_t)RES_MAXP_ROUND);  // |M'|
-  // ---- 1. lists -> LDS (stride kp, zero padded), M' rows -> LDS, clear maps
+  DevPod *lpod = reinterpret_cast<DevPod *>(lds + ofs.pods);
+  // ---- 1. every global read of the prologue at once: lists -> LDS (stride
+  //         kp, zero padded), pod records, M' rows, and the rows of the list
+  //         heads (slot s = pod s % n, position s / n, taken from the lists as
+  //         delivered; the refresh below rarely changes a head)
   __shared__ int32_t bad;
   if (t == 0) bad = 0;
   __syncthreads();
@@ -771,92 +810,32 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
     if (e != 0 && (uint32_t)key_node(e) >= (uint32_t)d.n) bad = 1 + x;
     lk[x] = e;
   }
-  if (t <= mp && t > 0 && (uint32_t)prev_mod[t] >= (uint32_t)d.n) bad = -1000 - t;
-  __syncthreads();
-  if (bad) {  // broken input contract: report, touch nothing
-    for (int32_t j = t; j < n_pods; j += RES_THREADS) out_node[j] = -1000000 - bad;
-    if (t == 0) next_mod[0] = 0;
-    return;
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(pods);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lpod);
+    for (int32_t x = t; x < n_pods * (int32_t)(sizeof(DevPod) / 4); x += RES_THREADS) dst[x] = src[x];
   }
-  for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
-  const int32_t words = (d.n + 31) >> 5;
-  for (int32_t x = t; x < words; x += RES_THREADS) modmap[x] = 0;
   if (t < mp) {
     const int32_t nd = prev_mod[1 + t];
-    NV v;
-    load_row(v, d, nd);
-    prow[t] = v;
-    if constexpr (NUMA) {
-      NumaRow r;
-      load_numa_row(r, d, nd);
-      pnr[t] = r;
-    }
-  }
-  __syncthreads();
-  if (t == 0) {  // M' hash (<= 64 inserts, serial: no insert races)
-    for (int32_t s = 0; s < mp; s++) {
-      const int32_t nd = prev_mod[1 + s];
-      uint32_t h = res_hash(nd);
-      while (hnode[h] >= 0) h = (h + 1) & (RES_HASH - 1);
-      hnode[h] = nd;
-      hslot[h] = s;
-    }
-  }
-  __syncthreads();
-  auto prev_slot = [&](int32_t nd) -> int32_t {
-    uint32_t h = res_hash(nd);
-    for (;;) {
-      const int32_t x = hnode[h];
-      if (x == nd) return hslot[h];
-      if (x < 0) return -1;
-      h = (h + 1) & (RES_HASH - 1);
-    }
-  };
-  // ---- 2. refresh the keys of list entries on M' nodes (exact, current rows)
-  if (mp > 0) {
-    for (int32_t x = t; x < n_pods * kp; x += RES_THREADS) {
-      const uint64_t e = lk[x];
-      if (e == 0) continue;
-      const int32_t nd = key_node(e);
-      const int32_t s = prev_slot(nd);
-      if (s < 0) continue;
-      const int32_t j = x / kp;
-      const DevPod pod = pods[j];
-      int32_t tot;
+    if ((uint32_t)nd >= (uint32_t)d.n) {
+      bad = -1000 - t;
+    } else {
+      NV v;
+      load_row(v, d, nd);
+      prow[t] = v;
       if constexpr (NUMA) {
-        tot = eval_total_numa(pod, prow[s], pnr[s], d.nu.cls, c);
-      } else {
-        tot = eval_total(pod, prow[s], c);
-      }
-      lk[x] = make_key(tot, nd);
-    }
-    __syncthreads();
-    // ---- 3. bitonic sort of every list, descending
-    const int32_t half = n_pods * (kp >> 1);
-    for (int32_t size = 2; size <= kp; size <<= 1) {
-      for (int32_t stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int32_t x = t; x < half; x += RES_THREADS) {
-          const int32_t j = x / (kp >> 1), i = x - j * (kp >> 1);
-          const int32_t a = 2 * stride * (i / stride) + (i % stride), b = a + stride;
-          uint64_t *L = lk + (size_t)j * kp;
-          const uint64_t va = L[a], vb = L[b];
-          const bool desc = (a & size) == 0;
-          if (desc ? va < vb : va > vb) {
-            L[a] = vb;
-            L[b] = va;
-          }
-        }
-        __syncthreads();
+        NumaRow r;
+        load_numa_row(r, d, nd);
+        pnr[t] = r;
       }
     }
   }
-  // ---- 4. prefetch the rows of the list heads: slot s = pod s % n, position s / n
-  if (t < RES_PRE) {
-    const int32_t j = t % n_pods, q = t / n_pods;
+  if (t < RES_PRE) {  // slot t: pod t / 2, list position t % 2
+    const int32_t j = t >> 1, q = t & 1;
     int32_t nd = -1;
-    if (q < k) {
-      const uint64_t e = lk[(size_t)j * kp + q];
-      if (e != 0) nd = key_node(e);
+    if (j < n_pods && q < k) {
+      const uint64_t e = lists[(size_t)j * k + q];
+      if (e != 0 && (uint32_t)key_node(e) < (uint32_t)d.n) nd = key_node(e);
     }
     if (nd >= 0) {
       NV v;
@@ -870,36 +849,140 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
     }
     pre_node[t] = nd;
   }
+  for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
+  const int32_t words = (d.n + 31) >> 5;
+  for (int32_t x = t; x < words; x += RES_THREADS) modmap[x] = 0;
   __syncthreads();
+  if (bad) {  // broken input contract: report, touch nothing
+    for (int32_t j = t; j < n_pods; j += RES_THREADS) out_node[j] = -1000000 - bad;
+    if (t == 0) next_mod[0] = 0;
+    return;
+  }
+  if (t < mp) {  // M' hash: node -> slot, linear probing, lock-free inserts
+    const int32_t nd = prev_mod[1 + t];
+    uint32_t h = res_hash(nd);
+    while (atomicCAS(&hnode[h], -1, nd) != -1) h = (h + 1) & (RES_HASH - 1);
+    hslot[h] = t;
+  }
+  __syncthreads();
+  auto prev_slot = [&](int32_t nd) -> int32_t {
+    uint32_t h = res_hash(nd);
+    for (;;) {
+      const int32_t x = hnode[h];
+      if (x == nd) return hslot[h];
+      if (x < 0) return -1;
+      h = (h + 1) & (RES_HASH - 1);
+    }
+  };
+  const uint64_t t_load = (dbg && t == 0) ? stamp() : 0;
+  // ---- 2. per pod (one wave each, pod record wave-uniform, lane = list
+  //         position): refresh the keys of the entries on M' nodes (exact,
+  //         current rows), then extract the RES_TOP best keys in order -- the
+  //         loop nearly always finds its candidate among them; the lists
+  //         themselves stay unsorted
+  {
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
+      uint64_t *L = lk + (size_t)j * kp;
+      if (mp > 0) {
+        const DevPod pod = pods[j];
+        for (int32_t q = lane; q < kp; q += 64) {
+          const uint64_t e = L[q];
+          const int32_t sl = e ? prev_slot(key_node(e)) : -1;
+          if (__ballot(sl >= 0) == 0) continue;
+          if (sl >= 0) {
+            int32_t tot;
+            if constexpr (NUMA) {
+              tot = eval_total_numa(pod, prow[sl], pnr[sl], d.nu.cls, c);
+            } else {
+              tot = eval_total(pod, prow[sl], c);
+            }
+            L[q] = make_key(tot, key_node(e));
+          }
+        }
+      }
+      uint64_t x0 = lane < kp ? L[lane] : 0ull, x1 = 64 + lane < kp ? L[64 + lane] : 0ull;
+      if (lane == 0) lcnt[j] = 0;
+      const int32_t cnt = __popcll(__ballot(x0 != 0)) + __popcll(__ballot(x1 != 0));
+      for (int tt = 0; tt < RES_TOP; tt++) {
+        const uint64_t m = wave_max_u64_dpp(x0 > x1 ? x0 : x1);
+        if (lane == 0) top[j * RES_TOP + tt] = m;
+        x0 = x0 == m ? 0ull : x0;
+        x1 = x1 == m ? 0ull : x1;
+        if (tt < 2 && lane == 0) {  // the two best: rows to prefetch (M' rows are in LDS already)
+          const int32_t nd = m ? key_node(m) : -1;
+          want[2 * j + tt] = (nd >= 0 && (mp == 0 || prev_slot(nd) < 0)) ? nd : -1;
+        }
+      }
+      if (lane == 0) lcnt[j] = cnt;
+    }
+    __syncthreads();
+    if (t < RES_PRE && t < 2 * n_pods) {  // reload the slots whose head changed
+      const int32_t nd = want[t];
+      if (nd >= 0 && nd != pre_node[t]) {
+        NV v;
+        load_row(v, d, nd);
+        pre[t] = v;
+        if constexpr (NUMA) {
+          NumaRow r;
+          load_numa_row(r, d, nd);
+          prenr[t] = r;
+        }
+        pre_node[t] = nd;
+      }
+    }
+    __syncthreads();
+  }
+  if (dbg && t == 0) {
+    atomicAdd((unsigned long long *)&dbg[1], (unsigned long long)(t_load - t_entry));
+    atomicAdd((unsigned long long *)&dbg[2], (unsigned long long)(stamp() - t_load));
+  }
   if (t >= 64) return;  // the sequential part is wave 0's
   __builtin_amdgcn_s_setprio(3);
   const uint64_t t_pro = dbg ? stamp() : 0;
-  uint64_t n_eval = 0, n_miss = 0;
-  NV my{};
-  NumaRow mynr{};
+  uint64_t n_eval = 0, n_miss = 0, t_a = 0, t_b = 0, t_c = 0, t_m = t_pro;
+  NV my{}, stg{};
+  NumaRow mynr{}, stgnr{};
   int32_t my_node = -1;
   int32_t nm = 0;  // |M| (wave-uniform)
   const bool two = k > 64;
   for (int32_t j = 0; j < n_pods; j++) {
-    const DevPod pod = pods[j];  // uniform index: scalar loads
-    const uint64_t *L = lk + (size_t)j * kp;
-    const uint64_t e0 = lane < k ? L[lane] : 0ull;  // lanes past k hold nothing (k may be < 64)
-    const uint64_t e1 = two && 64 + lane < k ? L[64 + lane] : 0ull;
-    bool mod0 = false, mod1 = false;
-    if (e0) {
-      const int32_t nd = key_node(e0);
-      mod0 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+    const DevPod pod = uniform_pod(lpod[j]);
+    // candidate: the best entry outside M (every list key is exact); first
+    // among the pod's RES_TOP best, else from the whole list
+    const uint64_t tv = lane < RES_TOP ? top[j * RES_TOP + lane] : 0ull;
+    bool tmod = false;
+    if (tv) {
+      const int32_t nd = key_node(tv);
+      tmod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
     }
-    if (e1) {
-      const int32_t nd = key_node(e1);
-      mod1 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+    const uint64_t tfree = __ballot(tv != 0 && !tmod);
+    uint64_t cand = 0;
+    bool prefix_modified;
+    if (tfree || lcnt[j] <= RES_TOP) {
+      const int first = tfree ? __builtin_ctzll(tfree) : 64;
+      cand = tfree ? readlane_u64(tv, first) : 0ull;
+      // an M node can only win if its (upper-bound) list key beats the candidate
+      prefix_modified = __ballot(tv != 0 && tmod && lane < first) != 0;
+    } else {
+      const uint64_t *L = lk + (size_t)j * kp;
+      const uint64_t e0 = lane < k ? L[lane] : 0ull;  // lanes past k hold nothing (k may be < 64)
+      const uint64_t e1 = two && 64 + lane < k ? L[64 + lane] : 0ull;
+      bool mod0 = false, mod1 = false;
+      if (e0) {
+        const int32_t nd = key_node(e0);
+        mod0 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+      }
+      if (e1) {
+        const int32_t nd = key_node(e1);
+        mod1 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+      }
+      const uint64_t f0 = (e0 != 0 && !mod0) ? e0 : 0ull, f1 = (e1 != 0 && !mod1) ? e1 : 0ull;
+      cand = wave_max_u64_dpp(f0 > f1 ? f0 : f1);
+      prefix_modified = (__ballot(mod0 && e0 > cand) | __ballot(mod1 && e1 > cand)) != 0;
     }
-    const uint64_t f0 = __ballot(e0 != 0 && !mod0), f1 = __ballot(e1 != 0 && !mod1);
-    const int first = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
-    const uint64_t cand = first < 64 ? readlane_u64(e0, first) : (first < 128 ? readlane_u64(e1, first - 64) : 0ull);
-    const bool prefix_modified =
-        (__ballot(e0 != 0 && mod0 && lane < first) | __ballot(e1 != 0 && mod1 && lane + 64 < first)) != 0;
-    // stage the candidate's row into lane nm (the owner a new row gets)
+    // stage the candidate's row into lane nm's staging registers (separate
+    // from the M rows, so the re-evaluation below does not wait for it)
     int32_t staged = -1;
     if (cand != 0) {
       const int32_t cn = key_node(cand);
@@ -908,19 +991,32 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
       const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
       if (src >= 0) {
         if (lane == nm) {
-          my = pre[src];
+          stg = pre[src];
           if constexpr (NUMA) {
-            mynr = prenr[src];
+            stgnr = prenr[src];
           }
         }
       } else {
-        n_miss++;
-        if (lane == nm) {
-          load_row(my, d, cn);
-          if constexpr (NUMA) load_numa_row(mynr, d, cn);
+        const int32_t sl = mp > 0 ? prev_slot(cn) : -1;  // an M' node: its row is in LDS
+        if (sl >= 0) {
+          if (lane == nm) {
+            stg = prow[sl];
+            if constexpr (NUMA) stgnr = pnr[sl];
+          }
+        } else {
+          n_miss++;
+          if (lane == nm) {
+            load_row(stg, d, cn);
+            if constexpr (NUMA) load_numa_row(stgnr, d, cn);
+          }
         }
       }
       staged = cn;
+    }
+    if (dbg) {
+      const uint64_t x = stamp();
+      t_a += x - t_m;
+      t_m = x;
     }
     const bool nonmono = !monotone || (NUMA && is_cpuset(pod) && KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
     uint64_t best = cand;
@@ -955,12 +1051,17 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
     }
     if (j == trace_j) {  // diagnostics (KOORDHIP_TRACE_POD)
       if (lane == 0)
-        printf("[trace] j=%d cand=%d/%d first=%d best=%d/%d nm=%d mp=%d nonmono=%d prefix=%d\n", j,
-               cand ? key_node(cand) : -1, cand ? key_score(cand) : -1, first, best ? key_node(best) : -1,
+        printf("[trace] j=%d cand=%d/%d best=%d/%d nm=%d mp=%d nonmono=%d prefix=%d\n", j,
+               cand ? key_node(cand) : -1, cand ? key_score(cand) : -1, best ? key_node(best) : -1,
                best ? key_score(best) : -1, nm, mp, (int)nonmono, (int)prefix_modified);
       if (lane < nm) printf("[trace] M lane %d node %d\n", lane, my_node);
       if (lane < mp) printf("[trace] M' lane %d node %d\n", lane, prev_mod[1 + lane]);
-      if (lane < 8) printf("[trace] list %d: %d/%d mod %d\n", lane, e0 ? key_node(e0) : -1, e0 ? key_score(e0) : -1, (int)mod0);
+      if (lane < RES_TOP) printf("[trace] top %d: %d/%d mod %d\n", lane, tv ? key_node(tv) : -1, tv ? key_score(tv) : -1, (int)tmod);
+    }
+    if (dbg) {
+      const uint64_t x = stamp();
+      t_b += x - t_m;
+      t_m = x;
     }
     uint64_t cpus[NW] = {0, 0, 0, 0};
     if (best == 0) {
@@ -971,9 +1072,14 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
       // w is a row of M (lane `hit`) or new this round: then it is the staged
       // candidate, or (non-monotone pods only) an M' node
       const int32_t r = hit ? __builtin_ctzll(hit) : nm;
-      if (!hit && staged != w && lane == r) {
-        load_row(my, d, w);
-        if constexpr (NUMA) load_numa_row(mynr, d, w);
+      if (!hit && lane == r) {  // a new row: the staged candidate, or (non-monotone pods) an M' node
+        if (staged == w) {
+          my = stg;
+          if constexpr (NUMA) mynr = stgnr;
+        } else {
+          load_row(my, d, w);
+          if constexpr (NUMA) load_numa_row(mynr, d, w);
+        }
       }
       bool ok = true;
       if constexpr (NUMA) {
@@ -1010,6 +1116,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
         }
       }
     }
+    if (dbg) {
+      const uint64_t x = stamp();
+      t_c += x - t_m;
+      t_m = x;
+    }
     if (out_cpus && lane < NW)
       out_cpus[(size_t)j * NW + lane] = lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
   }
@@ -1022,6 +1133,9 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
   if (dbg && lane == 0) {
     const uint64_t t_end = stamp();
     atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)(t_pro - t_entry));
+    atomicAdd((unsigned long long *)&dbg[14], (unsigned long long)t_a);
+    atomicAdd((unsigned long long *)&dbg[15], (unsigned long long)t_b);
+    atomicAdd((unsigned long long *)&dbg[3], (unsigned long long)t_c);
     atomicAdd((unsigned long long *)&dbg[4], (unsigned long long)(t_end - t_entry));
     atomicAdd((unsigned long long *)&dbg[5], (unsigned long long)n_eval);
     atomicAdd((unsigned long long *)&dbg[6], (unsigned long long)n_miss);
