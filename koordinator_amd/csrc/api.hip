@@ -113,10 +113,11 @@ struct koordhip_ctx {
   uint64_t *d_gather = nullptr;  // [world][batch][k]
   int32_t gather_world = 1;
   uint64_t *d_final = nullptr;   // [2][batch][k] (merged lists, multi-rank)
-  int32_t *d_mod = nullptr;      // [2][1 + batch]: {count, nodes} committed by a round (ping-pong)
+  int32_t *d_mod = nullptr;      // {count, nodes} M' between resolve launches, then PipeSync
   const uint64_t *d_cur_lists = nullptr;  // this round's rank-local lists (local-group exchange)
   hipStream_t rstream = nullptr;  // resolve stream (the eval kernels use `stream`)
-  hipEvent_t ev_sel[kRing] = {}, ev_res[kRing] = {}, ev_start = nullptr;
+  hipEvent_t ev_res[kRing] = {}, ev_start = nullptr;
+  bool pipe_check = false;       // a place call ran: check PipeSync.err when it completes
   kh::DevPod *d_tmp_pod = nullptr;
   uint64_t *d_dbg = nullptr;  // KOORDHIP_STAMPS diagnostic counters (resolve segments)
 
@@ -470,8 +471,7 @@ int koordhip_destroy(koordhip_ctx *c) {
                   (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
-    for (hipEvent_t e : {c->ev_sel[i], c->ev_res[i]})
-      if (e) (void)hipEventDestroy(e);
+    if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->rstream) {
     (void)hipStreamSynchronize(c->rstream);
@@ -868,12 +868,9 @@ int place_staged_impl(koordhip_ctx *c) {
   if (!c->d_lists) {
     HIP_TRY(hipMalloc(&c->d_lists, 2 * lbytes));
     HIP_TRY(hipMalloc(&c->d_final, 2 * lbytes));
-    HIP_TRY(hipMalloc(&c->d_mod, 2 * (1 + kMaxBatch) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&c->d_mod, (1 + kMaxBatch) * sizeof(int32_t) + kh::kPipeSyncBytes));
     HIP_TRY(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
-    for (int i = 0; i < kRing; i++) {
-      HIP_TRY(hipEventCreateWithFlags(&c->ev_sel[i], hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&c->ev_res[i], hipEventDisableTiming));
-    }
+    for (int i = 0; i < kRing; i++) HIP_TRY(hipEventCreateWithFlags(&c->ev_res[i], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
   }
   if (c->world > c->gather_world) {
@@ -895,45 +892,57 @@ int place_staged_impl(koordhip_ctx *c) {
     if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 16 * sizeof(uint64_t)));
     HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(uint64_t), c->stream));
   }
+  int32_t *mbuf = c->d_mod;  // M' handed between resolve launches
+  kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
   HIP_TRY(hipEventRecord(c->t0, c->stream));
-  // round 0 has no predecessor: M' = {}
-  HIP_TRY(hipMemsetAsync(c->d_mod + (1 + kMaxBatch), 0, sizeof(int32_t), c->stream));
+  HIP_TRY(hipMemsetAsync(sync, 0, kh::kPipeSyncBytes, c->stream));
   HIP_TRY(hipEventRecord(c->ev_start, c->stream));
   HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_start, 0));
   // Lag-1 pipeline: round r's lists are evaluated (stream) while round r-1 is
-  // resolved (rstream); they wait only for round r-2's commits.
+  // resolved (rstream); round r's evaluation waits only for round r-2's
+  // commits.  Both sides synchronise through device flags (PipeSync).  A lone
+  // context runs ONE persistent resolve launch for the whole stream (no
+  // per-round launch or event latency on the sequential path); contexts of a
+  // local group share hardware queues with their peers, so they launch one
+  // resolve per round, enqueued after that round's lists (deadlock-free
+  // whatever the stream -> queue mapping).
   const int32_t total = c->n_staged;
-  const int lag = std::getenv("KOORDHIP_NO_OVERLAP") ? 1 : 2;  // diagnostics: serialise eval after resolve
-  const char *trace_env = std::getenv("KOORDHIP_TRACE_POD");      // diagnostics: printf one pod's resolve step
+  const int32_t rounds = (total + P - 1) / P;
+  const bool persistent = !c->group && !std::getenv("KOORDHIP_ROUND_LAUNCH");
+  const char *trace_env = std::getenv("KOORDHIP_TRACE_POD");  // diagnostics: printf one pod's resolve step
   const int32_t trace = trace_env ? std::atoi(trace_env) : -1;
-  int32_t r = 0;
-  for (int32_t p0 = 0; p0 < total; p0 += P, r++) {
-    const int32_t np = std::min(P, total - p0);
+  const int64_t list_buf = (int64_t)(lbytes / sizeof(uint64_t));
+  uint64_t *lists0 = c->world > 1 ? c->d_final : c->d_lists;
+  uint64_t *cpus = c->d_cpus;
+  if (persistent && rounds > 0)
+    HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, sync,
+                               mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
+  for (int32_t r = 0; r < rounds; r++) {
+    const int32_t p0 = r * P, np = std::min(P, total - p0);
     const kh::DevPod *pods = c->d_pods + p0;
-    uint64_t *lists = c->d_lists + (size_t)(r & 1) * (lbytes / sizeof(uint64_t));
-    uint64_t *final_lists = lists;
-    if (r >= lag) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[(r - lag) % kRing], 0));
+    uint64_t *lists = c->d_lists + (size_t)(r & 1) * list_buf;
+    if (r >= 2) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, c->stream));
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
       if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true)) return e;
       if (int e = exchange(c, lists, (size_t)P * K)) return e;
-      final_lists = c->d_final + (size_t)(r & 1) * (lbytes / sizeof(uint64_t));
-      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits, final_lists,
-                                    c->stream));
+      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits,
+                                    c->d_final + (size_t)(r & 1) * list_buf, c->stream));
     } else {
       if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true)) return e;
     }
-    HIP_TRY(hipEventRecord(c->ev_sel[r % kRing], c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_sel[r % kRing], 0));
-    const int32_t *prev = c->d_mod + (size_t)((r + 1) & 1) * (1 + kMaxBatch);
-    int32_t *next = c->d_mod + (size_t)(r & 1) * (1 + kMaxBatch);
-    HIP_TRY(kh::launch_resolve(c->dc, c->d, pods, np, K, final_lists, c->monotone, prev, next, c->d_out + p0,
-                               c->d_cpus ? c->d_cpus + (size_t)p0 * KOORDHIP_NUMA_WORDS : nullptr, c->d_dbg,
-                               trace >= p0 && trace < p0 + np ? trace - p0 : -1, c->rstream));
-    HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->rstream));
+    HIP_TRY(kh::launch_signal_lists(sync, r + 1, c->stream));
+    if (!persistent) {
+      HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
+      HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_res[r % kRing], 0));
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, sync,
+                                 mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
+    }
   }
-  if (r > 0) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[(r - 1) % kRing], 0));
+  HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[0], 0));
   HIP_TRY(hipEventRecord(c->t1, c->stream));
+  c->pipe_check = true;
   if (c->d_dbg) {
     uint64_t h[16];
     HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -943,13 +952,22 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[8], (unsigned long long)h[9], (unsigned long long)h[10],
                  (unsigned long long)h[11], (unsigned long long)h[12], (unsigned long long)h[13]);
     std::fprintf(stderr,
-                 "[koordhip stamps] resolve cycles: prologue %llu (loads %llu refresh %llu)  loop: candidate %llu evals %llu "
-                 "commit %llu  kernel %llu  | re-evals %llu prefetch-misses %llu pods %llu\n",
-                 (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2],
-                 (unsigned long long)h[14], (unsigned long long)h[15], (unsigned long long)h[3],
-                 (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
-                 (unsigned long long)h[7]);
+                 "[koordhip stamps] resolve cycles: prologue %llu  waiting for lists %llu  loop %llu  | re-evals %llu "
+                 "prefetch-misses %llu pods %llu\n",
+                 (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[4],
+                 (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7]);
   }
+  return 0;
+}
+
+// After a place call: did either side of the pipeline give up waiting?
+int pipe_status(koordhip_ctx *c) {
+  if (!c->pipe_check || !c->d_mod) return 0;
+  c->pipe_check = false;
+  kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
+  int32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, reinterpret_cast<int32_t *>(sync) + 2, sizeof(err), hipMemcpyDeviceToHost));
+  if (err) return fail(KOORDHIP_EDEVICE, "round pipeline stalled (watchdog): placements are incomplete");
   return 0;
 }
 
@@ -961,7 +979,7 @@ int koordhip_synchronize(koordhip_ctx *c) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  return 0;
+  return pipe_status(c);
 }
 
 int koordhip_fetch_placements(koordhip_ctx *c, int32_t *out_node, int32_t n_pods) {
@@ -969,6 +987,7 @@ int koordhip_fetch_placements(koordhip_ctx *c, int32_t *out_node, int32_t n_pods
   if (n_pods > c->n_staged) return fail(KOORDHIP_EINVAL, "n_pods exceeds the staged stream");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int e = pipe_status(c)) return e;
   if (n_pods) HIP_TRY(hipMemcpy(out_node, c->d_out, (size_t)n_pods * sizeof(int32_t), hipMemcpyDeviceToHost));
   return 0;
 }

@@ -35,12 +35,21 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
                              int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s);
 template <typename T>
 hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
-// k_resolve: one round of the greedy, lag-1 (see kernels.hip); prev_mod / next_mod =
-// {count, nodes...} of the previous / this round's committed nodes.  LDS bytes it needs:
+// The lag-1 round pipeline (kernels.hip): k_resolve resolves rounds [r_begin,
+// r_end) of the staged stream (P pods per round, k keys per list, lists double
+// buffered at lists0 + (r & 1) * list_buf); it waits for sel_round and
+// publishes res_round in `sync`; M' is handed between launches in mbuf
+// ({count, nodes}).  The evaluation stream brackets each round with
+// k_wait_resolved (before k_scan) and k_signal_lists (after the lists).
+struct PipeSync;
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa);
-hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t k,
-                          const uint64_t *lists, int32_t monotone, const int32_t *prev_mod, int32_t *next_mod,
-                          int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg, int32_t trace_j, hipStream_t s);
+hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t total, int32_t P, int32_t k,
+                          int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
+                          PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
+                          int32_t trace, hipStream_t s);
+hipError_t launch_wait_resolved(PipeSync *sync, int32_t rounds, hipStream_t s);
+hipError_t launch_signal_lists(PipeSync *sync, int32_t rounds, hipStream_t s);
+constexpr size_t kPipeSyncBytes = 16;
 // single Reserve (sign +1, cpus <- allocated CPUs, *rc = KOORDHIP_ERESERVE on failure) / Unreserve (cpus given)
 hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const DevPod *pod, int32_t node, int32_t sign,
                          uint64_t *cpus, int32_t *rc, hipStream_t s);

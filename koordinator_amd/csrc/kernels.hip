@@ -770,15 +770,58 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
 
 __device__ __forceinline__ uint32_t res_hash(int32_t node) { return ((uint32_t)node * 2654435761u) >> 24; }
 
+// Device-side handshake between the evaluation stream and the persistent
+// resolve kernel (one per koordhip_place_staged call):
+//   sel_round  rounds whose lists are ready   (k_signal, after k_select / merge)
+//   res_round  rounds resolved + written back (k_resolve, release store)
+//   err        a side gave up waiting (watchdog): the call fails, nothing hangs
+struct PipeSync {
+  int32_t sel_round, res_round, err, pad;
+};
+
+constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up
+
+__device__ __forceinline__ int32_t load_acquire(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Spin (one thread) until *p >= v; false when the watchdog fires or the other
+// side reported an error.
+__device__ bool wait_at_least(const int32_t *p, int32_t v, PipeSync *sy) {
+  const uint64_t t0 = stamp();
+  while (load_acquire(p) < v) {
+    if (load_acquire(&sy->err)) return false;
+    if (stamp() - t0 > PIPE_WATCHDOG) {
+      store_release(&sy->err, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  return true;
+}
+
+// Evaluation stream, before k_scan of round r: rounds < r - 1 must be written back.
+__global__ void k_wait_resolved(PipeSync *sy, int32_t rounds) {
+  if (threadIdx.x == 0) (void)wait_at_least(&sy->res_round, rounds, sy);
+}
+// Evaluation stream, after round r's lists are complete (kernel boundary = visible).
+__global__ void k_signal_lists(PipeSync *sy, int32_t rounds) {
+  if (threadIdx.x == 0) store_release(&sy->sel_round, rounds);
+}
+
 template <bool NUMA>
 __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
-                                                         int32_t n_pods, int32_t k, int32_t kp,
-                                                         const uint64_t *__restrict__ lists, int32_t monotone,
-                                                         const int32_t *__restrict__ prev_mod,
-                                                         int32_t *__restrict__ next_mod, ResLds ofs,
-                                                         int32_t *__restrict__ out_node,
-                                                         uint64_t *__restrict__ out_cpus, uint64_t *__restrict__ dbg,
-                                                         int32_t trace_j) {
+                                                                 int32_t total, int32_t P, int32_t k, int32_t kp,
+                                                                 int32_t r_begin, int32_t r_end,
+                                                                 int32_t *__restrict__ mbuf,
+                                                                 const uint64_t *__restrict__ lists0,
+                                                                 int64_t list_buf, int32_t monotone, PipeSync *sy,
+                                                                 ResLds ofs, int32_t *__restrict__ out_node,
+                                                                 uint64_t *__restrict__ out_cpus,
+                                                                 uint64_t *__restrict__ dbg, int32_t trace) {
   constexpr int RES_THREADS = res_threads<NUMA>();
   extern __shared__ __attribute__((aligned(16))) char lds[];
   uint64_t *lk = reinterpret_cast<uint64_t *>(lds + ofs.lists);
@@ -793,353 +836,349 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
   uint64_t *top = reinterpret_cast<uint64_t *>(lds + ofs.top);
   int32_t *lcnt = reinterpret_cast<int32_t *>(lds + ofs.lcnt);
   uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
-  const int t = threadIdx.x, lane = lane_id();
-  const uint64_t t_entry = (dbg && t == 0) ? stamp() : 0;
-  const int32_t mp = min(prev_mod[0], (int32_t)RES_MAXP_ROUND);  // |M'|
   DevPod *lpod = reinterpret_cast<DevPod *>(lds + ofs.pods);
-  // ---- 1. every global read of the prologue at once: lists -> LDS (stride
-  //         kp, zero padded), pod records, M' rows, and the rows of the list
-  //         heads (slot s = pod s % n, position s / n, taken from the lists as
-  //         delivered; the refresh below rarely changes a head)
-  __shared__ int32_t bad;
-  if (t == 0) bad = 0;
-  __syncthreads();
-  for (int32_t x = t; x < n_pods * kp; x += RES_THREADS) {
-    const int32_t j = x / kp, q = x - j * kp;
-    const uint64_t e = q < k ? lists[(size_t)j * k + q] : 0ull;
-    if (e != 0 && (uint32_t)key_node(e) >= (uint32_t)d.n) bad = 1 + x;
-    lk[x] = e;
-  }
-  {
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(pods);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(lpod);
-    for (int32_t x = t; x < n_pods * (int32_t)(sizeof(DevPod) / 4); x += RES_THREADS) dst[x] = src[x];
-  }
-  if (t < mp) {
-    const int32_t nd = prev_mod[1 + t];
-    if ((uint32_t)nd >= (uint32_t)d.n) {
-      bad = -1000 - t;
-    } else {
-      NV v;
-      load_row(v, d, nd);
-      prow[t] = v;
-      if constexpr (NUMA) {
-        NumaRow r;
-        load_numa_row(r, d, nd);
-        pnr[t] = r;
-      }
-    }
-  }
-  if (t < RES_PRE) {  // slot t: pod t / 2, list position t % 2
-    const int32_t j = t >> 1, q = t & 1;
-    int32_t nd = -1;
-    if (j < n_pods && q < k) {
-      const uint64_t e = lists[(size_t)j * k + q];
-      if (e != 0 && (uint32_t)key_node(e) < (uint32_t)d.n) nd = key_node(e);
-    }
-    if (nd >= 0) {
-      NV v;
-      load_row(v, d, nd);
-      pre[t] = v;
-      if constexpr (NUMA) {
-        NumaRow r;
-        load_numa_row(r, d, nd);
-        prenr[t] = r;
-      }
-    }
-    pre_node[t] = nd;
-  }
-  for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
+  __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous round committed to
+  __shared__ int32_t sh_mp, sh_stop;
+  const int t = threadIdx.x, lane = lane_id();
   const int32_t words = (d.n + 31) >> 5;
+  const bool two = k > 64;
+  if (t == 0) {
+    sh_mp = r_begin > 0 ? min(mbuf[0], (int32_t)RES_MAXP_ROUND) : 0;
+    sh_stop = 0;
+  }
   for (int32_t x = t; x < words; x += RES_THREADS) modmap[x] = 0;
   __syncthreads();
-  if (bad) {  // broken input contract: report, touch nothing
-    for (int32_t j = t; j < n_pods; j += RES_THREADS) out_node[j] = -1000000 - bad;
-    if (t == 0) next_mod[0] = 0;
-    return;
-  }
-  if (t < mp) {  // M' hash: node -> slot, linear probing, lock-free inserts
-    const int32_t nd = prev_mod[1 + t];
-    uint32_t h = res_hash(nd);
-    while (atomicCAS(&hnode[h], -1, nd) != -1) h = (h + 1) & (RES_HASH - 1);
-    hslot[h] = t;
+  if (t < sh_mp) {  // resumed pipeline (one launch per round): M' from the previous launch
+    const int32_t nd = mbuf[1 + t];
+    pnode[t] = nd;
+    NV v;
+    load_row(v, d, nd);
+    prow[t] = v;
+    if constexpr (NUMA) {
+      NumaRow rr;
+      load_numa_row(rr, d, nd);
+      pnr[t] = rr;
+    }
   }
   __syncthreads();
-  auto prev_slot = [&](int32_t nd) -> int32_t {
-    uint32_t h = res_hash(nd);
-    for (;;) {
-      const int32_t x = hnode[h];
-      if (x == nd) return hslot[h];
-      if (x < 0) return -1;
-      h = (h + 1) & (RES_HASH - 1);
-    }
-  };
-  const uint64_t t_load = (dbg && t == 0) ? stamp() : 0;
-  // ---- 2. per pod (one wave each, pod record wave-uniform, lane = list
-  //         position): refresh the keys of the entries on M' nodes (exact,
-  //         current rows), then extract the RES_TOP best keys in order -- the
-  //         loop nearly always finds its candidate among them; the lists
-  //         themselves stay unsorted
-  {
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
-      uint64_t *L = lk + (size_t)j * kp;
-      if (mp > 0) {
-        const DevPod pod = pods[j];
-        for (int32_t q = lane; q < kp; q += 64) {
-          const uint64_t e = L[q];
-          const int32_t sl = e ? prev_slot(key_node(e)) : -1;
-          if (__ballot(sl >= 0) == 0) continue;
-          if (sl >= 0) {
-            int32_t tot;
-            if constexpr (NUMA) {
-              tot = eval_total_numa(pod, prow[sl], pnr[sl], d.nu.cls, c);
-            } else {
-              tot = eval_total(pod, prow[sl], c);
-            }
-            L[q] = make_key(tot, key_node(e));
-          }
-        }
-      }
-      uint64_t x0 = lane < kp ? L[lane] : 0ull, x1 = 64 + lane < kp ? L[64 + lane] : 0ull;
-      if (lane == 0) lcnt[j] = 0;
-      const int32_t cnt = __popcll(__ballot(x0 != 0)) + __popcll(__ballot(x1 != 0));
-      for (int tt = 0; tt < RES_TOP; tt++) {
-        const uint64_t m = wave_max_u64_dpp(x0 > x1 ? x0 : x1);
-        if (lane == 0) top[j * RES_TOP + tt] = m;
-        x0 = x0 == m ? 0ull : x0;
-        x1 = x1 == m ? 0ull : x1;
-        if (tt < 2 && lane == 0) {  // the two best: rows to prefetch (M' rows are in LDS already)
-          const int32_t nd = m ? key_node(m) : -1;
-          want[2 * j + tt] = (nd >= 0 && (mp == 0 || prev_slot(nd) < 0)) ? nd : -1;
-        }
-      }
-      if (lane == 0) lcnt[j] = cnt;
-    }
+  // wave 0's lane-owned rows (M of the current round) and staging registers
+  NV my{}, stg{};
+  NumaRow mynr{}, stgnr{};
+  int32_t my_node = -1;
+  uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0;
+  for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
+    const int32_t n_pods = min(P, total - p0);
+    const DevPod *rp = pods + p0;
+    const uint64_t *lists = lists0 + (size_t)(r & 1) * list_buf;
+    const int32_t trace_j = (trace >= p0 && trace < p0 + n_pods) ? trace - p0 : -1;
+    // ---- 0. wait for this round's lists (thread 0), then every wave reads them
+    const uint64_t t_w0 = (dbg && t == 0) ? stamp() : 0;
+    if (t == 0 && !wait_at_least(&sy->sel_round, r + 1, sy)) sh_stop = 1;
     __syncthreads();
-    if (t < RES_PRE && t < 2 * n_pods) {  // reload the slots whose head changed
-      const int32_t nd = want[t];
-      if (nd >= 0 && nd != pre_node[t]) {
+    if (sh_stop) return;  // the evaluation side failed: give up, the host reports it
+    const uint64_t t_entry = (dbg && t == 0) ? stamp() : 0;
+    const int32_t mp = sh_mp;
+    // ---- 1. every global read of the prologue at once: lists -> LDS (stride
+    //         kp, zero padded), pod records, and the rows of the list heads
+    //         (slot s = pod s / 2, position s % 2, as delivered); M' rows are
+    //         in LDS already (wave 0 left them there at the end of the last round)
+    for (int32_t x = t; x < n_pods * kp; x += RES_THREADS) {
+      const int32_t j = x / kp, q = x - j * kp;
+      lk[x] = q < k ? lists[(size_t)j * k + q] : 0ull;
+    }
+    {
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(rp);
+      uint32_t *dst = reinterpret_cast<uint32_t *>(lpod);
+      for (int32_t x = t; x < n_pods * (int32_t)(sizeof(DevPod) / 4); x += RES_THREADS) dst[x] = src[x];
+    }
+    if (t < RES_PRE) {
+      const int32_t j = t >> 1, q = t & 1;
+      int32_t nd = -1;
+      if (j < n_pods && q < k) {
+        const uint64_t e = lists[(size_t)j * k + q];
+        if (e != 0) nd = key_node(e);
+      }
+      if (nd >= 0) {
         NV v;
         load_row(v, d, nd);
         pre[t] = v;
         if constexpr (NUMA) {
-          NumaRow r;
-          load_numa_row(r, d, nd);
-          prenr[t] = r;
+          NumaRow rr;
+          load_numa_row(rr, d, nd);
+          prenr[t] = rr;
         }
-        pre_node[t] = nd;
+      }
+      pre_node[t] = nd;
+    }
+    for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
+    __syncthreads();
+    if (t < mp) {  // M' hash: node -> slot, linear probing, lock-free inserts
+      const int32_t nd = pnode[t];
+      uint32_t h = res_hash(nd);
+      while (atomicCAS(&hnode[h], -1, nd) != -1) h = (h + 1) & (RES_HASH - 1);
+      hslot[h] = t;
+    }
+    __syncthreads();
+    auto prev_slot = [&](int32_t nd) -> int32_t {
+      uint32_t h = res_hash(nd);
+      for (;;) {
+        const int32_t x = hnode[h];
+        if (x == nd) return hslot[h];
+        if (x < 0) return -1;
+        h = (h + 1) & (RES_HASH - 1);
+      }
+    };
+    // ---- 2. per pod (one wave each, pod record wave-uniform, lane = list
+    //         position): refresh the keys of the entries on M' nodes (exact,
+    //         current rows), then extract the RES_TOP best keys in order -- the
+    //         loop nearly always finds its candidate among them; the lists
+    //         themselves stay unsorted
+    {
+      const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+      for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
+        uint64_t *L = lk + (size_t)j * kp;
+        if (mp > 0) {
+          const DevPod pod = uniform_pod(lpod[j]);
+          for (int32_t q = lane; q < kp; q += 64) {
+            const uint64_t e = L[q];
+            const int32_t sl = e ? prev_slot(key_node(e)) : -1;
+            if (__ballot(sl >= 0) == 0) continue;
+            if (sl >= 0) {
+              int32_t tot;
+              if constexpr (NUMA) {
+                tot = eval_total_numa(pod, prow[sl], pnr[sl], d.nu.cls, c);
+              } else {
+                tot = eval_total(pod, prow[sl], c);
+              }
+              L[q] = make_key(tot, key_node(e));
+            }
+          }
+        }
+        uint64_t x0 = lane < kp ? L[lane] : 0ull, x1 = 64 + lane < kp ? L[64 + lane] : 0ull;
+        const int32_t cnt = __popcll(__ballot(x0 != 0)) + __popcll(__ballot(x1 != 0));
+        for (int tt = 0; tt < RES_TOP; tt++) {
+          const uint64_t m = wave_max_u64_dpp(x0 > x1 ? x0 : x1);
+          if (lane == 0) top[j * RES_TOP + tt] = m;
+          x0 = x0 == m ? 0ull : x0;
+          x1 = x1 == m ? 0ull : x1;
+          if (tt < 2 && lane == 0) {  // the two best: rows to prefetch (M' rows are in LDS already)
+            const int32_t nd = m ? key_node(m) : -1;
+            want[2 * j + tt] = (nd >= 0 && (mp == 0 || prev_slot(nd) < 0)) ? nd : -1;
+          }
+        }
+        if (lane == 0) lcnt[j] = cnt;
+      }
+      __syncthreads();
+      if (t < RES_PRE && t < 2 * n_pods) {  // reload the slots whose head changed
+        const int32_t nd = want[t];
+        if (nd >= 0 && nd != pre_node[t]) {
+          NV v;
+          load_row(v, d, nd);
+          pre[t] = v;
+          if constexpr (NUMA) {
+            NumaRow rr;
+            load_numa_row(rr, d, nd);
+            prenr[t] = rr;
+          }
+          pre_node[t] = nd;
+        }
+      }
+      __syncthreads();
+    }
+    if (t < 64) {  // ---- 3. the sequential greedy over the round (wave 0)
+      __builtin_amdgcn_s_setprio(3);
+      const uint64_t t_pro = dbg ? stamp() : 0;
+      int32_t nm = 0;  // |M| (wave-uniform)
+      my_node = -1;
+      for (int32_t j = 0; j < n_pods; j++) {
+        const DevPod pod = uniform_pod(lpod[j]);
+        // candidate: the best entry outside M (every list key is exact); first
+        // among the pod's RES_TOP best, else from the whole list
+        const uint64_t tv = lane < RES_TOP ? top[j * RES_TOP + lane] : 0ull;
+        bool tmod = false;
+        if (tv) {
+          const int32_t nd = key_node(tv);
+          tmod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+        }
+        const uint64_t tfree = __ballot(tv != 0 && !tmod);
+        uint64_t cand = 0;
+        bool prefix_modified;
+        if (tfree || lcnt[j] <= RES_TOP) {
+          const int first = tfree ? __builtin_ctzll(tfree) : 64;
+          cand = tfree ? readlane_u64(tv, first) : 0ull;
+          // an M node can only win if its (upper-bound) list key beats the candidate
+          prefix_modified = __ballot(tv != 0 && tmod && lane < first) != 0;
+        } else {
+          const uint64_t *L = lk + (size_t)j * kp;
+          const uint64_t e0 = lane < k ? L[lane] : 0ull;  // lanes past k hold nothing (k may be < 64)
+          const uint64_t e1 = two && 64 + lane < k ? L[64 + lane] : 0ull;
+          bool mod0 = false, mod1 = false;
+          if (e0) {
+            const int32_t nd = key_node(e0);
+            mod0 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+          }
+          if (e1) {
+            const int32_t nd = key_node(e1);
+            mod1 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+          }
+          const uint64_t f0 = (e0 != 0 && !mod0) ? e0 : 0ull, f1 = (e1 != 0 && !mod1) ? e1 : 0ull;
+          cand = wave_max_u64_dpp(f0 > f1 ? f0 : f1);
+          prefix_modified = (__ballot(mod0 && e0 > cand) | __ballot(mod1 && e1 > cand)) != 0;
+        }
+        // stage the candidate's row into lane nm's staging registers (separate
+        // from the M rows, so the re-evaluation below does not wait for it)
+        int32_t staged = -1;
+        if (cand != 0) {
+          const int32_t cn = key_node(cand);
+          const uint64_t pm0 = __ballot(pre_node[lane] == cn);
+          const uint64_t pm1 = __ballot(pre_node[lane + 64] == cn);
+          const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
+          if (src >= 0) {
+            if (lane == nm) {
+              stg = pre[src];
+              if constexpr (NUMA) stgnr = prenr[src];
+            }
+          } else {
+            const int32_t sl = mp > 0 ? prev_slot(cn) : -1;  // an M' node: its row is in LDS
+            if (sl >= 0) {
+              if (lane == nm) {
+                stg = prow[sl];
+                if constexpr (NUMA) stgnr = pnr[sl];
+              }
+            } else {
+              n_miss++;
+              if (lane == nm) {
+                load_row(stg, d, cn);
+                if constexpr (NUMA) load_numa_row(stgnr, d, cn);
+              }
+            }
+          }
+          staged = cn;
+        }
+        const bool nonmono = !monotone || (NUMA && is_cpuset(pod) &&
+                                           KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
+        uint64_t best = cand;
+        if (nm > 0 && (prefix_modified || nonmono)) {
+          uint64_t key = 0;
+          if (lane < nm) {
+            if constexpr (NUMA) {
+              key = make_key(eval_total_numa(pod, my, mynr, d.nu.cls, c), my_node);
+            } else {
+              key = make_key(eval_total(pod, my, c), my_node);
+            }
+          }
+          key = wave_max_u64_dpp(key);
+          best = key > best ? key : best;
+          n_eval++;
+        }
+        if (nonmono && mp > 0) {  // M' nodes outside M: current rows in LDS
+          uint64_t key = 0;
+          if (lane < mp) {
+            const int32_t nd = pnode[lane];
+            const bool in_m = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+            if (!in_m) {
+              if constexpr (NUMA) {
+                key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], d.nu.cls, c), nd);
+              } else {
+                key = make_key(eval_total(pod, prow[lane], c), nd);
+              }
+            }
+          }
+          key = wave_max_u64_dpp(key);
+          best = key > best ? key : best;
+        }
+        if (j == trace_j) {  // diagnostics (KOORDHIP_TRACE_POD)
+          if (lane == 0)
+            printf("[trace] j=%d cand=%d/%d best=%d/%d nm=%d mp=%d nonmono=%d prefix=%d\n", j,
+                   cand ? key_node(cand) : -1, cand ? key_score(cand) : -1, best ? key_node(best) : -1,
+                   best ? key_score(best) : -1, nm, mp, (int)nonmono, (int)prefix_modified);
+          if (lane < nm) printf("[trace] M lane %d node %d\n", lane, my_node);
+          if (lane < mp) printf("[trace] M' lane %d node %d\n", lane, pnode[lane]);
+        }
+        uint64_t cpus[NW] = {0, 0, 0, 0};
+        int32_t result = KOORDHIP_UNSCHEDULABLE;
+        if (best != 0) {
+          const int32_t w = key_node(best);
+          const uint64_t hit = __ballot(lane < nm && my_node == w);
+          // w is a row of M (lane `hit`) or new this round: then it is the staged
+          // candidate, or (non-monotone pods only) an M' node
+          const int32_t rw = hit ? __builtin_ctzll(hit) : nm;
+          if (!hit && lane == rw) {
+            if (staged == w) {
+              my = stg;
+              if constexpr (NUMA) mynr = stgnr;
+            } else {
+              load_row(my, d, w);
+              if constexpr (NUMA) load_numa_row(mynr, d, w);
+            }
+          }
+          bool ok = true;
+          if constexpr (NUMA) {
+            if (numa_on(c) && is_cpuset(pod)) {
+              // NodeNUMAResource Reserve: lane rw replays the accumulator on its
+              // row, the chosen CPUs are broadcast to the wave
+              uint64_t mc[NW] = {0, 0, 0, 0};
+              int okl = 0;
+              if (lane == rw) okl = mynr.cls >= 0 && numa_allocate(d.nu.cls[mynr.cls], mynr, pod, mc);
+              ok = __builtin_amdgcn_readlane(okl, rw) != 0;
+#pragma unroll
+              for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], rw);
+            }
+          }
+          if (!ok) {
+            result = KOORDHIP_RESERVE_FAILED;  // every Reserve is rolled back
+          } else {
+            result = w;
+            if (!hit) {
+              nm++;
+              if (lane == rw) {
+                my_node = w;
+                modmap[w >> 5] |= 1u << (w & 31);
+              }
+            }
+            if (lane == rw) {
+              apply_delta(my, pod, +1);
+              if constexpr (NUMA) {
+                if (numa_on(c) && is_cpuset(pod)) numa_apply(mynr, pod, cpus, +1);
+              }
+            }
+          }
+        }
+        if (lane == 0) out_node[p0 + j] = result;
+        if (out_cpus && lane < NW)
+          out_cpus[(size_t)(p0 + j) * NW + lane] =
+              lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
+      }
+      // ---- 4. write M back, hand it to the next round as M' (rows stay in LDS)
+      if (lane < nm) {
+        store_row(my, d, my_node);
+        if constexpr (NUMA) store_numa_row(mynr, d, my_node);
+        prow[lane] = my;
+        if constexpr (NUMA) pnr[lane] = mynr;
+        pnode[lane] = my_node;
+        modmap[my_node >> 5] = 0;  // clear the round's bits (whole words: every bit set is M's)
+      }
+      if (lane == 0) {
+        sh_mp = nm;
+        store_release(&sy->res_round, r + 1);  // after every lane's stores (one wave: program order)
+      }
+      if (dbg && lane == 0) {
+        const uint64_t t_end = stamp();
+        c_pro += t_pro - t_entry;
+        c_loop += t_end - t_pro;
+        c_wait += t_entry - t_w0;
       }
     }
     __syncthreads();
   }
+  if (t <= RES_MAXP_ROUND && t <= sh_mp) mbuf[t] = t == 0 ? sh_mp : pnode[t - 1];  // hand M' on
   if (dbg && t == 0) {
-    atomicAdd((unsigned long long *)&dbg[1], (unsigned long long)(t_load - t_entry));
-    atomicAdd((unsigned long long *)&dbg[2], (unsigned long long)(stamp() - t_load));
-  }
-  if (t >= 64) return;  // the sequential part is wave 0's
-  __builtin_amdgcn_s_setprio(3);
-  const uint64_t t_pro = dbg ? stamp() : 0;
-  uint64_t n_eval = 0, n_miss = 0, t_a = 0, t_b = 0, t_c = 0, t_m = t_pro;
-  NV my{}, stg{};
-  NumaRow mynr{}, stgnr{};
-  int32_t my_node = -1;
-  int32_t nm = 0;  // |M| (wave-uniform)
-  const bool two = k > 64;
-  for (int32_t j = 0; j < n_pods; j++) {
-    const DevPod pod = uniform_pod(lpod[j]);
-    // candidate: the best entry outside M (every list key is exact); first
-    // among the pod's RES_TOP best, else from the whole list
-    const uint64_t tv = lane < RES_TOP ? top[j * RES_TOP + lane] : 0ull;
-    bool tmod = false;
-    if (tv) {
-      const int32_t nd = key_node(tv);
-      tmod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-    }
-    const uint64_t tfree = __ballot(tv != 0 && !tmod);
-    uint64_t cand = 0;
-    bool prefix_modified;
-    if (tfree || lcnt[j] <= RES_TOP) {
-      const int first = tfree ? __builtin_ctzll(tfree) : 64;
-      cand = tfree ? readlane_u64(tv, first) : 0ull;
-      // an M node can only win if its (upper-bound) list key beats the candidate
-      prefix_modified = __ballot(tv != 0 && tmod && lane < first) != 0;
-    } else {
-      const uint64_t *L = lk + (size_t)j * kp;
-      const uint64_t e0 = lane < k ? L[lane] : 0ull;  // lanes past k hold nothing (k may be < 64)
-      const uint64_t e1 = two && 64 + lane < k ? L[64 + lane] : 0ull;
-      bool mod0 = false, mod1 = false;
-      if (e0) {
-        const int32_t nd = key_node(e0);
-        mod0 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-      }
-      if (e1) {
-        const int32_t nd = key_node(e1);
-        mod1 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-      }
-      const uint64_t f0 = (e0 != 0 && !mod0) ? e0 : 0ull, f1 = (e1 != 0 && !mod1) ? e1 : 0ull;
-      cand = wave_max_u64_dpp(f0 > f1 ? f0 : f1);
-      prefix_modified = (__ballot(mod0 && e0 > cand) | __ballot(mod1 && e1 > cand)) != 0;
-    }
-    // stage the candidate's row into lane nm's staging registers (separate
-    // from the M rows, so the re-evaluation below does not wait for it)
-    int32_t staged = -1;
-    if (cand != 0) {
-      const int32_t cn = key_node(cand);
-      const uint64_t pm0 = __ballot(pre_node[lane] == cn);
-      const uint64_t pm1 = __ballot(pre_node[lane + 64] == cn);
-      const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
-      if (src >= 0) {
-        if (lane == nm) {
-          stg = pre[src];
-          if constexpr (NUMA) {
-            stgnr = prenr[src];
-          }
-        }
-      } else {
-        const int32_t sl = mp > 0 ? prev_slot(cn) : -1;  // an M' node: its row is in LDS
-        if (sl >= 0) {
-          if (lane == nm) {
-            stg = prow[sl];
-            if constexpr (NUMA) stgnr = pnr[sl];
-          }
-        } else {
-          n_miss++;
-          if (lane == nm) {
-            load_row(stg, d, cn);
-            if constexpr (NUMA) load_numa_row(stgnr, d, cn);
-          }
-        }
-      }
-      staged = cn;
-    }
-    if (dbg) {
-      const uint64_t x = stamp();
-      t_a += x - t_m;
-      t_m = x;
-    }
-    const bool nonmono = !monotone || (NUMA && is_cpuset(pod) && KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
-    uint64_t best = cand;
-    if (nm > 0 && (prefix_modified || nonmono)) {
-      uint64_t key = 0;
-      if (lane < nm) {
-        if constexpr (NUMA) {
-          key = make_key(eval_total_numa(pod, my, mynr, d.nu.cls, c), my_node);
-        } else {
-          key = make_key(eval_total(pod, my, c), my_node);
-        }
-      }
-      key = wave_max_u64_dpp(key);
-      best = key > best ? key : best;
-      n_eval++;
-    }
-    if (nonmono && mp > 0) {  // M' nodes outside M: current rows in LDS
-      uint64_t key = 0;
-      if (lane < mp) {
-        const int32_t nd = prev_mod[1 + lane];
-        const bool in_m = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-        if (!in_m) {
-          if constexpr (NUMA) {
-            key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], d.nu.cls, c), nd);
-          } else {
-            key = make_key(eval_total(pod, prow[lane], c), nd);
-          }
-        }
-      }
-      key = wave_max_u64_dpp(key);
-      best = key > best ? key : best;
-    }
-    if (j == trace_j) {  // diagnostics (KOORDHIP_TRACE_POD)
-      if (lane == 0)
-        printf("[trace] j=%d cand=%d/%d best=%d/%d nm=%d mp=%d nonmono=%d prefix=%d\n", j,
-               cand ? key_node(cand) : -1, cand ? key_score(cand) : -1, best ? key_node(best) : -1,
-               best ? key_score(best) : -1, nm, mp, (int)nonmono, (int)prefix_modified);
-      if (lane < nm) printf("[trace] M lane %d node %d\n", lane, my_node);
-      if (lane < mp) printf("[trace] M' lane %d node %d\n", lane, prev_mod[1 + lane]);
-      if (lane < RES_TOP) printf("[trace] top %d: %d/%d mod %d\n", lane, tv ? key_node(tv) : -1, tv ? key_score(tv) : -1, (int)tmod);
-    }
-    if (dbg) {
-      const uint64_t x = stamp();
-      t_b += x - t_m;
-      t_m = x;
-    }
-    uint64_t cpus[NW] = {0, 0, 0, 0};
-    if (best == 0) {
-      if (lane == 0) out_node[j] = KOORDHIP_UNSCHEDULABLE;
-    } else {
-      const int32_t w = key_node(best);
-      const uint64_t hit = __ballot(lane < nm && my_node == w);
-      // w is a row of M (lane `hit`) or new this round: then it is the staged
-      // candidate, or (non-monotone pods only) an M' node
-      const int32_t r = hit ? __builtin_ctzll(hit) : nm;
-      if (!hit && lane == r) {  // a new row: the staged candidate, or (non-monotone pods) an M' node
-        if (staged == w) {
-          my = stg;
-          if constexpr (NUMA) mynr = stgnr;
-        } else {
-          load_row(my, d, w);
-          if constexpr (NUMA) load_numa_row(mynr, d, w);
-        }
-      }
-      bool ok = true;
-      if constexpr (NUMA) {
-        if (numa_on(c) && is_cpuset(pod)) {
-          // NodeNUMAResource Reserve: lane r replays the accumulator on its row,
-          // the chosen CPUs are broadcast to the wave
-          uint64_t mc[NW] = {0, 0, 0, 0};
-          int okl = 0;
-          if (lane == r) okl = mynr.cls >= 0 && numa_allocate(d.nu.cls[mynr.cls], mynr, pod, mc);
-          ok = __builtin_amdgcn_readlane(okl, r) != 0;
-#pragma unroll
-          for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], r);
-          if (j == trace_j && lane == 0)
-            printf("[trace] reserve node %d ok %d cpus %llx %llx %llx %llx\n", w, (int)ok, (unsigned long long)cpus[0],
-                   (unsigned long long)cpus[1], (unsigned long long)cpus[2], (unsigned long long)cpus[3]);
-        }
-      }
-      if (!ok) {
-        if (lane == 0) out_node[j] = KOORDHIP_RESERVE_FAILED;  // every Reserve is rolled back
-      } else {
-        if (lane == 0) out_node[j] = w;
-        if (!hit) {
-          nm++;
-          if (lane == r) {
-            my_node = w;
-            modmap[w >> 5] |= 1u << (w & 31);
-          }
-        }
-        if (lane == r) {
-          apply_delta(my, pod, +1);
-          if constexpr (NUMA) {
-            if (numa_on(c) && is_cpuset(pod)) numa_apply(mynr, pod, cpus, +1);
-          }
-        }
-      }
-    }
-    if (dbg) {
-      const uint64_t x = stamp();
-      t_c += x - t_m;
-      t_m = x;
-    }
-    if (out_cpus && lane < NW)
-      out_cpus[(size_t)j * NW + lane] = lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
-  }
-  if (lane < nm) {
-    store_row(my, d, my_node);
-    if constexpr (NUMA) store_numa_row(mynr, d, my_node);
-    next_mod[1 + lane] = my_node;
-  }
-  if (lane == 0) next_mod[0] = nm;
-  if (dbg && lane == 0) {
-    const uint64_t t_end = stamp();
-    atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)(t_pro - t_entry));
-    atomicAdd((unsigned long long *)&dbg[14], (unsigned long long)t_a);
-    atomicAdd((unsigned long long *)&dbg[15], (unsigned long long)t_b);
-    atomicAdd((unsigned long long *)&dbg[3], (unsigned long long)t_c);
-    atomicAdd((unsigned long long *)&dbg[4], (unsigned long long)(t_end - t_entry));
+    atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)c_pro);
+    atomicAdd((unsigned long long *)&dbg[1], (unsigned long long)c_wait);
+    atomicAdd((unsigned long long *)&dbg[4], (unsigned long long)c_loop);
     atomicAdd((unsigned long long *)&dbg[5], (unsigned long long)n_eval);
     atomicAdd((unsigned long long *)&dbg[6], (unsigned long long)n_miss);
-    atomicAdd((unsigned long long *)&dbg[7], (unsigned long long)n_pods);
+    atomicAdd((unsigned long long *)&dbg[7], (unsigned long long)total);
   }
 }
 
@@ -1276,15 +1315,16 @@ int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool n
   return res_lds(n_pods_max, kp, n_nodes, numa).total;
 }
 
-hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t k,
-                          const uint64_t *lists, int32_t monotone, const int32_t *prev_mod, int32_t *next_mod,
-                          int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg, int32_t trace_j, hipStream_t s) {
-  if (n_pods <= 0) return hipSuccess;
-  if (n_pods > RES_MAXP_ROUND || k > RES_MAXP || k < 1) return hipErrorInvalidValue;
+hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t total, int32_t P, int32_t k,
+                          int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
+                          PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
+                          int32_t trace, hipStream_t s) {
+  if (total <= 0 || r_end <= r_begin) return hipSuccess;
+  if (P > RES_MAXP_ROUND || P < 1 || k > RES_MAXP || k < 1) return hipErrorInvalidValue;
   int32_t kp = 1;
   while (kp < k) kp <<= 1;
   const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
-  const ResLds o = res_lds(n_pods, kp, d.n, numa);
+  const ResLds o = res_lds(P, kp, d.n, numa);
   static bool attr[2] = {false, false};
   if (!attr[numa]) {
     const void *f = numa ? (const void *)k_resolve<true> : (const void *)k_resolve<false>;
@@ -1294,11 +1334,21 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods
   }
   if (o.total > RES_LDS_MAX) return hipErrorInvalidValue;
   if (numa)
-    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(res_threads<true>()), o.total, s, c, d, pods, n_pods, k, kp, lists,
-                       monotone, prev_mod, next_mod, o, out_node, out_cpus, dbg, trace_j);
+    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(res_threads<true>()), o.total, s, c, d, pods, total, P, k, kp,
+                       r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace);
   else
-    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(res_threads<false>()), o.total, s, c, d, pods, n_pods, k, kp, lists,
-                       monotone, prev_mod, next_mod, o, out_node, out_cpus, dbg, trace_j);
+    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(res_threads<false>()), o.total, s, c, d, pods, total, P, k, kp,
+                       r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace);
+  return hipGetLastError();
+}
+
+hipError_t launch_wait_resolved(PipeSync *sync, int32_t rounds, hipStream_t s) {
+  hipLaunchKernelGGL(k_wait_resolved, dim3(1), dim3(64), 0, s, sync, rounds);
+  return hipGetLastError();
+}
+
+hipError_t launch_signal_lists(PipeSync *sync, int32_t rounds, hipStream_t s) {
+  hipLaunchKernelGGL(k_signal_lists, dim3(1), dim3(64), 0, s, sync, rounds);
   return hipGetLastError();
 }
 
