@@ -991,7 +991,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
       int32_t nm = 0;  // |M| (wave-uniform)
       my_node = -1;
       for (int32_t j = 0; j < n_pods; j++) {
-        const DevPod pod = uniform_pod(lpod[j]);
+        const DevPod pod = lpod[j];  // VGPR copy: SGPRs are the scarce register file here
         // candidate: the best entry outside M (every list key is exact); first
         // among the pod's RES_TOP best, else from the whole list
         const uint64_t tv = lane < RES_TOP ? top[j * RES_TOP + lane] : 0ull;
