@@ -166,7 +166,7 @@ def main():
     pods_total = args.pods * args.steps
     evals_total = args.pods * args.nodes * args.steps   # every pod is evaluated against every node
     value = pods_total / elapsed
-    # roofline of the dominant kernel (k_topk_partial), this rank's launches
+    # roofline of the evaluation kernel (k_scan), this rank's launches
     b_eval = bytes_per_eval(pods, cfg)
     b_per_pod = float(b_eval.mean())
     avg_launch_ms = eval_ms / max(launches, 1)
@@ -189,12 +189,12 @@ def main():
         "data": "synthetic (seeded splitmix64 cluster + pod stream, SURVEY.md §8(d))",
         "config": {"workload": f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
                                "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile",
-                   "nodes": args.nodes, "pods": args.pods, "batch_pods": eng.cfg.batch_pods or 64,
+                   "nodes": args.nodes, "pods": args.pods, "batch_pods": eng.cfg.batch_pods or 32,
                    "parallelism": f"node-shard x{world}"},
         "unschedulable": int((placements < 0).sum()),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 3) if achieved else None,
-                     "traffic": traffic, "kernel": "k_topk_partial",
+                     "traffic": traffic, "kernel": "k_scan",
                      "avg_launch_us": round(avg_launch_ms * 1e3, 3), "evals_per_launch": evals_per_launch,
                      "bytes_per_eval": round(b_per_pod, 2), "traffic_source": traffic_src},
     }

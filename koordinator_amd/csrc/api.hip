@@ -908,7 +908,13 @@ int place_staged_impl(koordhip_ctx *c) {
   // whatever the stream -> queue mapping).
   const int32_t total = c->n_staged;
   const int32_t rounds = (total + P - 1) / P;
-  const bool persistent = !c->group && !std::getenv("KOORDHIP_ROUND_LAUNCH");
+  // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises
+  // dispatches): every launch on one stream in dependency order, one resolve
+  // per round; the lists are then one round fresher than in the pipeline,
+  // which the resolve treats exactly like refreshed entries.
+  const bool serial = std::getenv("KOORDHIP_SERIAL") != nullptr;
+  hipStream_t rs = serial ? c->stream : c->rstream;
+  const bool persistent = !serial && !c->group && !std::getenv("KOORDHIP_ROUND_LAUNCH");
   const char *trace_env = std::getenv("KOORDHIP_TRACE_POD");  // diagnostics: printf one pod's resolve step
   const int32_t trace = trace_env ? std::atoi(trace_env) : -1;
   const int64_t list_buf = (int64_t)(lbytes / sizeof(uint64_t));
@@ -921,7 +927,7 @@ int place_staged_impl(koordhip_ctx *c) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
     const kh::DevPod *pods = c->d_pods + p0;
     uint64_t *lists = c->d_lists + (size_t)(r & 1) * list_buf;
-    if (r >= 2) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, c->stream));
+    if (r >= 2 && !serial) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, c->stream));
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
       if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true)) return e;
@@ -933,14 +939,18 @@ int place_staged_impl(koordhip_ctx *c) {
     }
     HIP_TRY(kh::launch_signal_lists(sync, r + 1, c->stream));
     if (!persistent) {
-      HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
-      HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_res[r % kRing], 0));
+      if (!serial) {
+        HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
+        HIP_TRY(hipStreamWaitEvent(rs, c->ev_res[r % kRing], 0));
+      }
       HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, sync,
-                                 mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
+                                 mbuf, c->d_out, cpus, c->d_dbg, trace, rs));
     }
   }
-  HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));
-  HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[0], 0));
+  if (!serial) {
+    HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[0], 0));
+  }
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   c->pipe_check = true;
   if (c->d_dbg) {

@@ -784,8 +784,15 @@ constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) be
 __device__ __forceinline__ int32_t load_acquire(const int32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Publish a flag after this wave's global stores (MI355X_MICROARCH.md
+// cross-XCD hand-off: wait for the stores, write the XCD L2 back, wait for
+// the write-back -- spelled out in asm because ROCm 7.2 can drop the wait
+// after buffer_wbl2 -- then a relaxed agent-scope flag store).
 __device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Spin (one thread) until *p >= v; false when the watchdog fires or the other

@@ -247,3 +247,23 @@ def test_sharded_group_bit_exact(Engine, world, n_nodes, n_pods, be, batch):
     for s in states:
         for k in ("requested", "npods", "la_used"):
             assert np.array_equal(s[k], rs[k]), k
+
+
+# ----------------------------------------------------------- launch modes
+@pytest.mark.parametrize("mode", ["KOORDHIP_ROUND_LAUNCH", "KOORDHIP_SERIAL"])
+@pytest.mark.parametrize("numa", [False, True])
+def test_launch_modes_bit_exact(Engine, monkeypatch, mode, numa):
+    """The per-round resolve launch (local groups) and the single-stream
+    profiling order place exactly like the persistent pipeline and the oracle."""
+    monkeypatch.setenv(mode, "1")
+    prof = shipped_profile(numa=numa)
+    prof.batch_pods = 16
+    table = synth.make_cluster(synth.ClusterSpec(400), prof)
+    if numa:
+        synth.add_numa(table, synth.NumaSpec(), prof)
+    pods = synth.make_pods(synth.StreamSpec(700, be_frac=0.3, cpuset_frac=0.4 if numa else 0.0), prof)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(table)
+        got = e.place_stream(pods)
+    ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods)
+    assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
