@@ -963,9 +963,10 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[11], (unsigned long long)h[12], (unsigned long long)h[13]);
     std::fprintf(stderr,
                  "[koordhip stamps] resolve cycles: prologue %llu  waiting for lists %llu  loop %llu  | re-evals %llu "
-                 "prefetch-misses %llu pods %llu\n",
+                 "prefetch-misses %llu pods %llu | prologue: loads+hash %llu refresh+top %llu (refresh %llu) | release %llu\n",
                  (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[4],
-                 (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7]);
+                 (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7],
+                 (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[15], (unsigned long long)h[14]);
   }
   return 0;
 }

@@ -453,7 +453,6 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
 
 constexpr int SEL_THREADS = 1024;
 constexpr int SEL_WAVES = SEL_THREADS / 64;
-constexpr int SEL_MAXCHUNKS = 8192;  // chunk maxima staged in LDS
 
 // inclusive block prefix sum of one value per thread (SEL_THREADS threads)
 __device__ __forceinline__ int32_t sel_scan(int32_t v, int32_t *wsum, int32_t *total) {
@@ -539,6 +538,36 @@ __device__ __forceinline__ uint64_t sel_mask_eq(const uint4 *q, uint32_t x) {
   return m;
 }
 
+// Wave-level walk of a histogram from the top bin down to bin `floor`: the
+// k-th largest value (0 if fewer than k values >= floor) and how many values
+// lie strictly above it.  `count(v)` reads bin v; wave-uniform results.
+template <typename F>
+__device__ __forceinline__ void sel_walk(F count, int32_t nbins, int32_t floor, int32_t k, int32_t &thr, int32_t &gt) {
+  const int lane = lane_id();
+  int32_t cum = 0;
+  thr = 0;
+  gt = 0;
+  for (int32_t top = nbins - 1; top >= floor && thr == 0; top -= 64) {
+    const int32_t v = top - lane;
+    const int32_t c = v >= floor ? count(v) : 0;
+    if (__ballot(c != 0) == 0) continue;  // wave-uniform
+    int32_t x = c;  // inclusive prefix over lanes = bins top, top-1, ...
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    const uint64_t hit = __ballot(c != 0 && cum + x >= k);
+    if (hit) {
+      const int l = __builtin_ctzll(hit);
+      thr = top - l;
+      gt = cum + __shfl(x, l, 64) - __shfl(c, l, 64);
+    } else {
+      cum += __shfl(x, 63, 64);
+    }
+  }
+}
+
 __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restrict__ S, int64_t s_stride, int32_t lo,
                                                         int32_t m, int32_t k, int32_t nbins,
                                                         const uint16_t *__restrict__ Mx, int32_t m_stride,
@@ -547,9 +576,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
   // dbg (diagnostic builds only, KOORDHIP_STAMPS): per-phase s_memtime sums of thread 0
   uint64_t ts[6] = {0, 0, 0, 0, 0, 0};
   if (dbg && threadIdx.x == 0) ts[0] = stamp();
-  extern __shared__ uint32_t hist[];  // nbins
+  extern __shared__ uint32_t hist[];  // nbins score bins, then (nbins + 1) / 2 packed u16 chunk-max bins
+  uint32_t *mhist = hist + nbins;
   __shared__ uint64_t gtbuf[RES_MAXP];
-  __shared__ uint16_t mxs[SEL_MAXCHUNKS];
   __shared__ int32_t wsum[SEL_WAVES];
   __shared__ int32_t sh_thr, sh_gt, sh_cnt_gt;
   const int t = threadIdx.x, lane = lane_id();
@@ -559,25 +588,28 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
   // first tile in flight while the lower bound is computed
   uint4 q[SEL_ITER];
   sel_load(row, m, 0, t, q);
-  for (int32_t j = t; j < nbins; j += SEL_THREADS) hist[j] = 0;
+  const int32_t mwords = nchunks >= k ? (nbins + 1) >> 1 : 0;
+  for (int32_t j = t; j < nbins + mwords; j += SEL_THREADS) hist[j] = 0;
   if (t == 0) sh_cnt_gt = 0;
-  // ---- lower bound L: k-th largest chunk maximum (radix select, MSB first)
+  // ---- lower bound L: k-th largest chunk maximum (histogram of the chunk
+  //      maxima, then one wave walks it top-down)
   uint32_t L = 1;
-  if (nchunks >= k) {
+  if (mwords) {
     const uint16_t *mrow = Mx + (size_t)p * m_stride;
-    for (int32_t j = t; j < nchunks; j += SEL_THREADS) mxs[j] = mrow[j];
     __syncthreads();
-    const int bits = 32 - __builtin_clz((uint32_t)(nbins - 1));
-    uint32_t acc = 0;
-    for (int b = bits - 1; b >= 0; b--) {
-      const uint32_t cand = acc | (1u << b);
-      int32_t cnt = 0;
-      for (int32_t j = t; j < nchunks; j += SEL_THREADS) cnt += (uint32_t)mxs[j] >= cand;
-      int32_t total;
-      (void)sel_scan(cnt, wsum, &total);
-      if (total >= k) acc = cand;
+    for (int32_t j = t; j < nchunks; j += SEL_THREADS) {
+      const uint32_t v = mrow[j];
+      if (v) atomicAdd(&mhist[v >> 1], 1u << (16 * (v & 1)));  // counts <= nchunks < 2^16
     }
-    L = acc > 1 ? acc : 1;
+    __syncthreads();
+    if (t < 64) {
+      int32_t thr, gt;
+      sel_walk([&](int32_t v) { return (int32_t)((mhist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu); }, nbins, 1, k, thr,
+               gt);
+      if (lane == 0) sh_thr = thr;
+    }
+    __syncthreads();
+    L = sh_thr > 1 ? (uint32_t)sh_thr : 1u;
   }
   __syncthreads();
   if (dbg && t == 0) ts[1] = stamp();
@@ -595,26 +627,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
   if (dbg && t == 0) ts[2] = stamp();
   // ---- k-th largest value S*: wave 0 walks the bins top-down, 64 at a time
   if (t < 64) {
-    int32_t cum = 0, thr = 0, gt = 0;
-    for (int32_t top = nbins - 1; top >= (int32_t)L && thr == 0; top -= 64) {
-      const int32_t v = top - lane;
-      const int32_t c = v >= (int32_t)L ? (int32_t)hist[v] : 0;
-      if (__ballot(c != 0) == 0) continue;  // wave-uniform
-      int32_t x = c;  // inclusive prefix over lanes = bins top, top-1, ...
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int32_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-      }
-      const uint64_t hit = __ballot(c != 0 && cum + x >= k);
-      if (hit) {
-        const int l = __builtin_ctzll(hit);
-        thr = top - l;
-        gt = cum + __shfl(x, l, 64) - __shfl(c, l, 64);
-      } else {
-        cum += __shfl(x, 63, 64);
-      }
-    }
+    int32_t thr, gt;
+    sel_walk([&](int32_t v) { return (int32_t)hist[v]; }, nbins, (int32_t)L, k, thr, gt);
     if (thr == 0) {  // fewer than k feasible (then L == 1): take every feasible node
       thr = 1;
       gt = 0;
@@ -729,8 +743,8 @@ constexpr int RES_HASH = 256;  // node -> M' slot (open addressing)
 constexpr int RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (static LDS: a few flags)
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
-  int32_t lists, pods, prev_rows, prev_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node, want, top, lcnt, modmap,
-      total;
+  int32_t lists, pods, prev_rows, prev_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node, want, top, lcnt, hits,
+      hmask, modmap, total;
 };
 
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
@@ -762,6 +776,10 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * RES_TOP * 8;
   o.lcnt = at;
   at += RES_MAXP_ROUND * 4;
+  o.hits = at;  // (pod, list position, M' slot) of the entries to refresh: <= P x |M'|
+  at += res_align(n_pods_max * n_pods_max * 4);
+  o.hmask = at;  // per pod: which list positions were refreshed (2 x 64 bits)
+  at += RES_MAXP_ROUND * 2 * 8;
   o.modmap = at;
   at += res_align(((n_nodes + 31) >> 5) * 4);
   o.total = at;
@@ -843,9 +861,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
   uint64_t *top = reinterpret_cast<uint64_t *>(lds + ofs.top);
   int32_t *lcnt = reinterpret_cast<int32_t *>(lds + ofs.lcnt);
   uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
+  int32_t *hits = reinterpret_cast<int32_t *>(lds + ofs.hits);
+  uint64_t *hmask = reinterpret_cast<uint64_t *>(lds + ofs.hmask);
   DevPod *lpod = reinterpret_cast<DevPod *>(lds + ofs.pods);
   __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous round committed to
-  __shared__ int32_t sh_mp, sh_stop;
+  __shared__ int32_t sh_mp, sh_stop, sh_nhit;
   const int t = threadIdx.x, lane = lane_id();
   const int32_t words = (d.n + 31) >> 5;
   const bool two = k > 64;
@@ -872,7 +892,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
   NV my{}, stg{};
   NumaRow mynr{}, stgnr{};
   int32_t my_node = -1;
-  uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0;
+  uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0, c_ph_a = 0, c_ph_b = 0, c_ph_r = 0, c_rel = 0;
   for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
     const int32_t n_pods = min(P, total - p0);
     const DevPod *rp = pods + p0;
@@ -918,6 +938,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
       pre_node[t] = nd;
     }
     for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
+    if (t == 0) sh_nhit = 0;
     __syncthreads();
     if (t < mp) {  // M' hash: node -> slot, linear probing, lock-free inserts
       const int32_t nd = pnode[t];
@@ -926,6 +947,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
       hslot[h] = t;
     }
     __syncthreads();
+    const uint64_t t_a = (dbg && t == 0) ? stamp() : 0;
     auto prev_slot = [&](int32_t nd) -> int32_t {
       uint32_t h = res_hash(nd);
       for (;;) {
@@ -935,47 +957,84 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
         h = (h + 1) & (RES_HASH - 1);
       }
     };
-    // ---- 2. per pod (one wave each, pod record wave-uniform, lane = list
-    //         position): refresh the keys of the entries on M' nodes (exact,
-    //         current rows), then extract the RES_TOP best keys in order -- the
-    //         loop nearly always finds its candidate among them; the lists
-    //         themselves stay unsorted
+    // ---- 2. refresh the keys of the list entries on M' nodes (exact, current
+    //         rows): (a) one wave per pod collects them, (b) every thread
+    //         evaluates one -- at most one entry per (pod, M' node), so one
+    //         pass for |M'| x P <= threads; (c) one wave per pod extracts the
+    //         RES_TOP best keys in order -- the loop nearly always finds its
+    //         candidate among them; the lists themselves stay unsorted
     {
       const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-      for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
-        uint64_t *L = lk + (size_t)j * kp;
-        if (mp > 0) {
-          const DevPod pod = uniform_pod(lpod[j]);
+      if (mp > 0) {
+        for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
+          const uint64_t *L = lk + (size_t)j * kp;
           for (int32_t q = lane; q < kp; q += 64) {
             const uint64_t e = L[q];
             const int32_t sl = e ? prev_slot(key_node(e)) : -1;
-            if (__ballot(sl >= 0) == 0) continue;
-            if (sl >= 0) {
-              int32_t tot;
-              if constexpr (NUMA) {
-                tot = eval_total_numa(pod, prow[sl], pnr[sl], d.nu.cls, c);
-              } else {
-                tot = eval_total(pod, prow[sl], c);
-              }
-              L[q] = make_key(tot, key_node(e));
-            }
+            const uint64_t b = __ballot(sl >= 0);
+            if (lane == 0) hmask[2 * j + (q >> 6)] = b;
+            if (b == 0) continue;
+            int32_t base = 0;
+            if (lane == 0) base = atomicAdd(&sh_nhit, __popcll(b));
+            base = __shfl(base, 0, 64);
+            if (sl >= 0) hits[base + __popcll(b & ((1ull << lane) - 1))] = (j << 16) | (q << 8) | sl;
           }
         }
-        uint64_t x0 = lane < kp ? L[lane] : 0ull, x1 = 64 + lane < kp ? L[64 + lane] : 0ull;
-        const int32_t cnt = __popcll(__ballot(x0 != 0)) + __popcll(__ballot(x1 != 0));
-        for (int tt = 0; tt < RES_TOP; tt++) {
-          const uint64_t m = wave_max_u64_dpp(x0 > x1 ? x0 : x1);
-          if (lane == 0) top[j * RES_TOP + tt] = m;
-          x0 = x0 == m ? 0ull : x0;
-          x1 = x1 == m ? 0ull : x1;
-          if (tt < 2 && lane == 0) {  // the two best: rows to prefetch (M' rows are in LDS already)
-            const int32_t nd = m ? key_node(m) : -1;
-            want[2 * j + tt] = (nd >= 0 && (mp == 0 || prev_slot(nd) < 0)) ? nd : -1;
+        __syncthreads();
+        const int32_t nh = sh_nhit;
+        for (int32_t h = t; h < nh; h += RES_THREADS) {
+          const int32_t x = hits[h], j = x >> 16, q = (x >> 8) & 0xFF, sl = x & 0xFF;
+          const DevPod pod = lpod[j];
+          int32_t tot;
+          if constexpr (NUMA) {
+            tot = eval_total_numa(pod, prow[sl], pnr[sl], d.nu.cls, c);
+          } else {
+            tot = eval_total(pod, prow[sl], c);
           }
+          lk[(size_t)j * kp + q] = make_key(tot, pnode[sl]);
+        }
+        __syncthreads();
+      }
+      if (dbg && t == 0) c_ph_r += stamp() - t_a;
+      // (c) the lists arrive sorted (descending keys; k_select / k_topk_merge
+      //     output contract) and only the refreshed entries moved, so each
+      //     entry's rank = unrefreshed entries before it + refreshed entries
+      //     above it (a refreshed entry: every entry above it)
+      const uint64_t lt = (1ull << lane) - 1;
+      for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
+        const uint64_t *L = lk + (size_t)j * kp;
+        const uint64_t x0 = lane < kp ? L[lane] : 0ull, x1 = 64 + lane < kp ? L[64 + lane] : 0ull;
+        const int32_t cnt = __popcll(__ballot(x0 != 0)) + __popcll(__ballot(x1 != 0));
+        const uint64_t m0 = mp > 0 ? hmask[2 * j] : 0ull, m1 = (mp > 0 && two) ? hmask[2 * j + 1] : 0ull;
+        const bool f0 = (m0 >> lane) & 1, f1 = (m1 >> lane) & 1;  // refreshed
+        int32_t r0 = __popcll(~m0 & lt), r1 = __popcll(~m0) + __popcll(~m1 & lt);
+        for (uint64_t mm = m0; mm; mm &= mm - 1) {
+          const int l = __builtin_ctzll(mm);
+          const uint64_t v = readlane_u64(x0, l);
+          const int32_t rv = __popcll(__ballot(x0 > v)) + __popcll(__ballot(x1 > v));
+          r0 = lane == l ? rv : r0 + (!f0 && v > x0);
+          r1 += !f1 && v > x1;
+        }
+        for (uint64_t mm = m1; mm; mm &= mm - 1) {
+          const int l = __builtin_ctzll(mm);
+          const uint64_t v = readlane_u64(x1, l);
+          const int32_t rv = __popcll(__ballot(x0 > v)) + __popcll(__ballot(x1 > v));
+          r1 = lane == l ? rv : r1 + (!f1 && v > x1);
+          r0 += !f0 && v > x0;
+        }
+        uint64_t *tp = top + j * RES_TOP;
+        if (lane < RES_TOP) tp[lane] = 0ull;
+        if (x0 != 0 && r0 < RES_TOP) tp[r0] = x0;
+        if (x1 != 0 && r1 < RES_TOP) tp[r1] = x1;
+        if (lane < 2) {  // the two best: rows to prefetch (M' rows are in LDS already)
+          const uint64_t m = tp[lane];
+          const int32_t nd = m ? key_node(m) : -1;
+          want[2 * j + lane] = (nd >= 0 && (mp == 0 || prev_slot(nd) < 0)) ? nd : -1;
         }
         if (lane == 0) lcnt[j] = cnt;
       }
       __syncthreads();
+      if (dbg && t == 0) c_ph_a += t_a - t_entry, c_ph_b += stamp() - t_a;
       if (t < RES_PRE && t < 2 * n_pods) {  // reload the slots whose head changed
         const int32_t nd = want[t];
         if (nd >= 0 && nd != pre_node[t]) {
@@ -1165,10 +1224,12 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
         pnode[lane] = my_node;
         modmap[my_node >> 5] = 0;  // clear the round's bits (whole words: every bit set is M's)
       }
+      const uint64_t t_rel = dbg ? stamp() : 0;
       if (lane == 0) {
         sh_mp = nm;
         store_release(&sy->res_round, r + 1);  // after every lane's stores (one wave: program order)
       }
+      if (dbg) c_rel += stamp() - t_rel;
       if (dbg && lane == 0) {
         const uint64_t t_end = stamp();
         c_pro += t_pro - t_entry;
@@ -1186,6 +1247,10 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
     atomicAdd((unsigned long long *)&dbg[5], (unsigned long long)n_eval);
     atomicAdd((unsigned long long *)&dbg[6], (unsigned long long)n_miss);
     atomicAdd((unsigned long long *)&dbg[7], (unsigned long long)total);
+    atomicAdd((unsigned long long *)&dbg[2], (unsigned long long)c_ph_a);
+    atomicAdd((unsigned long long *)&dbg[3], (unsigned long long)c_ph_b);
+    atomicAdd((unsigned long long *)&dbg[14], (unsigned long long)c_rel);
+    atomicAdd((unsigned long long *)&dbg[15], (unsigned long long)c_ph_r);
   }
 }
 
@@ -1295,8 +1360,11 @@ hipError_t launch_select(const uint16_t *S, int64_t s_stride, int32_t lo, int32_
                          uint64_t *dbg, hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   if (k < 1 || k > RES_MAXP || nbins < 2 || nbins > 32768) return hipErrorInvalidValue;
-  if (nchunks > SEL_MAXCHUNKS) nchunks = 0;  // no lower bound: histogram the whole row
-  const size_t lds = (size_t)nbins * sizeof(uint32_t);
+  if (nchunks > 65535) nchunks = 0;  // no lower bound: histogram the whole row
+  size_t lds = (size_t)nbins * sizeof(uint32_t);
+  if (lds + (size_t)((nbins + 1) / 2) * sizeof(uint32_t) > 128 * 1024)
+    nchunks = 0;  // chunk-max histogram does not fit beside the score histogram
+  if (nchunks >= k) lds += (size_t)((nbins + 1) / 2) * sizeof(uint32_t);
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void *)k_select, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
