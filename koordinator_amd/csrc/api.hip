@@ -114,6 +114,8 @@ struct koordhip_ctx {
   int32_t gather_world = 1;
   uint64_t *d_final = nullptr;   // [2][batch][k] (merged lists, multi-rank)
   int32_t *d_mod = nullptr;      // {count, nodes} M' between resolve launches, then PipeSync
+  kh::DevNodes *d_desc = nullptr;  // device copy of d (column pointers) for k_resolve
+  kh::DevNodes desc_host{};        // its host source (stable while the copy is in flight)
   const uint64_t *d_cur_lists = nullptr;  // this round's rank-local lists (local-group exchange)
   hipStream_t rstream = nullptr;  // resolve stream (the eval kernels use `stream`)
   hipEvent_t ev_res[kRing] = {}, ev_start = nullptr;
@@ -468,7 +470,7 @@ int koordhip_destroy(koordhip_ctx *c) {
   for (void *p : c->ckpt) (void)hipFree(p);
   for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
                   (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
-                  (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod})
+                  (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -869,6 +871,7 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipMalloc(&c->d_lists, 2 * lbytes));
     HIP_TRY(hipMalloc(&c->d_final, 2 * lbytes));
     HIP_TRY(hipMalloc(&c->d_mod, (1 + kMaxBatch) * sizeof(int32_t) + kh::kPipeSyncBytes));
+    HIP_TRY(hipMalloc(&c->d_desc, sizeof(kh::DevNodes)));
     HIP_TRY(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
     for (int i = 0; i < kRing; i++) HIP_TRY(hipEventCreateWithFlags(&c->ev_res[i], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
@@ -895,6 +898,8 @@ int place_staged_impl(koordhip_ctx *c) {
   int32_t *mbuf = c->d_mod;  // M' handed between resolve launches
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
   HIP_TRY(hipEventRecord(c->t0, c->stream));
+  c->desc_host = c->d;  // the resolve kernel reads the column pointers from this device copy
+  HIP_TRY(hipMemcpyAsync(c->d_desc, &c->desc_host, sizeof(kh::DevNodes), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemsetAsync(sync, 0, kh::kPipeSyncBytes, c->stream));
   HIP_TRY(hipEventRecord(c->ev_start, c->stream));
   HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_start, 0));
@@ -921,7 +926,7 @@ int place_staged_impl(koordhip_ctx *c) {
   uint64_t *lists0 = c->world > 1 ? c->d_final : c->d_lists;
   uint64_t *cpus = c->d_cpus;
   if (persistent && rounds > 0)
-    HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, sync,
+    HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
   for (int32_t r = 0; r < rounds; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
@@ -943,7 +948,7 @@ int place_staged_impl(koordhip_ctx *c) {
         HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
         HIP_TRY(hipStreamWaitEvent(rs, c->ev_res[r % kRing], 0));
       }
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, sync,
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, sync,
                                  mbuf, c->d_out, cpus, c->d_dbg, trace, rs));
     }
   }

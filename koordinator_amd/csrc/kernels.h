@@ -43,7 +43,7 @@ hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, h
 // k_wait_resolved (before k_scan) and k_signal_lists (after the lists).
 struct PipeSync;
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa);
-hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t total, int32_t P, int32_t k,
+hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
                           PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
                           int32_t trace, hipStream_t s);

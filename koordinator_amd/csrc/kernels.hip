@@ -838,7 +838,8 @@ __global__ void k_signal_lists(PipeSync *sy, int32_t rounds) {
 }
 
 template <bool NUMA>
-__global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
+__global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const DevNodes *__restrict__ dn, int32_t n_nodes,
+                                                                 const DevNumaClass *__restrict__ ncls, const DevPod *__restrict__ pods,
                                                                  int32_t total, int32_t P, int32_t k, int32_t kp,
                                                                  int32_t r_begin, int32_t r_end,
                                                                  int32_t *__restrict__ mbuf,
@@ -867,7 +868,15 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
   __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous round committed to
   __shared__ int32_t sh_mp, sh_stop, sh_nhit;
   const int t = threadIdx.x, lane = lane_id();
-  const int32_t words = (d.n + 31) >> 5;
+  const int32_t words = (n_nodes + 31) >> 5;
+  // The column pointers are read from a device-side copy of DevNodes at each
+  // (rare) row load/store instead of living in SGPRs for the whole kernel:
+  // ~40 pointers would otherwise spill through VGPR lanes in the hot loop.
+  auto nodes = [dn]() -> DevNodes {
+    const DevNodes *p = dn;
+    asm volatile("" : "+s"(p));
+    return *p;
+  };
   const bool two = k > 64;
   if (t == 0) {
     sh_mp = r_begin > 0 ? min(mbuf[0], (int32_t)RES_MAXP_ROUND) : 0;
@@ -879,11 +888,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
     const int32_t nd = mbuf[1 + t];
     pnode[t] = nd;
     NV v;
-    load_row(v, d, nd);
+    load_row(v, nodes(), nd);
     prow[t] = v;
     if constexpr (NUMA) {
       NumaRow rr;
-      load_numa_row(rr, d, nd);
+      load_numa_row(rr, nodes(), nd);
       pnr[t] = rr;
     }
   }
@@ -927,11 +936,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
       }
       if (nd >= 0) {
         NV v;
-        load_row(v, d, nd);
+        load_row(v, nodes(), nd);
         pre[t] = v;
         if constexpr (NUMA) {
           NumaRow rr;
-          load_numa_row(rr, d, nd);
+          load_numa_row(rr, nodes(), nd);
           prenr[t] = rr;
         }
       }
@@ -987,7 +996,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
           const DevPod pod = lpod[j];
           int32_t tot;
           if constexpr (NUMA) {
-            tot = eval_total_numa(pod, prow[sl], pnr[sl], d.nu.cls, c);
+            tot = eval_total_numa(pod, prow[sl], pnr[sl], ncls, c);
           } else {
             tot = eval_total(pod, prow[sl], c);
           }
@@ -1039,11 +1048,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
         const int32_t nd = want[t];
         if (nd >= 0 && nd != pre_node[t]) {
           NV v;
-          load_row(v, d, nd);
+          load_row(v, nodes(), nd);
           pre[t] = v;
           if constexpr (NUMA) {
             NumaRow rr;
-            load_numa_row(rr, d, nd);
+            load_numa_row(rr, nodes(), nd);
             prenr[t] = rr;
           }
           pre_node[t] = nd;
@@ -1114,8 +1123,8 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
             } else {
               n_miss++;
               if (lane == nm) {
-                load_row(stg, d, cn);
-                if constexpr (NUMA) load_numa_row(stgnr, d, cn);
+                load_row(stg, nodes(), cn);
+                if constexpr (NUMA) load_numa_row(stgnr, nodes(), cn);
               }
             }
           }
@@ -1128,7 +1137,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
           uint64_t key = 0;
           if (lane < nm) {
             if constexpr (NUMA) {
-              key = make_key(eval_total_numa(pod, my, mynr, d.nu.cls, c), my_node);
+              key = make_key(eval_total_numa(pod, my, mynr, ncls, c), my_node);
             } else {
               key = make_key(eval_total(pod, my, c), my_node);
             }
@@ -1144,7 +1153,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
             const bool in_m = (modmap[nd >> 5] >> (nd & 31)) & 1u;
             if (!in_m) {
               if constexpr (NUMA) {
-                key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], d.nu.cls, c), nd);
+                key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], ncls, c), nd);
               } else {
                 key = make_key(eval_total(pod, prow[lane], c), nd);
               }
@@ -1174,8 +1183,8 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
               my = stg;
               if constexpr (NUMA) mynr = stgnr;
             } else {
-              load_row(my, d, w);
-              if constexpr (NUMA) load_numa_row(mynr, d, w);
+              load_row(my, nodes(), w);
+              if constexpr (NUMA) load_numa_row(mynr, nodes(), w);
             }
           }
           bool ok = true;
@@ -1185,7 +1194,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
               // row, the chosen CPUs are broadcast to the wave
               uint64_t mc[NW] = {0, 0, 0, 0};
               int okl = 0;
-              if (lane == rw) okl = mynr.cls >= 0 && numa_allocate(d.nu.cls[mynr.cls], mynr, pod, mc);
+              if (lane == rw) okl = mynr.cls >= 0 && numa_allocate(ncls[mynr.cls], mynr, pod, mc);
               ok = __builtin_amdgcn_readlane(okl, rw) != 0;
 #pragma unroll
               for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], rw);
@@ -1217,8 +1226,8 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, DevNo
       }
       // ---- 4. write M back, hand it to the next round as M' (rows stay in LDS)
       if (lane < nm) {
-        store_row(my, d, my_node);
-        if constexpr (NUMA) store_numa_row(mynr, d, my_node);
+        store_row(my, nodes(), my_node);
+        if constexpr (NUMA) store_numa_row(mynr, nodes(), my_node);
         prow[lane] = my;
         if constexpr (NUMA) pnr[lane] = mynr;
         pnode[lane] = my_node;
@@ -1390,7 +1399,7 @@ int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool n
   return res_lds(n_pods_max, kp, n_nodes, numa).total;
 }
 
-hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t total, int32_t P, int32_t k,
+hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
                           PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
                           int32_t trace, hipStream_t s) {
@@ -1409,10 +1418,10 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevPod *pods
   }
   if (o.total > RES_LDS_MAX) return hipErrorInvalidValue;
   if (numa)
-    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(res_threads<true>()), o.total, s, c, d, pods, total, P, k, kp,
+    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(res_threads<true>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, k, kp,
                        r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace);
   else
-    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(res_threads<false>()), o.total, s, c, d, pods, total, P, k, kp,
+    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(res_threads<false>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, k, kp,
                        r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace);
   return hipGetLastError();
 }
