@@ -108,6 +108,10 @@ struct koordhip_ctx {
   kh::DevNumaClass *d_classes = nullptr;
   int32_t *d_rc = nullptr;     // k_commit status
   uint64_t *d_partial = nullptr;  // score matrix of k_scan (u16 [pods][stride])
+  uint64_t *d_selpart = nullptr;  // k_select_split slice lists ([pods][G][k])
+  uint32_t *d_selcnt = nullptr;   // k_select_split arrival counters (zero between launches)
+  int32_t sel_g = kh::kSelGMax;   // workgroups per pod of k_select_split (KOORDHIP_SEL_G)
+  bool sel_split = false;         // k_select_split (KOORDHIP_SELECT_SPLIT) instead of k_select + signal kernel
   size_t partial_cap = 0;
   uint64_t *d_lists = nullptr;   // [2][batch][k] (rank-local lists; double buffer: round parity)
   uint64_t *d_gather = nullptr;  // [world][batch][k]
@@ -250,7 +254,7 @@ int ensure(koordhip_ctx *c, void **p, size_t *cap, size_t bytes) {
 // Exact per-pod top-k over node range [lo, hi) of np pods: k_scan fills the
 // score matrix, k_select reduces each row (best first, 0-padded).
 int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
-               uint64_t *out, bool timed) {
+               uint64_t *out, bool timed, int32_t *done) {
   const int R = c->partial_r;
   const int64_t stride = ((int64_t)(hi - lo) + 63) & ~63ll;
   const int32_t nchunks = kh::scan_chunks(R, lo, hi);
@@ -278,7 +282,17 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
   if (e1) HIP_TRY(hipEventRecord(*e1, c->stream));
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
-  HIP_TRY(kh::launch_select(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, out, c->d_dbg, c->stream));
+  if (!c->sel_split) {
+    HIP_TRY(kh::launch_select(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, out, c->d_dbg, c->stream));
+    return 0;
+  }
+  if (!c->d_selcnt) {
+    HIP_TRY(hipMalloc(&c->d_selpart, kh::kSelPartKeys * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_selcnt, kh::kSelMaxPods * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(c->d_selcnt, 0, kh::kSelMaxPods * sizeof(uint32_t), c->stream));
+  }
+  HIP_TRY(kh::launch_select_split(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, c->sel_g, c->d_selpart,
+                                  c->d_selcnt, out, done, c->stream));
   return 0;
 }
 
@@ -431,7 +445,11 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     const int v = std::atoi(r);
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
   }
-  if (c->numa && c->partial_r > 4) c->partial_r = 4;  // the NUMA scan kernel is built for R <= 4
+  if (c->numa && c->partial_r > 4) c->partial_r = 4;
+  if (const char *g = std::getenv("KOORDHIP_SEL_G")) c->sel_g = std::max(1, std::min(kh::kSelGMax, std::atoi(g)));
+  // the split select shortens the evaluation stream but its workgroups contend
+  // with the resolve wave, which bounds the pipeline at the default round size
+  c->sel_split = std::getenv("KOORDHIP_SELECT_SPLIT") != nullptr;  // the NUMA scan kernel is built for R <= 4
   c->monotone = 1;  // Fit LeastAllocated + LoadAware least-used: a commit never raises a key
   {
     int64_t max_total = 0;  // every plugin score is in [0, 100]
@@ -470,7 +488,8 @@ int koordhip_destroy(koordhip_ctx *c) {
   for (void *p : c->ckpt) (void)hipFree(p);
   for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
                   (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
-                  (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc})
+                  (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc,
+                  (void *)c->d_selpart, (void *)c->d_selcnt})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -749,7 +768,7 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
       e = fail(KOORDHIP_EDEVICE, "eval_full launch");
       break;
     }
-    if (topk) e = topk_batch(c, dp, np, k, 0, n, dk, false);
+    if (topk) e = topk_batch(c, dp, np, k, 0, n, dk, false, nullptr);
     if (e) break;
     if (hipStreamSynchronize(c->stream) != hipSuccess) {
       e = fail(KOORDHIP_EDEVICE, "eval sync");
@@ -892,8 +911,8 @@ int place_staged_impl(koordhip_ctx *c) {
   c->last_launches = 0;
   c->last_evals = 0;
   if (std::getenv("KOORDHIP_STAMPS")) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 16 * sizeof(uint64_t)));
-    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(uint64_t), c->stream));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 32 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 32 * sizeof(uint64_t), c->stream));
   }
   int32_t *mbuf = c->d_mod;  // M' handed between resolve launches
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
@@ -935,14 +954,15 @@ int place_staged_impl(koordhip_ctx *c) {
     if (r >= 2 && !serial) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, c->stream));
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true)) return e;
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, nullptr)) return e;
       if (int e = exchange(c, lists, (size_t)P * K)) return e;
       HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits,
                                     c->d_final + (size_t)(r & 1) * list_buf, c->stream));
     } else {
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true)) return e;
+      // the split select's merging workgroups count the round's pods into sync->sel_round themselves
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, c->sel_split ? kh::pipe_list_counter(sync) : nullptr)) return e;
     }
-    HIP_TRY(kh::launch_signal_lists(sync, r + 1, c->stream));
+    if (c->world > 1 || !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, p0 + np, c->stream));
     if (!persistent) {
       if (!serial) {
         HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
@@ -959,7 +979,7 @@ int place_staged_impl(koordhip_ctx *c) {
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   c->pipe_check = true;
   if (c->d_dbg) {
-    uint64_t h[16];
+    uint64_t h[32];
     HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     std::fprintf(stderr,
@@ -972,6 +992,9 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[4],
                  (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7],
                  (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[15], (unsigned long long)h[14]);
+    std::fprintf(stderr, "[koordhip stamps] resolve loop cycles: candidate %llu  staging %llu  re-eval %llu  commit %llu\n",
+                 (unsigned long long)h[16], (unsigned long long)h[17], (unsigned long long)h[18],
+                 (unsigned long long)h[19]);
   }
   return 0;
 }

@@ -18,6 +18,8 @@
 //                     modified rows and written back at the end of the round.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "eval.hpp"
 #include "kernels.h"
 
@@ -454,8 +456,9 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
 constexpr int SEL_THREADS = 1024;
 constexpr int SEL_WAVES = SEL_THREADS / 64;
 
-// inclusive block prefix sum of one value per thread (SEL_THREADS threads)
-__device__ __forceinline__ int32_t sel_scan(int32_t v, int32_t *wsum, int32_t *total) {
+// inclusive block prefix sum of one value per thread (WAVES x 64 threads)
+template <int WAVES>
+__device__ __forceinline__ int32_t block_scan_incl(int32_t v, int32_t *wsum, int32_t *total) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
   int32_t x = v;
 #pragma unroll
@@ -467,7 +470,7 @@ __device__ __forceinline__ int32_t sel_scan(int32_t v, int32_t *wsum, int32_t *t
   __syncthreads();
   int32_t base = 0, tot = 0;
 #pragma unroll
-  for (int q = 0; q < SEL_WAVES; q++) {
+  for (int q = 0; q < WAVES; q++) {
     const int32_t s = wsum[q];
     base += q < w ? s : 0;
     tot += s;
@@ -475,6 +478,9 @@ __device__ __forceinline__ int32_t sel_scan(int32_t v, int32_t *wsum, int32_t *t
   __syncthreads();
   *total = tot;
   return base + x;
+}
+__device__ __forceinline__ int32_t sel_scan(int32_t v, int32_t *wsum, int32_t *total) {
+  return block_scan_incl<SEL_WAVES>(v, wsum, total);
 }
 
 // Row layout: tiles of SEL_THREADS x SEL_PER nodes; thread t owns the
@@ -492,10 +498,13 @@ __device__ __forceinline__ int32_t sel_node(int32_t tile, int t, int h) {
   return tile * SEL_TILE + t * SEL_PER + h;
 }
 
-__device__ __forceinline__ void sel_load(const uint16_t *row, int32_t m, int32_t tile, int t, uint4 *q) {
+// IT 16-B loads of one thread's contiguous run of 8 * IT row values from i0
+// (values past the row end read as 0 = infeasible)
+template <int IT>
+__device__ __forceinline__ void row_load(const uint16_t *row, int32_t m, int32_t i0, uint4 *q) {
 #pragma unroll
-  for (int j = 0; j < SEL_ITER; j++) {
-    const int32_t i = sel_node(tile, t, 8 * j);
+  for (int j = 0; j < IT; j++) {
+    const int32_t i = i0 + 8 * j;
     if (i + 8 <= m) {
       q[j] = *reinterpret_cast<const uint4 *>(row + i);
     } else {
@@ -509,12 +518,16 @@ __device__ __forceinline__ void sel_load(const uint16_t *row, int32_t m, int32_t
     }
   }
 }
+__device__ __forceinline__ void sel_load(const uint16_t *row, int32_t m, int32_t tile, int t, uint4 *q) {
+  row_load<SEL_ITER>(row, m, sel_node(tile, t, 0), q);
+}
 
-// bit h of the result: value h of q satisfies (v >= lo_incl) [ge] or (v == x) [eq] / (v > x) [gt]
+// bit h of the result: value h of q satisfies (v >= x) [ge] or (v == x) [eq]
+template <int IT = SEL_ITER>
 __device__ __forceinline__ uint64_t sel_mask_ge(const uint4 *q, uint32_t x) {
   uint64_t m = 0;
 #pragma unroll
-  for (int j = 0; j < SEL_ITER; j++) {
+  for (int j = 0; j < IT; j++) {
     const uint32_t w4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
 #pragma unroll
     for (int h = 0; h < 4; h++) {
@@ -524,10 +537,11 @@ __device__ __forceinline__ uint64_t sel_mask_ge(const uint4 *q, uint32_t x) {
   }
   return m;
 }
+template <int IT = SEL_ITER>
 __device__ __forceinline__ uint64_t sel_mask_eq(const uint4 *q, uint32_t x) {
   uint64_t m = 0;
 #pragma unroll
-  for (int j = 0; j < SEL_ITER; j++) {
+  for (int j = 0; j < IT; j++) {
     const uint32_t w4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
 #pragma unroll
     for (int h = 0; h < 4; h++) {
@@ -692,6 +706,252 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
 }
 
 // ---------------------------------------------------------------------------
+// k_select_split: the same exact top-k with G workgroups per pod.
+//
+// One workgroup per pod (k_select) keeps 32 of 256 CUs busy at the default
+// round size and its walk over a 100 KB row is latency-bound.  Here
+// workgroup (g, p) owns slice g of pod p's row (whole tiles of SPL_TILE
+// nodes, 16 per thread, two 16-B loads).  It derives the pod's lower bound L
+// from the chunk maxima exactly like k_select, then the exact top-k by key of
+// its slice restricted to scores >= L: every node of the pod's top-k scores
+// >= S* >= L and has fewer than k better keys in its own slice, so the union
+// of the slice lists holds the whole answer.  Each slice list is written
+// sorted (best first; equal scores are then contiguous and in node order).
+//
+// Hand-off (cdna_hip_programming.md Guideline 16, counter form): plain list
+// stores -> every wave's vmcnt(0) -> barrier -> lane 0 agent release + asm
+// vmcnt(0) -> agent fetch_add on the pod's arrival counter.  The workgroup
+// that draws G-1 resets the counter (zeroed once at allocation; the next
+// launch is ordered by the kernel boundary), takes an agent acquire and
+// merges: the k-th largest score S over the G lists (LDS histogram walk), the
+// keys above S (fewer than k) rank-sorted, then the ties at S list by list
+// (lists ascend in node range, a list's ties are contiguous and ascending).
+// With `done`, it then publishes the pod's final list the same way and adds
+// 1 to the pipeline's list counter -- what k_resolve waits on, so no signal
+// kernel runs between the evaluation and the resolve.
+
+constexpr int SPL_THREADS = 256;
+constexpr int SPL_WAVES = SPL_THREADS / 64;
+constexpr int SPL_ITER = 2;
+constexpr int SPL_PER = SPL_ITER * 8;
+constexpr int32_t SPL_TILE = SPL_THREADS * SPL_PER;
+constexpr int SPL_GMAX = 16;
+
+struct SplHdr {  // start of k_select_split's dynamic LDS (all of its LDS: the base stays 16-B aligned)
+  uint64_t lst[RES_MAXP];
+  int32_t wsum[SPL_WAVES];
+  int32_t thr, gt, cnt_gt, last, nties;
+  int32_t gtc[SPL_GMAX], tie[SPL_GMAX];
+};
+static_assert(SPL_GMAX == kSelGMax, "k_select_split group bound");
+constexpr int32_t SPL_HDR = (int32_t)((sizeof(SplHdr) + 15) & ~(size_t)15);
+
+__global__ __launch_bounds__(SPL_THREADS) void k_select_split(
+    const uint16_t *__restrict__ S, int64_t s_stride, int32_t lo, int32_t m, int32_t k, int32_t nbins,
+    const uint16_t *__restrict__ Mx, int32_t m_stride, int32_t nchunks, int32_t G, int32_t tiles_per,
+    uint64_t *__restrict__ part, uint32_t *__restrict__ cnt, uint64_t *__restrict__ out, int32_t *__restrict__ done) {
+  extern __shared__ __attribute__((aligned(16))) char spl_lds[];
+  SplHdr &h = *reinterpret_cast<SplHdr *>(spl_lds);
+  uint64_t *mk = reinterpret_cast<uint64_t *>(spl_lds + SPL_HDR);                    // merge: G x k keys
+  uint32_t *hist = reinterpret_cast<uint32_t *>(spl_lds + SPL_HDR + (size_t)G * k * 8);  // nbins score bins
+  uint32_t *mhist = hist + nbins;                                                      // packed chunk-max bins
+  const int t = threadIdx.x, lane = lane_id();
+  const int32_t g = blockIdx.x, p = blockIdx.y;
+  const uint16_t *row = S + (size_t)p * s_stride;
+  const int32_t ntiles = (m + SPL_TILE - 1) / SPL_TILE;
+  const int32_t tb = min(ntiles, g * tiles_per), te = min(ntiles, tb + tiles_per);
+  auto first = [&](int32_t tile) -> int32_t { return tile * SPL_TILE + t * SPL_PER; };
+  uint4 q[SPL_ITER];
+  if (tb < te) row_load<SPL_ITER>(row, m, first(tb), q);
+  const int32_t mwords = nchunks >= k ? (nbins + 1) >> 1 : 0;
+  for (int32_t j = t; j < nbins + mwords; j += SPL_THREADS) hist[j] = 0;
+  if (t == 0) h.cnt_gt = 0;
+  // ---- lower bound L: the k-th largest chunk maximum of the whole row
+  uint32_t L = 1;
+  if (mwords) {
+    const uint16_t *mrow = Mx + (size_t)p * m_stride;
+    __syncthreads();
+    for (int32_t j = t; j < nchunks; j += SPL_THREADS) {
+      const uint32_t v = mrow[j];
+      if (v) atomicAdd(&mhist[v >> 1], 1u << (16 * (v & 1)));  // counts <= nchunks < 2^16
+    }
+    __syncthreads();
+    if (t < 64) {
+      int32_t thr, gt;
+      sel_walk([&](int32_t v) { return (int32_t)((mhist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu); }, nbins, 1, k, thr,
+               gt);
+      if (lane == 0) h.thr = thr;
+    }
+    __syncthreads();
+    L = h.thr > 1 ? (uint32_t)h.thr : 1u;
+  }
+  __syncthreads();
+  // ---- pass 1: histogram of the slice's scores >= L
+  for (int32_t tile = tb; tile < te; tile++) {
+    if (tile > tb) row_load<SPL_ITER>(row, m, first(tile), q);
+    uint64_t hit = sel_mask_ge<SPL_ITER>(q, L);
+    while (hit) {
+      const int b = __builtin_ctzll(hit);
+      hit &= hit - 1;
+      atomicAdd(&hist[row[first(tile) + b]], 1u);
+    }
+  }
+  __syncthreads();
+  // ---- the slice's k-th largest value T (or L with all of its >= L values)
+  if (t < 64) {
+    int32_t thr, gt;
+    sel_walk([&](int32_t v) { return (int32_t)hist[v]; }, nbins, (int32_t)L, k, thr, gt);
+    if (thr == 0) {
+      thr = (int32_t)L;
+      gt = 0;
+      for (int32_t v = thr + 1 + lane; v < nbins; v += 64) gt += (int32_t)hist[v];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) gt += __shfl_xor(gt, off, 64);
+    }
+    if (lane == 0) {
+      h.thr = thr;
+      h.gt = gt;
+    }
+  }
+  __syncthreads();
+  const uint32_t thr = (uint32_t)h.thr;
+  const int32_t gt = h.gt, need = k - gt;
+  // ---- pass 2: values > T (fewer than k) and the lowest-index ties at T
+  int32_t ties = 0;
+  for (int32_t tile = tb; tile < te; tile++) {
+    if (te - tb > 1) row_load<SPL_ITER>(row, m, first(tile), q);
+    const uint64_t above = sel_mask_ge<SPL_ITER>(q, thr + 1);
+    uint64_t eq = sel_mask_eq<SPL_ITER>(q, thr);
+    for (uint64_t x = above; x;) {
+      const int b = __builtin_ctzll(x);
+      x &= x - 1;
+      const int32_t i = first(tile) + b;
+      h.lst[atomicAdd(&h.cnt_gt, 1)] = ((uint64_t)row[i] << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(lo + i));
+    }
+    const int32_t mine = __popcll(eq);
+    int32_t total;
+    int32_t pos = ties + block_scan_incl<SPL_WAVES>(mine, h.wsum, &total) - mine;
+    while (eq && pos < need) {  // ties in node order: thread-major, then b
+      const int b = __builtin_ctzll(eq);
+      eq &= eq - 1;
+      h.lst[gt + pos] = ((uint64_t)thr << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(lo + first(tile) + b));
+      pos++;
+    }
+    ties += total;
+    if (ties >= need && h.cnt_gt >= gt) break;  // uniform: read after the scan's barriers, before any later add
+    __syncthreads();
+  }
+  __syncthreads();
+  // ---- the slice list, best first: values > T rank-sorted, then the ties
+  const int32_t filled = gt + min(need, ties);
+  uint64_t *dst = part + ((size_t)p * G + g) * k;
+  for (int32_t j = t; j < k; j += SPL_THREADS) {
+    if (j < gt) {
+      const uint64_t x = h.lst[j];
+      int32_t rank = 0;
+      for (int32_t q2 = 0; q2 < gt; q2++) rank += h.lst[q2] > x;
+      dst[rank] = x;
+    } else {
+      dst[j] = j < filled ? h.lst[j] : 0ull;
+    }
+  }
+  // ---- publish; the pod's last workgroup merges
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&cnt[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t last = old + 1 == (uint32_t)G;
+    if (last) {
+      __hip_atomic_store(&cnt[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    h.last = last;
+  }
+  __syncthreads();
+  if (!h.last) return;  // block-uniform
+  const int32_t total = G * k;
+  const uint64_t *src = part + (size_t)p * G * k;
+  for (int32_t j = t; j < total; j += SPL_THREADS) mk[j] = src[j];
+  for (int32_t j = t; j < nbins; j += SPL_THREADS) hist[j] = 0;
+  if (t < SPL_GMAX) {
+    h.gtc[t] = 0;
+    h.tie[t] = 0;
+  }
+  if (t == 0) h.cnt_gt = 0;
+  __syncthreads();
+  for (int32_t j = t; j < total; j += SPL_THREADS) {
+    const uint64_t x = mk[j];
+    if (x) atomicAdd(&hist[key_sc(x)], 1u);
+  }
+  __syncthreads();
+  if (t < 64) {
+    int32_t sth, sgt;
+    sel_walk([&](int32_t v) { return (int32_t)hist[v]; }, nbins, 1, k, sth, sgt);
+    if (sth == 0) {  // fewer than k keys in all: every one of them
+      sth = 1;
+      sgt = 0;
+      for (int32_t v = 2 + lane; v < nbins; v += 64) sgt += (int32_t)hist[v];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) sgt += __shfl_xor(sgt, off, 64);
+    }
+    if (lane == 0) {
+      h.thr = sth;
+      h.gt = sgt;
+    }
+  }
+  __syncthreads();
+  const int32_t St = h.thr, mgt = h.gt, mneed = k - mgt;
+  for (int32_t j = t; j < total; j += SPL_THREADS) {
+    const uint64_t x = mk[j];
+    const int32_t sc = key_sc(x), s = j / k;
+    if (sc > St) {
+      h.lst[atomicAdd(&h.cnt_gt, 1)] = x;
+      atomicAdd(&h.gtc[s], 1);
+    } else if (sc == St) {
+      atomicAdd(&h.tie[s], 1);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {  // ties before each list (exclusive prefix over the G lists)
+    int32_t run = 0;
+    for (int32_t s = 0; s < G; s++) {
+      const int32_t c = h.tie[s];
+      h.tie[s] = run;
+      run += c;
+    }
+    h.nties = run;
+  }
+  __syncthreads();
+  uint64_t *o = out + (size_t)p * k;
+  for (int32_t j = t; j < mgt; j += SPL_THREADS) {
+    const uint64_t x = h.lst[j];
+    int32_t rank = 0;
+    for (int32_t q2 = 0; q2 < mgt; q2++) rank += h.lst[q2] > x;
+    o[rank] = x;
+  }
+  for (int32_t j = t; j < total; j += SPL_THREADS) {
+    const uint64_t x = mk[j];
+    if (key_sc(x) != St) continue;
+    const int32_t s = j / k;
+    const int32_t pos = mgt + h.tie[s] + (j - s * k - h.gtc[s]);
+    if (pos < k) o[pos] = x;
+  }
+  for (int32_t j = mgt + min(mneed, h.nties) + t; j < k; j += SPL_THREADS) o[j] = 0;
+  if (done) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_resolve: the sequential greedy over one round of n_pods <= 64 pods,
 // lag-1 pipelined with the evaluation of the next round.
 //
@@ -790,17 +1050,24 @@ __device__ __forceinline__ uint32_t res_hash(int32_t node) { return ((uint32_t)n
 
 // Device-side handshake between the evaluation stream and the persistent
 // resolve kernel (one per koordhip_place_staged call):
-//   sel_round  rounds whose lists are ready   (k_signal, after k_select / merge)
+//   sel_round  pods of the stream whose final lists are ready (k_select_split's
+//              merging workgroups add 1 each; k_signal_lists stores the count
+//              after a separate merge)
 //   res_round  rounds resolved + written back (k_resolve, release store)
 //   err        a side gave up waiting (watchdog): the call fails, nothing hangs
 struct PipeSync {
   int32_t sel_round, res_round, err, pad;
 };
 
+int32_t *pipe_list_counter(PipeSync *sync) { return &sync->sel_round; }
+
 constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up
 
 __device__ __forceinline__ int32_t load_acquire(const int32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t load_relaxed(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Publish a flag after this wave's global stores (MI355X_MICROARCH.md
 // cross-XCD hand-off: wait for the stores, write the XCD L2 back, wait for
@@ -814,17 +1081,20 @@ __device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
 }
 
 // Spin (one thread) until *p >= v; false when the watchdog fires or the other
-// side reported an error.
+// side reported an error.  Relaxed polls, ONE agent acquire after the match
+// (an acquire per poll costs 2-3x per hop, Guideline 16 Pitfall 5).
 __device__ bool wait_at_least(const int32_t *p, int32_t v, PipeSync *sy) {
   const uint64_t t0 = stamp();
-  while (load_acquire(p) < v) {
-    if (load_acquire(&sy->err)) return false;
+  while (load_relaxed(p) < v) {
+    if (load_relaxed(&sy->err)) return false;
     if (stamp() - t0 > PIPE_WATCHDOG) {
       store_release(&sy->err, 1);
       return false;
     }
     __builtin_amdgcn_s_sleep(4);
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   return true;
 }
 
@@ -902,14 +1172,16 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   NumaRow mynr{}, stgnr{};
   int32_t my_node = -1;
   uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0, c_ph_a = 0, c_ph_b = 0, c_ph_r = 0, c_rel = 0;
+  uint64_t c_l[4] = {0, 0, 0, 0};  // loop phases: candidate, staging, re-evaluation, commit
   for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
     const int32_t n_pods = min(P, total - p0);
     const DevPod *rp = pods + p0;
     const uint64_t *lists = lists0 + (size_t)(r & 1) * list_buf;
     const int32_t trace_j = (trace >= p0 && trace < p0 + n_pods) ? trace - p0 : -1;
+    (void)trace_j;
     // ---- 0. wait for this round's lists (thread 0), then every wave reads them
     const uint64_t t_w0 = (dbg && t == 0) ? stamp() : 0;
-    if (t == 0 && !wait_at_least(&sy->sel_round, r + 1, sy)) sh_stop = 1;
+    if (t == 0 && !wait_at_least(&sy->sel_round, p0 + n_pods, sy)) sh_stop = 1;
     __syncthreads();
     if (sh_stop) return;  // the evaluation side failed: give up, the host reports it
     const uint64_t t_entry = (dbg && t == 0) ? stamp() : 0;
@@ -1065,11 +1337,24 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       const uint64_t t_pro = dbg ? stamp() : 0;
       int32_t nm = 0;  // |M| (wave-uniform)
       my_node = -1;
+      // loop-invariant LDS words in registers: the prefetched rows' nodes, and
+      // the next pod's best keys are read one pod ahead (off the dependent chain)
+      const int32_t pn0 = pre_node[lane], pn1 = pre_node[lane + 64];
+      uint64_t tv_next = lane < RES_TOP ? top[lane] : 0ull;
       for (int32_t j = 0; j < n_pods; j++) {
+        uint64_t ts = dbg ? stamp() : 0;
+        auto lap = [&](int ph) {
+          if (dbg) {
+            const uint64_t x = stamp();
+            c_l[ph] += x - ts;
+            ts = x;
+          }
+        };
         const DevPod pod = lpod[j];  // VGPR copy: SGPRs are the scarce register file here
         // candidate: the best entry outside M (every list key is exact); first
         // among the pod's RES_TOP best, else from the whole list
-        const uint64_t tv = lane < RES_TOP ? top[j * RES_TOP + lane] : 0ull;
+        const uint64_t tv = tv_next;
+        if (j + 1 < n_pods) tv_next = lane < RES_TOP ? top[(j + 1) * RES_TOP + lane] : 0ull;
         bool tmod = false;
         if (tv) {
           const int32_t nd = key_node(tv);
@@ -1100,13 +1385,14 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           cand = wave_max_u64_dpp(f0 > f1 ? f0 : f1);
           prefix_modified = (__ballot(mod0 && e0 > cand) | __ballot(mod1 && e1 > cand)) != 0;
         }
+        lap(0);
         // stage the candidate's row into lane nm's staging registers (separate
         // from the M rows, so the re-evaluation below does not wait for it)
         int32_t staged = -1;
         if (cand != 0) {
           const int32_t cn = key_node(cand);
-          const uint64_t pm0 = __ballot(pre_node[lane] == cn);
-          const uint64_t pm1 = __ballot(pre_node[lane + 64] == cn);
+          const uint64_t pm0 = __ballot(pn0 == cn);
+          const uint64_t pm1 = __ballot(pn1 == cn);
           const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
           if (src >= 0) {
             if (lane == nm) {
@@ -1130,6 +1416,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           }
           staged = cn;
         }
+        lap(1);
         const bool nonmono = !monotone || (NUMA && is_cpuset(pod) &&
                                            KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
         uint64_t best = cand;
@@ -1162,7 +1449,9 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           key = wave_max_u64_dpp(key);
           best = key > best ? key : best;
         }
-        if (j == trace_j) {  // diagnostics (KOORDHIP_TRACE_POD)
+        lap(2);
+#ifdef KOORDHIP_TRACE_BUILD
+        if (j == trace_j) {  // diagnostics (KOORDHIP_TRACE_POD, trace builds only: printf bloats the loop)
           if (lane == 0)
             printf("[trace] j=%d cand=%d/%d best=%d/%d nm=%d mp=%d nonmono=%d prefix=%d\n", j,
                    cand ? key_node(cand) : -1, cand ? key_score(cand) : -1, best ? key_node(best) : -1,
@@ -1170,6 +1459,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           if (lane < nm) printf("[trace] M lane %d node %d\n", lane, my_node);
           if (lane < mp) printf("[trace] M' lane %d node %d\n", lane, pnode[lane]);
         }
+#endif
         uint64_t cpus[NW] = {0, 0, 0, 0};
         int32_t result = KOORDHIP_UNSCHEDULABLE;
         if (best != 0) {
@@ -1208,7 +1498,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
               nm++;
               if (lane == rw) {
                 my_node = w;
-                modmap[w >> 5] |= 1u << (w & 31);
+                atomicOr(&modmap[w >> 5], 1u << (w & 31));
               }
             }
             if (lane == rw) {
@@ -1220,6 +1510,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           }
         }
         if (lane == 0) out_node[p0 + j] = result;
+        lap(3);
         if (out_cpus && lane < NW)
           out_cpus[(size_t)(p0 + j) * NW + lane] =
               lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
@@ -1260,6 +1551,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     atomicAdd((unsigned long long *)&dbg[3], (unsigned long long)c_ph_b);
     atomicAdd((unsigned long long *)&dbg[14], (unsigned long long)c_rel);
     atomicAdd((unsigned long long *)&dbg[15], (unsigned long long)c_ph_r);
+    for (int q = 0; q < 4; q++) atomicAdd((unsigned long long *)&dbg[16 + q], (unsigned long long)c_l[q]);
   }
 }
 
@@ -1382,6 +1674,38 @@ hipError_t launch_select(const uint16_t *S, int64_t s_stride, int32_t lo, int32_
   }
   hipLaunchKernelGGL(k_select, dim3(n_pods), dim3(SEL_THREADS), lds, s, S, s_stride, lo, m, k, nbins, Mx, m_stride,
                      nchunks, out, dbg);
+  return hipGetLastError();
+}
+
+int32_t select_split_groups(int32_t m, int32_t G) {
+  const int32_t ntiles = std::max<int32_t>(1, (m + SPL_TILE - 1) / SPL_TILE);
+  G = std::max<int32_t>(1, std::min<int32_t>(std::min<int32_t>(G, SPL_GMAX), ntiles));
+  const int32_t per = (ntiles + G - 1) / G;
+  return (ntiles + per - 1) / per;  // no workgroup without a tile
+}
+
+hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,
+                               int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, int32_t G,
+                               uint64_t *part, uint32_t *cnt, uint64_t *out, int32_t *done, hipStream_t s) {
+  if (n_pods <= 0) return hipSuccess;
+  if (k < 1 || k > RES_MAXP || nbins < 2 || nbins > 32768 || n_pods > kSelMaxPods) return hipErrorInvalidValue;
+  const int32_t ntiles = std::max<int32_t>(1, (m + SPL_TILE - 1) / SPL_TILE);
+  G = select_split_groups(m, G);
+  const int32_t per = (ntiles + G - 1) / G;
+  if (nchunks > 65535) nchunks = 0;  // no lower bound: histogram the slices whole
+  size_t hb = (size_t)nbins * sizeof(uint32_t);
+  if (hb + (size_t)((nbins + 1) / 2) * sizeof(uint32_t) > 112 * 1024) nchunks = 0;
+  if (nchunks >= k) hb += (size_t)((nbins + 1) / 2) * sizeof(uint32_t);
+  const size_t lds = (size_t)SPL_HDR + (size_t)G * k * sizeof(uint64_t) + hb;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e =
+        hipFuncSetAttribute((const void *)k_select_split, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_select_split, dim3(G, n_pods), dim3(SPL_THREADS), lds, s, S, s_stride, lo, m, k, nbins, Mx,
+                     m_stride, nchunks, G, per, part, cnt, out, done);
   return hipGetLastError();
 }
 
