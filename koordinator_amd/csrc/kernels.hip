@@ -987,6 +987,16 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
 template <bool NUMA>
 constexpr int res_threads() { return NUMA ? 256 : 512; }
 
+// An NV row as 8-byte words (the lane-parallel Reserve in k_resolve): words
+// 0-4 a[], 5-9 r[], 10-11 nz, 12-13 la_a, 14-15 la_u, 16-17 la_up (f64),
+// 18 = a_pods | npods << 32, 19 = flags.
+constexpr int RES_WORDS = 20;
+static_assert(sizeof(NV) == RES_WORDS * 8, "NV row = 20 words");
+static_assert(offsetof(NV, r) == 40 && offsetof(NV, nz_cpu) == 80 && offsetof(NV, la_u_cpu) == 112 &&
+                  offsetof(NV, la_up_cpu) == 128 && offsetof(NV, a_pods) == 144 && offsetof(NV, npods) == 148 &&
+                  offsetof(NV, flags) == 152,
+              "NV word layout");
+
 // A pod record read from LDS made wave-uniform (SGPRs): every lane read the
 // same record, readfirstlane tells the compiler so.
 __device__ __forceinline__ DevPod uniform_pod(const DevPod &src) {
@@ -1003,8 +1013,8 @@ constexpr int RES_HASH = 256;  // node -> M' slot (open addressing)
 constexpr int RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (static LDS: a few flags)
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
-  int32_t lists, pods, prev_rows, prev_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node, want, top, lcnt, hits,
-      hmask, modmap, total;
+  int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
+      want, top, lcnt, hits, hmask, modmap, total;
 };
 
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
@@ -1016,10 +1026,20 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += res_align(n_pods_max * kp * 8);
   o.pods = at;
   at += res_align(n_pods_max * (int32_t)sizeof(DevPod));
+  // two row regions, M' (prev) and M (cur), swapped at the end of every
+  // round: NV rows, then NumaRow rows; the cur region doubles as the
+  // prologue's refresh list (`hits`, (pod, list position, M' slot) of the
+  // entries on M' nodes: <= P x |M'|), which is dead before the loop writes M
+  const int32_t rows_b = res_align(RES_MAXP_ROUND * (int32_t)sizeof(NV));
+  const int32_t numa_b = numa ? res_align(RES_MAXP_ROUND * (int32_t)sizeof(NumaRow)) : 0;
+  const int32_t region = res_align(max(rows_b + numa_b, n_pods_max * n_pods_max * 4));
   o.prev_rows = at;
-  at += res_align(RES_MAXP_ROUND * (int32_t)sizeof(NV));
-  o.prev_numa = at;
-  at += numa ? res_align(RES_MAXP_ROUND * (int32_t)sizeof(NumaRow)) : 0;
+  o.prev_numa = at + rows_b;
+  at += region;
+  o.cur_rows = at;
+  o.cur_numa = at + rows_b;
+  o.hits = at;
+  at += region;
   o.hash_node = at;
   at += RES_HASH * 4;
   o.hash_slot = at;
@@ -1036,8 +1056,6 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * RES_TOP * 8;
   o.lcnt = at;
   at += RES_MAXP_ROUND * 4;
-  o.hits = at;  // (pod, list position, M' slot) of the entries to refresh: <= P x |M'|
-  at += res_align(n_pods_max * n_pods_max * 4);
   o.hmask = at;  // per pod: which list positions were refreshed (2 x 64 bits)
   at += RES_MAXP_ROUND * 2 * 8;
   o.modmap = at;
@@ -1123,6 +1141,8 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   uint64_t *lk = reinterpret_cast<uint64_t *>(lds + ofs.lists);
   NV *prow = reinterpret_cast<NV *>(lds + ofs.prev_rows);
   NumaRow *pnr = reinterpret_cast<NumaRow *>(lds + ofs.prev_numa);
+  NV *mrow = reinterpret_cast<NV *>(lds + ofs.cur_rows);          // M rows, slot = M index
+  NumaRow *mnr = reinterpret_cast<NumaRow *>(lds + ofs.cur_numa);
   int32_t *hnode = reinterpret_cast<int32_t *>(lds + ofs.hash_node);
   int32_t *hslot = reinterpret_cast<int32_t *>(lds + ofs.hash_slot);
   NV *pre = reinterpret_cast<NV *>(lds + ofs.pre_rows);
@@ -1132,7 +1152,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   uint64_t *top = reinterpret_cast<uint64_t *>(lds + ofs.top);
   int32_t *lcnt = reinterpret_cast<int32_t *>(lds + ofs.lcnt);
   uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
-  int32_t *hits = reinterpret_cast<int32_t *>(lds + ofs.hits);
+  int32_t *hits = reinterpret_cast<int32_t *>(mrow);  // aliases the M region (prologue only)
   uint64_t *hmask = reinterpret_cast<uint64_t *>(lds + ofs.hmask);
   DevPod *lpod = reinterpret_cast<DevPod *>(lds + ofs.pods);
   __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous round committed to
@@ -1167,10 +1187,14 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     }
   }
   __syncthreads();
-  // wave 0's lane-owned rows (M of the current round) and staging registers
-  NV my{}, stg{};
-  NumaRow mynr{}, stgnr{};
+  // wave 0: lane s < |M| holds the node of M slot s (its row is mrow[s] in LDS);
+  // lane q < RES_WORDS owns word q of a row in the lane-parallel Reserve
   int32_t my_node = -1;
+  int32_t doff = -1;  // byte offset in DevPod of word q's Reserve delta (apply_delta)
+  if (lane >= 5 && lane < 10) doff = (lane - 5) * 8;                     // r[] += req[]
+  if (lane == 10 || lane == 11) doff = (int32_t)offsetof(DevPod, nz_cpu_m) + (lane - 10) * 8;
+  if (lane == 14 || lane == 16) doff = (int32_t)offsetof(DevPod, est_cpu);  // la_u / la_up (prod)
+  if (lane == 15 || lane == 17) doff = (int32_t)offsetof(DevPod, est_mem);
   uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0, c_ph_a = 0, c_ph_b = 0, c_ph_r = 0, c_rel = 0;
   uint64_t c_l[4] = {0, 0, 0, 0};  // loop phases: candidate, staging, re-evaluation, commit
   for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
@@ -1341,6 +1365,31 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       // the next pod's best keys are read one pod ahead (off the dependent chain)
       const int32_t pn0 = pre_node[lane], pn1 = pre_node[lane + 64];
       uint64_t tv_next = lane < RES_TOP ? top[lane] : 0ull;
+      // The Reserve delta of a pod is applied lane-parallel (lane q on row word
+      // q) and deferred: its row words are read at the pod's decision and the
+      // update is finished after the next pod's candidate reads are issued, so
+      // the LDS round trip overlaps the next decision instead of stalling it.
+      bool pend = false;  // wave-uniform
+      int32_t pend_rw = 0;
+      uint64_t pend_x = 0;
+      double pend_dq = 0.0;
+      auto finish = [&]() {
+        if (!pend) return;
+        uint64_t x = pend_x;
+        if (lane < 18) x = (uint64_t)__double_as_longlong(__longlong_as_double((long long)x) + pend_dq);
+        if (lane == 18) x += 1ull << 32;  // npods + 1 (high half; a_pods below)
+        // over-commit bits from the new Requested vs Allocatable (cpu, mem, eph)
+        uint32_t over = 0;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          const double a = __longlong_as_double((long long)readlane_u64(x, q));
+          const double rq = __longlong_as_double((long long)readlane_u64(x, 5 + q));
+          over |= rq > a ? (uint32_t)NF_OVER_CPU << q : 0u;
+        }
+        if (lane == 19) x = (x & ~(uint64_t)(NF_OVER_CPU | NF_OVER_MEM | NF_OVER_EPH)) | over;
+        if (lane < RES_WORDS) reinterpret_cast<uint64_t *>(&mrow[pend_rw])[lane] = x;
+        pend = false;
+      };
       for (int32_t j = 0; j < n_pods; j++) {
         uint64_t ts = dbg ? stamp() : 0;
         auto lap = [&](int ph) {
@@ -1360,6 +1409,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           const int32_t nd = key_node(tv);
           tmod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
         }
+        finish();  // the previous pod's row update (reads issued at its decision)
         const uint64_t tfree = __ballot(tv != 0 && !tmod);
         uint64_t cand = 0;
         bool prefix_modified;
@@ -1386,36 +1436,6 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           prefix_modified = (__ballot(mod0 && e0 > cand) | __ballot(mod1 && e1 > cand)) != 0;
         }
         lap(0);
-        // stage the candidate's row into lane nm's staging registers (separate
-        // from the M rows, so the re-evaluation below does not wait for it)
-        int32_t staged = -1;
-        if (cand != 0) {
-          const int32_t cn = key_node(cand);
-          const uint64_t pm0 = __ballot(pn0 == cn);
-          const uint64_t pm1 = __ballot(pn1 == cn);
-          const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
-          if (src >= 0) {
-            if (lane == nm) {
-              stg = pre[src];
-              if constexpr (NUMA) stgnr = prenr[src];
-            }
-          } else {
-            const int32_t sl = mp > 0 ? prev_slot(cn) : -1;  // an M' node: its row is in LDS
-            if (sl >= 0) {
-              if (lane == nm) {
-                stg = prow[sl];
-                if constexpr (NUMA) stgnr = pnr[sl];
-              }
-            } else {
-              n_miss++;
-              if (lane == nm) {
-                load_row(stg, nodes(), cn);
-                if constexpr (NUMA) load_numa_row(stgnr, nodes(), cn);
-              }
-            }
-          }
-          staged = cn;
-        }
         lap(1);
         const bool nonmono = !monotone || (NUMA && is_cpuset(pod) &&
                                            KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
@@ -1423,10 +1443,12 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         if (nm > 0 && (prefix_modified || nonmono)) {
           uint64_t key = 0;
           if (lane < nm) {
+            const NV v = mrow[lane];
             if constexpr (NUMA) {
-              key = make_key(eval_total_numa(pod, my, mynr, ncls, c), my_node);
+              const NumaRow nr = mnr[lane];
+              key = make_key(eval_total_numa(pod, v, nr, ncls, c), my_node);
             } else {
-              key = make_key(eval_total(pod, my, c), my_node);
+              key = make_key(eval_total(pod, v, c), my_node);
             }
           }
           key = wave_max_u64_dpp(key);
@@ -1465,47 +1487,73 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         if (best != 0) {
           const int32_t w = key_node(best);
           const uint64_t hit = __ballot(lane < nm && my_node == w);
-          // w is a row of M (lane `hit`) or new this round: then it is the staged
-          // candidate, or (non-monotone pods only) an M' node
+          // w's M slot; its current row: the slot itself, else (new this round)
+          // a prefetched list-head row, an M' row, or HBM (rare)
           const int32_t rw = hit ? __builtin_ctzll(hit) : nm;
-          if (!hit && lane == rw) {
-            if (staged == w) {
-              my = stg;
-              if constexpr (NUMA) mynr = stgnr;
+          const NV *srow = &mrow[rw];
+          const NumaRow *snr = &mnr[rw];
+          if (!hit) {
+            const uint64_t pm0 = __ballot(pn0 == w), pm1 = __ballot(pn1 == w);
+            const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
+            const int32_t sl = (src < 0 && mp > 0) ? prev_slot(w) : -1;
+            if (src >= 0) {
+              srow = &pre[src];
+              snr = &prenr[src];
+            } else if (sl >= 0) {
+              srow = &prow[sl];
+              snr = &pnr[sl];
             } else {
-              load_row(my, nodes(), w);
-              if constexpr (NUMA) load_numa_row(mynr, nodes(), w);
+              n_miss++;
+              if (lane == 0) {
+                NV v;
+                load_row(v, nodes(), w);
+                mrow[rw] = v;
+                if constexpr (NUMA) {
+                  NumaRow nr;
+                  load_numa_row(nr, nodes(), w);
+                  mnr[rw] = nr;
+                }
+              }
             }
           }
           bool ok = true;
           if constexpr (NUMA) {
             if (numa_on(c) && is_cpuset(pod)) {
-              // NodeNUMAResource Reserve: lane rw replays the accumulator on its
+              // NodeNUMAResource Reserve: lane 0 replays the accumulator on the
               // row, the chosen CPUs are broadcast to the wave
               uint64_t mc[NW] = {0, 0, 0, 0};
               int okl = 0;
-              if (lane == rw) okl = mynr.cls >= 0 && numa_allocate(ncls[mynr.cls], mynr, pod, mc);
-              ok = __builtin_amdgcn_readlane(okl, rw) != 0;
+              if (lane == 0) {
+                NumaRow nr = *snr;
+                okl = nr.cls >= 0 && numa_allocate(ncls[nr.cls], nr, pod, mc);
+                if (okl) {
+                  numa_apply(nr, pod, mc, +1);
+                  mnr[rw] = nr;
+                }
+              }
+              ok = __builtin_amdgcn_readfirstlane(okl) != 0;
 #pragma unroll
-              for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], rw);
+              for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], 0);
+            } else if (!hit && lane < (int)(sizeof(NumaRow) / 8)) {
+              reinterpret_cast<uint64_t *>(&mnr[rw])[lane] = reinterpret_cast<const uint64_t *>(snr)[lane];
             }
           }
           if (!ok) {
             result = KOORDHIP_RESERVE_FAILED;  // every Reserve is rolled back
           } else {
             result = w;
+            // Reserve delta (apply_delta): issue the reads, finish() applies it
+            pend_x = lane < RES_WORDS ? reinterpret_cast<const uint64_t *>(srow)[lane] : 0ull;
+            const bool prod = (pod.flags & KOORDHIP_POD_PROD) != 0;
+            pend_dq = (doff >= 0 && (lane < 16 || prod))
+                          ? *reinterpret_cast<const double *>(reinterpret_cast<const char *>(&lpod[j]) + doff)
+                          : 0.0;
+            pend_rw = rw;
+            pend = true;
             if (!hit) {
               nm++;
-              if (lane == rw) {
-                my_node = w;
-                atomicOr(&modmap[w >> 5], 1u << (w & 31));
-              }
-            }
-            if (lane == rw) {
-              apply_delta(my, pod, +1);
-              if constexpr (NUMA) {
-                if (numa_on(c) && is_cpuset(pod)) numa_apply(mynr, pod, cpus, +1);
-              }
+              if (lane == rw) my_node = w;
+              if (lane == 0) atomicOr(&modmap[w >> 5], 1u << (w & 31));
             }
           }
         }
@@ -1515,12 +1563,15 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           out_cpus[(size_t)(p0 + j) * NW + lane] =
               lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
       }
+      finish();
       // ---- 4. write M back, hand it to the next round as M' (rows stay in LDS)
       if (lane < nm) {
-        store_row(my, nodes(), my_node);
-        if constexpr (NUMA) store_numa_row(mynr, nodes(), my_node);
-        prow[lane] = my;
-        if constexpr (NUMA) pnr[lane] = mynr;
+        const NV v = mrow[lane];
+        store_row(v, nodes(), my_node);
+        if constexpr (NUMA) {
+          const NumaRow nr = mnr[lane];
+          store_numa_row(nr, nodes(), my_node);
+        }
         pnode[lane] = my_node;
         modmap[my_node >> 5] = 0;  // clear the round's bits (whole words: every bit set is M's)
       }
@@ -1538,6 +1589,15 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       }
     }
     __syncthreads();
+    {  // M's rows become the next round's M' rows
+      NV *x = prow;
+      prow = mrow;
+      mrow = x;
+      NumaRow *y = pnr;
+      pnr = mnr;
+      mnr = y;
+      hits = reinterpret_cast<int32_t *>(mrow);
+    }
   }
   if (t <= RES_MAXP_ROUND && t <= sh_mp) mbuf[t] = t == 0 ? sh_mp : pnode[t - 1];  // hand M' on
   if (dbg && t == 0) {
