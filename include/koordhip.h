@@ -145,7 +145,9 @@ typedef struct koordhip_config {
   int32_t numa_weight_cpu;  /* NodeNUMAResourceArgs.ScoringStrategy LeastAllocated weights */
   int32_t numa_weight_mem;
   int32_t profile_kernels;  /* 1 = time every stream eval launch with HIP events (koordhip_last_stats) */
-  int32_t reserved[7];
+  int32_t numa_most_allocated; /* NodeNUMAResourceArgs.ScoringStrategy.Type == MostAllocated
+                                  (nodenumaresource/most_allocated.go:30-62); 0 = LeastAllocated */
+  int32_t reserved[6];
 } koordhip_config;
 
 /* Columnar node snapshot, all arrays of length n, little-endian, caller-owned

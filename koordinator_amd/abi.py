@@ -62,7 +62,8 @@ class KoordhipConfig(C.Structure):
         ("numa_weight_cpu", C.c_int32),
         ("numa_weight_mem", C.c_int32),
         ("profile_kernels", C.c_int32),
-        ("reserved", C.c_int32 * 7),
+        ("numa_most_allocated", C.c_int32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 

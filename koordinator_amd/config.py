@@ -122,11 +122,12 @@ class NodeNUMAResourceArgs:
         return self.scoring_type != "LeastAllocated"
 
     def validate(self):
-        """ValidateNodeNUMAResourceArgs + the engine's scope (LeastAllocated over cpu/memory)."""
+        """ValidateNodeNUMAResourceArgs + the engine's scope (Least/MostAllocated over cpu/memory)."""
         if self.default_cpu_bind_policy not in ("", "Default", "FullPCPUs", "SpreadByPCPUs", "ConstrainedBurst"):
             raise ArgsError(f"defaultCPUBindPolicy: unsupported value {self.default_cpu_bind_policy!r}")
-        if self.scoring_type != "LeastAllocated":
-            raise ArgsError("NodeNUMAResource scoringStrategy: only LeastAllocated is built into this engine")
+        if self.scoring_type not in ("LeastAllocated", "MostAllocated"):
+            raise ArgsError(f"NodeNUMAResource scoringStrategy.type {self.scoring_type!r}: LeastAllocated or "
+                            "MostAllocated (scoring.go:35-53)")
         for r, w in self.resources.items():
             if r not in (k8s.CPU, k8s.MEMORY):
                 raise ArgsError(f"NodeNUMAResource scoringStrategy.resources: {r} is not supported by this engine")
@@ -195,4 +196,5 @@ def to_c_config(profile: Profile, device: int = -1):
     cfg.batch_pods = p.batch_pods
     cfg.numa_weight_cpu = p.numa.resources.get(k8s.CPU, 0)
     cfg.numa_weight_mem = p.numa.resources.get(k8s.MEMORY, 0)
+    cfg.numa_most_allocated = 1 if p.numa.scoring_type == "MostAllocated" else 0
     return cfg

@@ -440,6 +440,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.according = cfg->la_score_according_prod_usage ? 1 : 0;
   c->dc.numa_w_cpu = cfg->numa_weight_cpu;
   c->dc.numa_w_mem = cfg->numa_weight_mem;
+  c->dc.numa_most = cfg->numa_most_allocated ? 1 : 0;
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   if (const char *r = std::getenv("KOORDHIP_TOPK_R")) {
     const int v = std::atoi(r);
@@ -450,7 +451,10 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   // the split select shortens the evaluation stream but its workgroups contend
   // with the resolve wave, which bounds the pipeline at the default round size
   c->sel_split = std::getenv("KOORDHIP_SELECT_SPLIT") != nullptr;  // the NUMA scan kernel is built for R <= 4
-  c->monotone = 1;  // Fit LeastAllocated + LoadAware least-used: a commit never raises a key
+  // Fit LeastAllocated + LoadAware least-used (+ NodeNUMAResource LeastAllocated):
+  // a commit never raises a key.  A MostAllocated NUMA score rises with every
+  // commit, so the resolve re-evaluates its modified nodes for every pod.
+  c->monotone = ((cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) && cfg->numa_most_allocated) ? 0 : 1;
   {
     int64_t max_total = 0;  // every plugin score is in [0, 100]
     for (int p = 0; p < KOORDHIP_NPLUGINS; p++)

@@ -39,7 +39,8 @@ struct DevCfg {
   int32_t la_w_cpu, la_w_mem;
   int32_t according;  // ScoreAccordingProdUsage
   int32_t la_alias;   // la_alloc columns equal alloc cpu/mem columns (loaded once)
-  int32_t numa_w_cpu, numa_w_mem;  // NodeNUMAResourceArgs LeastAllocated weights
+  int32_t numa_w_cpu, numa_w_mem;  // NodeNUMAResourceArgs scoring weights
+  int32_t numa_most;               // NodeNUMAResource MostAllocated scoring strategy
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -231,6 +232,17 @@ __device__ __forceinline__ int32_t lrs(double req, double cap) {
   return zero ? 0 : q;
 }
 
+// mostRequestedScore, nodenumaresource/most_allocated.go:51-62: min(req, cap)
+// * 100 / cap in int64 (cap == 0 -> 0), with the same exact quotient fix-up.
+__device__ __forceinline__ int32_t mrs(double req, double cap) {
+  const double f = (req > cap ? cap : req) * 100.0;
+  int32_t q = (int32_t)(f * __builtin_amdgcn_rcp(cap));
+  const double r = __builtin_fma(-(double)q, cap, f);
+  q -= (r < 0.0);
+  q += (r >= cap);
+  return cap == 0.0 ? 0 : q;
+}
+
 // Fit LeastAllocated score (upstream resource_allocation.go + least_allocated.go;
 // koord copy nodenumaresource/scoring.go:191-246): resources with Allocatable 0
 // are left out of both sums; scalar resources only when the pod requests them.
@@ -298,7 +310,8 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
                                               const DevNumaClass *classes, const DevCfg &c) {
   if (p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0;
   if (r.cls < 0) return 0;  // no CPU topology: getResourceOptions / Allocate error -> 0
-  auto lr = [](double a, double b) { return lrs(a, b); };
+  const bool most = c.numa_most != 0;  // leastResourceScorer / mostResourceScorer (scoring.go:35-53)
+  auto lr = [most](double a, double b) { return most ? mrs(a, b) : lrs(a, b); };
   auto dw = [](int32_t a, int32_t b) { return div_weights(a, b); };
   if (!(p.flags & KOORDHIP_POD_CPUSET))
     return numa_la(v.r[KOORDHIP_RES_CPU] + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],

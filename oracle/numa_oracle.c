@@ -558,17 +558,26 @@ int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koord
   return 1;
 }
 
-/* leastResourceScorer over {cpu, memory} (nodenumaresource/scoring.go:191-230,
- * least_allocated.go:30-58): resources with allocatable 0 are left out. */
+/* mostRequestedScore, nodenumaresource/most_allocated.go:51-62. */
+static int64_t most_requested(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) requested = capacity;
+  return (requested * 100) / capacity;
+}
+
+/* leastResourceScorer / mostResourceScorer over {cpu, memory}
+ * (nodenumaresource/scoring.go:35-53,191-230, least_allocated.go:30-58,
+ * most_allocated.go:30-44): resources with allocatable 0 are left out. */
 static int64_t numa_least_allocated(const koordhip_config *cfg, int64_t req_cpu, int64_t alloc_cpu, int64_t req_mem,
                                     int64_t alloc_mem) {
+  int64_t (*rs)(int64_t, int64_t) = cfg->numa_most_allocated ? most_requested : orc_least_requested;
   int64_t num = 0, wsum = 0;
   if (cfg->numa_weight_cpu && alloc_cpu != 0) {
-    num += orc_least_requested(req_cpu, alloc_cpu) * cfg->numa_weight_cpu;
+    num += rs(req_cpu, alloc_cpu) * cfg->numa_weight_cpu;
     wsum += cfg->numa_weight_cpu;
   }
   if (cfg->numa_weight_mem && alloc_mem != 0) {
-    num += orc_least_requested(req_mem, alloc_mem) * cfg->numa_weight_mem;
+    num += rs(req_mem, alloc_mem) * cfg->numa_weight_mem;
     wsum += cfg->numa_weight_mem;
   }
   return wsum ? num / wsum : 0;

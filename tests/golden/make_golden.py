@@ -305,6 +305,37 @@ spread_order_cases = [
          strategy="LeastAllocated", want=_SPREAD_ORDER),
 ]
 
+# ------------------------------------------------------------ scoring_test.go TestPlugin_Score
+SCORE_TEST = "pkg/scheduler/plugins/nodenumaresource/scoring_test.go"
+
+
+def nscore(name, line, want, topo=None, cpu_bind=True, policy="", need=0, labels=None, total_cpus=96):
+    """One Score call: topology = buildCPUTopologyForTest(sockets, nodesPerSocket, coresPerNode, cpusPerCore)
+    or None (no CPU topology) / "invalid" (&CPUTopology{}); the node's allocatable cpu is its CPU count
+    x 1000 (96 CPUs without a topology), memory 512Gi; empty NodeAllocation; requests = cpu only."""
+    return dict(name=name, source=f"{SCORE_TEST}:{line}", topology=topo, request_cpu_bind=cpu_bind,
+                preferred_bind_policy=policy, need=need, node_labels=labels or {}, want=want,
+                total_cpus=total_cpus)
+
+
+LBL_STRATEGY = "node.koordinator.sh/numa-allocate-strategy"
+LBL_BIND = "node.koordinator.sh/cpu-bind-policy"
+numa_score_cases = [
+    nscore("error with missing allocationState", 389, 0),
+    nscore("error with invalid cpu topology", 398, 0, topo="invalid", total_cpus=0),
+    nscore("succeed with skip", 408, 0, cpu_bind=False),
+    nscore("score with full empty node FullPCPUs", 417, 25, [2, 1, 4, 2], policy="FullPCPUs", need=4),
+    nscore("score with satisfied node FullPCPUs", 429, 50, [2, 1, 4, 2], policy="FullPCPUs", need=8),
+    nscore("score with full empty node SpreadByPCPUs", 442, 25, [2, 1, 4, 2], policy="SpreadByPCPUs", need=4),
+    nscore("score with exceed socket FullPCPUs", 454, 100, [2, 1, 4, 2], policy="FullPCPUs", need=16),
+    nscore("score with satisfied socket FullPCPUs", 466, 50, [2, 2, 4, 2], policy="FullPCPUs", need=16),
+    nscore("score with full empty socket SpreadByPCPUs", 478, 25, [2, 1, 4, 2], policy="SpreadByPCPUs", need=4),
+    nscore("score with Node NUMA Allocate Strategy", 490, 12, [2, 1, 4, 2], policy="SpreadByPCPUs", need=2,
+           labels={LBL_STRATEGY: "LeastAllocated"}),
+    nscore("score with Node CPU Bind Policy", 505, 50, [2, 1, 4, 2], policy="SpreadByPCPUs", need=8,
+           labels={LBL_BIND: "FullPCPUsOnly"}),
+]
+
 
 def dump(name, obj):
     with open(os.path.join(HERE, name), "w") as f:
@@ -324,4 +355,10 @@ if __name__ == "__main__":
                                   "not_transcribed": "TestTakeCPUsWithMaxRefCount / TestTakeCPUsSortByRefCount "
                                                      "(maxRefCount 2) and the preferred-CPU calls of "
                                                      "TestTakePreferredCPUs (Reservation): out of the engine's scope"})
+    dump("numa_score.json", {"cases": numa_score_cases,
+                             "harness": f"{SCORE_TEST}:520-594 (ScoringStrategy MostAllocated, resources cpu:1)",
+                             "not_transcribed": "error with missing preFilterState (:384, a framework.Status error, "
+                                                "not a score); TestNUMANodeScore (NUMA topology policies) and "
+                                                "TestScoreWithAmplifiedCPUs (amplification): out of the engine's "
+                                                "scope"})
     print("wrote golden fixtures")

@@ -94,3 +94,49 @@ def score_cases():
 def filter_cases():
     d = load("loadaware_filter.json")
     return [(c["name"], c, c.get("node", d["node"])) for c in d["cases"]]
+
+
+# ------------------------------------------------ NodeNUMAResource Score (scoring_test.go)
+def numa_score_cases():
+    return [(c["name"], c) for c in load("numa_score.json")["cases"]]
+
+
+def build_numa_score_case(case):
+    """-> (profile, NodeTable(1 row), pod record array(1)) for one TestPlugin_Score row
+    (scoring_test.go:520-594: MostAllocated over cpu weight 1, allocatable cpu = #CPUs x 1000,
+    memory 512Gi, an empty NodeAllocation, the test's preFilterState as the pod's NUMA state)."""
+    from koordinator_amd import abi
+    from koordinator_amd.config import PLUGIN_NUMA
+    from koordinator_amd.numa import ClassTable, node_numa_flags, reference_test_topology
+    from koordinator_amd.snapshot import NodeTable, pod_array
+    prof = Profile(filters=(), scores={PLUGIN_NUMA: 1})
+    prof.numa.scoring_type = "MostAllocated"
+    prof.numa.resources = {k8s.CPU: 1}
+    t = NodeTable.empty(1)
+    if isinstance(case["topology"], list):
+        topo = reference_test_topology(*case["topology"])
+        ct = ClassTable()
+        t["numa_class"][0] = ct.add(topo)
+        t.numa_classes = ct.records()
+        free = topo.all_mask()
+        for w in range(abi.NUMA_WORDS):
+            t[f"numa_free{w}"][0] = free[w]
+        cpus = topo.num_cpus
+    else:  # no CPU topology, or an invalid one (&CPUTopology{}: zero CPUs)
+        t["numa_class"][0] = -1
+        cpus = case["total_cpus"]
+    t["alloc0"][0] = cpus * 1000
+    t["alloc1"][0] = 512 * 2**30
+    t["la_alloc_cpu_m"][0], t["la_alloc_mem"][0] = t["alloc0"][0], t["alloc1"][0]
+    t["numa_flags"][0] = node_numa_flags(case["node_labels"], None, prof.numa.default_most_allocated)
+    p = pod_array(1)
+    if case["request_cpu_bind"]:
+        need = case["need"]
+        p["req"][0, abi.RES_CPU] = need * 1000
+        p["nz_cpu_m"][0] = need * 1000
+        p["flags"][0] = abi.POD_PROD | abi.POD_CPUSET | (abi.POD_HAS_REQ if need else 0)
+        p["numa_cpus"][0] = need
+        pol = {"": abi.CPUBIND_NONE, "FullPCPUs": abi.CPUBIND_FULL_PCPUS,
+               "SpreadByPCPUs": abi.CPUBIND_SPREAD_BY_PCPUS}[case["preferred_bind_policy"]]
+        p["numa_policy"][0] = abi.numa_policy(0, pol, 0)
+    return prof, t, p

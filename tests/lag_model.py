@@ -40,6 +40,8 @@ def _nonmono(pod) -> bool:
 
 def place_lagged(cfg, table, pods, batch: int) -> np.ndarray:
     k = 2 * batch
+    # a MostAllocated NodeNUMAResource score rises with commits: every pod re-evaluates M and M'
+    monotone = not ((cfg.score_plugins & abi.PLUGIN_NUMA) and cfg.numa_most_allocated)
     cur = oracle.Oracle(cfg, table)   # the live state
     lag = oracle.Oracle(cfg, table)   # state at the end of round r - 2
     out = np.full(len(pods), abi.UNSCHEDULABLE, np.int32)
@@ -69,7 +71,7 @@ def place_lagged(cfg, table, pods, batch: int) -> np.ndarray:
             cand = L[first] if first is not None else 0
             prefix_mod = any(_node(e) in M for e in L[:first if first is not None else len(L)])
             best = cand
-            nonmono = _nonmono(pod)
+            nonmono = _nonmono(pod) or not monotone
             if M and (prefix_mod or nonmono):
                 v = _totals(cur, cfg, pod)
                 best = max([best] + [_key(v[i], i) for i in M])

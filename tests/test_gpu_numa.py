@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
+import golden_cases as G
 from koordinator_amd import abi, synth
 from koordinator_amd.config import PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, shipped_profile, to_c_config
 from koordinator_amd.numa import (ClassTable, format_cpuset, linux_topology, parse_cpuset, reference_test_topology)
@@ -172,10 +173,14 @@ def test_gpu_numa_eval_parity(Engine):
     assert len(bad) == 0, bad[:5]
 
 
-@pytest.mark.parametrize("n_nodes,n_pods,batch,cpuset_frac", [(600, 1000, 0, 0.5), (300, 800, 17, 0.8),
-                                                              (2000, 1500, 64, 0.3)])
-def test_gpu_numa_stream_bit_exact(Engine, n_nodes, n_pods, batch, cpuset_frac):
+@pytest.mark.parametrize("n_nodes,n_pods,batch,cpuset_frac,scoring", [
+    (600, 1000, 0, 0.5, "LeastAllocated"), (300, 800, 17, 0.8, "LeastAllocated"),
+    (2000, 1500, 64, 0.3, "LeastAllocated"),
+    (600, 1000, 0, 0.5, "MostAllocated"),     # non-monotone score: M and M' re-evaluated for every pod
+    (300, 800, 17, 0.8, "MostAllocated")])
+def test_gpu_numa_stream_bit_exact(Engine, n_nodes, n_pods, batch, cpuset_frac, scoring):
     prof = shipped_profile(numa=True)
+    prof.numa.scoring_type = scoring
     prof.batch_pods = batch
     table = synth.make_cluster(synth.ClusterSpec(n_nodes), prof)
     synth.add_numa(table, synth.NumaSpec(), prof)
@@ -216,3 +221,13 @@ def test_gpu_reserve_failure(Engine):
     assert np.array_equal(got, ref)
     for k, v in o.numa_state().items():
         assert np.array_equal(nst[k], v), k
+
+
+@pytest.mark.parametrize("name,case", G.numa_score_cases(), ids=[c[0] for c in G.numa_score_cases()])
+def test_gpu_numa_score_kat(Engine, name, case):
+    """TestPlugin_Score (scoring_test.go:373-595) through libkoordhip.so."""
+    prof, table, pod = G.build_numa_score_case(case)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(table)
+        got = e.eval(pod)["scores"][0, 2, 0]
+    assert got == case["want"], case["source"]

@@ -23,10 +23,12 @@ def test_lag_model_fit_loadaware(n_nodes, n_pods, batch, be):
     assert np.array_equal(place_lagged(cfg, table, pods, batch), ref)
 
 
-@pytest.mark.parametrize("n_nodes,n_pods,batch,cpuset_frac", [(600, 1000, 64, 0.5), (300, 800, 17, 0.8),
-                                                              (60, 400, 8, 0.9)])
-def test_lag_model_numa(n_nodes, n_pods, batch, cpuset_frac):
+@pytest.mark.parametrize("n_nodes,n_pods,batch,cpuset_frac,scoring", [
+    (600, 1000, 64, 0.5, "LeastAllocated"), (300, 800, 17, 0.8, "LeastAllocated"),
+    (60, 400, 8, 0.9, "LeastAllocated"), (300, 800, 17, 0.6, "MostAllocated")])
+def test_lag_model_numa(n_nodes, n_pods, batch, cpuset_frac, scoring):
     prof = shipped_profile(numa=True)
+    prof.numa.scoring_type = scoring
     table = synth.make_cluster(synth.ClusterSpec(n_nodes), prof)
     synth.add_numa(table, synth.NumaSpec(), prof)
     pods = synth.make_pods(synth.StreamSpec(n_pods, be_frac=0.2, cpuset_frac=cpuset_frac), prof)

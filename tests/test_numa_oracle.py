@@ -7,7 +7,9 @@ import numpy as np
 import pytest
 
 import oracle
+import golden_cases as G
 from koordinator_amd import abi
+from koordinator_amd.config import to_c_config
 from koordinator_amd.numa import (Topology, TopologyError, CPUInfo, format_cpuset, linux_topology, parse_cpuset,
                                   reference_test_topology)
 
@@ -67,3 +69,11 @@ def test_take_cpus_never_exceeds_avail_and_counts():
             assert got is not None
             cs = topo.cpus(got)
             assert len(cs) == need and set(cs) <= set(free)
+
+
+@pytest.mark.parametrize("name,case", G.numa_score_cases(), ids=[c[0] for c in G.numa_score_cases()])
+def test_numa_score_kat(name, case):
+    """TestPlugin_Score (scoring_test.go:373-595): MostAllocated NodeNUMAResource score."""
+    prof, table, pod = G.build_numa_score_case(case)
+    got = oracle.Oracle(to_c_config(prof), table).eval(pod)["scores"][0, 2, 0]
+    assert got == case["want"], case["source"]
