@@ -44,6 +44,11 @@ def bytes_per_eval(pods: np.ndarray, cfg) -> np.ndarray:
     bc = (flags & abi.POD_REQ_BCPU) != 0
     bm = (flags & abi.POD_REQ_BMEM) != 0
     b += 16 * bc + 16 * bm                           # batch alloc + requested
+    if cfg.score_plugins & abi.PLUGIN_NUMA or cfg.filter_plugins & abi.PLUGIN_NUMA:
+        cs = (flags & abi.POD_CPUSET) != 0
+        b += 4                                       # NUMA topology class (i32)
+        b += (8 * ~rcpu) * ((flags & abi.POD_NUMA_SKIP) == 0)   # Score reads Requested cpu (non-cpuset pods)
+        b += cs * (3 * abi.NUMA_WORDS * 8 + 4 + 1)   # cpuset pods: free / exclusive masks, allocated count, flags
     return b
 
 
@@ -84,9 +89,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--nodes", type=int, default=50000)
-    ap.add_argument("--pods", type=int, default=100000)
-    ap.add_argument("--be-frac", type=float, default=0.3)
+    ap.add_argument("--workload", choices=["config4", "config3"], default="config4",
+                    help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
+                         "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods)")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--pods", type=int, default=None)
+    ap.add_argument("--be-frac", type=float, default=None)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -108,10 +116,18 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    prof = shipped_profile()
+    numa = args.workload == "config3"
+    c = synth.CONFIGS[3 if numa else 4]
+    args.nodes = args.nodes or c["nodes"]
+    args.pods = args.pods or c["pods"]
+    args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
+    prof = shipped_profile(numa=numa)
     prof.batch_pods = args.batch
     table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
-    pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac), prof)
+    if numa:
+        synth.add_numa(table, synth.NumaSpec(), prof)
+    pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac,
+                                            cpuset_frac=c.get("cpuset_frac", 0.0)), prof)
     cfg = to_c_config(prof)
 
     eng = PlacementEngine(prof, device=local_rank, profile_kernels=True)
@@ -172,7 +188,7 @@ def main():
     avg_launch_ms = eval_ms / max(launches, 1)
     evals_per_launch = evals / max(launches, 1)
     achieved = evals_per_launch * b_per_pod / (avg_launch_ms * 1e-3) / 1e9 if eval_ms > 0 else None
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src = pmc_traffic() if not numa else (None, None)   # the committed PMC pass is config 4's
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -187,8 +203,12 @@ def main():
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded splitmix64 cluster + pod stream, SURVEY.md §8(d))",
-        "config": {"workload": f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
-                               "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile",
+        "config": {"workload": (f"config3: {args.nodes} 2-socket nodes x {args.pods} pods, "
+                                f"{int(args.be_frac * 100)}% BE, {int(c.get('cpuset_frac', 0) * 100)}% of LS pods "
+                                "LSR/LSE cpuset, NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource"
+                                if numa else
+                                f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
+                                "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile"),
                    "nodes": args.nodes, "pods": args.pods, "batch_pods": eng.cfg.batch_pods or 32,
                    "parallelism": f"node-shard x{world}"},
         "unschedulable": int((placements < 0).sum()),

@@ -26,6 +26,14 @@
 
 namespace kh {
 
+// The running best of the node / socket selection loops (whose trip counts
+// come from the per-node topology class, i.e. divergent in the scan kernel) is
+// kept in memory: with ROCm 7.2's optimizer these selections came out wrong
+// (tests/test_gpu_numa.py: e.g. "allocate in the smallest idle socket") unless
+// the functions were built optnone, which made the scan 5x and the cpuset
+// Reserve 30x slower.  Pinning just these variables is enough.
+#define KH_PINNED volatile
+
 constexpr int NW = KOORDHIP_NUMA_WORDS;
 constexpr int NMAX = KOORDHIP_NUMA_MAX_NODES;
 
@@ -104,7 +112,7 @@ __device__ __forceinline__ int cores_in(const uint64_t *m, const uint64_t *g, in
 // per core.  Stages follow cpu_accumulator.go:184-229; a stage that finds a
 // group big enough returns immediately, with distinct cores iff the group has
 // that many distinct cores (spreadCPUs takes one CPU per core first).
-__device__ __attribute__((noinline, optnone)) bool numa_spread_ok(const DevNumaClass &C, const NumaRow &r, int need, int excl, bool most) {
+__device__ __attribute__((noinline)) bool numa_spread_ok(const DevNumaClass &C, const NumaRow &r, int need, int excl, bool most) {
   const int cpc = C.cpc;
   uint64_t X[NW], Xp[NW], F[NW];
   excluded_set(C, r, excl, false, X);
@@ -115,7 +123,7 @@ __device__ __attribute__((noinline, optnone)) bool numa_spread_ok(const DevNumaC
     for (int k = 0; k < C.nnuma; k++)
       if (cores_in(F, C.nm[k], cpc) >= need) return true;
     // pass false: the first node in (free, socket free, id) order with >= need CPUs decides
-    int best = -1, bf = 0, bs = 0;
+    KH_PINNED int best = -1, bf = 0, bs = 0;
     for (int k = 0; k < C.nnuma; k++) {
       const int f = popc_and(r.fr, C.nm[k]);
       if (f < need) continue;
@@ -132,7 +140,7 @@ __device__ __attribute__((noinline, optnone)) bool numa_spread_ok(const DevNumaC
     for (int w = 0; w < NW; w++) F[w] = r.fr[w] & ~Xp[w];  // socket pass true filters PCPULevel only (:612)
     for (int s = 0; s < C.nsock; s++)
       if (cores_in(F, C.sm[s], cpc) >= need) return true;
-    int best = -1, bf = 0;
+    KH_PINNED int best = -1, bf = 0;
     for (int s = 0; s < C.nsock; s++) {
       const int f = popc_and(r.fr, C.sm[s]);
       if (f < need) continue;
@@ -210,14 +218,12 @@ __device__ __forceinline__ int32_t numa_la(double rc, double ac, double rm, doub
 // ---------------------------------------------------------------------------
 // Exact accumulator replay for Reserve (cpu_accumulator.go:87-232, mask form).
 //
-// The non-inline functions of the replay (and numa_spread_ok) are built
-// noinline + optnone: with ROCm 7.2's optimizer (-O2 and -O3 alike) the node /
-// socket selection loops came out wrong once inlined into the 1-wave resolve
-// kernel (a different NUMA node than the reference's order picks; inserting a
-// printf or making the running best volatile "fixed" it, i.e. an optimizer
-// miscompile, not a data race).  These paths run once per cpuset Reserve and
-// for required-SpreadByPCPUs Filters only, so the unoptimized code costs
-// little; tests/test_gpu_numa.py pins every choice bit for bit.
+// The replay's functions stay noinline (one copy, called from the 1-wave
+// resolve and from k_commit); their node / socket selections keep the running
+// best in KH_PINNED variables (see the top of this file): ROCm 7.2 otherwise
+// picks a different NUMA node / socket than the reference's order for some
+// states, -O2 and -O3 alike.  tests/test_gpu_numa.py pins every choice bit for
+// bit (reference KATs, randomized states, streams).
 
 struct Acc {
   uint64_t A[NW];   // allocatable
@@ -269,7 +275,7 @@ __device__ __forceinline__ void acc_excluded(const DevNumaClass &C, const Acc &a
 // spread order of the CPUs of m listed in ascending CPU id (freeCPUsInNode /
 // freeCPUsInSocket + spreadCPUs): round t takes each core's t-th CPU by id,
 // rounds in id order; lists of <= cpc CPUs are kept in id order.  Takes n.
-__device__ __attribute__((noinline, optnone)) void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
+__device__ __attribute__((noinline)) void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
   const int len = popc4(m);
   if (len <= C.cpc) {
     for (int i = 0; i < C.ncpu && n > 0; i++) {
@@ -298,7 +304,7 @@ __device__ __attribute__((noinline, optnone)) void acc_take_spread_by_id(const D
 }
 
 // freeCPUs(filterExclusive) + spreadCPUs + one-by-one take (:218-229).
-__device__ __attribute__((noinline, optnone)) void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
+__device__ __attribute__((noinline)) void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
   uint64_t X[NW], F[NW];
   if (fe) acc_excluded(C, a, false, X);
   else
@@ -383,7 +389,7 @@ __device__ __attribute__((noinline, optnone)) void acc_fallback_pass(const DevNu
 }
 
 // takeCPUs; returns true with a.R filled.
-__device__ __attribute__((noinline, optnone)) bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
+__device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
   if (a.need < 1) return true;
   if (a.need > popc4(a.A)) return false;
   const int cpc = C.cpc;
@@ -399,7 +405,7 @@ __device__ __attribute__((noinline, optnone)) bool acc_take_cpus(const DevNumaCl
           FA[w] = expand(fold_and(allowed, cpc), cpc);
           X[w] = fe ? X[w] : 0;
         }
-        int best = -1, bc = 0, bs = 0;
+        KH_PINNED int best = -1, bc = 0, bs = 0;
         for (int k = 0; k < C.nnuma; k++) {
           const int cnt = popc_and(FA, C.nm[k]);
           if (cnt < a.need) continue;
@@ -424,7 +430,7 @@ __device__ __attribute__((noinline, optnone)) bool acc_take_cpus(const DevNumaCl
     }
     for (int w = 0; w < NW; w++) FA[w] = expand(fold_and(a.A[w], cpc), cpc);
     if (a.need <= C.cps) {  // :126-134
-      int best = -1, bc = 0;
+      KH_PINNED int best = -1, bc = 0;
       for (int s = 0; s < C.nsock; s++) {
         const int cnt = popc_and(FA, C.sm[s]);
         if (cnt < a.need) continue;
@@ -509,7 +515,7 @@ __device__ __attribute__((noinline, optnone)) bool acc_take_cpus(const DevNumaCl
         if (fe) acc_excluded(C, a, false, X);
         uint64_t Fl[NW];
         for (int w = 0; w < NW; w++) Fl[w] = a.A[w] & ~(fe ? X[w] : 0ull);
-        int best = -1, bf = 0, bs = 0;
+        KH_PINNED int best = -1, bf = 0, bs = 0;
         for (int k = 0; k < C.nnuma; k++) {
           const int nf = popc_and(Fl, C.nm[k]);
           if (nf == 0) continue;
@@ -543,7 +549,7 @@ __device__ __attribute__((noinline, optnone)) bool acc_take_cpus(const DevNumaCl
         if (fe) acc_excluded(C, a, true, X);
         uint64_t Fl[NW];
         for (int w = 0; w < NW; w++) Fl[w] = a.A[w] & ~(fe ? X[w] : 0ull);
-        int best = -1, bl = 0;
+        KH_PINNED int best = -1, bl = 0;
         for (int s = 0; s < C.nsock; s++) {
           const int nf = popc_and(Fl, C.sm[s]);
           if (nf == 0) continue;
@@ -578,7 +584,7 @@ __device__ __attribute__((noinline, optnone)) bool acc_take_cpus(const DevNumaCl
 }
 
 // Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
-__device__ __attribute__((noinline, optnone)) bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
+__device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
   for (int w = 0; w < NW; w++) cpus[w] = 0;
   const int need = p.numa_cpus;
   if (popc4(r.fr) < need) return false;
