@@ -357,6 +357,7 @@ int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   HIP_TRY(hipMemcpyAsync(c->d_classes, cls.data(), cls.size() * sizeof(kh::DevNumaClass), hipMemcpyHostToDevice,
                          c->stream));
   nu.cls = c->d_classes;
+  nu.ncls = c->n_classes;
   int e = 0;
   int32_t *nc = nullptr, *cnt = nullptr;
   uint8_t *nf = nullptr;

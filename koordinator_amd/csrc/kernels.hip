@@ -396,6 +396,16 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
   const int32_t chunk = xcd * cpx + local % cpx;
   const int32_t pg = local / cpx;
   if (chunk >= nchunks) return;  // block-uniform
+  const DevNumaClass *cls = d.nu.cls;
+  if constexpr (NUMA) {  // topology classes -> LDS (launch_scan sizes it when ncls <= NUMA_LDS_CLASSES)
+    extern __shared__ uint4 scan_cls[];
+    if (d.nu.ncls <= NUMA_LDS_CLASSES) {
+      const uint4 *src = reinterpret_cast<const uint4 *>(d.nu.cls);
+      for (int32_t x = threadIdx.x; x < d.nu.ncls * (int32_t)(sizeof(DevNumaClass) / 16); x += 256) scan_cls[x] = src[x];
+      __syncthreads();
+      cls = reinterpret_cast<const DevNumaClass *>(scan_cls);
+    }
+  }
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: pod fields in SGPRs
   const int32_t p = pg * 4 + wave;
@@ -419,7 +429,7 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
       if constexpr (NUMA) {
         NumaRow nr;
         load_numa(nr, d, i, need);
-        s[r] = eval_total_numa(pod, v, nr, d.nu.cls, c) + 1;
+        s[r] = eval_total_numa(pod, v, nr, cls, c) + 1;
       } else {
         s[r] = eval_total(pod, v, c) + 1;
       }
@@ -1014,7 +1024,7 @@ constexpr int RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (static LDS: 
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
-      want, top, lcnt, hits, hmask, modmap, total;
+      want, top, lcnt, hits, hmask, classes, modmap, total;
 };
 
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
@@ -1058,6 +1068,8 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * 4;
   o.hmask = at;  // per pod: which list positions were refreshed (2 x 64 bits)
   at += RES_MAXP_ROUND * 2 * 8;
+  o.classes = at;  // NodeNUMAResource topology classes (when <= NUMA_LDS_CLASSES)
+  at += numa ? NUMA_LDS_CLASSES * (int32_t)sizeof(DevNumaClass) : 0;
   o.modmap = at;
   at += res_align(((n_nodes + 31) >> 5) * 4);
   o.total = at;
@@ -1173,6 +1185,16 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     sh_stop = 0;
   }
   for (int32_t x = t; x < words; x += RES_THREADS) modmap[x] = 0;
+  const DevNumaClass *cls = ncls;
+  if constexpr (NUMA) {  // topology classes -> LDS
+    const int32_t nc = nodes().nu.ncls;
+    if (nc <= NUMA_LDS_CLASSES) {
+      uint4 *dst = reinterpret_cast<uint4 *>(lds + ofs.classes);
+      const uint4 *src = reinterpret_cast<const uint4 *>(ncls);
+      for (int32_t x = t; x < nc * (int32_t)(sizeof(DevNumaClass) / 16); x += RES_THREADS) dst[x] = src[x];
+      cls = reinterpret_cast<const DevNumaClass *>(lds + ofs.classes);
+    }
+  }
   __syncthreads();
   if (t < sh_mp) {  // resumed pipeline (one launch per round): M' from the previous launch
     const int32_t nd = mbuf[1 + t];
@@ -1292,7 +1314,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           const DevPod pod = lpod[j];
           int32_t tot;
           if constexpr (NUMA) {
-            tot = eval_total_numa(pod, prow[sl], pnr[sl], ncls, c);
+            tot = eval_total_numa(pod, prow[sl], pnr[sl], cls, c);
           } else {
             tot = eval_total(pod, prow[sl], c);
           }
@@ -1446,7 +1468,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             const NV v = mrow[lane];
             if constexpr (NUMA) {
               const NumaRow nr = mnr[lane];
-              key = make_key(eval_total_numa(pod, v, nr, ncls, c), my_node);
+              key = make_key(eval_total_numa(pod, v, nr, cls, c), my_node);
             } else {
               key = make_key(eval_total(pod, v, c), my_node);
             }
@@ -1462,7 +1484,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             const bool in_m = (modmap[nd >> 5] >> (nd & 31)) & 1u;
             if (!in_m) {
               if constexpr (NUMA) {
-                key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], ncls, c), nd);
+                key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], cls, c), nd);
               } else {
                 key = make_key(eval_total(pod, prow[lane], c), nd);
               }
@@ -1525,7 +1547,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
               int okl = 0;
               if (lane == 0) {
                 NumaRow nr = *snr;
-                okl = nr.cls >= 0 && numa_allocate(ncls[nr.cls], nr, pod, mc);
+                okl = nr.cls >= 0 && numa_allocate(cls[nr.cls], nr, pod, mc);
                 if (okl) {
                   numa_apply(nr, pod, mc, +1);
                   mnr[rw] = nr;
@@ -1693,8 +1715,9 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
   const int32_t nchunks = scan_chunks(R, lo, hi);
   const int32_t cpx = (nchunks + 7) / 8;
   const int32_t blocks = 8 * cpx * ((n_pods + 3) / 4);
-#define KH_SCAN(RR, NN)                                                                                          \
-  hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), 0, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, S, \
+  const size_t lds = (numa && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0;
+#define KH_SCAN(RR, NN)                                                                                            \
+  hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, S, \
                      s_stride, Mx, m_stride)
   if (numa) {
     switch (R) {

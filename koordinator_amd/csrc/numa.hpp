@@ -45,6 +45,8 @@ struct DevNumaClass {
   uint8_t pos_by_id[KOORDHIP_NUMA_MAX_CPUS];  // positions in ascending CPU id
 };
 
+static_assert(sizeof(DevNumaClass) % 16 == 0, "classes are staged in LDS as 16-B words");
+
 struct NumaRow {
   int32_t cls;     // -1: no CPU topology
   uint32_t nflags; // KOORDHIP_NODE_*
@@ -59,7 +61,13 @@ struct DevNuma {
   const uint8_t *nflags;
   uint64_t *fr[NW], *ep[NW], *en[NW];
   int32_t *cnt;
+  int32_t ncls;  // topology classes at cls
 };
+
+// Kernels stage up to this many topology classes in LDS (800 B each): the
+// accumulator's loops and the closed-form Filter read them with dependent,
+// data-driven indexes, at LDS instead of L2 latency.
+constexpr int NUMA_LDS_CLASSES = 8;
 
 __device__ __forceinline__ int popc4(const uint64_t *m) {
   return __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
