@@ -997,8 +997,9 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[4],
                  (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7],
                  (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[15], (unsigned long long)h[14]);
-    std::fprintf(stderr, "[koordhip stamps] resolve loop cycles: candidate %llu  staging %llu  re-eval %llu  commit %llu\n",
-                 (unsigned long long)h[16], (unsigned long long)h[17], (unsigned long long)h[18],
+    std::fprintf(stderr, "[koordhip stamps] resolve loop cycles: fast path %llu | general path: candidate %llu  re-eval %llu  "
+                 "commit %llu\n",
+                 (unsigned long long)h[17], (unsigned long long)h[16], (unsigned long long)h[18],
                  (unsigned long long)h[19]);
   }
   return 0;

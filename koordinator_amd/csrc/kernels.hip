@@ -1218,7 +1218,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   if (lane == 14 || lane == 16) doff = (int32_t)offsetof(DevPod, est_cpu);  // la_u / la_up (prod)
   if (lane == 15 || lane == 17) doff = (int32_t)offsetof(DevPod, est_mem);
   uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0, c_ph_a = 0, c_ph_b = 0, c_ph_r = 0, c_rel = 0;
-  uint64_t c_l[4] = {0, 0, 0, 0};  // loop phases: candidate, staging, re-evaluation, commit
+  uint64_t c_l[4] = {0, 0, 0, 0};  // loop phases: general-path candidate, fast path, re-evaluation, commit
   for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
     const int32_t n_pods = min(P, total - p0);
     const DevPod *rp = pods + p0;
@@ -1387,6 +1387,27 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       // the next pod's best keys are read one pod ahead (off the dependent chain)
       const int32_t pn0 = pre_node[lane], pn1 = pre_node[lane + 64];
       uint64_t tv_next = lane < RES_TOP ? top[lane] : 0ull;
+      // per-pod bits (lane j = pod j): prod (its Reserve adds to la_used_prod),
+      // and "slow" pods that never take the fast path below: a non-monotone
+      // configuration, NUMA cpuset pods (Allocate at Reserve, required-policy
+      // feasibility is not monotone)
+      uint64_t prodmask, slowmask;
+      {
+        uint32_t fl = 0, pol = 0;
+        if (lane < n_pods) {
+          fl = lpod[lane].flags;
+          pol = lpod[lane].numa_policy;
+        }
+        prodmask = __ballot(lane < n_pods && (fl & KOORDHIP_POD_PROD));
+        bool slow = !monotone;
+        if constexpr (NUMA) {
+          const bool cs = numa_on(c) && (fl & KOORDHIP_POD_CPUSET) &&
+                          !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+          slow = slow || cs;
+        }
+        (void)pol;
+        slowmask = __ballot(lane < n_pods && slow);
+      }
       // The Reserve delta of a pod is applied lane-parallel (lane q on row word
       // q) and deferred: its row words are read at the pod's decision and the
       // update is finished after the next pod's candidate reads are issued, so
@@ -1421,18 +1442,68 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             ts = x;
           }
         };
-        const DevPod pod = lpod[j];  // VGPR copy: SGPRs are the scarce register file here
         // candidate: the best entry outside M (every list key is exact); first
         // among the pod's RES_TOP best, else from the whole list
         const uint64_t tv = tv_next;
         if (j + 1 < n_pods) tv_next = lane < RES_TOP ? top[(j + 1) * RES_TOP + lane] : 0ull;
-        bool tmod = false;
-        if (tv) {
-          const int32_t nd = key_node(tv);
-          tmod = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-        }
+        // the M bits of the best keys: an unconditional read (no branch), so the
+        // previous pod's row update below issues while it is in flight
+        const int32_t tnd = key_node(tv);
+        const uint32_t tword = modmap[tv != 0 ? (tnd >> 5) : 0];
         finish();  // the previous pod's row update (reads issued at its decision)
+        const bool tmod = tv != 0 && ((tword >> (tnd & 31)) & 1u);
         const uint64_t tfree = __ballot(tv != 0 && !tmod);
+        // ---- fast path (monotone pod, the first free key of its best 8 has no
+        //      M node ranked above it): that key is the winner, a node new to M
+        if (tfree != 0 && !((slowmask >> j) & 1ull) &&
+            __ballot(tv != 0 && tmod && lane < __builtin_ctzll(tfree)) == 0) {
+          const int32_t w = key_node(readlane_u64(tv, __builtin_ctzll(tfree)));
+          const int32_t rw = nm;
+          const NV *srow = &mrow[rw];
+          const NumaRow *snr = &mnr[rw];
+          const uint64_t pm0 = __ballot(pn0 == w), pm1 = __ballot(pn1 == w);
+          const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
+          const int32_t sl = (src < 0 && mp > 0) ? prev_slot(w) : -1;
+          if (src >= 0) {
+            srow = &pre[src];
+            snr = &prenr[src];
+          } else if (sl >= 0) {
+            srow = &prow[sl];
+            snr = &pnr[sl];
+          } else {
+            n_miss++;
+            if (lane == 0) {
+              NV v;
+              load_row(v, nodes(), w);
+              mrow[rw] = v;
+              if constexpr (NUMA) {
+                NumaRow nr;
+                load_numa_row(nr, nodes(), w);
+                mnr[rw] = nr;
+              }
+            }
+          }
+          if constexpr (NUMA) {
+            if (lane < (int)(sizeof(NumaRow) / 8))
+              reinterpret_cast<uint64_t *>(&mnr[rw])[lane] = reinterpret_cast<const uint64_t *>(snr)[lane];
+          }
+          pend_x = lane < RES_WORDS ? reinterpret_cast<const uint64_t *>(srow)[lane] : 0ull;
+          pend_dq = (doff >= 0 && (lane < 16 || ((prodmask >> j) & 1ull)))
+                        ? *reinterpret_cast<const double *>(reinterpret_cast<const char *>(&lpod[j]) + doff)
+                        : 0.0;
+          pend_rw = rw;
+          pend = true;
+          nm++;
+          if (lane == rw) my_node = w;
+          if (lane == 0) {
+            atomicOr(&modmap[w >> 5], 1u << (w & 31));
+            out_node[p0 + j] = w;
+          }
+          if (out_cpus && lane < NW) out_cpus[(size_t)(p0 + j) * NW + lane] = 0ull;
+          lap(1);
+          continue;
+        }
+        const DevPod pod = lpod[j];  // VGPR copy: SGPRs are the scarce register file here
         uint64_t cand = 0;
         bool prefix_modified;
         if (tfree || lcnt[j] <= RES_TOP) {
@@ -1458,7 +1529,6 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           prefix_modified = (__ballot(mod0 && e0 > cand) | __ballot(mod1 && e1 > cand)) != 0;
         }
         lap(0);
-        lap(1);
         const bool nonmono = !monotone || (NUMA && is_cpuset(pod) &&
                                            KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
         uint64_t best = cand;
@@ -1566,8 +1636,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             result = w;
             // Reserve delta (apply_delta): issue the reads, finish() applies it
             pend_x = lane < RES_WORDS ? reinterpret_cast<const uint64_t *>(srow)[lane] : 0ull;
-            const bool prod = (pod.flags & KOORDHIP_POD_PROD) != 0;
-            pend_dq = (doff >= 0 && (lane < 16 || prod))
+            pend_dq = (doff >= 0 && (lane < 16 || ((prodmask >> j) & 1ull)))
                           ? *reinterpret_cast<const double *>(reinterpret_cast<const char *>(&lpod[j]) + doff)
                           : 0.0;
             pend_rw = rw;
