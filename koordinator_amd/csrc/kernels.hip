@@ -1001,6 +1001,19 @@ constexpr int res_threads() { return NUMA ? 256 : 512; }
 // 0-4 a[], 5-9 r[], 10-11 nz, 12-13 la_a, 14-15 la_u, 16-17 la_up (f64),
 // 18 = a_pods | npods << 32, 19 = flags.
 constexpr int RES_WORDS = 20;
+
+// M / M' rows in LDS carry a stale over-commit part of `flags` (the deferred
+// Reserve in k_resolve only adds the deltas); every read of such a row for an
+// evaluation or a write-back goes through here.
+__device__ __forceinline__ NV slot_row(const NV &src) {
+  NV v = src;
+  uint32_t f = v.flags & ~(uint32_t)(NF_OVER_CPU | NF_OVER_MEM | NF_OVER_EPH);
+  if (v.r[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU]) f |= NF_OVER_CPU;
+  if (v.r[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM]) f |= NF_OVER_MEM;
+  if (v.r[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH]) f |= NF_OVER_EPH;
+  v.flags = f;
+  return v;
+}
 static_assert(sizeof(NV) == RES_WORDS * 8, "NV row = 20 words");
 static_assert(offsetof(NV, r) == 40 && offsetof(NV, nz_cpu) == 80 && offsetof(NV, la_u_cpu) == 112 &&
                   offsetof(NV, la_up_cpu) == 128 && offsetof(NV, a_pods) == 144 && offsetof(NV, npods) == 148 &&
@@ -1314,9 +1327,9 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           const DevPod pod = lpod[j];
           int32_t tot;
           if constexpr (NUMA) {
-            tot = eval_total_numa(pod, prow[sl], pnr[sl], cls, c);
+            tot = eval_total_numa(pod, slot_row(prow[sl]), pnr[sl], cls, c);
           } else {
-            tot = eval_total(pod, prow[sl], c);
+            tot = eval_total(pod, slot_row(prow[sl]), c);
           }
           lk[(size_t)j * kp + q] = make_key(tot, pnode[sl]);
         }
@@ -1421,15 +1434,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         uint64_t x = pend_x;
         if (lane < 18) x = (uint64_t)__double_as_longlong(__longlong_as_double((long long)x) + pend_dq);
         if (lane == 18) x += 1ull << 32;  // npods + 1 (high half; a_pods below)
-        // over-commit bits from the new Requested vs Allocatable (cpu, mem, eph)
-        uint32_t over = 0;
-#pragma unroll
-        for (int q = 0; q < 3; q++) {
-          const double a = __longlong_as_double((long long)readlane_u64(x, q));
-          const double rq = __longlong_as_double((long long)readlane_u64(x, 5 + q));
-          over |= rq > a ? (uint32_t)NF_OVER_CPU << q : 0u;
-        }
-        if (lane == 19) x = (x & ~(uint64_t)(NF_OVER_CPU | NF_OVER_MEM | NF_OVER_EPH)) | over;
+        // word 19 (flags) is copied with stale over-commit bits: slot_row() recomputes them
         if (lane < RES_WORDS) reinterpret_cast<uint64_t *>(&mrow[pend_rw])[lane] = x;
         pend = false;
       };
@@ -1535,7 +1540,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         if (nm > 0 && (prefix_modified || nonmono)) {
           uint64_t key = 0;
           if (lane < nm) {
-            const NV v = mrow[lane];
+            const NV v = slot_row(mrow[lane]);
             if constexpr (NUMA) {
               const NumaRow nr = mnr[lane];
               key = make_key(eval_total_numa(pod, v, nr, cls, c), my_node);
@@ -1554,9 +1559,9 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             const bool in_m = (modmap[nd >> 5] >> (nd & 31)) & 1u;
             if (!in_m) {
               if constexpr (NUMA) {
-                key = make_key(eval_total_numa(pod, prow[lane], pnr[lane], cls, c), nd);
+                key = make_key(eval_total_numa(pod, slot_row(prow[lane]), pnr[lane], cls, c), nd);
               } else {
-                key = make_key(eval_total(pod, prow[lane], c), nd);
+                key = make_key(eval_total(pod, slot_row(prow[lane]), c), nd);
               }
             }
           }
@@ -1657,7 +1662,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       finish();
       // ---- 4. write M back, hand it to the next round as M' (rows stay in LDS)
       if (lane < nm) {
-        const NV v = mrow[lane];
+        const NV v = slot_row(mrow[lane]);
         store_row(v, nodes(), my_node);
         if constexpr (NUMA) {
           const NumaRow nr = mnr[lane];
