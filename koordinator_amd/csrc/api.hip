@@ -111,7 +111,7 @@ struct koordhip_ctx {
   uint64_t *d_selpart = nullptr;  // k_select_split slice lists ([pods][G][k])
   uint32_t *d_selcnt = nullptr;   // k_select_split arrival counters (zero between launches)
   int32_t sel_g = kh::kSelGMax;   // workgroups per pod of k_select_split (KOORDHIP_SEL_G)
-  bool sel_split = false;         // k_select_split (KOORDHIP_SELECT_SPLIT) instead of k_select + signal kernel
+  bool sel_split = true;          // k_select_split; false (KOORDHIP_SELECT_ONEWG): k_select + signal kernel
   size_t partial_cap = 0;
   uint64_t *d_lists = nullptr;   // [2][batch][k] (rank-local lists; double buffer: round parity)
   uint64_t *d_gather = nullptr;  // [world][batch][k]
@@ -447,11 +447,11 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     const int v = std::atoi(r);
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
   }
-  if (c->numa && c->partial_r > 4) c->partial_r = 4;
+  if (c->numa && c->partial_r > 4) c->partial_r = 4;  // the NUMA scan kernel is built for R <= 4
   if (const char *g = std::getenv("KOORDHIP_SEL_G")) c->sel_g = std::max(1, std::min(kh::kSelGMax, std::atoi(g)));
-  // the split select shortens the evaluation stream but its workgroups contend
-  // with the resolve wave, which bounds the pipeline at the default round size
-  c->sel_split = std::getenv("KOORDHIP_SELECT_SPLIT") != nullptr;  // the NUMA scan kernel is built for R <= 4
+  // the split select shortens the evaluation stream (and drops the signal
+  // kernel); KOORDHIP_SELECT_ONEWG restores one workgroup per pod for A/B runs
+  c->sel_split = std::getenv("KOORDHIP_SELECT_ONEWG") == nullptr;
   // Fit LeastAllocated + LoadAware least-used (+ NodeNUMAResource LeastAllocated):
   // a commit never raises a key.  A MostAllocated NUMA score rises with every
   // commit, so the resolve re-evaluates its modified nodes for every pod.
