@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "eval.hpp"
 #include "kernels.h"
@@ -1038,11 +1039,15 @@ constexpr int RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (static LDS: 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
       want, top, lcnt, hits, hmask, classes, modmap, total;
+  // second copies of the per-round inputs, filled by waves 1.. while wave 0
+  // resolves the previous round (overlap = 0: every round loads serially)
+  int32_t overlap, lists2, pods2, pre_rows2, pre_numa2, pre_node2;
 };
 
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
 
-__host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, bool numa) {
+__host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, bool numa,
+                                          bool overlap = false) {
   ResLds o;
   int32_t at = 0;
   o.lists = at;
@@ -1085,6 +1090,20 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += numa ? NUMA_LDS_CLASSES * (int32_t)sizeof(DevNumaClass) : 0;
   o.modmap = at;
   at += res_align(((n_nodes + 31) >> 5) * 4);
+  o.overlap = overlap ? 1 : 0;
+  o.lists2 = o.pods2 = o.pre_rows2 = o.pre_numa2 = o.pre_node2 = 0;
+  if (overlap) {
+    o.lists2 = at;
+    at += res_align(n_pods_max * kp * 8);
+    o.pods2 = at;
+    at += res_align(n_pods_max * (int32_t)sizeof(DevPod));
+    o.pre_rows2 = at;
+    at += res_align(RES_PRE * (int32_t)sizeof(NV));
+    o.pre_numa2 = at;
+    at += numa ? res_align(RES_PRE * (int32_t)sizeof(NumaRow)) : 0;
+    o.pre_node2 = at;
+    at += RES_PRE * 4;
+  }
   o.total = at;
   return o;
 }
@@ -1173,6 +1192,12 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   NV *pre = reinterpret_cast<NV *>(lds + ofs.pre_rows);
   NumaRow *prenr = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa);
   int32_t *pre_node = reinterpret_cast<int32_t *>(lds + ofs.pre_node);
+  // the next round's copies (ofs.overlap): swapped with the above every round
+  uint64_t *lk2 = reinterpret_cast<uint64_t *>(lds + ofs.lists2);
+  DevPod *lpod2 = reinterpret_cast<DevPod *>(lds + ofs.pods2);
+  NV *pre2 = reinterpret_cast<NV *>(lds + ofs.pre_rows2);
+  NumaRow *prenr2 = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa2);
+  int32_t *pre_node2 = reinterpret_cast<int32_t *>(lds + ofs.pre_node2);
   int32_t *want = reinterpret_cast<int32_t *>(lds + ofs.want);
   uint64_t *top = reinterpret_cast<uint64_t *>(lds + ofs.top);
   int32_t *lcnt = reinterpret_cast<int32_t *>(lds + ofs.lcnt);
@@ -1232,51 +1257,57 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   if (lane == 15 || lane == 17) doff = (int32_t)offsetof(DevPod, est_mem);
   uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0, c_ph_a = 0, c_ph_b = 0, c_ph_r = 0, c_rel = 0;
   uint64_t c_l[4] = {0, 0, 0, 0};  // loop phases: general-path candidate, fast path, re-evaluation, commit
-  for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
-    const int32_t n_pods = min(P, total - p0);
-    const DevPod *rp = pods + p0;
-    const uint64_t *lists = lists0 + (size_t)(r & 1) * list_buf;
-    const int32_t trace_j = (trace >= p0 && trace < p0 + n_pods) ? trace - p0 : -1;
-    (void)trace_j;
-    // ---- 0. wait for this round's lists (thread 0), then every wave reads them
-    const uint64_t t_w0 = (dbg && t == 0) ? stamp() : 0;
-    if (t == 0 && !wait_at_least(&sy->sel_round, p0 + n_pods, sy)) sh_stop = 1;
-    __syncthreads();
-    if (sh_stop) return;  // the evaluation side failed: give up, the host reports it
-    const uint64_t t_entry = (dbg && t == 0) ? stamp() : 0;
-    const int32_t mp = sh_mp;
-    // ---- 1. every global read of the prologue at once: lists -> LDS (stride
-    //         kp, zero padded), pod records, and the rows of the list heads
-    //         (slot s = pod s / 2, position s % 2, as delivered); M' rows are
-    //         in LDS already (wave 0 left them there at the end of the last round)
-    for (int32_t x = t; x < n_pods * kp; x += RES_THREADS) {
+  // ---- 1. a round's global reads: lists -> LDS (stride kp, zero padded), pod
+  //         records, and the rows of the list heads (slot s = pod s / 2,
+  //         position s % 2, as delivered), by threads tid = 0..nth-1
+  auto load_round = [&](int32_t rr, int32_t rp0, int32_t rn, uint64_t *Lk, DevPod *Lp, NV *Pr, NumaRow *Pn,
+                        int32_t *Pnode, int32_t tid, int32_t nth) {
+    const uint64_t *L = lists0 + (size_t)(rr & 1) * list_buf;
+    for (int32_t x = tid; x < rn * kp; x += nth) {
       const int32_t j = x / kp, q = x - j * kp;
-      lk[x] = q < k ? lists[(size_t)j * k + q] : 0ull;
+      Lk[x] = q < k ? L[(size_t)j * k + q] : 0ull;
     }
     {
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(rp);
-      uint32_t *dst = reinterpret_cast<uint32_t *>(lpod);
-      for (int32_t x = t; x < n_pods * (int32_t)(sizeof(DevPod) / 4); x += RES_THREADS) dst[x] = src[x];
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(pods + rp0);
+      uint32_t *dst = reinterpret_cast<uint32_t *>(Lp);
+      for (int32_t x = tid; x < rn * (int32_t)(sizeof(DevPod) / 4); x += nth) dst[x] = src[x];
     }
-    if (t < RES_PRE) {
-      const int32_t j = t >> 1, q = t & 1;
+    for (int32_t sl = tid; sl < RES_PRE; sl += nth) {
+      const int32_t j = sl >> 1, q = sl & 1;
       int32_t nd = -1;
-      if (j < n_pods && q < k) {
-        const uint64_t e = lists[(size_t)j * k + q];
+      if (j < rn && q < k) {
+        const uint64_t e = L[(size_t)j * k + q];
         if (e != 0) nd = key_node(e);
       }
       if (nd >= 0) {
         NV v;
         load_row(v, nodes(), nd);
-        pre[t] = v;
+        Pr[sl] = v;
         if constexpr (NUMA) {
-          NumaRow rr;
-          load_numa_row(rr, nodes(), nd);
-          prenr[t] = rr;
+          NumaRow rr2;
+          load_numa_row(rr2, nodes(), nd);
+          Pn[sl] = rr2;
         }
       }
-      pre_node[t] = nd;
+      Pnode[sl] = nd;
     }
+  };
+  for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
+    const int32_t n_pods = min(P, total - p0);
+    const int32_t trace_j = (trace >= p0 && trace < p0 + n_pods) ? trace - p0 : -1;
+    (void)trace_j;
+    // ---- 0. this round's inputs: loaded by waves 1.. during the previous
+    //         round's loop (overlap), else wait for the lists and load them now
+    const bool preloaded = ofs.overlap && r > r_begin;
+    const uint64_t t_w0 = (dbg && t == 0) ? stamp() : 0;
+    if (!preloaded) {
+      if (t == 0 && !wait_at_least(&sy->sel_round, p0 + n_pods, sy)) sh_stop = 1;
+      __syncthreads();
+    }
+    if (sh_stop) return;  // the evaluation side failed: give up, the host reports it
+    const uint64_t t_entry = (dbg && t == 0) ? stamp() : 0;
+    const int32_t mp = sh_mp;
+    if (!preloaded) load_round(r, p0, n_pods, lk, lpod, pre, prenr, pre_node, t, RES_THREADS);
     for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
     if (t == 0) sh_nhit = 0;
     __syncthreads();
@@ -1297,6 +1328,13 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         h = (h + 1) & (RES_HASH - 1);
       }
     };
+    // rows prefetched while the previous round ran are stale for its nodes (M'),
+    // whose current rows are the M' slots: drop those prefetch slots (read
+    // after the refresh barriers below)
+    if (preloaded && mp > 0 && t < RES_PRE) {
+      const int32_t nd = pre_node[t];
+      if (nd >= 0 && prev_slot(nd) >= 0) pre_node[t] = -1;
+    }
     // ---- 2. refresh the keys of the list entries on M' nodes (exact, current
     //         rows): (a) one wave per pod collects them, (b) every thread
     //         evaluates one -- at most one entry per (pod, M' node), so one
@@ -1683,8 +1721,36 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         c_loop += t_end - t_pro;
         c_wait += t_entry - t_w0;
       }
+    } else if (ofs.overlap && r + 1 < r_end && p0 + P < total) {
+      // ---- waves 1..: the next round's lists, pods and head rows, meanwhile
+      //      (each wave waits for the lists itself: no barrier without wave 0)
+      const int32_t np2 = min(P, total - (p0 + P));
+      int ok = 1;
+      if (lane == 0) ok = wait_at_least(&sy->sel_round, p0 + P + np2, sy) ? 1 : 0;
+      if (__builtin_amdgcn_readfirstlane(ok)) {
+        load_round(r + 1, p0 + P, np2, lk2, lpod2, pre2, prenr2, pre_node2, t - 64, RES_THREADS - 64);
+      } else if (lane == 0) {
+        sh_stop = 1;
+      }
     }
     __syncthreads();
+    if (ofs.overlap) {  // the next round's inputs become current
+      uint64_t *a = lk;
+      lk = lk2;
+      lk2 = a;
+      DevPod *b = lpod;
+      lpod = lpod2;
+      lpod2 = b;
+      NV *c2 = pre;
+      pre = pre2;
+      pre2 = c2;
+      NumaRow *d2 = prenr;
+      prenr = prenr2;
+      prenr2 = d2;
+      int32_t *e2 = pre_node;
+      pre_node = pre_node2;
+      pre_node2 = e2;
+    }
     {  // M's rows become the next round's M' rows
       NV *x = prow;
       prow = mrow;
@@ -1889,7 +1955,9 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   int32_t kp = 1;
   while (kp < k) kp <<= 1;
   const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
-  const ResLds o = res_lds(P, kp, d.n, numa);
+  // a persistent launch preloads round r+1 during round r when both copies fit
+  ResLds o = res_lds(P, kp, d.n, numa, r_end - r_begin > 1 && !std::getenv("KOORDHIP_NO_PRELOAD"));
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false);
   static bool attr[2] = {false, false};
   if (!attr[numa]) {
     const void *f = numa ? (const void *)k_resolve<true> : (const void *)k_resolve<false>;
