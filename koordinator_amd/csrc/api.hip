@@ -254,7 +254,7 @@ int ensure(koordhip_ctx *c, void **p, size_t *cap, size_t bytes) {
 // Exact per-pod top-k over node range [lo, hi) of np pods: k_scan fills the
 // score matrix, k_select reduces each row (best first, 0-padded).
 int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
-               uint64_t *out, bool timed, int32_t *done) {
+               uint64_t *out, bool timed, kh::PipeSync *sync, int32_t res_wait) {
   const int R = c->partial_r;
   const int64_t stride = ((int64_t)(hi - lo) + 63) & ~63ll;
   const int32_t nchunks = kh::scan_chunks(R, lo, hi);
@@ -292,7 +292,7 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
     HIP_TRY(hipMemsetAsync(c->d_selcnt, 0, kh::kSelMaxPods * sizeof(uint32_t), c->stream));
   }
   HIP_TRY(kh::launch_select_split(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, c->sel_g, c->d_selpart,
-                                  c->d_selcnt, out, done, c->stream));
+                                  c->d_selcnt, out, sync, res_wait, c->stream));
   return 0;
 }
 
@@ -773,7 +773,7 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
       e = fail(KOORDHIP_EDEVICE, "eval_full launch");
       break;
     }
-    if (topk) e = topk_batch(c, dp, np, k, 0, n, dk, false, nullptr);
+    if (topk) e = topk_batch(c, dp, np, k, 0, n, dk, false, nullptr, 0);
     if (e) break;
     if (hipStreamSynchronize(c->stream) != hipSuccess) {
       e = fail(KOORDHIP_EDEVICE, "eval sync");
@@ -942,6 +942,10 @@ int place_staged_impl(koordhip_ctx *c) {
   // per round; the lists are then one round fresher than in the pipeline,
   // which the resolve treats exactly like refreshed entries.
   const bool serial = std::getenv("KOORDHIP_SERIAL") != nullptr;
+  // KOORDHIP_FOLD_WAIT: the split select's merging workgroups hold the stream
+  // until the resolve is far enough instead of a k_wait_resolved launch
+  // (measured 2-3 % slower: their spinning delays the launch's end)
+  const bool wait_kernel = std::getenv("KOORDHIP_FOLD_WAIT") == nullptr;
   hipStream_t rs = serial ? c->stream : c->rstream;
   const bool persistent = !serial && !c->group && !std::getenv("KOORDHIP_ROUND_LAUNCH");
   const char *trace_env = std::getenv("KOORDHIP_TRACE_POD");  // diagnostics: printf one pod's resolve step
@@ -956,16 +960,19 @@ int place_staged_impl(koordhip_ctx *c) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
     const kh::DevPod *pods = c->d_pods + p0;
     uint64_t *lists = c->d_lists + (size_t)(r & 1) * list_buf;
-    if (r >= 2 && !serial) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, c->stream));
+    const bool select_waits = c->sel_split && c->world == 1 && !wait_kernel;  // the previous select held the stream
+    if (r >= 2 && !serial && !select_waits) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, c->stream));
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, nullptr)) return e;
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, nullptr, 0)) return e;
       if (int e = exchange(c, lists, (size_t)P * K)) return e;
       HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits,
                                     c->d_final + (size_t)(r & 1) * list_buf, c->stream));
     } else {
       // the split select's merging workgroups count the round's pods into sync->sel_round themselves
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, c->sel_split ? kh::pipe_list_counter(sync) : nullptr)) return e;
+      // and hold the stream until round r - 1 is resolved (what the next scan needs)
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, c->sel_split ? sync : nullptr, wait_kernel ? 0 : r))
+        return e;
     }
     if (c->world > 1 || !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, p0 + np, c->stream));
     if (!persistent) {

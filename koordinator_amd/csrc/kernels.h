@@ -33,15 +33,18 @@ hipError_t launch_select(const uint16_t *S, int64_t s_stride, int32_t lo, int32_
 // k_select_split: the same top-k with G workgroups per pod (row slices) and an
 // in-launch merge by each pod's last workgroup.  part: [n_pods][G][k] slice
 // lists (kSelPartKeys keys); cnt: kSelMaxPods arrival counters, zero before
-// the first launch (the kernel leaves them zero); done: optional, += 1 per pod
-// once its final list in `out` is published (PipeSync.sel_round).
+// the first launch (the kernel leaves them zero); sync: optional, sel_round
+// += 1 per pod once its final list in `out` is published, and with res_wait >
+// 0 the launch does not end before res_round >= res_wait.
+struct PipeSync;
 constexpr int kSelGMax = 16;
 constexpr int kSelMaxPods = 64;
 constexpr size_t kSelPartKeys = (size_t)kSelMaxPods * kSelGMax * 128;
 int32_t select_split_groups(int32_t m, int32_t G);
 hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,
                                int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, int32_t G,
-                               uint64_t *part, uint32_t *cnt, uint64_t *out, int32_t *done, hipStream_t s);
+                               uint64_t *part, uint32_t *cnt, uint64_t *out, PipeSync *sync, int32_t res_wait,
+                               hipStream_t s);
 // lists: ranges ascending with l, equal-score keys in ascending node order
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
                              int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s);
@@ -53,8 +56,6 @@ hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, h
 // publishes res_round in `sync`; M' is handed between launches in mbuf
 // ({count, nodes}).  The evaluation stream brackets each round with
 // k_wait_resolved (before k_scan) and k_signal_lists (after the lists).
-struct PipeSync;
-int32_t *pipe_list_counter(PipeSync *sync);  // &sync->sel_round (k_select_split's `done`)
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,

@@ -717,6 +717,55 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
 }
 
 // ---------------------------------------------------------------------------
+// Device-side handshake between the evaluation stream and the persistent
+// resolve kernel (one per koordhip_place_staged call):
+//   sel_round  pods of the stream whose final lists are ready (k_select_split's
+//              merging workgroups add 1 each; k_signal_lists stores the count
+//              after a separate merge)
+//   res_round  rounds resolved + written back (k_resolve, release store)
+//   err        a side gave up waiting (watchdog): the call fails, nothing hangs
+struct PipeSync {
+  int32_t sel_round, res_round, err, pad;
+};
+
+constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up
+
+__device__ __forceinline__ int32_t load_acquire(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t load_relaxed(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Publish a flag after this wave's global stores (MI355X_MICROARCH.md
+// cross-XCD hand-off: wait for the stores, write the XCD L2 back, wait for
+// the write-back -- spelled out in asm because ROCm 7.2 can drop the wait
+// after buffer_wbl2 -- then a relaxed agent-scope flag store).
+__device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Spin (one thread) until *p >= v; false when the watchdog fires or the other
+// side reported an error.  Relaxed polls, ONE agent acquire after the match
+// (an acquire per poll costs 2-3x per hop, Guideline 16 Pitfall 5).
+__device__ bool wait_at_least(const int32_t *p, int32_t v, PipeSync *sy) {
+  const uint64_t t0 = stamp();
+  while (load_relaxed(p) < v) {
+    if (load_relaxed(&sy->err)) return false;
+    if (stamp() - t0 > PIPE_WATCHDOG) {
+      store_release(&sy->err, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return true;
+}
+
+// ---------------------------------------------------------------------------
 // k_select_split: the same exact top-k with G workgroups per pod.
 //
 // One workgroup per pod (k_select) keeps 32 of 256 CUs busy at the default
@@ -760,7 +809,8 @@ constexpr int32_t SPL_HDR = (int32_t)((sizeof(SplHdr) + 15) & ~(size_t)15);
 __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
     const uint16_t *__restrict__ S, int64_t s_stride, int32_t lo, int32_t m, int32_t k, int32_t nbins,
     const uint16_t *__restrict__ Mx, int32_t m_stride, int32_t nchunks, int32_t G, int32_t tiles_per,
-    uint64_t *__restrict__ part, uint32_t *__restrict__ cnt, uint64_t *__restrict__ out, int32_t *__restrict__ done) {
+    uint64_t *__restrict__ part, uint32_t *__restrict__ cnt, uint64_t *__restrict__ out, PipeSync *__restrict__ sy,
+    int32_t res_wait) {
   extern __shared__ __attribute__((aligned(16))) char spl_lds[];
   SplHdr &h = *reinterpret_cast<SplHdr *>(spl_lds);
   uint64_t *mk = reinterpret_cast<uint64_t *>(spl_lds + SPL_HDR);                    // merge: G x k keys
@@ -951,13 +1001,17 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
     if (pos < k) o[pos] = x;
   }
   for (int32_t j = mgt + min(mneed, h.nties) + t; j < k; j += SPL_THREADS) o[j] = 0;
-  if (done) {
+  if (sy) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&sy->sel_round, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the next scan on this stream may read the node columns only once the
+      // resolve has written back round res_wait - 1: the launch ends no earlier
+      // (replaces a k_wait_resolved launch between this kernel and the scan)
+      if (res_wait > 0) (void)wait_at_least(&sy->res_round, res_wait, sy);
     }
   }
 }
@@ -1109,56 +1163,6 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
 }
 
 __device__ __forceinline__ uint32_t res_hash(int32_t node) { return ((uint32_t)node * 2654435761u) >> 24; }
-
-// Device-side handshake between the evaluation stream and the persistent
-// resolve kernel (one per koordhip_place_staged call):
-//   sel_round  pods of the stream whose final lists are ready (k_select_split's
-//              merging workgroups add 1 each; k_signal_lists stores the count
-//              after a separate merge)
-//   res_round  rounds resolved + written back (k_resolve, release store)
-//   err        a side gave up waiting (watchdog): the call fails, nothing hangs
-struct PipeSync {
-  int32_t sel_round, res_round, err, pad;
-};
-
-int32_t *pipe_list_counter(PipeSync *sync) { return &sync->sel_round; }
-
-constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up
-
-__device__ __forceinline__ int32_t load_acquire(const int32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int32_t load_relaxed(const int32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Publish a flag after this wave's global stores (MI355X_MICROARCH.md
-// cross-XCD hand-off: wait for the stores, write the XCD L2 back, wait for
-// the write-back -- spelled out in asm because ROCm 7.2 can drop the wait
-// after buffer_wbl2 -- then a relaxed agent-scope flag store).
-__device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Spin (one thread) until *p >= v; false when the watchdog fires or the other
-// side reported an error.  Relaxed polls, ONE agent acquire after the match
-// (an acquire per poll costs 2-3x per hop, Guideline 16 Pitfall 5).
-__device__ bool wait_at_least(const int32_t *p, int32_t v, PipeSync *sy) {
-  const uint64_t t0 = stamp();
-  while (load_relaxed(p) < v) {
-    if (load_relaxed(&sy->err)) return false;
-    if (stamp() - t0 > PIPE_WATCHDOG) {
-      store_release(&sy->err, 1);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  return true;
-}
 
 // Evaluation stream, before k_scan of round r: rounds < r - 1 must be written back.
 __global__ void k_wait_resolved(PipeSync *sy, int32_t rounds) {
@@ -1909,7 +1913,8 @@ int32_t select_split_groups(int32_t m, int32_t G) {
 
 hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,
                                int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, int32_t G,
-                               uint64_t *part, uint32_t *cnt, uint64_t *out, int32_t *done, hipStream_t s) {
+                               uint64_t *part, uint32_t *cnt, uint64_t *out, PipeSync *sync, int32_t res_wait,
+                               hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   if (k < 1 || k > RES_MAXP || nbins < 2 || nbins > 32768 || n_pods > kSelMaxPods) return hipErrorInvalidValue;
   const int32_t ntiles = std::max<int32_t>(1, (m + SPL_TILE - 1) / SPL_TILE);
@@ -1928,7 +1933,7 @@ hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, 
     attr = true;
   }
   hipLaunchKernelGGL(k_select_split, dim3(G, n_pods), dim3(SPL_THREADS), lds, s, S, s_stride, lo, m, k, nbins, Mx,
-                     m_stride, nchunks, G, per, part, cnt, out, done);
+                     m_stride, nchunks, G, per, part, cnt, out, sync, res_wait);
   return hipGetLastError();
 }
 
