@@ -448,7 +448,6 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
   }
   if (c->numa && c->partial_r > 4) c->partial_r = 4;  // the NUMA scan kernel is built for R <= 4
-  if (const char *g = std::getenv("KOORDHIP_SEL_G")) c->sel_g = std::max(1, std::min(kh::kSelGMax, std::atoi(g)));
   // the split select shortens the evaluation stream (and drops the signal
   // kernel); KOORDHIP_SELECT_ONEWG restores one workgroup per pod for A/B runs
   c->sel_split = std::getenv("KOORDHIP_SELECT_ONEWG") == nullptr;
@@ -471,6 +470,16 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   }
   c->device = dev;
   hipError_t e = hipSetDevice(dev);
+  {
+    // split select: one workgroup per CU over a round (G x batch ~ CUs).  More
+    // groups queue behind the persistent resolve workgroup's CU and lengthen
+    // the evaluation stream (config 4 sweep: G=8 748k, G=16 718k pods/s at 32 pods)
+    int cus = 256;
+    if (e == hipSuccess && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0))
+      cus = 256;
+    c->sel_g = std::max(1, std::min(kh::kSelGMax, cus / c->batch));
+    if (const char *g = std::getenv("KOORDHIP_SEL_G")) c->sel_g = std::max(1, std::min(kh::kSelGMax, std::atoi(g)));
+  }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->t0);
   if (e == hipSuccess) e = hipEventCreate(&c->t1);
