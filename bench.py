@@ -209,7 +209,7 @@ def main():
                                 if numa else
                                 f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
                                 "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile"),
-                   "nodes": args.nodes, "pods": args.pods, "batch_pods": eng.cfg.batch_pods or 32,
+                   "nodes": args.nodes, "pods": args.pods, "batch_pods": eng.cfg.batch_pods or (16 if args.workload == "config3" else 32),
                    "parallelism": f"node-shard x{world}"},
         "unschedulable": int((placements < 0).sum()),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,

@@ -141,7 +141,7 @@ typedef struct koordhip_config {
   int64_t la_weight_cpu;                    /* LoadAwareSchedulingArgs.ResourceWeights[cpu] (1..100) */
   int64_t la_weight_mem;                    /* LoadAwareSchedulingArgs.ResourceWeights[memory] (1..100) */
   int32_t la_score_according_prod_usage;    /* LoadAwareSchedulingArgs.ScoreAccordingProdUsage */
-  int32_t batch_pods;       /* pods per speculative round of place_stream (0 = default 64; max 64) */
+  int32_t batch_pods;       /* pods per pipelined round of place_stream (0 = default: 32, 16 with NodeNUMAResource; max 64) */
   int32_t numa_weight_cpu;  /* NodeNUMAResourceArgs.ScoringStrategy LeastAllocated weights */
   int32_t numa_weight_mem;
   int32_t profile_kernels;  /* 1 = time every stream eval launch with HIP events (koordhip_last_stats) */
