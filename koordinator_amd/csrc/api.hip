@@ -112,6 +112,8 @@ struct koordhip_ctx {
   uint64_t *d_selpart = nullptr;  // k_select_split slice lists ([pods][G][k])
   uint32_t *d_selcnt = nullptr;   // k_select_split arrival counters (zero between launches)
   int32_t sel_g = kh::kSelGMax;   // workgroups per pod of k_select_split (KOORDHIP_SEL_G)
+  int32_t n_cu = 256;             // device CU count
+  bool cu_reserve = false;        // KOORDHIP_CU_RESERVE: CU-masked streams, CU 0 for the resolve
   bool sel_split = true;          // k_select_split; false (KOORDHIP_SELECT_ONEWG): k_select + signal kernel
   size_t partial_cap = 0;
   uint64_t *d_lists = nullptr;   // [2][batch][k] (rank-local lists; double buffer: round parity)
@@ -482,10 +484,21 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     int cus = 256;
     if (e == hipSuccess && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0))
       cus = 256;
+    c->n_cu = cus;
     c->sel_g = std::max(1, std::min(kh::kSelGMax, cus / c->batch));
     if (const char *g = std::getenv("KOORDHIP_SEL_G")) c->sel_g = std::max(1, std::min(kh::kSelGMax, std::atoi(g)));
   }
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  c->cu_reserve = std::getenv("KOORDHIP_CU_RESERVE") != nullptr;
+  if (c->cu_reserve && e == hipSuccess) {
+    // the persistent resolve gets CU 0 to itself: the evaluation stream runs on
+    // every other CU (its workgroups no longer share the resolve wave's CU)
+    std::vector<uint32_t> m((size_t)(c->n_cu + 31) / 32, 0xffffffffu);
+    m[0] &= ~1u;
+    if (c->n_cu % 32) m.back() &= (1u << (c->n_cu % 32)) - 1u;
+    e = hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)m.size(), m.data());
+  } else if (e == hipSuccess) {
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  }
   if (e == hipSuccess) e = hipEventCreate(&c->t0);
   if (e == hipSuccess) e = hipEventCreate(&c->t1);
   if (e == hipSuccess) e = hipMalloc(&c->d_tmp_pod, sizeof(kh::DevPod));
@@ -910,7 +923,12 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipMalloc(&c->d_final, 2 * lbytes));
     HIP_TRY(hipMalloc(&c->d_mod, (1 + kMaxBatch) * sizeof(int32_t) + kh::kPipeSyncBytes));
     HIP_TRY(hipMalloc(&c->d_desc, sizeof(kh::DevNodes)));
-    HIP_TRY(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+    if (c->cu_reserve) {
+      const uint32_t m0 = 1u;
+      HIP_TRY(hipExtStreamCreateWithCUMask(&c->rstream, 1, &m0));
+    } else {
+      HIP_TRY(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+    }
     for (int i = 0; i < kRing; i++) HIP_TRY(hipEventCreateWithFlags(&c->ev_res[i], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
   }
