@@ -127,7 +127,11 @@ struct koordhip_ctx {
   hipStream_t rstream = nullptr;  // resolve stream (the eval kernels use `stream`)
   hipEvent_t ev_res[kRing] = {}, ev_start = nullptr;
   bool pipe_check = false;       // a place call ran: check PipeSync.err when it completes
+  bool pipe_err = false;         // ... and it had stalled (sticky until the next place call)
   kh::DevPod *d_tmp_pod = nullptr;
+  void *d_upd = nullptr;           // koordhip_update_nodes staging (grown, kept)
+  size_t upd_cap = 0;
+  std::vector<uint8_t> upd_host;   // its host image
   uint64_t *d_dbg = nullptr;  // KOORDHIP_STAMPS diagnostic counters (resolve segments)
 
   // checkpoint of the mutable columns
@@ -521,7 +525,7 @@ int koordhip_destroy(koordhip_ctx *c) {
   for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
                   (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
                   (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc,
-                  (void *)c->d_selpart, (void *)c->d_selcnt})
+                  (void *)c->d_selpart, (void *)c->d_selcnt, c->d_upd})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -630,92 +634,119 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   if (m <= 0) return 0;
   if (int e = validate_soa(rows)) return e;
-  for (int32_t j = 0; j < m; j++)
-    if (idx[j] < 0 || idx[j] >= c->n) return fail(KOORDHIP_EINVAL, "row index out of range");
-  HIP_TRY(hipSetDevice(c->device));
-  int32_t *d_idx = nullptr;
-  void *stage = nullptr;
-  HIP_TRY(hipMalloc(&d_idx, m * sizeof(int32_t)));
-  HIP_TRY(hipMalloc(&stage, (size_t)m * sizeof(int64_t)));
-  int e = 0;
-  auto put64 = [&](int64_t *dst, const int64_t *src) {
-    if (e) return;
-    e = upload(c, (int64_t *)stage, src, m);
-    if (!e && kh::launch_scatter<int64_t>(dst, (const int64_t *)stage, d_idx, m, c->stream) != hipSuccess)
-      e = fail(KOORDHIP_EDEVICE, "scatter");
-    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
+  // ---- validate everything before the first device write: a rejected call
+  //      leaves the snapshot untouched
+  {
+    std::vector<int32_t> sorted(idx, idx + m);
+    std::sort(sorted.begin(), sorted.end());
+    if (sorted.front() < 0 || sorted.back() >= c->n) return fail(KOORDHIP_EINVAL, "row index out of range");
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+      return fail(KOORDHIP_EINVAL, "duplicate row index (a row would mix fields of two updates)");
+  }
+  const bool numa_rows = c->numa && rows->numa_class;
+  if (numa_rows) {
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
+      if (!rows->numa_free[w] || !rows->numa_excl_pcpu[w] || !rows->numa_excl_numa[w])
+        return fail(KOORDHIP_EINVAL, "NUMA mask column missing");
+    if (!rows->numa_alloc_cnt || !rows->numa_flags) return fail(KOORDHIP_EINVAL, "NUMA column missing");
+    for (int32_t j = 0; j < m; j++)
+      if (rows->numa_class[j] >= c->n_classes)
+        return fail(KOORDHIP_EINVAL, "numa_class index out of range (classes are fixed at load_snapshot)");
+  }
+  // ---- one host staging image: [idx][column 0][column 1]..., 8-B aligned
+  //      segments, quantities converted to the device's exact f64
+  struct Col {
+    void *dst;
+    const void *src;
+    int32_t esize;  // 8, 4 or 1
+    bool q;         // int64 quantity -> f64
+    const char *what;
   };
-  auto putq = [&](double *dst, const int64_t *src, const char *what) {
-    if (e) return;
-    e = upload_q(c, (double *)stage, src, m, what);
-    if (!e && kh::launch_scatter<int64_t>((int64_t *)dst, (const int64_t *)stage, d_idx, m, c->stream) != hipSuccess)
-      e = fail(KOORDHIP_EDEVICE, "scatter");
-    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
-  };
-  auto put32 = [&](int32_t *dst, const int32_t *src) {
-    if (e) return;
-    e = upload(c, (int32_t *)stage, src, m);
-    if (!e && kh::launch_scatter<int32_t>(dst, (const int32_t *)stage, d_idx, m, c->stream) != hipSuccess)
-      e = fail(KOORDHIP_EDEVICE, "scatter");
-    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
-  };
-  auto put8 = [&](uint8_t *dst, const uint8_t *src) {
-    if (e) return;
-    e = upload(c, (uint8_t *)stage, src, m);
-    if (!e && kh::launch_scatter<uint8_t>(dst, (const uint8_t *)stage, d_idx, m, c->stream) != hipSuccess)
-      e = fail(KOORDHIP_EDEVICE, "scatter");
-    if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
-  };
-  e = upload(c, d_idx, idx, m);
   kh::DevNodes &d = c->d;
   kh::PrepIn &pi = c->prep;
+  std::vector<Col> cols;
   for (int r = 0; r < KOORDHIP_NRES; r++) {
-    putq(const_cast<double *>(d.alloc[r]), rows->alloc[r], "alloc");
-    putq(d.requested[r], rows->requested[r], "requested");
+    cols.push_back({const_cast<double *>(d.alloc[r]), rows->alloc[r], 8, true, "alloc"});
+    cols.push_back({d.requested[r], rows->requested[r], 8, true, "requested"});
   }
-  put32(const_cast<int32_t *>(d.alloc_pods), rows->alloc_pods);
-  put32(d.npods, rows->npods);
-  putq(d.nz_cpu, rows->nz_cpu_m, "nz_cpu_m");
-  putq(d.nz_mem, rows->nz_mem, "nz_mem");
-  putq(const_cast<double *>(d.la_alloc_cpu), rows->la_alloc_cpu_m, "la_alloc_cpu_m");
-  putq(const_cast<double *>(d.la_alloc_mem), rows->la_alloc_mem, "la_alloc_mem");
-  putq(d.la_used_cpu, rows->la_used_cpu_m, "la_used_cpu_m");
-  putq(d.la_used_mem, rows->la_used_mem, "la_used_mem");
-  putq(d.la_used_prod_cpu, rows->la_used_prod_cpu_m, "la_used_prod_cpu_m");
-  putq(d.la_used_prod_mem, rows->la_used_prod_mem, "la_used_prod_mem");
+  cols.push_back({const_cast<int32_t *>(d.alloc_pods), rows->alloc_pods, 4, false, "alloc_pods"});
+  cols.push_back({d.npods, rows->npods, 4, false, "npods"});
+  cols.push_back({d.nz_cpu, rows->nz_cpu_m, 8, true, "nz_cpu_m"});
+  cols.push_back({d.nz_mem, rows->nz_mem, 8, true, "nz_mem"});
+  cols.push_back({const_cast<double *>(d.la_alloc_cpu), rows->la_alloc_cpu_m, 8, true, "la_alloc_cpu_m"});
+  cols.push_back({const_cast<double *>(d.la_alloc_mem), rows->la_alloc_mem, 8, true, "la_alloc_mem"});
+  cols.push_back({d.la_used_cpu, rows->la_used_cpu_m, 8, true, "la_used_cpu_m"});
+  cols.push_back({d.la_used_mem, rows->la_used_mem, 8, true, "la_used_mem"});
+  cols.push_back({d.la_used_prod_cpu, rows->la_used_prod_cpu_m, 8, true, "la_used_prod_cpu_m"});
+  cols.push_back({d.la_used_prod_mem, rows->la_used_prod_mem, 8, true, "la_used_prod_mem"});
   for (int r = 0; r < 2; r++) {
-    put64(const_cast<int64_t *>(pi.used_m[r]), rows->laf_used_m[r]);
-    put64(const_cast<int64_t *>(pi.total_m[r]), rows->laf_total_m[r]);
-    put64(const_cast<int64_t *>(pi.prod_used_m[r]), rows->laf_prod_used_m[r]);
-    put64(const_cast<int64_t *>(pi.thr[r]), rows->laf_thr[r]);
-    put64(const_cast<int64_t *>(pi.prod_thr[r]), rows->laf_prod_thr[r]);
+    cols.push_back({const_cast<int64_t *>(pi.used_m[r]), rows->laf_used_m[r], 8, false, "laf_used_m"});
+    cols.push_back({const_cast<int64_t *>(pi.total_m[r]), rows->laf_total_m[r], 8, false, "laf_total_m"});
+    cols.push_back({const_cast<int64_t *>(pi.prod_used_m[r]), rows->laf_prod_used_m[r], 8, false, "laf_prod_used_m"});
+    cols.push_back({const_cast<int64_t *>(pi.thr[r]), rows->laf_thr[r], 8, false, "laf_thr"});
+    cols.push_back({const_cast<int64_t *>(pi.prod_thr[r]), rows->laf_prod_thr[r], 8, false, "laf_prod_thr"});
   }
-  put8(const_cast<uint8_t *>(pi.la_flags), rows->la_flags);
-  if (!e && c->numa && rows->numa_class) {
-    for (int32_t j = 0; j < m && !e; j++)
-      if (rows->numa_class[j] >= 0 && c->n_classes >= 0 && rows->numa_class[j] >= c->n_classes)
-        e = fail(KOORDHIP_EINVAL, "numa_class index out of range (classes are fixed at load_snapshot)");
+  cols.push_back({const_cast<uint8_t *>(pi.la_flags), rows->la_flags, 1, false, "la_flags"});
+  if (numa_rows) {
     kh::DevNuma &nu = c->d.nu;
-    put32(const_cast<int32_t *>(nu.node_cls), rows->numa_class);
-    put32(nu.cnt, rows->numa_alloc_cnt);
-    put8(const_cast<uint8_t *>(nu.nflags), rows->numa_flags);
+    cols.push_back({const_cast<int32_t *>(nu.node_cls), rows->numa_class, 4, false, "numa_class"});
+    cols.push_back({nu.cnt, rows->numa_alloc_cnt, 4, false, "numa_alloc_cnt"});
+    cols.push_back({const_cast<uint8_t *>(nu.nflags), rows->numa_flags, 1, false, "numa_flags"});
     for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
-      put64((int64_t *)nu.fr[w], (const int64_t *)rows->numa_free[w]);
-      put64((int64_t *)nu.ep[w], (const int64_t *)rows->numa_excl_pcpu[w]);
-      put64((int64_t *)nu.en[w], (const int64_t *)rows->numa_excl_numa[w]);
+      cols.push_back({nu.fr[w], rows->numa_free[w], 8, false, "numa_free"});
+      cols.push_back({nu.ep[w], rows->numa_excl_pcpu[w], 8, false, "numa_excl_pcpu"});
+      cols.push_back({nu.en[w], rows->numa_excl_numa[w], 8, false, "numa_excl_numa"});
     }
   }
-  if (!e && c->dc.la_alias) {
-    for (int32_t j = 0; j < m && c->dc.la_alias; j++)
-      if (rows->la_alloc_cpu_m[j] != rows->alloc[KOORDHIP_RES_CPU][j] ||
-          rows->la_alloc_mem[j] != rows->alloc[KOORDHIP_RES_MEM][j])
-        c->dc.la_alias = 0;
+  const size_t seg_idx = ((size_t)m * 4 + 7) & ~(size_t)7;
+  size_t bytes = seg_idx;
+  std::vector<size_t> off(cols.size());
+  for (size_t q = 0; q < cols.size(); q++) {
+    off[q] = bytes;
+    bytes += ((size_t)m * cols[q].esize + 7) & ~(size_t)7;
   }
-  if (!e && kh::launch_prep_flags(pi, d, d_idx, m, c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "prep");
-  if (!e && hipStreamSynchronize(c->stream) != hipSuccess) e = fail(KOORDHIP_EDEVICE, "sync");
-  (void)hipFree(d_idx);
-  (void)hipFree(stage);
-  return e;
+  std::vector<uint8_t> &img = c->upd_host;
+  img.assign(bytes, 0);
+  std::memcpy(img.data(), idx, (size_t)m * 4);
+  for (size_t q = 0; q < cols.size(); q++) {
+    const Col &k = cols[q];
+    if (k.q) {
+      const int64_t *src = static_cast<const int64_t *>(k.src);
+      double *o = reinterpret_cast<double *>(img.data() + off[q]);
+      for (int32_t j = 0; j < m; j++) {
+        if (!exact_ok(src[j]))
+          return fail(KOORDHIP_EINVAL, std::string(k.what) + ": quantity magnitude >= 2^45 is outside the engine's exact range");
+        o[j] = (double)src[j];
+      }
+    } else {
+      std::memcpy(img.data() + off[q], k.src, (size_t)m * k.esize);
+    }
+  }
+  bool alias = c->dc.la_alias;
+  for (int32_t j = 0; j < m && alias; j++)
+    if (rows->la_alloc_cpu_m[j] != rows->alloc[KOORDHIP_RES_CPU][j] || rows->la_alloc_mem[j] != rows->alloc[KOORDHIP_RES_MEM][j])
+      alias = false;
+  // ---- device: one upload into the persistent staging buffer, the scatters,
+  //      the flag recompute, one synchronisation
+  HIP_TRY(hipSetDevice(c->device));
+  if (int e = ensure(c, &c->d_upd, &c->upd_cap, bytes)) return e;
+  uint8_t *dev = static_cast<uint8_t *>(c->d_upd);
+  const int32_t *d_idx = reinterpret_cast<const int32_t *>(dev);
+  HIP_TRY(hipMemcpyAsync(dev, img.data(), bytes, hipMemcpyHostToDevice, c->stream));
+  for (size_t q = 0; q < cols.size(); q++) {
+    const Col &k = cols[q];
+    const void *src = dev + off[q];
+    if (k.esize == 8)
+      HIP_TRY(kh::launch_scatter<int64_t>(static_cast<int64_t *>(k.dst), static_cast<const int64_t *>(src), d_idx, m, c->stream));
+    else if (k.esize == 4)
+      HIP_TRY(kh::launch_scatter<int32_t>(static_cast<int32_t *>(k.dst), static_cast<const int32_t *>(src), d_idx, m, c->stream));
+    else
+      HIP_TRY(kh::launch_scatter<uint8_t>(static_cast<uint8_t *>(k.dst), static_cast<const uint8_t *>(src), d_idx, m, c->stream));
+  }
+  c->dc.la_alias = alias ? 1 : 0;
+  HIP_TRY(kh::launch_prep_flags(pi, d, d_idx, m, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));  // the host image may be reused by the next call
+  return 0;
 }
 
 int koordhip_read_nodes(koordhip_ctx *c, int64_t *requested, int64_t *nz, int32_t *npods, int64_t *la_used,
@@ -915,6 +946,8 @@ namespace {
 
 int place_staged_impl(koordhip_ctx *c) {
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  c->pipe_err = false;
+  c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
   const int32_t P = c->batch, K = 2 * c->batch;  // lag-1 needs k >= 2 x round size
   const size_t lbytes = (size_t)kMaxBatch * 2 * kMaxBatch * sizeof(uint64_t);
@@ -1044,14 +1077,21 @@ int place_staged_impl(koordhip_ctx *c) {
   return 0;
 }
 
-// After a place call: did either side of the pipeline give up waiting?
+// After a place call: did either side of the pipeline give up waiting?  The
+// error is sticky until the next place call: every later fetch / stats call
+// of this stream reports it.
 int pipe_status(koordhip_ctx *c) {
+  static const char *kStall = "round pipeline stalled (watchdog): placements are incomplete";
+  if (c->pipe_err) return fail(KOORDHIP_EDEVICE, kStall);
   if (!c->pipe_check || !c->d_mod) return 0;
   c->pipe_check = false;
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
   int32_t err = 0;
   HIP_TRY(hipMemcpy(&err, reinterpret_cast<int32_t *>(sync) + 2, sizeof(err), hipMemcpyDeviceToHost));
-  if (err) return fail(KOORDHIP_EDEVICE, "round pipeline stalled (watchdog): placements are incomplete");
+  if (err) {
+    c->pipe_err = true;
+    return fail(KOORDHIP_EDEVICE, kStall);
+  }
   return 0;
 }
 
@@ -1081,6 +1121,7 @@ int koordhip_fetch_cpusets(koordhip_ctx *c, uint64_t *cpus, int32_t n_pods) {
   if (n_pods > c->n_staged) return fail(KOORDHIP_EINVAL, "n_pods exceeds the staged stream");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int e = pipe_status(c)) return e;
   const size_t b = (size_t)n_pods * KOORDHIP_NUMA_WORDS * sizeof(uint64_t);
   if (!c->d_cpus) {
     if (b) std::memset(cpus, 0, b);
@@ -1184,6 +1225,7 @@ int koordhip_last_stats(koordhip_ctx *c, double *eval_ms, int64_t *eval_launches
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int e = pipe_status(c)) return e;
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, c->t0, c->t1));
   double em = 0;

@@ -396,6 +396,25 @@ __device__ __attribute__((noinline)) void acc_fallback_pass(const DevNumaClass &
   }
 }
 
+// The len-only socket sorts (cpu_accumulator.go:142-144, 161-163) with go 1.18's
+// sort.Slice for <= 12 elements (go.mod:3; zsortfunc.go quickSort_func): one
+// shell pass with gap 6, then an insertion sort.  The gap pass is not stable:
+// 7-8 tied sockets come out in Go's order, not in a stable sort's.
+__device__ __forceinline__ void go118_sort_by_count(int *ord, int *cnt, int n, bool desc) {
+  auto less = [&](int x, int y) { return desc ? cnt[x] > cnt[y] : cnt[x] < cnt[y]; };
+  auto swp = [&](int x, int y) {
+    const int to = ord[x], tc = cnt[x];
+    ord[x] = ord[y];
+    cnt[x] = cnt[y];
+    ord[y] = to;
+    cnt[y] = tc;
+  };
+  for (int i = 6; i < n; i++)
+    if (less(i, i - 6)) swp(i, i - 6);
+  for (int i = 1; i < n; i++)
+    for (int j = i; j > 0 && less(j, j - 1); j--) swp(j, j - 1);
+}
+
 // takeCPUs; returns true with a.R filled.
 __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
   if (a.need < 1) return true;
@@ -468,14 +487,7 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
       ord[j] = s;
       cnt[j] = c;
     }
-    for (int i = 1; i < no; i++)  // stable: count desc
-      for (int j = i; j > 0 && cnt[j] > cnt[j - 1]; j--) {
-        const int to = ord[j], tc = cnt[j];
-        ord[j] = ord[j - 1];
-        cnt[j] = cnt[j - 1];
-        ord[j - 1] = to;
-        cnt[j - 1] = tc;
-      }
+    go118_sort_by_count(ord, cnt, no, true);  // count desc (go 1.18 sort.Slice)
     int uo[NMAX], uc[NMAX], nu = 0;
     for (int i = 0; i < no; i++) {
       if (a.need < cnt[i]) {
@@ -489,14 +501,7 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
       }
     }
     if (a.need >= cpc) {  // :159-176: deferred sockets by count asc, core by core
-      for (int i = 1; i < nu; i++)
-        for (int j = i; j > 0 && uc[j] < uc[j - 1]; j--) {
-          const int to = uo[j], tc = uc[j];
-          uo[j] = uo[j - 1];
-          uc[j] = uc[j - 1];
-          uo[j - 1] = to;
-          uc[j - 1] = tc;
-        }
+      go118_sort_by_count(uo, uc, nu, false);  // count asc (go 1.18 sort.Slice)
       for (int i = 0; i < nu; i++) {
         for (int w = 0; w < NW; w++) T[w] = FA[w] & C.sm[uo[i]][w];
         bool stop = false;

@@ -8,10 +8,12 @@
  *   - Allocate / allocateCPUSet / satisfiedRequiredCPUBindPolicy
  *     (resource_manager.go:142-164,244-326,442-463);
  *   - Filter / Score / Reserve (plugin.go:266-324,365-405, scoring.go:55-168).
- * Go's sort.Slice is not stable; the only comparators without a final id
- * tie-break are the two len-only socket sorts (cpu_accumulator.go:142-144,
- * 161-163), which run on <= 8 elements where Go's pdqsort is an insertion sort,
- * i.e. stable: every sort here is a stable insertion sort.
+ * Go's sort.Slice is not stable.  Every comparator but two ends in an id
+ * tie-break, so any correct sort gives Go's order; those are insertion sorts
+ * here.  The two len-only socket sorts (cpu_accumulator.go:142-144, 161-163)
+ * reproduce go 1.18's sort.Slice for <= 12 elements exactly (a gap-6 shell
+ * pass, then insertion sort: sort_groups_len), which differs from a stable
+ * sort when 7-8 sockets tie.
  * Pinned by the known-answer tables of cpu_accumulator_test.go (tests/golden/).
  */
 #include <stdlib.h>
@@ -352,23 +354,29 @@ static void free_cpus(const acc *a, int filter_excl, list *out) {
   }
 }
 
-/* stable sort of groups by list length (desc = 1 / asc = 0), :142-144 / :161-163 */
+/* sort.Slice of groups by list length (desc = 1 / asc = 0), :142-144 / :161-163.
+ * The reference builds with go 1.18 (go.mod:3), whose sort.Slice on n <= 12
+ * elements (zsortfunc.go quickSort_func) runs ONE shell pass with gap 6 --
+ * swap(i, i-6) when less(i, i-6), for i = 6 .. n-1 -- and then an insertion
+ * sort.  The gap pass is not stable: with 7-8 sockets of tied length it can
+ * reorder them, so it is reproduced here (and in numa.hpp) literally. */
+static void swap_groups(groups *g, int x, int y) {
+  list tl = g->l[x];
+  g->l[x] = g->l[y];
+  g->l[y] = tl;
+  int ti = g->id[x];
+  g->id[x] = g->id[y];
+  g->id[y] = ti;
+}
+static int len_less(const groups *g, int x, int y, int desc) {
+  return desc ? g->l[x].n > g->l[y].n : g->l[x].n < g->l[y].n;
+}
 static void sort_groups_len(groups *g, int desc) {
-  for (int i = 1; i < g->n; i++) {
-    int j = i;
-    while (j > 0) {
-      int lx = g->l[j].n, ly = g->l[j - 1].n;
-      int before = desc ? lx > ly : lx < ly;
-      if (!before) break;
-      list tl = g->l[j];
-      g->l[j] = g->l[j - 1];
-      g->l[j - 1] = tl;
-      int ti = g->id[j];
-      g->id[j] = g->id[j - 1];
-      g->id[j - 1] = ti;
-      j--;
-    }
-  }
+  if (g->n > 12) abort(); /* quickSort_func proper: never reached (<= 8 sockets) */
+  for (int i = 6; i < g->n; i++)
+    if (len_less(g, i, i - 6, desc)) swap_groups(g, i, i - 6);
+  for (int i = 1; i < g->n; i++)
+    for (int j = i; j > 0 && len_less(g, j, j - 1, desc); j--) swap_groups(g, j, j - 1);
 }
 
 /* takeCPUs, cpu_accumulator.go:87-232.  Returns 1 and fills a->result on success. */

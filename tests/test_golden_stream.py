@@ -1,0 +1,31 @@
+"""The committed config-4 golden placements (tests/golden/make_stream_golden.py)
+still describe this generator and this oracle: the synthetic inputs hash to
+the recorded digests, and a prefix of the stream re-run through the oracle
+reproduces the recorded placements."""
+import hashlib
+import os
+
+import numpy as np
+
+import oracle
+from koordinator_amd import synth
+from koordinator_amd.config import shipped_profile, to_c_config
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "stream_config4.npz")
+
+
+def _sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_golden_inputs_and_prefix():
+    g = np.load(GOLDEN)
+    prof = shipped_profile()
+    table, pods = synth.config_workload(4, prof)
+    want = dict(zip(g["input_keys"].tolist(), g["input_sha"].tolist()))
+    got = {c: _sha(table[c]) for c in table.cols}
+    got["__pods__"] = _sha(pods)
+    assert got == want
+    assert g["placements"].shape == (100000,) and (g["placements"] >= 0).all()
+    ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods[:300])
+    assert np.array_equal(ref, g["placements"][:300])

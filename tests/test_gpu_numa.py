@@ -231,3 +231,16 @@ def test_gpu_numa_score_kat(Engine, name, case):
         e.load_snapshot(table)
         got = e.eval(pod)["scores"][0, 2, 0]
     assert got == case["want"], case["source"]
+
+
+def test_gpu_accumulator_go118_socket_sort(Engine):
+    """The device replay reproduces go 1.18's unstable sort.Slice on 7 tied sockets."""
+    from test_numa_oracle import _seven_socket_case
+    topo, free, want = _seven_socket_case()
+    t = numa_table([topo], [topo.mask(free)], flags=abi.NODE_NUMA_MOST_ALLOCATED,
+                   alloc_cnt=topo.num_cpus - len(free))
+    prof = shipped_profile(numa=True)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got = e.commit(cpuset_pod(8)[0], 0)
+    assert topo.cpus(got) == want

@@ -77,3 +77,22 @@ def test_numa_score_kat(name, case):
     prof, table, pod = G.build_numa_score_case(case)
     got = oracle.Oracle(to_c_config(prof), table).eval(pod)["scores"][0, 2, 0]
     assert got == case["want"], case["source"]
+
+
+def _seven_socket_case():
+    """7 sockets x 1 node x 2 cores x 2 threads; sockets 0-5 have one free core
+    (2 CPUs), socket 6 both (4 CPUs); MostAllocated orders the sockets 0..5, 6
+    (fewest free first, id asc); need 8 FullPCPUs > CPUsPerSocket skips to the
+    whole-socket pass (cpu_accumulator.go:141-155), whose len-desc sort.Slice
+    in go 1.18 (go.mod:3) moves socket 0 to the END with its gap-6 shell pass:
+    Go takes sockets 6, 1, 2 where a stable sort would take 6, 0, 1."""
+    topo = reference_test_topology(7, 1, 2, 2)
+    free = [24, 25, 26, 27] + [c for s in range(6) for c in (4 * s, 4 * s + 1)]
+    return topo, free, [4, 5, 8, 9, 24, 25, 26, 27]
+
+
+def test_take_cpus_go118_unstable_socket_sort():
+    topo, free, want = _seven_socket_case()
+    got = oracle.take_cpus(topo.record, topo.mask(free), 8, abi.CPUBIND_FULL_PCPUS, abi.CPUEXCL_NONE, True)
+    assert got is not None
+    assert topo.cpus(got) == want
