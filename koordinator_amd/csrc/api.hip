@@ -971,7 +971,7 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * lbytes));
     c->gather_world = c->world;
   }
-  if (kh::resolve_lds_bytes(P, K, c->n, c->numa) > 159 * 1024)
+  if (kh::resolve_lds_bytes(P, K, c->n, c->numa) > 157 * 1024)
     return fail(KOORDHIP_EINVAL, "snapshot too large for the resolve kernel's LDS");
   if (c->group)
     if (int e = group_agree(c)) return e;
@@ -1064,14 +1064,14 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[8], (unsigned long long)h[9], (unsigned long long)h[10],
                  (unsigned long long)h[11], (unsigned long long)h[12], (unsigned long long)h[13]);
     std::fprintf(stderr,
-                 "[koordhip stamps] resolve cycles: prologue %llu  waiting for lists %llu  loop %llu  | re-evals %llu "
-                 "prefetch-misses %llu pods %llu | prologue: loads+hash %llu refresh+top %llu (refresh %llu) | release %llu\n",
-                 (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[4],
-                 (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7],
-                 (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[15], (unsigned long long)h[14]);
-    std::fprintf(stderr, "[koordhip stamps] resolve loop cycles: fast path %llu | general path: candidate %llu  re-eval %llu  "
-                 "commit %llu\n",
-                 (unsigned long long)h[17], (unsigned long long)h[16], (unsigned long long)h[18],
+                 "[koordhip stamps] resolve cycles: prologue walk %llu  hash %llu  waiting for lists %llu  loop %llu  "
+                 "release %llu | pods %llu  bulk commits %llu  staged pods %llu  general-path pods %llu  HBM row loads %llu\n",
+                 (unsigned long long)h[0], (unsigned long long)h[2], (unsigned long long)h[1], (unsigned long long)h[4],
+                 (unsigned long long)h[14], (unsigned long long)h[7], (unsigned long long)h[20],
+                 (unsigned long long)h[21], (unsigned long long)h[5], (unsigned long long)h[6]);
+    std::fprintf(stderr, "[koordhip stamps] resolve loop cycles: conflict detection %llu  bulk commits %llu | "
+                 "general path: candidate+keys %llu  commit %llu\n",
+                 (unsigned long long)h[16], (unsigned long long)h[17], (unsigned long long)h[18],
                  (unsigned long long)h[19]);
   }
   return 0;

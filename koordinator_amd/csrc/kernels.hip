@@ -1017,49 +1017,61 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
 }
 
 // ---------------------------------------------------------------------------
-// k_resolve: the sequential greedy over one round of n_pods <= 64 pods,
-// lag-1 pipelined with the evaluation of the next round.
+// k_resolve: the sequential greedy over the staged stream -- one persistent
+// workgroup, rounds of n_pods <= 64 pods, lag-1 pipelined with the evaluation
+// of the next round.
 //
-// The round's lists (k >= 2 * round size keys per pod, the exact top-k of the
-// scanned nodes) were built by k_scan/k_select WHILE the previous round's
-// resolve ran on another stream: they are exact for every node except M' =
-// the nodes that round committed to, whose columns k_scan may even have read
-// half-updated.  A Reserve only raises the columns a key depends on and every
-// enabled score is non-increasing in them (a "monotone" config), so such a
-// stale key is an upper bound of the node's current key.
+// Round r's lists (k >= 2 x round size keys per pod, best first: the exact
+// top-k of the scanned nodes) were computed by k_scan / k_select WHILE round
+// r-1 was resolved: they are exact for every node except M' = the nodes round
+// r-1 committed to, whose columns k_scan may have read half-updated.  A
+// Reserve only raises the columns a key depends on and every enabled score is
+// non-increasing in them (a "monotone" configuration), so such a stale key is
+// an upper bound of the node's current key.
 //
-// Prologue (all waves): lists, pod records, the rows of M' and of the list
-// heads -> LDS (+ an M' node -> slot hash); every list entry on an M' node is
-// re-evaluated on its current row (one wave per pod).  Every list key is now
-// exact at the start of the round, and a node outside a list scores <= its
-// k-th stale key.  Lists are not re-sorted: the loop takes maxima.
+// X = M' u M (M = the nodes committed in THIS round) is the set of nodes whose
+// list keys may be stale.  Pod l's winner is the best of
+//   c  = its first list entry outside X: exact, and it bounds every node
+//        outside X, listed or not (the list is sorted; |X| < k keeps a full
+//        list from running out of entries outside X);
+//   the current keys of the X nodes (M' rows and M rows are in LDS).
+// With monotone scores only the X entries ranked above c can beat c.
 //
-// Loop (wave 0, s_setprio 3): pod j's candidate is its best list entry not
-// in M = the nodes committed in THIS round (lane-owned rows in registers).
-// Since |M' u M| < k, a full list always has an entry outside M' u M, whose
-// key (exact) bounds every node outside the list, so the candidate beats
-// every node outside M.  A node of M can only win if its list key (an upper
-// bound of its current key) beats the candidate, and only then are M's rows
-// re-evaluated (one row per lane, wave max).  Pods whose
-// feasibility is not monotone (NodeNUMAResource required SpreadByPCPUs)
-// re-evaluate M and M' every time.  The winner's Reserve delta is applied to
-// its lane-owned row; rows of M are written back at the end and M is handed
-// to the next round as its M'.
+// Prologue (all waves, every pod at once): walk each list from the top while
+// its entries are M' nodes (evaluated on their current M' rows), up to the
+// first entry outside M' -- that walk is the pod's decision if no earlier pod
+// of the round commits to a node it walked (its "examined" set E).  The
+// winner's row is staged (list-head prefetch, M' row, or one HBM load).
+// Loop (wave 0, s_setprio 3): pod l takes its staged decision unless E meets
+// M (one LDS gather of E against the M bitmap + a ballot) or the pod is
+// non-monotone / a cpuset pod; those take the general path (c, then every M
+// and M' row evaluated, one row per lane).  The Reserve delta is applied lane
+// per row word.  M is written back at the end of the round and becomes the
+// next round's M'.
 
-// Wave 0 runs the sequential loop with a lot of state in registers (the M
-// rows, the staged candidate row, NUMA masks and the accumulator replay):
-// 8 waves (4 for NUMA builds) keep 256 (512) VGPRs available to it.
+// Wave 0 runs the sequential loop with a lot of state in registers: 8 waves
+// (4 for NUMA builds) keep 256 (512) VGPRs available to it.
 template <bool NUMA>
 constexpr int res_threads() { return NUMA ? 256 : 512; }
 
-// An NV row as 8-byte words (the lane-parallel Reserve in k_resolve): words
-// 0-4 a[], 5-9 r[], 10-11 nz, 12-13 la_a, 14-15 la_u, 16-17 la_up (f64),
-// 18 = a_pods | npods << 32, 19 = flags.
-constexpr int RES_WORDS = 20;
+constexpr int RES_PRE = 128;    // prefetched rows of list heads (RES_PRE / round size per pod)
+constexpr int RES_HASH = 256;   // node -> M' slot (open addressing)
+constexpr int RES_WE = 8;       // list entries the prologue walks per pod
+constexpr int RES_LDS_MAX = 160 * 1024 - 3 * 1024;  // dynamic LDS cap (static LDS: M' nodes, hashes, flags)
 
-// M / M' rows in LDS carry a stale over-commit part of `flags` (the deferred
-// Reserve in k_resolve only adds the deltas); every read of such a row for an
-// evaluation or a write-back goes through here.
+// An NV row as 8-byte words (the lane-parallel Reserve): words 0-4 a[], 5-9
+// r[], 10-11 nz, 12-13 la_a, 14-15 la_u, 16-17 la_up (f64), 18 = a_pods |
+// npods << 32, 19 = flags.
+constexpr int RES_WORDS = 20;
+static_assert(sizeof(NV) == RES_WORDS * 8, "NV row = 20 words");
+static_assert(offsetof(NV, r) == 40 && offsetof(NV, nz_cpu) == 80 && offsetof(NV, la_u_cpu) == 112 &&
+                  offsetof(NV, la_up_cpu) == 128 && offsetof(NV, a_pods) == 144 && offsetof(NV, npods) == 148 &&
+                  offsetof(NV, flags) == 152,
+              "NV word layout");
+
+// M rows carry a stale over-commit part of `flags` (the lane-wise Reserve
+// only adds the deltas): every read of such a row for an evaluation or a
+// write-back goes through here.
 __device__ __forceinline__ NV slot_row(const NV &src) {
   NV v = src;
   uint32_t f = v.flags & ~(uint32_t)(NF_OVER_CPU | NF_OVER_MEM | NF_OVER_EPH);
@@ -1069,30 +1081,10 @@ __device__ __forceinline__ NV slot_row(const NV &src) {
   v.flags = f;
   return v;
 }
-static_assert(sizeof(NV) == RES_WORDS * 8, "NV row = 20 words");
-static_assert(offsetof(NV, r) == 40 && offsetof(NV, nz_cpu) == 80 && offsetof(NV, la_u_cpu) == 112 &&
-                  offsetof(NV, la_up_cpu) == 128 && offsetof(NV, a_pods) == 144 && offsetof(NV, npods) == 148 &&
-                  offsetof(NV, flags) == 152,
-              "NV word layout");
-
-// A pod record read from LDS made wave-uniform (SGPRs): every lane read the
-// same record, readfirstlane tells the compiler so.
-__device__ __forceinline__ DevPod uniform_pod(const DevPod &src) {
-  DevPod p;
-  const uint32_t *s = reinterpret_cast<const uint32_t *>(&src);
-  uint32_t *o = reinterpret_cast<uint32_t *>(&p);
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(DevPod) / 4); i++) o[i] = __builtin_amdgcn_readfirstlane(s[i]);
-  return p;
-}
-constexpr int RES_PRE = 128;   // prefetched rows of list heads
-constexpr int RES_TOP = 8;     // ordered best keys per pod (the loop's fast path)
-constexpr int RES_HASH = 256;  // node -> M' slot (open addressing)
-constexpr int RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (static LDS: a few flags)
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
-      want, top, lcnt, hits, hmask, classes, modmap, total;
+      dec_key, dec_n, dec_src, dec_e, moved, mbits, classes, modmap, total;
   // second copies of the per-round inputs, filled by waves 1.. while wave 0
   // resolves the previous round (overlap = 0: every round loads serially)
   int32_t overlap, lists2, pods2, pre_rows2, pre_numa2, pre_node2;
@@ -1104,24 +1096,20 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
                                           bool overlap = false) {
   ResLds o;
   int32_t at = 0;
+  const int32_t bitmap = res_align(((n_nodes + 31) >> 5) * 4);
   o.lists = at;
   at += res_align(n_pods_max * kp * 8);
   o.pods = at;
   at += res_align(n_pods_max * (int32_t)sizeof(DevPod));
-  // two row regions, M' (prev) and M (cur), swapped at the end of every
-  // round: NV rows, then NumaRow rows; the cur region doubles as the
-  // prologue's refresh list (`hits`, (pod, list position, M' slot) of the
-  // entries on M' nodes: <= P x |M'|), which is dead before the loop writes M
+  // two row regions, M' (prev) and M (cur), swapped at the end of every round
   const int32_t rows_b = res_align(RES_MAXP_ROUND * (int32_t)sizeof(NV));
   const int32_t numa_b = numa ? res_align(RES_MAXP_ROUND * (int32_t)sizeof(NumaRow)) : 0;
-  const int32_t region = res_align(max(rows_b + numa_b, n_pods_max * n_pods_max * 4));
   o.prev_rows = at;
   o.prev_numa = at + rows_b;
-  at += region;
+  at += rows_b + numa_b;
   o.cur_rows = at;
   o.cur_numa = at + rows_b;
-  o.hits = at;
-  at += region;
+  at += rows_b + numa_b;
   o.hash_node = at;
   at += RES_HASH * 4;
   o.hash_slot = at;
@@ -1132,18 +1120,24 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += numa ? res_align(RES_PRE * (int32_t)sizeof(NumaRow)) : 0;
   o.pre_node = at;
   at += RES_PRE * 4;
-  o.want = at;
-  at += RES_PRE * 4;
-  o.top = at;
-  at += RES_MAXP_ROUND * RES_TOP * 8;
-  o.lcnt = at;
+  // the prologue's per-pod decisions: winner key, walked entries (-1: general
+  // path), winner row source, the walked nodes
+  o.dec_key = at;
+  at += RES_MAXP_ROUND * 8;
+  o.dec_n = at;
   at += RES_MAXP_ROUND * 4;
-  o.hmask = at;  // per pod: which list positions were refreshed (2 x 64 bits)
-  at += RES_MAXP_ROUND * 2 * 8;
+  o.dec_src = at;
+  at += RES_MAXP_ROUND * 4;
+  o.dec_e = at;
+  at += RES_MAXP_ROUND * RES_WE * 4;
+  o.moved = at;  // per M' slot: committed to again this round (its row moved into M)
+  at += RES_MAXP_ROUND * 4;
+  o.mbits = at;  // M bitmap
+  at += bitmap;
   o.classes = at;  // NodeNUMAResource topology classes (when <= NUMA_LDS_CLASSES)
   at += numa ? NUMA_LDS_CLASSES * (int32_t)sizeof(DevNumaClass) : 0;
-  o.modmap = at;
-  at += res_align(((n_nodes + 31) >> 5) * 4);
+  o.modmap = at;  // X bitmap
+  at += bitmap;
   o.overlap = overlap ? 1 : 0;
   o.lists2 = o.pods2 = o.pre_rows2 = o.pre_numa2 = o.pre_node2 = 0;
   if (overlap) {
@@ -1163,6 +1157,29 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
 }
 
 __device__ __forceinline__ uint32_t res_hash(int32_t node) { return ((uint32_t)node * 2654435761u) >> 24; }
+// A pod record read from LDS made wave-uniform (SGPRs): every lane read the
+// same record, readfirstlane tells the compiler so.
+__device__ __forceinline__ DevPod uniform_pod(const DevPod &src) {
+  DevPod p;
+  const uint32_t *s = reinterpret_cast<const uint32_t *>(&src);
+  uint32_t *o = reinterpret_cast<uint32_t *>(&p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(DevPod) / 4); i++) o[i] = __builtin_amdgcn_readfirstlane(s[i]);
+  return p;
+}
+__device__ __forceinline__ bool xbit(const uint32_t *m, int32_t nd) { return (m[nd >> 5] >> (nd & 31)) & 1u; }
+
+template <bool NUMA>
+__device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const NumaRow &nr,
+                                            const DevNumaClass *cls, const DevCfg &c) {
+  if constexpr (NUMA) {
+    return eval_total_numa(p, v, nr, cls, c);
+  } else {
+    (void)nr;
+    (void)cls;
+    return eval_total(p, v, c);
+  }
+}
 
 // Evaluation stream, before k_scan of round r: rounds < r - 1 must be written back.
 __global__ void k_wait_resolved(PipeSync *sy, int32_t rounds) {
@@ -1185,34 +1202,39 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
                                                                  uint64_t *__restrict__ out_cpus,
                                                                  uint64_t *__restrict__ dbg, int32_t trace) {
   constexpr int RES_THREADS = res_threads<NUMA>();
+  (void)trace;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   uint64_t *lk = reinterpret_cast<uint64_t *>(lds + ofs.lists);
-  NV *prow = reinterpret_cast<NV *>(lds + ofs.prev_rows);
+  DevPod *lpod = reinterpret_cast<DevPod *>(lds + ofs.pods);
+  NV *prow = reinterpret_cast<NV *>(lds + ofs.prev_rows);  // M' rows, slot = M' index
   NumaRow *pnr = reinterpret_cast<NumaRow *>(lds + ofs.prev_numa);
-  NV *mrow = reinterpret_cast<NV *>(lds + ofs.cur_rows);          // M rows, slot = M index
+  NV *mrow = reinterpret_cast<NV *>(lds + ofs.cur_rows);   // M rows, slot = M index
   NumaRow *mnr = reinterpret_cast<NumaRow *>(lds + ofs.cur_numa);
   int32_t *hnode = reinterpret_cast<int32_t *>(lds + ofs.hash_node);
   int32_t *hslot = reinterpret_cast<int32_t *>(lds + ofs.hash_slot);
   NV *pre = reinterpret_cast<NV *>(lds + ofs.pre_rows);
   NumaRow *prenr = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa);
   int32_t *pre_node = reinterpret_cast<int32_t *>(lds + ofs.pre_node);
+  uint64_t *dec_key = reinterpret_cast<uint64_t *>(lds + ofs.dec_key);
+  int32_t *dec_n = reinterpret_cast<int32_t *>(lds + ofs.dec_n);
+  int32_t *dec_src = reinterpret_cast<int32_t *>(lds + ofs.dec_src);
+  int32_t *dec_e = reinterpret_cast<int32_t *>(lds + ofs.dec_e);
+  int32_t *moved = reinterpret_cast<int32_t *>(lds + ofs.moved);
+  uint32_t *mbits = reinterpret_cast<uint32_t *>(lds + ofs.mbits);
+  uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
   // the next round's copies (ofs.overlap): swapped with the above every round
   uint64_t *lk2 = reinterpret_cast<uint64_t *>(lds + ofs.lists2);
   DevPod *lpod2 = reinterpret_cast<DevPod *>(lds + ofs.pods2);
   NV *pre2 = reinterpret_cast<NV *>(lds + ofs.pre_rows2);
   NumaRow *prenr2 = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa2);
   int32_t *pre_node2 = reinterpret_cast<int32_t *>(lds + ofs.pre_node2);
-  int32_t *want = reinterpret_cast<int32_t *>(lds + ofs.want);
-  uint64_t *top = reinterpret_cast<uint64_t *>(lds + ofs.top);
-  int32_t *lcnt = reinterpret_cast<int32_t *>(lds + ofs.lcnt);
-  uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
-  int32_t *hits = reinterpret_cast<int32_t *>(mrow);  // aliases the M region (prologue only)
-  uint64_t *hmask = reinterpret_cast<uint64_t *>(lds + ofs.hmask);
-  DevPod *lpod = reinterpret_cast<DevPod *>(lds + ofs.pods);
   __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous round committed to
-  __shared__ int32_t sh_mp, sh_stop, sh_nhit;
+  __shared__ int32_t seg_w[RES_MAXP_ROUND];  // staged winners by M slot (bulk commits)
+  __shared__ int32_t ckey[RES_HASH], cval[RES_HASH];  // staged winner -> first pod (conflict detection)
+  __shared__ int32_t sh_mp, sh_stop;
   const int t = threadIdx.x, lane = lane_id();
   const int32_t words = (n_nodes + 31) >> 5;
+  const int32_t HP = max(1, RES_PRE / P);  // prefetched list heads per pod
   // The column pointers are read from a device-side copy of DevNodes at each
   // (rare) row load/store instead of living in SGPRs for the whole kernel:
   // ~40 pointers would otherwise spill through VGPR lanes in the hot loop.
@@ -1221,12 +1243,20 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     asm volatile("" : "+s"(p));
     return *p;
   };
-  const bool two = k > 64;
+  const bool two = kp > 64;
   if (t == 0) {
     sh_mp = r_begin > 0 ? min(mbuf[0], (int32_t)RES_MAXP_ROUND) : 0;
     sh_stop = 0;
   }
-  for (int32_t x = t; x < words; x += RES_THREADS) modmap[x] = 0;
+  for (int32_t x = t; x < words; x += RES_THREADS) {
+    modmap[x] = 0;
+    mbits[x] = 0;
+  }
+  for (int32_t x = t; x < RES_MAXP_ROUND; x += RES_THREADS) moved[x] = 0;
+  for (int32_t x = t; x < RES_HASH; x += RES_THREADS) {
+    ckey[x] = -1;
+    cval[x] = 64;
+  }
   const DevNumaClass *cls = ncls;
   if constexpr (NUMA) {  // topology classes -> LDS
     const int32_t nc = nodes().nu.ncls;
@@ -1249,6 +1279,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       load_numa_row(rr, nodes(), nd);
       pnr[t] = rr;
     }
+    atomicOr(&modmap[nd >> 5], 1u << (nd & 31));
   }
   __syncthreads();
   // wave 0: lane s < |M| holds the node of M slot s (its row is mrow[s] in LDS);
@@ -1259,11 +1290,12 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   if (lane == 10 || lane == 11) doff = (int32_t)offsetof(DevPod, nz_cpu_m) + (lane - 10) * 8;
   if (lane == 14 || lane == 16) doff = (int32_t)offsetof(DevPod, est_cpu);  // la_u / la_up (prod)
   if (lane == 15 || lane == 17) doff = (int32_t)offsetof(DevPod, est_mem);
-  uint64_t n_eval = 0, n_miss = 0, c_pro = 0, c_loop = 0, c_wait = 0, c_ph_a = 0, c_ph_b = 0, c_ph_r = 0, c_rel = 0;
-  uint64_t c_l[4] = {0, 0, 0, 0};  // loop phases: general-path candidate, fast path, re-evaluation, commit
-  // ---- 1. a round's global reads: lists -> LDS (stride kp, zero padded), pod
-  //         records, and the rows of the list heads (slot s = pod s / 2,
-  //         position s % 2, as delivered), by threads tid = 0..nth-1
+  // diagnostics (KOORDHIP_STAMPS): cycles and counts per phase
+  uint64_t c_pro = 0, c_wait = 0, c_loop = 0, c_rel = 0, c_hash = 0;
+  uint64_t c_l[4] = {0, 0, 0, 0};  // conflict detection, bulk commits, general-path candidate + keys, general commit
+  uint64_t n_slow = 0, n_miss = 0, n_staged = 0, n_bulk = 0;
+  // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
+  //      records, and the rows of each pod's first HP list entries (slot HP j + q)
   auto load_round = [&](int32_t rr, int32_t rp0, int32_t rn, uint64_t *Lk, DevPod *Lp, NV *Pr, NumaRow *Pn,
                         int32_t *Pnode, int32_t tid, int32_t nth) {
     const uint64_t *L = lists0 + (size_t)(rr & 1) * list_buf;
@@ -1277,7 +1309,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       for (int32_t x = tid; x < rn * (int32_t)(sizeof(DevPod) / 4); x += nth) dst[x] = src[x];
     }
     for (int32_t sl = tid; sl < RES_PRE; sl += nth) {
-      const int32_t j = sl >> 1, q = sl & 1;
+      const int32_t j = sl / HP, q = sl - j * HP;
       int32_t nd = -1;
       if (j < rn && q < k) {
         const uint64_t e = L[(size_t)j * k + q];
@@ -1296,10 +1328,17 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       Pnode[sl] = nd;
     }
   };
+  auto prev_slot = [&](int32_t nd) -> int32_t {
+    uint32_t h = res_hash(nd);
+    for (;;) {
+      const int32_t x = hnode[h];
+      if (x == nd) return hslot[h];
+      if (x < 0) return -1;
+      h = (h + 1) & (RES_HASH - 1);
+    }
+  };
   for (int32_t r = r_begin, p0 = r_begin * P; r < r_end && p0 < total; r++, p0 += P) {
     const int32_t n_pods = min(P, total - p0);
-    const int32_t trace_j = (trace >= p0 && trace < p0 + n_pods) ? trace - p0 : -1;
-    (void)trace_j;
     // ---- 0. this round's inputs: loaded by waves 1.. during the previous
     //         round's loop (overlap), else wait for the lists and load them now
     const bool preloaded = ofs.overlap && r > r_begin;
@@ -1313,7 +1352,6 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     const int32_t mp = sh_mp;
     if (!preloaded) load_round(r, p0, n_pods, lk, lpod, pre, prenr, pre_node, t, RES_THREADS);
     for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
-    if (t == 0) sh_nhit = 0;
     __syncthreads();
     if (t < mp) {  // M' hash: node -> slot, linear probing, lock-free inserts
       const int32_t nd = pnode[t];
@@ -1323,164 +1361,160 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     }
     __syncthreads();
     const uint64_t t_a = (dbg && t == 0) ? stamp() : 0;
-    auto prev_slot = [&](int32_t nd) -> int32_t {
-      uint32_t h = res_hash(nd);
-      for (;;) {
-        const int32_t x = hnode[h];
-        if (x == nd) return hslot[h];
-        if (x < 0) return -1;
-        h = (h + 1) & (RES_HASH - 1);
-      }
-    };
-    // rows prefetched while the previous round ran are stale for its nodes (M'),
-    // whose current rows are the M' slots: drop those prefetch slots (read
-    // after the refresh barriers below)
-    if (preloaded && mp > 0 && t < RES_PRE) {
+    // list-head rows of M' nodes: the M' slots hold their current rows (a
+    // prefetch made while the previous round ran is stale), and a commit to
+    // an M' node must go through its slot (moved[]): drop those slots
+    if (mp > 0 && t < RES_PRE) {
       const int32_t nd = pre_node[t];
       if (nd >= 0 && prev_slot(nd) >= 0) pre_node[t] = -1;
     }
-    // ---- 2. refresh the keys of the list entries on M' nodes (exact, current
-    //         rows): (a) one wave per pod collects them, (b) every thread
-    //         evaluates one -- at most one entry per (pod, M' node), so one
-    //         pass for |M'| x P <= threads; (c) one wave per pod extracts the
-    //         RES_TOP best keys in order -- the loop nearly always finds its
-    //         candidate among them; the lists themselves stay unsorted
-    {
-      const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-      if (mp > 0) {
-        for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
-          const uint64_t *L = lk + (size_t)j * kp;
-          for (int32_t q = lane; q < kp; q += 64) {
-            const uint64_t e = L[q];
-            const int32_t sl = e ? prev_slot(key_node(e)) : -1;
-            const uint64_t b = __ballot(sl >= 0);
-            if (lane == 0) hmask[2 * j + (q >> 6)] = b;
-            if (b == 0) continue;
-            int32_t base = 0;
-            if (lane == 0) base = atomicAdd(&sh_nhit, __popcll(b));
-            base = __shfl(base, 0, 64);
-            if (sl >= 0) hits[base + __popcll(b & ((1ull << lane) - 1))] = (j << 16) | (q << 8) | sl;
-          }
-        }
-        __syncthreads();
-        const int32_t nh = sh_nhit;
-        for (int32_t h = t; h < nh; h += RES_THREADS) {
-          const int32_t x = hits[h], j = x >> 16, q = (x >> 8) & 0xFF, sl = x & 0xFF;
-          const DevPod pod = lpod[j];
-          int32_t tot;
-          if constexpr (NUMA) {
-            tot = eval_total_numa(pod, slot_row(prow[sl]), pnr[sl], cls, c);
-          } else {
-            tot = eval_total(pod, slot_row(prow[sl]), c);
-          }
-          lk[(size_t)j * kp + q] = make_key(tot, pnode[sl]);
-        }
-        __syncthreads();
-      }
-      if (dbg && t == 0) c_ph_r += stamp() - t_a;
-      // (c) the lists arrive sorted (descending keys; k_select / k_topk_merge
-      //     output contract) and only the refreshed entries moved, so each
-      //     entry's rank = unrefreshed entries before it + refreshed entries
-      //     above it (a refreshed entry: every entry above it)
-      const uint64_t lt = (1ull << lane) - 1;
-      for (int32_t j = wv; j < n_pods; j += RES_THREADS / 64) {
-        const uint64_t *L = lk + (size_t)j * kp;
-        const uint64_t x0 = lane < kp ? L[lane] : 0ull, x1 = 64 + lane < kp ? L[64 + lane] : 0ull;
-        const int32_t cnt = __popcll(__ballot(x0 != 0)) + __popcll(__ballot(x1 != 0));
-        const uint64_t m0 = mp > 0 ? hmask[2 * j] : 0ull, m1 = (mp > 0 && two) ? hmask[2 * j + 1] : 0ull;
-        const bool f0 = (m0 >> lane) & 1, f1 = (m1 >> lane) & 1;  // refreshed
-        int32_t r0 = __popcll(~m0 & lt), r1 = __popcll(~m0) + __popcll(~m1 & lt);
-        for (uint64_t mm = m0; mm; mm &= mm - 1) {
-          const int l = __builtin_ctzll(mm);
-          const uint64_t v = readlane_u64(x0, l);
-          const int32_t rv = __popcll(__ballot(x0 > v)) + __popcll(__ballot(x1 > v));
-          r0 = lane == l ? rv : r0 + (!f0 && v > x0);
-          r1 += !f1 && v > x1;
-        }
-        for (uint64_t mm = m1; mm; mm &= mm - 1) {
-          const int l = __builtin_ctzll(mm);
-          const uint64_t v = readlane_u64(x1, l);
-          const int32_t rv = __popcll(__ballot(x0 > v)) + __popcll(__ballot(x1 > v));
-          r1 = lane == l ? rv : r1 + (!f1 && v > x1);
-          r0 += !f0 && v > x0;
-        }
-        uint64_t *tp = top + j * RES_TOP;
-        if (lane < RES_TOP) tp[lane] = 0ull;
-        if (x0 != 0 && r0 < RES_TOP) tp[r0] = x0;
-        if (x1 != 0 && r1 < RES_TOP) tp[r1] = x1;
-        if (lane < 2) {  // the two best: rows to prefetch (M' rows are in LDS already)
-          const uint64_t m = tp[lane];
-          const int32_t nd = m ? key_node(m) : -1;
-          want[2 * j + lane] = (nd >= 0 && (mp == 0 || prev_slot(nd) < 0)) ? nd : -1;
-        }
-        if (lane == 0) lcnt[j] = cnt;
-      }
-      __syncthreads();
-      if (dbg && t == 0) c_ph_a += t_a - t_entry, c_ph_b += stamp() - t_a;
-      if (t < RES_PRE && t < 2 * n_pods) {  // reload the slots whose head changed
-        const int32_t nd = want[t];
-        if (nd >= 0 && nd != pre_node[t]) {
-          NV v;
-          load_row(v, nodes(), nd);
-          pre[t] = v;
-          if constexpr (NUMA) {
-            NumaRow rr;
-            load_numa_row(rr, nodes(), nd);
-            prenr[t] = rr;
-          }
-          pre_node[t] = nd;
+    // ---- 1. every pod's staged decision: eight lanes per pod walk its first
+    //         RES_WE entries; M' entries (X = M' now) are evaluated on their
+    //         current rows, the first entry outside M' (exact) ends the walk
+    for (int32_t base = 0; base < n_pods * RES_WE; base += RES_THREADS) {
+      const int32_t x = base + t;
+      const int32_t l = x / RES_WE, q = x - l * RES_WE;
+      const bool live = l < n_pods;
+      const uint64_t e = (live && q < kp) ? lk[l * kp + q] : 0ull;
+      const int32_t nd = e ? key_node(e) : -1;
+      const bool inx = e != 0 && xbit(modmap, nd);
+      const int g = lane & ~(RES_WE - 1);
+      const uint32_t bx = (uint32_t)(__ballot(live && e != 0 && !inx) >> g) & 0xFFu;
+      const uint32_t bz = (uint32_t)(__ballot(live && e == 0) >> g) & 0xFFu;
+      const int f = bx ? __builtin_ctz(bx) : RES_WE, z = bz ? __builtin_ctz(bz) : RES_WE;
+      const bool general = f == RES_WE && z == RES_WE;  // RES_WE M' entries in a row
+      const bool walked = live && !general && (q < min(f, z) || (q == f && f < z));
+      uint64_t key = 0;
+      if (walked) {
+        if (q < min(f, z)) {  // an M' entry: its exact key on the current row
+          const int32_t s = prev_slot(nd);
+          const DevPod pod = lpod[l];
+          key = make_key(eval_row<NUMA>(pod, slot_row(prow[s]), pnr[s], cls, c), nd);
+        } else {
+          key = e;
         }
       }
-      __syncthreads();
+#pragma unroll
+      for (int m = 1; m < RES_WE; m <<= 1) {
+        const uint64_t o = shfl_xor_u64(key, m);
+        key = o > key ? o : key;
+      }
+      if (live) {
+        dec_e[l * RES_WE + q] = walked ? nd : -1;
+        if (q == 0) {
+          dec_key[l] = key;
+          dec_n[l] = general ? -1 : (f < z ? f + 1 : z);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 2. the staged winner's row: an M' slot (src < 0), a list-head
+    //         prefetch slot, or one HBM load into the pod's first head slot
+    for (int32_t l = t; l < n_pods; l += RES_THREADS) {
+      const uint64_t kk = dec_key[l];
+      int32_t src = 0;
+      if (kk != 0 && dec_n[l] >= 0) {
+        const int32_t w = key_node(kk);
+        const int32_t s = mp > 0 ? prev_slot(w) : -1;
+        if (s >= 0) {
+          src = -s - 1;
+        } else {
+          int32_t ps = -1;
+          for (int32_t q = 0; q < HP && ps < 0; q++)
+            if (pre_node[l * HP + q] == w) ps = l * HP + q;
+          if (ps < 0) {
+            ps = l * HP;
+            NV v;
+            load_row(v, nodes(), w);
+            pre[ps] = v;
+            if constexpr (NUMA) {
+              NumaRow nr;
+              load_numa_row(nr, nodes(), w);
+              prenr[ps] = nr;
+            }
+            pre_node[ps] = w;
+          }
+          src = ps;
+        }
+      }
+      dec_src[l] = src;
+    }
+    __syncthreads();
+    if (dbg && t == 0) {
+      c_hash += t_a - t_entry;
+      c_pro += stamp() - t_a;
+      c_wait += t_entry - t_w0;
     }
     if (t < 64) {  // ---- 3. the sequential greedy over the round (wave 0)
       __builtin_amdgcn_s_setprio(3);
-      const uint64_t t_pro = dbg ? stamp() : 0;
+      const uint64_t t_loop = dbg ? stamp() : 0;
       int32_t nm = 0;  // |M| (wave-uniform)
       my_node = -1;
-      // loop-invariant LDS words in registers: the prefetched rows' nodes, and
-      // the next pod's best keys are read one pod ahead (off the dependent chain)
       const int32_t pn0 = pre_node[lane], pn1 = pre_node[lane + 64];
-      uint64_t tv_next = lane < RES_TOP ? top[lane] : 0ull;
-      // per-pod bits (lane j = pod j): prod (its Reserve adds to la_used_prod),
-      // and "slow" pods that never take the fast path below: a non-monotone
-      // configuration, NUMA cpuset pods (Allocate at Reserve, required-policy
-      // feasibility is not monotone)
-      uint64_t prodmask, slowmask;
-      {
-        uint32_t fl = 0, pol = 0;
-        if (lane < n_pods) {
-          fl = lpod[lane].flags;
-          pol = lpod[lane].numa_policy;
-        }
-        prodmask = __ballot(lane < n_pods && (fl & KOORDHIP_POD_PROD));
-        bool slow = !monotone;
-        if constexpr (NUMA) {
-          const bool cs = numa_on(c) && (fl & KOORDHIP_POD_CPUSET) &&
-                          !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
-          slow = slow || cs;
-        }
-        (void)pol;
-        slowmask = __ballot(lane < n_pods && slow);
+      // ---- lane l = pod l: its staged decision in registers
+      const bool live = lane < n_pods;
+      uint32_t fl = 0;
+      int32_t sw = -1, ssrc = 0, sn = -1;
+      int32_t se[RES_WE];
+#pragma unroll
+      for (int q = 0; q < RES_WE; q++) se[q] = -1;
+      if (live) {
+        fl = lpod[lane].flags;
+        sn = dec_n[lane];
+        const uint64_t kk = dec_key[lane];
+        sw = kk ? key_node(kk) : -1;
+        ssrc = dec_src[lane];
+#pragma unroll
+        for (int q = 0; q < RES_WE; q++) se[q] = dec_e[lane * RES_WE + q];
       }
-      // The Reserve delta of a pod is applied lane-parallel (lane q on row word
-      // q) and deferred: its row words are read at the pod's decision and the
-      // update is finished after the next pod's candidate reads are issued, so
-      // the LDS round trip overlaps the next decision instead of stalling it.
-      bool pend = false;  // wave-uniform
-      int32_t pend_rw = 0;
-      uint64_t pend_x = 0;
-      double pend_dq = 0.0;
-      auto finish = [&]() {
-        if (!pend) return;
-        uint64_t x = pend_x;
-        if (lane < 18) x = (uint64_t)__double_as_longlong(__longlong_as_double((long long)x) + pend_dq);
-        if (lane == 18) x += 1ull << 32;  // npods + 1 (high half; a_pods below)
-        // word 19 (flags) is copied with stale over-commit bits: slot_row() recomputes them
-        if (lane < RES_WORDS) reinterpret_cast<uint64_t *>(&mrow[pend_rw])[lane] = x;
-        pend = false;
-      };
-      for (int32_t j = 0; j < n_pods; j++) {
+      const uint64_t prodmask = __ballot(live && (fl & KOORDHIP_POD_PROD));
+      // "slow" pods always take the general path: a non-monotone configuration,
+      // NUMA cpuset pods (Allocate at Reserve; required-policy feasibility is
+      // not monotone), a walk longer than RES_WE entries
+      bool slow = !monotone || sn < 0;
+      if constexpr (NUMA) {
+        slow = slow || (numa_on(c) && (fl & KOORDHIP_POD_CPUSET) &&
+                        !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
+      }
+      // ---- conflicts among the staged decisions: pod l's walk met the staged
+      //      winner of an earlier pod (exact node -> first pod hash, linear probing)
+      const bool claims = live && !slow && sw >= 0;
+      if (claims) {
+        uint32_t h = res_hash(sw);
+        for (;;) {
+          const int32_t prev = atomicCAS(&ckey[h], -1, sw);
+          if (prev == -1 || prev == sw) {
+            atomicMin(&cval[h], lane);
+            break;
+          }
+          h = (h + 1) & (RES_HASH - 1);
+        }
+      }
+      bool conflict = false;
+#pragma unroll
+      for (int q = 0; q < RES_WE; q++) {
+        const int32_t y = se[q];
+        if (live && !slow && y >= 0) {
+          uint32_t h = res_hash(y);
+          for (;;) {
+            const int32_t x = ckey[h];
+            if (x == y) {
+              conflict = conflict || cval[h] < lane;
+              break;
+            }
+            if (x < 0) break;
+            h = (h + 1) & (RES_HASH - 1);
+          }
+        }
+      }
+      for (int32_t x = lane; x < RES_HASH; x += 64) {  // table empty again for the next round
+        ckey[x] = -1;
+        cval[x] = 64;
+      }
+      uint64_t ok = __ballot(live && !slow && !conflict);  // staged decisions still valid
+      int32_t j = 0;
+      if (dbg) c_l[0] += stamp() - t_loop;
+      while (j < n_pods) {
         uint64_t ts = dbg ? stamp() : 0;
         auto lap = [&](int ph) {
           if (dbg) {
@@ -1489,138 +1523,72 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             ts = x;
           }
         };
-        // candidate: the best entry outside M (every list key is exact); first
-        // among the pod's RES_TOP best, else from the whole list
-        const uint64_t tv = tv_next;
-        if (j + 1 < n_pods) tv_next = lane < RES_TOP ? top[(j + 1) * RES_TOP + lane] : 0ull;
-        // the M bits of the best keys: an unconditional read (no branch), so the
-        // previous pod's row update below issues while it is in flight
-        const int32_t tnd = key_node(tv);
-        const uint32_t tword = modmap[tv != 0 ? (tnd >> 5) : 0];
-        finish();  // the previous pod's row update (reads issued at its decision)
-        const bool tmod = tv != 0 && ((tword >> (tnd & 31)) & 1u);
-        const uint64_t tfree = __ballot(tv != 0 && !tmod);
-        // ---- fast path (monotone pod, the first free key of its best 8 has no
-        //      M node ranked above it): that key is the winner, a node new to M
-        if (tfree != 0 && !((slowmask >> j) & 1ull) &&
-            __ballot(tv != 0 && tmod && lane < __builtin_ctzll(tfree)) == 0) {
-          const int32_t w = key_node(readlane_u64(tv, __builtin_ctzll(tfree)));
-          const int32_t rw = nm;
-          const NV *srow = &mrow[rw];
-          const NumaRow *snr = &mnr[rw];
-          const uint64_t pm0 = __ballot(pn0 == w), pm1 = __ballot(pn1 == w);
-          const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
-          const int32_t sl = (src < 0 && mp > 0) ? prev_slot(w) : -1;
-          if (src >= 0) {
-            srow = &pre[src];
-            snr = &prenr[src];
-          } else if (sl >= 0) {
-            srow = &prow[sl];
-            snr = &pnr[sl];
-          } else {
-            n_miss++;
-            if (lane == 0) {
-              NV v;
-              load_row(v, nodes(), w);
-              mrow[rw] = v;
-              if constexpr (NUMA) {
-                NumaRow nr;
-                load_numa_row(nr, nodes(), w);
-                mnr[rw] = nr;
-              }
+        // ---- the next general-path pod g; pods [j, g) commit their staged
+        //      decisions together (distinct winners: a shared winner is a conflict)
+        const uint64_t from_j = ~0ull << j;
+        const uint64_t gen = ~ok & from_j & (n_pods < 64 ? ((1ull << n_pods) - 1ull) : ~0ull);
+        const int32_t g = gen ? (int32_t)__builtin_ctzll(gen) : n_pods;
+        if (g > j) {
+          const bool mine = lane >= j && lane < g;
+          const bool com = mine && sw >= 0;
+          const uint64_t cb = __ballot(com);
+          const int32_t slot = nm + __popcll(cb & ((1ull << lane) - 1ull));
+          if (com) {
+            const NV *srow = ssrc >= 0 ? &pre[ssrc] : &prow[-ssrc - 1];
+            NV v = *srow;
+            const DevPod pod = lpod[lane];
+            apply_delta(v, pod, +1);
+            mrow[slot] = v;
+            if constexpr (NUMA) mnr[slot] = ssrc >= 0 ? prenr[ssrc] : pnr[-ssrc - 1];
+            if (ssrc < 0) moved[-ssrc - 1] = 1;
+            atomicOr(&mbits[sw >> 5], 1u << (sw & 31));
+            atomicOr(&modmap[sw >> 5], 1u << (sw & 31));
+            seg_w[slot] = sw;
+          }
+          if (mine) {
+            out_node[p0 + lane] = com ? sw : KOORDHIP_UNSCHEDULABLE;
+            if (out_cpus) {
+#pragma unroll
+              for (int q = 0; q < NW; q++) out_cpus[(size_t)(p0 + lane) * NW + q] = 0ull;
             }
           }
-          if constexpr (NUMA) {
-            if (lane < (int)(sizeof(NumaRow) / 8))
-              reinterpret_cast<uint64_t *>(&mnr[rw])[lane] = reinterpret_cast<const uint64_t *>(snr)[lane];
-          }
-          pend_x = lane < RES_WORDS ? reinterpret_cast<const uint64_t *>(srow)[lane] : 0ull;
-          pend_dq = (doff >= 0 && (lane < 16 || ((prodmask >> j) & 1ull)))
-                        ? *reinterpret_cast<const double *>(reinterpret_cast<const char *>(&lpod[j]) + doff)
-                        : 0.0;
-          pend_rw = rw;
-          pend = true;
-          nm++;
-          if (lane == rw) my_node = w;
-          if (lane == 0) {
-            atomicOr(&modmap[w >> 5], 1u << (w & 31));
-            out_node[p0 + j] = w;
-          }
-          if (out_cpus && lane < NW) out_cpus[(size_t)(p0 + j) * NW + lane] = 0ull;
-          lap(1);
-          continue;
+          const int32_t nc = __popcll(cb);
+          if (lane >= nm && lane < nm + nc) my_node = seg_w[lane];
+          nm += nc;
+          n_staged += g - j;
+          n_bulk++;
         }
-        const DevPod pod = lpod[j];  // VGPR copy: SGPRs are the scarce register file here
-        uint64_t cand = 0;
-        bool prefix_modified;
-        if (tfree || lcnt[j] <= RES_TOP) {
-          const int first = tfree ? __builtin_ctzll(tfree) : 64;
-          cand = tfree ? readlane_u64(tv, first) : 0ull;
-          // an M node can only win if its (upper-bound) list key beats the candidate
-          prefix_modified = __ballot(tv != 0 && tmod && lane < first) != 0;
-        } else {
-          const uint64_t *L = lk + (size_t)j * kp;
-          const uint64_t e0 = lane < k ? L[lane] : 0ull;  // lanes past k hold nothing (k may be < 64)
-          const uint64_t e1 = two && 64 + lane < k ? L[64 + lane] : 0ull;
-          bool mod0 = false, mod1 = false;
-          if (e0) {
-            const int32_t nd = key_node(e0);
-            mod0 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
+        lap(1);
+        if (g >= n_pods) break;
+        // ---- general path: pod g alone -- c, then every M and M' row's current key
+        n_slow++;
+        // the pod record made wave-uniform: its fields steer the evaluation's
+        // branches, which must be scalar (a VGPR copy runs every path masked)
+        const DevPod pod = uniform_pod(lpod[g]);
+        const uint64_t *L = lk + (size_t)g * kp;
+        const uint64_t e0 = lane < kp ? L[lane] : 0ull;
+        const uint64_t e1 = (two && 64 + lane < kp) ? L[64 + lane] : 0ull;
+        const bool x0 = e0 != 0 && xbit(modmap, key_node(e0));
+        const bool x1 = e1 != 0 && xbit(modmap, key_node(e1));
+        const uint64_t f0 = __ballot(e0 != 0 && !x0), f1 = __ballot(e1 != 0 && !x1);
+        uint64_t best = f0 ? readlane_u64(e0, __builtin_ctzll(f0)) : (f1 ? readlane_u64(e1, __builtin_ctzll(f1)) : 0ull);
+        const int32_t nrows = nm + mp;
+        for (int32_t b0 = 0; b0 < nrows; b0 += 64) {  // rows: M slots, then the M' slots not moved into M
+          const int32_t s = b0 + lane;
+          uint64_t kv = 0;
+          if (s < nm) {
+            NumaRow nr;
+            if constexpr (NUMA) nr = mnr[s];
+            kv = make_key(eval_row<NUMA>(pod, slot_row(mrow[s]), nr, cls, c), my_node);
+          } else if (s < nrows && !moved[s - nm]) {
+            NumaRow nr;
+            if constexpr (NUMA) nr = pnr[s - nm];
+            kv = make_key(eval_row<NUMA>(pod, slot_row(prow[s - nm]), nr, cls, c), pnode[s - nm]);
           }
-          if (e1) {
-            const int32_t nd = key_node(e1);
-            mod1 = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-          }
-          const uint64_t f0 = (e0 != 0 && !mod0) ? e0 : 0ull, f1 = (e1 != 0 && !mod1) ? e1 : 0ull;
-          cand = wave_max_u64_dpp(f0 > f1 ? f0 : f1);
-          prefix_modified = (__ballot(mod0 && e0 > cand) | __ballot(mod1 && e1 > cand)) != 0;
-        }
-        lap(0);
-        const bool nonmono = !monotone || (NUMA && is_cpuset(pod) &&
-                                           KOORDHIP_NUMA_REQUIRED(pod.numa_policy) != KOORDHIP_CPUBIND_NONE);
-        uint64_t best = cand;
-        if (nm > 0 && (prefix_modified || nonmono)) {
-          uint64_t key = 0;
-          if (lane < nm) {
-            const NV v = slot_row(mrow[lane]);
-            if constexpr (NUMA) {
-              const NumaRow nr = mnr[lane];
-              key = make_key(eval_total_numa(pod, v, nr, cls, c), my_node);
-            } else {
-              key = make_key(eval_total(pod, v, c), my_node);
-            }
-          }
-          key = wave_max_u64_dpp(key);
-          best = key > best ? key : best;
-          n_eval++;
-        }
-        if (nonmono && mp > 0) {  // M' nodes outside M: current rows in LDS
-          uint64_t key = 0;
-          if (lane < mp) {
-            const int32_t nd = pnode[lane];
-            const bool in_m = (modmap[nd >> 5] >> (nd & 31)) & 1u;
-            if (!in_m) {
-              if constexpr (NUMA) {
-                key = make_key(eval_total_numa(pod, slot_row(prow[lane]), pnr[lane], cls, c), nd);
-              } else {
-                key = make_key(eval_total(pod, slot_row(prow[lane]), c), nd);
-              }
-            }
-          }
-          key = wave_max_u64_dpp(key);
-          best = key > best ? key : best;
+          kv = wave_max_u64_dpp(kv);
+          best = kv > best ? kv : best;
         }
         lap(2);
-#ifdef KOORDHIP_TRACE_BUILD
-        if (j == trace_j) {  // diagnostics (KOORDHIP_TRACE_POD, trace builds only: printf bloats the loop)
-          if (lane == 0)
-            printf("[trace] j=%d cand=%d/%d best=%d/%d nm=%d mp=%d nonmono=%d prefix=%d\n", j,
-                   cand ? key_node(cand) : -1, cand ? key_score(cand) : -1, best ? key_node(best) : -1,
-                   best ? key_score(best) : -1, nm, mp, (int)nonmono, (int)prefix_modified);
-          if (lane < nm) printf("[trace] M lane %d node %d\n", lane, my_node);
-          if (lane < mp) printf("[trace] M' lane %d node %d\n", lane, pnode[lane]);
-        }
-#endif
         uint64_t cpus[NW] = {0, 0, 0, 0};
         int32_t result = KOORDHIP_UNSCHEDULABLE;
         if (best != 0) {
@@ -1631,6 +1599,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           const int32_t rw = hit ? __builtin_ctzll(hit) : nm;
           const NV *srow = &mrow[rw];
           const NumaRow *snr = &mnr[rw];
+          int32_t from_prev = -1;
           if (!hit) {
             const uint64_t pm0 = __ballot(pn0 == w), pm1 = __ballot(pn1 == w);
             const int src = pm0 ? __builtin_ctzll(pm0) : (pm1 ? 64 + __builtin_ctzll(pm1) : -1);
@@ -1641,6 +1610,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             } else if (sl >= 0) {
               srow = &prow[sl];
               snr = &pnr[sl];
+              from_prev = sl;
             } else {
               n_miss++;
               if (lane == 0) {
@@ -1655,7 +1625,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
               }
             }
           }
-          bool ok = true;
+          bool okr = true;
           if constexpr (NUMA) {
             if (numa_on(c) && is_cpuset(pod)) {
               // NodeNUMAResource Reserve: lane 0 replays the accumulator on the
@@ -1670,60 +1640,80 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
                   mnr[rw] = nr;
                 }
               }
-              ok = __builtin_amdgcn_readfirstlane(okl) != 0;
+              okr = __builtin_amdgcn_readfirstlane(okl) != 0;
 #pragma unroll
               for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], 0);
             } else if (!hit && lane < (int)(sizeof(NumaRow) / 8)) {
               reinterpret_cast<uint64_t *>(&mnr[rw])[lane] = reinterpret_cast<const uint64_t *>(snr)[lane];
             }
           }
-          if (!ok) {
-            result = KOORDHIP_RESERVE_FAILED;  // every Reserve is rolled back
+          if (!okr) {
+            result = KOORDHIP_RESERVE_FAILED;  // nothing is committed
           } else {
             result = w;
-            // Reserve delta (apply_delta): issue the reads, finish() applies it
-            pend_x = lane < RES_WORDS ? reinterpret_cast<const uint64_t *>(srow)[lane] : 0ull;
-            pend_dq = (doff >= 0 && (lane < 16 || ((prodmask >> j) & 1ull)))
-                          ? *reinterpret_cast<const double *>(reinterpret_cast<const char *>(&lpod[j]) + doff)
-                          : 0.0;
-            pend_rw = rw;
-            pend = true;
+            // Reserve delta, lane q on word q (flags: slot_row() on read)
+            const uint64_t xw = lane < RES_WORDS ? reinterpret_cast<const uint64_t *>(srow)[lane] : 0ull;
+            const double dq = (doff >= 0 && (lane < 16 || ((prodmask >> g) & 1ull)))
+                                  ? *reinterpret_cast<const double *>(reinterpret_cast<const char *>(&lpod[g]) + doff)
+                                  : 0.0;
+            uint64_t x = xw;
+            if (lane < 18) x = (uint64_t)__double_as_longlong(__longlong_as_double((long long)xw) + dq);
+            if (lane == 18) x += 1ull << 32;
+            if (lane < RES_WORDS) reinterpret_cast<uint64_t *>(&mrow[rw])[lane] = x;
             if (!hit) {
-              nm++;
               if (lane == rw) my_node = w;
-              if (lane == 0) atomicOr(&modmap[w >> 5], 1u << (w & 31));
+              if (lane == 0) {
+                atomicOr(&mbits[w >> 5], 1u << (w & 31));
+                atomicOr(&modmap[w >> 5], 1u << (w & 31));
+                if (from_prev >= 0) moved[from_prev] = 1;
+              }
+              nm++;
             }
+            // later staged decisions that walked w are void
+            bool met = false;
+#pragma unroll
+            for (int q = 0; q < RES_WE; q++) met = met || se[q] == w;
+            ok &= ~__ballot(lane > g && met);
           }
         }
-        if (lane == 0) out_node[p0 + j] = result;
-        lap(3);
+        if (lane == 0) out_node[p0 + g] = result;
         if (out_cpus && lane < NW)
-          out_cpus[(size_t)(p0 + j) * NW + lane] =
+          out_cpus[(size_t)(p0 + g) * NW + lane] =
               lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
+        lap(3);
+        j = g + 1;
       }
-      finish();
-      // ---- 4. write M back, hand it to the next round as M' (rows stay in LDS)
+      // ---- 4. write M back; M becomes the next round's M' (rows stay in LDS)
       if (lane < nm) {
         const NV v = slot_row(mrow[lane]);
+        mrow[lane] = v;
         store_row(v, nodes(), my_node);
         if constexpr (NUMA) {
           const NumaRow nr = mnr[lane];
           store_numa_row(nr, nodes(), my_node);
         }
-        pnode[lane] = my_node;
-        modmap[my_node >> 5] = 0;  // clear the round's bits (whole words: every bit set is M's)
       }
+      // X of the next round = M: clear the words of M' and M (every bit set in
+      // them is X's), then set M's bits; M's bitmap is cleared
+      if (lane < mp) modmap[pnode[lane] >> 5] = 0;
+      if (lane < nm) {
+        modmap[my_node >> 5] = 0;
+        mbits[my_node >> 5] = 0;
+      }
+      if (lane < nm) {
+        atomicOr(&modmap[my_node >> 5], 1u << (my_node & 31));
+        pnode[lane] = my_node;
+      }
+      moved[lane] = 0;
       const uint64_t t_rel = dbg ? stamp() : 0;
       if (lane == 0) {
         sh_mp = nm;
         store_release(&sy->res_round, r + 1);  // after every lane's stores (one wave: program order)
       }
-      if (dbg) c_rel += stamp() - t_rel;
-      if (dbg && lane == 0) {
+      if (dbg) {
         const uint64_t t_end = stamp();
-        c_pro += t_pro - t_entry;
-        c_loop += t_end - t_pro;
-        c_wait += t_entry - t_w0;
+        c_rel += t_end - t_rel;
+        c_loop += t_end - t_loop;
       }
     } else if (ofs.overlap && r + 1 < r_end && p0 + P < total) {
       // ---- waves 1..: the next round's lists, pods and head rows, meanwhile
@@ -1762,22 +1752,21 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       NumaRow *y = pnr;
       pnr = mnr;
       mnr = y;
-      hits = reinterpret_cast<int32_t *>(mrow);
     }
   }
   if (t <= RES_MAXP_ROUND && t <= sh_mp) mbuf[t] = t == 0 ? sh_mp : pnode[t - 1];  // hand M' on
   if (dbg && t == 0) {
     atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)c_pro);
     atomicAdd((unsigned long long *)&dbg[1], (unsigned long long)c_wait);
+    atomicAdd((unsigned long long *)&dbg[2], (unsigned long long)c_hash);
     atomicAdd((unsigned long long *)&dbg[4], (unsigned long long)c_loop);
-    atomicAdd((unsigned long long *)&dbg[5], (unsigned long long)n_eval);
+    atomicAdd((unsigned long long *)&dbg[5], (unsigned long long)n_slow);
     atomicAdd((unsigned long long *)&dbg[6], (unsigned long long)n_miss);
     atomicAdd((unsigned long long *)&dbg[7], (unsigned long long)total);
-    atomicAdd((unsigned long long *)&dbg[2], (unsigned long long)c_ph_a);
-    atomicAdd((unsigned long long *)&dbg[3], (unsigned long long)c_ph_b);
     atomicAdd((unsigned long long *)&dbg[14], (unsigned long long)c_rel);
-    atomicAdd((unsigned long long *)&dbg[15], (unsigned long long)c_ph_r);
     for (int q = 0; q < 4; q++) atomicAdd((unsigned long long *)&dbg[16 + q], (unsigned long long)c_l[q]);
+    atomicAdd((unsigned long long *)&dbg[20], (unsigned long long)n_bulk);
+    atomicAdd((unsigned long long *)&dbg[21], (unsigned long long)n_staged);
   }
 }
 
