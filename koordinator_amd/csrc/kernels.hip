@@ -1562,9 +1562,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         if (g >= n_pods) break;
         // ---- general path: pod g alone -- c, then every M and M' row's current key
         n_slow++;
-        // the pod record made wave-uniform: its fields steer the evaluation's
-        // branches, which must be scalar (a VGPR copy runs every path masked)
-        const DevPod pod = uniform_pod(lpod[g]);
+        const DevPod pod = lpod[g];  // VGPR copy: SGPRs are the scarce register file here (uniform_pod measured slower)
         const uint64_t *L = lk + (size_t)g * kp;
         const uint64_t e0 = lane < kp ? L[lane] : 0ull;
         const uint64_t e1 = (two && 64 + lane < kp) ? L[64 + lane] : 0ull;
