@@ -281,6 +281,30 @@ int koordhip_fetch_cpusets(koordhip_ctx *ctx, uint64_t *cpus, int32_t n_pods);
 int koordhip_last_stats(koordhip_ctx *ctx, double *eval_ms, int64_t *eval_launches, int64_t *evals,
                         double *total_ms);
 
+/* Per-kernel device time of the last place call (profile_kernels = 1: HIP
+ * event pairs on the stream each kernel is launched on): the evaluation
+ * (k_scan), the top-k selection (k_select_split / k_select) and the
+ * sequential resolve (k_resolve; one persistent launch per call unless the
+ * context is in a local group).  Roofline accounting in bench.py. */
+typedef struct koordhip_kernel_stats {
+  double scan_ms;
+  int64_t scan_launches;
+  double select_ms;
+  int64_t select_launches;
+  double resolve_ms;
+  int64_t resolve_launches;
+  double total_ms;   /* the place call, first to last event on the engine stream */
+  int64_t evals;     /* (pod, node) pairs evaluated by this rank */
+  int64_t pods;      /* pods of the staged stream */
+  int64_t rounds;    /* pipelined rounds */
+  int64_t reserved[4];
+} koordhip_kernel_stats;
+int koordhip_last_kernel_stats(koordhip_ctx *ctx, koordhip_kernel_stats *out);
+/* Turn the per-launch event timing on / off for later place calls (the
+ * events cost a few microseconds per round: bench.py times its steps with it
+ * off and takes the per-kernel split from one extra step). */
+int koordhip_set_profile_kernels(koordhip_ctx *ctx, int32_t on);
+
 /* ---- multi-GPU (node-index sharding, RCCL all-gather of per-shard top-k) -- */
 #define KOORDHIP_UNIQUE_ID_BYTES 128
 int koordhip_comm_unique_id(uint8_t *id_out /* KOORDHIP_UNIQUE_ID_BYTES */);

@@ -47,6 +47,15 @@ _u8p = C.POINTER(C.c_uint8)
 _u64p = C.POINTER(C.c_uint64)
 
 
+class KoordhipKernelStats(C.Structure):
+    """include/koordhip.h koordhip_kernel_stats"""
+    _fields_ = [("scan_ms", C.c_double), ("scan_launches", C.c_int64),
+                ("select_ms", C.c_double), ("select_launches", C.c_int64),
+                ("resolve_ms", C.c_double), ("resolve_launches", C.c_int64),
+                ("total_ms", C.c_double), ("evals", C.c_int64), ("pods", C.c_int64), ("rounds", C.c_int64),
+                ("reserved", C.c_int64 * 4)]
+
+
 class KoordhipConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32),
@@ -175,6 +184,8 @@ def load_library(path: str = LIB_PATH):
         "koordhip_read_numa": (C.c_int, [vp, _u64p, _u64p, _u64p, _i32p]),
         "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+        "koordhip_last_kernel_stats": (C.c_int, [vp, C.POINTER(KoordhipKernelStats)]),
+        "koordhip_set_profile_kernels": (C.c_int, [vp, C.c_int32]),
         "koordhip_comm_unique_id": (C.c_int, [C.c_char_p]),
         "koordhip_comm_init": (C.c_int, [vp, C.c_char_p, C.c_int32, C.c_int32]),
         "koordhip_comm_init_local": (C.c_int, [C.POINTER(vp), C.c_int32]),
@@ -194,7 +205,8 @@ EXPORTED_SYMBOLS = [
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
-    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_last_stats",
+    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_last_stats", "koordhip_last_kernel_stats",
+    "koordhip_set_profile_kernels",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]
 

@@ -144,7 +144,8 @@ struct koordhip_ctx {
   int32_t world = 1, rank = 0;
 
   // stats
-  std::vector<hipEvent_t> ev;  // pairs around eval launches (profile_kernels)
+  std::vector<hipEvent_t> ev;  // pairs around stream launches (profile_kernels)
+  std::vector<int8_t> ev_kind; // per pair: TK_SCAN / TK_SELECT / TK_RESOLVE
   hipEvent_t t0 = nullptr, t1 = nullptr;
   int32_t ev_used = 0;
   double last_eval_ms = 0, last_total_ms = 0;
@@ -258,6 +259,31 @@ int ensure(koordhip_ctx *c, void **p, size_t *cap, size_t bytes) {
   return 0;
 }
 
+// profile_kernels: HIP event pairs around the stream's launches, by kernel
+enum { TK_SCAN = 0, TK_SELECT = 1, TK_RESOLVE = 2, TK_KINDS = 3 };
+
+int timed_begin(koordhip_ctx *c, int kind, hipStream_t s, int32_t *idx) {
+  *idx = -1;
+  if (!c->cfg.profile_kernels) return 0;
+  if (c->ev_used + 2 > (int32_t)c->ev.size()) {
+    for (int i = 0; i < 1024; i++) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      c->ev.push_back(e);
+    }
+    c->ev_kind.resize(c->ev.size() / 2);
+  }
+  *idx = c->ev_used;
+  c->ev_kind[c->ev_used / 2] = (int8_t)kind;
+  c->ev_used += 2;
+  HIP_TRY(hipEventRecord(c->ev[*idx], s));
+  return 0;
+}
+int timed_end(koordhip_ctx *c, int32_t idx, hipStream_t s) {
+  if (idx >= 0) HIP_TRY(hipEventRecord(c->ev[idx + 1], s));
+  return 0;
+}
+
 // Exact per-pod top-k over node range [lo, hi) of np pods: k_scan fills the
 // score matrix, k_select reduces each row (best first, 0-padded).
 int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
@@ -271,22 +297,11 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
   if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial), &c->partial_cap, need)) return e;
   uint16_t *S = reinterpret_cast<uint16_t *>(c->d_partial);
   uint16_t *Mx = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(c->d_partial) + sbytes);
-  hipEvent_t *e0 = nullptr, *e1 = nullptr;
-  if (timed && c->cfg.profile_kernels) {
-    if (c->ev_used + 2 > (int32_t)c->ev.size()) {
-      for (int i = 0; i < 1024; i++) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
-        c->ev.push_back(e);
-      }
-    }
-    e0 = &c->ev[c->ev_used];
-    e1 = &c->ev[c->ev_used + 1];
-    c->ev_used += 2;
-    HIP_TRY(hipEventRecord(*e0, c->stream));
-  }
+  int32_t tm = -1;
+  if (timed)
+    if (int e = timed_begin(c, TK_SCAN, c->stream, &tm)) return e;
   HIP_TRY(kh::launch_scan(R, c->dc, c->d, d_pods, np, lo, hi, S, stride, Mx, mstride, c->stream));
-  if (e1) HIP_TRY(hipEventRecord(*e1, c->stream));
+  if (int e = timed_end(c, tm, c->stream)) return e;
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
   if (!c->sel_split) {
@@ -298,8 +313,11 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
     HIP_TRY(hipMalloc(&c->d_selcnt, kh::kSelMaxPods * sizeof(uint32_t)));
     HIP_TRY(hipMemsetAsync(c->d_selcnt, 0, kh::kSelMaxPods * sizeof(uint32_t), c->stream));
   }
+  if (timed)
+    if (int e = timed_begin(c, TK_SELECT, c->stream, &tm)) return e;
   HIP_TRY(kh::launch_select_split(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, c->sel_g, c->d_selpart,
                                   c->d_selcnt, out, sync, res_wait, c->stream));
+  if (int e = timed_end(c, tm, c->stream)) return e;
   return 0;
 }
 
@@ -1018,9 +1036,13 @@ int place_staged_impl(koordhip_ctx *c) {
   const int64_t list_buf = (int64_t)(lbytes / sizeof(uint64_t));
   uint64_t *lists0 = c->world > 1 ? c->d_final : c->d_lists;
   uint64_t *cpus = c->d_cpus;
-  if (persistent && rounds > 0)
+  if (persistent && rounds > 0) {
+    int32_t tm = -1;
+    if (int e = timed_begin(c, TK_RESOLVE, c->rstream, &tm)) return e;
     HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
+    if (int e = timed_end(c, tm, c->rstream)) return e;
+  }
   for (int32_t r = 0; r < rounds; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
     const kh::DevPod *pods = c->d_pods + p0;
@@ -1045,8 +1067,11 @@ int place_staged_impl(koordhip_ctx *c) {
         HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
         HIP_TRY(hipStreamWaitEvent(rs, c->ev_res[r % kRing], 0));
       }
+      int32_t tm = -1;
+      if (int e = timed_begin(c, TK_RESOLVE, rs, &tm)) return e;
       HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, sync,
                                  mbuf, c->d_out, cpus, c->d_dbg, trace, rs));
+      if (int e = timed_end(c, tm, rs)) return e;
     }
   }
   if (!serial) {
@@ -1230,6 +1255,7 @@ int koordhip_last_stats(koordhip_ctx *c, double *eval_ms, int64_t *eval_launches
   HIP_TRY(hipEventElapsedTime(&ms, c->t0, c->t1));
   double em = 0;
   for (int32_t i = 0; i + 1 < c->ev_used; i += 2) {
+    if (c->ev_kind[i / 2] != TK_SCAN) continue;
     float x = 0;
     HIP_TRY(hipEventElapsedTime(&x, c->ev[i], c->ev[i + 1]));
     em += x;
@@ -1238,6 +1264,41 @@ int koordhip_last_stats(koordhip_ctx *c, double *eval_ms, int64_t *eval_launches
   if (eval_launches) *eval_launches = c->last_launches;
   if (evals) *evals = c->last_evals;
   if (total_ms) *total_ms = ms;
+  return 0;
+}
+
+int koordhip_last_kernel_stats(koordhip_ctx *c, koordhip_kernel_stats *out) {
+  if (!c || !out) return fail(KOORDHIP_EINVAL, "NULL argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int e = pipe_status(c)) return e;
+  std::memset(out, 0, sizeof(*out));
+  double ms[TK_KINDS] = {0, 0, 0};
+  int64_t n[TK_KINDS] = {0, 0, 0};
+  for (int32_t i = 0; i + 1 < c->ev_used; i += 2) {
+    float x = 0;
+    HIP_TRY(hipEventElapsedTime(&x, c->ev[i], c->ev[i + 1]));
+    ms[c->ev_kind[i / 2]] += x;
+    n[c->ev_kind[i / 2]]++;
+  }
+  float tot = 0;
+  HIP_TRY(hipEventElapsedTime(&tot, c->t0, c->t1));
+  out->scan_ms = ms[TK_SCAN];
+  out->scan_launches = n[TK_SCAN];
+  out->select_ms = ms[TK_SELECT];
+  out->select_launches = n[TK_SELECT];
+  out->resolve_ms = ms[TK_RESOLVE];
+  out->resolve_launches = n[TK_RESOLVE];
+  out->total_ms = tot;
+  out->evals = c->last_evals;
+  out->pods = c->n_staged;
+  out->rounds = (c->n_staged + c->batch - 1) / std::max(c->batch, 1);
+  return 0;
+}
+
+int koordhip_set_profile_kernels(koordhip_ctx *c, int32_t on) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  c->cfg.profile_kernels = on ? 1 : 0;
   return 0;
 }
 

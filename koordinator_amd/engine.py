@@ -142,6 +142,15 @@ class PlacementEngine:
         abi.check(self.lib, self.lib.koordhip_last_stats(self._ctx, C.byref(em), C.byref(nl), C.byref(ne), C.byref(tm)))
         return {"eval_ms": em.value, "eval_launches": nl.value, "evals": ne.value, "total_ms": tm.value}
 
+    def set_profile_kernels(self, on: bool):
+        abi.check(self.lib, self.lib.koordhip_set_profile_kernels(self._ctx, 1 if on else 0))
+
+    def kernel_stats(self) -> dict:
+        """Per-kernel device time of the last place call (profile_kernels=True)."""
+        st = abi.KoordhipKernelStats()
+        abi.check(self.lib, self.lib.koordhip_last_kernel_stats(self._ctx, C.byref(st)))
+        return {f: getattr(st, f) for f, _ in abi.KoordhipKernelStats._fields_ if f != "reserved"}
+
     # ---- multi-GPU ----------------------------------------------------------
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -350,10 +350,12 @@ typedef void (*piece_fn)(void *arg, int32_t lo, int32_t hi);
 typedef struct pool {
   int32_t nthreads;
   pthread_t *tid;
-  _Atomic int64_t gen;      /* job generation */
-  _Atomic int32_t done;     /* workers finished this generation */
-  _Atomic int32_t next;     /* next piece */
-  _Atomic int32_t quit;
+  pthread_mutex_t mu;
+  pthread_cond_t work, idle;
+  int64_t gen;          /* job generation (under mu) */
+  int32_t done;         /* workers finished this generation (under mu) */
+  int32_t quit;
+  _Atomic int32_t next; /* next piece */
   int32_t pieces, chunk;
   piece_fn fn;
   void *arg;
@@ -378,19 +380,24 @@ static void run_pieces(pool *p) {
   }
 }
 
+/* Workers block between jobs (a goroutine pool parks the same way); spinning
+ * waiters would compete with the working threads for a shared CPU quota. */
 static void *worker(void *a) {
   pool *p = (pool *)a;
   int64_t seen = 0;
   for (;;) {
-    int64_t g;
-    int spins = 0;
-    while ((g = atomic_load(&p->gen)) == seen && !atomic_load(&p->quit)) {
-      if (++spins > 64) sched_yield();
+    pthread_mutex_lock(&p->mu);
+    while (p->gen == seen && !p->quit) pthread_cond_wait(&p->work, &p->mu);
+    if (p->quit) {
+      pthread_mutex_unlock(&p->mu);
+      return NULL;
     }
-    if (atomic_load(&p->quit)) return NULL;
-    seen = g;
+    seen = p->gen;
+    pthread_mutex_unlock(&p->mu);
     run_pieces(p);
-    atomic_fetch_add(&p->done, 1);
+    pthread_mutex_lock(&p->mu);
+    if (++p->done == p->nthreads - 1) pthread_cond_signal(&p->idle);
+    pthread_mutex_unlock(&p->mu);
   }
 }
 
@@ -398,6 +405,9 @@ static int pool_init(pool *p, int32_t nthreads) {
   memset(p, 0, sizeof(*p));
   p->nthreads = nthreads;
   if (nthreads <= 1) return 0;
+  pthread_mutex_init(&p->mu, NULL);
+  pthread_cond_init(&p->work, NULL);
+  pthread_cond_init(&p->idle, NULL);
   p->tid = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
   for (int32_t t = 0; t < nthreads - 1; t++) /* the caller is the last worker */
     if (pthread_create(&p->tid[t], NULL, worker, p)) return -1;
@@ -406,9 +416,15 @@ static int pool_init(pool *p, int32_t nthreads) {
 
 static void pool_free(pool *p) {
   if (p->nthreads > 1) {
-    atomic_store(&p->quit, 1);
+    pthread_mutex_lock(&p->mu);
+    p->quit = 1;
+    pthread_cond_broadcast(&p->work);
+    pthread_mutex_unlock(&p->mu);
     for (int32_t t = 0; t < p->nthreads - 1; t++) pthread_join(p->tid[t], NULL);
     free(p->tid);
+    pthread_mutex_destroy(&p->mu);
+    pthread_cond_destroy(&p->work);
+    pthread_cond_destroy(&p->idle);
   }
 }
 
@@ -424,12 +440,15 @@ static void pool_until(pool *p, int32_t pieces, piece_fn fn, void *arg) {
   p->fn = fn;
   p->arg = arg;
   atomic_store(&p->next, 0);
-  atomic_store(&p->done, 0);
-  atomic_fetch_add(&p->gen, 1);
+  pthread_mutex_lock(&p->mu);
+  p->done = 0;
+  p->gen++;
+  pthread_cond_broadcast(&p->work);
+  pthread_mutex_unlock(&p->mu);
   run_pieces(p);
-  int spins = 0;
-  while (atomic_load(&p->done) < p->nthreads - 1)
-    if (++spins > 64) sched_yield();
+  pthread_mutex_lock(&p->mu);
+  while (p->done < p->nthreads - 1) pthread_cond_wait(&p->idle, &p->mu);
+  pthread_mutex_unlock(&p->mu);
 }
 
 /* ------------------------------------------------------------------------ */

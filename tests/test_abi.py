@@ -43,6 +43,7 @@ PROBE = r"""
 int main(void) {
   printf("%zu %zu %zu %zu\n", sizeof(koordhip_config), sizeof(koordhip_node_soa), sizeof(koordhip_pod), sizeof(koordhip_topk));
   printf("%zu %zu %zu %zu\n", offsetof(koordhip_pod, est_mem), offsetof(koordhip_pod, flags), offsetof(koordhip_config, batch_pods), offsetof(koordhip_node_soa, la_flags));
+  printf("%zu %zu\n", sizeof(koordhip_kernel_stats), offsetof(koordhip_kernel_stats, rounds));
   return 0;
 }
 """
@@ -63,6 +64,8 @@ def test_struct_layout_matches_header():
     assert offs[1] == abi.POD_DTYPE.fields["flags"][1]
     assert offs[2] == abi.KoordhipConfig.batch_pods.offset
     assert offs[3] == abi.KoordhipNodeSoa.la_flags.offset
+    ks = [int(x) for x in lines[2].split()]
+    assert ks == [C.sizeof(abi.KoordhipKernelStats), abi.KoordhipKernelStats.rounds.offset]
 
 
 def test_create_rejects_bad_config_without_gpu():
