@@ -108,14 +108,19 @@ struct koordhip_ctx {
   int32_t n_classes = 0;
   kh::DevNumaClass *d_classes = nullptr;
   int32_t *d_rc = nullptr;     // k_commit status
-  uint64_t *d_partial = nullptr;  // score matrix of k_scan (u16 [pods][stride])
-  uint64_t *d_selpart = nullptr;  // k_select_split slice lists ([pods][G][k])
-  uint32_t *d_selcnt = nullptr;   // k_select_split arrival counters (zero between launches)
+  // per evaluation stream (rounds alternate between two): score matrix of
+  // k_scan (u16 [pods][stride]), k_select_split slice lists ([pods][G][k]) and
+  // arrival counters (zero between launches)
+  uint64_t *d_partial[2] = {nullptr, nullptr};
+  uint64_t *d_selpart[2] = {nullptr, nullptr};
+  uint32_t *d_selcnt[2] = {nullptr, nullptr};
   int32_t sel_g = kh::kSelGMax;   // workgroups per pod of k_select_split (KOORDHIP_SEL_G)
   int32_t n_cu = 256;             // device CU count
   bool cu_reserve = false;        // KOORDHIP_CU_RESERVE: CU-masked streams, CU 0 for the resolve
   bool sel_split = true;          // k_select_split; false (KOORDHIP_SELECT_ONEWG): k_select + signal kernel
-  size_t partial_cap = 0;
+  size_t partial_cap[2] = {0, 0};
+  hipStream_t stream2 = nullptr;  // second evaluation stream (odd rounds) of a single-GPU place call
+  hipEvent_t ev_eval2 = nullptr;
   uint64_t *d_lists = nullptr;   // [2][batch][k] (rank-local lists; double buffer: round parity)
   uint64_t *d_gather = nullptr;  // [world][batch][k]
   int32_t gather_world = 1;
@@ -284,40 +289,54 @@ int timed_end(koordhip_ctx *c, int32_t idx, hipStream_t s) {
   return 0;
 }
 
+// The evaluation buffers of one stream slot, sized for np pods over [lo, hi):
+// the score matrix + chunk maxima, the split select's slice lists and arrival
+// counters.  place_staged sizes them before it launches the persistent
+// resolve: an allocation (or a free) inside the round loop could wait for a
+// device that is busy with that resolve.
+int eval_buffers(koordhip_ctx *c, int32_t np, int32_t lo, int32_t hi, int slot, hipStream_t es) {
+  const int64_t stride = ((int64_t)(hi - lo) + 63) & ~63ll;
+  const int32_t nchunks = kh::scan_chunks(c->partial_r, lo, hi);
+  const int32_t mstride = (nchunks + 63) & ~63;
+  const size_t need = (size_t)np * stride * sizeof(uint16_t) + (size_t)np * mstride * sizeof(uint16_t) + 64;
+  if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial[slot]), &c->partial_cap[slot], need)) return e;
+  if (c->sel_split && !c->d_selcnt[slot]) {
+    HIP_TRY(hipMalloc(&c->d_selpart[slot], kh::kSelPartKeys * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_selcnt[slot], kh::kSelMaxPods * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(c->d_selcnt[slot], 0, kh::kSelMaxPods * sizeof(uint32_t), es));
+  }
+  return 0;
+}
+
 // Exact per-pod top-k over node range [lo, hi) of np pods: k_scan fills the
 // score matrix, k_select reduces each row (best first, 0-padded).
 int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
-               uint64_t *out, bool timed, kh::PipeSync *sync, int32_t res_wait) {
+               uint64_t *out, bool timed, kh::PipeSync *sync, int32_t sel_par, int32_t res_wait, hipStream_t es,
+               int slot) {
   const int R = c->partial_r;
   const int64_t stride = ((int64_t)(hi - lo) + 63) & ~63ll;
   const int32_t nchunks = kh::scan_chunks(R, lo, hi);
   const int32_t mstride = (nchunks + 63) & ~63;
   const size_t sbytes = (size_t)np * stride * sizeof(uint16_t);
-  const size_t need = sbytes + (size_t)np * mstride * sizeof(uint16_t) + 64;
-  if (int e = ensure(c, reinterpret_cast<void **>(&c->d_partial), &c->partial_cap, need)) return e;
-  uint16_t *S = reinterpret_cast<uint16_t *>(c->d_partial);
-  uint16_t *Mx = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(c->d_partial) + sbytes);
+  if (int e = eval_buffers(c, np, lo, hi, slot, es)) return e;
+  uint16_t *S = reinterpret_cast<uint16_t *>(c->d_partial[slot]);
+  uint16_t *Mx = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(c->d_partial[slot]) + sbytes);
   int32_t tm = -1;
   if (timed)
-    if (int e = timed_begin(c, TK_SCAN, c->stream, &tm)) return e;
-  HIP_TRY(kh::launch_scan(R, c->dc, c->d, d_pods, np, lo, hi, S, stride, Mx, mstride, c->stream));
-  if (int e = timed_end(c, tm, c->stream)) return e;
+    if (int e = timed_begin(c, TK_SCAN, es, &tm)) return e;
+  HIP_TRY(kh::launch_scan(R, c->dc, c->d, d_pods, np, lo, hi, S, stride, Mx, mstride, es));
+  if (int e = timed_end(c, tm, es)) return e;
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
   if (!c->sel_split) {
-    HIP_TRY(kh::launch_select(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, out, c->d_dbg, c->stream));
+    HIP_TRY(kh::launch_select(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, out, c->d_dbg, es));
     return 0;
   }
-  if (!c->d_selcnt) {
-    HIP_TRY(hipMalloc(&c->d_selpart, kh::kSelPartKeys * sizeof(uint64_t)));
-    HIP_TRY(hipMalloc(&c->d_selcnt, kh::kSelMaxPods * sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(c->d_selcnt, 0, kh::kSelMaxPods * sizeof(uint32_t), c->stream));
-  }
   if (timed)
-    if (int e = timed_begin(c, TK_SELECT, c->stream, &tm)) return e;
-  HIP_TRY(kh::launch_select_split(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, c->sel_g, c->d_selpart,
-                                  c->d_selcnt, out, sync, res_wait, c->stream));
-  if (int e = timed_end(c, tm, c->stream)) return e;
+    if (int e = timed_begin(c, TK_SELECT, es, &tm)) return e;
+  HIP_TRY(kh::launch_select_split(S, stride, lo, hi - lo, np, k, c->nbins, Mx, mstride, nchunks, c->sel_g,
+                                  c->d_selpart[slot], c->d_selcnt[slot], out, sync, sel_par, res_wait, es));
+  if (int e = timed_end(c, tm, es)) return e;
   return 0;
 }
 
@@ -540,10 +559,11 @@ int koordhip_destroy(koordhip_ctx *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_cols(c);
   for (void *p : c->ckpt) (void)hipFree(p);
-  for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial, (void *)c->d_lists,
+  for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial[0], (void *)c->d_partial[1], (void *)c->d_lists,
                   (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
                   (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc,
-                  (void *)c->d_selpart, (void *)c->d_selcnt, c->d_upd})
+                  (void *)c->d_selpart[0], (void *)c->d_selcnt[0], (void *)c->d_selpart[1], (void *)c->d_selcnt[1],
+                  c->d_upd})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -552,6 +572,11 @@ int koordhip_destroy(koordhip_ctx *c) {
     (void)hipStreamSynchronize(c->rstream);
     (void)hipStreamDestroy(c->rstream);
   }
+  if (c->stream2) {
+    (void)hipStreamSynchronize(c->stream2);
+    (void)hipStreamDestroy(c->stream2);
+  }
+  if (c->ev_eval2) (void)hipEventDestroy(c->ev_eval2);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
@@ -849,7 +874,7 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
       e = fail(KOORDHIP_EDEVICE, "eval_full launch");
       break;
     }
-    if (topk) e = topk_batch(c, dp, np, k, 0, n, dk, false, nullptr, 0);
+    if (topk) e = topk_batch(c, dp, np, k, 0, n, dk, false, nullptr, 0, 0, c->stream, 0);
     if (e) break;
     if (hipStreamSynchronize(c->stream) != hipSuccess) {
       e = fail(KOORDHIP_EDEVICE, "eval sync");
@@ -947,6 +972,13 @@ int group_agree(koordhip_ctx *c) {
 
 int place_staged_impl(koordhip_ctx *c);
 
+// every CU of the device as a hipExtStreamCreateWithCUMask mask
+std::vector<uint32_t> full_cu_mask(const koordhip_ctx *c) {
+  std::vector<uint32_t> m((size_t)(c->n_cu + 31) / 32, 0xffffffffu);
+  if (c->n_cu % 32) m.back() &= (1u << (c->n_cu % 32)) - 1u;
+  return m;
+}
+
 }  // namespace
 
 extern "C" {
@@ -974,11 +1006,16 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipMalloc(&c->d_final, 2 * lbytes));
     HIP_TRY(hipMalloc(&c->d_mod, (1 + kMaxBatch) * sizeof(int32_t) + kh::kPipeSyncBytes));
     HIP_TRY(hipMalloc(&c->d_desc, sizeof(kh::DevNodes)));
+    // The persistent resolve occupies its hardware queue for the whole call:
+    // a CU-masked stream gets a dedicated queue (HIP pools plain streams over
+    // GPU_MAX_HW_QUEUES queues, and an evaluation stream sharing the resolve's
+    // queue would wait behind it forever).  KOORDHIP_CU_RESERVE: CU 0 only.
     if (c->cu_reserve) {
       const uint32_t m0 = 1u;
       HIP_TRY(hipExtStreamCreateWithCUMask(&c->rstream, 1, &m0));
     } else {
-      HIP_TRY(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+      const std::vector<uint32_t> all = full_cu_mask(c);
+      HIP_TRY(hipExtStreamCreateWithCUMask(&c->rstream, (uint32_t)all.size(), all.data()));
     }
     for (int i = 0; i < kRing; i++) HIP_TRY(hipEventCreateWithFlags(&c->ev_res[i], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
@@ -1036,6 +1073,20 @@ int place_staged_impl(koordhip_ctx *c) {
   const int64_t list_buf = (int64_t)(lbytes / sizeof(uint64_t));
   uint64_t *lists0 = c->world > 1 ? c->d_final : c->d_lists;
   uint64_t *cpus = c->d_cpus;
+  // A lone single-GPU context alternates the rounds between two evaluation
+  // streams: round r+1's scan needs only round r-1's commits, so it runs while
+  // round r's select finishes (each stream keeps its own score matrix and
+  // select buffers; the resolve counts finished lists per round parity).
+  const bool two = persistent && c->world == 1 && c->sel_split && wait_kernel && !std::getenv("KOORDHIP_ONE_EVAL_STREAM");
+  if (two && !c->stream2) {
+    std::vector<uint32_t> m = full_cu_mask(c);  // its own queue too (see rstream)
+    if (c->cu_reserve) m[0] &= ~1u;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&c->stream2, (uint32_t)m.size(), m.data()));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_eval2, hipEventDisableTiming));
+  }
+  if (two) HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+  for (int slot = 0; slot < (two ? 2 : 1) && rounds > 0; slot++)
+    if (int e = eval_buffers(c, std::min(P, total), lo, hi, slot, slot ? c->stream2 : c->stream)) return e;
   if (persistent && rounds > 0) {
     int32_t tm = -1;
     if (int e = timed_begin(c, TK_RESOLVE, c->rstream, &tm)) return e;
@@ -1045,23 +1096,28 @@ int place_staged_impl(koordhip_ctx *c) {
   }
   for (int32_t r = 0; r < rounds; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
+    const int par = r & 1;
+    const int32_t cum = P * (r >> 1) + np;  // pods of the rounds of parity `par` up to r
+    hipStream_t es = (two && par) ? c->stream2 : c->stream;
+    const int slot = two ? par : 0;
     const kh::DevPod *pods = c->d_pods + p0;
-    uint64_t *lists = c->d_lists + (size_t)(r & 1) * list_buf;
+    uint64_t *lists = c->d_lists + (size_t)par * list_buf;
     const bool select_waits = c->sel_split && c->world == 1 && !wait_kernel;  // the previous select held the stream
-    if (r >= 2 && !serial && !select_waits) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, c->stream));
+    if (r >= 2 && !serial && !select_waits) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, es));
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, nullptr, 0)) return e;
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, nullptr, 0, 0, c->stream, 0)) return e;
       if (int e = exchange(c, lists, (size_t)P * K)) return e;
       HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits,
-                                    c->d_final + (size_t)(r & 1) * list_buf, c->stream));
+                                    c->d_final + (size_t)par * list_buf, c->stream));
     } else {
-      // the split select's merging workgroups count the round's pods into sync->sel_round themselves
-      // and hold the stream until round r - 1 is resolved (what the next scan needs)
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, c->sel_split ? sync : nullptr, wait_kernel ? 0 : r))
+      // the split select's merging workgroups count the round's pods into sync->sel[par] themselves
+      // (KOORDHIP_FOLD_WAIT: and hold the stream until round r - 1 is resolved, what the next scan needs)
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, c->sel_split ? sync : nullptr, par,
+                             wait_kernel ? 0 : r, es, slot))
         return e;
     }
-    if (c->world > 1 || !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, p0 + np, c->stream));
+    if (c->world > 1 || !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, par, cum, es));
     if (!persistent) {
       if (!serial) {
         HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
@@ -1073,6 +1129,10 @@ int place_staged_impl(koordhip_ctx *c) {
                                  mbuf, c->d_out, cpus, c->d_dbg, trace, rs));
       if (int e = timed_end(c, tm, rs)) return e;
     }
+  }
+  if (two) {
+    HIP_TRY(hipEventRecord(c->ev_eval2, c->stream2));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_eval2, 0));
   }
   if (!serial) {
     HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));
@@ -1098,6 +1158,8 @@ int place_staged_impl(koordhip_ctx *c) {
                  "general path: candidate+keys %llu  commit %llu\n",
                  (unsigned long long)h[16], (unsigned long long)h[17], (unsigned long long)h[18],
                  (unsigned long long)h[19]);
+    std::fprintf(stderr, "[koordhip stamps] general path detail: candidate %llu  row evaluations %llu\n",
+                 (unsigned long long)h[22], (unsigned long long)h[23]);
   }
   return 0;
 }
@@ -1112,7 +1174,7 @@ int pipe_status(koordhip_ctx *c) {
   c->pipe_check = false;
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
   int32_t err = 0;
-  HIP_TRY(hipMemcpy(&err, reinterpret_cast<int32_t *>(sync) + 2, sizeof(err), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&err, reinterpret_cast<int32_t *>(sync) + kh::kPipeSyncErrWord, sizeof(err), hipMemcpyDeviceToHost));
   if (err) {
     c->pipe_err = true;
     return fail(KOORDHIP_EDEVICE, kStall);

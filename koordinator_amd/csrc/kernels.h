@@ -33,7 +33,7 @@ hipError_t launch_select(const uint16_t *S, int64_t s_stride, int32_t lo, int32_
 // k_select_split: the same top-k with G workgroups per pod (row slices) and an
 // in-launch merge by each pod's last workgroup.  part: [n_pods][G][k] slice
 // lists (kSelPartKeys keys); cnt: kSelMaxPods arrival counters, zero before
-// the first launch (the kernel leaves them zero); sync: optional, sel_round
+// the first launch (the kernel leaves them zero); sync: optional, sel[sel_par]
 // += 1 per pod once its final list in `out` is published, and with res_wait >
 // 0 the launch does not end before res_round >= res_wait.
 struct PipeSync;
@@ -43,8 +43,8 @@ constexpr size_t kSelPartKeys = (size_t)kSelMaxPods * kSelGMax * 128;
 int32_t select_split_groups(int32_t m, int32_t G);
 hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,
                                int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, int32_t G,
-                               uint64_t *part, uint32_t *cnt, uint64_t *out, PipeSync *sync, int32_t res_wait,
-                               hipStream_t s);
+                               uint64_t *part, uint32_t *cnt, uint64_t *out, PipeSync *sync, int32_t sel_par,
+                               int32_t res_wait, hipStream_t s);
 // lists: ranges ascending with l, equal-score keys in ascending node order
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
                              int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s);
@@ -52,18 +52,20 @@ template <typename T>
 hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
 // The lag-1 round pipeline (kernels.hip): k_resolve resolves rounds [r_begin,
 // r_end) of the staged stream (P pods per round, k keys per list, lists double
-// buffered at lists0 + (r & 1) * list_buf); it waits for sel_round and
-// publishes res_round in `sync`; M' is handed between launches in mbuf
-// ({count, nodes}).  The evaluation stream brackets each round with
-// k_wait_resolved (before k_scan) and k_signal_lists (after the lists).
+// buffered at lists0 + (r & 1) * list_buf); it waits for sel[r & 1] (the
+// cumulative pods of the rounds of r's parity) and publishes res_round in
+// `sync`; M' is handed between launches in mbuf ({count, nodes}).  The
+// evaluation stream(s) bracket each round with k_wait_resolved (before k_scan)
+// and k_signal_lists (after the lists).
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
                           PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
                           int32_t trace, hipStream_t s);
 hipError_t launch_wait_resolved(PipeSync *sync, int32_t rounds, hipStream_t s);
-hipError_t launch_signal_lists(PipeSync *sync, int32_t rounds, hipStream_t s);
+hipError_t launch_signal_lists(PipeSync *sync, int32_t par, int32_t pods, hipStream_t s);
 constexpr size_t kPipeSyncBytes = 16;
+constexpr int kPipeSyncErrWord = 3;  // PipeSync {sel[2], res_round, err}: err's int32 index
 // single Reserve (sign +1, cpus <- allocated CPUs, *rc = KOORDHIP_ERESERVE on failure) / Unreserve (cpus given)
 hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const DevPod *pod, int32_t node, int32_t sign,
                          uint64_t *cpus, int32_t *rc, hipStream_t s);

@@ -719,13 +719,15 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
 // ---------------------------------------------------------------------------
 // Device-side handshake between the evaluation stream and the persistent
 // resolve kernel (one per koordhip_place_staged call):
-//   sel_round  pods of the stream whose final lists are ready (k_select_split's
+//   sel[b]     pods of the rounds with parity b whose final lists are ready
+//              (cumulative; rounds alternate between two evaluation streams, so
+//              a later round may finish first) (k_select_split's
 //              merging workgroups add 1 each; k_signal_lists stores the count
 //              after a separate merge)
 //   res_round  rounds resolved + written back (k_resolve, release store)
 //   err        a side gave up waiting (watchdog): the call fails, nothing hangs
 struct PipeSync {
-  int32_t sel_round, res_round, err, pad;
+  int32_t sel[2], res_round, err;
 };
 
 constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up
@@ -810,7 +812,7 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
     const uint16_t *__restrict__ S, int64_t s_stride, int32_t lo, int32_t m, int32_t k, int32_t nbins,
     const uint16_t *__restrict__ Mx, int32_t m_stride, int32_t nchunks, int32_t G, int32_t tiles_per,
     uint64_t *__restrict__ part, uint32_t *__restrict__ cnt, uint64_t *__restrict__ out, PipeSync *__restrict__ sy,
-    int32_t res_wait) {
+    int32_t sel_par, int32_t res_wait) {
   extern __shared__ __attribute__((aligned(16))) char spl_lds[];
   SplHdr &h = *reinterpret_cast<SplHdr *>(spl_lds);
   uint64_t *mk = reinterpret_cast<uint64_t *>(spl_lds + SPL_HDR);                    // merge: G x k keys
@@ -1007,7 +1009,7 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
     if (t == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(&sy->sel_round, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&sy->sel[sel_par], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // the next scan on this stream may read the node columns only once the
       // resolve has written back round res_wait - 1: the launch ends no earlier
       // (replaces a k_wait_resolved launch between this kernel and the scan)
@@ -1186,8 +1188,8 @@ __global__ void k_wait_resolved(PipeSync *sy, int32_t rounds) {
   if (threadIdx.x == 0) (void)wait_at_least(&sy->res_round, rounds, sy);
 }
 // Evaluation stream, after round r's lists are complete (kernel boundary = visible).
-__global__ void k_signal_lists(PipeSync *sy, int32_t rounds) {
-  if (threadIdx.x == 0) store_release(&sy->sel_round, rounds);
+__global__ void k_signal_lists(PipeSync *sy, int32_t par, int32_t pods) {
+  if (threadIdx.x == 0) store_release(&sy->sel[par], pods);
 }
 
 template <bool NUMA>
@@ -1294,6 +1296,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   uint64_t c_pro = 0, c_wait = 0, c_loop = 0, c_rel = 0, c_hash = 0;
   uint64_t c_l[4] = {0, 0, 0, 0};  // conflict detection, bulk commits, general-path candidate + keys, general commit
   uint64_t n_slow = 0, n_miss = 0, n_staged = 0, n_bulk = 0;
+  uint64_t c_g[2] = {0, 0};  // general path: candidate from the list, row evaluations (to the last value)
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
   auto load_round = [&](int32_t rr, int32_t rp0, int32_t rn, uint64_t *Lk, DevPod *Lp, NV *Pr, NumaRow *Pn,
@@ -1344,7 +1347,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     const bool preloaded = ofs.overlap && r > r_begin;
     const uint64_t t_w0 = (dbg && t == 0) ? stamp() : 0;
     if (!preloaded) {
-      if (t == 0 && !wait_at_least(&sy->sel_round, p0 + n_pods, sy)) sh_stop = 1;
+      if (t == 0 && !wait_at_least(&sy->sel[r & 1], P * (r >> 1) + n_pods, sy)) sh_stop = 1;
       __syncthreads();
     }
     if (sh_stop) return;  // the evaluation side failed: give up, the host reports it
@@ -1570,6 +1573,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         const bool x1 = e1 != 0 && xbit(modmap, key_node(e1));
         const uint64_t f0 = __ballot(e0 != 0 && !x0), f1 = __ballot(e1 != 0 && !x1);
         uint64_t best = f0 ? readlane_u64(e0, __builtin_ctzll(f0)) : (f1 ? readlane_u64(e1, __builtin_ctzll(f1)) : 0ull);
+        if (dbg) {
+          const uint64_t x = stamp();
+          c_g[0] += x - ts;
+          ts = x;
+        }
         const int32_t nrows = nm + mp;
         for (int32_t b0 = 0; b0 < nrows; b0 += 64) {  // rows: M slots, then the M' slots not moved into M
           const int32_t s = b0 + lane;
@@ -1582,6 +1590,10 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             NumaRow nr;
             if constexpr (NUMA) nr = pnr[s - nm];
             kv = make_key(eval_row<NUMA>(pod, slot_row(prow[s - nm]), nr, cls, c), pnode[s - nm]);
+          }
+          if (dbg) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            c_g[1] += stamp() - ts;
           }
           kv = wave_max_u64_dpp(kv);
           best = kv > best ? kv : best;
@@ -1718,7 +1730,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       //      (each wave waits for the lists itself: no barrier without wave 0)
       const int32_t np2 = min(P, total - (p0 + P));
       int ok = 1;
-      if (lane == 0) ok = wait_at_least(&sy->sel_round, p0 + P + np2, sy) ? 1 : 0;
+      if (lane == 0) ok = wait_at_least(&sy->sel[(r + 1) & 1], P * ((r + 1) >> 1) + np2, sy) ? 1 : 0;
       if (__builtin_amdgcn_readfirstlane(ok)) {
         load_round(r + 1, p0 + P, np2, lk2, lpod2, pre2, prenr2, pre_node2, t - 64, RES_THREADS - 64);
       } else if (lane == 0) {
@@ -1765,6 +1777,8 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     for (int q = 0; q < 4; q++) atomicAdd((unsigned long long *)&dbg[16 + q], (unsigned long long)c_l[q]);
     atomicAdd((unsigned long long *)&dbg[20], (unsigned long long)n_bulk);
     atomicAdd((unsigned long long *)&dbg[21], (unsigned long long)n_staged);
+    atomicAdd((unsigned long long *)&dbg[22], (unsigned long long)c_g[0]);
+    atomicAdd((unsigned long long *)&dbg[23], (unsigned long long)c_g[1]);
   }
 }
 
@@ -1900,8 +1914,8 @@ int32_t select_split_groups(int32_t m, int32_t G) {
 
 hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,
                                int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, int32_t G,
-                               uint64_t *part, uint32_t *cnt, uint64_t *out, PipeSync *sync, int32_t res_wait,
-                               hipStream_t s) {
+                               uint64_t *part, uint32_t *cnt, uint64_t *out, PipeSync *sync, int32_t sel_par,
+                               int32_t res_wait, hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   if (k < 1 || k > RES_MAXP || nbins < 2 || nbins > 32768 || n_pods > kSelMaxPods) return hipErrorInvalidValue;
   const int32_t ntiles = std::max<int32_t>(1, (m + SPL_TILE - 1) / SPL_TILE);
@@ -1920,7 +1934,7 @@ hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, 
     attr = true;
   }
   hipLaunchKernelGGL(k_select_split, dim3(G, n_pods), dim3(SPL_THREADS), lds, s, S, s_stride, lo, m, k, nbins, Mx,
-                     m_stride, nchunks, G, per, part, cnt, out, sync, res_wait);
+                     m_stride, nchunks, G, per, part, cnt, out, sync, sel_par, res_wait);
   return hipGetLastError();
 }
 
@@ -1972,8 +1986,8 @@ hipError_t launch_wait_resolved(PipeSync *sync, int32_t rounds, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_signal_lists(PipeSync *sync, int32_t rounds, hipStream_t s) {
-  hipLaunchKernelGGL(k_signal_lists, dim3(1), dim3(64), 0, s, sync, rounds);
+hipError_t launch_signal_lists(PipeSync *sync, int32_t par, int32_t pods, hipStream_t s) {
+  hipLaunchKernelGGL(k_signal_lists, dim3(1), dim3(64), 0, s, sync, par, pods);
   return hipGetLastError();
 }
 
