@@ -1158,8 +1158,9 @@ int place_staged_impl(koordhip_ctx *c) {
                  "general path: candidate+keys %llu  commit %llu\n",
                  (unsigned long long)h[16], (unsigned long long)h[17], (unsigned long long)h[18],
                  (unsigned long long)h[19]);
-    std::fprintf(stderr, "[koordhip stamps] general path detail: candidate %llu  row evaluations %llu\n",
-                 (unsigned long long)h[22], (unsigned long long)h[23]);
+    std::fprintf(stderr, "[koordhip stamps] general path detail: candidate + table keys %llu  row evaluations %llu | "
+                 "pods served by the key tables %llu\n",
+                 (unsigned long long)h[22], (unsigned long long)h[23], (unsigned long long)h[24]);
   }
   return 0;
 }

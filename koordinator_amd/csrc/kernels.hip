@@ -1086,7 +1086,7 @@ __device__ __forceinline__ NV slot_row(const NV &src) {
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
-      dec_key, dec_n, dec_src, dec_e, moved, mbits, classes, modmap, total;
+      dec_key, dec_n, dec_src, dec_e, moved, mbits, gbits, kpre, ktab, ready, classes, modmap, total;
   // second copies of the per-round inputs, filled by waves 1.. while wave 0
   // resolves the previous round (overlap = 0: every round loads serially)
   int32_t overlap, lists2, pods2, pre_rows2, pre_numa2, pre_node2;
@@ -1095,7 +1095,7 @@ struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
 
 __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, bool numa,
-                                          bool overlap = false) {
+                                          bool overlap = false, bool tables = true) {
   ResLds o;
   int32_t at = 0;
   const int32_t bitmap = res_align(((n_nodes + 31) >> 5) * 4);
@@ -1136,6 +1136,22 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * 4;
   o.mbits = at;  // M bitmap
   at += bitmap;
+  o.gbits = at;  // the nodes general-path pods committed to this round
+  at += bitmap;
+  // helper waves' key tables, per pod l (total + 1 as u16, 0 = infeasible):
+  // kpre[l][i] on the row staged pod i commits to (its staged source row +
+  // its Reserve delta), ktab[l][s] on M' row s; ready[l] once both are written
+  // (tables = false when they do not fit: kpre = -1, the general path then
+  // always evaluates and the helper waves idle)
+  o.kpre = o.ktab = -1;
+  o.ready = at;
+  at += RES_MAXP_ROUND * 4;
+  if (tables) {
+    o.kpre = at;
+    at += RES_MAXP_ROUND * RES_MAXP_ROUND * 2;
+    o.ktab = at;
+    at += RES_MAXP_ROUND * RES_MAXP_ROUND * 2;
+  }
   o.classes = at;  // NodeNUMAResource topology classes (when <= NUMA_LDS_CLASSES)
   at += numa ? NUMA_LDS_CLASSES * (int32_t)sizeof(DevNumaClass) : 0;
   o.modmap = at;  // X bitmap
@@ -1170,6 +1186,10 @@ __device__ __forceinline__ DevPod uniform_pod(const DevPod &src) {
   return p;
 }
 __device__ __forceinline__ bool xbit(const uint32_t *m, int32_t nd) { return (m[nd >> 5] >> (nd & 31)) & 1u; }
+// a key-table entry (total + 1, 0 = infeasible) -> the ranking key of node nd
+__device__ __forceinline__ uint64_t ktab_key(uint32_t v, int32_t nd) {
+  return v ? ((uint64_t)v << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)nd) : 0ull;
+}
 
 template <bool NUMA>
 __device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const NumaRow &nr,
@@ -1223,6 +1243,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   int32_t *dec_e = reinterpret_cast<int32_t *>(lds + ofs.dec_e);
   int32_t *moved = reinterpret_cast<int32_t *>(lds + ofs.moved);
   uint32_t *mbits = reinterpret_cast<uint32_t *>(lds + ofs.mbits);
+  uint32_t *gbits = reinterpret_cast<uint32_t *>(lds + ofs.gbits);
+  uint16_t *kpre = reinterpret_cast<uint16_t *>(lds + (ofs.kpre >= 0 ? ofs.kpre : 0));
+  uint16_t *ktab = reinterpret_cast<uint16_t *>(lds + (ofs.ktab >= 0 ? ofs.ktab : 0));
+  const bool have_tables = ofs.kpre >= 0;
+  int32_t *ready = reinterpret_cast<int32_t *>(lds + ofs.ready);
   uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
   // the next round's copies (ofs.overlap): swapped with the above every round
   uint64_t *lk2 = reinterpret_cast<uint64_t *>(lds + ofs.lists2);
@@ -1233,7 +1258,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous round committed to
   __shared__ int32_t seg_w[RES_MAXP_ROUND];  // staged winners by M slot (bulk commits)
   __shared__ int32_t ckey[RES_HASH], cval[RES_HASH];  // staged winner -> first pod (conflict detection)
-  __shared__ int32_t sh_mp, sh_stop;
+  __shared__ int32_t sh_mp, sh_stop, sh_done;
   const int t = threadIdx.x, lane = lane_id();
   const int32_t words = (n_nodes + 31) >> 5;
   const int32_t HP = max(1, RES_PRE / P);  // prefetched list heads per pod
@@ -1253,8 +1278,12 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   for (int32_t x = t; x < words; x += RES_THREADS) {
     modmap[x] = 0;
     mbits[x] = 0;
+    gbits[x] = 0;
   }
-  for (int32_t x = t; x < RES_MAXP_ROUND; x += RES_THREADS) moved[x] = 0;
+  for (int32_t x = t; x < RES_MAXP_ROUND; x += RES_THREADS) {
+    moved[x] = 0;
+    ready[x] = 0;
+  }
   for (int32_t x = t; x < RES_HASH; x += RES_THREADS) {
     ckey[x] = -1;
     cval[x] = 64;
@@ -1295,7 +1324,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   // diagnostics (KOORDHIP_STAMPS): cycles and counts per phase
   uint64_t c_pro = 0, c_wait = 0, c_loop = 0, c_rel = 0, c_hash = 0;
   uint64_t c_l[4] = {0, 0, 0, 0};  // conflict detection, bulk commits, general-path candidate + keys, general commit
-  uint64_t n_slow = 0, n_miss = 0, n_staged = 0, n_bulk = 0;
+  uint64_t n_slow = 0, n_miss = 0, n_staged = 0, n_bulk = 0, n_tab = 0;
   uint64_t c_g[2] = {0, 0};  // general path: candidate from the list, row evaluations (to the last value)
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
@@ -1355,6 +1384,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     const int32_t mp = sh_mp;
     if (!preloaded) load_round(r, p0, n_pods, lk, lpod, pre, prenr, pre_node, t, RES_THREADS);
     for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
+    if (t == 0) sh_done = 0;
     __syncthreads();
     if (t < mp) {  // M' hash: node -> slot, linear probing, lock-free inserts
       const int32_t nd = pnode[t];
@@ -1510,11 +1540,9 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           }
         }
       }
-      for (int32_t x = lane; x < RES_HASH; x += 64) {  // table empty again for the next round
-        ckey[x] = -1;
-        cval[x] = 64;
-      }
       uint64_t ok = __ballot(live && !slow && !conflict);  // staged decisions still valid
+      uint64_t cstaged = 0;                                 // pods committed with their staged decision
+      const uint64_t slowmask = __ballot(live && slow);
       int32_t j = 0;
       if (dbg) c_l[0] += stamp() - t_loop;
       while (j < n_pods) {
@@ -1558,6 +1586,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           const int32_t nc = __popcll(cb);
           if (lane >= nm && lane < nm + nc) my_node = seg_w[lane];
           nm += nc;
+          cstaged |= cb;
           n_staged += g - j;
           n_bulk++;
         }
@@ -1573,12 +1602,57 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         const bool x1 = e1 != 0 && xbit(modmap, key_node(e1));
         const uint64_t f0 = __ballot(e0 != 0 && !x0), f1 = __ballot(e1 != 0 && !x1);
         uint64_t best = f0 ? readlane_u64(e0, __builtin_ctzll(f0)) : (f1 ? readlane_u64(e1, __builtin_ctzll(f1)) : 0ull);
+        // Monotone pod whose key tables the helper waves have finished: only
+        // the X entries ranked above c can win, and their current keys are
+        // table entries unless a general-path pod changed their row.
+        bool tables = have_tables && monotone && !((slowmask >> g) & 1ull) &&
+                      __hip_atomic_load(&ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+        if (tables) {
+          const int first = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
+          bool need = false;
+          uint64_t kv = 0;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const uint64_t e = h ? e1 : e0;
+            const bool xh = h ? x1 : x0;
+            if (xh && 64 * h + lane < first) {
+              const int32_t y = key_node(e);
+              int32_t i = -1;  // the first staged pod that claimed y
+              uint32_t q = res_hash(y);
+              for (;;) {
+                const int32_t xk = ckey[q];
+                if (xk == y) {
+                  i = cval[q];
+                  break;
+                }
+                if (xk < 0) break;
+                q = (q + 1) & (RES_HASH - 1);
+              }
+              uint64_t k2 = 0;
+              if (i >= 0 && i < 64 && ((cstaged >> i) & 1ull) && !xbit(gbits, y)) {
+                k2 = ktab_key(kpre[g * RES_MAXP_ROUND + i], y);
+              } else {
+                const int32_t sl = mp > 0 ? prev_slot(y) : -1;
+                if (sl >= 0 && !moved[sl]) {
+                  k2 = ktab_key(ktab[g * RES_MAXP_ROUND + sl], y);
+                } else {
+                  need = true;
+                }
+              }
+              kv = k2 > kv ? k2 : kv;
+            }
+          }
+          kv = wave_max_u64_dpp(kv);
+          best = kv > best ? kv : best;
+          tables = __ballot(need) == 0;  // a row a general pod changed: evaluate the M rows
+          n_tab += tables;
+        }
         if (dbg) {
           const uint64_t x = stamp();
           c_g[0] += x - ts;
           ts = x;
         }
-        const int32_t nrows = nm + mp;
+        const int32_t nrows = tables ? 0 : nm + mp;
         for (int32_t b0 = 0; b0 < nrows; b0 += 64) {  // rows: M slots, then the M' slots not moved into M
           const int32_t s = b0 + lane;
           uint64_t kv = 0;
@@ -1670,6 +1744,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             if (lane < 18) x = (uint64_t)__double_as_longlong(__longlong_as_double((long long)xw) + dq);
             if (lane == 18) x += 1ull << 32;
             if (lane < RES_WORDS) reinterpret_cast<uint64_t *>(&mrow[rw])[lane] = x;
+            if (lane == 0) atomicOr(&gbits[w >> 5], 1u << (w & 31));
             if (!hit) {
               if (lane == rw) my_node = w;
               if (lane == 0) {
@@ -1703,12 +1778,19 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           store_numa_row(nr, nodes(), my_node);
         }
       }
+      if (lane == 0) __hip_atomic_store(&sh_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // helpers stop
       // X of the next round = M: clear the words of M' and M (every bit set in
-      // them is X's), then set M's bits; M's bitmap is cleared
+      // them is X's), then set M's bits; M's and the general pods' bitmaps are
+      // cleared (both are subsets of M), and the staged-winner claims
       if (lane < mp) modmap[pnode[lane] >> 5] = 0;
       if (lane < nm) {
         modmap[my_node >> 5] = 0;
         mbits[my_node >> 5] = 0;
+        gbits[my_node >> 5] = 0;
+      }
+      for (int32_t x = lane; x < RES_HASH; x += 64) {
+        ckey[x] = -1;
+        cval[x] = 64;
       }
       if (lane < nm) {
         atomicOr(&modmap[my_node >> 5], 1u << (my_node & 31));
@@ -1725,19 +1807,55 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         c_rel += t_end - t_rel;
         c_loop += t_end - t_loop;
       }
-    } else if (ofs.overlap && r + 1 < r_end && p0 + P < total) {
-      // ---- waves 1..: the next round's lists, pods and head rows, meanwhile
-      //      (each wave waits for the lists itself: no barrier without wave 0)
-      const int32_t np2 = min(P, total - (p0 + P));
-      int ok = 1;
-      if (lane == 0) ok = wait_at_least(&sy->sel[(r + 1) & 1], P * ((r + 1) >> 1) + np2, sy) ? 1 : 0;
-      if (__builtin_amdgcn_readfirstlane(ok)) {
-        load_round(r + 1, p0 + P, np2, lk2, lpod2, pre2, prenr2, pre_node2, t - 64, RES_THREADS - 64);
-      } else if (lane == 0) {
-        sh_stop = 1;
+    } else if (t < 128) {
+      if (ofs.overlap && r + 1 < r_end && p0 + P < total) {
+        // ---- wave 1: the next round's lists, pods and head rows, meanwhile
+        //      (it waits for the lists itself: no barrier without wave 0)
+        const int32_t np2 = min(P, total - (p0 + P));
+        int ok = 1;
+        if (lane == 0) ok = wait_at_least(&sy->sel[(r + 1) & 1], P * ((r + 1) >> 1) + np2, sy) ? 1 : 0;
+        if (__builtin_amdgcn_readfirstlane(ok)) {
+          load_round(r + 1, p0 + P, np2, lk2, lpod2, pre2, prenr2, pre_node2, lane, 64);
+        } else if (lane == 0) {
+          sh_stop = 1;
+        }
+      }
+    } else {
+      // ---- waves 2..: key tables for the general path, pod by pod (one pod
+      //      per wave: its record is wave-uniform), lanes over the rows --
+      //      kpre[l][i] on staged pod i's committed row, ktab[l][s] on M' row s
+      const int hw = __builtin_amdgcn_readfirstlane((t >> 6) - 2), nh = RES_THREADS / 64 - 2;
+      for (int32_t l = 1 + hw; have_tables && l < n_pods; l += nh) {
+        if (__hip_atomic_load(&sh_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        const DevPod pod = uniform_pod(lpod[l]);
+        for (int32_t b0 = 0; b0 < l + mp; b0 += 64) {
+          const int32_t x = b0 + lane;
+          int32_t v = 0;
+          if (x < l) {  // staged pod i = x
+            const uint64_t kk = dec_key[x];
+            if (kk != 0 && dec_n[x] >= 0) {
+              const int32_t src = dec_src[x];
+              NV row = src >= 0 ? pre[src] : prow[-src - 1];
+              NumaRow nr;
+              if constexpr (NUMA) nr = src >= 0 ? prenr[src] : pnr[-src - 1];
+              const DevPod pi = lpod[x];
+              apply_delta(row, pi, +1);
+              v = eval_row<NUMA>(pod, row, nr, cls, c) + 1;
+            }
+            kpre[l * RES_MAXP_ROUND + x] = (uint16_t)v;
+          } else if (x < l + mp) {  // M' slot s
+            const int32_t sl = x - l;
+            NumaRow nr;
+            if constexpr (NUMA) nr = pnr[sl];
+            v = eval_row<NUMA>(pod, slot_row(prow[sl]), nr, cls, c) + 1;
+            ktab[l * RES_MAXP_ROUND + sl] = (uint16_t)v;
+          }
+        }
+        if (lane == 0) __hip_atomic_store(&ready[l], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     __syncthreads();
+    for (int32_t x = t; x < RES_MAXP_ROUND; x += RES_THREADS) ready[x] = 0;
     if (ofs.overlap) {  // the next round's inputs become current
       uint64_t *a = lk;
       lk = lk2;
@@ -1778,6 +1896,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     atomicAdd((unsigned long long *)&dbg[20], (unsigned long long)n_bulk);
     atomicAdd((unsigned long long *)&dbg[21], (unsigned long long)n_staged);
     atomicAdd((unsigned long long *)&dbg[22], (unsigned long long)c_g[0]);
+    atomicAdd((unsigned long long *)&dbg[24], (unsigned long long)n_tab);
     atomicAdd((unsigned long long *)&dbg[23], (unsigned long long)c_g[1]);
   }
 }
@@ -1949,7 +2068,7 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa) {
   int32_t kp = 1;
   while (kp < k) kp <<= 1;
-  return res_lds(n_pods_max, kp, n_nodes, numa).total;
+  return res_lds(n_pods_max, kp, n_nodes, numa, false, false).total;
 }
 
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
@@ -1962,8 +2081,14 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   while (kp < k) kp <<= 1;
   const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
   // a persistent launch preloads round r+1 during round r when both copies fit
-  ResLds o = res_lds(P, kp, d.n, numa, r_end - r_begin > 1 && !std::getenv("KOORDHIP_NO_PRELOAD"));
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false);
+  // the largest layout that fits: key tables and the next round's preload,
+  // then without the preload, then without the tables
+  const bool pre = r_end - r_begin > 1 && !std::getenv("KOORDHIP_NO_PRELOAD");
+  const bool tab = !std::getenv("KOORDHIP_NO_KEY_TABLES");
+  ResLds o = res_lds(P, kp, d.n, numa, pre, tab);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, tab);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, pre, false);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, false);
   static bool attr[2] = {false, false};
   if (!attr[numa]) {
     const void *f = numa ? (const void *)k_resolve<true> : (const void *)k_resolve<false>;
