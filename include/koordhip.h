@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 2
+#define KOORDHIP_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -99,6 +99,19 @@ extern "C" {
  * (GetNUMAAllocateStrategy, nodenumaresource/util.go:34-40). */
 #define KOORDHIP_NODE_CPUBIND_MASK 3u   /* 0 None, 1 FullPCPUsOnly, 2 SpreadByPCPUs */
 #define KOORDHIP_NODE_NUMA_MOST_ALLOCATED 4u
+/* bits 3-4: the node's NUMA topology policy (getNUMATopologyPolicy: label
+ * node.koordinator.sh/numa-topology-policy over the NRT's policy,
+ * nodenumaresource/util.go; apis/extension/numa_aware.go:56-64) */
+#define KOORDHIP_NODE_NUMA_POLICY_SHIFT 3
+#define KOORDHIP_NODE_NUMA_POLICY(f) (((f) >> KOORDHIP_NODE_NUMA_POLICY_SHIFT) & 3u)
+#define KOORDHIP_NUMA_TOPO_NONE 0u
+#define KOORDHIP_NUMA_TOPO_BEST_EFFORT 1u
+#define KOORDHIP_NUMA_TOPO_RESTRICTED 2u
+#define KOORDHIP_NUMA_TOPO_SINGLE_NUMA_NODE 3u
+/* NUMA zones (NRT zones "node-<k>", zone k = NUMA node rank k) of a node with
+ * a topology policy: at most this many on the device (hint merge over <= 15
+ * masks per (pod, node)); the host rejects more. */
+#define KOORDHIP_NUMA_MAX_ZONES 4
 
 /* CPU topology of a node (cpu_topology.go:25-103), shared by every node of
  * the same shape.  CPU "positions" are core-major: pos = core_rank *
@@ -188,6 +201,14 @@ typedef struct koordhip_node_soa {
   const uint64_t *numa_excl_numa[KOORDHIP_NUMA_WORDS]; /* allocated CPUs whose ExclusivePolicy is NUMANodeLevel */
   const int32_t *numa_alloc_cnt;           /* |allocatedCPUs| (scoring.go:161-166) */
   const uint8_t *numa_flags;               /* KOORDHIP_NODE_* */
+  /* NUMA zone resources, [n][2][KOORDHIP_NUMA_MAX_NODES] row-major, [.][0][k] cpu
+   * (milli), [.][1][k] memory (bytes) of zone k: NRT zone allocatable
+   * (TopologyOptions.NUMANodeResources, topology_options.go:181-211) and the
+   * amounts allocated by pods (NodeAllocation.allocatedResources,
+   * node_allocation.go:76-103).  Read only for nodes with a topology policy;
+   * NULL when no node has one. */
+  const int64_t *numa_zone_alloc;
+  const int64_t *numa_zone_used;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -231,6 +252,9 @@ int koordhip_read_nodes(koordhip_ctx *ctx, int64_t *requested /* [NRES][n] */, i
 /* NodeNUMAResource mutable state: free / exclusive masks [WORDS][n], allocated CPU counts [n]. */
 int koordhip_read_numa(koordhip_ctx *ctx, uint64_t *free_mask, uint64_t *excl_pcpu, uint64_t *excl_numa,
                        int32_t *alloc_cnt);
+/* ... and the NUMA zone allocations, [n][2][KOORDHIP_NUMA_MAX_NODES] like numa_zone_used
+ * (rows of nodes without a topology policy read as 0: the engine does not keep them). */
+int koordhip_read_numa_zones(koordhip_ctx *ctx, int64_t *zone_used);
 
 /* Parity/debug mode, no commit: for n_pods pods against the current state.
  *   status : optional, [n_pods][n] KOORDHIP_ST_* bits (every plugin evaluated)

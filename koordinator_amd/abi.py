@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 2
+KOORDHIP_ABI_VERSION = 3
 NRES = 5
 NPLUGINS = 3
 
@@ -30,7 +30,10 @@ CPUBIND_NONE, CPUBIND_FULL_PCPUS, CPUBIND_SPREAD_BY_PCPUS = 0, 1, 2
 CPUEXCL_NONE, CPUEXCL_PCPU, CPUEXCL_NUMA = 0, 1, 2
 NODE_CPUBIND_NONE, NODE_CPUBIND_FULL_PCPUS_ONLY, NODE_CPUBIND_SPREAD_BY_PCPUS = 0, 1, 2
 NODE_NUMA_MOST_ALLOCATED = 4
+NODE_NUMA_POLICY_SHIFT = 3
+NUMA_TOPO_NONE, NUMA_TOPO_BEST_EFFORT, NUMA_TOPO_RESTRICTED, NUMA_TOPO_SINGLE_NUMA_NODE = 0, 1, 2, 3
 NUMA_MAX_CPUS, NUMA_MAX_NODES, NUMA_WORDS = 256, 8, 4
+NUMA_MAX_ZONES = 4
 
 
 def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> int:
@@ -38,7 +41,7 @@ def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> in
 
 ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL = 1, 2, 4
 UNSCHEDULABLE, RESERVE_FAILED = -1, -2
-E_RESERVE = -6
+E_INVAL, E_RESERVE = -1, -6
 UNIQUE_ID_BYTES = 128
 
 _i64p = C.POINTER(C.c_int64)
@@ -105,6 +108,8 @@ class KoordhipNodeSoa(C.Structure):
         ("numa_excl_numa", _u64p * NUMA_WORDS),
         ("numa_alloc_cnt", _i32p),
         ("numa_flags", _u8p),
+        ("numa_zone_alloc", _i64p),
+        ("numa_zone_used", _i64p),
     ]
 
 
@@ -182,6 +187,7 @@ def load_library(path: str = LIB_PATH):
         "koordhip_uncommit": (C.c_int, [vp, vp, C.c_int32, _u64p]),
         "koordhip_fetch_cpusets": (C.c_int, [vp, _u64p, C.c_int32]),
         "koordhip_read_numa": (C.c_int, [vp, _u64p, _u64p, _u64p, _i32p]),
+        "koordhip_read_numa_zones": (C.c_int, [vp, _i64p]),
         "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_last_kernel_stats": (C.c_int, [vp, C.POINTER(KoordhipKernelStats)]),
@@ -205,7 +211,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
-    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_last_stats", "koordhip_last_kernel_stats",
+    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_last_stats", "koordhip_last_kernel_stats",
     "koordhip_set_profile_kernels",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]

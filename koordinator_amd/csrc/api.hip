@@ -89,6 +89,7 @@ struct koordhip_ctx {
   int32_t n = 0;
   bool loaded = false;
   int32_t batch = kDefaultBatch;
+  int32_t last_P = 1;  // pods per round of the last place call (batch, LDS-clamped)
   int32_t monotone = 1;
   int32_t score_bits = 16;  // bits of (max total score + 1)
   int32_t nbins = 2;        // score histogram bins of k_select: max total score + 2
@@ -141,6 +142,7 @@ struct koordhip_ctx {
 
   // checkpoint of the mutable columns
   std::vector<void *> ckpt;
+  std::vector<kh::DevNumaClass> host_classes;  // the loaded topology classes (host copy)
 
   // sharding
   ncclComm_t comm = nullptr;
@@ -375,6 +377,33 @@ int build_numa_class(const koordhip_numa_class &t, kh::DevNumaClass &o) {
   return 0;
 }
 
+// NUMA zone rows [m][2][KOORDHIP_NUMA_MAX_NODES] int64 -> the device's
+// [m][2][KOORDHIP_NUMA_MAX_ZONES] f64; rows of topology-policy nodes are
+// checked (<= KOORDHIP_NUMA_MAX_ZONES NUMA nodes, exact quantities)
+int zone_rows(const int64_t *src, const int32_t *cls_of, const uint8_t *flags, const kh::DevNumaClass *cls, int32_t m,
+              std::vector<double> &out, bool *any_policy) {
+  constexpr int Z = KOORDHIP_NUMA_MAX_ZONES, NM = KOORDHIP_NUMA_MAX_NODES;
+  out.assign((size_t)m * 2 * Z, 0.0);
+  for (int32_t i = 0; i < m; i++) {
+    if (!KOORDHIP_NODE_NUMA_POLICY(flags[i])) continue;
+    *any_policy = true;
+    if (!src) return fail(KOORDHIP_EINVAL, "a node has a NUMA topology policy but numa_zone_alloc / numa_zone_used are NULL");
+    if (cls_of[i] >= 0 && cls[cls_of[i]].nnuma > Z)
+      return fail(KOORDHIP_EINVAL, "a node with a NUMA topology policy has more than 4 NUMA nodes");
+    for (int q = 0; q < 2; q++)
+      for (int k = 0; k < NM; k++) {
+        const int64_t v = src[((size_t)i * 2 + q) * NM + k];
+        if (!exact_ok(v)) return fail(KOORDHIP_EINVAL, "numa zone: quantity magnitude >= 2^45 is outside the engine's exact range");
+        if (k >= Z) {
+          if (v != 0) return fail(KOORDHIP_EINVAL, "numa zone: values past the node's NUMA nodes must be 0");
+          continue;
+        }
+        out[((size_t)i * 2 + q) * Z + k] = (double)v;
+      }
+  }
+  return 0;
+}
+
 int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   kh::DevNuma &nu = c->d.nu;
   nu = kh::DevNuma{};
@@ -434,6 +463,29 @@ int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   nu.node_cls = nc;
   nu.cnt = cnt;
   nu.nflags = nf;
+  // NUMA zones: kept when the snapshot carries the columns (a later
+  // update_nodes may give a node a topology policy); zones mode once any
+  // node has a policy
+  bool any = false;
+  c->dc.zones = 0;
+  if (!e && have) {
+    std::vector<double> za, zu;
+    e = zone_rows(s->numa_zone_alloc, s->numa_class, s->numa_flags, cls.data(), n, za, &any);
+    if (!e) e = zone_rows(s->numa_zone_used, s->numa_class, s->numa_flags, cls.data(), n, zu, &any);
+    if (!e && s->numa_zone_alloc && s->numa_zone_used) {
+      // rows of nodes without a policy are never read: converted as zeros
+      double *a = nullptr, *u = nullptr;
+      e = dev_alloc(c, &a, (size_t)n * 2 * KOORDHIP_NUMA_MAX_ZONES);
+      if (!e) e = dev_alloc(c, &u, (size_t)n * 2 * KOORDHIP_NUMA_MAX_ZONES);
+      if (!e) e = upload(c, a, za.data(), za.size());
+      if (!e) e = upload(c, u, zu.data(), zu.size());
+      if (!e) HIP_TRY(hipStreamSynchronize(c->stream));
+      nu.za = a;
+      nu.zu = u;
+    }
+    c->dc.zones = any ? 1 : 0;
+  }
+  c->host_classes = cls;
   return e;
 }
 
@@ -696,6 +748,20 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       if (rows->numa_class[j] >= c->n_classes)
         return fail(KOORDHIP_EINVAL, "numa_class index out of range (classes are fixed at load_snapshot)");
   }
+  std::vector<double> zrow_a, zrow_u;
+  bool zrows = false, zpolicy = false;
+  if (numa_rows) {
+    if (int e = zone_rows(rows->numa_zone_alloc, rows->numa_class, rows->numa_flags, c->host_classes.data(), m, zrow_a,
+                          &zpolicy))
+      return e;
+    if (int e = zone_rows(rows->numa_zone_used, rows->numa_class, rows->numa_flags, c->host_classes.data(), m, zrow_u,
+                          &zpolicy))
+      return e;
+    zrows = rows->numa_zone_alloc && rows->numa_zone_used;
+    if (zpolicy && !c->d.nu.za)
+      return fail(KOORDHIP_EINVAL, "a NUMA topology policy needs the zone columns at load_snapshot");
+    zrows = zrows && c->d.nu.za;
+  }
   // ---- one host staging image: [idx][column 0][column 1]..., 8-B aligned
   //      segments, quantities converted to the device's exact f64
   struct Col {
@@ -741,6 +807,11 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       cols.push_back({nu.en[w], rows->numa_excl_numa[w], 8, false, "numa_excl_numa"});
     }
   }
+  if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one 64-B element per row
+    kh::DevNuma &nu = c->d.nu;
+    cols.push_back({const_cast<double *>(nu.za), zrow_a.data(), 64, false, "numa_zone_alloc"});
+    cols.push_back({nu.zu, zrow_u.data(), 64, false, "numa_zone_used"});
+  }
   const size_t seg_idx = ((size_t)m * 4 + 7) & ~(size_t)7;
   size_t bytes = seg_idx;
   std::vector<size_t> off(cols.size());
@@ -779,7 +850,10 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   for (size_t q = 0; q < cols.size(); q++) {
     const Col &k = cols[q];
     const void *src = dev + off[q];
-    if (k.esize == 8)
+    if (k.esize == 64)
+      HIP_TRY(kh::launch_scatter<kh::ZoneRow>(static_cast<kh::ZoneRow *>(k.dst), static_cast<const kh::ZoneRow *>(src),
+                                              d_idx, m, c->stream));
+    else if (k.esize == 8)
       HIP_TRY(kh::launch_scatter<int64_t>(static_cast<int64_t *>(k.dst), static_cast<const int64_t *>(src), d_idx, m, c->stream));
     else if (k.esize == 4)
       HIP_TRY(kh::launch_scatter<int32_t>(static_cast<int32_t *>(k.dst), static_cast<const int32_t *>(src), d_idx, m, c->stream));
@@ -787,6 +861,7 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       HIP_TRY(kh::launch_scatter<uint8_t>(static_cast<uint8_t *>(k.dst), static_cast<const uint8_t *>(src), d_idx, m, c->stream));
   }
   c->dc.la_alias = alias ? 1 : 0;
+  if (zpolicy) c->dc.zones = 1;
   HIP_TRY(kh::launch_prep_flags(pi, d, d_idx, m, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));  // the host image may be reused by the next call
   return 0;
@@ -831,6 +906,24 @@ int koordhip_read_numa(koordhip_ctx *c, uint64_t *free_mask, uint64_t *excl_pcpu
     if (excl_numa) HIP_TRY(hipMemcpy(excl_numa + w * n, nu.en[w], b, hipMemcpyDeviceToHost));
   }
   if (alloc_cnt) HIP_TRY(hipMemcpy(alloc_cnt, nu.cnt, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int koordhip_read_numa_zones(koordhip_ctx *c, int64_t *zone_used) {
+  if (!c || !zone_used) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (!c->numa) return fail(KOORDHIP_ESTATE, "NodeNUMAResource is not enabled");
+  constexpr int Z = KOORDHIP_NUMA_MAX_ZONES, NM = KOORDHIP_NUMA_MAX_NODES;
+  const size_t n = c->n;
+  std::memset(zone_used, 0, n * 2 * NM * sizeof(int64_t));
+  if (n == 0 || !c->d.nu.zu) return 0;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  std::vector<double> zu(n * 2 * Z);
+  HIP_TRY(hipMemcpy(zu.data(), c->d.nu.zu, zu.size() * sizeof(double), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n; i++)
+    for (int q = 0; q < 2; q++)
+      for (int k = 0; k < Z; k++) zone_used[(i * 2 + q) * NM + k] = (int64_t)zu[(i * 2 + q) * Z + k];
   return 0;
 }
 
@@ -999,7 +1092,12 @@ int place_staged_impl(koordhip_ctx *c) {
   c->pipe_err = false;
   c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
-  const int32_t P = c->batch, K = 2 * c->batch;  // lag-1 needs k >= 2 x round size
+  // pods per round: batch_pods, lowered until the resolve kernel's LDS holds
+  // the round (NodeNUMAResource rows are large); lag-1 needs k >= 2 x round size
+  int32_t P = c->batch;
+  while (P > 1 && kh::resolve_lds_bytes(P, 2 * P, c->n, c->numa) > 157 * 1024) P--;
+  const int32_t K = 2 * P;
+  c->last_P = P;
   const size_t lbytes = (size_t)kMaxBatch * 2 * kMaxBatch * sizeof(uint64_t);
   if (!c->d_lists) {
     HIP_TRY(hipMalloc(&c->d_lists, 2 * lbytes));
@@ -1246,6 +1344,7 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
       v.push_back({nu.en[w], n * sizeof(uint64_t)});
     }
     v.push_back({nu.cnt, n * sizeof(int32_t)});
+    if (nu.zu) v.push_back({nu.zu, n * 2 * KOORDHIP_NUMA_MAX_ZONES * sizeof(double)});
   }
   return v;
 }
@@ -1297,6 +1396,8 @@ static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, i
   HIP_TRY(hipMemcpyAsync(&rc, c->d_rc, sizeof(rc), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(got, d_cpus, sizeof(got), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (rc == KOORDHIP_EINVAL)
+    return fail(rc, "Unreserve of a NodeNUMAResource pod on a NUMA topology-policy node (its zone amounts are not passed back)");
   if (rc) return fail(rc, "Reserve failed: NodeNUMAResource could not allocate the cpuset");
   if (sign > 0 && cpus_io) std::memcpy(cpus_io, got, sizeof(got));
   return 0;
@@ -1355,7 +1456,7 @@ int koordhip_last_kernel_stats(koordhip_ctx *c, koordhip_kernel_stats *out) {
   out->total_ms = tot;
   out->evals = c->last_evals;
   out->pods = c->n_staged;
-  out->rounds = (c->n_staged + c->batch - 1) / std::max(c->batch, 1);
+  out->rounds = (c->n_staged + c->last_P - 1) / std::max(c->last_P, 1);
   return 0;
 }
 

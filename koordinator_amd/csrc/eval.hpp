@@ -41,6 +41,7 @@ struct DevCfg {
   int32_t la_alias;   // la_alloc columns equal alloc cpu/mem columns (loaded once)
   int32_t numa_w_cpu, numa_w_mem;  // NodeNUMAResourceArgs scoring weights
   int32_t numa_most;               // NodeNUMAResource MostAllocated scoring strategy
+  int32_t zones;                   // some node has a NUMA topology policy (zone columns loaded)
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -72,6 +73,7 @@ struct NV {
 struct Need {
   bool pods, r_cpu, r_mem, eph, bcpu, bmem, a_cpu, a_mem, nz_cpu, nz_mem, la, la_nonprod, la_prod;
   bool numa, numa_masks;  // NUMA class (+ the cpuset masks for a cpuset pod)
+  bool zones;             // node flags + NUMA zones (topology-policy nodes)
 };
 
 __device__ __forceinline__ bool numa_on(const DevCfg &c) {
@@ -79,6 +81,11 @@ __device__ __forceinline__ bool numa_on(const DevCfg &c) {
 }
 __device__ __forceinline__ bool is_cpuset(const DevPod &p) {
   return (p.flags & KOORDHIP_POD_CPUSET) && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+}
+// NodeNUMAResource acts on this pod at Filter / Reserve on some node: a cpuset
+// pod, or any pod with requests once a node has a topology policy
+__device__ __forceinline__ bool numa_active(const DevPod &p, const DevCfg &c) {
+  return is_cpuset(p) || (c.zones && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
 }
 
 __device__ __forceinline__ Need pod_needs(const DevPod &p, const DevCfg &c) {
@@ -101,8 +108,9 @@ __device__ __forceinline__ Need pod_needs(const DevPod &p, const DevCfg &c) {
   n.la_nonprod = n.la && !n.la_prod;
   // NodeNUMAResource: Score reads Requested cpu/memory + Allocatable (scoring.go:104-106, :161-166)
   const bool ns = (c.score & KOORDHIP_PLUGIN_NUMA) && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
-  n.numa = ns || ((c.filt & KOORDHIP_PLUGIN_NUMA) && is_cpuset(p));
+  n.numa = ns || ((c.filt & KOORDHIP_PLUGIN_NUMA) && numa_active(p, c));
   n.numa_masks = numa_on(c) && is_cpuset(p);
+  n.zones = n.numa && c.zones && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
   if (ns) {
     n.r_cpu |= !is_cpuset(p);
     n.r_mem = true;
@@ -120,16 +128,33 @@ __device__ __forceinline__ Need need_all(const DevCfg &c) {
   n.la_nonprod = true;
   n.la_prod = c.according != 0;
   n.numa = n.numa_masks = numa_on(c);
+  n.zones = n.numa && c.zones;
   return n;
 }
 
 // NodeNUMAResource columns of node i.
+__device__ __forceinline__ void load_zones(NumaRow &r, const DevNodes &d, int32_t i) {
+  const double *za = d.nu.za + (size_t)i * 2 * ZMAX, *zu = d.nu.zu + (size_t)i * 2 * ZMAX;
+#pragma unroll
+  for (int q = 0; q < ZMAX; q++) {
+    r.za[0][q] = za[q];
+    r.za[1][q] = za[ZMAX + q];
+    r.zu[0][q] = zu[q];
+    r.zu[1][q] = zu[ZMAX + q];
+  }
+}
+
+template <bool Z>
 __device__ __forceinline__ void load_numa(NumaRow &r, const DevNodes &d, int32_t i, const Need &n) {
   r.cls = -1;
+  r.nflags = 0;
   if (!n.numa) return;
   r.cls = d.nu.node_cls[i];
+  if (n.numa_masks || (Z && n.zones)) r.nflags = d.nu.nflags[i];
+  if constexpr (Z) {
+    if (n.zones && topo_policy(r.nflags) != 0) load_zones(r, d, i);
+  }
   if (n.numa_masks) {
-    r.nflags = d.nu.nflags[i];
     r.cnt = d.nu.cnt[i];
 #pragma unroll
     for (int w = 0; w < NW; w++) {
@@ -306,6 +331,7 @@ __device__ __forceinline__ int32_t la_score(const DevPod &p, const NV &v, const 
 }
 
 // NodeNUMAResource Score (scoring.go:55-168).
+template <bool Z>
 __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, const NumaRow &r,
                                               const DevNumaClass *classes, const DevCfg &c) {
   if (p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0;
@@ -313,14 +339,44 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
   const bool most = c.numa_most != 0;  // leastResourceScorer / mostResourceScorer (scoring.go:35-53)
   auto lr = [most](double a, double b) { return most ? mrs(a, b) : lrs(a, b); };
   auto dw = [](int32_t a, int32_t b) { return div_weights(a, b); };
-  if (!(p.flags & KOORDHIP_POD_CPUSET))
+  const bool cs = (p.flags & KOORDHIP_POD_CPUSET) != 0;
+  const int tp = Z ? topo_policy(r.nflags) : 0;
+  if (!cs && tp == 0)
     return numa_la(v.r[KOORDHIP_RES_CPU] + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
                    v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM], v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem,
                    lr, dw);
-  if (!numa_alloc_ok(classes[r.cls], r, p)) return 0;
-  return numa_la((double)r.cnt * 1000.0 + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
-                 v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM], v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem,
-                 lr, dw);
+  const DevNumaClass &C = classes[r.cls];
+  double ac = v.a[KOORDHIP_RES_CPU], am = v.a[KOORDHIP_RES_MEM];
+  double rc = v.r[KOORDHIP_RES_CPU], rm = v.r[KOORDHIP_RES_MEM];
+  uint32_t mask = 0;
+  if (Z && tp != 0) {  // the affinity stored by Filter's admit, then Allocate with it (:80-89)
+    if (!zone_hint(C.nnuma, r, p, tp, &mask)) return 0;
+    if (mask) {
+      double z[2][ZMAX];
+      if (!zone_alloc(C.nnuma, r, p, mask, z)) return 0;
+      if (cs) {
+        uint64_t m[NW];
+        if (!(KOORDHIP_NUMA_REQUIRED(p.numa_policy) == KOORDHIP_CPUBIND_NONE ? zone_cpus_ok(C, r, p, z)
+                                                                              : zone_allocate(C, r, p, z, m)))
+          return 0;
+      }
+      // calculateAllocatableAndRequested over the pod's zones (:134-152)
+      ac = am = rc = rm = 0.0;
+#pragma unroll
+      for (int k = 0; k < ZMAX; k++)
+        if (zone_used(z, k)) {
+          ac += r.za[0][k];
+          am += r.za[1][k];
+          rc += r.zu[0][k];
+          rm += r.zu[1][k];
+        }
+    }
+  }
+  if (cs) {
+    if (!mask && !numa_alloc_ok(C, r, p)) return 0;
+    rc = (double)r.cnt * 1000.0;  // requested cpu := allocated cpuset size (:161-166)
+  }
+  return numa_la(rc + p.req[KOORDHIP_RES_CPU], ac, rm + p.req[KOORDHIP_RES_MEM], am, c.numa_w_cpu, c.numa_w_mem, lr, dw);
 }
 
 // Total weighted score, or -1 when any enabled Filter fails.
@@ -335,12 +391,13 @@ __device__ __forceinline__ int32_t eval_total(const DevPod &p, const NV &v, cons
 }
 
 // ... with NodeNUMAResource
+template <bool Z>
 __device__ __forceinline__ int32_t eval_total_numa(const DevPod &p, const NV &v, const NumaRow &r,
                                                    const DevNumaClass *classes, const DevCfg &c) {
   int32_t t = eval_total(p, v, c);
   if (t < 0) return t;
-  if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter(p, r, classes)) return -1;
-  if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score(p, v, r, classes, c);
+  if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter<Z>(p, r, classes)) return -1;
+  if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score<Z>(p, v, r, classes, c);
   return t;
 }
 
@@ -393,6 +450,7 @@ __device__ __forceinline__ void load_row(NV &v, const DevNodes &d, int32_t i) {
   v.flags = d.flags[i];
 }
 
+template <bool Z = true>
 __device__ __forceinline__ void load_numa_row(NumaRow &r, const DevNodes &d, int32_t i) {
   r.cls = d.nu.node_cls[i];
   r.nflags = d.nu.nflags[i];
@@ -403,8 +461,10 @@ __device__ __forceinline__ void load_numa_row(NumaRow &r, const DevNodes &d, int
     r.ep[w] = d.nu.ep[w][i];
     r.en[w] = d.nu.en[w][i];
   }
+  if (Z && d.nu.za && topo_policy(r.nflags) != 0) load_zones(r, d, i);
 }
 
+template <bool Z = true>
 __device__ __forceinline__ void store_numa_row(const NumaRow &r, const DevNodes &d, int32_t i) {
   d.nu.cnt[i] = r.cnt;
 #pragma unroll
@@ -412,6 +472,14 @@ __device__ __forceinline__ void store_numa_row(const NumaRow &r, const DevNodes 
     d.nu.fr[w][i] = r.fr[w];
     d.nu.ep[w][i] = r.ep[w];
     d.nu.en[w][i] = r.en[w];
+  }
+  if (Z && d.nu.za && topo_policy(r.nflags) != 0) {
+    double *zu = d.nu.zu + (size_t)i * 2 * ZMAX;
+#pragma unroll
+    for (int q = 0; q < ZMAX; q++) {
+      zu[q] = r.zu[0][q];
+      zu[ZMAX + q] = r.zu[1][q];
+    }
   }
 }
 
@@ -447,6 +515,42 @@ __device__ __forceinline__ void store_row(const NV &v, const DevNodes &d, int32_
   d.la_used_prod_cpu[i] = v.la_up_cpu;
   d.la_used_prod_mem[i] = v.la_up_mem;
   d.flags[i] = (uint8_t)v.flags;
+}
+
+// NodeNUMAResource Reserve on a row for a pod with numa_active(): the cpuset
+// (Allocate, resource_manager.go:142-164) and, on a topology-policy node, the
+// hinted zones' amounts (resourceManager.Update, node_allocation.go:76-103).
+// false = Allocate fails (nothing applied).
+template <bool Z>
+__device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *classes, NumaRow &r, const DevPod &p,
+                                                       uint64_t *cpus) {
+  for (int w = 0; w < NW; w++) cpus[w] = 0;
+  const bool cs = (p.flags & KOORDHIP_POD_CPUSET) != 0;
+  const int tp = Z ? topo_policy(r.nflags) : 0;
+  if (!cs && tp == 0) return true;
+  if (r.cls < 0) return false;
+  const DevNumaClass &C = classes[r.cls];
+  if (!Z || tp == 0) {
+    if (!numa_allocate(C, r, p, cpus)) return false;
+    numa_apply(r, p, cpus, +1);
+    return true;
+  }
+  uint32_t mask;
+  if (!zone_hint(C.nnuma, r, p, tp, &mask)) return false;
+  double z[2][ZMAX];
+  if (mask && !zone_alloc(C.nnuma, r, p, mask, z)) return false;
+  if (cs) {
+    if (!(mask ? zone_allocate(C, r, p, z, cpus) : numa_allocate(C, r, p, cpus))) return false;
+    numa_apply(r, p, cpus, +1);
+  }
+  if (mask) {
+#pragma unroll
+    for (int k = 0; k < ZMAX; k++) {
+      r.zu[0][k] += z[0][k];
+      r.zu[1][k] += z[1][k];
+    }
+  }
+  return true;
 }
 
 }  // namespace kh

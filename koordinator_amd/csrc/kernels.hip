@@ -167,19 +167,19 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
   NumaRow nr{};
-  load_numa(nr, d, i, all);
+  load_numa<true>(nr, d, i, all);
   if (status) {
     uint8_t b = 0;
     if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(pod, v)) b |= KOORDHIP_ST_FIT_FAIL;
     if ((c.filt & KOORDHIP_PLUGIN_LOADAWARE) && !la_filter(pod, v)) b |= KOORDHIP_ST_LA_FAIL;
-    if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter(pod, nr, d.nu.cls)) b |= KOORDHIP_ST_NUMA_FAIL;
+    if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter<true>(pod, nr, d.nu.cls)) b |= KOORDHIP_ST_NUMA_FAIL;
     status[(size_t)p * d.n + i] = b;
   }
   if (scores) {
     int32_t *row = scores + (size_t)p * KOORDHIP_NPLUGINS * d.n;
     row[i] = (c.score & KOORDHIP_PLUGIN_FIT) ? fit_score(pod, v, c) : 0;
     row[(size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_LOADAWARE) ? la_score(pod, v, c) : 0;
-    row[2 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_NUMA) ? numa_score(pod, v, nr, d.nu.cls, c) : 0;
+    row[2 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_NUMA) ? numa_score<true>(pod, v, nr, d.nu.cls, c) : 0;
   }
 }
 
@@ -387,7 +387,9 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 // XCD's 4 MB L2 then holds its eighth of the node table (50k nodes: ~0.5 MB)
 // and the 4 x (pods/4) re-reads of a row hit L2 instead of the MALL.
 
-template <int R, bool NUMA>
+// NM: 0 = no NodeNUMAResource, 1 = NodeNUMAResource, 2 = ... with
+// topology-policy nodes (the zone code is compiled only here)
+template <int R, int NM>
 __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
                                               int32_t lo, int32_t hi, int32_t nchunks, int32_t cpx,
                                               uint16_t *__restrict__ S, int64_t s_stride,
@@ -398,7 +400,7 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
   const int32_t pg = local / cpx;
   if (chunk >= nchunks) return;  // block-uniform
   const DevNumaClass *cls = d.nu.cls;
-  if constexpr (NUMA) {  // topology classes -> LDS (launch_scan sizes it when ncls <= NUMA_LDS_CLASSES)
+  if constexpr (NM != 0) {  // topology classes -> LDS (launch_scan sizes it when ncls <= NUMA_LDS_CLASSES)
     extern __shared__ uint4 scan_cls[];
     if (d.nu.ncls <= NUMA_LDS_CLASSES) {
       const uint4 *src = reinterpret_cast<const uint4 *>(d.nu.cls);
@@ -427,10 +429,10 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
     if (full || i < hi) {
       NV v;
       load_node(v, d, i, need, c);
-      if constexpr (NUMA) {
+      if constexpr (NM != 0) {
         NumaRow nr;
-        load_numa(nr, d, i, need);
-        s[r] = eval_total_numa(pod, v, nr, cls, c) + 1;
+        load_numa<NM == 2>(nr, d, i, need);
+        s[r] = eval_total_numa<NM == 2>(pod, v, nr, cls, c) + 1;
       } else {
         s[r] = eval_total(pod, v, c) + 1;
       }
@@ -1053,8 +1055,8 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
 
 // Wave 0 runs the sequential loop with a lot of state in registers: 8 waves
 // (4 for NUMA builds) keep 256 (512) VGPRs available to it.
-template <bool NUMA>
-constexpr int res_threads() { return NUMA ? 256 : 512; }
+template <int NM>
+constexpr int res_threads() { return NM ? 256 : 512; }
 
 constexpr int RES_PRE = 128;    // prefetched rows of list heads (RES_PRE / round size per pod)
 constexpr int RES_HASH = 256;   // node -> M' slot (open addressing)
@@ -1103,9 +1105,10 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += res_align(n_pods_max * kp * 8);
   o.pods = at;
   at += res_align(n_pods_max * (int32_t)sizeof(DevPod));
-  // two row regions, M' (prev) and M (cur), swapped at the end of every round
-  const int32_t rows_b = res_align(RES_MAXP_ROUND * (int32_t)sizeof(NV));
-  const int32_t numa_b = numa ? res_align(RES_MAXP_ROUND * (int32_t)sizeof(NumaRow)) : 0;
+  // two row regions, M' (prev) and M (cur), swapped at the end of every round;
+  // a round commits to at most n_pods_max nodes
+  const int32_t rows_b = res_align(n_pods_max * (int32_t)sizeof(NV));
+  const int32_t numa_b = numa ? res_align(n_pods_max * (int32_t)sizeof(NumaRow)) : 0;
   o.prev_rows = at;
   o.prev_numa = at + rows_b;
   at += rows_b + numa_b;
@@ -1191,11 +1194,11 @@ __device__ __forceinline__ uint64_t ktab_key(uint32_t v, int32_t nd) {
   return v ? ((uint64_t)v << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)nd) : 0ull;
 }
 
-template <bool NUMA>
+template <int NM>
 __device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const NumaRow &nr,
                                             const DevNumaClass *cls, const DevCfg &c) {
-  if constexpr (NUMA) {
-    return eval_total_numa(p, v, nr, cls, c);
+  if constexpr (NM != 0) {
+    return eval_total_numa<NM == 2>(p, v, nr, cls, c);
   } else {
     (void)nr;
     (void)cls;
@@ -1212,8 +1215,8 @@ __global__ void k_signal_lists(PipeSync *sy, int32_t par, int32_t pods) {
   if (threadIdx.x == 0) store_release(&sy->sel[par], pods);
 }
 
-template <bool NUMA>
-__global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const DevNodes *__restrict__ dn, int32_t n_nodes,
+template <int NM>
+__global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const DevNodes *__restrict__ dn, int32_t n_nodes,
                                                                  const DevNumaClass *__restrict__ ncls, const DevPod *__restrict__ pods,
                                                                  int32_t total, int32_t P, int32_t k, int32_t kp,
                                                                  int32_t r_begin, int32_t r_end,
@@ -1223,7 +1226,8 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
                                                                  ResLds ofs, int32_t *__restrict__ out_node,
                                                                  uint64_t *__restrict__ out_cpus,
                                                                  uint64_t *__restrict__ dbg, int32_t trace) {
-  constexpr int RES_THREADS = res_threads<NUMA>();
+  constexpr int RES_THREADS = res_threads<NM>();
+  constexpr bool NUMA = NM != 0, ZONES = NM == 2;
   (void)trace;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   uint64_t *lk = reinterpret_cast<uint64_t *>(lds + ofs.lists);
@@ -1272,7 +1276,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
   };
   const bool two = kp > 64;
   if (t == 0) {
-    sh_mp = r_begin > 0 ? min(mbuf[0], (int32_t)RES_MAXP_ROUND) : 0;
+    sh_mp = r_begin > 0 ? min(mbuf[0], P) : 0;
     sh_stop = 0;
   }
   for (int32_t x = t; x < words; x += RES_THREADS) {
@@ -1307,7 +1311,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
     prow[t] = v;
     if constexpr (NUMA) {
       NumaRow rr;
-      load_numa_row(rr, nodes(), nd);
+      load_numa_row<ZONES>(rr, nodes(), nd);
       pnr[t] = rr;
     }
     atomicOr(&modmap[nd >> 5], 1u << (nd & 31));
@@ -1353,7 +1357,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         Pr[sl] = v;
         if constexpr (NUMA) {
           NumaRow rr2;
-          load_numa_row(rr2, nodes(), nd);
+          load_numa_row<ZONES>(rr2, nodes(), nd);
           Pn[sl] = rr2;
         }
       }
@@ -1422,7 +1426,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         if (q < min(f, z)) {  // an M' entry: its exact key on the current row
           const int32_t s = prev_slot(nd);
           const DevPod pod = lpod[l];
-          key = make_key(eval_row<NUMA>(pod, slot_row(prow[s]), pnr[s], cls, c), nd);
+          key = make_key(eval_row<NM>(pod, slot_row(prow[s]), pnr[s], cls, c), nd);
         } else {
           key = e;
         }
@@ -1462,7 +1466,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
             pre[ps] = v;
             if constexpr (NUMA) {
               NumaRow nr;
-              load_numa_row(nr, nodes(), w);
+              load_numa_row<ZONES>(nr, nodes(), w);
               prenr[ps] = nr;
             }
             pre_node[ps] = w;
@@ -1506,7 +1510,9 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
       // not monotone), a walk longer than RES_WE entries
       bool slow = !monotone || sn < 0;
       if constexpr (NUMA) {
-        slow = slow || (numa_on(c) && (fl & KOORDHIP_POD_CPUSET) &&
+        // (with topology-policy nodes every NUMA pod: its zone hint can move
+        // to emptier zones as a node fills, so its score is not monotone)
+        slow = slow || (numa_on(c) && ((fl & KOORDHIP_POD_CPUSET) || c.zones) &&
                         !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
       }
       // ---- conflicts among the staged decisions: pod l's walk met the staged
@@ -1659,11 +1665,11 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           if (s < nm) {
             NumaRow nr;
             if constexpr (NUMA) nr = mnr[s];
-            kv = make_key(eval_row<NUMA>(pod, slot_row(mrow[s]), nr, cls, c), my_node);
+            kv = make_key(eval_row<NM>(pod, slot_row(mrow[s]), nr, cls, c), my_node);
           } else if (s < nrows && !moved[s - nm]) {
             NumaRow nr;
             if constexpr (NUMA) nr = pnr[s - nm];
-            kv = make_key(eval_row<NUMA>(pod, slot_row(prow[s - nm]), nr, cls, c), pnode[s - nm]);
+            kv = make_key(eval_row<NM>(pod, slot_row(prow[s - nm]), nr, cls, c), pnode[s - nm]);
           }
           if (dbg) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1703,7 +1709,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
                 mrow[rw] = v;
                 if constexpr (NUMA) {
                   NumaRow nr;
-                  load_numa_row(nr, nodes(), w);
+                  load_numa_row<ZONES>(nr, nodes(), w);
                   mnr[rw] = nr;
                 }
               }
@@ -1711,18 +1717,15 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
           }
           bool okr = true;
           if constexpr (NUMA) {
-            if (numa_on(c) && is_cpuset(pod)) {
-              // NodeNUMAResource Reserve: lane 0 replays the accumulator on the
-              // row, the chosen CPUs are broadcast to the wave
+            if (numa_on(c) && numa_active(pod, c)) {
+              // NodeNUMAResource Reserve: lane 0 replays the accumulator (and the
+              // zone hint) on the row, the chosen CPUs are broadcast to the wave
               uint64_t mc[NW] = {0, 0, 0, 0};
               int okl = 0;
               if (lane == 0) {
                 NumaRow nr = *snr;
-                okl = nr.cls >= 0 && numa_allocate(cls[nr.cls], nr, pod, mc);
-                if (okl) {
-                  numa_apply(nr, pod, mc, +1);
-                  mnr[rw] = nr;
-                }
+                okl = numa_reserve<ZONES>(cls, nr, pod, mc);
+                if (okl) mnr[rw] = nr;
               }
               okr = __builtin_amdgcn_readfirstlane(okl) != 0;
 #pragma unroll
@@ -1775,7 +1778,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
         store_row(v, nodes(), my_node);
         if constexpr (NUMA) {
           const NumaRow nr = mnr[lane];
-          store_numa_row(nr, nodes(), my_node);
+          store_numa_row<ZONES>(nr, nodes(), my_node);
         }
       }
       if (lane == 0) __hip_atomic_store(&sh_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // helpers stop
@@ -1840,14 +1843,14 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(DevCfg c, const
               if constexpr (NUMA) nr = src >= 0 ? prenr[src] : pnr[-src - 1];
               const DevPod pi = lpod[x];
               apply_delta(row, pi, +1);
-              v = eval_row<NUMA>(pod, row, nr, cls, c) + 1;
+              v = eval_row<NM>(pod, row, nr, cls, c) + 1;
             }
             kpre[l * RES_MAXP_ROUND + x] = (uint16_t)v;
           } else if (x < l + mp) {  // M' slot s
             const int32_t sl = x - l;
             NumaRow nr;
             if constexpr (NUMA) nr = pnr[sl];
-            v = eval_row<NUMA>(pod, slot_row(prow[sl]), nr, cls, c) + 1;
+            v = eval_row<NM>(pod, slot_row(prow[sl]), nr, cls, c) + 1;
             ktab[l * RES_MAXP_ROUND + sl] = (uint16_t)v;
           }
         }
@@ -1909,19 +1912,22 @@ __global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, i
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const DevPod p = *pod;
   *rc = 0;
-  if (numa_on(c) && is_cpuset(p)) {
+  if (numa_on(c) && numa_active(p, c)) {
     NumaRow r;
     load_numa_row(r, d, node);
     uint64_t m[NW];
     if (sign > 0) {
-      if (r.cls < 0 || !numa_allocate(d.nu.cls[r.cls], r, p, m)) {
+      if (!numa_reserve<true>(d.nu.cls, r, p, m)) {
         *rc = KOORDHIP_ERESERVE;  // Reserve fails: nothing is committed
         return;
       }
-    } else {
+    } else if (topo_policy(r.nflags) != 0) {
+      *rc = KOORDHIP_EINVAL;  // the zone amounts of the Reserve are not passed back
+      return;
+    } else if (is_cpuset(p)) {
       for (int w = 0; w < NW; w++) m[w] = cpus[w];
+      numa_apply(r, p, m, sign);
     }
-    numa_apply(r, p, m, sign);
     store_numa_row(r, d, node);
     if (sign > 0)
       for (int w = 0; w < NW; w++) cpus[w] = m[w];
@@ -1955,6 +1961,7 @@ hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, h
 template hipError_t launch_scatter<int64_t>(int64_t *, const int64_t *, const int32_t *, int32_t, hipStream_t);
 template hipError_t launch_scatter<int32_t>(int32_t *, const int32_t *, const int32_t *, int32_t, hipStream_t);
 template hipError_t launch_scatter<uint8_t>(uint8_t *, const uint8_t *, const int32_t *, int32_t, hipStream_t);
+template hipError_t launch_scatter<ZoneRow>(ZoneRow *, const ZoneRow *, const int32_t *, int32_t, hipStream_t);
 
 hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t *rows, int32_t m, hipStream_t s) {
   if (m <= 0) return hipSuccess;
@@ -1983,19 +1990,26 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
 #define KH_SCAN(RR, NN)                                                                                            \
   hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, S, \
                      s_stride, Mx, m_stride)
-  if (numa) {
+  if (numa && c.zones) {
     switch (R) {
-      case 1: KH_SCAN(1, true); break;
-      case 2: KH_SCAN(2, true); break;
-      case 4: KH_SCAN(4, true); break;
+      case 1: KH_SCAN(1, 2); break;
+      case 2: KH_SCAN(2, 2); break;
+      case 4: KH_SCAN(4, 2); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (numa) {
+    switch (R) {
+      case 1: KH_SCAN(1, 1); break;
+      case 2: KH_SCAN(2, 1); break;
+      case 4: KH_SCAN(4, 1); break;
       default: return hipErrorInvalidValue;
     }
   } else {
     switch (R) {
-      case 1: KH_SCAN(1, false); break;
-      case 2: KH_SCAN(2, false); break;
-      case 4: KH_SCAN(4, false); break;
-      case 8: KH_SCAN(8, false); break;
+      case 1: KH_SCAN(1, 0); break;
+      case 2: KH_SCAN(2, 0); break;
+      case 4: KH_SCAN(4, 0); break;
+      case 8: KH_SCAN(8, 0); break;
       default: return hipErrorInvalidValue;
     }
   }
@@ -2089,20 +2103,25 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, tab);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, pre, false);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, false);
-  static bool attr[2] = {false, false};
-  if (!attr[numa]) {
-    const void *f = numa ? (const void *)k_resolve<true> : (const void *)k_resolve<false>;
+  const int nm = numa ? (c.zones ? 2 : 1) : 0;
+  static bool attr[3] = {false, false, false};
+  if (!attr[nm]) {
+    const void *f = nm == 2 ? (const void *)k_resolve<2> : (nm == 1 ? (const void *)k_resolve<1> : (const void *)k_resolve<0>);
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS_MAX);
     if (e != hipSuccess) return e;
-    attr[numa] = true;
+    attr[nm] = true;
   }
   if (o.total > RES_LDS_MAX) return hipErrorInvalidValue;
-  if (numa)
-    hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(res_threads<true>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, k, kp,
-                       r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace);
+#define KH_RESOLVE(NN)                                                                                                \
+  hipLaunchKernelGGL(k_resolve<NN>, dim3(1), dim3(res_threads<NN>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, \
+                     k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace)
+  if (nm == 2)
+    KH_RESOLVE(2);
+  else if (nm == 1)
+    KH_RESOLVE(1);
   else
-    hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(res_threads<false>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, k, kp,
-                       r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace);
+    KH_RESOLVE(0);
+#undef KH_RESOLVE
   return hipGetLastError();
 }
 

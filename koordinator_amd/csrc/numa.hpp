@@ -1,5 +1,6 @@
-// numa.hpp -- NodeNUMAResource on CDNA4 (NUMA topology policy None,
-// maxRefCount 1, no reservation-preferred CPUs, cpus_per_core 1 or 2).
+// numa.hpp -- NodeNUMAResource on CDNA4 (maxRefCount 1, no
+// reservation-preferred CPUs, cpus_per_core 1 or 2; NUMA topology policies
+// None / BestEffort / Restricted / SingleNUMANode over <= 4 NUMA zones).
 //
 // Node state is a handful of 4 x 64-bit masks over core-major CPU positions
 // (pos = core_rank * cpc + t), so a core is an aligned group of cpc bits:
@@ -36,6 +37,7 @@ namespace kh {
 
 constexpr int NW = KOORDHIP_NUMA_WORDS;
 constexpr int NMAX = KOORDHIP_NUMA_MAX_NODES;
+constexpr int ZMAX = KOORDHIP_NUMA_MAX_ZONES;
 
 struct DevNumaClass {
   int32_t ncpu, cpc, cpn, cps, nnuma, nsock;
@@ -49,10 +51,14 @@ static_assert(sizeof(DevNumaClass) % 16 == 0, "classes are staged in LDS as 16-B
 
 struct NumaRow {
   int32_t cls;     // -1: no CPU topology
-  uint32_t nflags; // KOORDHIP_NODE_*
+  uint32_t nflags; // KOORDHIP_NODE_* (0 unless loaded)
   int32_t cnt;     // allocated CPUs
   int32_t pad;
   uint64_t fr[NW], ep[NW], en[NW];
+  // NUMA zones of a node with a topology policy (zone k = NUMA node rank k):
+  // NRT allocatable and NodeAllocation.allocatedResources, [cpu milli, memory][zone]
+  double za[2][ZMAX];
+  double zu[2][ZMAX];
 };
 
 struct DevNuma {
@@ -61,8 +67,18 @@ struct DevNuma {
   const uint8_t *nflags;
   uint64_t *fr[NW], *ep[NW], *en[NW];
   int32_t *cnt;
-  int32_t ncls;  // topology classes at cls
+  const double *za;  // [n][2][ZMAX], NULL when no node has a topology policy
+  double *zu;        // [n][2][ZMAX]
+  int32_t ncls;      // topology classes at cls
 };
+
+struct ZoneRow {  // one node's [2][ZMAX] zone row (update_nodes scatter element)
+  double v[2 * ZMAX];
+};
+
+__device__ __forceinline__ int topo_policy(uint32_t nflags) {
+  return (int)KOORDHIP_NODE_NUMA_POLICY(nflags);
+}
 
 // Kernels stage up to this many topology classes in LDS (800 B each): the
 // accumulator's loops and the closed-form Filter read them with dependent,
@@ -189,12 +205,21 @@ __device__ __forceinline__ bool numa_alloc_ok(const DevNumaClass &C, const NumaR
                         (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0);
 }
 
-// Filter, plugin.go:266-324; true = passes.
+__device__ __forceinline__ bool numa_policy_ok(const DevNumaClass &C, const NumaRow &r, const DevPod &p);
+
+// Filter, plugin.go:266-324; true = passes.  Z = false: no node has a
+// topology policy (the zone code is compiled out).
+template <bool Z>
 __device__ __forceinline__ bool numa_filter(const DevPod &p, const NumaRow &r, const DevNumaClass *classes) {
   if (p.flags & KOORDHIP_POD_NUMA_ERROR) return false;
-  if ((p.flags & KOORDHIP_POD_NUMA_SKIP) || !(p.flags & KOORDHIP_POD_CPUSET)) return true;
-  if (r.cls < 0) return false;
+  const int tp = Z ? topo_policy(r.nflags) : 0;
+  const bool cs = (p.flags & KOORDHIP_POD_CPUSET) != 0;
+  if ((p.flags & KOORDHIP_POD_NUMA_SKIP) || (!cs && tp == 0)) return true;  // skipTheNode, util.go:59-61
+  if (r.cls < 0) return false;  // no CPU topology (a policy node: getResourceOptions fails in Allocate)
   const DevNumaClass &C = classes[r.cls];
+  if constexpr (Z) {
+    if (!cs) return numa_policy_ok(C, r, p);
+  }
   const int req = (int)KOORDHIP_NUMA_REQUIRED(p.numa_policy);
   const bool full_only = (r.nflags & KOORDHIP_NODE_CPUBIND_MASK) == 1u;
   if (full_only || req == (int)KOORDHIP_CPUBIND_FULL_PCPUS) {
@@ -202,6 +227,9 @@ __device__ __forceinline__ bool numa_filter(const DevPod &p, const NumaRow &r, c
     if (full_only && (req != (int)KOORDHIP_CPUBIND_FULL_PCPUS ||
                       (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy) != (int)KOORDHIP_CPUBIND_FULL_PCPUS))
       return false;
+  }
+  if constexpr (Z) {
+    if (tp != 0) return numa_policy_ok(C, r, p);
   }
   if (req != (int)KOORDHIP_CPUBIND_NONE) return numa_alloc_ok(C, r, p);
   return true;
@@ -596,14 +624,12 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
   return a.need < 1;
 }
 
-// Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
-__device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
-  for (int w = 0; w < NW; w++) cpus[w] = 0;
-  const int need = p.numa_cpus;
-  if (popc4(r.fr) < need) return false;
+// takeCPUs over the available set A (cpu_accumulator.go:87-232) into out[]
+__device__ __attribute__((noinline)) bool acc_run(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                                  const uint64_t *A, int need, uint64_t *out) {
   Acc a;
   for (int w = 0; w < NW; w++) {
-    a.A[w] = r.fr[w];
+    a.A[w] = A[w];
     a.R[w] = 0;
     a.XC[w] = fold_or(r.ep[w], C.cpc);
   }
@@ -614,15 +640,174 @@ __device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, c
   a.excl = (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy);
   a.most = (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) ? 1 : 0;
   const int pol = node_policy(r.nflags, (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy));
-  if (!acc_take_cpus(C, a, pol)) return false;
-  if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE) {  // satisfiedRequiredCPUBindPolicy
-    int n = popc4(a.R), cores = 0;
-    for (int w = 0; w < NW; w++) cores += __popcll(fold_or(a.R[w], C.cpc));
-    if (pol == (int)KOORDHIP_CPUBIND_FULL_PCPUS && cores * C.cpc != n) return false;
-    if (pol == (int)KOORDHIP_CPUBIND_SPREAD_BY_PCPUS && cores != n) return false;
-  }
-  for (int w = 0; w < NW; w++) cpus[w] = a.R[w];
+  const bool ok = acc_take_cpus(C, a, pol);
+  for (int w = 0; w < NW; w++) out[w] = a.R[w];
+  return ok;
+}
+
+// satisfiedRequiredCPUBindPolicy (resource_manager.go:442-463) on the result
+__device__ __forceinline__ bool required_ok(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                            const uint64_t *R) {
+  if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) == KOORDHIP_CPUBIND_NONE) return true;
+  const int pol = node_policy(r.nflags, (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy));
+  int n = popc4(R), cores = 0;
+  for (int w = 0; w < NW; w++) cores += __popcll(fold_or(R[w], C.cpc));
+  if (pol == (int)KOORDHIP_CPUBIND_FULL_PCPUS && cores * C.cpc != n) return false;
+  if (pol == (int)KOORDHIP_CPUBIND_SPREAD_BY_PCPUS && cores != n) return false;
   return true;
+}
+
+// Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
+__device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
+  for (int w = 0; w < NW; w++) cpus[w] = 0;
+  const int need = p.numa_cpus;
+  if (popc4(r.fr) < need) return false;
+  uint64_t R[NW];
+  if (!acc_run(C, r, p, r.fr, need, R)) return false;
+  if (!required_ok(C, r, p, R)) return false;
+  for (int w = 0; w < NW; w++) cpus[w] = R[w];
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// NUMA topology policies (frameworkext/topologymanager, topology_hint.go,
+// resource_manager.go:142-242,384-428).  The plugin is the only hint
+// provider; its hints for cpu and memory (the requested ones) are the same
+// list S of zone masks whose summed availability covers the request,
+// preferred = minimal size.  Merging one hint per list (policy.go:52-208) then
+// has a closed form: with one list the narrowest minimal mask, with two the
+// narrowest non-empty AND of two minimal masks; no list or an empty S is a
+// provider without preference ({default affinity, preferred}).
+
+// getAvailableNUMANodeResources: allocatable - allocated, non-negative
+__device__ __forceinline__ double zone_avail(const NumaRow &r, int res, int k) {
+  const double a = r.za[res][k] - r.zu[res][k];
+  return a > 0.0 ? a : 0.0;
+}
+
+// bitmask.IsNarrowerThan order as one integer (masks < 16)
+__device__ __forceinline__ int narrow_key(uint32_t m) { return __popc(m) * 16 + (int)m; }
+
+// Merge + canAdmitPodResult for policy tp; *mask = the hint (0 = nil affinity)
+__device__ __forceinline__ bool zone_hint(int M, const NumaRow &r, const DevPod &p, int tp, uint32_t *mask) {
+  const double qc = p.req[KOORDHIP_RES_CPU], qm = p.req[KOORDHIP_RES_MEM];
+  const bool rc = qc != 0.0, rm = qm != 0.0;
+  const uint32_t all = (1u << M) - 1u;
+  uint32_t S = 0;
+  int minsize = M;
+  for (uint32_t m = 1; m <= all; m++) {  // generateResourceHints :384-428
+    double sc = 0.0, sm = 0.0;
+    for (int k = 0; k < ZMAX; k++)
+      if ((m >> k) & 1u) {
+        sc += zone_avail(r, 0, k);
+        sm += zone_avail(r, 1, k);
+      }
+    if ((!rc || qc <= sc) && (!rm || qm <= sm)) {
+      S |= 1u << m;
+      minsize = min(minsize, __popc(m));
+    }
+  }
+  if ((!rc && !rm) || S == 0) {  // no hints: {default, preferred}
+    *mask = tp == (int)KOORDHIP_NUMA_TOPO_SINGLE_NUMA_NODE ? 0u : all;
+    return true;
+  }
+  if (tp == (int)KOORDHIP_NUMA_TOPO_SINGLE_NUMA_NODE) {  // policy_single_numa_node.go:37-78
+    if (minsize != 1) return false;                        // nothing survives the filter: {default, false}
+    uint32_t best = 0;
+    for (int k = M - 1; k >= 0; k--)
+      if ((S >> (1u << k)) & 1u) best = 1u << k;
+    *mask = best == all ? 0u : best;
+    return true;
+  }
+  uint32_t best = all;
+  int bk = 1 << 30;
+  for (uint32_t a = 1; a <= all; a++) {
+    if (!((S >> a) & 1u) || __popc(a) != minsize) continue;
+    if (!(rc && rm)) {
+      if (narrow_key(a) < bk) {
+        bk = narrow_key(a);
+        best = a;
+      }
+      continue;
+    }
+    for (uint32_t b = 1; b <= all; b++) {
+      if (!((S >> b) & 1u) || __popc(b) != minsize || !(a & b)) continue;
+      if (narrow_key(a & b) < bk) {
+        bk = narrow_key(a & b);
+        best = a & b;
+      }
+    }
+  }
+  *mask = best;
+  return true;  // preferred: BestEffort and Restricted admit
+}
+
+// allocateResourcesByHint (:166-242): the hinted zones in ascending id take
+// min(available, still requested) of cpu and memory
+__device__ __forceinline__ bool zone_alloc(int M, const NumaRow &r, const DevPod &p, uint32_t mask, double z[2][ZMAX]) {
+  double rem[2] = {p.req[KOORDHIP_RES_CPU], p.req[KOORDHIP_RES_MEM]};
+#pragma unroll
+  for (int k = 0; k < ZMAX; k++) {
+    z[0][k] = 0.0;
+    z[1][k] = 0.0;
+    if (k < M && ((mask >> k) & 1u)) {
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const double av = zone_avail(r, q, k);
+        const double a = av < rem[q] ? av : rem[q];
+        z[q][k] = a;
+        rem[q] -= a;
+      }
+    }
+  }
+  return rem[0] == 0.0 && rem[1] == 0.0;
+}
+
+__device__ __forceinline__ bool zone_used(const double z[2][ZMAX], int k) { return z[0][k] != 0.0 || z[1][k] != 0.0; }
+
+// allocateCPUSet with allocated NUMA nodes (:264-295): zone k takes
+// min(|its available CPUs|, floor(cpu_k / 1000)) CPUs; the sum must be exact.
+// Preferred-only: takeCPUs never fails below |available| (closed form).
+__device__ __forceinline__ bool zone_cpus_ok(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                             const double z[2][ZMAX]) {
+  if (popc4(r.fr) < p.numa_cpus) return false;
+  int got = 0;
+  for (int k = 0; k < C.nnuma && k < ZMAX; k++)
+    if (zone_used(z, k)) got += min(popc_and(r.fr, C.nm[k]), (int)((long long)z[0][k] / 1000));
+  return got == p.numa_cpus;
+}
+
+// ... exact CPUs (Reserve, and Filter / Score under a required policy)
+__device__ __attribute__((noinline)) bool zone_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                                        const double z[2][ZMAX], uint64_t *cpus) {
+  for (int w = 0; w < NW; w++) cpus[w] = 0;
+  if (popc4(r.fr) < p.numa_cpus) return false;
+  int got = 0;
+  for (int k = 0; k < C.nnuma && k < ZMAX; k++) {
+    if (!zone_used(z, k)) continue;
+    uint64_t A[NW], o[NW];
+    for (int w = 0; w < NW; w++) A[w] = r.fr[w] & C.nm[k][w];
+    const int n = min(popc4(A), (int)((long long)z[0][k] / 1000));
+    if (n <= 0) continue;
+    if (!acc_run(C, r, p, A, n, o)) return false;
+    for (int w = 0; w < NW; w++) cpus[w] |= o[w];
+    got += popc4(o);
+  }
+  if (got != p.numa_cpus) return false;
+  return required_ok(C, r, p, cpus);
+}
+
+// Filter's FilterByNUMANode -> Admit -> Allocate on a policy node (topology_hint.go:30-86)
+__device__ __forceinline__ bool numa_policy_ok(const DevNumaClass &C, const NumaRow &r, const DevPod &p) {
+  uint32_t mask;
+  if (!zone_hint(C.nnuma, r, p, topo_policy(r.nflags), &mask)) return false;
+  double z[2][ZMAX];
+  if (mask && !zone_alloc(C.nnuma, r, p, mask, z)) return false;
+  if (!(p.flags & KOORDHIP_POD_CPUSET)) return true;
+  if (!mask) return numa_alloc_ok(C, r, p);
+  if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) == KOORDHIP_CPUBIND_NONE) return zone_cpus_ok(C, r, p, z);
+  uint64_t m[NW];
+  return zone_allocate(C, r, p, z, m);
 }
 
 }  // namespace kh

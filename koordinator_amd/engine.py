@@ -129,7 +129,9 @@ class PlacementEngine:
         cnt = np.zeros(n, np.int32)
         abi.check(self.lib, self.lib.koordhip_read_numa(self._ctx, abi.ptr(fr, C.c_uint64), abi.ptr(ep, C.c_uint64),
                                                         abi.ptr(en, C.c_uint64), abi.ptr(cnt, C.c_int32)))
-        return {"free": fr, "excl_pcpu": ep, "excl_numa": en, "alloc_cnt": cnt}
+        zu = np.zeros((n, 2, abi.NUMA_MAX_NODES), np.int64)
+        abi.check(self.lib, self.lib.koordhip_read_numa_zones(self._ctx, abi.ptr(zu, C.c_int64)))
+        return {"free": fr, "excl_pcpu": ep, "excl_numa": en, "alloc_cnt": cnt, "zone_used": zu}
 
     def fetch_cpusets(self, n: int) -> np.ndarray:
         out = np.zeros((n, abi.NUMA_WORDS), np.uint64)

@@ -252,6 +252,36 @@ def node_numa_flags(labels: Dict[str, str], kubelet_policy: Optional[dict], defa
     most = default_most_allocated if strat == "" else strat == "MostAllocated"
     if most:
         f |= abi.NODE_NUMA_MOST_ALLOCATED
-    if labels.get(LABEL_NUMA_TOPOLOGY_POLICY, "") not in ("", "None"):
-        raise TopologyError("NUMA topology policy other than None is not supported by this engine version")
+    f |= numa_topology_policy(labels, kubelet_policy) << abi.NODE_NUMA_POLICY_SHIFT
     return f
+
+
+NUMA_TOPOLOGY_POLICIES = {"": abi.NUMA_TOPO_NONE, "BestEffort": abi.NUMA_TOPO_BEST_EFFORT,
+                          "Restricted": abi.NUMA_TOPO_RESTRICTED, "SingleNUMANode": abi.NUMA_TOPO_SINGLE_NUMA_NODE}
+
+
+def numa_topology_policy(labels: Dict[str, str], nrt_policy: Optional[dict] = None) -> int:
+    """getNUMATopologyPolicy (nodenumaresource/util.go:51-57): the node label
+    node.koordinator.sh/numa-topology-policy, else the NRT's kubelet topology
+    manager policy (convertToNUMATopologyPolicy, topology_options.go:213-225)."""
+    lab = labels.get(LABEL_NUMA_TOPOLOGY_POLICY, "")
+    if lab not in NUMA_TOPOLOGY_POLICIES:
+        # createNUMATopologyPolicy (manager.go:112-123) has no policy for it: the
+        # reference would dereference a nil Policy
+        raise TopologyError(f"unknown NUMA topology policy {lab!r}")
+    if lab:
+        return NUMA_TOPOLOGY_POLICIES[lab]
+    tm = (nrt_policy or {}).get("topologyManagerPolicy", "")
+    return {"best-effort": abi.NUMA_TOPO_BEST_EFFORT, "restricted": abi.NUMA_TOPO_RESTRICTED,
+            "single-numa-node": abi.NUMA_TOPO_SINGLE_NUMA_NODE}.get(tm, abi.NUMA_TOPO_NONE)
+
+
+def zone_row(zones: Sequence[Tuple[int, int]]) -> np.ndarray:
+    """NRT zones node-0..node-(M-1) -> the numa_zone_alloc row [2][NUMA_MAX_NODES]
+    (cpu milli, memory bytes per zone)."""
+    if len(zones) > abi.NUMA_MAX_NODES:
+        raise TopologyError("more than 8 NUMA zones")
+    row = np.zeros((2, abi.NUMA_MAX_NODES), np.int64)
+    for k, (cpu_m, mem) in enumerate(zones):
+        row[0, k], row[1, k] = cpu_m, mem
+    return row

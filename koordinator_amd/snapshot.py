@@ -24,9 +24,15 @@ I32_COLS = ["alloc_pods", "npods", "numa_class", "numa_alloc_cnt"]
 U8_COLS = ["la_flags", "numa_flags"]
 U64_COLS = ([f"numa_free{w}" for w in range(abi.NUMA_WORDS)] + [f"numa_excl_pcpu{w}" for w in range(abi.NUMA_WORDS)]
             + [f"numa_excl_numa{w}" for w in range(abi.NUMA_WORDS)])
-ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS
-# NodeNUMAResource mutable columns (advanced by cpuset Reserves)
-NUMA_MUTABLE = [c for c in U64_COLS] + ["numa_alloc_cnt"]
+# NUMA zone resources, [n][2][NUMA_MAX_NODES] int64 per column (cpu milli, memory bytes)
+ZONE_COLS = ["numa_zone_alloc", "numa_zone_used"]
+ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS + ZONE_COLS
+# NodeNUMAResource mutable columns (advanced by cpuset / NUMA-zone Reserves)
+NUMA_MUTABLE = [c for c in U64_COLS] + ["numa_alloc_cnt", "numa_zone_used"]
+
+
+def _shape(col: str, n: int):
+    return (n, 2, abi.NUMA_MAX_NODES) if col in ZONE_COLS else (n,)
 
 
 def _dtype(col: str):
@@ -52,7 +58,7 @@ class NodeTable:
     def empty(cls, n: int) -> "NodeTable":
         t = cls(n=n)
         for c in ALL_COLS:
-            t.cols[c] = np.zeros(n, dtype=_dtype(c))
+            t.cols[c] = np.zeros(_shape(c, n), dtype=_dtype(c))
         t.cols["numa_class"][:] = -1
         t.names = [f"node-{i}" for i in range(n)]
         return t
@@ -80,8 +86,8 @@ class NodeTable:
         """Build a koordhip_node_soa pointing at this table's arrays (keep `self` alive)."""
         for c in ALL_COLS:
             a = self.cols[c]
-            if not a.flags.c_contiguous or a.dtype != _dtype(c) or a.shape != (self.n,):
-                self.cols[c] = np.ascontiguousarray(a, dtype=_dtype(c))
+            if not a.flags.c_contiguous or a.dtype != _dtype(c) or a.shape != _shape(c, self.n):
+                self.cols[c] = np.ascontiguousarray(a, dtype=_dtype(c)).reshape(_shape(c, self.n))
         s = abi.KoordhipNodeSoa()
         p64 = lambda c: self.cols[c].ctypes.data_as(C.POINTER(C.c_int64))
         p32 = lambda c: self.cols[c].ctypes.data_as(C.POINTER(C.c_int32))
@@ -111,6 +117,8 @@ class NodeTable:
             s.numa_excl_numa[w] = p64u(f"numa_excl_numa{w}")
         s.numa_alloc_cnt = p32("numa_alloc_cnt")
         s.numa_flags = self.cols["numa_flags"].ctypes.data_as(C.POINTER(C.c_uint8))
+        s.numa_zone_alloc = p64("numa_zone_alloc")
+        s.numa_zone_used = p64("numa_zone_used")
         return s
 
     def nbytes(self) -> int:

@@ -120,6 +120,8 @@ class NumaSpec:
     spread_frac: float = 0.05          # node label cpu-bind-policy=SpreadByPCPUs
     most_allocated_frac: float = 0.3   # node label numa-allocate-strategy=MostAllocated
     linux_numbering: bool = True
+    policy_frac: float = 0.0           # nodes with a NUMA topology policy (BestEffort / Restricted / SingleNUMANode)
+    zone_used_frac: float = 0.6        # policy nodes: zone usage of non-cpuset pods, U[0, max] of the zone
 
 
 def add_numa(t: NodeTable, spec: NumaSpec, profile: Profile, seed: int = SEED) -> NodeTable:
@@ -184,6 +186,19 @@ def add_numa(t: NodeTable, spec: NumaSpec, profile: Profile, seed: int = SEED) -
             f = abi.NODE_CPUBIND_SPREAD_BY_PCPUS
         if (most[i] if spec.most_allocated_frac > 0 else default_most):
             f |= abi.NODE_NUMA_MOST_ALLOCATED
+        if spec.policy_frac and rng.random() < spec.policy_frac:
+            # NRT zones node-0..: the zone's CPUs and an even memory share; used =
+            # its cpuset CPUs + other pods' requests (sometimes past allocatable)
+            f |= int(rng.integers(1, 4)) << abi.NODE_NUMA_POLICY_SHIFT
+            nn = topo.num_nodes
+            node_of = topo.record["node_of"][:topo.num_cpus]
+            for k in range(nn):
+                in_k = node_of == k
+                t["numa_zone_alloc"][i, 0, k] = int(in_k.sum()) * 1000
+                t["numa_zone_alloc"][i, 1, k] = int(t["alloc1"][i]) // nn
+                extra = rng.random() * spec.zone_used_frac * 1.1
+                t["numa_zone_used"][i, 0, k] = int((used & in_k).sum()) * 1000 + int(extra * in_k.sum() * 1000) // 100 * 100
+                t["numa_zone_used"][i, 1, k] = int(extra * t["numa_zone_alloc"][i, 1, k]) // MI * MI
         t["numa_flags"][i] = f
     return t
 

@@ -37,6 +37,7 @@ class OrcState(C.Structure):
         ("numa_excl_pcpu", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
         ("numa_excl_numa", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
         ("numa_alloc_cnt", C.POINTER(C.c_int32)),
+        ("numa_zone_used", C.POINTER(C.c_int64)),
         ("cpuset_out", C.c_void_p),
     ]
 
@@ -73,6 +74,10 @@ def lib():
         L.orc_place_stream.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32,
                                        vp, C.c_int32]
         L.orc_la_flags.argtypes = [C.POINTER(abi.KoordhipNodeSoa), C.c_int32, vp]
+        L.orc_tm_merge.argtypes = [C.c_int, C.c_uint64, vp, C.c_int32, vp]
+        L.orc_tm_merge.restype = C.c_int
+        L.orc_numa_hint_alloc.argtypes = [C.POINTER(OrcState), vp, C.c_int32, vp, vp, vp, vp]
+        L.orc_numa_hint_alloc.restype = C.c_int
         _lib = L
     return _lib
 
@@ -152,7 +157,18 @@ class Oracle:
             "excl_pcpu": np.stack([a(self.st.numa_excl_pcpu[w]) for w in range(abi.NUMA_WORDS)]),
             "excl_numa": np.stack([a(self.st.numa_excl_numa[w]) for w in range(abi.NUMA_WORDS)]),
             "alloc_cnt": a(self.st.numa_alloc_cnt),
+            "zone_used": a(self.st.numa_zone_used, (n, 2, abi.NUMA_MAX_NODES)),
         }
+
+    def hint_alloc(self, pod: np.ndarray, node: int):
+        """The topology-manager admit + allocateResourcesByHint for (pod, node):
+        (ok, mask or None for a nil hint, admit, zones [2][NUMA_MAX_NODES])."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        mask, nil, admit = C.c_uint64(), C.c_int32(), C.c_int32()
+        zones = np.zeros((2, abi.NUMA_MAX_NODES), np.int64)
+        ok = lib().orc_numa_hint_alloc(C.byref(self.st), pod.ctypes.data, node, C.byref(mask), C.byref(nil),
+                                       C.byref(admit), zones.ctypes.data)
+        return bool(ok), (None if nil.value else mask.value), bool(admit.value), zones
 
 
 def take_cpus(cls: np.ndarray, avail, need: int, bind_policy: int, excl_policy: int = 0, most_allocated: bool = True,
@@ -174,6 +190,30 @@ def spread_order(cls: np.ndarray, avail, most_allocated: bool = True):
     ids = np.zeros(abi.NUMA_MAX_CPUS, np.int32)
     n = lib().orc_spread_order(cls.ctypes.data, av.ctypes.data, int(most_allocated), ids.ctypes.data)
     return ids[:n].tolist()
+
+
+TM_PROVIDER_EMPTY, TM_RES_NIL, TM_RES_EMPTY, TM_RES_HINTS = 0, 1, 2, 3
+TM_HINT_DTYPE = np.dtype([("mask", "<u8"), ("preferred", "<i4"), ("nil", "<i4")])
+TM_ENTRY_DTYPE = np.dtype([("kind", "<i4"), ("n", "<i4"), ("h", TM_HINT_DTYPE, (255,))])
+
+
+def tm_merge(policy: int, numa_nodes: int, entries):
+    """Topology-manager Merge.  entries: one item per filterProvidersHints
+    list -- "provider-empty", "nil", "empty", or a list of (mask|None,
+    preferred).  Returns (admit, mask|None, preferred)."""
+    e = np.zeros(max(1, len(entries)), TM_ENTRY_DTYPE)
+    for q, ent in enumerate(entries):
+        if isinstance(ent, str):
+            e[q]["kind"] = {"provider-empty": TM_PROVIDER_EMPTY, "nil": TM_RES_NIL, "empty": TM_RES_EMPTY}[ent]
+            continue
+        e[q]["kind"] = TM_RES_HINTS
+        e[q]["n"] = len(ent)
+        for j, (m, pref) in enumerate(ent):
+            e[q]["h"][j] = (0 if m is None else m, int(pref), int(m is None))
+    out = np.zeros(1, TM_HINT_DTYPE)
+    admit = lib().orc_tm_merge(policy, numa_nodes, e.ctypes.data, len(entries), out.ctypes.data)
+    h = out[0]
+    return bool(admit), (None if h["nil"] else int(h["mask"])), bool(h["preferred"])
 
 
 def usage_percent(used_milli: int, total_milli: int) -> int:

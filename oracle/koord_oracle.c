@@ -125,7 +125,11 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
   }
   st->numa_alloc_cnt = (int32_t *)calloc((size_t)(n > 0 ? n : 1), sizeof(int32_t));
   if (soa->numa_class && soa->numa_alloc_cnt) memcpy(st->numa_alloc_cnt, soa->numa_alloc_cnt, sizeof(int32_t) * (size_t)n);
-  if (!st->flags || !st->npods || !st->numa_alloc_cnt) return -1;
+  const size_t zn = (size_t)(n > 0 ? n : 1) * 2 * KOORDHIP_NUMA_MAX_NODES;
+  st->numa_zone_used = (int64_t *)calloc(zn, sizeof(int64_t));
+  if (soa->numa_zone_used && st->numa_zone_used)
+    memcpy(st->numa_zone_used, soa->numa_zone_used, sizeof(int64_t) * (size_t)n * 2 * KOORDHIP_NUMA_MAX_NODES);
+  if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used) return -1;
   orc_la_flags(soa, n, st->flags);
   return 0;
 }
@@ -146,6 +150,7 @@ void orc_state_free(orc_state *st) {
     free(st->numa_excl_numa[w]);
   }
   free(st->numa_alloc_cnt);
+  free(st->numa_zone_used);
   memset(st, 0, sizeof(*st));
 }
 
@@ -310,16 +315,17 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
  * one pod (mirror: reservation/transformer.go:280-333).  sign = -1: Unreserve.
  * NodeNUMAResource Reserve allocates a cpuset for a cpuset pod (plugin.go:365-405);
  * when it fails the framework unreserves every plugin: nothing is committed. */
-static int numa_reserve_active(const koordhip_config *cfg, const koordhip_pod *pod) {
-  return ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) && (pod->flags & KOORDHIP_POD_CPUSET) &&
-         !(pod->flags & KOORDHIP_POD_NUMA_SKIP);
+static int numa_on(const koordhip_config *cfg) {
+  return ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
 }
 
 int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t i, int sign,
                uint64_t *cpus) {
-  if (numa_reserve_active(cfg, pod)) {
+  if (numa_on(cfg) && orc_numa_reserve_active(st, pod, i)) {
     if (sign > 0) {
       if (!orc_numa_reserve(st, pod, i, cpus)) return KOORDHIP_ERESERVE;
+    } else if (st->soa->numa_flags && KOORDHIP_NODE_NUMA_POLICY(st->soa->numa_flags[i]) != KOORDHIP_NUMA_TOPO_NONE) {
+      return KOORDHIP_EINVAL; /* the zone amounts of an earlier Reserve are not passed back */
     } else if (cpus) {
       orc_numa_release(st, i, cpus);
     }

@@ -51,6 +51,7 @@ typedef struct orc_state {
   uint64_t *numa_excl_pcpu[KOORDHIP_NUMA_WORDS];
   uint64_t *numa_excl_numa[KOORDHIP_NUMA_WORDS];
   int32_t *numa_alloc_cnt;
+  int64_t *numa_zone_used; /* [n][2][KOORDHIP_NUMA_MAX_NODES] NUMA zone allocations */
   uint64_t *cpuset_out; /* optional [n_pods][WORDS] output of orc_place_stream */
 } orc_state;
 
@@ -67,6 +68,7 @@ int64_t orc_la_score(const koordhip_config *cfg, const orc_state *st, const koor
 int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
+int orc_numa_reserve_active(const orc_state *st, const koordhip_pod *pod, int32_t i);
 int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
 void orc_numa_release(orc_state *st, int32_t node, const uint64_t *cpus);
 /* takeCPUs on one topology (cpu_accumulator.go:87-232), maxRefCount 1; 1 = ok. */
@@ -74,6 +76,34 @@ int orc_take_cpus(const koordhip_numa_class *t, const uint64_t *avail, const uin
                   const uint64_t *excl_numa, int need, int bind_policy, int excl_policy, int most_allocated,
                   uint64_t *out);
 int orc_spread_order(const koordhip_numa_class *t, const uint64_t *avail, int most_allocated, int32_t *cpu_ids);
+
+/* Topology manager Merge (frameworkext/topologymanager/policy*.go) over the
+ * provider hints as filterProvidersHints (policy.go:93-117) sees them: one
+ * entry per provider without hints (ORC_TM_PROVIDER_EMPTY) or per resource of
+ * a provider (a nil slice: ORC_TM_RES_NIL, an empty one: ORC_TM_RES_EMPTY,
+ * else ORC_TM_RES_HINTS with n hints).  numa_nodes = the default affinity
+ * mask.  Returns admit (canAdmitPodResult); *out = the best hint. */
+#define ORC_TM_PROVIDER_EMPTY 0
+#define ORC_TM_RES_NIL 1
+#define ORC_TM_RES_EMPTY 2
+#define ORC_TM_RES_HINTS 3
+#define ORC_TM_MAX_HINTS 255
+typedef struct orc_tm_hint {
+  uint64_t mask;
+  int32_t preferred;
+  int32_t nil; /* NUMANodeAffinity == nil */
+} orc_tm_hint;
+typedef struct orc_tm_entry {
+  int32_t kind;
+  int32_t n;
+  orc_tm_hint h[ORC_TM_MAX_HINTS];
+} orc_tm_entry;
+int orc_tm_merge(int policy, uint64_t numa_nodes, const orc_tm_entry *e, int32_t ne, orc_tm_hint *out);
+/* The NUMA-zone part of Allocate for node i under its topology policy: the
+ * merged hint (nil -> *nil = 1), admit, and allocateResourcesByHint's amounts
+ * [2][KOORDHIP_NUMA_MAX_NODES]; returns 1 when Admit + Allocate succeed. */
+int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *mask, int32_t *nil,
+                        int32_t *admit, int64_t *zones);
 
 /* Same contract as koordhip_eval (status / scores / topk all optional). */
 int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, int32_t n_pods,

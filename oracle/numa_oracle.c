@@ -1,13 +1,17 @@
 /*
  * numa_oracle.c -- TEST INFRASTRUCTURE (see koord_oracle.h).  Plain-C
- * restatement of NodeNUMAResource for NUMA topology policy None:
+ * restatement of NodeNUMAResource:
  *   - the cpuAccumulator (pkg/scheduler/plugins/nodenumaresource/cpu_accumulator.go),
  *     kept in the reference's own shape: per-call grouping of the allocatable
  *     CPUs into per-core / per-NUMA-node / per-socket lists, the same sort
  *     keys, the same passes;
  *   - Allocate / allocateCPUSet / satisfiedRequiredCPUBindPolicy
  *     (resource_manager.go:142-164,244-326,442-463);
- *   - Filter / Score / Reserve (plugin.go:266-324,365-405, scoring.go:55-168).
+ *   - Filter / Score / Reserve (plugin.go:266-324,365-405, scoring.go:55-168);
+ *   - NUMA topology policies: the topology manager's hint merge and admit
+ *     (frameworkext/topologymanager/manager.go:58-111, policy*.go), the
+ *     plugin's hints (topology_hint.go:30-86, resource_manager.go:384-428)
+ *     and allocateResourcesByHint (:166-242).
  * Go's sort.Slice is not stable.  Every comparator but two ends in an id
  * tie-break, so any correct sort gives Go's order; those are insertion sorts
  * here.  The two len-only socket sorts (cpu_accumulator.go:142-144, 161-163)
@@ -506,9 +510,216 @@ static int effective_bind_policy(uint8_t node_flags, int preferred) {
   }
 }
 
-/* resourceManager.Allocate for a cpuset pod with an empty hint and no
- * reservation (resource_manager.go:142-164, allocateCPUSet :244-326). */
-int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *out) {
+/* ------------------------------------------------------------------------ */
+/* NUMA topology policies                                                    */
+/* ------------------------------------------------------------------------ */
+
+static int popc64(uint64_t x) { return __builtin_popcountll(x); }
+
+static int node_policy(const orc_state *st, int32_t i) {
+  return st->soa->numa_flags ? (int)KOORDHIP_NODE_NUMA_POLICY(st->soa->numa_flags[i]) : 0;
+}
+
+/* bitmask.IsNarrowerThan (pkg/util/bitmask/bitmask.go:142-157): fewer bits,
+ * or as many and numerically smaller. */
+static int narrower(uint64_t a, uint64_t b) {
+  const int ca = popc64(a), cb = popc64(b);
+  return ca == cb ? a < b : ca < cb;
+}
+
+typedef struct tm_list {
+  int n;
+  orc_tm_hint h[ORC_TM_MAX_HINTS];
+} tm_list;
+
+#define TM_MAXL 16
+
+/* mergeFilteredHints (policy.go:119-151): every permutation of one hint per
+ * list (iterateAllProviderTopologyHints :170-208), AND-ed into the default
+ * affinity (mergePermutation :52-72); preferred beats non-preferred, then the
+ * narrowest wins.  A list with no hint yields no permutation. */
+static orc_tm_hint merge_filtered(uint64_t deflt, const tm_list *L, int nl) {
+  orc_tm_hint best = {deflt, 0, 0};
+  int idx[TM_MAXL] = {0};
+  for (int i = 0; i < nl; i++)
+    if (L[i].n == 0) return best;
+  for (;;) {
+    uint64_t m = deflt;
+    int pref = 1;
+    for (int i = 0; i < nl; i++) {
+      const orc_tm_hint *h = &L[i].h[idx[i]];
+      m &= h->nil ? deflt : h->mask;
+      if (!h->preferred) pref = 0;
+    }
+    if (popc64(m) != 0) {
+      if (pref && !best.preferred) {
+        best.mask = m;
+        best.preferred = 1;
+      } else if (!(!pref && best.preferred) && narrower(m, best.mask)) {
+        best.mask = m;
+        best.preferred = pref;
+      }
+    }
+    int k = nl - 1;
+    while (k >= 0 && ++idx[k] == L[k].n) idx[k--] = 0;
+    if (k < 0) break;
+  }
+  return best;
+}
+
+int orc_tm_merge(int policy, uint64_t numa_nodes, const orc_tm_entry *e, int32_t ne, orc_tm_hint *out) {
+  static __thread tm_list L[TM_MAXL];
+  int nl = 0;
+  /* filterProvidersHints (policy.go:93-117) */
+  for (int32_t q = 0; q < ne && nl < TM_MAXL; q++, nl++) {
+    L[nl].n = 1;
+    L[nl].h[0].mask = 0;
+    L[nl].h[0].nil = 1;
+    switch (e[q].kind) {
+      case ORC_TM_PROVIDER_EMPTY:
+      case ORC_TM_RES_NIL: L[nl].h[0].preferred = 1; break;
+      case ORC_TM_RES_EMPTY: L[nl].h[0].preferred = 0; break;
+      default:
+        L[nl].n = e[q].n;
+        for (int j = 0; j < e[q].n; j++) L[nl].h[j] = e[q].h[j];
+    }
+  }
+  orc_tm_hint best;
+  int admit = 1;
+  switch (policy) {
+    case KOORDHIP_NUMA_TOPO_SINGLE_NUMA_NODE: /* policy_single_numa_node.go:37-78 */
+      for (int i = 0; i < nl; i++) {
+        int m = 0;
+        for (int j = 0; j < L[i].n; j++) {
+          const orc_tm_hint h = L[i].h[j];
+          if (h.preferred && (h.nil || popc64(h.mask) == 1)) L[i].h[m++] = h;
+        }
+        L[i].n = m;
+      }
+      best = merge_filtered(numa_nodes, L, nl);
+      if (!best.nil && best.mask == numa_nodes) {
+        best.nil = 1;
+        best.mask = 0;
+      }
+      admit = best.preferred;
+      break;
+    case KOORDHIP_NUMA_TOPO_RESTRICTED: /* policy_restricted.go:34-47 */
+      best = merge_filtered(numa_nodes, L, nl);
+      admit = best.preferred;
+      break;
+    case KOORDHIP_NUMA_TOPO_BEST_EFFORT: /* policy_best_effort.go:35-48 */
+      best = merge_filtered(numa_nodes, L, nl);
+      break;
+    default: /* policy_none.go:37-42 */
+      best.mask = 0;
+      best.nil = 1;
+      best.preferred = 0;
+  }
+  *out = best;
+  return admit;
+}
+
+static int64_t zone_at(const int64_t *z, int32_t i, int r, int k) {
+  return z[((size_t)i * 2 + (size_t)r) * KOORDHIP_NUMA_MAX_NODES + (size_t)k];
+}
+
+/* NodeAllocation.getAvailableNUMANodeResources (node_allocation.go:158-177):
+ * allocatable - allocated, non-negative (no amplification, no reservation). */
+static int64_t zone_avail(const orc_state *st, int32_t i, int r, int k) {
+  const int64_t a = zone_at(st->soa->numa_zone_alloc, i, r, k) - zone_at(st->numa_zone_used, i, r, k);
+  return a > 0 ? a : 0;
+}
+
+static int zones_of(const orc_state *st, int32_t i) {
+  const koordhip_node_soa *s = st->soa;
+  if (!s->numa_class || s->numa_class[i] < 0 || !s->numa_zone_alloc) return 0;
+  return s->numa_classes[s->numa_class[i]].num_nodes;
+}
+
+/* GetPodTopologyHints + generateResourceHints (topology_hint.go:41-62,
+ * resource_manager.go:384-428) for the pod's cpu / memory requests (a request
+ * of 0 counts as absent: the marshaller drops explicit zero requests), then
+ * the node policy's Merge. */
+static int node_merge(const orc_state *st, const koordhip_pod *pod, int32_t i, int M, int policy, orc_tm_hint *best) {
+  static __thread orc_tm_entry e[2];
+  const int64_t req[2] = {pod->req[KOORDHIP_RES_CPU], pod->req[KOORDHIP_RES_MEM]};
+  int minsize = M, nh = 0;
+  uint64_t hm[ORC_TM_MAX_HINTS];
+  /* IterateBitMasks order (bitmask.go:200-222): by size, then lexicographic */
+  for (int size = 1; size <= M; size++)
+    for (uint64_t m = 1; m < (1ull << M); m++) {
+      if (popc64(m) != size) continue;
+      int sat = 1;
+      for (int r = 0; r < 2; r++) {
+        if (req[r] == 0) continue;
+        int64_t sum = 0;
+        for (int k = 0; k < M; k++)
+          if ((m >> k) & 1) sum += zone_avail(st, i, r, k);
+        if (req[r] > sum) sat = 0;
+      }
+      if (!sat) continue;
+      if (size < minsize) minsize = size;
+      hm[nh++] = m;
+    }
+  int ne = 0;
+  for (int r = 0; r < 2 && nh > 0; r++) {
+    if (req[r] == 0) continue;
+    e[ne].kind = ORC_TM_RES_HINTS;
+    e[ne].n = nh;
+    for (int j = 0; j < nh; j++) {
+      e[ne].h[j].mask = hm[j];
+      e[ne].h[j].nil = 0;
+      e[ne].h[j].preferred = popc64(hm[j]) == minsize;
+    }
+    ne++;
+  }
+  if (ne == 0) { /* no hint map entries: the provider has no preference */
+    e[0].kind = ORC_TM_PROVIDER_EMPTY;
+    ne = 1;
+  }
+  return orc_tm_merge(policy, (1ull << M) - 1, e, ne, best);
+}
+
+/* allocateResourcesByHint (resource_manager.go:166-227): the hinted zones in
+ * ascending id take min(available, still requested) of cpu and memory. */
+static int alloc_by_hint(const orc_state *st, const koordhip_pod *pod, int32_t i, int M, uint64_t mask, int64_t *zones) {
+  int64_t rem[2] = {pod->req[KOORDHIP_RES_CPU], pod->req[KOORDHIP_RES_MEM]};
+  for (int q = 0; q < 2 * KOORDHIP_NUMA_MAX_NODES; q++) zones[q] = 0;
+  for (int k = 0; k < M; k++) {
+    if (!((mask >> k) & 1)) continue;
+    for (int r = 0; r < 2; r++) {
+      const int64_t av = zone_avail(st, i, r, k);
+      const int64_t a = av < rem[r] ? av : rem[r];
+      zones[r * KOORDHIP_NUMA_MAX_NODES + k] = a;
+      rem[r] -= a;
+    }
+  }
+  return rem[0] == 0 && rem[1] == 0; /* :230-241 Insufficient NUMA <resource> */
+}
+
+int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *mask, int32_t *nil,
+                        int32_t *admit, int64_t *zones) {
+  for (int q = 0; q < 2 * KOORDHIP_NUMA_MAX_NODES; q++) zones[q] = 0;
+  *mask = 0;
+  *nil = 1;
+  *admit = 0;
+  const int M = zones_of(st, i);
+  const int policy = node_policy(st, i);
+  if (M == 0) return 0; /* FilterByNUMANode: missing NUMA resources (topology_hint.go:34-37) */
+  orc_tm_hint best;
+  *admit = node_merge(st, pod, i, M, policy, &best);
+  *mask = best.mask;
+  *nil = best.nil;
+  if (!*admit) return 0;
+  if (best.nil) return 1;
+  return alloc_by_hint(st, pod, i, M, best.mask, zones);
+}
+
+/* allocateCPUSet (resource_manager.go:244-326) with no reservation: zones =
+ * NULL for a nil hint, else the pod's per-zone allocation from
+ * allocateResourcesByHint -- every zone holding a non-zero amount takes
+ * floor(cpu / 1000) CPUs from its own available CPUs (:264-295). */
+static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i, const int64_t *zones, uint64_t *out) {
   const koordhip_node_soa *s = st->soa;
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) out[w] = 0;
   int cls = s->numa_class[i];
@@ -523,12 +734,31 @@ int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, u
   const int need = pod->numa_cpus;
   const int required = KOORDHIP_NUMA_REQUIRED(pod->numa_policy) != KOORDHIP_CPUBIND_NONE;
   const int policy = effective_bind_policy(s->numa_flags[i], (int)KOORDHIP_NUMA_PREFERRED(pod->numa_policy));
+  const int excl = (int)KOORDHIP_NUMA_EXCLUSIVE(pod->numa_policy);
+  const int most = (s->numa_flags[i] & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0;
   /* filterAvailableCPUsByRequiredCPUBindPolicy (:430-440) returns a set equal
    * to availableCPUs on both branches: no-op. */
   if (popc(avail) < need) return 0; /* :257-259 */
-  if (!orc_take_cpus(t, avail, ep, en, need, policy, (int)KOORDHIP_NUMA_EXCLUSIVE(pod->numa_policy),
-                     (s->numa_flags[i] & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0, out))
+  if (zones) {
+    int got = 0;
+    for (int k = 0; k < t->num_nodes && k < KOORDHIP_NUMA_MAX_NODES; k++) {
+      if (zones[k] == 0 && zones[KOORDHIP_NUMA_MAX_NODES + k] == 0) continue; /* not in NUMANodeResources */
+      uint64_t zav[KOORDHIP_NUMA_WORDS] = {0, 0, 0, 0}, zo[KOORDHIP_NUMA_WORDS];
+      for (int p = 0; p < t->num_cpus; p++)
+        if (t->node_of[p] == k && bit(avail, p)) zav[p >> 6] |= 1ull << (p & 63);
+      int n = popc(zav);
+      const int64_t want = zones[k] / 1000;
+      if (want < n) n = (int)want;
+      if (n > 0) {
+        if (!orc_take_cpus(t, zav, ep, en, n, policy, excl, most, zo)) return 0;
+        for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) out[w] |= zo[w];
+        got += popc(zo);
+      }
+    }
+    if (got != need) return 0; /* :290-293 */
+  } else if (!orc_take_cpus(t, avail, ep, en, need, policy, excl, most, out)) {
     return 0;
+  }
   if (required) { /* satisfiedRequiredCPUBindPolicy :442-463 */
     const int cpc = t->num_cpus / t->num_cores;
     int cores = 0, n = popc(out);
@@ -543,25 +773,57 @@ int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, u
   return 1;
 }
 
-/* Filter, plugin.go:266-324 (NUMA topology policy None; amplification ratio <= 1). */
+/* resourceManager.Allocate for a cpuset pod with an empty hint and no
+ * reservation (resource_manager.go:142-164). */
+int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *out) {
+  return alloc_cpuset(st, pod, i, NULL, out);
+}
+
+
+/* The whole Allocate of Filter's topology-manager admit / Reserve on a node
+ * with a topology policy (manager.go:58-79 -> plugin Allocate, topology_hint.go:
+ * 66-86): the merged hint's zones, then the cpuset inside them. */
+static int policy_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, int64_t *zones, uint64_t *cpus,
+                           int *has_zones) {
+  uint64_t mask;
+  int32_t nil, admit;
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
+  if (!orc_numa_hint_alloc(st, pod, i, &mask, &nil, &admit, zones)) return 0;
+  *has_zones = !nil;
+  if (pod->flags & KOORDHIP_POD_CPUSET) return alloc_cpuset(st, pod, i, nil ? NULL : zones, cpus);
+  return 1;
+}
+
+/* Filter, plugin.go:266-324 (amplification ratio <= 1). */
 int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
   (void)cfg;
   const koordhip_node_soa *s = st->soa;
-  if (pod->flags & KOORDHIP_POD_NUMA_ERROR) return 0;            /* PreFilter error */
-  if ((pod->flags & KOORDHIP_POD_NUMA_SKIP) || !(pod->flags & KOORDHIP_POD_CPUSET)) return 1; /* skipTheNode :280-282 */
-  if (!s->numa_class || s->numa_class[i] < 0) return 0;          /* :285-294 */
-  const koordhip_numa_class *t = &s->numa_classes[s->numa_class[i]];
-  const int req = (int)KOORDHIP_NUMA_REQUIRED(pod->numa_policy);
-  const int pref = (int)KOORDHIP_NUMA_PREFERRED(pod->numa_policy);
-  const int node_full_only = (s->numa_flags[i] & KOORDHIP_NODE_CPUBIND_MASK) == 1;
-  if (node_full_only || req == KOORDHIP_CPUBIND_FULL_PCPUS) { /* :295-305 */
-    const int cpc = t->num_cpus / t->num_cores;
-    if (pod->numa_cpus % cpc != 0) return 0;
-    if (node_full_only && (req != KOORDHIP_CPUBIND_FULL_PCPUS || pref != KOORDHIP_CPUBIND_FULL_PCPUS)) return 0;
+  const int tp = node_policy(st, i);
+  const int cpuset = (pod->flags & KOORDHIP_POD_CPUSET) != 0;
+  if (pod->flags & KOORDHIP_POD_NUMA_ERROR) return 0;   /* PreFilter error */
+  if ((pod->flags & KOORDHIP_POD_NUMA_SKIP) || (!cpuset && tp == KOORDHIP_NUMA_TOPO_NONE))
+    return 1;                                          /* skipTheNode, util.go:59-61 */
+  if (cpuset) {
+    if (!s->numa_class || s->numa_class[i] < 0) return 0; /* :285-294 */
+    const koordhip_numa_class *t = &s->numa_classes[s->numa_class[i]];
+    const int req = (int)KOORDHIP_NUMA_REQUIRED(pod->numa_policy);
+    const int pref = (int)KOORDHIP_NUMA_PREFERRED(pod->numa_policy);
+    const int node_full_only = (s->numa_flags[i] & KOORDHIP_NODE_CPUBIND_MASK) == 1;
+    if (node_full_only || req == KOORDHIP_CPUBIND_FULL_PCPUS) { /* :295-305 */
+      const int cpc = t->num_cpus / t->num_cores;
+      if (pod->numa_cpus % cpc != 0) return 0;
+      if (node_full_only && (req != KOORDHIP_CPUBIND_FULL_PCPUS || pref != KOORDHIP_CPUBIND_FULL_PCPUS)) return 0;
+    }
+    if (req != KOORDHIP_CPUBIND_NONE && tp == KOORDHIP_NUMA_TOPO_NONE) { /* :307-316 */
+      uint64_t out[KOORDHIP_NUMA_WORDS];
+      if (!orc_numa_allocate(st, pod, i, out)) return 0;
+    }
   }
-  if (req != KOORDHIP_CPUBIND_NONE) { /* :307-316 */
-    uint64_t out[KOORDHIP_NUMA_WORDS];
-    if (!orc_numa_allocate(st, pod, i, out)) return 0;
+  if (tp != KOORDHIP_NUMA_TOPO_NONE) { /* FilterByNUMANode, :319-321 */
+    int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES];
+    uint64_t cpus[KOORDHIP_NUMA_WORDS];
+    int hz;
+    return policy_allocate(st, pod, i, zones, cpus, &hz);
   }
   return 1;
 }
@@ -596,25 +858,54 @@ int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const ko
   const koordhip_node_soa *s = st->soa;
   if (pod->flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0; /* :70-72 */
   const int has_topo = s->numa_class && s->numa_class[i] >= 0;
-  const int64_t acpu = s->alloc[KOORDHIP_RES_CPU][i], amem = s->alloc[KOORDHIP_RES_MEM][i];
-  if (!(pod->flags & KOORDHIP_POD_CPUSET)) {
-    if (!has_topo) return 0; /* scoreWithAmplifiedCPUs -> getResourceOptions error :97-100 */
-    return numa_least_allocated(cfg, st->requested[KOORDHIP_RES_CPU][i] + pod->req[KOORDHIP_RES_CPU], acpu,
-                                st->requested[KOORDHIP_RES_MEM][i] + pod->req[KOORDHIP_RES_MEM], amem); /* :104-106 */
+  const int cpuset = (pod->flags & KOORDHIP_POD_CPUSET) != 0;
+  const int tp = node_policy(st, i);
+  int64_t acpu = s->alloc[KOORDHIP_RES_CPU][i], amem = s->alloc[KOORDHIP_RES_MEM][i];
+  int64_t rcpu = st->requested[KOORDHIP_RES_CPU][i], rmem = st->requested[KOORDHIP_RES_MEM][i];
+  /* no topology: getResourceOptions fails (:82-85, :97-100) */
+  if (!has_topo) return 0;
+  if (!cpuset && tp == KOORDHIP_NUMA_TOPO_NONE) /* scoreWithAmplifiedCPUs :104-106 */
+    return numa_least_allocated(cfg, rcpu + pod->req[KOORDHIP_RES_CPU], acpu, rmem + pod->req[KOORDHIP_RES_MEM], amem);
+  int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES];
+  uint64_t cpus[KOORDHIP_NUMA_WORDS];
+  int hz = 0;
+  if (tp != KOORDHIP_NUMA_TOPO_NONE) {
+    if (!policy_allocate(st, pod, i, zones, cpus, &hz)) return 0; /* :86-89 */
+  } else if (!alloc_cpuset(st, pod, i, NULL, cpus)) {
+    return 0;
   }
-  if (!has_topo) return 0; /* :76-78 */
-  uint64_t out[KOORDHIP_NUMA_WORDS];
-  if (!orc_numa_allocate(st, pod, i, out)) return 0; /* :86-89 */
-  /* calculateAllocatableAndRequested: requested cpu := allocated cpuset size (:161-166) */
-  return numa_least_allocated(cfg, (int64_t)st->numa_alloc_cnt[i] * 1000 + pod->req[KOORDHIP_RES_CPU], acpu,
-                              st->requested[KOORDHIP_RES_MEM][i] + pod->req[KOORDHIP_RES_MEM], amem);
+  if (hz) { /* calculateAllocatableAndRequested over the pod's zones :134-152 */
+    acpu = amem = rcpu = rmem = 0;
+    for (int k = 0; k < KOORDHIP_NUMA_MAX_NODES; k++) {
+      if (zones[k] == 0 && zones[KOORDHIP_NUMA_MAX_NODES + k] == 0) continue;
+      acpu += zone_at(s->numa_zone_alloc, i, 0, k);
+      amem += zone_at(s->numa_zone_alloc, i, 1, k);
+      rcpu += zone_at(st->numa_zone_used, i, 0, k);
+      rmem += zone_at(st->numa_zone_used, i, 1, k);
+    }
+  }
+  /* requested cpu := allocated cpuset size (:161-166) */
+  if (cpuset) rcpu = (int64_t)st->numa_alloc_cnt[i] * 1000;
+  return numa_least_allocated(cfg, rcpu + pod->req[KOORDHIP_RES_CPU], acpu, rmem + pod->req[KOORDHIP_RES_MEM], amem);
+}
+
+int orc_numa_reserve_active(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  if (pod->flags & KOORDHIP_POD_NUMA_SKIP) return 0;
+  return (pod->flags & KOORDHIP_POD_CPUSET) || node_policy(st, i) != KOORDHIP_NUMA_TOPO_NONE;
 }
 
 /* Reserve (plugin.go:365-405) + resourceManager.Update (resource_manager.go:328-339,
- * node_allocation.go:76-103) for a cpuset pod; returns 0 when Allocate fails. */
+ * node_allocation.go:76-103): the cpuset and the zone amounts; returns 0 when
+ * Allocate fails. */
 int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *cpus_out) {
-  uint64_t out[KOORDHIP_NUMA_WORDS];
-  if (!orc_numa_allocate(st, pod, i, out)) return 0;
+  uint64_t out[KOORDHIP_NUMA_WORDS] = {0, 0, 0, 0};
+  int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES] = {0};
+  int hz = 0;
+  if (node_policy(st, i) != KOORDHIP_NUMA_TOPO_NONE) {
+    if (!policy_allocate(st, pod, i, zones, out, &hz)) return 0;
+  } else if (!alloc_cpuset(st, pod, i, NULL, out)) {
+    return 0;
+  }
   const int ex = (int)KOORDHIP_NUMA_EXCLUSIVE(pod->numa_policy);
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
     st->numa_free[w][i] &= ~out[w];
@@ -623,6 +914,8 @@ int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t
     if (cpus_out) cpus_out[w] = out[w];
   }
   st->numa_alloc_cnt[i] += popc(out);
+  if (hz)
+    for (int q = 0; q < 2 * KOORDHIP_NUMA_MAX_NODES; q++) st->numa_zone_used[(size_t)i * 2 * KOORDHIP_NUMA_MAX_NODES + q] += zones[q];
   return 1;
 }
 

@@ -140,3 +140,61 @@ def build_numa_score_case(case):
                "SpreadByPCPUs": abi.CPUBIND_SPREAD_BY_PCPUS}[case["preferred_bind_policy"]]
         p["numa_policy"][0] = abi.numa_policy(0, pol, 0)
     return prof, t, p
+
+
+def numa_node_score_cases():
+    return [(c["name"], c) for c in load("topology_policy_cases.json")["numa_node_score"]]
+
+
+def build_numa_node_score_case(case):
+    """-> (profile, NodeTable, pod record array(1)) for one TestNUMANodeScore row
+    (scoring_test.go:302-352)."""
+    import numpy as np
+    from koordinator_amd import abi
+    from koordinator_amd.config import PLUGIN_NUMA
+    from koordinator_amd.numa import (ClassTable, LABEL_NUMA_TOPOLOGY_POLICY, node_numa_flags,
+                                      reference_test_topology, zone_row)
+    from koordinator_amd.snapshot import NodeTable, pod_array
+    prof = Profile(filters=(PLUGIN_NUMA,), scores={PLUGIN_NUMA: 1})
+    prof.numa.scoring_type = "MostAllocated"
+    prof.numa.resources = {k8s.CPU: 1, k8s.MEMORY: 1}
+    gi = 2 ** 30
+    n = len(case["nodes"])
+    t = NodeTable.empty(n)
+    ct = ClassTable()
+    topos = []
+    for i, (name, cores, mem_gi, policy, count) in enumerate(case["nodes"]):
+        t.names[i] = name
+        alloc_m, mem = cores * 1000, mem_gi * gi
+        t["alloc0"][i], t["alloc1"][i] = alloc_m, mem
+        t["alloc_pods"][i] = 110
+        t["la_alloc_cpu_m"][i], t["la_alloc_mem"][i] = alloc_m, mem
+        topo = reference_test_topology(count, 1, cores // 2 // count, 2)
+        topos.append(topo)
+        t["numa_class"][i] = ct.add(topo)
+        t["numa_flags"][i] = node_numa_flags({LABEL_NUMA_TOPOLOGY_POLICY: policy}, None,
+                                             prof.numa.default_most_allocated)
+        t["numa_zone_alloc"][i] = zone_row([(alloc_m // count, mem // count)] * count)
+    t.numa_classes = ct.records()
+    used_cpus = [set() for _ in range(n)]
+    for node, cpu, mem_gi, lsr in case["existing"]:
+        t["numa_zone_used"][node, 0, 0] += cpu * 1000
+        t["numa_zone_used"][node, 1, 0] += mem_gi * gi
+        if lsr:
+            used_cpus[node] |= set(range(cpu))
+    for i, topo in enumerate(topos):
+        free = topo.mask([c for c in topo.cpu_of if c not in used_cpus[i]])
+        for w in range(abi.NUMA_WORDS):
+            t[f"numa_free{w}"][i] = free[w]
+        t["numa_alloc_cnt"][i] = len(used_cpus[i])
+    cpu, mem_gi, lsr = case["pod"]
+    p = pod_array(1)
+    p["req"][0, abi.RES_CPU] = cpu * 1000
+    p["req"][0, abi.RES_MEM] = mem_gi * gi
+    p["nz_cpu_m"][0], p["nz_mem"][0] = cpu * 1000, mem_gi * gi
+    p["flags"][0] = abi.POD_HAS_REQ
+    if lsr:  # AllowUseCPUSet: LSR + prod priority; default preferred policy FullPCPUs
+        p["flags"][0] |= abi.POD_PROD | abi.POD_CPUSET
+        p["numa_cpus"][0] = cpu
+        p["numa_policy"][0] = abi.numa_policy(0, abi.CPUBIND_FULL_PCPUS, 0)
+    return prof, t, p

@@ -23,9 +23,12 @@ def test_golden_inputs_and_prefix():
     prof = shipped_profile()
     table, pods = synth.config_workload(4, prof)
     want = dict(zip(g["input_keys"].tolist(), g["input_sha"].tolist()))
-    got = {c: _sha(table[c]) for c in table.cols}
+    got = {c: _sha(table[c]) for c in table.cols if c in want}
     got["__pods__"] = _sha(pods)
     assert got == want
+    # columns added after the fixture was written must be empty for this workload
+    for c in set(table.cols) - set(want):
+        assert not table[c].any(), c
     assert g["placements"].shape == (100000,) and (g["placements"] >= 0).all()
     ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods[:300])
     assert np.array_equal(ref, g["placements"][:300])
