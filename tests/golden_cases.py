@@ -198,3 +198,88 @@ def build_numa_node_score_case(case):
         p["numa_cpus"][0] = cpu
         p["numa_policy"][0] = abi.numa_policy(0, abi.CPUBIND_FULL_PCPUS, 0)
     return prof, t, p
+
+
+def numa_plugin_cases(kind):
+    return [(c["name"], c) for c in load("numa_plugin_cases.json")[kind]]
+
+
+BIND = {"": 0, "FullPCPUs": 1, "SpreadByPCPUs": 2}
+
+
+def build_numa_plugin_case(case):
+    """-> (profile, NodeTable(1 row), pod(1), topology or None) for one
+    TestPlugin_Filter / TestPlugin_Reserve row (plugin_test.go:740-811, :1060-1145)."""
+    from koordinator_amd import abi
+    from koordinator_amd.config import PLUGIN_NUMA
+    from koordinator_amd.numa import ClassTable, node_numa_flags, reference_test_topology, zone_row
+    from koordinator_amd.snapshot import NodeTable, pod_array
+    prof = Profile(filters=(PLUGIN_NUMA,), scores={PLUGIN_NUMA: 1})
+    t = NodeTable.empty(1)
+    t["alloc0"][0], t["alloc1"][0] = 96000, 512 * 2**30
+    t["alloc_pods"][0] = 110
+    t["la_alloc_cpu_m"][0], t["la_alloc_mem"][0] = t["alloc0"][0], t["alloc1"][0]
+    topo = None
+    if isinstance(case["topology"], list):
+        topo = reference_test_topology(*case["topology"])
+        ct = ClassTable()
+        t["numa_class"][0] = ct.add(topo)
+        t.numa_classes = ct.records()
+        alloc = set(case["allocated_cpus"])
+        free = topo.mask([c for c in topo.cpu_of if c not in alloc])
+        for w in range(abi.NUMA_WORDS):
+            t[f"numa_free{w}"][0] = free[w]
+        t["numa_alloc_cnt"][0] = len(alloc)
+        per_node = topo.num_cpus // topo.num_nodes
+        t["numa_zone_alloc"][0] = zone_row([(per_node * 1000, 32 * 2**30)] * topo.num_nodes)
+    else:  # none, or &CPUTopology{} (invalid: the marshaller drops it)
+        t["numa_class"][0] = -1
+    t["numa_flags"][0] = node_numa_flags(case["labels"], case["kubelet_policy"], prof.numa.default_most_allocated)
+    p = pod_array(1)
+    if case["request_cpu_bind"]:
+        need = case["need"]
+        p["req"][0, abi.RES_CPU] = need * 1000
+        p["nz_cpu_m"][0] = need * 1000
+        p["flags"][0] = abi.POD_CPUSET | (abi.POD_HAS_REQ if need else 0)
+        p["numa_cpus"][0] = need
+        p["numa_policy"][0] = abi.numa_policy(BIND[case["required"]], BIND[case["preferred"]], 0)
+    return prof, t, p, topo
+
+
+def build_numa_score_node1_case(case):
+    """-> (profile, NodeTable(1 row), pod(1)) for the node1 column of one
+    TestScoreWithAmplifiedCPUs row (scoring_test.go:797-851)."""
+    from koordinator_amd import abi
+    from koordinator_amd.config import PLUGIN_NUMA
+    from koordinator_amd.numa import ClassTable, node_numa_flags, reference_test_topology
+    from koordinator_amd.snapshot import NodeTable, pod_array
+    gi = 2**30
+    prof = Profile(filters=(PLUGIN_NUMA,), scores={PLUGIN_NUMA: 1})
+    prof.numa.scoring_type = case["scoring"]
+    t = NodeTable.empty(1)
+    t["alloc0"][0], t["alloc1"][0] = 32000, 40 * gi
+    t["alloc_pods"][0] = 110
+    t["la_alloc_cpu_m"][0], t["la_alloc_mem"][0] = t["alloc0"][0], t["alloc1"][0]
+    if case["existing"]:
+        t["requested0"][0], t["requested1"][0] = 20000, 4 * gi
+        t["npods"][0] = 1
+    if case["has_nrt"]:
+        topo = reference_test_topology(2, 1, 8, 2)
+        ct = ClassTable()
+        t["numa_class"][0] = ct.add(topo)
+        t.numa_classes = ct.records()
+        held = set(range(20)) if case["existing"] and case["existing_cpuset"] else set()
+        free = topo.mask([c for c in topo.cpu_of if c not in held])
+        for w in range(abi.NUMA_WORDS):
+            t[f"numa_free{w}"][0] = free[w]
+        t["numa_alloc_cnt"][0] = len(held)
+    t["numa_flags"][0] = node_numa_flags({}, None, prof.numa.default_most_allocated)
+    p = pod_array(1)
+    p["req"][0, abi.RES_CPU], p["req"][0, abi.RES_MEM] = 8000, 16 * gi
+    p["nz_cpu_m"][0], p["nz_mem"][0] = 8000, 16 * gi
+    p["flags"][0] = abi.POD_HAS_REQ | abi.POD_PROD
+    if case["pod_cpuset"]:
+        p["flags"][0] |= abi.POD_CPUSET
+        p["numa_cpus"][0] = 8
+        p["numa_policy"][0] = abi.numa_policy(0, abi.CPUBIND_FULL_PCPUS, 0)
+    return prof, t, p
