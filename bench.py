@@ -226,8 +226,9 @@ def main():
     pods_profiled = args.pods
     evals_total = args.pods * args.nodes * args.steps   # every pod is evaluated against every node
     value = pods_total / elapsed
-    batch = eng.cfg.batch_pods or (16 if numa else 32)
-    k = 2 * batch
+    batch = int(ks["round_pods"]) or eng.cfg.batch_pods or (16 if numa else 32)
+    lag = int(ks["lag"]) or 1
+    k = (lag + 1) * batch   # list length: the resolve re-checks the nodes of the last `lag` rounds
     # ---- the dominant kernel: k_resolve, the sequential greedy (one persistent
     #      launch per step spanning the round pipeline).  Algorithmic bytes per
     #      pod: its list (k x 8 B) + pod record (96 B) + the
@@ -269,7 +270,7 @@ def main():
                                 if numa else
                                 f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
                                 "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile"),
-                   "nodes": args.nodes, "pods": args.pods, "batch_pods": batch,
+                   "nodes": args.nodes, "pods": args.pods, "batch_pods": batch, "pipeline_lag": lag,
                    "parallelism": f"node-shard x{world}"},
         "unschedulable": int((placements < 0).sum()),
         "roofline": {"bound": "hbm", "kernel": "k_resolve",

@@ -321,7 +321,9 @@ typedef struct koordhip_kernel_stats {
   int64_t evals;     /* (pod, node) pairs evaluated by this rank */
   int64_t pods;      /* pods of the staged stream */
   int64_t rounds;    /* pipelined rounds */
-  int64_t reserved[4];
+  int64_t round_pods; /* pods per round (batch_pods, LDS-clamped) */
+  int64_t lag;        /* pipeline depth: round r's lists see the state after round r - 1 - lag */
+  int64_t reserved[2];
 } koordhip_kernel_stats;
 int koordhip_last_kernel_stats(koordhip_ctx *ctx, koordhip_kernel_stats *out);
 /* Turn the per-launch event timing on / off for later place calls (the

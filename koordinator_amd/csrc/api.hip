@@ -90,6 +90,7 @@ struct koordhip_ctx {
   bool loaded = false;
   int32_t batch = kDefaultBatch;
   int32_t last_P = 1;  // pods per round of the last place call (batch, LDS-clamped)
+  int32_t last_lag = 1;  // its pipeline depth
   int32_t monotone = 1;
   int32_t score_bits = 16;  // bits of (max total score + 1)
   int32_t nbins = 2;        // score histogram bins of k_select: max total score + 2
@@ -1092,15 +1093,36 @@ int place_staged_impl(koordhip_ctx *c) {
   c->pipe_err = false;
   c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
+  // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises
+  // dispatches): every launch on one stream in dependency order, one resolve
+  // per round; the lists are then fresher than in the pipeline, which the
+  // resolve treats exactly like refreshed entries.
+  const bool serial = std::getenv("KOORDHIP_SERIAL") != nullptr;
+  // KOORDHIP_FOLD_WAIT: the split select's merging workgroups hold the stream
+  // until the resolve is far enough instead of a k_wait_resolved launch
+  // (measured 2-3 % slower: their spinning delays the launch's end)
+  const bool wait_kernel = std::getenv("KOORDHIP_FOLD_WAIT") == nullptr;
+  const bool persistent = !serial && !c->group && !std::getenv("KOORDHIP_ROUND_LAUNCH");
+  // A lone single-GPU context alternates the rounds between two evaluation
+  // streams (each with its own score matrix and select buffers; the resolve
+  // counts finished lists per round parity).
+  const bool two = persistent && c->world == 1 && c->sel_split && wait_kernel && !std::getenv("KOORDHIP_ONE_EVAL_STREAM");
+  // Pipeline depth: round r's lists are evaluated on the state after round
+  // r - 1 - lag.  Lag 2 (the default with the two evaluation streams) lets an
+  // evaluation overlap two resolve rounds; the resolve then re-evaluates the
+  // nodes of the last two rounds (k >= 3P).  Lag 1: k >= 2P.
   // pods per round: batch_pods, lowered until the resolve kernel's LDS holds
-  // the round (NodeNUMAResource rows are large); lag-1 needs k >= 2 x round size
+  // the round (NodeNUMAResource rows are large)
   int32_t P = c->batch;
-  while (P > 1 && kh::resolve_lds_bytes(P, 2 * P, c->n, c->numa) > 157 * 1024) P--;
-  const int32_t K = 2 * P;
+  int32_t lag = (two && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
+  if (lag == 2 && 3 * P > kh::kResolveMaxK) lag = 1;
+  while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, c->numa, lag) > 157 * 1024) P--;
+  const int32_t K = (lag + 1) * P;
   c->last_P = P;
+  c->last_lag = lag;
   const size_t lbytes = (size_t)kMaxBatch * 2 * kMaxBatch * sizeof(uint64_t);
   if (!c->d_lists) {
-    HIP_TRY(hipMalloc(&c->d_lists, 2 * lbytes));
+    HIP_TRY(hipMalloc(&c->d_lists, 4 * lbytes));
     HIP_TRY(hipMalloc(&c->d_final, 2 * lbytes));
     HIP_TRY(hipMalloc(&c->d_mod, (1 + kMaxBatch) * sizeof(int32_t) + kh::kPipeSyncBytes));
     HIP_TRY(hipMalloc(&c->d_desc, sizeof(kh::DevNodes)));
@@ -1124,7 +1146,7 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * lbytes));
     c->gather_world = c->world;
   }
-  if (kh::resolve_lds_bytes(P, K, c->n, c->numa) > 157 * 1024)
+  if (kh::resolve_lds_bytes(P, K, c->n, c->numa, lag) > 157 * 1024)
     return fail(KOORDHIP_EINVAL, "snapshot too large for the resolve kernel's LDS");
   if (c->group)
     if (int e = group_agree(c)) return e;
@@ -1145,9 +1167,9 @@ int place_staged_impl(koordhip_ctx *c) {
   HIP_TRY(hipMemsetAsync(sync, 0, kh::kPipeSyncBytes, c->stream));
   HIP_TRY(hipEventRecord(c->ev_start, c->stream));
   HIP_TRY(hipStreamWaitEvent(c->rstream, c->ev_start, 0));
-  // Lag-1 pipeline: round r's lists are evaluated (stream) while round r-1 is
-  // resolved (rstream); round r's evaluation waits only for round r-2's
-  // commits.  Both sides synchronise through device flags (PipeSync).  A lone
+  // Round pipeline: round r's lists are evaluated (stream) while rounds
+  // r-lag.. are resolved (rstream); round r's evaluation waits only for round
+  // r-1-lag's commits.  Both sides synchronise through device flags (PipeSync).  A lone
   // context runs ONE persistent resolve launch for the whole stream (no
   // per-round launch or event latency on the sequential path); contexts of a
   // local group share hardware queues with their peers, so they launch one
@@ -1155,27 +1177,12 @@ int place_staged_impl(koordhip_ctx *c) {
   // whatever the stream -> queue mapping).
   const int32_t total = c->n_staged;
   const int32_t rounds = (total + P - 1) / P;
-  // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises
-  // dispatches): every launch on one stream in dependency order, one resolve
-  // per round; the lists are then one round fresher than in the pipeline,
-  // which the resolve treats exactly like refreshed entries.
-  const bool serial = std::getenv("KOORDHIP_SERIAL") != nullptr;
-  // KOORDHIP_FOLD_WAIT: the split select's merging workgroups hold the stream
-  // until the resolve is far enough instead of a k_wait_resolved launch
-  // (measured 2-3 % slower: their spinning delays the launch's end)
-  const bool wait_kernel = std::getenv("KOORDHIP_FOLD_WAIT") == nullptr;
   hipStream_t rs = serial ? c->stream : c->rstream;
-  const bool persistent = !serial && !c->group && !std::getenv("KOORDHIP_ROUND_LAUNCH");
   const char *trace_env = std::getenv("KOORDHIP_TRACE_POD");  // diagnostics: printf one pod's resolve step
   const int32_t trace = trace_env ? std::atoi(trace_env) : -1;
   const int64_t list_buf = (int64_t)(lbytes / sizeof(uint64_t));
   uint64_t *lists0 = c->world > 1 ? c->d_final : c->d_lists;
   uint64_t *cpus = c->d_cpus;
-  // A lone single-GPU context alternates the rounds between two evaluation
-  // streams: round r+1's scan needs only round r-1's commits, so it runs while
-  // round r's select finishes (each stream keeps its own score matrix and
-  // select buffers; the resolve counts finished lists per round parity).
-  const bool two = persistent && c->world == 1 && c->sel_split && wait_kernel && !std::getenv("KOORDHIP_ONE_EVAL_STREAM");
   if (two && !c->stream2) {
     std::vector<uint32_t> m = full_cu_mask(c);  // its own queue too (see rstream)
     if (c->cu_reserve) m[0] &= ~1u;
@@ -1188,7 +1195,7 @@ int place_staged_impl(koordhip_ctx *c) {
   if (persistent && rounds > 0) {
     int32_t tm = -1;
     if (int e = timed_begin(c, TK_RESOLVE, c->rstream, &tm)) return e;
-    HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, sync,
+    HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, lag, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
     if (int e = timed_end(c, tm, c->rstream)) return e;
   }
@@ -1199,9 +1206,9 @@ int place_staged_impl(koordhip_ctx *c) {
     hipStream_t es = (two && par) ? c->stream2 : c->stream;
     const int slot = two ? par : 0;
     const kh::DevPod *pods = c->d_pods + p0;
-    uint64_t *lists = c->d_lists + (size_t)par * list_buf;
+    uint64_t *lists = c->d_lists + (size_t)(r & (2 * lag - 1)) * list_buf;
     const bool select_waits = c->sel_split && c->world == 1 && !wait_kernel;  // the previous select held the stream
-    if (r >= 2 && !serial && !select_waits) HIP_TRY(kh::launch_wait_resolved(sync, r - 1, es));
+    if (r > lag && !serial && !select_waits) HIP_TRY(kh::launch_wait_resolved(sync, r - lag, es));
     if (c->world > 1) {
       if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
       if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, nullptr, 0, 0, c->stream, 0)) return e;
@@ -1223,7 +1230,7 @@ int place_staged_impl(koordhip_ctx *c) {
       }
       int32_t tm = -1;
       if (int e = timed_begin(c, TK_RESOLVE, rs, &tm)) return e;
-      HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, sync,
+      HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, 1, sync,
                                  mbuf, c->d_out, cpus, c->d_dbg, trace, rs));
       if (int e = timed_end(c, tm, rs)) return e;
     }
@@ -1253,9 +1260,12 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[14], (unsigned long long)h[7], (unsigned long long)h[20],
                  (unsigned long long)h[21], (unsigned long long)h[5], (unsigned long long)h[6]);
     std::fprintf(stderr, "[koordhip stamps] resolve loop cycles: conflict detection %llu  bulk commits %llu | "
-                 "general path: candidate+keys %llu  commit %llu\n",
+                 "general path: candidate+keys %llu  commit %llu | write-back %llu | kernel total %llu\n",
                  (unsigned long long)h[16], (unsigned long long)h[17], (unsigned long long)h[18],
-                 (unsigned long long)h[19]);
+                 (unsigned long long)h[19], (unsigned long long)h[25], (unsigned long long)h[26]);
+    std::fprintf(stderr, "[koordhip stamps] round overlap: wave-0 end-of-round barrier %llu | wave 1: waiting for the "
+                 "next lists %llu  loading them %llu\n",
+                 (unsigned long long)h[29], (unsigned long long)h[27], (unsigned long long)h[28]);
     std::fprintf(stderr, "[koordhip stamps] general path detail: candidate + table keys %llu  row evaluations %llu | "
                  "pods served by the key tables %llu\n",
                  (unsigned long long)h[22], (unsigned long long)h[23], (unsigned long long)h[24]);
@@ -1457,6 +1467,8 @@ int koordhip_last_kernel_stats(koordhip_ctx *c, koordhip_kernel_stats *out) {
   out->evals = c->last_evals;
   out->pods = c->n_staged;
   out->rounds = (c->n_staged + c->last_P - 1) / std::max(c->last_P, 1);
+  out->round_pods = c->last_P;
+  out->lag = c->last_lag;
   return 0;
 }
 

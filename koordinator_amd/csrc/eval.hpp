@@ -331,9 +331,11 @@ __device__ __forceinline__ int32_t la_score(const DevPod &p, const NV &v, const 
 }
 
 // NodeNUMAResource Score (scoring.go:55-168).
+// filtered: the NodeNUMAResource Filter passed on this (pod, node) -- under a
+// required bind policy that already proved Allocate feasible (plugin.go:307-316)
 template <bool Z>
 __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, const NumaRow &r,
-                                              const DevNumaClass *classes, const DevCfg &c) {
+                                              const DevNumaClass *classes, const DevCfg &c, bool filtered = false) {
   if (p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0;
   if (r.cls < 0) return 0;  // no CPU topology: getResourceOptions / Allocate error -> 0
   const bool most = c.numa_most != 0;  // leastResourceScorer / mostResourceScorer (scoring.go:35-53)
@@ -373,7 +375,8 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
     }
   }
   if (cs) {
-    if (!mask && !numa_alloc_ok(C, r, p)) return 0;
+    const bool proven = filtered && tp == 0 && KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE;
+    if (!mask && !proven && !numa_alloc_ok(C, r, p)) return 0;
     rc = (double)r.cnt * 1000.0;  // requested cpu := allocated cpuset size (:161-166)
   }
   return numa_la(rc + p.req[KOORDHIP_RES_CPU], ac, rm + p.req[KOORDHIP_RES_MEM], am, c.numa_w_cpu, c.numa_w_mem, lr, dw);
@@ -396,8 +399,9 @@ __device__ __forceinline__ int32_t eval_total_numa(const DevPod &p, const NV &v,
                                                    const DevNumaClass *classes, const DevCfg &c) {
   int32_t t = eval_total(p, v, c);
   if (t < 0) return t;
-  if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter<Z>(p, r, classes)) return -1;
-  if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score<Z>(p, v, r, classes, c);
+  const bool nf = (c.filt & KOORDHIP_PLUGIN_NUMA) != 0;
+  if (nf && !numa_filter<Z>(p, r, classes)) return -1;
+  if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score<Z>(p, v, r, classes, c, nf);
   return t;
 }
 

@@ -50,17 +50,20 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
                              int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s);
 template <typename T>
 hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
-// The lag-1 round pipeline (kernels.hip): k_resolve resolves rounds [r_begin,
-// r_end) of the staged stream (P pods per round, k keys per list, lists double
-// buffered at lists0 + (r & 1) * list_buf); it waits for sel[r & 1] (the
+// The round pipeline (kernels.hip): k_resolve resolves rounds [r_begin, r_end)
+// of the staged stream (P pods per round, k keys per list).  Round r's lists
+// are evaluated on the state after round r - 1 - lag (lag 1: k >= 2P, lists
+// double buffered at lists0 + (r & 1) * list_buf; lag 2: one persistent
+// launch, k >= 3P, four buffers at (r & 3)); it waits for sel[r & 1] (the
 // cumulative pods of the rounds of r's parity) and publishes res_round in
-// `sync`; M' is handed between launches in mbuf ({count, nodes}).  The
+// `sync`; M' is handed between launches in mbuf ({count, nodes}, lag 1).  The
 // evaluation stream(s) bracket each round with k_wait_resolved (before k_scan)
 // and k_signal_lists (after the lists).
-int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa);
+constexpr int32_t kResolveMaxK = 128;  // longest list the resolve takes (RES_MAXP)
+int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa, int32_t lag);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
-                          PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
+                          int32_t lag, PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
                           int32_t trace, hipStream_t s);
 hipError_t launch_wait_resolved(PipeSync *sync, int32_t rounds, hipStream_t s);
 hipError_t launch_signal_lists(PipeSync *sync, int32_t par, int32_t pods, hipStream_t s);

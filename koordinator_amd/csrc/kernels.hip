@@ -1061,6 +1061,7 @@ constexpr int res_threads() { return NM ? 256 : 512; }
 constexpr int RES_PRE = 128;    // prefetched rows of list heads (RES_PRE / round size per pod)
 constexpr int RES_HASH = 256;   // node -> M' slot (open addressing)
 constexpr int RES_WE = 8;       // list entries the prologue walks per pod
+constexpr int RES_MHASH = 128;  // M node -> slot hash (|M| <= RES_MAXP_ROUND / 2 with lag 2, P otherwise)
 constexpr int RES_LDS_MAX = 160 * 1024 - 3 * 1024;  // dynamic LDS cap (static LDS: M' nodes, hashes, flags)
 
 // An NV row as 8-byte words (the lane-parallel Reserve): words 0-4 a[], 5-9
@@ -1088,7 +1089,7 @@ __device__ __forceinline__ NV slot_row(const NV &src) {
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
-      dec_key, dec_n, dec_src, dec_e, moved, mbits, gbits, kpre, ktab, ready, classes, modmap, total;
+      dec_key, dec_n, dec_src, dec_e, moved, mhash, gbits, kpre, ktab, ready, classes, modmap, total;
   // second copies of the per-round inputs, filled by waves 1.. while wave 0
   // resolves the previous round (overlap = 0: every round loads serially)
   int32_t overlap, lists2, pods2, pre_rows2, pre_numa2, pre_node2;
@@ -1097,7 +1098,7 @@ struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
 
 __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, bool numa,
-                                          bool overlap = false, bool tables = true) {
+                                          bool overlap = false, bool tables = true, int32_t lag = 1) {
   ResLds o;
   int32_t at = 0;
   const int32_t bitmap = res_align(((n_nodes + 31) >> 5) * 4);
@@ -1106,9 +1107,9 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   o.pods = at;
   at += res_align(n_pods_max * (int32_t)sizeof(DevPod));
   // two row regions, M' (prev) and M (cur), swapped at the end of every round;
-  // a round commits to at most n_pods_max nodes
-  const int32_t rows_b = res_align(n_pods_max * (int32_t)sizeof(NV));
-  const int32_t numa_b = numa ? res_align(n_pods_max * (int32_t)sizeof(NumaRow)) : 0;
+  // a round commits to at most n_pods_max nodes, M' spans `lag` rounds
+  const int32_t rows_b = res_align(lag * n_pods_max * (int32_t)sizeof(NV));
+  const int32_t numa_b = numa ? res_align(lag * n_pods_max * (int32_t)sizeof(NumaRow)) : 0;
   o.prev_rows = at;
   o.prev_numa = at + rows_b;
   at += rows_b + numa_b;
@@ -1137,8 +1138,8 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * RES_WE * 4;
   o.moved = at;  // per M' slot: committed to again this round (its row moved into M)
   at += RES_MAXP_ROUND * 4;
-  o.mbits = at;  // M bitmap
-  at += bitmap;
+  o.mhash = at;  // M node -> M slot (open addressing, RES_MHASH keys then slots)
+  at += 2 * RES_MHASH * 4;
   o.gbits = at;  // the nodes general-path pods committed to this round
   at += bitmap;
   // helper waves' key tables, per pod l (total + 1 as u16, 0 = infeasible):
@@ -1222,8 +1223,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                                                                  int32_t r_begin, int32_t r_end,
                                                                  int32_t *__restrict__ mbuf,
                                                                  const uint64_t *__restrict__ lists0,
-                                                                 int64_t list_buf, int32_t monotone, PipeSync *sy,
-                                                                 ResLds ofs, int32_t *__restrict__ out_node,
+                                                                 int64_t list_buf, int32_t monotone, int32_t lag,
+                                                                 PipeSync *sy, ResLds ofs, int32_t *__restrict__ out_node,
                                                                  uint64_t *__restrict__ out_cpus,
                                                                  uint64_t *__restrict__ dbg, int32_t trace) {
   constexpr int RES_THREADS = res_threads<NM>();
@@ -1246,7 +1247,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   int32_t *dec_src = reinterpret_cast<int32_t *>(lds + ofs.dec_src);
   int32_t *dec_e = reinterpret_cast<int32_t *>(lds + ofs.dec_e);
   int32_t *moved = reinterpret_cast<int32_t *>(lds + ofs.moved);
-  uint32_t *mbits = reinterpret_cast<uint32_t *>(lds + ofs.mbits);
+  int32_t *mkey = reinterpret_cast<int32_t *>(lds + ofs.mhash);
+  int32_t *mval = mkey + RES_MHASH;
   uint32_t *gbits = reinterpret_cast<uint32_t *>(lds + ofs.gbits);
   uint16_t *kpre = reinterpret_cast<uint16_t *>(lds + (ofs.kpre >= 0 ? ofs.kpre : 0));
   uint16_t *ktab = reinterpret_cast<uint16_t *>(lds + (ofs.ktab >= 0 ? ofs.ktab : 0));
@@ -1259,7 +1261,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   NV *pre2 = reinterpret_cast<NV *>(lds + ofs.pre_rows2);
   NumaRow *prenr2 = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa2);
   int32_t *pre_node2 = reinterpret_cast<int32_t *>(lds + ofs.pre_node2);
-  __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous round committed to
+  __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous `lag` rounds committed to
+  __shared__ int32_t pgen[RES_MAXP_ROUND];   // ... and the round that last did (lag 2)
   __shared__ int32_t seg_w[RES_MAXP_ROUND];  // staged winners by M slot (bulk commits)
   __shared__ int32_t ckey[RES_HASH], cval[RES_HASH];  // staged winner -> first pod (conflict detection)
   __shared__ int32_t sh_mp, sh_stop, sh_done;
@@ -1275,19 +1278,20 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     return *p;
   };
   const bool two = kp > 64;
+  const uint64_t t_kernel = (dbg && t == 0) ? stamp() : 0;
   if (t == 0) {
     sh_mp = r_begin > 0 ? min(mbuf[0], P) : 0;
     sh_stop = 0;
   }
   for (int32_t x = t; x < words; x += RES_THREADS) {
     modmap[x] = 0;
-    mbits[x] = 0;
     gbits[x] = 0;
   }
   for (int32_t x = t; x < RES_MAXP_ROUND; x += RES_THREADS) {
     moved[x] = 0;
     ready[x] = 0;
   }
+  for (int32_t x = t; x < RES_MHASH; x += RES_THREADS) mkey[x] = -1;
   for (int32_t x = t; x < RES_HASH; x += RES_THREADS) {
     ckey[x] = -1;
     cval[x] = 64;
@@ -1326,43 +1330,91 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   if (lane == 14 || lane == 16) doff = (int32_t)offsetof(DevPod, est_cpu);  // la_u / la_up (prod)
   if (lane == 15 || lane == 17) doff = (int32_t)offsetof(DevPod, est_mem);
   // diagnostics (KOORDHIP_STAMPS): cycles and counts per phase
-  uint64_t c_pro = 0, c_wait = 0, c_loop = 0, c_rel = 0, c_hash = 0;
+  uint64_t c_pro = 0, c_wait = 0, c_loop = 0, c_rel = 0, c_hash = 0, c_wb = 0;
+  uint64_t c_w1wait = 0, c_w1load = 0, c_bar = 0;  // wave 1: waiting for the next lists, loading them; wave 0: end-of-round barrier
   uint64_t c_l[4] = {0, 0, 0, 0};  // conflict detection, bulk commits, general-path candidate + keys, general commit
   uint64_t n_slow = 0, n_miss = 0, n_staged = 0, n_bulk = 0, n_tab = 0;
   uint64_t c_g[2] = {0, 0};  // general path: candidate from the list, row evaluations (to the last value)
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
+  // Every loop keeps several global loads in flight per thread before its LDS
+  // stores: wave 1 alone runs this for the next round (64 threads), where one
+  // load-store pair per iteration serialised ~40 HBM round trips.
   auto load_round = [&](int32_t rr, int32_t rp0, int32_t rn, uint64_t *Lk, DevPod *Lp, NV *Pr, NumaRow *Pn,
                         int32_t *Pnode, int32_t tid, int32_t nth) {
-    const uint64_t *L = lists0 + (size_t)(rr & 1) * list_buf;
-    for (int32_t x = tid; x < rn * kp; x += nth) {
-      const int32_t j = x / kp, q = x - j * kp;
-      Lk[x] = q < k ? L[(size_t)j * k + q] : 0ull;
+    const uint64_t *L = lists0 + (size_t)(rr & (2 * lag - 1)) * list_buf;
+    const int32_t tot = rn * kp;
+    for (int32_t x0 = tid; x0 < tot; x0 += 8 * nth) {
+      uint64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int32_t x = x0 + u * nth;
+        const int32_t j = x / kp, q = x - j * kp;
+        v[u] = (x < tot && q < k) ? L[(size_t)j * k + q] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (x0 + u * nth < tot) Lk[x0 + u * nth] = v[u];
     }
     {
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(pods + rp0);
-      uint32_t *dst = reinterpret_cast<uint32_t *>(Lp);
-      for (int32_t x = tid; x < rn * (int32_t)(sizeof(DevPod) / 4); x += nth) dst[x] = src[x];
-    }
-    for (int32_t sl = tid; sl < RES_PRE; sl += nth) {
-      const int32_t j = sl / HP, q = sl - j * HP;
-      int32_t nd = -1;
-      if (j < rn && q < k) {
-        const uint64_t e = L[(size_t)j * k + q];
-        if (e != 0) nd = key_node(e);
+      const uint4 *src = reinterpret_cast<const uint4 *>(pods + rp0);
+      uint4 *dst = reinterpret_cast<uint4 *>(Lp);
+      const int32_t n16 = rn * (int32_t)(sizeof(DevPod) / 16);
+      for (int32_t x0 = tid; x0 < n16; x0 += 4 * nth) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (x0 + u * nth < n16) v[u] = src[x0 + u * nth];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (x0 + u * nth < n16) dst[x0 + u * nth] = v[u];
       }
-      if (nd >= 0) {
-        NV v;
-        load_row(v, nodes(), nd);
-        Pr[sl] = v;
-        if constexpr (NUMA) {
-          NumaRow rr2;
-          load_numa_row<ZONES>(rr2, nodes(), nd);
-          Pn[sl] = rr2;
+    }
+    for (int32_t s0 = tid; s0 < RES_PRE; s0 += 2 * nth) {
+      int32_t nd[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int32_t sl = s0 + u * nth, j = sl / HP, q = sl - j * HP;
+        nd[u] = -1;
+        if (sl < RES_PRE && j < rn && q < k) {
+          const uint64_t e = L[(size_t)j * k + q];
+          if (e != 0) nd[u] = key_node(e);
         }
       }
-      Pnode[sl] = nd;
+      NV v[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+        if (nd[u] >= 0) load_row(v[u], nodes(), nd[u]);
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int32_t sl = s0 + u * nth;
+        if (sl >= RES_PRE) continue;
+        if (nd[u] >= 0) {
+          Pr[sl] = v[u];
+          if constexpr (NUMA) {
+            NumaRow rr2;
+            load_numa_row<ZONES>(rr2, nodes(), nd[u]);
+            Pn[sl] = rr2;
+          }
+        }
+        Pnode[sl] = nd[u];
+      }
     }
+  };
+  // M slot of node nd, -1 when nd is not in M
+  auto m_slot = [&](int32_t nd) -> int32_t {
+    uint32_t h = res_hash(nd) & (RES_MHASH - 1);
+    for (;;) {
+      const int32_t x = mkey[h];
+      if (x == nd) return mval[h];
+      if (x < 0) return -1;
+      h = (h + 1) & (RES_MHASH - 1);
+    }
+  };
+  auto m_insert = [&](int32_t nd, int32_t slot) {
+    uint32_t h = res_hash(nd) & (RES_MHASH - 1);
+    while (atomicCAS(&mkey[h], -1, nd) != -1) h = (h + 1) & (RES_MHASH - 1);
+    mval[h] = slot;
   };
   auto prev_slot = [&](int32_t nd) -> int32_t {
     uint32_t h = res_hash(nd);
@@ -1578,7 +1630,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             mrow[slot] = v;
             if constexpr (NUMA) mnr[slot] = ssrc >= 0 ? prenr[ssrc] : pnr[-ssrc - 1];
             if (ssrc < 0) moved[-ssrc - 1] = 1;
-            atomicOr(&mbits[sw >> 5], 1u << (sw & 31));
+            m_insert(sw, slot);
             atomicOr(&modmap[sw >> 5], 1u << (sw & 31));
             seg_w[slot] = sw;
           }
@@ -1658,7 +1710,32 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           c_g[0] += x - ts;
           ts = x;
         }
-        const int32_t nrows = tables ? 0 : nm + mp;
+        // a monotone pod without (usable) tables: only the X entries ranked
+        // above c can beat it -- their current rows are M or M' slots
+        const bool mono_g = monotone && !((slowmask >> g) & 1ull);
+        if (!tables && mono_g) {
+          const int first = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const uint64_t e = h ? e1 : e0;
+            const bool xh = (h ? x1 : x0) && 64 * h + lane < first;
+            uint64_t kv = 0;
+            if (__ballot(xh)) {
+              if (xh) {
+                const int32_t y = key_node(e);
+                const int32_t ms = m_slot(y);
+                const int32_t sl = ms >= 0 ? -1 : prev_slot(y);
+                const NV *row = ms >= 0 ? &mrow[ms] : &prow[sl];
+                NumaRow nr;
+                if constexpr (NUMA) nr = ms >= 0 ? mnr[ms] : pnr[sl];
+                kv = make_key(eval_row<NM>(pod, slot_row(*row), nr, cls, c), y);
+              }
+              kv = wave_max_u64_dpp(kv);
+              best = kv > best ? kv : best;
+            }
+          }
+        }
+        const int32_t nrows = (tables || mono_g) ? 0 : nm + mp;
         for (int32_t b0 = 0; b0 < nrows; b0 += 64) {  // rows: M slots, then the M' slots not moved into M
           const int32_t s = b0 + lane;
           uint64_t kv = 0;
@@ -1751,7 +1828,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             if (!hit) {
               if (lane == rw) my_node = w;
               if (lane == 0) {
-                atomicOr(&mbits[w >> 5], 1u << (w & 31));
+                m_insert(w, rw);
                 atomicOr(&modmap[w >> 5], 1u << (w & 31));
                 if (from_prev >= 0) moved[from_prev] = 1;
               }
@@ -1772,6 +1849,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         j = g + 1;
       }
       // ---- 4. write M back; M becomes the next round's M' (rows stay in LDS)
+      const uint64_t t_wb = dbg ? stamp() : 0;
       if (lane < nm) {
         const NV v = slot_row(mrow[lane]);
         mrow[lane] = v;
@@ -1782,27 +1860,47 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         }
       }
       if (lane == 0) __hip_atomic_store(&sh_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // helpers stop
-      // X of the next round = M: clear the words of M' and M (every bit set in
-      // them is X's), then set M's bits; M's and the general pods' bitmaps are
-      // cleared (both are subsets of M), and the staged-winner claims
+      // lag 2: the next round's lists were evaluated before this round and the
+      // previous one, so the M' slots the previous round committed to (and this
+      // one did not) stay in X: their current rows follow M's in the M region
+      const bool surv = lag > 1 && lane < mp && pgen[lane] == r - 1 && !moved[lane];
+      const uint64_t sbm = __ballot(surv);
+      const int32_t ns = __popcll(sbm);
+      const int32_t sidx = nm + __popcll(sbm & ((1ull << lane) - 1ull));
+      int32_t snode = -1;
+      if (surv) {
+        snode = pnode[lane];
+        mrow[sidx] = prow[lane];
+        if constexpr (NUMA) mnr[sidx] = pnr[lane];
+      }
+      // X of the next round = M (+ those): clear the words of M' and M (every
+      // bit set in them is X's), then set the next X's bits; M's and the general
+      // pods' bitmaps are cleared (both are subsets of M), and the staged-winner claims
       if (lane < mp) modmap[pnode[lane] >> 5] = 0;
       if (lane < nm) {
         modmap[my_node >> 5] = 0;
-        mbits[my_node >> 5] = 0;
         gbits[my_node >> 5] = 0;
       }
       for (int32_t x = lane; x < RES_HASH; x += 64) {
         ckey[x] = -1;
         cval[x] = 64;
       }
+      for (int32_t x = lane; x < RES_MHASH; x += 64) mkey[x] = -1;
       if (lane < nm) {
         atomicOr(&modmap[my_node >> 5], 1u << (my_node & 31));
         pnode[lane] = my_node;
+        pgen[lane] = r;
+      }
+      if (surv) {
+        atomicOr(&modmap[snode >> 5], 1u << (snode & 31));
+        pnode[sidx] = snode;
+        pgen[sidx] = r - 1;
       }
       moved[lane] = 0;
       const uint64_t t_rel = dbg ? stamp() : 0;
+      if (dbg) c_wb += t_rel - t_wb;
       if (lane == 0) {
-        sh_mp = nm;
+        sh_mp = nm + ns;
         store_release(&sy->res_round, r + 1);  // after every lane's stores (one wave: program order)
       }
       if (dbg) {
@@ -1816,12 +1914,19 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         //      (it waits for the lists itself: no barrier without wave 0)
         const int32_t np2 = min(P, total - (p0 + P));
         int ok = 1;
+        const uint64_t t1 = dbg ? stamp() : 0;
         if (lane == 0) ok = wait_at_least(&sy->sel[(r + 1) & 1], P * ((r + 1) >> 1) + np2, sy) ? 1 : 0;
+        const uint64_t t2 = dbg ? stamp() : 0;
         if (__builtin_amdgcn_readfirstlane(ok)) {
           load_round(r + 1, p0 + P, np2, lk2, lpod2, pre2, prenr2, pre_node2, lane, 64);
+          if (dbg) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            c_w1load += stamp() - t2;
+          }
         } else if (lane == 0) {
           sh_stop = 1;
         }
+        if (dbg) c_w1wait += t2 - t1;
       }
     } else {
       // ---- waves 2..: key tables for the general path, pod by pod (one pod
@@ -1857,7 +1962,9 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         if (lane == 0) __hip_atomic_store(&ready[l], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+    const uint64_t t_bar = (dbg && t == 0) ? stamp() : 0;
     __syncthreads();
+    if (dbg && t == 0) c_bar += stamp() - t_bar;
     for (int32_t x = t; x < RES_MAXP_ROUND; x += RES_THREADS) ready[x] = 0;
     if (ofs.overlap) {  // the next round's inputs become current
       uint64_t *a = lk;
@@ -1886,6 +1993,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     }
   }
   if (t <= RES_MAXP_ROUND && t <= sh_mp) mbuf[t] = t == 0 ? sh_mp : pnode[t - 1];  // hand M' on
+  if (dbg && t == 64) {
+    atomicAdd((unsigned long long *)&dbg[27], (unsigned long long)c_w1wait);
+    atomicAdd((unsigned long long *)&dbg[28], (unsigned long long)c_w1load);
+  }
   if (dbg && t == 0) {
     atomicAdd((unsigned long long *)&dbg[0], (unsigned long long)c_pro);
     atomicAdd((unsigned long long *)&dbg[1], (unsigned long long)c_wait);
@@ -1895,6 +2006,9 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[6], (unsigned long long)n_miss);
     atomicAdd((unsigned long long *)&dbg[7], (unsigned long long)total);
     atomicAdd((unsigned long long *)&dbg[14], (unsigned long long)c_rel);
+    atomicAdd((unsigned long long *)&dbg[25], (unsigned long long)c_wb);
+    atomicAdd((unsigned long long *)&dbg[26], (unsigned long long)(stamp() - t_kernel));
+    atomicAdd((unsigned long long *)&dbg[29], (unsigned long long)c_bar);
     for (int q = 0; q < 4; q++) atomicAdd((unsigned long long *)&dbg[16 + q], (unsigned long long)c_l[q]);
     atomicAdd((unsigned long long *)&dbg[20], (unsigned long long)n_bulk);
     atomicAdd((unsigned long long *)&dbg[21], (unsigned long long)n_staged);
@@ -2079,30 +2193,34 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
   return hipGetLastError();
 }
 
-int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa) {
-  int32_t kp = 1;
-  while (kp < k) kp <<= 1;
-  return res_lds(n_pods_max, kp, n_nodes, numa, false, false).total;
+// LDS list stride: k rounded up to 8 entries (zero padded)
+static inline int32_t list_stride(int32_t k) { return (k + 7) & ~7; }
+
+int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa, int32_t lag) {
+  const int32_t kp = list_stride(k);
+  return res_lds(n_pods_max, kp, n_nodes, numa, false, false, lag).total;
 }
 
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
-                          PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
+                          int32_t lag, PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,
                           int32_t trace, hipStream_t s) {
   if (total <= 0 || r_end <= r_begin) return hipSuccess;
   if (P > RES_MAXP_ROUND || P < 1 || k > RES_MAXP || k < 1) return hipErrorInvalidValue;
-  int32_t kp = 1;
-  while (kp < k) kp <<= 1;
+  // lag 2 (one persistent launch): M' spans two rounds, lists hold >= 3P entries
+  if (lag < 1 || lag > 2 || lag * P > RES_MAXP_ROUND || (lag > 1 && (k < 3 * P || r_begin != 0)))
+    return hipErrorInvalidValue;
+  const int32_t kp = list_stride(k);
   const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
   // a persistent launch preloads round r+1 during round r when both copies fit
   // the largest layout that fits: key tables and the next round's preload,
   // then without the preload, then without the tables
   const bool pre = r_end - r_begin > 1 && !std::getenv("KOORDHIP_NO_PRELOAD");
   const bool tab = !std::getenv("KOORDHIP_NO_KEY_TABLES");
-  ResLds o = res_lds(P, kp, d.n, numa, pre, tab);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, tab);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, pre, false);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, false);
+  ResLds o = res_lds(P, kp, d.n, numa, pre, tab, lag);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, tab, lag);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, pre, false, lag);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, false, lag);
   const int nm = numa ? (c.zones ? 2 : 1) : 0;
   static bool attr[3] = {false, false, false};
   if (!attr[nm]) {
@@ -2114,7 +2232,7 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   if (o.total > RES_LDS_MAX) return hipErrorInvalidValue;
 #define KH_RESOLVE(NN)                                                                                                \
   hipLaunchKernelGGL(k_resolve<NN>, dim3(1), dim3(res_threads<NN>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, \
-                     k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, sync, o, out_node, out_cpus, dbg, trace)
+                     k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, lag, sync, o, out_node, out_cpus, dbg, trace)
   if (nm == 2)
     KH_RESOLVE(2);
   else if (nm == 1)

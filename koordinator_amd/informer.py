@@ -1,0 +1,273 @@
+"""Event-driven marshaller: the scheduler's informer handlers kept as a
+ClusterState, turned into row deltas for ``koordhip_update_nodes``.
+
+The reference keeps its plugin state current with informer callbacks:
+LoadAwareScheduling's podAssignCache (loadaware/pod_assign_cache.go:53-117),
+the scheduler cache's NodeInfo (upstream: assigned, non-terminated pods),
+the pod lister that buildPodMetricMap consults (loadaware/helper.go:153-170)
+and the NodeMetric lister (load_aware.go:123-133, 269-287).  Every Filter /
+Score call then reads that state.  Here each event updates the same
+ClusterState that ``marshal.build_table`` reads and marks the node rows it can
+change dirty; ``flush`` recomputes only those rows (``marshal.node_row``) and
+hands them to the engine in one ``update_nodes`` call.  A flush also
+re-derives the rows whose NodeMetric crossed its expiry since the previous
+flush (the only input that changes with time alone).
+
+The node SET is positional on the device: adding or deleting a node needs a
+new snapshot (``flush`` returns ``needs_reload``; ``table()`` builds it).
+NodeNUMAResource columns are not derived from objects here (the host has no
+NodeResourceTopology object model); rows keep the NUMA columns of the table
+they were loaded from.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Set
+
+import numpy as np
+
+from . import k8s
+from .config import Profile
+from .marshal import AssignedPod, ClusterState, build_table, is_node_metric_expired, node_row
+from .snapshot import NodeTable
+
+
+class PodAssignCache:
+    """podAssignCache (loadaware/pod_assign_cache.go:35-117): node name ->
+    pod UID -> (pod, assign timestamp)."""
+
+    def __init__(self):
+        self.items: Dict[str, Dict[str, AssignedPod]] = {}
+
+    def assign(self, node_name: str, pod: k8s.Pod, now: float):
+        """:53-68 -- pods without a node or terminated are not cached."""
+        if node_name == "" or k8s.is_terminated(pod):
+            return
+        self.items.setdefault(node_name, {})[pod.uid] = AssignedPod(pod, now)
+
+    def unassign(self, node_name: str, pod: k8s.Pod):
+        """:70-80 -- the node's map goes away with its last pod."""
+        if node_name == "":
+            return
+        m = self.items.get(node_name)
+        if m is None:
+            return
+        m.pop(pod.uid, None)
+        if not m:
+            del self.items[node_name]
+
+    def on_add(self, pod: k8s.Pod, now: float):
+        self.assign(pod.node_name, pod, now)
+
+    def on_update(self, old: Optional[k8s.Pod], new: k8s.Pod, now: float):
+        """:91-101 -- a terminated pod leaves the cache, any other is (re)assigned."""
+        if k8s.is_terminated(new):
+            self.unassign(new.node_name, new)
+        else:
+            self.assign(new.node_name, new, now)
+
+    def on_delete(self, pod: k8s.Pod):
+        self.unassign(pod.node_name, pod)
+
+    def node_list(self, node_name: str) -> List[AssignedPod]:
+        return list(self.items.get(node_name, {}).values())
+
+
+@dataclass
+class FlushResult:
+    rows: int = 0                 # rows handed to update_nodes
+    needs_reload: bool = False    # the node set changed: load a new snapshot (table())
+    expired_flips: int = 0        # rows re-derived because a NodeMetric crossed its expiry
+
+
+class Informer:
+    """Node / Pod / NodeMetric event handlers over one ClusterState."""
+
+    def __init__(self, profile: Profile, nodes: List[k8s.Node] = (), now: float = 0.0):
+        self.profile = profile
+        self.cluster = ClusterState(nodes=list(nodes))
+        self.assign_cache = PodAssignCache()
+        self._index: Dict[str, int] = {n.name: i for i, n in enumerate(self.cluster.nodes)}
+        self._pods_by_uid: Dict[str, k8s.Pod] = {}
+        self._pod_node: Dict[str, str] = {}           # pod UID -> the node whose NodeInfo holds it
+        self._metric_refs: Dict[str, Set[str]] = {}   # pod key -> nodes whose NodeMetric lists it
+        self._dirty: Set[str] = set()
+        self._reload = False
+        self._expired: Dict[str, bool] = {}
+        self._table: Optional[NodeTable] = None
+        self._now = now
+
+    # ---- full snapshot --------------------------------------------------------
+    def table(self, now: float) -> NodeTable:
+        """A full snapshot of the current state (initial load, or after the node set changed)."""
+        self._sync_assigned()
+        t = build_table(self.cluster, self.profile, now)
+        if self._table is not None and self._table.n == t.n and self._table.names == t.names:
+            _keep_numa(t, self._table)
+        self._table = t
+        self._dirty.clear()
+        self._reload = False
+        self._expired = self._expiry_states(now)
+        self._now = now
+        return t
+
+    def attach(self, table: NodeTable, now: float):
+        """Adopt `table` (already loaded into the engine) as the current image."""
+        if table.names != [n.name for n in self.cluster.nodes]:
+            raise ValueError("table rows do not match the informer's node set")
+        self._table = table
+        self._expired = self._expiry_states(now)
+        self._now = now
+
+    # ---- node events -------------------------------------------------------------
+    def on_node_add(self, node: k8s.Node):
+        if node.name in self._index:
+            return self.on_node_update(None, node)
+        self._index[node.name] = len(self.cluster.nodes)
+        self.cluster.nodes.append(node)
+        self._reload = True
+
+    def on_node_update(self, old: Optional[k8s.Node], node: k8s.Node):
+        i = self._index.get(node.name)
+        if i is None:
+            return self.on_node_add(node)
+        self.cluster.nodes[i] = node
+        self._dirty.add(node.name)
+
+    def on_node_delete(self, node: k8s.Node):
+        i = self._index.pop(node.name, None)
+        if i is None:
+            return
+        del self.cluster.nodes[i]
+        self._index = {n.name: j for j, n in enumerate(self.cluster.nodes)}
+        self.cluster.node_metrics.pop(node.name, None)
+        self._reload = True
+
+    # ---- pod events ----------------------------------------------------------------
+    def _node_pods_set(self, pod: k8s.Pod, present: bool):
+        """NodeInfo.Pods: assigned, non-terminated pods (upstream scheduler cache)."""
+        nn = self._pod_node.pop(pod.uid, None)
+        if nn is not None:
+            self.cluster.node_pods[nn] = [p for p in self.cluster.node_pods.get(nn, []) if p.uid != pod.uid]
+            self._dirty.add(nn)
+        if present and pod.node_name and not k8s.is_terminated(pod):
+            self.cluster.node_pods.setdefault(pod.node_name, []).append(pod)
+            self._pod_node[pod.uid] = pod.node_name
+            self._dirty.add(pod.node_name)
+
+    def _touch_metric_refs(self, pod: k8s.Pod):
+        for nn in self._metric_refs.get(pod.key, ()):
+            self._dirty.add(nn)
+
+    def on_pod_add(self, pod: k8s.Pod, now: float):
+        old = self._pods_by_uid.get(pod.uid)
+        if old is not None:
+            return self.on_pod_update(old, pod, now)
+        self._pods_by_uid[pod.uid] = pod
+        self.cluster.pods[pod.key] = pod
+        self._node_pods_set(pod, True)
+        self.assign_cache.on_add(pod, now)
+        if pod.node_name:
+            self._dirty.add(pod.node_name)
+        self._touch_metric_refs(pod)
+
+    def on_pod_update(self, old: Optional[k8s.Pod], pod: k8s.Pod, now: float):
+        prev = self._pods_by_uid.get(pod.uid)
+        if prev is not None and prev.key != pod.key:
+            self.cluster.pods.pop(prev.key, None)
+            self._touch_metric_refs(prev)
+        self._pods_by_uid[pod.uid] = pod
+        self.cluster.pods[pod.key] = pod
+        self._node_pods_set(pod, True)
+        if prev is not None and prev.node_name and prev.node_name != pod.node_name:
+            # the assign cache is keyed by the pod's current node (pod_assign_cache.go:91-101)
+            self.assign_cache.unassign(prev.node_name, prev)
+            self._dirty.add(prev.node_name)
+        self.assign_cache.on_update(old, pod, now)
+        if pod.node_name:
+            self._dirty.add(pod.node_name)
+        self._touch_metric_refs(pod)
+
+    def on_pod_delete(self, pod: k8s.Pod):
+        prev = self._pods_by_uid.pop(pod.uid, pod)
+        self.cluster.pods.pop(prev.key, None)
+        self._node_pods_set(prev, False)
+        self.assign_cache.on_delete(prev)
+        if prev.node_name:
+            self._dirty.add(prev.node_name)
+        self._touch_metric_refs(prev)
+
+    # ---- NodeMetric events -------------------------------------------------------------
+    def on_node_metric(self, nm: k8s.NodeMetric):
+        """Add or update."""
+        old = self.cluster.node_metrics.get(nm.name)
+        if old is not None:
+            for pm in old.pods_metric:
+                self._metric_refs.get(f"{pm.namespace}/{pm.name}", set()).discard(nm.name)
+        self.cluster.node_metrics[nm.name] = nm
+        for pm in nm.pods_metric:
+            self._metric_refs.setdefault(f"{pm.namespace}/{pm.name}", set()).add(nm.name)
+        self._dirty.add(nm.name)
+
+    def on_node_metric_delete(self, name: str):
+        old = self.cluster.node_metrics.pop(name, None)
+        if old is not None:
+            for pm in old.pods_metric:
+                self._metric_refs.get(f"{pm.namespace}/{pm.name}", set()).discard(name)
+        self._dirty.add(name)
+
+    # ---- deltas ----------------------------------------------------------------------------
+    def _sync_assigned(self):
+        self.cluster.assigned = {nn: list(m.values()) for nn, m in self.assign_cache.items.items()}
+
+    def _expiry_states(self, now: float) -> Dict[str, bool]:
+        exp = self.profile.resolved().loadaware.node_metric_expiration_seconds
+        return {nn: is_node_metric_expired(nm, exp, now) for nn, nm in self.cluster.node_metrics.items()}
+
+    def pending(self) -> Set[str]:
+        return set(self._dirty)
+
+    def delta(self, now: float):
+        """(row indices, NodeTable of those rows, FlushResult); applies them to
+        the informer's own table image too."""
+        res = FlushResult(needs_reload=self._reload)
+        if self._reload or self._table is None:
+            res.needs_reload = True
+            return np.zeros(0, np.int32), None, res
+        states = self._expiry_states(now)
+        dirty = set(n for n in self._dirty if n in self._index)
+        for nn, st in states.items():
+            if self._expired.get(nn) != st and nn in self._index and nn not in dirty:
+                dirty.add(nn)
+                res.expired_flips += 1
+        self._expired = states
+        self._now = now
+        if not dirty:
+            self._dirty.clear()
+            return np.zeros(0, np.int32), None, res
+        self._sync_assigned()
+        idx = np.array(sorted(self._index[n] for n in dirty), np.int32)
+        rows = self._table.rows(idx)
+        for j, i in enumerate(idx):
+            node_row(rows, j, self.cluster.nodes[int(i)], self.cluster, self.profile, now)
+        for c in rows.cols:
+            self._table.cols[c][idx] = rows.cols[c]
+        self._dirty.clear()
+        res.rows = len(idx)
+        return idx, rows, res
+
+    def flush(self, engine, now: float) -> FlushResult:
+        """Push the pending row deltas into `engine` (one koordhip_update_nodes call)."""
+        idx, rows, res = self.delta(now)
+        if res.needs_reload or rows is None:
+            return res
+        engine.update_nodes(idx, rows)
+        return res
+
+
+def _keep_numa(dst: NodeTable, src: NodeTable):
+    """NUMA columns are not derived from objects: carry them over."""
+    from .snapshot import NUMA_MUTABLE, U64_COLS, ZONE_COLS
+    for c in set(U64_COLS) | set(NUMA_MUTABLE) | set(ZONE_COLS) | {"numa_class", "numa_flags"}:
+        dst.cols[c] = src.cols[c].copy()
+    dst.numa_classes = src.numa_classes

@@ -251,7 +251,7 @@ def test_sharded_group_bit_exact(Engine, world, n_nodes, n_pods, be, batch):
 
 # ----------------------------------------------------------- launch modes
 @pytest.mark.parametrize("mode", ["KOORDHIP_ROUND_LAUNCH", "KOORDHIP_SERIAL", "KOORDHIP_CU_RESERVE", "KOORDHIP_ONE_EVAL_STREAM", "KOORDHIP_NO_KEY_TABLES",
-                                  "KOORDHIP_FOLD_WAIT", "KOORDHIP_SELECT_ONEWG"])
+                                  "KOORDHIP_FOLD_WAIT", "KOORDHIP_SELECT_ONEWG", "KOORDHIP_LAG1"])
 @pytest.mark.parametrize("numa", [False, True])
 def test_launch_modes_bit_exact(Engine, monkeypatch, mode, numa):
     """The per-round resolve launch (local groups), the single-stream

@@ -1,0 +1,215 @@
+"""The event-driven marshaller (koordinator_amd/informer.py): podAssignCache
+semantics pinned by the reference's pod_assign_cache_test.go tables, and
+randomized event streams whose incremental row deltas equal a from-scratch
+build_table of the same ClusterState after every flush."""
+import copy
+
+import numpy as np
+import pytest
+
+from koordinator_amd import k8s
+from koordinator_amd.config import shipped_profile
+from koordinator_amd.informer import Informer, PodAssignCache
+from koordinator_amd.marshal import build_table
+from koordinator_amd.snapshot import ALL_COLS
+
+NOW = 1_000_000.0
+
+
+def _pod(uid="123456789", node="test-node", phase="Running", ns="default", name="test"):
+    return k8s.Pod(namespace=ns, name=name, uid=uid, node_name=node, phase=phase)
+
+
+def _cache(c: PodAssignCache):
+    return {n: sorted(m) for n, m in c.items.items()}
+
+
+# pod_assign_cache_test.go:35-107 TestPodAssignCache_OnAdd
+@pytest.mark.parametrize("pod,want", [
+    (k8s.Pod(), {}),                                               # update pending pod (:42-45)
+    (_pod(uid="", phase="Failed"), {}),                            # update terminated pod (:46-57)
+    (_pod(), {"test-node": ["123456789"]}),                        # update scheduled running pod (:58-93)
+], ids=["pending", "terminated", "running"])
+def test_assign_cache_on_add(pod, want):
+    c = PodAssignCache()
+    c.on_add(pod, NOW)
+    assert _cache(c) == want
+    for n, m in c.items.items():
+        assert all(info.timestamp == NOW for info in m.values())
+
+
+# pod_assign_cache_test.go:109-212 TestPodAssignCache_OnUpdate
+@pytest.mark.parametrize("start,pod,want", [
+    (None, k8s.Pod(), {}),                                          # update pending pod (:116-120)
+    ({"test-node": [_pod()]}, _pod(phase="Failed"), {}),            # update terminated pod (:121-159)
+    (None, _pod(), {"test-node": ["123456789"]}),                   # update scheduled running pod (:160-195)
+], ids=["pending", "terminated", "running"])
+def test_assign_cache_on_update(start, pod, want):
+    c = PodAssignCache()
+    for n, pods in (start or {}).items():
+        for p in pods:
+            c.assign(n, p, NOW)
+    c.on_update(None, pod, NOW)
+    assert _cache(c) == want
+
+
+def test_assign_cache_on_delete():
+    """pod_assign_cache_test.go:214-250: deleting the node's last pod drops the node."""
+    c = PodAssignCache()
+    c.assign("test-node", _pod(), NOW)
+    c.on_delete(_pod(phase="Failed"))
+    assert _cache(c) == {}
+
+
+# ------------------------------------------------------------------ random event streams
+GI = 1 << 30
+
+
+def _rand_pod(rng, i, nodes):
+    prio = [None, 9500, 5500, 3500][rng.integers(0, 4)]
+    cpu = int(rng.choice([100, 250, 500, 1000, 2000]))
+    mem = int(rng.choice([128, 256, 1024, 2048])) << 20
+    req = {k8s.CPU: k8s.Q(f"{cpu}m"), k8s.MEMORY: k8s.Q(mem)}
+    if prio == 5500:  # batch resources
+        req = {k8s.BATCH_CPU: k8s.Q(cpu), k8s.BATCH_MEMORY: k8s.Q(mem)}
+    node = nodes[rng.integers(0, len(nodes))].name if rng.random() < 0.8 else ""
+    return k8s.Pod(namespace="ns", name=f"p{i}", uid=f"u{i}", priority=prio, node_name=node,
+                   containers=[k8s.Container(requests=req, limits=dict(req))])
+
+
+def _rand_metric(rng, node, pods, now):
+    on = [p for p in pods if p.node_name == node.name]
+    pm = [k8s.PodMetric(p.namespace, p.name, {k8s.CPU: k8s.Q(f"{int(rng.integers(10, 900))}m"),
+                                               k8s.MEMORY: k8s.Q(int(rng.integers(1, 500)) << 20)})
+          for p in on if rng.random() < 0.7]
+    return k8s.NodeMetric(name=node.name, update_time=now - float(rng.integers(0, 400)), report_interval_s=60,
+                          node_usage={k8s.CPU: k8s.Q(f"{int(rng.integers(0, 30000))}m"),
+                                      k8s.MEMORY: k8s.Q(int(rng.integers(0, 60)) * GI)},
+                          pods_metric=pm)
+
+
+class _TableEngine:
+    """Stands in for the device: applies update_nodes rows to a NodeTable."""
+
+    def __init__(self, table):
+        self.table = table.copy()
+
+    def update_nodes(self, idx, rows):
+        for c in ALL_COLS:
+            self.table.cols[c][idx] = rows.cols[c]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_incremental_rows_equal_rebuild(seed):
+    rng = np.random.default_rng(seed)
+    prof = shipped_profile()
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110),
+                                                 k8s.BATCH_CPU: k8s.Q(20000), k8s.BATCH_MEMORY: k8s.Q(40 * GI)})
+             for i in range(12)]
+    inf = Informer(prof, nodes, NOW)
+    pods = [_rand_pod(rng, i, nodes) for i in range(40)]
+    now = NOW
+    for p in pods:
+        inf.on_pod_add(p, now)
+    for n in nodes:
+        if rng.random() < 0.8:
+            inf.on_node_metric(_rand_metric(rng, n, pods, now))
+    eng = _TableEngine(inf.table(now))
+    live = {p.uid: p for p in pods}
+    nxt = len(pods)
+    for step in range(25):
+        now += float(rng.integers(1, 120))
+        for _ in range(int(rng.integers(1, 8))):
+            op = rng.random()
+            if op < 0.3:                                   # new pod (pending or bound)
+                p = _rand_pod(rng, nxt, nodes)
+                nxt += 1
+                live[p.uid] = p
+                inf.on_pod_add(p, now)
+            elif op < 0.5 and live:                        # bind / move / finish a pod
+                p = copy.deepcopy(live[list(live)[int(rng.integers(0, len(live)))]])
+                r = rng.random()
+                if r < 0.4:
+                    p.node_name = nodes[int(rng.integers(0, len(nodes)))].name
+                elif r < 0.7:
+                    p.phase = "Succeeded"
+                else:
+                    p.labels = {"x": str(step)}
+                live[p.uid] = p
+                inf.on_pod_update(None, p, now)
+            elif op < 0.65 and live:                       # delete a pod
+                p = live.pop(list(live)[int(rng.integers(0, len(live)))])
+                inf.on_pod_delete(p)
+            elif op < 0.85:                                # NodeMetric report
+                n = nodes[int(rng.integers(0, len(nodes)))]
+                inf.on_node_metric(_rand_metric(rng, n, list(live.values()), now))
+            elif op < 0.92:                                # NodeMetric gone
+                inf.on_node_metric_delete(nodes[int(rng.integers(0, len(nodes)))].name)
+            else:                                          # node allocatable change
+                i = int(rng.integers(0, len(nodes)))
+                n = copy.deepcopy(nodes[i])
+                n.allocatable[k8s.CPU] = k8s.Q(int(rng.choice([16, 32, 48])))
+                nodes[i] = n
+                inf.on_node_update(None, n)
+        res = inf.flush(eng, now)
+        assert not res.needs_reload
+        want = build_table(inf.cluster, prof, now)
+        for c in ALL_COLS:
+            assert np.array_equal(eng.table.cols[c], want.cols[c]), (step, c)
+
+
+def test_node_set_change_needs_reload():
+    prof = shipped_profile()
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(8), k8s.MEMORY: k8s.Q(GI), k8s.PODS: k8s.Q(10)})
+             for i in range(3)]
+    inf = Informer(prof, nodes, NOW)
+    inf.table(NOW)
+    inf.on_node_add(k8s.Node(name="n3", allocatable={k8s.CPU: k8s.Q(8)}))
+    assert inf.flush(_TableEngine(inf.table(NOW)), NOW).needs_reload is False  # table() rebuilt it
+    inf.on_node_delete(nodes[0])
+    assert inf.delta(NOW)[2].needs_reload
+    t = inf.table(NOW)
+    assert t.names == ["n1", "n2", "n3"]
+
+
+@pytest.mark.gpu
+def test_gpu_informer_deltas_then_stream():
+    """Informer deltas through koordhip_update_nodes, then a greedy stream: the
+    device state and placements equal a fresh snapshot of the same objects."""
+    import torch  # noqa: F401
+    import oracle
+    from koordinator_amd.config import to_c_config
+    from koordinator_amd.engine import PlacementEngine
+    from koordinator_amd import synth
+    rng = np.random.default_rng(9)
+    prof = shipped_profile()
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110),
+                                                 k8s.BATCH_CPU: k8s.Q(20000), k8s.BATCH_MEMORY: k8s.Q(40 * GI)})
+             for i in range(200)]
+    inf = Informer(prof, nodes, NOW)
+    pods = [_rand_pod(rng, i, nodes) for i in range(600)]
+    for p in pods:
+        inf.on_pod_add(p, NOW)
+    for n in nodes:
+        inf.on_node_metric(_rand_metric(rng, n, pods, NOW))
+    stream = synth.make_pods(synth.StreamSpec(400, be_frac=0.3), prof)
+    with PlacementEngine(prof, device=0) as e:
+        e.load_snapshot(inf.table(NOW))
+        now = NOW + 30
+        for p in pods[::7]:
+            q = copy.deepcopy(p)
+            q.phase = "Succeeded"
+            inf.on_pod_update(None, q, now)
+        for n in nodes[::5]:
+            inf.on_node_metric(_rand_metric(rng, n, pods, now))
+        res = inf.flush(e, now)
+        assert res.rows > 0 and not res.needs_reload
+        got = e.place_stream(stream)
+        st = e.read_nodes()
+    fresh = build_table(inf.cluster, prof, now)
+    o = oracle.Oracle(to_c_config(prof), fresh)
+    ref = o.place_stream(stream)
+    assert np.array_equal(got, ref)
+    rs = o.state()
+    for k in ("requested", "npods", "la_used"):
+        assert np.array_equal(st[k], rs[k]), k
