@@ -1114,7 +1114,9 @@ int place_staged_impl(koordhip_ctx *c) {
   // pods per round: batch_pods, lowered until the resolve kernel's LDS holds
   // the round (NodeNUMAResource rows are large)
   int32_t P = c->batch;
-  int32_t lag = (two && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
+  // (NodeNUMAResource streams are bound by the resolve's cpuset Reserve: the
+  // longer re-evaluated set of lag 2 measured slower there, 87k vs 93k pods/s)
+  int32_t lag = (two && !c->numa && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
   if (lag == 2 && 3 * P > kh::kResolveMaxK) lag = 1;
   while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, c->numa, lag) > 157 * 1024) P--;
   const int32_t K = (lag + 1) * P;
@@ -1156,8 +1158,8 @@ int place_staged_impl(koordhip_ctx *c) {
   c->last_launches = 0;
   c->last_evals = 0;
   if (std::getenv("KOORDHIP_STAMPS")) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 32 * sizeof(uint64_t)));
-    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 32 * sizeof(uint64_t), c->stream));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 48 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 48 * sizeof(uint64_t), c->stream));
   }
   int32_t *mbuf = c->d_mod;  // M' handed between resolve launches
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
@@ -1246,7 +1248,7 @@ int place_staged_impl(koordhip_ctx *c) {
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   c->pipe_check = true;
   if (c->d_dbg) {
-    uint64_t h[32];
+    uint64_t h[48];
     HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     std::fprintf(stderr,
@@ -1266,6 +1268,12 @@ int place_staged_impl(koordhip_ctx *c) {
     std::fprintf(stderr, "[koordhip stamps] round overlap: wave-0 end-of-round barrier %llu | wave 1: waiting for the "
                  "next lists %llu  loading them %llu\n",
                  (unsigned long long)h[29], (unsigned long long)h[27], (unsigned long long)h[28]);
+    if (c->numa)
+      std::fprintf(stderr, "[koordhip stamps] NUMA: accumulator replays full %llu cycles / %llu, spread %llu / %llu | "
+                   "row passes of required-spread pods %llu / %llu, of other pods %llu / %llu\n",
+                   (unsigned long long)h[32], (unsigned long long)h[33], (unsigned long long)h[34],
+                   (unsigned long long)h[35], (unsigned long long)h[36], (unsigned long long)h[37],
+                   (unsigned long long)h[38], (unsigned long long)h[39]);
     std::fprintf(stderr, "[koordhip stamps] general path detail: candidate + table keys %llu  row evaluations %llu | "
                  "pods served by the key tables %llu\n",
                  (unsigned long long)h[22], (unsigned long long)h[23], (unsigned long long)h[24]);

@@ -1335,6 +1335,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t c_l[4] = {0, 0, 0, 0};  // conflict detection, bulk commits, general-path candidate + keys, general commit
   uint64_t n_slow = 0, n_miss = 0, n_staged = 0, n_bulk = 0, n_tab = 0;
   uint64_t c_g[2] = {0, 0};  // general path: candidate from the list, row evaluations (to the last value)
+  uint64_t c_nx[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // NUMA: accumulator replays {full, spread} and row passes {req. spread, other}: cycles, count
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
   // Every loop keeps several global loads in flight per thread before its LDS
@@ -1736,6 +1737,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           }
         }
         const int32_t nrows = (tables || mono_g) ? 0 : nm + mp;
+        const uint64_t t_rows = dbg ? stamp() : 0;
         for (int32_t b0 = 0; b0 < nrows; b0 += 64) {  // rows: M slots, then the M' slots not moved into M
           const int32_t s = b0 + lane;
           uint64_t kv = 0;
@@ -1754,6 +1756,11 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           }
           kv = wave_max_u64_dpp(kv);
           best = kv > best ? kv : best;
+        }
+        if (dbg && NUMA && nrows > 0) {
+          const int b = KOORDHIP_NUMA_REQUIRED(pod.numa_policy) == KOORDHIP_CPUBIND_SPREAD_BY_PCPUS ? 4 : 6;
+          c_nx[b] += stamp() - t_rows;
+          c_nx[b + 1]++;
         }
         lap(2);
         uint64_t cpus[NW] = {0, 0, 0, 0};
@@ -1799,10 +1806,16 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               // zone hint) on the row, the chosen CPUs are broadcast to the wave
               uint64_t mc[NW] = {0, 0, 0, 0};
               int okl = 0;
+              const uint64_t t_acc = dbg ? stamp() : 0;
               if (lane == 0) {
                 NumaRow nr = *snr;
                 okl = numa_reserve<ZONES>(cls, nr, pod, mc);
                 if (okl) mnr[rw] = nr;
+              }
+              if (dbg) {
+                const int b = KOORDHIP_NUMA_PREFERRED(pod.numa_policy) == KOORDHIP_CPUBIND_SPREAD_BY_PCPUS ? 2 : 0;
+                c_nx[b] += stamp() - t_acc;
+                c_nx[b + 1]++;
               }
               okr = __builtin_amdgcn_readfirstlane(okl) != 0;
 #pragma unroll
@@ -2009,6 +2022,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[25], (unsigned long long)c_wb);
     atomicAdd((unsigned long long *)&dbg[26], (unsigned long long)(stamp() - t_kernel));
     atomicAdd((unsigned long long *)&dbg[29], (unsigned long long)c_bar);
+    for (int q = 0; q < 8; q++) atomicAdd((unsigned long long *)&dbg[32 + q], (unsigned long long)c_nx[q]);
     for (int q = 0; q < 4; q++) atomicAdd((unsigned long long *)&dbg[16 + q], (unsigned long long)c_l[q]);
     atomicAdd((unsigned long long *)&dbg[20], (unsigned long long)n_bulk);
     atomicAdd((unsigned long long *)&dbg[21], (unsigned long long)n_staged);

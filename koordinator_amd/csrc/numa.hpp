@@ -29,11 +29,27 @@ namespace kh {
 
 // The running best of the node / socket selection loops (whose trip counts
 // come from the per-node topology class, i.e. divergent in the scan kernel) is
-// kept in memory: with ROCm 7.2's optimizer these selections came out wrong
+// pinned: with ROCm 7.2's optimizer these selections came out wrong
 // (tests/test_gpu_numa.py: e.g. "allocate in the smallest idle socket") unless
 // the functions were built optnone, which made the scan 5x and the cpuset
-// Reserve 30x slower.  Pinning just these variables is enough.
-#define KH_PINNED volatile
+// Reserve 30x slower.  Pinning just these variables is enough: after every
+// iteration an empty asm takes the value in a VGPR and hands it back "changed":
+// the optimizer can neither fold the running best into a select chain nor
+// move it across iterations, and the value stays in a register (a volatile
+// stack slot cost a scratch round trip per access: ~30k cycles per Reserve).
+#define KH_PIN(x) asm volatile("" : "+v"(x))
+
+// The selections themselves are a max over one integer key per candidate:
+// the strategy-ordered primary and secondary counts (MostAllocated:
+// ascending, LeastAllocated: descending; <= 256 each), then the lower index
+// (ties keep the first candidate, like the reference's strict comparisons).
+// A plain integer max-reduction is what the optimizer handles robustly.
+__device__ __forceinline__ int sel_key(int most, int primary, int secondary, int idx) {
+  const int p = most ? 511 - primary : primary;
+  const int q = most ? 511 - secondary : secondary;
+  return (1 << 30) | (p << 20) | (q << 10) | (1023 - idx);
+}
+__device__ __forceinline__ int sel_index(int key) { return key ? 1023 - (key & 1023) : -1; }
 
 constexpr int NW = KOORDHIP_NUMA_WORDS;
 constexpr int NMAX = KOORDHIP_NUMA_MAX_NODES;
@@ -147,32 +163,27 @@ __device__ __attribute__((noinline)) bool numa_spread_ok(const DevNumaClass &C, 
     for (int k = 0; k < C.nnuma; k++)
       if (cores_in(F, C.nm[k], cpc) >= need) return true;
     // pass false: the first node in (free, socket free, id) order with >= need CPUs decides
-    KH_PINNED int best = -1, bf = 0, bs = 0;
+    int bkey = 0;
     for (int k = 0; k < C.nnuma; k++) {
       const int f = popc_and(r.fr, C.nm[k]);
       if (f < need) continue;
       const int sf = popc_and(r.fr, C.sm[C.sock_of_node[k]]);
-      if (best < 0 || (f != bf ? free_before(most, f, bf) : (sf != bs ? free_before(most, sf, bs) : false))) {
-        best = k;
-        bf = f;
-        bs = sf;
-      }
+      bkey = max(bkey, sel_key(most, f, sf, k));
     }
+    const int best = sel_index(bkey);
     if (best >= 0) return cores_in(r.fr, C.nm[best], cpc) >= need;
   }
   if (need <= C.cps) {
     for (int w = 0; w < NW; w++) F[w] = r.fr[w] & ~Xp[w];  // socket pass true filters PCPULevel only (:612)
     for (int s = 0; s < C.nsock; s++)
       if (cores_in(F, C.sm[s], cpc) >= need) return true;
-    KH_PINNED int best = -1, bf = 0;
+    int bkey = 0;
     for (int s = 0; s < C.nsock; s++) {
       const int f = popc_and(r.fr, C.sm[s]);
       if (f < need) continue;
-      if (best < 0 || (f != bf && free_before(most, f, bf))) {
-        best = s;
-        bf = f;
-      }
+      bkey = max(bkey, sel_key(most, f, 0, s));
     }
+    const int best = sel_index(bkey);
     if (best >= 0) return cores_in(r.fr, C.sm[best], cpc) >= need;
   }
   // freeCPUs(true) spread, then freeCPUs(false) over what is left (:218-229)
@@ -256,7 +267,7 @@ __device__ __forceinline__ int32_t numa_la(double rc, double ac, double rm, doub
 //
 // The replay's functions stay noinline (one copy, called from the 1-wave
 // resolve and from k_commit); their node / socket selections keep the running
-// best in KH_PINNED variables (see the top of this file): ROCm 7.2 otherwise
+// best pinned by KH_PIN (see the top of this file): ROCm 7.2 otherwise
 // picks a different NUMA node / socket than the reference's order for some
 // states, -O2 and -O3 alike.  tests/test_gpu_numa.py pins every choice bit for
 // bit (reference KATs, randomized states, streams).
@@ -312,7 +323,7 @@ __device__ __forceinline__ void acc_excluded(const DevNumaClass &C, const Acc &a
 // freeCPUsInSocket + spreadCPUs): round t takes each core's t-th CPU by id,
 // rounds in id order; lists of <= cpc CPUs are kept in id order.  Takes n.
 __device__ __attribute__((noinline)) void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
-  const int len = popc4(m);
+  int len = popc4(m);
   if (len <= C.cpc) {
     for (int i = 0; i < C.ncpu && n > 0; i++) {
       const int p = C.pos_by_id[i];
@@ -460,7 +471,7 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
           FA[w] = expand(fold_and(allowed, cpc), cpc);
           X[w] = fe ? X[w] : 0;
         }
-        KH_PINNED int best = -1, bc = 0, bs = 0;
+        int bkey = 0;
         for (int k = 0; k < C.nnuma; k++) {
           const int cnt = popc_and(FA, C.nm[k]);
           if (cnt < a.need) continue;
@@ -470,12 +481,9 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
             if (fe && a.excl == (int)KOORDHIP_CPUEXCL_NUMA) allowed &= ~X[w];
             sf += __popcll(allowed & C.sm[C.sock_of_node[k]][w]);
           }
-          if (best < 0 || (cnt != bc ? free_before(a.most, cnt, bc) : (sf != bs && free_before(a.most, sf, bs)))) {
-            best = k;
-            bc = cnt;
-            bs = sf;
-          }
+          bkey = max(bkey, sel_key(a.most, cnt, sf, k));
         }
+        const int best = sel_index(bkey);
         if (best >= 0) {
           for (int w = 0; w < NW; w++) T[w] = FA[w] & C.nm[best][w];
           acc_take_low(C, a, T, a.need);
@@ -485,15 +493,13 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
     }
     for (int w = 0; w < NW; w++) FA[w] = expand(fold_and(a.A[w], cpc), cpc);
     if (a.need <= C.cps) {  // :126-134
-      KH_PINNED int best = -1, bc = 0;
+      int bkey = 0;
       for (int s = 0; s < C.nsock; s++) {
         const int cnt = popc_and(FA, C.sm[s]);
         if (cnt < a.need) continue;
-        if (best < 0 || (cnt != bc && free_before(a.most, cnt, bc))) {
-          best = s;
-          bc = cnt;
-        }
+        bkey = max(bkey, sel_key(a.most, cnt, 0, s));
       }
+      const int best = sel_index(bkey);
       if (best >= 0) {
         for (int w = 0; w < NW; w++) T[w] = FA[w] & C.sm[best][w];
         acc_take_low(C, a, T, a.need);
@@ -556,19 +562,16 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
         if (fe) acc_excluded(C, a, false, X);
         uint64_t Fl[NW];
         for (int w = 0; w < NW; w++) Fl[w] = a.A[w] & ~(fe ? X[w] : 0ull);
-        KH_PINNED int best = -1, bf = 0, bs = 0;
+        int bkey = 0;
         for (int k = 0; k < C.nnuma; k++) {
           const int nf = popc_and(Fl, C.nm[k]);
           if (nf == 0) continue;
           const int len = fe ? cores_in(Fl, C.nm[k], cpc) : nf;
           if (len < a.need) continue;
           const int sf = popc_and(Fl, C.sm[C.sock_of_node[k]]);
-          if (best < 0 || (nf != bf ? free_before(a.most, nf, bf) : (sf != bs && free_before(a.most, sf, bs)))) {
-            best = k;
-            bf = nf;
-            bs = sf;
-          }
+          bkey = max(bkey, sel_key(a.most, nf, sf, k));
         }
+        const int best = sel_index(bkey);
         if (best >= 0) {
           for (int w = 0; w < NW; w++) T[w] = Fl[w] & C.nm[best][w];
           if (fe) {  // extractCPU: each core's lowest-id allowed CPU
@@ -590,17 +593,15 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
         if (fe) acc_excluded(C, a, true, X);
         uint64_t Fl[NW];
         for (int w = 0; w < NW; w++) Fl[w] = a.A[w] & ~(fe ? X[w] : 0ull);
-        KH_PINNED int best = -1, bl = 0;
+        int bkey = 0;
         for (int s = 0; s < C.nsock; s++) {
           const int nf = popc_and(Fl, C.sm[s]);
           if (nf == 0) continue;
           const int len = fe ? cores_in(Fl, C.sm[s], cpc) : nf;
           if (len < a.need) continue;
-          if (best < 0 || (len != bl && free_before(a.most, len, bl))) {
-            best = s;
-            bl = len;
-          }
+          bkey = max(bkey, sel_key(a.most, len, 0, s));
         }
+        const int best = sel_index(bkey);
         if (best >= 0) {
           for (int w = 0; w < NW; w++) T[w] = Fl[w] & C.sm[best][w];
           if (fe) {
