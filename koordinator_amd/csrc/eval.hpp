@@ -526,34 +526,40 @@ __device__ __forceinline__ void store_row(const NV &v, const DevNodes &d, int32_
 // hinted zones' amounts (resourceManager.Update, node_allocation.go:76-103).
 // false = Allocate fails (nothing applied).
 template <bool Z>
-__device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *classes, NumaRow &r, const DevPod &p,
-                                                       uint64_t *cpus) {
-  for (int w = 0; w < NW; w++) cpus[w] = 0;
+__device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *classes, NumaRow &row, const DevPod &pod,
+                                                       uint64_t *cpus_out) {
+  // registers for the whole replay (the references point at the caller's stack)
+  NumaRow r = row;
+  const DevPod p = pod;
+  uint64_t cpus[NW] = {0, 0, 0, 0};
+  for (int w = 0; w < NW; w++) cpus_out[w] = 0;
   const bool cs = (p.flags & KOORDHIP_POD_CPUSET) != 0;
   const int tp = Z ? topo_policy(r.nflags) : 0;
   if (!cs && tp == 0) return true;
   if (r.cls < 0) return false;
   const DevNumaClass &C = classes[r.cls];
   if (!Z || tp == 0) {
-    if (!numa_allocate(C, r, p, cpus)) return false;
+    if (!numa_allocate_in(C, r, p, cpus)) return false;
     numa_apply(r, p, cpus, +1);
-    return true;
-  }
-  uint32_t mask;
-  if (!zone_hint(C.nnuma, r, p, tp, &mask)) return false;
-  double z[2][ZMAX];
-  if (mask && !zone_alloc(C.nnuma, r, p, mask, z)) return false;
-  if (cs) {
-    if (!(mask ? zone_allocate(C, r, p, z, cpus) : numa_allocate(C, r, p, cpus))) return false;
-    numa_apply(r, p, cpus, +1);
-  }
-  if (mask) {
+  } else {
+    uint32_t mask;
+    if (!zone_hint(C.nnuma, r, p, tp, &mask)) return false;
+    double z[2][ZMAX];
+    if (mask && !zone_alloc(C.nnuma, r, p, mask, z)) return false;
+    if (cs) {
+      if (!(mask ? zone_allocate_in(C, r, p, z, cpus) : numa_allocate_in(C, r, p, cpus))) return false;
+      numa_apply(r, p, cpus, +1);
+    }
+    if (mask) {
 #pragma unroll
-    for (int k = 0; k < ZMAX; k++) {
-      r.zu[0][k] += z[0][k];
-      r.zu[1][k] += z[1][k];
+      for (int k = 0; k < ZMAX; k++) {
+        r.zu[0][k] += z[0][k];
+        r.zu[1][k] += z[1][k];
+      }
     }
   }
+  row = r;
+  for (int w = 0; w < NW; w++) cpus_out[w] = cpus[w];
   return true;
 }
 

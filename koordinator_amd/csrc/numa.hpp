@@ -152,7 +152,15 @@ __device__ __forceinline__ int cores_in(const uint64_t *m, const uint64_t *g, in
 // per core.  Stages follow cpu_accumulator.go:184-229; a stage that finds a
 // group big enough returns immediately, with distinct cores iff the group has
 // that many distinct cores (spreadCPUs takes one CPU per core first).
-__device__ __attribute__((noinline)) bool numa_spread_ok(const DevNumaClass &C, const NumaRow &r, int need, int excl, bool most) {
+// (masks by value: the caller's row never has to go through scratch memory)
+__device__ __attribute__((noinline)) bool numa_spread_ok(const DevNumaClass &C, uint64_t f0, uint64_t f1, uint64_t f2,
+                                                         uint64_t f3, uint64_t p0, uint64_t p1, uint64_t p2, uint64_t p3,
+                                                         uint64_t n0, uint64_t n1, uint64_t n2, uint64_t n3, int need,
+                                                         int excl, bool most) {
+  NumaRow r;
+  r.fr[0] = f0, r.fr[1] = f1, r.fr[2] = f2, r.fr[3] = f3;
+  r.ep[0] = p0, r.ep[1] = p1, r.ep[2] = p2, r.ep[3] = p3;
+  r.en[0] = n0, r.en[1] = n1, r.en[2] = n2, r.en[3] = n3;
   const int cpc = C.cpc;
   uint64_t X[NW], Xp[NW], F[NW];
   excluded_set(C, r, excl, false, X);
@@ -212,7 +220,8 @@ __device__ __forceinline__ bool numa_alloc_ok(const DevNumaClass &C, const NumaR
     return full * C.cpc >= need;
   }
   if (C.cpc == 1) return true;
-  return numa_spread_ok(C, r, need, (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy),
+  return numa_spread_ok(C, r.fr[0], r.fr[1], r.fr[2], r.fr[3], r.ep[0], r.ep[1], r.ep[2], r.ep[3], r.en[0], r.en[1],
+                        r.en[2], r.en[3], need, (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy),
                         (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) != 0);
 }
 
@@ -322,7 +331,7 @@ __device__ __forceinline__ void acc_excluded(const DevNumaClass &C, const Acc &a
 // spread order of the CPUs of m listed in ascending CPU id (freeCPUsInNode /
 // freeCPUsInSocket + spreadCPUs): round t takes each core's t-th CPU by id,
 // rounds in id order; lists of <= cpc CPUs are kept in id order.  Takes n.
-__device__ __attribute__((noinline)) void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
+__device__ __forceinline__ void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
   int len = popc4(m);
   if (len <= C.cpc) {
     for (int i = 0; i < C.ncpu && n > 0; i++) {
@@ -351,7 +360,7 @@ __device__ __attribute__((noinline)) void acc_take_spread_by_id(const DevNumaCla
 }
 
 // freeCPUs(filterExclusive) + spreadCPUs + one-by-one take (:218-229).
-__device__ __attribute__((noinline)) void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
+__device__ __forceinline__ void acc_fallback_pass(const DevNumaClass &C, Acc &a, bool fe) {
   uint64_t X[NW], F[NW];
   if (fe) acc_excluded(C, a, false, X);
   else
@@ -455,7 +464,7 @@ __device__ __forceinline__ void go118_sort_by_count(int *ord, int *cnt, int n, b
 }
 
 // takeCPUs; returns true with a.R filled.
-__device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
+__device__ __forceinline__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
   if (a.need < 1) return true;
   if (a.need > popc4(a.A)) return false;
   const int cpc = C.cpc;
@@ -626,7 +635,7 @@ __device__ __attribute__((noinline)) bool acc_take_cpus(const DevNumaClass &C, A
 }
 
 // takeCPUs over the available set A (cpu_accumulator.go:87-232) into out[]
-__device__ __attribute__((noinline)) bool acc_run(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+__device__ __forceinline__ bool acc_run(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
                                                   const uint64_t *A, int need, uint64_t *out) {
   Acc a;
   for (int w = 0; w < NW; w++) {
@@ -659,7 +668,7 @@ __device__ __forceinline__ bool required_ok(const DevNumaClass &C, const NumaRow
 }
 
 // Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
-__device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
+__device__ __forceinline__ bool numa_allocate_in(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
   for (int w = 0; w < NW; w++) cpus[w] = 0;
   const int need = p.numa_cpus;
   if (popc4(r.fr) < need) return false;
@@ -668,6 +677,17 @@ __device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, c
   if (!required_ok(C, r, p, R)) return false;
   for (int w = 0; w < NW; w++) cpus[w] = R[w];
   return true;
+}
+
+// The outlined entry points copy their by-reference inputs into registers
+// first: the accumulator then never touches the caller's stack copy.
+__device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
+  const NumaRow rl = r;
+  const DevPod pl = p;
+  uint64_t o[NW];
+  const bool ok = numa_allocate_in(C, rl, pl, o);
+  for (int w = 0; w < NW; w++) cpus[w] = o[w];
+  return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -779,8 +799,8 @@ __device__ __forceinline__ bool zone_cpus_ok(const DevNumaClass &C, const NumaRo
 }
 
 // ... exact CPUs (Reserve, and Filter / Score under a required policy)
-__device__ __attribute__((noinline)) bool zone_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
-                                                        const double z[2][ZMAX], uint64_t *cpus) {
+__device__ __forceinline__ bool zone_allocate_in(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                                 const double z[2][ZMAX], uint64_t *cpus) {
   for (int w = 0; w < NW; w++) cpus[w] = 0;
   if (popc4(r.fr) < p.numa_cpus) return false;
   int got = 0;
@@ -796,6 +816,19 @@ __device__ __attribute__((noinline)) bool zone_allocate(const DevNumaClass &C, c
   }
   if (got != p.numa_cpus) return false;
   return required_ok(C, r, p, cpus);
+}
+
+__device__ __attribute__((noinline)) bool zone_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                                        const double z[2][ZMAX], uint64_t *cpus) {
+  const NumaRow rl = r;
+  const DevPod pl = p;
+  double zl[2][ZMAX];
+  for (int q = 0; q < 2; q++)
+    for (int k = 0; k < ZMAX; k++) zl[q][k] = z[q][k];
+  uint64_t o[NW];
+  const bool ok = zone_allocate_in(C, rl, pl, zl, o);
+  for (int w = 0; w < NW; w++) cpus[w] = o[w];
+  return ok;
 }
 
 // Filter's FilterByNUMANode -> Admit -> Allocate on a policy node (topology_hint.go:30-86)
