@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 3
+#define KOORDHIP_ABI_VERSION 4
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -209,6 +209,12 @@ typedef struct koordhip_node_soa {
    * NULL when no node has one. */
   const int64_t *numa_zone_alloc;
   const int64_t *numa_zone_used;
+  /* CPU amplification ratio of the node (annotation node.koordinator.sh/
+   * resource-amplification-ratio, apis/extension/node_resource_amplification.go:
+   * 56-76; the same ratio the NodeResourceTopology carries): NodeNUMAResource's
+   * filterAmplifiedCPUs / scoreWithAmplifiedCPUs / amplified cpuset requests
+   * (plugin.go:326-363, scoring.go:95-168).  NULL or <= 1: not amplified. */
+  const double *numa_amp_cpu;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */

@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 3
+KOORDHIP_ABI_VERSION = 4
 NRES = 5
 NPLUGINS = 3
 
@@ -110,6 +110,7 @@ class KoordhipNodeSoa(C.Structure):
         ("numa_flags", _u8p),
         ("numa_zone_alloc", _i64p),
         ("numa_zone_used", _i64p),
+        ("numa_amp_cpu", C.POINTER(C.c_double)),
     ]
 
 

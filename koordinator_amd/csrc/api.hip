@@ -378,6 +378,21 @@ int build_numa_class(const koordhip_numa_class &t, kh::DevNumaClass &o) {
   return 0;
 }
 
+// CPU amplification ratios: finite, >= 0; > 1 is supported only on nodes
+// without a NUMA topology policy (zone amplification is not modelled)
+int check_amp(const double *amp, const uint8_t *flags, int32_t m, bool *any) {
+  for (int32_t i = 0; i < m; i++) {
+    const double v = amp[i];
+    if (!std::isfinite(v) || v < 0.0) return fail(KOORDHIP_EINVAL, "numa_amp_cpu: ratio must be finite and >= 0");
+    if (v > 1.0) {
+      *any = true;
+      if (flags && KOORDHIP_NODE_NUMA_POLICY(flags[i]))
+        return fail(KOORDHIP_EINVAL, "CPU amplification on a node with a NUMA topology policy is not supported");
+    }
+  }
+  return 0;
+}
+
 // NUMA zone rows [m][2][KOORDHIP_NUMA_MAX_NODES] int64 -> the device's
 // [m][2][KOORDHIP_NUMA_MAX_ZONES] f64; rows of topology-policy nodes are
 // checked (<= KOORDHIP_NUMA_MAX_ZONES NUMA nodes, exact quantities)
@@ -485,6 +500,18 @@ int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
       nu.zu = u;
     }
     c->dc.zones = any ? 1 : 0;
+  }
+  // CPU amplification ratios (kept whenever the snapshot carries the column)
+  c->dc.amp = 0;
+  if (!e && have && s->numa_amp_cpu) {
+    bool any_amp = false;
+    e = check_amp(s->numa_amp_cpu, s->numa_flags, n, &any_amp);
+    double *a = nullptr;
+    if (!e) e = dev_alloc(c, &a, (size_t)n);
+    if (!e) e = upload(c, a, s->numa_amp_cpu, (size_t)n);
+    if (!e) HIP_TRY(hipStreamSynchronize(c->stream));
+    nu.amp = a;
+    c->dc.amp = any_amp ? 1 : 0;
   }
   c->host_classes = cls;
   return e;
@@ -763,6 +790,15 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       return fail(KOORDHIP_EINVAL, "a NUMA topology policy needs the zone columns at load_snapshot");
     zrows = zrows && c->d.nu.za;
   }
+  bool amp_rows = false, amp_any = false;
+  if (numa_rows && rows->numa_amp_cpu) {
+    if (int e = check_amp(rows->numa_amp_cpu, rows->numa_flags, m, &amp_any)) return e;
+    if (!c->d.nu.amp) {
+      bool any = amp_any;
+      if (any) return fail(KOORDHIP_EINVAL, "a CPU amplification ratio needs the numa_amp_cpu column at load_snapshot");
+    }
+    amp_rows = c->d.nu.amp != nullptr;
+  }
   // ---- one host staging image: [idx][column 0][column 1]..., 8-B aligned
   //      segments, quantities converted to the device's exact f64
   struct Col {
@@ -808,6 +844,8 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       cols.push_back({nu.en[w], rows->numa_excl_numa[w], 8, false, "numa_excl_numa"});
     }
   }
+  if (amp_rows)
+    cols.push_back({const_cast<double *>(c->d.nu.amp), rows->numa_amp_cpu, 8, false, "numa_amp_cpu"});
   if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one 64-B element per row
     kh::DevNuma &nu = c->d.nu;
     cols.push_back({const_cast<double *>(nu.za), zrow_a.data(), 64, false, "numa_zone_alloc"});
@@ -863,6 +901,7 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   }
   c->dc.la_alias = alias ? 1 : 0;
   if (zpolicy) c->dc.zones = 1;
+  if (amp_any) c->dc.amp = 1;
   HIP_TRY(kh::launch_prep_flags(pi, d, d_idx, m, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));  // the host image may be reused by the next call
   return 0;

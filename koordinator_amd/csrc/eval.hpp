@@ -42,6 +42,7 @@ struct DevCfg {
   int32_t numa_w_cpu, numa_w_mem;  // NodeNUMAResourceArgs scoring weights
   int32_t numa_most;               // NodeNUMAResource MostAllocated scoring strategy
   int32_t zones;                   // some node has a NUMA topology policy (zone columns loaded)
+  int32_t amp;                     // some node has a CPU amplification ratio > 1
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -74,6 +75,7 @@ struct Need {
   bool pods, r_cpu, r_mem, eph, bcpu, bmem, a_cpu, a_mem, nz_cpu, nz_mem, la, la_nonprod, la_prod;
   bool numa, numa_masks;  // NUMA class (+ the cpuset masks for a cpuset pod)
   bool zones;             // node flags + NUMA zones (topology-policy nodes)
+  bool amp;               // the CPU amplification ratio + allocated cpuset count
 };
 
 __device__ __forceinline__ bool numa_on(const DevCfg &c) {
@@ -111,6 +113,14 @@ __device__ __forceinline__ Need pod_needs(const DevPod &p, const DevCfg &c) {
   n.numa = ns || ((c.filt & KOORDHIP_PLUGIN_NUMA) && numa_active(p, c));
   n.numa_masks = numa_on(c) && is_cpuset(p);
   n.zones = n.numa && c.zones && !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+  // filterAmplifiedCPUs / the amplified scores read Requested + Allocatable cpu,
+  // the allocated cpuset count and the ratio (plugin.go:326-363, scoring.go:95-168)
+  n.amp = c.amp && numa_on(c) && p.req[KOORDHIP_RES_CPU] != 0.0 &&
+          !(p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+  if (n.amp) {
+    n.numa = true;
+    n.r_cpu = n.a_cpu = true;
+  }
   if (ns) {
     n.r_cpu |= !is_cpuset(p);
     n.r_mem = true;
@@ -129,6 +139,7 @@ __device__ __forceinline__ Need need_all(const DevCfg &c) {
   n.la_prod = c.according != 0;
   n.numa = n.numa_masks = numa_on(c);
   n.zones = n.numa && c.zones;
+  n.amp = n.numa && c.amp;
   return n;
 }
 
@@ -148,8 +159,13 @@ template <bool Z>
 __device__ __forceinline__ void load_numa(NumaRow &r, const DevNodes &d, int32_t i, const Need &n) {
   r.cls = -1;
   r.nflags = 0;
+  r.amp = 1.0;
   if (!n.numa) return;
   r.cls = d.nu.node_cls[i];
+  if (n.amp) {
+    r.amp = d.nu.amp[i];
+    r.cnt = d.nu.cnt[i];
+  }
   if (n.numa_masks || (Z && n.zones)) r.nflags = d.nu.nflags[i];
   if constexpr (Z) {
     if (n.zones && topo_policy(r.nflags) != 0) load_zones(r, d, i);
@@ -330,6 +346,21 @@ __device__ __forceinline__ int32_t la_score(const DevPod &p, const NV &v, const 
   return (v.flags & NF_LA_SCORE_ZERO) ? 0 : s;
 }
 
+// extension.Amplify (node_resource_amplification.go:191-196) on an exact f64 integer
+__device__ __forceinline__ double amplify(double v, double ratio) { return ratio <= 1.0 ? v : ceil(v * ratio); }
+
+// filterAmplifiedCPUs, plugin.go:326-363: the allocated cpuset CPUs count
+// amplified in Requested; a cpuset pod's request is amplified too.
+__device__ __forceinline__ bool amp_filter_ok(const DevPod &p, const NV &v, const NumaRow &r) {
+  const double cpu = p.req[KOORDHIP_RES_CPU];
+  if (cpu == 0.0 || r.amp <= 1.0) return true;
+  const double req = is_cpuset(p) ? amplify(cpu, r.amp) : cpu;
+  const double allocm = r.cls >= 0 ? (double)r.cnt * 1000.0 : 0.0;  // GetAvailableCPUs
+  double requested = v.r[KOORDHIP_RES_CPU];
+  if (requested >= allocm && allocm > 0.0) requested = requested - allocm + amplify(allocm, r.amp);
+  return !(req > v.a[KOORDHIP_RES_CPU] - requested);
+}
+
 // NodeNUMAResource Score (scoring.go:55-168).
 // filtered: the NodeNUMAResource Filter passed on this (pod, node) -- under a
 // required bind policy that already proved Allocate feasible (plugin.go:307-316)
@@ -343,10 +374,15 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
   auto dw = [](int32_t a, int32_t b) { return div_weights(a, b); };
   const bool cs = (p.flags & KOORDHIP_POD_CPUSET) != 0;
   const int tp = Z ? topo_policy(r.nflags) : 0;
-  if (!cs && tp == 0)
-    return numa_la(v.r[KOORDHIP_RES_CPU] + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU],
-                   v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM], v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem,
-                   lr, dw);
+  if (!cs && tp == 0) {  // scoreWithAmplifiedCPUs (:95-120)
+    double rq = v.r[KOORDHIP_RES_CPU];
+    if (c.amp && p.req[KOORDHIP_RES_CPU] != 0.0 && r.amp > 1.0) {
+      const double allocm = (double)r.cnt * 1000.0;
+      rq = rq - allocm + amplify(allocm, r.amp);
+    }
+    return numa_la(rq + p.req[KOORDHIP_RES_CPU], v.a[KOORDHIP_RES_CPU], v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM],
+                   v.a[KOORDHIP_RES_MEM], c.numa_w_cpu, c.numa_w_mem, lr, dw);
+  }
   const DevNumaClass &C = classes[r.cls];
   double ac = v.a[KOORDHIP_RES_CPU], am = v.a[KOORDHIP_RES_MEM];
   double rc = v.r[KOORDHIP_RES_CPU], rm = v.r[KOORDHIP_RES_MEM];
@@ -374,12 +410,16 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
         }
     }
   }
+  double qc = p.req[KOORDHIP_RES_CPU];
   if (cs) {
     const bool proven = filtered && tp == 0 && KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE;
     if (!mask && !proven && !numa_alloc_ok(C, r, p)) return 0;
-    rc = (double)r.cnt * 1000.0;  // requested cpu := allocated cpuset size (:161-166)
+    // requested cpu := the allocated cpuset size, amplified (:161-166); the
+    // pod's own request amplified too (getResourceOptions, plugin.go:481-485)
+    rc = amplify((double)r.cnt * 1000.0, r.amp);
+    qc = amplify(qc, r.amp);
   }
-  return numa_la(rc + p.req[KOORDHIP_RES_CPU], ac, rm + p.req[KOORDHIP_RES_MEM], am, c.numa_w_cpu, c.numa_w_mem, lr, dw);
+  return numa_la(rc + qc, ac, rm + p.req[KOORDHIP_RES_MEM], am, c.numa_w_cpu, c.numa_w_mem, lr, dw);
 }
 
 // Total weighted score, or -1 when any enabled Filter fails.
@@ -400,6 +440,8 @@ __device__ __forceinline__ int32_t eval_total_numa(const DevPod &p, const NV &v,
   int32_t t = eval_total(p, v, c);
   if (t < 0) return t;
   const bool nf = (c.filt & KOORDHIP_PLUGIN_NUMA) != 0;
+  if (nf && (p.flags & KOORDHIP_POD_NUMA_ERROR)) return -1;
+  if (nf && c.amp && !amp_filter_ok(p, v, r)) return -1;
   if (nf && !numa_filter<Z>(p, r, classes)) return -1;
   if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score<Z>(p, v, r, classes, c, nf);
   return t;
@@ -466,6 +508,7 @@ __device__ __forceinline__ void load_numa_row(NumaRow &r, const DevNodes &d, int
     r.en[w] = d.nu.en[w][i];
   }
   if (Z && d.nu.za && topo_policy(r.nflags) != 0) load_zones(r, d, i);
+  r.amp = d.nu.amp ? d.nu.amp[i] : 1.0;
 }
 
 template <bool Z = true>

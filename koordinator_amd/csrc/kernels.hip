@@ -172,7 +172,9 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
     uint8_t b = 0;
     if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(pod, v)) b |= KOORDHIP_ST_FIT_FAIL;
     if ((c.filt & KOORDHIP_PLUGIN_LOADAWARE) && !la_filter(pod, v)) b |= KOORDHIP_ST_LA_FAIL;
-    if ((c.filt & KOORDHIP_PLUGIN_NUMA) && !numa_filter<true>(pod, nr, d.nu.cls)) b |= KOORDHIP_ST_NUMA_FAIL;
+    if ((c.filt & KOORDHIP_PLUGIN_NUMA) &&
+        (!numa_filter<true>(pod, nr, d.nu.cls) || (c.amp && !amp_filter_ok(pod, v, nr))))
+      b |= KOORDHIP_ST_NUMA_FAIL;
     status[(size_t)p * d.n + i] = b;
   }
   if (scores) {

@@ -75,6 +75,7 @@ struct NumaRow {
   // NRT allocatable and NodeAllocation.allocatedResources, [cpu milli, memory][zone]
   double za[2][ZMAX];
   double zu[2][ZMAX];
+  double amp;  // CPU amplification ratio (1 unless loaded)
 };
 
 struct DevNuma {
@@ -85,6 +86,7 @@ struct DevNuma {
   int32_t *cnt;
   const double *za;  // [n][2][ZMAX], NULL when no node has a topology policy
   double *zu;        // [n][2][ZMAX]
+  const double *amp; // CPU amplification ratio per node, NULL when none is > 1
   int32_t ncls;      // topology classes at cls
 };
 

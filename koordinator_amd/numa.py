@@ -285,3 +285,24 @@ def zone_row(zones: Sequence[Tuple[int, int]]) -> np.ndarray:
     for k, (cpu_m, mem) in enumerate(zones):
         row[0, k], row[1, k] = cpu_m, mem
     return row
+
+
+ANNOTATION_AMPLIFICATION_RATIO = "node.koordinator.sh/resource-amplification-ratio"
+
+
+def cpu_amplification_ratio(annotations: Dict[str, str]) -> float:
+    """GetNodeResourceAmplificationRatio(annotations, cpu)
+    (apis/extension/node_resource_amplification.go:56-76) -> the numa_amp_cpu
+    column value: the ratio, 1.0 when unset (the reference's -1 means "none"
+    too: every use checks ratio <= 1).  A malformed annotation is an error
+    (the reference's Filter then fails UnschedulableAndUnresolvable)."""
+    import json
+    raw = annotations.get(ANNOTATION_AMPLIFICATION_RATIO)
+    if raw is None:
+        return 1.0
+    try:
+        ratios = json.loads(raw)
+        v = float(ratios.get("cpu", -1))
+    except (ValueError, TypeError, AttributeError) as e:
+        raise TopologyError(f"invalid {ANNOTATION_AMPLIFICATION_RATIO}: {e}")
+    return v if v > 1.0 else 1.0

@@ -26,7 +26,8 @@ U64_COLS = ([f"numa_free{w}" for w in range(abi.NUMA_WORDS)] + [f"numa_excl_pcpu
             + [f"numa_excl_numa{w}" for w in range(abi.NUMA_WORDS)])
 # NUMA zone resources, [n][2][NUMA_MAX_NODES] int64 per column (cpu milli, memory bytes)
 ZONE_COLS = ["numa_zone_alloc", "numa_zone_used"]
-ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS + ZONE_COLS
+F64_COLS = ["numa_amp_cpu"]   # CPU amplification ratio (1.0 = none)
+ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS + ZONE_COLS + F64_COLS
 # NodeNUMAResource mutable columns (advanced by cpuset / NUMA-zone Reserves)
 NUMA_MUTABLE = [c for c in U64_COLS] + ["numa_alloc_cnt", "numa_zone_used"]
 
@@ -42,6 +43,8 @@ def _dtype(col: str):
         return np.uint8
     if col in U64_COLS:
         return np.uint64
+    if col in F64_COLS:
+        return np.float64
     return np.int64
 
 
@@ -60,6 +63,7 @@ class NodeTable:
         for c in ALL_COLS:
             t.cols[c] = np.zeros(_shape(c, n), dtype=_dtype(c))
         t.cols["numa_class"][:] = -1
+        t.cols["numa_amp_cpu"][:] = 1.0
         t.names = [f"node-{i}" for i in range(n)]
         return t
 
@@ -119,6 +123,7 @@ class NodeTable:
         s.numa_flags = self.cols["numa_flags"].ctypes.data_as(C.POINTER(C.c_uint8))
         s.numa_zone_alloc = p64("numa_zone_alloc")
         s.numa_zone_used = p64("numa_zone_used")
+        s.numa_amp_cpu = self.cols["numa_amp_cpu"].ctypes.data_as(C.POINTER(C.c_double))
         return s
 
     def nbytes(self) -> int:

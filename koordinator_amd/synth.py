@@ -121,6 +121,7 @@ class NumaSpec:
     most_allocated_frac: float = 0.3   # node label numa-allocate-strategy=MostAllocated
     linux_numbering: bool = True
     policy_frac: float = 0.0           # nodes with a NUMA topology policy (BestEffort / Restricted / SingleNUMANode)
+    amp_frac: float = 0.0              # nodes with a CPU amplification ratio (1.25 / 1.5 / 2.0), no topology policy
     zone_used_frac: float = 0.6        # policy nodes: zone usage of non-cpuset pods, U[0, max] of the zone
 
 
@@ -199,6 +200,13 @@ def add_numa(t: NodeTable, spec: NumaSpec, profile: Profile, seed: int = SEED) -
                 extra = rng.random() * spec.zone_used_frac * 1.1
                 t["numa_zone_used"][i, 0, k] = int((used & in_k).sum()) * 1000 + int(extra * in_k.sum() * 1000) // 100 * 100
                 t["numa_zone_used"][i, 1, k] = int(extra * t["numa_zone_alloc"][i, 1, k]) // MI * MI
+        if spec.amp_frac and not (f >> abi.NODE_NUMA_POLICY_SHIFT) and rng.random() < spec.amp_frac:
+            # the node's allocatable cpu is the amplified figure (koord-manager's NodeResource)
+            ratio = float(rng.choice([1.25, 1.5, 2.0]))
+            t["numa_amp_cpu"][i] = ratio
+            t["alloc0"][i] = int(np.ceil(t["alloc0"][i] * ratio))
+            t["la_alloc_cpu_m"][i] = t["alloc0"][i]
+            t["laf_total_m0"][i] = t["alloc0"][i]
         t["numa_flags"][i] = f
     return t
 

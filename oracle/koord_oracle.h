@@ -66,6 +66,7 @@ int64_t orc_la_score(const koordhip_config *cfg, const orc_state *st, const koor
 
 /* NodeNUMAResource (numa_oracle.c). */
 int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
+int64_t orc_amplify(int64_t origin, double ratio);
 int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
 int orc_numa_reserve_active(const orc_state *st, const koordhip_pod *pod, int32_t i);

@@ -20,6 +20,7 @@
  * sort when 7-8 sockets tie.
  * Pinned by the known-answer tables of cpu_accumulator_test.go (tests/golden/).
  */
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -794,13 +795,42 @@ static int policy_allocate(const orc_state *st, const koordhip_pod *pod, int32_t
   return 1;
 }
 
-/* Filter, plugin.go:266-324 (amplification ratio <= 1). */
+/* The node's CPU amplification ratio (<= 1: none). */
+static double amp_ratio(const orc_state *st, int32_t i) {
+  return st->soa->numa_amp_cpu ? st->soa->numa_amp_cpu[i] : 1.0;
+}
+
+/* extension.Amplify, apis/extension/node_resource_amplification.go:191-196 */
+int64_t orc_amplify(int64_t origin, double ratio) {
+  if (ratio <= 1.0) return origin;
+  return (int64_t)ceil((double)origin * ratio);
+}
+
+/* filterAmplifiedCPUs, plugin.go:326-363: the node's allocated cpuset CPUs
+ * count amplified in Requested; a cpuset pod's request is amplified too. */
+static int amp_filter_ok(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  const int64_t cpu = pod->req[KOORDHIP_RES_CPU];
+  const double ratio = amp_ratio(st, i);
+  if (cpu == 0 || ratio <= 1.0) return 1;
+  const int cpuset = (pod->flags & KOORDHIP_POD_CPUSET) && !(pod->flags & KOORDHIP_POD_NUMA_SKIP);
+  const int64_t req = cpuset ? orc_amplify(cpu, ratio) : cpu;
+  const koordhip_node_soa *s = st->soa;
+  const int has_topo = s->numa_class && s->numa_class[i] >= 0;
+  const int64_t allocm = has_topo ? (int64_t)st->numa_alloc_cnt[i] * 1000 : 0; /* GetAvailableCPUs */
+  int64_t requested = st->requested[KOORDHIP_RES_CPU][i];
+  if (requested >= allocm && allocm > 0) requested = requested - allocm + orc_amplify(allocm, ratio);
+  return !(req > s->alloc[KOORDHIP_RES_CPU][i] - requested);
+}
+
+/* Filter, plugin.go:266-324.  A CPU amplification ratio > 1 is supported on
+ * nodes without a NUMA topology policy (the host rejects the combination). */
 int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
   (void)cfg;
   const koordhip_node_soa *s = st->soa;
   const int tp = node_policy(st, i);
   const int cpuset = (pod->flags & KOORDHIP_POD_CPUSET) != 0;
   if (pod->flags & KOORDHIP_POD_NUMA_ERROR) return 0;   /* PreFilter error */
+  if (!amp_filter_ok(st, pod, i)) return 0;           /* :272-274 */
   if ((pod->flags & KOORDHIP_POD_NUMA_SKIP) || (!cpuset && tp == KOORDHIP_NUMA_TOPO_NONE))
     return 1;                                          /* skipTheNode, util.go:59-61 */
   if (cpuset) {
@@ -864,8 +894,14 @@ int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const ko
   int64_t rcpu = st->requested[KOORDHIP_RES_CPU][i], rmem = st->requested[KOORDHIP_RES_MEM][i];
   /* no topology: getResourceOptions fails (:82-85, :97-100) */
   if (!has_topo) return 0;
-  if (!cpuset && tp == KOORDHIP_NUMA_TOPO_NONE) /* scoreWithAmplifiedCPUs :104-106 */
+  const double ratio = amp_ratio(st, i);
+  if (!cpuset && tp == KOORDHIP_NUMA_TOPO_NONE) { /* scoreWithAmplifiedCPUs :95-120 */
+    if (pod->req[KOORDHIP_RES_CPU] != 0 && ratio > 1.0) {
+      const int64_t allocm = (int64_t)st->numa_alloc_cnt[i] * 1000;
+      rcpu = rcpu - allocm + orc_amplify(allocm, ratio);
+    }
     return numa_least_allocated(cfg, rcpu + pod->req[KOORDHIP_RES_CPU], acpu, rmem + pod->req[KOORDHIP_RES_MEM], amem);
+  }
   int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES];
   uint64_t cpus[KOORDHIP_NUMA_WORDS];
   int hz = 0;
@@ -884,9 +920,14 @@ int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const ko
       rmem += zone_at(st->numa_zone_used, i, 1, k);
     }
   }
-  /* requested cpu := allocated cpuset size (:161-166) */
-  if (cpuset) rcpu = (int64_t)st->numa_alloc_cnt[i] * 1000;
-  return numa_least_allocated(cfg, rcpu + pod->req[KOORDHIP_RES_CPU], acpu, rmem + pod->req[KOORDHIP_RES_MEM], amem);
+  /* requested cpu := allocated cpuset size, amplified (:161-166); the cpuset
+   * pod's request is amplified too (getResourceOptions, plugin.go:481-485) */
+  int64_t qcpu = pod->req[KOORDHIP_RES_CPU];
+  if (cpuset) {
+    rcpu = orc_amplify((int64_t)st->numa_alloc_cnt[i] * 1000, ratio);
+    qcpu = orc_amplify(qcpu, ratio);
+  }
+  return numa_least_allocated(cfg, rcpu + qcpu, acpu, rmem + pod->req[KOORDHIP_RES_MEM], amem);
 }
 
 int orc_numa_reserve_active(const orc_state *st, const koordhip_pod *pod, int32_t i) {

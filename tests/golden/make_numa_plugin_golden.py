@@ -4,7 +4,8 @@ tests transcribed from the reference's table tests (data only):
   plugins/nodenumaresource/plugin_test.go:544-812   TestPlugin_Filter
   plugins/nodenumaresource/plugin_test.go:927-1146  TestPlugin_Reserve
   plugins/nodenumaresource/scoring_test.go:597-852  TestScoreWithAmplifiedCPUs, the node1
-                                                    (ratio 1.0) column of every row
+                                                    (ratio 1.0) and node2 (ratio 2.0) columns
+  plugins/nodenumaresource/plugin_test.go:814-925   TestFilterWithAmplifiedCPUs
 
 Every case runs on the tests' node (allocatable cpu 96, memory 512Gi) with the
 case's CPU topology (buildCPUTopologyForTest args; "invalid" = &CPUTopology{},
@@ -106,10 +107,38 @@ SCORE_NODE1 = [
 ]
 
 
+# TestScoreWithAmplifiedCPUs node2: cpu 64 (= Amplify(32 CPUs, 2.0)), memory
+# 60Gi, ratio 2.0, same pods and topology as node1 (scoring_test.go:610-794).
+SCORE_NODE2 = [dict(c, want=w) for c, w in zip(SCORE_NODE1, [0, 54, 29, 60, 0, 45, 70, 39])]
+
+# TestFilterWithAmplifiedCPUs (plugin_test.go:814-925): buildCPUTopologyForTest(2, 1, 8, 2)
+# (32 CPUs), node cpu = Amplify(32, ratio), memory 40Gi; existing pod [cpu, LSR]
+# (LSR: CPUs 0..cpu-1 allocated); NRT zones of Amplify(16, ratio) cpu and 20Gi
+# when has_nrt (:894-909); pod [cpu, LSR].  want: Filter passes.
+P = "plugin_test.go:"
+FILTER_AMP = [
+    {"name": "no resources requested always fits", "source": P + "825-830", "ratio": 2.0, "has_nrt": False,
+     "existing": [4, False], "pod": None, "want": True},
+    {"name": "no filtering without node cpu amplification", "source": P + "831-837", "ratio": 1.0,
+     "has_nrt": False, "existing": [32, False], "pod": [32, False], "want": True},
+    {"name": "cpu fits on no NRT node", "source": P + "838-844", "ratio": 2.0, "has_nrt": False,
+     "existing": [32, False], "pod": [32, False], "want": True},
+    {"name": "insufficient cpu", "source": P + "845-852", "ratio": 2.0, "has_nrt": False,
+     "existing": [64, False], "pod": [32, False], "want": False},
+    {"name": "insufficient cpu with cpuset pod on node", "source": P + "853-861", "ratio": 2.0, "has_nrt": True,
+     "existing": [32, True], "pod": [32, False], "want": False},
+    {"name": "insufficient cpu when scheduling cpuset pod", "source": P + "862-870", "ratio": 2.0,
+     "has_nrt": True, "existing": [32, False], "pod": [32, True], "want": False},
+    {"name": "insufficient cpu when scheduling cpuset pod with cpuset pod on node", "source": P + "871-879",
+     "ratio": 2.0, "has_nrt": True, "existing": [32, True], "pod": [32, True], "want": False},
+]
+
+
 def main():
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "numa_plugin_cases.json")
     with open(path, "w") as f:
-        json.dump({"filter": FILTER, "reserve": RESERVE, "score_node1": SCORE_NODE1}, f, indent=1)
+        json.dump({"filter": FILTER, "reserve": RESERVE, "score_node1": SCORE_NODE1, "score_node2": SCORE_NODE2,
+                   "filter_amp": FILTER_AMP}, f, indent=1)
     print("wrote", path)
 
 

@@ -246,9 +246,9 @@ def build_numa_plugin_case(case):
     return prof, t, p, topo
 
 
-def build_numa_score_node1_case(case):
-    """-> (profile, NodeTable(1 row), pod(1)) for the node1 column of one
-    TestScoreWithAmplifiedCPUs row (scoring_test.go:797-851)."""
+def build_numa_score_node1_case(case, node=1):
+    """-> (profile, NodeTable(1 row), pod(1)) for the node1 (ratio 1.0) or node2
+    (ratio 2.0) column of one TestScoreWithAmplifiedCPUs row (scoring_test.go:797-851)."""
     from koordinator_amd import abi
     from koordinator_amd.config import PLUGIN_NUMA
     from koordinator_amd.numa import ClassTable, node_numa_flags, reference_test_topology
@@ -257,7 +257,8 @@ def build_numa_score_node1_case(case):
     prof = Profile(filters=(PLUGIN_NUMA,), scores={PLUGIN_NUMA: 1})
     prof.numa.scoring_type = case["scoring"]
     t = NodeTable.empty(1)
-    t["alloc0"][0], t["alloc1"][0] = 32000, 40 * gi
+    t["alloc0"][0], t["alloc1"][0] = (32000, 40 * gi) if node == 1 else (64000, 60 * gi)
+    t["numa_amp_cpu"][0] = 1.0 if node == 1 else 2.0
     t["alloc_pods"][0] = 110
     t["la_alloc_cpu_m"][0], t["la_alloc_mem"][0] = t["alloc0"][0], t["alloc1"][0]
     if case["existing"]:
@@ -282,4 +283,49 @@ def build_numa_score_node1_case(case):
         p["flags"][0] |= abi.POD_CPUSET
         p["numa_cpus"][0] = 8
         p["numa_policy"][0] = abi.numa_policy(0, abi.CPUBIND_FULL_PCPUS, 0)
+    return prof, t, p
+
+
+def build_numa_filter_amp_case(case):
+    """-> (profile, NodeTable(1 row), pod(1)) for one TestFilterWithAmplifiedCPUs
+    row (plugin_test.go:882-924)."""
+    import math
+    from koordinator_amd import abi
+    from koordinator_amd.config import PLUGIN_NUMA
+    from koordinator_amd.numa import ClassTable, node_numa_flags, reference_test_topology
+    from koordinator_amd.snapshot import NodeTable, pod_array
+    gi = 2**30
+    prof = Profile(filters=(PLUGIN_NUMA,), scores={PLUGIN_NUMA: 1})
+    ratio = case["ratio"]
+    amp = lambda v: v if ratio <= 1 else int(math.ceil(v * ratio))
+    t = NodeTable.empty(1)
+    t["alloc0"][0], t["alloc1"][0], t["alloc_pods"][0] = amp(32) * 1000, 40 * gi, 110
+    t["la_alloc_cpu_m"][0], t["la_alloc_mem"][0] = t["alloc0"][0], t["alloc1"][0]
+    t["numa_amp_cpu"][0] = ratio
+    ecpu, elsr = case["existing"]
+    t["requested0"][0], t["npods"][0] = ecpu * 1000, 1
+    if case["has_nrt"]:
+        topo = reference_test_topology(2, 1, 8, 2)
+        ct = ClassTable()
+        t["numa_class"][0] = ct.add(topo)
+        t.numa_classes = ct.records()
+        held = set(range(ecpu)) if elsr else set()
+        free = topo.mask([c for c in topo.cpu_of if c not in held])
+        for w in range(abi.NUMA_WORDS):
+            t[f"numa_free{w}"][0] = free[w]
+        t["numa_alloc_cnt"][0] = len(held)
+    t["numa_flags"][0] = node_numa_flags({}, None, prof.numa.default_most_allocated)
+    p = pod_array(1)
+    if case["pod"] is None:
+        p["flags"][0] = abi.POD_NUMA_SKIP
+        p["nz_cpu_m"][0], p["nz_mem"][0] = 100, 200 << 20
+    else:
+        cpu, lsr = case["pod"]
+        p["req"][0, abi.RES_CPU] = cpu * 1000
+        p["nz_cpu_m"][0], p["nz_mem"][0] = cpu * 1000, 200 << 20
+        p["flags"][0] = abi.POD_HAS_REQ | abi.POD_PROD
+        if lsr:
+            p["flags"][0] |= abi.POD_CPUSET
+            p["numa_cpus"][0] = cpu
+            p["numa_policy"][0] = abi.numa_policy(0, abi.CPUBIND_FULL_PCPUS, 0)
     return prof, t, p

@@ -134,3 +134,50 @@ def test_gpu_policy_commit_and_uncommit(Engine):
     assert rc == 0 and np.array_equal(cpus, rcpus)
     for k, v in o.numa_state().items():
         assert np.array_equal(nst[k], v), k
+
+
+# ------------------------------------------------------------ CPU amplification
+def _amp_cluster(n, prof, seed=5):
+    t = synth.make_cluster(synth.ClusterSpec(n, seed=seed), prof)
+    synth.add_numa(t, synth.NumaSpec(amp_frac=0.6), prof, seed=seed)
+    return t
+
+
+def test_gpu_amplified_eval_parity(Engine):
+    """filterAmplifiedCPUs / scoreWithAmplifiedCPUs / amplified cpuset scores on
+    random amplified nodes (ratios 1.25 / 1.5 / 2)."""
+    rng = np.random.default_rng(33)
+    prof = shipped_profile(numa=True)
+    t = _amp_cluster(400, prof)
+    assert (t["numa_amp_cpu"] > 1).sum() > 100
+    pods = _mixed_pods(rng, 64, prof)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got = e.eval(pods, k=8)
+    ref = oracle.Oracle(to_c_config(prof), t).eval(pods, k=8)
+    assert np.array_equal(got["status"], ref["status"])
+    assert np.array_equal(got["topk"], ref["topk"])
+    ok = (ref["status"] & abi.ST_NUMA_FAIL) == 0
+    bad = np.argwhere(ok & (got["scores"][:, 2] != ref["scores"][:, 2]))
+    assert len(bad) == 0, bad[:5]
+
+
+@pytest.mark.parametrize("scoring", ["LeastAllocated", "MostAllocated"])
+def test_gpu_amplified_stream_bit_exact(Engine, scoring):
+    prof = shipped_profile(numa=True)
+    prof.numa.scoring_type = scoring
+    table = _amp_cluster(600, prof, seed=8)
+    pods = synth.make_pods(synth.StreamSpec(1200, be_frac=0.2, cpuset_frac=0.5), prof)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(table)
+        got = e.place_stream(pods)
+        cs = e.fetch_cpusets(len(pods))
+        st, nst = e.read_nodes(), e.read_numa()
+    o = oracle.Oracle(to_c_config(prof), table)
+    ref, rcs = o.place_stream(pods, cpusets=True)
+    assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
+    assert np.array_equal(cs, rcs)
+    for k, v in o.state().items():
+        assert np.array_equal(st[k], v), k
+    for k, v in o.numa_state().items():
+        assert np.array_equal(nst[k], v), k

@@ -85,3 +85,43 @@ def test_score_node1_kat_gpu(Engine, name, case):
         e.load_snapshot(t)
         got = e.eval(pod)["scores"][0, 2, 0]
     assert got == case["want"], case["source"]
+
+
+SCORE2 = G.numa_plugin_cases("score_node2")
+FAMP = G.numa_plugin_cases("filter_amp")
+
+
+@pytest.mark.parametrize("name,case", SCORE2, ids=[c[0] for c in SCORE2])
+def test_score_node2_amplified_kat_oracle(name, case):
+    """TestScoreWithAmplifiedCPUs, ratio-2.0 node: scoreWithAmplifiedCPUs and the
+    amplified cpuset requests (scoring.go:95-168)."""
+    prof, t, pod = G.build_numa_score_node1_case(case, node=2)
+    assert oracle.Oracle(to_c_config(prof), t).eval(pod)["scores"][0, 2, 0] == case["want"], case["source"]
+
+
+@pytest.mark.parametrize("name,case", FAMP, ids=[c[0] for c in FAMP])
+def test_filter_amplified_kat_oracle(name, case):
+    """TestFilterWithAmplifiedCPUs (plugin.go:326-363)."""
+    prof, t, pod = G.build_numa_filter_amp_case(case)
+    st = oracle.Oracle(to_c_config(prof), t).eval(pod)["status"][0, 0]
+    assert (st & abi.ST_NUMA_FAIL == 0) == case["want"], case["source"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,case", SCORE2, ids=[c[0] for c in SCORE2])
+def test_score_node2_amplified_kat_gpu(Engine, name, case):
+    prof, t, pod = G.build_numa_score_node1_case(case, node=2)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got = e.eval(pod)["scores"][0, 2, 0]
+    assert got == case["want"], case["source"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,case", FAMP, ids=[c[0] for c in FAMP])
+def test_filter_amplified_kat_gpu(Engine, name, case):
+    prof, t, pod = G.build_numa_filter_amp_case(case)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        st = e.eval(pod)["status"][0, 0]
+    assert (st & abi.ST_NUMA_FAIL == 0) == case["want"], case["source"]
