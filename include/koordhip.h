@@ -25,6 +25,10 @@
  *   koordhip_commit         <- Reserve  load_aware.go:260-263 (podAssignCache.assign, pod_assign_cache.go:53-68),
  *                              (upstream) cache.AssumePod -> NodeInfo.AddPod
  *   koordhip_uncommit       <- Unreserve load_aware.go:265-267 (pod_assign_cache.go:70-80)
+ *   reservation columns     <- Reservation BeforePreFilter restore reservation/transformer.go:48-293,
+ *                              filterWithReservations plugin.go:373-494, PreScore/Score scoring.go:42-200,
+ *                              NominateReservation nominator.go:32-85, Reserve -> reservationCache.assumePod
+ *                              plugin.go:537-575 / cache.go:170-191
  */
 #ifndef KOORDHIP_H
 #define KOORDHIP_H
@@ -35,7 +39,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 4
+#define KOORDHIP_ABI_VERSION 5
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -50,7 +54,9 @@ extern "C" {
 #define KOORDHIP_PLUGIN_FIT 1u        /* NodeResourcesFit (upstream) */
 #define KOORDHIP_PLUGIN_LOADAWARE 2u  /* LoadAwareScheduling */
 #define KOORDHIP_PLUGIN_NUMA 4u       /* NodeNUMAResource */
-#define KOORDHIP_NPLUGINS 3
+#define KOORDHIP_PLUGIN_RESERVATION 8u /* Reservation (restore + filterWithReservations + Score, weight
+                                          koordhip_config.reservation_weight) */
+#define KOORDHIP_NPLUGINS 3            /* plugins with a per-node score in koordhip_eval's scores */
 
 /* Fit resource slots (ResourceSpec names in scheduler-config.yaml:21-31). */
 #define KOORDHIP_RES_CPU 0   /* "cpu", milli-CPU */
@@ -80,6 +86,23 @@ extern "C" {
 #define KOORDHIP_POD_CPUSET 32u       /* NUMA: requestCPUBind (plugin.go:230-245) */
 #define KOORDHIP_POD_NUMA_SKIP 64u    /* NUMA: PreFilter skip (zero request) (plugin.go:218-226) */
 #define KOORDHIP_POD_NUMA_ERROR 128u  /* NUMA: PreFilter error (non-integral cpuset request, plugin.go:242-245) */
+#define KOORDHIP_POD_KEY_CPU 256u     /* "cpu" key present in PodRequestsAndLimits (Reservation nominate / score / Restricted) */
+#define KOORDHIP_POD_KEY_MEM 512u     /* "memory" key present */
+
+/* koordhip_node_soa.resv_flags: the node's Available reservation (at most one
+ * per node: with several, the reference's order among them is Go map
+ * iteration order, cache.go:236-252).  0 = none. */
+#define KOORDHIP_RESV_PRESENT 1u       /* IsAvailable && ParseError == nil (transformer.go:87-89) */
+#define KOORDHIP_RESV_ALLOCATE_ONCE 2u /* IsReservationAllocateOnce (apis/extension/reservation.go:98-100) */
+#define KOORDHIP_RESV_UNSCHEDULABLE 4u /* IsUnschedulable: spec.unschedulable or terminating (reservation_info.go:248-255) */
+#define KOORDHIP_RESV_ORDERED 8u       /* label scheduling.koordinator.sh/reservation-order parses to != 0 (scoring.go:156-175) */
+#define KOORDHIP_RESV_KEY_CPU 16u      /* "cpu" in ResourceNames (the Allocatable keys, reservation_info.go:80-81) */
+#define KOORDHIP_RESV_KEY_MEM 32u      /* "memory" in ResourceNames */
+#define KOORDHIP_RESV_POLICY_SHIFT 6   /* bits 6-7 AllocatePolicy: 0 Default, 1 Aligned, 2 Restricted */
+#define KOORDHIP_RESV_POLICY(f) (((f) >> KOORDHIP_RESV_POLICY_SHIFT) & 3u)
+#define KOORDHIP_RESV_GROUP_SHIFT 8    /* bits 8-13: owner group g, the pod matches iff bit g of koordhip_pod.resv_match */
+#define KOORDHIP_RESV_GROUP(f) (((f) >> KOORDHIP_RESV_GROUP_SHIFT) & 63u)
+#define KOORDHIP_RESV_MAX_ORDERS 1024  /* distinct reservation-order values (resv_order_rank < this) */
 
 /* koordhip_pod.numa_policy, the NUMA PreFilter state (plugin.go:227-255):
  * bits 0-1 requiredCPUBindPolicy, 2-3 preferredCPUBindPolicy (= required when
@@ -135,6 +158,7 @@ typedef struct koordhip_numa_class {
 #define KOORDHIP_ST_FIT_FAIL 1u
 #define KOORDHIP_ST_LA_FAIL 2u
 #define KOORDHIP_ST_NUMA_FAIL 4u
+#define KOORDHIP_ST_RESV_FAIL 8u  /* filterWithReservations (reservation/plugin.go:373-440) */
 
 /* place_stream out_node values */
 #define KOORDHIP_UNSCHEDULABLE (-1)
@@ -160,7 +184,9 @@ typedef struct koordhip_config {
   int32_t profile_kernels;  /* 1 = time every stream eval launch with HIP events (koordhip_last_stats) */
   int32_t numa_most_allocated; /* NodeNUMAResourceArgs.ScoringStrategy.Type == MostAllocated
                                   (nodenumaresource/most_allocated.go:30-62); 0 = LeastAllocated */
-  int32_t reserved[6];
+  int32_t reservation_weight;  /* Reservation score weight (scheduler-config.yaml:90-91: 5000); must exceed
+                                  100 x the sum of the other score weights (Reservation key) */
+  int32_t reserved[5];
 } koordhip_config;
 
 /* Columnar node snapshot, all arrays of length n, little-endian, caller-owned
@@ -215,6 +241,20 @@ typedef struct koordhip_node_soa {
    * filterAmplifiedCPUs / scoreWithAmplifiedCPUs / amplified cpuset requests
    * (plugin.go:326-363, scoring.go:95-168).  NULL or <= 1: not amplified. */
   const double *numa_amp_cpu;
+  /* Reservation (KOORDHIP_PLUGIN_RESERVATION): the node's Available reservation,
+   * KOORDHIP_RESV_* flags (NULL = no reservations), the rank of its order label
+   * among the snapshot's distinct orders (ascending, smaller order = preferred),
+   * ReservationInfo.Allocatable / .Allocated (cpu milli, memory bytes; masked to
+   * ResourceNames) and len(AssignedPods).  Allocated / assigned are advanced by
+   * commits of pods the reservation is nominated for.  resv_nz: the reserve
+   * pod's non-zero cpu / memory request (calculateResource, transformer.go:
+   * 302-333; Requested of the reserve pod is resv_alloc). */
+  const uint32_t *resv_flags;
+  const int32_t *resv_order_rank;
+  const int64_t *resv_alloc[2];
+  const int64_t *resv_nz[2];
+  const int64_t *resv_allocated[2];
+  const int32_t *resv_assigned;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -228,7 +268,7 @@ typedef struct koordhip_pod {
   int32_t numa_cpus;          /* NUMA numCPUsNeeded (plugin.go:252) */
   uint32_t numa_policy;       /* KOORDHIP_NUMA_* packed policies */
   int32_t reserved0;
-  int64_t reserved1;
+  uint64_t resv_match;        /* bit g: MatchReservationOwners(pod, owner group g) (util/reservation/reservation.go:389-410) */
 } koordhip_pod;
 
 /* One top-k record of koordhip_eval. */
@@ -261,13 +301,17 @@ int koordhip_read_numa(koordhip_ctx *ctx, uint64_t *free_mask, uint64_t *excl_pc
 /* ... and the NUMA zone allocations, [n][2][KOORDHIP_NUMA_MAX_NODES] like numa_zone_used
  * (rows of nodes without a topology policy read as 0: the engine does not keep them). */
 int koordhip_read_numa_zones(koordhip_ctx *ctx, int64_t *zone_used);
+/* Reservation mutable state: Allocated [2][n] (cpu milli, memory), len(AssignedPods) [n]. */
+int koordhip_read_reservations(koordhip_ctx *ctx, int64_t *allocated, int32_t *assigned);
 
 /* Parity/debug mode, no commit: for n_pods pods against the current state.
  *   status : optional, [n_pods][n] KOORDHIP_ST_* bits (every plugin evaluated)
  *   scores : optional, [n_pods][KOORDHIP_NPLUGINS][n] per-plugin scores (0 where the plugin is disabled;
  *            the NodeNUMAResource score of a pair failing the NUMA Filter is unspecified, as the
  *            framework never scores such a node)
- *   topk   : optional, [n_pods][k] best feasible nodes by (total desc, index asc), node = -1 past the end */
+ *   topk   : optional, [n_pods][k] best feasible nodes by (total desc, index asc), node = -1 past the end
+ *            (with the Reservation plugin, `score` is the ranking total of DESIGN.md's Reservation key:
+ *            its order equals the order of the normalized weighted sums for the pod) */
 int koordhip_eval(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, uint8_t *status, int32_t *scores,
                   koordhip_topk *topk, int32_t k);
 

@@ -11,13 +11,13 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 4
+KOORDHIP_ABI_VERSION = 5
 NRES = 5
 NPLUGINS = 3
 
-PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA = 1, 2, 4
+PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_RESERVATION = 1, 2, 4, 8
 PLUGIN_BITS = {"NodeResourcesFit": PLUGIN_FIT, "LoadAwareScheduling": PLUGIN_LOADAWARE,
-               "NodeNUMAResource": PLUGIN_NUMA}
+               "NodeNUMAResource": PLUGIN_NUMA, "Reservation": PLUGIN_RESERVATION}
 RES_CPU, RES_MEM, RES_EPH, RES_BCPU, RES_BMEM = range(5)
 
 LA_HAS_METRIC, LA_FILTER_SKIP, LA_SCORE_EXPIRED, LA_FILTER_USAGE = 1, 2, 4, 8
@@ -25,6 +25,13 @@ LA_PROD_MODE, LA_HAS_PODS_METRIC, LA_AGGREGATED = 16, 32, 64
 
 POD_PROD, POD_DAEMONSET, POD_HAS_REQ, POD_REQ_BCPU, POD_REQ_BMEM = 1, 2, 4, 8, 16
 POD_CPUSET, POD_NUMA_SKIP, POD_NUMA_ERROR = 32, 64, 128
+POD_KEY_CPU, POD_KEY_MEM = 256, 512
+
+RESV_PRESENT, RESV_ALLOCATE_ONCE, RESV_UNSCHEDULABLE, RESV_ORDERED = 1, 2, 4, 8
+RESV_KEY_CPU, RESV_KEY_MEM = 16, 32
+RESV_POLICY_SHIFT, RESV_GROUP_SHIFT = 6, 8
+RESV_POLICY_DEFAULT, RESV_POLICY_ALIGNED, RESV_POLICY_RESTRICTED = 0, 1, 2
+RESV_MAX_GROUPS, RESV_MAX_ORDERS = 64, 1024
 
 CPUBIND_NONE, CPUBIND_FULL_PCPUS, CPUBIND_SPREAD_BY_PCPUS = 0, 1, 2
 CPUEXCL_NONE, CPUEXCL_PCPU, CPUEXCL_NUMA = 0, 1, 2
@@ -39,7 +46,7 @@ NUMA_MAX_ZONES = 4
 def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> int:
     return (required & 3) | ((preferred & 3) << 2) | ((exclusive & 3) << 4)
 
-ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL = 1, 2, 4
+ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL, ST_RESV_FAIL = 1, 2, 4, 8
 UNSCHEDULABLE, RESERVE_FAILED = -1, -2
 E_INVAL, E_RESERVE = -1, -6
 UNIQUE_ID_BYTES = 128
@@ -75,7 +82,8 @@ class KoordhipConfig(C.Structure):
         ("numa_weight_mem", C.c_int32),
         ("profile_kernels", C.c_int32),
         ("numa_most_allocated", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("reservation_weight", C.c_int32),
+        ("reserved", C.c_int32 * 5),
     ]
 
 
@@ -111,6 +119,12 @@ class KoordhipNodeSoa(C.Structure):
         ("numa_zone_alloc", _i64p),
         ("numa_zone_used", _i64p),
         ("numa_amp_cpu", C.POINTER(C.c_double)),
+        ("resv_flags", C.POINTER(C.c_uint32)),
+        ("resv_order_rank", _i32p),
+        ("resv_alloc", _i64p * 2),
+        ("resv_nz", _i64p * 2),
+        ("resv_allocated", _i64p * 2),
+        ("resv_assigned", _i32p),
     ]
 
 
@@ -140,7 +154,7 @@ POD_DTYPE = np.dtype([
     ("numa_cpus", "<i4"),
     ("numa_policy", "<u4"),
     ("reserved0", "<i4"),
-    ("reserved1", "<i8"),
+    ("resv_match", "<u8"),
 ], align=True)
 assert POD_DTYPE.itemsize == 96
 TOPK_DTYPE = np.dtype([("node", "<i4"), ("score", "<i4")])
@@ -189,6 +203,7 @@ def load_library(path: str = LIB_PATH):
         "koordhip_fetch_cpusets": (C.c_int, [vp, _u64p, C.c_int32]),
         "koordhip_read_numa": (C.c_int, [vp, _u64p, _u64p, _u64p, _i32p]),
         "koordhip_read_numa_zones": (C.c_int, [vp, _i64p]),
+        "koordhip_read_reservations": (C.c_int, [vp, _i64p, _i32p]),
         "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_last_kernel_stats": (C.c_int, [vp, C.POINTER(KoordhipKernelStats)]),
@@ -212,7 +227,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
-    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_last_stats", "koordhip_last_kernel_stats",
+    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations", "koordhip_last_stats", "koordhip_last_kernel_stats",
     "koordhip_set_profile_kernels",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]

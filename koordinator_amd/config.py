@@ -21,6 +21,7 @@ FIT_RESOURCES = [k8s.CPU, k8s.MEMORY, k8s.EPHEMERAL, k8s.BATCH_CPU, k8s.BATCH_ME
 PLUGIN_FIT = "NodeResourcesFit"
 PLUGIN_LOADAWARE = "LoadAwareScheduling"
 PLUGIN_NUMA = "NodeNUMAResource"
+PLUGIN_RESERVATION = "Reservation"
 
 
 class ArgsError(ValueError):
@@ -151,9 +152,10 @@ class Profile:
         return p
 
 
-def shipped_profile(numa: bool = False) -> Profile:
+def shipped_profile(numa: bool = False, reservation: bool = False) -> Profile:
     """config/manager/scheduler-config.yaml:17-46,82-91 restricted to Fit + LoadAware
-    (+ NodeNUMAResource with default args and score weight 1 when `numa`)."""
+    (+ NodeNUMAResource with default args and score weight 1 when `numa`; + the
+    Reservation plugin, Filter and Score weight 5000 (:60-91), when `reservation`)."""
     la = LoadAwareSchedulingArgs(
         filter_expired_node_metrics=False,
         node_metric_expiration_seconds=300,
@@ -162,6 +164,12 @@ def shipped_profile(numa: bool = False) -> Profile:
         estimated_scaling_factors={k8s.CPU: 85, k8s.MEMORY: 70},
     )
     fit = NodeResourcesFitArgs(resources={k8s.CPU: 1, k8s.MEMORY: 1, k8s.BATCH_CPU: 1, k8s.BATCH_MEMORY: 1})
+    if reservation:
+        filters = (PLUGIN_FIT, PLUGIN_LOADAWARE) + ((PLUGIN_NUMA,) if numa else ()) + (PLUGIN_RESERVATION,)
+        scores = {PLUGIN_FIT: 1, PLUGIN_LOADAWARE: 1, PLUGIN_RESERVATION: 5000}
+        if numa:
+            scores[PLUGIN_NUMA] = 1
+        return Profile(filters=filters, scores=scores, fit=fit, loadaware=la)
     if numa:
         return Profile(filters=(PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA),
                        scores={PLUGIN_FIT: 1, PLUGIN_LOADAWARE: 1, PLUGIN_NUMA: 1}, fit=fit, loadaware=la)
@@ -188,6 +196,16 @@ def to_c_config(profile: Profile, device: int = -1):
         if name in p.scores and not (1 <= w <= 100):
             raise ArgsError(f"score weight of {name} out of range, got {w}")
         cfg.plugin_weight[i] = w
+    if PLUGIN_RESERVATION in p.scores:
+        w = p.scores[PLUGIN_RESERVATION]
+        bmax = 100 * sum(p.scores.get(x, 0) for x in order)
+        if not (1 <= w <= 1000000):
+            raise ArgsError(f"score weight of {PLUGIN_RESERVATION} out of range, got {w}")
+        if w <= bmax:
+            # the engine ranks by (normalized reservation score, other plugins' total): exact only
+            # when one unit of the former outweighs the latter (Reservation key)
+            raise ArgsError(f"Reservation weight {w} must exceed 100 x the other score weights ({bmax})")
+        cfg.reservation_weight = w
     for i, r in enumerate(FIT_RESOURCES):
         cfg.fit_weight[i] = p.fit.resources.get(r, 0)
     cfg.la_weight_cpu = p.loadaware.resource_weights.get(k8s.CPU, 0)

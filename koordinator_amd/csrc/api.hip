@@ -107,6 +107,8 @@ struct koordhip_ctx {
   uint64_t *d_cpus = nullptr;  // [pods_cap][KOORDHIP_NUMA_WORDS] cpusets of the last place call (NUMA)
   int32_t out_cap = 0;
   bool numa = false;           // NodeNUMAResource enabled (Filter or Score)
+  bool resv = false;           // Reservation enabled (Filter or Score)
+  bool side = false;           // the kernels keep NUMA side rows (NodeNUMAResource or Reservation)
   int32_t n_classes = 0;
   kh::DevNumaClass *d_classes = nullptr;
   int32_t *d_rc = nullptr;     // k_commit status
@@ -241,6 +243,7 @@ int to_dev_pods(const koordhip_pod *src, int32_t n, std::vector<kh::DevPod> &out
     o.flags = p.flags;
     o.numa_cpus = p.numa_cpus;
     o.numa_policy = p.numa_policy;
+    o.resv_match = p.resv_match;
   }
   return 0;
 }
@@ -427,7 +430,7 @@ int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     (void)hipFree(c->d_classes);
     c->d_classes = nullptr;
   }
-  if (!c->numa) return 0;
+  if (!c->side) return 0;
   const bool have = s->numa_class != nullptr;
   if (have && s->n_numa_classes > 0 && !s->numa_classes) return fail(KOORDHIP_EINVAL, "numa_classes is NULL");
   if (have)
@@ -517,6 +520,60 @@ int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   return e;
 }
 
+// Reservation columns (one Available reservation per node): validated, then
+// uploaded; without them (or with the plugin off) the device sees none.
+int check_resv_rows(const koordhip_node_soa *s, int32_t m) {
+  for (int k = 0; k < 2; k++)
+    if (!s->resv_alloc[k] || !s->resv_nz[k] || !s->resv_allocated[k]) return fail(KOORDHIP_EINVAL, "reservation column missing");
+  if (!s->resv_order_rank || !s->resv_assigned) return fail(KOORDHIP_EINVAL, "reservation column missing");
+  for (int32_t i = 0; i < m; i++) {
+    const uint32_t f = s->resv_flags[i];
+    if (!(f & KOORDHIP_RESV_PRESENT)) continue;
+    if (KOORDHIP_RESV_POLICY(f) > 2) return fail(KOORDHIP_EINVAL, "resv_flags: unknown allocate policy");
+    if ((f & KOORDHIP_RESV_ORDERED) && (s->resv_order_rank[i] < 0 || s->resv_order_rank[i] >= KOORDHIP_RESV_MAX_ORDERS))
+      return fail(KOORDHIP_EINVAL, "resv_order_rank out of [0, KOORDHIP_RESV_MAX_ORDERS)");
+    if (s->resv_assigned[i] < 0) return fail(KOORDHIP_EINVAL, "resv_assigned < 0");
+    for (int k = 0; k < 2; k++)
+      if (s->resv_alloc[k][i] < 0 || s->resv_allocated[k][i] < 0 || s->resv_nz[k][i] < 0 || !exact_ok(s->resv_alloc[k][i]) ||
+          !exact_ok(s->resv_allocated[k][i]) || !exact_ok(s->resv_nz[k][i]))
+        return fail(KOORDHIP_EINVAL, "reservation quantity out of range");
+  }
+  return 0;
+}
+
+int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
+  c->d.rv = kh::DevResv{};
+  c->dc.resv = 0;
+  if (!c->resv || !s->resv_flags) return 0;
+  if (int e = check_resv_rows(s, n)) return e;
+  kh::DevResv &rv = c->d.rv;
+  uint32_t *f = nullptr;
+  int32_t *rk = nullptr, *rn = nullptr;
+  int e = dev_alloc(c, &f, n);
+  if (!e) e = upload(c, f, s->resv_flags, n);
+  if (!e) e = dev_alloc(c, &rk, n);
+  if (!e) e = upload(c, rk, s->resv_order_rank, n);
+  if (!e) e = dev_alloc(c, &rn, n);
+  if (!e) e = upload(c, rn, s->resv_assigned, n);
+  for (int k = 0; k < 2 && !e; k++) {
+    double *a = nullptr, *z = nullptr, *d = nullptr;
+    e = dev_alloc(c, &a, n);
+    if (!e) e = upload_q(c, a, s->resv_alloc[k], n, "resv_alloc");
+    if (!e) e = dev_alloc(c, &z, n);
+    if (!e) e = upload_q(c, z, s->resv_nz[k], n, "resv_nz");
+    if (!e) e = dev_alloc(c, &d, n);
+    if (!e) e = upload_q(c, d, s->resv_allocated[k], n, "resv_allocated");
+    rv.ra[k] = a;
+    rv.rz[k] = z;
+    rv.rd[k] = d;
+  }
+  rv.flags = f;
+  rv.rank = rk;
+  rv.rn = rn;
+  if (!e) c->dc.resv = 1;
+  return e;
+}
+
 void shard(const koordhip_ctx *c, int32_t *lo, int32_t *hi) {
   *lo = (int32_t)((int64_t)c->n * c->rank / c->world);
   *hi = (int32_t)((int64_t)c->n * (c->rank + 1) / c->world);
@@ -532,7 +589,7 @@ int koordhip_abi_version(void) { return KOORDHIP_ABI_VERSION; }
 int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (!cfg || !out) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (cfg->abi_version != KOORDHIP_ABI_VERSION) return fail(KOORDHIP_EINVAL, "abi_version mismatch");
-  const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA;
+  const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA | KOORDHIP_PLUGIN_RESERVATION;
   if ((cfg->filter_plugins | cfg->score_plugins) & ~known) return fail(KOORDHIP_EINVAL, "unknown plugin bit");
   if (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) {
     if (cfg->numa_weight_cpu < 0 || cfg->numa_weight_cpu > 100 || cfg->numa_weight_mem < 0 || cfg->numa_weight_mem > 100)
@@ -571,11 +628,13 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.numa_w_mem = cfg->numa_weight_mem;
   c->dc.numa_most = cfg->numa_most_allocated ? 1 : 0;
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
+  c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
+  c->side = c->numa || c->resv;
   if (const char *r = std::getenv("KOORDHIP_TOPK_R")) {
     const int v = std::atoi(r);
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
   }
-  if (c->numa && c->partial_r > 4) c->partial_r = 4;  // the NUMA scan kernel is built for R <= 4
+  if (c->side && c->partial_r > 4) c->partial_r = 4;  // the NUMA / Reservation scan kernels are built for R <= 4
   // the split select shortens the evaluation stream (and drops the signal
   // kernel); KOORDHIP_SELECT_ONEWG restores one workgroup per pod for A/B runs
   c->sel_split = std::getenv("KOORDHIP_SELECT_ONEWG") == nullptr;
@@ -587,6 +646,21 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     int64_t max_total = 0;  // every plugin score is in [0, 100]
     for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
       if (cfg->score_plugins & (1u << p)) max_total += 100 * cfg->plugin_weight[p];
+    c->dc.resv_b1 = (int32_t)max_total + 1;
+    if (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION) {
+      // the ranking totals of resv.hpp: one normalised Reservation unit must
+      // outweigh every other total, and they must fit the u16 score matrix /
+      // the selection histogram
+      if ((int64_t)cfg->reservation_weight <= max_total) {
+        delete c;
+        return fail(KOORDHIP_EINVAL, "reservation_weight must exceed 100 x the other score weights");
+      }
+      max_total = 101 * (max_total + 1) + KOORDHIP_RESV_MAX_ORDERS - 1;
+      if (max_total + 2 > 32768) {
+        delete c;
+        return fail(KOORDHIP_EINVAL, "with Reservation scoring the other score weights may sum to at most 3");
+      }
+    }
     int bits = 1;
     while ((1ll << bits) <= max_total + 1) bits++;
     c->score_bits = bits;
@@ -738,6 +812,7 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   if (!e) e = upload(c, lf, s->la_flags, n);
   pi.la_flags = lf;
   if (!e) e = load_numa_columns(c, s, n);
+  if (!e) e = load_resv_columns(c, s, n);
   if (e) {
     free_cols(c);
     return e;
@@ -799,6 +874,14 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     }
     amp_rows = c->d.nu.amp != nullptr;
   }
+  const bool resv_rows = c->dc.resv && rows->resv_flags;
+  if (c->resv && rows->resv_flags && !c->dc.resv) {
+    for (int32_t j = 0; j < m; j++)
+      if (rows->resv_flags[j] & KOORDHIP_RESV_PRESENT)
+        return fail(KOORDHIP_EINVAL, "a reservation needs the reservation columns at load_snapshot");
+  }
+  if (resv_rows)
+    if (int e = check_resv_rows(rows, m)) return e;
   // ---- one host staging image: [idx][column 0][column 1]..., 8-B aligned
   //      segments, quantities converted to the device's exact f64
   struct Col {
@@ -846,6 +929,17 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   }
   if (amp_rows)
     cols.push_back({const_cast<double *>(c->d.nu.amp), rows->numa_amp_cpu, 8, false, "numa_amp_cpu"});
+  if (resv_rows) {
+    kh::DevResv &rv = c->d.rv;
+    cols.push_back({const_cast<uint32_t *>(rv.flags), rows->resv_flags, 4, false, "resv_flags"});
+    cols.push_back({const_cast<int32_t *>(rv.rank), rows->resv_order_rank, 4, false, "resv_order_rank"});
+    cols.push_back({rv.rn, rows->resv_assigned, 4, false, "resv_assigned"});
+    for (int k = 0; k < 2; k++) {
+      cols.push_back({const_cast<double *>(rv.ra[k]), rows->resv_alloc[k], 8, true, "resv_alloc"});
+      cols.push_back({const_cast<double *>(rv.rz[k]), rows->resv_nz[k], 8, true, "resv_nz"});
+      cols.push_back({rv.rd[k], rows->resv_allocated[k], 8, true, "resv_allocated"});
+    }
+  }
   if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one 64-B element per row
     kh::DevNuma &nu = c->d.nu;
     cols.push_back({const_cast<double *>(nu.za), zrow_a.data(), 64, false, "numa_zone_alloc"});
@@ -964,6 +1058,27 @@ int koordhip_read_numa_zones(koordhip_ctx *c, int64_t *zone_used) {
   for (size_t i = 0; i < n; i++)
     for (int q = 0; q < 2; q++)
       for (int k = 0; k < Z; k++) zone_used[(i * 2 + q) * NM + k] = (int64_t)zu[(i * 2 + q) * Z + k];
+  return 0;
+}
+
+int koordhip_read_reservations(koordhip_ctx *c, int64_t *allocated, int32_t *assigned) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (!c->resv) return fail(KOORDHIP_ESTATE, "Reservation is not enabled");
+  const size_t n = c->n;
+  if (n == 0) return 0;
+  if (!c->dc.resv) {  // no reservation columns: nothing is reserved anywhere
+    if (allocated) std::memset(allocated, 0, 2 * n * sizeof(int64_t));
+    if (assigned) std::memset(assigned, 0, n * sizeof(int32_t));
+    return 0;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  int e = 0;
+  if (allocated) e = download_q(c->d.rv.rd[0], allocated, n);
+  if (allocated && !e) e = download_q(c->d.rv.rd[1], allocated + n, n);
+  if (e) return e;
+  if (assigned) HIP_TRY(hipMemcpy(assigned, c->d.rv.rn, n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -1155,9 +1270,10 @@ int place_staged_impl(koordhip_ctx *c) {
   int32_t P = c->batch;
   // (NodeNUMAResource streams are bound by the resolve's cpuset Reserve: the
   // longer re-evaluated set of lag 2 measured slower there, 87k vs 93k pods/s)
-  int32_t lag = (two && !c->numa && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
+  int32_t lag = (two && !c->side && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
   if (lag == 2 && 3 * P > kh::kResolveMaxK) lag = 1;
-  while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, c->numa, lag) > 157 * 1024) P--;
+  const int nm = kh::side_mode(c->dc);
+  while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, nm, lag) > 157 * 1024) P--;
   const int32_t K = (lag + 1) * P;
   c->last_P = P;
   c->last_lag = lag;
@@ -1187,7 +1303,7 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * lbytes));
     c->gather_world = c->world;
   }
-  if (kh::resolve_lds_bytes(P, K, c->n, c->numa, lag) > 157 * 1024)
+  if (kh::resolve_lds_bytes(P, K, c->n, nm, lag) > 157 * 1024)
     return fail(KOORDHIP_EINVAL, "snapshot too large for the resolve kernel's LDS");
   if (c->group)
     if (int e = group_agree(c)) return e;
@@ -1403,6 +1519,11 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
     v.push_back({nu.cnt, n * sizeof(int32_t)});
     if (nu.zu) v.push_back({nu.zu, n * 2 * KOORDHIP_NUMA_MAX_ZONES * sizeof(double)});
   }
+  if (c->dc.resv) {
+    v.push_back({c->d.rv.rd[0], b});
+    v.push_back({c->d.rv.rd[1], b});
+    v.push_back({c->d.rv.rn, n * sizeof(int32_t)});
+  }
   return v;
 }
 
@@ -1454,7 +1575,9 @@ static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, i
   HIP_TRY(hipMemcpyAsync(got, d_cpus, sizeof(got), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (rc == KOORDHIP_EINVAL)
-    return fail(rc, "Unreserve of a NodeNUMAResource pod on a NUMA topology-policy node (its zone amounts are not passed back)");
+    return fail(rc, "Unreserve not supported here: a NodeNUMAResource pod on a NUMA topology-policy node (its zone amounts "
+                    "are not passed back) or a pod its node's reservation matches (whether the Reserve took the "
+                    "reservation is not passed back)");
   if (rc) return fail(rc, "Reserve failed: NodeNUMAResource could not allocate the cpuset");
   if (sign > 0 && cpus_io) std::memcpy(cpus_io, got, sizeof(got));
   return 0;

@@ -43,6 +43,8 @@ struct DevCfg {
   int32_t numa_most;               // NodeNUMAResource MostAllocated scoring strategy
   int32_t zones;                   // some node has a NUMA topology policy (zone columns loaded)
   int32_t amp;                     // some node has a CPU amplification ratio > 1
+  int32_t resv;                    // Reservation enabled and the snapshot carries reservation columns
+  int32_t resv_b1;                 // 1 + the other plugins' maximum weighted total (resv.hpp ranking total)
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -58,6 +60,7 @@ struct DevNodes {
   uint8_t *flags;
   int32_t n;
   DevNuma nu;  // NodeNUMAResource columns (unused unless the plugin is enabled)
+  DevResv rv;  // Reservation columns (NM == 3 builds)
 };
 
 // One node's values as the evaluation consumes them (registers or an LDS row).
@@ -76,6 +79,7 @@ struct Need {
   bool numa, numa_masks;  // NUMA class (+ the cpuset masks for a cpuset pod)
   bool zones;             // node flags + NUMA zones (topology-policy nodes)
   bool amp;               // the CPU amplification ratio + allocated cpuset count
+  bool resv;              // the reservation columns (the restore rewrites Requested / NonZero / pods)
 };
 
 __device__ __forceinline__ bool numa_on(const DevCfg &c) {
@@ -126,6 +130,14 @@ __device__ __forceinline__ Need pod_needs(const DevPod &p, const DevCfg &c) {
     n.r_mem = true;
     n.a_cpu = n.a_mem = true;
   }
+  if (c.resv) {
+    // the restore rewrites Requested (the over-commit bits are re-derived from
+    // it), NonZeroRequested and the pod count; a matched reservation's Aligned /
+    // Restricted filter reads ephemeral storage too
+    n.resv = true;
+    n.r_cpu = n.r_mem = n.pods = true;
+    n.eph |= (c.filt & KOORDHIP_PLUGIN_RESERVATION) && p.resv_match != 0ull;
+  }
   n.a_cpu = n.a_cpu || n.r_cpu || n.nz_cpu || (n.la && c.la_alias);
   n.a_mem = n.a_mem || n.r_mem || n.nz_mem || (n.la && c.la_alias);
   return n;
@@ -140,6 +152,7 @@ __device__ __forceinline__ Need need_all(const DevCfg &c) {
   n.numa = n.numa_masks = numa_on(c);
   n.zones = n.numa && c.zones;
   n.amp = n.numa && c.amp;
+  n.resv = c.resv != 0;
   return n;
 }
 
@@ -444,6 +457,30 @@ __device__ __forceinline__ int32_t eval_total_numa(const DevPod &p, const NV &v,
   if (nf && c.amp && !amp_filter_ok(p, v, r)) return -1;
   if (nf && !numa_filter<Z>(p, r, classes)) return -1;
   if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score<Z>(p, v, r, classes, c, nf);
+  return t;
+}
+
+}  // namespace kh
+
+#include "resv.hpp"
+
+namespace kh {
+
+// ... with the Reservation plugin (NM == 3): the cycle's restore of the
+// node's reservation first (every plugin sees the restored NodeInfo), then
+// filterWithReservations and the ranking total of resv.hpp.
+__device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v, const NumaRowR &r,
+                                                   const DevNumaClass *classes, const DevCfg &c) {
+  NV w = v;
+  const int cls = resv_class(r, p);
+  resv_restore(w, r, cls);
+  int32_t t = eval_total_numa<false>(p, w, r, classes, c);
+  if (t < 0 || cls != 1) return t;
+  if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !resv_filter(p, w, r)) return -1;
+  if (c.score & KOORDHIP_PLUGIN_RESERVATION) {
+    if (r.rf & KOORDHIP_RESV_ORDERED) return 101 * c.resv_b1 + (KOORDHIP_RESV_MAX_ORDERS - 1 - r.rk);
+    if (resv_nominated(p, r)) t += resv_score(p, r) * c.resv_b1;
+  }
   return t;
 }
 

@@ -60,7 +60,9 @@ hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, h
 // evaluation stream(s) bracket each round with k_wait_resolved (before k_scan)
 // and k_signal_lists (after the lists).
 constexpr int32_t kResolveMaxK = 128;  // longest list the resolve takes (RES_MAXP)
-int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa, int32_t lag);
+// nm: the kernels' node-row mode, 0 none, 1 NodeNUMAResource, 2 + topology-policy zones, 3 + Reservation
+int side_mode(const DevCfg &c);
+int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, int nm, int32_t lag);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,
                           int32_t lag, PipeSync *sync, int32_t *mbuf, int32_t *out_node, uint64_t *out_cpus, uint64_t *dbg,

@@ -166,8 +166,14 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
   NV v{};
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
-  NumaRow nr{};
+  NumaRowR nr{};
   load_numa<true>(nr, d, i, all);
+  int rcls = 0;
+  if (c.resv) {  // the cycle's Reservation restore: every plugin sees the restored node
+    load_resv(nr, d.rv, i);
+    rcls = resv_class(nr, pod);
+    resv_restore(v, nr, rcls);
+  }
   if (status) {
     uint8_t b = 0;
     if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(pod, v)) b |= KOORDHIP_ST_FIT_FAIL;
@@ -175,6 +181,7 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
     if ((c.filt & KOORDHIP_PLUGIN_NUMA) &&
         (!numa_filter<true>(pod, nr, d.nu.cls) || (c.amp && !amp_filter_ok(pod, v, nr))))
       b |= KOORDHIP_ST_NUMA_FAIL;
+    if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && rcls == 1 && !resv_filter(pod, v, nr)) b |= KOORDHIP_ST_RESV_FAIL;
     status[(size_t)p * d.n + i] = b;
   }
   if (scores) {
@@ -390,7 +397,8 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 // and the 4 x (pods/4) re-reads of a row hit L2 instead of the MALL.
 
 // NM: 0 = no NodeNUMAResource, 1 = NodeNUMAResource, 2 = ... with
-// topology-policy nodes (the zone code is compiled only here)
+// topology-policy nodes (the zone code is compiled only here), 3 = with the
+// Reservation plugin (NUMA side rows carry the node's reservation)
 template <int R, int NM>
 __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
                                               int32_t lo, int32_t hi, int32_t nchunks, int32_t cpx,
@@ -431,7 +439,12 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
     if (full || i < hi) {
       NV v;
       load_node(v, d, i, need, c);
-      if constexpr (NM != 0) {
+      if constexpr (NM == 3) {
+        NumaRowR nr;
+        load_numa<false>(nr, d, i, need);
+        load_resv(nr, d.rv, i);
+        s[r] = eval_total_resv(pod, v, nr, cls, c) + 1;
+      } else if constexpr (NM != 0) {
         NumaRow nr;
         load_numa<NM == 2>(nr, d, i, need);
         s[r] = eval_total_numa<NM == 2>(pod, v, nr, cls, c) + 1;
@@ -1099,8 +1112,9 @@ struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
 
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
 
-__host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, bool numa,
+__host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, int32_t nrow,
                                           bool overlap = false, bool tables = true, int32_t lag = 1) {
+  const bool numa = nrow > 0;  // nrow: bytes of a NUMA side row (0: none)
   ResLds o;
   int32_t at = 0;
   const int32_t bitmap = res_align(((n_nodes + 31) >> 5) * 4);
@@ -1111,7 +1125,7 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   // two row regions, M' (prev) and M (cur), swapped at the end of every round;
   // a round commits to at most n_pods_max nodes, M' spans `lag` rounds
   const int32_t rows_b = res_align(lag * n_pods_max * (int32_t)sizeof(NV));
-  const int32_t numa_b = numa ? res_align(lag * n_pods_max * (int32_t)sizeof(NumaRow)) : 0;
+  const int32_t numa_b = numa ? res_align(lag * n_pods_max * nrow) : 0;
   o.prev_rows = at;
   o.prev_numa = at + rows_b;
   at += rows_b + numa_b;
@@ -1125,7 +1139,7 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   o.pre_rows = at;
   at += res_align(RES_PRE * (int32_t)sizeof(NV));
   o.pre_numa = at;
-  at += numa ? res_align(RES_PRE * (int32_t)sizeof(NumaRow)) : 0;
+  at += numa ? res_align(RES_PRE * nrow) : 0;
   o.pre_node = at;
   at += RES_PRE * 4;
   // the prologue's per-pod decisions: winner key, walked entries (-1: general
@@ -1172,7 +1186,7 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
     o.pre_rows2 = at;
     at += res_align(RES_PRE * (int32_t)sizeof(NV));
     o.pre_numa2 = at;
-    at += numa ? res_align(RES_PRE * (int32_t)sizeof(NumaRow)) : 0;
+    at += numa ? res_align(RES_PRE * nrow) : 0;
     o.pre_node2 = at;
     at += RES_PRE * 4;
   }
@@ -1198,9 +1212,25 @@ __device__ __forceinline__ uint64_t ktab_key(uint32_t v, int32_t nd) {
 }
 
 template <int NM>
-__device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const NumaRow &nr,
+using side_row_t = typename std::conditional<NM == 3, NumaRowR, NumaRow>::type;
+
+template <int NM>
+__device__ __forceinline__ void load_side_row(side_row_t<NM> &r, const DevNodes &d, int32_t i) {
+  load_numa_row<NM == 2>(r, d, i);
+  if constexpr (NM == 3) load_resv(r, d.rv, i);
+}
+template <int NM>
+__device__ __forceinline__ void store_side_row(const side_row_t<NM> &r, const DevNodes &d, int32_t i) {
+  store_numa_row<NM == 2>(r, d, i);
+  if constexpr (NM == 3) store_resv(r, d.rv, i);
+}
+
+template <int NM>
+__device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const side_row_t<NM> &nr,
                                             const DevNumaClass *cls, const DevCfg &c) {
-  if constexpr (NM != 0) {
+  if constexpr (NM == 3) {
+    return eval_total_resv(p, v, nr, cls, c);
+  } else if constexpr (NM != 0) {
     return eval_total_numa<NM == 2>(p, v, nr, cls, c);
   } else {
     (void)nr;
@@ -1231,18 +1261,19 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                                                                  uint64_t *__restrict__ dbg, int32_t trace) {
   constexpr int RES_THREADS = res_threads<NM>();
   constexpr bool NUMA = NM != 0, ZONES = NM == 2;
+  using NR = side_row_t<NM>;  // the NUMA side row (+ the node's reservation with NM == 3)
   (void)trace;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   uint64_t *lk = reinterpret_cast<uint64_t *>(lds + ofs.lists);
   DevPod *lpod = reinterpret_cast<DevPod *>(lds + ofs.pods);
   NV *prow = reinterpret_cast<NV *>(lds + ofs.prev_rows);  // M' rows, slot = M' index
-  NumaRow *pnr = reinterpret_cast<NumaRow *>(lds + ofs.prev_numa);
+  NR *pnr = reinterpret_cast<NR *>(lds + ofs.prev_numa);
   NV *mrow = reinterpret_cast<NV *>(lds + ofs.cur_rows);   // M rows, slot = M index
-  NumaRow *mnr = reinterpret_cast<NumaRow *>(lds + ofs.cur_numa);
+  NR *mnr = reinterpret_cast<NR *>(lds + ofs.cur_numa);
   int32_t *hnode = reinterpret_cast<int32_t *>(lds + ofs.hash_node);
   int32_t *hslot = reinterpret_cast<int32_t *>(lds + ofs.hash_slot);
   NV *pre = reinterpret_cast<NV *>(lds + ofs.pre_rows);
-  NumaRow *prenr = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa);
+  NR *prenr = reinterpret_cast<NR *>(lds + ofs.pre_numa);
   int32_t *pre_node = reinterpret_cast<int32_t *>(lds + ofs.pre_node);
   uint64_t *dec_key = reinterpret_cast<uint64_t *>(lds + ofs.dec_key);
   int32_t *dec_n = reinterpret_cast<int32_t *>(lds + ofs.dec_n);
@@ -1261,7 +1292,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t *lk2 = reinterpret_cast<uint64_t *>(lds + ofs.lists2);
   DevPod *lpod2 = reinterpret_cast<DevPod *>(lds + ofs.pods2);
   NV *pre2 = reinterpret_cast<NV *>(lds + ofs.pre_rows2);
-  NumaRow *prenr2 = reinterpret_cast<NumaRow *>(lds + ofs.pre_numa2);
+  NR *prenr2 = reinterpret_cast<NR *>(lds + ofs.pre_numa2);
   int32_t *pre_node2 = reinterpret_cast<int32_t *>(lds + ofs.pre_node2);
   __shared__ int32_t pnode[RES_MAXP_ROUND];  // M' = the nodes the previous `lag` rounds committed to
   __shared__ int32_t pgen[RES_MAXP_ROUND];   // ... and the round that last did (lag 2)
@@ -1316,8 +1347,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     load_row(v, nodes(), nd);
     prow[t] = v;
     if constexpr (NUMA) {
-      NumaRow rr;
-      load_numa_row<ZONES>(rr, nodes(), nd);
+      NR rr;
+      load_side_row<NM>(rr, nodes(), nd);
       pnr[t] = rr;
     }
     atomicOr(&modmap[nd >> 5], 1u << (nd & 31));
@@ -1343,7 +1374,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   // Every loop keeps several global loads in flight per thread before its LDS
   // stores: wave 1 alone runs this for the next round (64 threads), where one
   // load-store pair per iteration serialised ~40 HBM round trips.
-  auto load_round = [&](int32_t rr, int32_t rp0, int32_t rn, uint64_t *Lk, DevPod *Lp, NV *Pr, NumaRow *Pn,
+  auto load_round = [&](int32_t rr, int32_t rp0, int32_t rn, uint64_t *Lk, DevPod *Lp, NV *Pr, NR *Pn,
                         int32_t *Pnode, int32_t tid, int32_t nth) {
     const uint64_t *L = lists0 + (size_t)(rr & (2 * lag - 1)) * list_buf;
     const int32_t tot = rn * kp;
@@ -1395,8 +1426,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         if (nd[u] >= 0) {
           Pr[sl] = v[u];
           if constexpr (NUMA) {
-            NumaRow rr2;
-            load_numa_row<ZONES>(rr2, nodes(), nd[u]);
+            NR rr2;
+            load_side_row<NM>(rr2, nodes(), nd[u]);
             Pn[sl] = rr2;
           }
         }
@@ -1520,8 +1551,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             load_row(v, nodes(), w);
             pre[ps] = v;
             if constexpr (NUMA) {
-              NumaRow nr;
-              load_numa_row<ZONES>(nr, nodes(), w);
+              NR nr;
+              load_side_row<NM>(nr, nodes(), w);
               prenr[ps] = nr;
             }
             pre_node[ps] = w;
@@ -1569,6 +1600,11 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         // to emptier zones as a node fills, so its score is not monotone)
         slow = slow || (numa_on(c) && ((fl & KOORDHIP_POD_CPUSET) || c.zones) &&
                         !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
+      }
+      if constexpr (NM == 3) {
+        // a pod some reservation may match: committing into a reservation raises
+        // its (MostAllocated) reservation score elsewhere -- not monotone
+        slow = slow || (live && lpod[lane].resv_match != 0ull);
       }
       // ---- conflicts among the staged decisions: pod l's walk met the staged
       //      winner of an earlier pod (exact node -> first pod hash, linear probing)
@@ -1729,7 +1765,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                 const int32_t ms = m_slot(y);
                 const int32_t sl = ms >= 0 ? -1 : prev_slot(y);
                 const NV *row = ms >= 0 ? &mrow[ms] : &prow[sl];
-                NumaRow nr;
+                NR nr;
                 if constexpr (NUMA) nr = ms >= 0 ? mnr[ms] : pnr[sl];
                 kv = make_key(eval_row<NM>(pod, slot_row(*row), nr, cls, c), y);
               }
@@ -1744,11 +1780,11 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           const int32_t s = b0 + lane;
           uint64_t kv = 0;
           if (s < nm) {
-            NumaRow nr;
+            NR nr;
             if constexpr (NUMA) nr = mnr[s];
             kv = make_key(eval_row<NM>(pod, slot_row(mrow[s]), nr, cls, c), my_node);
           } else if (s < nrows && !moved[s - nm]) {
-            NumaRow nr;
+            NR nr;
             if constexpr (NUMA) nr = pnr[s - nm];
             kv = make_key(eval_row<NM>(pod, slot_row(prow[s - nm]), nr, cls, c), pnode[s - nm]);
           }
@@ -1774,7 +1810,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           // a prefetched list-head row, an M' row, or HBM (rare)
           const int32_t rw = hit ? __builtin_ctzll(hit) : nm;
           const NV *srow = &mrow[rw];
-          const NumaRow *snr = &mnr[rw];
+          const NR *snr = &mnr[rw];
           int32_t from_prev = -1;
           if (!hit) {
             const uint64_t pm0 = __ballot(pn0 == w), pm1 = __ballot(pn1 == w);
@@ -1794,8 +1830,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                 load_row(v, nodes(), w);
                 mrow[rw] = v;
                 if constexpr (NUMA) {
-                  NumaRow nr;
-                  load_numa_row<ZONES>(nr, nodes(), w);
+                  NR nr;
+                  load_side_row<NM>(nr, nodes(), w);
                   mnr[rw] = nr;
                 }
               }
@@ -1810,7 +1846,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               int okl = 0;
               const uint64_t t_acc = dbg ? stamp() : 0;
               if (lane == 0) {
-                NumaRow nr = *snr;
+                NR nr = *snr;
                 okl = numa_reserve<ZONES>(cls, nr, pod, mc);
                 if (okl) mnr[rw] = nr;
               }
@@ -1822,8 +1858,16 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               okr = __builtin_amdgcn_readfirstlane(okl) != 0;
 #pragma unroll
               for (int q = 0; q < NW; q++) cpus[q] = readlane_u64(mc[q], 0);
-            } else if (!hit && lane < (int)(sizeof(NumaRow) / 8)) {
+            } else if (!hit && lane < (int)(sizeof(NR) / 8)) {
               reinterpret_cast<uint64_t *>(&mnr[rw])[lane] = reinterpret_cast<const uint64_t *>(snr)[lane];
+            }
+          }
+          if constexpr (NM == 3) {
+            // Reservation Reserve: assumePod into the node's nominated reservation
+            if (okr && c.resv && pod.resv_match != 0ull && lane == 0) {
+              NR nr = mnr[rw];
+              resv_assume(nr, pod);
+              mnr[rw] = nr;
             }
           }
           if (!okr) {
@@ -1870,8 +1914,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         mrow[lane] = v;
         store_row(v, nodes(), my_node);
         if constexpr (NUMA) {
-          const NumaRow nr = mnr[lane];
-          store_numa_row<ZONES>(nr, nodes(), my_node);
+          const NR nr = mnr[lane];
+          store_side_row<NM>(nr, nodes(), my_node);
         }
       }
       if (lane == 0) __hip_atomic_store(&sh_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // helpers stop
@@ -1959,7 +2003,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             if (kk != 0 && dec_n[x] >= 0) {
               const int32_t src = dec_src[x];
               NV row = src >= 0 ? pre[src] : prow[-src - 1];
-              NumaRow nr;
+              NR nr;
               if constexpr (NUMA) nr = src >= 0 ? prenr[src] : pnr[-src - 1];
               const DevPod pi = lpod[x];
               apply_delta(row, pi, +1);
@@ -1968,7 +2012,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             kpre[l * RES_MAXP_ROUND + x] = (uint16_t)v;
           } else if (x < l + mp) {  // M' slot s
             const int32_t sl = x - l;
-            NumaRow nr;
+            NR nr;
             if constexpr (NUMA) nr = pnr[sl];
             v = eval_row<NM>(pod, slot_row(prow[sl]), nr, cls, c) + 1;
             ktab[l * RES_MAXP_ROUND + sl] = (uint16_t)v;
@@ -1991,7 +2035,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       NV *c2 = pre;
       pre = pre2;
       pre2 = c2;
-      NumaRow *d2 = prenr;
+      NR *d2 = prenr;
       prenr = prenr2;
       prenr2 = d2;
       int32_t *e2 = pre_node;
@@ -2002,7 +2046,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       NV *x = prow;
       prow = mrow;
       mrow = x;
-      NumaRow *y = pnr;
+      NR *y = pnr;
       pnr = mnr;
       mnr = y;
     }
@@ -2042,6 +2086,16 @@ __global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, i
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const DevPod p = *pod;
   *rc = 0;
+  NumaRowR rv{};
+  if (c.resv) {
+    load_resv(rv, d.rv, node);
+    // Unreserve: whether the Reserve went into the node's reservation
+    // (state.assumed, reservation/plugin.go:591-597) is not passed back
+    if (sign < 0 && (rv.rf & KOORDHIP_RESV_PRESENT) && ((p.resv_match >> KOORDHIP_RESV_GROUP(rv.rf)) & 1ull)) {
+      *rc = KOORDHIP_EINVAL;
+      return;
+    }
+  }
   if (numa_on(c) && numa_active(p, c)) {
     NumaRow r;
     load_numa_row(r, d, node);
@@ -2063,6 +2117,10 @@ __global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, i
       for (int w = 0; w < NW; w++) cpus[w] = m[w];
   } else if (sign > 0) {
     for (int w = 0; w < NW; w++) cpus[w] = 0;
+  }
+  if (c.resv && sign > 0) {  // Reservation Reserve: assumePod into the nominated reservation
+    resv_assume(rv, p);
+    store_resv(rv, d.rv, node);
   }
   NV v;
   load_row(v, d, node);
@@ -2092,6 +2150,8 @@ template hipError_t launch_scatter<int64_t>(int64_t *, const int64_t *, const in
 template hipError_t launch_scatter<int32_t>(int32_t *, const int32_t *, const int32_t *, int32_t, hipStream_t);
 template hipError_t launch_scatter<uint8_t>(uint8_t *, const uint8_t *, const int32_t *, int32_t, hipStream_t);
 template hipError_t launch_scatter<ZoneRow>(ZoneRow *, const ZoneRow *, const int32_t *, int32_t, hipStream_t);
+template hipError_t launch_scatter<uint32_t>(uint32_t *, const uint32_t *, const int32_t *, int32_t, hipStream_t);
+template hipError_t launch_scatter<double>(double *, const double *, const int32_t *, int32_t, hipStream_t);
 
 hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t *rows, int32_t m, hipStream_t s) {
   if (m <= 0) return hipSuccess;
@@ -2112,7 +2172,8 @@ int32_t scan_chunks(int R, int32_t lo, int32_t hi) { return hi > lo ? (hi - lo +
 hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t lo,
                        int32_t hi, uint16_t *S, int64_t s_stride, uint16_t *Mx, int32_t m_stride, hipStream_t s) {
   if (n_pods <= 0 || hi <= lo) return hipSuccess;
-  const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
+  const int nm = side_mode(c);
+  const bool numa = nm != 0;
   const int32_t nchunks = scan_chunks(R, lo, hi);
   const int32_t cpx = (nchunks + 7) / 8;
   const int32_t blocks = 8 * cpx * ((n_pods + 3) / 4);
@@ -2120,7 +2181,14 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
 #define KH_SCAN(RR, NN)                                                                                            \
   hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, S, \
                      s_stride, Mx, m_stride)
-  if (numa && c.zones) {
+  if (nm == 3) {
+    switch (R) {
+      case 1: KH_SCAN(1, 3); break;
+      case 2: KH_SCAN(2, 3); break;
+      case 4: KH_SCAN(4, 3); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (nm == 2) {
     switch (R) {
       case 1: KH_SCAN(1, 2); break;
       case 2: KH_SCAN(2, 2); break;
@@ -2212,9 +2280,19 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
 // LDS list stride: k rounded up to 8 entries (zero padded)
 static inline int32_t list_stride(int32_t k) { return (k + 7) & ~7; }
 
-int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, bool numa, int32_t lag) {
+int side_mode(const DevCfg &c) {
+  if (c.resv) return 3;
+  if (!((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA)) return 0;
+  return c.zones ? 2 : 1;
+}
+
+static int32_t side_row_bytes(int nm) {
+  return nm == 3 ? (int32_t)sizeof(NumaRowR) : (nm ? (int32_t)sizeof(NumaRow) : 0);
+}
+
+int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, int nm, int32_t lag) {
   const int32_t kp = list_stride(k);
-  return res_lds(n_pods_max, kp, n_nodes, numa, false, false, lag).total;
+  return res_lds(n_pods_max, kp, n_nodes, side_row_bytes(nm), false, false, lag).total;
 }
 
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
@@ -2227,20 +2305,22 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   if (lag < 1 || lag > 2 || lag * P > RES_MAXP_ROUND || (lag > 1 && (k < 3 * P || r_begin != 0)))
     return hipErrorInvalidValue;
   const int32_t kp = list_stride(k);
-  const bool numa = ((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) != 0;
+  const int nm = side_mode(c);
+  const int32_t nrow = side_row_bytes(nm);
   // a persistent launch preloads round r+1 during round r when both copies fit
   // the largest layout that fits: key tables and the next round's preload,
   // then without the preload, then without the tables
   const bool pre = r_end - r_begin > 1 && !std::getenv("KOORDHIP_NO_PRELOAD");
   const bool tab = !std::getenv("KOORDHIP_NO_KEY_TABLES");
-  ResLds o = res_lds(P, kp, d.n, numa, pre, tab, lag);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, tab, lag);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, pre, false, lag);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, numa, false, false, lag);
-  const int nm = numa ? (c.zones ? 2 : 1) : 0;
-  static bool attr[3] = {false, false, false};
+  ResLds o = res_lds(P, kp, d.n, nrow, pre, tab, lag);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag);
+  static bool attr[4] = {false, false, false, false};
   if (!attr[nm]) {
-    const void *f = nm == 2 ? (const void *)k_resolve<2> : (nm == 1 ? (const void *)k_resolve<1> : (const void *)k_resolve<0>);
+    const void *f = nm == 3 ? (const void *)k_resolve<3>
+                    : nm == 2 ? (const void *)k_resolve<2>
+                              : (nm == 1 ? (const void *)k_resolve<1> : (const void *)k_resolve<0>);
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS_MAX);
     if (e != hipSuccess) return e;
     attr[nm] = true;
@@ -2249,7 +2329,9 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
 #define KH_RESOLVE(NN)                                                                                                \
   hipLaunchKernelGGL(k_resolve<NN>, dim3(1), dim3(res_threads<NN>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, \
                      k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, lag, sync, o, out_node, out_cpus, dbg, trace)
-  if (nm == 2)
+  if (nm == 3)
+    KH_RESOLVE(3);
+  else if (nm == 2)
     KH_RESOLVE(2);
   else if (nm == 1)
     KH_RESOLVE(1);

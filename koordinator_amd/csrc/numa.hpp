@@ -90,6 +90,16 @@ struct DevNuma {
   int32_t ncls;      // topology classes at cls
 };
 
+// Reservation columns on device (f64 hold the int64 values exactly), see resv.hpp.
+struct DevResv {
+  const uint32_t *flags;  // NULL: no reservation columns
+  const int32_t *rank;
+  const double *ra[2];    // Allocatable cpu milli, memory
+  const double *rz[2];    // the reserve pod's non-zero cpu / memory request
+  double *rd[2];          // Allocated
+  int32_t *rn;            // len(AssignedPods)
+};
+
 struct ZoneRow {  // one node's [2][ZMAX] zone row (update_nodes scatter element)
   double v[2 * ZMAX];
 };

@@ -20,7 +20,7 @@ struct DevPod {
   int32_t numa_cpus;
   uint32_t numa_policy;
   int32_t reserved0;
-  int64_t reserved1;
+  uint64_t resv_match;
 };
 static_assert(sizeof(DevPod) == 96, "DevPod is 96 bytes");
 

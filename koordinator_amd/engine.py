@@ -133,6 +133,14 @@ class PlacementEngine:
         abi.check(self.lib, self.lib.koordhip_read_numa_zones(self._ctx, abi.ptr(zu, C.c_int64)))
         return {"free": fr, "excl_pcpu": ep, "excl_numa": en, "alloc_cnt": cnt, "zone_used": zu}
 
+    def read_reservations(self) -> dict:
+        """Reservation mutable state: Allocated [2][n] (cpu milli, memory), len(AssignedPods) [n]."""
+        n = self.n
+        al = np.zeros((2, n), np.int64)
+        asg = np.zeros(n, np.int32)
+        abi.check(self.lib, self.lib.koordhip_read_reservations(self._ctx, abi.ptr(al, C.c_int64), abi.ptr(asg, C.c_int32)))
+        return {"allocated": al, "assigned": asg}
+
     def fetch_cpusets(self, n: int) -> np.ndarray:
         out = np.zeros((n, abi.NUMA_WORDS), np.uint64)
         abi.check(self.lib, self.lib.koordhip_fetch_cpusets(self._ctx, abi.ptr(out, C.c_uint64), n))

@@ -137,6 +137,16 @@ class Container:
 
 
 @dataclass
+class OwnerReference:
+    """metav1.OwnerReference of a pod (reservation owner matching)."""
+    kind: str = ""
+    name: str = ""
+    uid: str = ""
+    api_version: str = ""
+    controller: Optional[bool] = None
+
+
+@dataclass
 class Pod:
     namespace: str = "default"
     name: str = "pod"
@@ -151,6 +161,8 @@ class Pod:
     node_name: str = ""
     qos_status: str = ""          # Status.QOSClass
     phase: str = "Running"
+    owner_refs: List[OwnerReference] = field(default_factory=list)
+    api_version: str = "v1"
 
     @property
     def key(self) -> str:

@@ -153,8 +153,10 @@ def nonzero_request(pod: k8s.Pod) -> Tuple[int, int]:
     return cpu, mem
 
 
-def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None) -> np.ndarray:
-    """One koordhip_pod record for `pod` (the per-pod PreFilter products)."""
+def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None, resv_index=None) -> np.ndarray:
+    """One koordhip_pod record for `pod` (the per-pod PreFilter products);
+    `resv_index` (reservation.ReservationIndex): the snapshot's reservation
+    owner groups the pod is matched against."""
     p = profile.resolved()
     rec = out if out is not None else pod_array(1)[0]
     req, present = fit_request(pod)
@@ -183,17 +185,20 @@ def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None)
                                               p.numa.default_cpu_bind_policy)
     except numa.PreFilterError:
         nf, ncpus, pol = abi.POD_NUMA_ERROR, 0, 0
+    from . import reservation as rv
+    flags |= rv.pod_keys(pod)
     rec["flags"] = flags | nf
     rec["numa_cpus"] = ncpus
     rec["numa_policy"] = pol
+    rec["resv_match"] = resv_index.pod_mask(pod) if resv_index is not None else 0
     return rec
 
 
-def pod_records(pods: Iterable[k8s.Pod], profile: Profile) -> np.ndarray:
+def pod_records(pods: Iterable[k8s.Pod], profile: Profile, resv_index=None) -> np.ndarray:
     pods = list(pods)
     arr = pod_array(len(pods))
     for i, p in enumerate(pods):
-        pod_record(p, profile, arr[i])
+        pod_record(p, profile, arr[i], resv_index)
     return arr
 
 

@@ -1,0 +1,314 @@
+"""Host side of the Reservation plugin: the Reservation object model, owner
+matching and the per-node reservation columns of koordhip_node_soa.
+
+Restated from the reference:
+  * ReservationInfo           pkg/scheduler/frameworkext/reservation_info.go:36-126
+    (Allocatable = ReservationRequests, ResourceNames = its keys, Allocated
+    masked to them, AssignedPods)
+  * IsAvailable / ReservationRequests   pkg/util/reservation/reservation.go:213-215, 334-345
+  * owner matchers            reservation.go:357-442 (ObjectReference, controller
+    reference, label selector; DNF over the owners list)
+  * IsAllocateOnce            apis/extension/reservation.go:98-100 (default true)
+  * IsUnschedulable           reservation_info.go:248-255
+  * reservation order label   reservation/scoring.go:156-175 (strconv.ParseInt, 0 = none)
+  * reserve pod non-zero request: calculateResource, reservation/transformer.go:302-333
+
+The device evaluates owner matching as bit tests: every distinct owner spec
+of the snapshot's reservations is an owner group g (<= 64), a reservation
+carries its group, a pod carries the bit mask of the groups it matches.
+Pods with a reservation affinity (reservation.go:449-487) and reserve pods
+are not streamed by this engine (MarshalError).
+"""
+from __future__ import annotations
+
+import json
+import re
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi, k8s
+from .snapshot import NodeTable
+
+LABEL_RESERVATION_ORDER = "scheduling.koordinator.sh/reservation-order"   # apis/extension/reservation.go
+ANNOTATION_RESERVATION_AFFINITY = "scheduling.koordinator.sh/reservation-affinity"
+ANNOTATION_RESERVE_POD = "scheduling.koordinator.sh/reserve-pod"
+
+POLICY_DEFAULT, POLICY_ALIGNED, POLICY_RESTRICTED = "", "Aligned", "Restricted"
+_POLICY_CODE = {POLICY_DEFAULT: abi.RESV_POLICY_DEFAULT, POLICY_ALIGNED: abi.RESV_POLICY_ALIGNED,
+                POLICY_RESTRICTED: abi.RESV_POLICY_RESTRICTED}
+
+
+class ReservationError(ValueError):
+    pass
+
+
+OwnerReference = k8s.OwnerReference
+
+
+@dataclass
+class LabelSelectorRequirement:
+    key: str
+    operator: str                 # In, NotIn, Exists, DoesNotExist
+    values: List[str] = field(default_factory=list)
+
+
+@dataclass
+class LabelSelector:
+    match_labels: Dict[str, str] = field(default_factory=dict)
+    match_expressions: List[LabelSelectorRequirement] = field(default_factory=list)
+
+    def validate(self):
+        """metav1.LabelSelectorAsSelector's validation (the owner's ParseError)."""
+        for r in self.match_expressions:
+            if r.operator in ("In", "NotIn"):
+                if not r.values:
+                    raise ReservationError(f"values must be non-empty for operator {r.operator}")
+            elif r.operator in ("Exists", "DoesNotExist"):
+                if r.values:
+                    raise ReservationError(f"values must be empty for operator {r.operator}")
+            else:
+                raise ReservationError(f"{r.operator!r} is not a valid label selector operator")
+
+    def matches(self, labels: Dict[str, str]) -> bool:
+        for k, v in self.match_labels.items():
+            if labels.get(k) != v:
+                return False
+        for r in self.match_expressions:
+            has = r.key in labels
+            if r.operator == "In" and not (has and labels[r.key] in r.values):
+                return False
+            if r.operator == "NotIn" and has and labels[r.key] in r.values:
+                return False
+            if r.operator == "Exists" and not has:
+                return False
+            if r.operator == "DoesNotExist" and has:
+                return False
+        return True
+
+
+@dataclass
+class ObjectRef:
+    """corev1.ObjectReference of ReservationOwner.Object."""
+    uid: str = ""
+    name: str = ""
+    namespace: str = ""
+    api_version: str = ""
+
+
+@dataclass
+class ControllerRef:
+    """ReservationControllerReference."""
+    kind: str = ""
+    name: str = ""
+    uid: str = ""
+    api_version: str = ""
+    namespace: str = ""
+    controller: Optional[bool] = None
+
+
+@dataclass
+class ReservationOwner:
+    object: Optional[ObjectRef] = None
+    controller: Optional[ControllerRef] = None
+    label_selector: Optional[LabelSelector] = None
+
+    def key(self) -> str:
+        """Canonical form (owner groups are distinct owner lists)."""
+        def enc(x):
+            if x is None:
+                return None
+            if isinstance(x, LabelSelector):
+                return {"l": sorted(x.match_labels.items()),
+                        "e": [(r.key, r.operator, sorted(r.values)) for r in x.match_expressions]}
+            return sorted(vars(x).items())
+        return json.dumps([enc(self.object), enc(self.controller), enc(self.label_selector)], sort_keys=True)
+
+
+def match_object_ref(pod: k8s.Pod, ref: Optional[ObjectRef]) -> bool:
+    """MatchObjectRef, reservation.go:412-420."""
+    if ref is None:
+        return True
+    return ((not ref.uid or pod.uid == ref.uid) and (not ref.name or pod.name == ref.name)
+            and (not ref.namespace or pod.namespace == ref.namespace)
+            and (not ref.api_version or pod.api_version == ref.api_version))
+
+
+def match_controller_ref(pod: k8s.Pod, ref: Optional[ControllerRef]) -> bool:
+    """MatchReservationControllerReference, reservation.go:422-442."""
+    if ref is None:
+        return True
+    if ref.namespace and ref.namespace != pod.namespace:
+        return False
+    for o in pod.owner_refs:
+        if ((ref.controller is None or (o.controller is not None and ref.controller == o.controller))
+                and (not ref.uid or ref.uid == o.uid) and (not ref.name or ref.name == o.name)
+                and (not ref.kind or ref.kind == o.kind) and (not ref.api_version or ref.api_version == o.api_version)):
+            return True
+    return False
+
+
+def match_owners(pod: k8s.Pod, owners: Sequence[ReservationOwner]) -> bool:
+    """MatchReservationOwners (reservation.go:389-410): owners == [] matches nothing."""
+    for m in owners:
+        if (match_object_ref(pod, m.object) and match_controller_ref(pod, m.controller)
+                and (m.label_selector is None or m.label_selector.matches(pod.labels))):
+            return True
+    return False
+
+
+@dataclass
+class Reservation:
+    """A scheduling.koordinator.sh/v1alpha1 Reservation as the scheduler cache holds it."""
+    name: str
+    node_name: str = ""                      # Status.NodeName
+    phase: str = "Available"
+    uid: str = ""
+    labels: Dict[str, str] = field(default_factory=dict)
+    owners: List[ReservationOwner] = field(default_factory=list)
+    allocatable: k8s.ResourceList = field(default_factory=dict)   # Status.Allocatable (Available)
+    template: List[k8s.Container] = field(default_factory=list)    # Spec.Template containers (the reserve pod)
+    allocated: k8s.ResourceList = field(default_factory=dict)      # ReservationInfo.Allocated
+    assigned: int = 0                                              # len(AssignedPods)
+    allocate_once: Optional[bool] = None                           # Spec.AllocateOnce (nil -> true)
+    allocate_policy: str = POLICY_DEFAULT
+    unschedulable: bool = False
+    deleting: bool = False                                         # DeletionTimestamp set
+
+    def is_available(self) -> bool:
+        return bool(self.node_name) and self.phase == "Available"
+
+    def reserve_pod(self) -> k8s.Pod:
+        return k8s.Pod(name=f"reserve-{self.name}", containers=list(self.template) or
+                       [k8s.Container(requests=dict(self.allocatable))])
+
+
+def parse_order(labels: Dict[str, str]) -> int:
+    """findMostPreferredReservationByOrder's label parse (scoring.go:160-167): 0 = unordered."""
+    s = labels.get(LABEL_RESERVATION_ORDER, "")
+    if not re.fullmatch(r"[+-]?[0-9]+", s):
+        return 0
+    v = int(s)
+    if not (-(1 << 63) <= v < (1 << 63)):
+        return 0                              # ParseInt range error
+    return v
+
+
+@dataclass
+class ReservationIndex:
+    """Owner groups of a snapshot's reservations (pods are matched against them)."""
+    groups: List[List[ReservationOwner]] = field(default_factory=list)
+    group_of: Dict[str, int] = field(default_factory=dict)
+
+    def group(self, owners: List[ReservationOwner]) -> int:
+        key = json.dumps([o.key() for o in owners])
+        g = self.group_of.get(key)
+        if g is None:
+            if len(self.groups) >= abi.RESV_MAX_GROUPS:
+                raise ReservationError(f"more than {abi.RESV_MAX_GROUPS} distinct reservation owner specs")
+            g = len(self.groups)
+            self.groups.append(list(owners))
+            self.group_of[key] = g
+        return g
+
+    def pod_mask(self, pod: k8s.Pod) -> int:
+        """koordhip_pod.resv_match: bit g set iff the pod matches owner group g."""
+        if (pod.annotations or {}).get(ANNOTATION_RESERVE_POD) == "true":
+            raise ReservationError("reserve pods are not scheduled by this engine")
+        aff = (pod.annotations or {}).get(ANNOTATION_RESERVATION_AFFINITY, "")
+        if aff:
+            try:
+                a = json.loads(aff)
+            except ValueError as e:
+                raise ReservationError(f"reservation affinity: {e}") from e
+            if a.get("reservationSelector") or a.get("requiredDuringSchedulingIgnoredDuringExecution"):
+                raise ReservationError("pods with a reservation affinity are not supported by this engine")
+        m = 0
+        for g, owners in enumerate(self.groups):
+            if match_owners(pod, owners):
+                m |= 1 << g
+        return m
+
+
+def _q2(rl: k8s.ResourceList, name: str) -> int:
+    q = rl.get(name)
+    if q is None:
+        return 0
+    return q.milli_value() if name == k8s.CPU else q.value()
+
+
+def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservations: Sequence[Reservation],
+                        index: Optional[ReservationIndex] = None) -> ReservationIndex:
+    """Fill the resv_* columns of `table` (the reservation cache's view,
+    cache.go:236-252) and return the owner groups for the pod masks."""
+    from .marshal import nonzero_request, fit_request
+
+    index = index or ReservationIndex()
+    for c in ("resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1",
+              "resv_allocated0", "resv_allocated1", "resv_assigned"):
+        table[c][:] = 0
+    placed: List[Tuple[int, Reservation]] = []
+    for r in reservations:
+        if not r.is_available() or r.node_name not in node_index:
+            continue
+        i = node_index[r.node_name]
+        if any(j == i for j, _ in placed):
+            raise ReservationError(f"node {r.node_name}: more than one Available reservation (unsupported)")
+        placed.append((i, r))
+    orders = sorted({parse_order(r.labels) for _, r in placed} - {0})
+    if len(orders) > abi.RESV_MAX_ORDERS:
+        raise ReservationError(f"more than {abi.RESV_MAX_ORDERS} distinct reservation orders")
+    rank = {v: k for k, v in enumerate(orders)}
+    for i, r in placed:
+        names = set(r.allocatable)
+        extra = names - {k8s.CPU, k8s.MEMORY}
+        if extra:
+            raise ReservationError(f"reservation {r.name}: resources {sorted(extra)} are not supported")
+        parse_ok = True
+        try:
+            for o in r.owners:
+                if o.label_selector is not None:
+                    o.label_selector.validate()
+        except ReservationError:
+            parse_ok = False                                  # ReservationInfo.ParseError
+        pod = r.reserve_pod()
+        req, present = fit_request(pod)
+        if present - {k8s.CPU, k8s.MEMORY} or any(req[k] for k in range(abi.NRES) if k not in (abi.RES_CPU, abi.RES_MEM)):
+            raise ReservationError(f"reservation {r.name}: the reserve pod requests resources other than cpu/memory")
+        if req[abi.RES_CPU] != _q2(r.allocatable, k8s.CPU) or req[abi.RES_MEM] != _q2(r.allocatable, k8s.MEMORY):
+            raise ReservationError(f"reservation {r.name}: allocatable differs from the reserve pod's requests")
+        f = abi.RESV_PRESENT if parse_ok else 0
+        if r.allocate_once is None or r.allocate_once:
+            f |= abi.RESV_ALLOCATE_ONCE
+        if r.unschedulable or r.deleting:
+            f |= abi.RESV_UNSCHEDULABLE
+        order = parse_order(r.labels)
+        if order != 0:
+            f |= abi.RESV_ORDERED
+            table["resv_order_rank"][i] = rank[order]
+        if k8s.CPU in names:
+            f |= abi.RESV_KEY_CPU
+        if k8s.MEMORY in names:
+            f |= abi.RESV_KEY_MEM
+        if r.allocate_policy not in _POLICY_CODE:
+            raise ReservationError(f"reservation {r.name}: unknown allocate policy {r.allocate_policy!r}")
+        f |= _POLICY_CODE[r.allocate_policy] << abi.RESV_POLICY_SHIFT
+        f |= index.group(r.owners) << abi.RESV_GROUP_SHIFT
+        table["resv_flags"][i] = f
+        table["resv_alloc0"][i] = _q2(r.allocatable, k8s.CPU)
+        table["resv_alloc1"][i] = _q2(r.allocatable, k8s.MEMORY)
+        nzc, nzm = nonzero_request(pod)
+        table["resv_nz0"][i] = nzc
+        table["resv_nz1"][i] = nzm
+        # Allocated masked to ResourceNames (reservation_info.go:286, 303)
+        table["resv_allocated0"][i] = _q2(r.allocated, k8s.CPU) if k8s.CPU in names else 0
+        table["resv_allocated1"][i] = _q2(r.allocated, k8s.MEMORY) if k8s.MEMORY in names else 0
+        table["resv_assigned"][i] = r.assigned
+    return index
+
+
+def pod_keys(pod: k8s.Pod) -> int:
+    """KOORDHIP_POD_KEY_* bits: the cpu / memory keys of PodRequestsAndLimits."""
+    reqs, _ = k8s.pod_requests_and_limits(pod)
+    return (abi.POD_KEY_CPU if k8s.CPU in reqs else 0) | (abi.POD_KEY_MEM if k8s.MEMORY in reqs else 0)

@@ -18,18 +18,24 @@ I64_COLS = (
     + ["nz_cpu_m", "nz_mem", "la_alloc_cpu_m", "la_alloc_mem", "la_used_cpu_m", "la_used_mem",
        "la_used_prod_cpu_m", "la_used_prod_mem",
        "laf_used_m0", "laf_used_m1", "laf_total_m0", "laf_total_m1", "laf_prod_used_m0", "laf_prod_used_m1",
-       "laf_thr0", "laf_thr1", "laf_prod_thr0", "laf_prod_thr1"]
+       "laf_thr0", "laf_thr1", "laf_prod_thr0", "laf_prod_thr1",
+       "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1", "resv_allocated0", "resv_allocated1"]
 )
-I32_COLS = ["alloc_pods", "npods", "numa_class", "numa_alloc_cnt"]
+I32_COLS = ["alloc_pods", "npods", "numa_class", "numa_alloc_cnt", "resv_order_rank", "resv_assigned"]
 U8_COLS = ["la_flags", "numa_flags"]
+U32_COLS = ["resv_flags"]   # KOORDHIP_RESV_* (0 = no reservation on the node)
 U64_COLS = ([f"numa_free{w}" for w in range(abi.NUMA_WORDS)] + [f"numa_excl_pcpu{w}" for w in range(abi.NUMA_WORDS)]
             + [f"numa_excl_numa{w}" for w in range(abi.NUMA_WORDS)])
 # NUMA zone resources, [n][2][NUMA_MAX_NODES] int64 per column (cpu milli, memory bytes)
 ZONE_COLS = ["numa_zone_alloc", "numa_zone_used"]
 F64_COLS = ["numa_amp_cpu"]   # CPU amplification ratio (1.0 = none)
-ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS + ZONE_COLS + F64_COLS
+ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS + ZONE_COLS + F64_COLS + U32_COLS
 # NodeNUMAResource mutable columns (advanced by cpuset / NUMA-zone Reserves)
 NUMA_MUTABLE = [c for c in U64_COLS] + ["numa_alloc_cnt", "numa_zone_used"]
+# Reservation columns (the node's Available reservation) and the mutable ones
+RESV_COLS = ["resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1",
+             "resv_allocated0", "resv_allocated1", "resv_assigned"]
+RESV_MUTABLE = ["resv_allocated0", "resv_allocated1", "resv_assigned"]
 
 
 def _shape(col: str, n: int):
@@ -43,6 +49,8 @@ def _dtype(col: str):
         return np.uint8
     if col in U64_COLS:
         return np.uint64
+    if col in U32_COLS:
+        return np.uint32
     if col in F64_COLS:
         return np.float64
     return np.int64
@@ -124,6 +132,13 @@ class NodeTable:
         s.numa_zone_alloc = p64("numa_zone_alloc")
         s.numa_zone_used = p64("numa_zone_used")
         s.numa_amp_cpu = self.cols["numa_amp_cpu"].ctypes.data_as(C.POINTER(C.c_double))
+        s.resv_flags = self.cols["resv_flags"].ctypes.data_as(C.POINTER(C.c_uint32))
+        s.resv_order_rank = p32("resv_order_rank")
+        for k in range(2):
+            s.resv_alloc[k] = p64(f"resv_alloc{k}")
+            s.resv_nz[k] = p64(f"resv_nz{k}")
+            s.resv_allocated[k] = p64(f"resv_allocated{k}")
+        s.resv_assigned = p32("resv_assigned")
         return s
 
     def nbytes(self) -> int:

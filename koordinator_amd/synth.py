@@ -211,12 +211,78 @@ def add_numa(t: NodeTable, spec: NumaSpec, profile: Profile, seed: int = SEED) -
     return t
 
 
+# ------------------------------------------------------------------ Reservation (config 5)
+RESV_CPU = [4000, 8000, 16000]
+RESV_MEM = [8 * GI, 16 * GI, 32 * GI]
+
+
+@dataclass
+class ResvSpec:
+    node_frac: float = 0.10          # nodes holding an Available reservation (one each)
+    groups: int = 8                  # distinct owner specs (e.g. one label selector per workload)
+    allocate_once_frac: float = 0.5  # Spec.AllocateOnce (else reusable until full)
+    aligned_frac: float = 0.15
+    restricted_frac: float = 0.15
+    unschedulable_frac: float = 0.02
+    ordered_frac: float = 0.05       # reservation-order label, values 1..100
+    cpu_only_frac: float = 0.05      # ResourceNames = {cpu}
+    assigned_frac: float = 0.3       # already holding 1-3 pods
+
+
+def add_reservations(t: NodeTable, spec: ResvSpec, seed: int = SEED) -> NodeTable:
+    """resv_* columns (the layout reservation.reservation_columns builds from
+    objects) plus the reserve pods' and assigned pods' share of each node's
+    Requested / NonZeroRequested / pod count."""
+    n, s = t.n, seed + 11
+    has = uniform(s, n, 60) < spec.node_frac
+    g = (splitmix64(s, n, 61) % np.uint64(max(1, spec.groups))).astype(np.int64)
+    rc = choice(s, n, 62, RESV_CPU).astype(np.int64)
+    cpu_only = uniform(s, n, 63) < spec.cpu_only_frac
+    rm = np.where(cpu_only, 0, choice(s, n, 64, RESV_MEM).astype(np.int64))
+    once = uniform(s, n, 65) < spec.allocate_once_frac
+    up = uniform(s, n, 66)
+    pol = np.where(up < spec.aligned_frac, abi.RESV_POLICY_ALIGNED,
+                   np.where(up < spec.aligned_frac + spec.restricted_frac, abi.RESV_POLICY_RESTRICTED,
+                            abi.RESV_POLICY_DEFAULT))
+    unsched = uniform(s, n, 67) < spec.unschedulable_frac
+    ordered = uniform(s, n, 68) < spec.ordered_frac
+    order = (splitmix64(s, n, 69) % np.uint64(100)).astype(np.int64) + 1
+    assigned = np.where(uniform(s, n, 70) < spec.assigned_frac,
+                        (splitmix64(s, n, 71) % np.uint64(3)).astype(np.int64) + 1, 0)
+    fa = uniform(s, n, 72)
+    dc = np.where(assigned > 0, np.floor(rc * fa).astype(np.int64) // 100 * 100, 0)
+    dm = np.where(assigned > 0, np.floor(rm * fa).astype(np.int64) // MI * MI, 0)
+    f = (abi.RESV_PRESENT | abi.RESV_KEY_CPU | np.where(cpu_only, 0, abi.RESV_KEY_MEM)
+         | np.where(once, abi.RESV_ALLOCATE_ONCE, 0) | np.where(unsched, abi.RESV_UNSCHEDULABLE, 0)
+         | np.where(ordered, abi.RESV_ORDERED, 0) | (pol << abi.RESV_POLICY_SHIFT) | (g << abi.RESV_GROUP_SHIFT))
+    t["resv_flags"][:] = np.where(has, f, 0).astype(np.uint32)
+    vals = np.unique(order[has & ordered])
+    t["resv_order_rank"][:] = np.where(has & ordered, np.searchsorted(vals, order), 0).astype(np.int32)
+    t["resv_alloc0"][:] = np.where(has, rc, 0)
+    t["resv_alloc1"][:] = np.where(has, rm, 0)
+    nzm = np.where(cpu_only, 200 * MI, rm)         # the reserve pod lists no memory: GetNonzeroRequests default
+    t["resv_nz0"][:] = np.where(has, rc, 0)
+    t["resv_nz1"][:] = np.where(has, nzm, 0)
+    t["resv_allocated0"][:] = np.where(has, dc, 0)
+    t["resv_allocated1"][:] = np.where(has, dm, 0)
+    t["resv_assigned"][:] = np.where(has, assigned, 0).astype(np.int32)
+    # the reserve pod and the pods it holds are NodeInfo pods
+    t["requested0"][:] += np.where(has, rc + dc, 0)
+    t["requested1"][:] += np.where(has, rm + dm, 0)
+    t["nz_cpu_m"][:] += np.where(has, rc + dc, 0)
+    t["nz_mem"][:] += np.where(has, nzm + dm, 0)
+    t["npods"][:] += np.where(has, 1 + assigned, 0).astype(np.int32)
+    return t
+
+
 @dataclass
 class StreamSpec:
     n_pods: int
     be_frac: float = 0.0
     seed: int = SEED
     cpuset_frac: float = 0.0   # share of LS pods that are LSR/LSE cpuset pods (NodeNUMAResource)
+    resv_match_frac: float = 0.0  # pods matching one reservation owner group (Reservation)
+    resv_groups: int = 8
 
 
 LS_CPU = [250, 500, 1000, 2000, 4000]
@@ -263,9 +329,13 @@ def make_pods(spec: StreamSpec, profile: Profile) -> np.ndarray:
     pods["est_cpu"] = np.where(be, be_est_cpu, ls_est_cpu)
     pods["est_mem"] = np.where(be, be_est_mem, ls_est_mem)
     pods["flags"] = np.where(be, abi.POD_HAS_REQ | abi.POD_REQ_BCPU | abi.POD_REQ_BMEM,
-                             abi.POD_PROD | abi.POD_HAS_REQ).astype(np.uint32)
+                             abi.POD_PROD | abi.POD_HAS_REQ | abi.POD_KEY_CPU | abi.POD_KEY_MEM).astype(np.uint32)
     if spec.cpuset_frac > 0:
         _make_cpuset_pods(pods, be, spec, fc, fm)
+    if spec.resv_match_frac > 0:
+        m = uniform(s, n, 50) < spec.resv_match_frac
+        g = (splitmix64(s, n, 51) % np.uint64(max(1, spec.resv_groups))).astype(np.uint64)
+        pods["resv_match"] = np.where(m, np.uint64(1) << g, np.uint64(0))
     return pods
 
 
@@ -333,7 +403,7 @@ CONFIGS = {
     2: dict(nodes=5000, pods=10000, be_frac=0.0),
     3: dict(nodes=5000, pods=10000, be_frac=0.2, cpuset_frac=0.5, numa=True),
     4: dict(nodes=50000, pods=100000, be_frac=0.3),
-    5: dict(nodes=200000, pods=100000, be_frac=0.3),
+    5: dict(nodes=200000, pods=100000, be_frac=0.3, numa=True, reservation=True, resv_match_frac=0.2),
 }
 
 
@@ -342,6 +412,8 @@ def config_workload(cfg_id: int, profile: Profile, n_nodes: int = None, n_pods: 
     table = make_cluster(ClusterSpec(n_nodes or c["nodes"]), profile)
     if c.get("numa"):
         add_numa(table, NumaSpec(), profile)
-    pods = make_pods(StreamSpec(n_pods or c["pods"], be_frac=c["be_frac"], cpuset_frac=c.get("cpuset_frac", 0.0)),
-                     profile)
+    if c.get("reservation"):
+        add_reservations(table, ResvSpec())
+    pods = make_pods(StreamSpec(n_pods or c["pods"], be_frac=c["be_frac"], cpuset_frac=c.get("cpuset_frac", 0.0),
+                                resv_match_frac=c.get("resv_match_frac", 0.0)), profile)
     return table, pods

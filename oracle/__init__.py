@@ -39,6 +39,8 @@ class OrcState(C.Structure):
         ("numa_alloc_cnt", C.POINTER(C.c_int32)),
         ("numa_zone_used", C.POINTER(C.c_int64)),
         ("cpuset_out", C.c_void_p),
+        ("resv_allocated", C.POINTER(C.c_int64) * 2),
+        ("resv_assigned", C.POINTER(C.c_int32)),
     ]
 
 
@@ -78,6 +80,15 @@ def lib():
         L.orc_tm_merge.restype = C.c_int
         L.orc_numa_hint_alloc.argtypes = [C.POINTER(OrcState), vp, C.c_int32, vp, vp, vp, vp]
         L.orc_numa_hint_alloc.restype = C.c_int
+        L.orc_resv_restore.argtypes = [C.POINTER(OrcState), vp, C.c_int]
+        L.orc_resv_filter.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
+        L.orc_resv_filter.restype = C.c_int
+        L.orc_resv_nominated.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
+        L.orc_resv_nominated.restype = C.c_int
+        L.orc_resv_score.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
+        L.orc_resv_score.restype = C.c_int64
+        L.orc_resv_normalized.argtypes = [C.POINTER(OrcState), vp, vp, C.c_int32, vp]
+        L.orc_resv_restore_delta.argtypes = [C.POINTER(OrcState), vp, C.c_int32, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -159,6 +170,44 @@ class Oracle:
             "alloc_cnt": a(self.st.numa_alloc_cnt),
             "zone_used": a(self.st.numa_zone_used, (n, 2, abi.NUMA_MAX_NODES)),
         }
+
+    def resv_state(self) -> dict:
+        n = self.n
+        a = lambda p: np.ctypeslib.as_array(p, shape=(n,)).copy()
+        return {"allocated": np.stack([a(self.st.resv_allocated[0]), a(self.st.resv_allocated[1])]),
+                "assigned": a(self.st.resv_assigned)}
+
+    def resv_restore_delta(self, pod: np.ndarray, node: int):
+        """(requested delta [cpu, mem], non-zero delta [cpu, mem], pod-count delta) of the restore."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        dr, dn, dp = np.zeros(2, np.int64), np.zeros(2, np.int64), np.zeros(1, np.int32)
+        lib().orc_resv_restore_delta(C.byref(self.st), pod.ctypes.data, node, dr.ctypes.data, dn.ctypes.data,
+                                     dp.ctypes.data)
+        return dr, dn, int(dp[0])
+
+    def resv_filter(self, pod: np.ndarray, node: int) -> bool:
+        """filterWithReservations of (pod, node) inside the pod's cycle (restore applied)."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        lib().orc_resv_restore(C.byref(self.st), pod.ctypes.data, 1)
+        ok = lib().orc_resv_filter(C.byref(self.st), pod.ctypes.data, node)
+        lib().orc_resv_restore(C.byref(self.st), pod.ctypes.data, -1)
+        return bool(ok)
+
+    def resv_nominated(self, pod: np.ndarray, node: int) -> bool:
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        return bool(lib().orc_resv_nominated(C.byref(self.st), pod.ctypes.data, node))
+
+    def resv_score(self, pod: np.ndarray, node: int) -> int:
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        return int(lib().orc_resv_score(C.byref(self.st), pod.ctypes.data, node))
+
+    def resv_normalized(self, pod: np.ndarray, feasible) -> np.ndarray:
+        """PreScore + Score + DefaultNormalizeScore of the Reservation plugin over `feasible`."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        f = np.ascontiguousarray(feasible, np.int32)
+        out = np.zeros(len(f), np.int64)
+        lib().orc_resv_normalized(C.byref(self.st), pod.ctypes.data, f.ctypes.data, len(f), out.ctypes.data)
+        return out
 
     def hint_alloc(self, pod: np.ndarray, node: int):
         """The topology-manager admit + allocateResourcesByHint for (pod, node):

@@ -129,7 +129,12 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
   st->numa_zone_used = (int64_t *)calloc(zn, sizeof(int64_t));
   if (soa->numa_zone_used && st->numa_zone_used)
     memcpy(st->numa_zone_used, soa->numa_zone_used, sizeof(int64_t) * (size_t)n * 2 * KOORDHIP_NUMA_MAX_NODES);
-  if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used) return -1;
+  for (int r = 0; r < 2; r++)
+    st->resv_allocated[r] = dup64(soa->resv_flags && soa->resv_allocated[r] ? soa->resv_allocated[r] : NULL, n);
+  st->resv_assigned = (int32_t *)calloc((size_t)(n > 0 ? n : 1), sizeof(int32_t));
+  if (soa->resv_flags && soa->resv_assigned && st->resv_assigned)
+    memcpy(st->resv_assigned, soa->resv_assigned, sizeof(int32_t) * (size_t)n);
+  if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned) return -1;
   orc_la_flags(soa, n, st->flags);
   return 0;
 }
@@ -151,6 +156,9 @@ void orc_state_free(orc_state *st) {
   }
   free(st->numa_alloc_cnt);
   free(st->numa_zone_used);
+  free(st->resv_allocated[0]);
+  free(st->resv_allocated[1]);
+  free(st->resv_assigned);
   memset(st, 0, sizeof(*st));
 }
 
@@ -242,6 +250,8 @@ static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const k
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && st->soa->resv_flags && !orc_resv_filter(st, pod, i))
+    return 0;
   return 1;
 }
 
@@ -267,9 +277,12 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
              uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
   const int32_t n = st->n;
   uint64_t *keys = (topk && k > 0) ? (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1)) : NULL;
+  const int rv = orc_resv_on(cfg, st);
   for (int32_t p = 0; p < n_pods; p++) {
     const koordhip_pod *pod = &pods[p];
     int32_t nk = 0;
+    /* the cycle sees the Reservation restore (transformer.go:48-221); undone below */
+    if (rv) orc_resv_restore((orc_state *)st, pod, +1);
     for (int32_t i = 0; i < n; i++) {
       int fit_ok = orc_fit_filter(cfg, st, pod, i);
       int la_ok = orc_la_filter(cfg, st, pod, i);
@@ -279,6 +292,8 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !fit_ok) b |= KOORDHIP_ST_FIT_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !la_ok) b |= KOORDHIP_ST_LA_FAIL;
         if (!numa_ok) b |= KOORDHIP_ST_NUMA_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && st->soa->resv_flags && !orc_resv_filter(st, pod, i))
+          b |= KOORDHIP_ST_RESV_FAIL;
         status[(size_t)p * n + i] = b;
       }
       if (scores) {
@@ -289,8 +304,13 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
         row[2 * (size_t)n + i] =
             (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) ? (int32_t)orc_numa_score(cfg, st, pod, i) : 0;
       }
-      if (keys && orc_feasible(cfg, st, pod, i)) keys[nk++] = mkkey(orc_total(cfg, st, pod, i), i);
+      if (keys && orc_feasible(cfg, st, pod, i)) {
+        int64_t t = orc_total(cfg, st, pod, i);
+        if (rv) t = orc_resv_rank_total(cfg, st, pod, i, t);
+        keys[nk++] = mkkey(t, i);
+      }
     }
+    if (rv) orc_resv_restore((orc_state *)st, pod, -1);
     if (keys) {
       qsort(keys, (size_t)nk, sizeof(uint64_t), cmp_key_desc);
       for (int32_t j = 0; j < k; j++) {
@@ -321,6 +341,10 @@ static int numa_on(const koordhip_config *cfg) {
 
 int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t i, int sign,
                uint64_t *cpus) {
+  const int rv = orc_resv_on(cfg, st) && (st->soa->resv_flags[i] & KOORDHIP_RESV_PRESENT);
+  /* Unreserve of a pod its node's reservation could have taken: whether it did
+   * (state.assumed, plugin.go:591-597) is not passed back */
+  if (rv && sign < 0 && ((pod->resv_match >> KOORDHIP_RESV_GROUP(st->soa->resv_flags[i])) & 1u)) return KOORDHIP_EINVAL;
   if (numa_on(cfg) && orc_numa_reserve_active(st, pod, i)) {
     if (sign > 0) {
       if (!orc_numa_reserve(st, pod, i, cpus)) return KOORDHIP_ERESERVE;
@@ -332,6 +356,7 @@ int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *po
   } else if (cpus && sign > 0) {
     for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
   }
+  if (rv && sign > 0) orc_resv_assume(st, pod, i); /* Reservation Reserve: assumePod (plugin.go:550-573) */
   for (int r = 0; r < KOORDHIP_NRES; r++) st->requested[r][i] += sign * pod->req[r];
   st->nz_cpu_m[i] += sign * pod->nz_cpu_m;
   st->nz_mem[i] += sign * pod->nz_mem;
@@ -501,18 +526,26 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
   c.cfg = cfg;
   c.st = st;
   c.feasible = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
-  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * 3 * (size_t)(n > 0 ? n : 1));
+  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * 4 * (size_t)(n > 0 ? n : 1));
+  const int rv = orc_resv_on(cfg, st);
   for (int32_t p = 0; p < n_pods; p++) {
     c.pod = &pods[p];
+    /* Reservation BeforePreFilter: the cycle's NodeInfos are the restored ones */
+    if (rv) orc_resv_restore(st, &pods[p], +1);
     atomic_store(&c.nfeasible, 0);
     pool_until(&pl, n, filter_piece, &c);
     int32_t nf = atomic_load(&c.nfeasible);
     if (nf == 0) {
+      if (rv) orc_resv_restore(st, &pods[p], -1);
       out_node[p] = KOORDHIP_UNSCHEDULABLE;
       if (st->cpuset_out) memset(st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS, 0, 8 * KOORDHIP_NUMA_WORDS);
       continue;
     }
     pool_until(&pl, nf, score_piece, &c);
+    /* Reservation PreScore + Score + NormalizeScore over the feasible list */
+    int64_t *norm = c.plugin_scores + 3 * (size_t)nf;
+    const int rs = rv && (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION);
+    if (rs) orc_resv_normalized(st, &pods[p], c.feasible, nf, norm);
     /* (upstream) prioritizeNodes: sum of score x weight; selectHost: max,
      * reservoir-random tie-break REPLACED by lowest node index (BASELINE.json). */
     int64_t best = -1;
@@ -521,11 +554,13 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
       int32_t i = c.feasible[j];
       int64_t t = cfg->plugin_weight[0] * c.plugin_scores[j] + cfg->plugin_weight[1] * c.plugin_scores[(size_t)nf + j] +
                   cfg->plugin_weight[2] * c.plugin_scores[2 * (size_t)nf + j];
+      if (rs) t += (int64_t)cfg->reservation_weight * norm[j];
       if (t > best || (t == best && i < best_node)) {
         best = t;
         best_node = i;
       }
     }
+    if (rv) orc_resv_restore(st, &pods[p], -1);
     uint64_t *cs = st->cpuset_out ? st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS : NULL;
     /* Reserve (+ AssumePod); a failed Reserve leaves no state and is not retried */
     out_node[p] = orc_commit(cfg, st, &pods[p], best_node, +1, cs) ? KOORDHIP_RESERVE_FAILED : best_node;

@@ -1,6 +1,6 @@
 /*
  * koord_oracle.h -- TEST INFRASTRUCTURE.  CPU restatement of koord-scheduler's
- * Filter/Score hot path (NodeResourcesFit, LoadAwareScheduling, NodeNUMAResource) used ONLY as the
+ * Filter/Score hot path (NodeResourcesFit, LoadAwareScheduling, NodeNUMAResource, Reservation) used ONLY as the
  * checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
  * Nothing in the product (koordinator_amd/, libkoordhip.so) links or calls it.
  *
@@ -53,6 +53,9 @@ typedef struct orc_state {
   int32_t *numa_alloc_cnt;
   int64_t *numa_zone_used; /* [n][2][KOORDHIP_NUMA_MAX_NODES] NUMA zone allocations */
   uint64_t *cpuset_out; /* optional [n_pods][WORDS] output of orc_place_stream */
+  /* Reservation: Allocated (cpu milli, memory) and len(AssignedPods) of each node's reservation */
+  int64_t *resv_allocated[2];
+  int32_t *resv_assigned;
 } orc_state;
 
 int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n);
@@ -105,6 +108,24 @@ int orc_tm_merge(int policy, uint64_t numa_nodes, const orc_tm_entry *e, int32_t
  * [2][KOORDHIP_NUMA_MAX_NODES]; returns 1 when Admit + Allocate succeed. */
 int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *mask, int32_t *nil,
                         int32_t *admit, int64_t *zones);
+
+/* Reservation (resv_oracle.c): the cycle's restore (sign +1 apply, -1 undo),
+ * classification, filterWithReservations on the restored state, nomination,
+ * scoreReservation, the normalized scores over a feasible list, Reserve, and
+ * the device's ranking total. */
+int orc_resv_on(const koordhip_config *cfg, const orc_state *st);
+void orc_resv_classify(const orc_state *st, const koordhip_pod *pod, int32_t i, int *matched, int *unmatched);
+void orc_resv_restore_delta(const orc_state *st, const koordhip_pod *pod, int32_t i, int64_t *dreq, int64_t *dnz,
+                            int32_t *dpods);
+void orc_resv_restore(orc_state *st, const koordhip_pod *pod, int sign);
+int orc_resv_filter(const orc_state *st, const koordhip_pod *pod, int32_t i);
+int orc_resv_nominated(const orc_state *st, const koordhip_pod *pod, int32_t i);
+int64_t orc_resv_score(const orc_state *st, const koordhip_pod *pod, int32_t i);
+void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i);
+void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int32_t *feasible, int32_t nf,
+                         int64_t *norm);
+int64_t orc_resv_rank_total(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i,
+                            int64_t b);
 
 /* Same contract as koordhip_eval (status / scores / topk all optional). */
 int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, int32_t n_pods,

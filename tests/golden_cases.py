@@ -329,3 +329,39 @@ def build_numa_filter_amp_case(case):
             p["numa_cpus"][0] = cpu
             p["numa_policy"][0] = abi.numa_policy(0, abi.CPUBIND_FULL_PCPUS, 0)
     return prof, t, p
+
+
+# ------------------------------------------------ Reservation (reservation/*_test.go)
+def reservation_cases():
+    return load("reservation_cases.json")
+
+
+def resv_profile(fit_weight: int = 1):
+    from koordinator_amd.config import PLUGIN_FIT, PLUGIN_RESERVATION, NodeResourcesFitArgs
+    return Profile(filters=(PLUGIN_FIT, PLUGIN_RESERVATION), scores={PLUGIN_FIT: fit_weight, PLUGIN_RESERVATION: 5000},
+                   fit=NodeResourcesFitArgs(resources={k8s.CPU: 1, k8s.MEMORY: 1}))
+
+
+def resv_pod(req: dict, labels=None, name="pod"):
+    return k8s.Pod(name=name, labels=dict(labels or {}), priority=9500,
+                   containers=[k8s.Container(requests=rlist(req))] if req else [k8s.Container()])
+
+
+def build_resv_nodes(nodes, reservations, profile, node_pods=None):
+    """nodes: [(name, allocatable dict)]; reservations: reservation.Reservation
+    objects (their reserve pods and assigned pods are NodeInfo pods)."""
+    from koordinator_amd import reservation as rv
+    cluster = marshal.ClusterState(nodes=[k8s.Node(name=n, allocatable=rlist(a)) for n, a in nodes])
+    for name, pods in (node_pods or {}).items():
+        cluster.node_pods.setdefault(name, []).extend(pods)
+    for r in reservations:
+        cluster.node_pods.setdefault(r.node_name, []).append(r.reserve_pod())
+    table = marshal.build_table(cluster, profile, NOW)
+    idx = rv.reservation_columns(table, {n: i for i, (n, _) in enumerate(nodes)}, reservations)
+    return table, idx
+
+
+def match_all_owner():
+    """Owners = [{}]: matches every pod (reservation.go:403)."""
+    from koordinator_amd import reservation as rv
+    return [rv.ReservationOwner()]

@@ -1,0 +1,118 @@
+"""Reservation host logic and the ranking-total claim, on CPU.
+
+The device ranks nodes by a per-node total (resv.hpp) instead of the
+reference's score normalized over the feasible nodes; the oracle implements
+both (orc_eval's top-k: the ranking total; orc_place_stream: PreScore + Score
++ DefaultNormalizeScore + the weighted sum).  Here they must pick the same
+node for every pod on random states."""
+import numpy as np
+import pytest
+
+import golden_cases as G
+import oracle
+from koordinator_amd import abi, k8s, marshal, synth
+from koordinator_amd import reservation as rv
+from koordinator_amd.config import ArgsError, shipped_profile, to_c_config
+
+
+@pytest.mark.parametrize("seed,ordered", [(1, 0.0), (2, 0.05), (3, 0.3)])
+def test_ranking_total_argmax_equals_normalized(seed, ordered):
+    prof = shipped_profile(reservation=True)
+    t = synth.make_cluster(synth.ClusterSpec(400, seed=seed), prof)
+    synth.add_reservations(t, synth.ResvSpec(node_frac=0.4, groups=3, ordered_frac=ordered), seed=seed)
+    pods = synth.make_pods(synth.StreamSpec(120, be_frac=0.3, seed=seed, resv_match_frac=0.6, resv_groups=3), prof)
+    cfg = to_c_config(prof)
+    top = oracle.Oracle(cfg, t).eval(pods, status=False, scores=False, k=1)["topk"][:, 0]["node"]
+    for j in range(len(pods)):
+        got = oracle.Oracle(cfg, t).place_stream(pods[j:j + 1])[0]
+        assert got == top[j], j
+
+
+def test_parse_order():
+    L = rv.LABEL_RESERVATION_ORDER
+    assert rv.parse_order({}) == 0
+    assert rv.parse_order({L: "123456"}) == 123456
+    assert rv.parse_order({L: "-5"}) == -5
+    assert rv.parse_order({L: "abc"}) == 0
+    assert rv.parse_order({L: "1.5"}) == 0
+    assert rv.parse_order({L: str(1 << 63)}) == 0  # ParseInt out of range
+
+
+def test_reservation_columns():
+    prof = G.resv_profile()
+    sel = rv.ReservationOwner(label_selector=rv.LabelSelector(match_labels={"app": "a"}))
+    bad = rv.ReservationOwner(label_selector=rv.LabelSelector(
+        match_expressions=[rv.LabelSelectorRequirement("k", "In", [])]))
+    rs = [
+        rv.Reservation("r0", "n0", allocatable=G.rlist({"cpu": "4", "memory": "8Gi"}), owners=[sel],
+                       labels={rv.LABEL_RESERVATION_ORDER: "7"}, allocate_policy="Restricted"),
+        rv.Reservation("r1", "n1", allocatable=G.rlist({"cpu": "2"}), owners=[sel], allocate_once=False,
+                       allocated=G.rlist({"cpu": "1", "memory": "1Gi"}), assigned=1),
+        rv.Reservation("r2", "n2", allocatable=G.rlist({"cpu": "2"}), owners=[bad]),
+        rv.Reservation("r3", "n3", allocatable=G.rlist({"cpu": "2"}), phase="Pending"),
+    ]
+    nodes = [(f"n{i}", {"cpu": "32", "memory": "64Gi", "pods": "110"}) for i in range(4)]
+    t, idx = G.build_resv_nodes(nodes, [r for r in rs if r.is_available()], prof)
+    f = t["resv_flags"]
+    assert f[0] & abi.RESV_PRESENT and f[0] & abi.RESV_ORDERED and f[0] & abi.RESV_ALLOCATE_ONCE
+    assert (f[0] >> abi.RESV_POLICY_SHIFT) & 3 == abi.RESV_POLICY_RESTRICTED
+    assert f[0] & abi.RESV_KEY_CPU and f[0] & abi.RESV_KEY_MEM
+    assert f[1] & abi.RESV_KEY_CPU and not f[1] & abi.RESV_KEY_MEM and not f[1] & abi.RESV_ALLOCATE_ONCE
+    assert t["resv_allocated0"][1] == 1000 and t["resv_allocated1"][1] == 0  # masked to ResourceNames
+    assert t["resv_nz1"][1] == 200 << 20  # the reserve pod lists no memory: the non-zero default
+    assert not f[2] & abi.RESV_PRESENT    # invalid owner selector: ParseError
+    assert f[3] == 0                      # not Available
+    assert (f[0] >> abi.RESV_GROUP_SHIFT) & 63 == (f[1] >> abi.RESV_GROUP_SHIFT) & 63  # same owner spec
+    # reserve pods are NodeInfo pods
+    assert t["npods"][0] == 1 and t["requested0"][0] == 4000
+    pa = G.resv_pod({"cpu": "1"}, labels={"app": "a"})
+    pb = G.resv_pod({"cpu": "1"}, labels={"app": "b"})
+    g = int((f[0] >> abi.RESV_GROUP_SHIFT) & 63)
+    assert idx.pod_mask(pa) == 1 << g and idx.pod_mask(pb) == 0
+    rec = marshal.pod_records([pa], prof, idx)
+    assert rec["resv_match"][0] == 1 << g and rec["flags"][0] & abi.POD_KEY_CPU and not rec["flags"][0] & abi.POD_KEY_MEM
+
+
+def test_two_reservations_on_a_node_rejected():
+    prof = G.resv_profile()
+    rs = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": "2"})) for i in range(2)]
+    with pytest.raises(rv.ReservationError):
+        G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"})], rs, prof)
+
+
+def test_reservation_weight_must_dominate():
+    prof = shipped_profile(reservation=True)
+    prof.scores["Reservation"] = 200  # <= 100 x (Fit 1 + LoadAware 1)
+    with pytest.raises(ArgsError):
+        to_c_config(prof)
+
+
+def test_synth_reservations_match_objects():
+    """add_reservations' columns equal reservation_columns of the same reservations as objects."""
+    prof = G.resv_profile()
+    t = synth.make_cluster(synth.ClusterSpec(200, seed=4), prof)
+    base = t.copy()
+    synth.add_reservations(t, synth.ResvSpec(node_frac=0.5, groups=3, ordered_frac=0.3, cpu_only_frac=0.3), seed=4)
+    owners = [[rv.ReservationOwner(label_selector=rv.LabelSelector(match_labels={"g": str(g)}))] for g in range(3)]
+    idx = rv.ReservationIndex()
+    for o in owners:
+        idx.group(o)
+    objs = []
+    for i in np.flatnonzero(t["resv_flags"]):
+        f = int(t["resv_flags"][i])
+        alloc = {"cpu": f"{int(t['resv_alloc0'][i])}m"}
+        if f & abi.RESV_KEY_MEM:
+            alloc["memory"] = str(int(t["resv_alloc1"][i]))
+        allocated = {"cpu": f"{int(t['resv_allocated0'][i])}m", "memory": str(int(t["resv_allocated1"][i]))}
+        pol = ["", "Aligned", "Restricted"][(f >> abi.RESV_POLICY_SHIFT) & 3]
+        labels = {}
+        if f & abi.RESV_ORDERED:
+            labels[rv.LABEL_RESERVATION_ORDER] = str(100 + int(t["resv_order_rank"][i]))
+        objs.append(rv.Reservation(f"r{i}", t.names[i], allocatable=G.rlist(alloc), allocated=G.rlist(allocated),
+                                   owners=owners[(f >> abi.RESV_GROUP_SHIFT) & 63], labels=labels,
+                                   allocate_policy=pol, allocate_once=bool(f & abi.RESV_ALLOCATE_ONCE),
+                                   unschedulable=bool(f & abi.RESV_UNSCHEDULABLE), assigned=int(t["resv_assigned"][i])))
+    rv.reservation_columns(base, {n: i for i, n in enumerate(base.names)}, objs, idx)
+    for c in ("resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1",
+              "resv_allocated0", "resv_allocated1", "resv_assigned"):
+        assert np.array_equal(base[c], t[c]), c
