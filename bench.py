@@ -49,6 +49,11 @@ def bytes_per_eval(pods: np.ndarray, cfg) -> np.ndarray:
         b += 4                                       # NUMA topology class (i32)
         b += (8 * ~rcpu) * ((flags & abi.POD_NUMA_SKIP) == 0)   # Score reads Requested cpu (non-cpuset pods)
         b += cs * (3 * abi.NUMA_WORDS * 8 + 4 + 1)   # cpuset pods: free / exclusive masks, allocated count, flags
+    if (cfg.score_plugins | cfg.filter_plugins) & abi.PLUGIN_RESERVATION:
+        # reservation flags (u32) on every node; on a reservation node (10%) the
+        # restore reads Allocatable / Allocated / NonZero / assigned (6 f64 + i32 + rank)
+        b += 4 + (6 * 8 + 8) // 10
+        b += 8 * ~rcpu + 8 * ~rmem                   # the restore rewrites Requested: always read
     return b
 
 
@@ -132,9 +137,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["config4", "config3"], default="config4",
+    ap.add_argument("--workload", choices=["config4", "config3", "config5"], default="config4",
                     help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
-                         "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods)")
+                         "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods); "
+                         "config5: 200k nodes, 10%% holding a Reservation matched by 20%% of the pods, "
+                         "+ LoadAware + NodeNUMAResource")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--be-frac", type=float, default=None)
@@ -159,18 +166,21 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    numa = args.workload == "config3"
-    c = synth.CONFIGS[3 if numa else 4]
+    resv = args.workload == "config5"
+    numa = args.workload == "config3" or resv
+    c = synth.CONFIGS[{"config3": 3, "config4": 4, "config5": 5}[args.workload]]
     args.nodes = args.nodes or c["nodes"]
     args.pods = args.pods or c["pods"]
     args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
-    prof = shipped_profile(numa=numa)
+    prof = shipped_profile(numa=numa, reservation=resv)
     prof.batch_pods = args.batch
     table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
     if numa:
         synth.add_numa(table, synth.NumaSpec(), prof)
-    pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac,
-                                            cpuset_frac=c.get("cpuset_frac", 0.0)), prof)
+    if resv:
+        synth.add_reservations(table, synth.ResvSpec())
+    pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac, cpuset_frac=c.get("cpuset_frac", 0.0),
+                                            resv_match_frac=c.get("resv_match_frac", 0.0)), prof)
     cfg = to_c_config(prof)
 
     eng = PlacementEngine(prof, device=local_rank, profile_kernels=False)
@@ -264,7 +274,12 @@ def main():
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded splitmix64 cluster + pod stream, SURVEY.md §8(d))",
-        "config": {"workload": (f"config3: {args.nodes} 2-socket nodes x {args.pods} pods, "
+        "config": {"workload": (f"config5: {args.nodes} nodes (10% holding an Available Reservation) x "
+                                f"{args.pods} pods, {int(args.be_frac * 100)}% BE, "
+                                f"{int(c.get('resv_match_frac', 0) * 100)}% matching a reservation owner, "
+                                "NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource + Reservation (weight 5000)"
+                                if resv else
+                                f"config3: {args.nodes} 2-socket nodes x {args.pods} pods, "
                                 f"{int(args.be_frac * 100)}% BE, {int(c.get('cpuset_frac', 0) * 100)}% of LS pods "
                                 "LSR/LSE cpuset, NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource"
                                 if numa else

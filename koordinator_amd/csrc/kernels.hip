@@ -584,12 +584,14 @@ __device__ __forceinline__ uint64_t sel_mask_eq(const uint4 *q, uint32_t x) {
 // k-th largest value (0 if fewer than k values >= floor) and how many values
 // lie strictly above it.  `count(v)` reads bin v; wave-uniform results.
 template <typename F>
-__device__ __forceinline__ void sel_walk(F count, int32_t nbins, int32_t floor, int32_t k, int32_t &thr, int32_t &gt) {
+__device__ __forceinline__ void sel_walk(F count, int32_t nbins, int32_t floor, int32_t k, int32_t &thr, int32_t &gt,
+                                         int32_t top0 = -1) {
   const int lane = lane_id();
   int32_t cum = 0;
   thr = 0;
   gt = 0;
-  for (int32_t top = nbins - 1; top >= floor && thr == 0; top -= 64) {
+  // top0: no value lies above it (the walk starts there instead of at the top bin)
+  for (int32_t top = top0 >= 0 ? min(top0, nbins - 1) : nbins - 1; top >= floor && thr == 0; top -= 64) {
     const int32_t v = top - lane;
     const int32_t c = v >= floor ? count(v) : 0;
     if (__ballot(c != 0) == 0) continue;  // wave-uniform
@@ -820,11 +822,17 @@ struct SplHdr {  // start of k_select_split's dynamic LDS (all of its LDS: the b
   uint64_t lst[RES_MAXP];
   int32_t wsum[SPL_WAVES];
   int32_t thr, gt, cnt_gt, last, nties;
+  int32_t hmax, smax, mmax;  // largest chunk maximum / slice value >= L / merged key value (walk starts)
   int32_t gtc[SPL_GMAX], tie[SPL_GMAX];
 };
 static_assert(SPL_GMAX == kSelGMax, "k_select_split group bound");
 constexpr int32_t SPL_HDR = (int32_t)((sizeof(SplHdr) + 15) & ~(size_t)15);
 
+// PK: the score histogram holds two u16 counts per word (ranking totals of the
+// Reservation plugin span ~31k values: a u32 per bin plus the chunk-max
+// histogram would not fit LDS, and without the chunk-max lower bound every
+// feasible node of the slice is counted).  Slices stay below 65536 nodes.
+template <bool PK>
 __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
     const uint16_t *__restrict__ S, int64_t s_stride, int32_t lo, int32_t m, int32_t k, int32_t nbins,
     const uint16_t *__restrict__ Mx, int32_t m_stride, int32_t nchunks, int32_t G, int32_t tiles_per,
@@ -833,8 +841,23 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
   extern __shared__ __attribute__((aligned(16))) char spl_lds[];
   SplHdr &h = *reinterpret_cast<SplHdr *>(spl_lds);
   uint64_t *mk = reinterpret_cast<uint64_t *>(spl_lds + SPL_HDR);                    // merge: G x k keys
-  uint32_t *hist = reinterpret_cast<uint32_t *>(spl_lds + SPL_HDR + (size_t)G * k * 8);  // nbins score bins
-  uint32_t *mhist = hist + nbins;                                                      // packed chunk-max bins
+  uint32_t *hist = reinterpret_cast<uint32_t *>(spl_lds + SPL_HDR + (((size_t)G * k * 8 + 15) & ~(size_t)15));  // score bins
+  const int32_t hwords = PK ? (nbins + 1) >> 1 : nbins;
+  uint32_t *mhist = hist + hwords;                                                     // packed chunk-max bins
+  auto hadd = [&](uint32_t v) {
+    if constexpr (PK) {
+      atomicAdd(&hist[v >> 1], 1u << (16 * (v & 1)));
+    } else {
+      atomicAdd(&hist[v], 1u);
+    }
+  };
+  auto hget = [&](int32_t v) -> int32_t {
+    if constexpr (PK) {
+      return (int32_t)((hist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu);
+    } else {
+      return (int32_t)hist[v];
+    }
+  };
   const int t = threadIdx.x, lane = lane_id();
   const int32_t g = blockIdx.x, p = blockIdx.y;
   const uint16_t *row = S + (size_t)p * s_stride;
@@ -844,22 +867,34 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
   uint4 q[SPL_ITER];
   if (tb < te) row_load<SPL_ITER>(row, m, first(tb), q);
   const int32_t mwords = nchunks >= k ? (nbins + 1) >> 1 : 0;
-  for (int32_t j = t; j < nbins + mwords; j += SPL_THREADS) hist[j] = 0;
-  if (t == 0) h.cnt_gt = 0;
+  {  // zero both histograms, 16 B per store (the launch rounds the LDS size up)
+    uint4 *h4 = reinterpret_cast<uint4 *>(hist);
+    const int32_t n4 = (hwords + mwords + 3) >> 2;
+    for (int32_t j = t; j < n4; j += SPL_THREADS) h4[j] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (t == 0) {
+    h.cnt_gt = 0;
+    h.hmax = 0;
+    h.smax = 0;
+  }
   // ---- lower bound L: the k-th largest chunk maximum of the whole row
   uint32_t L = 1;
   if (mwords) {
     const uint16_t *mrow = Mx + (size_t)p * m_stride;
     __syncthreads();
+    uint32_t mx = 0;
     for (int32_t j = t; j < nchunks; j += SPL_THREADS) {
       const uint32_t v = mrow[j];
       if (v) atomicAdd(&mhist[v >> 1], 1u << (16 * (v & 1)));  // counts <= nchunks < 2^16
+      mx = v > mx ? v : mx;
     }
+    const int32_t wm = wave_max_i32_dpp((int32_t)mx);
+    if (lane == 0 && wm > 0) atomicMax(&h.hmax, wm);
     __syncthreads();
     if (t < 64) {
       int32_t thr, gt;
       sel_walk([&](int32_t v) { return (int32_t)((mhist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu); }, nbins, 1, k, thr,
-               gt);
+               gt, h.hmax);
       if (lane == 0) h.thr = thr;
     }
     __syncthreads();
@@ -867,24 +902,32 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
   }
   __syncthreads();
   // ---- pass 1: histogram of the slice's scores >= L
+  uint32_t sx = 0;
   for (int32_t tile = tb; tile < te; tile++) {
     if (tile > tb) row_load<SPL_ITER>(row, m, first(tile), q);
     uint64_t hit = sel_mask_ge<SPL_ITER>(q, L);
     while (hit) {
       const int b = __builtin_ctzll(hit);
       hit &= hit - 1;
-      atomicAdd(&hist[row[first(tile) + b]], 1u);
+      const uint32_t v = row[first(tile) + b];
+      hadd(v);
+      sx = v > sx ? v : sx;
     }
+  }
+  {
+    const int32_t wm = wave_max_i32_dpp((int32_t)sx);
+    if (lane == 0 && wm > 0) atomicMax(&h.smax, wm);
   }
   __syncthreads();
   // ---- the slice's k-th largest value T (or L with all of its >= L values)
   if (t < 64) {
     int32_t thr, gt;
-    sel_walk([&](int32_t v) { return (int32_t)hist[v]; }, nbins, (int32_t)L, k, thr, gt);
+    const int32_t top = h.smax;
+    sel_walk(hget, nbins, (int32_t)L, k, thr, gt, top);
     if (thr == 0) {
       thr = (int32_t)L;
       gt = 0;
-      for (int32_t v = thr + 1 + lane; v < nbins; v += 64) gt += (int32_t)hist[v];
+      for (int32_t v = thr + 1 + lane; v <= top && v < nbins; v += 64) gt += hget(v);
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) gt += __shfl_xor(gt, off, 64);
     }
@@ -955,25 +998,37 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
   const int32_t total = G * k;
   const uint64_t *src = part + (size_t)p * G * k;
   for (int32_t j = t; j < total; j += SPL_THREADS) mk[j] = src[j];
-  for (int32_t j = t; j < nbins; j += SPL_THREADS) hist[j] = 0;
+  for (int32_t j = t; j < hwords; j += SPL_THREADS) hist[j] = 0;
   if (t < SPL_GMAX) {
     h.gtc[t] = 0;
     h.tie[t] = 0;
   }
-  if (t == 0) h.cnt_gt = 0;
+  if (t == 0) {
+    h.cnt_gt = 0;
+    h.mmax = 0;
+  }
   __syncthreads();
-  for (int32_t j = t; j < total; j += SPL_THREADS) {
-    const uint64_t x = mk[j];
-    if (x) atomicAdd(&hist[key_sc(x)], 1u);
+  {
+    int32_t mx = 0;
+    for (int32_t j = t; j < total; j += SPL_THREADS) {
+      const uint64_t x = mk[j];
+      if (x) {
+        hadd((uint32_t)key_sc(x));
+        mx = max(mx, key_sc(x));
+      }
+    }
+    const int32_t wm = wave_max_i32_dpp(mx);
+    if (lane == 0 && wm > 0) atomicMax(&h.mmax, wm);
   }
   __syncthreads();
   if (t < 64) {
     int32_t sth, sgt;
-    sel_walk([&](int32_t v) { return (int32_t)hist[v]; }, nbins, 1, k, sth, sgt);
+    const int32_t top = h.mmax;
+    sel_walk(hget, nbins, 1, k, sth, sgt, top);
     if (sth == 0) {  // fewer than k keys in all: every one of them
       sth = 1;
       sgt = 0;
-      for (int32_t v = 2 + lane; v < nbins; v += 64) sgt += (int32_t)hist[v];
+      for (int32_t v = 2 + lane; v <= top && v < nbins; v += 64) sgt += hget(v);
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) sgt += __shfl_xor(sgt, off, 64);
     }
@@ -2250,22 +2305,32 @@ hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, 
   if (n_pods <= 0) return hipSuccess;
   if (k < 1 || k > RES_MAXP || nbins < 2 || nbins > 32768 || n_pods > kSelMaxPods) return hipErrorInvalidValue;
   const int32_t ntiles = std::max<int32_t>(1, (m + SPL_TILE - 1) / SPL_TILE);
+  // large score ranges (Reservation ranking totals): u16-packed score bins,
+  // with slices short enough that a count stays below 2^16
+  const bool pk = nbins > 8192;
+  if (pk)
+    while (G < SPL_GMAX && (int64_t)((ntiles + G - 1) / G) * SPL_TILE >= 65536) G++;
   G = select_split_groups(m, G);
   const int32_t per = (ntiles + G - 1) / G;
+  if (pk && (int64_t)per * SPL_TILE >= 65536) return hipErrorInvalidValue;
   if (nchunks > 65535) nchunks = 0;  // no lower bound: histogram the slices whole
-  size_t hb = (size_t)nbins * sizeof(uint32_t);
-  if (hb + (size_t)((nbins + 1) / 2) * sizeof(uint32_t) > 112 * 1024) nchunks = 0;
+  size_t hb = (size_t)(pk ? (nbins + 1) / 2 : nbins) * sizeof(uint32_t);
+  if (hb + (size_t)((nbins + 1) / 2) * sizeof(uint32_t) > 136 * 1024) nchunks = 0;
   if (nchunks >= k) hb += (size_t)((nbins + 1) / 2) * sizeof(uint32_t);
-  const size_t lds = (size_t)SPL_HDR + (size_t)G * k * sizeof(uint64_t) + hb;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e =
-        hipFuncSetAttribute((const void *)k_select_split, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  const size_t lds = (size_t)SPL_HDR + (((size_t)G * k * sizeof(uint64_t) + 15) & ~(size_t)15) + hb + 16;
+  static bool attr[2] = {false, false};
+  const void *fn = pk ? (const void *)k_select_split<true> : (const void *)k_select_split<false>;
+  if (!attr[pk]) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr = true;
+    attr[pk] = true;
   }
-  hipLaunchKernelGGL(k_select_split, dim3(G, n_pods), dim3(SPL_THREADS), lds, s, S, s_stride, lo, m, k, nbins, Mx,
-                     m_stride, nchunks, G, per, part, cnt, out, sync, sel_par, res_wait);
+  if (pk)
+    hipLaunchKernelGGL(k_select_split<true>, dim3(G, n_pods), dim3(SPL_THREADS), lds, s, S, s_stride, lo, m, k, nbins,
+                       Mx, m_stride, nchunks, G, per, part, cnt, out, sync, sel_par, res_wait);
+  else
+    hipLaunchKernelGGL(k_select_split<false>, dim3(G, n_pods), dim3(SPL_THREADS), lds, s, S, s_stride, lo, m, k, nbins,
+                       Mx, m_stride, nchunks, G, per, part, cnt, out, sync, sel_par, res_wait);
   return hipGetLastError();
 }
 
