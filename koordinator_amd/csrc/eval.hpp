@@ -143,6 +143,27 @@ __device__ __forceinline__ Need pod_needs(const DevPod &p, const DevCfg &c) {
   return n;
 }
 
+__device__ __forceinline__ void need_or(Need &a, const Need &b) {
+  a.pods |= b.pods;
+  a.r_cpu |= b.r_cpu;
+  a.r_mem |= b.r_mem;
+  a.eph |= b.eph;
+  a.bcpu |= b.bcpu;
+  a.bmem |= b.bmem;
+  a.a_cpu |= b.a_cpu;
+  a.a_mem |= b.a_mem;
+  a.nz_cpu |= b.nz_cpu;
+  a.nz_mem |= b.nz_mem;
+  a.la |= b.la;
+  a.la_nonprod |= b.la_nonprod;
+  a.la_prod |= b.la_prod;
+  a.numa |= b.numa;
+  a.numa_masks |= b.numa_masks;
+  a.zones |= b.zones;
+  a.amp |= b.amp;
+  a.resv |= b.resv;
+}
+
 __device__ __forceinline__ Need need_all(const DevCfg &c) {
   Need n;
   n.pods = n.r_cpu = n.r_mem = n.eph = n.bcpu = n.bmem = n.a_cpu = n.a_mem = n.nz_cpu = n.nz_mem = true;

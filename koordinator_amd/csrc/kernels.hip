@@ -396,6 +396,9 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 // XCD's 4 MB L2 then holds its eighth of the node table (50k nodes: ~0.5 MB)
 // and the 4 x (pods/4) re-reads of a row hit L2 instead of the MALL.
 
+template <int NM>
+using side_row_t = typename std::conditional<NM == 3, NumaRowR, NumaRow>::type;
+
 // NM: 0 = no NodeNUMAResource, 1 = NodeNUMAResource, 2 = ... with
 // topology-policy nodes (the zone code is compiled only here), 3 = with the
 // Reservation plugin (NUMA side rows carry the node's reservation)
@@ -1265,9 +1268,6 @@ __device__ __forceinline__ bool xbit(const uint32_t *m, int32_t nd) { return (m[
 __device__ __forceinline__ uint64_t ktab_key(uint32_t v, int32_t nd) {
   return v ? ((uint64_t)v << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)nd) : 0ull;
 }
-
-template <int NM>
-using side_row_t = typename std::conditional<NM == 3, NumaRowR, NumaRow>::type;
 
 template <int NM>
 __device__ __forceinline__ void load_side_row(side_row_t<NM> &r, const DevNodes &d, int32_t i) {

@@ -1,9 +1,19 @@
 #!/bin/bash
-# k_scan shape sweep (bench only): KOORDHIP_TOPK_R nodes per lane x KOORDHIP_SCAN_PW pods per wave.
+# k_scan pods-per-wave / nodes-per-lane sweep (bench only).
+# Usage: scripts/sweep_scan.sh OUTDIR WORKLOAD "R:PPW ..."   (PPW 0 = automatic)
 set -u
-mkdir -p gpurun_out
-for cfg in ${SWEEP:-"1 2" "1 4" "2 1" "2 2" "2 4" "4 1" "4 2"}; do
-  set -- $cfg
-  KOORDHIP_TOPK_R=$1 KOORDHIP_SCAN_PW=$2 timeout -k 10 120 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/sweep_$1_$2.json 2>/dev/null || exit $?
-  python3 -c "import json,sys; d=json.load(open('gpurun_out/sweep_$1_$2.json')); print('R=$1 pw=$2', d['value'], d['eval_roofline']['avg_launch_us'], d['select']['avg_launch_us'])"
+out=gpurun_out/${1:-scan_sweep}
+w=${2:-config4}
+mkdir -p $out
+for rp in ${3:-"1:1 1:4 1:0 2:1 2:4 2:0"}; do
+  r=${rp%%:*}; ppw=${rp##*:}
+  tag=${w}_r${r}_p${ppw}
+  if [ $ppw = 0 ]; then unset KOORDHIP_SCAN_PPW; else export KOORDHIP_SCAN_PPW=$ppw; fi
+  KOORDHIP_TOPK_R=$r timeout -k 10 300 python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline \
+    > $out/$tag.json 2> $out/$tag.err || { echo "failed $tag"; exit 1; }
+  python - "$out/$tag.json" "$tag" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1]))
+print(sys.argv[2], d["value"], d["eval_roofline"]["avg_launch_us"], d["select"]["avg_launch_us"], flush=True)
+PY
 done

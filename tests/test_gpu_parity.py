@@ -251,14 +251,16 @@ def test_sharded_group_bit_exact(Engine, world, n_nodes, n_pods, be, batch):
 
 # ----------------------------------------------------------- launch modes
 @pytest.mark.parametrize("mode", ["KOORDHIP_ROUND_LAUNCH", "KOORDHIP_SERIAL", "KOORDHIP_CU_RESERVE", "KOORDHIP_ONE_EVAL_STREAM", "KOORDHIP_NO_KEY_TABLES",
-                                  "KOORDHIP_FOLD_WAIT", "KOORDHIP_SELECT_ONEWG", "KOORDHIP_LAG1"])
+                                  "KOORDHIP_FOLD_WAIT", "KOORDHIP_SELECT_ONEWG", "KOORDHIP_LAG1",
+                                  "KOORDHIP_TOPK_R=1"])
 @pytest.mark.parametrize("numa", [False, True])
 def test_launch_modes_bit_exact(Engine, monkeypatch, mode, numa):
     """The per-round resolve launch (local groups), the single-stream
     profiling order and the opt-in pipeline knobs (CU-masked streams, the wait
     folded into the select, one select workgroup per pod) place exactly like
     the default persistent pipeline and the oracle."""
-    monkeypatch.setenv(mode, "1")
+    name, _, val = mode.partition("=")
+    monkeypatch.setenv(name, val or "1")
     prof = shipped_profile(numa=numa)
     prof.batch_pods = 16
     table = synth.make_cluster(synth.ClusterSpec(400), prof)

@@ -63,10 +63,12 @@ def test_gpu_resv_eval_parity(Engine, numa):
 
 
 @pytest.mark.parametrize("numa,mode", [(False, "persistent"), (True, "persistent"), (False, "rounds"),
-                                       (True, "cpuset")])
+                                       (True, "cpuset"), (True, "r1")])
 def test_gpu_resv_stream_parity(Engine, numa, mode, monkeypatch):
     if mode == "rounds":
         monkeypatch.setenv("KOORDHIP_ROUND_LAUNCH", "1")
+    if mode == "r1":  # one node per scan lane
+        monkeypatch.setenv("KOORDHIP_TOPK_R", "1")
     prof, t, pods = _workload(3000, 2500, numa, cpuset=0.2 if mode == "cpuset" else 0.0)
     o = oracle.Oracle(to_c_config(prof), t)
     ref = o.place_stream(pods, threads=8)
@@ -135,3 +137,27 @@ def test_gpu_resv_update_nodes(Engine):
         e.update_nodes(idx, t2.rows(idx))
         got = e.place_stream(pods)
     assert np.array_equal(ref, got)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_resv_sharded_group(Engine, world):
+    """Node-index shards (the multi-GPU layout, here `world` contexts on one
+    GPU): per-shard top-k of the Reservation ranking totals merged, then the
+    replicated resolve -- every rank returns the unsharded placements."""
+    from koordinator_amd.engine import place_stream_group
+    prof, t, pods = _workload(2000, 800, True)
+    engines = [Engine(prof, device=0) for _ in range(world)]
+    try:
+        for e in engines:
+            e.load_snapshot(t)
+        Engine.comm_init_local(engines)
+        outs = place_stream_group(engines, pods)
+        resv = [e.read_reservations() for e in engines]
+    finally:
+        for e in engines:
+            e.close()
+    o = oracle.Oracle(to_c_config(prof), t)
+    ref = o.place_stream(pods, threads=8)
+    for r in range(world):
+        assert np.array_equal(outs[r], ref), (r, int(np.flatnonzero(outs[r] != ref)[0]))
+        assert np.array_equal(resv[r]["allocated"], o.resv_state()["allocated"])
