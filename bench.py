@@ -149,6 +149,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--check", action="store_true", help="verify placements vs the oracle (slow)")
+    ap.add_argument("--one-rank-comm", action="store_true",
+                    help="N=1 only: attach a one-rank RCCL communicator, so every round takes the multi-GPU "
+                         "exchange path (all-gather + merge) -- measures that pipeline on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +192,8 @@ def main():
         t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
         dist.broadcast(t, 0)
         eng.comm_init(bytes(t.cpu().tolist()), world, rank)
+    elif args.one_rank_comm:
+        eng.comm_init(PlacementEngine.comm_unique_id(), 1, 0)
     eng.load_snapshot(table)
     eng.checkpoint()
     eng.stage_pods(pods)
@@ -286,7 +291,7 @@ def main():
                                 f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
                                 "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile"),
                    "nodes": args.nodes, "pods": args.pods, "batch_pods": batch, "pipeline_lag": lag,
-                   "parallelism": f"node-shard x{world}"},
+                   "parallelism": f"node-shard x{world}" + (" (one-rank RCCL exchange path)" if args.one_rank_comm and world == 1 else "")},
         "unschedulable": int((placements < 0).sum()),
         "roofline": {"bound": "hbm", "kernel": "k_resolve",
                      "limiter": "latency: one wave's sequential greedy (not bandwidth)",

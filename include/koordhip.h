@@ -385,7 +385,9 @@ int koordhip_set_profile_kernels(koordhip_ctx *ctx, int32_t on);
 #define KOORDHIP_UNIQUE_ID_BYTES 128
 int koordhip_comm_unique_id(uint8_t *id_out /* KOORDHIP_UNIQUE_ID_BYTES */);
 /* Attach an RCCL communicator: this context then evaluates only node shard
- * [rank*n/world, (rank+1)*n/world) and merges per-shard top-k over xGMI. */
+ * [rank*n/world, (rank+1)*n/world) and merges per-shard top-k over xGMI.
+ * world == 1 attaches a one-rank communicator: the whole table, through the
+ * same per-round all-gather + merge path (lag 1, one evaluation stream). */
 int koordhip_comm_init(koordhip_ctx *ctx, const uint8_t *id, int32_t world, int32_t rank);
 /* The same sharding for `world` contexts driven by ONE process (one host
  * thread per context, e.g. one scheduler process owning several GPUs, or

@@ -95,6 +95,7 @@ struct koordhip_ctx {
   int32_t score_bits = 16;  // bits of (max total score + 1)
   int32_t nbins = 2;        // score histogram bins of k_select: max total score + 2
   int32_t partial_r = 2;    // nodes per lane of k_scan (tuning knob KOORDHIP_TOPK_R)
+  int32_t scan_ppw = 0;     // pods per node-major scan wave: 0 = pod-major k_scan, -1 auto (KOORDHIP_SCAN_PPW)
 
   std::vector<void *> cols;  // every device column allocation
   kh::DevNodes d{};
@@ -126,9 +127,9 @@ struct koordhip_ctx {
   hipStream_t stream2 = nullptr;  // second evaluation stream (odd rounds) of a single-GPU place call
   hipEvent_t ev_eval2 = nullptr;
   uint64_t *d_lists = nullptr;   // [2][batch][k] (rank-local lists; double buffer: round parity)
-  uint64_t *d_gather = nullptr;  // [world][batch][k]
+  uint64_t *d_gather = nullptr;  // [2 streams][world][batch][k]
   int32_t gather_world = 1;
-  uint64_t *d_final = nullptr;   // [2][batch][k] (merged lists, multi-rank)
+  uint64_t *d_final = nullptr;   // [4][batch][k] (merged lists, multi-rank; indexed like d_lists)
   int32_t *d_mod = nullptr;      // {count, nodes} M' between resolve launches, then PipeSync
   kh::DevNodes *d_desc = nullptr;  // device copy of d (column pointers) for k_resolve
   kh::DevNodes desc_host{};        // its host source (stable while the copy is in flight)
@@ -149,6 +150,7 @@ struct koordhip_ctx {
 
   // sharding
   ncclComm_t comm = nullptr;
+  ncclComm_t comm2 = nullptr;              // split of `comm` for the second evaluation stream's rounds
   std::shared_ptr<LocalGroup> group;       // koordhip_comm_init_local
   hipEvent_t ev_part = nullptr, ev_copy = nullptr;
   int32_t world = 1, rank = 0;
@@ -330,7 +332,8 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
   int32_t tm = -1;
   if (timed)
     if (int e = timed_begin(c, TK_SCAN, es, &tm)) return e;
-  HIP_TRY(kh::launch_scan(R, c->dc, c->d, d_pods, np, lo, hi, S, stride, Mx, mstride, es));
+  const int32_t ppw = c->scan_ppw < 0 ? kh::scan_ppw(R, lo, hi, np) : c->scan_ppw;
+  HIP_TRY(kh::launch_scan(R, c->dc, c->d, d_pods, np, lo, hi, S, stride, Mx, mstride, ppw, es));
   if (int e = timed_end(c, tm, es)) return e;
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
@@ -635,6 +638,11 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
   }
   if (c->side && c->partial_r > 4) c->partial_r = 4;  // the NUMA / Reservation scan kernels are built for R <= 4
+  // node-major scan (k_scan_nm) group size, "auto" = ~2 waves per SIMD; the
+  // pod-major k_scan stays the default (node-major measured equal on config 4
+  // and slower on config 5: DESIGN.md §5)
+  if (const char *q = std::getenv("KOORDHIP_SCAN_PPW"))
+    c->scan_ppw = std::strcmp(q, "auto") == 0 ? -1 : std::max(0, std::min(kMaxBatch, std::atoi(q)));
   // the split select shortens the evaluation stream (and drops the signal
   // kernel); KOORDHIP_SELECT_ONEWG restores one workgroup per pod for A/B runs
   c->sel_split = std::getenv("KOORDHIP_SELECT_ONEWG") == nullptr;
@@ -734,6 +742,7 @@ int koordhip_destroy(koordhip_ctx *c) {
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
+  if (c->comm2) (void)ncclCommDestroy(c->comm2);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->group) c->group->abort();
   for (hipEvent_t e : {c->ev_part, c->ev_copy})
@@ -1180,13 +1189,21 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
 
 namespace {
 
+// the gather buffer of evaluation stream `slot` ([world][batch][k] each)
+uint64_t *gather_buf(koordhip_ctx *c, int slot) {
+  return c->d_gather + (size_t)slot * c->gather_world * ((size_t)kMaxBatch * 2 * kMaxBatch);
+}
+
 // All-gather of the per-shard lists of one round: RCCL, or for a local group
 // a device-to-device pull of every member's list after its eval finished
 // (events + host barrier), then a second barrier so no member overwrites its
 // list before every peer has copied it.
-int exchange(koordhip_ctx *c, const uint64_t *lists, size_t count) {
+// With two evaluation streams, the rounds of stream `slot` exchange on their
+// own communicator (comm / comm2: every rank issues each communicator's
+// all-gathers in the same round order) into their own gather buffer.
+int exchange(koordhip_ctx *c, const uint64_t *lists, size_t count, int slot, hipStream_t es) {
   if (c->comm) {
-    NCCL_TRY(ncclAllGather(lists, c->d_gather, count, ncclUint64, c->comm, c->stream));
+    NCCL_TRY(ncclAllGather(lists, gather_buf(c, slot), count, ncclUint64, slot ? c->comm2 : c->comm, es));
     return 0;
   }
   LocalGroup &g = *c->group;
@@ -1260,7 +1277,12 @@ int place_staged_impl(koordhip_ctx *c) {
   // A lone single-GPU context alternates the rounds between two evaluation
   // streams (each with its own score matrix and select buffers; the resolve
   // counts finished lists per round parity).
-  const bool two = persistent && c->world == 1 && c->sel_split && wait_kernel && !std::getenv("KOORDHIP_ONE_EVAL_STREAM");
+  // exchanged: node-sharded, or a one-rank RCCL communicator (the exchange
+  // path end to end on one GPU: all-gather, merge, per-round signal)
+  const bool exch = c->world > 1 || c->comm != nullptr;
+  // (node-sharded: the rounds of the second stream exchange on comm2)
+  const bool two = persistent && (!exch || c->comm2) && c->sel_split && wait_kernel &&
+                   !std::getenv("KOORDHIP_ONE_EVAL_STREAM");
   // Pipeline depth: round r's lists are evaluated on the state after round
   // r - 1 - lag.  Lag 2 (the default with the two evaluation streams) lets an
   // evaluation overlap two resolve rounds; the resolve then re-evaluates the
@@ -1280,7 +1302,7 @@ int place_staged_impl(koordhip_ctx *c) {
   const size_t lbytes = (size_t)kMaxBatch * 2 * kMaxBatch * sizeof(uint64_t);
   if (!c->d_lists) {
     HIP_TRY(hipMalloc(&c->d_lists, 4 * lbytes));
-    HIP_TRY(hipMalloc(&c->d_final, 2 * lbytes));
+    HIP_TRY(hipMalloc(&c->d_final, 4 * lbytes));
     HIP_TRY(hipMalloc(&c->d_mod, (1 + kMaxBatch) * sizeof(int32_t) + kh::kPipeSyncBytes));
     HIP_TRY(hipMalloc(&c->d_desc, sizeof(kh::DevNodes)));
     // The persistent resolve occupies its hardware queue for the whole call:
@@ -1297,16 +1319,35 @@ int place_staged_impl(koordhip_ctx *c) {
     for (int i = 0; i < kRing; i++) HIP_TRY(hipEventCreateWithFlags(&c->ev_res[i], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
   }
-  if (c->world > c->gather_world) {
+  if (exch && (c->world > c->gather_world || !c->d_gather)) {
     if (c->d_gather) HIP_TRY(hipFree(c->d_gather));
     c->d_gather = nullptr;
-    HIP_TRY(hipMalloc(&c->d_gather, (size_t)c->world * lbytes));
+    HIP_TRY(hipMalloc(&c->d_gather, 2 * (size_t)c->world * lbytes));
     c->gather_world = c->world;
   }
   if (kh::resolve_lds_bytes(P, K, c->n, nm, lag) > 157 * 1024)
     return fail(KOORDHIP_EINVAL, "snapshot too large for the resolve kernel's LDS");
   if (c->group)
     if (int e = group_agree(c)) return e;
+  // profile_kernels: event pairs around the evaluation launches of at most
+  // ~256 evenly spaced rounds (the per-kernel averages need no more; every
+  // outstanding timed event holds a runtime signal, and a host thread that
+  // runs out of them waits for the oldest -- possibly behind the persistent
+  // resolve, which waits for rounds that thread has not enqueued yet)
+  const int32_t tstride = std::max<int32_t>(1, (((c->n_staged + P - 1) / P) + 255) / 256);
+  if (c->cfg.profile_kernels) {
+    // every event pair of this call created now: hipEventCreate inside the
+    // round loop could wait on a device that is busy with the persistent
+    // resolve, which itself waits for rounds not yet enqueued
+    const size_t nr = ((size_t)c->n_staged + P - 1) / P;  // rounds; per-round resolve launches are all timed
+    const size_t want = (size_t)6 * ((persistent ? nr / tstride : nr) + 2) + 8;
+    while (c->ev.size() < want) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      c->ev.push_back(e);
+    }
+    c->ev_kind.resize(c->ev.size() / 2);
+  }
   int32_t lo = 0, hi = c->n;
   shard(c, &lo, &hi);
   c->ev_used = 0;
@@ -1338,7 +1379,7 @@ int place_staged_impl(koordhip_ctx *c) {
   const char *trace_env = std::getenv("KOORDHIP_TRACE_POD");  // diagnostics: printf one pod's resolve step
   const int32_t trace = trace_env ? std::atoi(trace_env) : -1;
   const int64_t list_buf = (int64_t)(lbytes / sizeof(uint64_t));
-  uint64_t *lists0 = c->world > 1 ? c->d_final : c->d_lists;
+  uint64_t *lists0 = exch ? c->d_final : c->d_lists;
   uint64_t *cpus = c->d_cpus;
   if (two && !c->stream2) {
     std::vector<uint32_t> m = full_cu_mask(c);  // its own queue too (see rstream)
@@ -1349,12 +1390,13 @@ int place_staged_impl(koordhip_ctx *c) {
   if (two) HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
   for (int slot = 0; slot < (two ? 2 : 1) && rounds > 0; slot++)
     if (int e = eval_buffers(c, std::min(P, total), lo, hi, slot, slot ? c->stream2 : c->stream)) return e;
+  int32_t res_tm = -1;
   if (persistent && rounds > 0) {
     int32_t tm = -1;
     if (int e = timed_begin(c, TK_RESOLVE, c->rstream, &tm)) return e;
     HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, lag, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
-    if (int e = timed_end(c, tm, c->rstream)) return e;
+    res_tm = tm;  // its end event is recorded after the round loop (nothing else runs on rstream)
   }
   for (int32_t r = 0; r < rounds; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
@@ -1364,22 +1406,22 @@ int place_staged_impl(koordhip_ctx *c) {
     const int slot = two ? par : 0;
     const kh::DevPod *pods = c->d_pods + p0;
     uint64_t *lists = c->d_lists + (size_t)(r & (2 * lag - 1)) * list_buf;
-    const bool select_waits = c->sel_split && c->world == 1 && !wait_kernel;  // the previous select held the stream
+    const bool select_waits = c->sel_split && !exch && !wait_kernel;  // the previous select held the stream
     if (r > lag && !serial && !select_waits) HIP_TRY(kh::launch_wait_resolved(sync, r - lag, es));
-    if (c->world > 1) {
-      if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), c->stream));
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, nullptr, 0, 0, c->stream, 0)) return e;
-      if (int e = exchange(c, lists, (size_t)P * K)) return e;
-      HIP_TRY(kh::launch_topk_merge(c->d_gather, K, (int64_t)P * K, np, c->world, K, c->score_bits,
-                                    c->d_final + (size_t)par * list_buf, c->stream));
+    if (exch) {
+      if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), es));
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, r % tstride == 0, nullptr, 0, 0, es, slot)) return e;
+      if (int e = exchange(c, lists, (size_t)P * K, slot, es)) return e;
+      HIP_TRY(kh::launch_topk_merge(gather_buf(c, slot), K, (int64_t)P * K, np, c->world, K, c->score_bits,
+                                    c->d_final + (size_t)(r & (2 * lag - 1)) * list_buf, es));
     } else {
       // the split select's merging workgroups count the round's pods into sync->sel[par] themselves
       // (KOORDHIP_FOLD_WAIT: and hold the stream until round r - 1 is resolved, what the next scan needs)
-      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, true, c->sel_split ? sync : nullptr, par,
+      if (int e = topk_batch(c, pods, np, K, lo, hi, lists, r % tstride == 0, c->sel_split ? sync : nullptr, par,
                              wait_kernel ? 0 : r, es, slot))
         return e;
     }
-    if (c->world > 1 || !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, par, cum, es));
+    if (exch || !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, par, cum, es));
     if (!persistent) {
       if (!serial) {
         HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
@@ -1392,6 +1434,7 @@ int place_staged_impl(koordhip_ctx *c) {
       if (int e = timed_end(c, tm, rs)) return e;
     }
   }
+  if (int e = timed_end(c, res_tm, c->rstream)) return e;
   if (two) {
     HIP_TRY(hipEventRecord(c->ev_eval2, c->stream2));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_eval2, 0));
@@ -1662,16 +1705,23 @@ int koordhip_comm_init(koordhip_ctx *c, const uint8_t *id, int32_t world, int32_
   if (!c || !id) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (world < 1 || rank < 0 || rank >= world) return fail(KOORDHIP_EINVAL, "bad world/rank");
   HIP_TRY(hipSetDevice(c->device));
+  if (c->comm2) {
+    (void)ncclCommDestroy(c->comm2);
+    c->comm2 = nullptr;
+  }
   if (c->comm) {
     (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
   }
   c->group.reset();
-  if (world > 1) {
-    ncclUniqueId uid;
-    std::memcpy(&uid, id, sizeof(uid));
-    NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
-  }
+  // world 1 creates a one-rank communicator too: the same exchange path as a
+  // sharded group (RCCL all-gather of the lists + k_topk_merge), on one GPU
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
+  // a second communicator over the same ranks for the second evaluation
+  // stream (collective: every rank splits here, in the same order)
+  NCCL_TRY(ncclCommSplit(c->comm, 0, rank, &c->comm2, nullptr));
   c->world = world;
   c->rank = rank;
   return 0;
@@ -1692,6 +1742,10 @@ int koordhip_comm_init_local(koordhip_ctx **ctxs, int32_t world) {
   for (int32_t r = 0; r < world; r++) {
     koordhip_ctx *c = ctxs[r];
     HIP_TRY(hipSetDevice(c->device));
+    if (c->comm2) {
+      (void)ncclCommDestroy(c->comm2);
+      c->comm2 = nullptr;
+    }
     if (c->comm) {
       (void)ncclCommDestroy(c->comm);
       c->comm = nullptr;

@@ -19,12 +19,17 @@ struct PrepIn {
 hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t *rows, int32_t m, hipStream_t s);
 hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods,
                             uint8_t *status, int32_t *scores, hipStream_t s);
-// k_scan: score matrix S[p][i - lo] = total score + 1 (0 = infeasible) over the
-// shard [lo, hi), one wave per (pod, 64 x R nodes), XCD-aware grid; Mx[p][chunk]
-// = the chunk's best value.  R in {1, 2, 4, 8} (NUMA: {1, 2, 4}).
+// k_scan / k_scan_nm: score matrix S[p][i - lo] = total score + 1 (0 =
+// infeasible) over the shard [lo, hi), XCD-aware grid; Mx[p][chunk] = the
+// best value of chunk (64 x R nodes).  ppw > 0 and R <= 2: node-major, one
+// wave per (chunk, group of ppw pods) with the node columns loaded once into
+// VGPRs; ppw == 0: pod-major, one wave per (pod, chunk), R in {1, 2, 4, 8}
+// (NUMA: {1, 2, 4}).  scan_ppw: the default group size (~2 waves per SIMD).
 int32_t scan_chunks(int R, int32_t lo, int32_t hi);
+int32_t scan_ppw(int R, int32_t lo, int32_t hi, int32_t n_pods);
 hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t lo,
-                       int32_t hi, uint16_t *S, int64_t s_stride, uint16_t *Mx, int32_t m_stride, hipStream_t s);
+                       int32_t hi, uint16_t *S, int64_t s_stride, uint16_t *Mx, int32_t m_stride, int32_t ppw,
+                       hipStream_t s);
 // k_select: per pod the exact top-k keys of its S row (best first, 0-padded);
 // nbins = max total score + 2
 hipError_t launch_select(const uint16_t *S, int64_t s_stride, int32_t lo, int32_t m, int32_t n_pods, int32_t k,

@@ -470,6 +470,174 @@ __global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod
 }
 
 // ---------------------------------------------------------------------------
+// k_scan_nm: the node-major evaluation (the default).
+//
+// k_scan above gives every (pod, chunk) pair its own wave, so each of a
+// round's P pods re-issues the loads of the same node columns: P x the
+// column VMEM instructions, served by L1/L2, and the kernel is bound by that
+// issue rate.  Here a wave owns one chunk of 64*R nodes, loads the columns
+// the union of its pod group's needs ONCE into VGPRs (lane l: nodes
+// c0 + 64r + l), and then loops over the group's pods with the pod record in
+// SGPRs (a uniform scalar load per pod).  The output is the same score matrix
+// S and chunk maxima Mx, so k_select / k_select_split are unchanged.
+//
+// A workgroup = 4 waves = 4 consecutive chunks x one pod group of `ppw` pods;
+// the host sizes ppw so the grid still holds ~2 waves per SIMD (fewer pods per
+// wave when the node table is small).  XCD-aware like k_scan: block b runs on
+// XCD b % 8 and XCD x only touches the x-th eighth of the chunk quads.
+//
+// Semantics: a pod's evaluation must see exactly the side row its own needs
+// would load (pod_needs: e.g. cls = -1 / amp = 1 / nflags = 0 when the pod's
+// NodeNUMAResource work is skipped), so the union row is narrowed per pod by
+// numa_view before the evaluation; NV fields outside a pod's needs are never
+// read by its evaluation.
+__device__ __forceinline__ uint32_t need_pack(const Need &n) {
+  return (uint32_t)n.pods | (uint32_t)n.r_cpu << 1 | (uint32_t)n.r_mem << 2 | (uint32_t)n.eph << 3 |
+         (uint32_t)n.bcpu << 4 | (uint32_t)n.bmem << 5 | (uint32_t)n.a_cpu << 6 | (uint32_t)n.a_mem << 7 |
+         (uint32_t)n.nz_cpu << 8 | (uint32_t)n.nz_mem << 9 | (uint32_t)n.la << 10 | (uint32_t)n.la_nonprod << 11 |
+         (uint32_t)n.la_prod << 12 | (uint32_t)n.numa << 13 | (uint32_t)n.numa_masks << 14 | (uint32_t)n.zones << 15 |
+         (uint32_t)n.amp << 16 | (uint32_t)n.resv << 17;
+}
+__device__ __forceinline__ Need need_unpack(uint32_t b) {
+  b = __builtin_amdgcn_readfirstlane(b);
+  Need n;
+  n.pods = b & 1;
+  n.r_cpu = (b >> 1) & 1;
+  n.r_mem = (b >> 2) & 1;
+  n.eph = (b >> 3) & 1;
+  n.bcpu = (b >> 4) & 1;
+  n.bmem = (b >> 5) & 1;
+  n.a_cpu = (b >> 6) & 1;
+  n.a_mem = (b >> 7) & 1;
+  n.nz_cpu = (b >> 8) & 1;
+  n.nz_mem = (b >> 9) & 1;
+  n.la = (b >> 10) & 1;
+  n.la_nonprod = (b >> 11) & 1;
+  n.la_prod = (b >> 12) & 1;
+  n.numa = (b >> 13) & 1;
+  n.numa_masks = (b >> 14) & 1;
+  n.zones = (b >> 15) & 1;
+  n.amp = (b >> 16) & 1;
+  n.resv = (b >> 17) & 1;
+  return n;
+}
+// OR over the wave (DPP within rows, then the row broadcasts), result in every lane
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+template <bool Z>
+__device__ __forceinline__ void numa_view(NumaRow &r, const Need &n) {
+  if (!n.numa) {
+    r.cls = -1;
+    r.nflags = 0;
+    r.amp = 1.0;
+    return;
+  }
+  if (!n.amp) r.amp = 1.0;
+  if (!(n.numa_masks || (Z && n.zones))) r.nflags = 0;
+}
+
+template <int R, int NM>
+__global__ __launch_bounds__(256) void k_scan_nm(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
+                                                 int32_t lo, int32_t hi, int32_t nchunks, int32_t cqx, int32_t ppw,
+                                                 uint16_t *__restrict__ S, int64_t s_stride,
+                                                 uint16_t *__restrict__ Mx, int32_t m_stride) {
+  const int32_t b = blockIdx.x;
+  const int32_t xcd = b & 7, local = b >> 3;
+  const int32_t cq = xcd * cqx + local % cqx;
+  const int32_t pg = local / cqx;
+  if (cq * 4 >= nchunks) return;  // block-uniform
+  const DevNumaClass *cls = d.nu.cls;
+  if constexpr (NM != 0) {  // topology classes -> LDS (as k_scan)
+    extern __shared__ uint4 scan_cls[];
+    if (d.nu.ncls <= NUMA_LDS_CLASSES) {
+      const uint4 *src = reinterpret_cast<const uint4 *>(d.nu.cls);
+      for (int32_t x = threadIdx.x; x < d.nu.ncls * (int32_t)(sizeof(DevNumaClass) / 16); x += 256) scan_cls[x] = src[x];
+      __syncthreads();
+      cls = reinterpret_cast<const DevNumaClass *>(scan_cls);
+    }
+  }
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int32_t chunk = cq * 4 + wave;
+  const int32_t p0 = pg * ppw, p1 = min(p0 + ppw, n_pods);
+  if (chunk >= nchunks || p0 >= p1) return;  // wave-uniform, no barrier follows
+  // the union of the group's needs: lane j evaluates pod p0 + j's needs (one
+  // round of vector loads instead of a chain of dependent scalar loads), the
+  // packed bits are OR-reduced across the wave
+  uint32_t nb = 0;
+  if (lane < p1 - p0) {
+    // the whole record in six 16-B loads issued together (pod_needs reads its
+    // fields under short-circuit conditions: field-wise loads would chain)
+    const uint4 *q = reinterpret_cast<const uint4 *>(pods + p0 + lane);
+    uint4 t[sizeof(DevPod) / 16];
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(DevPod) / 16); k++) t[k] = q[k];
+    DevPod pl;
+    __builtin_memcpy(&pl, t, sizeof(DevPod));
+    nb = need_pack(pod_needs(pl, c));
+  }
+  const Need need = need_unpack(wave_or_u32(nb));
+  const int32_t c0 = lo + chunk * (64 * R);
+  NV v[R];
+  side_row_t<NM> nr[R];
+  bool in[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int32_t i = c0 + r * 64 + lane;
+    in[r] = i < hi;
+    const int32_t ii = in[r] ? i : hi - 1;  // out-of-range lanes evaluate a valid row, stored nowhere
+    load_node(v[r], d, ii, need, c);
+    if constexpr (NM == 3) {
+      load_numa<false>(nr[r], d, ii, need);
+      load_resv(nr[r], d.rv, ii);
+    } else if constexpr (NM != 0) {
+      load_numa<NM == 2>(nr[r], d, ii, need);
+    }
+  }
+  // pod records in SGPRs, the next one's scalar loads issued before this
+  // pod's evaluation so their latency hides behind it
+  DevPod nxt = pods[p0];
+  for (int32_t p = p0; p < p1; p++) {
+    const DevPod pod = nxt;
+    nxt = pods[min(p + 1, p1 - 1)];
+    uint16_t *row = S + (size_t)p * s_stride;
+    int32_t s[R];
+    if constexpr (NM != 0) {
+      const Need pn = pod_needs(pod, c);
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        side_row_t<NM> w = nr[r];
+        numa_view<NM == 2>(w, pn);
+        if constexpr (NM == 3)
+          s[r] = eval_total_resv(pod, v[r], w, cls, c) + 1;
+        else
+          s[r] = eval_total_numa<NM == 2>(pod, v[r], w, cls, c) + 1;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; r++) s[r] = eval_total(pod, v[r], c) + 1;
+    }
+    int32_t mx = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      s[r] = in[r] ? s[r] : 0;
+      if (in[r]) col(row, c0 + r * 64 + lane - lo) = (uint16_t)s[r];
+      mx = max(mx, s[r]);
+    }
+    mx = wave_max_i32_dpp(mx);
+    if (lane == 0) Mx[(size_t)p * m_stride + chunk] = (uint16_t)mx;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_select: one workgroup per pod, the exact top-k of its score row.
 //
 // Keys order by (score desc, node asc), i.e. the reference's selectHost with
@@ -2224,15 +2392,44 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const DevPod *po
 
 int32_t scan_chunks(int R, int32_t lo, int32_t hi) { return hi > lo ? (hi - lo + 64 * R - 1) / (64 * R) : 0; }
 
+int32_t scan_ppw(int R, int32_t lo, int32_t hi, int32_t n_pods) {
+  const int32_t nq = (scan_chunks(R, lo, hi) + 3) / 4;
+  if (nq <= 0 || n_pods <= 0) return 1;
+  // ~2048 waves (2 per SIMD) over nq chunk quads x 4 waves
+  const int32_t groups = std::max(1, std::min(n_pods, (2048 + 4 * nq - 1) / (4 * nq)));
+  return (n_pods + groups - 1) / groups;
+}
+
 hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t lo,
-                       int32_t hi, uint16_t *S, int64_t s_stride, uint16_t *Mx, int32_t m_stride, hipStream_t s) {
+                       int32_t hi, uint16_t *S, int64_t s_stride, uint16_t *Mx, int32_t m_stride, int32_t ppw,
+                       hipStream_t s) {
   if (n_pods <= 0 || hi <= lo) return hipSuccess;
   const int nm = side_mode(c);
   const bool numa = nm != 0;
   const int32_t nchunks = scan_chunks(R, lo, hi);
+  const size_t lds = (numa && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0;
+  if (ppw > 0 && R <= 2) {  // node-major (k_scan_nm)
+    const int32_t cqx = ((nchunks + 3) / 4 + 7) / 8;
+    const int32_t nblocks = 8 * cqx * ((n_pods + ppw - 1) / ppw);
+#define KH_SCAN_NM(RR, NN)                                                                                          \
+  hipLaunchKernelGGL((k_scan_nm<RR, NN>), dim3(nblocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cqx, \
+                     ppw, S, s_stride, Mx, m_stride)
+    switch (nm * 2 + (R - 1)) {
+      case 0: KH_SCAN_NM(1, 0); break;
+      case 1: KH_SCAN_NM(2, 0); break;
+      case 2: KH_SCAN_NM(1, 1); break;
+      case 3: KH_SCAN_NM(2, 1); break;
+      case 4: KH_SCAN_NM(1, 2); break;
+      case 5: KH_SCAN_NM(2, 2); break;
+      case 6: KH_SCAN_NM(1, 3); break;
+      case 7: KH_SCAN_NM(2, 3); break;
+      default: return hipErrorInvalidValue;
+    }
+#undef KH_SCAN_NM
+    return hipGetLastError();
+  }
   const int32_t cpx = (nchunks + 7) / 8;
   const int32_t blocks = 8 * cpx * ((n_pods + 3) / 4);
-  const size_t lds = (numa && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0;
 #define KH_SCAN(RR, NN)                                                                                            \
   hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, S, \
                      s_stride, Mx, m_stride)

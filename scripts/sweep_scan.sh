@@ -1,14 +1,14 @@
 #!/bin/bash
 # k_scan pods-per-wave / nodes-per-lane sweep (bench only).
-# Usage: scripts/sweep_scan.sh OUTDIR WORKLOAD "R:PPW ..."   (PPW 0 = automatic)
+# Usage: scripts/sweep_scan.sh OUTDIR WORKLOAD "R:PPW ..."   (PPW a = automatic node-major, 0 = pod-major k_scan)
 set -u
 out=gpurun_out/${1:-scan_sweep}
 w=${2:-config4}
 mkdir -p $out
-for rp in ${3:-"1:1 1:4 1:0 2:1 2:4 2:0"}; do
+for rp in ${3:-"2:a 2:0 1:a 2:4 2:8"}; do
   r=${rp%%:*}; ppw=${rp##*:}
   tag=${w}_r${r}_p${ppw}
-  if [ $ppw = 0 ]; then unset KOORDHIP_SCAN_PPW; else export KOORDHIP_SCAN_PPW=$ppw; fi
+  if [ $ppw = a ]; then export KOORDHIP_SCAN_PPW=auto; else export KOORDHIP_SCAN_PPW=$ppw; fi
   KOORDHIP_TOPK_R=$r timeout -k 10 300 python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline \
     > $out/$tag.json 2> $out/$tag.err || { echo "failed $tag"; exit 1; }
   python - "$out/$tag.json" "$tag" <<'PY'

@@ -9,6 +9,10 @@ pods, 30% BE, shipped profile) and writes
   tests/golden/stream_config4.npz   placements (int32 [100000]), and sha256
                                      digests of the generated inputs and of
                                      every final mutable node column
+  tests/golden/stream_config5.npz   the same for config 5 (200k nodes with
+                                     reservations + NUMA): also the digests of
+                                     the final NUMA / reservation columns and
+                                     of the pods' cpusets
 
 so the GPU tests (tests/test_gpu_fullsize.py) can compare libkoordhip.so's
 full-size stream bit for bit without re-running a ~6-minute oracle on the box.
@@ -54,14 +58,25 @@ def main():
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--threads", type=int, default=1)
     args = ap.parse_args()
-    prof = shipped_profile(numa=bool(synth.CONFIGS[args.config].get("numa")))
+    cc = synth.CONFIGS[args.config]
+    prof = shipped_profile(numa=bool(cc.get("numa")), reservation=bool(cc.get("reservation")))
     table, pods = synth.config_workload(args.config, prof)
     cfg = to_c_config(prof)
     o = oracle.Oracle(cfg, table)
     t = time.time()
-    out = o.place_stream(pods, threads=args.threads)
+    numa = bool(cc.get("numa"))
+    cpus = None
+    if numa:
+        out, cpus = o.place_stream(pods, threads=args.threads, cpusets=True)
+    else:
+        out = o.place_stream(pods, threads=args.threads)
     dt = time.time() - t
     st = o.state()
+    if numa:
+        st.update({"numa." + k: v for k, v in o.numa_state().items()})
+        st["__cpusets__"] = cpus
+    if cc.get("reservation"):
+        st.update({"resv." + k: v for k, v in o.resv_state().items()})
     ind = input_digests(table, pods)
     sd = state_digests(st)
     path = os.path.join(HERE, f"stream_config{args.config}.npz")

@@ -249,10 +249,36 @@ def test_sharded_group_bit_exact(Engine, world, n_nodes, n_pods, be, batch):
             assert np.array_equal(s[k], rs[k]), k
 
 
+@pytest.mark.parametrize("numa,n_nodes,n_pods", [(False, 3000, 1200), (True, 600, 700)])
+def test_rccl_one_rank_exchange(Engine, numa, n_nodes, n_pods):
+    """koordhip_comm_init with world 1: a real one-rank RCCL communicator, so
+    every round goes through the multi-GPU exchange path on this GPU
+    (ncclAllGather of the lists on the engine stream, k_topk_merge, the
+    per-round list signal, the lag-1 persistent resolve over the merged lists)
+    and must place exactly like the oracle."""
+    prof = shipped_profile(numa=numa)
+    table = synth.make_cluster(synth.ClusterSpec(n_nodes), prof)
+    if numa:
+        synth.add_numa(table, synth.NumaSpec(), prof)
+    pods = synth.make_pods(synth.StreamSpec(n_pods, be_frac=0.3, cpuset_frac=0.4 if numa else 0.0), prof)
+    with Engine(prof, device=0) as e:
+        e.comm_init(Engine.comm_unique_id(), 1, 0)
+        e.load_snapshot(table)
+        got = e.place_stream(pods)
+        again = e.place_stream(pods[: n_pods // 3])
+    o = oracle.Oracle(to_c_config(prof), table)
+    ref = o.place_stream(pods)
+    assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
+    o2 = oracle.Oracle(to_c_config(prof), table)
+    o2.place_stream(pods)
+    ref2 = o2.place_stream(pods[: n_pods // 3])
+    assert np.array_equal(again, ref2)
+
+
 # ----------------------------------------------------------- launch modes
 @pytest.mark.parametrize("mode", ["KOORDHIP_ROUND_LAUNCH", "KOORDHIP_SERIAL", "KOORDHIP_CU_RESERVE", "KOORDHIP_ONE_EVAL_STREAM", "KOORDHIP_NO_KEY_TABLES",
                                   "KOORDHIP_FOLD_WAIT", "KOORDHIP_SELECT_ONEWG", "KOORDHIP_LAG1",
-                                  "KOORDHIP_TOPK_R=1"])
+                                  "KOORDHIP_TOPK_R=1", "KOORDHIP_SCAN_PPW=auto", "KOORDHIP_SCAN_PPW=3"])
 @pytest.mark.parametrize("numa", [False, True])
 def test_launch_modes_bit_exact(Engine, monkeypatch, mode, numa):
     """The per-round resolve launch (local groups), the single-stream
