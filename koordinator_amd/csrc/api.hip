@@ -40,7 +40,7 @@ int fail(int code, const std::string &msg) {
     if (_r != ncclSuccess) return fail(KOORDHIP_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
   } while (0)
 
-constexpr int kDefaultBatch = 32;
+constexpr int kDefaultBatch = 24;  // config-4 round-size sweep: 24 best (970k pods/s vs 911k at 32)
 constexpr int kDefaultBatchNuma = 16;
 constexpr int32_t kMaxNodes = 400000;  // the resolve keeps a per-node bit in LDS (next to 2 x 64 x 128 list keys)
 constexpr int kMaxBatch = 64;
@@ -1293,7 +1293,7 @@ int place_staged_impl(koordhip_ctx *c) {
   // (NodeNUMAResource streams are bound by the resolve's cpuset Reserve: the
   // longer re-evaluated set of lag 2 measured slower there, 87k vs 93k pods/s)
   int32_t lag = (two && !c->side && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
-  if (lag == 2 && 3 * P > kh::kResolveMaxK) lag = 1;
+  if (lag == 2 && (3 * P > kh::kResolveMaxK || 2 * P > kMaxBatch)) lag = 1;  // M' spans 2 rounds <= 64 slots
   const int nm = kh::side_mode(c->dc);
   while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, nm, lag) > 157 * 1024) P--;
   const int32_t K = (lag + 1) * P;

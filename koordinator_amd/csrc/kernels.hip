@@ -1599,63 +1599,111 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   // load-store pair per iteration serialised ~40 HBM round trips.
   auto load_round = [&](int32_t rr, int32_t rp0, int32_t rn, uint64_t *Lk, DevPod *Lp, NV *Pr, NR *Pn,
                         int32_t *Pnode, int32_t tid, int32_t nth) {
+    // Issue order keeps the HBM round trips few for wave 1 alone (one
+    // load-store pair per iteration serialised ~40 of them): the list-head
+    // entries with the first batch of list loads (16-B vectors of the dense
+    // [rn][k] global lists), then the head rows' column loads while the
+    // remaining list batches stream in.
     const uint64_t *L = lists0 + (size_t)(rr & (2 * lag - 1)) * list_buf;
-    const int32_t tot = rn * kp;
-    for (int32_t x0 = tid; x0 < tot; x0 += 8 * nth) {
-      uint64_t v[8];
+    const int32_t tot = rn * k;
+    int32_t nd[2];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int32_t x = x0 + u * nth;
-        const int32_t j = x / kp, q = x - j * kp;
-        v[u] = (x < tot && q < k) ? L[(size_t)j * k + q] : 0ull;
+    for (int u = 0; u < 2; u++) {
+      const int32_t sl = tid + u * nth, j = sl / HP, q = sl - j * HP;
+      nd[u] = -1;
+      if (sl < RES_PRE && j < rn && q < k) {
+        const uint64_t e = L[(size_t)j * k + q];
+        if (e != 0) nd[u] = key_node(e);
       }
+    }
+    constexpr int LB = 4;  // 16-B list loads in flight per thread (more: the kernel spills)
+    const uint4 *L4 = reinterpret_cast<const uint4 *>(L);  // list buffers are 16-B aligned
+    const int32_t n16 = (tot + 1) >> 1;
+    auto put = [&](int32_t e, uint64_t v) {
+      if (e < tot) {
+        const int32_t j = e / k, q = e - j * k;
+        Lk[j * kp + q] = v;
+      }
+    };
+    uint4 lv[LB];
 #pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (x0 + u * nth < tot) Lk[x0 + u * nth] = v[u];
+    for (int u = 0; u < LB; u++)
+      if (tid + u * nth < n16) lv[u] = L4[tid + u * nth];
+#pragma unroll
+    for (int u = 0; u < LB; u++) {
+      const int32_t x = tid + u * nth;
+      if (x < n16) {
+        put(2 * x, ((uint64_t)lv[u].y << 32) | lv[u].x);
+        put(2 * x + 1, ((uint64_t)lv[u].w << 32) | lv[u].z);
+      }
+    }
+    NV v[2];  // (issued after the first list batch's stores: both at once spill)
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+      if (nd[u] >= 0) load_row(v[u], nodes(), nd[u]);
+    for (int32_t x0 = tid + LB * nth; x0 < n16; x0 += LB * nth) {  // rounds whose lists exceed one batch
+#pragma unroll
+      for (int u = 0; u < LB; u++)
+        if (x0 + u * nth < n16) lv[u] = L4[x0 + u * nth];
+#pragma unroll
+      for (int u = 0; u < LB; u++) {
+        const int32_t x = x0 + u * nth;
+        if (x < n16) {
+          put(2 * x, ((uint64_t)lv[u].y << 32) | lv[u].x);
+          put(2 * x + 1, ((uint64_t)lv[u].w << 32) | lv[u].z);
+        }
+      }
+    }
+    for (int32_t x = tid; x < rn * (kp - k); x += nth) {  // zero padding of each row up to kp
+      const int32_t j = x / (kp - k), q = k + x - j * (kp - k);
+      Lk[j * kp + q] = 0ull;
     }
     {
       const uint4 *src = reinterpret_cast<const uint4 *>(pods + rp0);
       uint4 *dst = reinterpret_cast<uint4 *>(Lp);
-      const int32_t n16 = rn * (int32_t)(sizeof(DevPod) / 16);
-      for (int32_t x0 = tid; x0 < n16; x0 += 4 * nth) {
-        uint4 v[4];
+      const int32_t p16 = rn * (int32_t)(sizeof(DevPod) / 16);
+      for (int32_t x0 = tid; x0 < p16; x0 += 8 * nth) {
+        uint4 pv[8];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (x0 + u * nth < n16) v[u] = src[x0 + u * nth];
+        for (int u = 0; u < 8; u++)
+          if (x0 + u * nth < p16) pv[u] = src[x0 + u * nth];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (x0 + u * nth < n16) dst[x0 + u * nth] = v[u];
+        for (int u = 0; u < 8; u++)
+          if (x0 + u * nth < p16) dst[x0 + u * nth] = pv[u];
       }
     }
-    for (int32_t s0 = tid; s0 < RES_PRE; s0 += 2 * nth) {
-      int32_t nd[2];
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
-        const int32_t sl = s0 + u * nth, j = sl / HP, q = sl - j * HP;
-        nd[u] = -1;
-        if (sl < RES_PRE && j < rn && q < k) {
-          const uint64_t e = L[(size_t)j * k + q];
-          if (e != 0) nd[u] = key_node(e);
+    for (int u = 0; u < 2; u++) {
+      const int32_t sl = tid + u * nth;
+      if (sl >= RES_PRE) continue;
+      if (nd[u] >= 0) {
+        Pr[sl] = v[u];
+        if constexpr (NUMA) {
+          NR rr2;
+          load_side_row<NM>(rr2, nodes(), nd[u]);
+          Pn[sl] = rr2;
         }
       }
-      NV v[2];
-#pragma unroll
-      for (int u = 0; u < 2; u++)
-        if (nd[u] >= 0) load_row(v[u], nodes(), nd[u]);
-#pragma unroll
-      for (int u = 0; u < 2; u++) {
-        const int32_t sl = s0 + u * nth;
-        if (sl >= RES_PRE) continue;
-        if (nd[u] >= 0) {
-          Pr[sl] = v[u];
-          if constexpr (NUMA) {
-            NR rr2;
-            load_side_row<NM>(rr2, nodes(), nd[u]);
-            Pn[sl] = rr2;
-          }
-        }
-        Pnode[sl] = nd[u];
+      Pnode[sl] = nd[u];
+    }
+    for (int32_t sl = tid + 2 * nth; sl < RES_PRE; sl += nth) {  // more head slots than 2 per thread (never with 64+ threads)
+      const int32_t j = sl / HP, q = sl - j * HP;
+      int32_t n1 = -1;
+      if (j < rn && q < k) {
+        const uint64_t e = L[(size_t)j * k + q];
+        if (e != 0) n1 = key_node(e);
       }
+      if (n1 >= 0) {
+        NV v1;
+        load_row(v1, nodes(), n1);
+        Pr[sl] = v1;
+        if constexpr (NUMA) {
+          NR rr2;
+          load_side_row<NM>(rr2, nodes(), n1);
+          Pn[sl] = rr2;
+        }
+      }
+      Pnode[sl] = n1;
     }
   };
   // M slot of node nd, -1 when nd is not in M
