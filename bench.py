@@ -259,7 +259,7 @@ def main():
     #      pod loop), + the u16 score-matrix row per (pod, node) + chunk maxima
     b_eval = bytes_per_eval(pods, cfg)
     scan_us = ks["scan_ms"] * 1e3 / max(ks["scan_launches"], 1)
-    evals_per_launch = ks["evals"] / max(ks["scan_launches"], 1)
+    evals_per_launch = ks["evals"] / max(ks["rounds"], 1)   # one scan launch per round (the timed ones are a sample)
     pods_per_round = evals_per_launch / max(args.nodes, 1)
     col_bytes = float(b_eval.max()) * args.nodes
     phys = col_bytes + pods_per_round * args.nodes * 2 + pods_per_round * args.nodes / 64 * 2

@@ -361,6 +361,9 @@ int koordhip_last_stats(koordhip_ctx *ctx, double *eval_ms, int64_t *eval_launch
  * sequential resolve (k_resolve; one persistent launch per call unless the
  * context is in a local group).  Roofline accounting in bench.py. */
 typedef struct koordhip_kernel_stats {
+  /* *_ms / *_launches: the timed launches only -- a persistent pipeline times
+   * the evaluation launches of ~256 evenly spaced rounds (their averages are
+   * what the sample is for); `rounds` counts every round */
   double scan_ms;
   int64_t scan_launches;
   double select_ms;

@@ -369,6 +369,9 @@ int build_numa_class(const koordhip_numa_class &t, kh::DevNumaClass &o) {
       return fail(KOORDHIP_EINVAL, "NUMA topology class: more than 8 NUMA nodes / sockets");
     if (p % cpc != 0 && (t.node_of[p - 1] != k || t.socket_of[p - 1] != sck))
       return fail(KOORDHIP_EINVAL, "NUMA topology class: a core spans NUMA nodes");
+    // the resolve's lane-parallel spread take relies on it (numa.hpp acc_take_spread_by_id)
+    if (p % cpc != 0 && t.cpu_id[p - 1] >= t.cpu_id[p])
+      return fail(KOORDHIP_EINVAL, "NUMA topology class: positions inside a core must ascend by CPU id");
     nn = std::max(nn, k + 1);
     ns = std::max(ns, sck + 1);
     o.nm[k][p >> 6] |= 1ull << (p & 63);

@@ -626,7 +626,9 @@ __device__ __forceinline__ void store_row(const NV &v, const DevNodes &d, int32_
 // (Allocate, resource_manager.go:142-164) and, on a topology-policy node, the
 // hinted zones' amounts (resourceManager.Update, node_allocation.go:76-103).
 // false = Allocate fails (nothing applied).
-template <bool Z>
+// WAVE: called by every lane of one wave with the same inputs (the resolve's
+// Reserve): the accumulator's CPU-id ordered takes run lane-parallel.
+template <bool Z, bool WAVE = false>
 __device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *classes, NumaRow &row, const DevPod &pod,
                                                        uint64_t *cpus_out) {
   // registers for the whole replay (the references point at the caller's stack)
@@ -640,7 +642,7 @@ __device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *class
   if (r.cls < 0) return false;
   const DevNumaClass &C = classes[r.cls];
   if (!Z || tp == 0) {
-    if (!numa_allocate_in(C, r, p, cpus)) return false;
+    if (!numa_allocate_in<WAVE>(C, r, p, cpus)) return false;
     numa_apply(r, p, cpus, +1);
   } else {
     uint32_t mask;
@@ -648,7 +650,7 @@ __device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *class
     double z[2][ZMAX];
     if (mask && !zone_alloc(C.nnuma, r, p, mask, z)) return false;
     if (cs) {
-      if (!(mask ? zone_allocate_in(C, r, p, z, cpus) : numa_allocate_in(C, r, p, cpus))) return false;
+      if (!(mask ? zone_allocate_in(C, r, p, z, cpus) : numa_allocate_in<WAVE>(C, r, p, cpus))) return false;
       numa_apply(r, p, cpus, +1);
     }
     if (mask) {

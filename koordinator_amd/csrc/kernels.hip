@@ -2116,10 +2116,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               uint64_t mc[NW] = {0, 0, 0, 0};
               int okl = 0;
               const uint64_t t_acc = dbg ? stamp() : 0;
-              if (lane == 0) {
+              {  // every lane: the accumulator's id-ordered takes run lane-parallel
                 NR nr = *snr;
-                okl = numa_reserve<ZONES>(cls, nr, pod, mc);
-                if (okl) mnr[rw] = nr;
+                okl = numa_reserve<ZONES, true>(cls, nr, pod, mc);
+                if (okl && lane == 0) mnr[rw] = nr;
               }
               if (dbg) {
                 const int b = KOORDHIP_NUMA_PREFERRED(pod.numa_policy) == KOORDHIP_CPUBIND_SPREAD_BY_PCPUS ? 2 : 0;

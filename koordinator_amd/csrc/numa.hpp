@@ -315,17 +315,84 @@ __device__ __forceinline__ void acc_take1(const DevNumaClass &C, Acc &a, int p) 
   a.need--;
 }
 
+// take every position of T at once: the result, the available set, the
+// exclusivity state and `need` are order-free functions of the taken set,
+// so this equals acc_take1 over T's positions in any order
+__device__ __forceinline__ void acc_take_mask(const DevNumaClass &C, Acc &a, const uint64_t *T) {
+  int n = 0;
+  for (int w = 0; w < NW; w++) {
+    a.R[w] |= T[w];
+    a.A[w] &= ~T[w];
+    n += __popcll(T[w]);
+  }
+  if (a.excl == (int)KOORDHIP_CPUEXCL_PCPU)
+    for (int w = 0; w < NW; w++) a.XC[w] |= fold_or(T[w], C.cpc);
+  if (a.excl == (int)KOORDHIP_CPUEXCL_NUMA)
+    for (int k = 0; k < C.nnuma; k++)
+      if (popc_and(T, C.nm[k])) a.XN |= 1u << k;
+  a.need -= n;
+}
+
+// the lowest k set bits of x (binary search on prefix popcounts)
+__device__ __forceinline__ uint64_t low_bits(uint64_t x, int k) {
+  if (k <= 0) return 0ull;
+  if (k >= __popcll(x)) return x;
+  int lo = 0;  // popc(x & mask(lo)) < k, mask(t) = bits [0, t)
+  for (int st = 32; st; st >>= 1) {
+    const int t = lo + st;
+    if (__popcll(x & (t >= 64 ? ~0ull : ((1ull << t) - 1ull))) < k) lo = t;
+  }
+  const int t = lo + 1;
+  return x & (t >= 64 ? ~0ull : ((1ull << t) - 1ull));
+}
+
 // take the lowest n positions of m
 __device__ __forceinline__ void acc_take_low(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
-  for (int w = 0; w < NW && n > 0; w++) {
-    uint64_t x = m[w];
-    while (x && n > 0) {
-      const int b = __builtin_ctzll(x);
-      x &= x - 1;
-      acc_take1(C, a, w * 64 + b);
-      n--;
-    }
+  uint64_t T[NW];
+  for (int w = 0; w < NW; w++) {
+    T[w] = low_bits(m[w], n);
+    n -= __popcll(T[w]);
   }
+  acc_take_mask(C, a, T);
+}
+
+// ---- WAVE = true: the replay runs in every lane of one wave with the same
+// inputs (the resolve's Reserve); the CPU-id ordered takes then split the ids
+// over the lanes and combine with ballots instead of walking them one by one.
+__device__ __forceinline__ uint64_t acc_wave_or(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  for (int m = 1; m < 64; m <<= 1) {
+    lo |= (uint32_t)__shfl_xor((int)lo, m, 64);
+    hi |= (uint32_t)__shfl_xor((int)hi, m, 64);
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t word_of(const uint64_t *S, int w) {
+  return w == 0 ? S[0] : (w == 1 ? S[1] : (w == 2 ? S[2] : S[3]));
+}
+// T |= the n positions of S with the smallest CPU ids (every lane, same inputs)
+__device__ __forceinline__ void acc_first_by_id(const DevNumaClass &C, const uint64_t *S, int n, uint64_t *T) {
+  if (n <= 0) return;
+  const int lane = __lane_id();
+  uint64_t t[NW] = {0, 0, 0, 0};
+  int taken = 0;
+  for (int base = 0; base < C.ncpu && taken < n; base += 64) {
+    const int i = base + lane;
+    const int p = i < C.ncpu ? (int)C.pos_by_id[i] : 0;
+    const bool in = i < C.ncpu && ((word_of(S, p >> 6) >> (p & 63)) & 1ull);
+    const uint64_t b = __ballot(in);
+    const int rank = taken + __popcll(b & ((1ull << lane) - 1ull));
+    if (in && rank < n) {
+      const uint64_t bit = 1ull << (p & 63);
+      const int w = p >> 6;
+      t[0] |= w == 0 ? bit : 0ull;
+      t[1] |= w == 1 ? bit : 0ull;
+      t[2] |= w == 2 ? bit : 0ull;
+      t[3] |= w == 3 ? bit : 0ull;
+    }
+    taken += __popcll(b);
+  }
+  for (int w = 0; w < NW; w++) T[w] |= acc_wave_or(t[w]);
 }
 
 // the accumulator's exclusion mask for filterExclusive passes
@@ -343,7 +410,25 @@ __device__ __forceinline__ void acc_excluded(const DevNumaClass &C, const Acc &a
 // spread order of the CPUs of m listed in ascending CPU id (freeCPUsInNode /
 // freeCPUsInSocket + spreadCPUs): round t takes each core's t-th CPU by id,
 // rounds in id order; lists of <= cpc CPUs are kept in id order.  Takes n.
+// WAVE: the order is (round, id) with round 1 = the second CPU of a core whose
+// first is in m too -- positions ascend by id inside a core (build_numa_class
+// checks it), so that is the odd position of a core with both bits in m.
+template <bool WAVE = false>
 __device__ __forceinline__ void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
+  if constexpr (WAVE) {
+    if (n <= 0) return;
+    uint64_t S0[NW], S1[NW], T[NW];
+    for (int w = 0; w < NW; w++) {
+      S1[w] = C.cpc == 2 ? (m[w] & (m[w] << 1) & 0xAAAAAAAAAAAAAAAAull) : 0ull;
+      S0[w] = m[w] & ~S1[w];
+      T[w] = 0ull;
+    }
+    const int n0 = popc4(S0);
+    acc_first_by_id(C, S0, min(n, n0), T);
+    if (n > n0) acc_first_by_id(C, S1, n - n0, T);
+    acc_take_mask(C, a, T);
+    return;
+  }
   int len = popc4(m);
   if (len <= C.cpc) {
     for (int i = 0; i < C.ncpu && n > 0; i++) {
@@ -476,6 +561,7 @@ __device__ __forceinline__ void go118_sort_by_count(int *ord, int *cnt, int n, b
 }
 
 // takeCPUs; returns true with a.R filled.
+template <bool WAVE = false>
 __device__ __forceinline__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int policy) {
   if (a.need < 1) return true;
   if (a.need > popc4(a.A)) return false;
@@ -601,9 +687,9 @@ __device__ __forceinline__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int
               const uint64_t any = fold_or(T[w], cpc);
               E[w] = cpc == 1 ? T[w] : ((T[w] & 0x5555555555555555ull) | ((any & ~T[w]) << 1));
             }
-            acc_take_spread_by_id(C, a, E, a.need);
+            acc_take_spread_by_id<WAVE>(C, a, E, a.need);
           } else {
-            acc_take_spread_by_id(C, a, T, a.need);
+            acc_take_spread_by_id<WAVE>(C, a, T, a.need);
           }
           return true;
         }
@@ -631,9 +717,9 @@ __device__ __forceinline__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int
               const uint64_t any = fold_or(T[w], cpc);
               E[w] = cpc == 1 ? T[w] : ((T[w] & 0x5555555555555555ull) | ((any & ~T[w]) << 1));
             }
-            acc_take_spread_by_id(C, a, E, a.need);
+            acc_take_spread_by_id<WAVE>(C, a, E, a.need);
           } else {
-            acc_take_spread_by_id(C, a, T, a.need);
+            acc_take_spread_by_id<WAVE>(C, a, T, a.need);
           }
           return true;
         }
@@ -647,6 +733,7 @@ __device__ __forceinline__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int
 }
 
 // takeCPUs over the available set A (cpu_accumulator.go:87-232) into out[]
+template <bool WAVE = false>
 __device__ __forceinline__ bool acc_run(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
                                                   const uint64_t *A, int need, uint64_t *out) {
   Acc a;
@@ -662,7 +749,7 @@ __device__ __forceinline__ bool acc_run(const DevNumaClass &C, const NumaRow &r,
   a.excl = (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy);
   a.most = (r.nflags & KOORDHIP_NODE_NUMA_MOST_ALLOCATED) ? 1 : 0;
   const int pol = node_policy(r.nflags, (int)KOORDHIP_NUMA_PREFERRED(p.numa_policy));
-  const bool ok = acc_take_cpus(C, a, pol);
+  const bool ok = acc_take_cpus<WAVE>(C, a, pol);
   for (int w = 0; w < NW; w++) out[w] = a.R[w];
   return ok;
 }
@@ -680,12 +767,13 @@ __device__ __forceinline__ bool required_ok(const DevNumaClass &C, const NumaRow
 }
 
 // Allocate for Reserve: exact CPUs into cpus[]; false = Allocate fails.
+template <bool WAVE = false>
 __device__ __forceinline__ bool numa_allocate_in(const DevNumaClass &C, const NumaRow &r, const DevPod &p, uint64_t *cpus) {
   for (int w = 0; w < NW; w++) cpus[w] = 0;
   const int need = p.numa_cpus;
   if (popc4(r.fr) < need) return false;
   uint64_t R[NW];
-  if (!acc_run(C, r, p, r.fr, need, R)) return false;
+  if (!acc_run<WAVE>(C, r, p, r.fr, need, R)) return false;
   if (!required_ok(C, r, p, R)) return false;
   for (int w = 0; w < NW; w++) cpus[w] = R[w];
   return true;

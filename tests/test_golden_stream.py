@@ -1,4 +1,4 @@
-"""The committed config-4 golden placements (tests/golden/make_stream_golden.py)
+"""The committed config-4 / config-5 golden placements (tests/golden/make_stream_golden.py)
 still describe this generator and this oracle: the synthetic inputs hash to
 the recorded digests, and a prefix of the stream re-run through the oracle
 reproduces the recorded placements."""
@@ -44,3 +44,18 @@ def test_golden_inputs_and_prefix():
     assert g["placements"].shape == (100000,) and (g["placements"] >= 0).all()
     ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods[:300])
     assert np.array_equal(ref, g["placements"][:300])
+
+
+def test_golden_config5_inputs_and_prefix():
+    """config 5 (200k nodes with reservations + NUMA): the inputs hash to the
+    fixture's digests and the oracle reproduces a prefix of its placements."""
+    g = np.load(os.path.join(os.path.dirname(GOLDEN), "stream_config5.npz"))
+    prof = shipped_profile(numa=True, reservation=True)
+    table, pods = synth.config_workload(5, prof)
+    want = dict(zip(g["input_keys"].tolist(), g["input_sha"].tolist()))
+    got = {c: _sha(table[c]) for c in table.cols if c in want}
+    got["__pods__"] = _sha(pods)
+    assert got == want
+    assert g["placements"].shape == (100000,)
+    ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods[:40])
+    assert np.array_equal(ref, g["placements"][:40])

@@ -1,8 +1,9 @@
 """Full-size parity of the BASELINE configurations through libkoordhip.so.
 
-* config 4 (the headline: 50k nodes x 100k pods) against committed golden
-  placements + final-state digests (tests/golden/make_stream_golden.py ran the
-  oracle on the exact bench.py workload);
+* config 4 (the headline: 50k nodes x 100k pods) and config 5 (200k nodes
+  with reservations + NUMA x 100k pods) against committed golden placements +
+  final-state digests (tests/golden/make_stream_golden.py ran the oracle on
+  the exact bench.py workloads);
 * config 2 (5k x 10k) and config 3 (5k 2-socket nodes x 10k pods with
   NodeNUMAResource cpusets) against the live oracle;
 * the size-dependent launch shapes the small streams never reach: the split
@@ -91,6 +92,34 @@ def test_config4_repeated_steps_identical(Engine):
             e.place_staged()
             got = e.fetch_placements(len(pods))
             assert np.array_equal(got, g["placements"]), _first_diff(got, g["placements"])
+
+
+def test_config5_stream_matches_golden(Engine):
+    """BASELINE config 5: 200k nodes (10% holding an Available Reservation) x
+    100k pods (20% matching a reservation owner), Fit + LoadAware +
+    NodeNUMAResource + Reservation: every placement and the digests of every
+    final node / NUMA / reservation column equal the oracle's (fixture made by
+    tests/golden/make_stream_golden.py --config 5, ~45 min of oracle time)."""
+    g = np.load(os.path.join(GOLDEN, "stream_config5.npz"))
+    prof = shipped_profile(numa=True, reservation=True)
+    table, pods = synth.config_workload(5, prof)
+    want_in = dict(zip(g["input_keys"].tolist(), g["input_sha"].tolist()))
+    got_in = {c: _sha(table[c]) for c in table.cols if c in want_in}
+    got_in["__pods__"] = _sha(pods)
+    assert got_in == want_in
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(table)
+        got = e.place_stream(pods)
+        cpus = e.fetch_cpusets(len(pods))
+        state = e.read_nodes()
+        state.update({"numa." + k: v for k, v in e.read_numa().items()})
+        state.update({"resv." + k: v for k, v in e.read_reservations().items()})
+    state["__cpusets__"] = cpus
+    ref = g["placements"]
+    assert len(got) == 100000 and table.n == 200000
+    assert np.array_equal(got, ref), _first_diff(got, ref)
+    want_st = dict(zip(g["state_keys"].tolist(), g["state_sha"].tolist()))
+    assert {k: _sha(state[k]) for k in want_st} == want_st
 
 
 def test_config2_full_stream(Engine):
