@@ -1330,7 +1330,7 @@ __device__ __forceinline__ NV slot_row(const NV &src) {
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
-      dec_key, dec_n, dec_src, dec_e, moved, mhash, gbits, kpre, ktab, ready, classes, modmap, total;
+      dec_key, dec_n, dec_src, dec_e, dec_c, moved, mhash, gbits, kpre, ktab, ready, classes, modmap, total;
   // second copies of the per-round inputs, filled by waves 1.. while wave 0
   // resolves the previous round (overlap = 0: every round loads serially)
   int32_t overlap, lists2, pods2, pre_rows2, pre_numa2, pre_node2;
@@ -1378,6 +1378,8 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * 4;
   o.dec_e = at;
   at += RES_MAXP_ROUND * RES_WE * 4;
+  o.dec_c = at;  // per pod: bit 0 = its walk met an earlier pod's staged winner, bit 1 = general path only
+  at += RES_MAXP_ROUND * 4;
   o.moved = at;  // per M' slot: committed to again this round (its row moved into M)
   at += RES_MAXP_ROUND * 4;
   o.mhash = at;  // M node -> M slot (open addressing, RES_MHASH keys then slots)
@@ -1502,6 +1504,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   int32_t *dec_n = reinterpret_cast<int32_t *>(lds + ofs.dec_n);
   int32_t *dec_src = reinterpret_cast<int32_t *>(lds + ofs.dec_src);
   int32_t *dec_e = reinterpret_cast<int32_t *>(lds + ofs.dec_e);
+  int32_t *dec_c = reinterpret_cast<int32_t *>(lds + ofs.dec_c);
   int32_t *moved = reinterpret_cast<int32_t *>(lds + ofs.moved);
   int32_t *mkey = reinterpret_cast<int32_t *>(lds + ofs.mhash);
   int32_t *mval = mkey + RES_MHASH;
@@ -1832,6 +1835,55 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         }
       }
       dec_src[l] = src;
+      // "slow" pods always take the general path: a non-monotone configuration,
+      // NUMA cpuset pods (Allocate at Reserve; required-policy feasibility is
+      // not monotone), a walk longer than RES_WE entries
+      const uint32_t fl = lpod[l].flags;
+      bool slow = !monotone || dec_n[l] < 0;
+      if constexpr (NUMA) {
+        // (with topology-policy nodes every NUMA pod: its zone hint can move
+        // to emptier zones as a node fills, so its score is not monotone)
+        slow = slow || (numa_on(c) && ((fl & KOORDHIP_POD_CPUSET) || c.zones) &&
+                        !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
+      }
+      if constexpr (NM == 3) {
+        // a pod some reservation may match: committing into a reservation raises
+        // its (MostAllocated) reservation score elsewhere -- not monotone
+        slow = slow || lpod[l].resv_match != 0ull;
+      }
+      dec_c[l] = slow ? 2 : 0;
+      // claims for the conflict check: staged winner -> first pod (linear probing)
+      if (!slow && kk != 0) {
+        const int32_t sw = key_node(kk);
+        uint32_t h = res_hash(sw);
+        for (;;) {
+          const int32_t prev = atomicCAS(&ckey[h], -1, sw);
+          if (prev == -1 || prev == sw) {
+            atomicMin(&cval[h], l);
+            break;
+          }
+          h = (h + 1) & (RES_HASH - 1);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 2b. conflicts among the staged decisions (one walked entry per
+    //          thread): pod l's walk met the staged winner of an earlier pod
+    for (int32_t x = t; x < n_pods * RES_WE; x += RES_THREADS) {
+      const int32_t l = x / RES_WE;
+      const int32_t y = dec_e[x];
+      if (y >= 0 && !(dec_c[l] & 2)) {
+        uint32_t h = res_hash(y);
+        for (;;) {
+          const int32_t xk = ckey[h];
+          if (xk == y) {
+            if (cval[h] < l) atomicOr(&dec_c[l], 1);
+            break;
+          }
+          if (xk < 0) break;
+          h = (h + 1) & (RES_HASH - 1);
+        }
+      }
     }
     __syncthreads();
     if (dbg && t == 0) {
@@ -1848,13 +1900,12 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       // ---- lane l = pod l: its staged decision in registers
       const bool live = lane < n_pods;
       uint32_t fl = 0;
-      int32_t sw = -1, ssrc = 0, sn = -1;
+      int32_t sw = -1, ssrc = 0;
       int32_t se[RES_WE];
 #pragma unroll
       for (int q = 0; q < RES_WE; q++) se[q] = -1;
       if (live) {
         fl = lpod[lane].flags;
-        sn = dec_n[lane];
         const uint64_t kk = dec_key[lane];
         sw = kk ? key_node(kk) : -1;
         ssrc = dec_src[lane];
@@ -1862,52 +1913,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         for (int q = 0; q < RES_WE; q++) se[q] = dec_e[lane * RES_WE + q];
       }
       const uint64_t prodmask = __ballot(live && (fl & KOORDHIP_POD_PROD));
-      // "slow" pods always take the general path: a non-monotone configuration,
-      // NUMA cpuset pods (Allocate at Reserve; required-policy feasibility is
-      // not monotone), a walk longer than RES_WE entries
-      bool slow = !monotone || sn < 0;
-      if constexpr (NUMA) {
-        // (with topology-policy nodes every NUMA pod: its zone hint can move
-        // to emptier zones as a node fills, so its score is not monotone)
-        slow = slow || (numa_on(c) && ((fl & KOORDHIP_POD_CPUSET) || c.zones) &&
-                        !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
-      }
-      if constexpr (NM == 3) {
-        // a pod some reservation may match: committing into a reservation raises
-        // its (MostAllocated) reservation score elsewhere -- not monotone
-        slow = slow || (live && lpod[lane].resv_match != 0ull);
-      }
-      // ---- conflicts among the staged decisions: pod l's walk met the staged
-      //      winner of an earlier pod (exact node -> first pod hash, linear probing)
-      const bool claims = live && !slow && sw >= 0;
-      if (claims) {
-        uint32_t h = res_hash(sw);
-        for (;;) {
-          const int32_t prev = atomicCAS(&ckey[h], -1, sw);
-          if (prev == -1 || prev == sw) {
-            atomicMin(&cval[h], lane);
-            break;
-          }
-          h = (h + 1) & (RES_HASH - 1);
-        }
-      }
-      bool conflict = false;
-#pragma unroll
-      for (int q = 0; q < RES_WE; q++) {
-        const int32_t y = se[q];
-        if (live && !slow && y >= 0) {
-          uint32_t h = res_hash(y);
-          for (;;) {
-            const int32_t x = ckey[h];
-            if (x == y) {
-              conflict = conflict || cval[h] < lane;
-              break;
-            }
-            if (x < 0) break;
-            h = (h + 1) & (RES_HASH - 1);
-          }
-        }
-      }
+      // general-path-only pods and conflicts: from the prologue (phase 2 / 2b)
+      const int32_t dc = live ? dec_c[lane] : 2;
+      const bool slow = (dc & 2) != 0;
+      const bool conflict = (dc & 1) != 0;
       uint64_t ok = __ballot(live && !slow && !conflict);  // staged decisions still valid
       uint64_t cstaged = 0;                                 // pods committed with their staged decision
       const uint64_t slowmask = __ballot(live && slow);
