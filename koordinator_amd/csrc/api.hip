@@ -42,6 +42,7 @@ int fail(int code, const std::string &msg) {
 
 constexpr int kDefaultBatch = 24;  // config-4 round-size sweep: 24 best (970k pods/s vs 911k at 32)
 constexpr int kDefaultBatchNuma = 16;
+constexpr int kDefaultBatchResv = 32;  // config 5 (evaluation-bound): 143k pods/s vs 135k at 16
 constexpr int32_t kMaxNodes = 400000;  // the resolve keeps a per-node bit in LDS (next to 2 x 64 x 128 list keys)
 constexpr int kMaxBatch = 64;
 constexpr int kRing = 4;               // per-round events in flight (lag-1 pipeline needs 3)
@@ -618,9 +619,11 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->cfg = *cfg;
   // NodeNUMAResource streams are bound by the resolve's cpuset Reserve: shorter
   // rounds re-evaluate fewer stale list entries (config 3: 16 pods 106k, 32 pods 98k pods/s)
+  const uint32_t plugins = cfg->filter_plugins | cfg->score_plugins;
   c->batch = cfg->batch_pods ? cfg->batch_pods
-                             : (((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) ? kDefaultBatchNuma
-                                                                                                  : kDefaultBatch);
+                             : ((plugins & KOORDHIP_PLUGIN_RESERVATION) ? kDefaultBatchResv
+                                : (plugins & KOORDHIP_PLUGIN_NUMA)     ? kDefaultBatchNuma
+                                                                       : kDefaultBatch);
   c->dc.filt = cfg->filter_plugins;
   c->dc.score = cfg->score_plugins;
   c->dc.w_fit = (int32_t)cfg->plugin_weight[0];

@@ -754,31 +754,54 @@ __device__ __forceinline__ uint64_t sel_mask_eq(const uint4 *q, uint32_t x) {
 // Wave-level walk of a histogram from the top bin down to bin `floor`: the
 // k-th largest value (0 if fewer than k values >= floor) and how many values
 // lie strictly above it.  `count(v)` reads bin v; wave-uniform results.
-template <typename F>
+// `words` (BPW bins per 32-bit word, the histogram's storage): windows of
+// 256 words whose bins are all zero are skipped in one probe (4 words per
+// lane + a ballot) -- the Reservation ranking totals put a few reservation
+// nodes ~30k values above the rest, which one-bin-per-lane steps crossed in
+// ~500 iterations.
+template <int BPW = 1, typename F>
 __device__ __forceinline__ void sel_walk(F count, int32_t nbins, int32_t floor, int32_t k, int32_t &thr, int32_t &gt,
-                                         int32_t top0 = -1) {
+                                         int32_t top0 = -1, const uint32_t *words = nullptr) {
   const int lane = lane_id();
   int32_t cum = 0;
   thr = 0;
   gt = 0;
   // top0: no value lies above it (the walk starts there instead of at the top bin)
-  for (int32_t top = top0 >= 0 ? min(top0, nbins - 1) : nbins - 1; top >= floor && thr == 0; top -= 64) {
-    const int32_t v = top - lane;
-    const int32_t c = v >= floor ? count(v) : 0;
-    if (__ballot(c != 0) == 0) continue;  // wave-uniform
-    int32_t x = c;  // inclusive prefix over lanes = bins top, top-1, ...
+  int32_t top = top0 >= 0 ? min(top0, nbins - 1) : nbins - 1;
+  while (top >= floor && thr == 0) {
+    int32_t stop = floor - 1;  // the fine walk below runs down to bin stop + 1
+    if (words) {
+      const int32_t w1 = top / BPW, w0 = w1 - 255;
+      uint32_t any = 0;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
+      for (int u = 0; u < 4; u++) {
+        const int32_t wi = w0 + lane * 4 + u;
+        if (wi >= 0 && wi <= w1) any |= words[wi];
+      }
+      if (__ballot(any != 0) == 0) {  // bins [w0 * BPW, top] are all empty
+        top = w0 * BPW - 1;
+        continue;
+      }
+      stop = max(stop, w0 * BPW - 1);
     }
-    const uint64_t hit = __ballot(c != 0 && cum + x >= k);
-    if (hit) {
-      const int l = __builtin_ctzll(hit);
-      thr = top - l;
-      gt = cum + __shfl(x, l, 64) - __shfl(c, l, 64);
-    } else {
-      cum += __shfl(x, 63, 64);
+    for (; top > stop && thr == 0; top -= 64) {
+      const int32_t v = top - lane;
+      const int32_t c = v >= floor ? count(v) : 0;
+      if (__ballot(c != 0) == 0) continue;  // wave-uniform
+      int32_t x = c;  // inclusive prefix over lanes = bins top, top-1, ...
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      const uint64_t hit = __ballot(c != 0 && cum + x >= k);
+      if (hit) {
+        const int l = __builtin_ctzll(hit);
+        thr = top - l;
+        gt = cum + __shfl(x, l, 64) - __shfl(c, l, 64);
+      } else {
+        cum += __shfl(x, 63, 64);
+      }
     }
   }
 }
@@ -819,8 +842,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
     __syncthreads();
     if (t < 64) {
       int32_t thr, gt;
-      sel_walk([&](int32_t v) { return (int32_t)((mhist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu); }, nbins, 1, k, thr,
-               gt);
+      sel_walk<2>([&](int32_t v) { return (int32_t)((mhist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu); }, nbins, 1, k, thr,
+                  gt, -1, mhist);
       if (lane == 0) sh_thr = thr;
     }
     __syncthreads();
@@ -843,7 +866,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
   // ---- k-th largest value S*: wave 0 walks the bins top-down, 64 at a time
   if (t < 64) {
     int32_t thr, gt;
-    sel_walk([&](int32_t v) { return (int32_t)hist[v]; }, nbins, (int32_t)L, k, thr, gt);
+    sel_walk<1>([&](int32_t v) { return (int32_t)hist[v]; }, nbins, (int32_t)L, k, thr, gt, -1, hist);
     if (thr == 0) {  // fewer than k feasible (then L == 1): take every feasible node
       thr = 1;
       gt = 0;
@@ -1064,8 +1087,8 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
     __syncthreads();
     if (t < 64) {
       int32_t thr, gt;
-      sel_walk([&](int32_t v) { return (int32_t)((mhist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu); }, nbins, 1, k, thr,
-               gt, h.hmax);
+      sel_walk<2>([&](int32_t v) { return (int32_t)((mhist[v >> 1] >> (16 * (v & 1))) & 0xFFFFu); }, nbins, 1, k, thr,
+                  gt, h.hmax, mhist);
       if (lane == 0) h.thr = thr;
     }
     __syncthreads();
@@ -1094,7 +1117,7 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
   if (t < 64) {
     int32_t thr, gt;
     const int32_t top = h.smax;
-    sel_walk(hget, nbins, (int32_t)L, k, thr, gt, top);
+    sel_walk<PK ? 2 : 1>(hget, nbins, (int32_t)L, k, thr, gt, top, hist);
     if (thr == 0) {
       thr = (int32_t)L;
       gt = 0;
@@ -1195,7 +1218,7 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
   if (t < 64) {
     int32_t sth, sgt;
     const int32_t top = h.mmax;
-    sel_walk(hget, nbins, 1, k, sth, sgt, top);
+    sel_walk<PK ? 2 : 1>(hget, nbins, 1, k, sth, sgt, top, hist);
     if (sth == 0) {  // fewer than k keys in all: every one of them
       sth = 1;
       sgt = 0;
