@@ -244,3 +244,19 @@ def test_gpu_accumulator_go118_socket_sort(Engine):
         e.load_snapshot(t)
         got = e.commit(cpuset_pod(8)[0], 0)
     assert topo.cpus(got) == want
+
+
+def test_gpu_class_core_order_checked(Engine):
+    """Positions inside a core must ascend by CPU id (the header's core-major
+    rule, which the resolve's lane-parallel spread take relies on): a class
+    whose first core lists its CPUs in descending id is rejected at load."""
+    topo = linux_topology(1, 1, 4, 2)
+    t = numa_table([topo], [topo.mask(topo.cpu_of)])
+    recs = t.numa_classes.copy()
+    a, b = int(recs[0]["cpu_id"][0]), int(recs[0]["cpu_id"][1])
+    recs[0]["cpu_id"][0], recs[0]["cpu_id"][1] = b, a
+    t.numa_classes = recs
+    prof = shipped_profile(numa=True)
+    with Engine(prof, device=0) as e:
+        with pytest.raises(abi.KoordhipError, match="ascend by CPU id"):
+            e.load_snapshot(t)
