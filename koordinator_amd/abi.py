@@ -173,10 +173,14 @@ _lib = None
 
 
 def load_library(path: str = LIB_PATH):
-    """Load libkoordhip.so.  Fails loudly when it has not been built."""
+    """Load libkoordhip.so.  Fails loudly when it has not been built.
+
+    KOORDHIP_LIB names another build of the same library (A/B of compile-time
+    variants, e.g. `make VARIANT=...`); it must still be a libkoordhip build."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("KOORDHIP_LIB", path)
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                            " (there is no CPU fallback)")

@@ -396,6 +396,14 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 // XCD's 4 MB L2 then holds its eighth of the node table (50k nodes: ~0.5 MB)
 // and the 4 x (pods/4) re-reads of a row hit L2 instead of the MALL.
 
+// SCAN_WPE1 / SCAN_WPE3: minimum waves per SIMD the compiler must fit the
+// NodeNUMAResource / Reservation scans into (1 = no constraint; A/B variants)
+#ifndef SCAN_WPE1
+#define SCAN_WPE1 1
+#endif
+#ifndef SCAN_WPE3
+#define SCAN_WPE3 1
+#endif
 template <int NM>
 using side_row_t = typename std::conditional<NM == 3, NumaRowR, NumaRow>::type;
 
@@ -403,7 +411,7 @@ using side_row_t = typename std::conditional<NM == 3, NumaRowR, NumaRow>::type;
 // topology-policy nodes (the zone code is compiled only here), 3 = with the
 // Reservation plugin (NUMA side rows carry the node's reservation)
 template <int R, int NM>
-__global__ __launch_bounds__(256) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NM == 3 ? SCAN_WPE3 : (NM == 1 ? SCAN_WPE1 : 1)))) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
                                               int32_t lo, int32_t hi, int32_t nchunks, int32_t cpx,
                                               uint16_t *__restrict__ S, int64_t s_stride,
                                               uint16_t *__restrict__ Mx, int32_t m_stride) {
@@ -1496,7 +1504,7 @@ __global__ void k_signal_lists(PipeSync *sy, int32_t par, int32_t pods) {
   if (threadIdx.x == 0) store_release(&sy->sel[par], pods);
 }
 
-template <int NM>
+template <int NM, bool DBG>
 __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const DevNodes *__restrict__ dn, int32_t n_nodes,
                                                                  const DevNumaClass *__restrict__ ncls, const DevPod *__restrict__ pods,
                                                                  int32_t total, int32_t P, int32_t k, int32_t kp,
@@ -1509,6 +1517,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                                                                  uint64_t *__restrict__ dbg, int32_t trace) {
   constexpr int RES_THREADS = res_threads<NM>();
   constexpr bool NUMA = NM != 0, ZONES = NM == 2;
+  // the cycle stamps (KOORDHIP_STAMPS) are a separate instantiation: their ~20
+  // running counters otherwise stay live across the loop and push the product
+  // build of the kernel into scratch spills
+  if constexpr (!DBG) dbg = nullptr;
   using NR = side_row_t<NM>;  // the NUMA side row (+ the node's reservation with NM == 3)
   (void)trace;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -2658,19 +2670,29 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag);
-  static bool attr[4] = {false, false, false, false};
-  if (!attr[nm]) {
-    const void *f = nm == 3 ? (const void *)k_resolve<3>
-                    : nm == 2 ? (const void *)k_resolve<2>
-                              : (nm == 1 ? (const void *)k_resolve<1> : (const void *)k_resolve<0>);
+  static bool attr[8] = {false, false, false, false, false, false, false, false};
+  const int ai = nm * 2 + (dbg ? 1 : 0);
+  if (!attr[ai]) {
+    const void *f = dbg ? (nm == 3   ? (const void *)k_resolve<3, true>
+                           : nm == 2 ? (const void *)k_resolve<2, true>
+                                     : (nm == 1 ? (const void *)k_resolve<1, true> : (const void *)k_resolve<0, true>))
+                        : (nm == 3   ? (const void *)k_resolve<3, false>
+                           : nm == 2 ? (const void *)k_resolve<2, false>
+                                     : (nm == 1 ? (const void *)k_resolve<1, false> : (const void *)k_resolve<0, false>));
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS_MAX);
     if (e != hipSuccess) return e;
-    attr[nm] = true;
+    attr[ai] = true;
   }
   if (o.total > RES_LDS_MAX) return hipErrorInvalidValue;
-#define KH_RESOLVE(NN)                                                                                                \
-  hipLaunchKernelGGL(k_resolve<NN>, dim3(1), dim3(res_threads<NN>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, total, P, \
-                     k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, lag, sync, o, out_node, out_cpus, dbg, trace)
+#define KH_RESOLVE_D(NN, DD)                                                                                  \
+  hipLaunchKernelGGL((k_resolve<NN, DD>), dim3(1), dim3(res_threads<NN>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, \
+                     total, P, k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, lag, sync, o, out_node, out_cpus, \
+                     dbg, trace)
+#define KH_RESOLVE(NN)       \
+  if (dbg)                   \
+    KH_RESOLVE_D(NN, true);  \
+  else                       \
+    KH_RESOLVE_D(NN, false)
   if (nm == 3)
     KH_RESOLVE(3);
   else if (nm == 2)
@@ -2680,6 +2702,7 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   else
     KH_RESOLVE(0);
 #undef KH_RESOLVE
+#undef KH_RESOLVE_D
   return hipGetLastError();
 }
 
