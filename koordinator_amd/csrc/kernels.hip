@@ -397,12 +397,15 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 // and the 4 x (pods/4) re-reads of a row hit L2 instead of the MALL.
 
 // SCAN_WPE1 / SCAN_WPE3: minimum waves per SIMD the compiler must fit the
-// NodeNUMAResource / Reservation scans into (1 = no constraint; A/B variants)
+// NodeNUMAResource / Reservation scans into (1 = no constraint).  The
+// Reservation scan at 4 waves (<= 128 VGPRs, a few spilled dwords instead of
+// 162 VGPRs at 3 waves): config 5 scan 175 -> 138 us, 150k -> 169k pods/s;
+// the NUMA scan measured no different (config 3 is resolve-bound)
 #ifndef SCAN_WPE1
 #define SCAN_WPE1 1
 #endif
 #ifndef SCAN_WPE3
-#define SCAN_WPE3 1
+#define SCAN_WPE3 4
 #endif
 template <int NM>
 using side_row_t = typename std::conditional<NM == 3, NumaRowR, NumaRow>::type;
