@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round evidence: full GPU suite + smoke, bench lines of configs 4 / 3 / 5, rocprofv3 kernel stats of configs 3 and 4.
+# Round evidence: full GPU suite + smoke, bench lines of configs 4 / 3 / 5, rocprofv3 kernel stats of configs 3, 4 and 5.
 # Usage: ROUND=r02x bash scripts/gpu_round.sh (through scripts/gpu.sh)
 set -u
 R=${ROUND:-r02c}
@@ -12,4 +12,5 @@ timeout -k 10 300 python bench.py --workload config3 --steps 3 --warmup 1 --cpu-
 timeout -k 10 400 python bench.py --workload config5 --steps 2 --warmup 1 --cpu-budget 8 > gpurun_out/bench_${R}_config5.json 2> gpurun_out/bench_${R}_config5.err || exit 1
 bash scripts/profile.sh ${R}_config3 --workload config3 --steps 2 --warmup 1 || exit 1
 bash scripts/profile.sh ${R}_config4 --steps 2 --warmup 1 || exit 1
+bash scripts/profile.sh ${R}_config5 --workload config5 --steps 1 --warmup 1 || exit 1
 for f in bench_${R} bench_${R}_config3 bench_${R}_config5; do cut -c1-200 gpurun_out/$f.json; done
