@@ -120,9 +120,13 @@ def cpu_baseline(table, pods, cfg, budget_s=12.0):
                       f"(legs: {ncpu} workers, 1 worker); the Go reference itself cannot run here (no Go toolchain)"}
 
 
-def pmc_traffic():
-    """HBM bytes per eval launch from the committed rocprofv3 PMC summary, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def pmc_traffic(workload="config4"):
+    """HBM bytes per eval launch from the committed rocprofv3 PMC summary of
+    this workload (profiles/pmc_summary_<workload>.json; config 4's is also
+    profiles/pmc_summary.json), if any."""
+    p = os.path.join(ROOT, "profiles", f"pmc_summary_{workload}.json")
+    if not os.path.exists(p) and workload == "config4":
+        p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
         return None, None
     try:
@@ -264,7 +268,7 @@ def main():
     col_bytes = float(b_eval.max()) * args.nodes
     phys = col_bytes + pods_per_round * args.nodes * 2 + pods_per_round * args.nodes / 64 * 2
     scan_gbs = phys / (scan_us * 1e-6) / 1e9 if scan_us > 0 else None
-    traffic, traffic_src = pmc_traffic() if not numa else (None, None)   # the committed PMC pass is config 4's
+    traffic, traffic_src = pmc_traffic(args.workload)
     out = {
         "metric": METRIC,
         "value": round(value, 2),
