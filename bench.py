@@ -113,8 +113,10 @@ def cpu_baseline(table, pods, cfg, budget_s=12.0):
         legs[name] = {"threads": threads, "pods": n, "pods_per_s": round(n / dt, 2),
                       "evals_per_s": round(n * table.n / dt, 1)}
     ref = legs["ref16"]
+    best = max(legs, key=lambda k: legs[k]["pods_per_s"])
     return {"value": ref["pods_per_s"], "unit": "pods/s", "cores": ref["threads"], "kind": "port",
-            "evals_per_s": ref["evals_per_s"], "legs": legs, "cpu_model": _cpu_model(), "nproc": ncpu,
+            "evals_per_s": ref["evals_per_s"], "legs": legs,
+            "best_leg": {"name": best, **legs[best]}, "cpu_model": _cpu_model(), "nproc": ncpu,
             "sample": f"first {ref['pods']} pods of the same stream on the same {table.n}-node snapshot, "
                       f"oracle/koord_oracle.c orc_place_stream with {ref['threads']} workers "
                       f"(legs: {ncpu} workers, 1 worker); the Go reference itself cannot run here (no Go toolchain)"}
@@ -134,6 +136,20 @@ def pmc_traffic(workload="config4"):
         return d.get("hbm_bytes_per_launch"), d.get("source")
     except Exception:
         return None, None
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N > 1` without a torch.distributed launcher: start one as a CHILD
+    process (nothing here has touched the GPU yet) with this command line, and
+    return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ))
 
 
 def main():
@@ -156,11 +172,20 @@ def main():
     ap.add_argument("--one-rank-comm", action="store_true",
                     help="N=1 only: attach a one-rank RCCL communicator, so every round takes the multi-GPU "
                          "exchange path (all-gather + merge) -- measures that pipeline on one GPU")
+    ap.add_argument("--probe-ranks", action="store_true",
+                    help="print this rank's RANK / WORLD_SIZE and exit before any GPU work (launcher test)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.probe_ranks:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank}), flush=True)
+        return
 
     import torch
     from koordinator_amd import synth
@@ -321,7 +346,9 @@ def main():
         ref = oracle.Oracle(cfg, table).place_stream(pods, threads=min(16, os.cpu_count() or 1))
         out["check"] = bool(np.array_equal(ref, placements))
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(table, pods, cfg, args.cpu_budget)
+        cb = cpu_baseline(table, pods, cfg, args.cpu_budget)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_best_cpu_leg"] = round(value / cb["best_leg"]["pods_per_s"], 1)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -830,6 +830,8 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   pi.la_flags = lf;
   if (!e) e = load_numa_columns(c, s, n);
   if (!e) e = load_resv_columns(c, s, n);
+  if (!e && c->dc.resv && c->dc.zones)
+    e = fail(KOORDHIP_EINVAL, "the Reservation plugin with NUMA topology-policy nodes is not supported");
   if (e) {
     free_cols(c);
     return e;
@@ -880,6 +882,8 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     zrows = rows->numa_zone_alloc && rows->numa_zone_used;
     if (zpolicy && !c->d.nu.za)
       return fail(KOORDHIP_EINVAL, "a NUMA topology policy needs the zone columns at load_snapshot");
+    if (zpolicy && c->dc.resv)
+      return fail(KOORDHIP_EINVAL, "the Reservation plugin with NUMA topology-policy nodes is not supported");
     zrows = zrows && c->d.nu.za;
   }
   bool amp_rows = false, amp_any = false;

@@ -17,7 +17,14 @@ The node SET is positional on the device: adding or deleting a node needs a
 new snapshot (``flush`` returns ``needs_reload``; ``table()`` builds it).
 NodeNUMAResource columns are not derived from objects here (the host has no
 NodeResourceTopology object model); rows keep the NUMA columns of the table
-they were loaded from.
+they were loaded from, carried over by node name across a reload.
+
+Reservations (the Reservation plugin's reservationCache, reservation/cache.go:
+117-252, fed by the reservation informer) are kept by name; an add / update /
+delete re-derives the resv_* columns of the nodes it leaves and enters.  Owner
+groups are append-only (``resv_index``): pod masks made earlier stay valid.  A
+reservation-order value the snapshot has no rank for needs a reload (ranks are
+snapshot-wide).
 """
 from __future__ import annotations
 
@@ -28,6 +35,7 @@ import numpy as np
 
 from . import k8s
 from .config import Profile
+from . import reservation as rv
 from .marshal import AssignedPod, ClusterState, build_table, is_node_metric_expired, node_row
 from .snapshot import NodeTable
 
@@ -96,14 +104,19 @@ class Informer:
         self._expired: Dict[str, bool] = {}
         self._table: Optional[NodeTable] = None
         self._now = now
+        self.reservations: Dict[str, rv.Reservation] = {}
+        self.resv_index = rv.ReservationIndex()
+        self._resv_rank: Dict[int, int] = {}
 
     # ---- full snapshot --------------------------------------------------------
     def table(self, now: float) -> NodeTable:
         """A full snapshot of the current state (initial load, or after the node set changed)."""
         self._sync_assigned()
         t = build_table(self.cluster, self.profile, now)
-        if self._table is not None and self._table.n == t.n and self._table.names == t.names:
+        if self._table is not None:
             _keep_numa(t, self._table)
+        self._resv_rank = rv.order_ranks(rv.available_by_node(self._index, list(self.reservations.values())).values())
+        rv.reservation_columns(t, self._index, list(self.reservations.values()), self.resv_index)
         self._table = t
         self._dirty.clear()
         self._reload = False
@@ -216,6 +229,28 @@ class Informer:
                 self._metric_refs.get(f"{pm.namespace}/{pm.name}", set()).discard(name)
         self._dirty.add(name)
 
+    # ---- Reservation events (reservation/cache.go:117-252) ------------------------------------------
+    def on_reservation(self, r: rv.Reservation):
+        """Add or update."""
+        old = self.reservations.get(r.name)
+        self.reservations[r.name] = r
+        for nn in ({old.node_name} if old is not None else set()) | {r.node_name}:
+            if nn:
+                self._dirty.add(nn)
+        order = rv.parse_order(r.labels)
+        if r.is_available() and order != 0 and order not in self._resv_rank:
+            self._reload = True
+
+    def on_reservation_delete(self, name: str):
+        old = self.reservations.pop(name, None)
+        if old is not None and old.node_name:
+            self._dirty.add(old.node_name)
+
+    def pod_records(self, pods):
+        """Pod records with the current owner groups' match masks."""
+        from .marshal import pod_records
+        return pod_records(pods, self.profile, self.resv_index)
+
     # ---- deltas ----------------------------------------------------------------------------
     def _sync_assigned(self):
         self.cluster.assigned = {nn: list(m.values()) for nn, m in self.assign_cache.items.items()}
@@ -248,8 +283,14 @@ class Informer:
         self._sync_assigned()
         idx = np.array(sorted(self._index[n] for n in dirty), np.int32)
         rows = self._table.rows(idx)
+        placed = rv.available_by_node(self._index, list(self.reservations.values()))
         for j, i in enumerate(idx):
             node_row(rows, j, self.cluster.nodes[int(i)], self.cluster, self.profile, now)
+            r = placed.get(int(i))
+            if r is None:
+                rv.clear_reservation_row(rows, j)
+            else:
+                rv.reservation_row(rows, j, r, self.resv_index, self._resv_rank)
         for c in rows.cols:
             self._table.cols[c][idx] = rows.cols[c]
         self._dirty.clear()
@@ -266,8 +307,16 @@ class Informer:
 
 
 def _keep_numa(dst: NodeTable, src: NodeTable):
-    """NUMA columns are not derived from objects: carry them over."""
+    """NUMA columns are not derived from objects: carry them over, row by node
+    name (rows of nodes new to `dst` keep build_table's no-topology values)."""
     from .snapshot import NUMA_MUTABLE, U64_COLS, ZONE_COLS
-    for c in set(U64_COLS) | set(NUMA_MUTABLE) | set(ZONE_COLS) | {"numa_class", "numa_flags"}:
-        dst.cols[c] = src.cols[c].copy()
+    pos = {nm: i for i, nm in enumerate(src.names)}
+    pairs = [(j, pos[nm]) for j, nm in enumerate(dst.names) if nm in pos]
+    if not pairs:
+        return
+    dj = np.array([a for a, _ in pairs], np.int64)
+    sj = np.array([b for _, b in pairs], np.int64)
+    for c in set(U64_COLS) | set(NUMA_MUTABLE) | set(ZONE_COLS) | {"numa_class", "numa_flags", "numa_amp_cpu"}:
+        if c in src.cols and c in dst.cols:
+            dst.cols[c][dj] = src.cols[c][sj]
     dst.numa_classes = src.numa_classes

@@ -24,12 +24,12 @@ from __future__ import annotations
 import json
 import re
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import abi, k8s
-from .snapshot import NodeTable
+from .snapshot import RESV_COLS as RESV_COLUMNS, NodeTable
 
 LABEL_RESERVATION_ORDER = "scheduling.koordinator.sh/reservation-order"   # apis/extension/reservation.go
 ANNOTATION_RESERVATION_AFFINITY = "scheduling.koordinator.sh/reservation-affinity"
@@ -238,73 +238,96 @@ def _q2(rl: k8s.ResourceList, name: str) -> int:
     return q.milli_value() if name == k8s.CPU else q.value()
 
 
-def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservations: Sequence[Reservation],
-                        index: Optional[ReservationIndex] = None) -> ReservationIndex:
-    """Fill the resv_* columns of `table` (the reservation cache's view,
-    cache.go:236-252) and return the owner groups for the pod masks."""
-    from .marshal import nonzero_request, fit_request
-
-    index = index or ReservationIndex()
-    for c in ("resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1",
-              "resv_allocated0", "resv_allocated1", "resv_assigned"):
-        table[c][:] = 0
-    placed: List[Tuple[int, Reservation]] = []
+def available_by_node(node_index: Dict[str, int], reservations: Sequence[Reservation]) -> Dict[int, Reservation]:
+    """The reservation cache's Available reservations by node row (cache.go:236-252);
+    at most one per node (several: the reference orders them by map iteration)."""
+    placed: Dict[int, Reservation] = {}
     for r in reservations:
         if not r.is_available() or r.node_name not in node_index:
             continue
         i = node_index[r.node_name]
-        if any(j == i for j, _ in placed):
+        if i in placed:
             raise ReservationError(f"node {r.node_name}: more than one Available reservation (unsupported)")
-        placed.append((i, r))
-    orders = sorted({parse_order(r.labels) for _, r in placed} - {0})
+        placed[i] = r
+    return placed
+
+
+def order_ranks(reservations: Iterable[Reservation]) -> Dict[int, int]:
+    """Rank of every distinct non-zero reservation-order label value (ascending)."""
+    orders = sorted({parse_order(r.labels) for r in reservations} - {0})
     if len(orders) > abi.RESV_MAX_ORDERS:
         raise ReservationError(f"more than {abi.RESV_MAX_ORDERS} distinct reservation orders")
-    rank = {v: k for k, v in enumerate(orders)}
-    for i, r in placed:
-        names = set(r.allocatable)
-        extra = names - {k8s.CPU, k8s.MEMORY}
-        if extra:
-            raise ReservationError(f"reservation {r.name}: resources {sorted(extra)} are not supported")
-        parse_ok = True
-        try:
-            for o in r.owners:
-                if o.label_selector is not None:
-                    o.label_selector.validate()
-        except ReservationError:
-            parse_ok = False                                  # ReservationInfo.ParseError
-        pod = r.reserve_pod()
-        req, present = fit_request(pod)
-        if present - {k8s.CPU, k8s.MEMORY} or any(req[k] for k in range(abi.NRES) if k not in (abi.RES_CPU, abi.RES_MEM)):
-            raise ReservationError(f"reservation {r.name}: the reserve pod requests resources other than cpu/memory")
-        if req[abi.RES_CPU] != _q2(r.allocatable, k8s.CPU) or req[abi.RES_MEM] != _q2(r.allocatable, k8s.MEMORY):
-            raise ReservationError(f"reservation {r.name}: allocatable differs from the reserve pod's requests")
-        f = abi.RESV_PRESENT if parse_ok else 0
-        if r.allocate_once is None or r.allocate_once:
-            f |= abi.RESV_ALLOCATE_ONCE
-        if r.unschedulable or r.deleting:
-            f |= abi.RESV_UNSCHEDULABLE
-        order = parse_order(r.labels)
-        if order != 0:
-            f |= abi.RESV_ORDERED
-            table["resv_order_rank"][i] = rank[order]
-        if k8s.CPU in names:
-            f |= abi.RESV_KEY_CPU
-        if k8s.MEMORY in names:
-            f |= abi.RESV_KEY_MEM
-        if r.allocate_policy not in _POLICY_CODE:
-            raise ReservationError(f"reservation {r.name}: unknown allocate policy {r.allocate_policy!r}")
-        f |= _POLICY_CODE[r.allocate_policy] << abi.RESV_POLICY_SHIFT
-        f |= index.group(r.owners) << abi.RESV_GROUP_SHIFT
-        table["resv_flags"][i] = f
-        table["resv_alloc0"][i] = _q2(r.allocatable, k8s.CPU)
-        table["resv_alloc1"][i] = _q2(r.allocatable, k8s.MEMORY)
-        nzc, nzm = nonzero_request(pod)
-        table["resv_nz0"][i] = nzc
-        table["resv_nz1"][i] = nzm
-        # Allocated masked to ResourceNames (reservation_info.go:286, 303)
-        table["resv_allocated0"][i] = _q2(r.allocated, k8s.CPU) if k8s.CPU in names else 0
-        table["resv_allocated1"][i] = _q2(r.allocated, k8s.MEMORY) if k8s.MEMORY in names else 0
-        table["resv_assigned"][i] = r.assigned
+    return {v: k for k, v in enumerate(orders)}
+
+
+def clear_reservation_row(table: NodeTable, i):
+    for c in RESV_COLUMNS:
+        table[c][i] = 0
+
+
+def reservation_row(table: NodeTable, i: int, r: Reservation, index: "ReservationIndex", rank: Dict[int, int]):
+    """Row i of the resv_* columns for node i's Available reservation r."""
+    from .marshal import nonzero_request, fit_request
+
+    clear_reservation_row(table, i)
+    names = set(r.allocatable)
+    extra = names - {k8s.CPU, k8s.MEMORY}
+    if extra:
+        raise ReservationError(f"reservation {r.name}: resources {sorted(extra)} are not supported")
+    parse_ok = True
+    try:
+        for o in r.owners:
+            if o.label_selector is not None:
+                o.label_selector.validate()
+    except ReservationError:
+        parse_ok = False                                  # ReservationInfo.ParseError
+    pod = r.reserve_pod()
+    req, present = fit_request(pod)
+    if present - {k8s.CPU, k8s.MEMORY} or any(req[k] for k in range(abi.NRES) if k not in (abi.RES_CPU, abi.RES_MEM)):
+        raise ReservationError(f"reservation {r.name}: the reserve pod requests resources other than cpu/memory")
+    if req[abi.RES_CPU] != _q2(r.allocatable, k8s.CPU) or req[abi.RES_MEM] != _q2(r.allocatable, k8s.MEMORY):
+        raise ReservationError(f"reservation {r.name}: allocatable differs from the reserve pod's requests")
+    f = abi.RESV_PRESENT if parse_ok else 0
+    if r.allocate_once is None or r.allocate_once:
+        f |= abi.RESV_ALLOCATE_ONCE
+    if r.unschedulable or r.deleting:
+        f |= abi.RESV_UNSCHEDULABLE
+    order = parse_order(r.labels)
+    if order != 0:
+        if order not in rank:
+            raise ReservationError(f"reservation {r.name}: order {order} has no rank in this snapshot")
+        f |= abi.RESV_ORDERED
+        table["resv_order_rank"][i] = rank[order]
+    if k8s.CPU in names:
+        f |= abi.RESV_KEY_CPU
+    if k8s.MEMORY in names:
+        f |= abi.RESV_KEY_MEM
+    if r.allocate_policy not in _POLICY_CODE:
+        raise ReservationError(f"reservation {r.name}: unknown allocate policy {r.allocate_policy!r}")
+    f |= _POLICY_CODE[r.allocate_policy] << abi.RESV_POLICY_SHIFT
+    f |= index.group(r.owners) << abi.RESV_GROUP_SHIFT
+    table["resv_flags"][i] = f
+    table["resv_alloc0"][i] = _q2(r.allocatable, k8s.CPU)
+    table["resv_alloc1"][i] = _q2(r.allocatable, k8s.MEMORY)
+    nzc, nzm = nonzero_request(pod)
+    table["resv_nz0"][i] = nzc
+    table["resv_nz1"][i] = nzm
+    # Allocated masked to ResourceNames (reservation_info.go:286, 303)
+    table["resv_allocated0"][i] = _q2(r.allocated, k8s.CPU) if k8s.CPU in names else 0
+    table["resv_allocated1"][i] = _q2(r.allocated, k8s.MEMORY) if k8s.MEMORY in names else 0
+    table["resv_assigned"][i] = r.assigned
+
+
+def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservations: Sequence[Reservation],
+                        index: Optional[ReservationIndex] = None) -> ReservationIndex:
+    """Fill the resv_* columns of `table` (the reservation cache's view,
+    cache.go:236-252) and return the owner groups for the pod masks."""
+    index = index or ReservationIndex()
+    clear_reservation_row(table, slice(None))
+    placed = available_by_node(node_index, reservations)
+    rank = order_ranks(placed.values())
+    for i, r in placed.items():
+        reservation_row(table, i, r, index, rank)
     return index
 
 

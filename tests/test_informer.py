@@ -213,3 +213,97 @@ def test_gpu_informer_deltas_then_stream():
     rs = o.state()
     for k in ("requested", "npods", "la_used"):
         assert np.array_equal(st[k], rs[k]), k
+
+
+def _rand_resv(rng, i, nodes):
+    from koordinator_amd import reservation as rv
+    cpu = int(rng.choice([1000, 2000, 4000]))
+    mem = int(rng.choice([1, 2, 4])) * GI
+    order = str(int(rng.choice([1, 2, 3]))) if rng.random() < 0.3 else None
+    return rv.Reservation(
+        name=f"r{i}", node_name=nodes[int(rng.integers(0, len(nodes)))].name, uid=f"ru{i}",
+        labels={rv.LABEL_RESERVATION_ORDER: order} if order else {},
+        owners=[rv.ReservationOwner(label_selector=rv.LabelSelector(match_labels={"app": f"a{int(rng.integers(0, 3))}"}))],
+        allocatable={k8s.CPU: k8s.Q(f"{cpu}m"), k8s.MEMORY: k8s.Q(mem)},
+        allocated={k8s.CPU: k8s.Q(f"{int(rng.integers(0, 2)) * 500}m")}, assigned=int(rng.integers(0, 2)),
+        allocate_once=bool(rng.random() < 0.5))
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_reservation_events_rows_equal_rebuild(seed):
+    """Reservation add / update / delete events (reservation/cache.go:117-252):
+    the incremental resv_* rows equal reservation_columns over the same
+    reservations, and a reload keeps the owner groups and the NUMA columns."""
+    from koordinator_amd import reservation as rv
+    rng = np.random.default_rng(seed)
+    prof = shipped_profile(numa=True, reservation=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110)})
+             for i in range(16)]
+    inf = Informer(prof, nodes, NOW)
+    live = {}
+    for i in range(5):   # distinct nodes to start with (at most one Available reservation per node)
+        r = _rand_resv(rng, i, nodes)
+        r.node_name = nodes[i].name
+        r.labels = {rv.LABEL_RESERVATION_ORDER: str(1 + i % 3)}
+        live[r.name] = r
+        inf.on_reservation(r)
+    eng = _TableEngine(inf.table(NOW))
+    nxt = 5
+    for step in range(30):
+        op = rng.random()
+        if op < 0.4:
+            r = _rand_resv(rng, nxt, nodes)
+            nxt += 1
+        elif op < 0.75 and live:
+            r = copy.deepcopy(live[list(live)[int(rng.integers(0, len(live)))]])
+            r.allocated = {k8s.CPU: k8s.Q(f"{int(rng.integers(0, 4)) * 250}m")}
+            r.assigned = int(rng.integers(0, 3))
+            if rng.random() < 0.3:
+                r.node_name = nodes[int(rng.integers(0, len(nodes)))].name
+            if rng.random() < 0.2:
+                r.phase = "Succeeded"
+        else:
+            if live:
+                inf.on_reservation_delete(live.pop(list(live)[int(rng.integers(0, len(live)))]).name)
+            r = None
+        if r is not None:
+            busy = {x.node_name for x in live.values() if x.name != r.name and x.is_available()}
+            if r.is_available() and r.node_name in busy:
+                continue                                  # a second Available reservation on a node: unsupported
+            live[r.name] = r
+            inf.on_reservation(r)
+        res = inf.flush(eng, NOW)
+        if res.needs_reload:                              # a reservation order the snapshot has no rank for
+            eng = _TableEngine(inf.table(NOW))
+        want = build_table(inf.cluster, prof, NOW)
+        rv.reservation_columns(want, {n.name: i for i, n in enumerate(nodes)}, list(live.values()),
+                               rv.ReservationIndex(groups=list(inf.resv_index.groups),
+                                                   group_of=dict(inf.resv_index.group_of)))
+        for c in ("resv_flags", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1", "resv_allocated0",
+                  "resv_allocated1", "resv_assigned"):
+            assert np.array_equal(eng.table.cols[c], want.cols[c]), (step, c)
+        # order ranks: the same relative order of the order labels
+        ordered = (want.cols["resv_flags"] & 8) != 0
+        assert np.array_equal((eng.table.cols["resv_flags"] & 8) != 0, ordered)
+        a, b = eng.table.cols["resv_order_rank"][ordered], want.cols["resv_order_rank"][ordered]
+        assert np.array_equal(np.argsort(a, kind="stable"), np.argsort(b, kind="stable"))
+
+
+def test_reload_keeps_reservations_and_numa_by_name():
+    """a node add / delete reload must keep every reservation (and
+    the NUMA columns) of the nodes that stay."""
+    from koordinator_amd import reservation as rv
+    prof = shipped_profile(numa=True, reservation=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(16), k8s.MEMORY: k8s.Q(32 * GI), k8s.PODS: k8s.Q(110)})
+             for i in range(4)]
+    inf = Informer(prof, nodes, NOW)
+    inf.on_reservation(rv.Reservation(name="r", node_name="n2", owners=[rv.ReservationOwner(
+        label_selector=rv.LabelSelector(match_labels={"app": "x"}))], allocatable={k8s.CPU: k8s.Q(2), k8s.MEMORY: k8s.Q(GI)}))
+    t = inf.table(NOW)
+    t.cols["numa_class"][2] = 7                            # stands for NUMA columns loaded from an NRT
+    inf.on_node_delete(nodes[0])
+    t2 = inf.table(NOW)
+    assert t2.names == ["n1", "n2", "n3"]
+    assert t2.cols["resv_flags"][1] & 1 and t2.cols["resv_alloc0"][1] == 2000
+    assert t2.cols["resv_flags"][0] == 0 and t2.cols["resv_flags"][2] == 0
+    assert t2.cols["numa_class"][1] == 7

@@ -116,3 +116,29 @@ def test_synth_reservations_match_objects():
     for c in ("resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1",
               "resv_allocated0", "resv_allocated1", "resv_assigned"):
         assert np.array_equal(base[c], t[c]), c
+
+
+@pytest.mark.parametrize("loaded", [0, 1])
+def test_same_order_reservations_tie_to_lowest_index(loaded):
+    """Two matched reservations with the same order label: upstream
+    PreScore makes the FIRST node of the smallest order the preferred node
+    (scoring.go:89-98, strict '>' keeps the first) whatever its other plugins'
+    total; the harness's node list is in index order, so the lower index wins.
+    The device's ranking total gives both nodes the same key (resv.hpp), so its
+    argmax is the lower index too -- checked against the oracle's literal
+    PreScore + Score + DefaultNormalizeScore cycle."""
+    prof = G.resv_profile()
+    sel = rv.ReservationOwner(label_selector=rv.LabelSelector(match_labels={"app": "a"}))
+    L = rv.LABEL_RESERVATION_ORDER
+    nodes = [(f"n{i}", {"cpu": "32", "memory": "64Gi", "pods": "110"}) for i in range(4)]
+    busy = {"n1": [G.resv_pod({"cpu": "20", "memory": "40Gi"}, name="load")]} if loaded else None
+    rs = [rv.Reservation("r1", "n1", allocatable=G.rlist({"cpu": "4", "memory": "8Gi"}), owners=[sel], labels={L: "5"}),
+          rv.Reservation("r2", "n2", allocatable=G.rlist({"cpu": "4", "memory": "8Gi"}), owners=[sel], labels={L: "5"}),
+          rv.Reservation("r3", "n3", allocatable=G.rlist({"cpu": "4", "memory": "8Gi"}), owners=[sel], labels={L: "9"})]
+    t, idx = G.build_resv_nodes(nodes, rs, prof, node_pods=busy)
+    pods = marshal.pod_records([G.resv_pod({"cpu": "1", "memory": "1Gi"}, labels={"app": "a"})], prof, idx)
+    cfg = to_c_config(prof)
+    placed = oracle.Oracle(cfg, t).place_stream(pods)[0]
+    top = oracle.Oracle(cfg, t).eval(pods, status=False, scores=False, k=4)["topk"][0]
+    assert placed == 1
+    assert top["node"][0] == 1 and top["score"][0] == top["score"][1] and top["node"][1] == 2
