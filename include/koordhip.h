@@ -132,9 +132,9 @@ extern "C" {
 #define KOORDHIP_NUMA_TOPO_RESTRICTED 2u
 #define KOORDHIP_NUMA_TOPO_SINGLE_NUMA_NODE 3u
 /* NUMA zones (NRT zones "node-<k>", zone k = NUMA node rank k) of a node with
- * a topology policy: at most this many on the device (hint merge over <= 15
- * masks per (pod, node)); the host rejects more. */
-#define KOORDHIP_NUMA_MAX_ZONES 4
+ * a topology policy: up to this many (hint merge over <= 255 masks per
+ * (pod, node), e.g. a 2-socket host in NPS4 mode). */
+#define KOORDHIP_NUMA_MAX_ZONES 8
 
 /* CPU topology of a node (cpu_topology.go:25-103), shared by every node of
  * the same shape.  CPU "positions" are core-major: pos = core_rank *

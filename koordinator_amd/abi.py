@@ -40,7 +40,7 @@ NODE_NUMA_MOST_ALLOCATED = 4
 NODE_NUMA_POLICY_SHIFT = 3
 NUMA_TOPO_NONE, NUMA_TOPO_BEST_EFFORT, NUMA_TOPO_RESTRICTED, NUMA_TOPO_SINGLE_NUMA_NODE = 0, 1, 2, 3
 NUMA_MAX_CPUS, NUMA_MAX_NODES, NUMA_WORDS = 256, 8, 4
-NUMA_MAX_ZONES = 4
+NUMA_MAX_ZONES = 8
 
 
 def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> int:

@@ -123,7 +123,16 @@ struct koordhip_ctx {
   int32_t sel_g = kh::kSelGMax;   // workgroups per pod of k_select_split (KOORDHIP_SEL_G)
   int32_t n_cu = 256;             // device CU count
   bool cu_reserve = false;        // KOORDHIP_CU_RESERVE: CU-masked streams, CU 0 for the resolve
-  bool sel_split = true;          // k_select_split; false (KOORDHIP_SELECT_ONEWG): k_select + signal kernel
+  bool sel_split = true;          // the list producer counts pods into the pipeline (k_eval_topk / k_select_split);
+                                  // false (KOORDHIP_SELECT_ONEWG): k_select + signal kernel
+  bool eval_fused = true;         // k_eval_topk (no score matrix); false (KOORDHIP_EVAL_SPLIT): k_scan + select
+  // k_eval_topk per evaluation stream: slice lists, their counts, and the
+  // per-pod bound / arrival words ([2][kSelMaxPods], zero between launches)
+  uint64_t *d_etk_part[2] = {nullptr, nullptr};
+  int32_t *d_etk_pcnt[2] = {nullptr, nullptr};
+  uint32_t *d_etk_sync[2] = {nullptr, nullptr};
+  size_t etk_cap[2] = {0, 0}, etk_ccap[2] = {0, 0};
+  int etk_vt[2] = {0, 0};
   size_t partial_cap[2] = {0, 0};
   hipStream_t stream2 = nullptr;  // second evaluation stream (odd rounds) of a single-GPU place call
   hipEvent_t ev_eval2 = nullptr;
@@ -303,7 +312,27 @@ int timed_end(koordhip_ctx *c, int32_t idx, hipStream_t s) {
 // counters.  place_staged sizes them before it launches the persistent
 // resolve: an allocation (or a free) inside the round loop could wait for a
 // device that is busy with that resolve.
-int eval_buffers(koordhip_ctx *c, int32_t np, int32_t lo, int32_t hi, int slot, hipStream_t es) {
+int eval_buffers(koordhip_ctx *c, int32_t np, int32_t lo, int32_t hi, int slot, hipStream_t es,
+                 int32_t kmax = kh::kResolveMaxK) {
+  if (c->eval_fused) {
+    // the slice width is fixed here for every launch until the next call (a
+    // shorter last round must not pick narrower slices: more of them than the
+    // buffers hold)
+    const int vt = kh::eval_topk_vt(kh::side_mode(c->dc), c->n_cu, np, lo, hi, kmax);
+    c->etk_vt[slot] = vt;
+    const size_t ns = (size_t)std::max(1, kh::eval_topk_slices(vt, lo, hi));
+    const size_t pods = (size_t)std::max(np, 1);
+    if (int e = ensure(c, reinterpret_cast<void **>(&c->d_etk_part[slot]), &c->etk_cap[slot],
+                       pods * ns * kh::kResolveMaxK * sizeof(uint64_t)))
+      return e;
+    if (int e = ensure(c, reinterpret_cast<void **>(&c->d_etk_pcnt[slot]), &c->etk_ccap[slot], pods * ns * sizeof(int32_t)))
+      return e;
+    if (!c->d_etk_sync[slot]) {
+      HIP_TRY(hipMalloc(&c->d_etk_sync[slot], 2 * kh::kSelMaxPods * sizeof(uint32_t)));
+      HIP_TRY(hipMemsetAsync(c->d_etk_sync[slot], 0, 2 * kh::kSelMaxPods * sizeof(uint32_t), es));
+    }
+    return 0;
+  }
   const int64_t stride = ((int64_t)(hi - lo) + 63) & ~63ll;
   const int32_t nchunks = kh::scan_chunks(c->partial_r, lo, hi);
   const int32_t mstride = (nchunks + 63) & ~63;
@@ -322,6 +351,22 @@ int eval_buffers(koordhip_ctx *c, int32_t np, int32_t lo, int32_t hi, int slot, 
 int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k, int32_t lo, int32_t hi,
                uint64_t *out, bool timed, kh::PipeSync *sync, int32_t sel_par, int32_t res_wait, hipStream_t es,
                int slot) {
+  if (c->eval_fused) {
+    // buffers sized by eval_buffers before the call's first launch
+    const int vt = c->etk_vt[slot];
+    if (!vt || kh::eval_topk_slices(vt, lo, hi) * (size_t)np * kh::kResolveMaxK * sizeof(uint64_t) > c->etk_cap[slot])
+      return fail(KOORDHIP_EINVAL, "k_eval_topk buffers not sized for this launch");
+    int32_t tm = -1;
+    if (timed)
+      if (int e = timed_begin(c, TK_SCAN, es, &tm)) return e;
+    uint32_t *w = c->d_etk_sync[slot];
+    HIP_TRY(kh::launch_eval_topk(c->dc, c->d, d_pods, np, lo, hi, k, vt, c->d_etk_part[slot], c->d_etk_pcnt[slot],
+                                 w + kh::kSelMaxPods, out, sync, sel_par, res_wait, c->d_dbg, es));
+    if (int e = timed_end(c, tm, es)) return e;
+    c->last_launches++;
+    c->last_evals += (int64_t)np * (hi - lo);
+    return 0;
+  }
   const int R = c->partial_r;
   const int64_t stride = ((int64_t)(hi - lo) + 63) & ~63ll;
   const int32_t nchunks = kh::scan_chunks(R, lo, hi);
@@ -415,7 +460,7 @@ int zone_rows(const int64_t *src, const int32_t *cls_of, const uint8_t *flags, c
     *any_policy = true;
     if (!src) return fail(KOORDHIP_EINVAL, "a node has a NUMA topology policy but numa_zone_alloc / numa_zone_used are NULL");
     if (cls_of[i] >= 0 && cls[cls_of[i]].nnuma > Z)
-      return fail(KOORDHIP_EINVAL, "a node with a NUMA topology policy has more than 4 NUMA nodes");
+      return fail(KOORDHIP_EINVAL, "a node with a NUMA topology policy has more NUMA nodes than KOORDHIP_NUMA_MAX_ZONES");
     for (int q = 0; q < 2; q++)
       for (int k = 0; k < NM; k++) {
         const int64_t v = src[((size_t)i * 2 + q) * NM + k];
@@ -617,6 +662,18 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return fail(KOORDHIP_EINVAL, "batch_pods must be in [0, 64]");
   auto *c = new koordhip_ctx();
   c->cfg = *cfg;
+  // evaluation path: k_eval_topk (fused, no score matrix) for the NUMA /
+  // Reservation plugin sets, whose heavier rows make the split path's matrix
+  // round trip the longer chain (config 5: 177k -> 207k pods/s); k_scan +
+  // k_select_split for the plain Fit + LoadAware set, where the fused
+  // launch's 24x column re-reads from L2 cost more than the u16 matrix
+  // (config 4: 43 vs 39.5 us per round).  KOORDHIP_EVAL=fused|split forces one.
+  {
+    const uint32_t pl = cfg->filter_plugins | cfg->score_plugins;
+    c->eval_fused = (pl & (KOORDHIP_PLUGIN_NUMA | KOORDHIP_PLUGIN_RESERVATION)) != 0;
+    if (const char *ev = std::getenv("KOORDHIP_EVAL")) c->eval_fused = std::strcmp(ev, "split") != 0;
+    if (std::getenv("KOORDHIP_EVAL_SPLIT") || std::getenv("KOORDHIP_SELECT_ONEWG")) c->eval_fused = false;
+  }
   // NodeNUMAResource streams are bound by the resolve's cpuset Reserve: shorter
   // rounds re-evaluate fewer stale list entries (config 3: 16 pods 106k, 32 pods 98k pods/s)
   const uint32_t plugins = cfg->filter_plugins | cfg->score_plugins;
@@ -672,15 +729,22 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
         return fail(KOORDHIP_EINVAL, "reservation_weight must exceed 100 x the other score weights");
       }
       max_total = 101 * (max_total + 1) + KOORDHIP_RESV_MAX_ORDERS - 1;
-      if (max_total + 2 > 32768) {
-        delete c;
-        return fail(KOORDHIP_EINVAL, "with Reservation scoring the other score weights may sum to at most 3");
-      }
+    }
+    // ranking totals travel as 32-bit key halves (total + 1); the split
+    // evaluation (k_scan's u16 score matrix) only takes totals below 2^15
+    if (max_total + 2 > (1ll << 30)) {
+      delete c;
+      return fail(KOORDHIP_EINVAL, "score weights too large: the ranking total must stay below 2^30");
+    }
+    if (!c->eval_fused && max_total + 2 > 32768) {
+      delete c;
+      return fail(KOORDHIP_EINVAL, "KOORDHIP_EVAL_SPLIT takes ranking totals below 2^15 only");
     }
     int bits = 1;
     while ((1ll << bits) <= max_total + 1) bits++;
     c->score_bits = bits;
-    c->nbins = (int32_t)max_total + 2;
+    c->nbins = (int32_t)std::min<int64_t>(max_total + 2, 32768);
+    c->dc.wide_keys = max_total + 1 >= 65536 ? 1 : 0;
   }
   int dev = cfg->device;
   if (dev < 0) {
@@ -733,7 +797,8 @@ int koordhip_destroy(koordhip_ctx *c) {
                   (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
                   (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc,
                   (void *)c->d_selpart[0], (void *)c->d_selcnt[0], (void *)c->d_selpart[1], (void *)c->d_selcnt[1],
-                  c->d_upd})
+                  (void *)c->d_etk_part[0], (void *)c->d_etk_part[1], (void *)c->d_etk_pcnt[0],
+                  (void *)c->d_etk_pcnt[1], (void *)c->d_etk_sync[0], (void *)c->d_etk_sync[1], c->d_upd})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -908,7 +973,7 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   struct Col {
     void *dst;
     const void *src;
-    int32_t esize;  // 8, 4 or 1
+    int32_t esize;  // 8, 4 or 1 (or a whole ZoneRow)
     bool q;         // int64 quantity -> f64
     const char *what;
   };
@@ -961,10 +1026,10 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       cols.push_back({rv.rd[k], rows->resv_allocated[k], 8, true, "resv_allocated"});
     }
   }
-  if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one 64-B element per row
+  if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one ZoneRow element per row
     kh::DevNuma &nu = c->d.nu;
-    cols.push_back({const_cast<double *>(nu.za), zrow_a.data(), 64, false, "numa_zone_alloc"});
-    cols.push_back({nu.zu, zrow_u.data(), 64, false, "numa_zone_used"});
+    cols.push_back({const_cast<double *>(nu.za), zrow_a.data(), (int32_t)sizeof(kh::ZoneRow), false, "numa_zone_alloc"});
+    cols.push_back({nu.zu, zrow_u.data(), (int32_t)sizeof(kh::ZoneRow), false, "numa_zone_used"});
   }
   const size_t seg_idx = ((size_t)m * 4 + 7) & ~(size_t)7;
   size_t bytes = seg_idx;
@@ -1004,7 +1069,7 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   for (size_t q = 0; q < cols.size(); q++) {
     const Col &k = cols[q];
     const void *src = dev + off[q];
-    if (k.esize == 64)
+    if (k.esize == (int32_t)sizeof(kh::ZoneRow))
       HIP_TRY(kh::launch_scatter<kh::ZoneRow>(static_cast<kh::ZoneRow *>(k.dst), static_cast<const kh::ZoneRow *>(src),
                                               d_idx, m, c->stream));
     else if (k.esize == 8)
@@ -1133,6 +1198,7 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
     return fail(KOORDHIP_ENOMEM, "eval buffers");
   }
   std::vector<uint64_t> hk(topk ? (size_t)per * k : 0);
+  if (topk) e = eval_buffers(c, std::min(per, n_pods), 0, n, 0, c->stream, k);
   for (int32_t p0 = 0; p0 < n_pods && !e; p0 += per) {
     const int32_t np = std::min(per, n_pods - p0);
     if (hipMemcpyAsync(dp, hp.data() + p0, np * sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
@@ -1400,8 +1466,14 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_eval2, hipEventDisableTiming));
   }
   if (two) HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
-  for (int slot = 0; slot < (two ? 2 : 1) && rounds > 0; slot++)
-    if (int e = eval_buffers(c, std::min(P, total), lo, hi, slot, slot ? c->stream2 : c->stream)) return e;
+  for (int slot = 0; slot < (two ? 2 : 1) && rounds > 0; slot++) {
+    hipStream_t es = slot ? c->stream2 : c->stream;
+    if (int e = eval_buffers(c, std::min(P, total), lo, hi, slot, es, K)) return e;
+    // the per-pod hand-off words start every call at zero (Guideline 16: a
+    // call the watchdog stopped can leave them set); in-kernel resets keep
+    // them zero between the rounds of a call
+    if (c->eval_fused) HIP_TRY(hipMemsetAsync(c->d_etk_sync[slot], 0, 2 * kh::kSelMaxPods * sizeof(uint32_t), es));
+  }
   int32_t res_tm = -1;
   if (persistent && rounds > 0) {
     int32_t tm = -1;
@@ -1424,8 +1496,9 @@ int place_staged_impl(koordhip_ctx *c) {
       if (np < P) HIP_TRY(hipMemsetAsync(lists, 0, (size_t)P * K * sizeof(uint64_t), es));
       if (int e = topk_batch(c, pods, np, K, lo, hi, lists, r % tstride == 0, nullptr, 0, 0, es, slot)) return e;
       if (int e = exchange(c, lists, (size_t)P * K, slot, es)) return e;
+      // the merge counts each pod's list into the pipeline itself (no signal kernel on the chain)
       HIP_TRY(kh::launch_topk_merge(gather_buf(c, slot), K, (int64_t)P * K, np, c->world, K, c->score_bits,
-                                    c->d_final + (size_t)(r & (2 * lag - 1)) * list_buf, es));
+                                    c->d_final + (size_t)(r & (2 * lag - 1)) * list_buf, sync, par, es));
     } else {
       // the split select's merging workgroups count the round's pods into sync->sel[par] themselves
       // (KOORDHIP_FOLD_WAIT: and hold the stream until round r - 1 is resolved, what the next scan needs)
@@ -1433,7 +1506,7 @@ int place_staged_impl(koordhip_ctx *c) {
                              wait_kernel ? 0 : r, es, slot))
         return e;
     }
-    if (exch || !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, par, cum, es));
+    if (!exch && !c->sel_split) HIP_TRY(kh::launch_signal_lists(sync, par, cum, es));
     if (!persistent) {
       if (!serial) {
         HIP_TRY(hipEventRecord(c->ev_res[r % kRing], c->stream));
@@ -1465,6 +1538,12 @@ int place_staged_impl(koordhip_ctx *c) {
                  "[koordhip stamps] select blocks %llu cycles: bound %llu  pass1 %llu  kth %llu  pass2 %llu  out %llu\n",
                  (unsigned long long)h[8], (unsigned long long)h[9], (unsigned long long)h[10],
                  (unsigned long long)h[11], (unsigned long long)h[12], (unsigned long long)h[13]);
+    if (c->eval_fused && h[40])
+      std::fprintf(stderr,
+                   "[koordhip stamps] k_eval_topk: %llu workgroups, cycles per workgroup: evaluate %.0f  select+emit %.0f  "
+                   "publish %.0f | %llu merges, cycles per merge %.0f, candidates per merge %.1f\n",
+                   (unsigned long long)h[40], (double)h[41] / h[40], (double)h[42] / h[40], (double)h[43] / h[40],
+                   (unsigned long long)h[45], h[45] ? (double)h[44] / h[45] : 0.0, h[45] ? (double)h[46] / h[45] : 0.0);
     std::fprintf(stderr,
                  "[koordhip stamps] resolve cycles: prologue walk %llu  hash %llu  waiting for lists %llu  loop %llu  "
                  "release %llu | pods %llu  bulk commits %llu  staged pods %llu  general-path pods %llu  HBM row loads %llu\n",

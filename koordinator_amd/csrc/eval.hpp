@@ -45,6 +45,7 @@ struct DevCfg {
   int32_t amp;                     // some node has a CPU amplification ratio > 1
   int32_t resv;                    // Reservation enabled and the snapshot carries reservation columns
   int32_t resv_b1;                 // 1 + the other plugins' maximum weighted total (resv.hpp ranking total)
+  int32_t wide_keys;               // ranking totals + 1 exceed 16 bits (the resolve's key tables hold u32)
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -179,11 +180,10 @@ __device__ __forceinline__ Need need_all(const DevCfg &c) {
 
 // NodeNUMAResource columns of node i.
 __device__ __forceinline__ void load_zones(NumaRow &r, const DevNodes &d, int32_t i) {
-  const double *za = d.nu.za + (size_t)i * 2 * ZMAX, *zu = d.nu.zu + (size_t)i * 2 * ZMAX;
+  const double *zu = d.nu.zu + (size_t)i * 2 * ZMAX;
+  r.za = d.nu.za + (size_t)i * 2 * ZMAX;  // static: read in place by the zone code
 #pragma unroll
   for (int q = 0; q < ZMAX; q++) {
-    r.za[0][q] = za[q];
-    r.za[1][q] = za[ZMAX + q];
     r.zu[0][q] = zu[q];
     r.zu[1][q] = zu[ZMAX + q];
   }
@@ -422,10 +422,12 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
   double rc = v.r[KOORDHIP_RES_CPU], rm = v.r[KOORDHIP_RES_MEM];
   uint32_t mask = 0;
   if (Z && tp != 0) {  // the affinity stored by Filter's admit, then Allocate with it (:80-89)
-    if (!zone_hint(C.nnuma, r, p, tp, &mask)) return 0;
+    double av[2][ZMAX];
+    zone_avail_all(r, C.nnuma, av);
+    if (!zone_hint(C.nnuma, av, p, tp, &mask)) return 0;
     if (mask) {
       double z[2][ZMAX];
-      if (!zone_alloc(C.nnuma, r, p, mask, z)) return 0;
+      if (!zone_alloc(C.nnuma, av, p, mask, z)) return 0;
       if (cs) {
         uint64_t m[NW];
         if (!(KOORDHIP_NUMA_REQUIRED(p.numa_policy) == KOORDHIP_CPUBIND_NONE ? zone_cpus_ok(C, r, p, z)
@@ -437,8 +439,8 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
 #pragma unroll
       for (int k = 0; k < ZMAX; k++)
         if (zone_used(z, k)) {
-          ac += r.za[0][k];
-          am += r.za[1][k];
+          ac += r.za[k];
+          am += r.za[ZMAX + k];
           rc += r.zu[0][k];
           rm += r.zu[1][k];
         }
@@ -646,9 +648,11 @@ __device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *class
     numa_apply(r, p, cpus, +1);
   } else {
     uint32_t mask;
-    if (!zone_hint(C.nnuma, r, p, tp, &mask)) return false;
+    double av[2][ZMAX];
+    zone_avail_all(r, C.nnuma, av);
+    if (!zone_hint(C.nnuma, av, p, tp, &mask)) return false;
     double z[2][ZMAX];
-    if (mask && !zone_alloc(C.nnuma, r, p, mask, z)) return false;
+    if (mask && !zone_alloc(C.nnuma, av, p, mask, z)) return false;
     if (cs) {
       if (!(mask ? zone_allocate_in(C, r, p, z, cpus) : numa_allocate_in<WAVE>(C, r, p, cpus))) return false;
       numa_apply(r, p, cpus, +1);

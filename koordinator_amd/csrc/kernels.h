@@ -50,9 +50,24 @@ hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, 
                                int32_t nbins, const uint16_t *Mx, int32_t m_stride, int32_t nchunks, int32_t G,
                                uint64_t *part, uint32_t *cnt, uint64_t *out, PipeSync *sync, int32_t sel_par,
                                int32_t res_wait, hipStream_t s);
+// k_eval_topk: evaluation + exact per-pod top-k in one launch, no score
+// matrix: one workgroup per (pod, slice of 256 x VT nodes); each slice hands
+// on its own top-k keys, the pod's last slice merges them into out[p][k]
+// (best first, 0-padded) and, with `sync`, counts the pod into sel[sel_par]
+// (like k_select_split).  part: [n_pods][slices][k] keys, pcnt:
+// [n_pods][slices], arrive: [n_pods] words that are zero before a launch and
+// left zero by it.  eval_topk_vt: the slice width for k-key lists.
+int32_t eval_topk_slices(int VT, int32_t lo, int32_t hi);
+int eval_topk_vt(int nm, int32_t n_cu, int32_t n_pods, int32_t lo, int32_t hi, int32_t k);
+hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t lo,
+                            int32_t hi, int32_t k, int VT, uint64_t *part, int32_t *pcnt, uint32_t *arrive,
+                            uint64_t *out, PipeSync *sync, int32_t sel_par, int32_t res_wait, uint64_t *dbg,
+                            hipStream_t s);
 // lists: ranges ascending with l, equal-score keys in ascending node order
+// sync: optional, sel[sel_par] += 1 per pod once its merged list is published
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
-                             int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s);
+                             int32_t k, int32_t score_bits, uint64_t *out, PipeSync *sync, int32_t sel_par,
+                             hipStream_t s);
 template <typename T>
 hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, hipStream_t s);
 // The round pipeline (kernels.hip): k_resolve resolves rounds [r_begin, r_end)

@@ -255,9 +255,13 @@ __device__ __forceinline__ int32_t block_exclusive_scan(int32_t v, int32_t *wsum
   return base + x - v;
 }
 
+struct PipeSync;
+__device__ void pipe_count_pod(PipeSync *sy, int32_t par);
+
 __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__restrict__ in, int64_t pod_stride,
                                                               int64_t list_stride, int32_t L, int32_t k,
-                                                              int32_t score_bits, uint64_t *__restrict__ out) {
+                                                              int32_t score_bits, uint64_t *__restrict__ out,
+                                                              PipeSync *sy, int32_t sel_par) {
   __shared__ __attribute__((aligned(16))) uint64_t stage[MERGE_STAGE + 128];
   __shared__ int32_t tie_pre[MERGE_MAXL];
   __shared__ uint64_t gtbuf[RES_MAXP];
@@ -378,6 +382,11 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
   }
   const int32_t filled = gt + min(need, all_ties);
   for (int32_t j = filled + t; j < k; j += MERGE_THREADS) o[j] = 0;
+  if (sy) {  // the pod's merged list is published: count it into the pipeline (no signal kernel)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) pipe_count_pod(sy, sel_par);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -980,6 +989,14 @@ __device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// One pod's final list is stored (every wave drained its stores and met at a
+// barrier): agent release, then count it into sel[par] (Guideline 16 counter form).
+__device__ void pipe_count_pod(PipeSync *sy, int32_t par) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_fetch_add(&sy->sel[par], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Spin (one thread) until *p >= v; false when the watchdog fires or the other
 // side reported an error.  Relaxed polls, ONE agent acquire after the match
 // (an acquire per poll costs 2-3x per hop, Guideline 16 Pitfall 5).
@@ -1306,6 +1323,364 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
 }
 
 // ---------------------------------------------------------------------------
+// k_eval_topk: evaluation AND the exact per-pod top-k in one launch, without
+// a score matrix.
+//
+// Workgroup (p, s) evaluates pod p on slice s of the shard (256 x VT nodes:
+// evaluation q of thread t takes node c0 + q * 256 + t, so every column read
+// is a coalesced wave access, and all R evaluations of an iteration have their
+// loads in flight together) and parks the values (total + 1, 0 = infeasible;
+// 32 bits, so any ranking total fits) in LDS.  Thread t then takes the
+// contiguous run [t * VT, t * VT + VT) back into registers -- node order is
+// thread-major from here on -- and the workgroup finds the slice's k-th
+// largest value T by an LDS radix select (11-bit digit histograms from the top
+// digit down: one or two levels for ranking totals below 2^22).  Every node of
+// the pod's top-k scores >= S* >= T and has fewer than k better keys in its
+// slice, so the slice's own top-k -- its keys above T, then its lowest-index
+// ties at T -- holds all of the pod's answer that lies in the slice.  The
+// slice list is written in node order per part ([keys > T][ties at T]), with
+// its length in pcnt[p][s].
+//
+// Hand-off (cdna_hip_programming.md Guideline 16): the list is stored
+// write-through (sc1), every wave drains its stores, a barrier, then one lane
+// adds to arrive[p] (agent scope) -- no release fence, i.e. no L2 write-back
+// per workgroup.  The last slice of pod p to arrive takes one agent acquire,
+// gathers the slice lists (slice order = node order, and inside a list the
+// keys of one value are in node order, so equal values are in node order
+// everywhere), radix-selects their k-th largest value S and writes the final
+// list: the keys above S rank-sorted, then the lowest-index ties at S.  With
+// `sy` it then counts the pod into the pipeline's list counter (release +
+// counter add, like k_select_split), so the resolve needs no signal kernel.
+constexpr int ETK_THREADS = 256;
+constexpr int ETK_WAVES = ETK_THREADS / 64;
+constexpr int ETK_MAX_SLICES = 256;   // one slice list per thread in the merge's offset scan
+constexpr int ETK_MERGE_KEYS = 4096;  // candidates the merge stages in LDS (more: read from L2)
+constexpr int ETK_DIGIT = 11;         // radix-select digit: 2048 bins, 8 per thread
+constexpr int ETK_BINS = 1 << ETK_DIGIT;
+
+struct EtkHdr {
+  uint64_t gtk[RES_MAXP];             // merge: the keys above S (fewer than k)
+  int32_t off[ETK_MAX_SLICES + 1];    // merge: first candidate of each slice list
+  uint32_t hist[ETK_BINS];            // radix-select digit histogram
+  int32_t wsum[ETK_WAVES];            // block scans
+  int32_t rmax[ETK_WAVES], rcnt[ETK_WAVES];
+  int32_t cnt_gt, last, sel_b, sel_above;
+};
+constexpr int32_t ETK_HDR = (int32_t)((sizeof(EtkHdr) + 15) & ~(size_t)15);
+
+// block max of v and sum of c, one barrier
+__device__ __forceinline__ void etk_maxsum(uint32_t v, int32_t c, EtkHdr &h, uint32_t *mx, int32_t *sum) {
+  v = (uint32_t)wave_max_u32_dpp(v);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
+  if (lane_id() == 0) {
+    h.rmax[threadIdx.x >> 6] = (int32_t)v;
+    h.rcnt[threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  uint32_t m = 0;
+  int32_t s = 0;
+#pragma unroll
+  for (int w = 0; w < ETK_WAVES; w++) {
+    m = max(m, (uint32_t)h.rmax[w]);
+    s += h.rcnt[w];
+  }
+  *mx = m;
+  *sum = s;
+}
+
+// The k-th largest T of the block's values (every thread passes its values
+// through `each`, which calls its argument once per value) and gt = how many
+// values exceed T; T = 1 and gt = #values > 1 when at most k are nonzero.
+// top: the largest value; nnz: the nonzero count.  Radix select, one 11-bit
+// digit per level from the top: histogram of the digit among the values that
+// match the digits fixed so far, then the bucket where the count from the top
+// reaches k (thread t owns bins [2040 - 8t, 2048 - 8t): a block prefix over
+// threads is a count from the top).
+template <typename F>
+__device__ __forceinline__ uint32_t etk_kth(F each, uint32_t top, int32_t nnz, int32_t k, EtkHdr &h, int32_t *gt_out) {
+  const int t = threadIdx.x;
+  if (nnz <= k || top <= 1) {
+    int32_t g = 0;
+    each([&](uint32_t v) { g += v > 1u; });
+    uint32_t dummy;
+    int32_t tot;
+    etk_maxsum(0u, g, h, &dummy, &tot);
+    *gt_out = tot;
+    return 1u;
+  }
+  const int hb = 31 - __builtin_clz(top);
+  int shift = max(0, hb + 1 - ETK_DIGIT);
+  int fixed = 32;       // bits >= fixed are fixed to prefix's
+  uint32_t prefix = 0;
+  int32_t above = 0;    // values above every bucket range examined (they exceed T)
+  for (;;) {
+    uint4 *h4 = reinterpret_cast<uint4 *>(h.hist);
+    for (int x = t; x < ETK_BINS / 4; x += ETK_THREADS) h4[x] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    each([&](uint32_t v) {
+      if (v != 0u && (fixed >= 32 || (v >> fixed) == (prefix >> fixed)))
+        atomicAdd(&h.hist[(v >> shift) & (ETK_BINS - 1)], 1u);
+    });
+    __syncthreads();
+    const int b0 = ETK_BINS - 8 * (t + 1);  // this thread's 8 bins, from the top
+    uint32_t c[8];
+    int32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      c[j] = h.hist[b0 + 7 - j];
+      mine += (int32_t)c[j];
+    }
+    int32_t total;
+    const int32_t incl = block_scan_incl<ETK_WAVES>(mine, h.wsum, &total);
+    const int32_t before = above + incl - mine;  // values in the digit buckets above this thread's
+    if (before < k && before + mine >= k) {      // exactly one thread
+      int32_t run = before;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        if (run + (int32_t)c[j] >= k) {
+          h.sel_b = b0 + 7 - j;
+          h.sel_above = run;
+          break;
+        }
+        run += (int32_t)c[j];
+      }
+    }
+    __syncthreads();
+    const uint32_t b = (uint32_t)h.sel_b;
+    above = h.sel_above;
+    prefix |= b << shift;
+    if (shift == 0) break;
+    fixed = shift;
+    shift = max(0, shift - ETK_DIGIT);
+    __syncthreads();  // h.sel_* / hist reused by the next level
+  }
+  *gt_out = above;
+  return prefix;
+}
+
+template <int NM, int VT, int R>
+__global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM >= 3 ? 4 : 1))) void k_eval_topk(
+    DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods, int32_t lo, int32_t hi, int32_t nslices,
+    int32_t spx, int32_t k, uint64_t *part, int32_t *pcnt, uint32_t *arrive, uint64_t *__restrict__ out,
+    PipeSync *__restrict__ sy, int32_t sel_par, int32_t res_wait, int32_t stage_cap, uint64_t *dbg) {
+  static_assert(VT % 4 == 0 && VT % R == 0, "slice shape");
+  constexpr int32_t SL = ETK_THREADS * VT;
+  // slice values, or (merge) up to stage_cap candidate keys: what the launch sized
+  const int32_t VBYTES = (SL * 4 > stage_cap * 8) ? SL * 4 : stage_cap * 8;
+  extern __shared__ __attribute__((aligned(16))) char etk_lds[];
+  EtkHdr &h = *reinterpret_cast<EtkHdr *>(etk_lds);
+  uint32_t *vals = reinterpret_cast<uint32_t *>(etk_lds + ETK_HDR);  // slice values, then merge candidates
+  uint64_t *mk = reinterpret_cast<uint64_t *>(etk_lds + ETK_HDR);
+  // dbg (KOORDHIP_STAMPS): per-phase s_memtime sums of thread 0 at dbg[40..47]
+  uint64_t ts[4] = {0, 0, 0, 0};
+  // XCD-aware: block b runs on XCD b % 8, which owns slices [xcd * spx, ...):
+  // a slice's pods are consecutive blocks of one XCD and share its columns in L2
+  const int32_t b = blockIdx.x, xcd = b & 7, local = b >> 3;
+  const int32_t p = local % n_pods;
+  const int32_t s = xcd * spx + local / n_pods;
+  if (s >= nslices) return;  // block-uniform
+  const int t = threadIdx.x;
+  if (dbg && t == 0) ts[0] = stamp();
+  const DevNumaClass *cls = d.nu.cls;
+  if constexpr (NM != 0) {  // topology classes -> LDS (launch_eval_topk sizes it when ncls <= NUMA_LDS_CLASSES)
+    if (d.nu.ncls <= NUMA_LDS_CLASSES) {
+      uint4 *dst = reinterpret_cast<uint4 *>(etk_lds + ETK_HDR + VBYTES);
+      const uint4 *src = reinterpret_cast<const uint4 *>(d.nu.cls);
+      for (int32_t x = t; x < d.nu.ncls * (int32_t)(sizeof(DevNumaClass) / 16); x += ETK_THREADS) dst[x] = src[x];
+      __syncthreads();
+      cls = reinterpret_cast<const DevNumaClass *>(dst);
+    }
+  }
+  const DevPod pod = pods[p];
+  const Need need = pod_needs(pod, c);
+  const int32_t c0 = lo + s * SL;
+  // ---- evaluate: R nodes in flight per thread, values parked in LDS
+  uint32_t vmax = 0;
+  int32_t vnz = 0;
+#pragma unroll 1
+  for (int q0 = 0; q0 < VT; q0 += R) {
+    uint32_t sv[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int32_t i = c0 + (q0 + r) * ETK_THREADS + t;
+      int32_t tot = -1;
+      if (i < hi) {
+        NV v;
+        load_node(v, d, i, need, c);
+        if constexpr (NM == 3) {
+          NumaRowR nr;
+          load_numa<false>(nr, d, i, need);
+          load_resv(nr, d.rv, i);
+          tot = eval_total_resv(pod, v, nr, cls, c);
+        } else if constexpr (NM != 0) {
+          NumaRow nr;
+          load_numa<NM == 2>(nr, d, i, need);
+          tot = eval_total_numa<NM == 2>(pod, v, nr, cls, c);
+        } else {
+          tot = eval_total(pod, v, c);
+        }
+      }
+      sv[r] = (uint32_t)(tot + 1);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      vals[(q0 + r) * ETK_THREADS + t] = sv[r];
+      vmax = max(vmax, sv[r]);
+      vnz += sv[r] != 0u;
+    }
+  }
+  uint32_t top;
+  int32_t nnz;
+  etk_maxsum(vmax, vnz, h, &top, &nnz);  // (its barrier also publishes vals)
+  if (dbg && t == 0) ts[1] = stamp();
+  uint32_t v[VT];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(vals + t * VT);
+#pragma unroll
+    for (int q = 0; q < VT / 4; q++) {
+      const uint4 x = src[q];
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+  }
+  int32_t gt;
+  const uint32_t T = etk_kth(
+      [&](auto f) {
+#pragma unroll
+        for (int q = 0; q < VT; q++) f(v[q]);
+      },
+      top, nnz, k, h, &gt);
+  // the slice list: its keys above T, then its first k - gt ties at T, each
+  // part in node order (one block scan of packed per-thread counts)
+  int32_t ngt = 0, nt = 0;
+#pragma unroll
+  for (int q = 0; q < VT; q++) {
+    ngt += v[q] > T;
+    nt += v[q] == T;
+  }
+  int32_t packed_total;
+  const int32_t pre = block_scan_incl<ETK_WAVES>((ngt << 16) | nt, h.wsum, &packed_total) - ((ngt << 16) | nt);
+  const int32_t all_ties = packed_total & 0xFFFF;
+  const int32_t tie_budget = k - gt;
+  uint64_t *dst = part + ((size_t)p * nslices + s) * k;
+  {
+    int32_t pg = pre >> 16, pt = pre & 0xFFFF;
+#pragma unroll
+    for (int q = 0; q < VT; q++) {
+      const uint64_t key = ((uint64_t)v[q] << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(c0 + t * VT + q));
+      if (v[q] > T) {
+        __hip_atomic_store(dst + pg, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+        pg++;
+      } else if (v[q] == T) {
+        if (pt < tie_budget) __hip_atomic_store(dst + gt + pt, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pt++;
+      }
+    }
+  }
+  const int32_t emitted = gt + min(tie_budget, all_ties);
+  if (t == 0) __hip_atomic_store(pcnt + (size_t)p * nslices + s, emitted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (dbg && t == 0) ts[2] = stamp();
+  // ---- publish (Guideline 16 R1: every wave drains its sc1 stores, barrier,
+  //      one relaxed agent-scope counter add); the pod's last slice merges
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&arrive[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t last = old + 1 == (uint32_t)nslices;
+    if (last) {
+      __hip_atomic_store(&arrive[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    h.last = last;
+    h.cnt_gt = 0;
+  }
+  __syncthreads();
+  if (dbg && t == 0) {
+    ts[3] = stamp();
+    for (int q = 1; q < 4; q++) atomicAdd((unsigned long long *)&dbg[40 + q], (unsigned long long)(ts[q] - ts[q - 1]));
+    atomicAdd((unsigned long long *)&dbg[40], 1ull);
+  }
+  if (!h.last) return;  // block-uniform
+  // ---- merge: offsets of the slice lists (one per thread), then the candidates
+  const int32_t ns = t < nslices ? pcnt[(size_t)p * nslices + t] : 0;
+  int32_t total;
+  const int32_t o0 = block_scan_incl<ETK_WAVES>(ns, h.wsum, &total) - ns;
+  if (t < nslices) h.off[t] = o0;
+  if (t == 0) h.off[nslices] = total;
+  __syncthreads();
+  const bool staged = total <= stage_cap;
+  const uint64_t *src = part + (size_t)p * nslices * k;
+  auto gkey = [&](int32_t x) -> uint64_t {  // candidate x (flattened slice order) from L2
+    int32_t a = 0, z = nslices;               // largest slice a with off[a] <= x
+    while (z - a > 1) {
+      const int32_t m = (a + z) >> 1;
+      if (h.off[m] <= x) a = m; else z = m;
+    }
+    return src[(size_t)a * k + (x - h.off[a])];
+  };
+  // thread t owns the flattened run [x0, x1): node order is thread-major
+  const int32_t per = (total + ETK_THREADS - 1) / ETK_THREADS;
+  const int32_t x0 = min(total, t * per), x1 = min(total, x0 + per);
+  if (staged)
+    for (int32_t x = x0; x < x1; x++) mk[x] = gkey(x);
+  auto key = [&](int32_t x) -> uint64_t { return staged ? mk[x] : gkey(x); };
+  uint32_t mtop = 0;
+  for (int32_t x = x0; x < x1; x++) mtop = max(mtop, (uint32_t)(key(x) >> 32));
+  uint32_t mmax;
+  int32_t dummy;
+  etk_maxsum(mtop, 0, h, &mmax, &dummy);
+  int32_t mgt;
+  const uint32_t S = etk_kth(
+      [&](auto f) {
+        for (int32_t x = x0; x < x1; x++) f((uint32_t)(key(x) >> 32));
+      },
+      mmax, total, k, h, &mgt);
+  // keys above S (fewer than k) rank-sorted; ties at S in flattened order
+  int32_t myt = 0;
+  for (int32_t x = x0; x < x1; x++) {
+    const uint64_t kk = key(x);
+    const uint32_t sc = (uint32_t)(kk >> 32);
+    if (sc > S) h.gtk[atomicAdd(&h.cnt_gt, 1)] = kk;
+    myt += sc == S;
+  }
+  int32_t mties;
+  const int32_t tpos0 = block_scan_incl<ETK_WAVES>(myt, h.wsum, &mties) - myt;  // (its barriers order the gtk adds)
+  const int32_t mneed = k - mgt;
+  uint64_t *o = out + (size_t)p * k;
+  for (int32_t j = t; j < mgt; j += ETK_THREADS) {
+    const uint64_t x = h.gtk[j];
+    int32_t rank = 0;
+    for (int32_t q = 0; q < mgt; q++) rank += h.gtk[q] > x;
+    o[rank] = x;
+  }
+  {
+    int32_t pos = tpos0;
+    for (int32_t x = x0; x < x1 && pos < mneed; x++) {
+      const uint64_t kk = key(x);
+      if ((uint32_t)(kk >> 32) == S) o[mgt + pos++] = kk;
+    }
+  }
+  for (int32_t j = mgt + min(mneed, mties) + t; j < k; j += ETK_THREADS) o[j] = 0ull;
+  if (dbg && t == 0) {
+    atomicAdd((unsigned long long *)&dbg[44], (unsigned long long)(stamp() - ts[3]));
+    atomicAdd((unsigned long long *)&dbg[45], 1ull);
+    atomicAdd((unsigned long long *)&dbg[46], (unsigned long long)total);
+  }
+  if (sy) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      pipe_count_pod(sy, sel_par);
+      if (res_wait > 0) (void)wait_at_least(&sy->res_round, res_wait, sy);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_resolve: the sequential greedy over the staged stream -- one persistent
 // workgroup, rounds of n_pods <= 64 pods, lag-1 pipelined with the evaluation
 // of the next round.
@@ -1375,6 +1750,7 @@ __device__ __forceinline__ NV slot_row(const NV &src) {
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
       dec_key, dec_n, dec_src, dec_e, dec_c, moved, mhash, gbits, kpre, ktab, ready, classes, modmap, total;
+  int32_t kwide;  // key-table entries are u32 (ranking totals above 16 bits), else u16
   // second copies of the per-round inputs, filled by waves 1.. while wave 0
   // resolves the previous round (overlap = 0: every round loads serially)
   int32_t overlap, lists2, pods2, pre_rows2, pre_numa2, pre_node2;
@@ -1383,7 +1759,8 @@ struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
 
 __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, int32_t nrow,
-                                          bool overlap = false, bool tables = true, int32_t lag = 1) {
+                                          bool overlap = false, bool tables = true, int32_t lag = 1,
+                                          bool wide = false) {
   const bool numa = nrow > 0;  // nrow: bytes of a NUMA side row (0: none)
   ResLds o;
   int32_t at = 0;
@@ -1430,19 +1807,20 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += 2 * RES_MHASH * 4;
   o.gbits = at;  // the nodes general-path pods committed to this round
   at += bitmap;
-  // helper waves' key tables, per pod l (total + 1 as u16, 0 = infeasible):
+  // helper waves' key tables, per pod l (total + 1 as u16 / u32, 0 = infeasible):
   // kpre[l][i] on the row staged pod i commits to (its staged source row +
   // its Reserve delta), ktab[l][s] on M' row s; ready[l] once both are written
   // (tables = false when they do not fit: kpre = -1, the general path then
   // always evaluates and the helper waves idle)
   o.kpre = o.ktab = -1;
+  o.kwide = wide ? 1 : 0;
   o.ready = at;
   at += RES_MAXP_ROUND * 4;
   if (tables) {
     o.kpre = at;
-    at += RES_MAXP_ROUND * RES_MAXP_ROUND * 2;
+    at += RES_MAXP_ROUND * RES_MAXP_ROUND * (wide ? 4 : 2);
     o.ktab = at;
-    at += RES_MAXP_ROUND * RES_MAXP_ROUND * 2;
+    at += RES_MAXP_ROUND * RES_MAXP_ROUND * (wide ? 4 : 2);
   }
   o.classes = at;  // NodeNUMAResource topology classes (when <= NUMA_LDS_CLASSES)
   at += numa ? NUMA_LDS_CLASSES * (int32_t)sizeof(DevNumaClass) : 0;
@@ -1557,8 +1935,18 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   int32_t *mkey = reinterpret_cast<int32_t *>(lds + ofs.mhash);
   int32_t *mval = mkey + RES_MHASH;
   uint32_t *gbits = reinterpret_cast<uint32_t *>(lds + ofs.gbits);
-  uint16_t *kpre = reinterpret_cast<uint16_t *>(lds + (ofs.kpre >= 0 ? ofs.kpre : 0));
-  uint16_t *ktab = reinterpret_cast<uint16_t *>(lds + (ofs.ktab >= 0 ? ofs.ktab : 0));
+  char *kpre = lds + (ofs.kpre >= 0 ? ofs.kpre : 0);
+  char *ktab = lds + (ofs.ktab >= 0 ? ofs.ktab : 0);
+  const bool kwide = ofs.kwide != 0;  // wave-uniform
+  auto kget = [kwide](const char *tb, int32_t x) -> uint32_t {
+    return kwide ? reinterpret_cast<const uint32_t *>(tb)[x] : (uint32_t)reinterpret_cast<const uint16_t *>(tb)[x];
+  };
+  auto kput = [kwide](char *tb, int32_t x, uint32_t v) {
+    if (kwide)
+      reinterpret_cast<uint32_t *>(tb)[x] = v;
+    else
+      reinterpret_cast<uint16_t *>(tb)[x] = (uint16_t)v;
+  };
   const bool have_tables = ofs.kpre >= 0;
   int32_t *ready = reinterpret_cast<int32_t *>(lds + ofs.ready);
   uint32_t *modmap = reinterpret_cast<uint32_t *>(lds + ofs.modmap);
@@ -2055,11 +2443,11 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               }
               uint64_t k2 = 0;
               if (i >= 0 && i < 64 && ((cstaged >> i) & 1ull) && !xbit(gbits, y)) {
-                k2 = ktab_key(kpre[g * RES_MAXP_ROUND + i], y);
+                k2 = ktab_key(kget(kpre, g * RES_MAXP_ROUND + i), y);
               } else {
                 const int32_t sl = mp > 0 ? prev_slot(y) : -1;
                 if (sl >= 0 && !moved[sl]) {
-                  k2 = ktab_key(ktab[g * RES_MAXP_ROUND + sl], y);
+                  k2 = ktab_key(kget(ktab, g * RES_MAXP_ROUND + sl), y);
                 } else {
                   need = true;
                 }
@@ -2337,13 +2725,13 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               apply_delta(row, pi, +1);
               v = eval_row<NM>(pod, row, nr, cls, c) + 1;
             }
-            kpre[l * RES_MAXP_ROUND + x] = (uint16_t)v;
+            kput(kpre, l * RES_MAXP_ROUND + x, (uint32_t)v);
           } else if (x < l + mp) {  // M' slot s
             const int32_t sl = x - l;
             NR nr;
             if constexpr (NUMA) nr = pnr[sl];
             v = eval_row<NM>(pod, slot_row(prow[sl]), nr, cls, c) + 1;
-            ktab[l * RES_MAXP_ROUND + sl] = (uint16_t)v;
+            kput(ktab, l * RES_MAXP_ROUND + sl, (uint32_t)v);
           }
         }
         if (lane == 0) __hip_atomic_store(&ready[l], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2639,11 +3027,101 @@ hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, 
   return hipGetLastError();
 }
 
+__global__ void k_empty_lists(uint64_t *out, int32_t n, PipeSync *sy, int32_t par, int32_t pods) {
+  for (int32_t j = threadIdx.x; j < n; j += blockDim.x) out[j] = 0ull;
+  if (sy) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&sy->sel[par], pods, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+int32_t eval_topk_slices(int VT, int32_t lo, int32_t hi) {
+  const int32_t sl = ETK_THREADS * VT;
+  return hi > lo ? (hi - lo + sl - 1) / sl : 0;
+}
+
+int eval_topk_vt(int nm, int32_t n_cu, int32_t n_pods, int32_t lo, int32_t hi, int32_t k) {
+  if (const char *e = std::getenv("KOORDHIP_ETK_VT")) {
+    const int v = std::atoi(e);
+    if (v == 8 || v == 16 || v == 32) return eval_topk_slices(v, lo, hi) <= ETK_MAX_SLICES ? v : 32;
+  }
+  (void)nm;
+  (void)n_cu;
+  (void)n_pods;
+  // the narrowest slices (most workgroups, shortest evaluation chains) whose
+  // lists the merge still stages in LDS
+  for (int v : {8, 16})
+    if (eval_topk_slices(v, lo, hi) <= ETK_MAX_SLICES && (int64_t)eval_topk_slices(v, lo, hi) * k <= ETK_MERGE_KEYS)
+      return v;
+  return 32;
+}
+
+hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *pods, int32_t n_pods, int32_t lo,
+                            int32_t hi, int32_t k, int VT, uint64_t *part, int32_t *pcnt, uint32_t *arrive,
+                            uint64_t *out, PipeSync *sync, int32_t sel_par, int32_t res_wait, uint64_t *dbg,
+                            hipStream_t s) {
+  if (n_pods <= 0) return hipSuccess;
+  if (k < 1 || k > RES_MAXP || n_pods > kSelMaxPods) return hipErrorInvalidValue;
+  const int32_t nslices = eval_topk_slices(VT, lo, hi);
+  if (nslices > ETK_MAX_SLICES) return hipErrorInvalidValue;
+  if (nslices == 0) {  // an empty shard: empty lists (and the pods counted in, like a merge would)
+    hipLaunchKernelGGL(k_empty_lists, dim3(1), dim3(256), 0, s, out, n_pods * k, sync, sel_par, n_pods);
+    return hipGetLastError();
+  }
+  const int nm = side_mode(c);
+  const int32_t sl = ETK_THREADS * VT;
+  // merge staging: as many candidates as the slice lists can hold, up to ETK_MERGE_KEYS
+  const int32_t stage_cap = (int32_t)std::min<int64_t>((int64_t)nslices * k, ETK_MERGE_KEYS);
+  const size_t vbytes = (size_t)std::max<int32_t>(sl * 4, stage_cap * 8);
+  const size_t lds = (size_t)ETK_HDR + vbytes +
+                     ((nm != 0 && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0);
+  const int32_t spx = (nslices + 7) / 8;
+  const int32_t blocks = 8 * spx * n_pods;
+  static bool attr[5][3] = {};
+  const int vi = VT == 8 ? 0 : (VT == 16 ? 1 : 2);
+#define KH_ETK(NN, VV, RR)                                                                                          \
+  do {                                                                                                              \
+    if (!attr[NN][vi]) {                                                                                            \
+      const hipError_t e = hipFuncSetAttribute((const void *)k_eval_topk<NN, VV, RR>,                              \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);              \
+      if (e != hipSuccess) return e;                                                                                \
+      attr[NN][vi] = true;                                                                                          \
+    }                                                                                                               \
+    hipLaunchKernelGGL((k_eval_topk<NN, VV, RR>), dim3(blocks), dim3(ETK_THREADS), lds, s, c, d, pods, n_pods, lo,    \
+                       hi, nslices, spx, k, part, pcnt, arrive, out, sync, sel_par, res_wait, stage_cap, dbg);      \
+  } while (0)
+  // R: evaluations in flight per thread (all of a slice's for the plain plugin
+  // set; the NUMA / Reservation rows are large: two or four at a time)
+  switch (nm * 4 + vi) {
+    case 0: KH_ETK(0, 8, 8); break;
+    case 1: KH_ETK(0, 16, 8); break;
+    case 2: KH_ETK(0, 32, 8); break;
+    case 4: KH_ETK(1, 8, 2); break;
+    case 5: KH_ETK(1, 16, 2); break;
+    case 6: KH_ETK(1, 32, 2); break;
+    case 8: KH_ETK(2, 8, 2); break;
+    case 9: KH_ETK(2, 16, 2); break;
+    case 10: KH_ETK(2, 32, 2); break;
+    case 12: KH_ETK(3, 8, 4); break;
+    case 13: KH_ETK(3, 16, 4); break;
+    case 14: KH_ETK(3, 32, 4); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef KH_ETK
+  return hipGetLastError();
+}
+
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
-                             int32_t k, int32_t score_bits, uint64_t *out, hipStream_t s) {
-  if (score_bits > 16 || L > MERGE_MAXL) return hipErrorInvalidValue;
+                             int32_t k, int32_t score_bits, uint64_t *out, PipeSync *sync, int32_t sel_par,
+                             hipStream_t s) {
+  if (score_bits > 31 || L > MERGE_MAXL) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_topk_merge, dim3(n_pods), dim3(MERGE_THREADS), 0, s, in, pod_stride, list_stride, L, k,
-                     score_bits, out);
+                     score_bits, out, sync, sel_par);
   return hipGetLastError();
 }
 
@@ -2682,10 +3160,11 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   // then without the preload, then without the tables
   const bool pre = r_end - r_begin > 1 && !std::getenv("KOORDHIP_NO_PRELOAD");
   const bool tab = !std::getenv("KOORDHIP_NO_KEY_TABLES");
-  ResLds o = res_lds(P, kp, d.n, nrow, pre, tab, lag);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag);
+  const bool wide = c.wide_keys != 0;
+  ResLds o = res_lds(P, kp, d.n, nrow, pre, tab, lag, wide);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag, wide);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag, wide);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag, wide);
   static bool attr[8] = {false, false, false, false, false, false, false, false};
   const int ai = nm * 2 + (dbg ? 1 : 0);
   if (!attr[ai]) {

@@ -1,6 +1,6 @@
 // numa.hpp -- NodeNUMAResource on CDNA4 (maxRefCount 1, no
 // reservation-preferred CPUs, cpus_per_core 1 or 2; NUMA topology policies
-// None / BestEffort / Restricted / SingleNUMANode over <= 4 NUMA zones).
+// None / BestEffort / Restricted / SingleNUMANode over <= 8 NUMA zones).
 //
 // Node state is a handful of 4 x 64-bit masks over core-major CPU positions
 // (pos = core_rank * cpc + t), so a core is an aligned group of cpc bits:
@@ -72,8 +72,10 @@ struct NumaRow {
   int32_t pad;
   uint64_t fr[NW], ep[NW], en[NW];
   // NUMA zones of a node with a topology policy (zone k = NUMA node rank k):
-  // NRT allocatable and NodeAllocation.allocatedResources, [cpu milli, memory][zone]
-  double za[2][ZMAX];
+  // the NRT allocatable is static and stays in HBM (za: the node's [2][ZMAX]
+  // row there, read only by the zone code); NodeAllocation.allocatedResources
+  // is mutable and travels with the row, [cpu milli, memory][zone]
+  const double *za;
   double zu[2][ZMAX];
   double amp;  // CPU amplification ratio (1 unless loaded)
 };
@@ -103,6 +105,7 @@ struct DevResv {
 struct ZoneRow {  // one node's [2][ZMAX] zone row (update_nodes scatter element)
   double v[2 * ZMAX];
 };
+static_assert(sizeof(ZoneRow) == 128, "zone rows are 8 zones x 2 resources");
 
 __device__ __forceinline__ int topo_policy(uint32_t nflags) {
   return (int)KOORDHIP_NODE_NUMA_POLICY(nflags);
@@ -800,35 +803,67 @@ __device__ __attribute__((noinline)) bool numa_allocate(const DevNumaClass &C, c
 // narrowest non-empty AND of two minimal masks; no list or an empty S is a
 // provider without preference ({default affinity, preferred}).
 
-// getAvailableNUMANodeResources: allocatable - allocated, non-negative
-__device__ __forceinline__ double zone_avail(const NumaRow &r, int res, int k) {
-  const double a = r.za[res][k] - r.zu[res][k];
-  return a > 0.0 ? a : 0.0;
+// getAvailableNUMANodeResources: allocatable - allocated, non-negative, of
+// every zone (one pass over the row's HBM allocatable)
+__device__ __forceinline__ void zone_avail_all(const NumaRow &r, int M, double av[2][ZMAX]) {
+#pragma unroll
+  for (int k = 0; k < ZMAX; k++)
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const double a = k < M ? r.za[q * ZMAX + k] - r.zu[q][k] : 0.0;
+      av[q][k] = a > 0.0 ? a : 0.0;
+    }
 }
 
-// bitmask.IsNarrowerThan order as one integer (masks < 16)
-__device__ __forceinline__ int narrow_key(uint32_t m) { return __popc(m) * 16 + (int)m; }
+// bitmask.IsNarrowerThan order as one integer (masks < 256)
+__device__ __forceinline__ int narrow_key(uint32_t m) { return __popc(m) * 256 + (int)m; }
 
-// Merge + canAdmitPodResult for policy tp; *mask = the hint (0 = nil affinity)
-__device__ __forceinline__ bool zone_hint(int M, const NumaRow &r, const DevPod &p, int tp, uint32_t *mask) {
+// Merge + canAdmitPodResult for policy tp; *mask = the hint (0 = nil affinity).
+// S (256 bits): the zone masks whose summed availability covers the request,
+// enumerated in Gray-code order so each mask's sums are one add / subtract
+// away from the previous mask's (exact: integers below 2^53).
+__device__ __forceinline__ bool zone_hint(int M, const double av[2][ZMAX], const DevPod &p, int tp, uint32_t *mask) {
   const double qc = p.req[KOORDHIP_RES_CPU], qm = p.req[KOORDHIP_RES_MEM];
   const bool rc = qc != 0.0, rm = qm != 0.0;
   const uint32_t all = (1u << M) - 1u;
-  uint32_t S = 0;
+  uint32_t S[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int minsize = M;
-  for (uint32_t m = 1; m <= all; m++) {  // generateResourceHints :384-428
-    double sc = 0.0, sm = 0.0;
-    for (int k = 0; k < ZMAX; k++)
-      if ((m >> k) & 1u) {
-        sc += zone_avail(r, 0, k);
-        sm += zone_avail(r, 1, k);
+  double sc = 0.0, sm = 0.0;
+  for (uint32_t i = 1; i <= all; i++) {  // generateResourceHints :384-428
+    const uint32_t m = i ^ (i >> 1), b = __builtin_ctz(i);
+    const double dc = av[0][0], dm = av[1][0];  // (placeholders: the switch below picks zone b)
+    double zc = dc, zm = dm;
+#pragma unroll
+    for (int k = 1; k < ZMAX; k++)
+      if ((int)b == k) {
+        zc = av[0][k];
+        zm = av[1][k];
       }
+    if ((m >> b) & 1u) {
+      sc += zc;
+      sm += zm;
+    } else {
+      sc -= zc;
+      sm -= zm;
+    }
     if ((!rc || qc <= sc) && (!rm || qm <= sm)) {
-      S |= 1u << m;
+#pragma unroll
+      for (int w = 0; w < 8; w++)
+        if ((int)(m >> 5) == w) S[w] |= 1u << (m & 31);
       minsize = min(minsize, __popc(m));
     }
   }
-  if ((!rc && !rm) || S == 0) {  // no hints: {default, preferred}
+  auto inS = [&](uint32_t m) -> bool {
+    uint32_t x = 0;
+#pragma unroll
+    for (int w = 0; w < 8; w++)
+      if ((int)(m >> 5) == w) x = S[w];
+    return (x >> (m & 31)) & 1u;
+  };
+  bool any = false;
+#pragma unroll
+  for (int w = 0; w < 8; w++) any |= S[w] != 0u;
+  if ((!rc && !rm) || !any) {  // no hints: {default, preferred}
     *mask = tp == (int)KOORDHIP_NUMA_TOPO_SINGLE_NUMA_NODE ? 0u : all;
     return true;
   }
@@ -836,27 +871,25 @@ __device__ __forceinline__ bool zone_hint(int M, const NumaRow &r, const DevPod 
     if (minsize != 1) return false;                        // nothing survives the filter: {default, false}
     uint32_t best = 0;
     for (int k = M - 1; k >= 0; k--)
-      if ((S >> (1u << k)) & 1u) best = 1u << k;
+      if (inS(1u << k)) best = 1u << k;
     *mask = best == all ? 0u : best;
     return true;
   }
+  // preferred merged hints: AND of one minimal mask per requested resource
+  // (both lists are S); the narrowest non-empty one wins (policy.go:124-169)
   uint32_t best = all;
   int bk = 1 << 30;
   for (uint32_t a = 1; a <= all; a++) {
-    if (!((S >> a) & 1u) || __popc(a) != minsize) continue;
-    if (!(rc && rm)) {
-      if (narrow_key(a) < bk) {
-        bk = narrow_key(a);
-        best = a;
-      }
-      continue;
+    if (__popc(a) != minsize || !inS(a)) continue;
+    if (narrow_key(a) < bk) {  // a & a
+      bk = narrow_key(a);
+      best = a;
     }
-    for (uint32_t b = 1; b <= all; b++) {
-      if (!((S >> b) & 1u) || __popc(b) != minsize || !(a & b)) continue;
-      if (narrow_key(a & b) < bk) {
-        bk = narrow_key(a & b);
-        best = a & b;
-      }
+    if (!(rc && rm)) continue;
+    for (uint32_t b = a + 1; b <= all; b++) {
+      if (__popc(b) != minsize || !(a & b) || narrow_key(a & b) >= bk || !inS(b)) continue;
+      bk = narrow_key(a & b);
+      best = a & b;
     }
   }
   *mask = best;
@@ -865,7 +898,8 @@ __device__ __forceinline__ bool zone_hint(int M, const NumaRow &r, const DevPod 
 
 // allocateResourcesByHint (:166-242): the hinted zones in ascending id take
 // min(available, still requested) of cpu and memory
-__device__ __forceinline__ bool zone_alloc(int M, const NumaRow &r, const DevPod &p, uint32_t mask, double z[2][ZMAX]) {
+__device__ __forceinline__ bool zone_alloc(int M, const double av[2][ZMAX], const DevPod &p, uint32_t mask,
+                                           double z[2][ZMAX]) {
   double rem[2] = {p.req[KOORDHIP_RES_CPU], p.req[KOORDHIP_RES_MEM]};
 #pragma unroll
   for (int k = 0; k < ZMAX; k++) {
@@ -874,8 +908,7 @@ __device__ __forceinline__ bool zone_alloc(int M, const NumaRow &r, const DevPod
     if (k < M && ((mask >> k) & 1u)) {
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const double av = zone_avail(r, q, k);
-        const double a = av < rem[q] ? av : rem[q];
+        const double a = av[q][k] < rem[q] ? av[q][k] : rem[q];
         z[q][k] = a;
         rem[q] -= a;
       }
@@ -934,9 +967,11 @@ __device__ __attribute__((noinline)) bool zone_allocate(const DevNumaClass &C, c
 // Filter's FilterByNUMANode -> Admit -> Allocate on a policy node (topology_hint.go:30-86)
 __device__ __forceinline__ bool numa_policy_ok(const DevNumaClass &C, const NumaRow &r, const DevPod &p) {
   uint32_t mask;
-  if (!zone_hint(C.nnuma, r, p, topo_policy(r.nflags), &mask)) return false;
+  double av[2][ZMAX];
+  zone_avail_all(r, C.nnuma, av);
+  if (!zone_hint(C.nnuma, av, p, topo_policy(r.nflags), &mask)) return false;
   double z[2][ZMAX];
-  if (mask && !zone_alloc(C.nnuma, r, p, mask, z)) return false;
+  if (mask && !zone_alloc(C.nnuma, av, p, mask, z)) return false;
   if (!(p.flags & KOORDHIP_POD_CPUSET)) return true;
   if (!mask) return numa_alloc_ok(C, r, p);
   if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) == KOORDHIP_CPUBIND_NONE) return zone_cpus_ok(C, r, p, z);

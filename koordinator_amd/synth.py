@@ -123,6 +123,7 @@ class NumaSpec:
     policy_frac: float = 0.0           # nodes with a NUMA topology policy (BestEffort / Restricted / SingleNUMANode)
     amp_frac: float = 0.0              # nodes with a CPU amplification ratio (1.25 / 1.5 / 2.0), no topology policy
     zone_used_frac: float = 0.6        # policy nodes: zone usage of non-cpuset pods, U[0, max] of the zone
+    nodes_per_socket: int = 0          # NUMA nodes per socket (4: 2-socket NPS4 hosts, 8 NUMA zones); 0 = NUMA_SHAPES
 
 
 def add_numa(t: NodeTable, spec: NumaSpec, profile: Profile, seed: int = SEED) -> NodeTable:
@@ -134,6 +135,12 @@ def add_numa(t: NodeTable, spec: NumaSpec, profile: Profile, seed: int = SEED) -
     classes = nm.ClassTable()
     cls_of = {}
     for cpu, shape in NUMA_SHAPES.items():
+        if spec.nodes_per_socket:
+            sk, nps0, cpn0, th = shape
+            per_socket = nps0 * cpn0
+            if per_socket % spec.nodes_per_socket:
+                raise ValueError(f"{per_socket} cores per socket do not split into {spec.nodes_per_socket} NUMA nodes")
+            shape = (sk, spec.nodes_per_socket, per_socket // spec.nodes_per_socket, th)
         topo = nm.linux_topology(*shape) if spec.linux_numbering else nm.reference_test_topology(*shape)
         cls_of[cpu] = (classes.add(topo), topo)
     t.numa_classes = classes.records()

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-3 iteration pass: a GPU test selection (TESTS_K, default the parity
+# files), then short bench lines for each workload in WORKLOADS under each
+# environment variant in VARIANTS ("X=1" = none).  Every GPU step has its own
+# time limit; the first crash / abort / timeout stops the script.
+set -u
+mkdir -p gpurun_out
+FILES=${TESTS_FILES:-"tests/test_gpu_parity.py tests/test_gpu_reservation.py tests/test_gpu_numa.py tests/test_fit_kat.py"}
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+  timeout -k 10 900 python -u -m pytest $FILES -m gpu -x -q --timeout 120 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} > gpurun_out/r03_tests.log 2>&1
+  rc=$?; tail -25 gpurun_out/r03_tests.log; [ $rc -eq 0 ] || exit $rc
+fi
+for w in ${WORKLOADS:-config4 config5 config3}; do
+  for v in ${VARIANTS:-X=1}; do
+    env $v timeout -k 10 300 python bench.py --workload $w --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
+      > gpurun_out/r03_${w}_${v}.json 2> gpurun_out/r03_${w}_${v}.err
+    rc=$?
+    python3 - gpurun_out/r03_${w}_${v}.json "$w $v" <<'PY'
+import json, sys
+try:
+    d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+    print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], "scan us", d["eval_roofline"]["avg_launch_us"],
+          "select us", d["select"]["avg_launch_us"], "unsched", d["unschedulable"])
+except Exception as e:
+    print(sys.argv[2], "no result", e)
+PY
+    [ $rc -eq 0 ] || { tail -20 gpurun_out/r03_${w}_${v}.err; exit $rc; }
+  done
+done
+exit 0

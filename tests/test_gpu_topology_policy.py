@@ -181,3 +181,55 @@ def test_gpu_amplified_stream_bit_exact(Engine, scoring):
         assert np.array_equal(st[k], v), k
     for k, v in o.numa_state().items():
         assert np.array_equal(nst[k], v), k
+
+
+# ------------------------------------------- 8 NUMA zones (2-socket NPS4 hosts)
+def _nps4_cluster(n, prof, seed):
+    t = synth.make_cluster(synth.ClusterSpec(n, seed=seed), prof)
+    synth.add_numa(t, synth.NumaSpec(policy_frac=0.8, nodes_per_socket=4), prof, seed=seed)
+    assert (t.numa_classes["num_nodes"] == 8).all()
+    pol = (t["numa_flags"] >> abi.NODE_NUMA_POLICY_SHIFT) & 3
+    assert {1, 2, 3} <= set(pol.tolist())       # best-effort, restricted, single-numa-node all present
+    return t
+
+
+@pytest.mark.parametrize("scoring", ["LeastAllocated", "MostAllocated"])
+def test_gpu_policy_eval_parity_8_zones(Engine, scoring):
+    """Hint generation over 255 zone masks and the policy merges
+    (frameworkext/topologymanager/policy.go:124-169, resource_manager.go:384-428)
+    on 8-zone nodes: status, scores and top-k vs the oracle's literal merge."""
+    rng = np.random.default_rng(41)
+    prof = shipped_profile(numa=True)
+    prof.numa.scoring_type = scoring
+    t = _nps4_cluster(400, prof, seed=13)
+    pods = _mixed_pods(rng, 64, prof)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got = e.eval(pods, k=8)
+    ref = oracle.Oracle(to_c_config(prof), t).eval(pods, k=8)
+    assert np.array_equal(got["status"], ref["status"])
+    assert np.array_equal(got["topk"], ref["topk"])
+    ok = (ref["status"] & abi.ST_NUMA_FAIL) == 0
+    bad = np.argwhere(ok & (got["scores"][:, 2] != ref["scores"][:, 2]))
+    assert len(bad) == 0, bad[:5]
+
+
+@pytest.mark.parametrize("n_nodes,n_pods,cpuset_frac,scoring", [
+    (400, 800, 0.4, "LeastAllocated"), (600, 1000, 0.6, "MostAllocated")])
+def test_gpu_policy_stream_8_zones(Engine, n_nodes, n_pods, cpuset_frac, scoring):
+    prof = shipped_profile(numa=True)
+    prof.numa.scoring_type = scoring
+    table = _nps4_cluster(n_nodes, prof, seed=n_nodes + 1)
+    pods = synth.make_pods(synth.StreamSpec(n_pods, be_frac=0.2, cpuset_frac=cpuset_frac), prof)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(table)
+        got = e.place_stream(pods)
+        cs = e.fetch_cpusets(len(pods))
+        nst = e.read_numa()
+    o = oracle.Oracle(to_c_config(prof), table)
+    ref, rcs = o.place_stream(pods, cpusets=True)
+    assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
+    assert np.array_equal(cs, rcs)
+    for k, v in o.numa_state().items():
+        assert np.array_equal(nst[k], v), k
+    assert o.numa_state()["zone_used"][:, :, 4:].sum() != table["numa_zone_used"][:, :, 4:].sum()  # zones 4-7 used

@@ -110,3 +110,20 @@ def test_reserve_advances_zone_used_and_cpus():
     assert len(got) == 4 and all(topo.details[c].node == 0 for c in got)
     rc, _ = o.commit(pod, 0, sign=-1, cpus=cpus)
     assert rc == abi.E_INVAL
+
+
+def test_oracle_8_zone_streams_self_consistent():
+    """The oracle on 2-socket NPS4 nodes (8 NUMA zones, every policy): a stream's
+    final zone allocations equal the sum of what each pod's Reserve took."""
+    import oracle
+    from koordinator_amd import abi, synth
+    from koordinator_amd.config import shipped_profile, to_c_config
+    prof = shipped_profile(numa=True)
+    t = synth.make_cluster(synth.ClusterSpec(200, seed=17), prof)
+    synth.add_numa(t, synth.NumaSpec(policy_frac=0.9, nodes_per_socket=4), prof, seed=17)
+    pods = synth.make_pods(synth.StreamSpec(300, be_frac=0.2, cpuset_frac=0.5), prof)
+    o = oracle.Oracle(to_c_config(prof), t)
+    out = o.place_stream(pods)
+    assert (out >= 0).sum() > 200
+    zu = o.numa_state()["zone_used"]
+    assert zu[:, :, 4:].sum() > t["numa_zone_used"][:, :, 4:].sum()
