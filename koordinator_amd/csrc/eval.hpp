@@ -22,6 +22,23 @@
 
 namespace kh {
 
+// Write-through (sc1) stores: the row reaches the coherence point without an
+// agent release fence, i.e. without a write-back of the whole XCD L2
+// (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md fence table).
+template <typename T>
+__device__ __forceinline__ void st_wt(T *p, T v) {
+  if constexpr (sizeof(T) == 8) {
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (sizeof(T) == 4) {
+    __hip_atomic_store(reinterpret_cast<uint32_t *>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(reinterpret_cast<uint8_t *>(p), __builtin_bit_cast(uint8_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // device-side node flag bits (flags column, maintained on device)
 enum : uint32_t {
   NF_LA_OK_NONPROD = 1u,  // LoadAware Filter passes for non-prod pods
@@ -622,6 +639,39 @@ __device__ __forceinline__ void store_row(const NV &v, const DevNodes &d, int32_
   d.la_used_prod_cpu[i] = v.la_up_cpu;
   d.la_used_prod_mem[i] = v.la_up_mem;
   d.flags[i] = (uint8_t)v.flags;
+}
+
+// The resolve's write-back of a committed row (the mutable columns), write-through.
+__device__ __forceinline__ void store_row_wt(const NV &v, const DevNodes &d, int32_t i) {
+#pragma unroll
+  for (int r = 0; r < KOORDHIP_NRES; r++) st_wt(&d.requested[r][i], v.r[r]);
+  st_wt(&d.npods[i], v.npods);
+  st_wt(&d.nz_cpu[i], v.nz_cpu);
+  st_wt(&d.nz_mem[i], v.nz_mem);
+  st_wt(&d.la_used_cpu[i], v.la_u_cpu);
+  st_wt(&d.la_used_mem[i], v.la_u_mem);
+  st_wt(&d.la_used_prod_cpu[i], v.la_up_cpu);
+  st_wt(&d.la_used_prod_mem[i], v.la_up_mem);
+  st_wt(&d.flags[i], (uint8_t)v.flags);
+}
+
+template <bool Z = true>
+__device__ __forceinline__ void store_numa_row_wt(const NumaRow &r, const DevNodes &d, int32_t i) {
+  st_wt(&d.nu.cnt[i], r.cnt);
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    st_wt(&d.nu.fr[w][i], r.fr[w]);
+    st_wt(&d.nu.ep[w][i], r.ep[w]);
+    st_wt(&d.nu.en[w][i], r.en[w]);
+  }
+  if (Z && d.nu.za && topo_policy(r.nflags) != 0) {
+    double *zu = d.nu.zu + (size_t)i * 2 * ZMAX;
+#pragma unroll
+    for (int q = 0; q < ZMAX; q++) {
+      st_wt(&zu[q], r.zu[0][q]);
+      st_wt(&zu[ZMAX + q], r.zu[1][q]);
+    }
+  }
 }
 
 // NodeNUMAResource Reserve on a row for a pod with numa_active(): the cpuset

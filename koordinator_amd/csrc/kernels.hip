@@ -1871,6 +1871,11 @@ __device__ __forceinline__ void store_side_row(const side_row_t<NM> &r, const De
   store_numa_row<NM == 2>(r, d, i);
   if constexpr (NM == 3) store_resv(r, d.rv, i);
 }
+template <int NM>
+__device__ __forceinline__ void store_side_row_wt(const side_row_t<NM> &r, const DevNodes &d, int32_t i) {
+  store_numa_row_wt<NM == 2>(r, d, i);
+  if constexpr (NM == 3) store_resv_wt(r, d.rv, i);
+}
 
 template <int NM>
 __device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const side_row_t<NM> &nr,
@@ -2628,10 +2633,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       if (lane < nm) {
         const NV v = slot_row(mrow[lane]);
         mrow[lane] = v;
-        store_row(v, nodes(), my_node);
+        store_row_wt(v, nodes(), my_node);  // write-through: no L2 write-back fence at the publish
         if constexpr (NUMA) {
           const NR nr = mnr[lane];
-          store_side_row<NM>(nr, nodes(), my_node);
+          store_side_row_wt<NM>(nr, nodes(), my_node);
         }
       }
       if (lane == 0) __hip_atomic_store(&sh_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // helpers stop
@@ -2676,7 +2681,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       if (dbg) c_wb += t_rel - t_wb;
       if (lane == 0) {
         sh_mp = nm + ns;
-        store_release(&sy->res_round, r + 1);  // after every lane's stores (one wave: program order)
+        // the rows were stored write-through: drain them, then the relaxed
+        // agent-scope flag (Guideline 16 R1; the evaluation side acquires)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&sy->res_round, r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (dbg) {
         const uint64_t t_end = stamp();

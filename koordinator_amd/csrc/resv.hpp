@@ -60,6 +60,12 @@ __device__ __forceinline__ void store_resv(const NumaRowR &r, const DevResv &d, 
   d.rd[1][i] = r.rd[1];
   d.rn[i] = r.rn;
 }
+__device__ __forceinline__ void store_resv_wt(const NumaRowR &r, const DevResv &d, int32_t i) {  // write-through
+  if (!(r.rf & KOORDHIP_RESV_PRESENT)) return;
+  st_wt(&d.rd[0][i], r.rd[0]);
+  st_wt(&d.rd[1][i], r.rd[1]);
+  st_wt(&d.rn[i], r.rn);
+}
 
 __device__ __forceinline__ bool rkey(uint32_t rf, int k) {
   return (rf & (k == 0 ? KOORDHIP_RESV_KEY_CPU : KOORDHIP_RESV_KEY_MEM)) != 0;

@@ -15,9 +15,14 @@ flush (the only input that changes with time alone).
 
 The node SET is positional on the device: adding or deleting a node needs a
 new snapshot (``flush`` returns ``needs_reload``; ``table()`` builds it).
-NodeNUMAResource columns are not derived from objects here (the host has no
-NodeResourceTopology object model); rows keep the NUMA columns of the table
-they were loaded from, carried over by node name across a reload.
+NodeNUMAResource columns come from NodeResourceTopology events (the NRT
+handler, nodenumaresource/topology_eventhandler.go:62-113: TopologyOptions per
+node) and from the pods' resource-status annotations (the NUMA pod handler,
+pod_eventhandler.go:94-144: NodeAllocation per node, applied in event order --
+an allocation that arrives while its node has no CPU topology is dropped, like
+resourceManager.Update).  A table loaded without NRT objects keeps its NUMA
+columns, carried over by node name across a reload.  Topology classes are
+fixed at load_snapshot: an NRT with a new CPU topology shape needs a reload.
 
 Reservations (the Reservation plugin's reservationCache, reservation/cache.go:
 117-252, fed by the reservation informer) are kept by name; an add / update /
@@ -35,6 +40,7 @@ import numpy as np
 
 from . import k8s
 from .config import Profile
+from . import numa as nm
 from . import reservation as rv
 from .marshal import AssignedPod, ClusterState, build_table, is_node_metric_expired, node_row
 from .snapshot import NodeTable
@@ -105,6 +111,11 @@ class Informer:
         self._table: Optional[NodeTable] = None
         self._now = now
         self.reservations: Dict[str, rv.Reservation] = {}
+        self.nrts: Dict[str, nm.NodeResourceTopology] = {}
+        self._topo: Dict[str, nm.TopologyOptions] = {}      # topologyManager.topologyOptions
+        self._alloc: Dict[str, nm.NodeAllocation] = {}      # resourceManager.nodeAllocations
+        self._pod_alloc_node: Dict[str, str] = {}           # pod UID -> node whose NodeAllocation holds it
+        self._classes: Optional[nm.ClassTable] = None
         self.resv_index = rv.ReservationIndex()
         self._resv_rank: Dict[int, int] = {}
 
@@ -113,7 +124,12 @@ class Informer:
         """A full snapshot of the current state (initial load, or after the node set changed)."""
         self._sync_assigned()
         t = build_table(self.cluster, self.profile, now)
-        if self._table is not None:
+        if self.nrts:
+            self._classes = nm.ClassTable()
+            for i, node in enumerate(self.cluster.nodes):
+                self._numa_row(t, i, node, frozen=False)
+            t.numa_classes = self._classes.records()
+        elif self._table is not None:
             _keep_numa(t, self._table)
         self._resv_rank = rv.order_ranks(rv.available_by_node(self._index, list(self.reservations.values())).values())
         rv.reservation_columns(t, self._index, list(self.reservations.values()), self.resv_index)
@@ -179,6 +195,7 @@ class Informer:
         self._pods_by_uid[pod.uid] = pod
         self.cluster.pods[pod.key] = pod
         self._node_pods_set(pod, True)
+        self._numa_pod(pod, True)
         self.assign_cache.on_add(pod, now)
         if pod.node_name:
             self._dirty.add(pod.node_name)
@@ -192,6 +209,7 @@ class Informer:
         self._pods_by_uid[pod.uid] = pod
         self.cluster.pods[pod.key] = pod
         self._node_pods_set(pod, True)
+        self._numa_pod(pod, True)
         if prev is not None and prev.node_name and prev.node_name != pod.node_name:
             # the assign cache is keyed by the pod's current node (pod_assign_cache.go:91-101)
             self.assign_cache.unassign(prev.node_name, prev)
@@ -205,6 +223,7 @@ class Informer:
         prev = self._pods_by_uid.pop(pod.uid, pod)
         self.cluster.pods.pop(prev.key, None)
         self._node_pods_set(prev, False)
+        self._numa_pod(prev, False)
         self.assign_cache.on_delete(prev)
         if prev.node_name:
             self._dirty.add(prev.node_name)
@@ -228,6 +247,40 @@ class Informer:
             for pm in old.pods_metric:
                 self._metric_refs.get(f"{pm.namespace}/{pm.name}", set()).discard(name)
         self._dirty.add(name)
+
+    # ---- NodeResourceTopology events (topology_eventhandler.go:62-113) ------------------------------
+    def on_nrt(self, nrt: nm.NodeResourceTopology):
+        """Add or update: the node's TopologyOptions are replaced (its NodeAllocation stays)."""
+        self.nrts[nrt.name] = nrt
+        self._topo[nrt.name] = nm.topology_options(nrt)
+        self._dirty.add(nrt.name)
+
+    def on_nrt_delete(self, name: str):
+        self.nrts.pop(name, None)
+        self._topo.pop(name, None)
+        self._dirty.add(name)
+
+    def _numa_pod(self, pod: k8s.Pod, present: bool):
+        """podEventHandler.updatePod / deletePod (pod_eventhandler.go:94-144)."""
+        if not pod.node_name:
+            return
+        if not present or k8s.is_terminated(pod):
+            self._alloc.setdefault(pod.node_name, nm.NodeAllocation()).release(pod.uid)
+            self._dirty.add(pod.node_name)
+            return
+        a = nm.pod_allocation(pod.annotations or {})
+        if a is None:
+            return
+        opts = self._topo.get(pod.node_name)
+        if opts is None or opts.topology is None:     # resourceManager.Update: no valid CPU topology
+            return
+        self._alloc.setdefault(pod.node_name, nm.NodeAllocation()).update(pod.uid, *a)
+        self._dirty.add(pod.node_name)
+
+    def _numa_row(self, table, j: int, node: k8s.Node, frozen: bool):
+        prof = self.profile.resolved()
+        nm.numa_row(table, j, self._topo.get(node.name), self._alloc.get(node.name), self._classes,
+                    node.labels or {}, prof.numa.default_most_allocated, frozen=frozen)
 
     # ---- Reservation events (reservation/cache.go:117-252) ------------------------------------------
     def on_reservation(self, r: rv.Reservation):
@@ -284,6 +337,13 @@ class Informer:
         idx = np.array(sorted(self._index[n] for n in dirty), np.int32)
         rows = self._table.rows(idx)
         placed = rv.available_by_node(self._index, list(self.reservations.values()))
+        if self.nrts or self._classes is not None:
+            try:
+                for j, i in enumerate(idx):
+                    self._numa_row(rows, j, self.cluster.nodes[int(i)], frozen=True)
+            except nm.TopologyError:
+                res.needs_reload = True              # a CPU topology shape the loaded snapshot has no class for
+                return np.zeros(0, np.int32), None, res
         for j, i in enumerate(idx):
             node_row(rows, j, self.cluster.nodes[int(i)], self.cluster, self.profile, now)
             r = placed.get(int(i))

@@ -306,3 +306,228 @@ def cpu_amplification_ratio(annotations: Dict[str, str]) -> float:
     except (ValueError, TypeError, AttributeError) as e:
         raise TopologyError(f"invalid {ANNOTATION_AMPLIFICATION_RATIO}: {e}")
     return v if v > 1.0 else 1.0
+
+
+# --------------------------------------------------------------- NodeResourceTopology objects
+ANNOTATION_CPU_TOPOLOGY = "node.koordinator.sh/cpu-topology"                  # apis/extension/numa_aware.go:40
+ANNOTATION_POD_CPU_ALLOCS = "node.koordinator.sh/pod-cpu-allocs"              # :42
+ANNOTATION_KUBELET_CPU_MANAGER_POLICY = "kubelet.koordinator.sh/cpu-manager-policy"  # :149
+ANNOTATION_NODE_RESERVATION = "node.koordinator.sh/reservation"               # node_reservation.go:28
+ANNOTATION_SYSTEM_QOS_RESOURCE = "node.koordinator.sh/system-qos-resource"     # system_qos.go:24
+ANNOTATION_RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"      # numa_aware.go:34
+
+# nrtv1alpha1.TopologyManagerPolicy values -> convertToNUMATopologyPolicy (topology_options.go:213-225)
+NRT_POLICIES = {"BestEffort": abi.NUMA_TOPO_BEST_EFFORT, "Restricted": abi.NUMA_TOPO_RESTRICTED,
+                "SingleNUMANodePodLevel": abi.NUMA_TOPO_SINGLE_NUMA_NODE}
+
+
+@dataclass
+class Zone:
+    """nrtv1alpha1.Zone: name "node-<id>", type "Node", resources name -> allocatable."""
+    name: str
+    type: str = "Node"
+    resources: Optional[Dict[str, int]] = None      # cpu in milli, memory in bytes
+
+
+@dataclass
+class NodeResourceTopology:
+    """The NRT object koordlet reports (one per node, same name)."""
+    name: str
+    annotations: Optional[Dict[str, str]] = None
+    topology_policies: Optional[List[str]] = None
+    zones: Optional[List[Zone]] = None
+
+
+@dataclass
+class TopologyOptions:
+    """NewTopologyOptions (topology_options.go:90-158) as the engine needs it."""
+    topology: Optional[Topology]
+    reserved: List[int]
+    kubelet_policy: Optional[dict]
+    policy: int
+    zones: List[Tuple[int, Dict[str, int]]]        # (NUMA node id, resources), ascending id
+    amp_cpu: float
+
+
+def _json_or_none(annotations: Dict[str, str], key: str):
+    raw = annotations.get(key)
+    if not raw:
+        return None
+    try:
+        return json.loads(raw)
+    except ValueError:
+        return None                               # the reference logs the error and goes on without it
+
+
+def topology_options(nrt: NodeResourceTopology) -> TopologyOptions:
+    """NewTopologyOptions: CPU topology from the cpu-topology annotation,
+    reserved CPUs = kubelet-managed pod allocs + kubelet reserved + node
+    reservation + exclusive system-QoS CPUs, the NRT's topology policy, the
+    "node-<id>" zones and the amplification ratios."""
+    ann = nrt.annotations or {}
+    topo = None
+    ct = _json_or_none(ann, ANNOTATION_CPU_TOPOLOGY)
+    infos = [CPUInfo(int(d["id"]), int(d.get("core", 0)), int(d.get("node", 0)), int(d.get("socket", 0)))
+             for d in ((ct or {}).get("detail") or [])]
+    if infos:
+        try:
+            topo = Topology(infos, shift_core=True)
+        except TopologyError:
+            topo = None                            # IsValid false / unsupported shape: no topology
+    reserved = set()
+    for a in (_json_or_none(ann, ANNOTATION_POD_CPU_ALLOCS) or []):   # getPodAllocsCPUSet :160-175
+        if a.get("managedByKubelet") and a.get("uid") and a.get("cpuset"):
+            try:
+                reserved.update(parse_cpuset(a["cpuset"]))
+            except ValueError:
+                pass
+    kp = _json_or_none(ann, ANNOTATION_KUBELET_CPU_MANAGER_POLICY)
+    if kp and kp.get("reservedCPUs"):
+        try:
+            reserved.update(parse_cpuset(kp["reservedCPUs"]))
+        except ValueError:
+            pass
+    nr = _json_or_none(ann, ANNOTATION_NODE_RESERVATION)            # GetReservedCPUs
+    if nr and nr.get("reservedCPUs"):
+        try:
+            reserved.update(parse_cpuset(nr["reservedCPUs"]))
+        except ValueError:
+            pass
+    sq = _json_or_none(ann, ANNOTATION_SYSTEM_QOS_RESOURCE)
+    if sq and sq.get("cpusetExclusive", True) and sq.get("cpuset"):
+        try:
+            reserved.update(parse_cpuset(sq["cpuset"]))
+        except ValueError:
+            pass
+    policy = abi.NUMA_TOPO_NONE
+    for p in nrt.topology_policies or []:
+        if p in NRT_POLICIES:
+            policy = NRT_POLICIES[p]
+            break
+    zones = []
+    for z in nrt.zones or []:                                        # extractNUMANodeResources :183-211
+        if z.type != "Node":
+            continue
+        parts = z.name.split("node-")
+        if len(parts) != 2 or not parts[1].isdigit():
+            continue
+        zones.append((int(parts[1]), dict(z.resources or {})))
+    zones.sort(key=lambda x: x[0])
+    return TopologyOptions(topo, sorted(reserved), kp, policy, zones, cpu_amplification_ratio(ann))
+
+
+class NodeAllocation:
+    """NodeAllocation (node_allocation.go:32-177) of one node: pod allocations
+    by UID, per-CPU ref count + exclusive policy, per-NUMA-node allocated
+    resources."""
+
+    def __init__(self):
+        self.pods: Dict[str, Tuple[List[int], str, List[Tuple[int, Dict[str, int]]]]] = {}
+        self.cpus: Dict[int, List] = {}            # cpu -> [refcount, exclusive policy]
+        self.resources: Dict[int, Dict[str, int]] = {}
+
+    def add(self, uid: str, cpus: List[int], excl: str, numa_res: List[Tuple[int, Dict[str, int]]]):
+        if uid in self.pods:                        # addPodAllocation :74-100
+            return
+        self.pods[uid] = (cpus, excl, numa_res)
+        for c in cpus:
+            info = self.cpus.setdefault(c, [0, ""])
+            info[1] = excl
+            info[0] += 1
+        for node, res in numa_res:
+            acc = self.resources.setdefault(node, {})
+            for k, v in res.items():
+                acc[k] = acc.get(k, 0) + v
+
+    def release(self, uid: str):                   # release :102-131
+        req = self.pods.pop(uid, None)
+        if req is None:
+            return
+        cpus, _, numa_res = req
+        for c in cpus:
+            info = self.cpus.get(c)
+            if info is None:
+                continue
+            info[0] -= 1
+            if info[0] == 0:
+                del self.cpus[c]
+        for node, res in numa_res:
+            acc = self.resources.get(node)
+            if acc is not None:
+                for k, v in res.items():              # SubtractWithNonNegativeResult
+                    acc[k] = max(0, acc.get(k, 0) - v)
+
+    def update(self, uid: str, cpus: List[int], excl: str, numa_res):
+        self.release(uid)
+        self.add(uid, cpus, excl, numa_res)
+
+
+def pod_allocation(annotations: Dict[str, str]):
+    """podEventHandler.updatePod's parse (pod_eventhandler.go:94-131): (cpus,
+    exclusive policy, NUMA node resources), or None when the pod holds
+    neither a cpuset nor NUMA node resources (or an annotation is malformed)."""
+    try:
+        st = json.loads(annotations[ANNOTATION_RESOURCE_STATUS]) if annotations.get(ANNOTATION_RESOURCE_STATUS) else {}
+        sp = json.loads(annotations[ANNOTATION_RESOURCE_SPEC]) if annotations.get(ANNOTATION_RESOURCE_SPEC) else {}
+        cpus = parse_cpuset(st.get("cpuset", "") or "")
+    except (ValueError, TypeError):
+        return None
+    nres = []
+    for x in st.get("numaNodeResources") or []:
+        res = {}
+        for k, v in (x.get("resources") or {}).items():
+            res[k] = int(v)
+        nres.append((int(x.get("node", 0)), res))
+    if not nres and not cpus:
+        return None
+    return cpus, sp.get("preferredCPUExclusivePolicy", "") or "", nres
+
+
+def numa_row(table, i: int, opts: Optional[TopologyOptions], alloc: Optional[NodeAllocation], classes: ClassTable,
+             labels: Dict[str, str], default_most_allocated: bool, frozen: bool = False):
+    """Row i of the NodeNUMAResource columns from the node's TopologyOptions and
+    NodeAllocation.  frozen: the class table is fixed (a row update); a
+    topology it does not hold raises TopologyError (the caller reloads)."""
+    for w in range(abi.NUMA_WORDS):
+        table[f"numa_free{w}"][i] = 0
+        table[f"numa_excl_pcpu{w}"][i] = 0
+        table[f"numa_excl_numa{w}"][i] = 0
+    table["numa_alloc_cnt"][i] = 0
+    table["numa_zone_alloc"][i] = 0
+    table["numa_zone_used"][i] = 0
+    table["numa_amp_cpu"][i] = 1.0
+    topo = opts.topology if opts is not None else None
+    if topo is None:
+        table["numa_class"][i] = -1
+        table["numa_flags"][i] = node_numa_flags(labels, None, default_most_allocated) & ~(3 << abi.NODE_NUMA_POLICY_SHIFT)
+        return
+    if frozen and topo.key not in classes._index:
+        raise TopologyError("a topology class the loaded snapshot does not hold (reload)")
+    table["numa_class"][i] = classes.add(topo)
+    cpus = (alloc.cpus if alloc is not None else {})
+    allocated = [c for c in cpus if c in topo.pos_of]
+    free = [c for c in topo.cpu_of if c not in cpus and c not in set(opts.reserved)]   # getAvailableCPUs, maxRefCount 1
+    fm = topo.mask(free)
+    pm = topo.mask([c for c in allocated if cpus[c][1] == "PCPULevel"])
+    nm = topo.mask([c for c in allocated if cpus[c][1] == "NUMANodeLevel"])
+    for w in range(abi.NUMA_WORDS):
+        table[f"numa_free{w}"][i] = fm[w]
+        table[f"numa_excl_pcpu{w}"][i] = pm[w]
+        table[f"numa_excl_numa{w}"][i] = nm[w]
+    table["numa_alloc_cnt"][i] = len(cpus)
+    flags = node_numa_flags(labels, opts.kubelet_policy, default_most_allocated) & ~(3 << abi.NODE_NUMA_POLICY_SHIFT)
+    pol = numa_topology_policy(labels) or opts.policy                       # getNUMATopologyPolicy: the label wins
+    flags |= pol << abi.NODE_NUMA_POLICY_SHIFT
+    table["numa_flags"][i] = flags
+    if opts.zones and pol:  # zone rows are read only on topology-policy nodes
+        node_rank = {n: r for r, n in enumerate(sorted({topo.details[c].node for c in topo.cpu_of}))}
+        for nid, res in opts.zones:
+            r = node_rank.get(nid)
+            if r is None:
+                continue
+            table["numa_zone_alloc"][i, 0, r] = res.get("cpu", 0)
+            table["numa_zone_alloc"][i, 1, r] = res.get("memory", 0)
+            used = (alloc.resources.get(nid, {}) if alloc is not None else {})
+            table["numa_zone_used"][i, 0, r] = used.get("cpu", 0)
+            table["numa_zone_used"][i, 1, r] = used.get("memory", 0)
+    table["numa_amp_cpu"][i] = opts.amp_cpu

@@ -307,3 +307,161 @@ def test_reload_keeps_reservations_and_numa_by_name():
     assert t2.cols["resv_flags"][1] & 1 and t2.cols["resv_alloc0"][1] == 2000
     assert t2.cols["resv_flags"][0] == 0 and t2.cols["resv_flags"][2] == 0
     assert t2.cols["numa_class"][1] == 7
+
+
+# ------------------------------------------------ NodeResourceTopology + NUMA pod events
+def _nrt(rng, name, sockets=2, nps=1, cores=8, policy=None):
+    import json as _j
+    from koordinator_amd import numa as nm
+    topo = nm.linux_topology(sockets, nps, cores, 2)
+    detail = [{"id": c, "core": topo.details[c].core & 0xFFFF, "socket": topo.details[c].socket,
+               "node": topo.details[c].node} for c in topo.cpu_of]
+    ann = {nm.ANNOTATION_CPU_TOPOLOGY: _j.dumps({"detail": detail})}
+    if rng.random() < 0.5:
+        ann[nm.ANNOTATION_KUBELET_CPU_MANAGER_POLICY] = _j.dumps({"policy": "static", "reservedCPUs": "0-1"})
+    nn = sockets * nps
+    zones = [nm.Zone(f"node-{k}", resources={"cpu": cores * 2 * 1000, "memory": 16 * GI}) for k in range(nn)]
+    return nm.NodeResourceTopology(name=name, annotations=ann, zones=zones,
+                                   topology_policies=[policy] if policy else ["None"])
+
+
+def _numa_pod(rng, i, node, topo_cpus):
+    import json as _j
+    from koordinator_amd import numa as nm
+    k = int(rng.integers(1, 5)) * 2
+    start = int(rng.integers(0, max(1, len(topo_cpus) - k)))
+    cpus = topo_cpus[start:start + k]
+    status = {"cpuset": nm.format_cpuset(cpus),
+              "numaNodeResources": [{"node": int(rng.integers(0, 2)), "resources": {"cpu": k * 1000, "memory": GI}}]}
+    spec = {"preferredCPUBindPolicy": "FullPCPUs",
+            "preferredCPUExclusivePolicy": str(rng.choice(["", "PCPULevel", "NUMANodeLevel"]))}
+    return k8s.Pod(namespace="ns", name=f"np{i}", uid=f"nu{i}", node_name=node, priority=9500,
+                   annotations={nm.ANNOTATION_RESOURCE_STATUS: _j.dumps(status), nm.ANNOTATION_RESOURCE_SPEC: _j.dumps(spec)},
+                   containers=[k8s.Container(requests={k8s.CPU: k8s.Q(k), k8s.MEMORY: k8s.Q(GI)})])
+
+
+NUMA_COLS = ([f"numa_free{w}" for w in range(4)] + [f"numa_excl_pcpu{w}" for w in range(4)]
+             + [f"numa_excl_numa{w}" for w in range(4)] + ["numa_alloc_cnt", "numa_class", "numa_flags",
+                                                         "numa_zone_alloc", "numa_zone_used", "numa_amp_cpu"])
+
+
+@pytest.mark.parametrize("seed", [6, 7, 8])
+def test_numa_events_rows_equal_rebuild(seed):
+    """NRT add / update / delete and NUMA pod bind / finish / delete events
+    (topology_eventhandler.go:62-113, pod_eventhandler.go:94-144): after every
+    flush the device-row image equals a from-scratch table() of the same state."""
+    from koordinator_amd import numa as nm
+    rng = np.random.default_rng(seed)
+    prof = shipped_profile(numa=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110)},
+                      labels={nm.LABEL_NUMA_TOPOLOGY_POLICY: "BestEffort"} if i % 5 == 0 else {})
+             for i in range(10)]
+    inf = Informer(prof, nodes, NOW)
+    shapes = [(2, 1, 8), (2, 2, 4)]
+    for i, n in enumerate(nodes[:8]):
+        inf.on_nrt(_nrt(rng, n.name, *shapes[i % 2], policy=["Restricted", None][i % 2]))
+    eng = _TableEngine(inf.table(NOW))
+    live, nxt = {}, 0
+    cpus_of = {n: list(range(32)) for n in (x.name for x in nodes)}
+    for step in range(40):
+        op = rng.random()
+        if op < 0.45:
+            n = nodes[int(rng.integers(0, len(nodes)))].name
+            p = _numa_pod(rng, nxt, n, cpus_of[n])
+            nxt += 1
+            live[p.uid] = p
+            inf.on_pod_add(p, NOW)
+        elif op < 0.6 and live:
+            p = copy.deepcopy(live[list(live)[int(rng.integers(0, len(live)))]])
+            p.phase = "Succeeded"
+            live.pop(p.uid)
+            inf.on_pod_update(None, p, NOW)
+        elif op < 0.75 and live:
+            inf.on_pod_delete(live.pop(list(live)[int(rng.integers(0, len(live)))]))
+        elif op < 0.9:
+            i = int(rng.integers(0, len(nodes)))
+            inf.on_nrt(_nrt(rng, nodes[i].name, *shapes[int(rng.integers(0, 2))],
+                            policy=[None, "BestEffort", "SingleNUMANodePodLevel"][int(rng.integers(0, 3))]))
+        else:
+            inf.on_nrt_delete(nodes[int(rng.integers(0, len(nodes)))].name)
+        res = inf.flush(eng, NOW)
+        if res.needs_reload:
+            eng = _TableEngine(inf.table(NOW))
+        classes = inf._classes
+        want = inf.table(NOW)
+        # the rebuild may number classes differently: compare the class records
+        for c in NUMA_COLS:
+            if c == "numa_class":
+                a, b = eng.table.cols[c], want.cols[c]
+                assert np.array_equal(a < 0, b < 0), step
+                ra = [classes.records()[x].tobytes() for x in a[a >= 0]]
+                rb = [want.numa_classes[x].tobytes() for x in b[b >= 0]]
+                assert ra == rb, step
+            else:
+                assert np.array_equal(eng.table.cols[c], want.cols[c]), (step, c)
+        eng = _TableEngine(want)
+        inf.attach(want, NOW)
+    assert inf._alloc and any(a.cpus for a in inf._alloc.values())
+
+
+def test_numa_pod_before_its_nrt_is_dropped():
+    """resourceManager.Update (resource_manager.go:328-339) ignores an allocation
+    while the node has no CPU topology: the event order matters."""
+    from koordinator_amd import numa as nm
+    rng = np.random.default_rng(1)
+    prof = shipped_profile(numa=True)
+    nodes = [k8s.Node(name="n0", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110)})]
+    inf = Informer(prof, nodes, NOW)
+    inf.on_pod_add(_numa_pod(rng, 0, "n0", list(range(32))), NOW)
+    inf.on_nrt(_nrt(rng, "n0"))
+    t = inf.table(NOW)
+    assert t["numa_class"][0] == 0 and t["numa_alloc_cnt"][0] == 0
+    inf.on_pod_add(_numa_pod(rng, 1, "n0", list(range(32))), NOW)
+    assert inf.table(NOW)["numa_alloc_cnt"][0] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_numa_events_then_stream():
+    """§8(f)#2: a burst of NRT and NUMA pod events pushed through
+    koordhip_update_nodes, then a greedy stream with cpuset pods: placements,
+    cpusets and the NUMA state equal the oracle's on a fresh snapshot."""
+    import torch  # noqa: F401
+    import oracle
+    from koordinator_amd import numa as nm, synth
+    from koordinator_amd.config import to_c_config
+    from koordinator_amd.engine import PlacementEngine
+    rng = np.random.default_rng(12)
+    prof = shipped_profile(numa=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110)})
+             for i in range(120)]
+    inf = Informer(prof, nodes, NOW)
+    for i, n in enumerate(nodes):
+        if i % 10:
+            inf.on_nrt(_nrt(rng, n.name, *[(2, 1, 8), (2, 2, 4)][i % 2], policy=[None, "BestEffort", "Restricted"][i % 3]))
+    for j in range(150):
+        n = nodes[int(rng.integers(0, len(nodes)))].name
+        inf.on_pod_add(_numa_pod(rng, j, n, list(range(32))), NOW)
+    stream = synth.make_pods(synth.StreamSpec(300, be_frac=0.2, cpuset_frac=0.5), prof)
+    with PlacementEngine(prof, device=0) as e:
+        e.load_snapshot(inf.table(NOW))
+        for j in range(150, 230):                  # the burst: new NUMA pods, finished pods, NRT updates
+            n = nodes[int(rng.integers(0, len(nodes)))].name
+            inf.on_pod_add(_numa_pod(rng, j, n, list(range(32))), NOW)
+        for j in range(0, 150, 4):
+            p = copy.deepcopy(inf._pods_by_uid[f"nu{j}"])
+            p.phase = "Succeeded"
+            inf.on_pod_update(None, p, NOW)
+        for i in range(1, 120, 7):
+            inf.on_nrt(_nrt(rng, nodes[i].name, *[(2, 1, 8), (2, 2, 4)][i % 2], policy="SingleNUMANodePodLevel"))
+        res = inf.flush(e, NOW)
+        assert res.rows > 0 and not res.needs_reload
+        got = e.place_stream(stream)
+        cs = e.fetch_cpusets(len(stream))
+        nst = e.read_numa()
+    fresh = inf.table(NOW)
+    o = oracle.Oracle(to_c_config(prof), fresh)
+    ref, rcs = o.place_stream(stream, cpusets=True)
+    assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
+    assert np.array_equal(cs, rcs)
+    for k, v in o.numa_state().items():
+        assert np.array_equal(nst[k], v), k
