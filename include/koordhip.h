@@ -88,6 +88,8 @@ extern "C" {
 #define KOORDHIP_POD_NUMA_ERROR 128u  /* NUMA: PreFilter error (non-integral cpuset request, plugin.go:242-245) */
 #define KOORDHIP_POD_KEY_CPU 256u     /* "cpu" key present in PodRequestsAndLimits (Reservation nominate / score / Restricted) */
 #define KOORDHIP_POD_KEY_MEM 512u     /* "memory" key present */
+#define KOORDHIP_POD_RESV_AFFINITY 1024u /* a required reservation affinity (util/reservation/reservation.go:444-487): a node
+                                            without a matched reservation fails the Reservation Filter (plugin.go:378-381) */
 
 /* koordhip_node_soa.resv_flags: the node's Available reservation (at most one
  * per node: with several, the reference's order among them is Go map

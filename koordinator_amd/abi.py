@@ -26,6 +26,7 @@ LA_PROD_MODE, LA_HAS_PODS_METRIC, LA_AGGREGATED = 16, 32, 64
 POD_PROD, POD_DAEMONSET, POD_HAS_REQ, POD_REQ_BCPU, POD_REQ_BMEM = 1, 2, 4, 8, 16
 POD_CPUSET, POD_NUMA_SKIP, POD_NUMA_ERROR = 32, 64, 128
 POD_KEY_CPU, POD_KEY_MEM = 256, 512
+POD_RESV_AFFINITY = 1024
 
 RESV_PRESENT, RESV_ALLOCATE_ONCE, RESV_UNSCHEDULABLE, RESV_ORDERED = 1, 2, 4, 8
 RESV_KEY_CPU, RESV_KEY_MEM = 16, 32

@@ -477,7 +477,9 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
 
 // Total weighted score, or -1 when any enabled Filter fails.
 __device__ __forceinline__ int32_t eval_total(const DevPod &p, const NV &v, const DevCfg &c) {
-  bool ok = true;
+  // the Reservation Filter without reservation columns (NM != 3 builds): a pod
+  // with a required reservation affinity has no matched reservation anywhere
+  bool ok = !((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !c.resv && (p.flags & KOORDHIP_POD_RESV_AFFINITY));
   if (c.filt & KOORDHIP_PLUGIN_FIT) ok &= fit_filter(p, v);
   if (c.filt & KOORDHIP_PLUGIN_LOADAWARE) ok &= la_filter(p, v);
   int32_t t = 0;
@@ -515,7 +517,9 @@ __device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v,
   const int cls = resv_class(r, p);
   resv_restore(w, r, cls);
   int32_t t = eval_total_numa<false>(p, w, r, classes, c);
-  if (t < 0 || cls != 1) return t;
+  if (t < 0) return t;
+  if (cls != 1)  // a required reservation affinity needs a matched reservation on the node (plugin.go:378-381)
+    return ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && (p.flags & KOORDHIP_POD_RESV_AFFINITY)) ? -1 : t;
   if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !resv_filter(p, w, r)) return -1;
   if (c.score & KOORDHIP_PLUGIN_RESERVATION) {
     if (r.rf & KOORDHIP_RESV_ORDERED) return 101 * c.resv_b1 + (KOORDHIP_RESV_MAX_ORDERS - 1 - r.rk);

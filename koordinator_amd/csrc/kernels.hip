@@ -181,7 +181,9 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
     if ((c.filt & KOORDHIP_PLUGIN_NUMA) &&
         (!numa_filter<true>(pod, nr, d.nu.cls) || (c.amp && !amp_filter_ok(pod, v, nr))))
       b |= KOORDHIP_ST_NUMA_FAIL;
-    if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && rcls == 1 && !resv_filter(pod, v, nr)) b |= KOORDHIP_ST_RESV_FAIL;
+    if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) &&
+        (rcls == 1 ? !resv_filter(pod, v, nr) : (pod.flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
+      b |= KOORDHIP_ST_RESV_FAIL;
     status[(size_t)p * d.n + i] = b;
   }
   if (scores) {

@@ -14,10 +14,12 @@ Restated from the reference:
   * reserve pod non-zero request: calculateResource, reservation/transformer.go:302-333
 
 The device evaluates owner matching as bit tests: every distinct owner spec
-of the snapshot's reservations is an owner group g (<= 64), a reservation
-carries its group, a pod carries the bit mask of the groups it matches.
-Pods with a reservation affinity (reservation.go:449-487) and reserve pods
-are not streamed by this engine (MarshalError).
+(x the results of the registered reservation affinities) of the snapshot's
+reservations is a group g (<= 64), a reservation carries its group, a pod
+carries the bit mask of the groups it matches and KOORDHIP_POD_RESV_AFFINITY
+when it has a required reservation affinity (reservation.go:444-487: no
+matched reservation on a node -> UnschedulableAndUnresolvable, plugin.go:
+378-381).  Reserve pods are not streamed by this engine (MarshalError).
 """
 from __future__ import annotations
 
@@ -159,6 +161,113 @@ def match_owners(pod: k8s.Pod, owners: Sequence[ReservationOwner]) -> bool:
 
 
 @dataclass
+class NodeSelectorRequirement:
+    key: str
+    operator: str                 # In, NotIn, Exists, DoesNotExist, Gt, Lt
+    values: List[str] = field(default_factory=list)
+
+
+@dataclass
+class NodeSelectorTerm:
+    match_expressions: List[NodeSelectorRequirement] = field(default_factory=list)
+    match_fields: List[NodeSelectorRequirement] = field(default_factory=list)
+
+
+def _req_matches(r: NodeSelectorRequirement, labels: Dict[str, str]) -> bool:
+    """(upstream) component-helpers nodeaffinity / labels.Requirement.Matches."""
+    has = r.key in labels
+    if r.operator == "In":
+        return has and labels[r.key] in r.values
+    if r.operator == "NotIn":
+        return not has or labels[r.key] not in r.values
+    if r.operator == "Exists":
+        return has
+    if r.operator == "DoesNotExist":
+        return not has
+    if r.operator in ("Gt", "Lt"):
+        if not has:
+            return False
+        try:
+            a, b = int(labels[r.key]), int(r.values[0])
+        except (ValueError, IndexError):
+            return False
+        return a > b if r.operator == "Gt" else a < b
+    return False
+
+
+@dataclass
+class ReservationAffinity:
+    """apis/extension ReservationAffinity as GetRequiredReservationAffinity reads it
+    (pkg/util/reservation/reservation.go:444-487): a label set the reservation
+    must carry and node-selector terms over a fake node whose labels are the
+    node's overlaid with the reservation's and whose name is the reservation's
+    (reservation/transformer.go:335-359)."""
+    selector: Dict[str, str] = field(default_factory=dict)
+    terms: Optional[List[NodeSelectorTerm]] = None
+
+    def key(self) -> str:
+        return json.dumps([sorted(self.selector.items()),
+                           None if self.terms is None else
+                           [[[(r.key, r.operator, sorted(r.values)) for r in t.match_expressions],
+                             [(r.key, r.operator, sorted(r.values)) for r in t.match_fields]] for t in self.terms]])
+
+    def matches(self, node_labels: Dict[str, str], resv: "Reservation") -> bool:
+        labels = dict(node_labels or {})
+        labels.update(resv.labels or {})
+        for k, v in self.selector.items():
+            if labels.get(k) != v:
+                return False
+        if self.terms is None:
+            return True
+        for t in self.terms:                          # NodeSelector: terms ORed, a term's parts ANDed
+            if not t.match_expressions and not t.match_fields:
+                continue
+            ok = all(_req_matches(r, labels) for r in t.match_expressions)
+            ok = ok and all(_req_matches(r, {"metadata.name": resv.name}) for r in t.match_fields)
+            if ok:
+                return True
+        return False
+
+
+_NODE_SELECTOR_OPS = {"In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt"}
+
+
+def parse_reservation_affinity(annotations: Dict[str, str]) -> Optional[ReservationAffinity]:
+    """GetRequiredReservationAffinity: None without a selector or required terms;
+    ReservationError on a malformed annotation / selector (the reference's
+    BeforePreFilter error)."""
+    raw = (annotations or {}).get(ANNOTATION_RESERVATION_AFFINITY, "")
+    if not raw:
+        return None
+    try:
+        a = json.loads(raw)
+    except ValueError as e:
+        raise ReservationError(f"reservation affinity: {e}") from e
+    sel = a.get("reservationSelector") or {}
+    req = a.get("requiredDuringSchedulingIgnoredDuringExecution")
+    if not sel and req is None:
+        return None
+    terms = None
+    if req is not None:
+        terms = []
+        for t in req.get("reservationSelectorTerms") or []:
+            def reqs(xs, fields=False):
+                out = []
+                for x in xs or []:
+                    op = x.get("operator", "")
+                    vals = list(x.get("values") or [])
+                    if op not in _NODE_SELECTOR_OPS or (fields and (x.get("key") != "metadata.name" or op not in ("In", "NotIn"))):
+                        raise ReservationError(f"reservation affinity: unsupported requirement {x}")
+                    if op in ("In", "NotIn") and not vals or op in ("Exists", "DoesNotExist") and vals \
+                            or op in ("Gt", "Lt") and len(vals) != 1:
+                        raise ReservationError(f"reservation affinity: invalid requirement {x}")
+                    out.append(NodeSelectorRequirement(x.get("key", ""), op, vals))
+                return out
+            terms.append(NodeSelectorTerm(reqs(t.get("matchExpressions")), reqs(t.get("matchFields"), True)))
+    return ReservationAffinity(dict(sel), terms)
+
+
+@dataclass
 class Reservation:
     """A scheduling.koordinator.sh/v1alpha1 Reservation as the scheduler cache holds it."""
     name: str
@@ -197,36 +306,63 @@ def parse_order(labels: Dict[str, str]) -> int:
 
 @dataclass
 class ReservationIndex:
-    """Owner groups of a snapshot's reservations (pods are matched against them)."""
+    """Owner groups of a snapshot's reservations (pods are matched against them).
+
+    A group is a distinct (owner spec, results of the registered reservation
+    affinities on the reservation) pair: a pod's bit g is MatchReservationOwners
+    against the group's owners AND, for a pod with a required reservation
+    affinity, that affinity's result on the group's reservations
+    (matchReservation, reservation/transformer.go:335-359).  Affinities must be
+    registered before the columns are built (register_affinities); a new one
+    regroups every reservation (the columns and earlier pod masks are stale)."""
     groups: List[List[ReservationOwner]] = field(default_factory=list)
     group_of: Dict[str, int] = field(default_factory=dict)
+    affinities: List[ReservationAffinity] = field(default_factory=list)
+    group_aff: List[Tuple[bool, ...]] = field(default_factory=list)
 
-    def group(self, owners: List[ReservationOwner]) -> int:
-        key = json.dumps([o.key() for o in owners])
+    def register_affinities(self, pods) -> bool:
+        """Register the required reservation affinities of `pods`; True when any
+        was new (then rebuild the reservation columns and the pod masks)."""
+        known = {a.key() for a in self.affinities}
+        new = False
+        for p in pods:
+            a = parse_reservation_affinity(p.annotations or {})
+            if a is not None and a.key() not in known:
+                self.affinities.append(a)
+                known.add(a.key())
+                new = True
+        if new:
+            self.groups, self.group_of, self.group_aff = [], {}, []
+        return new
+
+    def group(self, owners: List[ReservationOwner], node_labels: Optional[Dict[str, str]] = None,
+              resv: Optional["Reservation"] = None) -> int:
+        res = tuple(a.matches(node_labels or {}, resv) if resv is not None else False for a in self.affinities)
+        key = json.dumps([[o.key() for o in owners], res])
         g = self.group_of.get(key)
         if g is None:
             if len(self.groups) >= abi.RESV_MAX_GROUPS:
-                raise ReservationError(f"more than {abi.RESV_MAX_GROUPS} distinct reservation owner specs")
+                raise ReservationError(f"more than {abi.RESV_MAX_GROUPS} distinct reservation owner / affinity groups")
             g = len(self.groups)
             self.groups.append(list(owners))
+            self.group_aff.append(res)
             self.group_of[key] = g
         return g
 
     def pod_mask(self, pod: k8s.Pod) -> int:
-        """koordhip_pod.resv_match: bit g set iff the pod matches owner group g."""
+        """koordhip_pod.resv_match: bit g set iff the pod matches group g."""
         if (pod.annotations or {}).get(ANNOTATION_RESERVE_POD) == "true":
             raise ReservationError("reserve pods are not scheduled by this engine")
-        aff = (pod.annotations or {}).get(ANNOTATION_RESERVATION_AFFINITY, "")
-        if aff:
-            try:
-                a = json.loads(aff)
-            except ValueError as e:
-                raise ReservationError(f"reservation affinity: {e}") from e
-            if a.get("reservationSelector") or a.get("requiredDuringSchedulingIgnoredDuringExecution"):
-                raise ReservationError("pods with a reservation affinity are not supported by this engine")
+        aff = parse_reservation_affinity(pod.annotations or {})
+        ai = None
+        if aff is not None:
+            keys = [a.key() for a in self.affinities]
+            if aff.key() not in keys:
+                raise ReservationError("a reservation affinity not registered with this snapshot's index")
+            ai = keys.index(aff.key())
         m = 0
         for g, owners in enumerate(self.groups):
-            if match_owners(pod, owners):
+            if match_owners(pod, owners) and (ai is None or self.group_aff[g][ai]):
                 m |= 1 << g
         return m
 
@@ -265,8 +401,10 @@ def clear_reservation_row(table: NodeTable, i):
         table[c][i] = 0
 
 
-def reservation_row(table: NodeTable, i: int, r: Reservation, index: "ReservationIndex", rank: Dict[int, int]):
-    """Row i of the resv_* columns for node i's Available reservation r."""
+def reservation_row(table: NodeTable, i: int, r: Reservation, index: "ReservationIndex", rank: Dict[int, int],
+                    node_labels: Optional[Dict[str, str]] = None):
+    """Row i of the resv_* columns for node i's Available reservation r
+    (node_labels: what reservation affinities see of the node)."""
     from .marshal import nonzero_request, fit_request
 
     clear_reservation_row(table, i)
@@ -305,7 +443,7 @@ def reservation_row(table: NodeTable, i: int, r: Reservation, index: "Reservatio
     if r.allocate_policy not in _POLICY_CODE:
         raise ReservationError(f"reservation {r.name}: unknown allocate policy {r.allocate_policy!r}")
     f |= _POLICY_CODE[r.allocate_policy] << abi.RESV_POLICY_SHIFT
-    f |= index.group(r.owners) << abi.RESV_GROUP_SHIFT
+    f |= index.group(r.owners, node_labels, r) << abi.RESV_GROUP_SHIFT
     table["resv_flags"][i] = f
     table["resv_alloc0"][i] = _q2(r.allocatable, k8s.CPU)
     table["resv_alloc1"][i] = _q2(r.allocatable, k8s.MEMORY)
@@ -319,19 +457,25 @@ def reservation_row(table: NodeTable, i: int, r: Reservation, index: "Reservatio
 
 
 def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservations: Sequence[Reservation],
-                        index: Optional[ReservationIndex] = None) -> ReservationIndex:
+                        index: Optional[ReservationIndex] = None,
+                        node_labels: Optional[Dict[str, Dict[str, str]]] = None) -> ReservationIndex:
     """Fill the resv_* columns of `table` (the reservation cache's view,
-    cache.go:236-252) and return the owner groups for the pod masks."""
+    cache.go:236-252) and return the owner groups for the pod masks
+    (node_labels: node name -> labels, for reservation affinities)."""
     index = index or ReservationIndex()
     clear_reservation_row(table, slice(None))
     placed = available_by_node(node_index, reservations)
     rank = order_ranks(placed.values())
     for i, r in placed.items():
-        reservation_row(table, i, r, index, rank)
+        reservation_row(table, i, r, index, rank, (node_labels or {}).get(r.node_name))
     return index
 
 
 def pod_keys(pod: k8s.Pod) -> int:
-    """KOORDHIP_POD_KEY_* bits: the cpu / memory keys of PodRequestsAndLimits."""
+    """KOORDHIP_POD_KEY_* bits: the cpu / memory keys of PodRequestsAndLimits,
+    and KOORDHIP_POD_RESV_AFFINITY for a required reservation affinity."""
     reqs, _ = k8s.pod_requests_and_limits(pod)
-    return (abi.POD_KEY_CPU if k8s.CPU in reqs else 0) | (abi.POD_KEY_MEM if k8s.MEMORY in reqs else 0)
+    f = (abi.POD_KEY_CPU if k8s.CPU in reqs else 0) | (abi.POD_KEY_MEM if k8s.MEMORY in reqs else 0)
+    if parse_reservation_affinity(pod.annotations or {}) is not None:
+        f |= abi.POD_RESV_AFFINITY
+    return f

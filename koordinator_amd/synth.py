@@ -290,6 +290,7 @@ class StreamSpec:
     cpuset_frac: float = 0.0   # share of LS pods that are LSR/LSE cpuset pods (NodeNUMAResource)
     resv_match_frac: float = 0.0  # pods matching one reservation owner group (Reservation)
     resv_groups: int = 8
+    resv_affinity_frac: float = 0.0  # pods with a required reservation affinity (match: a subset of their group)
 
 
 LS_CPU = [250, 500, 1000, 2000, 4000]
@@ -343,6 +344,15 @@ def make_pods(spec: StreamSpec, profile: Profile) -> np.ndarray:
         m = uniform(s, n, 50) < spec.resv_match_frac
         g = (splitmix64(s, n, 51) % np.uint64(max(1, spec.resv_groups))).astype(np.uint64)
         pods["resv_match"] = np.where(m, np.uint64(1) << g, np.uint64(0))
+        if spec.resv_affinity_frac > 0:
+            # a required reservation affinity: KOORDHIP_POD_RESV_AFFINITY, and a
+            # second owner group standing for "the group's reservations whose
+            # labels the affinity selects" (or none: unschedulable everywhere)
+            a = uniform(s, n, 52) < spec.resv_affinity_frac
+            g2 = (splitmix64(s, n, 53) % np.uint64(max(1, spec.resv_groups))).astype(np.uint64)
+            keep = uniform(s, n, 54) < 0.8
+            pods["flags"] |= np.where(a, abi.POD_RESV_AFFINITY, 0).astype(pods["flags"].dtype)
+            pods["resv_match"] = np.where(a, np.where(keep, np.uint64(1) << g2, np.uint64(0)), pods["resv_match"])
     return pods
 
 

@@ -250,7 +250,8 @@ static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const k
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) return 0;
-  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && st->soa->resv_flags && !orc_resv_filter(st, pod, i))
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) &&
+      (st->soa->resv_flags ? !orc_resv_filter(st, pod, i) : (pod->flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
     return 0;
   return 1;
 }
@@ -292,7 +293,8 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !fit_ok) b |= KOORDHIP_ST_FIT_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !la_ok) b |= KOORDHIP_ST_LA_FAIL;
         if (!numa_ok) b |= KOORDHIP_ST_NUMA_FAIL;
-        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && st->soa->resv_flags && !orc_resv_filter(st, pod, i))
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) &&
+      (st->soa->resv_flags ? !orc_resv_filter(st, pod, i) : (pod->flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
           b |= KOORDHIP_ST_RESV_FAIL;
         status[(size_t)p * n + i] = b;
       }

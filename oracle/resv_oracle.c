@@ -106,7 +106,7 @@ int orc_resv_filter(const orc_state *st, const koordhip_pod *pod, int32_t i) {
   const koordhip_node_soa *s = st->soa;
   int matched, unmatched;
   orc_resv_classify(st, pod, i, &matched, &unmatched);
-  if (!matched) return 1; /* :378-392 (no reservation affinity, nothing preemptible) */
+  if (!matched) return (pod->flags & KOORDHIP_POD_RESV_AFFINITY) ? 0 : 1; /* :378-392 (hasAffinity; nothing preemptible) */
   const uint32_t rf = s->resv_flags[i];
   const uint32_t policy = KOORDHIP_RESV_POLICY(rf);
   if (policy == 0) return 1; /* Default: insufficient only with preemptible resources (:405-412) */

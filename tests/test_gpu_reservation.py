@@ -161,3 +161,33 @@ def test_gpu_resv_sharded_group(Engine, world):
     for r in range(world):
         assert np.array_equal(outs[r], ref), (r, int(np.flatnonzero(outs[r] != ref)[0]))
         assert np.array_equal(resv[r]["allocated"], o.resv_state()["allocated"])
+
+
+@pytest.mark.parametrize("numa,evalpath", [(False, "fused"), (True, "fused"), (False, "split")])
+def test_gpu_resv_affinity_stream(Engine, numa, evalpath, monkeypatch):
+    """Pods with a required reservation affinity (KOORDHIP_POD_RESV_AFFINITY):
+    feasible only on nodes where a reservation matched them
+    (reservation/plugin.go:378-381), through both evaluation paths; status,
+    top-k and the placement stream vs the oracle."""
+    monkeypatch.setenv("KOORDHIP_EVAL", evalpath)
+    prof = shipped_profile(numa=numa, reservation=True)
+    t = synth.make_cluster(synth.ClusterSpec(2500, seed=17), prof)
+    if numa:
+        synth.add_numa(t, synth.NumaSpec(), prof, seed=17)
+    synth.add_reservations(t, synth.ResvSpec(node_frac=0.3, groups=4), seed=17)
+    pods = synth.make_pods(synth.StreamSpec(2000, be_frac=0.3, seed=17, resv_match_frac=0.5, resv_groups=4,
+                                            resv_affinity_frac=0.3), prof)
+    assert (pods["flags"] & abi.POD_RESV_AFFINITY).sum() > 200
+    o = oracle.Oracle(to_c_config(prof), t)
+    rev = oracle.Oracle(to_c_config(prof), t).eval(pods[:32], k=16)
+    ref = o.place_stream(pods, threads=8)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got_eval = e.eval(pods[:32], k=16)
+        got = e.place_stream(pods)
+        assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
+        _state_eq(e, o, numa)
+    assert np.array_equal(rev["status"], got_eval["status"])
+    assert np.array_equal(rev["topk"], got_eval["topk"])
+    aff = (pods["flags"] & abi.POD_RESV_AFFINITY) != 0
+    assert (ref[aff] >= 0).sum() > 50 and (ref[aff] < 0).sum() > 10

@@ -142,3 +142,78 @@ def test_same_order_reservations_tie_to_lowest_index(loaded):
     top = oracle.Oracle(cfg, t).eval(pods, status=False, scores=False, k=4)["topk"][0]
     assert placed == 1
     assert top["node"][0] == 1 and top["score"][0] == top["score"][1] and top["node"][1] == 2
+
+
+# ------------------------------------------------------------ reservation affinity
+def _aff_pod(aff_json, labels=None):
+    return k8s.Pod(name="p", labels=dict(labels or {}), priority=9500,
+                   annotations={rv.ANNOTATION_RESERVATION_AFFINITY: aff_json},
+                   containers=[k8s.Container(requests=G.rlist({"cpu": "1"}))])
+
+
+def test_match_reservation_kat():
+    """Test_matchReservation (reservation/transformer_test.go:345-442): owners
+    only, and owners + a required affinity term on the reservation's labels."""
+    sel = rv.ReservationOwner(label_selector=rv.LabelSelector(match_labels={"app": "test"}))
+    r = rv.Reservation("r", "n0", labels={"reservation-type": "reservation-test"}, owners=[sel],
+                       allocatable=G.rlist({"cpu": "1"}))
+    pod = k8s.Pod(name="p", labels={"app": "test"})
+    idx = rv.ReservationIndex()
+    idx.group(r.owners, {}, r)
+    assert idx.pod_mask(pod) == 1                                   # :355-377 only match reservation owners
+    aff = ('{"requiredDuringSchedulingIgnoredDuringExecution": {"reservationSelectorTerms": [{"matchExpressions": '
+           '[{"key": "reservation-type", "operator": "In", "values": ["reservation-test"]}]}]}}')
+    p2 = _aff_pod(aff, {"app": "test"})
+    idx = rv.ReservationIndex()
+    assert idx.register_affinities([p2])
+    idx.group(r.owners, {}, r)
+    assert idx.pod_mask(p2) == 1                                    # :378-422 owners + affinity
+    assert rv.pod_keys(p2) & abi.POD_RESV_AFFINITY
+
+
+def test_reservation_affinity_selects_by_labels_and_name():
+    """matchReservation's fake node (transformer.go:340-356): node labels
+    overlaid with the reservation's, the reservation's name for matchFields."""
+    own = [rv.ReservationOwner(label_selector=rv.LabelSelector(match_labels={"app": "a"}))]
+    rs = [rv.Reservation("ra", "n0", labels={"tier": "gold"}, owners=own, allocatable=G.rlist({"cpu": "2"})),
+          rv.Reservation("rb", "n1", labels={"tier": "silver"}, owners=own, allocatable=G.rlist({"cpu": "2"})),
+          rv.Reservation("rc", "n2", owners=own, allocatable=G.rlist({"cpu": "2"}))]
+    node_labels = {"n0": {"zone": "z1"}, "n1": {"zone": "z2", "tier": "gold"}, "n2": {"zone": "z1", "tier": "gold"}}
+    pods = [_aff_pod('{"reservationSelector": {"tier": "gold"}}', {"app": "a"}),
+            _aff_pod('{"requiredDuringSchedulingIgnoredDuringExecution": {"reservationSelectorTerms": ['
+                     '{"matchFields": [{"key": "metadata.name", "operator": "In", "values": ["rb"]}]}]}}', {"app": "a"}),
+            _aff_pod('{"requiredDuringSchedulingIgnoredDuringExecution": {"reservationSelectorTerms": ['
+                     '{"matchExpressions": [{"key": "zone", "operator": "In", "values": ["z1"]}]}]}}', {"app": "b"}),
+            k8s.Pod(name="plain", labels={"app": "a"})]
+    idx = rv.ReservationIndex()
+    idx.register_affinities(pods)
+    prof = G.resv_profile()
+    nodes = [(f"n{i}", {"cpu": "32", "memory": "64Gi", "pods": "110"}) for i in range(3)]
+    from koordinator_amd import marshal
+    cluster = marshal.ClusterState(nodes=[k8s.Node(name=n, allocatable=G.rlist(a), labels=node_labels[n]) for n, a in nodes])
+    for r in rs:
+        cluster.node_pods.setdefault(r.node_name, []).append(r.reserve_pod())
+    t = marshal.build_table(cluster, prof, G.NOW)
+    rv.reservation_columns(t, {n: i for i, (n, _) in enumerate(nodes)}, rs, idx, node_labels)
+    recs = marshal.pod_records(pods, prof, idx)
+    grp = [(int(t["resv_flags"][i]) >> abi.RESV_GROUP_SHIFT) & 63 for i in range(3)]
+    matched = [[bool((int(recs["resv_match"][j]) >> grp[i]) & 1) for i in range(3)] for j in range(4)]
+    # reservation labels win over the node's (ra gold; rb silver although n1 is gold; rc takes n2's gold)
+    assert matched[0] == [True, False, True]
+    assert matched[1] == [False, True, False]                       # matchFields metadata.name
+    assert matched[2] == [False, False, False]                      # owners do not match app=b
+    assert matched[3] == [True, True, True]                         # no affinity: owners only
+    # the Filter: an affinity pod fits only where a reservation matched it (plugin.go:378-381)
+    cfg = to_c_config(prof)
+    st = oracle.Oracle(cfg, t).eval(recs, status=True, scores=False)["status"]
+    assert [(st[0, i] & abi.ST_RESV_FAIL) != 0 for i in range(3)] == [False, True, False]
+    assert all(st[2, i] & abi.ST_RESV_FAIL for i in range(3))
+    assert not any(st[3, i] & abi.ST_RESV_FAIL for i in range(3))
+
+
+def test_unregistered_affinity_is_an_error():
+    idx = rv.ReservationIndex()
+    with pytest.raises(rv.ReservationError):
+        idx.pod_mask(_aff_pod('{"reservationSelector": {"x": "y"}}'))
+    with pytest.raises(rv.ReservationError):
+        rv.parse_reservation_affinity({rv.ANNOTATION_RESERVATION_AFFINITY: "{bad"})
