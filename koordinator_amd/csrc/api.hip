@@ -596,7 +596,25 @@ int check_resv_rows(const koordhip_node_soa *s, int32_t m) {
 int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   c->d.rv = kh::DevResv{};
   c->dc.resv = 0;
-  if (!c->resv || !s->resv_flags) return 0;
+  if (!c->resv) return 0;
+  // a snapshot without reservation columns gets zero columns: the Reservation
+  // build (NM 3) still runs the plugin, e.g. a pod with a required reservation
+  // affinity fails its Filter on every node (plugin.go:378-381)
+  std::vector<uint32_t> zf;
+  std::vector<int32_t> zi;
+  std::vector<int64_t> zq;
+  koordhip_node_soa zs;
+  if (!s->resv_flags) {
+    zf.assign(std::max(n, 1), 0u);
+    zi.assign(std::max(n, 1), 0);
+    zq.assign(std::max(n, 1), 0);
+    zs = *s;
+    zs.resv_flags = zf.data();
+    zs.resv_order_rank = zi.data();
+    zs.resv_assigned = zi.data();
+    for (int k = 0; k < 2; k++) zs.resv_alloc[k] = zs.resv_nz[k] = zs.resv_allocated[k] = zq.data();
+    s = &zs;
+  }
   if (int e = check_resv_rows(s, n)) return e;
   kh::DevResv &rv = c->d.rv;
   uint32_t *f = nullptr;

@@ -477,9 +477,7 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
 
 // Total weighted score, or -1 when any enabled Filter fails.
 __device__ __forceinline__ int32_t eval_total(const DevPod &p, const NV &v, const DevCfg &c) {
-  // the Reservation Filter without reservation columns (NM != 3 builds): a pod
-  // with a required reservation affinity has no matched reservation anywhere
-  bool ok = !((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !c.resv && (p.flags & KOORDHIP_POD_RESV_AFFINITY));
+  bool ok = true;
   if (c.filt & KOORDHIP_PLUGIN_FIT) ok &= fit_filter(p, v);
   if (c.filt & KOORDHIP_PLUGIN_LOADAWARE) ok &= la_filter(p, v);
   int32_t t = 0;

@@ -2635,10 +2635,18 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       if (lane < nm) {
         const NV v = slot_row(mrow[lane]);
         mrow[lane] = v;
+#ifdef KH_PUBLISH_RELEASE
+        store_row(v, nodes(), my_node);
+#else
         store_row_wt(v, nodes(), my_node);  // write-through: no L2 write-back fence at the publish
+#endif
         if constexpr (NUMA) {
           const NR nr = mnr[lane];
+#ifdef KH_PUBLISH_RELEASE
+          store_side_row<NM>(nr, nodes(), my_node);
+#else
           store_side_row_wt<NM>(nr, nodes(), my_node);
+#endif
         }
       }
       if (lane == 0) __hip_atomic_store(&sh_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // helpers stop
@@ -2685,8 +2693,12 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         sh_mp = nm + ns;
         // the rows were stored write-through: drain them, then the relaxed
         // agent-scope flag (Guideline 16 R1; the evaluation side acquires)
+#ifdef KH_PUBLISH_RELEASE
+        store_release(&sy->res_round, r + 1);
+#else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&sy->res_round, r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       }
       if (dbg) {
         const uint64_t t_end = stamp();
