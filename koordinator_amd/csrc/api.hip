@@ -789,6 +789,12 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     m[0] &= ~1u;
     if (c->n_cu % 32) m.back() &= (1u << (c->n_cu % 32)) - 1u;
     e = hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)m.size(), m.data());
+  } else if (e == hipSuccess && std::getenv("KOORDHIP_DEDICATED_STREAM")) {
+    // diagnostics: the main stream on a hardware queue of its own (a CU-masked
+    // stream is never pooled with other streams)
+    std::vector<uint32_t> m((size_t)(c->n_cu + 31) / 32, 0xffffffffu);
+    if (c->n_cu % 32) m.back() &= (1u << (c->n_cu % 32)) - 1u;
+    e = hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)m.size(), m.data());
   } else if (e == hipSuccess) {
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   }
@@ -1299,6 +1305,10 @@ uint64_t *gather_buf(koordhip_ctx *c, int slot) {
 // all-gathers in the same round order) into their own gather buffer.
 int exchange(koordhip_ctx *c, const uint64_t *lists, size_t count, int slot, hipStream_t es) {
   if (c->comm) {
+    if (c->world == 1 && std::getenv("KOORDHIP_EXCH_MEMCPY")) {  // diagnostics: RCCL's one-rank all-gather as a plain copy
+      HIP_TRY(hipMemcpyAsync(gather_buf(c, slot), lists, count * sizeof(uint64_t), hipMemcpyDeviceToDevice, es));
+      return 0;
+    }
     NCCL_TRY(ncclAllGather(lists, gather_buf(c, slot), count, ncclUint64, slot ? c->comm2 : c->comm, es));
     return 0;
   }

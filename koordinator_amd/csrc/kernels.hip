@@ -276,11 +276,18 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
   const bool staged = total <= MERGE_STAGE && L <= MERGE_MAXL;
   auto gkey = [&](int32_t l, int32_t j) -> uint64_t { return lists[(size_t)l * list_stride + j]; };
   auto key = [&](int32_t l, int32_t j) -> uint64_t { return staged ? stage[l * k + j] : gkey(l, j); };
-  // ---- 1. stage the lists in LDS
-  if (t == 0) {
-
-    cnt_gt = 0;
+  uint64_t *o = out + (size_t)p * k;
+  if (L == 1) {  // one shard: its list is already in the output form
+    for (int32_t j = t; j < k; j += MERGE_THREADS) st_wt(&o[j], lists[j]);
+    if (sy) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) pipe_count_pod(sy, sel_par);
+    }
+    return;
   }
+  // ---- 1. stage the lists in LDS
+  if (t == 0) cnt_gt = 0;
   if (staged && list_stride == k) {
     // contiguous lists: one LDS-DMA burst (the buffer is padded to 1 KiB)
     dma_to_lds_block(stage, lists, (total * 8 + 1023) & ~1023);
@@ -362,12 +369,11 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
   // ---- 4. output: sorted keys above S, then the lowest-index ties
   const int32_t gt = cnt_gt;
   const int32_t need = k - gt;
-  uint64_t *o = out + (size_t)p * k;
   for (int32_t j = t; j < gt; j += MERGE_THREADS) {
     const uint64_t x = gtbuf[j];
     int32_t rank = 0;
     for (int32_t q = 0; q < gt; q++) rank += gtbuf[q] > x;
-    o[rank] = x;
+    st_wt(&o[rank], x);
   }
   for (int32_t l = w; l < L; l += MERGE_THREADS / 64) {
     int32_t base = tie_pre[l];
@@ -378,12 +384,12 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
       const bool tie = key_sc(x) == S;
       const uint64_t tb = __ballot(tie);
       const int32_t pos = base + __popcll(tb & lt);
-      if (tie && pos < need) o[gt + pos] = x;
+      if (tie && pos < need) st_wt(&o[gt + pos], x);
       base += __popcll(tb);
     }
   }
   const int32_t filled = gt + min(need, all_ties);
-  for (int32_t j = filled + t; j < k; j += MERGE_THREADS) o[j] = 0;
+  for (int32_t j = filled + t; j < k; j += MERGE_THREADS) st_wt(&o[j], (uint64_t)0);
   if (sy) {  // the pod's merged list is published: count it into the pipeline (no signal kernel)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -946,7 +952,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
     const uint64_t x = gtbuf[j];
     int32_t rank = 0;
     for (int32_t q2 = 0; q2 < gt; q2++) rank += gtbuf[q2] > x;
-    o[rank] = x;
+    st_wt(&o[rank], x);
   }
   const int32_t filled = gt + min(need, ties);
   for (int32_t j = filled + t; j < k; j += SEL_THREADS) o[j] = 0;
@@ -991,11 +997,11 @@ __device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One pod's final list is stored (every wave drained its stores and met at a
-// barrier): agent release, then count it into sel[par] (Guideline 16 counter form).
+// One pod's final list is stored write-through (st_wt: every byte sc1, every
+// storing wave drained vmcnt and met at a barrier): count it into sel[par]
+// with a relaxed agent add, no release fence (Guideline 16 R1; the resolve's
+// wave acquires after its poll).
 __device__ void pipe_count_pod(PipeSync *sy, int32_t par) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_fetch_add(&sy->sel[par], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1299,23 +1305,21 @@ __global__ __launch_bounds__(SPL_THREADS) void k_select_split(
     const uint64_t x = h.lst[j];
     int32_t rank = 0;
     for (int32_t q2 = 0; q2 < mgt; q2++) rank += h.lst[q2] > x;
-    o[rank] = x;
+    st_wt(&o[rank], x);
   }
   for (int32_t j = t; j < total; j += SPL_THREADS) {
     const uint64_t x = mk[j];
     if (key_sc(x) != St) continue;
     const int32_t s = j / k;
     const int32_t pos = mgt + h.tie[s] + (j - s * k - h.gtc[s]);
-    if (pos < k) o[pos] = x;
+    if (pos < k) st_wt(&o[pos], x);
   }
-  for (int32_t j = mgt + min(mneed, h.nties) + t; j < k; j += SPL_THREADS) o[j] = 0;
+  for (int32_t j = mgt + min(mneed, h.nties) + t; j < k; j += SPL_THREADS) st_wt(&o[j], (uint64_t)0);
   if (sy) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(&sy->sel[sel_par], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pipe_count_pod(sy, sel_par);
       // the next scan on this stream may read the node columns only once the
       // resolve has written back round res_wait - 1: the launch ends no earlier
       // (replaces a k_wait_resolved launch between this kernel and the scan)
@@ -1657,16 +1661,16 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
     const uint64_t x = h.gtk[j];
     int32_t rank = 0;
     for (int32_t q = 0; q < mgt; q++) rank += h.gtk[q] > x;
-    o[rank] = x;
+    st_wt(&o[rank], x);
   }
   {
     int32_t pos = tpos0;
     for (int32_t x = x0; x < x1 && pos < mneed; x++) {
       const uint64_t kk = key(x);
-      if ((uint32_t)(kk >> 32) == S) o[mgt + pos++] = kk;
+      if ((uint32_t)(kk >> 32) == S) st_wt(&o[mgt + pos++], kk);
     }
   }
-  for (int32_t j = mgt + min(mneed, mties) + t; j < k; j += ETK_THREADS) o[j] = 0ull;
+  for (int32_t j = mgt + min(mneed, mties) + t; j < k; j += ETK_THREADS) st_wt(&o[j], (uint64_t)0);
   if (dbg && t == 0) {
     atomicAdd((unsigned long long *)&dbg[44], (unsigned long long)(stamp() - ts[3]));
     atomicAdd((unsigned long long *)&dbg[45], 1ull);
@@ -3050,14 +3054,12 @@ hipError_t launch_select_split(const uint16_t *S, int64_t s_stride, int32_t lo, 
 }
 
 __global__ void k_empty_lists(uint64_t *out, int32_t n, PipeSync *sy, int32_t par, int32_t pods) {
-  for (int32_t j = threadIdx.x; j < n; j += blockDim.x) out[j] = 0ull;
+  for (int32_t j = threadIdx.x; j < n; j += blockDim.x) st_wt(&out[j], (uint64_t)0);
   if (sy) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(&sy->sel[par], pods, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&sy->sel[par], pods, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // stores sc1 + drained
     }
   }
 }
