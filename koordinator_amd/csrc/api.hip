@@ -647,6 +647,11 @@ int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
 void shard(const koordhip_ctx *c, int32_t *lo, int32_t *hi) {
   *lo = (int32_t)((int64_t)c->n * c->rank / c->world);
   *hi = (int32_t)((int64_t)c->n * (c->rank + 1) / c->world);
+  // KOORDHIP_SHARD_SIM=W (timing diagnostics for the multi-GPU estimate, a
+  // one-rank communicator only): evaluate shard 0 of W, as rank 0 of a
+  // W-GPU job would; the placements then differ from the full table's
+  if (c->comm && c->world == 1)
+    if (const char *w = std::getenv("KOORDHIP_SHARD_SIM")) *hi = (int32_t)((int64_t)c->n / std::max(1, std::atoi(w)));
 }
 
 }  // namespace
@@ -789,9 +794,13 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     m[0] &= ~1u;
     if (c->n_cu % 32) m.back() &= (1u << (c->n_cu % 32)) - 1u;
     e = hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)m.size(), m.data());
-  } else if (e == hipSuccess && std::getenv("KOORDHIP_DEDICATED_STREAM")) {
-    // diagnostics: the main stream on a hardware queue of its own (a CU-masked
-    // stream is never pooled with other streams)
+  } else if (e == hipSuccess && !std::getenv("KOORDHIP_POOLED_STREAM")) {
+    // the main evaluation stream on a hardware queue of its own: a CU-masked
+    // stream is never pooled.  A pooled stream shares its queue with other
+    // streams of the process (the null stream, RCCL's internal streams), and
+    // with a communicator attached the one-rank exchange path measured 468k
+    // pods/s on config 4 there against 1.00M on a dedicated queue (its small
+    // per-round kernels waited ~40 us behind the queue's other work).
     std::vector<uint32_t> m((size_t)(c->n_cu + 31) / 32, 0xffffffffu);
     if (c->n_cu % 32) m.back() &= (1u << (c->n_cu % 32)) - 1u;
     e = hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)m.size(), m.data());

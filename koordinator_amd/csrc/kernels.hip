@@ -264,8 +264,10 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
                                                               int64_t list_stride, int32_t L, int32_t k,
                                                               int32_t score_bits, uint64_t *__restrict__ out,
                                                               PipeSync *sy, int32_t sel_par) {
-  __shared__ __attribute__((aligned(16))) uint64_t stage[MERGE_STAGE + 128];
-  __shared__ int32_t tie_pre[MERGE_MAXL];
+  // dynamic LDS (merge_lds_bytes): the staged lists, padded to the 1 KiB
+  // LDS-DMA granule, then one tie count per list -- a one-shard copy asks for
+  // none, so it fits beside a co-running evaluation's workgroups
+  extern __shared__ __attribute__((aligned(16))) char mlds[];
   __shared__ uint64_t gtbuf[RES_MAXP];
   __shared__ int32_t wsum[MERGE_THREADS / 64];
   __shared__ int32_t cnt_gt;
@@ -274,6 +276,8 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
   const uint64_t *lists = in + (size_t)p * pod_stride;
   const int32_t total = L * k;
   const bool staged = total <= MERGE_STAGE && L <= MERGE_MAXL;
+  uint64_t *stage = reinterpret_cast<uint64_t *>(mlds);
+  int32_t *tie_pre = reinterpret_cast<int32_t *>(mlds + (staged ? ((total * 8 + 1023) & ~1023) : 0));
   auto gkey = [&](int32_t l, int32_t j) -> uint64_t { return lists[(size_t)l * list_stride + j]; };
   auto key = [&](int32_t l, int32_t j) -> uint64_t { return staged ? stage[l * k + j] : gkey(l, j); };
   uint64_t *o = out + (size_t)p * k;
@@ -3143,8 +3147,16 @@ hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *po
 hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t list_stride, int32_t n_pods, int32_t L,
                              int32_t k, int32_t score_bits, uint64_t *out, PipeSync *sync, int32_t sel_par,
                              hipStream_t s) {
-  if (score_bits > 31 || L > MERGE_MAXL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_topk_merge, dim3(n_pods), dim3(MERGE_THREADS), 0, s, in, pod_stride, list_stride, L, k,
+  if (score_bits > 31 || L > MERGE_MAXL || k < 1) return hipErrorInvalidValue;
+  const int32_t total = L * k;
+  const size_t lds = L == 1 ? 0 : (size_t)(total <= MERGE_STAGE ? ((total * 8 + 1023) & ~1023) : 0) + (size_t)L * 4;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void *)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_topk_merge, dim3(n_pods), dim3(MERGE_THREADS), lds, s, in, pod_stride, list_stride, L, k,
                      score_bits, out, sync, sel_par);
   return hipGetLastError();
 }
