@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 5
+#define KOORDHIP_ABI_VERSION 6
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -56,7 +56,17 @@ extern "C" {
 #define KOORDHIP_PLUGIN_NUMA 4u       /* NodeNUMAResource */
 #define KOORDHIP_PLUGIN_RESERVATION 8u /* Reservation (restore + filterWithReservations + Score, weight
                                           koordhip_config.reservation_weight) */
-#define KOORDHIP_NPLUGINS 3            /* plugins with a per-node score in koordhip_eval's scores */
+/* Upstream default-profile plugins (k8s v1.24.15, un-vendored: SURVEY.md
+ * section 8(f)#4; restated in DESIGN.md, parity unpinned by reference tests): */
+#define KOORDHIP_PLUGIN_NODE_STATIC 16u /* Filter: NodeUnschedulable + NodeAffinity (nodeSelector +
+                                           requiredDuringScheduling) + TaintToleration (NoSchedule /
+                                           NoExecute), resolved per (pod static class, node) by the host
+                                           into koordhip_node_soa.static_allow */
+#define KOORDHIP_PLUGIN_BALANCED 32u    /* Score: NodeResourcesBalancedAllocation (cpu + memory,
+                                           Requested + the pod request, 1 - |f_cpu - f_mem| / 2) */
+#define KOORDHIP_NPLUGINS 4             /* plugins with a per-node score in koordhip_eval's scores:
+                                           Fit, LoadAware, NUMA, BalancedAllocation */
+#define KOORDHIP_MAX_STATIC_CLASSES 32  /* distinct pod static classes (koordhip_pod.static_class) */
 
 /* Fit resource slots (ResourceSpec names in scheduler-config.yaml:21-31). */
 #define KOORDHIP_RES_CPU 0   /* "cpu", milli-CPU */
@@ -161,6 +171,7 @@ typedef struct koordhip_numa_class {
 #define KOORDHIP_ST_LA_FAIL 2u
 #define KOORDHIP_ST_NUMA_FAIL 4u
 #define KOORDHIP_ST_RESV_FAIL 8u  /* filterWithReservations (reservation/plugin.go:373-440) */
+#define KOORDHIP_ST_STATIC_FAIL 16u /* NodeUnschedulable / NodeAffinity / TaintToleration */
 
 /* place_stream out_node values */
 #define KOORDHIP_UNSCHEDULABLE (-1)
@@ -175,7 +186,7 @@ typedef struct koordhip_config {
   uint32_t filter_plugins;  /* KOORDHIP_PLUGIN_* bits enabled at Filter */
   uint32_t score_plugins;   /* KOORDHIP_PLUGIN_* bits enabled at Score */
   int32_t device;           /* HIP device ordinal; -1 = current device */
-  int64_t plugin_weight[KOORDHIP_NPLUGINS]; /* score weight: Fit, LoadAware, NUMA (1..100) */
+  int64_t plugin_weight[KOORDHIP_NPLUGINS]; /* score weight: Fit, LoadAware, NUMA, BalancedAllocation (1..100) */
   int64_t fit_weight[KOORDHIP_NRES];        /* NodeResourcesFitArgs LeastAllocated weights, 0 = resource not listed */
   int64_t la_weight_cpu;                    /* LoadAwareSchedulingArgs.ResourceWeights[cpu] (1..100) */
   int64_t la_weight_mem;                    /* LoadAwareSchedulingArgs.ResourceWeights[memory] (1..100) */
@@ -257,6 +268,11 @@ typedef struct koordhip_node_soa {
   const int64_t *resv_nz[2];
   const int64_t *resv_allocated[2];
   const int32_t *resv_assigned;
+  /* KOORDHIP_PLUGIN_NODE_STATIC: bit c set = pods of static class c pass
+   * NodeUnschedulable, NodeAffinity and TaintToleration's Filter on this node
+   * (the node's labels, taints and spec.unschedulable against the class's
+   * nodeSelector, required affinity and tolerations); NULL = every class. */
+  const uint32_t *static_allow;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -269,7 +285,8 @@ typedef struct koordhip_pod {
   uint32_t flags;             /* KOORDHIP_POD_* */
   int32_t numa_cpus;          /* NUMA numCPUsNeeded (plugin.go:252) */
   uint32_t numa_policy;       /* KOORDHIP_NUMA_* packed policies */
-  int32_t reserved0;
+  int32_t static_class;       /* KOORDHIP_PLUGIN_NODE_STATIC: the pod's class (0 .. MAX_STATIC_CLASSES-1): pods
+                                 of one class share nodeSelector, required node affinity and tolerations */
   uint64_t resv_match;        /* bit g: MatchReservationOwners(pod, owner group g) (util/reservation/reservation.go:389-410) */
 } koordhip_pod;
 

@@ -11,13 +11,21 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 5
+KOORDHIP_ABI_VERSION = 6
 NRES = 5
-NPLUGINS = 3
+NPLUGINS = 4
 
 PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_RESERVATION = 1, 2, 4, 8
+PLUGIN_NODE_STATIC, PLUGIN_BALANCED = 16, 32
+# upstream NodeUnschedulable / NodeAffinity / TaintToleration all map to the
+# host-resolved static filter bit
 PLUGIN_BITS = {"NodeResourcesFit": PLUGIN_FIT, "LoadAwareScheduling": PLUGIN_LOADAWARE,
-               "NodeNUMAResource": PLUGIN_NUMA, "Reservation": PLUGIN_RESERVATION}
+               "NodeNUMAResource": PLUGIN_NUMA, "Reservation": PLUGIN_RESERVATION,
+               "NodeUnschedulable": PLUGIN_NODE_STATIC, "NodeAffinity": PLUGIN_NODE_STATIC,
+               "TaintToleration": PLUGIN_NODE_STATIC, "NodeResourcesBalancedAllocation": PLUGIN_BALANCED}
+# plugin_weight[p] / score plane p
+SCORE_PLUGIN_BITS = (PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_BALANCED)
+MAX_STATIC_CLASSES = 32
 RES_CPU, RES_MEM, RES_EPH, RES_BCPU, RES_BMEM = range(5)
 
 LA_HAS_METRIC, LA_FILTER_SKIP, LA_SCORE_EXPIRED, LA_FILTER_USAGE = 1, 2, 4, 8
@@ -47,7 +55,7 @@ NUMA_MAX_ZONES = 8
 def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> int:
     return (required & 3) | ((preferred & 3) << 2) | ((exclusive & 3) << 4)
 
-ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL, ST_RESV_FAIL = 1, 2, 4, 8
+ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL, ST_RESV_FAIL, ST_STATIC_FAIL = 1, 2, 4, 8, 16
 UNSCHEDULABLE, RESERVE_FAILED = -1, -2
 E_INVAL, E_RESERVE = -1, -6
 UNIQUE_ID_BYTES = 128
@@ -126,6 +134,7 @@ class KoordhipNodeSoa(C.Structure):
         ("resv_nz", _i64p * 2),
         ("resv_allocated", _i64p * 2),
         ("resv_assigned", _i32p),
+        ("static_allow", C.POINTER(C.c_uint32)),
     ]
 
 
@@ -154,7 +163,7 @@ POD_DTYPE = np.dtype([
     ("flags", "<u4"),
     ("numa_cpus", "<i4"),
     ("numa_policy", "<u4"),
-    ("reserved0", "<i4"),
+    ("static_class", "<i4"),
     ("resv_match", "<u8"),
 ], align=True)
 assert POD_DTYPE.itemsize == 96

@@ -22,6 +22,13 @@ PLUGIN_FIT = "NodeResourcesFit"
 PLUGIN_LOADAWARE = "LoadAwareScheduling"
 PLUGIN_NUMA = "NodeNUMAResource"
 PLUGIN_RESERVATION = "Reservation"
+# upstream default-profile plugins (k8s v1.24.15): three static node filters
+# (resolved by the host into static_allow) and one score
+PLUGIN_NODE_UNSCHEDULABLE = "NodeUnschedulable"
+PLUGIN_NODE_AFFINITY = "NodeAffinity"
+PLUGIN_TAINT_TOLERATION = "TaintToleration"
+PLUGIN_BALANCED = "NodeResourcesBalancedAllocation"
+STATIC_FILTERS = (PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
 
 
 class ArgsError(ValueError):
@@ -176,6 +183,18 @@ def shipped_profile(numa: bool = False, reservation: bool = False) -> Profile:
     return Profile(fit=fit, loadaware=la)
 
 
+def with_upstream(profile: Profile, static_filters=STATIC_FILTERS, balanced_weight: int = 0) -> Profile:
+    """The profile plus upstream default-profile plugins: the static node
+    filters (Filter) and NodeResourcesBalancedAllocation (Score, weight
+    `balanced_weight`; 0 = not enabled)."""
+    p = copy.deepcopy(profile)
+    p.filters = tuple(p.filters) + tuple(f for f in static_filters if f not in p.filters)
+    if balanced_weight:
+        p.scores = dict(p.scores)
+        p.scores[PLUGIN_BALANCED] = balanced_weight
+    return p
+
+
 def to_c_config(profile: Profile, device: int = -1):
     """Lower a resolved profile to the koordhip_config ctypes struct."""
     from .abi import (KOORDHIP_ABI_VERSION, PLUGIN_BITS, KoordhipConfig)
@@ -190,7 +209,12 @@ def to_c_config(profile: Profile, device: int = -1):
     cfg.filter_plugins = sum(PLUGIN_BITS[x] for x in set(p.filters))
     cfg.score_plugins = sum(PLUGIN_BITS[x] for x in p.scores)
     cfg.device = device
-    order = [PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA]
+    for name in p.scores:
+        if name in STATIC_FILTERS:
+            # their upstream Scores (preferred node affinity, PreferNoSchedule
+            # taints) normalise over the feasible nodes: not supported
+            raise ArgsError(f"the Score of {name} is not supported (Filter only)")
+    order = [PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_BALANCED]
     for i, name in enumerate(order):
         w = p.scores.get(name, 0)
         if name in p.scores and not (1 <= w <= 100):

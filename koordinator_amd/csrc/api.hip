@@ -45,6 +45,9 @@ constexpr int kDefaultBatchNuma = 16;
 constexpr int kDefaultBatchResv = 32;  // config 5 (evaluation-bound): 143k pods/s vs 135k at 16
 constexpr int32_t kMaxNodes = 400000;  // the resolve keeps a per-node bit in LDS (next to 2 x 64 x 128 list keys)
 constexpr int kMaxBatch = 64;
+// plugin_weight[p] / koordhip_eval's score plane p belong to these plugins
+constexpr uint32_t kScorePluginBit[KOORDHIP_NPLUGINS] = {KOORDHIP_PLUGIN_FIT, KOORDHIP_PLUGIN_LOADAWARE,
+                                                          KOORDHIP_PLUGIN_NUMA, KOORDHIP_PLUGIN_BALANCED};
 constexpr int kRing = 4;               // per-round events in flight (lag-1 pipeline needs 3)
 
 // Contexts of one process sharing node shards without RCCL
@@ -255,6 +258,9 @@ int to_dev_pods(const koordhip_pod *src, int32_t n, std::vector<kh::DevPod> &out
     o.flags = p.flags;
     o.numa_cpus = p.numa_cpus;
     o.numa_policy = p.numa_policy;
+    if (p.static_class < 0 || p.static_class >= KOORDHIP_MAX_STATIC_CLASSES)
+      return fail(KOORDHIP_EINVAL, "pod static_class out of range");
+    o.sclass = p.static_class;
     o.resv_match = p.resv_match;
   }
   return 0;
@@ -664,14 +670,17 @@ int koordhip_abi_version(void) { return KOORDHIP_ABI_VERSION; }
 int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (!cfg || !out) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (cfg->abi_version != KOORDHIP_ABI_VERSION) return fail(KOORDHIP_EINVAL, "abi_version mismatch");
-  const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA | KOORDHIP_PLUGIN_RESERVATION;
+  const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA |
+                         KOORDHIP_PLUGIN_RESERVATION | KOORDHIP_PLUGIN_NODE_STATIC | KOORDHIP_PLUGIN_BALANCED;
   if ((cfg->filter_plugins | cfg->score_plugins) & ~known) return fail(KOORDHIP_EINVAL, "unknown plugin bit");
+  if (cfg->score_plugins & KOORDHIP_PLUGIN_NODE_STATIC) return fail(KOORDHIP_EINVAL, "the static node filters have no Score");
+  if (cfg->filter_plugins & KOORDHIP_PLUGIN_BALANCED) return fail(KOORDHIP_EINVAL, "BalancedAllocation has no Filter");
   if (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) {
     if (cfg->numa_weight_cpu < 0 || cfg->numa_weight_cpu > 100 || cfg->numa_weight_mem < 0 || cfg->numa_weight_mem > 100)
       return fail(KOORDHIP_EINVAL, "NodeNUMAResource resource weights must be in [0, 100]");
   }
   for (int p = 0; p < KOORDHIP_NPLUGINS; p++) {
-    const uint32_t bit = 1u << p;
+    const uint32_t bit = kScorePluginBit[p];
     if ((cfg->score_plugins & bit) && (cfg->plugin_weight[p] < 1 || cfg->plugin_weight[p] > 100))
       return fail(KOORDHIP_EINVAL, "plugin score weight must be in [1, 100]");
   }
@@ -709,6 +718,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.w_fit = (int32_t)cfg->plugin_weight[0];
   c->dc.w_la = (int32_t)cfg->plugin_weight[1];
   c->dc.w_numa = (int32_t)cfg->plugin_weight[2];
+  c->dc.w_bal = (int32_t)cfg->plugin_weight[3];
   for (int r = 0; r < KOORDHIP_NRES; r++) c->dc.fit_w[r] = (int32_t)cfg->fit_weight[r];
   c->dc.la_w_cpu = (int32_t)cfg->la_weight_cpu;
   c->dc.la_w_mem = (int32_t)cfg->la_weight_mem;
@@ -737,11 +747,16 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   // Fit LeastAllocated + LoadAware least-used (+ NodeNUMAResource LeastAllocated):
   // a commit never raises a key.  A MostAllocated NUMA score rises with every
   // commit, so the resolve re-evaluates its modified nodes for every pod.
-  c->monotone = ((cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) && cfg->numa_most_allocated) ? 0 : 1;
+  // BalancedAllocation rewards the balance of cpu and memory, which a commit
+  // can improve: not monotone either.
+  c->monotone = (((cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) && cfg->numa_most_allocated) ||
+                 (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED))
+                    ? 0
+                    : 1;
   {
     int64_t max_total = 0;  // every plugin score is in [0, 100]
     for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
-      if (cfg->score_plugins & (1u << p)) max_total += 100 * cfg->plugin_weight[p];
+      if (cfg->score_plugins & kScorePluginBit[p]) max_total += 100 * cfg->plugin_weight[p];
     c->dc.resv_b1 = (int32_t)max_total + 1;
     if (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION) {
       // the ranking totals of resv.hpp: one normalised Reservation unit must
@@ -926,6 +941,14 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   if (!e) e = dev_alloc(c, &lf, n);
   if (!e) e = upload(c, lf, s->la_flags, n);
   pi.la_flags = lf;
+  // static node filters: the allow mask per node (no column = every class)
+  d.sallow = nullptr;
+  if (!e && (c->dc.filt & KOORDHIP_PLUGIN_NODE_STATIC) && s->static_allow) {
+    uint32_t *sa = nullptr;
+    e = dev_alloc(c, &sa, n);
+    if (!e) e = upload(c, sa, s->static_allow, n);
+    d.sallow = sa;
+  }
   if (!e) e = load_numa_columns(c, s, n);
   if (!e) e = load_resv_columns(c, s, n);
   if (!e && c->dc.resv && c->dc.zones)
@@ -993,6 +1016,10 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     }
     amp_rows = c->d.nu.amp != nullptr;
   }
+  if ((c->dc.filt & KOORDHIP_PLUGIN_NODE_STATIC) && rows->static_allow && !c->d.sallow)
+    for (int32_t j = 0; j < m; j++)
+      if (rows->static_allow[j] != 0xFFFFFFFFu)
+        return fail(KOORDHIP_EINVAL, "a static node filter needs the static_allow column at load_snapshot");
   const bool resv_rows = c->dc.resv && rows->resv_flags;
   if (c->resv && rows->resv_flags && !c->dc.resv) {
     for (int32_t j = 0; j < m; j++)
@@ -1048,6 +1075,8 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   }
   if (amp_rows)
     cols.push_back({const_cast<double *>(c->d.nu.amp), rows->numa_amp_cpu, 8, false, "numa_amp_cpu"});
+  if (c->d.sallow && rows->static_allow)
+    cols.push_back({const_cast<uint32_t *>(c->d.sallow), rows->static_allow, 4, false, "static_allow"});
   if (resv_rows) {
     kh::DevResv &rv = c->d.rv;
     cols.push_back({const_cast<uint32_t *>(rv.flags), rows->resv_flags, 4, false, "resv_flags"});

@@ -51,7 +51,7 @@ enum : uint32_t {
 
 struct DevCfg {
   uint32_t filt, score;
-  int32_t w_fit, w_la, w_numa;
+  int32_t w_fit, w_la, w_numa, w_bal;
   int32_t fit_w[KOORDHIP_NRES];
   int32_t la_w_cpu, la_w_mem;
   int32_t according;  // ScoreAccordingProdUsage
@@ -76,6 +76,7 @@ struct DevNodes {
   const double *la_alloc_cpu, *la_alloc_mem;
   double *la_used_cpu, *la_used_mem, *la_used_prod_cpu, *la_used_prod_mem;
   uint8_t *flags;
+  const uint32_t *sallow;  // KOORDHIP_PLUGIN_NODE_STATIC: allowed pod static classes (NULL = all)
   int32_t n;
   DevNuma nu;  // NodeNUMAResource columns (unused unless the plugin is enabled)
   DevResv rv;  // Reservation columns (NM == 3 builds)
@@ -89,6 +90,7 @@ struct NV {
   double la_a_cpu, la_a_mem, la_u_cpu, la_u_mem, la_up_cpu, la_up_mem;
   int32_t a_pods, npods;
   uint32_t flags;
+  uint32_t sa;  // static_allow (the row's last word: static, copied along, never written back)
 };
 
 // What one pod's evaluation needs from the node columns (wave-uniform).
@@ -98,6 +100,7 @@ struct Need {
   bool zones;             // node flags + NUMA zones (topology-policy nodes)
   bool amp;               // the CPU amplification ratio + allocated cpuset count
   bool resv;              // the reservation columns (the restore rewrites Requested / NonZero / pods)
+  bool sa;                // the static-filter allow mask
 };
 
 __device__ __forceinline__ bool numa_on(const DevCfg &c) {
@@ -148,6 +151,9 @@ __device__ __forceinline__ Need pod_needs(const DevPod &p, const DevCfg &c) {
     n.r_mem = true;
     n.a_cpu = n.a_mem = true;
   }
+  // NodeResourcesBalancedAllocation: Requested + Allocatable cpu / memory
+  if (c.score & KOORDHIP_PLUGIN_BALANCED) n.r_cpu = n.r_mem = n.a_cpu = n.a_mem = true;
+  n.sa = (c.filt & KOORDHIP_PLUGIN_NODE_STATIC) != 0;
   if (c.resv) {
     // the restore rewrites Requested (the over-commit bits are re-derived from
     // it), NonZeroRequested and the pod count; a matched reservation's Aligned /
@@ -192,6 +198,7 @@ __device__ __forceinline__ Need need_all(const DevCfg &c) {
   n.zones = n.numa && c.zones;
   n.amp = n.numa && c.amp;
   n.resv = c.resv != 0;
+  n.sa = true;
   return n;
 }
 
@@ -247,6 +254,7 @@ __device__ __forceinline__ T &col(T *base, int32_t i) {
 // Load node i's columns the evaluation needs (coalesced across lanes).
 __device__ __forceinline__ void load_node(NV &v, const DevNodes &d, int32_t i, const Need &n, const DevCfg &c) {
   v.flags = col(d.flags, i);
+  v.sa = (n.sa && d.sallow) ? col(d.sallow, i) : 0xFFFFFFFFu;
   if (n.pods) {
     v.a_pods = col(d.alloc_pods, i);
     v.npods = col(d.npods, i);
@@ -475,14 +483,32 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
   return numa_la(rc + qc, ac, rm + p.req[KOORDHIP_RES_MEM], am, c.numa_w_cpu, c.numa_w_mem, lr, dw);
 }
 
+// NodeResourcesBalancedAllocation Score (upstream k8s v1.24.15
+// balanced_allocation.go balancedResourceScorer over resource_allocation.go's
+// calculateResourceAllocatableRequest with useRequested: Requested + the
+// pod's request, cpu and memory with weight 1, resources with Allocatable 0
+// left out): fraction = min(1, req / alloc) in f64, std = |f_cpu - f_mem| / 2
+// for two fractions (0 for fewer), score = int64((1 - std) * 100).
+__device__ __forceinline__ int32_t bal_score(const DevPod &p, const NV &v) {
+  const double ac = v.a[KOORDHIP_RES_CPU], am = v.a[KOORDHIP_RES_MEM];
+  double fc = (v.r[KOORDHIP_RES_CPU] + p.req[KOORDHIP_RES_CPU]) / ac;
+  double fm = (v.r[KOORDHIP_RES_MEM] + p.req[KOORDHIP_RES_MEM]) / am;
+  fc = fc > 1.0 ? 1.0 : fc;
+  fm = fm > 1.0 ? 1.0 : fm;
+  const double std = (ac != 0.0 && am != 0.0) ? fabs((fc - fm) / 2.0) : 0.0;
+  return (int32_t)((1.0 - std) * 100.0);
+}
+
 // Total weighted score, or -1 when any enabled Filter fails.
 __device__ __forceinline__ int32_t eval_total(const DevPod &p, const NV &v, const DevCfg &c) {
   bool ok = true;
+  if (c.filt & KOORDHIP_PLUGIN_NODE_STATIC) ok &= ((v.sa >> p.sclass) & 1u) != 0;
   if (c.filt & KOORDHIP_PLUGIN_FIT) ok &= fit_filter(p, v);
   if (c.filt & KOORDHIP_PLUGIN_LOADAWARE) ok &= la_filter(p, v);
   int32_t t = 0;
   if (c.score & KOORDHIP_PLUGIN_FIT) t += c.w_fit * fit_score(p, v, c);
   if (c.score & KOORDHIP_PLUGIN_LOADAWARE) t += c.w_la * la_score(p, v, c);
+  if (c.score & KOORDHIP_PLUGIN_BALANCED) t += c.w_bal * bal_score(p, v);
   return ok ? t : -1;
 }
 
@@ -573,6 +599,7 @@ __device__ __forceinline__ void load_row(NV &v, const DevNodes &d, int32_t i) {
   v.la_up_cpu = d.la_used_prod_cpu[i];
   v.la_up_mem = d.la_used_prod_mem[i];
   v.flags = d.flags[i];
+  v.sa = d.sallow ? d.sallow[i] : 0xFFFFFFFFu;
 }
 
 template <bool Z = true>

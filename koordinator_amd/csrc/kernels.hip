@@ -176,6 +176,7 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
   }
   if (status) {
     uint8_t b = 0;
+    if ((c.filt & KOORDHIP_PLUGIN_NODE_STATIC) && !((v.sa >> pod.sclass) & 1u)) b |= KOORDHIP_ST_STATIC_FAIL;
     if ((c.filt & KOORDHIP_PLUGIN_FIT) && !fit_filter(pod, v)) b |= KOORDHIP_ST_FIT_FAIL;
     if ((c.filt & KOORDHIP_PLUGIN_LOADAWARE) && !la_filter(pod, v)) b |= KOORDHIP_ST_LA_FAIL;
     if ((c.filt & KOORDHIP_PLUGIN_NUMA) &&
@@ -191,6 +192,7 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
     row[i] = (c.score & KOORDHIP_PLUGIN_FIT) ? fit_score(pod, v, c) : 0;
     row[(size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_LOADAWARE) ? la_score(pod, v, c) : 0;
     row[2 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_NUMA) ? numa_score<true>(pod, v, nr, d.nu.cls, c) : 0;
+    row[3 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_BALANCED) ? bal_score(pod, v) : 0;
   }
 }
 

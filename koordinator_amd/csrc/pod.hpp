@@ -19,7 +19,7 @@ struct DevPod {
   uint32_t flags;
   int32_t numa_cpus;
   uint32_t numa_policy;
-  int32_t reserved0;
+  int32_t sclass;  // static class (KOORDHIP_PLUGIN_NODE_STATIC), 0 .. 31
   uint64_t resv_match;
 };
 static_assert(sizeof(DevPod) == 96, "DevPod is 96 bytes");

@@ -23,7 +23,8 @@ I64_COLS = (
 )
 I32_COLS = ["alloc_pods", "npods", "numa_class", "numa_alloc_cnt", "resv_order_rank", "resv_assigned"]
 U8_COLS = ["la_flags", "numa_flags"]
-U32_COLS = ["resv_flags"]   # KOORDHIP_RESV_* (0 = no reservation on the node)
+U32_COLS = ["resv_flags",   # KOORDHIP_RESV_* (0 = no reservation on the node)
+            "static_allow"]  # static node filters: allowed pod static classes (all ones = every class)
 U64_COLS = ([f"numa_free{w}" for w in range(abi.NUMA_WORDS)] + [f"numa_excl_pcpu{w}" for w in range(abi.NUMA_WORDS)]
             + [f"numa_excl_numa{w}" for w in range(abi.NUMA_WORDS)])
 # NUMA zone resources, [n][2][NUMA_MAX_NODES] int64 per column (cpu milli, memory bytes)
@@ -72,6 +73,7 @@ class NodeTable:
             t.cols[c] = np.zeros(_shape(c, n), dtype=_dtype(c))
         t.cols["numa_class"][:] = -1
         t.cols["numa_amp_cpu"][:] = 1.0
+        t.cols["static_allow"][:] = 0xFFFFFFFF
         t.names = [f"node-{i}" for i in range(n)]
         return t
 
@@ -139,6 +141,7 @@ class NodeTable:
             s.resv_nz[k] = p64(f"resv_nz{k}")
             s.resv_allocated[k] = p64(f"resv_allocated{k}")
         s.resv_assigned = p32("resv_assigned")
+        s.static_allow = self.cols["static_allow"].ctypes.data_as(C.POINTER(C.c_uint32))
         return s
 
     def nbytes(self) -> int:

@@ -283,6 +283,90 @@ def add_reservations(t: NodeTable, spec: ResvSpec, seed: int = SEED) -> NodeTabl
 
 
 @dataclass
+class StaticSpec:
+    """Node labels / taints / cordons and pod nodeSelector / required node
+    affinity / tolerations for the upstream static filters (SURVEY.md 8(f)#4)."""
+    tainted_frac: float = 0.15        # dedicated=<team>:NoSchedule
+    noexec_frac: float = 0.03         # maintenance:NoExecute
+    prefer_frac: float = 0.10         # soft=yes:PreferNoSchedule (Filter ignores it)
+    unschedulable_frac: float = 0.02  # spec.unschedulable (cordoned)
+    constrained_frac: float = 0.5     # pods with a non-empty static spec
+
+
+ZONES = ["zone-a", "zone-b", "zone-c", "zone-d"]
+TEAMS = ["team-1", "team-2"]
+
+
+def static_nodes(n: int, spec: StaticSpec, seed: int = SEED):
+    """NodeStatic records: zone / disktype / cpu-gen labels, taints, cordons."""
+    from .nodefilters import NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, NodeStatic, Taint
+    s = seed + 31
+    zone = splitmix64(s, n, 90) % np.uint64(len(ZONES))
+    ssd = uniform(s, n, 91) < 0.5
+    gen = (splitmix64(s, n, 92) % np.uint64(4)).astype(np.int64) + 2
+    tainted = uniform(s, n, 93) < spec.tainted_frac
+    team = splitmix64(s, n, 94) % np.uint64(len(TEAMS))
+    noexec = uniform(s, n, 95) < spec.noexec_frac
+    prefer = uniform(s, n, 96) < spec.prefer_frac
+    cordon = uniform(s, n, 97) < spec.unschedulable_frac
+    out = []
+    for i in range(n):
+        labels = {"topology.kubernetes.io/zone": ZONES[int(zone[i])], "cpu-gen": str(int(gen[i]))}
+        if ssd[i]:
+            labels["disktype"] = "ssd"
+        taints = []
+        if tainted[i]:
+            taints.append(Taint("dedicated", TEAMS[int(team[i])], NO_SCHEDULE))
+        if noexec[i]:
+            taints.append(Taint("maintenance", "", NO_EXECUTE))
+        if prefer[i]:
+            taints.append(Taint("soft", "yes", PREFER_NO_SCHEDULE))
+        out.append(NodeStatic(labels=labels, taints=taints, unschedulable=bool(cordon[i]), name=f"node-{i}"))
+    return out
+
+
+def static_templates():
+    """Pod static specs the stream draws from (template 0: unconstrained)."""
+    from .nodefilters import PodStatic, Toleration
+    from .reservation import NodeSelectorRequirement as R, NodeSelectorTerm as T
+    zone = "topology.kubernetes.io/zone"
+    return [
+        PodStatic(),
+        PodStatic(node_selector={zone: "zone-a"}),
+        PodStatic(node_selector={"disktype": "ssd"}),
+        PodStatic(required_terms=[T([R(zone, "In", ["zone-b", "zone-c"])])]),
+        PodStatic(required_terms=[T([R(zone, "NotIn", ["zone-a"]), R("disktype", "Exists")])]),
+        PodStatic(required_terms=[T([R("cpu-gen", "Gt", ["3"])]), T([R("disktype", "DoesNotExist")])]),
+        PodStatic(tolerations=[Toleration("dedicated", "Equal", "team-1", "NoSchedule")]),
+        PodStatic(tolerations=[Toleration("dedicated", "Exists")]),
+        PodStatic(node_selector={zone: "zone-d"}, tolerations=[Toleration(operator="Exists")]),
+        PodStatic(tolerations=[Toleration("node.kubernetes.io/unschedulable", "Exists", "", "NoSchedule"),
+                               Toleration("maintenance", "Exists", "", "NoExecute")]),
+        PodStatic(required_terms=[T([R("cpu-gen", "Lt", ["4"])], [R("metadata.name", "NotIn", ["node-0"])])]),
+        PodStatic(required_terms=[]),  # an empty term list matches no node
+    ]
+
+
+def add_static(t: NodeTable, pods: np.ndarray, spec: StaticSpec, profile: Profile, seed: int = SEED):
+    """Static classes for the pods (pods['static_class']) and the
+    static_allow column for the profile's enabled static filters.  Returns
+    (node specs, pod class specs) for tests."""
+    from .config import STATIC_FILTERS
+    from .nodefilters import StaticClasses, static_allow
+    nodes = static_nodes(t.n, spec, seed)
+    tmpl = static_templates()
+    n, s = len(pods), seed + 37
+    constrained = uniform(s, n, 98) < spec.constrained_frac
+    pick = (splitmix64(s, n, 99) % np.uint64(len(tmpl) - 1)).astype(np.int64) + 1
+    cls = StaticClasses()
+    cls.classify(tmpl[0])
+    ids = [cls.classify(tmpl[int(pick[j])]) if constrained[j] else 0 for j in range(n)]
+    pods["static_class"][:] = np.asarray(ids, dtype=np.int32)
+    t["static_allow"][:] = static_allow(nodes, cls, [f for f in profile.filters if f in STATIC_FILTERS])
+    return nodes, cls
+
+
+@dataclass
 class StreamSpec:
     n_pods: int
     be_frac: float = 0.0

@@ -242,11 +242,56 @@ int64_t orc_la_score(const koordhip_config *cfg, const orc_state *st, const koor
   return num / wsum;
 }
 
+/* UPSTREAM-ASSUMED (k8s v1.24.15, un-vendored; parity unpinned): the static
+ * node filters NodeUnschedulable (node_unschedulable.go: spec.unschedulable
+ * without a toleration of node.kubernetes.io/unschedulable:NoSchedule),
+ * NodeAffinity (node_affinity.go: nodeSelector + requiredDuringScheduling
+ * node selector terms) and TaintToleration (taint_toleration.go: every
+ * NoSchedule / NoExecute taint tolerated) depend only on the node's labels /
+ * taints and the pod's spec: the host marshaller resolves them per (pod
+ * static class, node) into static_allow (koordinator_amd/k8s.py
+ * static_allow); this is the per-(pod, node) lookup. */
+int orc_static_filter(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  const uint32_t *sa = st->soa->static_allow;
+  return !sa || ((sa[i] >> pod->static_class) & 1u);
+}
+
+/* UPSTREAM-ASSUMED (k8s v1.24.15 noderesources/balanced_allocation.go,
+ * resource_allocation.go; un-vendored, parity unpinned):
+ * NodeResourcesBalancedAllocation with its default resources cpu and memory
+ * (weight 1) and useRequested = true: requested = NodeInfo.Requested + the
+ * pod's request; a resource with Allocatable 0 is left out; fraction =
+ * float64(requested) / float64(allocatable), capped at 1; two fractions:
+ * std = |f0 - f1| / 2, fewer: 0; score = int64((1 - std) * MaxNodeScore). */
+int64_t orc_bal_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  (void)cfg;
+  const koordhip_node_soa *s = st->soa;
+  double f[2];
+  int nf = 0;
+  for (int r = KOORDHIP_RES_CPU; r <= KOORDHIP_RES_MEM; r++) {
+    const int64_t alloc = s->alloc[r][i];
+    if (alloc == 0) continue;
+    double x = (double)(st->requested[r][i] + pod->req[r]) / (double)alloc;
+    if (x > 1) x = 1;
+    f[nf++] = x;
+  }
+  double sd = 0.0;
+  if (nf == 2) sd = fabs((f[0] - f[1]) / 2);
+  return (int64_t)((1 - sd) * 100.0);
+}
+
+uint32_t orc_score_plugin_bit(int p) {
+  static const uint32_t bits[KOORDHIP_NPLUGINS] = {KOORDHIP_PLUGIN_FIT, KOORDHIP_PLUGIN_LOADAWARE,
+                                                   KOORDHIP_PLUGIN_NUMA, KOORDHIP_PLUGIN_BALANCED};
+  return p >= 0 && p < KOORDHIP_NPLUGINS ? bits[p] : 0u;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Combined evaluation                                                       */
 /* ------------------------------------------------------------------------ */
 
 static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NODE_STATIC) && !orc_static_filter(st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) return 0;
@@ -261,6 +306,7 @@ static int64_t orc_total(const koordhip_config *cfg, const orc_state *st, const 
   if (cfg->score_plugins & KOORDHIP_PLUGIN_FIT) t += cfg->plugin_weight[0] * orc_fit_score(cfg, st, pod, i);
   if (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) t += cfg->plugin_weight[1] * orc_la_score(cfg, st, pod, i);
   if (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) t += cfg->plugin_weight[2] * orc_numa_score(cfg, st, pod, i);
+  if (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) t += cfg->plugin_weight[3] * orc_bal_score(cfg, st, pod, i);
   return t;
 }
 
@@ -290,6 +336,8 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
       int numa_ok = (cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) ? orc_numa_filter(cfg, st, pod, i) : 1;
       if (status) {
         uint8_t b = 0;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NODE_STATIC) && !orc_static_filter(st, pod, i))
+          b |= KOORDHIP_ST_STATIC_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !fit_ok) b |= KOORDHIP_ST_FIT_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !la_ok) b |= KOORDHIP_ST_LA_FAIL;
         if (!numa_ok) b |= KOORDHIP_ST_NUMA_FAIL;
@@ -305,6 +353,8 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
             (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) ? (int32_t)orc_la_score(cfg, st, pod, i) : 0;
         row[2 * (size_t)n + i] =
             (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) ? (int32_t)orc_numa_score(cfg, st, pod, i) : 0;
+        row[3 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) ? (int32_t)orc_bal_score(cfg, st, pod, i) : 0;
       }
       if (keys && orc_feasible(cfg, st, pod, i)) {
         int64_t t = orc_total(cfg, st, pod, i);
@@ -494,7 +544,7 @@ typedef struct stream_ctx {
   const koordhip_pod *pod;
   _Atomic int32_t nfeasible;
   int32_t *feasible;      /* node ids (unordered, like upstream's atomic append) */
-  int64_t *plugin_scores; /* [3][nfeasible] */
+  int64_t *plugin_scores; /* [KOORDHIP_NPLUGINS][nfeasible] */
 } stream_ctx;
 
 /* (upstream) findNodesThatPassFilters checkNode: RunFilterPlugins, append on success. */
@@ -516,6 +566,8 @@ static void score_piece(void *a, int32_t lo, int32_t hi) {
         (c->cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) ? orc_la_score(c->cfg, c->st, c->pod, i) : 0;
     c->plugin_scores[2 * (size_t)nf + j] =
         (c->cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) ? orc_numa_score(c->cfg, c->st, c->pod, i) : 0;
+    c->plugin_scores[3 * (size_t)nf + j] =
+        (c->cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) ? orc_bal_score(c->cfg, c->st, c->pod, i) : 0;
   }
 }
 
@@ -528,7 +580,7 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
   c.cfg = cfg;
   c.st = st;
   c.feasible = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
-  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * 4 * (size_t)(n > 0 ? n : 1));
+  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * (KOORDHIP_NPLUGINS + 1) * (size_t)(n > 0 ? n : 1));
   const int rv = orc_resv_on(cfg, st);
   for (int32_t p = 0; p < n_pods; p++) {
     c.pod = &pods[p];
@@ -545,7 +597,7 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
     }
     pool_until(&pl, nf, score_piece, &c);
     /* Reservation PreScore + Score + NormalizeScore over the feasible list */
-    int64_t *norm = c.plugin_scores + 3 * (size_t)nf;
+    int64_t *norm = c.plugin_scores + KOORDHIP_NPLUGINS * (size_t)nf;
     const int rs = rv && (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION);
     if (rs) orc_resv_normalized(st, &pods[p], c.feasible, nf, norm);
     /* (upstream) prioritizeNodes: sum of score x weight; selectHost: max,
@@ -555,7 +607,8 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
     for (int32_t j = 0; j < nf; j++) {
       int32_t i = c.feasible[j];
       int64_t t = cfg->plugin_weight[0] * c.plugin_scores[j] + cfg->plugin_weight[1] * c.plugin_scores[(size_t)nf + j] +
-                  cfg->plugin_weight[2] * c.plugin_scores[2 * (size_t)nf + j];
+                  cfg->plugin_weight[2] * c.plugin_scores[2 * (size_t)nf + j] +
+                  cfg->plugin_weight[3] * c.plugin_scores[3 * (size_t)nf + j];
       if (rs) t += (int64_t)cfg->reservation_weight * norm[j];
       if (t > best || (t == best && i < best_node)) {
         best = t;

@@ -66,6 +66,12 @@ int orc_fit_filter(const koordhip_config *cfg, const orc_state *st, const koordh
 int64_t orc_fit_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 int orc_la_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 int64_t orc_la_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
+/* upstream static node filters (host-resolved static_allow lookup) and
+ * NodeResourcesBalancedAllocation (k8s v1.24.15, parity unpinned) */
+int orc_static_filter(const orc_state *st, const koordhip_pod *pod, int32_t node);
+int64_t orc_bal_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
+/* the KOORDHIP_PLUGIN_* bit of plugin_weight[p] / score plane p */
+uint32_t orc_score_plugin_bit(int p);
 
 /* NodeNUMAResource (numa_oracle.c). */
 int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);

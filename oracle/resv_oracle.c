@@ -217,7 +217,7 @@ int64_t orc_resv_rank_total(const koordhip_config *cfg, const orc_state *st, con
                             int64_t b) {
   int64_t bmax = 0;
   for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
-    if (cfg->score_plugins & (1u << p)) bmax += 100 * cfg->plugin_weight[p];
+    if (cfg->score_plugins & orc_score_plugin_bit(p)) bmax += 100 * cfg->plugin_weight[p];
   if (!(cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION)) return b;
   int matched, unmatched;
   orc_resv_classify(st, pod, i, &matched, &unmatched);

@@ -1,0 +1,166 @@
+"""Upstream default-profile plugins on the host and in the
+oracle: the static node filters (NodeUnschedulable, NodeAffinity,
+TaintToleration) resolved into static_allow, and
+NodeResourcesBalancedAllocation.
+
+The upstream sources (k8s v1.24.15) are not in the container: the rules are
+restated from the published plugins and the vectors below are worked from
+those rules (the BalancedAllocation ones are the worked examples of upstream
+balanced_allocation_test.go's "resources requested" case) -- parity with the
+reference's own tests is unpinned."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+from koordinator_amd import abi, synth
+from koordinator_amd.config import (PLUGIN_BALANCED, STATIC_FILTERS, ArgsError, shipped_profile, to_c_config,
+                                    with_upstream)
+from koordinator_amd.nodefilters import (NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, NodeStatic, PodStatic,
+                                         StaticClasses, Taint, Toleration, node_affinity_ok, node_static_ok,
+                                         node_unschedulable_ok, static_allow, taint_toleration_ok)
+from koordinator_amd.reservation import NodeSelectorRequirement as R, NodeSelectorTerm as T
+from koordinator_amd.snapshot import NodeTable, pod_array
+
+
+# ------------------------------------------------------------ tolerations
+@pytest.mark.parametrize("tol,taint,want", [
+    (Toleration("k", "Equal", "v", NO_SCHEDULE), Taint("k", "v", NO_SCHEDULE), True),
+    (Toleration("k", "", "v", NO_SCHEDULE), Taint("k", "v", NO_SCHEDULE), True),     # "" = Equal
+    (Toleration("k", "Equal", "w", NO_SCHEDULE), Taint("k", "v", NO_SCHEDULE), False),
+    (Toleration("k", "Exists", "", NO_SCHEDULE), Taint("k", "v", NO_SCHEDULE), True),
+    (Toleration("k", "Exists", "", NO_EXECUTE), Taint("k", "v", NO_SCHEDULE), False),  # effect differs
+    (Toleration("k", "Exists", "", ""), Taint("k", "v", NO_EXECUTE), True),           # every effect
+    (Toleration("", "Exists", "", ""), Taint("any", "x", NO_SCHEDULE), True),         # tolerates everything
+    (Toleration("", "Equal", "", ""), Taint("any", "", NO_SCHEDULE), True),           # empty key, Equal "" == ""
+    (Toleration("j", "Exists"), Taint("k", "v", NO_SCHEDULE), False),
+    (Toleration("k", "Bogus", "v"), Taint("k", "v", NO_SCHEDULE), False),
+])
+def test_toleration_tolerates_taint(tol, taint, want):
+    assert tol.tolerates(taint) is want
+
+
+def test_taint_toleration_filter_effects():
+    node = NodeStatic(taints=[Taint("a", "1", NO_SCHEDULE), Taint("b", "", PREFER_NO_SCHEDULE)])
+    assert not taint_toleration_ok(PodStatic(), node)
+    assert taint_toleration_ok(PodStatic(tolerations=[Toleration("a", "Equal", "1")]), node)  # PreferNoSchedule ignored
+    node2 = NodeStatic(taints=[Taint("m", "", NO_EXECUTE)])
+    assert not taint_toleration_ok(PodStatic(tolerations=[Toleration("m", "Exists", "", NO_SCHEDULE)]), node2)
+    assert taint_toleration_ok(PodStatic(tolerations=[Toleration("m", "Exists", "", NO_EXECUTE)]), node2)
+
+
+def test_node_unschedulable_filter():
+    cordoned = NodeStatic(unschedulable=True)
+    assert node_unschedulable_ok(PodStatic(), NodeStatic())
+    assert not node_unschedulable_ok(PodStatic(), cordoned)
+    tol = Toleration("node.kubernetes.io/unschedulable", "Exists", "", NO_SCHEDULE)
+    assert node_unschedulable_ok(PodStatic(tolerations=[tol]), cordoned)
+    assert node_unschedulable_ok(PodStatic(tolerations=[Toleration(operator="Exists")]), cordoned)
+    assert not node_unschedulable_ok(PodStatic(tolerations=[Toleration("node.kubernetes.io/unschedulable", "Exists",
+                                                                        "", NO_EXECUTE)]), cordoned)
+
+
+@pytest.mark.parametrize("pod,labels,name,want", [
+    (PodStatic(node_selector={"a": "1"}), {"a": "1", "b": "2"}, "n", True),
+    (PodStatic(node_selector={"a": "1", "c": "3"}), {"a": "1"}, "n", False),
+    (PodStatic(required_terms=[T([R("a", "In", ["1", "2"])])]), {"a": "2"}, "n", True),
+    (PodStatic(required_terms=[T([R("a", "NotIn", ["1"])])]), {}, "n", True),            # absent key passes NotIn
+    (PodStatic(required_terms=[T([R("a", "Exists")]), T([R("b", "Exists")])]), {"b": ""}, "n", True),  # ORed terms
+    (PodStatic(required_terms=[T([R("a", "Exists"), R("b", "Exists")])]), {"b": ""}, "n", False),      # ANDed parts
+    (PodStatic(required_terms=[T([R("g", "Gt", ["3"])])]), {"g": "4"}, "n", True),
+    (PodStatic(required_terms=[T([R("g", "Gt", ["3"])])]), {"g": "x"}, "n", False),     # not an integer
+    (PodStatic(required_terms=[T([R("g", "Lt", ["3"])])]), {"g": "3"}, "n", False),
+    (PodStatic(required_terms=[T([], [R("metadata.name", "In", ["n"])])]), {}, "n", True),
+    (PodStatic(required_terms=[T([], [R("metadata.name", "NotIn", ["n"])])]), {}, "n", False),
+    (PodStatic(required_terms=[T()]), {"a": "1"}, "n", False),                            # empty term: no match
+    (PodStatic(required_terms=[]), {"a": "1"}, "n", False),                               # no terms: no node
+    (PodStatic(required_terms=[T([R("a", "DoesNotExist")])], node_selector={"b": "1"}), {"b": "1"}, "n", True),
+])
+def test_node_affinity_required(pod, labels, name, want):
+    assert node_affinity_ok(pod, NodeStatic(labels=labels, name=name)) is want
+
+
+def test_static_allow_matches_direct_checks():
+    n = 600
+    prof = with_upstream(shipped_profile())
+    t = synth.make_cluster(synth.ClusterSpec(n), prof)
+    pods = synth.make_pods(synth.StreamSpec(400, be_frac=0.3), prof)
+    nodes, cls = synth.add_static(t, pods, synth.StaticSpec(), prof)
+    assert len(cls.specs) == len(synth.static_templates())
+    for i in range(n):
+        for c, spec in enumerate(cls.specs):
+            assert bool((int(t["static_allow"][i]) >> c) & 1) == node_static_ok(spec, nodes[i], STATIC_FILTERS)
+    # some class is filtered somewhere, none everywhere except the empty-terms one
+    assert (t["static_allow"] != 0xFFFFFFFF).any()
+    # a subset of the filters: only TaintToleration
+    m = static_allow(nodes, cls, ["TaintToleration"])
+    for i in range(0, n, 7):
+        for c, spec in enumerate(cls.specs):
+            assert bool((int(m[i]) >> c) & 1) == taint_toleration_ok(spec, nodes[i])
+
+
+def test_static_class_limit():
+    cls = StaticClasses()
+    for j in range(abi.MAX_STATIC_CLASSES):
+        cls.classify(PodStatic(node_selector={"k": str(j)}))
+    assert cls.classify(PodStatic(node_selector={"k": "0"})) == 0   # an existing class
+    with pytest.raises(ValueError):
+        cls.classify(PodStatic(node_selector={"k": "new"}))
+
+
+def test_static_score_rejected():
+    p = with_upstream(shipped_profile())
+    p.scores = dict(p.scores)
+    p.scores["TaintToleration"] = 1
+    with pytest.raises(ArgsError):
+        to_c_config(p)
+
+
+# ------------------------------------------------------- BalancedAllocation
+def _one_node(cpu, mem, rcpu, rmem):
+    t = NodeTable.empty(1)
+    t["alloc0"][0], t["alloc1"][0] = cpu, mem
+    t["requested0"][0], t["requested1"][0] = rcpu, rmem
+    t["alloc_pods"][0] = 110
+    return t
+
+
+@pytest.mark.parametrize("node,req,want", [
+    # upstream balanced_allocation_test.go worked examples ("resources requested"):
+    ((4000, 10000, 0, 0), (3000, 5000), 87),    # fractions 0.75 / 0.5: std 0.125
+    ((6000, 10000, 0, 0), (3000, 5000), 100),   # 0.5 / 0.5
+    # worked from the same rules
+    ((4000, 8000, 1000, 6000), (2000, 1000), 93),   # 0.75 / 0.875: std 0.0625, 93.75 truncated
+    ((4000, 8000, 5000, 0), (0, 0), 50),        # cpu fraction capped at 1, mem 0: std 0.5
+    ((4000, 0, 1000, 0), (1000, 0), 100),       # memory Allocatable 0: one fraction, std 0
+    ((0, 0, 0, 0), (0, 0), 100),
+])
+def test_balanced_allocation_oracle(node, req, want):
+    t = _one_node(*node)
+    p = pod_array(1)
+    p["req"][0, 0], p["req"][0, 1] = req
+    prof = shipped_profile()
+    prof.scores = {PLUGIN_BALANCED: 1}
+    cfg = to_c_config(prof)
+    o = oracle.Oracle(cfg, t)
+    got = o.eval(p, status=False, scores=True)["scores"][0, 3, 0]
+    fc = min(1.0, (node[2] + req[0]) / node[0]) if node[0] else None
+    fm = min(1.0, (node[3] + req[1]) / node[1]) if node[1] else None
+    fr = [f for f in (fc, fm) if f is not None]
+    std = abs((fr[0] - fr[1]) / 2) if len(fr) == 2 else 0.0
+    assert got == int((1 - std) * 100) == want
+
+
+def test_oracle_static_status_bit():
+    prof = with_upstream(shipped_profile(), balanced_weight=5)
+    t = synth.make_cluster(synth.ClusterSpec(300), prof)
+    pods = synth.make_pods(synth.StreamSpec(60, be_frac=0.3), prof)
+    nodes, cls = synth.add_static(t, pods, synth.StaticSpec(), prof)
+    r = oracle.Oracle(to_c_config(prof), t).eval(pods, k=4)
+    for j in range(len(pods)):
+        spec = cls.specs[int(pods["static_class"][j])]
+        for i in range(0, 300, 5):
+            fail = bool(r["status"][j, i] & abi.ST_STATIC_FAIL)
+            assert fail == (not node_static_ok(spec, nodes[i], STATIC_FILTERS))
+    assert (r["scores"][:, 3, :] > 0).all()
