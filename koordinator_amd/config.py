@@ -206,8 +206,12 @@ def to_c_config(profile: Profile, device: int = -1):
         p.numa.validate()
     cfg = KoordhipConfig()
     cfg.abi_version = KOORDHIP_ABI_VERSION
-    cfg.filter_plugins = sum(PLUGIN_BITS[x] for x in set(p.filters))
-    cfg.score_plugins = sum(PLUGIN_BITS[x] for x in p.scores)
+    cfg.filter_plugins = 0
+    for x in p.filters:  # (the three static filters share one bit)
+        cfg.filter_plugins |= PLUGIN_BITS[x]
+    cfg.score_plugins = 0
+    for x in p.scores:
+        cfg.score_plugins |= PLUGIN_BITS[x]
     cfg.device = device
     for name in p.scores:
         if name in STATIC_FILTERS:

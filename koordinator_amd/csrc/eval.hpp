@@ -189,7 +189,7 @@ __device__ __forceinline__ void need_or(Need &a, const Need &b) {
 }
 
 __device__ __forceinline__ Need need_all(const DevCfg &c) {
-  Need n;
+  Need n{};
   n.pods = n.r_cpu = n.r_mem = n.eph = n.bcpu = n.bmem = n.a_cpu = n.a_mem = n.nz_cpu = n.nz_mem = true;
   n.la = true;
   n.la_nonprod = true;

@@ -537,11 +537,11 @@ __device__ __forceinline__ uint32_t need_pack(const Need &n) {
          (uint32_t)n.bcpu << 4 | (uint32_t)n.bmem << 5 | (uint32_t)n.a_cpu << 6 | (uint32_t)n.a_mem << 7 |
          (uint32_t)n.nz_cpu << 8 | (uint32_t)n.nz_mem << 9 | (uint32_t)n.la << 10 | (uint32_t)n.la_nonprod << 11 |
          (uint32_t)n.la_prod << 12 | (uint32_t)n.numa << 13 | (uint32_t)n.numa_masks << 14 | (uint32_t)n.zones << 15 |
-         (uint32_t)n.amp << 16 | (uint32_t)n.resv << 17;
+         (uint32_t)n.amp << 16 | (uint32_t)n.resv << 17 | (uint32_t)n.sa << 18;
 }
 __device__ __forceinline__ Need need_unpack(uint32_t b) {
   b = __builtin_amdgcn_readfirstlane(b);
-  Need n;
+  Need n{};
   n.pods = b & 1;
   n.r_cpu = (b >> 1) & 1;
   n.r_mem = (b >> 2) & 1;
@@ -560,6 +560,7 @@ __device__ __forceinline__ Need need_unpack(uint32_t b) {
   n.zones = (b >> 15) & 1;
   n.amp = (b >> 16) & 1;
   n.resv = (b >> 17) & 1;
+  n.sa = (b >> 18) & 1;
   return n;
 }
 // OR over the wave (DPP within rows, then the row broadcasts), result in every lane
