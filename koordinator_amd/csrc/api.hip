@@ -1498,8 +1498,8 @@ int place_staged_impl(koordhip_ctx *c) {
   c->last_launches = 0;
   c->last_evals = 0;
   if (std::getenv("KOORDHIP_STAMPS")) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 48 * sizeof(uint64_t)));
-    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 48 * sizeof(uint64_t), c->stream));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 64 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 64 * sizeof(uint64_t), c->stream));
   }
   int32_t *mbuf = c->d_mod;  // M' handed between resolve launches
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
@@ -1597,7 +1597,7 @@ int place_staged_impl(koordhip_ctx *c) {
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   c->pipe_check = true;
   if (c->d_dbg) {
-    uint64_t h[48];
+    uint64_t h[64];
     HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     std::fprintf(stderr,
@@ -1632,6 +1632,11 @@ int place_staged_impl(koordhip_ctx *c) {
     std::fprintf(stderr, "[koordhip stamps] general path detail: candidate + table keys %llu  row evaluations %llu | "
                  "pods served by the key tables %llu\n",
                  (unsigned long long)h[22], (unsigned long long)h[23], (unsigned long long)h[24]);
+    std::fprintf(stderr, "[koordhip stamps] prologue phases: walk %llu  winner rows %llu (HBM loads %llu)  conflicts %llu | "
+                 "general-path causes: staged conflict %llu  slow %llu  voided by a general commit %llu\n",
+                 (unsigned long long)h[48], (unsigned long long)h[49], (unsigned long long)h[51],
+                 (unsigned long long)h[50], (unsigned long long)h[52], (unsigned long long)h[53],
+                 (unsigned long long)h[54]);
   }
   return 0;
 }

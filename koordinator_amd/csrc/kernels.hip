@@ -2049,6 +2049,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t n_slow = 0, n_miss = 0, n_staged = 0, n_bulk = 0, n_tab = 0;
   uint64_t c_g[2] = {0, 0};  // general path: candidate from the list, row evaluations (to the last value)
   uint64_t c_nx[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // NUMA: accumulator replays {full, spread} and row passes {req. spread, other}: cycles, count
+  // prologue phases 1 / 2 / 2b (cycles), phase-2 HBM row loads, general-path causes: conflicts, slow, voided by a general commit
+  uint64_t c_p[3] = {0, 0, 0}, n_p2 = 0, n_conf = 0, n_slowc = 0, n_void = 0;
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
   // Every loop keeps several global loads in flight per thread before its LDS
@@ -2259,6 +2261,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       }
     }
     __syncthreads();
+    const uint64_t t_p1 = (dbg && t == 0) ? stamp() : 0;
     // ---- 2. the staged winner's row: an M' slot (src < 0), a list-head
     //         prefetch slot, or one HBM load into the pod's first head slot
     for (int32_t l = t; l < n_pods; l += RES_THREADS) {
@@ -2275,6 +2278,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             if (pre_node[l * HP + q] == w) ps = l * HP + q;
           if (ps < 0) {
             ps = l * HP;
+            if (dbg) n_p2++;
             NV v;
             load_row(v, nodes(), w);
             pre[ps] = v;
@@ -2321,6 +2325,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       }
     }
     __syncthreads();
+    const uint64_t t_p2 = (dbg && t == 0) ? stamp() : 0;
     // ---- 2b. conflicts among the staged decisions (one walked entry per
     //          thread): pod l's walk met the staged winner of an earlier pod
     for (int32_t x = t; x < n_pods * RES_WE; x += RES_THREADS) {
@@ -2341,9 +2346,13 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     }
     __syncthreads();
     if (dbg && t == 0) {
+      const uint64_t t_p3 = stamp();
       c_hash += t_a - t_entry;
-      c_pro += stamp() - t_a;
+      c_pro += t_p3 - t_a;
       c_wait += t_entry - t_w0;
+      c_p[0] += t_p1 - t_a;
+      c_p[1] += t_p2 - t_p1;
+      c_p[2] += t_p3 - t_p2;
     }
     if (t < 64) {  // ---- 3. the sequential greedy over the round (wave 0)
       __builtin_amdgcn_s_setprio(3);
@@ -2374,6 +2383,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       uint64_t ok = __ballot(live && !slow && !conflict);  // staged decisions still valid
       uint64_t cstaged = 0;                                 // pods committed with their staged decision
       const uint64_t slowmask = __ballot(live && slow);
+      if (dbg) {
+        n_conf += __popcll(__ballot(live && !slow && conflict));
+        n_slowc += __popcll(slowmask);
+      }
       int32_t j = 0;
       if (dbg) c_l[0] += stamp() - t_loop;
       while (j < n_pods) {
@@ -2631,7 +2644,9 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             bool met = false;
 #pragma unroll
             for (int q = 0; q < RES_WE; q++) met = met || se[q] == w;
-            ok &= ~__ballot(lane > g && met);
+            const uint64_t voided = __ballot(lane > g && met);
+            if (dbg) n_void += __popcll(ok & voided);
+            ok &= ~voided;
           }
         }
         if (lane == 0) out_node[p0 + g] = result;
@@ -2801,6 +2816,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     }
   }
   if (t <= RES_MAXP_ROUND && t <= sh_mp) mbuf[t] = t == 0 ? sh_mp : pnode[t - 1];  // hand M' on
+  if (dbg && n_p2) atomicAdd((unsigned long long *)&dbg[51], (unsigned long long)n_p2);
   if (dbg && t == 64) {
     atomicAdd((unsigned long long *)&dbg[27], (unsigned long long)c_w1wait);
     atomicAdd((unsigned long long *)&dbg[28], (unsigned long long)c_w1load);
@@ -2824,6 +2840,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[22], (unsigned long long)c_g[0]);
     atomicAdd((unsigned long long *)&dbg[24], (unsigned long long)n_tab);
     atomicAdd((unsigned long long *)&dbg[23], (unsigned long long)c_g[1]);
+    for (int q = 0; q < 3; q++) atomicAdd((unsigned long long *)&dbg[48 + q], (unsigned long long)c_p[q]);
+    atomicAdd((unsigned long long *)&dbg[52], (unsigned long long)n_conf);
+    atomicAdd((unsigned long long *)&dbg[53], (unsigned long long)n_slowc);
+    atomicAdd((unsigned long long *)&dbg[54], (unsigned long long)n_void);
   }
 }
 
