@@ -125,7 +125,7 @@ struct koordhip_ctx {
   uint32_t *d_selcnt[2] = {nullptr, nullptr};
   int32_t sel_g = kh::kSelGMax;   // workgroups per pod of k_select_split (KOORDHIP_SEL_G)
   int32_t n_cu = 256;             // device CU count
-  bool cu_reserve = false;        // KOORDHIP_CU_RESERVE: CU-masked streams, CU 0 for the resolve
+  uint32_t cu_reserve = 0;        // KOORDHIP_CU_RESERVE: CUs (mask word 0) of the resolve alone, 0 = shared
   bool sel_split = true;          // the list producer counts pods into the pipeline (k_eval_topk / k_select_split);
                                   // false (KOORDHIP_SELECT_ONEWG): k_select + signal kernel
   bool eval_fused = true;         // k_eval_topk (no score matrix); false (KOORDHIP_EVAL_SPLIT): k_scan + select
@@ -801,12 +801,13 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     c->sel_g = std::max(1, std::min(kh::kSelGMax, cus / c->batch));
     if (const char *g = std::getenv("KOORDHIP_SEL_G")) c->sel_g = std::max(1, std::min(kh::kSelGMax, std::atoi(g)));
   }
-  c->cu_reserve = std::getenv("KOORDHIP_CU_RESERVE") != nullptr;
+  // KOORDHIP_CU_RESERVE=<mask>: the persistent resolve gets the CUs of bit
+  // mask <mask> (word 0 of the stream CU mask; "1" = CU 0) to itself, the
+  // evaluation streams run on every other CU
+  if (const char *r = std::getenv("KOORDHIP_CU_RESERVE")) c->cu_reserve = (uint32_t)std::strtoul(r, nullptr, 0);
   if (c->cu_reserve && e == hipSuccess) {
-    // the persistent resolve gets CU 0 to itself: the evaluation stream runs on
-    // every other CU (its workgroups no longer share the resolve wave's CU)
     std::vector<uint32_t> m((size_t)(c->n_cu + 31) / 32, 0xffffffffu);
-    m[0] &= ~1u;
+    m[0] &= ~c->cu_reserve;
     if (c->n_cu % 32) m.back() &= (1u << (c->n_cu % 32)) - 1u;
     e = hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)m.size(), m.data());
   } else if (e == hipSuccess && !std::getenv("KOORDHIP_POOLED_STREAM")) {
@@ -1454,7 +1455,7 @@ int place_staged_impl(koordhip_ctx *c) {
     // GPU_MAX_HW_QUEUES queues, and an evaluation stream sharing the resolve's
     // queue would wait behind it forever).  KOORDHIP_CU_RESERVE: CU 0 only.
     if (c->cu_reserve) {
-      const uint32_t m0 = 1u;
+      const uint32_t m0 = c->cu_reserve;
       HIP_TRY(hipExtStreamCreateWithCUMask(&c->rstream, 1, &m0));
     } else {
       const std::vector<uint32_t> all = full_cu_mask(c);
@@ -1527,7 +1528,7 @@ int place_staged_impl(koordhip_ctx *c) {
   uint64_t *cpus = c->d_cpus;
   if (two && !c->stream2) {
     std::vector<uint32_t> m = full_cu_mask(c);  // its own queue too (see rstream)
-    if (c->cu_reserve) m[0] &= ~1u;
+    if (c->cu_reserve) m[0] &= ~c->cu_reserve;
     HIP_TRY(hipExtStreamCreateWithCUMask(&c->stream2, (uint32_t)m.size(), m.data()));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_eval2, hipEventDisableTiming));
   }

@@ -1734,7 +1734,6 @@ constexpr int res_threads() { return NM ? 256 : 512; }
 constexpr int RES_PRE = 128;    // prefetched rows of list heads (RES_PRE / round size per pod)
 constexpr int RES_HASH = 256;   // node -> M' slot (open addressing)
 constexpr int RES_WE = 8;       // list entries the prologue walks per pod
-constexpr int RES_MHASH = 128;  // M node -> slot hash (|M| <= RES_MAXP_ROUND / 2 with lag 2, P otherwise)
 constexpr int RES_LDS_MAX = 160 * 1024 - 3 * 1024;  // dynamic LDS cap (static LDS: M' nodes, hashes, flags)
 
 // An NV row as 8-byte words (the lane-parallel Reserve): words 0-4 a[], 5-9
@@ -1816,8 +1815,8 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * 4;
   o.moved = at;  // per M' slot: committed to again this round (its row moved into M)
   at += RES_MAXP_ROUND * 4;
-  o.mhash = at;  // M node -> M slot (open addressing, RES_MHASH keys then slots)
-  at += 2 * RES_MHASH * 4;
+  o.mhash = at;  // lazy staged rows: the pod of each M slot, the M slot of each pod
+  at += 2 * RES_MAXP_ROUND * 4;
   o.gbits = at;  // the nodes general-path pods committed to this round
   at += bitmap;
   // helper waves' key tables, per pod l (total + 1 as u16 / u32, 0 = infeasible):
@@ -1950,8 +1949,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   int32_t *dec_e = reinterpret_cast<int32_t *>(lds + ofs.dec_e);
   int32_t *dec_c = reinterpret_cast<int32_t *>(lds + ofs.dec_c);
   int32_t *moved = reinterpret_cast<int32_t *>(lds + ofs.moved);
-  int32_t *mkey = reinterpret_cast<int32_t *>(lds + ofs.mhash);
-  int32_t *mval = mkey + RES_MHASH;
+  // lazy staged rows: the pod a bulk commit put in M slot s (its row =
+  // that pod's staged source row + its Reserve delta until materialised),
+  // and the M slot each staged pod committed to
+  int32_t *seg_p = reinterpret_cast<int32_t *>(lds + ofs.mhash);
   uint32_t *gbits = reinterpret_cast<uint32_t *>(lds + ofs.gbits);
   char *kpre = lds + (ofs.kpre >= 0 ? ofs.kpre : 0);
   char *ktab = lds + (ofs.ktab >= 0 ? ofs.ktab : 0);
@@ -2004,7 +2005,6 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     moved[x] = 0;
     ready[x] = 0;
   }
-  for (int32_t x = t; x < RES_MHASH; x += RES_THREADS) mkey[x] = -1;
   for (int32_t x = t; x < RES_HASH; x += RES_THREADS) {
     ckey[x] = -1;
     cval[x] = 64;
@@ -2037,11 +2037,15 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   // wave 0: lane s < |M| holds the node of M slot s (its row is mrow[s] in LDS);
   // lane q < RES_WORDS owns word q of a row in the lane-parallel Reserve
   int32_t my_node = -1;
-  int32_t doff = -1;  // byte offset in DevPod of word q's Reserve delta (apply_delta)
-  if (lane >= 5 && lane < 10) doff = (lane - 5) * 8;                     // r[] += req[]
-  if (lane == 10 || lane == 11) doff = (int32_t)offsetof(DevPod, nz_cpu_m) + (lane - 10) * 8;
-  if (lane == 14 || lane == 16) doff = (int32_t)offsetof(DevPod, est_cpu);  // la_u / la_up (prod)
-  if (lane == 15 || lane == 17) doff = (int32_t)offsetof(DevPod, est_mem);
+  // byte offset in DevPod of word q's Reserve delta (apply_delta), -1: none
+  auto word_doff = [](int q) -> int32_t {
+    if (q >= 5 && q < 10) return (q - 5) * 8;  // r[] += req[]
+    if (q == 10 || q == 11) return (int32_t)offsetof(DevPod, nz_cpu_m) + (q - 10) * 8;
+    if (q == 14 || q == 16) return (int32_t)offsetof(DevPod, est_cpu);  // la_u / la_up (prod)
+    if (q == 15 || q == 17) return (int32_t)offsetof(DevPod, est_mem);
+    return -1;
+  };
+  const int32_t doff = word_doff(lane);
   // diagnostics (KOORDHIP_STAMPS): cycles and counts per phase
   uint64_t c_pro = 0, c_wait = 0, c_loop = 0, c_rel = 0, c_hash = 0, c_wb = 0;
   uint64_t c_w1wait = 0, c_w1load = 0, c_bar = 0;  // wave 1: waiting for the next lists, loading them; wave 0: end-of-round barrier
@@ -2121,14 +2125,17 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       const uint4 *src = reinterpret_cast<const uint4 *>(pods + rp0);
       uint4 *dst = reinterpret_cast<uint4 *>(Lp);
       const int32_t p16 = rn * (int32_t)(sizeof(DevPod) / 16);
-      for (int32_t x0 = tid; x0 < p16; x0 += 8 * nth) {
-        uint4 pv[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-          if (x0 + u * nth < p16) pv[u] = src[x0 + u * nth];
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-          if (x0 + u * nth < p16) dst[x0 + u * nth] = pv[u];
+      // four loads in flight per thread, named (an array here went to scratch)
+      for (int32_t x0 = tid; x0 < p16; x0 += 4 * nth) {
+        const int32_t x1 = x0 + nth, x2 = x0 + 2 * nth, x3 = x0 + 3 * nth;
+        const uint4 a0 = src[x0];
+        const uint4 a1 = x1 < p16 ? src[x1] : a0;
+        const uint4 a2 = x2 < p16 ? src[x2] : a0;
+        const uint4 a3 = x3 < p16 ? src[x3] : a0;
+        dst[x0] = a0;
+        if (x1 < p16) dst[x1] = a1;
+        if (x2 < p16) dst[x2] = a2;
+        if (x3 < p16) dst[x3] = a3;
       }
     }
 #pragma unroll
@@ -2164,21 +2171,6 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       }
       Pnode[sl] = n1;
     }
-  };
-  // M slot of node nd, -1 when nd is not in M
-  auto m_slot = [&](int32_t nd) -> int32_t {
-    uint32_t h = res_hash(nd) & (RES_MHASH - 1);
-    for (;;) {
-      const int32_t x = mkey[h];
-      if (x == nd) return mval[h];
-      if (x < 0) return -1;
-      h = (h + 1) & (RES_MHASH - 1);
-    }
-  };
-  auto m_insert = [&](int32_t nd, int32_t slot) {
-    uint32_t h = res_hash(nd) & (RES_MHASH - 1);
-    while (atomicCAS(&mkey[h], -1, nd) != -1) h = (h + 1) & (RES_MHASH - 1);
-    mval[h] = slot;
   };
   auto prev_slot = [&](int32_t nd) -> int32_t {
     uint32_t h = res_hash(nd);
@@ -2382,11 +2374,53 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       const bool conflict = (dc & 1) != 0;
       uint64_t ok = __ballot(live && !slow && !conflict);  // staged decisions still valid
       uint64_t cstaged = 0;                                 // pods committed with their staged decision
+      // Lazy staged rows: a bulk commit only records (slot, pod); the row is
+      // materialised when a general commit hits it, before a non-monotone
+      // pass over all M rows, and at the write-back.  my_node (node of slot
+      // lane s) is valid for the slots of gvalid (general commits and
+      // materialised slots); lane l of a staged pod holds its slot (pslot_r).
+      uint64_t lazy = 0, gvalid = 0;
+      int32_t pslot_r = -1;
       const uint64_t slowmask = __ballot(live && slow);
       if (dbg) {
         n_conf += __popcll(__ballot(live && !slow && conflict));
         n_slowc += __popcll(slowmask);
       }
+      // materialise lazy slot s (uniform): its staged pod's source row + Reserve
+      // delta, word-parallel (over-commit flags left to slot_row), and its side row
+      auto materialize = [&](int32_t s) {
+        const int32_t pi = seg_p[s];
+        const int32_t src = dec_src[pi];
+        const int32_t nd = seg_w[s];
+        if (lane < RES_WORDS) {
+          const uint64_t *srow = reinterpret_cast<const uint64_t *>(src >= 0 ? &pre[src] : &prow[-src - 1]);
+          uint64_t x = srow[lane];
+          if (doff >= 0 && (lane < 16 || ((prodmask >> pi) & 1ull))) {
+            const double dq = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(&lpod[pi]) + doff);
+            x = (uint64_t)__double_as_longlong(__longlong_as_double((long long)x) + dq);
+          }
+          if (lane == 18) x += 1ull << 32;
+          reinterpret_cast<uint64_t *>(&mrow[s])[lane] = x;
+        }
+        if constexpr (NUMA) {
+          constexpr int NRW = (int)(sizeof(NR) / 8);
+          const uint64_t *sn = reinterpret_cast<const uint64_t *>(src >= 0 ? &prenr[src] : &pnr[-src - 1]);
+          for (int32_t w = lane; w < NRW; w += 64) reinterpret_cast<uint64_t *>(&mnr[s])[w] = sn[w];
+        }
+        if (lane == s) my_node = nd;
+        lazy &= ~(1ull << s);
+        gvalid |= 1ull << s;
+      };
+      // the first pod whose staged winner is node y (64: none)
+      auto claimer = [&](int32_t y) -> int32_t {
+        uint32_t q = res_hash(y);
+        for (;;) {
+          const int32_t xk = ckey[q];
+          if (xk == y) return cval[q];
+          if (xk < 0) return 64;
+          q = (q + 1) & (RES_HASH - 1);
+        }
+      };
       int32_t j = 0;
       if (dbg) c_l[0] += stamp() - t_loop;
       while (j < n_pods) {
@@ -2409,16 +2443,11 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           const uint64_t cb = __ballot(com);
           const int32_t slot = nm + __popcll(cb & ((1ull << lane) - 1ull));
           if (com) {
-            const NV *srow = ssrc >= 0 ? &pre[ssrc] : &prow[-ssrc - 1];
-            NV v = *srow;
-            const DevPod pod = lpod[lane];
-            apply_delta(v, pod, +1);
-            mrow[slot] = v;
-            if constexpr (NUMA) mnr[slot] = ssrc >= 0 ? prenr[ssrc] : pnr[-ssrc - 1];
             if (ssrc < 0) moved[-ssrc - 1] = 1;
-            m_insert(sw, slot);
             atomicOr(&modmap[sw >> 5], 1u << (sw & 31));
             seg_w[slot] = sw;
+            seg_p[slot] = lane;
+            pslot_r = slot;
           }
           if (mine) {
             out_node[p0 + lane] = com ? sw : KOORDHIP_UNSCHEDULABLE;
@@ -2428,7 +2457,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             }
           }
           const int32_t nc = __popcll(cb);
-          if (lane >= nm && lane < nm + nc) my_node = seg_w[lane];
+          lazy |= (nc >= 64 ? ~0ull : ((1ull << nc) - 1ull)) << nm;
           nm += nc;
           cstaged |= cb;
           n_staged += g - j;
@@ -2446,83 +2475,78 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         const bool x1 = e1 != 0 && xbit(modmap, key_node(e1));
         const uint64_t f0 = __ballot(e0 != 0 && !x0), f1 = __ballot(e1 != 0 && !x1);
         uint64_t best = f0 ? readlane_u64(e0, __builtin_ctzll(f0)) : (f1 ? readlane_u64(e1, __builtin_ctzll(f1)) : 0ull);
-        // Monotone pod whose key tables the helper waves have finished: only
-        // the X entries ranked above c can win, and their current keys are
-        // table entries unless a general-path pod changed their row.
-        bool tables = have_tables && monotone && !((slowmask >> g) & 1ull) &&
-                      __hip_atomic_load(&ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-        if (tables) {
+        // A monotone pod: only the X entries ranked above c can win.  Each one's
+        // current key: from the helper waves' key tables when they are ready
+        // (kpre: the row its staged claimer committed to; ktab: an M' row no
+        // commit touched), else one evaluation on its current row -- a
+        // materialised M slot (a general commit changed it), its staged
+        // claimer's lazy row, or its M' row.
+        const bool mono_g = monotone && !((slowmask >> g) & 1ull);
+        if (mono_g) {
+          const bool tabs = have_tables && __hip_atomic_load(&ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
           const int first = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
-          bool need = false;
-          uint64_t kv = 0;
+          bool used = false;
 #pragma unroll
           for (int h = 0; h < 2; h++) {
             const uint64_t e = h ? e1 : e0;
-            const bool xh = h ? x1 : x0;
-            if (xh && 64 * h + lane < first) {
-              const int32_t y = key_node(e);
-              int32_t i = -1;  // the first staged pod that claimed y
-              uint32_t q = res_hash(y);
-              for (;;) {
-                const int32_t xk = ckey[q];
-                if (xk == y) {
-                  i = cval[q];
-                  break;
+            const bool xh = (h ? x1 : x0) && 64 * h + lane < first;
+            if (__ballot(xh)) {
+              uint64_t kv = 0;
+              if (xh) {
+                const int32_t y = key_node(e);
+                const bool gb = xbit(gbits, y);
+                const int32_t cl = gb ? 64 : claimer(y);
+                const bool st = cl < 64 && ((cstaged >> cl) & 1ull);
+                const int32_t sl = (gb || st || mp == 0) ? -1 : prev_slot(y);
+                bool have = false;
+                if (tabs && !gb) {
+                  if (st) {
+                    kv = ktab_key(kget(kpre, g * RES_MAXP_ROUND + cl), y);
+                    have = true;
+                  } else if (sl >= 0) {
+                    kv = ktab_key(kget(ktab, g * RES_MAXP_ROUND + sl), y);
+                    have = true;
+                  }
                 }
-                if (xk < 0) break;
-                q = (q + 1) & (RES_HASH - 1);
-              }
-              uint64_t k2 = 0;
-              if (i >= 0 && i < 64 && ((cstaged >> i) & 1ull) && !xbit(gbits, y)) {
-                k2 = ktab_key(kget(kpre, g * RES_MAXP_ROUND + i), y);
-              } else {
-                const int32_t sl = mp > 0 ? prev_slot(y) : -1;
-                if (sl >= 0 && !moved[sl]) {
-                  k2 = ktab_key(kget(ktab, g * RES_MAXP_ROUND + sl), y);
-                } else {
-                  need = true;
+                if (!have) {
+                  NV v;
+                  NR nr;
+                  if (gb) {
+                    int32_t ms = 0;
+                    for (uint64_t gm = gvalid; gm; gm &= gm - 1ull) {
+                      const int sx = __builtin_ctzll(gm);
+                      if (__builtin_amdgcn_readlane(my_node, sx) == y) ms = sx;
+                    }
+                    v = slot_row(mrow[ms]);
+                    if constexpr (NUMA) nr = mnr[ms];
+                  } else if (st) {
+                    const int32_t src = dec_src[cl];
+                    v = src >= 0 ? pre[src] : prow[-src - 1];
+                    if constexpr (NUMA) nr = src >= 0 ? prenr[src] : pnr[-src - 1];
+                    apply_delta(v, lpod[cl], +1);
+                  } else {
+                    v = slot_row(prow[sl]);
+                    if constexpr (NUMA) nr = pnr[sl];
+                  }
+                  kv = make_key(eval_row<NM>(pod, v, nr, cls, c), y);
                 }
+                used = used || have;
               }
-              kv = k2 > kv ? k2 : kv;
+              kv = wave_max_u64_dpp(kv);
+              best = kv > best ? kv : best;
             }
           }
-          kv = wave_max_u64_dpp(kv);
-          best = kv > best ? kv : best;
-          tables = __ballot(need) == 0;  // a row a general pod changed: evaluate the M rows
-          n_tab += tables;
+          n_tab += __ballot(used) != 0;
         }
         if (dbg) {
           const uint64_t x = stamp();
           c_g[0] += x - ts;
           ts = x;
         }
-        // a monotone pod without (usable) tables: only the X entries ranked
-        // above c can beat it -- their current rows are M or M' slots
-        const bool mono_g = monotone && !((slowmask >> g) & 1ull);
-        if (!tables && mono_g) {
-          const int first = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const uint64_t e = h ? e1 : e0;
-            const bool xh = (h ? x1 : x0) && 64 * h + lane < first;
-            uint64_t kv = 0;
-            if (__ballot(xh)) {
-              if (xh) {
-                const int32_t y = key_node(e);
-                const int32_t ms = m_slot(y);
-                const int32_t sl = ms >= 0 ? -1 : prev_slot(y);
-                const NV *row = ms >= 0 ? &mrow[ms] : &prow[sl];
-                NR nr;
-                if constexpr (NUMA) nr = ms >= 0 ? mnr[ms] : pnr[sl];
-                kv = make_key(eval_row<NM>(pod, slot_row(*row), nr, cls, c), y);
-              }
-              kv = wave_max_u64_dpp(kv);
-              best = kv > best ? kv : best;
-            }
-          }
-        }
-        const int32_t nrows = (tables || mono_g) ? 0 : nm + mp;
+        const int32_t nrows = mono_g ? 0 : nm + mp;
         const uint64_t t_rows = dbg ? stamp() : 0;
+        if (nrows > 0)  // a pass over every M row: materialise the lazy ones first
+          while (lazy) materialize((int32_t)__builtin_ctzll(lazy));
         for (int32_t b0 = 0; b0 < nrows; b0 += 64) {  // rows: M slots, then the M' slots not moved into M
           const int32_t s = b0 + lane;
           uint64_t kv = 0;
@@ -2552,10 +2576,19 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         int32_t result = KOORDHIP_UNSCHEDULABLE;
         if (best != 0) {
           const int32_t w = key_node(best);
-          const uint64_t hit = __ballot(lane < nm && my_node == w);
-          // w's M slot; its current row: the slot itself, else (new this round)
+          // w's M slot (a staged pod's, materialised now if lazy, or a general
+          // commit's); its current row: the slot itself, else (new this round)
           // a prefetched list-head row, an M' row, or HBM (rare)
-          const int32_t rw = hit ? __builtin_ctzll(hit) : nm;
+          const uint64_t hit_s = __ballot(lane < n_pods && ((cstaged >> lane) & 1ull) && sw == w);
+          int32_t rw = nm;
+          if (hit_s) {
+            rw = __builtin_amdgcn_readlane(pslot_r, __builtin_ctzll(hit_s));
+            if ((lazy >> rw) & 1ull) materialize(rw);
+          } else {
+            const uint64_t hit_g = __ballot(((gvalid >> lane) & 1ull) && my_node == w);
+            if (hit_g) rw = __builtin_ctzll(hit_g);
+          }
+          const bool hit = rw < nm;
           const NV *srow = &mrow[rw];
           const NR *snr = &mnr[rw];
           int32_t from_prev = -1;
@@ -2633,8 +2666,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             if (lane == 0) atomicOr(&gbits[w >> 5], 1u << (w & 31));
             if (!hit) {
               if (lane == rw) my_node = w;
+              gvalid |= 1ull << rw;
               if (lane == 0) {
-                m_insert(w, rw);
                 atomicOr(&modmap[w >> 5], 1u << (w & 31));
                 if (from_prev >= 0) moved[from_prev] = 1;
               }
@@ -2659,7 +2692,17 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       // ---- 4. write M back; M becomes the next round's M' (rows stay in LDS)
       const uint64_t t_wb = dbg ? stamp() : 0;
       if (lane < nm) {
-        const NV v = slot_row(mrow[lane]);
+        NV v;
+        if ((lazy >> lane) & 1ull) {  // a lazy staged row: materialised here
+          const int32_t pi = seg_p[lane];
+          my_node = seg_w[lane];
+          const int32_t src = dec_src[pi];
+          v = src >= 0 ? pre[src] : prow[-src - 1];
+          apply_delta(v, lpod[pi], +1);
+          if constexpr (NUMA) mnr[lane] = src >= 0 ? prenr[src] : pnr[-src - 1];
+        } else {
+          v = slot_row(mrow[lane]);
+        }
         mrow[lane] = v;
 #ifdef KH_PUBLISH_RELEASE
         store_row(v, nodes(), my_node);
@@ -2701,7 +2744,6 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         ckey[x] = -1;
         cval[x] = 64;
       }
-      for (int32_t x = lane; x < RES_MHASH; x += 64) mkey[x] = -1;
       if (lane < nm) {
         atomicOr(&modmap[my_node >> 5], 1u << (my_node & 31));
         pnode[lane] = my_node;
@@ -2755,8 +2797,14 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       // ---- waves 2..: key tables for the general path, pod by pod (one pod
       //      per wave: its record is wave-uniform), lanes over the rows --
       //      kpre[l][i] on staged pod i's committed row, ktab[l][s] on M' row s
+      //      Only the pods whose staged decision conflicts use them (general
+      //      path, monotone): those pods are dealt round-robin to the waves.
       const int hw = __builtin_amdgcn_readfirstlane((t >> 6) - 2), nh = RES_THREADS / 64 - 2;
-      for (int32_t l = 1 + hw; have_tables && l < n_pods; l += nh) {
+      uint64_t todo = __ballot(lane < n_pods && dec_c[lane] == 1);
+      for (int32_t x = 0; x < hw && todo; x++) todo &= todo - 1ull;
+      for (; have_tables && todo;) {
+        const int32_t l = (int32_t)__builtin_ctzll(todo);
+        for (int32_t x = 0; x < nh && todo; x++) todo &= todo - 1ull;
         if (__hip_atomic_load(&sh_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
         const DevPod pod = uniform_pod(lpod[l]);
         for (int32_t b0 = 0; b0 < l + mp; b0 += 64) {
