@@ -1638,6 +1638,9 @@ int place_staged_impl(koordhip_ctx *c) {
                  (unsigned long long)h[48], (unsigned long long)h[49], (unsigned long long)h[51],
                  (unsigned long long)h[50], (unsigned long long)h[52], (unsigned long long)h[53],
                  (unsigned long long)h[54]);
+    std::fprintf(stderr, "[koordhip stamps] general path split: list + X + c %llu cycles | pods with ready key tables %llu | "
+                 "evaluation passes %llu\n",
+                 (unsigned long long)h[55], (unsigned long long)h[56], (unsigned long long)h[57]);
   }
   return 0;
 }

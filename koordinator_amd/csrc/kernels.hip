@@ -1730,6 +1730,10 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
 // (4 for NUMA builds) keep 256 (512) VGPRs available to it.
 template <int NM>
 constexpr int res_threads() { return NM ? 256 : 512; }
+// waves 1 .. RES_LOADERS load the next round while wave 0 resolves this one
+// (the rest build key tables): three of eight, one of four
+template <int NM>
+constexpr int res_loaders() { return res_threads<NM>() >= 512 ? 3 : 1; }
 
 constexpr int RES_PRE = 128;    // prefetched rows of list heads (RES_PRE / round size per pod)
 constexpr int RES_HASH = 256;   // node -> M' slot (open addressing)
@@ -2055,6 +2059,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t c_nx[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // NUMA: accumulator replays {full, spread} and row passes {req. spread, other}: cycles, count
   // prologue phases 1 / 2 / 2b (cycles), phase-2 HBM row loads, general-path causes: conflicts, slow, voided by a general commit
   uint64_t c_p[3] = {0, 0, 0}, n_p2 = 0, n_conf = 0, n_slowc = 0, n_void = 0;
+  uint64_t c_cand = 0, n_evpass = 0, n_tready = 0;  // general path: list + X + c cycles, evaluation passes, pods with ready tables
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
   // Every loop keeps several global loads in flight per thread before its LDS
@@ -2230,92 +2235,88 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       const bool general = f == RES_WE && z == RES_WE;  // RES_WE M' entries in a row
       const bool walked = live && !general && (q < min(f, z) || (q == f && f < z));
       uint64_t key = 0;
+      int32_t ms = -1;
       if (walked) {
         if (q < min(f, z)) {  // an M' entry: its exact key on the current row
-          const int32_t s = prev_slot(nd);
+          ms = prev_slot(nd);
           const DevPod pod = lpod[l];
-          key = make_key(eval_row<NM>(pod, slot_row(prow[s]), pnr[s], cls, c), nd);
+          key = make_key(eval_row<NM>(pod, slot_row(prow[ms]), pnr[ms], cls, c), nd);
         } else {
           key = e;
         }
       }
+      uint64_t mx = key;
 #pragma unroll
       for (int m = 1; m < RES_WE; m <<= 1) {
-        const uint64_t o = shfl_xor_u64(key, m);
-        key = o > key ? o : key;
+        const uint64_t o = shfl_xor_u64(mx, m);
+        mx = o > mx ? o : mx;
       }
       if (live) {
         dec_e[l * RES_WE + q] = walked ? nd : -1;
-        if (q == 0) {
-          dec_key[l] = key;
-          dec_n[l] = general ? -1 : (f < z ? f + 1 : z);
-        }
-      }
-    }
-    __syncthreads();
-    const uint64_t t_p1 = (dbg && t == 0) ? stamp() : 0;
-    // ---- 2. the staged winner's row: an M' slot (src < 0), a list-head
-    //         prefetch slot, or one HBM load into the pod's first head slot
-    for (int32_t l = t; l < n_pods; l += RES_THREADS) {
-      const uint64_t kk = dec_key[l];
-      int32_t src = 0;
-      if (kk != 0 && dec_n[l] >= 0) {
-        const int32_t w = key_node(kk);
-        const int32_t s = mp > 0 ? prev_slot(w) : -1;
-        if (s >= 0) {
-          src = -s - 1;
-        } else {
-          int32_t ps = -1;
-          for (int32_t q = 0; q < HP && ps < 0; q++)
-            if (pre_node[l * HP + q] == w) ps = l * HP + q;
-          if (ps < 0) {
-            ps = l * HP;
+        // ---- (2) the staged winner's row, by the lane that walked it: its M'
+        //          slot (src < 0), its list-head prefetch slot (entry q < HP:
+        //          slot l HP + q), or one HBM load into the pod's first head
+        //          slot (entries before it were M' entries: that slot is free)
+        if (walked && key == mx && mx != 0) {
+          int32_t src;
+          if (ms >= 0) {
+            src = -ms - 1;
+          } else if (q < HP && pre_node[l * HP + q] == nd) {
+            src = l * HP + q;
+          } else {
+            src = l * HP;
             if (dbg) n_p2++;
             NV v;
-            load_row(v, nodes(), w);
-            pre[ps] = v;
+            load_row(v, nodes(), nd);
+            pre[src] = v;
             if constexpr (NUMA) {
               NR nr;
-              load_side_row<NM>(nr, nodes(), w);
-              prenr[ps] = nr;
+              load_side_row<NM>(nr, nodes(), nd);
+              prenr[src] = nr;
             }
-            pre_node[ps] = w;
+            pre_node[src] = nd;
           }
-          src = ps;
+          dec_src[l] = src;
         }
-      }
-      dec_src[l] = src;
-      // "slow" pods always take the general path: a non-monotone configuration,
-      // NUMA cpuset pods (Allocate at Reserve; required-policy feasibility is
-      // not monotone), a walk longer than RES_WE entries
-      const uint32_t fl = lpod[l].flags;
-      bool slow = !monotone || dec_n[l] < 0;
-      if constexpr (NUMA) {
-        // (with topology-policy nodes every NUMA pod: its zone hint can move
-        // to emptier zones as a node fills, so its score is not monotone)
-        slow = slow || (numa_on(c) && ((fl & KOORDHIP_POD_CPUSET) || c.zones) &&
-                        !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
-      }
-      if constexpr (NM == 3) {
-        // a pod some reservation may match: committing into a reservation raises
-        // its (MostAllocated) reservation score elsewhere -- not monotone
-        slow = slow || lpod[l].resv_match != 0ull;
-      }
-      dec_c[l] = slow ? 2 : 0;
-      // claims for the conflict check: staged winner -> first pod (linear probing)
-      if (!slow && kk != 0) {
-        const int32_t sw = key_node(kk);
-        uint32_t h = res_hash(sw);
-        for (;;) {
-          const int32_t prev = atomicCAS(&ckey[h], -1, sw);
-          if (prev == -1 || prev == sw) {
-            atomicMin(&cval[h], l);
-            break;
+        if (q == 0) {
+          const int32_t dn = general ? -1 : (f < z ? f + 1 : z);
+          dec_key[l] = mx;
+          dec_n[l] = dn;
+          if (mx == 0 || dn < 0) dec_src[l] = 0;
+          // "slow" pods always take the general path: a non-monotone configuration,
+          // NUMA cpuset pods (Allocate at Reserve; required-policy feasibility is
+          // not monotone), a walk longer than RES_WE entries
+          const uint32_t fl = lpod[l].flags;
+          bool slow = !monotone || dn < 0;
+          if constexpr (NUMA) {
+            // (with topology-policy nodes every NUMA pod: its zone hint can move
+            // to emptier zones as a node fills, so its score is not monotone)
+            slow = slow || (numa_on(c) && ((fl & KOORDHIP_POD_CPUSET) || c.zones) &&
+                            !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
           }
-          h = (h + 1) & (RES_HASH - 1);
+          if constexpr (NM == 3) {
+            // a pod some reservation may match: committing into a reservation raises
+            // its (MostAllocated) reservation score elsewhere -- not monotone
+            slow = slow || lpod[l].resv_match != 0ull;
+          }
+          dec_c[l] = slow ? 2 : 0;
+          // claims for the conflict check: staged winner -> first pod (linear probing)
+          if (!slow && mx != 0) {
+            const int32_t sw = key_node(mx);
+            uint32_t h = res_hash(sw);
+            for (;;) {
+              const int32_t prev = atomicCAS(&ckey[h], -1, sw);
+              if (prev == -1 || prev == sw) {
+                atomicMin(&cval[h], l);
+                break;
+              }
+              h = (h + 1) & (RES_HASH - 1);
+            }
+          }
         }
       }
     }
+    const uint64_t t_p1 = (dbg && t == 0) ? stamp() : 0;
     __syncthreads();
     const uint64_t t_p2 = (dbg && t == 0) ? stamp() : 0;
     // ---- 2b. conflicts among the staged decisions (one walked entry per
@@ -2482,8 +2483,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         // materialised M slot (a general commit changed it), its staged
         // claimer's lazy row, or its M' row.
         const bool mono_g = monotone && !((slowmask >> g) & 1ull);
+        if (dbg) c_cand += stamp() - ts;
         if (mono_g) {
           const bool tabs = have_tables && __hip_atomic_load(&ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+          if (dbg) n_tready += tabs;
           const int first = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
           bool used = false;
 #pragma unroll
@@ -2508,6 +2511,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                     have = true;
                   }
                 }
+                if (dbg && __ballot(!have) != 0ull && lane == (int)__builtin_ctzll(__ballot(true))) n_evpass++;
                 if (!have) {
                   NV v;
                   NR nr;
@@ -2691,18 +2695,45 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       }
       // ---- 4. write M back; M becomes the next round's M' (rows stay in LDS)
       const uint64_t t_wb = dbg ? stamp() : 0;
-      if (lane < nm) {
-        NV v;
-        if ((lazy >> lane) & 1ull) {  // a lazy staged row: materialised here
-          const int32_t pi = seg_p[lane];
-          my_node = seg_w[lane];
-          const int32_t src = dec_src[pi];
-          v = src >= 0 ? pre[src] : prow[-src - 1];
-          apply_delta(v, lpod[pi], +1);
-          if constexpr (NUMA) mnr[lane] = src >= 0 ? prenr[src] : pnr[-src - 1];
-        } else {
-          v = slot_row(mrow[lane]);
+      if (lane < nm && ((lazy >> lane) & 1ull)) {  // a lazy staged row: materialised here, word by word
+        const int32_t pi = seg_p[lane];
+        my_node = seg_w[lane];
+        const int32_t src = dec_src[pi];
+        const uint64_t *sr = reinterpret_cast<const uint64_t *>(src >= 0 ? &pre[src] : &prow[-src - 1]);
+        uint64_t *dr = reinterpret_cast<uint64_t *>(&mrow[lane]);
+        const char *pp = reinterpret_cast<const char *>(&lpod[pi]);
+        const bool prod = ((prodmask >> pi) & 1ull) != 0;
+        // two halves, each loaded whole before its stores (LDS pointers may
+        // alias for the compiler: word-by-word would serialise 20 round trips)
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          uint64_t x[RES_WORDS / 2];
+          double dq[RES_WORDS / 2];
+#pragma unroll
+          for (int u = 0; u < RES_WORDS / 2; u++) {
+            const int q = h * (RES_WORDS / 2) + u;
+            const int32_t o = word_doff(q);
+            x[u] = sr[q];
+            dq[u] = (o >= 0 && (q < 16 || prod)) ? *reinterpret_cast<const double *>(pp + o) : 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < RES_WORDS / 2; u++) {
+            const int q = h * (RES_WORDS / 2) + u;
+            uint64_t y = x[u];
+            if (word_doff(q) >= 0) y = (uint64_t)__double_as_longlong(__longlong_as_double((long long)y) + dq[u]);
+            if (q == 18) y += 1ull << 32;
+            dr[q] = y;
+          }
         }
+        if constexpr (NUMA) {
+          const uint64_t *sn = reinterpret_cast<const uint64_t *>(src >= 0 ? &prenr[src] : &pnr[-src - 1]);
+          uint64_t *dn2 = reinterpret_cast<uint64_t *>(&mnr[lane]);
+#pragma unroll 4
+          for (int w = 0; w < (int)(sizeof(NR) / 8); w++) dn2[w] = sn[w];
+        }
+      }
+      if (lane < nm) {
+        const NV v = slot_row(mrow[lane]);
         mrow[lane] = v;
 #ifdef KH_PUBLISH_RELEASE
         store_row(v, nodes(), my_node);
@@ -2773,17 +2804,17 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         c_rel += t_end - t_rel;
         c_loop += t_end - t_loop;
       }
-    } else if (t < 128) {
+    } else if (t < 64 * (1 + res_loaders<NM>())) {
       if (ofs.overlap && r + 1 < r_end && p0 + P < total) {
-        // ---- wave 1: the next round's lists, pods and head rows, meanwhile
-        //      (it waits for the lists itself: no barrier without wave 0)
+        // ---- waves 1..: the next round's lists, pods and head rows, meanwhile
+        //      (each waits for the lists itself: no barrier without wave 0)
         const int32_t np2 = min(P, total - (p0 + P));
         int ok = 1;
         const uint64_t t1 = dbg ? stamp() : 0;
         if (lane == 0) ok = wait_at_least(&sy->sel[(r + 1) & 1], P * ((r + 1) >> 1) + np2, sy) ? 1 : 0;
         const uint64_t t2 = dbg ? stamp() : 0;
         if (__builtin_amdgcn_readfirstlane(ok)) {
-          load_round(r + 1, p0 + P, np2, lk2, lpod2, pre2, prenr2, pre_node2, lane, 64);
+          load_round(r + 1, p0 + P, np2, lk2, lpod2, pre2, prenr2, pre_node2, t - 64, 64 * res_loaders<NM>());
           if (dbg) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             c_w1load += stamp() - t2;
@@ -2799,7 +2830,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       //      kpre[l][i] on staged pod i's committed row, ktab[l][s] on M' row s
       //      Only the pods whose staged decision conflicts use them (general
       //      path, monotone): those pods are dealt round-robin to the waves.
-      const int hw = __builtin_amdgcn_readfirstlane((t >> 6) - 2), nh = RES_THREADS / 64 - 2;
+      const int hw = __builtin_amdgcn_readfirstlane((t >> 6) - 1 - res_loaders<NM>()),
+                nh = RES_THREADS / 64 - 1 - res_loaders<NM>();
       uint64_t todo = __ballot(lane < n_pods && dec_c[lane] == 1);
       for (int32_t x = 0; x < hw && todo; x++) todo &= todo - 1ull;
       for (; have_tables && todo;) {
@@ -2865,6 +2897,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   }
   if (t <= RES_MAXP_ROUND && t <= sh_mp) mbuf[t] = t == 0 ? sh_mp : pnode[t - 1];  // hand M' on
   if (dbg && n_p2) atomicAdd((unsigned long long *)&dbg[51], (unsigned long long)n_p2);
+  if (dbg && n_evpass) atomicAdd((unsigned long long *)&dbg[57], (unsigned long long)n_evpass);
   if (dbg && t == 64) {
     atomicAdd((unsigned long long *)&dbg[27], (unsigned long long)c_w1wait);
     atomicAdd((unsigned long long *)&dbg[28], (unsigned long long)c_w1load);
@@ -2892,6 +2925,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[52], (unsigned long long)n_conf);
     atomicAdd((unsigned long long *)&dbg[53], (unsigned long long)n_slowc);
     atomicAdd((unsigned long long *)&dbg[54], (unsigned long long)n_void);
+    atomicAdd((unsigned long long *)&dbg[55], (unsigned long long)c_cand);
+    atomicAdd((unsigned long long *)&dbg[56], (unsigned long long)n_tready);
   }
 }
 
