@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 6
+#define KOORDHIP_ABI_VERSION 7
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -101,9 +101,12 @@ extern "C" {
 #define KOORDHIP_POD_RESV_AFFINITY 1024u /* a required reservation affinity (util/reservation/reservation.go:444-487): a node
                                             without a matched reservation fails the Reservation Filter (plugin.go:378-381) */
 
-/* koordhip_node_soa.resv_flags: the node's Available reservation (at most one
- * per node: with several, the reference's order among them is Go map
- * iteration order, cache.go:236-252).  0 = none. */
+/* koordhip_node_soa.resv_flags: a node's Available reservations, one per slot
+ * (koordhip_node_soa.resv_slots).  The reference keeps them in a map
+ * (cache.go:236-252: forEachAvailableReservationOnNode iterates in Go map
+ * order) and its nomination ties (findMostPreferredReservationByOrder's first
+ * smallest order, nominator.go:60; sort.Slice by score, nominator.go:69-71)
+ * follow that order: here they go to the lowest slot.  0 = empty slot. */
 #define KOORDHIP_RESV_PRESENT 1u       /* IsAvailable && ParseError == nil (transformer.go:87-89) */
 #define KOORDHIP_RESV_ALLOCATE_ONCE 2u /* IsReservationAllocateOnce (apis/extension/reservation.go:98-100) */
 #define KOORDHIP_RESV_UNSCHEDULABLE 4u /* IsUnschedulable: spec.unschedulable or terminating (reservation_info.go:248-255) */
@@ -115,6 +118,7 @@ extern "C" {
 #define KOORDHIP_RESV_GROUP_SHIFT 8    /* bits 8-13: owner group g, the pod matches iff bit g of koordhip_pod.resv_match */
 #define KOORDHIP_RESV_GROUP(f) (((f) >> KOORDHIP_RESV_GROUP_SHIFT) & 63u)
 #define KOORDHIP_RESV_MAX_ORDERS 1024  /* distinct reservation-order values (resv_order_rank < this) */
+#define KOORDHIP_RESV_SLOTS 4          /* Available reservations per node (koordhip_node_soa.resv_slots <= this) */
 
 /* koordhip_pod.numa_policy, the NUMA PreFilter state (plugin.go:227-255):
  * bits 0-1 requiredCPUBindPolicy, 2-3 preferredCPUBindPolicy (= required when
@@ -273,6 +277,13 @@ typedef struct koordhip_node_soa {
    * (the node's labels, taints and spec.unschedulable against the class's
    * nodeSelector, required affinity and tolerations); NULL = every class. */
   const uint32_t *static_allow;
+  /* Reservation slots per node held by the resv_* columns: 0 or 1 = one
+   * reservation per node (columns of n values); S in [2, KOORDHIP_RESV_SLOTS]
+   * = up to S per node, every resv_* column then holds S x n values,
+   * slot-major (slot s of node i at [s * n + i]); a node's reservations fill
+   * its slots from 0, unused slots have resv_flags 0.  koordhip_update_nodes
+   * rows use the loaded snapshot's slot count. */
+  int32_t resv_slots;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -320,7 +331,8 @@ int koordhip_read_numa(koordhip_ctx *ctx, uint64_t *free_mask, uint64_t *excl_pc
 /* ... and the NUMA zone allocations, [n][2][KOORDHIP_NUMA_MAX_NODES] like numa_zone_used
  * (rows of nodes without a topology policy read as 0: the engine does not keep them). */
 int koordhip_read_numa_zones(koordhip_ctx *ctx, int64_t *zone_used);
-/* Reservation mutable state: Allocated [2][n] (cpu milli, memory), len(AssignedPods) [n]. */
+/* Reservation mutable state: Allocated [2][S n] (cpu milli, memory), len(AssignedPods) [S n],
+ * S = the loaded snapshot's reservation slots (1 when resv_slots <= 1), slot-major like the columns. */
 int koordhip_read_reservations(koordhip_ctx *ctx, int64_t *allocated, int32_t *assigned);
 
 /* Parity/debug mode, no commit: for n_pods pods against the current state.

@@ -578,8 +578,9 @@ int load_numa_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   return e;
 }
 
-// Reservation columns (one Available reservation per node): validated, then
-// uploaded; without them (or with the plugin off) the device sees none.
+// Reservation columns (resv_slots Available reservations per node, slot-major):
+// validated, then uploaded; without them (or with the plugin off) the device
+// sees none.  m: the column length (slots x rows).
 int check_resv_rows(const koordhip_node_soa *s, int32_t m) {
   for (int k = 0; k < 2; k++)
     if (!s->resv_alloc[k] || !s->resv_nz[k] || !s->resv_allocated[k]) return fail(KOORDHIP_EINVAL, "reservation column missing");
@@ -602,7 +603,10 @@ int check_resv_rows(const koordhip_node_soa *s, int32_t m) {
 int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   c->d.rv = kh::DevResv{};
   c->dc.resv = 0;
+  c->dc.resv_slots = 1;
   if (!c->resv) return 0;
+  if (s->resv_slots < 0 || s->resv_slots > KOORDHIP_RESV_SLOTS)
+    return fail(KOORDHIP_EINVAL, "resv_slots out of [0, KOORDHIP_RESV_SLOTS]");
   // a snapshot without reservation columns gets zero columns: the Reservation
   // build (NM 3) still runs the plugin, e.g. a pod with a required reservation
   // affinity fails its Filter on every node (plugin.go:378-381)
@@ -621,24 +625,26 @@ int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     for (int k = 0; k < 2; k++) zs.resv_alloc[k] = zs.resv_nz[k] = zs.resv_allocated[k] = zq.data();
     s = &zs;
   }
-  if (int e = check_resv_rows(s, n)) return e;
+  const int32_t slots = std::max(1, s->resv_slots);
+  const int32_t sn = slots * n;  // slot-major columns
+  if (int e = check_resv_rows(s, sn)) return e;
   kh::DevResv &rv = c->d.rv;
   uint32_t *f = nullptr;
   int32_t *rk = nullptr, *rn = nullptr;
-  int e = dev_alloc(c, &f, n);
-  if (!e) e = upload(c, f, s->resv_flags, n);
-  if (!e) e = dev_alloc(c, &rk, n);
-  if (!e) e = upload(c, rk, s->resv_order_rank, n);
-  if (!e) e = dev_alloc(c, &rn, n);
-  if (!e) e = upload(c, rn, s->resv_assigned, n);
+  int e = dev_alloc(c, &f, sn);
+  if (!e) e = upload(c, f, s->resv_flags, sn);
+  if (!e) e = dev_alloc(c, &rk, sn);
+  if (!e) e = upload(c, rk, s->resv_order_rank, sn);
+  if (!e) e = dev_alloc(c, &rn, sn);
+  if (!e) e = upload(c, rn, s->resv_assigned, sn);
   for (int k = 0; k < 2 && !e; k++) {
     double *a = nullptr, *z = nullptr, *d = nullptr;
-    e = dev_alloc(c, &a, n);
-    if (!e) e = upload_q(c, a, s->resv_alloc[k], n, "resv_alloc");
-    if (!e) e = dev_alloc(c, &z, n);
-    if (!e) e = upload_q(c, z, s->resv_nz[k], n, "resv_nz");
-    if (!e) e = dev_alloc(c, &d, n);
-    if (!e) e = upload_q(c, d, s->resv_allocated[k], n, "resv_allocated");
+    e = dev_alloc(c, &a, sn);
+    if (!e) e = upload_q(c, a, s->resv_alloc[k], sn, "resv_alloc");
+    if (!e) e = dev_alloc(c, &z, sn);
+    if (!e) e = upload_q(c, z, s->resv_nz[k], sn, "resv_nz");
+    if (!e) e = dev_alloc(c, &d, sn);
+    if (!e) e = upload_q(c, d, s->resv_allocated[k], sn, "resv_allocated");
     rv.ra[k] = a;
     rv.rz[k] = z;
     rv.rd[k] = d;
@@ -646,7 +652,12 @@ int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   rv.flags = f;
   rv.rank = rk;
   rv.rn = rn;
-  if (!e) c->dc.resv = 1;
+  rv.slots = slots;
+  rv.stride = n;
+  if (!e) {
+    c->dc.resv = 1;
+    c->dc.resv_slots = slots;
+  }
   return e;
 }
 
@@ -1022,13 +1033,16 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       if (rows->static_allow[j] != 0xFFFFFFFFu)
         return fail(KOORDHIP_EINVAL, "a static node filter needs the static_allow column at load_snapshot");
   const bool resv_rows = c->dc.resv && rows->resv_flags;
+  const int32_t rslots = std::max(1, rows->resv_slots);
   if (c->resv && rows->resv_flags && !c->dc.resv) {
-    for (int32_t j = 0; j < m; j++)
+    for (int32_t j = 0; j < rslots * m; j++)
       if (rows->resv_flags[j] & KOORDHIP_RESV_PRESENT)
         return fail(KOORDHIP_EINVAL, "a reservation needs the reservation columns at load_snapshot");
   }
+  if (resv_rows && rslots != c->d.rv.slots)
+    return fail(KOORDHIP_EINVAL, "update rows: resv_slots differs from the loaded snapshot's");
   if (resv_rows)
-    if (int e = check_resv_rows(rows, m)) return e;
+    if (int e = check_resv_rows(rows, rslots * m)) return e;
   // ---- one host staging image: [idx][column 0][column 1]..., 8-B aligned
   //      segments, quantities converted to the device's exact f64
   struct Col {
@@ -1078,15 +1092,18 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     cols.push_back({const_cast<double *>(c->d.nu.amp), rows->numa_amp_cpu, 8, false, "numa_amp_cpu"});
   if (c->d.sallow && rows->static_allow)
     cols.push_back({const_cast<uint32_t *>(c->d.sallow), rows->static_allow, 4, false, "static_allow"});
-  if (resv_rows) {
+  if (resv_rows) {  // slot q of the rows -> slot q of the nodes (the same indices)
     kh::DevResv &rv = c->d.rv;
-    cols.push_back({const_cast<uint32_t *>(rv.flags), rows->resv_flags, 4, false, "resv_flags"});
-    cols.push_back({const_cast<int32_t *>(rv.rank), rows->resv_order_rank, 4, false, "resv_order_rank"});
-    cols.push_back({rv.rn, rows->resv_assigned, 4, false, "resv_assigned"});
-    for (int k = 0; k < 2; k++) {
-      cols.push_back({const_cast<double *>(rv.ra[k]), rows->resv_alloc[k], 8, true, "resv_alloc"});
-      cols.push_back({const_cast<double *>(rv.rz[k]), rows->resv_nz[k], 8, true, "resv_nz"});
-      cols.push_back({rv.rd[k], rows->resv_allocated[k], 8, true, "resv_allocated"});
+    const size_t dn = (size_t)rv.stride, sm = (size_t)m;
+    for (int32_t q = 0; q < rslots; q++) {
+      cols.push_back({const_cast<uint32_t *>(rv.flags) + q * dn, rows->resv_flags + q * sm, 4, false, "resv_flags"});
+      cols.push_back({const_cast<int32_t *>(rv.rank) + q * dn, rows->resv_order_rank + q * sm, 4, false, "resv_order_rank"});
+      cols.push_back({rv.rn + q * dn, rows->resv_assigned + q * sm, 4, false, "resv_assigned"});
+      for (int k = 0; k < 2; k++) {
+        cols.push_back({const_cast<double *>(rv.ra[k]) + q * dn, rows->resv_alloc[k] + q * sm, 8, true, "resv_alloc"});
+        cols.push_back({const_cast<double *>(rv.rz[k]) + q * dn, rows->resv_nz[k] + q * sm, 8, true, "resv_nz"});
+        cols.push_back({rv.rd[k] + q * dn, rows->resv_allocated[k] + q * sm, 8, true, "resv_allocated"});
+      }
     }
   }
   if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one ZoneRow element per row
@@ -1214,7 +1231,7 @@ int koordhip_read_reservations(koordhip_ctx *c, int64_t *allocated, int32_t *ass
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   if (!c->resv) return fail(KOORDHIP_ESTATE, "Reservation is not enabled");
-  const size_t n = c->n;
+  const size_t n = (size_t)c->n * (size_t)(c->dc.resv ? c->d.rv.slots : 1);
   if (n == 0) return 0;
   if (!c->dc.resv) {  // no reservation columns: nothing is reserved anywhere
     if (allocated) std::memset(allocated, 0, 2 * n * sizeof(int64_t));
@@ -1729,9 +1746,10 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
     if (nu.zu) v.push_back({nu.zu, n * 2 * KOORDHIP_NUMA_MAX_ZONES * sizeof(double)});
   }
   if (c->dc.resv) {
-    v.push_back({c->d.rv.rd[0], b});
-    v.push_back({c->d.rv.rd[1], b});
-    v.push_back({c->d.rv.rn, n * sizeof(int32_t)});
+    const size_t sl = (size_t)c->d.rv.slots;
+    v.push_back({c->d.rv.rd[0], b * sl});
+    v.push_back({c->d.rv.rd[1], b * sl});
+    v.push_back({c->d.rv.rn, n * sl * sizeof(int32_t)});
   }
   return v;
 }

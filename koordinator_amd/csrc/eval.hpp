@@ -61,6 +61,7 @@ struct DevCfg {
   int32_t zones;                   // some node has a NUMA topology policy (zone columns loaded)
   int32_t amp;                     // some node has a CPU amplification ratio > 1
   int32_t resv;                    // Reservation enabled and the snapshot carries reservation columns
+  int32_t resv_slots;              // reservation slots per node (the NM 4 build when > 1)
   int32_t resv_b1;                 // 1 + the other plugins' maximum weighted total (resv.hpp ranking total)
   int32_t wide_keys;               // ranking totals + 1 exceed 16 bits (the resolve's key tables hold u32)
 };
@@ -535,19 +536,22 @@ namespace kh {
 // ... with the Reservation plugin (NM == 3): the cycle's restore of the
 // node's reservation first (every plugin sees the restored NodeInfo), then
 // filterWithReservations and the ranking total of resv.hpp.
-__device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v, const NumaRowR &r,
+template <int S>
+__device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v, const NumaRowRS<S> &r,
                                                    const DevNumaClass *classes, const DevCfg &c) {
   NV w = v;
-  const int cls = resv_class(r, p);
-  resv_restore(w, r, cls);
+  uint32_t mm;
+  const int nmatch = resv_restore(w, r, p, mm);
   int32_t t = eval_total_numa<false>(p, w, r, classes, c);
   if (t < 0) return t;
-  if (cls != 1)  // a required reservation affinity needs a matched reservation on the node (plugin.go:378-381)
+  if (nmatch == 0)  // a required reservation affinity needs a matched reservation on the node (plugin.go:378-381)
     return ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && (p.flags & KOORDHIP_POD_RESV_AFFINITY)) ? -1 : t;
-  if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !resv_filter(p, w, r)) return -1;
+  if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !resv_filter(p, w, r, mm, nmatch)) return -1;
   if (c.score & KOORDHIP_PLUGIN_RESERVATION) {
-    if (r.rf & KOORDHIP_RESV_ORDERED) return 101 * c.resv_b1 + (KOORDHIP_RESV_MAX_ORDERS - 1 - r.rk);
-    if (resv_nominated(p, r)) t += resv_score(p, r) * c.resv_b1;
+    const int rk = resv_node_rank(r, mm);
+    if (rk >= 0) return 101 * c.resv_b1 + (KOORDHIP_RESV_MAX_ORDERS - 1 - rk);
+    const int q = resv_nominate(p, r, mm);
+    if (q >= 0) t += resv_score(p, r.rs[q]) * c.resv_b1;
   }
   return t;
 }

@@ -166,13 +166,13 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
   NV v{};
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
-  NumaRowR nr{};
+  NumaRowR4 nr{};
   load_numa<true>(nr, d, i, all);
-  int rcls = 0;
+  int nmatch = 0;
+  uint32_t mm = 0;
   if (c.resv) {  // the cycle's Reservation restore: every plugin sees the restored node
     load_resv(nr, d.rv, i);
-    rcls = resv_class(nr, pod);
-    resv_restore(v, nr, rcls);
+    nmatch = resv_restore(v, nr, pod, mm);
   }
   if (status) {
     uint8_t b = 0;
@@ -183,7 +183,7 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
         (!numa_filter<true>(pod, nr, d.nu.cls) || (c.amp && !amp_filter_ok(pod, v, nr))))
       b |= KOORDHIP_ST_NUMA_FAIL;
     if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) &&
-        (rcls == 1 ? !resv_filter(pod, v, nr) : (pod.flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
+        (nmatch > 0 ? !resv_filter(pod, v, nr, mm, nmatch) : (pod.flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
       b |= KOORDHIP_ST_RESV_FAIL;
     status[(size_t)p * d.n + i] = b;
   }
@@ -432,13 +432,15 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 #endif
 constexpr int32_t kScanPodFastNodes = 65536;
 template <int NM>
-using side_row_t = typename std::conditional<NM == 3, NumaRowR, NumaRow>::type;
+using side_row_t = typename std::conditional<NM == 4, NumaRowR4,
+                                             typename std::conditional<NM == 3, NumaRowR, NumaRow>::type>::type;
 
 // NM: 0 = no NodeNUMAResource, 1 = NodeNUMAResource, 2 = ... with
 // topology-policy nodes (the zone code is compiled only here), 3 = with the
-// Reservation plugin (NUMA side rows carry the node's reservation)
+// Reservation plugin (NUMA side rows carry the node's reservation), 4 = ...
+// with several reservations per node (KOORDHIP_RESV_SLOTS slots per row)
 template <int R, int NM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NM == 3 ? SCAN_WPE3 : (NM == 1 ? SCAN_WPE1 : 1)))) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NM >= 3 ? SCAN_WPE3 : (NM == 1 ? SCAN_WPE1 : 1)))) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
                                               int32_t lo, int32_t hi, int32_t nchunks, int32_t cpx, int32_t pfast,
                                               uint16_t *__restrict__ S, int64_t s_stride,
                                               uint16_t *__restrict__ Mx, int32_t m_stride) {
@@ -483,8 +485,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NM == 3 ? S
     if (full || i < hi) {
       NV v;
       load_node(v, d, i, need, c);
-      if constexpr (NM == 3) {
-        NumaRowR nr;
+      if constexpr (NM >= 3) {
+        side_row_t<NM> nr;
         load_numa<false>(nr, d, i, need);
         load_resv(nr, d.rv, i);
         s[r] = eval_total_resv(pod, v, nr, cls, c) + 1;
@@ -637,7 +639,7 @@ __global__ __launch_bounds__(256) void k_scan_nm(DevCfg c, DevNodes d, const Dev
     in[r] = i < hi;
     const int32_t ii = in[r] ? i : hi - 1;  // out-of-range lanes evaluate a valid row, stored nowhere
     load_node(v[r], d, ii, need, c);
-    if constexpr (NM == 3) {
+    if constexpr (NM >= 3) {
       load_numa<false>(nr[r], d, ii, need);
       load_resv(nr[r], d.rv, ii);
     } else if constexpr (NM != 0) {
@@ -658,7 +660,7 @@ __global__ __launch_bounds__(256) void k_scan_nm(DevCfg c, DevNodes d, const Dev
       for (int r = 0; r < R; r++) {
         side_row_t<NM> w = nr[r];
         numa_view<NM == 2>(w, pn);
-        if constexpr (NM == 3)
+        if constexpr (NM >= 3)
           s[r] = eval_total_resv(pod, v[r], w, cls, c) + 1;
         else
           s[r] = eval_total_numa<NM == 2>(pod, v[r], w, cls, c) + 1;
@@ -1521,8 +1523,8 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
       if (i < hi) {
         NV v;
         load_node(v, d, i, need, c);
-        if constexpr (NM == 3) {
-          NumaRowR nr;
+        if constexpr (NM >= 3) {
+          side_row_t<NM> nr;
           load_numa<false>(nr, d, i, need);
           load_resv(nr, d.rv, i);
           tot = eval_total_resv(pod, v, nr, cls, c);
@@ -1880,23 +1882,23 @@ __device__ __forceinline__ uint64_t ktab_key(uint32_t v, int32_t nd) {
 template <int NM>
 __device__ __forceinline__ void load_side_row(side_row_t<NM> &r, const DevNodes &d, int32_t i) {
   load_numa_row<NM == 2>(r, d, i);
-  if constexpr (NM == 3) load_resv(r, d.rv, i);
+  if constexpr (NM >= 3) load_resv(r, d.rv, i);
 }
 template <int NM>
 __device__ __forceinline__ void store_side_row(const side_row_t<NM> &r, const DevNodes &d, int32_t i) {
   store_numa_row<NM == 2>(r, d, i);
-  if constexpr (NM == 3) store_resv(r, d.rv, i);
+  if constexpr (NM >= 3) store_resv(r, d.rv, i);
 }
 template <int NM>
 __device__ __forceinline__ void store_side_row_wt(const side_row_t<NM> &r, const DevNodes &d, int32_t i) {
   store_numa_row_wt<NM == 2>(r, d, i);
-  if constexpr (NM == 3) store_resv_wt(r, d.rv, i);
+  if constexpr (NM >= 3) store_resv_wt(r, d.rv, i);
 }
 
 template <int NM>
 __device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const side_row_t<NM> &nr,
                                             const DevNumaClass *cls, const DevCfg &c) {
-  if constexpr (NM == 3) {
+  if constexpr (NM >= 3) {
     return eval_total_resv(p, v, nr, cls, c);
   } else if constexpr (NM != 0) {
     return eval_total_numa<NM == 2>(p, v, nr, cls, c);
@@ -1933,7 +1935,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   // running counters otherwise stay live across the loop and push the product
   // build of the kernel into scratch spills
   if constexpr (!DBG) dbg = nullptr;
-  using NR = side_row_t<NM>;  // the NUMA side row (+ the node's reservation with NM == 3)
+  using NR = side_row_t<NM>;  // the NUMA side row (+ the node's reservation with NM >= 3)
   (void)trace;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   uint64_t *lk = reinterpret_cast<uint64_t *>(lds + ofs.lists);
@@ -2294,7 +2296,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             slow = slow || (numa_on(c) && ((fl & KOORDHIP_POD_CPUSET) || c.zones) &&
                             !(fl & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)));
           }
-          if constexpr (NM == 3) {
+          if constexpr (NM >= 3) {
             // a pod some reservation may match: committing into a reservation raises
             // its (MostAllocated) reservation score elsewhere -- not monotone
             slow = slow || lpod[l].resv_match != 0ull;
@@ -2646,7 +2648,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               reinterpret_cast<uint64_t *>(&mnr[rw])[lane] = reinterpret_cast<const uint64_t *>(snr)[lane];
             }
           }
-          if constexpr (NM == 3) {
+          if constexpr (NM >= 3) {
             // Reservation Reserve: assumePod into the node's nominated reservation
             if (okr && c.resv && pod.resv_match != 0ull && lane == 0) {
               NR nr = mnr[rw];
@@ -2938,12 +2940,12 @@ __global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, i
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const DevPod p = *pod;
   *rc = 0;
-  NumaRowR rv{};
+  NumaRowR4 rv{};
   if (c.resv) {
     load_resv(rv, d.rv, node);
-    // Unreserve: whether the Reserve went into the node's reservation
+    // Unreserve: whether the Reserve went into one of the node's reservations
     // (state.assumed, reservation/plugin.go:591-597) is not passed back
-    if (sign < 0 && (rv.rf & KOORDHIP_RESV_PRESENT) && ((p.resv_match >> KOORDHIP_RESV_GROUP(rv.rf)) & 1ull)) {
+    if (sign < 0 && resv_matchable(rv, p)) {
       *rc = KOORDHIP_EINVAL;
       return;
     }
@@ -3037,7 +3039,7 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
   const bool numa = nm != 0;
   const int32_t nchunks = scan_chunks(R, lo, hi);
   const size_t lds = (numa && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0;
-  if (ppw > 0 && R <= 2) {  // node-major (k_scan_nm)
+  if (ppw > 0 && R <= 2 && nm < 4) {  // node-major (k_scan_nm)
     const int32_t cqx = ((nchunks + 3) / 4 + 7) / 8;
     const int32_t nblocks = 8 * cqx * ((n_pods + ppw - 1) / ppw);
 #define KH_SCAN_NM(RR, NN)                                                                                          \
@@ -3065,7 +3067,12 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
 #define KH_SCAN(RR, NN)                                                                                            \
   hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, \
                      pfast, S, s_stride, Mx, m_stride)
-  if (nm == 3) {
+  if (nm == 4) {
+    switch (R) {
+      case 4: KH_SCAN(4, 4); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (nm == 3) {
     switch (R) {
       case 1: KH_SCAN(1, 3); break;
       case 2: KH_SCAN(2, 3); break;
@@ -3244,6 +3251,9 @@ hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *po
     case 12: KH_ETK(3, 8, 4); break;
     case 13: KH_ETK(3, 16, 4); break;
     case 14: KH_ETK(3, 32, 4); break;
+    case 16: KH_ETK(4, 8, 4); break;
+    case 17: KH_ETK(4, 16, 4); break;
+    case 18: KH_ETK(4, 32, 4); break;
     default: return hipErrorInvalidValue;
   }
 #undef KH_ETK
@@ -3271,13 +3281,13 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
 static inline int32_t list_stride(int32_t k) { return (k + 7) & ~7; }
 
 int side_mode(const DevCfg &c) {
-  if (c.resv) return 3;
+  if (c.resv) return c.resv_slots > 1 ? 4 : 3;
   if (!((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA)) return 0;
   return c.zones ? 2 : 1;
 }
 
 static int32_t side_row_bytes(int nm) {
-  return nm == 3 ? (int32_t)sizeof(NumaRowR) : (nm ? (int32_t)sizeof(NumaRow) : 0);
+  return nm == 4 ? (int32_t)sizeof(NumaRowR4) : nm == 3 ? (int32_t)sizeof(NumaRowR) : (nm ? (int32_t)sizeof(NumaRow) : 0);
 }
 
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, int nm, int32_t lag) {
@@ -3307,13 +3317,15 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag, wide);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag, wide);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag, wide);
-  static bool attr[8] = {false, false, false, false, false, false, false, false};
+  static bool attr[10] = {};
   const int ai = nm * 2 + (dbg ? 1 : 0);
   if (!attr[ai]) {
-    const void *f = dbg ? (nm == 3   ? (const void *)k_resolve<3, true>
+    const void *f = dbg ? (nm == 4   ? (const void *)k_resolve<4, true>
+                           : nm == 3 ? (const void *)k_resolve<3, true>
                            : nm == 2 ? (const void *)k_resolve<2, true>
                                      : (nm == 1 ? (const void *)k_resolve<1, true> : (const void *)k_resolve<0, true>))
-                        : (nm == 3   ? (const void *)k_resolve<3, false>
+                        : (nm == 4   ? (const void *)k_resolve<4, false>
+                           : nm == 3 ? (const void *)k_resolve<3, false>
                            : nm == 2 ? (const void *)k_resolve<2, false>
                                      : (nm == 1 ? (const void *)k_resolve<1, false> : (const void *)k_resolve<0, false>));
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, RES_LDS_MAX);
@@ -3330,7 +3342,9 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
     KH_RESOLVE_D(NN, true);  \
   else                       \
     KH_RESOLVE_D(NN, false)
-  if (nm == 3)
+  if (nm == 4)
+    KH_RESOLVE(4);
+  else if (nm == 3)
     KH_RESOLVE(3);
   else if (nm == 2)
     KH_RESOLVE(2);

@@ -100,6 +100,8 @@ struct DevResv {
   const double *rz[2];    // the reserve pod's non-zero cpu / memory request
   double *rd[2];          // Allocated
   int32_t *rn;            // len(AssignedPods)
+  int32_t slots;          // reservation slots per node: the columns hold slots x stride values, slot-major
+  int32_t stride;         // = the node count
 };
 
 struct ZoneRow {  // one node's [2][ZMAX] zone row (update_nodes scatter element)

@@ -1,8 +1,14 @@
 // resv.hpp -- the Reservation plugin's per-(pod, node) part on CDNA4: the
-// BeforePreFilter restore of the node's reservation (reservation/
+// BeforePreFilter restore of the node's reservations (reservation/
 // transformer.go:48-293), filterWithReservations (plugin.go:373-494), the
-// nomination filter (plugin.go:504-535), scoreReservation (scoring.go:177-200)
-// and the Reserve into the nominated reservation (reservation_info.go:297-306).
+// nomination (FilterReservation plugin.go:504-535, NominateReservation
+// nominator.go:32-85), scoreReservation (scoring.go:177-200) and the Reserve
+// into the nominated reservation (reservation_info.go:297-306).
+//
+// A node holds up to S reservations (slots; the reference's map order is
+// replaced by the slot order, include/koordhip.h): NumaRowRS<1> for the
+// common one-per-node snapshot (NM 3 builds), NumaRowRS<KOORDHIP_RESV_SLOTS>
+// otherwise (NM 4).
 //
 // The reference normalises the Reservation score over the pod's feasible
 // nodes (DefaultNormalizeScore) and weighs it 5000.  With a weight above 100 x
@@ -24,47 +30,74 @@
 
 namespace kh {
 
-// A NUMA side row with the node's reservation (NM == 3 builds).
-struct NumaRowR : NumaRow {
-  double ra[2], rd[2], rz[2];
-  int32_t rn;
-  uint32_t rf;  // KOORDHIP_RESV_* (0: none)
-  int32_t rk;
+// One reservation of a node (64 B).
+struct ResvSlot {
+  double ra[2], rd[2], rz[2];  // Allocatable, Allocated, the reserve pod's non-zero request (cpu milli, memory)
+  int32_t rn;                  // len(AssignedPods)
+  uint32_t rf;                 // KOORDHIP_RESV_* (0: empty slot)
+  int32_t rk;                  // order rank
   int32_t rpad;
 };
+static_assert(sizeof(ResvSlot) == 64, "reservation slot = 64 B");
+
+// A NUMA side row with the node's reservations (NM >= 3 builds).
+template <int S>
+struct NumaRowRS : NumaRow {
+  ResvSlot rs[S];
+};
+using NumaRowR = NumaRowRS<1>;
+using NumaRowR4 = NumaRowRS<KOORDHIP_RESV_SLOTS>;
 
 constexpr double RESV_NZ_CPU = 100.0;                         // (upstream) DefaultMilliCPURequest
 constexpr double RESV_NZ_MEM = 200.0 * 1024.0 * 1024.0;       // (upstream) DefaultMemoryRequest
 
-__device__ __forceinline__ void load_resv(NumaRowR &r, const DevResv &d, int32_t i) {
-  r.rf = d.flags[i];
-  r.rn = 0;
-  r.rk = 0;
+template <int S>
+__device__ __forceinline__ void load_resv(NumaRowRS<S> &r, const DevResv &d, int32_t i) {
 #pragma unroll
-  for (int k = 0; k < 2; k++) r.ra[k] = r.rd[k] = r.rz[k] = 0.0;
-  if (r.rf & KOORDHIP_RESV_PRESENT) {
-    r.rn = d.rn[i];
-    r.rk = d.rank[i];
+  for (int q = 0; q < S; q++) {
+    ResvSlot &x = r.rs[q];
+    const size_t at = (size_t)q * (size_t)d.stride + (size_t)i;
+    x.rf = q < d.slots ? d.flags[at] : 0u;
+    x.rn = 0;
+    x.rk = 0;
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-      r.ra[k] = d.ra[k][i];
-      r.rd[k] = d.rd[k][i];
-      r.rz[k] = d.rz[k][i];
+    for (int k = 0; k < 2; k++) x.ra[k] = x.rd[k] = x.rz[k] = 0.0;
+    if (x.rf & KOORDHIP_RESV_PRESENT) {
+      x.rn = d.rn[at];
+      x.rk = d.rank[at];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        x.ra[k] = d.ra[k][at];
+        x.rd[k] = d.rd[k][at];
+        x.rz[k] = d.rz[k][at];
+      }
     }
   }
 }
 
-__device__ __forceinline__ void store_resv(const NumaRowR &r, const DevResv &d, int32_t i) {
-  if (!(r.rf & KOORDHIP_RESV_PRESENT)) return;
-  d.rd[0][i] = r.rd[0];
-  d.rd[1][i] = r.rd[1];
-  d.rn[i] = r.rn;
+template <int S>
+__device__ __forceinline__ void store_resv(const NumaRowRS<S> &r, const DevResv &d, int32_t i) {
+#pragma unroll
+  for (int q = 0; q < S; q++) {
+    const ResvSlot &x = r.rs[q];
+    if (!(x.rf & KOORDHIP_RESV_PRESENT)) continue;
+    const size_t at = (size_t)q * (size_t)d.stride + (size_t)i;
+    d.rd[0][at] = x.rd[0];
+    d.rd[1][at] = x.rd[1];
+    d.rn[at] = x.rn;
+  }
 }
-__device__ __forceinline__ void store_resv_wt(const NumaRowR &r, const DevResv &d, int32_t i) {  // write-through
-  if (!(r.rf & KOORDHIP_RESV_PRESENT)) return;
-  st_wt(&d.rd[0][i], r.rd[0]);
-  st_wt(&d.rd[1][i], r.rd[1]);
-  st_wt(&d.rn[i], r.rn);
+template <int S>
+__device__ __forceinline__ void store_resv_wt(const NumaRowRS<S> &r, const DevResv &d, int32_t i) {  // write-through
+#pragma unroll
+  for (int q = 0; q < S; q++) {
+    const ResvSlot &x = r.rs[q];
+    if (!(x.rf & KOORDHIP_RESV_PRESENT)) continue;
+    const size_t at = (size_t)q * (size_t)d.stride + (size_t)i;
+    st_wt(&d.rd[0][at], x.rd[0]);
+    st_wt(&d.rd[1][at], x.rd[1]);
+    st_wt(&d.rn[at], x.rn);
+  }
 }
 
 __device__ __forceinline__ bool rkey(uint32_t rf, int k) {
@@ -73,13 +106,13 @@ __device__ __forceinline__ bool rkey(uint32_t rf, int k) {
 __device__ __forceinline__ bool pkey(const DevPod &p, int k) {
   return (p.flags & (k == 0 ? KOORDHIP_POD_KEY_CPU : KOORDHIP_POD_KEY_MEM)) != 0;
 }
-__device__ __forceinline__ double rem_of(const NumaRowR &r, int k) {
+__device__ __forceinline__ double rem_of(const ResvSlot &r, int k) {
   const double x = r.ra[k] - r.rd[k];
   return rkey(r.rf, k) && x > 0.0 ? x : 0.0;  // SubtractWithNonNegativeResult(Allocatable, Allocated)
 }
 
 // transformer.go:86-103: 1 = matched, 2 = unmatched with assigned pods, 0 = untouched
-__device__ __forceinline__ int resv_class(const NumaRowR &r, const DevPod &p) {
+__device__ __forceinline__ int resv_class(const ResvSlot &r, const DevPod &p) {
   if (!(r.rf & KOORDHIP_RESV_PRESENT)) return 0;
   if ((r.rf & KOORDHIP_RESV_ALLOCATE_ONCE) && r.rn > 0) return 0;
   const bool match = (p.resv_match >> KOORDHIP_RESV_GROUP(r.rf)) & 1ull;
@@ -87,56 +120,99 @@ __device__ __forceinline__ int resv_class(const NumaRowR &r, const DevPod &p) {
   return r.rn > 0 ? 2 : 0;
 }
 
-// The restore on the node's values (restoreMatchedReservation /
-// restoreUnmatchedReservations), then the Fit over-commit bits of the result.
-__device__ __forceinline__ void resv_restore(NV &v, const NumaRowR &r, int cls) {
-  if (cls == 0) return;
-  v.r[KOORDHIP_RES_CPU] -= r.ra[0];
-  v.r[KOORDHIP_RES_MEM] -= r.ra[1];
-  v.nz_cpu -= r.rz[0];
-  v.nz_mem -= r.rz[1];
-  if (cls == 1) {
-    v.npods -= 1;  // NodeInfo.RemovePod(reservePod)
-  } else {
-    const double rc = rem_of(r, 0), rm = rem_of(r, 1);
-    if (rc > 0.0 || rm > 0.0) {  // a pod requesting the remainder comes back
-      v.r[KOORDHIP_RES_CPU] += rc;
-      v.r[KOORDHIP_RES_MEM] += rm;
-      v.nz_cpu += rkey(r.rf, 0) ? rc : RESV_NZ_CPU;
-      v.nz_mem += rkey(r.rf, 1) ? rm : RESV_NZ_MEM;
+// The restore of every reservation of the node on its values
+// (restoreMatchedReservation / restoreUnmatchedReservations; the sums do not
+// depend on the order), then the Fit over-commit bits of the result.  Returns
+// the matched count; mm: the matched slots.
+template <int S>
+__device__ __forceinline__ int resv_restore(NV &v, const NumaRowRS<S> &r, const DevPod &p, uint32_t &mm) {
+  int nmatch = 0;
+  bool touched = false;
+  mm = 0;
+#pragma unroll
+  for (int q = 0; q < S; q++) {
+    const ResvSlot &x = r.rs[q];
+    const int cls = resv_class(x, p);
+    if (cls == 0) continue;
+    touched = true;
+    v.r[KOORDHIP_RES_CPU] -= x.ra[0];
+    v.r[KOORDHIP_RES_MEM] -= x.ra[1];
+    v.nz_cpu -= x.rz[0];
+    v.nz_mem -= x.rz[1];
+    if (cls == 1) {
+      v.npods -= 1;  // NodeInfo.RemovePod(reservePod)
+      nmatch++;
+      mm |= 1u << q;
+    } else {
+      const double rc = rem_of(x, 0), rm = rem_of(x, 1);
+      if (rc > 0.0 || rm > 0.0) {  // a pod requesting the remainder comes back
+        v.r[KOORDHIP_RES_CPU] += rc;
+        v.r[KOORDHIP_RES_MEM] += rm;
+        v.nz_cpu += rkey(x.rf, 0) ? rc : RESV_NZ_CPU;
+        v.nz_mem += rkey(x.rf, 1) ? rm : RESV_NZ_MEM;
+      }
     }
   }
-  uint32_t f = v.flags & ~(uint32_t)(NF_OVER_CPU | NF_OVER_MEM);
-  if (v.r[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU]) f |= NF_OVER_CPU;
-  if (v.r[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM]) f |= NF_OVER_MEM;
-  v.flags = f;
-}
-
-// filterWithReservations for a matched reservation on the restored values v
-// (podRequested = v.r + Allocatable: the matched restore undone).
-__device__ __forceinline__ bool resv_filter(const DevPod &p, const NV &v, const NumaRowR &r) {
-  const uint32_t pol = KOORDHIP_RESV_POLICY(r.rf);
-  if (pol == 0) return true;  // Default: only preemptible resources can make it insufficient
-  bool fits = !(v.npods > v.a_pods);  // len(Pods) - len(matched) + 1 > allowed, on the restored NodeInfo
-  if (p.flags & KOORDHIP_POD_HAS_REQ) {
-#pragma unroll
-    for (int k = 0; k < 2; k++)
-      fits &= !(p.req[k] > v.a[k] - ((v.r[k] + r.ra[k]) - rem_of(r, k) - r.rd[k]));
-    fits &= !(p.req[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH] - v.r[KOORDHIP_RES_EPH]);
-    if (p.flags & KOORDHIP_POD_REQ_BCPU)
-      fits &= !(p.req[KOORDHIP_RES_BCPU] > v.a[KOORDHIP_RES_BCPU] - v.r[KOORDHIP_RES_BCPU]);
-    if (p.flags & KOORDHIP_POD_REQ_BMEM)
-      fits &= !(p.req[KOORDHIP_RES_BMEM] > v.a[KOORDHIP_RES_BMEM] - v.r[KOORDHIP_RES_BMEM]);
+  if (touched) {
+    uint32_t f = v.flags & ~(uint32_t)(NF_OVER_CPU | NF_OVER_MEM);
+    if (v.r[KOORDHIP_RES_CPU] > v.a[KOORDHIP_RES_CPU]) f |= NF_OVER_CPU;
+    if (v.r[KOORDHIP_RES_MEM] > v.a[KOORDHIP_RES_MEM]) f |= NF_OVER_MEM;
+    v.flags = f;
   }
-  if (pol == 1) return fits;  // Aligned
-  bool le = true;             // Restricted: LessThanOrEqual(podRequests, rRemained)
-#pragma unroll
-  for (int k = 0; k < 2; k++) le &= !(rkey(r.rf, k) && pkey(p, k) && p.req[k] > rem_of(r, k));
-  return le && fits;
+  return nmatch;
 }
 
-// FilterReservation of a matched reservation: it is the nominated one
-__device__ __forceinline__ bool resv_nominated(const DevPod &p, const NumaRowR &r) {
+// filterWithReservations on the restored values v, fitsNode per matched
+// reservation (podRequested = v.r + the matched Allocatable: their restore
+// undone; rAllocated = the matched Allocated): an Aligned reservation that
+// fits, or a Restricted one that fits and holds the pod's requests, passes the
+// node; without any the node fails if it has Aligned / Restricted ones
+// (Default ones are insufficient only with preemptible resources).
+template <int S>
+__device__ __forceinline__ bool resv_filter(const DevPod &p, const NV &v, const NumaRowRS<S> &r, uint32_t mm,
+                                            int nmatch) {
+  double podreq[2] = {v.r[KOORDHIP_RES_CPU], v.r[KOORDHIP_RES_MEM]}, rall[2] = {0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < S; q++)
+    if ((mm >> q) & 1u)
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        podreq[k] += r.rs[q].ra[k];
+        rall[k] += r.rs[q].rd[k];
+      }
+  bool pass = false;
+  int nar = 0;
+#pragma unroll
+  for (int q = 0; q < S; q++) {
+    if (!((mm >> q) & 1u)) continue;
+    const ResvSlot &x = r.rs[q];
+    const uint32_t pol = KOORDHIP_RESV_POLICY(x.rf);
+    if (pol == 0) continue;
+    nar++;
+    bool fits = !(v.npods - nmatch + 1 > v.a_pods);  // len(Pods) - len(matched) + 1 > allowed, restored NodeInfo
+    if (p.flags & KOORDHIP_POD_HAS_REQ) {
+#pragma unroll
+      for (int k = 0; k < 2; k++) fits &= !(p.req[k] > v.a[k] - (podreq[k] - rem_of(x, k) - rall[k]));
+      fits &= !(p.req[KOORDHIP_RES_EPH] > v.a[KOORDHIP_RES_EPH] - v.r[KOORDHIP_RES_EPH]);
+      if (p.flags & KOORDHIP_POD_REQ_BCPU)
+        fits &= !(p.req[KOORDHIP_RES_BCPU] > v.a[KOORDHIP_RES_BCPU] - v.r[KOORDHIP_RES_BCPU]);
+      if (p.flags & KOORDHIP_POD_REQ_BMEM)
+        fits &= !(p.req[KOORDHIP_RES_BMEM] > v.a[KOORDHIP_RES_BMEM] - v.r[KOORDHIP_RES_BMEM]);
+    }
+    if (pol == 1) {  // Aligned
+      pass |= fits;
+    } else {  // Restricted: LessThanOrEqual(podRequests, rRemained)
+      bool le = true;
+#pragma unroll
+      for (int k = 0; k < 2; k++) le &= !(rkey(x.rf, k) && pkey(p, k) && p.req[k] > rem_of(x, k));
+      pass |= le && fits;
+    }
+  }
+  return pass || nar == 0;
+}
+
+// FilterReservation of a matched reservation: a nomination candidate
+__device__ __forceinline__ bool resv_candidate(const DevPod &p, const ResvSlot &r) {
   bool inter = false, nonzero = false;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -148,7 +224,7 @@ __device__ __forceinline__ bool resv_nominated(const DevPod &p, const NumaRowR &
 }
 
 // scoreReservation: MostAllocated (weights 1) over the non-zero Allocatable
-__device__ __forceinline__ int32_t resv_score(const DevPod &p, const NumaRowR &r) {
+__device__ __forceinline__ int32_t resv_score(const DevPod &p, const ResvSlot &r) {
   int32_t s = 0, w = 0;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -161,14 +237,74 @@ __device__ __forceinline__ int32_t resv_score(const DevPod &p, const NumaRowR &r
   return w == 2 ? (s >> 1) : s;
 }
 
+// NominateReservation: among the matched candidates the smallest order label,
+// else the highest scoreReservation; ties -> the lowest slot.  -1: none.
+template <int S>
+__device__ __forceinline__ int resv_nominate(const DevPod &p, const NumaRowRS<S> &r, uint32_t mm) {
+  int best = -1, brk = 0;
+  bool ord = false;
+  int32_t bsc = -1;
+#pragma unroll
+  for (int q = 0; q < S; q++) {
+    if (!((mm >> q) & 1u) || !resv_candidate(p, r.rs[q])) continue;
+    const ResvSlot &x = r.rs[q];
+    if (x.rf & KOORDHIP_RESV_ORDERED) {
+      if (!ord || x.rk < brk) {
+        best = q;
+        brk = x.rk;
+        ord = true;
+      }
+    } else if (!ord) {
+      const int32_t sc = resv_score(p, x);
+      if (sc > bsc) {
+        best = q;
+        bsc = sc;
+      }
+    }
+  }
+  return best;
+}
+
+// the matched slots of the pod (their classes only)
+template <int S>
+__device__ __forceinline__ uint32_t resv_matched(const NumaRowRS<S> &r, const DevPod &p) {
+  uint32_t mm = 0;
+#pragma unroll
+  for (int q = 0; q < S; q++) mm |= (resv_class(r.rs[q], p) == 1 ? 1u : 0u) << q;
+  return mm;
+}
+
+// PreScore's node order: the smallest order rank among the matched slots, -1 none
+template <int S>
+__device__ __forceinline__ int resv_node_rank(const NumaRowRS<S> &r, uint32_t mm) {
+  int rk = -1;
+#pragma unroll
+  for (int q = 0; q < S; q++)
+    if (((mm >> q) & 1u) && (r.rs[q].rf & KOORDHIP_RESV_ORDERED) && (rk < 0 || r.rs[q].rk < rk)) rk = r.rs[q].rk;
+  return rk;
+}
+
 // Reserve: AddAssignedPod to the nominated reservation (Allocated += the
 // pod's requests masked to ResourceNames).
-__device__ __forceinline__ void resv_assume(NumaRowR &r, const DevPod &p) {
-  if (resv_class(r, p) != 1 || !resv_nominated(p, r)) return;
+template <int S>
+__device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p) {
+  const int q = resv_nominate(p, r, resv_matched(r, p));
+  if (q < 0) return;
+  ResvSlot &x = r.rs[q];
 #pragma unroll
   for (int k = 0; k < 2; k++)
-    if (rkey(r.rf, k) && pkey(p, k)) r.rd[k] += p.req[k];
-  r.rn += 1;
+    if (rkey(x.rf, k) && pkey(p, k)) x.rd[k] += p.req[k];
+  x.rn += 1;
+}
+
+// a slot of the node holds an Available reservation whose owner group `p` matches
+template <int S>
+__device__ __forceinline__ bool resv_matchable(const NumaRowRS<S> &r, const DevPod &p) {
+  bool m = false;
+#pragma unroll
+  for (int q = 0; q < S; q++)
+    m |= (r.rs[q].rf & KOORDHIP_RESV_PRESENT) && ((p.resv_match >> KOORDHIP_RESV_GROUP(r.rs[q].rf)) & 1ull);
+  return m;
 }
 
 }  // namespace kh

@@ -134,8 +134,9 @@ class PlacementEngine:
         return {"free": fr, "excl_pcpu": ep, "excl_numa": en, "alloc_cnt": cnt, "zone_used": zu}
 
     def read_reservations(self) -> dict:
-        """Reservation mutable state: Allocated [2][n] (cpu milli, memory), len(AssignedPods) [n]."""
-        n = self.n
+        """Reservation mutable state: Allocated [2][S n] (cpu milli, memory), len(AssignedPods) [S n],
+        S = the loaded table's reservation slots, slot-major."""
+        n = self.n * max(1, self._table.resv_slots)
         al = np.zeros((2, n), np.int64)
         asg = np.zeros(n, np.int32)
         abi.check(self.lib, self.lib.koordhip_read_reservations(self._ctx, abi.ptr(al, C.c_int64), abi.ptr(asg, C.c_int32)))

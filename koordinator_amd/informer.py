@@ -344,6 +344,9 @@ class Informer:
             except nm.TopologyError:
                 res.needs_reload = True              # a CPU topology shape the loaded snapshot has no class for
                 return np.zeros(0, np.int32), None, res
+        if any(len(placed.get(int(i), [])) > rows.resv_slots for i in idx):
+            res.needs_reload = True                  # more reservations on a node than the snapshot's slots
+            return np.zeros(0, np.int32), None, res
         for j, i in enumerate(idx):
             node_row(rows, j, self.cluster.nodes[int(i)], self.cluster, self.profile, now)
             r = placed.get(int(i))

@@ -31,7 +31,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import abi, k8s
-from .snapshot import RESV_COLS as RESV_COLUMNS, NodeTable
+from .snapshot import RESV_COLS as RESV_COLUMNS, NodeTable, slot_col
 
 LABEL_RESERVATION_ORDER = "scheduling.koordinator.sh/reservation-order"   # apis/extension/reservation.go
 ANNOTATION_RESERVATION_AFFINITY = "scheduling.koordinator.sh/reservation-affinity"
@@ -374,40 +374,60 @@ def _q2(rl: k8s.ResourceList, name: str) -> int:
     return q.milli_value() if name == k8s.CPU else q.value()
 
 
-def available_by_node(node_index: Dict[str, int], reservations: Sequence[Reservation]) -> Dict[int, Reservation]:
-    """The reservation cache's Available reservations by node row (cache.go:236-252);
-    at most one per node (several: the reference orders them by map iteration)."""
-    placed: Dict[int, Reservation] = {}
+def available_by_node(node_index: Dict[str, int], reservations: Sequence[Reservation]) -> Dict[int, List[Reservation]]:
+    """The reservation cache's Available reservations by node row (cache.go:236-252),
+    each node's in the given order: its reservation slots.  The reference keeps
+    them in a map and breaks nomination ties by its iteration order; here the
+    lowest slot wins (include/koordhip.h KOORDHIP_RESV_SLOTS)."""
+    placed: Dict[int, List[Reservation]] = {}
     for r in reservations:
         if not r.is_available() or r.node_name not in node_index:
             continue
-        i = node_index[r.node_name]
-        if i in placed:
-            raise ReservationError(f"node {r.node_name}: more than one Available reservation (unsupported)")
-        placed[i] = r
+        rs = placed.setdefault(node_index[r.node_name], [])
+        if len(rs) >= abi.RESV_SLOTS:
+            raise ReservationError(f"node {r.node_name}: more than {abi.RESV_SLOTS} Available reservations")
+        rs.append(r)
     return placed
 
 
-def order_ranks(reservations: Iterable[Reservation]) -> Dict[int, int]:
-    """Rank of every distinct non-zero reservation-order label value (ascending)."""
-    orders = sorted({parse_order(r.labels) for r in reservations} - {0})
+def slots_needed(placed: Dict[int, List[Reservation]]) -> int:
+    return max([1] + [len(rs) for rs in placed.values()])
+
+
+def order_ranks(reservations: Iterable) -> Dict[int, int]:
+    """Rank of every distinct non-zero reservation-order label value (ascending)
+    (reservations: Reservation objects or per-node lists of them)."""
+    flat = [x for r in reservations for x in (r if isinstance(r, list) else [r])]
+    orders = sorted({parse_order(r.labels) for r in flat} - {0})
     if len(orders) > abi.RESV_MAX_ORDERS:
         raise ReservationError(f"more than {abi.RESV_MAX_ORDERS} distinct reservation orders")
     return {v: k for k, v in enumerate(orders)}
 
 
 def clear_reservation_row(table: NodeTable, i):
-    for c in RESV_COLUMNS:
-        table[c][i] = 0
+    for q in range(table.resv_slots):
+        for c in RESV_COLUMNS:
+            table[slot_col(c, q)][i] = 0
 
 
-def reservation_row(table: NodeTable, i: int, r: Reservation, index: "ReservationIndex", rank: Dict[int, int],
+def reservation_row(table: NodeTable, i: int, r, index: "ReservationIndex", rank: Dict[int, int],
                     node_labels: Optional[Dict[str, str]] = None):
-    """Row i of the resv_* columns for node i's Available reservation r
-    (node_labels: what reservation affinities see of the node)."""
+    """Row i of the resv_* columns for node i's Available reservations r (one
+    Reservation or a list, one per slot; node_labels: what reservation
+    affinities see of the node)."""
+    rs = r if isinstance(r, list) else [r]
+    if len(rs) > table.resv_slots:
+        raise ReservationError(f"{len(rs)} reservations on a node of a table with {table.resv_slots} slots")
+    clear_reservation_row(table, i)
+    for q, x in enumerate(rs):
+        _reservation_slot(table, i, q, x, index, rank, node_labels)
+
+
+def _reservation_slot(table: NodeTable, i: int, q: int, r: Reservation, index: "ReservationIndex",
+                      rank: Dict[int, int], node_labels: Optional[Dict[str, str]]):
     from .marshal import nonzero_request, fit_request
 
-    clear_reservation_row(table, i)
+    col = lambda c: table[slot_col(c, q)]
     names = set(r.allocatable)
     extra = names - {k8s.CPU, k8s.MEMORY}
     if extra:
@@ -435,7 +455,7 @@ def reservation_row(table: NodeTable, i: int, r: Reservation, index: "Reservatio
         if order not in rank:
             raise ReservationError(f"reservation {r.name}: order {order} has no rank in this snapshot")
         f |= abi.RESV_ORDERED
-        table["resv_order_rank"][i] = rank[order]
+        col("resv_order_rank")[i] = rank[order]
     if k8s.CPU in names:
         f |= abi.RESV_KEY_CPU
     if k8s.MEMORY in names:
@@ -444,16 +464,16 @@ def reservation_row(table: NodeTable, i: int, r: Reservation, index: "Reservatio
         raise ReservationError(f"reservation {r.name}: unknown allocate policy {r.allocate_policy!r}")
     f |= _POLICY_CODE[r.allocate_policy] << abi.RESV_POLICY_SHIFT
     f |= index.group(r.owners, node_labels, r) << abi.RESV_GROUP_SHIFT
-    table["resv_flags"][i] = f
-    table["resv_alloc0"][i] = _q2(r.allocatable, k8s.CPU)
-    table["resv_alloc1"][i] = _q2(r.allocatable, k8s.MEMORY)
+    col("resv_flags")[i] = f
+    col("resv_alloc0")[i] = _q2(r.allocatable, k8s.CPU)
+    col("resv_alloc1")[i] = _q2(r.allocatable, k8s.MEMORY)
     nzc, nzm = nonzero_request(pod)
-    table["resv_nz0"][i] = nzc
-    table["resv_nz1"][i] = nzm
+    col("resv_nz0")[i] = nzc
+    col("resv_nz1")[i] = nzm
     # Allocated masked to ResourceNames (reservation_info.go:286, 303)
-    table["resv_allocated0"][i] = _q2(r.allocated, k8s.CPU) if k8s.CPU in names else 0
-    table["resv_allocated1"][i] = _q2(r.allocated, k8s.MEMORY) if k8s.MEMORY in names else 0
-    table["resv_assigned"][i] = r.assigned
+    col("resv_allocated0")[i] = _q2(r.allocated, k8s.CPU) if k8s.CPU in names else 0
+    col("resv_allocated1")[i] = _q2(r.allocated, k8s.MEMORY) if k8s.MEMORY in names else 0
+    col("resv_assigned")[i] = r.assigned
 
 
 def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservations: Sequence[Reservation],
@@ -463,11 +483,12 @@ def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservatio
     cache.go:236-252) and return the owner groups for the pod masks
     (node_labels: node name -> labels, for reservation affinities)."""
     index = index or ReservationIndex()
-    clear_reservation_row(table, slice(None))
     placed = available_by_node(node_index, reservations)
+    table.set_resv_slots(max(table.resv_slots, slots_needed(placed)))
+    clear_reservation_row(table, slice(None))
     rank = order_ranks(placed.values())
-    for i, r in placed.items():
-        reservation_row(table, i, r, index, rank, (node_labels or {}).get(r.node_name))
+    for i, rs in placed.items():
+        reservation_row(table, i, rs, index, rank, (node_labels or {}).get(rs[0].node_name))
     return index
 
 

@@ -39,6 +39,11 @@ RESV_COLS = ["resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "res
 RESV_MUTABLE = ["resv_allocated0", "resv_allocated1", "resv_assigned"]
 
 
+def slot_col(col: str, s: int) -> str:
+    """Column name of reservation slot s (slot 0 is the plain column)."""
+    return col if s == 0 else f"{col}@{s}"
+
+
 def _shape(col: str, n: int):
     return (n, 2, abi.NUMA_MAX_NODES) if col in ZONE_COLS else (n,)
 
@@ -65,6 +70,25 @@ class NodeTable:
     names: List[str] = field(default_factory=list)
     # NodeNUMAResource topology classes (abi.NUMA_CLASS_DTYPE), indexed by numa_class
     numa_classes: np.ndarray = field(default_factory=lambda: np.zeros(0, abi.NUMA_CLASS_DTYPE))
+    # reservation slots per node: slot 0 in the RESV_COLS columns, slot s >= 1
+    # in the columns slot_col(c, s) (koordhip_node_soa.resv_slots)
+    resv_slots: int = 1
+
+    def set_resv_slots(self, slots: int):
+        """Hold up to `slots` reservations per node (new slots empty)."""
+        if not 1 <= slots <= abi.RESV_SLOTS:
+            raise ValueError(f"resv_slots must be in [1, {abi.RESV_SLOTS}]")
+        for s in range(1, abi.RESV_SLOTS):
+            for c in RESV_COLS:
+                name = slot_col(c, s)
+                if s < slots and name not in self.cols:
+                    self.cols[name] = np.zeros(self.n, dtype=_dtype(c))
+                elif s >= slots:
+                    self.cols.pop(name, None)
+        self.resv_slots = slots
+
+    def col_names(self) -> List[str]:
+        return ALL_COLS + [slot_col(c, s) for s in range(1, self.resv_slots) for c in RESV_COLS]
 
     @classmethod
     def empty(cls, n: int) -> "NodeTable":
@@ -83,10 +107,11 @@ class NodeTable:
     def rows(self, idx) -> "NodeTable":
         idx = np.asarray(idx, dtype=np.int64)
         t = NodeTable(n=len(idx))
-        for c in ALL_COLS:
+        for c in self.col_names():
             t.cols[c] = np.ascontiguousarray(self.cols[c][idx])
         t.names = [self.names[i] for i in idx] if self.names else []
         t.numa_classes = self.numa_classes
+        t.resv_slots = self.resv_slots
         return t
 
     def copy(self) -> "NodeTable":
@@ -94,6 +119,7 @@ class NodeTable:
         t.cols = {k: v.copy() for k, v in self.cols.items()}
         t.names = list(self.names)
         t.numa_classes = self.numa_classes.copy()
+        t.resv_slots = self.resv_slots
         return t
 
     def as_soa(self) -> abi.KoordhipNodeSoa:
@@ -134,13 +160,23 @@ class NodeTable:
         s.numa_zone_alloc = p64("numa_zone_alloc")
         s.numa_zone_used = p64("numa_zone_used")
         s.numa_amp_cpu = self.cols["numa_amp_cpu"].ctypes.data_as(C.POINTER(C.c_double))
-        s.resv_flags = self.cols["resv_flags"].ctypes.data_as(C.POINTER(C.c_uint32))
-        s.resv_order_rank = p32("resv_order_rank")
+        if self.resv_slots > 1:
+            # slot-major [S][n] copies of the reservation columns, kept alive by
+            # the returned struct (each call makes its own: a caller holding an
+            # earlier struct keeps valid pointers)
+            rc = {c: np.ascontiguousarray(np.concatenate(
+                [self.cols[slot_col(c, q)] for q in range(self.resv_slots)]), dtype=_dtype(c)) for c in RESV_COLS}
+        else:
+            rc = self.cols
+        s.resv_flags = rc["resv_flags"].ctypes.data_as(C.POINTER(C.c_uint32))
+        s.resv_order_rank = rc["resv_order_rank"].ctypes.data_as(C.POINTER(C.c_int32))
         for k in range(2):
-            s.resv_alloc[k] = p64(f"resv_alloc{k}")
-            s.resv_nz[k] = p64(f"resv_nz{k}")
-            s.resv_allocated[k] = p64(f"resv_allocated{k}")
-        s.resv_assigned = p32("resv_assigned")
+            s.resv_alloc[k] = rc[f"resv_alloc{k}"].ctypes.data_as(C.POINTER(C.c_int64))
+            s.resv_nz[k] = rc[f"resv_nz{k}"].ctypes.data_as(C.POINTER(C.c_int64))
+            s.resv_allocated[k] = rc[f"resv_allocated{k}"].ctypes.data_as(C.POINTER(C.c_int64))
+        s.resv_assigned = rc["resv_assigned"].ctypes.data_as(C.POINTER(C.c_int32))
+        s.resv_slots = self.resv_slots if self.resv_slots > 1 else 0
+        s._keep = rc
         s.static_allow = self.cols["static_allow"].ctypes.data_as(C.POINTER(C.c_uint32))
         return s
 
@@ -150,7 +186,12 @@ class NodeTable:
 
 def concat(tables: List[NodeTable]) -> NodeTable:
     t = NodeTable(n=sum(x.n for x in tables))
-    for c in ALL_COLS:
+    slots = max(x.resv_slots for x in tables)
+    for x in tables:
+        if x.resv_slots < slots:
+            x.set_resv_slots(slots)
+    t.resv_slots = slots
+    for c in tables[0].col_names():
         t.cols[c] = np.concatenate([x.cols[c] for x in tables])
     t.names = [nm for x in tables for nm in x.names]
     # merge topology class tables, re-indexing each part's numa_class

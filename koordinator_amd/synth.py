@@ -18,7 +18,7 @@ import numpy as np
 
 from . import abi, k8s
 from .config import Profile
-from .snapshot import NodeTable, pod_array
+from .snapshot import slot_col, NodeTable, pod_array
 
 SEED = 0x6B6F6F7264
 GI = 1 << 30
@@ -225,7 +225,7 @@ RESV_MEM = [8 * GI, 16 * GI, 32 * GI]
 
 @dataclass
 class ResvSpec:
-    node_frac: float = 0.10          # nodes holding an Available reservation (one each)
+    node_frac: float = 0.10          # nodes holding an Available reservation
     groups: int = 8                  # distinct owner specs (e.g. one label selector per workload)
     allocate_once_frac: float = 0.5  # Spec.AllocateOnce (else reusable until full)
     aligned_frac: float = 0.15
@@ -234,51 +234,64 @@ class ResvSpec:
     ordered_frac: float = 0.05       # reservation-order label, values 1..100
     cpu_only_frac: float = 0.05      # ResourceNames = {cpu}
     assigned_frac: float = 0.3       # already holding 1-3 pods
+    slots: int = 1                   # reservations per node at most (koordhip_node_soa.resv_slots)
+    multi_frac: float = 0.0          # P(a node holding q reservations holds a (q+1)-th), q < slots
 
 
 def add_reservations(t: NodeTable, spec: ResvSpec, seed: int = SEED) -> NodeTable:
     """resv_* columns (the layout reservation.reservation_columns builds from
     objects) plus the reserve pods' and assigned pods' share of each node's
-    Requested / NonZeroRequested / pod count."""
+    Requested / NonZeroRequested / pod count.  Slot 0 draws from the streams
+    of the one-per-node layout (so slots = 1 reproduces it); slot q >= 1 is
+    filled on a multi_frac share of the nodes whose slot q - 1 is."""
     n, s = t.n, seed + 11
-    has = uniform(s, n, 60) < spec.node_frac
-    g = (splitmix64(s, n, 61) % np.uint64(max(1, spec.groups))).astype(np.int64)
-    rc = choice(s, n, 62, RESV_CPU).astype(np.int64)
-    cpu_only = uniform(s, n, 63) < spec.cpu_only_frac
-    rm = np.where(cpu_only, 0, choice(s, n, 64, RESV_MEM).astype(np.int64))
-    once = uniform(s, n, 65) < spec.allocate_once_frac
-    up = uniform(s, n, 66)
-    pol = np.where(up < spec.aligned_frac, abi.RESV_POLICY_ALIGNED,
-                   np.where(up < spec.aligned_frac + spec.restricted_frac, abi.RESV_POLICY_RESTRICTED,
-                            abi.RESV_POLICY_DEFAULT))
-    unsched = uniform(s, n, 67) < spec.unschedulable_frac
-    ordered = uniform(s, n, 68) < spec.ordered_frac
-    order = (splitmix64(s, n, 69) % np.uint64(100)).astype(np.int64) + 1
-    assigned = np.where(uniform(s, n, 70) < spec.assigned_frac,
-                        (splitmix64(s, n, 71) % np.uint64(3)).astype(np.int64) + 1, 0)
-    fa = uniform(s, n, 72)
-    dc = np.where(assigned > 0, np.floor(rc * fa).astype(np.int64) // 100 * 100, 0)
-    dm = np.where(assigned > 0, np.floor(rm * fa).astype(np.int64) // MI * MI, 0)
-    f = (abi.RESV_PRESENT | abi.RESV_KEY_CPU | np.where(cpu_only, 0, abi.RESV_KEY_MEM)
-         | np.where(once, abi.RESV_ALLOCATE_ONCE, 0) | np.where(unsched, abi.RESV_UNSCHEDULABLE, 0)
-         | np.where(ordered, abi.RESV_ORDERED, 0) | (pol << abi.RESV_POLICY_SHIFT) | (g << abi.RESV_GROUP_SHIFT))
-    t["resv_flags"][:] = np.where(has, f, 0).astype(np.uint32)
-    vals = np.unique(order[has & ordered])
-    t["resv_order_rank"][:] = np.where(has & ordered, np.searchsorted(vals, order), 0).astype(np.int32)
-    t["resv_alloc0"][:] = np.where(has, rc, 0)
-    t["resv_alloc1"][:] = np.where(has, rm, 0)
-    nzm = np.where(cpu_only, 200 * MI, rm)         # the reserve pod lists no memory: GetNonzeroRequests default
-    t["resv_nz0"][:] = np.where(has, rc, 0)
-    t["resv_nz1"][:] = np.where(has, nzm, 0)
-    t["resv_allocated0"][:] = np.where(has, dc, 0)
-    t["resv_allocated1"][:] = np.where(has, dm, 0)
-    t["resv_assigned"][:] = np.where(has, assigned, 0).astype(np.int32)
-    # the reserve pod and the pods it holds are NodeInfo pods
-    t["requested0"][:] += np.where(has, rc + dc, 0)
-    t["requested1"][:] += np.where(has, rm + dm, 0)
-    t["nz_cpu_m"][:] += np.where(has, rc + dc, 0)
-    t["nz_mem"][:] += np.where(has, nzm + dm, 0)
-    t["npods"][:] += np.where(has, 1 + assigned, 0).astype(np.int32)
+    t.set_resv_slots(max(t.resv_slots, spec.slots))
+    prev = uniform(s, n, 60) < spec.node_frac
+    slots = []
+    for q in range(spec.slots):
+        o = 0 if q == 0 else 1000 + 20 * q    # stream offset of slot q
+        has = prev if q == 0 else prev & (uniform(s, n, o + 0) < spec.multi_frac)
+        g = (splitmix64(s, n, 61 + o) % np.uint64(max(1, spec.groups))).astype(np.int64)
+        rc = choice(s, n, 62 + o, RESV_CPU).astype(np.int64)
+        cpu_only = uniform(s, n, 63 + o) < spec.cpu_only_frac
+        rm = np.where(cpu_only, 0, choice(s, n, 64 + o, RESV_MEM).astype(np.int64))
+        once = uniform(s, n, 65 + o) < spec.allocate_once_frac
+        up = uniform(s, n, 66 + o)
+        pol = np.where(up < spec.aligned_frac, abi.RESV_POLICY_ALIGNED,
+                       np.where(up < spec.aligned_frac + spec.restricted_frac, abi.RESV_POLICY_RESTRICTED,
+                                abi.RESV_POLICY_DEFAULT))
+        unsched = uniform(s, n, 67 + o) < spec.unschedulable_frac
+        ordered = uniform(s, n, 68 + o) < spec.ordered_frac
+        order = (splitmix64(s, n, 69 + o) % np.uint64(100)).astype(np.int64) + 1
+        assigned = np.where(uniform(s, n, 70 + o) < spec.assigned_frac,
+                            (splitmix64(s, n, 71 + o) % np.uint64(3)).astype(np.int64) + 1, 0)
+        fa = uniform(s, n, 72 + o)
+        dc = np.where(assigned > 0, np.floor(rc * fa).astype(np.int64) // 100 * 100, 0)
+        dm = np.where(assigned > 0, np.floor(rm * fa).astype(np.int64) // MI * MI, 0)
+        f = (abi.RESV_PRESENT | abi.RESV_KEY_CPU | np.where(cpu_only, 0, abi.RESV_KEY_MEM)
+             | np.where(once, abi.RESV_ALLOCATE_ONCE, 0) | np.where(unsched, abi.RESV_UNSCHEDULABLE, 0)
+             | np.where(ordered, abi.RESV_ORDERED, 0) | (pol << abi.RESV_POLICY_SHIFT) | (g << abi.RESV_GROUP_SHIFT))
+        col = lambda c: t[slot_col(c, q)]
+        col("resv_flags")[:] = np.where(has, f, 0).astype(np.uint32)
+        col("resv_alloc0")[:] = np.where(has, rc, 0)
+        col("resv_alloc1")[:] = np.where(has, rm, 0)
+        nzm = np.where(cpu_only, 200 * MI, rm)         # the reserve pod lists no memory: GetNonzeroRequests default
+        col("resv_nz0")[:] = np.where(has, rc, 0)
+        col("resv_nz1")[:] = np.where(has, nzm, 0)
+        col("resv_allocated0")[:] = np.where(has, dc, 0)
+        col("resv_allocated1")[:] = np.where(has, dm, 0)
+        col("resv_assigned")[:] = np.where(has, assigned, 0).astype(np.int32)
+        # the reserve pod and the pods it holds are NodeInfo pods
+        t["requested0"][:] += np.where(has, rc + dc, 0)
+        t["requested1"][:] += np.where(has, rm + dm, 0)
+        t["nz_cpu_m"][:] += np.where(has, rc + dc, 0)
+        t["nz_mem"][:] += np.where(has, nzm + dm, 0)
+        t["npods"][:] += np.where(has, 1 + assigned, 0).astype(np.int32)
+        slots.append((has & ordered, order))
+        prev = has
+    vals = np.unique(np.concatenate([order[m] for m, order in slots]))
+    for q, (m, order) in enumerate(slots):
+        t[slot_col("resv_order_rank", q)][:] = np.where(m, np.searchsorted(vals, order), 0).astype(np.int32)
     return t
 
 

@@ -83,6 +83,8 @@ def lib():
         L.orc_resv_restore.argtypes = [C.POINTER(OrcState), vp, C.c_int]
         L.orc_resv_filter.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
         L.orc_resv_filter.restype = C.c_int
+        L.orc_resv_nominate.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
+        L.orc_resv_nominate.restype = C.c_int
         L.orc_resv_nominated.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
         L.orc_resv_nominated.restype = C.c_int
         L.orc_resv_score.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
@@ -172,7 +174,8 @@ class Oracle:
         }
 
     def resv_state(self) -> dict:
-        n = self.n
+        """Allocated [2][S n], assigned [S n] (S = the table's reservation slots, slot-major)."""
+        n = self.n * max(1, self.table.resv_slots)
         a = lambda p: np.ctypeslib.as_array(p, shape=(n,)).copy()
         return {"allocated": np.stack([a(self.st.resv_allocated[0]), a(self.st.resv_allocated[1])]),
                 "assigned": a(self.st.resv_assigned)}
@@ -196,6 +199,11 @@ class Oracle:
     def resv_nominated(self, pod: np.ndarray, node: int) -> bool:
         pod = np.ascontiguousarray(np.atleast_1d(pod))
         return bool(lib().orc_resv_nominated(C.byref(self.st), pod.ctypes.data, node))
+
+    def resv_nominate(self, pod: np.ndarray, node: int) -> int:
+        """NominateReservation on `node`: the nominated reservation's slot, -1 for none."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        return int(lib().orc_resv_nominate(C.byref(self.st), pod.ctypes.data, node))
 
     def resv_score(self, pod: np.ndarray, node: int) -> int:
         pod = np.ascontiguousarray(np.atleast_1d(pod))

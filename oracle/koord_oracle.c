@@ -129,11 +129,13 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
   st->numa_zone_used = (int64_t *)calloc(zn, sizeof(int64_t));
   if (soa->numa_zone_used && st->numa_zone_used)
     memcpy(st->numa_zone_used, soa->numa_zone_used, sizeof(int64_t) * (size_t)n * 2 * KOORDHIP_NUMA_MAX_NODES);
+  /* reservation state: one value per slot of every node ([slots][n]) */
+  const int32_t rn = n * (soa->resv_slots > 1 ? soa->resv_slots : 1);
   for (int r = 0; r < 2; r++)
-    st->resv_allocated[r] = dup64(soa->resv_flags && soa->resv_allocated[r] ? soa->resv_allocated[r] : NULL, n);
-  st->resv_assigned = (int32_t *)calloc((size_t)(n > 0 ? n : 1), sizeof(int32_t));
+    st->resv_allocated[r] = dup64(soa->resv_flags && soa->resv_allocated[r] ? soa->resv_allocated[r] : NULL, rn);
+  st->resv_assigned = (int32_t *)calloc((size_t)(rn > 0 ? rn : 1), sizeof(int32_t));
   if (soa->resv_flags && soa->resv_assigned && st->resv_assigned)
-    memcpy(st->resv_assigned, soa->resv_assigned, sizeof(int32_t) * (size_t)n);
+    memcpy(st->resv_assigned, soa->resv_assigned, sizeof(int32_t) * (size_t)rn);
   if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned) return -1;
   orc_la_flags(soa, n, st->flags);
   return 0;
@@ -393,10 +395,10 @@ static int numa_on(const koordhip_config *cfg) {
 
 int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t i, int sign,
                uint64_t *cpus) {
-  const int rv = orc_resv_on(cfg, st) && (st->soa->resv_flags[i] & KOORDHIP_RESV_PRESENT);
-  /* Unreserve of a pod its node's reservation could have taken: whether it did
-   * (state.assumed, plugin.go:591-597) is not passed back */
-  if (rv && sign < 0 && ((pod->resv_match >> KOORDHIP_RESV_GROUP(st->soa->resv_flags[i])) & 1u)) return KOORDHIP_EINVAL;
+  const int rv = orc_resv_on(cfg, st) && orc_resv_node_present(st, i);
+  /* Unreserve of a pod one of its node's reservations could have taken: whether
+   * it did (state.assumed, plugin.go:591-597) is not passed back */
+  if (rv && sign < 0 && orc_resv_node_matchable(st, pod, i)) return KOORDHIP_EINVAL;
   if (numa_on(cfg) && orc_numa_reserve_active(st, pod, i)) {
     if (sign > 0) {
       if (!orc_numa_reserve(st, pod, i, cpus)) return KOORDHIP_ERESERVE;

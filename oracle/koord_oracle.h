@@ -120,6 +120,10 @@ int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t no
  * scoreReservation, the normalized scores over a feasible list, Reserve, and
  * the device's ranking total. */
 int orc_resv_on(const koordhip_config *cfg, const orc_state *st);
+int orc_resv_slots(const orc_state *st); /* reservation slots per node (resv_* columns hold slots x n) */
+int orc_resv_nominate(const orc_state *st, const koordhip_pod *pod, int32_t i); /* nominated slot, -1 none */
+int orc_resv_node_present(const orc_state *st, int32_t i);
+int orc_resv_node_matchable(const orc_state *st, const koordhip_pod *pod, int32_t i);
 void orc_resv_classify(const orc_state *st, const koordhip_pod *pod, int32_t i, int *matched, int *unmatched);
 void orc_resv_restore_delta(const orc_state *st, const koordhip_pod *pod, int32_t i, int64_t *dreq, int64_t *dnz,
                             int32_t *dpods);

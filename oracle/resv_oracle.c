@@ -17,8 +17,15 @@
  * keys with max(0, a - b); Mask keeps the named keys; IsZero = every value 0;
  * LessThanOrEqual(a, b) compares a[k] <= b[k] for the keys of b present in a.
  *
- * One reservation per node (KOORDHIP_RESV_*); a node's reservation state is
- * Allocated (cpu, memory; masked to ResourceNames) and len(AssignedPods).
+ * A node holds up to koordhip_node_soa.resv_slots Available reservations
+ * (KOORDHIP_RESV_SLOTS, slot s of node i at [s n + i]); a reservation's state is
+ * Allocated (cpu, memory; masked to ResourceNames) and len(AssignedPods).  The
+ * reference iterates a node's reservations in Go map order
+ * (forEachAvailableReservationOnNode, cache.go:236-252); the filter and the
+ * restore do not depend on that order, the nomination's ties do
+ * (findMostPreferredReservationByOrder keeps the first smallest order,
+ * nominator.go:60; sort.Slice by score keeps an unspecified first,
+ * nominator.go:69-71): here the lowest slot wins both.
  */
 #include <string.h>
 
@@ -33,60 +40,80 @@ int orc_resv_on(const koordhip_config *cfg, const orc_state *st) {
   return ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) && st->soa->resv_flags;
 }
 
+int orc_resv_slots(const orc_state *st) { return st->soa->resv_slots > 1 ? st->soa->resv_slots : 1; }
+/* column index of slot s of node i */
+static size_t at(const orc_state *st, int s, int32_t i) { return (size_t)s * (size_t)st->n + (size_t)i; }
+
 static int has_key(uint32_t rf, int r) { return (rf & (r == 0 ? KOORDHIP_RESV_KEY_CPU : KOORDHIP_RESV_KEY_MEM)) != 0; }
 static int pod_key(const koordhip_pod *p, int r) {
   return (p->flags & (r == 0 ? KOORDHIP_POD_KEY_CPU : KOORDHIP_POD_KEY_MEM)) != 0;
 }
+/* SubtractWithNonNegativeResult(Allocatable, Allocated) of slot x, resource r */
+static int64_t rem_of(const orc_state *st, size_t x, int r) {
+  return has_key(st->soa->resv_flags[x], r) ? max0(st->soa->resv_alloc[r][x] - st->resv_allocated[r][x]) : 0;
+}
 
-/* transformer.go:86-103: matched / unmatched classification of node i's
- * reservation for `pod` (isReservedPod is false: reserve pods are not streamed). */
+/* transformer.go:86-103: 1 = matched, 2 = unmatched with assigned pods, 0 =
+ * untouched, for slot x (isReservedPod is false: reserve pods are not streamed). */
+static int slot_class(const orc_state *st, const koordhip_pod *pod, size_t x) {
+  const uint32_t rf = st->soa->resv_flags[x];
+  if (!(rf & KOORDHIP_RESV_PRESENT)) return 0;                                     /* :87-89 */
+  const int32_t assigned = st->resv_assigned[x];
+  if ((rf & KOORDHIP_RESV_ALLOCATE_ONCE) && assigned > 0) return 0;               /* :93-95 */
+  const int match = (int)((pod->resv_match >> KOORDHIP_RESV_GROUP(rf)) & 1u);     /* matchReservation :335-359 */
+  if (!(rf & KOORDHIP_RESV_UNSCHEDULABLE) && match) return 1;                     /* :97-98 */
+  return assigned > 0 ? 2 : 0;                                                     /* :100-101 */
+}
+
 void orc_resv_classify(const orc_state *st, const koordhip_pod *pod, int32_t i, int *matched, int *unmatched) {
   *matched = *unmatched = 0;
-  const uint32_t rf = st->soa->resv_flags ? st->soa->resv_flags[i] : 0;
-  if (!(rf & KOORDHIP_RESV_PRESENT)) return;                                       /* :87-89 */
-  const int32_t assigned = st->resv_assigned[i];
-  if ((rf & KOORDHIP_RESV_ALLOCATE_ONCE) && assigned > 0) return;                 /* :93-95 */
-  const int match = (int)((pod->resv_match >> KOORDHIP_RESV_GROUP(rf)) & 1u);     /* matchReservation :335-359 */
-  if (!(rf & KOORDHIP_RESV_UNSCHEDULABLE) && match) *matched = 1;                 /* :97-98 */
-  else if (assigned > 0) *unmatched = 1;                                           /* :100-101 */
+  if (!st->soa->resv_flags) return;
+  for (int s = 0; s < orc_resv_slots(st); s++) {
+    const int c = slot_class(st, pod, at(st, s, i));
+    *matched += c == 1;
+    *unmatched += c == 2;
+  }
 }
 
 /* The NodeInfo delta the restore applies for `pod` on node i (requested cpu /
- * memory, non-zero cpu / memory, pod count): restoreUnmatchedReservations
- * (transformer.go:252-278, updateNodeInfoRequested :280-293) or
- * restoreMatchedReservation (:227-250, NodeInfo.RemovePod of the reserve pod). */
+ * memory, non-zero cpu / memory, pod count), summed over its reservations:
+ * restoreUnmatchedReservations (transformer.go:252-278, updateNodeInfoRequested
+ * :280-293) or restoreMatchedReservation (:227-250, NodeInfo.RemovePod of the
+ * reserve pod).  The sums do not depend on the reservations' order. */
 void orc_resv_restore_delta(const orc_state *st, const koordhip_pod *pod, int32_t i, int64_t *dreq, int64_t *dnz,
                             int32_t *dpods) {
-  const koordhip_node_soa *s = st->soa;
-  int matched, unmatched;
-  orc_resv_classify(st, pod, i, &matched, &unmatched);
+  const koordhip_node_soa *so = st->soa;
   dreq[0] = dreq[1] = dnz[0] = dnz[1] = 0;
   *dpods = 0;
-  if (!matched && !unmatched) return;
-  const uint32_t rf = s->resv_flags[i];
-  for (int r = 0; r < 2; r++) { /* the reserve pod leaves: Requested and NonZeroRequested */
-    dreq[r] -= s->resv_alloc[r][i];
-    dnz[r] -= s->resv_nz[r][i];
-  }
-  if (matched) {
-    *dpods = -1; /* RemovePod */
-    return;
-  }
-  /* unmatched: a pod requesting SubtractWithNonNegativeResult(Allocatable, Allocated) comes back unless IsZero */
-  int64_t rem[2];
-  for (int r = 0; r < 2; r++) rem[r] = has_key(rf, r) ? max0(s->resv_alloc[r][i] - st->resv_allocated[r][i]) : 0;
-  if (rem[0] == 0 && rem[1] == 0) return;
-  for (int r = 0; r < 2; r++) {
-    dreq[r] += rem[r];
-    /* GetNonzeroRequests of that pod: a key it lists counts as is, a missing one as the default */
-    dnz[r] += has_key(rf, r) ? rem[r] : (r == 0 ? NZ_DEFAULT_CPU : NZ_DEFAULT_MEM);
+  if (!so->resv_flags) return;
+  for (int s = 0; s < orc_resv_slots(st); s++) {
+    const size_t x = at(st, s, i);
+    const int c = slot_class(st, pod, x);
+    if (!c) continue;
+    for (int r = 0; r < 2; r++) { /* the reserve pod leaves: Requested and NonZeroRequested */
+      dreq[r] -= so->resv_alloc[r][x];
+      dnz[r] -= so->resv_nz[r][x];
+    }
+    if (c == 1) {
+      *dpods -= 1; /* RemovePod */
+      continue;
+    }
+    /* unmatched: a pod requesting SubtractWithNonNegativeResult(Allocatable, Allocated) comes back unless IsZero */
+    const uint32_t rf = so->resv_flags[x];
+    const int64_t rem0 = rem_of(st, x, 0), rem1 = rem_of(st, x, 1);
+    if (rem0 == 0 && rem1 == 0) continue;
+    for (int r = 0; r < 2; r++) {
+      const int64_t rem = r ? rem1 : rem0;
+      dreq[r] += rem;
+      /* GetNonzeroRequests of that pod: a key it lists counts as is, a missing one as the default */
+      dnz[r] += has_key(rf, r) ? rem : (r == 0 ? NZ_DEFAULT_CPU : NZ_DEFAULT_MEM);
+    }
   }
 }
 
 /* Apply (sign +1) / undo (-1) the restore of `pod` on every node holding a reservation. */
 void orc_resv_restore(orc_state *st, const koordhip_pod *pod, int sign) {
   for (int32_t i = 0; i < st->n; i++) {
-    if (!(st->soa->resv_flags[i] & KOORDHIP_RESV_PRESENT)) continue;
     int64_t dreq[2], dnz[2];
     int32_t dp;
     orc_resv_restore_delta(st, pod, i, dreq, dnz, &dp);
@@ -99,100 +126,168 @@ void orc_resv_restore(orc_state *st, const koordhip_pod *pod, int sign) {
 }
 
 /* filterWithReservations (plugin.go:373-440) on the RESTORED node i, with
- * fitsNode (:445-494): podRequested = Requested after the unmatched restore
- * (= before the matched one), rAllocated = the matched reservations'
- * Allocated, rRemained = the reservation's Allocatable - Allocated.  1 = pass. */
+ * fitsNode (:445-494) per matched reservation: podRequested = Requested after
+ * the unmatched restore (= before the matched one), rAllocated = the matched
+ * reservations' Allocated, rRemained = the reservation's Allocatable -
+ * Allocated.  Default-policy reservations are insufficient only with
+ * preemptible resources (none in a stream, :405-412); an Aligned one that fits
+ * or a Restricted one that fits and holds the pod's requests passes the node
+ * (:414-431); otherwise it fails when it has Aligned or Restricted ones
+ * (:434-438, all of them insufficient).  1 = pass. */
 int orc_resv_filter(const orc_state *st, const koordhip_pod *pod, int32_t i) {
-  const koordhip_node_soa *s = st->soa;
+  const koordhip_node_soa *so = st->soa;
   int matched, unmatched;
   orc_resv_classify(st, pod, i, &matched, &unmatched);
   if (!matched) return (pod->flags & KOORDHIP_POD_RESV_AFFINITY) ? 0 : 1; /* :378-392 (hasAffinity; nothing preemptible) */
-  const uint32_t rf = s->resv_flags[i];
-  const uint32_t policy = KOORDHIP_RESV_POLICY(rf);
-  if (policy == 0) return 1; /* Default: insufficient only with preemptible resources (:405-412) */
-  int64_t rem[2], podreq[2];
-  for (int r = 0; r < 2; r++) {
-    rem[r] = has_key(rf, r) ? max0(s->resv_alloc[r][i] - st->resv_allocated[r][i]) : 0;
-    podreq[r] = st->requested[r][i] + s->resv_alloc[r][i]; /* undo the matched restore (:129) */
+  const int S = orc_resv_slots(st);
+  int64_t podreq[2] = {st->requested[0][i], st->requested[1][i]}, rall[2] = {0, 0};
+  for (int s = 0; s < S; s++) {
+    const size_t x = at(st, s, i);
+    if (slot_class(st, pod, x) != 1) continue;
+    for (int r = 0; r < 2; r++) {
+      podreq[r] += so->resv_alloc[r][x]; /* undo the matched restore (:129) */
+      rall[r] += st->resv_allocated[r][x];
+    }
   }
-  /* fitsNode */
-  int fits = 1;
-  if ((int64_t)st->npods[i] + 1 - 1 > (int64_t)s->alloc_pods[i]) fits = 0; /* len(Pods) - len(matched) + 1, restored Pods */
-  if (fits && (pod->flags & KOORDHIP_POD_HAS_REQ)) {
-    for (int r = 0; r < 2 && fits; r++)
-      if (pod->req[r] > s->alloc[r][i] - (podreq[r] - rem[r] - st->resv_allocated[r][i])) fits = 0;
-    if (fits && pod->req[KOORDHIP_RES_EPH] > s->alloc[KOORDHIP_RES_EPH][i] - st->requested[KOORDHIP_RES_EPH][i]) fits = 0;
-    if (fits && (pod->flags & KOORDHIP_POD_REQ_BCPU) &&
-        pod->req[KOORDHIP_RES_BCPU] > s->alloc[KOORDHIP_RES_BCPU][i] - st->requested[KOORDHIP_RES_BCPU][i])
-      fits = 0;
-    if (fits && (pod->flags & KOORDHIP_POD_REQ_BMEM) &&
-        pod->req[KOORDHIP_RES_BMEM] > s->alloc[KOORDHIP_RES_BMEM][i] - st->requested[KOORDHIP_RES_BMEM][i])
-      fits = 0;
+  int n_ar = 0;
+  for (int s = 0; s < S; s++) {
+    const size_t x = at(st, s, i);
+    if (slot_class(st, pod, x) != 1) continue;
+    const uint32_t policy = KOORDHIP_RESV_POLICY(so->resv_flags[x]);
+    if (policy == 0) continue;
+    n_ar++;
+    /* fitsNode: len(Pods) - len(matched) + 1 > allowed on the restored NodeInfo */
+    int fits = !((int64_t)st->npods[i] - matched + 1 > (int64_t)so->alloc_pods[i]);
+    if (fits && (pod->flags & KOORDHIP_POD_HAS_REQ)) {
+      for (int r = 0; r < 2 && fits; r++)
+        if (pod->req[r] > so->alloc[r][i] - (podreq[r] - rem_of(st, x, r) - rall[r])) fits = 0;
+      if (fits && pod->req[KOORDHIP_RES_EPH] > so->alloc[KOORDHIP_RES_EPH][i] - st->requested[KOORDHIP_RES_EPH][i]) fits = 0;
+      if (fits && (pod->flags & KOORDHIP_POD_REQ_BCPU) &&
+          pod->req[KOORDHIP_RES_BCPU] > so->alloc[KOORDHIP_RES_BCPU][i] - st->requested[KOORDHIP_RES_BCPU][i])
+        fits = 0;
+      if (fits && (pod->flags & KOORDHIP_POD_REQ_BMEM) &&
+          pod->req[KOORDHIP_RES_BMEM] > so->alloc[KOORDHIP_RES_BMEM][i] - st->requested[KOORDHIP_RES_BMEM][i])
+        fits = 0;
+    }
+    if (policy == 1 && fits) return 1; /* Aligned :415-419 */
+    if (policy == 2) {                  /* Restricted :420-432: LessThanOrEqual(podRequests, rRemained) */
+      int le = 1;
+      for (int r = 0; r < 2; r++)
+        if (has_key(so->resv_flags[x], r) && pod_key(pod, r) && pod->req[r] > rem_of(st, x, r)) le = 0;
+      if (le && fits) return 1;
+    }
   }
-  if (policy == 1) return fits; /* Aligned :415-419 */
-  /* Restricted :420-432: LessThanOrEqual(podRequests, rRemained) over rRemained's keys */
-  int le = 1;
-  for (int r = 0; r < 2; r++)
-    if (has_key(rf, r) && pod_key(pod, r) && pod->req[r] > rem[r]) le = 0;
-  return le && fits;
+  return n_ar == 0;
 }
 
-/* FilterReservation (plugin.go:504-535) of node i's matched reservation: the
- * nominated one when it passes (nominator.go:48-63, one candidate). */
-int orc_resv_nominated(const orc_state *st, const koordhip_pod *pod, int32_t i) {
-  int matched, unmatched;
-  orc_resv_classify(st, pod, i, &matched, &unmatched);
-  if (!matched) return 0;
-  const uint32_t rf = st->soa->resv_flags[i];
+/* FilterReservation (plugin.go:504-535) of slot x, a matched reservation */
+static int slot_passes(const orc_state *st, const koordhip_pod *pod, size_t x) {
+  const uint32_t rf = st->soa->resv_flags[x];
   int inter = 0, nonzero = 0;
   for (int r = 0; r < 2; r++) {
     if (!(has_key(rf, r) && pod_key(pod, r))) continue; /* Intersection(ResourceNames, podRequests names) */
     inter = 1;
-    if (max0(st->soa->resv_alloc[r][i] - st->resv_allocated[r][i]) != 0) nonzero = 1;
+    if (rem_of(st, x, r) != 0) nonzero = 1;
   }
   return inter && nonzero;
 }
 
-/* scoreReservation (scoring.go:177-200): MostAllocated over
+/* scoreReservation (scoring.go:177-200) of slot x: MostAllocated over
  * RemoveZeros(Allocatable) of podRequests + Allocated. */
-int64_t orc_resv_score(const orc_state *st, const koordhip_pod *pod, int32_t i) {
-  const uint32_t rf = st->soa->resv_flags[i];
+static int64_t slot_score(const orc_state *st, const koordhip_pod *pod, size_t x) {
+  const uint32_t rf = st->soa->resv_flags[x];
   int64_t s = 0, w = 0;
   for (int r = 0; r < 2; r++) {
-    const int64_t cap = has_key(rf, r) ? st->soa->resv_alloc[r][i] : 0;
+    const int64_t cap = has_key(rf, r) ? st->soa->resv_alloc[r][x] : 0;
     if (cap == 0) continue;
     w++;
-    const int64_t req = (pod_key(pod, r) ? pod->req[r] : 0) + st->resv_allocated[r][i];
+    const int64_t req = (pod_key(pod, r) ? pod->req[r] : 0) + st->resv_allocated[r][x];
     if (req <= cap) s += 100 * req / cap; /* MaxNodeScore * MilliValue / MilliValue */
   }
   return w ? s / w : 0;
 }
 
+/* NominateReservation (nominator.go:32-85) on node i: the slot of the
+ * reservation nominated for `pod`, -1 for none.  Candidates: the matched
+ * reservations passing FilterReservation; the smallest order label among them
+ * (findMostPreferredReservationByOrder), else the highest scoreReservation
+ * (prioritizeReservations: the Reservation plugin is the only
+ * ReservationScorePlugin here); ties: the lowest slot. */
+int orc_resv_nominate(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  if (!st->soa->resv_flags) return -1;
+  int best = -1, best_rank = 0, ord = 0;
+  int64_t best_sc = -1;
+  for (int s = 0; s < orc_resv_slots(st); s++) {
+    const size_t x = at(st, s, i);
+    if (slot_class(st, pod, x) != 1 || !slot_passes(st, pod, x)) continue;
+    const uint32_t rf = st->soa->resv_flags[x];
+    if (rf & KOORDHIP_RESV_ORDERED) {
+      const int rk = st->soa->resv_order_rank[x];
+      if (!ord || rk < best_rank) {
+        best = s;
+        best_rank = rk;
+        ord = 1;
+      }
+    } else if (!ord) {
+      const int64_t sc = slot_score(st, pod, x);
+      if (sc > best_sc) {
+        best = s;
+        best_sc = sc;
+      }
+    }
+  }
+  return best;
+}
+
+int orc_resv_nominated(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  return orc_resv_nominate(st, pod, i) >= 0;
+}
+
+/* Score (scoring.go:105-121) of a node that is not the preferred one: the
+ * nominated reservation's scoreReservation, 0 without one. */
+int64_t orc_resv_score(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  const int s = orc_resv_nominate(st, pod, i);
+  return s < 0 ? 0 : slot_score(st, pod, at(st, s, i));
+}
+
+/* PreScore's node order (scoring.go:58-67): the smallest order label among the
+ * node's matched reservations (before FilterReservation); -1 for none. */
+static int node_order_rank(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  int rk = -1;
+  if (!st->soa->resv_flags) return -1;
+  for (int s = 0; s < orc_resv_slots(st); s++) {
+    const size_t x = at(st, s, i);
+    if (slot_class(st, pod, x) != 1 || !(st->soa->resv_flags[x] & KOORDHIP_RESV_ORDERED)) continue;
+    const int r = st->soa->resv_order_rank[x];
+    if (rk < 0 || r < rk) rk = r;
+  }
+  return rk;
+}
+
 /* Reserve: assumePod into the nominated reservation (Allocated += the pod's
  * requests masked to ResourceNames, one more assigned pod). */
 void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i) {
-  if (!orc_resv_nominated(st, pod, i)) return;
-  const uint32_t rf = st->soa->resv_flags[i];
+  const int s = orc_resv_nominate(st, pod, i);
+  if (s < 0) return;
+  const size_t x = at(st, s, i);
+  const uint32_t rf = st->soa->resv_flags[x];
   for (int r = 0; r < 2; r++)
-    if (has_key(rf, r) && pod_key(pod, r)) st->resv_allocated[r][i] += pod->req[r];
-  st->resv_assigned[i] += 1;
+    if (has_key(rf, r) && pod_key(pod, r)) st->resv_allocated[r][x] += pod->req[r];
+  st->resv_assigned[x] += 1;
 }
 
 /* The Reservation plugin's contribution for one pod over its feasible nodes
  * (PreScore + Score + DefaultNormalizeScore): norm[j] for feasible[j].
- * preferredNode: the feasible node whose matched reservation has the smallest
+ * preferredNode: the feasible node whose matched reservations hold the smallest
  * order; the reference keeps the first such node of its (unordered) feasible
  * list, here the lowest node index (the selectHost tie rule, BASELINE.json). */
 void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int32_t *feasible, int32_t nf,
                          int64_t *norm) {
-  const koordhip_node_soa *s = st->soa;
   int32_t pref = -1, pref_rank = 0;
   for (int32_t j = 0; j < nf; j++) {
     const int32_t i = feasible[j];
-    int matched, unmatched;
-    orc_resv_classify(st, pod, i, &matched, &unmatched);
-    if (!matched || !(s->resv_flags[i] & KOORDHIP_RESV_ORDERED)) continue;
-    const int32_t rk = s->resv_order_rank[i];
+    const int rk = node_order_rank(st, pod, i);
+    if (rk < 0) continue;
     if (pref < 0 || rk < pref_rank || (rk == pref_rank && i < pref)) {
       pref = i;
       pref_rank = rk;
@@ -201,9 +296,7 @@ void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int
   int64_t mx = 0;
   for (int32_t j = 0; j < nf; j++) {
     const int32_t i = feasible[j];
-    int64_t raw = 0;
-    if (i == pref) raw = 1000; /* mostPreferredScore */
-    else if (orc_resv_nominated(st, pod, i)) raw = orc_resv_score(st, pod, i);
+    const int64_t raw = i == pref ? 1000 /* mostPreferredScore */ : orc_resv_score(st, pod, i);
     norm[j] = raw;
     if (raw > mx) mx = raw;
   }
@@ -219,10 +312,23 @@ int64_t orc_resv_rank_total(const koordhip_config *cfg, const orc_state *st, con
   for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
     if (cfg->score_plugins & orc_score_plugin_bit(p)) bmax += 100 * cfg->plugin_weight[p];
   if (!(cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION)) return b;
-  int matched, unmatched;
-  orc_resv_classify(st, pod, i, &matched, &unmatched);
-  if (matched && (st->soa->resv_flags[i] & KOORDHIP_RESV_ORDERED))
-    return 101 * (bmax + 1) + (KOORDHIP_RESV_MAX_ORDERS - 1 - st->soa->resv_order_rank[i]);
-  const int64_t raw = orc_resv_nominated(st, pod, i) ? orc_resv_score(st, pod, i) : 0;
-  return raw * (bmax + 1) + b;
+  const int rk = node_order_rank(st, pod, i);
+  if (rk >= 0) return 101 * (bmax + 1) + (KOORDHIP_RESV_MAX_ORDERS - 1 - rk);
+  return orc_resv_score(st, pod, i) * (bmax + 1) + b;
+}
+
+/* node i holds an Available reservation; `pod` matches the owner group of one */
+int orc_resv_node_present(const orc_state *st, int32_t i) {
+  if (!st->soa->resv_flags) return 0;
+  for (int s = 0; s < orc_resv_slots(st); s++)
+    if (st->soa->resv_flags[at(st, s, i)] & KOORDHIP_RESV_PRESENT) return 1;
+  return 0;
+}
+int orc_resv_node_matchable(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  if (!st->soa->resv_flags) return 0;
+  for (int s = 0; s < orc_resv_slots(st); s++) {
+    const uint32_t rf = st->soa->resv_flags[at(st, s, i)];
+    if ((rf & KOORDHIP_RESV_PRESENT) && ((pod->resv_match >> KOORDHIP_RESV_GROUP(rf)) & 1u)) return 1;
+  }
+  return 0;
 }

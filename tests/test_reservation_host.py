@@ -8,6 +8,8 @@ node for every pod on random states."""
 import numpy as np
 import pytest
 
+from koordinator_amd.snapshot import slot_col
+
 import golden_cases as G
 import oracle
 from koordinator_amd import abi, k8s, marshal, synth
@@ -73,11 +75,22 @@ def test_reservation_columns():
     assert rec["resv_match"][0] == 1 << g and rec["flags"][0] & abi.POD_KEY_CPU and not rec["flags"][0] & abi.POD_KEY_MEM
 
 
-def test_two_reservations_on_a_node_rejected():
+def test_reservations_fill_node_slots():
+    """Several Available reservations on a node take its slots in the given
+    order (the nomination tie rule: lowest slot); more than KOORDHIP_RESV_SLOTS
+    are rejected."""
     prof = G.resv_profile()
-    rs = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": "2"})) for i in range(2)]
+    rs = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": str(2 + i)})) for i in range(3)]
+    t, _ = G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"}),
+                               ("n1", {"cpu": "32", "memory": "64Gi", "pods": "110"})], rs, prof)
+    assert t.resv_slots == 3
+    assert [int(t[slot_col("resv_alloc0", q)][0]) for q in range(3)] == [2000, 3000, 4000]
+    assert all(int(t[slot_col("resv_flags", q)][1]) == 0 for q in range(3))
+    soa = t.as_soa()
+    assert soa.resv_slots == 3 and soa.resv_alloc[0][2] == 3000 and soa.resv_alloc[0][1] == 0   # slot-major [s * n + i]
+    rs5 = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": "1"})) for i in range(abi.RESV_SLOTS + 1)]
     with pytest.raises(rv.ReservationError):
-        G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"})], rs, prof)
+        G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"})], rs5, prof)
 
 
 def test_reservation_weight_must_dominate():
