@@ -29,6 +29,8 @@
  *                              filterWithReservations plugin.go:373-494, PreScore/Score scoring.go:42-200,
  *                              NominateReservation nominator.go:32-85, Reserve -> reservationCache.assumePod
  *                              plugin.go:537-575 / cache.go:170-191
+ *   resv_cpus columns       <- NodeNUMAResource RestoreReservation nodenumaresource/reservation.go:68-122 and the
+ *                              reservation-preferred CPUs of getResourceOptions plugin.go:455-524 (Score / Reserve)
  */
 #ifndef KOORDHIP_H
 #define KOORDHIP_H
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 7
+#define KOORDHIP_ABI_VERSION 8
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -284,6 +286,17 @@ typedef struct koordhip_node_soa {
    * its slots from 0, unused slots have resv_flags 0.  koordhip_update_nodes
    * rows use the loaded snapshot's slot count. */
   int32_t resv_slots;
+  int32_t reserved1;
+  /* NodeNUMAResource's reservation restore (RestoreReservation,
+   * nodenumaresource/reservation.go:76-113): per reservation slot, the CPUs of
+   * the reservation's cpuset allocation not held by its AssignedPods (core-major
+   * positions of the node's topology class, slot-major like the resv_* columns).
+   * These CPUs are allocated in the node's NodeAllocation (not in numa_free).  A
+   * cpuset pod nominated into the reservation (PreScore) takes them first
+   * (takePreferredCPUs, cpu_accumulator.go:29-85) at Score and Reserve; a
+   * Reserve removes the pod's CPUs.  NULL = no reservation holds CPUs (also
+   * the update_nodes default). */
+  const uint64_t *resv_cpus[KOORDHIP_NUMA_WORDS];
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -334,6 +347,8 @@ int koordhip_read_numa_zones(koordhip_ctx *ctx, int64_t *zone_used);
 /* Reservation mutable state: Allocated [2][S n] (cpu milli, memory), len(AssignedPods) [S n],
  * S = the loaded snapshot's reservation slots (1 when resv_slots <= 1), slot-major like the columns. */
 int koordhip_read_reservations(koordhip_ctx *ctx, int64_t *allocated, int32_t *assigned);
+/* ... and the reservations' remaining reserved CPUs [WORDS][S n] (zeros when no loaded reservation holds CPUs). */
+int koordhip_read_resv_cpus(koordhip_ctx *ctx, uint64_t *cpus);
 
 /* Parity/debug mode, no commit: for n_pods pods against the current state.
  *   status : optional, [n_pods][n] KOORDHIP_ST_* bits (every plugin evaluated)

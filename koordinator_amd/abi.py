@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 7
+KOORDHIP_ABI_VERSION = 8
 NRES = 5
 NPLUGINS = 4
 
@@ -137,6 +137,8 @@ class KoordhipNodeSoa(C.Structure):
         ("resv_assigned", _i32p),
         ("static_allow", C.POINTER(C.c_uint32)),
         ("resv_slots", C.c_int32),
+        ("reserved1", C.c_int32),
+        ("resv_cpus", _u64p * NUMA_WORDS),
     ]
 
 
@@ -220,6 +222,7 @@ def load_library(path: str = LIB_PATH):
         "koordhip_read_numa": (C.c_int, [vp, _u64p, _u64p, _u64p, _i32p]),
         "koordhip_read_numa_zones": (C.c_int, [vp, _i64p]),
         "koordhip_read_reservations": (C.c_int, [vp, _i64p, _i32p]),
+        "koordhip_read_resv_cpus": (C.c_int, [vp, _u64p]),
         "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_last_kernel_stats": (C.c_int, [vp, C.POINTER(KoordhipKernelStats)]),
@@ -243,7 +246,8 @@ EXPORTED_SYMBOLS = [
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
-    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations", "koordhip_last_stats", "koordhip_last_kernel_stats",
+    "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
+    "koordhip_read_resv_cpus", "koordhip_last_stats", "koordhip_last_kernel_stats",
     "koordhip_set_profile_kernels",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]

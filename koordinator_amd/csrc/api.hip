@@ -600,6 +600,36 @@ int check_resv_rows(const koordhip_node_soa *s, int32_t m) {
   return 0;
 }
 
+// reserved CPUs: only on present slots of nodes with a CPU topology and no
+// NUMA topology policy, inside the topology's positions, and allocated (not
+// free: the reservation's own allocation holds them)
+int check_resv_cpus(const koordhip_node_soa *s, int32_t m, int32_t slots, const std::vector<int32_t> &class_cpus) {
+  const int32_t nclasses = (int32_t)class_cpus.size();
+  for (int32_t q = 0; q < slots; q++)
+    for (int32_t i = 0; i < m; i++) {
+      const size_t at = (size_t)q * (size_t)m + (size_t)i;
+      uint64_t any = 0;
+      for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) any |= s->resv_cpus[w][at];
+      if (!any) continue;
+      if (!(s->resv_flags[at] & KOORDHIP_RESV_PRESENT))
+        return fail(KOORDHIP_EINVAL, "resv_cpus on an empty reservation slot");
+      const int32_t cls = s->numa_class ? s->numa_class[i] : -1;
+      if (cls < 0 || cls >= nclasses) return fail(KOORDHIP_EINVAL, "resv_cpus on a node without a CPU topology");
+      if (s->numa_flags && KOORDHIP_NODE_NUMA_POLICY(s->numa_flags[i]) != 0)
+        return fail(KOORDHIP_EINVAL, "resv_cpus on a NUMA topology-policy node");
+      const int32_t ncpu = class_cpus[cls];
+      for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+        const uint64_t x = s->resv_cpus[w][at];
+        const int32_t lo = 64 * w;
+        const uint64_t valid = ncpu >= lo + 64 ? ~0ull : (ncpu <= lo ? 0ull : ((1ull << (ncpu - lo)) - 1));
+        if (x & ~valid) return fail(KOORDHIP_EINVAL, "resv_cpus outside the node's CPU positions");
+        if (s->numa_free[w] && (x & s->numa_free[w][i]))
+          return fail(KOORDHIP_EINVAL, "resv_cpus must be allocated CPUs (the reservation holds them), not free ones");
+      }
+    }
+  return 0;
+}
+
 int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   c->d.rv = kh::DevResv{};
   c->dc.resv = 0;
@@ -648,6 +678,22 @@ int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     rv.ra[k] = a;
     rv.rz[k] = z;
     rv.rd[k] = d;
+  }
+  // the reserved CPUs left per slot (NodeNUMAResource RestoreReservation)
+  c->dc.resv_cpus = 0;
+  if (!e && s->resv_cpus[0] && c->numa) {  // (without NodeNUMAResource nothing reads them)
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
+      if (!s->resv_cpus[w]) e = fail(KOORDHIP_EINVAL, "resv_cpus: every word column or none");
+    std::vector<int32_t> ncpu;
+    for (int32_t k = 0; k < s->n_numa_classes && s->numa_classes; k++) ncpu.push_back(s->numa_classes[k].num_cpus);
+    if (!e) e = check_resv_cpus(s, n, slots, ncpu);
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS && !e; w++) {
+      uint64_t *m = nullptr;
+      e = dev_alloc(c, &m, sn);
+      if (!e) e = upload(c, m, s->resv_cpus[w], sn);
+      rv.rc[w] = m;
+    }
+    if (!e) c->dc.resv_cpus = 1;
   }
   rv.flags = f;
   rv.rank = rk;
@@ -1043,6 +1089,27 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     return fail(KOORDHIP_EINVAL, "update rows: resv_slots differs from the loaded snapshot's");
   if (resv_rows)
     if (int e = check_resv_rows(rows, rslots * m)) return e;
+  // reserved CPUs of the rows (NULL: none), only into a snapshot loaded with them
+  std::vector<uint64_t> zero_rc;
+  const uint64_t *rc_rows[KOORDHIP_NUMA_WORDS] = {};
+  if (resv_rows && c->numa && rows->resv_cpus[0]) {
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
+      if (!rows->resv_cpus[w]) return fail(KOORDHIP_EINVAL, "resv_cpus: every word column or none");
+    if (!numa_rows) return fail(KOORDHIP_EINVAL, "update rows with resv_cpus need the NUMA columns");
+    std::vector<int32_t> ncpu;
+    for (const auto &k : c->host_classes) ncpu.push_back(k.ncpu);
+    if (int e = check_resv_cpus(rows, m, rslots, ncpu)) return e;
+    if (!c->dc.resv_cpus) {
+      for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
+        for (int32_t j = 0; j < rslots * m; j++)
+          if (rows->resv_cpus[w][j]) return fail(KOORDHIP_EINVAL, "reserved CPUs need the resv_cpus columns at load_snapshot");
+    } else {
+      for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) rc_rows[w] = rows->resv_cpus[w];
+    }
+  } else if (resv_rows && c->dc.resv_cpus) {
+    zero_rc.assign((size_t)rslots * (size_t)m, 0ull);
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) rc_rows[w] = zero_rc.data();
+  }
   // ---- one host staging image: [idx][column 0][column 1]..., 8-B aligned
   //      segments, quantities converted to the device's exact f64
   struct Col {
@@ -1104,6 +1171,9 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
         cols.push_back({const_cast<double *>(rv.rz[k]) + q * dn, rows->resv_nz[k] + q * sm, 8, true, "resv_nz"});
         cols.push_back({rv.rd[k] + q * dn, rows->resv_allocated[k] + q * sm, 8, true, "resv_allocated"});
       }
+      if (rc_rows[0])
+        for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
+          cols.push_back({rv.rc[w] + q * dn, rc_rows[w] + q * sm, 8, false, "resv_cpus"});
     }
   }
   if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one ZoneRow element per row
@@ -1245,6 +1315,23 @@ int koordhip_read_reservations(koordhip_ctx *c, int64_t *allocated, int32_t *ass
   if (allocated && !e) e = download_q(c->d.rv.rd[1], allocated + n, n);
   if (e) return e;
   if (assigned) HIP_TRY(hipMemcpy(assigned, c->d.rv.rn, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int koordhip_read_resv_cpus(koordhip_ctx *c, uint64_t *cpus) {
+  if (!c || !cpus) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (!c->resv) return fail(KOORDHIP_ESTATE, "Reservation is not enabled");
+  const size_t n = (size_t)c->n * (size_t)(c->dc.resv ? c->d.rv.slots : 1);
+  if (n == 0) return 0;
+  if (!c->dc.resv_cpus) {
+    std::memset(cpus, 0, KOORDHIP_NUMA_WORDS * n * sizeof(uint64_t));
+    return 0;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
+    HIP_TRY(hipMemcpy(cpus + (size_t)w * n, c->d.rv.rc[w], n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -1750,6 +1837,8 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
     v.push_back({c->d.rv.rd[0], b * sl});
     v.push_back({c->d.rv.rd[1], b * sl});
     v.push_back({c->d.rv.rn, n * sl * sizeof(int32_t)});
+    if (c->dc.resv_cpus)
+      for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) v.push_back({c->d.rv.rc[w], n * sl * sizeof(uint64_t)});
   }
   return v;
 }

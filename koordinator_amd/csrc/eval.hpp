@@ -62,6 +62,7 @@ struct DevCfg {
   int32_t amp;                     // some node has a CPU amplification ratio > 1
   int32_t resv;                    // Reservation enabled and the snapshot carries reservation columns
   int32_t resv_slots;              // reservation slots per node (the NM 4 build when > 1)
+  int32_t resv_cpus;               // some reservation holds CPUs (resv_cpus columns; the NM 4 build)
   int32_t resv_b1;                 // 1 + the other plugins' maximum weighted total (resv.hpp ranking total)
   int32_t wide_keys;               // ranking totals + 1 exceed 16 bits (the resolve's key tables hold u32)
 };
@@ -424,9 +425,12 @@ __device__ __forceinline__ bool amp_filter_ok(const DevPod &p, const NV &v, cons
 // NodeNUMAResource Score (scoring.go:55-168).
 // filtered: the NodeNUMAResource Filter passed on this (pod, node) -- under a
 // required bind policy that already proved Allocate feasible (plugin.go:307-316)
+// P: the reservation-preferred CPUs of the pod on this node (resv_pref_cpus;
+// NULL or zero: none)
 template <bool Z>
 __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, const NumaRow &r,
-                                              const DevNumaClass *classes, const DevCfg &c, bool filtered = false) {
+                                              const DevNumaClass *classes, const DevCfg &c, bool filtered = false,
+                                              const uint64_t *P = nullptr) {
   if (p.flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR)) return 0;
   if (r.cls < 0) return 0;  // no CPU topology: getResourceOptions / Allocate error -> 0
   const bool most = c.numa_most != 0;  // leastResourceScorer / mostResourceScorer (scoring.go:35-53)
@@ -473,7 +477,19 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
     }
   }
   double qc = p.req[KOORDHIP_RES_CPU];
-  if (cs) {
+  if (cs && P && any4(P)) {  // (no topology policy: Reservation builds have no zones)
+    // Allocate with the preferred CPUs (free | P; P is allocated, so disjoint
+    // from the free CPUs); calculateAllocatableAndRequested then counts the
+    // allocated CPUs less P's CPUs the pod did not take (:161-166): the pod
+    // takes min(need, |P|) of them
+    const int need = p.numa_cpus, np = popc4(P);
+    if (popc4(r.fr) + np < need) return 0;
+    if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE &&
+        !numa_allocate_pref(C, r, p, P[0], P[1], P[2], P[3]))
+      return 0;
+    rc = amplify((double)(r.cnt - (np - (need < np ? need : np))) * 1000.0, r.amp);
+    qc = amplify(qc, r.amp);
+  } else if (cs) {
     const bool proven = filtered && tp == 0 && KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE;
     if (!mask && !proven && !numa_alloc_ok(C, r, p)) return 0;
     // requested cpu := the allocated cpuset size, amplified (:161-166); the
@@ -516,14 +532,15 @@ __device__ __forceinline__ int32_t eval_total(const DevPod &p, const NV &v, cons
 // ... with NodeNUMAResource
 template <bool Z>
 __device__ __forceinline__ int32_t eval_total_numa(const DevPod &p, const NV &v, const NumaRow &r,
-                                                   const DevNumaClass *classes, const DevCfg &c) {
+                                                   const DevNumaClass *classes, const DevCfg &c,
+                                                   const uint64_t *P = nullptr) {
   int32_t t = eval_total(p, v, c);
   if (t < 0) return t;
   const bool nf = (c.filt & KOORDHIP_PLUGIN_NUMA) != 0;
   if (nf && (p.flags & KOORDHIP_POD_NUMA_ERROR)) return -1;
   if (nf && c.amp && !amp_filter_ok(p, v, r)) return -1;
   if (nf && !numa_filter<Z>(p, r, classes)) return -1;
-  if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score<Z>(p, v, r, classes, c, nf);
+  if (c.score & KOORDHIP_PLUGIN_NUMA) t += c.w_numa * numa_score<Z>(p, v, r, classes, c, nf, P);
   return t;
 }
 
@@ -536,13 +553,23 @@ namespace kh {
 // ... with the Reservation plugin (NM == 3): the cycle's restore of the
 // node's reservation first (every plugin sees the restored NodeInfo), then
 // filterWithReservations and the ranking total of resv.hpp.
-template <int S>
+// RC: some reservation holds CPUs (the NM 5 build)
+template <int S, bool RC = false>
 __device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v, const NumaRowRS<S> &r,
                                                    const DevNumaClass *classes, const DevCfg &c) {
   NV w = v;
   uint32_t mm;
   const int nmatch = resv_restore(w, r, p, mm);
-  int32_t t = eval_total_numa<false>(p, w, r, classes, c);
+  int32_t t;
+  if constexpr (RC && S > 1) {
+    // the NodeNUMAResource Score reads the reserved CPUs of the reservation
+    // PreScore nominated on the node (scoring.go:86-166, plugin.go:503-524)
+    uint64_t P[NW];
+    resv_pref_cpus(r, p, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P);
+    t = eval_total_numa<false>(p, w, r, classes, c, P);
+  } else {
+    t = eval_total_numa<false>(p, w, r, classes, c);
+  }
   if (t < 0) return t;
   if (nmatch == 0)  // a required reservation affinity needs a matched reservation on the node (plugin.go:378-381)
     return ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && (p.flags & KOORDHIP_POD_RESV_AFFINITY)) ? -1 : t;
@@ -642,16 +669,20 @@ __device__ __forceinline__ void store_numa_row(const NumaRow &r, const DevNodes 
 
 // NodeNUMAResource Reserve / Release on a row (resourceManager.Update / Release,
 // node_allocation.go:76-131).
-__device__ __forceinline__ void numa_apply(NumaRow &r, const DevPod &p, const uint64_t *cpus, int sign) {
+// P (Reserve only): reservation-preferred CPUs the pod may have taken -- they
+// were allocated already (RefCount 1 -> 2: the allocated count does not grow),
+// and addPodAllocation overwrites their exclusive policy with the pod's.
+__device__ __forceinline__ void numa_apply(NumaRow &r, const DevPod &p, const uint64_t *cpus, int sign,
+                                           const uint64_t *P = nullptr) {
   const int ex = (int)KOORDHIP_NUMA_EXCLUSIVE(p.numa_policy);
   int n = 0;
 #pragma unroll
   for (int w = 0; w < NW; w++) {
-    n += __popcll(cpus[w]);
+    n += __popcll(P ? (cpus[w] & ~P[w]) : cpus[w]);
     if (sign > 0) {
       r.fr[w] &= ~cpus[w];
-      if (ex == (int)KOORDHIP_CPUEXCL_PCPU) r.ep[w] |= cpus[w];
-      if (ex == (int)KOORDHIP_CPUEXCL_NUMA) r.en[w] |= cpus[w];
+      r.ep[w] = (r.ep[w] & ~cpus[w]) | (ex == (int)KOORDHIP_CPUEXCL_PCPU ? cpus[w] : 0ull);
+      r.en[w] = (r.en[w] & ~cpus[w]) | (ex == (int)KOORDHIP_CPUEXCL_NUMA ? cpus[w] : 0ull);
     } else {
       r.fr[w] |= cpus[w];
       r.ep[w] &= ~cpus[w];
@@ -713,13 +744,17 @@ __device__ __forceinline__ void store_numa_row_wt(const NumaRow &r, const DevNod
 // false = Allocate fails (nothing applied).
 // WAVE: called by every lane of one wave with the same inputs (the resolve's
 // Reserve): the accumulator's CPU-id ordered takes run lane-parallel.
+// pref: the reservation-preferred CPUs (resv_pref_cpus), NULL or zero: none.
 template <bool Z, bool WAVE = false>
 __device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *classes, NumaRow &row, const DevPod &pod,
-                                                       uint64_t *cpus_out) {
+                                                       uint64_t *cpus_out, const uint64_t *pref = nullptr) {
   // registers for the whole replay (the references point at the caller's stack)
   NumaRow r = row;
   const DevPod p = pod;
   uint64_t cpus[NW] = {0, 0, 0, 0};
+  uint64_t P[NW] = {0, 0, 0, 0};
+  if (pref)
+    for (int w = 0; w < NW; w++) P[w] = pref[w];
   for (int w = 0; w < NW; w++) cpus_out[w] = 0;
   const bool cs = (p.flags & KOORDHIP_POD_CPUSET) != 0;
   const int tp = Z ? topo_policy(r.nflags) : 0;
@@ -727,8 +762,12 @@ __device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *class
   if (r.cls < 0) return false;
   const DevNumaClass &C = classes[r.cls];
   if (!Z || tp == 0) {
-    if (!numa_allocate_in<WAVE>(C, r, p, cpus)) return false;
-    numa_apply(r, p, cpus, +1);
+    if (cs && any4(P)) {
+      if (!numa_allocate_pref_in<WAVE>(C, r, p, P, cpus)) return false;
+    } else if (!numa_allocate_in<WAVE>(C, r, p, cpus)) {
+      return false;
+    }
+    numa_apply(r, p, cpus, +1, P);
   } else {
     uint32_t mask;
     double av[2][ZMAX];

@@ -191,7 +191,10 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
     int32_t *row = scores + (size_t)p * KOORDHIP_NPLUGINS * d.n;
     row[i] = (c.score & KOORDHIP_PLUGIN_FIT) ? fit_score(pod, v, c) : 0;
     row[(size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_LOADAWARE) ? la_score(pod, v, c) : 0;
-    row[2 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_NUMA) ? numa_score<true>(pod, v, nr, d.nu.cls, c) : 0;
+    uint64_t P[NW];  // the nominated reservation's reserved CPUs (scoring.go:82 -> plugin.go:503-524)
+    resv_pref_cpus(nr, pod, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P);
+    row[2 * (size_t)d.n + i] =
+        (c.score & KOORDHIP_PLUGIN_NUMA) ? numa_score<true>(pod, v, nr, d.nu.cls, c, false, P) : 0;
     row[3 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_BALANCED) ? bal_score(pod, v) : 0;
   }
 }
@@ -432,15 +435,17 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 #endif
 constexpr int32_t kScanPodFastNodes = 65536;
 template <int NM>
-using side_row_t = typename std::conditional<NM == 4, NumaRowR4,
+using side_row_t = typename std::conditional<NM >= 4, NumaRowR4,
                                              typename std::conditional<NM == 3, NumaRowR, NumaRow>::type>::type;
 
 // NM: 0 = no NodeNUMAResource, 1 = NodeNUMAResource, 2 = ... with
 // topology-policy nodes (the zone code is compiled only here), 3 = with the
 // Reservation plugin (NUMA side rows carry the node's reservation), 4 = ...
-// with several reservations per node (KOORDHIP_RESV_SLOTS slots per row)
+// with several reservations per node (KOORDHIP_RESV_SLOTS slots per row), 5 =
+// ... with reservations holding CPUs (the Score's preferred-CPU Allocate runs
+// the accumulator: its registers cap these kernels at 2 waves per SIMD)
 template <int R, int NM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NM >= 3 ? SCAN_WPE3 : (NM == 1 ? SCAN_WPE1 : 1)))) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NM == 5 ? 2 : (NM >= 3 ? SCAN_WPE3 : (NM == 1 ? SCAN_WPE1 : 1))))) void k_scan(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods,
                                               int32_t lo, int32_t hi, int32_t nchunks, int32_t cpx, int32_t pfast,
                                               uint16_t *__restrict__ S, int64_t s_stride,
                                               uint16_t *__restrict__ Mx, int32_t m_stride) {
@@ -489,7 +494,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NM >= 3 ? S
         side_row_t<NM> nr;
         load_numa<false>(nr, d, i, need);
         load_resv(nr, d.rv, i);
-        s[r] = eval_total_resv(pod, v, nr, cls, c) + 1;
+        s[r] = eval_total_resv<side_row_t<NM>::kSlots, NM == 5>(pod, v, nr, cls, c) + 1;
       } else if constexpr (NM != 0) {
         NumaRow nr;
         load_numa<NM == 2>(nr, d, i, need);
@@ -1475,7 +1480,7 @@ __device__ __forceinline__ uint32_t etk_kth(F each, uint32_t top, int32_t nnz, i
 }
 
 template <int NM, int VT, int R>
-__global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM >= 3 ? 4 : 1))) void k_eval_topk(
+__global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM == 5 ? 2 : (NM >= 3 ? 4 : 1)))) void k_eval_topk(
     DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods, int32_t lo, int32_t hi, int32_t nslices,
     int32_t spx, int32_t k, uint64_t *part, int32_t *pcnt, uint32_t *arrive, uint64_t *__restrict__ out,
     PipeSync *__restrict__ sy, int32_t sel_par, int32_t res_wait, int32_t stage_cap, uint64_t *dbg) {
@@ -1527,7 +1532,7 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
           side_row_t<NM> nr;
           load_numa<false>(nr, d, i, need);
           load_resv(nr, d.rv, i);
-          tot = eval_total_resv(pod, v, nr, cls, c);
+          tot = eval_total_resv<side_row_t<NM>::kSlots, NM == 5>(pod, v, nr, cls, c);
         } else if constexpr (NM != 0) {
           NumaRow nr;
           load_numa<NM == 2>(nr, d, i, need);
@@ -1899,7 +1904,7 @@ template <int NM>
 __device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const side_row_t<NM> &nr,
                                             const DevNumaClass *cls, const DevCfg &c) {
   if constexpr (NM >= 3) {
-    return eval_total_resv(p, v, nr, cls, c);
+    return eval_total_resv<side_row_t<NM>::kSlots, NM == 5>(p, v, nr, cls, c);
   } else if constexpr (NM != 0) {
     return eval_total_numa<NM == 2>(p, v, nr, cls, c);
   } else {
@@ -2633,7 +2638,13 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               const uint64_t t_acc = dbg ? stamp() : 0;
               {  // every lane: the accumulator's id-ordered takes run lane-parallel
                 NR nr = *snr;
-                okl = numa_reserve<ZONES, true>(cls, nr, pod, mc);
+                if constexpr (NM == 5) {  // the nominated reservation's reserved CPUs first
+                  uint64_t pref[NW];
+                  resv_pref_cpus(nr, pod, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? resv_matched(nr, pod) : 0u, pref);
+                  okl = numa_reserve<ZONES, true>(cls, nr, pod, mc, pref);
+                } else {
+                  okl = numa_reserve<ZONES, true>(cls, nr, pod, mc);
+                }
                 if (okl && lane == 0) mnr[rw] = nr;
               }
               if (dbg) {
@@ -2652,7 +2663,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             // Reservation Reserve: assumePod into the node's nominated reservation
             if (okr && c.resv && pod.resv_match != 0ull && lane == 0) {
               NR nr = mnr[rw];
-              resv_assume(nr, pod);
+              resv_assume(nr, pod, cpus);
               mnr[rw] = nr;
             }
           }
@@ -2950,12 +2961,14 @@ __global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, i
       return;
     }
   }
+  uint64_t m[NW] = {0, 0, 0, 0};
   if (numa_on(c) && numa_active(p, c)) {
     NumaRow r;
     load_numa_row(r, d, node);
-    uint64_t m[NW];
     if (sign > 0) {
-      if (!numa_reserve<true>(d.nu.cls, r, p, m)) {
+      uint64_t pref[NW];
+      resv_pref_cpus(rv, p, (c.resv && (c.score & KOORDHIP_PLUGIN_RESERVATION)) ? resv_matched(rv, p) : 0u, pref);
+      if (!numa_reserve<true>(d.nu.cls, r, p, m, pref)) {
         *rc = KOORDHIP_ERESERVE;  // Reserve fails: nothing is committed
         return;
       }
@@ -2973,7 +2986,7 @@ __global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, i
     for (int w = 0; w < NW; w++) cpus[w] = 0;
   }
   if (c.resv && sign > 0) {  // Reservation Reserve: assumePod into the nominated reservation
-    resv_assume(rv, p);
+    resv_assume(rv, p, m);
     store_resv(rv, d.rv, node);
   }
   NV v;
@@ -3067,7 +3080,12 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
 #define KH_SCAN(RR, NN)                                                                                            \
   hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, \
                      pfast, S, s_stride, Mx, m_stride)
-  if (nm == 4) {
+  if (nm == 5) {
+    switch (R) {
+      case 4: KH_SCAN(4, 5); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (nm == 4) {
     switch (R) {
       case 4: KH_SCAN(4, 4); break;
       default: return hipErrorInvalidValue;
@@ -3223,7 +3241,7 @@ hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *po
                      ((nm != 0 && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0);
   const int32_t spx = (nslices + 7) / 8;
   const int32_t blocks = 8 * spx * n_pods;
-  static bool attr[5][3] = {};
+  static bool attr[6][3] = {};
   const int vi = VT == 8 ? 0 : (VT == 16 ? 1 : 2);
 #define KH_ETK(NN, VV, RR)                                                                                          \
   do {                                                                                                              \
@@ -3254,6 +3272,9 @@ hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *po
     case 16: KH_ETK(4, 8, 4); break;
     case 17: KH_ETK(4, 16, 4); break;
     case 18: KH_ETK(4, 32, 4); break;
+    case 20: KH_ETK(5, 8, 4); break;
+    case 21: KH_ETK(5, 16, 4); break;
+    case 22: KH_ETK(5, 32, 4); break;
     default: return hipErrorInvalidValue;
   }
 #undef KH_ETK
@@ -3281,13 +3302,13 @@ hipError_t launch_topk_merge(const uint64_t *in, int64_t pod_stride, int64_t lis
 static inline int32_t list_stride(int32_t k) { return (k + 7) & ~7; }
 
 int side_mode(const DevCfg &c) {
-  if (c.resv) return c.resv_slots > 1 ? 4 : 3;
+  if (c.resv) return c.resv_cpus ? 5 : (c.resv_slots > 1 ? 4 : 3);
   if (!((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA)) return 0;
   return c.zones ? 2 : 1;
 }
 
 static int32_t side_row_bytes(int nm) {
-  return nm == 4 ? (int32_t)sizeof(NumaRowR4) : nm == 3 ? (int32_t)sizeof(NumaRowR) : (nm ? (int32_t)sizeof(NumaRow) : 0);
+  return nm >= 4 ? (int32_t)sizeof(NumaRowR4) : nm == 3 ? (int32_t)sizeof(NumaRowR) : (nm ? (int32_t)sizeof(NumaRow) : 0);
 }
 
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, int nm, int32_t lag) {
@@ -3317,14 +3338,16 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag, wide);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag, wide);
   if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag, wide);
-  static bool attr[10] = {};
+  static bool attr[12] = {};
   const int ai = nm * 2 + (dbg ? 1 : 0);
   if (!attr[ai]) {
-    const void *f = dbg ? (nm == 4   ? (const void *)k_resolve<4, true>
+    const void *f = dbg ? (nm == 5   ? (const void *)k_resolve<5, true>
+                           : nm == 4 ? (const void *)k_resolve<4, true>
                            : nm == 3 ? (const void *)k_resolve<3, true>
                            : nm == 2 ? (const void *)k_resolve<2, true>
                                      : (nm == 1 ? (const void *)k_resolve<1, true> : (const void *)k_resolve<0, true>))
-                        : (nm == 4   ? (const void *)k_resolve<4, false>
+                        : (nm == 5   ? (const void *)k_resolve<5, false>
+                           : nm == 4 ? (const void *)k_resolve<4, false>
                            : nm == 3 ? (const void *)k_resolve<3, false>
                            : nm == 2 ? (const void *)k_resolve<2, false>
                                      : (nm == 1 ? (const void *)k_resolve<1, false> : (const void *)k_resolve<0, false>));
@@ -3342,7 +3365,9 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
     KH_RESOLVE_D(NN, true);  \
   else                       \
     KH_RESOLVE_D(NN, false)
-  if (nm == 4)
+  if (nm == 5)
+    KH_RESOLVE(5);
+  else if (nm == 4)
     KH_RESOLVE(4);
   else if (nm == 3)
     KH_RESOLVE(3);

@@ -76,9 +76,16 @@ struct NumaRow {
   // row there, read only by the zone code); NodeAllocation.allocatedResources
   // is mutable and travels with the row, [cpu milli, memory][zone]
   const double *za;
-  double zu[2][ZMAX];
+  union {
+    double zu[2][ZMAX];
+    // Reservation builds (no topology-policy nodes, so no zones): the reserved
+    // CPUs left in each reservation slot of the node (RestoreReservation,
+    // nodenumaresource/reservation.go:76-113), see resv.hpp
+    uint64_t rcm[KOORDHIP_RESV_SLOTS][NW];
+  };
   double amp;  // CPU amplification ratio (1 unless loaded)
 };
+static_assert(sizeof(uint64_t[KOORDHIP_RESV_SLOTS][NW]) == sizeof(double[2][ZMAX]), "rcm shares the zone row's bytes");
 
 struct DevNuma {
   const DevNumaClass *cls;
@@ -102,6 +109,7 @@ struct DevResv {
   int32_t *rn;            // len(AssignedPods)
   int32_t slots;          // reservation slots per node: the columns hold slots x stride values, slot-major
   int32_t stride;         // = the node count
+  uint64_t *rc[KOORDHIP_NUMA_WORDS];  // reserved CPUs left per slot (RestoreReservation); NULL: none hold CPUs
 };
 
 struct ZoneRow {  // one node's [2][ZMAX] zone row (update_nodes scatter element)
@@ -782,6 +790,52 @@ __device__ __forceinline__ bool numa_allocate_in(const DevNumaClass &C, const Nu
   if (!required_ok(C, r, p, R)) return false;
   for (int w = 0; w < NW; w++) cpus[w] = R[w];
   return true;
+}
+
+// Allocate with reservation-preferred CPUs P (getResourceOptions' preferredCPUs,
+// plugin.go:503-524; no hint): the available set is free | P -- P's RefCount
+// drops to 0 in getAvailableCPUs, so its exclusive policy leaves allocateInfo
+// too (node_allocation.go:133-153) -- and takePreferredCPUs
+// (cpu_accumulator.go:29-85) takes min(need, |P|) CPUs from P, then the rest
+// from the available CPUs outside P, each by its own accumulator over the
+// same allocateInfo; the required bind policy holds for the union
+// (resource_manager.go:244-326).
+template <bool WAVE = false>
+__device__ __forceinline__ bool numa_allocate_pref_in(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                                      const uint64_t *P, uint64_t *cpus) {
+  for (int w = 0; w < NW; w++) cpus[w] = 0;
+  const int need = p.numa_cpus;
+  uint64_t A[NW];
+  for (int w = 0; w < NW; w++) A[w] = r.fr[w] | P[w];
+  if (popc4(A) < need) return false;
+  NumaRow q = r;
+  for (int w = 0; w < NW; w++) {
+    q.ep[w] &= ~P[w];
+    q.en[w] &= ~P[w];
+    A[w] &= ~P[w];
+  }
+  const int np = popc4(P);
+  const int n1 = need < np ? need : np;
+  uint64_t R1[NW] = {0, 0, 0, 0}, R2[NW] = {0, 0, 0, 0};
+  if (n1 > 0 && !acc_run<WAVE>(C, q, p, P, n1, R1)) return false;
+  if (need > n1 && !acc_run<WAVE>(C, q, p, A, need - n1, R2)) return false;
+  for (int w = 0; w < NW; w++) R1[w] |= R2[w];
+  if (!required_ok(C, r, p, R1)) return false;
+  for (int w = 0; w < NW; w++) cpus[w] = R1[w];
+  return true;
+}
+
+__device__ __forceinline__ bool any4(const uint64_t *m) { return (m[0] | m[1] | m[2] | m[3]) != 0ull; }
+
+// Score-time Allocate with reservation-preferred CPUs (outlined: only cpuset
+// pods on nodes whose nominated reservation holds CPUs get here)
+__device__ __attribute__((noinline)) bool numa_allocate_pref(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
+                                                             uint64_t P0, uint64_t P1, uint64_t P2, uint64_t P3) {
+  const NumaRow rl = r;
+  const DevPod pl = p;
+  const uint64_t P[NW] = {P0, P1, P2, P3};
+  uint64_t o[NW];
+  return numa_allocate_pref_in(C, rl, pl, P, o);
 }
 
 // The outlined entry points copy their by-reference inputs into registers

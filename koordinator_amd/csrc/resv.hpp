@@ -40,9 +40,12 @@ struct ResvSlot {
 };
 static_assert(sizeof(ResvSlot) == 64, "reservation slot = 64 B");
 
-// A NUMA side row with the node's reservations (NM >= 3 builds).
+// A NUMA side row with the node's reservations (NM >= 3 builds).  The
+// several-slot rows (NM 4, which every snapshot with CPU-holding reservations
+// runs) keep each slot's reserved CPUs in NumaRow::rcm.
 template <int S>
 struct NumaRowRS : NumaRow {
+  static constexpr int kSlots = S;
   ResvSlot rs[S];
 };
 using NumaRowR = NumaRowRS<1>;
@@ -72,6 +75,11 @@ __device__ __forceinline__ void load_resv(NumaRowRS<S> &r, const DevResv &d, int
         x.rz[k] = d.rz[k][at];
       }
     }
+    if constexpr (S > 1) {
+      const bool on = d.rc[0] != nullptr && (x.rf & KOORDHIP_RESV_PRESENT);
+#pragma unroll
+      for (int w = 0; w < NW; w++) r.rcm[q][w] = on ? d.rc[w][at] : 0ull;
+    }
   }
 }
 
@@ -85,6 +93,11 @@ __device__ __forceinline__ void store_resv(const NumaRowRS<S> &r, const DevResv 
     d.rd[0][at] = x.rd[0];
     d.rd[1][at] = x.rd[1];
     d.rn[at] = x.rn;
+    if constexpr (S > 1) {
+      if (d.rc[0])
+#pragma unroll
+        for (int w = 0; w < NW; w++) d.rc[w][at] = r.rcm[q][w];
+    }
   }
 }
 template <int S>
@@ -97,6 +110,11 @@ __device__ __forceinline__ void store_resv_wt(const NumaRowRS<S> &r, const DevRe
     st_wt(&d.rd[0][at], x.rd[0]);
     st_wt(&d.rd[1][at], x.rd[1]);
     st_wt(&d.rn[at], x.rn);
+    if constexpr (S > 1) {
+      if (d.rc[0])
+#pragma unroll
+        for (int w = 0; w < NW; w++) st_wt(&d.rc[w][at], r.rcm[q][w]);
+    }
   }
 }
 
@@ -285,9 +303,11 @@ __device__ __forceinline__ int resv_node_rank(const NumaRowRS<S> &r, uint32_t mm
 }
 
 // Reserve: AddAssignedPod to the nominated reservation (Allocated += the
-// pod's requests masked to ResourceNames).
+// pod's requests masked to ResourceNames); the pod's CPUs leave the slot's
+// reserved CPUs (the next cycle's RestoreReservation subtracts the assigned
+// pods' cpusets, reservation.go:90-97).
 template <int S>
-__device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p) {
+__device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p, const uint64_t *cpus) {
   const int q = resv_nominate(p, r, resv_matched(r, p));
   if (q < 0) return;
   ResvSlot &x = r.rs[q];
@@ -295,6 +315,33 @@ __device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p) {
   for (int k = 0; k < 2; k++)
     if (rkey(x.rf, k) && pkey(p, k)) x.rd[k] += p.req[k];
   x.rn += 1;
+  if constexpr (S > 1) {
+#pragma unroll
+    for (int w = 0; w < NW; w++) r.rcm[q][w] &= ~cpus[w];
+  } else {
+    (void)cpus;
+  }
+}
+
+// The reservation-preferred CPUs of a pod on the node (getReservationReservedCPUs,
+// nodenumaresource/plugin.go:503-524): the reserved CPUs left in the nominated
+// reservation, for a pod AllowUseCPUSet lets restore them (PreRestoreReservation
+// :68-74; only cpuset pods -- requestCPUBind -- read them).  Zero: none.
+template <int S>
+__device__ __forceinline__ void resv_pref_cpus(const NumaRowRS<S> &r, const DevPod &p, uint32_t mm, uint64_t *P) {
+#pragma unroll
+  for (int w = 0; w < NW; w++) P[w] = 0ull;
+  if constexpr (S > 1) {
+    if (!(p.flags & KOORDHIP_POD_CPUSET) || (p.flags & KOORDHIP_POD_NUMA_SKIP) || mm == 0u) return;
+    const int q = resv_nominate(p, r, mm);
+    if (q < 0) return;
+#pragma unroll
+    for (int w = 0; w < NW; w++) P[w] = r.rcm[q][w];
+  } else {
+    (void)r;
+    (void)p;
+    (void)mm;
+  }
 }
 
 // a slot of the node holds an Available reservation whose owner group `p` matches

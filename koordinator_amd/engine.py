@@ -140,7 +140,9 @@ class PlacementEngine:
         al = np.zeros((2, n), np.int64)
         asg = np.zeros(n, np.int32)
         abi.check(self.lib, self.lib.koordhip_read_reservations(self._ctx, abi.ptr(al, C.c_int64), abi.ptr(asg, C.c_int32)))
-        return {"allocated": al, "assigned": asg}
+        rc = np.zeros((abi.NUMA_WORDS, n), np.uint64)
+        abi.check(self.lib, self.lib.koordhip_read_resv_cpus(self._ctx, abi.ptr(rc, C.c_uint64)))
+        return {"allocated": al, "assigned": asg, "cpus": rc}
 
     def fetch_cpusets(self, n: int) -> np.ndarray:
         out = np.zeros((n, abi.NUMA_WORDS), np.uint64)

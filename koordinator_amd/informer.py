@@ -283,10 +283,27 @@ class Informer:
                     node.labels or {}, prof.numa.default_most_allocated, frozen=frozen)
 
     # ---- Reservation events (reservation/cache.go:117-252) ------------------------------------------
+    def _numa_reservation(self, r: rv.Reservation, present: bool):
+        """The reserve pod's cpuset in NodeAllocation (ReservationToPodEventHandler ->
+        podEventHandler, nodenumaresource/pod_eventhandler.go:40-50,94-144)."""
+        uid = r.uid or f"reservation/{r.name}"
+        if not r.node_name:
+            return
+        alloc = self._alloc.setdefault(r.node_name, nm.NodeAllocation())
+        opts = self._topo.get(r.node_name)
+        if present and r.is_available() and r.cpus and opts is not None and opts.topology is not None:
+            alloc.update(uid, list(r.cpus), r.cpu_exclusive, [])
+        else:
+            alloc.release(uid)
+        self._dirty.add(r.node_name)
+
     def on_reservation(self, r: rv.Reservation):
         """Add or update."""
         old = self.reservations.get(r.name)
+        if old is not None:
+            self._numa_reservation(old, False)
         self.reservations[r.name] = r
+        self._numa_reservation(r, True)
         for nn in ({old.node_name} if old is not None else set()) | {r.node_name}:
             if nn:
                 self._dirty.add(nn)
@@ -296,6 +313,8 @@ class Informer:
 
     def on_reservation_delete(self, name: str):
         old = self.reservations.pop(name, None)
+        if old is not None:
+            self._numa_reservation(old, False)
         if old is not None and old.node_name:
             self._dirty.add(old.node_name)
 

@@ -284,6 +284,19 @@ class Reservation:
     allocate_policy: str = POLICY_DEFAULT
     unschedulable: bool = False
     deleting: bool = False                                         # DeletionTimestamp set
+    # NodeNUMAResource: the reserve pod's cpuset allocation (its resource-status
+    # annotation, held in NodeAllocation under the reservation's UID) and the
+    # union of its AssignedPods' cpusets (RestoreReservation,
+    # nodenumaresource/reservation.go:84-104)
+    cpus: List[int] = field(default_factory=list)
+    assigned_cpus: List[int] = field(default_factory=list)
+    cpu_exclusive: str = ""                                        # the reserve pod's preferredCPUExclusivePolicy
+
+    def reserved_cpus(self) -> List[int]:
+        """RestoreReservation's reservedCPUs of this reservation: its allocated
+        CPUs less its assigned pods' (reservation.go:84-104)."""
+        taken = set(self.assigned_cpus)
+        return sorted(c for c in set(self.cpus) if c not in taken)
 
     def is_available(self) -> bool:
         return bool(self.node_name) and self.phase == "Available"
@@ -474,6 +487,35 @@ def _reservation_slot(table: NodeTable, i: int, q: int, r: Reservation, index: "
     col("resv_allocated0")[i] = _q2(r.allocated, k8s.CPU) if k8s.CPU in names else 0
     col("resv_allocated1")[i] = _q2(r.allocated, k8s.MEMORY) if k8s.MEMORY in names else 0
     col("resv_assigned")[i] = r.assigned
+    m = reserved_cpu_mask(table, i, r)
+    for w in range(abi.NUMA_WORDS):
+        col(f"resv_cpus{w}")[i] = m[w]
+
+
+def reserved_cpu_mask(table: NodeTable, i: int, r: Reservation) -> List[int]:
+    """The resv_cpus words of reservation r on node i: its reserved CPUs as
+    core-major positions of the node's topology class.  A node without a (valid)
+    CPU topology holds no allocation (resourceManager.Update skips it,
+    resource_manager.go:328-339), so nothing is reserved there."""
+    words = [0] * abi.NUMA_WORDS
+    cpus = r.reserved_cpus()
+    cls = int(table["numa_class"][i])
+    if not cpus or cls < 0 or cls >= len(table.numa_classes):
+        return words
+    if (int(table["numa_flags"][i]) >> abi.NODE_NUMA_POLICY_SHIFT) & 3:
+        raise ReservationError(f"reservation {r.name}: reserved CPUs on a NUMA topology-policy node are not supported")
+    rec = table.numa_classes[cls]
+    pos_of = {int(rec["cpu_id"][p]): p for p in range(int(rec["num_cpus"]))}
+    for c in cpus:
+        p = pos_of.get(c)
+        if p is None:
+            raise ReservationError(f"reservation {r.name}: CPU {c} is not in node {i}'s topology")
+        words[p >> 6] |= 1 << (p & 63)
+    for w in range(abi.NUMA_WORDS):
+        if words[w] & int(table[f"numa_free{w}"][i]):
+            raise ReservationError(f"reservation {r.name}: its CPUs must be allocated on node {i} (NodeAllocation "
+                                   "holds the reserve pod's cpuset)")
+    return words
 
 
 def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservations: Sequence[Reservation],

@@ -27,16 +27,19 @@ U32_COLS = ["resv_flags",   # KOORDHIP_RESV_* (0 = no reservation on the node)
             "static_allow"]  # static node filters: allowed pod static classes (all ones = every class)
 U64_COLS = ([f"numa_free{w}" for w in range(abi.NUMA_WORDS)] + [f"numa_excl_pcpu{w}" for w in range(abi.NUMA_WORDS)]
             + [f"numa_excl_numa{w}" for w in range(abi.NUMA_WORDS)])
+# per reservation slot: the reserved CPUs not held by its assigned pods
+# (NodeNUMAResource RestoreReservation, nodenumaresource/reservation.go:76-113)
+RESV_CPU_COLS = [f"resv_cpus{w}" for w in range(abi.NUMA_WORDS)]
 # NUMA zone resources, [n][2][NUMA_MAX_NODES] int64 per column (cpu milli, memory bytes)
 ZONE_COLS = ["numa_zone_alloc", "numa_zone_used"]
 F64_COLS = ["numa_amp_cpu"]   # CPU amplification ratio (1.0 = none)
-ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS + ZONE_COLS + F64_COLS + U32_COLS
+ALL_COLS = I64_COLS + I32_COLS + U8_COLS + U64_COLS + ZONE_COLS + F64_COLS + U32_COLS + RESV_CPU_COLS
 # NodeNUMAResource mutable columns (advanced by cpuset / NUMA-zone Reserves)
 NUMA_MUTABLE = [c for c in U64_COLS] + ["numa_alloc_cnt", "numa_zone_used"]
 # Reservation columns (the node's Available reservation) and the mutable ones
 RESV_COLS = ["resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1",
-             "resv_allocated0", "resv_allocated1", "resv_assigned"]
-RESV_MUTABLE = ["resv_allocated0", "resv_allocated1", "resv_assigned"]
+             "resv_allocated0", "resv_allocated1", "resv_assigned"] + RESV_CPU_COLS
+RESV_MUTABLE = ["resv_allocated0", "resv_allocated1", "resv_assigned"] + RESV_CPU_COLS
 
 
 def slot_col(col: str, s: int) -> str:
@@ -53,7 +56,7 @@ def _dtype(col: str):
         return np.int32
     if col in U8_COLS:
         return np.uint8
-    if col in U64_COLS:
+    if col in U64_COLS or col in RESV_CPU_COLS:
         return np.uint64
     if col in U32_COLS:
         return np.uint32
@@ -176,6 +179,9 @@ class NodeTable:
             s.resv_allocated[k] = rc[f"resv_allocated{k}"].ctypes.data_as(C.POINTER(C.c_int64))
         s.resv_assigned = rc["resv_assigned"].ctypes.data_as(C.POINTER(C.c_int32))
         s.resv_slots = self.resv_slots if self.resv_slots > 1 else 0
+        if any(rc[c].any() for c in RESV_CPU_COLS):   # NULL: no reservation holds CPUs
+            for w in range(abi.NUMA_WORDS):
+                s.resv_cpus[w] = rc[f"resv_cpus{w}"].ctypes.data_as(C.POINTER(C.c_uint64))
         s._keep = rc
         s.static_allow = self.cols["static_allow"].ctypes.data_as(C.POINTER(C.c_uint32))
         return s

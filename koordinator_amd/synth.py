@@ -295,6 +295,60 @@ def add_reservations(t: NodeTable, spec: ResvSpec, seed: int = SEED) -> NodeTabl
     return t
 
 
+def add_reserved_cpus(t: NodeTable, frac: float = 0.6, partial_frac: float = 0.4, excl_frac: float = 0.3,
+                      seed: int = SEED) -> NodeTable:
+    """Give a `frac` share of the reservations on NUMA nodes (a CPU topology, no
+    topology policy) a cpuset: ~Allocatable cpu / 1000 CPUs of the node's free
+    ones, whole free cores first (the reserve pod's allocation in NodeAllocation,
+    some with an exclusive policy); on a `partial_frac` share of those with
+    assigned pods some of the CPUs went to the assigned pods (still allocated,
+    no longer reserved: RestoreReservation, nodenumaresource/reservation.go:84-104).
+    Call after add_numa and add_reservations."""
+    n, s = t.n, seed + 17
+    rnd = splitmix64(s, n, 80)
+    for i in range(n):
+        cls = int(t["numa_class"][i])
+        if cls < 0 or (int(t["numa_flags"][i]) >> abi.NODE_NUMA_POLICY_SHIFT) & 3:
+            continue
+        rng = np.random.default_rng(int(rnd[i]))
+        rec = t.numa_classes[cls]
+        ncpu, cpc = int(rec["num_cpus"]), int(rec["cpus_per_core"])
+        for q in range(t.resv_slots):
+            if not (int(t[slot_col("resv_flags", q)][i]) & abi.RESV_PRESENT) or rng.random() >= frac:
+                continue
+            free = [int(t[f"numa_free{w}"][i]) for w in range(abi.NUMA_WORDS)]
+            isfree = lambda p: (free[p >> 6] >> (p & 63)) & 1
+            want = max(1, int(t[slot_col("resv_alloc0", q)][i]) // 1000)
+            start = int(rng.integers(0, ncpu // cpc))
+            order = [(start + k) % (ncpu // cpc) for k in range(ncpu // cpc)]
+            full = [c for c in order if all(isfree(c * cpc + x) for x in range(cpc))]
+            pick = [c * cpc + x for c in full for x in range(cpc)][:want]
+            if len(pick) < want:
+                pick += [p for p in range(ncpu) if isfree(p) and p not in pick][:want - len(pick)]
+            if not pick:
+                continue
+            r = rng.random()
+            ex = "PCPULevel" if r < excl_frac / 2 else ("NUMANodeLevel" if r < excl_frac else "")
+            m = [0] * abi.NUMA_WORDS
+            for p in pick:
+                m[p >> 6] |= 1 << (p & 63)
+            for w in range(abi.NUMA_WORDS):
+                t[f"numa_free{w}"][i] = np.uint64(free[w] & ~m[w] & 0xFFFFFFFFFFFFFFFF)
+                if ex == "PCPULevel":
+                    t[f"numa_excl_pcpu{w}"][i] |= np.uint64(m[w])
+                elif ex == "NUMANodeLevel":
+                    t[f"numa_excl_numa{w}"][i] |= np.uint64(m[w])
+            t["numa_alloc_cnt"][i] += len(pick)
+            if int(t[slot_col("resv_assigned", q)][i]) > 0 and rng.random() < partial_frac and len(pick) > 1:
+                gone = rng.choice(len(pick), size=int(rng.integers(1, len(pick) // 2 + 1)), replace=False)
+                for g in gone:
+                    p = pick[int(g)]
+                    m[p >> 6] &= ~(1 << (p & 63))
+            for w in range(abi.NUMA_WORDS):
+                t[slot_col(f"resv_cpus{w}", q)][i] = np.uint64(m[w])
+    return t
+
+
 @dataclass
 class StaticSpec:
     """Node labels / taints / cordons and pod nodeSelector / required node

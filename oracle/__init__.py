@@ -41,6 +41,7 @@ class OrcState(C.Structure):
         ("cpuset_out", C.c_void_p),
         ("resv_allocated", C.POINTER(C.c_int64) * 2),
         ("resv_assigned", C.POINTER(C.c_int32)),
+        ("resv_cpus", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
     ]
 
 
@@ -177,8 +178,10 @@ class Oracle:
         """Allocated [2][S n], assigned [S n] (S = the table's reservation slots, slot-major)."""
         n = self.n * max(1, self.table.resv_slots)
         a = lambda p: np.ctypeslib.as_array(p, shape=(n,)).copy()
+        rc = (np.stack([a(self.st.resv_cpus[w]) for w in range(abi.NUMA_WORDS)]) if self.st.resv_cpus[0]
+              else np.zeros((abi.NUMA_WORDS, n), np.uint64))
         return {"allocated": np.stack([a(self.st.resv_allocated[0]), a(self.st.resv_allocated[1])]),
-                "assigned": a(self.st.resv_assigned)}
+                "assigned": a(self.st.resv_assigned), "cpus": rc}
 
     def resv_restore_delta(self, pod: np.ndarray, node: int):
         """(requested delta [cpu, mem], non-zero delta [cpu, mem], pod-count delta) of the restore."""

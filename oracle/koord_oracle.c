@@ -136,6 +136,8 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
   st->resv_assigned = (int32_t *)calloc((size_t)(rn > 0 ? rn : 1), sizeof(int32_t));
   if (soa->resv_flags && soa->resv_assigned && st->resv_assigned)
     memcpy(st->resv_assigned, soa->resv_assigned, sizeof(int32_t) * (size_t)rn);
+  if (soa->resv_flags && soa->resv_cpus[0])
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) st->resv_cpus[w] = (uint64_t *)dup64((const int64_t *)soa->resv_cpus[w], rn);
   if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned) return -1;
   orc_la_flags(soa, n, st->flags);
   return 0;
@@ -161,6 +163,7 @@ void orc_state_free(orc_state *st) {
   free(st->resv_allocated[0]);
   free(st->resv_allocated[1]);
   free(st->resv_assigned);
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) free(st->resv_cpus[w]);
   memset(st, 0, sizeof(*st));
 }
 
@@ -399,9 +402,15 @@ int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *po
   /* Unreserve of a pod one of its node's reservations could have taken: whether
    * it did (state.assumed, plugin.go:591-597) is not passed back */
   if (rv && sign < 0 && orc_resv_node_matchable(st, pod, i)) return KOORDHIP_EINVAL;
+  uint64_t got[KOORDHIP_NUMA_WORDS] = {0, 0, 0, 0};
   if (numa_on(cfg) && orc_numa_reserve_active(st, pod, i)) {
     if (sign > 0) {
-      if (!orc_numa_reserve(st, pod, i, cpus)) return KOORDHIP_ERESERVE;
+      /* the reserved CPUs of the reservation PreScore nominated (RestoreReservation state) */
+      uint64_t pref[KOORDHIP_NUMA_WORDS];
+      orc_resv_pref(cfg, st, pod, i, pref);
+      if (!orc_numa_reserve(st, pod, i, got, pref)) return KOORDHIP_ERESERVE;
+      if (cpus)
+        for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = got[w];
     } else if (st->soa->numa_flags && KOORDHIP_NODE_NUMA_POLICY(st->soa->numa_flags[i]) != KOORDHIP_NUMA_TOPO_NONE) {
       return KOORDHIP_EINVAL; /* the zone amounts of an earlier Reserve are not passed back */
     } else if (cpus) {
@@ -410,7 +419,7 @@ int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *po
   } else if (cpus && sign > 0) {
     for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
   }
-  if (rv && sign > 0) orc_resv_assume(st, pod, i); /* Reservation Reserve: assumePod (plugin.go:550-573) */
+  if (rv && sign > 0) orc_resv_assume(st, pod, i, got); /* Reservation Reserve: assumePod (plugin.go:550-573) */
   for (int r = 0; r < KOORDHIP_NRES; r++) st->requested[r][i] += sign * pod->req[r];
   st->nz_cpu_m[i] += sign * pod->nz_cpu_m;
   st->nz_mem[i] += sign * pod->nz_mem;

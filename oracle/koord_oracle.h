@@ -56,6 +56,9 @@ typedef struct orc_state {
   /* Reservation: Allocated (cpu milli, memory) and len(AssignedPods) of each node's reservation */
   int64_t *resv_allocated[2];
   int32_t *resv_assigned;
+  /* NodeNUMAResource RestoreReservation: the reserved CPUs each reservation
+   * slot has left ([WORDS][slots x n]; NULL when the snapshot has none) */
+  uint64_t *resv_cpus[KOORDHIP_NUMA_WORDS];
 } orc_state;
 
 int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n);
@@ -79,7 +82,8 @@ int64_t orc_amplify(int64_t origin, double ratio);
 int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t node);
 int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
 int orc_numa_reserve_active(const orc_state *st, const koordhip_pod *pod, int32_t i);
-int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
+/* pref: the reservation-preferred CPUs (orc_resv_pref), NULL = none */
+int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out, const uint64_t *pref);
 void orc_numa_release(orc_state *st, int32_t node, const uint64_t *cpus);
 /* takeCPUs on one topology (cpu_accumulator.go:87-232), maxRefCount 1; 1 = ok. */
 int orc_take_cpus(const koordhip_numa_class *t, const uint64_t *avail, const uint64_t *excl_pcpu,
@@ -131,7 +135,11 @@ void orc_resv_restore(orc_state *st, const koordhip_pod *pod, int sign);
 int orc_resv_filter(const orc_state *st, const koordhip_pod *pod, int32_t i);
 int orc_resv_nominated(const orc_state *st, const koordhip_pod *pod, int32_t i);
 int64_t orc_resv_score(const orc_state *st, const koordhip_pod *pod, int32_t i);
-void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i);
+void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i, const uint64_t *cpus);
+/* getReservationReservedCPUs (nodenumaresource/plugin.go:503-524): the reserved
+ * CPUs left in the reservation PreScore nominated on node i, for a cpuset pod;
+ * zero when none */
+void orc_resv_pref(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *P);
 void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int32_t *feasible, int32_t nf,
                          int64_t *norm);
 int64_t orc_resv_rank_total(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i,

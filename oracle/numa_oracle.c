@@ -716,11 +716,45 @@ int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t i,
   return alloc_by_hint(st, pod, i, M, best.mask, zones);
 }
 
-/* allocateCPUSet (resource_manager.go:244-326) with no reservation: zones =
- * NULL for a nil hint, else the pod's per-zone allocation from
- * allocateResourcesByHint -- every zone holding a non-zero amount takes
- * floor(cpu / 1000) CPUs from its own available CPUs (:264-295). */
-static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i, const int64_t *zones, uint64_t *out) {
+/* takePreferredCPUs (cpu_accumulator.go:29-85): the preferred CPUs among the
+ * available ones first (at most need of them), then the rest from the
+ * available CPUs outside the preferred set; both accumulators see the same
+ * allocateInfo (ep / en). */
+static int take_preferred(const koordhip_numa_class *t, const uint64_t *avail_in, const uint64_t *pref,
+                          const uint64_t *ep, const uint64_t *en, int need, int policy, int excl, int most,
+                          uint64_t *out) {
+  uint64_t avail[KOORDHIP_NUMA_WORDS], pr[KOORDHIP_NUMA_WORDS], got[KOORDHIP_NUMA_WORDS];
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    out[w] = 0;
+    avail[w] = avail_in[w];
+    pr[w] = avail[w] & (pref ? pref[w] : 0); /* preferredCPUs = availableCPUs.Intersection(preferredCPUs) :41 */
+  }
+  if (popc(pr) > 0) {
+    const int needed = need > popc(pr) ? popc(pr) : need; /* :43-46 */
+    if (!orc_take_cpus(t, pr, ep, en, needed, policy, excl, most, got)) return 0;
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+      out[w] = got[w];
+      avail[w] &= ~pr[w]; /* availableCPUs.Difference(preferredCPUs) :61 */
+    }
+    need -= popc(got);
+  }
+  if (need > 0) { /* :64-82 */
+    if (!orc_take_cpus(t, avail, ep, en, need, policy, excl, most, got)) return 0;
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) out[w] |= got[w];
+  }
+  return 1;
+}
+
+/* allocateCPUSet (resource_manager.go:244-326): zones = NULL for a nil hint,
+ * else the pod's per-zone allocation from allocateResourcesByHint -- every
+ * zone holding a non-zero amount takes floor(cpu / 1000) CPUs from its own
+ * available CPUs (:264-295).  pref: the reservation-preferred CPUs (NULL =
+ * none): GetAvailableCPUs(preferredCPUs) drops their RefCount 1 -> 0, so they
+ * join the available CPUs and leave allocateInfo (node_allocation.go:133-153;
+ * Reservation builds have no topology-policy nodes, so pref comes with no
+ * zones). */
+static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i, const int64_t *zones, uint64_t *out,
+                        const uint64_t *pref) {
   const koordhip_node_soa *s = st->soa;
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) out[w] = 0;
   int cls = s->numa_class[i];
@@ -728,9 +762,10 @@ static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i,
   const koordhip_numa_class *t = &s->numa_classes[cls];
   uint64_t avail[KOORDHIP_NUMA_WORDS], ep[KOORDHIP_NUMA_WORDS], en[KOORDHIP_NUMA_WORDS];
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
-    avail[w] = st->numa_free[w][i];
-    ep[w] = st->numa_excl_pcpu[w][i];
-    en[w] = st->numa_excl_numa[w][i];
+    const uint64_t p = pref ? pref[w] : 0;
+    avail[w] = st->numa_free[w][i] | p;
+    ep[w] = st->numa_excl_pcpu[w][i] & ~p;
+    en[w] = st->numa_excl_numa[w][i] & ~p;
   }
   const int need = pod->numa_cpus;
   const int required = KOORDHIP_NUMA_REQUIRED(pod->numa_policy) != KOORDHIP_CPUBIND_NONE;
@@ -757,7 +792,7 @@ static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i,
       }
     }
     if (got != need) return 0; /* :290-293 */
-  } else if (!orc_take_cpus(t, avail, ep, en, need, policy, excl, most, out)) {
+  } else if (!take_preferred(t, avail, pref, ep, en, need, policy, excl, most, out)) {
     return 0;
   }
   if (required) { /* satisfiedRequiredCPUBindPolicy :442-463 */
@@ -777,7 +812,7 @@ static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i,
 /* resourceManager.Allocate for a cpuset pod with an empty hint and no
  * reservation (resource_manager.go:142-164). */
 int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *out) {
-  return alloc_cpuset(st, pod, i, NULL, out);
+  return alloc_cpuset(st, pod, i, NULL, out, NULL);
 }
 
 
@@ -791,7 +826,7 @@ static int policy_allocate(const orc_state *st, const koordhip_pod *pod, int32_t
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
   if (!orc_numa_hint_alloc(st, pod, i, &mask, &nil, &admit, zones)) return 0;
   *has_zones = !nil;
-  if (pod->flags & KOORDHIP_POD_CPUSET) return alloc_cpuset(st, pod, i, nil ? NULL : zones, cpus);
+  if (pod->flags & KOORDHIP_POD_CPUSET) return alloc_cpuset(st, pod, i, nil ? NULL : zones, cpus, NULL);
   return 1;
 }
 
@@ -903,11 +938,12 @@ int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const ko
     return numa_least_allocated(cfg, rcpu + pod->req[KOORDHIP_RES_CPU], acpu, rmem + pod->req[KOORDHIP_RES_MEM], amem);
   }
   int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES];
-  uint64_t cpus[KOORDHIP_NUMA_WORDS];
+  uint64_t cpus[KOORDHIP_NUMA_WORDS], pref[KOORDHIP_NUMA_WORDS];
   int hz = 0;
+  orc_resv_pref(cfg, st, pod, i, pref); /* getResourceOptions' preferredCPUs (plugin.go:465-495) */
   if (tp != KOORDHIP_NUMA_TOPO_NONE) {
     if (!policy_allocate(st, pod, i, zones, cpus, &hz)) return 0; /* :86-89 */
-  } else if (!alloc_cpuset(st, pod, i, NULL, cpus)) {
+  } else if (!alloc_cpuset(st, pod, i, NULL, cpus, pref)) {
     return 0;
   }
   if (hz) { /* calculateAllocatableAndRequested over the pod's zones :134-152 */
@@ -924,7 +960,11 @@ int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const ko
    * pod's request is amplified too (getResourceOptions, plugin.go:481-485) */
   int64_t qcpu = pod->req[KOORDHIP_RES_CPU];
   if (cpuset) {
-    rcpu = orc_amplify((int64_t)st->numa_alloc_cnt[i] * 1000, ratio);
+    /* getAvailableCPUs(preferredCPUs - the pod's CPUs): the preferred CPUs the
+     * pod leaves drop out of the allocated set (RefCount 1 -> 0) */
+    int64_t left = 0;
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) left += __builtin_popcountll(pref[w] & ~cpus[w]);
+    rcpu = orc_amplify(((int64_t)st->numa_alloc_cnt[i] - left) * 1000, ratio);
     qcpu = orc_amplify(qcpu, ratio);
   }
   return numa_least_allocated(cfg, rcpu + qcpu, acpu, rmem + pod->req[KOORDHIP_RES_MEM], amem);
@@ -938,23 +978,29 @@ int orc_numa_reserve_active(const orc_state *st, const koordhip_pod *pod, int32_
 /* Reserve (plugin.go:365-405) + resourceManager.Update (resource_manager.go:328-339,
  * node_allocation.go:76-103): the cpuset and the zone amounts; returns 0 when
  * Allocate fails. */
-int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *cpus_out) {
+int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *cpus_out, const uint64_t *pref) {
   uint64_t out[KOORDHIP_NUMA_WORDS] = {0, 0, 0, 0};
   int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES] = {0};
   int hz = 0;
   if (node_policy(st, i) != KOORDHIP_NUMA_TOPO_NONE) {
     if (!policy_allocate(st, pod, i, zones, out, &hz)) return 0;
-  } else if (!alloc_cpuset(st, pod, i, NULL, out)) {
+  } else if (!alloc_cpuset(st, pod, i, NULL, out, pref)) {
     return 0;
   }
+  /* addPodAllocation (node_allocation.go:76-103): every CPU's ExclusivePolicy
+   * becomes the pod's, RefCount + 1 -- a preferred CPU was allocated already
+   * (the reservation's), so the allocated count grows by the others only */
   const int ex = (int)KOORDHIP_NUMA_EXCLUSIVE(pod->numa_policy);
+  int grow = 0;
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
+    const uint64_t was_alloc = ~st->numa_free[w][i] & (pref ? pref[w] : 0);
+    grow += __builtin_popcountll(out[w] & ~was_alloc);
     st->numa_free[w][i] &= ~out[w];
-    if (ex == KOORDHIP_CPUEXCL_PCPU) st->numa_excl_pcpu[w][i] |= out[w];
-    if (ex == KOORDHIP_CPUEXCL_NUMA) st->numa_excl_numa[w][i] |= out[w];
+    st->numa_excl_pcpu[w][i] = (st->numa_excl_pcpu[w][i] & ~out[w]) | (ex == KOORDHIP_CPUEXCL_PCPU ? out[w] : 0);
+    st->numa_excl_numa[w][i] = (st->numa_excl_numa[w][i] & ~out[w]) | (ex == KOORDHIP_CPUEXCL_NUMA ? out[w] : 0);
     if (cpus_out) cpus_out[w] = out[w];
   }
-  st->numa_alloc_cnt[i] += popc(out);
+  st->numa_alloc_cnt[i] += grow;
   if (hz)
     for (int q = 0; q < 2 * KOORDHIP_NUMA_MAX_NODES; q++) st->numa_zone_used[(size_t)i * 2 * KOORDHIP_NUMA_MAX_NODES + q] += zones[q];
   return 1;

@@ -265,8 +265,10 @@ static int node_order_rank(const orc_state *st, const koordhip_pod *pod, int32_t
 }
 
 /* Reserve: assumePod into the nominated reservation (Allocated += the pod's
- * requests masked to ResourceNames, one more assigned pod). */
-void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i) {
+ * requests masked to ResourceNames, one more assigned pod).  The pod's CPUs
+ * (cpus, NULL = none) join AssignedPods: the next RestoreReservation subtracts
+ * them from the reservation's cpuset (nodenumaresource/reservation.go:90-97). */
+void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i, const uint64_t *cpus) {
   const int s = orc_resv_nominate(st, pod, i);
   if (s < 0) return;
   const size_t x = at(st, s, i);
@@ -274,6 +276,27 @@ void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i) {
   for (int r = 0; r < 2; r++)
     if (has_key(rf, r) && pod_key(pod, r)) st->resv_allocated[r][x] += pod->req[r];
   st->resv_assigned[x] += 1;
+  if (cpus && st->resv_cpus[0])
+    for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) st->resv_cpus[w][x] &= ~cpus[w];
+}
+
+/* getReservationReservedCPUs (nodenumaresource/plugin.go:503-524): the
+ * nominated reservation is PreScore's (scoring.go:42-89, so the Reservation
+ * plugin must score), its reserved CPUs the RestoreReservation state
+ * (reservation.go:76-113: the reservation's cpuset less its AssignedPods'),
+ * restored only for pods AllowUseCPUSet admits (PreRestoreReservation :68-74)
+ * and read only by cpuset pods (requestCPUBind).  Upstream skips PreScore when
+ * exactly one node is feasible (schedule_one.go, v1.24.15), so its NUMA
+ * Reserve then sees no nomination; the engine keeps the nomination there too
+ * (the one divergence of the restore). */
+void orc_resv_pref(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *P) {
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) P[w] = 0;
+  if (!st->resv_cpus[0] || !orc_resv_on(cfg, st) || !(cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION)) return;
+  if (!(pod->flags & KOORDHIP_POD_CPUSET) || (pod->flags & KOORDHIP_POD_NUMA_SKIP)) return;
+  const int s = orc_resv_nominate(st, pod, i);
+  if (s < 0) return;
+  const size_t x = at(st, s, i);
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) P[w] = st->resv_cpus[w][x];
 }
 
 /* The Reservation plugin's contribution for one pod over its feasible nodes

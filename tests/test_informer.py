@@ -465,3 +465,39 @@ def test_gpu_numa_events_then_stream():
     assert np.array_equal(cs, rcs)
     for k, v in o.numa_state().items():
         assert np.array_equal(nst[k], v), k
+
+
+def test_reservation_cpuset_events_rows_equal_rebuild():
+    """A reservation holding a cpuset: its reserve pod's CPUs are a NodeAllocation
+    entry (ReservationToPodEventHandler, nodenumaresource/pod_eventhandler.go:
+    40-50), its reserved CPUs (less the assigned pods', reservation.go:84-104)
+    the slot's resv_cpus; deleting it frees them.  Each flush equals a rebuild."""
+    from koordinator_amd import numa as nm
+    from koordinator_amd import reservation as rv
+    rng = np.random.default_rng(3)
+    prof = shipped_profile(numa=True, reservation=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110)})
+             for i in range(3)]
+    inf = Informer(prof, nodes, NOW)
+    for n in nodes:
+        inf.on_nrt(_nrt(rng, n.name))
+    t0 = inf.table(NOW)
+    cnt0 = int(t0["numa_alloc_cnt"][1])
+    eng = _TableEngine(t0)
+    r = rv.Reservation("r0", "n1", uid="ru0", allocatable={k8s.CPU: k8s.Q(4)}, owners=[rv.ReservationOwner()],
+                       cpus=[4, 5, 6, 7], assigned_cpus=[4, 5])
+    inf.on_reservation(r)
+    inf.flush(eng, NOW)
+    want = inf.table(NOW)
+    for c in NUMA_COLS[:13] + [f"resv_cpus{w}" for w in range(4)]:
+        assert np.array_equal(eng.table.cols[c], want.cols[c]), c
+    topo = nm.linux_topology(2, 1, 8, 2)
+    held = topo.mask([4, 5, 6, 7])
+    assert not any(int(want[f"numa_free{w}"][1]) & int(held[w]) for w in range(4))
+    assert [int(want[f"resv_cpus{w}"][1]) for w in range(4)] == [int(x) for x in topo.mask([6, 7])]
+    inf.attach(want, NOW)
+    eng = _TableEngine(want)
+    inf.on_reservation_delete("r0")
+    inf.flush(eng, NOW)
+    assert int(eng.table["numa_alloc_cnt"][1]) == cnt0
+    assert not any(int(eng.table[f"resv_cpus{w}"][1]) for w in range(4))
