@@ -462,6 +462,19 @@ class NodeAllocation:
         self.add(uid, cpus, excl, numa_res)
 
 
+def available_cpus(topo: Topology, alloc: Optional[NodeAllocation], reserved: Iterable[int] = (),
+                   preferred: Iterable[int] = ()) -> List[int]:
+    """NodeAllocation.getAvailableCPUs with maxRefCount 1 (node_allocation.go:133-153):
+    every CPU minus those still allocated once the preferred CPUs' RefCount
+    dropped by one, minus the node's reserved CPUs."""
+    held = {c: info[0] for c, info in (alloc.cpus.items() if alloc is not None else [])}
+    for c in preferred:
+        if c in held:
+            held[c] -= 1
+    res = set(reserved)
+    return sorted(c for c in topo.cpu_of if held.get(c, 0) < 1 and c not in res)
+
+
 def pod_allocation(annotations: Dict[str, str]):
     """podEventHandler.updatePod's parse (pod_eventhandler.go:94-131): (cpus,
     exclusive policy, NUMA node resources), or None when the pod holds
@@ -506,7 +519,7 @@ def numa_row(table, i: int, opts: Optional[TopologyOptions], alloc: Optional[Nod
     table["numa_class"][i] = classes.add(topo)
     cpus = (alloc.cpus if alloc is not None else {})
     allocated = [c for c in cpus if c in topo.pos_of]
-    free = [c for c in topo.cpu_of if c not in cpus and c not in set(opts.reserved)]   # getAvailableCPUs, maxRefCount 1
+    free = available_cpus(topo, alloc, opts.reserved)
     fm = topo.mask(free)
     pm = topo.mask([c for c in allocated if cpus[c][1] == "PCPULevel"])
     nm = topo.mask([c for c in allocated if cpus[c][1] == "NUMANodeLevel"])

@@ -74,6 +74,8 @@ def lib():
         L.orc_spread_order.argtypes = [vp, vp, C.c_int, vp]
         L.orc_spread_order.restype = C.c_int
         L.orc_set_cpuset_out.argtypes = [C.POINTER(OrcState), vp]
+        L.orc_numa_allocate_hint.argtypes = [C.POINTER(OrcState), vp, C.c_int32, C.c_uint64, vp, vp]
+        L.orc_numa_allocate_hint.restype = C.c_int
         L.orc_place_stream.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32,
                                        vp, C.c_int32]
         L.orc_la_flags.argtypes = [C.POINTER(abi.KoordhipNodeSoa), C.c_int32, vp]
@@ -182,6 +184,15 @@ class Oracle:
               else np.zeros((abi.NUMA_WORDS, n), np.uint64))
         return {"allocated": np.stack([a(self.st.resv_allocated[0]), a(self.st.resv_allocated[1])]),
                 "assigned": a(self.st.resv_assigned), "cpus": rc}
+
+    def numa_allocate_hint(self, pod: np.ndarray, node: int, mask: int):
+        """resourceManager.Allocate with hint `mask` (0 = none): (ok, zone
+        amounts [2][NUMA_MAX_NODES] (cpu milli, memory), cpus [WORDS])."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        z = np.zeros((2, abi.NUMA_MAX_NODES), np.int64)
+        c = np.zeros(abi.NUMA_WORDS, np.uint64)
+        ok = lib().orc_numa_allocate_hint(C.byref(self.st), pod.ctypes.data, node, mask, z.ctypes.data, c.ctypes.data)
+        return bool(ok), z, c
 
     def resv_restore_delta(self, pod: np.ndarray, node: int):
         """(requested delta [cpu, mem], non-zero delta [cpu, mem], pod-count delta) of the restore."""

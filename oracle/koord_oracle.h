@@ -116,6 +116,8 @@ int orc_tm_merge(int policy, uint64_t numa_nodes, const orc_tm_entry *e, int32_t
 /* The NUMA-zone part of Allocate for node i under its topology policy: the
  * merged hint (nil -> *nil = 1), admit, and allocateResourcesByHint's amounts
  * [2][KOORDHIP_NUMA_MAX_NODES]; returns 1 when Admit + Allocate succeed. */
+int orc_numa_allocate_hint(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t mask, int64_t *zones,
+                           uint64_t *cpus);
 int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t node, uint64_t *mask, int32_t *nil,
                         int32_t *admit, int64_t *zones);
 

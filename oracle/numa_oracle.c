@@ -918,6 +918,22 @@ static int64_t numa_least_allocated(const koordhip_config *cfg, int64_t req_cpu,
   return wsum ? num / wsum : 0;
 }
 
+/* resourceManager.Allocate with a given hint (resource_manager.go:142-164, the
+ * entry resource_manager_test.go drives): mask = NUMANodeAffinity (0 = no
+ * hint), zones = allocateResourcesByHint's amounts, cpus = allocateCPUSet's
+ * (cpuset pods).  1 = ok. */
+int orc_numa_allocate_hint(const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t mask, int64_t *zones,
+                           uint64_t *cpus) {
+  for (int q = 0; q < 2 * KOORDHIP_NUMA_MAX_NODES; q++) zones[q] = 0;
+  for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
+  if (mask) {
+    const int M = zones_of(st, i);
+    if (M == 0 || !alloc_by_hint(st, pod, i, M, mask, zones)) return 0; /* :167-169, :209-219 */
+  }
+  if (!(pod->flags & KOORDHIP_POD_CPUSET)) return 1;
+  return alloc_cpuset(st, pod, i, mask ? zones : NULL, cpus, NULL);
+}
+
 /* Score, scoring.go:55-120,122-168. */
 int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
   const koordhip_node_soa *s = st->soa;
