@@ -1540,8 +1540,13 @@ int place_staged_impl(koordhip_ctx *c) {
   // the round (NodeNUMAResource rows are large)
   int32_t P = c->batch;
   // (NodeNUMAResource streams are bound by the resolve's cpuset Reserve: the
-  // longer re-evaluated set of lag 2 measured slower there, 87k vs 93k pods/s)
-  int32_t lag = (two && !c->side && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
+  // longer re-evaluated set of lag 2 measured slower there, 87k vs 93k pods/s
+  // (round 2), 149k vs 154k (round 3, config 3); the Reservation streams are
+  // bound by the evaluation -- the period of a round is (eval + resolve) / 2 at
+  // lag 1, / 3 at lag 2 -- and run lag 2: config 5 170k -> 182k pods/s in
+  // spite of the shorter rounds the resolve's LDS then allows (24 -> 15 pods).
+  // KOORDHIP_LAG2: lag 2 with NodeNUMAResource alone too.)
+  int32_t lag = (two && (!c->side || c->resv || std::getenv("KOORDHIP_LAG2")) && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
   if (lag == 2 && (3 * P > kh::kResolveMaxK || 2 * P > kMaxBatch)) lag = 1;  // M' spans 2 rounds <= 64 slots
   const int nm = kh::side_mode(c->dc);
   while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, nm, lag) > 157 * 1024) P--;

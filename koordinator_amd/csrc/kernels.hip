@@ -1479,15 +1479,19 @@ __device__ __forceinline__ uint32_t etk_kth(F each, uint32_t top, int32_t nnz, i
   return prefix;
 }
 
-template <int NM, int VT, int R>
+// G: pods per workgroup -- one load of a node's columns serves G evaluations
+// (the evaluation phase is bound by the column loads' latency); the slice
+// selections then run pod after pod, and the workgroup merges every pod whose
+// last slice it was.
+template <int NM, int VT, int R, int G>
 __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM == 5 ? 2 : (NM >= 3 ? 4 : 1)))) void k_eval_topk(
     DevCfg c, DevNodes d, const DevPod *__restrict__ pods, int32_t n_pods, int32_t lo, int32_t hi, int32_t nslices,
     int32_t spx, int32_t k, uint64_t *part, int32_t *pcnt, uint32_t *arrive, uint64_t *__restrict__ out,
     PipeSync *__restrict__ sy, int32_t sel_par, int32_t res_wait, int32_t stage_cap, uint64_t *dbg) {
   static_assert(VT % 4 == 0 && VT % R == 0, "slice shape");
   constexpr int32_t SL = ETK_THREADS * VT;
-  // slice values, or (merge) up to stage_cap candidate keys: what the launch sized
-  const int32_t VBYTES = (SL * 4 > stage_cap * 8) ? SL * 4 : stage_cap * 8;
+  // slice values (G rows), or (merge) up to stage_cap candidate keys: what the launch sized
+  const int32_t VBYTES = (G * SL * 4 > stage_cap * 8) ? G * SL * 4 : stage_cap * 8;
   extern __shared__ __attribute__((aligned(16))) char etk_lds[];
   EtkHdr &h = *reinterpret_cast<EtkHdr *>(etk_lds);
   uint32_t *vals = reinterpret_cast<uint32_t *>(etk_lds + ETK_HDR);  // slice values, then merge candidates
@@ -1497,9 +1501,11 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
   // XCD-aware: block b runs on XCD b % 8, which owns slices [xcd * spx, ...):
   // a slice's pods are consecutive blocks of one XCD and share its columns in L2
   const int32_t b = blockIdx.x, xcd = b & 7, local = b >> 3;
-  const int32_t p = local % n_pods;
-  const int32_t s = xcd * spx + local / n_pods;
+  const int32_t npg = (n_pods + G - 1) / G;
+  const int32_t p0 = (local % npg) * G;
+  const int32_t s = xcd * spx + local / npg;
   if (s >= nslices) return;  // block-uniform
+  const int ng = min(G, n_pods - p0);
   const int t = threadIdx.x;
   if (dbg && t == 0) ts[0] = stamp();
   const DevNumaClass *cls = d.nu.cls;
@@ -1512,19 +1518,29 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
       cls = reinterpret_cast<const DevNumaClass *>(dst);
     }
   }
-  const DevPod pod = pods[p];
-  const Need need = pod_needs(pod, c);
+  DevPod gpod[G];
+  Need need{};
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    gpod[g] = pods[p0 + (g < ng ? g : 0)];
+    if (g == 0) need = pod_needs(gpod[g], c);
+    else need_or(need, pod_needs(gpod[g], c));
+  }
   const int32_t c0 = lo + s * SL;
-  // ---- evaluate: R nodes in flight per thread, values parked in LDS
-  uint32_t vmax = 0;
-  int32_t vnz = 0;
+  // ---- evaluate: R nodes in flight per thread, each row evaluated for the G
+  //      pods, values parked in LDS (pod g's at vals[g * SL ...])
+  uint32_t vmax[G];
+  int32_t vnz[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) vmax[g] = 0u, vnz[g] = 0;
 #pragma unroll 1
   for (int q0 = 0; q0 < VT; q0 += R) {
-    uint32_t sv[R];
+    uint32_t sv[R][G];
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const int32_t i = c0 + (q0 + r) * ETK_THREADS + t;
-      int32_t tot = -1;
+#pragma unroll
+      for (int g = 0; g < G; g++) sv[r][g] = 0u;
       if (i < hi) {
         NV v;
         load_node(v, d, i, need, c);
@@ -1532,31 +1548,40 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
           side_row_t<NM> nr;
           load_numa<false>(nr, d, i, need);
           load_resv(nr, d.rv, i);
-          tot = eval_total_resv<side_row_t<NM>::kSlots, NM == 5>(pod, v, nr, cls, c);
+#pragma unroll
+          for (int g = 0; g < G; g++)
+            sv[r][g] = (uint32_t)(eval_total_resv<side_row_t<NM>::kSlots, NM == 5>(gpod[g], v, nr, cls, c) + 1);
         } else if constexpr (NM != 0) {
           NumaRow nr;
           load_numa<NM == 2>(nr, d, i, need);
-          tot = eval_total_numa<NM == 2>(pod, v, nr, cls, c);
+#pragma unroll
+          for (int g = 0; g < G; g++) sv[r][g] = (uint32_t)(eval_total_numa<NM == 2>(gpod[g], v, nr, cls, c) + 1);
         } else {
-          tot = eval_total(pod, v, c);
+#pragma unroll
+          for (int g = 0; g < G; g++) sv[r][g] = (uint32_t)(eval_total(gpod[g], v, c) + 1);
         }
       }
-      sv[r] = (uint32_t)(tot + 1);
     }
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      vals[(q0 + r) * ETK_THREADS + t] = sv[r];
-      vmax = max(vmax, sv[r]);
-      vnz += sv[r] != 0u;
-    }
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        vals[g * SL + (q0 + r) * ETK_THREADS + t] = sv[r][g];
+        vmax[g] = max(vmax[g], sv[r][g]);
+        vnz[g] += sv[r][g] != 0u;
+      }
   }
+  uint32_t lastmask = 0;  // (thread 0) pods whose last slice this workgroup is
+#pragma unroll 1
+  for (int g = 0; g < ng; g++) {
+  const int32_t p = p0 + g;
   uint32_t top;
   int32_t nnz;
-  etk_maxsum(vmax, vnz, h, &top, &nnz);  // (its barrier also publishes vals)
-  if (dbg && t == 0) ts[1] = stamp();
+  etk_maxsum(vmax[g], vnz[g], h, &top, &nnz);  // (its barrier also publishes vals)
+  if (dbg && t == 0 && g == 0) ts[1] = stamp();
   uint32_t v[VT];
   {
-    const uint4 *src = reinterpret_cast<const uint4 *>(vals + t * VT);
+    const uint4 *src = reinterpret_cast<const uint4 *>(vals + g * SL + t * VT);
 #pragma unroll
     for (int q = 0; q < VT / 4; q++) {
       const uint4 x = src[q];
@@ -1602,21 +1627,25 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
   }
   const int32_t emitted = gt + min(tie_budget, all_ties);
   if (t == 0) __hip_atomic_store(pcnt + (size_t)p * nslices + s, emitted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }  // pods g
   if (dbg && t == 0) ts[2] = stamp();
   // ---- publish (Guideline 16 R1: every wave drains its sc1 stores, barrier,
-  //      one relaxed agent-scope counter add); the pod's last slice merges
+  //      one relaxed agent-scope counter add per pod); a pod's last slice merges
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(&arrive[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int32_t last = old + 1 == (uint32_t)nslices;
-    if (last) {
-      __hip_atomic_store(&arrive[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int g = 0; g < ng; g++) {
+      const uint32_t old = __hip_atomic_fetch_add(&arrive[p0 + g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1 == (uint32_t)nslices) {
+        __hip_atomic_store(&arrive[p0 + g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lastmask |= 1u << g;
+      }
+    }
+    if (lastmask) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    h.last = last;
-    h.cnt_gt = 0;
+    h.last = (int32_t)lastmask;
   }
   __syncthreads();
   if (dbg && t == 0) {
@@ -1624,7 +1653,14 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
     for (int q = 1; q < 4; q++) atomicAdd((unsigned long long *)&dbg[40 + q], (unsigned long long)(ts[q] - ts[q - 1]));
     atomicAdd((unsigned long long *)&dbg[40], 1ull);
   }
-  if (!h.last) return;  // block-uniform
+  lastmask = (uint32_t)h.last;
+  if (!lastmask) return;  // block-uniform
+#pragma unroll 1
+  for (int g = 0; g < ng; g++) {
+  if (!((lastmask >> g) & 1u)) continue;  // block-uniform
+  const int32_t p = p0 + g;
+  __syncthreads();  // the previous merge's LDS reads are done
+  if (t == 0) h.cnt_gt = 0;
   // ---- merge: offsets of the slice lists (one per thread), then the candidates
   const int32_t ns = t < nslices ? pcnt[(size_t)p * nslices + t] : 0;
   int32_t total;
@@ -1693,11 +1729,10 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
   if (sy) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) {
-      pipe_count_pod(sy, sel_par);
-      if (res_wait > 0) (void)wait_at_least(&sy->res_round, res_wait, sy);
-    }
+    if (t == 0) pipe_count_pod(sy, sel_par);
   }
+  }  // merged pods g
+  if (sy && res_wait > 0 && t == 0) (void)wait_at_least(&sy->res_round, res_wait, sy);
 }
 
 // ---------------------------------------------------------------------------
@@ -3233,50 +3268,65 @@ hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *po
     return hipGetLastError();
   }
   const int nm = side_mode(c);
+  // pods per workgroup (KOORDHIP_ETK_G: 1, 2 or 4; built for the plain, NUMA
+  // and one-reservation plugin sets at 8 / 16 nodes per thread)
+  int G = 1;
+  if (const char *e = std::getenv("KOORDHIP_ETK_G")) G = std::atoi(e);
+  if (!(G == 2 || G == 4) || VT == 32 || !(nm == 0 || nm == 1 || nm == 3)) G = 1;
   const int32_t sl = ETK_THREADS * VT;
   // merge staging: as many candidates as the slice lists can hold, up to ETK_MERGE_KEYS
   const int32_t stage_cap = (int32_t)std::min<int64_t>((int64_t)nslices * k, ETK_MERGE_KEYS);
-  const size_t vbytes = (size_t)std::max<int32_t>(sl * 4, stage_cap * 8);
+  const size_t vbytes = (size_t)std::max<int32_t>(G * sl * 4, stage_cap * 8);
   const size_t lds = (size_t)ETK_HDR + vbytes +
                      ((nm != 0 && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0);
   const int32_t spx = (nslices + 7) / 8;
-  const int32_t blocks = 8 * spx * n_pods;
-  static bool attr[6][3] = {};
+  const int32_t blocks = 8 * spx * ((n_pods + G - 1) / G);
+  static bool attr[6][3][5] = {};
   const int vi = VT == 8 ? 0 : (VT == 16 ? 1 : 2);
-#define KH_ETK(NN, VV, RR)                                                                                          \
+#define KH_ETK(NN, VV, RR, GG)                                                                                      \
   do {                                                                                                              \
-    if (!attr[NN][vi]) {                                                                                            \
-      const hipError_t e = hipFuncSetAttribute((const void *)k_eval_topk<NN, VV, RR>,                              \
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);              \
+    if (!attr[NN][vi][GG]) {                                                                                        \
+      const hipError_t e = hipFuncSetAttribute((const void *)k_eval_topk<NN, VV, RR, GG>,                          \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);             \
       if (e != hipSuccess) return e;                                                                                \
-      attr[NN][vi] = true;                                                                                          \
+      attr[NN][vi][GG] = true;                                                                                      \
     }                                                                                                               \
-    hipLaunchKernelGGL((k_eval_topk<NN, VV, RR>), dim3(blocks), dim3(ETK_THREADS), lds, s, c, d, pods, n_pods, lo,    \
-                       hi, nslices, spx, k, part, pcnt, arrive, out, sync, sel_par, res_wait, stage_cap, dbg);      \
+    hipLaunchKernelGGL((k_eval_topk<NN, VV, RR, GG>), dim3(blocks), dim3(ETK_THREADS), lds, s, c, d, pods, n_pods,   \
+                       lo, hi, nslices, spx, k, part, pcnt, arrive, out, sync, sel_par, res_wait, stage_cap, dbg);  \
+  } while (0)
+#define KH_ETK_G(NN, VV, RR)       \
+  do {                             \
+    if (G == 4)                    \
+      KH_ETK(NN, VV, RR, 4);       \
+    else if (G == 2)               \
+      KH_ETK(NN, VV, RR, 2);       \
+    else                           \
+      KH_ETK(NN, VV, RR, 1);       \
   } while (0)
   // R: evaluations in flight per thread (all of a slice's for the plain plugin
   // set; the NUMA / Reservation rows are large: two or four at a time)
   switch (nm * 4 + vi) {
-    case 0: KH_ETK(0, 8, 8); break;
-    case 1: KH_ETK(0, 16, 8); break;
-    case 2: KH_ETK(0, 32, 8); break;
-    case 4: KH_ETK(1, 8, 2); break;
-    case 5: KH_ETK(1, 16, 2); break;
-    case 6: KH_ETK(1, 32, 2); break;
-    case 8: KH_ETK(2, 8, 2); break;
-    case 9: KH_ETK(2, 16, 2); break;
-    case 10: KH_ETK(2, 32, 2); break;
-    case 12: KH_ETK(3, 8, 4); break;
-    case 13: KH_ETK(3, 16, 4); break;
-    case 14: KH_ETK(3, 32, 4); break;
-    case 16: KH_ETK(4, 8, 4); break;
-    case 17: KH_ETK(4, 16, 4); break;
-    case 18: KH_ETK(4, 32, 4); break;
-    case 20: KH_ETK(5, 8, 4); break;
-    case 21: KH_ETK(5, 16, 4); break;
-    case 22: KH_ETK(5, 32, 4); break;
+    case 0: KH_ETK_G(0, 8, 8); break;
+    case 1: KH_ETK_G(0, 16, 8); break;
+    case 2: KH_ETK(0, 32, 8, 1); break;
+    case 4: KH_ETK_G(1, 8, 2); break;
+    case 5: KH_ETK_G(1, 16, 2); break;
+    case 6: KH_ETK(1, 32, 2, 1); break;
+    case 8: KH_ETK(2, 8, 2, 1); break;
+    case 9: KH_ETK(2, 16, 2, 1); break;
+    case 10: KH_ETK(2, 32, 2, 1); break;
+    case 12: KH_ETK_G(3, 8, 4); break;
+    case 13: KH_ETK_G(3, 16, 4); break;
+    case 14: KH_ETK(3, 32, 4, 1); break;
+    case 16: KH_ETK(4, 8, 4, 1); break;
+    case 17: KH_ETK(4, 16, 4, 1); break;
+    case 18: KH_ETK(4, 32, 4, 1); break;
+    case 20: KH_ETK(5, 8, 4, 1); break;
+    case 21: KH_ETK(5, 16, 4, 1); break;
+    case 22: KH_ETK(5, 32, 4, 1); break;
     default: return hipErrorInvalidValue;
   }
+#undef KH_ETK_G
 #undef KH_ETK
   return hipGetLastError();
 }

@@ -28,7 +28,8 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         per[k][ctr + "_KB_avg"] = sum(d.values()) / len(d)
         per[k]["launches"] = len(d)
 table = {k: dict(v) for k, v in per.items()}
-scan = next(k for k in table if "k_scan" in k)
+# the evaluation kernel: the fused k_eval_topk where it ran, else k_scan
+scan = next((k for k in table if "k_eval_topk" in k), None) or next(k for k in table if "k_scan" in k)
 f_kb, w_kb = table[scan]["FETCH_SIZE_KB_avg"], table[scan]["WRITE_SIZE_KB_avg"]
 summary = {
     "source": f"profiles/{prefix or name}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
