@@ -198,3 +198,26 @@ def test_gpu_resv_cpus_stream_parity(Engine, mode, monkeypatch):
         for k in rn:
             assert np.array_equal(gn[k], rn[k]), k
     assert (rr["cpus"] != _resv_cpu_masks(t)).any(axis=0).sum() > 10
+
+
+@pytest.mark.gpu
+def test_gpu_resv_cpus_config5_variant(Engine):
+    """A config-5-shaped variant at reduced size (20k nodes x 4k pods, the
+    shipped profile with NodeNUMAResource + Reservation): up to 2 reservations
+    per node, 70 % of them holding a cpuset, half the LS pods cpuset pods;
+    placements, cpusets and every state column bit-exact vs the oracle."""
+    prof, t, pods = _workload(20000, 4000, seed=9)
+    o = oracle.Oracle(to_c_config(prof), t)
+    ref, cs_ref = o.place_stream(pods, threads=16, cpusets=True)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got = e.place_stream(pods)
+        assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
+        assert np.array_equal(e.fetch_cpusets(len(pods)), cs_ref)
+        gr, rr = e.read_reservations(), o.resv_state()
+        for k in ("allocated", "assigned", "cpus"):
+            assert np.array_equal(gr[k], rr[k]), k
+        gs, rs = e.read_nodes(), o.state()
+        for k in ("requested", "nz", "npods", "la_used"):
+            assert np.array_equal(gs[k], rs[k]), k
+    assert (rr["cpus"] != _resv_cpu_masks(t)).any(axis=0).sum() > 50
