@@ -221,3 +221,38 @@ def test_gpu_resv_cpus_config5_variant(Engine):
         for k in ("requested", "nz", "npods", "la_used"):
             assert np.array_equal(gs[k], rs[k]), k
     assert (rr["cpus"] != _resv_cpu_masks(t)).any(axis=0).sum() > 50
+
+
+@pytest.mark.gpu
+def test_gpu_resv_cpus_update_nodes(Engine):
+    """koordhip_update_nodes replaces a row's reserved CPUs with the rows' own
+    (clearing them when the rows carry none): a stream after the update
+    matches the oracle on the updated table."""
+    prof, t, pods = _workload(1500, 800, seed=13)
+    t2 = t.copy()
+    rng = np.random.default_rng(2)
+    has = np.flatnonzero(_resv_cpu_masks(t).any(axis=0)[:t.n])
+    idx = np.sort(rng.choice(has, size=min(60, len(has)), replace=False))
+    # half of them: the reservation's CPUs all went to assigned pods (nothing restored)
+    for i in idx[::2]:
+        for w in range(abi.NUMA_WORDS):
+            t2[f"resv_cpus{w}"][i] = 0
+    ref = oracle.Oracle(to_c_config(prof), t2).place_stream(pods, threads=8)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        e.update_nodes(idx, t2.rows(idx))
+        got = e.place_stream(pods)
+    assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
+    # rows carrying no reserved CPUs at all clear them
+    rows = t.rows(idx[:4])
+    for c in list(rows.cols):
+        if c.startswith("resv_cpus"):
+            rows[c][:] = 0
+    assert not rows.as_soa().resv_cpus[0]
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        e.update_nodes(idx[:4], rows)
+        left = e.read_reservations()["cpus"]
+    n = t.n
+    for q in range(t.resv_slots):
+        assert not left[:, q * n + idx[:4]].any()
