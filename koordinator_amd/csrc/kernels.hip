@@ -2518,6 +2518,13 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         const bool x1 = e1 != 0 && xbit(modmap, key_node(e1));
         const uint64_t f0 = __ballot(e0 != 0 && !x0), f1 = __ballot(e1 != 0 && !x1);
         uint64_t best = f0 ? readlane_u64(e0, __builtin_ctzll(f0)) : (f1 ? readlane_u64(e1, __builtin_ctzll(f1)) : 0ull);
+        // (NM 5) how many nodes are feasible now: the list's entries outside X
+        // are exact, the X rows are all evaluated below (these pods are never
+        // monotone), and a list that was not full held every node feasible at
+        // its evaluation (feasibility only shrinks).  One: upstream returns it
+        // without PreScore, so no reservation is nominated for the Reserve.
+        int32_t nfeas = __popcll(f0) + __popcll(f1);
+        const bool lfull = (k <= 64 ? readlane_u64(e0, k - 1) : readlane_u64(e1, k - 65)) != 0ull;
         // A monotone pod: only the X entries ranked above c can win.  Each one's
         // current key: from the helper waves' key tables when they are ready
         // (kpre: the row its staged claimer committed to; ktab: an M' row no
@@ -2609,9 +2616,12 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             c_g[1] += stamp() - ts;
           }
+          if constexpr (NM == 5) nfeas += __popcll(__ballot(kv != 0ull));
           kv = wave_max_u64_dpp(kv);
           best = kv > best ? kv : best;
         }
+        const bool single = !mono_g && !lfull && nfeas == 1;  // (mono_g: the X rows were not all evaluated)
+        (void)single;
         if (dbg && NUMA && nrows > 0) {
           const int b = KOORDHIP_NUMA_REQUIRED(pod.numa_policy) == KOORDHIP_CPUBIND_SPREAD_BY_PCPUS ? 4 : 6;
           c_nx[b] += stamp() - t_rows;
@@ -2675,7 +2685,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                 NR nr = *snr;
                 if constexpr (NM == 5) {  // the nominated reservation's reserved CPUs first
                   uint64_t pref[NW];
-                  resv_pref_cpus(nr, pod, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? resv_matched(nr, pod) : 0u, pref);
+                  resv_pref_cpus(nr, pod,
+                                 ((c.score & KOORDHIP_PLUGIN_RESERVATION) && !single) ? resv_matched(nr, pod) : 0u, pref);
                   okl = numa_reserve<ZONES, true>(cls, nr, pod, mc, pref);
                 } else {
                   okl = numa_reserve<ZONES, true>(cls, nr, pod, mc);

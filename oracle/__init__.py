@@ -42,6 +42,7 @@ class OrcState(C.Structure):
         ("resv_allocated", C.POINTER(C.c_int64) * 2),
         ("resv_assigned", C.POINTER(C.c_int32)),
         ("resv_cpus", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
+        ("no_prescore", C.c_int32),
     ]
 
 

@@ -628,8 +628,12 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
     }
     if (rv) orc_resv_restore(st, &pods[p], -1);
     uint64_t *cs = st->cpuset_out ? st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS : NULL;
-    /* Reserve (+ AssumePod); a failed Reserve leaves no state and is not retried */
+    /* Reserve (+ AssumePod); a failed Reserve leaves no state and is not retried.
+     * One feasible node: (upstream) schedulePod returns it without
+     * prioritizeNodes, so PreScore nominates no reservation */
+    st->no_prescore = nf == 1;
     out_node[p] = orc_commit(cfg, st, &pods[p], best_node, +1, cs) ? KOORDHIP_RESERVE_FAILED : best_node;
+    st->no_prescore = 0;
   }
   free(c.feasible);
   free(c.plugin_scores);

@@ -59,6 +59,10 @@ typedef struct orc_state {
   /* NodeNUMAResource RestoreReservation: the reserved CPUs each reservation
    * slot has left ([WORDS][slots x n]; NULL when the snapshot has none) */
   uint64_t *resv_cpus[KOORDHIP_NUMA_WORDS];
+  /* set by orc_place_stream around the Reserve of a pod with exactly one
+   * feasible node: upstream then skips PreScore / Score, so no reservation is
+   * nominated before the NodeNUMAResource Reserve */
+  int32_t no_prescore;
 } orc_state;
 
 int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n);

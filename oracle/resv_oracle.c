@@ -286,12 +286,13 @@ void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i, const ui
  * (reservation.go:76-113: the reservation's cpuset less its AssignedPods'),
  * restored only for pods AllowUseCPUSet admits (PreRestoreReservation :68-74)
  * and read only by cpuset pods (requestCPUBind).  Upstream skips PreScore when
- * exactly one node is feasible (schedule_one.go, v1.24.15), so its NUMA
- * Reserve then sees no nomination; the engine keeps the nomination there too
- * (the one divergence of the restore). */
+ * exactly one node is feasible (schedule_one.go, v1.24.15: schedulePod returns
+ * the only feasible node), so its NUMA Reserve then sees no nomination
+ * (st->no_prescore). */
 void orc_resv_pref(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *P) {
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) P[w] = 0;
   if (!st->resv_cpus[0] || !orc_resv_on(cfg, st) || !(cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION)) return;
+  if (st->no_prescore) return;
   if (!(pod->flags & KOORDHIP_POD_CPUSET) || (pod->flags & KOORDHIP_POD_NUMA_SKIP)) return;
   const int s = orc_resv_nominate(st, pod, i);
   if (s < 0) return;

@@ -256,3 +256,39 @@ def test_gpu_resv_cpus_update_nodes(Engine):
     n = t.n
     for q in range(t.resv_slots):
         assert not left[:, q * n + idx[:4]].any()
+
+
+def _two_node_case():
+    """_reserve_case's node twice: two feasible nodes, so PreScore runs."""
+    from koordinator_amd.snapshot import concat
+    prof, t, p, topo = _reserve_case()
+    t2 = concat([t, t.copy()])
+    return prof, t2, p, topo
+
+
+def test_single_feasible_node_skips_the_nomination_oracle():
+    """(upstream) schedulePod returns the only feasible node without
+    prioritizeNodes, so no reservation is nominated before the NUMA Reserve:
+    the pod takes free CPUs (the Reservation Reserve still assumes it into the
+    reservation).  With two feasible nodes PreScore nominates and the pod gets
+    the reserved 4-7."""
+    prof, t, p, topo = _reserve_case()
+    o = oracle.Oracle(to_c_config(prof), t)
+    node, cs = o.place_stream(p, cpusets=True)
+    assert node[0] == 0 and not set(topo.cpus(cs[0])) & set(range(4, 11))
+    assert o.resv_state()["assigned"][0] == 1
+    prof, t2, p, topo = _two_node_case()
+    node, cs = oracle.Oracle(to_c_config(prof), t2).place_stream(p, cpusets=True)
+    assert node[0] == 0 and format_cpuset(topo.cpus(cs[0])) == "4-7"
+
+
+@pytest.mark.gpu
+def test_gpu_single_feasible_node_skips_the_nomination(Engine):
+    for case in (_reserve_case, _two_node_case):
+        prof, t, p, topo = case()
+        ref_node, ref_cs = oracle.Oracle(to_c_config(prof), t).place_stream(p, cpusets=True)
+        with Engine(prof, device=0) as e:
+            e.load_snapshot(t)
+            got = e.place_stream(p)
+            cs = e.fetch_cpusets(1)
+        assert np.array_equal(got, ref_node) and np.array_equal(cs, ref_cs), case.__name__
