@@ -292,3 +292,26 @@ def test_gpu_single_feasible_node_skips_the_nomination(Engine):
             got = e.place_stream(p)
             cs = e.fetch_cpusets(1)
         assert np.array_equal(got, ref_node) and np.array_equal(cs, ref_cs), case.__name__
+
+
+@pytest.mark.gpu
+def test_gpu_resv_cpus_checkpoint_restore(Engine):
+    """koordhip_checkpoint / koordhip_restore roll the reserved CPUs back with
+    the other mutable columns: a restored second pass repeats the first."""
+    prof, t, pods = _workload(2000, 1500, seed=17)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        e.checkpoint()
+        e.stage_pods(pods)
+        e.place_staged()
+        a = e.fetch_placements(len(pods))
+        ra = e.read_reservations()
+        e.restore()
+        assert np.array_equal(e.read_reservations()["cpus"], _resv_cpu_masks(t))
+        e.place_staged()
+        b = e.fetch_placements(len(pods))
+        rb = e.read_reservations()
+    assert np.array_equal(a, b)
+    for k in ("allocated", "assigned", "cpus"):
+        assert np.array_equal(ra[k], rb[k]), k
+    assert (ra["cpus"] != _resv_cpu_masks(t)).any()
