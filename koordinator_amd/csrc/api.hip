@@ -786,8 +786,10 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
   c->side = c->numa || c->resv;
-  // Reservation builds: 4 nodes per lane (config 5 scan 195 -> 170 us per launch, 143k -> 150k pods/s)
-  c->partial_r = c->resv ? 4 : 2;
+  // 4 nodes per lane: Reservation builds (config 5 scan 195 -> 170 us per launch, 143k -> 150k pods/s) and,
+  // since round 3's resolve, the plain set too (config 4 with 6 select workgroups per pod: 1.117M -> 1.157M
+  // pods/s, profiles/r03_ab/sweep4.txt); the NUMA-only scan stays at 2
+  c->partial_r = (c->resv || !c->numa) ? 4 : 2;
   if (const char *r = std::getenv("KOORDHIP_TOPK_R")) {
     const int v = std::atoi(r);
     if (v == 1 || v == 2 || v == 4 || v == 8) c->partial_r = v;
@@ -855,7 +857,8 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     if (e == hipSuccess && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0))
       cus = 256;
     c->n_cu = cus;
-    c->sel_g = std::max(1, std::min(kh::kSelGMax, cus / c->batch));
+    // (5/8 of a CU per pod and round: config 4 measured 6 per pod above 10)
+    c->sel_g = std::max(1, std::min(kh::kSelGMax, (cus * 5) / (8 * c->batch)));
     if (const char *g = std::getenv("KOORDHIP_SEL_G")) c->sel_g = std::max(1, std::min(kh::kSelGMax, std::atoi(g)));
   }
   // KOORDHIP_CU_RESERVE=<mask>: the persistent resolve gets the CUs of bit
