@@ -429,6 +429,11 @@ int koordhip_last_kernel_stats(koordhip_ctx *ctx, koordhip_kernel_stats *out);
  * events cost a few microseconds per round: bench.py times its steps with it
  * off and takes the per-kernel split from one extra step). */
 int koordhip_set_profile_kernels(koordhip_ctx *ctx, int32_t on);
+/* The template instantiations the last place call launched for its evaluation
+ * (k_scan / k_eval_topk) and its resolve, spelled as rocprofv3 names them
+ * ("kh::k_scan<4, 0>"), NUL-terminated in buffers of `cap` bytes -- so a
+ * profile can be matched to the exact kernel a timed run used. */
+int koordhip_last_kernel_names(koordhip_ctx *ctx, char *eval_out, char *resolve_out, int32_t cap);
 
 /* ---- multi-GPU (node-index sharding, RCCL all-gather of per-shard top-k) -- */
 #define KOORDHIP_UNIQUE_ID_BYTES 128

@@ -227,6 +227,7 @@ def load_library(path: str = LIB_PATH):
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_last_kernel_stats": (C.c_int, [vp, C.POINTER(KoordhipKernelStats)]),
         "koordhip_set_profile_kernels": (C.c_int, [vp, C.c_int32]),
+        "koordhip_last_kernel_names": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_int32]),
         "koordhip_comm_unique_id": (C.c_int, [C.c_char_p]),
         "koordhip_comm_init": (C.c_int, [vp, C.c_char_p, C.c_int32, C.c_int32]),
         "koordhip_comm_init_local": (C.c_int, [C.POINTER(vp), C.c_int32]),
@@ -248,7 +249,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
     "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
     "koordhip_read_resv_cpus", "koordhip_last_stats", "koordhip_last_kernel_stats",
-    "koordhip_set_profile_kernels",
+    "koordhip_set_profile_kernels", "koordhip_last_kernel_names",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]
 

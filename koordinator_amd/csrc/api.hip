@@ -174,6 +174,7 @@ struct koordhip_ctx {
   hipEvent_t t0 = nullptr, t1 = nullptr;
   int32_t ev_used = 0;
   double last_eval_ms = 0, last_total_ms = 0;
+  std::string eval_kernel, resolve_kernel;  // template instantiations of the last place call's launches
   int64_t last_launches = 0, last_evals = 0;
 };
 
@@ -368,6 +369,7 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
     uint32_t *w = c->d_etk_sync[slot];
     HIP_TRY(kh::launch_eval_topk(c->dc, c->d, d_pods, np, lo, hi, k, vt, c->d_etk_part[slot], c->d_etk_pcnt[slot],
                                  w + kh::kSelMaxPods, out, sync, sel_par, res_wait, c->d_dbg, es));
+    c->eval_kernel = kh::last_eval_kernel();
     if (int e = timed_end(c, tm, es)) return e;
     c->last_launches++;
     c->last_evals += (int64_t)np * (hi - lo);
@@ -386,6 +388,7 @@ int topk_batch(koordhip_ctx *c, const kh::DevPod *d_pods, int32_t np, int32_t k,
     if (int e = timed_begin(c, TK_SCAN, es, &tm)) return e;
   const int32_t ppw = c->scan_ppw < 0 ? kh::scan_ppw(R, lo, hi, np) : c->scan_ppw;
   HIP_TRY(kh::launch_scan(R, c->dc, c->d, d_pods, np, lo, hi, S, stride, Mx, mstride, ppw, es));
+  c->eval_kernel = kh::last_eval_kernel();
   if (int e = timed_end(c, tm, es)) return e;
   c->last_launches++;
   c->last_evals += (int64_t)np * (hi - lo);
@@ -1659,6 +1662,7 @@ int place_staged_impl(koordhip_ctx *c) {
     if (int e = timed_begin(c, TK_RESOLVE, c->rstream, &tm)) return e;
     HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, lag, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
+    c->resolve_kernel = kh::last_resolve_kernel();
     res_tm = tm;  // its end event is recorded after the round loop (nothing else runs on rstream)
   }
   for (int32_t r = 0; r < rounds; r++) {
@@ -1695,6 +1699,7 @@ int place_staged_impl(koordhip_ctx *c) {
       if (int e = timed_begin(c, TK_RESOLVE, rs, &tm)) return e;
       HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, r, r + 1, lists0, list_buf, c->monotone, 1, sync,
                                  mbuf, c->d_out, cpus, c->d_dbg, trace, rs));
+      c->resolve_kernel = kh::last_resolve_kernel();
       if (int e = timed_end(c, tm, rs)) return e;
     }
   }
@@ -1969,6 +1974,13 @@ int koordhip_last_kernel_stats(koordhip_ctx *c, koordhip_kernel_stats *out) {
 int koordhip_set_profile_kernels(koordhip_ctx *c, int32_t on) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
   c->cfg.profile_kernels = on ? 1 : 0;
+  return 0;
+}
+
+int koordhip_last_kernel_names(koordhip_ctx *c, char *eval_out, char *resolve_out, int32_t cap) {
+  if (!c || !eval_out || !resolve_out || cap < 1) return fail(KOORDHIP_EINVAL, "NULL argument");
+  std::snprintf(eval_out, (size_t)cap, "%s", c->eval_kernel.c_str());
+  std::snprintf(resolve_out, (size_t)cap, "%s", c->resolve_kernel.c_str());
   return 0;
 }
 

@@ -82,6 +82,10 @@ hipError_t launch_scatter(T *dst, const T *src, const int32_t *idx, int32_t m, h
 constexpr int32_t kResolveMaxK = 128;  // longest list the resolve takes (RES_MAXP)
 // nm: the kernels' node-row mode, 0 none, 1 NodeNUMAResource, 2 + topology-policy zones, 3 + Reservation
 int side_mode(const DevCfg &c);
+// the last evaluation / resolve kernel instantiation launched by this host
+// thread, as rocprofv3 names it ("kh::k_scan<4, 0>")
+const char *last_eval_kernel();
+const char *last_resolve_kernel();
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, int nm, int32_t lag);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "eval.hpp"
@@ -3080,6 +3081,17 @@ hipError_t launch_eval_full(const DevCfg &c, const DevNodes &d, const DevPod *po
   return hipGetLastError();
 }
 
+// the template instantiation of the last evaluation / resolve launch of this
+// host thread, spelled as rocprofv3 names it (bench.py matches the committed
+// PMC summary against it)
+static thread_local char g_eval_name[64], g_resolve_name[64];
+template <typename... A>
+static inline void note_kernel(char *dst, const char *fmt, A... a) {
+  std::snprintf(dst, 64, fmt, a...);
+}
+const char *last_eval_kernel() { return g_eval_name; }
+const char *last_resolve_kernel() { return g_resolve_name; }
+
 int32_t scan_chunks(int R, int32_t lo, int32_t hi) { return hi > lo ? (hi - lo + 64 * R - 1) / (64 * R) : 0; }
 
 int32_t scan_ppw(int R, int32_t lo, int32_t hi, int32_t n_pods) {
@@ -3102,6 +3114,7 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
     const int32_t cqx = ((nchunks + 3) / 4 + 7) / 8;
     const int32_t nblocks = 8 * cqx * ((n_pods + ppw - 1) / ppw);
 #define KH_SCAN_NM(RR, NN)                                                                                          \
+  note_kernel(g_eval_name, "kh::k_scan_nm<%d, %d>", RR, NN);                                                        \
   hipLaunchKernelGGL((k_scan_nm<RR, NN>), dim3(nblocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cqx, \
                      ppw, S, s_stride, Mx, m_stride)
     switch (nm * 2 + (R - 1)) {
@@ -3124,8 +3137,11 @@ hipError_t launch_scan(int R, const DevCfg &c, const DevNodes &d, const DevPod *
   // what its L2 keeps across a sweep (measured: neutral at 50k nodes, +5 % at 200k)
   const int32_t pfast = (hi - lo) > kScanPodFastNodes ? 1 : 0;
 #define KH_SCAN(RR, NN)                                                                                            \
-  hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks, cpx, \
-                     pfast, S, s_stride, Mx, m_stride)
+  do {                                                                                                        \
+    note_kernel(g_eval_name, "kh::k_scan<%d, %d>", RR, NN);                                                      \
+    hipLaunchKernelGGL((k_scan<RR, NN>), dim3(blocks), dim3(256), lds, s, c, d, pods, n_pods, lo, hi, nchunks,  \
+                       cpx, pfast, S, s_stride, Mx, m_stride);                                                  \
+  } while (0)
   if (nm == 5) {
     switch (R) {
       case 4: KH_SCAN(4, 5); break;
@@ -3302,6 +3318,7 @@ hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *po
       if (e != hipSuccess) return e;                                                                                \
       attr[NN][vi][GG] = true;                                                                                      \
     }                                                                                                               \
+    note_kernel(g_eval_name, "kh::k_eval_topk<%d, %d, %d, %d>", NN, VV, RR, GG);                                  \
     hipLaunchKernelGGL((k_eval_topk<NN, VV, RR, GG>), dim3(blocks), dim3(ETK_THREADS), lds, s, c, d, pods, n_pods,   \
                        lo, hi, nslices, spx, k, part, pcnt, arrive, out, sync, sel_par, res_wait, stage_cap, dbg);  \
   } while (0)
@@ -3418,9 +3435,12 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   }
   if (o.total > RES_LDS_MAX) return hipErrorInvalidValue;
 #define KH_RESOLVE_D(NN, DD)                                                                                  \
-  hipLaunchKernelGGL((k_resolve<NN, DD>), dim3(1), dim3(res_threads<NN>()), o.total, s, c, d_desc, d.n, d.nu.cls, pods, \
-                     total, P, k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, lag, sync, o, out_node, out_cpus, \
-                     dbg, trace)
+  do {                                                                                                        \
+    note_kernel(g_resolve_name, DD ? "kh::k_resolve<%d, true>" : "kh::k_resolve<%d, false>", NN);                \
+    hipLaunchKernelGGL((k_resolve<NN, DD>), dim3(1), dim3(res_threads<NN>()), o.total, s, c, d_desc, d.n, d.nu.cls, \
+                       pods, total, P, k, kp, r_begin, r_end, mbuf, lists0, list_buf, monotone, lag, sync, o, out_node, \
+                       out_cpus, dbg, trace);                                                                   \
+  } while (0)
 #define KH_RESOLVE(NN)       \
   if (dbg)                   \
     KH_RESOLVE_D(NN, true);  \

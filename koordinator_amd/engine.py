@@ -164,6 +164,13 @@ class PlacementEngine:
         abi.check(self.lib, self.lib.koordhip_last_kernel_stats(self._ctx, C.byref(st)))
         return {f: getattr(st, f) for f, _ in abi.KoordhipKernelStats._fields_ if f != "reserved"}
 
+    def kernel_names(self) -> dict:
+        """Template instantiations of the last place call's evaluation and
+        resolve launches, spelled as rocprofv3 names them."""
+        ev, rs = C.create_string_buffer(64), C.create_string_buffer(64)
+        abi.check(self.lib, self.lib.koordhip_last_kernel_names(self._ctx, ev, rs, 64))
+        return {"eval": ev.value.decode(), "resolve": rs.value.decode()}
+
     # ---- multi-GPU ----------------------------------------------------------
     @staticmethod
     def comm_unique_id() -> bytes:

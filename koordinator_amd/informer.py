@@ -29,7 +29,16 @@ Reservations (the Reservation plugin's reservationCache, reservation/cache.go:
 delete re-derives the resv_* columns of the nodes it leaves and enters.  Owner
 groups are append-only (``resv_index``): pod masks made earlier stay valid.  A
 reservation-order value the snapshot has no rank for needs a reload (ranks are
-snapshot-wide).
+snapshot-wide).  Every reload rebuilds the owner groups from the live
+reservations (pod masks made before it are stale); a new group past
+RESV_MAX_GROUPS, or reserved CPUs on a snapshot loaded without the resv_cpus
+columns, asks for a reload too.  ``register_pods`` registers the pods to
+schedule (their reservation affinities and upstream static-filter classes)
+before ``pod_records``; one the snapshot does not cover asks for a reload.
+
+``flush`` hands the rows to the engine first and adopts them into the
+informer's table image only when ``update_nodes`` succeeded, so a failed call
+leaves the rows dirty for the next flush.
 """
 from __future__ import annotations
 
@@ -38,7 +47,7 @@ from typing import Dict, List, Optional, Set
 
 import numpy as np
 
-from . import k8s
+from . import abi, k8s
 from .config import Profile
 from . import numa as nm
 from . import reservation as rv
@@ -118,12 +127,15 @@ class Informer:
         self._classes: Optional[nm.ClassTable] = None
         self.resv_index = rv.ReservationIndex()
         self._resv_rank: Dict[int, int] = {}
+        self._resv_cpus_loaded = False                      # the snapshot carried resv_cpus columns
+        from .nodefilters import StaticClasses
+        self.static_classes = StaticClasses()
 
     # ---- full snapshot --------------------------------------------------------
     def table(self, now: float) -> NodeTable:
         """A full snapshot of the current state (initial load, or after the node set changed)."""
         self._sync_assigned()
-        t = build_table(self.cluster, self.profile, now)
+        t = build_table(self.cluster, self.profile, now, self.static_classes)
         if self.nrts:
             self._classes = nm.ClassTable()
             for i, node in enumerate(self.cluster.nodes):
@@ -132,7 +144,11 @@ class Informer:
         elif self._table is not None:
             _keep_numa(t, self._table)
         self._resv_rank = rv.order_ranks(rv.available_by_node(self._index, list(self.reservations.values())).values())
-        rv.reservation_columns(t, self._index, list(self.reservations.values()), self.resv_index)
+        # owner groups from the live reservations only (the registered affinities stay)
+        self.resv_index = rv.ReservationIndex(affinities=list(self.resv_index.affinities))
+        rv.reservation_columns(t, self._index, list(self.reservations.values()), self.resv_index,
+                               self._node_labels())
+        self._resv_cpus_loaded = _has_resv_cpus(t)
         self._table = t
         self._dirty.clear()
         self._reload = False
@@ -145,8 +161,13 @@ class Informer:
         if table.names != [n.name for n in self.cluster.nodes]:
             raise ValueError("table rows do not match the informer's node set")
         self._table = table
+        self._resv_cpus_loaded = _has_resv_cpus(table)
         self._expired = self._expiry_states(now)
         self._now = now
+
+    def _node_labels(self) -> Dict[str, Dict[str, str]]:
+        """What reservation affinities see of each node (reservation/transformer.go:335-359)."""
+        return {n.name: dict(n.labels or {}) for n in self.cluster.nodes}
 
     # ---- node events -------------------------------------------------------------
     def on_node_add(self, node: k8s.Node):
@@ -318,10 +339,25 @@ class Informer:
         if old is not None and old.node_name:
             self._dirty.add(old.node_name)
 
+    def register_pods(self, pods) -> bool:
+        """Register the pods about to be scheduled: their required reservation
+        affinities (ReservationIndex.register_affinities) and upstream static
+        filter classes.  True when the loaded snapshot does not cover them:
+        rebuild it (table()) before pod_records."""
+        from .marshal import pod_static, static_filters_of
+        pods = list(pods)
+        if self.resv_index.register_affinities(pods):
+            self._reload = True
+        if static_filters_of(self.profile):
+            for p in pods:
+                if self.static_classes.classify(pod_static(p)) >= self.static_classes.frozen:
+                    self._reload = True
+        return self._reload
+
     def pod_records(self, pods):
-        """Pod records with the current owner groups' match masks."""
+        """Pod records with the current owner groups' match masks and static classes."""
         from .marshal import pod_records
-        return pod_records(pods, self.profile, self.resv_index)
+        return pod_records(pods, self.profile, self.resv_index, self.static_classes)
 
     # ---- deltas ----------------------------------------------------------------------------
     def _sync_assigned(self):
@@ -334,9 +370,10 @@ class Informer:
     def pending(self) -> Set[str]:
         return set(self._dirty)
 
-    def delta(self, now: float):
-        """(row indices, NodeTable of those rows, FlushResult); applies them to
-        the informer's own table image too."""
+    def delta(self, now: float, apply: bool = True):
+        """(row indices, NodeTable of those rows, FlushResult); with `apply` the
+        rows also go into the informer's own table image (flush applies them
+        only after the engine took them)."""
         res = FlushResult(needs_reload=self._reload)
         if self._reload or self._table is None:
             res.needs_reload = True
@@ -366,26 +403,49 @@ class Informer:
         if any(len(placed.get(int(i), [])) > rows.resv_slots for i in idx):
             res.needs_reload = True                  # more reservations on a node than the snapshot's slots
             return np.zeros(0, np.int32), None, res
+        labels = self._node_labels()
         for j, i in enumerate(idx):
-            node_row(rows, j, self.cluster.nodes[int(i)], self.cluster, self.profile, now)
+            node = self.cluster.nodes[int(i)]
+            node_row(rows, j, node, self.cluster, self.profile, now, self.static_classes)
             r = placed.get(int(i))
             if r is None:
                 rv.clear_reservation_row(rows, j)
-            else:
-                rv.reservation_row(rows, j, r, self.resv_index, self._resv_rank)
+                continue
+            try:
+                rv.reservation_row(rows, j, r, self.resv_index, self._resv_rank, labels.get(node.name))
+            except rv.ReservationError:
+                if len(self.resv_index.groups) < abi.RESV_MAX_GROUPS:
+                    raise
+                res.needs_reload = True              # owner groups full: a reload regroups the live reservations
+                return np.zeros(0, np.int32), None, res
+        if not self._resv_cpus_loaded and _has_resv_cpus(rows):
+            res.needs_reload = True                  # reserved CPUs need the resv_cpus columns at load_snapshot
+            return np.zeros(0, np.int32), None, res
+        res.rows = len(idx)
+        if apply:
+            self._adopt(idx, rows)
+        return idx, rows, res
+
+    def _adopt(self, idx, rows):
         for c in rows.cols:
             self._table.cols[c][idx] = rows.cols[c]
         self._dirty.clear()
-        res.rows = len(idx)
-        return idx, rows, res
 
     def flush(self, engine, now: float) -> FlushResult:
-        """Push the pending row deltas into `engine` (one koordhip_update_nodes call)."""
-        idx, rows, res = self.delta(now)
+        """Push the pending row deltas into `engine` (one koordhip_update_nodes
+        call); the informer's image takes them only once the engine has."""
+        idx, rows, res = self.delta(now, apply=False)
         if res.needs_reload or rows is None:
             return res
         engine.update_nodes(idx, rows)
+        self._adopt(idx, rows)
         return res
+
+
+def _has_resv_cpus(t: NodeTable) -> bool:
+    from .snapshot import RESV_CPU_COLS, slot_col
+    return any(t.cols[slot_col(c, q)].any() for q in range(t.resv_slots) for c in RESV_CPU_COLS
+               if slot_col(c, q) in t.cols)
 
 
 def _keep_numa(dst: NodeTable, src: NodeTable):

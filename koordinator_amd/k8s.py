@@ -163,6 +163,13 @@ class Pod:
     phase: str = "Running"
     owner_refs: List[OwnerReference] = field(default_factory=list)
     api_version: str = "v1"
+    # what the upstream static filters read (nodefilters.py): spec.nodeSelector,
+    # spec.affinity.nodeAffinity.requiredDuringScheduling... terms
+    # (reservation.NodeSelectorTerm; None = unset), spec.tolerations
+    # (nodefilters.Toleration)
+    node_selector: Dict[str, str] = field(default_factory=dict)
+    required_node_affinity: Optional[list] = None
+    tolerations: list = field(default_factory=list)
 
     @property
     def key(self) -> str:
@@ -175,6 +182,8 @@ class Node:
     allocatable: ResourceList = field(default_factory=dict)
     annotations: Dict[str, str] = field(default_factory=dict)
     labels: Dict[str, str] = field(default_factory=dict)
+    taints: list = field(default_factory=list)      # spec.taints (nodefilters.Taint)
+    unschedulable: bool = False                     # spec.unschedulable
 
 
 @dataclass

@@ -153,10 +153,47 @@ def nonzero_request(pod: k8s.Pod) -> Tuple[int, int]:
     return cpu, mem
 
 
-def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None, resv_index=None) -> np.ndarray:
+def node_static(node: k8s.Node):
+    """The node fields the upstream static filters read (nodefilters.NodeStatic)."""
+    from .nodefilters import NodeStatic
+    return NodeStatic(labels=dict(node.labels or {}), taints=list(node.taints), unschedulable=node.unschedulable,
+                      name=node.name)
+
+
+def pod_static(pod: k8s.Pod):
+    """The pod fields the upstream static filters read (its static class key)."""
+    from .nodefilters import PodStatic
+    return PodStatic(node_selector=dict(pod.node_selector or {}), required_terms=pod.required_node_affinity,
+                     tolerations=list(pod.tolerations))
+
+
+def static_filters_of(profile: Profile) -> List[str]:
+    from .config import STATIC_FILTERS
+    return [f for f in profile.resolved().filters if f in STATIC_FILTERS]
+
+
+def static_class_of(pod: k8s.Pod, profile: Profile, static_classes) -> int:
+    """The pod's static class in `static_classes` (nodefilters.StaticClasses).
+    Its node bits were computed when the snapshot was built: a class first seen
+    after that (index >= static_classes.frozen) has no bits on the device, so
+    the snapshot must be rebuilt (MarshalError)."""
+    if not static_filters_of(profile):
+        return 0
+    if static_classes is None:
+        raise MarshalError("the profile enables static node filters: pass the snapshot's StaticClasses")
+    c = static_classes.classify(pod_static(pod))
+    if c >= getattr(static_classes, "frozen", abi.MAX_STATIC_CLASSES):
+        raise MarshalError("pod static class first seen after the snapshot was built: rebuild it (static_allow)")
+    return c
+
+
+def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None, resv_index=None,
+               static_classes=None) -> np.ndarray:
     """One koordhip_pod record for `pod` (the per-pod PreFilter products);
     `resv_index` (reservation.ReservationIndex): the snapshot's reservation
-    owner groups the pod is matched against."""
+    owner groups the pod is matched against; `static_classes`
+    (nodefilters.StaticClasses): the snapshot's pod static classes (required
+    when the profile enables NodeUnschedulable / NodeAffinity / TaintToleration)."""
     p = profile.resolved()
     rec = out if out is not None else pod_array(1)[0]
     req, present = fit_request(pod)
@@ -191,15 +228,27 @@ def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None,
     rec["numa_cpus"] = ncpus
     rec["numa_policy"] = pol
     rec["resv_match"] = resv_index.pod_mask(pod) if resv_index is not None else 0
+    rec["static_class"] = static_class_of(pod, profile, static_classes)
     return rec
 
 
-def pod_records(pods: Iterable[k8s.Pod], profile: Profile, resv_index=None) -> np.ndarray:
+def pod_records(pods: Iterable[k8s.Pod], profile: Profile, resv_index=None, static_classes=None) -> np.ndarray:
     pods = list(pods)
     arr = pod_array(len(pods))
     for i, p in enumerate(pods):
-        pod_record(p, profile, arr[i], resv_index)
+        pod_record(p, profile, arr[i], resv_index, static_classes)
     return arr
+
+
+def static_classes_for(pods: Iterable[k8s.Pod], profile: Profile):
+    """A StaticClasses registry holding the static classes of `pods` (the pods
+    a snapshot will schedule), for build_table / pod_records."""
+    from .nodefilters import StaticClasses
+    sc = StaticClasses()
+    if static_filters_of(profile):
+        for pod in pods:
+            sc.classify(pod_static(pod))
+    return sc
 
 
 # ---------------------------------------------------------------------------
@@ -362,11 +411,22 @@ def estimated_assigned_pod_used(cluster: ClusterState, node_name: str, nm: k8s.N
     return est_used, est_pods
 
 
-def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, profile: Profile, now: float):
-    """Fill row i of `table` from the objects (Fit accounting + LoadAware state)."""
+def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, profile: Profile, now: float,
+             static_classes=None):
+    """Fill row i of `table` from the objects (Fit accounting + LoadAware state,
+    and the static_allow bits of `static_classes` when the profile enables the
+    upstream static filters)."""
     p = profile.resolved()
     args = p.loadaware
     t = table.cols
+    sf = static_filters_of(p)
+    if sf:
+        from .nodefilters import static_allow
+        if static_classes is None:
+            raise MarshalError("the profile enables static node filters: pass the snapshot's StaticClasses")
+        t["static_allow"][i] = static_allow([node_static(node)], static_classes, sf)[0]
+    else:
+        t["static_allow"][i] = 0xFFFFFFFF
     # ---- Fit: Allocatable / Requested / NonZeroRequested / len(Pods)
     alloc = node.allocatable
     t["alloc0"][i] = alloc[k8s.CPU].milli_value() if k8s.CPU in alloc else 0
@@ -474,9 +534,14 @@ def _check_thr_keys(th: Dict[str, int]):
             raise MarshalError(f"usage threshold on {k!r} is not supported by the engine (cpu, memory only)")
 
 
-def build_table(cluster: ClusterState, profile: Profile, now: float) -> NodeTable:
+def build_table(cluster: ClusterState, profile: Profile, now: float, static_classes=None) -> NodeTable:
+    """The snapshot of `cluster`; with static filters enabled the node bits
+    cover the classes `static_classes` holds now, which it then freezes (a pod
+    of a later class needs a rebuilt snapshot)."""
     t = NodeTable.empty(len(cluster.nodes))
     t.names = [n.name for n in cluster.nodes]
     for i, node in enumerate(cluster.nodes):
-        node_row(t, i, node, cluster, profile, now)
+        node_row(t, i, node, cluster, profile, now, static_classes)
+    if static_classes is not None:
+        static_classes.frozen = len(static_classes.specs)
     return t

@@ -127,6 +127,7 @@ class StaticClasses:
     def __init__(self):
         self.specs: List[PodStatic] = []
         self._index: Dict[Tuple, int] = {}
+        self.frozen = abi.MAX_STATIC_CLASSES   # classes with node bits on the device (set by marshal.build_table)
 
     def classify(self, pod: PodStatic) -> int:
         k = pod.key()

@@ -1,27 +1,35 @@
 #!/bin/bash
-# Iteration pass on the GPU box: GPU parity tests (optionally a -k filter),
-# the config-4 bench with resolve stamps and without, then a rocprofv3
-# kernel-stats pass (PROFILE=name).  Each GPU step is time-limited; the first
-# failure stops the script.
+# Iteration pass: a GPU test selection (TESTS_FILES / TESTS_K; SKIP_TESTS=1 for
+# none), then bench lines (no CPU baseline) of WORKLOADS under each
+# environment variant in VARIANTS ("X=1" = the defaults).  Time-limited steps;
+# the first failure stops the script.
 set -u
 mkdir -p gpurun_out
-K=${TESTS_K:-}
-if [ -n "$K" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$K" > gpurun_out/iter_tests.log 2>&1
-else
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/iter_tests.log 2>&1
+FILES=${TESTS_FILES:-"tests/test_gpu_parity.py tests/test_gpu_reservation.py tests/test_gpu_numa.py tests/test_fit_kat.py"}
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+  timeout -k 10 900 python -u -m pytest $FILES -m gpu -x -q --timeout 120 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} > gpurun_out/iter_tests.log 2>&1
+  rc=$?; tail -25 gpurun_out/iter_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
-rc=$?; tail -15 gpurun_out/iter_tests.log; [ $rc -eq 0 ] || exit $rc
-KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/iter_stamps.json 2> gpurun_out/iter_stamps.err || exit $?
-grep "stamps" gpurun_out/iter_stamps.err | tail -4
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/iter_bench.json 2> gpurun_out/iter_bench.err || exit $?
-cut -c1-300 gpurun_out/iter_bench.json
-if [ -n "${PROFILE:-}" ]; then
-  bash scripts/profile.sh $PROFILE --steps 2 --warmup 1 ${BENCH_ARGS:-} || exit $?
-  python3 - "$PROFILE" <<'PY'
-import csv, glob, sys
-f = glob.glob(f"gpurun_out/{sys.argv[1]}/**/*kernel_stats.csv", recursive=True)
-for row in csv.DictReader(open(f[0])):
-    print(row["Name"][:60], row["Calls"], row["AverageNs"], row["Percentage"])
+for w in ${WORKLOADS:-config4 config5 config3}; do
+  for v in ${VARIANTS:-X=1}; do
+    env $v timeout -k 10 300 python bench.py --workload $w --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
+      > gpurun_out/iter_${w}_${v}.json 2> gpurun_out/iter_${w}_${v}.err
+    rc=$?
+    python3 - gpurun_out/iter_${w}_${v}.json "$w $v" <<'PY'
+import json, sys
+try:
+    d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+    print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], "eval us", d["eval_roofline"]["avg_launch_us"],
+          "select us", d["select"]["avg_launch_us"], "unsched", d["unschedulable"])
+except Exception as e:
+    print(sys.argv[2], "no result", e)
 PY
-fi
+    [ $rc -eq 0 ] || { tail -20 gpurun_out/iter_${w}_${v}.err; exit $rc; }
+    if [ "${STAMPS:-0}" = 1 ]; then
+      env $v KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
+        > /dev/null 2> gpurun_out/iter_stamps_${w}_${v}.err || exit 1
+      grep "stamps\] \(resolve\|round\|prologue\)" gpurun_out/iter_stamps_${w}_${v}.err | tail -4 | cut -c1-300
+    fi
+  done
+done
+exit 0

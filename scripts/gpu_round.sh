@@ -1,16 +1,56 @@
 #!/bin/bash
-# Round evidence: full GPU suite + smoke, bench lines of configs 4 / 3 / 5, rocprofv3 kernel stats of configs 3, 4 and 5.
-# Usage: ROUND=r02x bash scripts/gpu_round.sh (through scripts/gpu.sh)
+# One GPU-box pass producing a round's evidence (or a subset of it).
+#   ROUND=r04a STAGES="tests smoke bench stamps prof pmc" bash scripts/gpu_round.sh
+# stages:
+#   tests   full `pytest -m gpu` (TESTS_FILES / TESTS_K narrow it)
+#   smoke   __graft_entry__.smoke()
+#   bench   bench lines of WORKLOADS (default config4 config3 config5), CPU baseline on
+#   quick   bench lines without the CPU baseline (iteration)
+#   stamps  KOORDHIP_STAMPS resolve / select cycle stamps per workload
+#   prof    rocprofv3 --kernel-trace --stats per workload
+#   pmc     FETCH_SIZE / WRITE_SIZE passes per workload (KOORDHIP_SERIAL: no persistent resolve)
+# Every GPU step has its own time limit; the first failure stops the script.
 set -u
-R=${ROUND:-r02c}
+R=${ROUND:-r04x}
+STAGES=${STAGES:-tests smoke bench stamps prof pmc}
+WORKLOADS=${WORKLOADS:-config4 config3 config5}
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${R}_pytest.log 2>&1
-rc=$?; tail -2 gpurun_out/${R}_pytest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${R}_smoke.log 2>&1 || exit 1
-timeout -k 10 400 python bench.py --steps 5 --warmup 2 > gpurun_out/bench_${R}.json 2> gpurun_out/bench_${R}.err || exit 1
-timeout -k 10 300 python bench.py --workload config3 --steps 3 --warmup 1 --cpu-budget 8 > gpurun_out/bench_${R}_config3.json 2> gpurun_out/bench_${R}_config3.err || exit 1
-timeout -k 10 400 python bench.py --workload config5 --steps 2 --warmup 1 --cpu-budget 8 > gpurun_out/bench_${R}_config5.json 2> gpurun_out/bench_${R}_config5.err || exit 1
-bash scripts/profile.sh ${R}_config3 --workload config3 --steps 2 --warmup 1 || exit 1
-bash scripts/profile.sh ${R}_config4 --steps 2 --warmup 1 || exit 1
-bash scripts/profile.sh ${R}_config5 --workload config5 --steps 1 --warmup 1 || exit 1
-for f in bench_${R} bench_${R}_config3 bench_${R}_config5; do cut -c1-200 gpurun_out/$f.json; done
+has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
+steps_of() { case $1 in config4) echo "--steps 5 --warmup 2";; config3) echo "--steps 3 --warmup 1";; *) echo "--steps 2 --warmup 1";; esac; }
+pods_pmc() { case $1 in config4) echo 30000;; config3) echo 10000;; *) echo 6000;; esac; }
+
+if has tests; then
+  FILES=${TESTS_FILES:-tests}
+  timeout -k 10 1100 python -u -m pytest $FILES -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} \
+    > gpurun_out/${R}_pytest.log 2>&1
+  rc=$?; tail -4 gpurun_out/${R}_pytest.log; [ $rc -eq 0 ] || { tail -40 gpurun_out/${R}_pytest.log; exit $rc; }
+fi
+if has smoke; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${R}_smoke.log 2>&1 || { cat gpurun_out/${R}_smoke.log; exit 1; }
+fi
+for w in $WORKLOADS; do
+  if has bench || has quick; then
+    extra=""; has bench || extra="--no-cpu-baseline"
+    timeout -k 10 400 python bench.py --workload $w $(steps_of $w) --cpu-budget 8 $extra ${BENCH_ARGS:-} \
+      > gpurun_out/bench_${R}_$w.json 2> gpurun_out/bench_${R}_$w.err || { tail -20 gpurun_out/bench_${R}_$w.err; exit 1; }
+    python3 - gpurun_out/bench_${R}_$w.json $w <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], d["eval_roofline"]["kernel"],
+      "eval us", d["eval_roofline"]["avg_launch_us"], "select us", d["select"]["avg_launch_us"],
+      "P", d["config"]["batch_pods"], "lag", d["config"]["pipeline_lag"], "unsched", d["unschedulable"])
+PY
+  fi
+  if has stamps; then
+    KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
+      > gpurun_out/stamps_${R}_$w.json 2> gpurun_out/stamps_${R}_$w.err || { tail -20 gpurun_out/stamps_${R}_$w.err; exit 1; }
+    grep "stamps\] resolve cycles" gpurun_out/stamps_${R}_$w.err | tail -1 | cut -c1-250
+  fi
+  if has prof; then
+    bash scripts/profile.sh ${R}_$w --workload $w --steps 1 --warmup 1 ${BENCH_ARGS:-} || exit 1
+  fi
+  if has pmc; then
+    KOORDHIP_SERIAL=1 bash scripts/pmc.sh pmc_${R}_$w --workload $w --steps 1 --warmup 0 --pods $(pods_pmc $w) ${BENCH_ARGS:-} || exit 1
+  fi
+done
+exit 0

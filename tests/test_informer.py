@@ -487,10 +487,26 @@ def test_reservation_cpuset_events_rows_equal_rebuild():
     r = rv.Reservation("r0", "n1", uid="ru0", allocatable={k8s.CPU: k8s.Q(4)}, owners=[rv.ReservationOwner()],
                        cpus=[4, 5, 6, 7], assigned_cpus=[4, 5])
     inf.on_reservation(r)
-    inf.flush(eng, NOW)
+    # the snapshot was loaded without resv_cpus columns -> a reload,
+    # not rows the engine would refuse (the image keeps its rows, still dirty)
+    before = {c: eng.table.cols[c].copy() for c in NUMA_COLS[:13]}
+    assert inf.flush(eng, NOW).needs_reload
+    assert all(np.array_equal(eng.table.cols[c], before[c]) for c in before)
+    assert inf.pending() == {"n1"}
+    want = inf.table(NOW)
+    eng = _TableEngine(want)
+    inf.attach(want, NOW)
+    r2 = copy.deepcopy(r)
+    r2.assigned_cpus = [4]
+    inf.on_reservation(r2)                     # now the columns exist: a plain row delta
+    res = inf.flush(eng, NOW)
+    assert not res.needs_reload and res.rows == 1
     want = inf.table(NOW)
     for c in NUMA_COLS[:13] + [f"resv_cpus{w}" for w in range(4)]:
         assert np.array_equal(eng.table.cols[c], want.cols[c]), c
+    inf.on_reservation(r)
+    assert not inf.flush(eng, NOW).needs_reload
+    want = inf.table(NOW)
     topo = nm.linux_topology(2, 1, 8, 2)
     held = topo.mask([4, 5, 6, 7])
     assert not any(int(want[f"numa_free{w}"][1]) & int(held[w]) for w in range(4))
