@@ -31,6 +31,14 @@
  *                              plugin.go:537-575 / cache.go:170-191
  *   resv_cpus columns       <- NodeNUMAResource RestoreReservation nodenumaresource/reservation.go:68-122 and the
  *                              reservation-preferred CPUs of getResourceOptions plugin.go:455-524 (Score / Reserve)
+ *   dev_* columns, koordhip_pod_ext
+ *                           <- DeviceShare PreFilter plugin.go:146-182, Filter :284-323, Score scoring.go:33-80,
+ *                              Reserve plugin.go:368-405 over nodeDevice (device_cache.go:44-482) and the
+ *                              default allocator (allocator.go:91-122)
+ *   static_score columns    <- (upstream) NodeAffinity / TaintToleration Score + NormalizeScore
+ *   koordhip_place_stream_ext / koordhip_eval_ext
+ *                           <- the exact sequential cycle for profiles with plugins whose scores are normalized
+ *                              over the feasible nodes (DefaultNormalizeScore, upstream helper/normalize_score.go)
  */
 #ifndef KOORDHIP_H
 #define KOORDHIP_H
@@ -41,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 8
+#define KOORDHIP_ABI_VERSION 9
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -68,6 +76,20 @@ extern "C" {
                                            Requested + the pod request, 1 - |f_cpu - f_mem| / 2) */
 #define KOORDHIP_NPLUGINS 4             /* plugins with a per-node score in koordhip_eval's scores:
                                            Fit, LoadAware, NUMA, BalancedAllocation */
+/* Plugins whose Score is normalized over the pod's feasible nodes
+ * (DefaultNormalizeScore(100, reverse)): a profile enabling any of them places
+ * through the exact sequential cycle (koordhip_place_stream_ext).
+ * Their raw scores are planes KOORDHIP_NPLUGINS.. of koordhip_eval_ext. */
+#define KOORDHIP_PLUGIN_DEVICESHARE 64u      /* DeviceShare Filter / Score / Reserve (koordhip_pod_ext, dev_* columns) */
+#define KOORDHIP_PLUGIN_AFFINITY_SCORE 128u  /* NodeAffinity Score: preferred terms (static_score[0]) */
+#define KOORDHIP_PLUGIN_TAINT_SCORE 256u     /* TaintToleration Score: intolerable PreferNoSchedule taints
+                                                (static_score[1], normalized reversed) */
+#define KOORDHIP_NEXT_PLUGINS 3              /* DeviceShare, NodeAffinity, TaintToleration */
+/* NodeResourcesFit's extended scalar resources of device pods (koordinator.sh/
+ * gpu-core, gpu-memory-ratio, gpu-memory, nvidia.com/gpu, ...): fitsRequest
+ * checks each one the pod requests against Allocatable - Requested (upstream
+ * fit.go); koordhip_pod_ext.xreq / koordhip_node_soa.xalloc, xrequested */
+#define KOORDHIP_NXRES 8
 #define KOORDHIP_MAX_STATIC_CLASSES 32  /* distinct pod static classes (koordhip_pod.static_class) */
 
 /* Fit resource slots (ResourceSpec names in scheduler-config.yaml:21-31). */
@@ -178,6 +200,20 @@ typedef struct koordhip_numa_class {
 #define KOORDHIP_ST_NUMA_FAIL 4u
 #define KOORDHIP_ST_RESV_FAIL 8u  /* filterWithReservations (reservation/plugin.go:373-440) */
 #define KOORDHIP_ST_STATIC_FAIL 16u /* NodeUnschedulable / NodeAffinity / TaintToleration */
+#define KOORDHIP_ST_DEVICE_FAIL 32u /* DeviceShare Filter (plugin.go:284-323) */
+#define KOORDHIP_ST_XFIT_FAIL 64u   /* NodeResourcesFit on an extended scalar resource (koordhip_pod_ext.xreq) */
+
+/* DeviceShare's device model (nodeDevice, device_cache.go:44-50): per node
+ * and device type up to KOORDHIP_DEV_SLOTS minors, each with the Device CR's
+ * resources (deviceTotal) and what pods hold (deviceUsed); free = total - used
+ * clamped at 0 per resource (resetDeviceFree, :185-202). */
+#define KOORDHIP_DEV_TYPES 3  /* 0 gpu, 1 rdma, 2 fpga (DeviceResourceNames, device_resources.go:42-53) */
+#define KOORDHIP_DEV_GPU 0
+#define KOORDHIP_DEV_RDMA 1
+#define KOORDHIP_DEV_FPGA 2
+#define KOORDHIP_DEV_SLOTS 8  /* minors per type per node */
+#define KOORDHIP_DEV_RES 3    /* gpu: [0] koordinator.sh/gpu-core, [1] gpu-memory-ratio, [2] gpu-memory (bytes);
+                                 rdma / fpga: [0] koordinator.sh/rdma | fpga */
 
 /* place_stream out_node values */
 #define KOORDHIP_UNSCHEDULABLE (-1)
@@ -206,6 +242,14 @@ typedef struct koordhip_config {
   int32_t reservation_weight;  /* Reservation score weight (scheduler-config.yaml:90-91: 5000); must exceed
                                   100 x the sum of the other score weights (Reservation key) */
   int32_t reserved[5];
+  /* ABI 9: the normalized-score plugins */
+  int32_t ext_weight[KOORDHIP_NEXT_PLUGINS]; /* score weights: DeviceShare (scheduler-config.yaml:88-89: 1),
+                                               NodeAffinity, TaintToleration (1..100) */
+  int32_t dev_most_allocated;  /* DeviceShareArgs.ScoringStrategy.Type == MostAllocated (scoring.go:125-132) */
+  int32_t dev_res_weight[5];   /* DeviceShareArgs.ScoringStrategy.Resources weights (0 = not listed): gpu-core,
+                                  gpu-memory-ratio, gpu-memory, rdma, fpga (defaults v1beta2/defaults.go:168-189:
+                                  gpu-memory-ratio, rdma, fpga at 1) */
+  int32_t reserved2[3];
 } koordhip_config;
 
 /* Columnar node snapshot, all arrays of length n, little-endian, caller-owned
@@ -297,6 +341,30 @@ typedef struct koordhip_node_soa {
    * Reserve removes the pod's CPUs.  NULL = no reservation holds CPUs (also
    * the update_nodes default). */
   const uint64_t *resv_cpus[KOORDHIP_NUMA_WORDS];
+  /* ---- ABI 9 (read only by the sequential cycle, koordhip_place_stream_ext) */
+  /* DeviceShare: minors per type per node held by the dev_* columns (0 = no
+   * devices anywhere: the columns may be NULL); dev_minor [n][TYPES][dev_slots]
+   * in ascending minor order, -1 = empty slot; dev_total / dev_used
+   * [n][TYPES][dev_slots][RES]: the minor's Device CR resources (all 0 for an
+   * unhealthy device, buildDeviceResources device_cache.go:550-568) and the
+   * amounts pods hold (advanced by Reserve) */
+  int32_t dev_slots;
+  int32_t reserved2;
+  const uint8_t *dev_present;  /* [n] 1 = the node has a nodeDevice entry (a Device CR); without one DeviceShare's
+                                  Filter passes, its Score is 0 and its Reserve allocates nothing (plugin.go:298-301,
+                                  scoring.go:42-45, :377-380) */
+  const int32_t *dev_minor;
+  const int64_t *dev_total;
+  const int64_t *dev_used;
+  /* NodeResourcesFit extended scalars [KOORDHIP_NXRES][n]: Allocatable and
+   * Requested (advanced by Reserve); NULL = 0 */
+  const int64_t *xalloc;
+  const int64_t *xrequested;
+  /* raw NodeAffinity (sum of the weights of the class's preferred terms that
+   * match) and TaintToleration (count of PreferNoSchedule taints the class does
+   * not tolerate) scores per (pod static class, node), [MAX_STATIC_CLASSES][n];
+   * NULL = 0 */
+  const uint16_t *static_score[2];
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -313,6 +381,20 @@ typedef struct koordhip_pod {
                                  of one class share nodeSelector, required node affinity and tolerations */
   uint64_t resv_match;        /* bit g: MatchReservationOwners(pod, owner group g) (util/reservation/reservation.go:389-410) */
 } koordhip_pod;
+
+/* Per-pod inputs of the normalized-score plugins (the host's DeviceShare
+ * PreFilter: PreparePod, plugin.go:162-182), beside koordhip_pod. */
+typedef struct koordhip_pod_ext {
+  /* ConvertDeviceRequest of each type's request (utils.go:86-181): gpu [0]
+   * core, [1] memory-ratio, [2] memory bytes, -1 = key absent (memory and
+   * ratio are completed per node from its GPU memory, fillGPUTotalMem
+   * utils.go:211-233); rdma / fpga [t][0], 0 = none */
+  int64_t dev_req[KOORDHIP_DEV_TYPES][KOORDHIP_DEV_RES];
+  int64_t xreq[KOORDHIP_NXRES];  /* NodeResourcesFit extended scalar requests */
+  uint32_t flags;                /* KOORDHIP_PODX_* */
+  uint32_t xmask;                /* bit j: the pod's request map holds extended scalar j (xreq[j], even 0) */
+} koordhip_pod_ext;
+#define KOORDHIP_PODX_DEVICE 1u  /* some device request (DeviceShare state.skip == false) */
 
 /* One top-k record of koordhip_eval. */
 typedef struct koordhip_topk {
@@ -361,12 +443,35 @@ int koordhip_read_resv_cpus(koordhip_ctx *ctx, uint64_t *cpus);
 int koordhip_eval(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, uint8_t *status, int32_t *scores,
                   koordhip_topk *topk, int32_t k);
 
+/* ABI 9: the same with koordhip_pod_ext records (ext may be NULL: no device
+ * requests), for every profile, including the normalized-score plugins.
+ * scores: [n_pods][KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS][n], planes
+ * NPLUGINS.. the raw (un-normalized) DeviceShare / NodeAffinity /
+ * TaintToleration scores; topk ranks the normalized weighted sums. */
+int koordhip_eval_ext(koordhip_ctx *ctx, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods,
+                      uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
+
 /* Greedy stream: pods attempted once, in order, each against the state left
  * by all earlier commits; winner = lowest-index max total score; the Reserve
  * delta is applied on device.  out_node[i] = node, -1 unschedulable, -2 the
  * winner's Reserve failed (NodeNUMAResource Allocate; nothing committed, no
  * retry). */
 int koordhip_place_stream(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, int32_t *out_node);
+/* ABI 9: the greedy stream with koordhip_pod_ext records (ext may be NULL).
+ * A profile enabling a normalized-score plugin (DeviceShare, NodeAffinity /
+ * TaintToleration Score) runs the exact sequential cycle: per pod, every node
+ * is filtered and scored on the state all earlier commits left, the
+ * normalized plugins' maxima are reduced over the feasible nodes, then the
+ * lowest-index argmax commits -- one persistent launch over every CU. */
+int koordhip_place_stream_ext(koordhip_ctx *ctx, const koordhip_pod *pods, const koordhip_pod_ext *ext,
+                              int32_t n_pods, int32_t *out_node);
+/* Devices each pod of the last place call got: [n_pods][KOORDHIP_DEV_TYPES]
+ * bit s = dev slot s of its node (the DeviceAllocations PreBind writes,
+ * plugin.go:465-478: every allocated minor holds the pod's per-card request). */
+int koordhip_fetch_devices(koordhip_ctx *ctx, uint32_t *slots, int32_t n_pods);
+/* DeviceShare and extended-scalar mutable state: dev_used [n][TYPES][dev_slots][RES],
+ * xrequested [NXRES][n] (either may be NULL). */
+int koordhip_read_devices(koordhip_ctx *ctx, int64_t *dev_used, int64_t *xrequested);
 
 /* The same split in two so a caller can time the device part alone: stage
  * (host -> HBM copy) then place (HBM-resident pods, result kept on device

@@ -11,12 +11,21 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 8
+KOORDHIP_ABI_VERSION = 9
 NRES = 5
 NPLUGINS = 4
 
 PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_RESERVATION = 1, 2, 4, 8
 PLUGIN_NODE_STATIC, PLUGIN_BALANCED = 16, 32
+# normalized-score plugins (the exact sequential cycle, koordhip_place_stream_ext)
+PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE = 64, 128, 256
+NEXT_PLUGINS = 3
+EXT_PLUGIN_BITS = (PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE)
+NORMALIZED_PLUGINS = PLUGIN_DEVICESHARE | PLUGIN_AFFINITY_SCORE | PLUGIN_TAINT_SCORE
+NXRES = 8
+DEV_TYPES, DEV_SLOTS, DEV_RES = 3, 8, 3
+DEV_GPU, DEV_RDMA, DEV_FPGA = 0, 1, 2
+PODX_DEVICE = 1
 # upstream NodeUnschedulable / NodeAffinity / TaintToleration all map to the
 # host-resolved static filter bit
 PLUGIN_BITS = {"NodeResourcesFit": PLUGIN_FIT, "LoadAwareScheduling": PLUGIN_LOADAWARE,
@@ -57,6 +66,7 @@ def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> in
     return (required & 3) | ((preferred & 3) << 2) | ((exclusive & 3) << 4)
 
 ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL, ST_RESV_FAIL, ST_STATIC_FAIL = 1, 2, 4, 8, 16
+ST_DEVICE_FAIL, ST_XFIT_FAIL = 32, 64
 UNSCHEDULABLE, RESERVE_FAILED = -1, -2
 E_INVAL, E_RESERVE = -1, -6
 UNIQUE_ID_BYTES = 128
@@ -94,6 +104,10 @@ class KoordhipConfig(C.Structure):
         ("numa_most_allocated", C.c_int32),
         ("reservation_weight", C.c_int32),
         ("reserved", C.c_int32 * 5),
+        ("ext_weight", C.c_int32 * 3),
+        ("dev_most_allocated", C.c_int32),
+        ("dev_res_weight", C.c_int32 * 5),
+        ("reserved2", C.c_int32 * 3),
     ]
 
 
@@ -139,6 +153,15 @@ class KoordhipNodeSoa(C.Structure):
         ("resv_slots", C.c_int32),
         ("reserved1", C.c_int32),
         ("resv_cpus", _u64p * NUMA_WORDS),
+        ("dev_slots", C.c_int32),
+        ("reserved2", C.c_int32),
+        ("dev_present", _u8p),
+        ("dev_minor", _i32p),
+        ("dev_total", _i64p),
+        ("dev_used", _i64p),
+        ("xalloc", _i64p),
+        ("xrequested", _i64p),
+        ("static_score", C.POINTER(C.c_uint16) * 2),
     ]
 
 
@@ -172,6 +195,21 @@ POD_DTYPE = np.dtype([
 ], align=True)
 assert POD_DTYPE.itemsize == 96
 TOPK_DTYPE = np.dtype([("node", "<i4"), ("score", "<i4")])
+# numpy twin of koordhip_pod_ext (144 bytes)
+POD_EXT_DTYPE = np.dtype([
+    ("dev_req", "<i8", (DEV_TYPES, DEV_RES)),
+    ("xreq", "<i8", (NXRES,)),
+    ("flags", "<u4"),
+    ("xmask", "<u4"),
+], align=True)
+assert POD_EXT_DTYPE.itemsize == 144
+
+
+def pod_ext_array(n: int) -> np.ndarray:
+    """n koordhip_pod_ext records with no device request (dev_req -1 / 0)."""
+    a = np.zeros(n, POD_EXT_DTYPE)
+    a["dev_req"][:, DEV_GPU, :] = -1
+    return a
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libkoordhip.so")
@@ -210,6 +248,10 @@ def load_library(path: str = LIB_PATH):
         "koordhip_read_nodes": (C.c_int, [vp, _i64p, _i64p, _i32p, _i64p, _i64p]),
         "koordhip_eval": (C.c_int, [vp, vp, C.c_int32, _u8p, _i32p, vp, C.c_int32]),
         "koordhip_place_stream": (C.c_int, [vp, vp, C.c_int32, _i32p]),
+        "koordhip_place_stream_ext": (C.c_int, [vp, vp, vp, C.c_int32, _i32p]),
+        "koordhip_eval_ext": (C.c_int, [vp, vp, vp, C.c_int32, _u8p, _i32p, vp, C.c_int32]),
+        "koordhip_fetch_devices": (C.c_int, [vp, C.POINTER(C.c_uint32), C.c_int32]),
+        "koordhip_read_devices": (C.c_int, [vp, _i64p, _i64p]),
         "koordhip_stage_pods": (C.c_int, [vp, vp, C.c_int32]),
         "koordhip_place_staged": (C.c_int, [vp]),
         "koordhip_fetch_placements": (C.c_int, [vp, _i32p, C.c_int32]),
@@ -245,7 +287,8 @@ def load_library(path: str = LIB_PATH):
 EXPORTED_SYMBOLS = [
     "koordhip_last_error", "koordhip_abi_version", "koordhip_create", "koordhip_destroy",
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
-    "koordhip_place_stream", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
+    "koordhip_place_stream", "koordhip_place_stream_ext", "koordhip_eval_ext", "koordhip_fetch_devices",
+    "koordhip_read_devices", "koordhip_stage_pods", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
     "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
     "koordhip_read_resv_cpus", "koordhip_last_stats", "koordhip_last_kernel_stats",

@@ -175,6 +175,14 @@ struct koordhip_ctx {
   int32_t ev_used = 0;
   double last_eval_ms = 0, last_total_ms = 0;
   std::string eval_kernel, resolve_kernel;  // template instantiations of the last place call's launches
+  // the exact sequential cycle (normalized-score plugins: seq.hip)
+  bool seq = false;                // the profile enables DeviceShare or a normalized upstream Score
+  kh::DevPodX *d_podx = nullptr;   // staged koordhip_pod_ext records (NULL: none staged)
+  int32_t podx_cap = 0;
+  bool podx_staged = false;
+  uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
+  uint64_t *d_seqg = nullptr;      // granules + timeout word of k_seq
+  int32_t seq_grid = 0;
   int64_t last_launches = 0, last_evals = 0;
 };
 
@@ -710,6 +718,76 @@ int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   return e;
 }
 
+// ABI 9 columns of the sequential cycle: DeviceShare devices, extended
+// scalars, static Scores (int64 on device: the device code is integer).
+int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
+  kh::DevDev &dv = c->d.dv;
+  dv = kh::DevDev{};
+  const bool dev = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+  if (!c->seq) {
+    if (s->dev_slots > 0 || s->xalloc || s->static_score[0] || s->static_score[1])
+      return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score columns need DeviceShare or a normalized "
+                                   "Score plugin in the profile (the sequential cycle)");
+    return 0;
+  }
+  int e = 0;
+  if (dev && s->dev_slots > 0) {
+    if (s->dev_slots > KOORDHIP_DEV_SLOTS || !s->dev_present || !s->dev_minor || !s->dev_total)
+      return fail(KOORDHIP_EINVAL, "dev_slots > KOORDHIP_DEV_SLOTS or a device column missing");
+    const size_t ns = (size_t)n * KOORDHIP_DEV_TYPES * s->dev_slots;
+    // a node holds one GPU model: every GPU with resources has the same memory
+    // (fillGPUTotalMem reads the first one, utils.go:211-233)
+    for (int32_t i = 0; i < n; i++) {
+      int64_t mem = -1;
+      for (int32_t q = 0; q < s->dev_slots; q++) {
+        const size_t a = ((size_t)i * KOORDHIP_DEV_TYPES + KOORDHIP_DEV_GPU) * s->dev_slots + q;
+        if (s->dev_minor[a] < 0) continue;
+        const int64_t *t = s->dev_total + a * KOORDHIP_DEV_RES;
+        if (t[0] == 0 && t[1] == 0 && t[2] == 0) continue;
+        if (t[2] <= 0) return fail(KOORDHIP_EINVAL, "a GPU with resources but no gpu-memory");
+        if (mem >= 0 && t[2] != mem) return fail(KOORDHIP_EINVAL, "GPUs of different memory sizes on one node");
+        mem = t[2];
+      }
+    }
+    uint8_t *pr = nullptr;
+    int32_t *mi = nullptr;
+    int64_t *tt = nullptr, *us = nullptr;
+    e = dev_alloc(c, &pr, n);
+    if (!e) e = upload(c, pr, s->dev_present, n);
+    if (!e) e = dev_alloc(c, &mi, ns);
+    if (!e) e = upload(c, mi, s->dev_minor, ns);
+    if (!e) e = dev_alloc(c, &tt, ns * KOORDHIP_DEV_RES);
+    if (!e) e = upload(c, tt, s->dev_total, ns * KOORDHIP_DEV_RES);
+    if (!e) e = dev_alloc(c, &us, ns * KOORDHIP_DEV_RES);
+    if (!e) e = upload(c, us, s->dev_used, ns * KOORDHIP_DEV_RES);  // NULL: zeros
+    dv.slots = s->dev_slots;
+    dv.present = pr;
+    dv.minor = mi;
+    dv.total = tt;
+    dv.used = us;
+  }
+  int64_t *xa = nullptr, *xr = nullptr;
+  if (!e && s->xalloc) {
+    e = dev_alloc(c, &xa, (size_t)n * KOORDHIP_NXRES);
+    if (!e) e = upload(c, xa, s->xalloc, (size_t)n * KOORDHIP_NXRES);
+  }
+  if (!e) e = dev_alloc(c, &xr, (size_t)n * KOORDHIP_NXRES);
+  if (!e) e = upload(c, xr, s->xrequested, (size_t)n * KOORDHIP_NXRES);
+  dv.xalloc = xa;
+  dv.xreq = xr;
+  for (int w = 0; w < 2 && !e; w++) {
+    const uint32_t bit = w == 0 ? KOORDHIP_PLUGIN_AFFINITY_SCORE : KOORDHIP_PLUGIN_TAINT_SCORE;
+    if (!(c->cfg.score_plugins & bit) || !s->static_score[w]) continue;
+    uint16_t *ss = nullptr;
+    e = dev_alloc(c, &ss, (size_t)n * KOORDHIP_MAX_STATIC_CLASSES);
+    if (!e) e = upload(c, ss, s->static_score[w], (size_t)n * KOORDHIP_MAX_STATIC_CLASSES);
+    dv.sscore[w] = ss;
+  }
+  return e;
+}
+
+int pipe_status(koordhip_ctx *c);
+
 void shard(const koordhip_ctx *c, int32_t *lo, int32_t *hi) {
   *lo = (int32_t)((int64_t)c->n * c->rank / c->world);
   *hi = (int32_t)((int64_t)c->n * (c->rank + 1) / c->world);
@@ -731,8 +809,20 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (!cfg || !out) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (cfg->abi_version != KOORDHIP_ABI_VERSION) return fail(KOORDHIP_EINVAL, "abi_version mismatch");
   const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA |
-                         KOORDHIP_PLUGIN_RESERVATION | KOORDHIP_PLUGIN_NODE_STATIC | KOORDHIP_PLUGIN_BALANCED;
+                         KOORDHIP_PLUGIN_RESERVATION | KOORDHIP_PLUGIN_NODE_STATIC | KOORDHIP_PLUGIN_BALANCED |
+                         KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE;
   if ((cfg->filter_plugins | cfg->score_plugins) & ~known) return fail(KOORDHIP_EINVAL, "unknown plugin bit");
+  if (cfg->filter_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE))
+    return fail(KOORDHIP_EINVAL, "the NodeAffinity / TaintToleration Score bits are Score plugins");
+  for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) {
+    static const uint32_t xb[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
+                                                       KOORDHIP_PLUGIN_TAINT_SCORE};
+    if ((cfg->score_plugins & xb[e]) && (cfg->ext_weight[e] < 1 || cfg->ext_weight[e] > 100))
+      return fail(KOORDHIP_EINVAL, "DeviceShare / NodeAffinity / TaintToleration score weight must be in [1, 100]");
+  }
+  for (int k = 0; k < 5; k++)
+    if (cfg->dev_res_weight[k] < 0 || cfg->dev_res_weight[k] > 100)
+      return fail(KOORDHIP_EINVAL, "DeviceShare scoring resource weights must be in [0, 100]");
   if (cfg->score_plugins & KOORDHIP_PLUGIN_NODE_STATIC) return fail(KOORDHIP_EINVAL, "the static node filters have no Score");
   if (cfg->filter_plugins & KOORDHIP_PLUGIN_BALANCED) return fail(KOORDHIP_EINVAL, "BalancedAllocation has no Filter");
   if (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) {
@@ -786,6 +876,12 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.numa_w_cpu = cfg->numa_weight_cpu;
   c->dc.numa_w_mem = cfg->numa_weight_mem;
   c->dc.numa_most = cfg->numa_most_allocated ? 1 : 0;
+  for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) c->dc.w_ext[e] = cfg->ext_weight[e];
+  c->dc.dev_most = cfg->dev_most_allocated ? 1 : 0;
+  for (int k = 0; k < 5; k++) c->dc.dev_w[k] = cfg->dev_res_weight[k];
+  // normalized scores couple a pod's nodes: the exact sequential cycle
+  c->seq = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) ||
+           (cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
   c->side = c->numa || c->resv;
@@ -819,6 +915,9 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     int64_t max_total = 0;  // every plugin score is in [0, 100]
     for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
       if (cfg->score_plugins & kScorePluginBit[p]) max_total += 100 * cfg->plugin_weight[p];
+    if (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) max_total += 100 * (int64_t)cfg->ext_weight[0];
+    if (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) max_total += 100 * (int64_t)cfg->ext_weight[1];
+    if (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) max_total += 100 * (int64_t)cfg->ext_weight[2];
     c->dc.resv_b1 = (int32_t)max_total + 1;
     if (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION) {
       // the ranking totals of resv.hpp: one normalised Reservation unit must
@@ -910,7 +1009,8 @@ int koordhip_destroy(koordhip_ctx *c) {
                   (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc,
                   (void *)c->d_selpart[0], (void *)c->d_selcnt[0], (void *)c->d_selpart[1], (void *)c->d_selcnt[1],
                   (void *)c->d_etk_part[0], (void *)c->d_etk_part[1], (void *)c->d_etk_pcnt[0],
-                  (void *)c->d_etk_pcnt[1], (void *)c->d_etk_sync[0], (void *)c->d_etk_sync[1], c->d_upd})
+                  (void *)c->d_etk_pcnt[1], (void *)c->d_etk_sync[0], (void *)c->d_etk_sync[1], c->d_upd,
+                  (void *)c->d_podx, (void *)c->d_devout, (void *)c->d_seqg})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -1015,6 +1115,7 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   }
   if (!e) e = load_numa_columns(c, s, n);
   if (!e) e = load_resv_columns(c, s, n);
+  if (!e) e = load_ext_columns(c, s, n);
   if (!e && c->dc.resv && c->dc.zones)
     e = fail(KOORDHIP_EINVAL, "the Reservation plugin with NUMA topology-policy nodes is not supported");
   if (e) {
@@ -1182,6 +1283,48 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
           cols.push_back({rv.rc[w] + q * dn, rc_rows[w] + q * sm, 8, false, "resv_cpus"});
     }
   }
+  // ABI 9: DeviceShare device rows, extended scalars, static Scores (the
+  // sequential cycle's columns; element = a node's whole device row)
+  if (c->seq) {
+    kh::DevDev &dv = c->d.dv;
+    if (rows->dev_slots > 0) {
+      if (!dv.used || rows->dev_slots != dv.slots || !rows->dev_present || !rows->dev_minor || !rows->dev_total)
+        return fail(KOORDHIP_EINVAL, "update rows: device columns must match the loaded snapshot's dev_slots");
+      const int32_t S = dv.slots;
+      for (int32_t j = 0; j < m; j++) {
+        int64_t mem = -1;
+        for (int32_t q = 0; q < S; q++) {
+          const size_t a = ((size_t)j * KOORDHIP_DEV_TYPES + KOORDHIP_DEV_GPU) * S + q;
+          const int64_t *t = rows->dev_total + a * KOORDHIP_DEV_RES;
+          if (rows->dev_minor[a] < 0 || (t[0] == 0 && t[1] == 0 && t[2] == 0)) continue;
+          if (t[2] <= 0 || (mem >= 0 && t[2] != mem)) return fail(KOORDHIP_EINVAL, "update rows: GPU memory sizes differ");
+          mem = t[2];
+        }
+      }
+      const int32_t rb = KOORDHIP_DEV_TYPES * S;
+      cols.push_back({const_cast<uint8_t *>(dv.present), rows->dev_present, 1, false, "dev_present"});
+      cols.push_back({const_cast<int32_t *>(dv.minor), rows->dev_minor, rb * 4, false, "dev_minor"});
+      cols.push_back({const_cast<int64_t *>(dv.total), rows->dev_total, rb * KOORDHIP_DEV_RES * 8, false, "dev_total"});
+      if (rows->dev_used) cols.push_back({dv.used, rows->dev_used, rb * KOORDHIP_DEV_RES * 8, false, "dev_used"});
+    }
+    if (rows->xalloc && !dv.xalloc) return fail(KOORDHIP_EINVAL, "extended scalars need the xalloc column at load_snapshot");
+    for (int j = 0; j < KOORDHIP_NXRES; j++) {
+      if (rows->xalloc)
+        cols.push_back({const_cast<int64_t *>(dv.xalloc) + (size_t)j * c->n, rows->xalloc + (size_t)j * m, 8, false, "xalloc"});
+      if (rows->xrequested)
+        cols.push_back({dv.xreq + (size_t)j * c->n, rows->xrequested + (size_t)j * m, 8, false, "xrequested"});
+    }
+    for (int w = 0; w < 2; w++) {
+      if (!rows->static_score[w]) continue;
+      if (!dv.sscore[w]) return fail(KOORDHIP_EINVAL, "static scores need their column at load_snapshot");
+      for (int q = 0; q < KOORDHIP_MAX_STATIC_CLASSES; q++)
+        cols.push_back({const_cast<uint16_t *>(dv.sscore[w]) + (size_t)q * c->n, rows->static_score[w] + (size_t)q * m, 2,
+                        false, "static_score"});
+    }
+  } else if (rows->dev_slots > 0 || rows->xalloc || rows->static_score[0] || rows->static_score[1]) {
+    return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score rows need DeviceShare or a normalized Score "
+                                 "plugin in the profile");
+  }
   if (zrows) {  // [m][2][ZMAX] f64 rows, scattered as one ZoneRow element per row
     kh::DevNuma &nu = c->d.nu;
     cols.push_back({const_cast<double *>(nu.za), zrow_a.data(), (int32_t)sizeof(kh::ZoneRow), false, "numa_zone_alloc"});
@@ -1225,9 +1368,11 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   for (size_t q = 0; q < cols.size(); q++) {
     const Col &k = cols[q];
     const void *src = dev + off[q];
-    if (k.esize == (int32_t)sizeof(kh::ZoneRow))
-      HIP_TRY(kh::launch_scatter<kh::ZoneRow>(static_cast<kh::ZoneRow *>(k.dst), static_cast<const kh::ZoneRow *>(src),
-                                              d_idx, m, c->stream));
+    if (k.esize > 8)  // whole rows (NUMA zone rows, device rows)
+      HIP_TRY(kh::launch_scatter_rows(k.dst, src, d_idx, m, k.esize, c->stream));
+    else if (k.esize == 2)
+      HIP_TRY(kh::launch_scatter<uint16_t>(static_cast<uint16_t *>(k.dst), static_cast<const uint16_t *>(src), d_idx, m,
+                                           c->stream));
     else if (k.esize == 8)
       HIP_TRY(kh::launch_scatter<int64_t>(static_cast<int64_t *>(k.dst), static_cast<const int64_t *>(src), d_idx, m, c->stream));
     else if (k.esize == 4)
@@ -1344,6 +1489,17 @@ int koordhip_read_resv_cpus(koordhip_ctx *c, uint64_t *cpus) {
 int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uint8_t *status, int32_t *scores,
                   koordhip_topk *topk, int32_t k) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (c->seq && n_pods > 0) {  // a normalized-score profile: the sequential cycle's evaluator, first planes
+    if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+    const size_t n = (size_t)c->n, NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
+    std::vector<int32_t> sc(scores ? (size_t)n_pods * NPX * n : 0);
+    if (int e = koordhip_eval_ext(c, pods, nullptr, n_pods, status, scores ? sc.data() : nullptr, topk, k)) return e;
+    if (scores)
+      for (int32_t p = 0; p < n_pods; p++)
+        std::memcpy(scores + (size_t)p * KOORDHIP_NPLUGINS * n, sc.data() + (size_t)p * NPX * n,
+                    (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t));
+    return 0;
+  }
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
   if (topk && (k < 1 || k > kMaxBatch)) return fail(KOORDHIP_EINVAL, "k must be in [1, 64]");
@@ -1421,9 +1577,11 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
     if (c->d_pods) HIP_TRY(hipFree(c->d_pods));
     if (c->d_out) HIP_TRY(hipFree(c->d_out));
     if (c->d_cpus) HIP_TRY(hipFree(c->d_cpus));
+    if (c->d_devout) HIP_TRY(hipFree(c->d_devout));
     c->d_pods = nullptr;
     c->d_out = nullptr;
     c->d_cpus = nullptr;
+    c->d_devout = nullptr;
     // +16 records of padding: the resolve kernel DMA-copies pod records in 1 KiB pieces
     HIP_TRY(hipMalloc(&c->d_pods, (size_t)(n_pods + 16) * sizeof(kh::DevPod)));
     HIP_TRY(hipMalloc(&c->d_out, (size_t)n_pods * sizeof(int32_t)));
@@ -1433,7 +1591,187 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
   if (n_pods) HIP_TRY(hipMemcpyAsync(c->d_pods, hp.data(), (size_t)n_pods * sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->n_staged = n_pods;
+  c->podx_staged = false;
   return 0;
+}
+
+// DeviceShare PreFilter products (PreparePod, deviceshare/plugin.go:162-182) validated
+static int check_pod_ext(const koordhip_pod_ext *x, int32_t n, bool *any) {
+  *any = false;
+  for (int32_t j = 0; j < n; j++) {
+    const koordhip_pod_ext &e = x[j];
+    if (e.flags & ~(uint32_t)KOORDHIP_PODX_DEVICE) return fail(KOORDHIP_EINVAL, "unknown koordhip_pod_ext flag");
+    if (e.xmask >> KOORDHIP_NXRES) return fail(KOORDHIP_EINVAL, "koordhip_pod_ext.xmask beyond KOORDHIP_NXRES");
+    for (int t = 0; t < KOORDHIP_DEV_TYPES; t++)
+      for (int r = 0; r < KOORDHIP_DEV_RES; r++)
+        if (e.dev_req[t][r] < -1 || e.dev_req[t][r] >= (1ll << 45))
+          return fail(KOORDHIP_EINVAL, "koordhip_pod_ext device request out of range");
+    if ((e.flags & KOORDHIP_PODX_DEVICE) && e.dev_req[KOORDHIP_DEV_GPU][1] < 0 && e.dev_req[KOORDHIP_DEV_GPU][2] < 0 &&
+        e.dev_req[KOORDHIP_DEV_GPU][0] > 0)
+      return fail(KOORDHIP_EINVAL, "a GPU request needs gpu-memory-ratio or gpu-memory (ValidDeviceResourceCombinations)");
+    *any = *any || e.flags != 0 || e.xmask != 0;
+  }
+  return 0;
+}
+
+static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pods) {
+  c->podx_staged = false;
+  if (!ext || n_pods <= 0) return 0;
+  bool any = false;
+  if (int e = check_pod_ext(ext, n_pods, &any)) return e;
+  if (!any) return 0;
+  if (!c->seq) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
+  if (n_pods > c->podx_cap) {
+    if (c->d_podx) HIP_TRY(hipFree(c->d_podx));
+    c->d_podx = nullptr;
+    HIP_TRY(hipMalloc(&c->d_podx, (size_t)n_pods * sizeof(kh::DevPodX)));
+    c->podx_cap = n_pods;
+  }
+  HIP_TRY(hipMemcpyAsync(c->d_podx, ext, (size_t)n_pods * sizeof(kh::DevPodX), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->podx_staged = true;
+  return 0;
+}
+
+int koordhip_place_stream_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods,
+                              int32_t *out_node) {
+  if (int e = koordhip_stage_pods(c, pods, n_pods)) return e;
+  if (int e = stage_ext(c, ext, n_pods)) return e;
+  if (int e = koordhip_place_staged(c)) return e;
+  return koordhip_fetch_placements(c, out_node, n_pods);
+}
+
+int koordhip_fetch_devices(koordhip_ctx *c, uint32_t *slots, int32_t n_pods) {
+  if (!c || (!slots && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (n_pods > c->n_staged) return fail(KOORDHIP_EINVAL, "n_pods exceeds the staged stream");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int e = pipe_status(c)) return e;
+  const size_t b = (size_t)n_pods * KOORDHIP_DEV_TYPES * sizeof(uint32_t);
+  if (!c->d_devout) {
+    if (b) std::memset(slots, 0, b);
+    return 0;
+  }
+  if (b) HIP_TRY(hipMemcpy(slots, c->d_devout, b, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int koordhip_read_devices(koordhip_ctx *c, int64_t *dev_used, int64_t *xrequested) {
+  if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t nd = (size_t)c->n * KOORDHIP_DEV_TYPES * c->d.dv.slots * KOORDHIP_DEV_RES;
+  if (dev_used && nd) {
+    if (c->d.dv.used) {
+      HIP_TRY(hipMemcpy(dev_used, c->d.dv.used, nd * sizeof(int64_t), hipMemcpyDeviceToHost));
+    } else {
+      std::memset(dev_used, 0, nd * sizeof(int64_t));
+    }
+  }
+  const size_t nx = (size_t)c->n * KOORDHIP_NXRES;
+  if (xrequested) {
+    if (c->d.dv.xreq) {
+      HIP_TRY(hipMemcpy(xrequested, c->d.dv.xreq, nx * sizeof(int64_t), hipMemcpyDeviceToHost));
+    } else {
+      std::memset(xrequested, 0, nx * sizeof(int64_t));
+    }
+  }
+  return 0;
+}
+
+int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods,
+                      uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
+  if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
+  if (topk && (k < 1 || k > kMaxBatch)) return fail(KOORDHIP_EINVAL, "k must be in [1, 64]");
+  if (n_pods == 0) return 0;
+  bool any = false;
+  if (ext)
+    if (int e = check_pod_ext(ext, n_pods, &any)) return e;
+  if (!c->seq) {
+    if (any) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
+    // the per-node plugins only: koordhip_eval, its planes widened
+    const int32_t n = c->n;
+    const int NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
+    std::vector<int32_t> sc(scores ? (size_t)n_pods * KOORDHIP_NPLUGINS * n : 0);
+    if (int e = koordhip_eval(c, pods, n_pods, status, scores ? sc.data() : nullptr, topk, k)) return e;
+    if (scores)
+      for (int32_t p = 0; p < n_pods; p++) {
+        std::memcpy(scores + (size_t)p * NPX * n, sc.data() + (size_t)p * KOORDHIP_NPLUGINS * n,
+                    (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t));
+        std::memset(scores + ((size_t)p * NPX + KOORDHIP_NPLUGINS) * n, 0, (size_t)KOORDHIP_NEXT_PLUGINS * n * sizeof(int32_t));
+      }
+    return 0;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  const int32_t n = c->n;
+  const int NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
+  const int32_t per = std::max<int32_t>(1, std::min<int32_t>(kMaxBatch, (int32_t)((256ll << 20) / (48ll * std::max(n, 1)))));
+  kh::DevPod *dp = nullptr;
+  kh::DevPodX *dx = nullptr;
+  uint8_t *dst = nullptr;
+  int32_t *dsc4 = nullptr, *dsc = nullptr, *work = nullptr;
+  uint64_t *dk = nullptr;
+  auto cleanup = [&]() {
+    for (void *p : {(void *)dp, (void *)dx, (void *)dst, (void *)dsc4, (void *)dsc, (void *)work, (void *)dk})
+      if (p) (void)hipFree(p);
+  };
+  std::vector<kh::DevPod> hp;
+  if (int ce = to_dev_pods(pods, n_pods, hp)) return ce;
+  if (hipMalloc(&dp, (size_t)per * sizeof(kh::DevPod)) != hipSuccess ||
+      (ext && hipMalloc(&dx, (size_t)per * sizeof(kh::DevPodX)) != hipSuccess) ||
+      hipMalloc(&dst, (size_t)per * std::max(n, 1)) != hipSuccess ||
+      hipMalloc(&dsc4, (size_t)per * KOORDHIP_NPLUGINS * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&dsc, (size_t)per * NPX * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&work, (size_t)per * 4 * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
+      (topk && hipMalloc(&dk, (size_t)per * k * sizeof(uint64_t)) != hipSuccess)) {
+    cleanup();
+    return fail(KOORDHIP_ENOMEM, "eval buffers");
+  }
+  const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
+  std::vector<uint64_t> hk(topk ? (size_t)per * k : 0);
+  int e = 0;
+  for (int32_t p0 = 0; p0 < n_pods && !e; p0 += per) {
+    const int32_t np = std::min(per, n_pods - p0);
+    if (hipMemcpyAsync(dp, hp.data() + p0, np * sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        (dx && hipMemcpyAsync(dx, ext + p0, np * sizeof(kh::DevPodX), hipMemcpyHostToDevice, c->stream) != hipSuccess)) {
+      e = fail(KOORDHIP_EDEVICE, "copy pods");
+      break;
+    }
+    if (kh::launch_eval_full(c->dc, c->d, dp, np, dst, dsc4, c->stream) != hipSuccess ||
+        hipMemcpy2DAsync(dsc, (size_t)NPX * n * sizeof(int32_t), dsc4, (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t),
+                         (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t), np, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
+        kh::launch_seq_eval(c->dc, c->d, dp, dx, np, rs, dst, dsc, work, topk ? k : 0, dk, c->stream) != hipSuccess) {
+      e = fail(KOORDHIP_EDEVICE, "eval_ext launch");
+      break;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) {
+      e = fail(KOORDHIP_EDEVICE, "eval sync");
+      break;
+    }
+    if (status && hipMemcpy(status + (size_t)p0 * n, dst, (size_t)np * n, hipMemcpyDeviceToHost) != hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "copy status");
+    if (!e && scores &&
+        hipMemcpy(scores + (size_t)p0 * NPX * n, dsc, (size_t)np * NPX * n * sizeof(int32_t), hipMemcpyDeviceToHost) !=
+            hipSuccess)
+      e = fail(KOORDHIP_EDEVICE, "copy scores");
+    if (!e && topk) {
+      if (hipMemcpy(hk.data(), dk, (size_t)np * k * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        e = fail(KOORDHIP_EDEVICE, "copy topk");
+        break;
+      }
+      for (size_t j = 0; j < (size_t)np * k; j++) {
+        koordhip_topk &o = topk[(size_t)p0 * k + j];
+        const uint64_t x = hk[j];
+        o.node = x ? (int32_t)(0xFFFFFFFFu - (uint32_t)x) : -1;
+        o.score = x ? (int32_t)(x >> 32) - 1 : 0;
+      }
+    }
+  }
+  cleanup();
+  return e;
 }
 
 }  // extern "C"
@@ -1514,11 +1852,48 @@ int koordhip_place_staged(koordhip_ctx *c) {
 
 namespace {
 
+// The exact sequential cycle (seq.hip): one persistent cooperative launch,
+// one block per CU, pod by pod.  The granules restart at epoch 1 every call.
+int seq_place(koordhip_ctx *c) {
+  const int32_t np = c->n_staged;
+  if (c->world > 1 || c->comm || c->group)
+    return fail(KOORDHIP_EINVAL, "the sequential cycle (DeviceShare / normalized Scores) runs on one GPU only");
+  const int32_t G = c->n_cu;
+  if ((int64_t)G * 256 * 8 < c->n) return fail(KOORDHIP_EINVAL, "too many nodes for the sequential cycle's grid");
+  const size_t gbytes = (size_t)2 * 2 * G * 4 * sizeof(uint64_t) + 64;
+  if (!c->d_seqg) {
+    HIP_TRY(hipMalloc(&c->d_seqg, gbytes));
+    c->seq_grid = G;
+  }
+  const bool dev = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+  if (dev && !c->d_devout && c->pods_cap > 0)
+    HIP_TRY(hipMalloc(&c->d_devout, (size_t)c->pods_cap * KOORDHIP_DEV_TYPES * sizeof(uint32_t)));
+  uint32_t *tmo = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(c->d_seqg) + gbytes - 64);
+  HIP_TRY(hipMemsetAsync(c->d_seqg, 0, gbytes, c->stream));
+  const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
+  HIP_TRY(hipEventRecord(c->t0, c->stream));
+  HIP_TRY(kh::launch_seq(c->dc, c->d, c->d_pods, c->podx_staged ? c->d_podx : nullptr, np, G, c->d_seqg, tmo,
+                         c->d_out, c->d_cpus, dev ? c->d_devout : nullptr, rs, c->stream));
+  HIP_TRY(hipEventRecord(c->t1, c->stream));
+  c->last_P = 1;
+  c->last_lag = 0;
+  c->last_evals = (int64_t)np * c->n;
+  c->last_launches = 1;
+  c->ev_used = 0;
+  c->eval_kernel = "kh::k_seq";
+  c->resolve_kernel = "kh::k_seq";
+  c->pipe_check = true;
+  return 0;
+}
+
 int place_staged_impl(koordhip_ctx *c) {
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   c->pipe_err = false;
   c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
+  if (c->seq) return seq_place(c);
+  if (c->podx_staged)
+    return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises
   // dispatches): every launch on one stream in dependency order, one resolve
   // per round; the lists are then fresher than in the pipeline, which the
@@ -1768,6 +2143,17 @@ int place_staged_impl(koordhip_ctx *c) {
 int pipe_status(koordhip_ctx *c) {
   static const char *kStall = "round pipeline stalled (watchdog): placements are incomplete";
   if (c->pipe_err) return fail(KOORDHIP_EDEVICE, kStall);
+  if (c->seq && c->pipe_check && c->d_seqg) {  // the sequential cycle's spin timeout word
+    c->pipe_check = false;
+    const size_t gbytes = (size_t)2 * 2 * c->seq_grid * 4 * sizeof(uint64_t) + 64;
+    uint32_t tmo = 0;
+    HIP_TRY(hipMemcpy(&tmo, reinterpret_cast<char *>(c->d_seqg) + gbytes - 64, sizeof(tmo), hipMemcpyDeviceToHost));
+    if (tmo) {
+      c->pipe_err = true;
+      return fail(KOORDHIP_EDEVICE, "sequential cycle stalled (watchdog): placements are incomplete");
+    }
+    return 0;
+  }
   if (!c->pipe_check || !c->d_mod) return 0;
   c->pipe_check = false;
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
@@ -1845,6 +2231,9 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
     v.push_back({nu.cnt, n * sizeof(int32_t)});
     if (nu.zu) v.push_back({nu.zu, n * 2 * KOORDHIP_NUMA_MAX_ZONES * sizeof(double)});
   }
+  if (c->d.dv.used)
+    v.push_back({c->d.dv.used, n * KOORDHIP_DEV_TYPES * (size_t)c->d.dv.slots * KOORDHIP_DEV_RES * sizeof(int64_t)});
+  if (c->d.dv.xreq) v.push_back({c->d.dv.xreq, n * KOORDHIP_NXRES * sizeof(int64_t)});
   if (c->dc.resv) {
     const size_t sl = (size_t)c->d.rv.slots;
     v.push_back({c->d.rv.rd[0], b * sl});

@@ -65,6 +65,23 @@ struct DevCfg {
   int32_t resv_cpus;               // some reservation holds CPUs (resv_cpus columns; the NM 4 build)
   int32_t resv_b1;                 // 1 + the other plugins' maximum weighted total (resv.hpp ranking total)
   int32_t wide_keys;               // ranking totals + 1 exceed 16 bits (the resolve's key tables hold u32)
+  // the normalized-score plugins (the sequential cycle, seq.hip)
+  int32_t w_ext[KOORDHIP_NEXT_PLUGINS];  // DeviceShare, NodeAffinity, TaintToleration score weights
+  int32_t dev_most;                      // DeviceShare MostAllocated scorer
+  int32_t dev_w[5];                      // DeviceShare scorer weights: gpu-core, ratio, memory, rdma, fpga
+};
+
+// DeviceShare devices, NodeResourcesFit extended scalars and the upstream
+// static Score columns (koordhip_node_soa ABI 9; read by the sequential cycle)
+struct DevDev {
+  int32_t slots;              // minors per type per node (0: no device columns)
+  const uint8_t *present;     // [n] nodeDevice entry exists
+  const int32_t *minor;       // [n][TYPES][slots], -1 = empty
+  const int64_t *total;       // [n][TYPES][slots][RES]
+  int64_t *used;              // [n][TYPES][slots][RES]
+  const int64_t *xalloc;      // [NXRES][n] (NULL: 0)
+  int64_t *xreq;              // [NXRES][n] Requested of the extended scalars
+  const uint16_t *sscore[2];  // [MAX_STATIC_CLASSES][n] NodeAffinity / TaintToleration raw scores (NULL: 0)
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -82,6 +99,7 @@ struct DevNodes {
   int32_t n;
   DevNuma nu;  // NodeNUMAResource columns (unused unless the plugin is enabled)
   DevResv rv;  // Reservation columns (NM == 3 builds)
+  DevDev dv;   // DeviceShare / extended scalars / static scores (the sequential cycle)
 };
 
 // One node's values as the evaluation consumes them (registers or an LDS row).

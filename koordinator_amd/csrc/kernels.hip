@@ -3065,6 +3065,26 @@ template hipError_t launch_scatter<int32_t>(int32_t *, const int32_t *, const in
 template hipError_t launch_scatter<uint8_t>(uint8_t *, const uint8_t *, const int32_t *, int32_t, hipStream_t);
 template hipError_t launch_scatter<ZoneRow>(ZoneRow *, const ZoneRow *, const int32_t *, int32_t, hipStream_t);
 template hipError_t launch_scatter<uint32_t>(uint32_t *, const uint32_t *, const int32_t *, int32_t, hipStream_t);
+template hipError_t launch_scatter<uint16_t>(uint16_t *, const uint16_t *, const int32_t *, int32_t, hipStream_t);
+
+// rows of `bytes` (a multiple of 4) per node: row j of src -> row idx[j] of dst
+__global__ void k_scatter_rows(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src,
+                               const int32_t *__restrict__ idx, int32_t m, int32_t words) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)m * words) return;
+  const int32_t j = (int32_t)(t / words), w = (int32_t)(t - (int64_t)j * words);
+  dst[(size_t)idx[j] * words + w] = src[t];
+}
+
+hipError_t launch_scatter_rows(void *dst, const void *src, const int32_t *idx, int32_t m, int32_t bytes, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  if (bytes % 4) return hipErrorInvalidValue;
+  const int32_t words = bytes / 4;
+  const int64_t tot = (int64_t)m * words;
+  hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, static_cast<uint32_t *>(dst),
+                     static_cast<const uint32_t *>(src), idx, m, words);
+  return hipGetLastError();
+}
 template hipError_t launch_scatter<double>(double *, const double *, const int32_t *, int32_t, hipStream_t);
 
 hipError_t launch_prep_flags(const PrepIn &in, const DevNodes &d, const int32_t *rows, int32_t m, hipStream_t s) {

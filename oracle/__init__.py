@@ -43,6 +43,9 @@ class OrcState(C.Structure):
         ("resv_assigned", C.POINTER(C.c_int32)),
         ("resv_cpus", C.POINTER(C.c_uint64) * abi.NUMA_WORDS),
         ("no_prescore", C.c_int32),
+        ("dev_used", C.POINTER(C.c_int64)),
+        ("xrequested", C.POINTER(C.c_int64)),
+        ("dev_out", C.c_void_p),
     ]
 
 

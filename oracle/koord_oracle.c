@@ -138,7 +138,13 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
     memcpy(st->resv_assigned, soa->resv_assigned, sizeof(int32_t) * (size_t)rn);
   if (soa->resv_flags && soa->resv_cpus[0])
     for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) st->resv_cpus[w] = (uint64_t *)dup64((const int64_t *)soa->resv_cpus[w], rn);
-  if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned) return -1;
+  /* DeviceShare deviceUsed and the extended scalars' Requested (dev_oracle.c) */
+  const int32_t dn = soa->dev_slots > 0 ? n * KOORDHIP_DEV_TYPES * soa->dev_slots * KOORDHIP_DEV_RES : 0;
+  st->dev_used = dup64(dn ? soa->dev_used : NULL, dn);
+  st->xrequested = dup64(soa->xrequested, n * KOORDHIP_NXRES);
+  if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned || !st->dev_used ||
+      !st->xrequested)
+    return -1;
   orc_la_flags(soa, n, st->flags);
   return 0;
 }
@@ -164,6 +170,8 @@ void orc_state_free(orc_state *st) {
   free(st->resv_allocated[1]);
   free(st->resv_assigned);
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) free(st->resv_cpus[w]);
+  free(st->dev_used);
+  free(st->xrequested);
   memset(st, 0, sizeof(*st));
 }
 
@@ -295,9 +303,12 @@ uint32_t orc_score_plugin_bit(int p) {
 /* Combined evaluation                                                       */
 /* ------------------------------------------------------------------------ */
 
-static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i) {
+static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod,
+                        const koordhip_pod_ext *x, int32_t i) {
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NODE_STATIC) && !orc_static_filter(st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_xfit_filter(st, x, i)) return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) &&
@@ -313,6 +324,17 @@ static int64_t orc_total(const koordhip_config *cfg, const orc_state *st, const 
   if (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) t += cfg->plugin_weight[2] * orc_numa_score(cfg, st, pod, i);
   if (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) t += cfg->plugin_weight[3] * orc_bal_score(cfg, st, pod, i);
   return t;
+}
+
+int64_t orc_bmax(const koordhip_config *cfg) {
+  static const uint32_t ext[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
+                                                      KOORDHIP_PLUGIN_TAINT_SCORE};
+  int64_t b = 0;
+  for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
+    if (cfg->score_plugins & orc_score_plugin_bit(p)) b += 100 * cfg->plugin_weight[p];
+  for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+    if (cfg->score_plugins & ext[e]) b += 100 * (int64_t)cfg->ext_weight[e];
+  return b;
 }
 
 /* key = (total+1) << 32 | (0xFFFFFFFF - node): larger is better, ties -> lower index. */
@@ -361,7 +383,7 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
         row[3 * (size_t)n + i] =
             (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) ? (int32_t)orc_bal_score(cfg, st, pod, i) : 0;
       }
-      if (keys && orc_feasible(cfg, st, pod, i)) {
+      if (keys && orc_feasible(cfg, st, pod, NULL, i)) {
         int64_t t = orc_total(cfg, st, pod, i);
         if (rv) t = orc_resv_rank_total(cfg, st, pod, i, t);
         keys[nk++] = mkkey(t, i);
@@ -382,6 +404,99 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
       }
     }
   }
+  free(keys);
+  return 0;
+}
+
+int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, const koordhip_pod_ext *ext,
+                 int32_t n_pods, uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
+  static const uint32_t xb[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
+                                                     KOORDHIP_PLUGIN_TAINT_SCORE};
+  const int32_t n = st->n;
+  const int NP = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
+  const size_t nn = (size_t)(n > 0 ? n : 1);
+  int32_t *feas = (int32_t *)malloc(sizeof(int32_t) * nn);
+  int64_t *base = (int64_t *)malloc(sizeof(int64_t) * nn);
+  int64_t *raw = (int64_t *)malloc(sizeof(int64_t) * KOORDHIP_NEXT_PLUGINS * nn);
+  uint64_t *keys = (uint64_t *)malloc(sizeof(uint64_t) * nn);
+  const int rv = orc_resv_on(cfg, st);
+  const int rs = rv && (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION);
+  for (int32_t p = 0; p < n_pods; p++) {
+    const koordhip_pod *pod = &pods[p];
+    const koordhip_pod_ext *x = ext ? &ext[p] : NULL;
+    if (rv) orc_resv_restore((orc_state *)st, pod, +1);
+    int32_t nf = 0;
+    for (int32_t i = 0; i < n; i++)
+      if (orc_feasible(cfg, st, pod, x, i)) feas[nf++] = i;
+    for (int32_t i = 0; i < n; i++) {
+      if (status) {
+        uint8_t b = 0;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NODE_STATIC) && !orc_static_filter(st, pod, i))
+          b |= KOORDHIP_ST_STATIC_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) b |= KOORDHIP_ST_FIT_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_xfit_filter(st, x, i)) b |= KOORDHIP_ST_XFIT_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) b |= KOORDHIP_ST_LA_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) b |= KOORDHIP_ST_NUMA_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) &&
+            (st->soa->resv_flags ? !orc_resv_filter(st, pod, i) : (pod->flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
+          b |= KOORDHIP_ST_RESV_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) b |= KOORDHIP_ST_DEVICE_FAIL;
+        status[(size_t)p * n + i] = b;
+      }
+      if (scores) {
+        int32_t *row = scores + (size_t)p * NP * n;
+        const int nom = rs && orc_resv_nominated(st, pod, i);
+        row[0 * (size_t)n + i] = (cfg->score_plugins & KOORDHIP_PLUGIN_FIT) ? (int32_t)orc_fit_score(cfg, st, pod, i) : 0;
+        row[1 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_LOADAWARE) ? (int32_t)orc_la_score(cfg, st, pod, i) : 0;
+        row[2 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) ? (int32_t)orc_numa_score(cfg, st, pod, i) : 0;
+        row[3 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) ? (int32_t)orc_bal_score(cfg, st, pod, i) : 0;
+        row[4 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? (int32_t)orc_dev_score(cfg, st, x, i, nom) : 0;
+        row[5 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? (int32_t)orc_static_score(st, pod, i, 0) : 0;
+        row[6 * (size_t)n + i] =
+            (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) ? (int32_t)orc_static_score(st, pod, i, 1) : 0;
+      }
+    }
+    if (topk && k > 0) {
+      for (int32_t j = 0; j < nf; j++) {
+        const int32_t i = feas[j];
+        const int nom = rs && orc_resv_nominated(st, pod, i);
+        base[j] = orc_total(cfg, st, pod, i);
+        raw[j] = (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? orc_dev_score(cfg, st, x, i, nom) : 0;
+        raw[(size_t)nf + j] = (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? orc_static_score(st, pod, i, 0) : 0;
+        raw[2 * (size_t)nf + j] = (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) ? orc_static_score(st, pod, i, 1) : 0;
+      }
+      for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+        if (cfg->score_plugins & xb[e]) orc_default_normalize(raw + (size_t)e * nf, nf, e == 2);
+      for (int32_t j = 0; j < nf; j++) {
+        const int32_t i = feas[j];
+        int64_t t = base[j];
+        for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+          if (cfg->score_plugins & xb[e]) t += (int64_t)cfg->ext_weight[e] * raw[(size_t)e * nf + j];
+        if (rv) t = orc_resv_rank_total(cfg, st, pod, i, t);
+        keys[j] = mkkey(t, i);
+      }
+      qsort(keys, (size_t)nf, sizeof(uint64_t), cmp_key_desc);
+      for (int32_t j = 0; j < k; j++) {
+        koordhip_topk *o = &topk[(size_t)p * k + j];
+        if (j < nf) {
+          o->node = (int32_t)(0xFFFFFFFFu - (uint32_t)(keys[j] & 0xFFFFFFFFu));
+          o->score = (int32_t)((keys[j] >> 32) - 1);
+        } else {
+          o->node = -1;
+          o->score = 0;
+        }
+      }
+    }
+    if (rv) orc_resv_restore((orc_state *)st, pod, -1);
+  }
+  free(feas);
+  free(base);
+  free(raw);
   free(keys);
   return 0;
 }
@@ -430,6 +545,28 @@ int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *po
     st->la_used_prod_cpu_m[i] += sign * pod->est_cpu;
     st->la_used_prod_mem[i] += sign * pod->est_mem;
   }
+  return 0;
+}
+
+/* The Reserve of a pod with its koordhip_pod_ext: DeviceShare's allocation
+ * is decided first without changing anything (the reserve plugins run in
+ * profile order -- LoadAwareScheduling, NodeNUMAResource, DeviceShare --
+ * and a failure unreserves every one of them, so any failure commits
+ * nothing), then the plugins' Reserve, then NodeInfo.AddPod of the pod's
+ * extended scalars. */
+int orc_commit_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x,
+                   int32_t i, uint64_t *cpus, int nominated, uint32_t *devs) {
+  uint32_t slots[KOORDHIP_DEV_TYPES] = {0, 0, 0};
+  const int dev = (cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE;
+  if (dev && orc_dev_reserve(cfg, st, x, i, nominated, slots, 0)) return KOORDHIP_ERESERVE;
+  const int rc = orc_commit(cfg, st, pod, i, +1, cpus);
+  if (rc) return rc;
+  if (dev) (void)orc_dev_reserve(cfg, st, x, i, nominated, slots, 1);
+  if (devs)
+    for (int t = 0; t < KOORDHIP_DEV_TYPES; t++) devs[t] = slots[t];
+  if (x)
+    for (int j = 0; j < KOORDHIP_NXRES; j++)
+      if ((x->xmask >> j) & 1u) st->xrequested[(size_t)j * st->n + i] += x->xreq[j];
   return 0;
 }
 
@@ -553,8 +690,10 @@ typedef struct stream_ctx {
   const koordhip_config *cfg;
   const orc_state *st;
   const koordhip_pod *pod;
+  const koordhip_pod_ext *ext;
   _Atomic int32_t nfeasible;
   int32_t *feasible;      /* node ids (unordered, like upstream's atomic append) */
+  int resv_score;         /* the Reservation plugin scores (its PreScore nominates) */
   int64_t *plugin_scores; /* [KOORDHIP_NPLUGINS][nfeasible] */
 } stream_ctx;
 
@@ -562,7 +701,7 @@ typedef struct stream_ctx {
 static void filter_piece(void *a, int32_t lo, int32_t hi) {
   stream_ctx *c = (stream_ctx *)a;
   for (int32_t i = lo; i < hi; i++)
-    if (orc_feasible(c->cfg, c->st, c->pod, i)) c->feasible[atomic_fetch_add(&c->nfeasible, 1)] = i;
+    if (orc_feasible(c->cfg, c->st, c->pod, c->ext, i)) c->feasible[atomic_fetch_add(&c->nfeasible, 1)] = i;
 }
 
 /* (upstream) framework.RunScorePlugins: one Until over nodes, every score plugin per node. */
@@ -579,11 +718,33 @@ static void score_piece(void *a, int32_t lo, int32_t hi) {
         (c->cfg->score_plugins & KOORDHIP_PLUGIN_NUMA) ? orc_numa_score(c->cfg, c->st, c->pod, i) : 0;
     c->plugin_scores[3 * (size_t)nf + j] =
         (c->cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) ? orc_bal_score(c->cfg, c->st, c->pod, i) : 0;
+    /* the normalized plugins' raw scores (planes NPLUGINS..; the Reservation
+     * plugin's normalized plane follows them) */
+    if (c->cfg->score_plugins & (KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_AFFINITY_SCORE |
+                                 KOORDHIP_PLUGIN_TAINT_SCORE)) {
+      int64_t *x = c->plugin_scores + (size_t)KOORDHIP_NPLUGINS * nf;
+      const int nom = c->resv_score && orc_resv_nominated(c->st, c->pod, i);
+      x[j] = (c->cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? orc_dev_score(c->cfg, c->st, c->ext, i, nom) : 0;
+      x[(size_t)nf + j] =
+          (c->cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? orc_static_score(c->st, c->pod, i, 0) : 0;
+      x[2 * (size_t)nf + j] =
+          (c->cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) ? orc_static_score(c->st, c->pod, i, 1) : 0;
+    }
   }
 }
 
 int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods, int32_t n_pods,
                      int32_t *out_node, int32_t threads) {
+  return orc_place_stream_ext(cfg, st, pods, NULL, n_pods, out_node, threads);
+}
+
+void orc_set_dev_out(orc_state *st, uint32_t *devs) { st->dev_out = devs; }
+
+static const uint32_t k_ext_bits[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
+                                                           KOORDHIP_PLUGIN_TAINT_SCORE};
+
+int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods,
+                         const koordhip_pod_ext *ext, int32_t n_pods, int32_t *out_node, int32_t threads) {
   const int32_t n = st->n;
   pool pl;
   if (pool_init(&pl, threads)) return -1;
@@ -591,10 +752,17 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
   c.cfg = cfg;
   c.st = st;
   c.feasible = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
-  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * (KOORDHIP_NPLUGINS + 1) * (size_t)(n > 0 ? n : 1));
+  /* planes: NPLUGINS plugins, NEXT_PLUGINS normalized ones, the Reservation's normalized */
+  c.plugin_scores = (int64_t *)malloc(sizeof(int64_t) * (KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS + 1) *
+                                      (size_t)(n > 0 ? n : 1));
   const int rv = orc_resv_on(cfg, st);
+  const int rs = rv && (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION);
+  c.resv_score = rs;
   for (int32_t p = 0; p < n_pods; p++) {
     c.pod = &pods[p];
+    c.ext = ext ? &ext[p] : NULL;
+    uint32_t *devs = st->dev_out ? st->dev_out + (size_t)p * KOORDHIP_DEV_TYPES : NULL;
+    if (devs) memset(devs, 0, sizeof(uint32_t) * KOORDHIP_DEV_TYPES);
     /* Reservation BeforePreFilter: the cycle's NodeInfos are the restored ones */
     if (rv) orc_resv_restore(st, &pods[p], +1);
     atomic_store(&c.nfeasible, 0);
@@ -607,32 +775,42 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
       continue;
     }
     pool_until(&pl, nf, score_piece, &c);
-    /* Reservation PreScore + Score + NormalizeScore over the feasible list */
-    int64_t *norm = c.plugin_scores + KOORDHIP_NPLUGINS * (size_t)nf;
-    const int rs = rv && (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION);
+    /* NormalizeScore of the normalized plugins (DefaultNormalizeScore over the
+     * feasible list: DeviceShare scoring.go:78-80, upstream NodeAffinity, and
+     * TaintToleration reversed), Reservation PreScore + Score + NormalizeScore */
+    int64_t *xs = c.plugin_scores + (size_t)KOORDHIP_NPLUGINS * nf;
+    for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+      if (cfg->score_plugins & k_ext_bits[e]) orc_default_normalize(xs + (size_t)e * nf, nf, e == 2);
+    int64_t *norm = c.plugin_scores + (size_t)(KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS) * nf;
     if (rs) orc_resv_normalized(st, &pods[p], c.feasible, nf, norm);
     /* (upstream) prioritizeNodes: sum of score x weight; selectHost: max,
      * reservoir-random tie-break REPLACED by lowest node index (BASELINE.json). */
     int64_t best = -1;
-    int32_t best_node = -1;
+    int32_t best_node = -1, best_j = -1;
     for (int32_t j = 0; j < nf; j++) {
       int32_t i = c.feasible[j];
       int64_t t = cfg->plugin_weight[0] * c.plugin_scores[j] + cfg->plugin_weight[1] * c.plugin_scores[(size_t)nf + j] +
                   cfg->plugin_weight[2] * c.plugin_scores[2 * (size_t)nf + j] +
                   cfg->plugin_weight[3] * c.plugin_scores[3 * (size_t)nf + j];
+      for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+        if (cfg->score_plugins & k_ext_bits[e]) t += (int64_t)cfg->ext_weight[e] * xs[(size_t)e * nf + j];
       if (rs) t += (int64_t)cfg->reservation_weight * norm[j];
       if (t > best || (t == best && i < best_node)) {
         best = t;
         best_node = i;
+        best_j = j;
       }
     }
+    (void)best_j;
+    /* One feasible node: (upstream) schedulePod returns it without
+     * prioritizeNodes, so PreScore nominates no reservation */
+    const int nominated = rs && nf > 1 && orc_resv_nominated(st, &pods[p], best_node);
     if (rv) orc_resv_restore(st, &pods[p], -1);
     uint64_t *cs = st->cpuset_out ? st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS : NULL;
-    /* Reserve (+ AssumePod); a failed Reserve leaves no state and is not retried.
-     * One feasible node: (upstream) schedulePod returns it without
-     * prioritizeNodes, so PreScore nominates no reservation */
+    /* Reserve (+ AssumePod); a failed Reserve leaves no state and is not retried. */
     st->no_prescore = nf == 1;
-    out_node[p] = orc_commit(cfg, st, &pods[p], best_node, +1, cs) ? KOORDHIP_RESERVE_FAILED : best_node;
+    out_node[p] = orc_commit_ext(cfg, st, &pods[p], c.ext, best_node, cs, nominated, devs) ? KOORDHIP_RESERVE_FAILED
+                                                                                            : best_node;
     st->no_prescore = 0;
   }
   free(c.feasible);

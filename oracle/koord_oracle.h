@@ -63,6 +63,11 @@ typedef struct orc_state {
    * feasible node: upstream then skips PreScore / Score, so no reservation is
    * nominated before the NodeNUMAResource Reserve */
   int32_t no_prescore;
+  /* DeviceShare deviceUsed [n][TYPES][dev_slots][RES] and NodeResourcesFit's
+   * extended scalar Requested [NXRES][n] (dev_oracle.c) */
+  int64_t *dev_used;
+  int64_t *xrequested;
+  uint32_t *dev_out; /* optional [n_pods][TYPES] device slots of the last orc_place_stream_ext call */
 } orc_state;
 
 int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n);
@@ -151,6 +156,21 @@ void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int
 int64_t orc_resv_rank_total(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i,
                             int64_t b);
 
+/* DeviceShare, extended scalars, upstream normalized Scores (dev_oracle.c). */
+int orc_dev_node_present(const orc_state *st, int32_t i);
+int orc_dev_filter(const orc_state *st, const koordhip_pod_ext *x, int32_t i);
+int64_t orc_dev_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x, int32_t i,
+                      int nominated);
+/* apply = 0: the allocation only (nothing changes) */
+int orc_dev_reserve(const koordhip_config *cfg, orc_state *st, const koordhip_pod_ext *x, int32_t i, int nominated,
+                    uint32_t *slots, int apply);
+int orc_xfit_filter(const orc_state *st, const koordhip_pod_ext *x, int32_t i);
+int64_t orc_static_score(const orc_state *st, const koordhip_pod *pod, int32_t i, int which);
+void orc_default_normalize(int64_t *scores, int32_t nf, int reverse);
+/* 100 x the score weights of every enabled plugin but Reservation (the
+ * ranking total's B, DESIGN.md Reservation key) */
+int64_t orc_bmax(const koordhip_config *cfg);
+
 /* Same contract as koordhip_eval (status / scores / topk all optional). */
 int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, int32_t n_pods,
              uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
@@ -159,6 +179,15 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
  * committed) when the NUMA Allocate fails; cpus: the cpuset given / taken back. */
 int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, int32_t node, int sign,
                uint64_t *cpus);
+/* ... with the pod's koordhip_pod_ext (NULL: none): DeviceShare Reserve
+ * (`nominated`: a reservation PreScore nominated on the node; devs: the slots
+ * allocated [TYPES], optional) and the extended scalars.  Reserve only. */
+int orc_commit_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x,
+                   int32_t node, uint64_t *cpus, int nominated, uint32_t *devs);
+/* koordhip_eval_ext: scores [n_pods][NPLUGINS + NEXT_PLUGINS][n] (raw), topk
+ * by the ranking total with the normalized plugins' weighted scores added. */
+int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, const koordhip_pod_ext *ext,
+                 int32_t n_pods, uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
 
 /* Greedy stream with the reference loop structure: per pod a parallel Filter
  * over all nodes, a parallel Score per plugin over the feasible nodes
@@ -166,6 +195,12 @@ int orc_commit(const koordhip_config *cfg, orc_state *st, const koordhip_pod *po
  * serial lowest-index argmax, serial Reserve.  threads <= 1 runs serially. */
 int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods, int32_t n_pods,
                      int32_t *out_node, int32_t threads);
+/* ... with koordhip_pod_ext records (NULL: none): DeviceShare, the extended
+ * scalars and the normalized Scores (NodeAffinity, TaintToleration,
+ * DeviceShare: DefaultNormalizeScore over the feasible nodes). */
+int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods,
+                         const koordhip_pod_ext *ext, int32_t n_pods, int32_t *out_node, int32_t threads);
+void orc_set_dev_out(orc_state *st, uint32_t *devs);
 /* cpusets of the last orc_place_stream call are written here when non-NULL ([n_pods][WORDS]). */
 void orc_set_cpuset_out(orc_state *st, uint64_t *cpus);
 

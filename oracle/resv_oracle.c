@@ -332,9 +332,7 @@ void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int
  * (pod, node) with plugin total b: koordhip_eval's topk score. */
 int64_t orc_resv_rank_total(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i,
                             int64_t b) {
-  int64_t bmax = 0;
-  for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
-    if (cfg->score_plugins & orc_score_plugin_bit(p)) bmax += 100 * cfg->plugin_weight[p];
+  const int64_t bmax = orc_bmax(cfg);
   if (!(cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION)) return b;
   const int rk = node_order_rank(st, pod, i);
   if (rk >= 0) return 101 * (bmax + 1) + (KOORDHIP_RESV_MAX_ORDERS - 1 - rk);
