@@ -29,6 +29,10 @@ PLUGIN_NODE_AFFINITY = "NodeAffinity"
 PLUGIN_TAINT_TOLERATION = "TaintToleration"
 PLUGIN_BALANCED = "NodeResourcesBalancedAllocation"
 STATIC_FILTERS = (PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
+PLUGIN_DEVICESHARE = "DeviceShare"
+# Scores normalized over the pod's feasible nodes (DefaultNormalizeScore): the
+# sequential cycle; NodeAffinity / TaintToleration in `scores` are their Scores
+NORMALIZED_SCORES = (PLUGIN_DEVICESHARE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
 
 
 class ArgsError(ValueError):
@@ -144,6 +148,27 @@ class NodeNUMAResourceArgs:
 
 
 @dataclass
+class DeviceShareArgs:
+    """DeviceShareArgs (pkg/scheduler/apis/config/types.go), defaults
+    v1beta2/defaults.go:168-189: LeastAllocated over gpu-memory-ratio, rdma, fpga."""
+    scoring_type: str = "LeastAllocated"
+    resources: Dict[str, int] = field(default_factory=lambda: {
+        "koordinator.sh/gpu-memory-ratio": 1, "koordinator.sh/rdma": 1, "koordinator.sh/fpga": 1})
+
+    SCORER_RESOURCES = ("koordinator.sh/gpu-core", "koordinator.sh/gpu-memory-ratio", "koordinator.sh/gpu-memory",
+                        "koordinator.sh/rdma", "koordinator.sh/fpga")
+
+    def validate(self):
+        if self.scoring_type not in ("LeastAllocated", "MostAllocated"):
+            raise ArgsError(f"DeviceShare scoringStrategy.type {self.scoring_type!r}: LeastAllocated or MostAllocated")
+        for r, w in self.resources.items():
+            if r not in self.SCORER_RESOURCES:
+                raise ArgsError(f"DeviceShare scoringStrategy.resources: {r!r} is not a device resource")
+            if not 0 <= w <= 100:
+                raise ArgsError(f"DeviceShare scoringStrategy.resources: weight of {r} out of range, got {w}")
+
+
+@dataclass
 class Profile:
     """The scheduling profile restricted to the hot-path plugins."""
     filters: tuple = (PLUGIN_FIT, PLUGIN_LOADAWARE)
@@ -151,6 +176,7 @@ class Profile:
     fit: NodeResourcesFitArgs = field(default_factory=NodeResourcesFitArgs)
     loadaware: LoadAwareSchedulingArgs = field(default_factory=LoadAwareSchedulingArgs)
     numa: NodeNUMAResourceArgs = field(default_factory=NodeNUMAResourceArgs)
+    deviceshare: DeviceShareArgs = field(default_factory=DeviceShareArgs)
     batch_pods: int = 0
 
     def resolved(self) -> "Profile":
@@ -195,6 +221,28 @@ def with_upstream(profile: Profile, static_filters=STATIC_FILTERS, balanced_weig
     return p
 
 
+def with_deviceshare(profile: Profile, weight: int = 1) -> Profile:
+    """The profile plus DeviceShare at Filter and Score (scheduler-config.yaml:62-105: weight 1)."""
+    p = copy.deepcopy(profile)
+    if PLUGIN_DEVICESHARE not in p.filters:
+        p.filters = tuple(p.filters) + (PLUGIN_DEVICESHARE,)
+    p.scores = dict(p.scores)
+    p.scores[PLUGIN_DEVICESHARE] = weight
+    return p
+
+
+def with_normalized_scores(profile: Profile, affinity: int = 0, taint: int = 0) -> Profile:
+    """The upstream NodeAffinity (preferred terms) / TaintToleration
+    (PreferNoSchedule) Scores at the given weights (0 = off)."""
+    p = copy.deepcopy(profile)
+    p.scores = dict(p.scores)
+    if affinity:
+        p.scores[PLUGIN_NODE_AFFINITY] = affinity
+    if taint:
+        p.scores[PLUGIN_TAINT_TOLERATION] = taint
+    return p
+
+
 def to_c_config(profile: Profile, device: int = -1):
     """Lower a resolved profile to the koordhip_config ctypes struct."""
     from .abi import (KOORDHIP_ABI_VERSION, PLUGIN_BITS, KoordhipConfig)
@@ -206,18 +254,30 @@ def to_c_config(profile: Profile, device: int = -1):
         p.numa.validate()
     cfg = KoordhipConfig()
     cfg.abi_version = KOORDHIP_ABI_VERSION
+    from . import abi
+    score_bits = {PLUGIN_NODE_AFFINITY: abi.PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_TOLERATION: abi.PLUGIN_TAINT_SCORE,
+                  PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE}
     cfg.filter_plugins = 0
     for x in p.filters:  # (the three static filters share one bit)
-        cfg.filter_plugins |= PLUGIN_BITS[x]
+        cfg.filter_plugins |= abi.PLUGIN_DEVICESHARE if x == PLUGIN_DEVICESHARE else PLUGIN_BITS[x]
     cfg.score_plugins = 0
     for x in p.scores:
-        cfg.score_plugins |= PLUGIN_BITS[x]
+        cfg.score_plugins |= score_bits[x] if x in score_bits else PLUGIN_BITS[x]
     cfg.device = device
     for name in p.scores:
-        if name in STATIC_FILTERS:
-            # their upstream Scores (preferred node affinity, PreferNoSchedule
-            # taints) normalise over the feasible nodes: not supported
+        if name in STATIC_FILTERS and name not in NORMALIZED_SCORES:
             raise ArgsError(f"the Score of {name} is not supported (Filter only)")
+    for e, name in enumerate(NORMALIZED_SCORES):
+        if name in p.scores:
+            w = p.scores[name]
+            if not 1 <= w <= 100:
+                raise ArgsError(f"score weight of {name} out of range, got {w}")
+            cfg.ext_weight[e] = w
+    if PLUGIN_DEVICESHARE in p.filters or PLUGIN_DEVICESHARE in p.scores:
+        p.deviceshare.validate()
+    cfg.dev_most_allocated = 1 if p.deviceshare.scoring_type == "MostAllocated" else 0
+    for k, r in enumerate(DeviceShareArgs.SCORER_RESOURCES):
+        cfg.dev_res_weight[k] = p.deviceshare.resources.get(r, 0)
     order = [PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_BALANCED]
     for i, name in enumerate(order):
         w = p.scores.get(name, 0)
@@ -226,7 +286,7 @@ def to_c_config(profile: Profile, device: int = -1):
         cfg.plugin_weight[i] = w
     if PLUGIN_RESERVATION in p.scores:
         w = p.scores[PLUGIN_RESERVATION]
-        bmax = 100 * sum(p.scores.get(x, 0) for x in order)
+        bmax = 100 * sum(p.scores.get(x, 0) for x in order + list(NORMALIZED_SCORES))
         if not (1 <= w <= 1000000):
             raise ArgsError(f"score weight of {PLUGIN_RESERVATION} out of range, got {w}")
         if w <= bmax:

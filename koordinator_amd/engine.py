@@ -84,6 +84,44 @@ class PlacementEngine:
                                                            abi.ptr(out, C.c_int32)))
         return out
 
+    def place_stream_ext(self, pods: np.ndarray, ext: Optional[np.ndarray] = None) -> np.ndarray:
+        """The greedy stream with koordhip_pod_ext records (DeviceShare requests,
+        extended scalars); profiles with a normalized Score run the exact
+        sequential cycle."""
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        x = None if ext is None else np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
+        out = np.zeros(len(pods), np.int32)
+        abi.check(self.lib, self.lib.koordhip_place_stream_ext(self._ctx, pods.ctypes.data,
+                                                               x.ctypes.data if x is not None else None, len(pods),
+                                                               abi.ptr(out, C.c_int32)))
+        return out
+
+    def eval_ext(self, pods: np.ndarray, ext: Optional[np.ndarray] = None, status: bool = True, scores: bool = True,
+                 k: int = 0) -> dict:
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        x = None if ext is None else np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
+        p, n = len(pods), self.n
+        st = np.zeros((p, n), np.uint8) if status else None
+        sc = np.zeros((p, abi.NPLUGINS + abi.NEXT_PLUGINS, n), np.int32) if scores else None
+        tk = np.zeros((p, k), abi.TOPK_DTYPE) if k else None
+        abi.check(self.lib, self.lib.koordhip_eval_ext(
+            self._ctx, pods.ctypes.data, x.ctypes.data if x is not None else None, p, abi.ptr(st, C.c_uint8),
+            abi.ptr(sc, C.c_int32), tk.ctypes.data if tk is not None else None, k))
+        return {"status": st, "scores": sc, "topk": tk}
+
+    def fetch_devices(self, n: int) -> np.ndarray:
+        """[n][DEV_TYPES] device-slot masks the last place call allocated."""
+        out = np.zeros((n, abi.DEV_TYPES), np.uint32)
+        abi.check(self.lib, self.lib.koordhip_fetch_devices(self._ctx, abi.ptr(out, C.c_uint32), n))
+        return out
+
+    def read_devices(self) -> dict:
+        S = max(1, self._table.dev_slots if self._table is not None else 0)
+        used = np.zeros((self.n, abi.DEV_TYPES, S, abi.DEV_RES), np.int64)
+        xr = np.zeros((abi.NXRES, self.n), np.int64)
+        abi.check(self.lib, self.lib.koordhip_read_devices(self._ctx, abi.ptr(used, C.c_int64), abi.ptr(xr, C.c_int64)))
+        return {"dev_used": used, "xrequested": xr.T.copy()}
+
     def stage_pods(self, pods: np.ndarray):
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         self._staged = pods

@@ -69,6 +69,11 @@ def estimate_pod(pod: k8s.Pod, args: LoadAwareSchedulingArgs) -> Dict[str, int]:
 
 _NATIVE_FIT = {k8s.CPU: abi.RES_CPU, k8s.MEMORY: abi.RES_MEM, k8s.EPHEMERAL: abi.RES_EPH}
 _SCALAR_FIT = {k8s.BATCH_CPU: abi.RES_BCPU, k8s.BATCH_MEMORY: abi.RES_BMEM}
+# DeviceShare's resources: NodeResourcesFit checks them as extended scalars
+# (koordhip_pod_ext.xreq / the xalloc columns, deviceshare.XRES)
+_DEVICE_SCALARS = {"nvidia.com/gpu", "dcu.com/gpu", "koordinator.sh/gpu", "koordinator.sh/gpu-core",
+                   "koordinator.sh/gpu-memory", "koordinator.sh/gpu-memory-ratio", "koordinator.sh/rdma",
+                   "koordinator.sh/fpga"}
 
 
 def _is_scalar(name: str) -> bool:
@@ -88,6 +93,9 @@ def _resource_add(acc: List[int], present: Set[str], rlist: k8s.ResourceList):
         elif n == k8s.PODS:
             pass
         elif _is_scalar(n):
+            if n in _DEVICE_SCALARS:      # extended scalars: koordhip_pod_ext.xreq (deviceshare.fit_xreq)
+                present.add(n)
+                continue
             if n not in _SCALAR_FIT:
                 raise MarshalError(f"scalar resource {n!r} is not supported by the engine")
             acc[_SCALAR_FIT[n]] += q.value()
@@ -106,6 +114,9 @@ def _resource_setmax(acc: List[int], present: Set[str], rlist: k8s.ResourceList)
         elif n == k8s.PODS:
             pass
         elif _is_scalar(n):
+            if n in _DEVICE_SCALARS:
+                present.add(n)
+                continue
             if n not in _SCALAR_FIT:
                 raise MarshalError(f"scalar resource {n!r} is not supported by the engine")
             i = _SCALAR_FIT[n]

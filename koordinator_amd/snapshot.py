@@ -40,6 +40,11 @@ NUMA_MUTABLE = [c for c in U64_COLS] + ["numa_alloc_cnt", "numa_zone_used"]
 RESV_COLS = ["resv_flags", "resv_order_rank", "resv_alloc0", "resv_alloc1", "resv_nz0", "resv_nz1",
              "resv_allocated0", "resv_allocated1", "resv_assigned"] + RESV_CPU_COLS
 RESV_MUTABLE = ["resv_allocated0", "resv_allocated1", "resv_assigned"] + RESV_CPU_COLS
+# ABI 9 (the sequential cycle): DeviceShare devices, NodeResourcesFit extended
+# scalars, upstream static Scores.  Present only after NodeTable.enable_ext();
+# every one is row-major per node here (as_soa transposes to the ABI's layouts).
+EXT_COLS = ["dev_present", "dev_minor", "dev_total", "dev_used", "xalloc", "xrequested", "static_score"]
+EXT_MUTABLE = ["dev_used", "xrequested"]
 
 
 def slot_col(col: str, s: int) -> str:
@@ -76,6 +81,31 @@ class NodeTable:
     # reservation slots per node: slot 0 in the RESV_COLS columns, slot s >= 1
     # in the columns slot_col(c, s) (koordhip_node_soa.resv_slots)
     resv_slots: int = 1
+    # DeviceShare minors per type per node held by the dev_* columns (0: none)
+    dev_slots: int = 0
+
+    @property
+    def has_ext(self) -> bool:
+        return "xalloc" in self.cols
+
+    def enable_ext(self, dev_slots: int = 0):
+        """Add the ABI 9 columns (empty): dev_present [n] u8, dev_minor
+        [n][TYPES][dev_slots] i32 (-1 empty), dev_total / dev_used
+        [n][TYPES][dev_slots][RES] i64, xalloc / xrequested [n][NXRES] i64,
+        static_score [n][2][MAX_STATIC_CLASSES] u16."""
+        if not 0 <= dev_slots <= abi.DEV_SLOTS:
+            raise ValueError(f"dev_slots must be in [0, {abi.DEV_SLOTS}]")
+        n = self.n
+        S = max(dev_slots, 1)
+        self.dev_slots = dev_slots
+        self.cols["dev_present"] = np.zeros(n, np.uint8)
+        self.cols["dev_minor"] = np.full((n, abi.DEV_TYPES, S), -1, np.int32)
+        self.cols["dev_total"] = np.zeros((n, abi.DEV_TYPES, S, abi.DEV_RES), np.int64)
+        self.cols["dev_used"] = np.zeros((n, abi.DEV_TYPES, S, abi.DEV_RES), np.int64)
+        self.cols["xalloc"] = np.zeros((n, abi.NXRES), np.int64)
+        self.cols["xrequested"] = np.zeros((n, abi.NXRES), np.int64)
+        self.cols["static_score"] = np.zeros((n, 2, abi.MAX_STATIC_CLASSES), np.uint16)
+        return self
 
     def set_resv_slots(self, slots: int):
         """Hold up to `slots` reservations per node (new slots empty)."""
@@ -91,7 +121,8 @@ class NodeTable:
         self.resv_slots = slots
 
     def col_names(self) -> List[str]:
-        return ALL_COLS + [slot_col(c, s) for s in range(1, self.resv_slots) for c in RESV_COLS]
+        return (ALL_COLS + [slot_col(c, s) for s in range(1, self.resv_slots) for c in RESV_COLS]
+                + (EXT_COLS if self.has_ext else []))
 
     @classmethod
     def empty(cls, n: int) -> "NodeTable":
@@ -115,6 +146,7 @@ class NodeTable:
         t.names = [self.names[i] for i in idx] if self.names else []
         t.numa_classes = self.numa_classes
         t.resv_slots = self.resv_slots
+        t.dev_slots = self.dev_slots
         return t
 
     def copy(self) -> "NodeTable":
@@ -123,6 +155,7 @@ class NodeTable:
         t.names = list(self.names)
         t.numa_classes = self.numa_classes.copy()
         t.resv_slots = self.resv_slots
+        t.dev_slots = self.dev_slots
         return t
 
     def as_soa(self) -> abi.KoordhipNodeSoa:
@@ -184,6 +217,26 @@ class NodeTable:
                 s.resv_cpus[w] = rc[f"resv_cpus{w}"].ctypes.data_as(C.POINTER(C.c_uint64))
         s._keep = rc
         s.static_allow = self.cols["static_allow"].ctypes.data_as(C.POINTER(C.c_uint32))
+        if self.has_ext:
+            keep = {}
+            if self.dev_slots > 0:
+                for c in ("dev_present", "dev_minor", "dev_total", "dev_used"):
+                    keep[c] = np.ascontiguousarray(self.cols[c])
+                s.dev_slots = self.dev_slots
+                s.dev_present = keep["dev_present"].ctypes.data_as(C.POINTER(C.c_uint8))
+                s.dev_minor = keep["dev_minor"].ctypes.data_as(C.POINTER(C.c_int32))
+                s.dev_total = keep["dev_total"].ctypes.data_as(C.POINTER(C.c_int64))
+                s.dev_used = keep["dev_used"].ctypes.data_as(C.POINTER(C.c_int64))
+            keep["xalloc"] = np.ascontiguousarray(self.cols["xalloc"].T)        # [NXRES][n]
+            keep["xrequested"] = np.ascontiguousarray(self.cols["xrequested"].T)
+            s.xalloc = keep["xalloc"].ctypes.data_as(C.POINTER(C.c_int64))
+            s.xrequested = keep["xrequested"].ctypes.data_as(C.POINTER(C.c_int64))
+            ss = self.cols["static_score"]
+            for w in range(2):
+                if ss[:, w].any():
+                    keep[f"ss{w}"] = np.ascontiguousarray(ss[:, w].T)      # [MAX_STATIC_CLASSES][n]
+                    s.static_score[w] = keep[f"ss{w}"].ctypes.data_as(C.POINTER(C.c_uint16))
+            s._keep_ext = keep
         return s
 
     def nbytes(self) -> int:
@@ -200,6 +253,7 @@ def concat(tables: List[NodeTable]) -> NodeTable:
     for c in tables[0].col_names():
         t.cols[c] = np.concatenate([x.cols[c] for x in tables])
     t.names = [nm for x in tables for nm in x.names]
+    t.dev_slots = max(x.dev_slots for x in tables)
     # merge topology class tables, re-indexing each part's numa_class
     classes, off = [], 0
     pos = 0

@@ -565,6 +565,112 @@ def pod_objects(spec: StreamSpec, limit: int = None) -> List[k8s.Pod]:
     return out
 
 
+@dataclass
+class DevSpec:
+    """DeviceShare cluster: a share of the nodes hold GPUs (one model per
+    node: 4 or 8 GPUs of 16 / 32 / 80 GiB, gpu-core = gpu-memory-ratio = 100
+    each, a few unhealthy) and some RDMA NICs; already-running device pods
+    hold part of them (deviceUsed).  Node allocatable carries the device
+    scalars (koordlet reports them): nvidia.com/gpu = GPU count, gpu-core /
+    gpu-memory-ratio = 100 per GPU, gpu-memory, rdma = 100 per NIC."""
+    gpu_frac: float = 0.3
+    rdma_frac: float = 0.5        # of the GPU nodes
+    unhealthy_frac: float = 0.03  # of the GPUs
+    used_frac: float = 0.4        # of the GPUs, partly used by running pods
+    no_entry_frac: float = 0.2    # of the non-GPU nodes: no Device CR (no nodeDevice entry)
+
+
+def add_devices(t: NodeTable, spec: DevSpec, seed: int = SEED) -> NodeTable:
+    """The DeviceShare columns (dev_*) and the extended scalars' allocatable /
+    requested (xalloc / xrequested) of a synthetic cluster."""
+    from .deviceshare import XRES_INDEX, NVIDIA_GPU, GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, RDMA
+    n, sd = t.n, seed + 7
+    t.enable_ext(dev_slots=8)
+    gpu = uniform(sd, n, 1) < spec.gpu_frac
+    ngpu = np.where(uniform(sd, n, 2) < 0.5, 4, 8)
+    mem = choice(sd, n, 3, [16 * GI, 32 * GI, 80 * GI]).astype(np.int64)
+    rdma = gpu & (uniform(sd, n, 4) < spec.rdma_frac)
+    entry = gpu | (uniform(sd, n, 5) >= spec.no_entry_frac)
+    t["dev_present"][:] = entry.astype(np.uint8)
+    G = abi.DEV_GPU
+    for s in range(8):
+        on = gpu & (s < ngpu)
+        t["dev_minor"][on, G, s] = s
+        healthy = on & (uniform(sd, n, 10 + s) >= spec.unhealthy_frac)
+        t["dev_total"][healthy, G, s, 0] = 100
+        t["dev_total"][healthy, G, s, 1] = 100
+        t["dev_total"][healthy, G, s, 2] = mem[healthy]
+        # running pods hold a share of some GPUs: 25 / 50 / 100 % of core / ratio / memory
+        part = healthy & (uniform(sd, n, 30 + s) < spec.used_frac)
+        share = choice(sd, n, 40 + s, [25, 50, 100]).astype(np.int64)
+        t["dev_used"][part, G, s, 0] = share[part]
+        t["dev_used"][part, G, s, 1] = share[part]
+        t["dev_used"][part, G, s, 2] = mem[part] * share[part] // 100
+    for s in range(2):
+        on = rdma
+        t["dev_minor"][on, abi.DEV_RDMA, s] = s
+        t["dev_total"][on, abi.DEV_RDMA, s, 0] = 100
+    xa, xr = t["xalloc"], t["xrequested"]
+    used = t["dev_used"][:, G]
+    xa[gpu, XRES_INDEX[NVIDIA_GPU]] = ngpu[gpu]
+    xa[gpu, XRES_INDEX[GPU_CORE]] = 100 * ngpu[gpu]
+    xa[gpu, XRES_INDEX[GPU_MEMORY_RATIO]] = 100 * ngpu[gpu]
+    xa[gpu, XRES_INDEX[GPU_MEMORY]] = mem[gpu] * ngpu[gpu]
+    xa[rdma, XRES_INDEX[RDMA]] = 200
+    xr[:, XRES_INDEX[GPU_CORE]] = used[:, :, 0].sum(axis=1)
+    xr[:, XRES_INDEX[GPU_MEMORY_RATIO]] = used[:, :, 1].sum(axis=1)
+    xr[:, XRES_INDEX[GPU_MEMORY]] = used[:, :, 2].sum(axis=1)
+    return t
+
+
+@dataclass
+class DevStreamSpec:
+    """Device pods of a stream (their koordhip_pod_ext records): a share of the
+    pods request GPUs in the reference's request forms -- koordinator.sh/gpu
+    (a percentage of one GPU, or 200 = two GPUs), nvidia.com/gpu (whole
+    GPUs), gpu-core + gpu-memory-ratio, gpu-memory alone -- some with RDMA."""
+    frac: float = 0.2
+    rdma_frac: float = 0.2
+    seed: int = SEED
+
+
+def make_device_ext(n: int, spec: DevStreamSpec) -> np.ndarray:
+    from .deviceshare import XRES_INDEX, NVIDIA_GPU, KOORD_GPU, GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, RDMA
+    sd = spec.seed + 9
+    ext = abi.pod_ext_array(n)
+    dev = uniform(sd, n, 1) < spec.frac
+    form = choice(sd, n, 2, [0, 1, 2, 3]).astype(np.int64)
+    pct = choice(sd, n, 3, [25, 50, 100, 200]).astype(np.int64)
+    whole = choice(sd, n, 4, [1, 1, 2, 4]).astype(np.int64)
+    gmem = choice(sd, n, 5, [4 * GI, 8 * GI, 16 * GI]).astype(np.int64)
+    rd = dev & (uniform(sd, n, 6) < spec.rdma_frac)
+    for j in np.flatnonzero(dev):
+        x = ext[j]
+        x["flags"] = abi.PODX_DEVICE
+        g = x["dev_req"][abi.DEV_GPU]
+        f = int(form[j])
+        if f == 0:      # koordinator.sh/gpu: core = ratio = the percentage
+            g[0] = g[1] = pct[j]
+            xr = {KOORD_GPU: int(pct[j])}
+        elif f == 1:    # nvidia.com/gpu: whole GPUs
+            g[0] = g[1] = 100 * whole[j]
+            xr = {NVIDIA_GPU: int(whole[j])}
+        elif f == 2:    # gpu-core + gpu-memory-ratio
+            g[0] = pct[j] if pct[j] <= 100 else 100
+            g[1] = pct[j]
+            xr = {GPU_CORE: int(g[0]), GPU_MEMORY_RATIO: int(g[1])}
+        else:           # gpu-memory alone
+            g[2] = gmem[j]
+            xr = {GPU_MEMORY: int(gmem[j])}
+        if rd[j]:
+            x["dev_req"][abi.DEV_RDMA, 0] = 100
+            xr[RDMA] = 100
+        for name, v in xr.items():
+            x["xreq"][XRES_INDEX[name]] = v
+            x["xmask"] |= 1 << XRES_INDEX[name]
+    return ext
+
+
 # Benchmark / parity configurations (BASELINE.json "configs")
 CONFIGS = {
     1: dict(nodes=500, pods=1000, be_frac=0.0),

@@ -98,6 +98,19 @@ def lib():
         L.orc_resv_score.restype = C.c_int64
         L.orc_resv_normalized.argtypes = [C.POINTER(OrcState), vp, vp, C.c_int32, vp]
         L.orc_resv_restore_delta.argtypes = [C.POINTER(OrcState), vp, C.c_int32, vp, vp, vp]
+        L.orc_place_stream_ext.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, vp, C.c_int32,
+                                           vp, C.c_int32]
+        L.orc_eval_ext.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, vp, C.c_int32,
+                                   vp, vp, vp, C.c_int32]
+        L.orc_set_dev_out.argtypes = [C.POINTER(OrcState), vp]
+        L.orc_dev_filter.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
+        L.orc_dev_filter.restype = C.c_int
+        L.orc_dev_score.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32, C.c_int]
+        L.orc_dev_score.restype = C.c_int64
+        L.orc_dev_reserve.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32, C.c_int, vp,
+                                      C.c_int]
+        L.orc_dev_reserve.restype = C.c_int
+        L.orc_default_normalize.argtypes = [vp, C.c_int32, C.c_int]
         _lib = L
     return _lib
 
@@ -133,6 +146,62 @@ class Oracle:
                        st.ctypes.data if st is not None else None, sc.ctypes.data if sc is not None else None,
                        tk.ctypes.data if tk is not None else None, k)
         return {"status": st, "scores": sc, "topk": tk}
+
+    def eval_ext(self, pods: np.ndarray, ext=None, status=True, scores=True, k=0):
+        """koordhip_eval_ext: raw planes of the normalized plugins too, topk by the normalized totals."""
+        n, p = self.n, len(pods)
+        st = np.zeros((p, n), np.uint8) if status else None
+        sc = np.zeros((p, abi.NPLUGINS + abi.NEXT_PLUGINS, n), np.int32) if scores else None
+        tk = np.zeros((p, k), abi.TOPK_DTYPE) if k else None
+        pods = np.ascontiguousarray(pods)
+        x = None if ext is None else np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
+        lib().orc_eval_ext(C.byref(self.cfg), C.byref(self.st), pods.ctypes.data, x.ctypes.data if x is not None else None,
+                           p, st.ctypes.data if st is not None else None, sc.ctypes.data if sc is not None else None,
+                           tk.ctypes.data if tk is not None else None, k)
+        return {"status": st, "scores": sc, "topk": tk}
+
+    def place_stream_ext(self, pods: np.ndarray, ext=None, threads: int = 1, cpusets: bool = False,
+                         devices: bool = False):
+        """The reference cycle with koordhip_pod_ext records: (placements[, cpusets][, device slots [n][TYPES]])."""
+        pods = np.ascontiguousarray(pods)
+        x = None if ext is None else np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
+        out = np.zeros(len(pods), np.int32)
+        cs = np.zeros((len(pods), abi.NUMA_WORDS), np.uint64) if cpusets else None
+        dv = np.zeros((len(pods), abi.DEV_TYPES), np.uint32) if devices else None
+        lib().orc_set_cpuset_out(C.byref(self.st), cs.ctypes.data if cs is not None else None)
+        lib().orc_set_dev_out(C.byref(self.st), dv.ctypes.data if dv is not None else None)
+        rc = lib().orc_place_stream_ext(C.byref(self.cfg), C.byref(self.st), pods.ctypes.data,
+                                        x.ctypes.data if x is not None else None, len(pods), out.ctypes.data, threads)
+        lib().orc_set_cpuset_out(C.byref(self.st), None)
+        lib().orc_set_dev_out(C.byref(self.st), None)
+        if rc != 0:
+            raise RuntimeError("orc_place_stream_ext failed")
+        res = (out,) + ((cs,) if cpusets else ()) + ((dv,) if devices else ())
+        return res if len(res) > 1 else out
+
+    def dev_state(self) -> dict:
+        """DeviceShare deviceUsed [n][TYPES][S][RES] and the extended scalars' Requested [n][NXRES]."""
+        n, S = self.n, max(1, self.table.dev_slots)
+        du = (np.ctypeslib.as_array(self.st.dev_used, shape=(n, abi.DEV_TYPES, S, abi.DEV_RES)).copy()
+              if self.table.dev_slots else np.zeros((n, abi.DEV_TYPES, S, abi.DEV_RES), np.int64))
+        xr = np.ctypeslib.as_array(self.st.xrequested, shape=(abi.NXRES, n)).T.copy()
+        return {"dev_used": du, "xrequested": xr}
+
+    def dev_filter(self, ext_rec, node: int) -> bool:
+        x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)
+        return bool(lib().orc_dev_filter(C.byref(self.st), x.ctypes.data, node))
+
+    def dev_score(self, ext_rec, node: int, nominated: bool = False) -> int:
+        x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)
+        return int(lib().orc_dev_score(C.byref(self.cfg), C.byref(self.st), x.ctypes.data, node, int(nominated)))
+
+    def dev_reserve(self, ext_rec, node: int, nominated: bool = False, apply: bool = True):
+        """(ok, slots [TYPES])"""
+        x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)
+        sl = np.zeros(abi.DEV_TYPES, np.uint32)
+        rc = lib().orc_dev_reserve(C.byref(self.cfg), C.byref(self.st), x.ctypes.data, node, int(nominated),
+                                   sl.ctypes.data, int(apply))
+        return rc == 0, sl
 
     def commit(self, pod: np.ndarray, node: int, sign: int = 1, cpus=None):
         """Reserve (sign 1) / Unreserve (sign -1).  Returns (rc, cpus): rc is
@@ -297,3 +366,10 @@ def usage_percent(used_milli: int, total_milli: int) -> int:
 
 def least_requested(req: int, cap: int) -> int:
     return lib().orc_least_requested(req, cap)
+
+
+def default_normalize(scores, reverse: bool = False) -> np.ndarray:
+    """(upstream) DefaultNormalizeScore(MaxNodeScore, reverse) over a list."""
+    a = np.ascontiguousarray(scores, dtype=np.int64).copy()
+    lib().orc_default_normalize(a.ctypes.data, len(a), int(reverse))
+    return a

@@ -1,0 +1,180 @@
+"""DeviceShare and the normalized upstream Scores through libkoordhip.so's
+exact sequential cycle (seq.hip) against the oracle (oracle/dev_oracle.c,
+the reference cycle with DefaultNormalizeScore over the feasible list):
+eval_ext planes / status / top-k, and greedy streams -- placements, device
+allocations, deviceUsed, the extended scalars' Requested and the node state
+-- bit for bit, beside Fit / LoadAware / NodeNUMAResource / Reservation."""
+import numpy as np
+import pytest
+
+import oracle
+from koordinator_amd import abi, synth
+from koordinator_amd.config import shipped_profile, to_c_config, with_deviceshare, with_normalized_scores
+
+pytestmark = pytest.mark.gpu
+
+
+def _cluster(n, prof, numa=False, resv=False, seed=synth.SEED, gpu_frac=0.3):
+    t = synth.make_cluster(synth.ClusterSpec(n, seed=seed), prof)
+    if numa:
+        synth.add_numa(t, synth.NumaSpec(), prof, seed=seed)
+    if resv:
+        synth.add_reservations(t, synth.ResvSpec(), seed=seed)
+    synth.add_devices(t, synth.DevSpec(gpu_frac=gpu_frac), seed=seed)
+    return t
+
+
+def _pods(n, prof, seed=synth.SEED, cpuset=0.0, resv_match=0.0, dev_frac=0.25):
+    pods = synth.make_pods(synth.StreamSpec(n, be_frac=0.3, seed=seed, cpuset_frac=cpuset,
+                                            resv_match_frac=resv_match), prof)
+    ext = synth.make_device_ext(n, synth.DevStreamSpec(frac=dev_frac, seed=seed))
+    return pods, ext
+
+
+def _static_scores(t, pods, seed=3):
+    """Random NodeAffinity / TaintToleration raw scores per (static class, node)."""
+    rng = np.random.default_rng(seed)
+    ncls = 6
+    pods["static_class"] = rng.integers(0, ncls, len(pods))
+    ss = t["static_score"]
+    ss[:, 0, :ncls] = rng.choice([0, 0, 10, 30, 60, 100], size=(t.n, ncls))
+    ss[:, 1, :ncls] = rng.choice([0, 0, 0, 1, 2], size=(t.n, ncls))
+
+
+def _engine(prof):
+    import torch  # noqa: F401
+    from koordinator_amd.engine import PlacementEngine
+    return PlacementEngine(prof, device=0)
+
+
+def _compare_stream(prof, t, pods, ext, cpusets=False):
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        got = e.place_stream_ext(pods, ext)
+        gdev = e.fetch_devices(len(pods))
+        gst = e.read_nodes()
+        gdv = e.read_devices()
+        gcs = e.fetch_cpusets(len(pods)) if cpusets else None
+    o = oracle.Oracle(to_c_config(prof), t)
+    res = o.place_stream_ext(pods, ext, cpusets=cpusets, devices=True)
+    ref, rcs, rdev = (res[0], res[1], res[2]) if cpusets else (res[0], None, res[1])
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, f"first mismatch at pod {bad[0]}: hip {got[bad[0]]} oracle {ref[bad[0]]}"
+    assert np.array_equal(gdev, rdev)
+    ost = o.state()
+    for k in ("requested", "nz", "npods", "la_used"):
+        assert np.array_equal(gst[k], ost[k]), k
+    ods = o.dev_state()
+    if t.dev_slots:
+        assert np.array_equal(gdv["dev_used"], ods["dev_used"])
+    assert np.array_equal(gdv["xrequested"], ods["xrequested"])
+    if cpusets:
+        assert np.array_equal(gcs, rcs)
+    return got
+
+
+def test_eval_ext_parity_deviceshare():
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(700, prof)
+    pods, ext = _pods(48, prof, dev_frac=0.5)
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        g = e.eval_ext(pods, ext, k=8)
+    r = oracle.Oracle(to_c_config(prof), t).eval_ext(pods, ext, k=8)
+    assert np.array_equal(g["status"], r["status"])
+    assert np.array_equal(g["scores"], r["scores"])
+    assert np.array_equal(g["topk"], r["topk"])
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_stream_deviceshare_fit_loadaware(seed):
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(1500, prof, seed=synth.SEED + seed)
+    pods, ext = _pods(2500, prof, seed=synth.SEED + seed)
+    got = _compare_stream(prof, t, pods, ext)
+    dev = (ext["flags"] & abi.PODX_DEVICE) != 0
+    assert (got[dev] >= 0).sum() > 50   # device pods do land (and take devices)
+
+
+def test_stream_deviceshare_most_allocated():
+    prof = with_deviceshare(shipped_profile())
+    prof.deviceshare.scoring_type = "MostAllocated"
+    prof.deviceshare.resources = {"koordinator.sh/gpu-core": 1, "koordinator.sh/gpu-memory-ratio": 2,
+                                  "koordinator.sh/rdma": 1}
+    t = _cluster(900, prof, seed=synth.SEED + 5)
+    pods, ext = _pods(1500, prof, seed=synth.SEED + 5)
+    _compare_stream(prof, t, pods, ext)
+
+
+def test_stream_deviceshare_numa_reservation():
+    """DeviceShare (weight 1) beside Fit, LoadAware, NodeNUMAResource (cpuset
+    pods) and Reservation (weight 5000): the shipped koord-scheduler profile."""
+    prof = with_deviceshare(shipped_profile(numa=True, reservation=True))
+    t = _cluster(1200, prof, numa=True, resv=True, seed=synth.SEED + 7)
+    pods, ext = _pods(1500, prof, seed=synth.SEED + 7, cpuset=0.3, resv_match=0.2)
+    _compare_stream(prof, t, pods, ext, cpusets=True)
+
+
+def test_stream_normalized_upstream_scores():
+    """NodeAffinity (preferred terms) and TaintToleration (PreferNoSchedule)
+    Scores, normalized over the feasible nodes (TaintToleration reversed)."""
+    prof = with_normalized_scores(shipped_profile(), affinity=2, taint=1)
+    t = synth.make_cluster(synth.ClusterSpec(1000, seed=synth.SEED + 11), prof)
+    t.enable_ext(0)
+    pods = synth.make_pods(synth.StreamSpec(1500, be_frac=0.3, seed=synth.SEED + 11), prof)
+    _static_scores(t, pods)
+    _compare_stream(prof, t, pods, None)
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        g = e.eval_ext(pods[:32], None, k=6)
+    r = oracle.Oracle(to_c_config(prof), t).eval_ext(pods[:32], None, k=6)
+    for k in ("status", "scores", "topk"):
+        assert np.array_equal(g[k], r[k]), k
+
+
+def test_stream_everything_normalized():
+    """DeviceShare + NodeAffinity + TaintToleration Scores + NUMA in one profile."""
+    prof = with_normalized_scores(with_deviceshare(shipped_profile(numa=True), weight=3), affinity=1, taint=2)
+    t = _cluster(800, prof, numa=True, seed=synth.SEED + 13)
+    pods, ext = _pods(1200, prof, seed=synth.SEED + 13, cpuset=0.3)
+    _static_scores(t, pods, seed=5)
+    _compare_stream(prof, t, pods, ext, cpusets=True)
+
+
+def test_update_nodes_device_rows_then_stream():
+    """koordhip_update_nodes of device rows (a Device CR / pod allocation
+    event), then a stream: equal to the oracle on the updated table."""
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(600, prof, seed=synth.SEED + 17)
+    pods, ext = _pods(800, prof, seed=synth.SEED + 17)
+    rng = np.random.default_rng(4)
+    idx = np.sort(rng.choice(t.n, 60, replace=False)).astype(np.int32)
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        t2 = t.copy()
+        t2["dev_used"][idx] = 0                       # pods holding devices finished
+        t2["xrequested"][idx] = 0
+        t2["dev_present"][idx[:10]] = 1 - t2["dev_present"][idx[:10]]
+        e.update_nodes(idx, t2.rows(idx))
+        got = e.place_stream_ext(pods, ext)
+    ref = oracle.Oracle(to_c_config(prof), t2).place_stream_ext(pods, ext)
+    assert np.array_equal(got, ref)
+
+
+def test_checkpoint_restore_devices():
+    """The sequential cycle's mutable columns (deviceUsed, extended scalars)
+    roll back with koordhip_restore: two steps from one snapshot agree."""
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(500, prof, seed=synth.SEED + 19)
+    pods, ext = _pods(600, prof, seed=synth.SEED + 19)
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        e.checkpoint()
+        a = e.place_stream_ext(pods, ext)
+        da = e.read_devices()
+        e.restore()
+        b = e.place_stream_ext(pods, ext)
+        db = e.read_devices()
+    assert np.array_equal(a, b)
+    assert np.array_equal(da["dev_used"], db["dev_used"])
+    assert np.array_equal(da["xrequested"], db["xrequested"])

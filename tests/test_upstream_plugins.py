@@ -110,11 +110,18 @@ def test_static_class_limit():
 
 
 def test_static_score_rejected():
+    """NodeUnschedulable has no Score; NodeAffinity / TaintToleration Scores
+    lower to the sequential cycle's normalized planes (weights 1..100)."""
     p = with_upstream(shipped_profile())
     p.scores = dict(p.scores)
-    p.scores["TaintToleration"] = 1
+    p.scores["NodeUnschedulable"] = 1
     with pytest.raises(ArgsError):
         to_c_config(p)
+    p.scores = {**with_upstream(shipped_profile()).scores, "TaintToleration": 101}
+    with pytest.raises(ArgsError):
+        to_c_config(p)
+    p.scores["TaintToleration"] = 3
+    assert to_c_config(p).ext_weight[2] == 3
 
 
 # ------------------------------------------------------- BalancedAllocation
