@@ -170,6 +170,8 @@ class Pod:
     node_selector: Dict[str, str] = field(default_factory=dict)
     required_node_affinity: Optional[list] = None
     tolerations: list = field(default_factory=list)
+    # spec.affinity.nodeAffinity.preferredDuringScheduling...: [(weight, NodeSelectorTerm)]
+    preferred_node_affinity: list = field(default_factory=list)
 
     @property
     def key(self) -> str:

@@ -175,7 +175,7 @@ def pod_static(pod: k8s.Pod):
     """The pod fields the upstream static filters read (its static class key)."""
     from .nodefilters import PodStatic
     return PodStatic(node_selector=dict(pod.node_selector or {}), required_terms=pod.required_node_affinity,
-                     tolerations=list(pod.tolerations))
+                     tolerations=list(pod.tolerations), preferred_terms=list(pod.preferred_node_affinity or []))
 
 
 def static_filters_of(profile: Profile) -> List[str]:
@@ -183,18 +183,37 @@ def static_filters_of(profile: Profile) -> List[str]:
     return [f for f in profile.resolved().filters if f in STATIC_FILTERS]
 
 
+def static_scores_of(profile: Profile) -> List[str]:
+    """The enabled NodeAffinity / TaintToleration Scores (static_score planes)."""
+    from .config import PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION
+    return [f for f in (PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION) if f in profile.scores]
+
+
+def static_keyed(profile: Profile) -> bool:
+    """Pods carry a static class (static_allow bits and / or static_score columns)."""
+    return bool(static_filters_of(profile) or static_scores_of(profile))
+
+
+def sequential_profile(profile: Profile) -> bool:
+    """DeviceShare or a normalized Score: the engine runs the sequential cycle
+    and the snapshot carries the ABI 9 columns (NodeTable.enable_ext)."""
+    from .config import NORMALIZED_SCORES, PLUGIN_DEVICESHARE
+    return PLUGIN_DEVICESHARE in profile.filters or any(x in profile.scores for x in NORMALIZED_SCORES)
+
+
 def static_class_of(pod: k8s.Pod, profile: Profile, static_classes) -> int:
     """The pod's static class in `static_classes` (nodefilters.StaticClasses).
     Its node bits were computed when the snapshot was built: a class first seen
     after that (index >= static_classes.frozen) has no bits on the device, so
     the snapshot must be rebuilt (MarshalError)."""
-    if not static_filters_of(profile):
+    if not static_keyed(profile):
         return 0
     if static_classes is None:
-        raise MarshalError("the profile enables static node filters: pass the snapshot's StaticClasses")
+        raise MarshalError("the profile enables static node filters / Scores: pass the snapshot's StaticClasses")
     c = static_classes.classify(pod_static(pod))
     if c >= getattr(static_classes, "frozen", abi.MAX_STATIC_CLASSES):
-        raise MarshalError("pod static class first seen after the snapshot was built: rebuild it (static_allow)")
+        raise MarshalError("pod static class first seen after the snapshot was built: rebuild it "
+                           "(static_allow / static_score)")
     return c
 
 
@@ -208,6 +227,11 @@ def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None,
     p = profile.resolved()
     rec = out if out is not None else pod_array(1)[0]
     req, present = fit_request(pod)
+    if present & _DEVICE_SCALARS and not sequential_profile(p):
+        # NodeResourcesFit checks them through koordhip_pod_ext.xreq, which only
+        # the sequential cycle reads (place_stream_ext / eval_ext)
+        raise MarshalError(f"pod {pod.key} requests device resources {sorted(present & _DEVICE_SCALARS)}: "
+                           "the profile needs DeviceShare (the sequential cycle)")
     rec["req"][:] = req
     nzc, nzm = nonzero_request(pod)
     rec["nz_cpu_m"], rec["nz_mem"] = nzc, nzm
@@ -256,7 +280,7 @@ def static_classes_for(pods: Iterable[k8s.Pod], profile: Profile):
     a snapshot will schedule), for build_table / pod_records."""
     from .nodefilters import StaticClasses
     sc = StaticClasses()
-    if static_filters_of(profile):
+    if static_keyed(profile):
         for pod in pods:
             sc.classify(pod_static(pod))
     return sc
@@ -281,6 +305,7 @@ class ClusterState:
     pods: Dict[str, k8s.Pod] = field(default_factory=dict)            # lister, key ns/name
     node_pods: Dict[str, List[k8s.Pod]] = field(default_factory=dict)  # NodeInfo.Pods per node
     assigned: Dict[str, List[AssignedPod]] = field(default_factory=dict)
+    devices: Dict[str, object] = field(default_factory=dict)          # Device CRs by node (deviceshare.Device)
 
 
 def estimate_node(node: k8s.Node) -> k8s.ResourceList:
@@ -438,6 +463,8 @@ def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, pr
         t["static_allow"][i] = static_allow([node_static(node)], static_classes, sf)[0]
     else:
         t["static_allow"][i] = 0xFFFFFFFF
+    if table.has_ext:
+        ext_row(table, i, node, cluster, profile, static_classes)
     # ---- Fit: Allocatable / Requested / NonZeroRequested / len(Pods)
     alloc = node.allocatable
     t["alloc0"][i] = alloc[k8s.CPU].milli_value() if k8s.CPU in alloc else 0
@@ -539,6 +566,46 @@ def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, pr
     t["la_flags"][i] = flags
 
 
+def ext_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, profile: Profile, static_classes=None):
+    """Row i of the sequential cycle's columns: the node's Device CR and its
+    pods' device allocations (dev_*), the extended scalars' Allocatable and
+    Requested (xalloc / xrequested), the NodeAffinity / TaintToleration raw
+    Scores per static class (static_score)."""
+    from . import deviceshare as ds
+    t = table.cols
+    pods_on_node = cluster.node_pods.get(node.name, [])
+    if table.dev_slots:
+        ds.device_rows(table, i, cluster.devices.get(node.name),
+                       [ds.parse_device_allocated(p.annotations) for p in pods_on_node])
+    t["xalloc"][i] = 0
+    t["xrequested"][i] = 0
+    for n, q in node.allocatable.items():
+        if n in ds.XRES_INDEX:
+            t["xalloc"][i, ds.XRES_INDEX[n]] = q.value()
+    for p in pods_on_node:
+        for n, v in ds.fit_xreq(p).items():
+            t["xrequested"][i, ds.XRES_INDEX[n]] += v
+    t["static_score"][i] = 0
+    if static_scores_of(profile):
+        from .nodefilters import static_scores
+        if static_classes is None:
+            raise MarshalError("the profile enables NodeAffinity / TaintToleration Scores: pass the StaticClasses")
+        t["static_score"][i] = static_scores([node_static(node)], static_classes)[0]
+
+
+def device_slots_of(cluster: ClusterState) -> int:
+    """The table's dev_slots: the most devices of one type any Device CR lists (>= 1)."""
+    m = 1
+    for d in cluster.devices.values():
+        per: Dict[str, int] = {}
+        for x in d.devices:
+            per[x.type] = per.get(x.type, 0) + 1
+        m = max([m] + list(per.values()))
+    if m > abi.DEV_SLOTS:
+        raise MarshalError(f"a node lists more than {abi.DEV_SLOTS} devices of one type")
+    return m
+
+
 def _check_thr_keys(th: Dict[str, int]):
     for k in th:
         if k not in (k8s.CPU, k8s.MEMORY):
@@ -551,6 +618,9 @@ def build_table(cluster: ClusterState, profile: Profile, now: float, static_clas
     of a later class needs a rebuilt snapshot)."""
     t = NodeTable.empty(len(cluster.nodes))
     t.names = [n.name for n in cluster.nodes]
+    if sequential_profile(profile):
+        from .config import PLUGIN_DEVICESHARE
+        t.enable_ext(device_slots_of(cluster) if PLUGIN_DEVICESHARE in profile.filters else 0)
     for i, node in enumerate(cluster.nodes):
         node_row(t, i, node, cluster, profile, now, static_classes)
     if static_classes is not None:

@@ -1,6 +1,9 @@
 """The upstream static node filters of a koord-scheduler profile, resolved on
 the host per (pod static class, node) into the snapshot's `static_allow`
-column.
+column, and the raw Scores of NodeAffinity
+(preferred terms) and TaintToleration (PreferNoSchedule) per (class, node)
+into `static_score` (normalized over the feasible nodes on the device, in the
+sequential cycle).
 
 NodeUnschedulable, NodeAffinity (required part) and TaintToleration (Filter)
 read only the node's labels, taints and spec.unschedulable and the pod's
@@ -68,12 +71,15 @@ class PodStatic:
     node_selector: Dict[str, str] = field(default_factory=dict)
     required_terms: Optional[List[NodeSelectorTerm]] = None   # requiredDuringSchedulingIgnoredDuringExecution
     tolerations: List[Toleration] = field(default_factory=list)
+    # preferredDuringSchedulingIgnoredDuringExecution: (weight, NodeSelectorTerm)
+    preferred_terms: List[Tuple[int, NodeSelectorTerm]] = field(default_factory=list)
 
     def key(self) -> Tuple:
-        terms = None if self.required_terms is None else tuple(
-            (tuple((r.key, r.operator, tuple(r.values)) for r in t.match_expressions),
-             tuple((r.key, r.operator, tuple(r.values)) for r in t.match_fields)) for t in self.required_terms)
-        return (tuple(sorted(self.node_selector.items())), terms, tuple(self.tolerations))
+        tk = lambda t: (tuple((r.key, r.operator, tuple(r.values)) for r in t.match_expressions),
+                        tuple((r.key, r.operator, tuple(r.values)) for r in t.match_fields))
+        terms = None if self.required_terms is None else tuple(tk(t) for t in self.required_terms)
+        pref = tuple((int(w), tk(t)) for w, t in self.preferred_terms)
+        return (tuple(sorted(self.node_selector.items())), terms, tuple(self.tolerations), pref)
 
 
 def tolerates_all(tolerations: Sequence[Toleration], taints: Iterable[Taint], effects) -> bool:
@@ -91,6 +97,15 @@ def node_unschedulable_ok(pod: PodStatic, node: NodeStatic) -> bool:
     return any(tol.tolerates(Taint(TAINT_NODE_UNSCHEDULABLE, "", NO_SCHEDULE)) for tol in pod.tolerations)
 
 
+def _term_matches(t: NodeSelectorTerm, node: NodeStatic) -> bool:
+    """(upstream) component-helpers nodeSelectorTerm.match: expressions on the
+    labels and fields (metadata.name) all match; an empty term matches nothing."""
+    if not t.match_expressions and not t.match_fields:
+        return False
+    return all(_req_matches(r, node.labels) for r in t.match_expressions) and \
+        all(_req_matches(r, {"metadata.name": node.name}) for r in t.match_fields)
+
+
 def node_affinity_ok(pod: PodStatic, node: NodeStatic) -> bool:
     """(upstream) nodeaffinity/node_affinity.go Filter with
     component-helpers RequiredNodeAffinity.Match: every nodeSelector label,
@@ -102,19 +117,31 @@ def node_affinity_ok(pod: PodStatic, node: NodeStatic) -> bool:
             return False
     if pod.required_terms is None:
         return True
-    for t in pod.required_terms:
-        if not t.match_expressions and not t.match_fields:
-            continue
-        if all(_req_matches(r, node.labels) for r in t.match_expressions) and \
-                all(_req_matches(r, {"metadata.name": node.name}) for r in t.match_fields):
-            return True
-    return False
+    return any(_term_matches(t, node) for t in pod.required_terms)
 
 
 def taint_toleration_ok(pod: PodStatic, node: NodeStatic) -> bool:
     """(upstream) tainttoleration/taint_toleration.go Filter: every NoSchedule
     / NoExecute taint of the node is tolerated (PreferNoSchedule is Score-only)."""
     return tolerates_all(pod.tolerations, node.taints, (NO_SCHEDULE, NO_EXECUTE))
+
+
+def node_affinity_score(pod: PodStatic, node: NodeStatic) -> int:
+    """(upstream) nodeaffinity/node_affinity.go Score with component-helpers
+    PreferredSchedulingTerms.Score: the sum of the weights of the preferred
+    terms the node matches (weight-0 terms dropped).  NormalizeScore:
+    DefaultNormalizeScore(100, reverse=false) over the feasible nodes."""
+    return sum(int(w) for w, t in pod.preferred_terms if w and _term_matches(t, node))
+
+
+def taint_toleration_score(pod: PodStatic, node: NodeStatic) -> int:
+    """(upstream) tainttoleration/taint_toleration.go Score,
+    countIntolerableTaintsPreferNoSchedule: the node's PreferNoSchedule taints
+    no toleration of effect "" / PreferNoSchedule tolerates
+    (getAllTolerationPreferNoSchedule).  NormalizeScore: DefaultNormalizeScore
+    (100, reverse=true)."""
+    tols = [t for t in pod.tolerations if t.effect in ("", PREFER_NO_SCHEDULE)]
+    return sum(1 for t in node.taints if t.effect == PREFER_NO_SCHEDULE and not any(x.tolerates(t) for x in tols))
 
 
 _CHECKS = {PLUGIN_NODE_UNSCHEDULABLE: node_unschedulable_ok, PLUGIN_NODE_AFFINITY: node_affinity_ok,
@@ -158,3 +185,17 @@ def static_allow(nodes: Sequence[NodeStatic], classes: StaticClasses, filters: I
 def node_static_ok(pod: PodStatic, node: NodeStatic, filters: Iterable[str]) -> bool:
     """Direct per-(pod, node) evaluation (the test's reference for static_allow)."""
     return all(_CHECKS[f](pod, node) for f in filters if f in _CHECKS)
+
+
+def static_scores(nodes: Sequence[NodeStatic], classes: StaticClasses) -> np.ndarray:
+    """The static_score column [n][2][MAX_STATIC_CLASSES] u16: plane 0 the
+    NodeAffinity raw Score, plane 1 the TaintToleration raw Score of each
+    class on each node (unused classes 0)."""
+    out = np.zeros((len(nodes), 2, abi.MAX_STATIC_CLASSES), np.uint16)
+    for i, nd in enumerate(nodes):
+        for c, spec in enumerate(classes.specs):
+            a, b = node_affinity_score(spec, nd), taint_toleration_score(spec, nd)
+            if a > 0xFFFF or b > 0xFFFF:
+                raise ValueError("a raw NodeAffinity / TaintToleration Score above 65535")
+            out[i, 0, c], out[i, 1, c] = a, b
+    return out

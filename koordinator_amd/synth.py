@@ -356,6 +356,7 @@ class StaticSpec:
     tainted_frac: float = 0.15        # dedicated=<team>:NoSchedule
     noexec_frac: float = 0.03         # maintenance:NoExecute
     prefer_frac: float = 0.10         # soft=yes:PreferNoSchedule (Filter ignores it)
+    spot_frac: float = 0.15           # spot=true:PreferNoSchedule (a second soft taint)
     unschedulable_frac: float = 0.02  # spec.unschedulable (cordoned)
     constrained_frac: float = 0.5     # pods with a non-empty static spec
 
@@ -376,6 +377,7 @@ def static_nodes(n: int, spec: StaticSpec, seed: int = SEED):
     noexec = uniform(s, n, 95) < spec.noexec_frac
     prefer = uniform(s, n, 96) < spec.prefer_frac
     cordon = uniform(s, n, 97) < spec.unschedulable_frac
+    spot = uniform(s, n, 100) < spec.spot_frac
     out = []
     for i in range(n):
         labels = {"topology.kubernetes.io/zone": ZONES[int(zone[i])], "cpu-gen": str(int(gen[i]))}
@@ -388,6 +390,8 @@ def static_nodes(n: int, spec: StaticSpec, seed: int = SEED):
             taints.append(Taint("maintenance", "", NO_EXECUTE))
         if prefer[i]:
             taints.append(Taint("soft", "yes", PREFER_NO_SCHEDULE))
+        if spot[i]:
+            taints.append(Taint("spot", "true", PREFER_NO_SCHEDULE))
         out.append(NodeStatic(labels=labels, taints=taints, unschedulable=bool(cordon[i]), name=f"node-{i}"))
     return out
 
@@ -411,15 +415,27 @@ def static_templates():
                                Toleration("maintenance", "Exists", "", "NoExecute")]),
         PodStatic(required_terms=[T([R("cpu-gen", "Lt", ["4"])], [R("metadata.name", "NotIn", ["node-0"])])]),
         PodStatic(required_terms=[]),  # an empty term list matches no node
+        # preferred terms (NodeAffinity Score) / PreferNoSchedule tolerations (TaintToleration Score)
+        PodStatic(preferred_terms=[(10, T([R(zone, "In", ["zone-a"])])), (5, T([R("disktype", "Exists")]))]),
+        PodStatic(preferred_terms=[(1, T([R("cpu-gen", "Gt", ["3"])])),
+                                   (50, T([], [R("metadata.name", "In", ["node-1", "node-2", "node-3"])]))],
+                  tolerations=[Toleration("soft", "Equal", "yes", "PreferNoSchedule")]),
+        PodStatic(node_selector={"disktype": "ssd"},
+                  preferred_terms=[(100, T([R(zone, "NotIn", ["zone-b"])])), (0, T([R("cpu-gen", "Exists")])),
+                                   (7, T())]),
+        PodStatic(tolerations=[Toleration("spot", "Exists", "", "NoSchedule")]),   # not a PreferNoSchedule one
+        PodStatic(tolerations=[Toleration("spot", "Exists")],
+                  preferred_terms=[(3, T([R("cpu-gen", "Lt", ["4"])])), (3, T([R("disktype", "DoesNotExist")]))]),
     ]
 
 
 def add_static(t: NodeTable, pods: np.ndarray, spec: StaticSpec, profile: Profile, seed: int = SEED):
-    """Static classes for the pods (pods['static_class']) and the
-    static_allow column for the profile's enabled static filters.  Returns
-    (node specs, pod class specs) for tests."""
+    """Static classes for the pods (pods['static_class']), the static_allow
+    column for the profile's enabled static filters and, on a table with the
+    sequential cycle's columns, the NodeAffinity / TaintToleration raw Scores
+    (static_score).  Returns (node specs, pod class specs) for tests."""
     from .config import STATIC_FILTERS
-    from .nodefilters import StaticClasses, static_allow
+    from .nodefilters import StaticClasses, static_allow, static_scores
     nodes = static_nodes(t.n, spec, seed)
     tmpl = static_templates()
     n, s = len(pods), seed + 37
@@ -430,6 +446,8 @@ def add_static(t: NodeTable, pods: np.ndarray, spec: StaticSpec, profile: Profil
     ids = [cls.classify(tmpl[int(pick[j])]) if constrained[j] else 0 for j in range(n)]
     pods["static_class"][:] = np.asarray(ids, dtype=np.int32)
     t["static_allow"][:] = static_allow(nodes, cls, [f for f in profile.filters if f in STATIC_FILTERS])
+    if t.has_ext:
+        t["static_score"][:] = static_scores(nodes, cls)
     return nodes, cls
 
 
