@@ -281,6 +281,23 @@ class Informer:
         self._topo.pop(name, None)
         self._dirty.add(name)
 
+    # ---- Device events (deviceshare/device_handler.go: the nodeDevice of the node) -----------------
+    def on_device(self, dev):
+        """Add or update a Device CR (deviceshare.Device, named after its node).
+        More devices of one type than the loaded snapshot's dev_slots: reload."""
+        self.cluster.devices[dev.name] = dev
+        self._dirty.add(dev.name)
+        if self._table is not None and self._table.has_ext:
+            per = {}
+            for d in dev.devices:
+                per[d.type] = per.get(d.type, 0) + 1
+            if max(per.values(), default=0) > self._table.dev_slots:
+                self._reload = True
+
+    def on_device_delete(self, name: str):
+        if self.cluster.devices.pop(name, None) is not None:
+            self._dirty.add(name)
+
     def _numa_pod(self, pod: k8s.Pod, present: bool):
         """podEventHandler.updatePod / deletePod (pod_eventhandler.go:94-144)."""
         if not pod.node_name:
@@ -344,11 +361,11 @@ class Informer:
         affinities (ReservationIndex.register_affinities) and upstream static
         filter classes.  True when the loaded snapshot does not cover them:
         rebuild it (table()) before pod_records."""
-        from .marshal import pod_static, static_filters_of
+        from .marshal import pod_static, static_keyed
         pods = list(pods)
         if self.resv_index.register_affinities(pods):
             self._reload = True
-        if static_filters_of(self.profile):
+        if static_keyed(self.profile):
             for p in pods:
                 if self.static_classes.classify(pod_static(p)) >= self.static_classes.frozen:
                     self._reload = True

@@ -601,7 +601,7 @@ class DevSpec:
 def add_devices(t: NodeTable, spec: DevSpec, seed: int = SEED) -> NodeTable:
     """The DeviceShare columns (dev_*) and the extended scalars' allocatable /
     requested (xalloc / xrequested) of a synthetic cluster."""
-    from .deviceshare import XRES_INDEX, NVIDIA_GPU, GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, RDMA
+    from .deviceshare import XRES_INDEX, NVIDIA_GPU, KOORD_GPU, GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, RDMA
     n, sd = t.n, seed + 7
     t.enable_ext(dev_slots=8)
     gpu = uniform(sd, n, 1) < spec.gpu_frac
@@ -630,10 +630,15 @@ def add_devices(t: NodeTable, spec: DevSpec, seed: int = SEED) -> NodeTable:
         t["dev_total"][on, abi.DEV_RDMA, s, 0] = 100
     xa, xr = t["xalloc"], t["xrequested"]
     used = t["dev_used"][:, G]
+    # the slo-controller syncs the healthy GPUs' resources into the node's
+    # allocatable, koordinator.sh/gpu = their gpu-core sum
+    # (noderesource/device_resource_calculator.go:84-100)
+    tot = t["dev_total"][:, G]
     xa[gpu, XRES_INDEX[NVIDIA_GPU]] = ngpu[gpu]
-    xa[gpu, XRES_INDEX[GPU_CORE]] = 100 * ngpu[gpu]
-    xa[gpu, XRES_INDEX[GPU_MEMORY_RATIO]] = 100 * ngpu[gpu]
-    xa[gpu, XRES_INDEX[GPU_MEMORY]] = mem[gpu] * ngpu[gpu]
+    xa[:, XRES_INDEX[KOORD_GPU]] = tot[:, :, 0].sum(axis=1)
+    xa[:, XRES_INDEX[GPU_CORE]] = tot[:, :, 0].sum(axis=1)
+    xa[:, XRES_INDEX[GPU_MEMORY_RATIO]] = tot[:, :, 1].sum(axis=1)
+    xa[:, XRES_INDEX[GPU_MEMORY]] = tot[:, :, 2].sum(axis=1)
     xa[rdma, XRES_INDEX[RDMA]] = 200
     xr[:, XRES_INDEX[GPU_CORE]] = used[:, :, 0].sum(axis=1)
     xr[:, XRES_INDEX[GPU_MEMORY_RATIO]] = used[:, :, 1].sum(axis=1)

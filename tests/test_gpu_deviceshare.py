@@ -178,3 +178,21 @@ def test_checkpoint_restore_devices():
     assert np.array_equal(a, b)
     assert np.array_equal(da["dev_used"], db["dev_used"])
     assert np.array_equal(da["xrequested"], db["xrequested"])
+
+
+@pytest.mark.parametrize("numa", [False, True])
+def test_stream_static_filters_and_scores(numa):
+    """The upstream static filters (static_allow) with the NodeAffinity /
+    TaintToleration Scores of the same classes (synth.add_static: preferred
+    terms, PreferNoSchedule taints), BalancedAllocation and DeviceShare."""
+    from koordinator_amd.config import with_upstream
+    prof = with_normalized_scores(with_deviceshare(with_upstream(shipped_profile(numa=numa), balanced_weight=2)),
+                                  affinity=3, taint=2)
+    t = _cluster(1500, prof, numa=numa, seed=synth.SEED + 23)
+    pods, ext = _pods(2000, prof, seed=synth.SEED + 23, cpuset=0.3 if numa else 0.0)
+    synth.add_static(t, pods, synth.StaticSpec(), prof, seed=synth.SEED + 23)
+    assert t["static_score"][:, 0].any() and t["static_score"][:, 1].any()
+    got = _compare_stream(prof, t, pods, ext, cpusets=numa)
+    ok = got >= 0
+    cls = pods["static_class"][ok].astype(np.uint32)
+    assert (((t["static_allow"][got[ok]] >> cls) & 1) == 1).all()

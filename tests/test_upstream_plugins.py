@@ -171,3 +171,74 @@ def test_oracle_static_status_bit():
             fail = bool(r["status"][j, i] & abi.ST_STATIC_FAIL)
             assert fail == (not node_static_ok(spec, nodes[i], STATIC_FILTERS))
     assert (r["scores"][:, 3, :] > 0).all()
+
+
+# ------------------------------------------------- NodeAffinity / TaintToleration Scores
+# Worked from the published k8s v1.24 plugins (parity unpinned, like the
+# filters above): NodeAffinity sums the weights of the matched preferred terms
+# and normalizes by the max; TaintToleration counts the intolerable
+# PreferNoSchedule taints and normalizes reversed.
+def _norm(raw, reverse=False):
+    return oracle.default_normalize(raw, reverse=reverse).tolist()
+
+
+def test_node_affinity_score_weights():
+    from koordinator_amd.nodefilters import node_affinity_score
+    pref = [(2, T([R("foo", "In", ["bar"])])), (4, T([R("key", "In", ["value"])])),
+            (5, T([R("foo", "In", ["bar"]), R("key", "In", ["value"]), R("az", "In", ["az1"])]))]
+    pod = PodStatic(preferred_terms=pref)
+    nodes = [NodeStatic(labels={"foo": "bar"}), NodeStatic(labels={"foo": "bar", "key": "value", "az": "az1"}),
+             NodeStatic(labels={"key": "value"})]
+    raw = [node_affinity_score(pod, n) for n in nodes]
+    assert raw == [2, 11, 4]
+    assert _norm(raw) == [18, 100, 36]
+    one = PodStatic(preferred_terms=pref[:1])
+    assert _norm([node_affinity_score(one, n) for n in nodes]) == [100, 100, 0]
+    assert _norm([node_affinity_score(PodStatic(), n) for n in nodes]) == [0, 0, 0]
+    # weight-0 and empty terms score nothing; match_fields read the node name
+    odd = PodStatic(preferred_terms=[(0, T([R("foo", "Exists")])), (9, T()),
+                                     (3, T([], [R("metadata.name", "In", ["n1"])]))])
+    assert node_affinity_score(odd, NodeStatic(labels={"foo": "x"}, name="n1")) == 3
+    assert node_affinity_score(odd, NodeStatic(labels={"foo": "x"}, name="n2")) == 0
+
+
+def test_taint_toleration_score_counts():
+    from koordinator_amd.nodefilters import taint_toleration_score
+    P = PREFER_NO_SCHEDULE
+    nodes = [NodeStatic(taints=[]), NodeStatic(taints=[Taint("a", "1", P)]),
+             NodeStatic(taints=[Taint("a", "1", P), Taint("b", "2", P), Taint("c", "", NO_SCHEDULE)])]
+    raw = [taint_toleration_score(PodStatic(), n) for n in nodes]
+    assert raw == [0, 1, 2]
+    assert _norm(raw, reverse=True) == [100, 50, 0]
+    tol = PodStatic(tolerations=[Toleration("a", "Equal", "1", P)])
+    assert [taint_toleration_score(tol, n) for n in nodes] == [0, 0, 1]
+    # a toleration of another effect does not count for the Score
+    ns = PodStatic(tolerations=[Toleration("a", "Exists", "", NO_SCHEDULE)])
+    assert [taint_toleration_score(ns, n) for n in nodes] == [0, 1, 2]
+    # every node tolerated: all raw 0 -> reversed normalize gives 100 everywhere
+    allt = PodStatic(tolerations=[Toleration(operator="Exists")])
+    assert _norm([taint_toleration_score(allt, n) for n in nodes], reverse=True) == [100, 100, 100]
+
+
+def test_static_score_columns_from_synth():
+    from koordinator_amd.config import with_normalized_scores
+    from koordinator_amd.nodefilters import node_affinity_score, taint_toleration_score
+    prof = with_normalized_scores(with_upstream(shipped_profile()), affinity=2, taint=1)
+    t = synth.make_cluster(synth.ClusterSpec(300), prof)
+    t.enable_ext(0)
+    pods = synth.make_pods(synth.StreamSpec(200, be_frac=0.3), prof)
+    nodes, cls = synth.add_static(t, pods, synth.StaticSpec(), prof)
+    ss = t["static_score"]
+    assert ss[:, 0].any() and ss[:, 1].any()
+    for i in range(0, 300, 5):
+        for c, spec in enumerate(cls.specs):
+            assert ss[i, 0, c] == node_affinity_score(spec, nodes[i])
+            assert ss[i, 1, c] == taint_toleration_score(spec, nodes[i])
+
+
+def test_static_class_key_includes_preferred_terms():
+    cls = StaticClasses()
+    a = cls.classify(PodStatic(preferred_terms=[(1, T([R("a", "Exists")]))]))
+    b = cls.classify(PodStatic(preferred_terms=[(2, T([R("a", "Exists")]))]))
+    c = cls.classify(PodStatic(preferred_terms=[(1, T([R("a", "Exists")]))]))
+    assert a != b and a == c
