@@ -87,7 +87,7 @@ def cpu_share() -> int:
     return n
 
 
-def cpu_baseline(table, pods, cfg, budget_s=12.0):
+def cpu_baseline(table, pods, cfg, budget_s=12.0, ext=None):
     """The oracle (C port of the reference loop: parallelize.Until over nodes,
     sqrt-n chunks, serial selectHost + Reserve) on this host, on a bounded
     prefix of the same stream, at the reference's parallelism (16 workers,
@@ -102,13 +102,15 @@ def cpu_baseline(table, pods, cfg, budget_s=12.0):
     for name, threads in (("ref16", min(16, ncpu)), ("nproc", ncpu), ("single", 1)):
         per = budget_s / 3
         probe = 32
+        run = ((lambda o, m: o.place_stream(pods[:m], threads=threads)) if ext is None else
+               (lambda o, m: o.place_stream_ext(pods[:m], ext[:m], threads=threads)))
         t = time.perf_counter()
-        oracle.Oracle(cfg, table).place_stream(pods[:probe], threads=threads)
+        run(oracle.Oracle(cfg, table), probe)
         dt = time.perf_counter() - t
         n = int(min(len(pods), max(probe, per / max(dt / probe, 1e-9))))
         o = oracle.Oracle(cfg, table)
         t = time.perf_counter()
-        o.place_stream(pods[:n], threads=threads)
+        run(o, n)
         dt = time.perf_counter() - t
         legs[name] = {"threads": threads, "pods": n, "pods_per_s": round(n / dt, 2),
                       "evals_per_s": round(n * table.n / dt, 1)}
@@ -118,7 +120,8 @@ def cpu_baseline(table, pods, cfg, budget_s=12.0):
             "evals_per_s": ref["evals_per_s"], "legs": legs,
             "best_leg": {"name": best, **legs[best]}, "cpu_model": _cpu_model(), "nproc": ncpu,
             "sample": f"first {ref['pods']} pods of the same stream on the same {table.n}-node snapshot, "
-                      f"oracle/koord_oracle.c orc_place_stream with {ref['threads']} workers "
+                      f"oracle/koord_oracle.c {'orc_place_stream' if ext is None else 'orc_place_stream_ext'} "
+                      f"with {ref['threads']} workers "
                       f"(legs: {ncpu} workers, 1 worker); the Go reference itself cannot run here (no Go toolchain)"}
 
 
@@ -157,15 +160,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["config4", "config3", "config5"], default="config4",
+    ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare"], default="config4",
                     help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
                          "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods); "
                          "config5: 200k nodes, 10%% holding a Reservation matched by 20%% of the pods, "
-                         "+ LoadAware + NodeNUMAResource")
+                         "+ LoadAware + NodeNUMAResource; deviceshare: config 4's cluster with GPU / RDMA "
+                         "devices and 20%% device pods, + DeviceShare (weight 1): the exact sequential cycle, "
+                         "one GPU")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--be-frac", type=float, default=None)
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--dev-frac", type=float, default=0.2, help="deviceshare workload: share of pods requesting GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--check", action="store_true", help="verify placements vs the oracle (slow)")
@@ -189,8 +195,13 @@ def main():
 
     import torch
     from koordinator_amd import synth
-    from koordinator_amd.config import shipped_profile, to_c_config
+    from koordinator_amd.config import shipped_profile, to_c_config, with_deviceshare
     from koordinator_amd.engine import PlacementEngine
+
+    if args.workload == "deviceshare":
+        if world > 1:
+            raise SystemExit("--workload deviceshare runs on one GPU (the sequential cycle is not node-sharded)")
+        return run_sequential(args, torch, synth, with_deviceshare(shipped_profile()), PlacementEngine)
 
     dist = None
     if world > 1:
@@ -365,6 +376,95 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def seq_bytes_per_eval(pods: np.ndarray, ext: np.ndarray, cfg, dev_slots: int) -> np.ndarray:
+    """Algorithmic node-column bytes per (pod, node) of the sequential cycle's
+    evaluation: the Fit / LoadAware columns (bytes_per_eval), the extended
+    scalars a pod requests (xalloc + xrequested, 16 B per requested name), and
+    for a device pod the node's nodeDevice entry (dev_present 1 B) and its GPU
+    and RDMA slots (minor i32, total + used of the requested resources i64)."""
+    from koordinator_amd import abi
+    b = bytes_per_eval(pods, cfg).copy()
+    xm = ext["xmask"].astype(np.int64)
+    b += 16 * np.array([bin(int(x)).count("1") for x in xm], np.int64)
+    dev = (ext["flags"] & abi.PODX_DEVICE) != 0
+    g = ext["dev_req"][:, abi.DEV_GPU]
+    gres = (g > 0).sum(axis=1)
+    rd = ext["dev_req"][:, abi.DEV_RDMA, 0] > 0
+    per = 1 + dev_slots * (4 + 16 * gres) + rd * dev_slots * (4 + 16)
+    return b + np.where(dev, per, 0)
+
+
+def run_sequential(args, torch, synth, prof, PlacementEngine):
+    """The DeviceShare workload: one persistent cooperative k_seq launch per
+    step (every node filtered and scored per pod, normalized over the
+    feasible nodes, the argmax committed before the next pod)."""
+    c = synth.CONFIGS[4]
+    args.nodes = args.nodes or c["nodes"]
+    args.pods = args.pods or 20000
+    args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
+    table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
+    synth.add_devices(table, synth.DevSpec())
+    pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac), prof)
+    ext = synth.make_device_ext(args.pods, synth.DevStreamSpec(frac=args.dev_frac))
+    from koordinator_amd.config import to_c_config
+    cfg = to_c_config(prof)
+    eng = PlacementEngine(prof, device=0, profile_kernels=False)
+    eng.load_snapshot(table)
+    eng.checkpoint()
+    eng.stage_pods_ext(pods, ext)
+
+    def step():
+        eng.restore()
+        eng.place_staged()
+
+    for _ in range(args.warmup):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ks = eng.kernel_stats()          # the last step's k_seq launch, HIP events on the engine's stream
+    kn = eng.kernel_names()
+    placements = eng.fetch_placements(len(pods))
+    seq_s = ks["total_ms"] * 1e-3
+    b = seq_bytes_per_eval(pods, ext, cfg, table.dev_slots)
+    alg = float(b.sum()) * args.nodes
+    gbs = alg / seq_s / 1e9 if seq_s > 0 else None
+    value = args.pods * args.steps / elapsed
+    dev = (ext["flags"] & 1) != 0
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "pods/s",
+        "evals_per_s": round(args.pods * args.nodes * args.steps / elapsed, 1),
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeded splitmix64 cluster + pod stream)",
+        "config": {"workload": f"deviceshare: {args.nodes} nodes (30% with 4/8 GPUs, half of those 2 RDMA NICs) x "
+                               f"{args.pods} pods ({int(dev.mean() * 100)}% requesting GPUs), "
+                               "NodeResourcesFit + LoadAwareScheduling + DeviceShare (weight 1, LeastAllocated), "
+                               "the exact sequential cycle",
+                   "nodes": args.nodes, "pods": args.pods, "parallelism": "single GPU (cooperative grid)"},
+        "unschedulable": int((placements < 0).sum()),
+        "device_pods_placed": int(((placements >= 0) & dev).sum()),
+        "roofline": {"bound": "latency", "kernel": kn["resolve"],
+                     "limiter": "four grid-wide hand-offs per pod (not bandwidth); priced against HBM peak",
+                     "timing": "HIP events around the k_seq launch of the last timed step",
+                     "achieved": round(gbs, 2) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs / HBM_PEAK_GBS, 5) if gbs else None, "traffic": None,
+                     "algorithmic_bytes_per_eval": round(float(b.mean()), 2),
+                     "avg_launch_ms": round(seq_s * 1e3, 3),
+                     "us_per_pod": round(seq_s * 1e6 / args.pods, 3)},
+    }
+    if not args.no_cpu_baseline:
+        cb = cpu_baseline(table, pods, cfg, args.cpu_budget, ext=ext)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_best_cpu_leg"] = round(value / cb["best_leg"]["pods_per_s"], 1)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

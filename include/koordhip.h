@@ -477,6 +477,10 @@ int koordhip_read_devices(koordhip_ctx *ctx, int64_t *dev_used, int64_t *xreques
  * (host -> HBM copy) then place (HBM-resident pods, result kept on device
  * until koordhip_fetch_placements). */
 int koordhip_stage_pods(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods);
+/* ABI 9: stage pods with their koordhip_pod_ext records (ext may be NULL),
+ * for koordhip_place_staged on a sequential-cycle profile. */
+int koordhip_stage_pods_ext(koordhip_ctx *ctx, const koordhip_pod *pods, const koordhip_pod_ext *ext,
+                            int32_t n_pods);
 int koordhip_place_staged(koordhip_ctx *ctx);
 int koordhip_fetch_placements(koordhip_ctx *ctx, int32_t *out_node, int32_t n_pods);
 int koordhip_synchronize(koordhip_ctx *ctx);

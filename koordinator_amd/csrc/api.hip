@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/koordhip.h"
+#include "dev.hpp"
 #include "kernels.h"
 
 namespace {
@@ -1633,10 +1634,14 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
   return 0;
 }
 
+int koordhip_stage_pods_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods) {
+  if (int e = koordhip_stage_pods(c, pods, n_pods)) return e;
+  return stage_ext(c, ext, n_pods);
+}
+
 int koordhip_place_stream_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods,
                               int32_t *out_node) {
-  if (int e = koordhip_stage_pods(c, pods, n_pods)) return e;
-  if (int e = stage_ext(c, ext, n_pods)) return e;
+  if (int e = koordhip_stage_pods_ext(c, pods, ext, n_pods)) return e;
   if (int e = koordhip_place_staged(c)) return e;
   return koordhip_fetch_placements(c, out_node, n_pods);
 }
@@ -1860,7 +1865,7 @@ int seq_place(koordhip_ctx *c) {
     return fail(KOORDHIP_EINVAL, "the sequential cycle (DeviceShare / normalized Scores) runs on one GPU only");
   const int32_t G = c->n_cu;
   if ((int64_t)G * 256 * 8 < c->n) return fail(KOORDHIP_EINVAL, "too many nodes for the sequential cycle's grid");
-  const size_t gbytes = (size_t)2 * 2 * G * 4 * sizeof(uint64_t) + 64;
+  const size_t gbytes = (size_t)2 * 2 * G * 8 * sizeof(uint64_t) + 64;  // [phase][parity][G][8] + the timeout word
   if (!c->d_seqg) {
     HIP_TRY(hipMalloc(&c->d_seqg, gbytes));
     c->seq_grid = G;
@@ -1871,10 +1876,25 @@ int seq_place(koordhip_ctx *c) {
   uint32_t *tmo = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(c->d_seqg) + gbytes - 64);
   HIP_TRY(hipMemsetAsync(c->d_seqg, 0, gbytes, c->stream));
   const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
+  const bool stamps = std::getenv("KOORDHIP_STAMPS") != nullptr;
+  if (stamps) {
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 64 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 64 * sizeof(uint64_t), c->stream));
+  }
   HIP_TRY(hipEventRecord(c->t0, c->stream));
   HIP_TRY(kh::launch_seq(c->dc, c->d, c->d_pods, c->podx_staged ? c->d_podx : nullptr, np, G, c->d_seqg, tmo,
-                         c->d_out, c->d_cpus, dev ? c->d_devout : nullptr, rs, c->stream));
+                         c->d_out, c->d_cpus, dev ? c->d_devout : nullptr, rs, stamps ? c->d_dbg : nullptr,
+                         c->stream));
   HIP_TRY(hipEventRecord(c->t1, c->stream));
+  if (stamps) {
+    uint64_t h[6];
+    HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const double q = 1.0 / std::max(np, 1);
+    std::fprintf(stderr, "[koordhip stamps] k_seq block 0 cycles per pod: evaluate %.0f  wait A %.0f  normalize+publish %.0f  "
+                 "wait B %.0f  commit barrier %.0f | owner commits %.0f\n", h[0] * q, h[1] * q, h[2] * q, h[3] * q,
+                 h[4] * q, h[5] * q);
+  }
   c->last_P = 1;
   c->last_lag = 0;
   c->last_evals = (int64_t)np * c->n;

@@ -33,19 +33,6 @@ __device__ __forceinline__ size_t dev_at(const DevDev &dv, int32_t i, int t, int
   return ((size_t)i * DT + (size_t)t) * (size_t)dv.slots + (size_t)s;
 }
 
-// one minor of type t: its total and free resources; false = empty slot
-__device__ __forceinline__ bool dev_slot(const DevDev &dv, int32_t i, int t, int s, int64_t tot[DR], int64_t fr[DR]) {
-  const size_t a = dev_at(dv, i, t, s);
-  if (dv.minor[a] < 0) return false;
-#pragma unroll
-  for (int r = 0; r < DR; r++) {
-    tot[r] = dv.total[a * DR + r];
-    const int64_t x = tot[r] - dv.used[a * DR + r];
-    fr[r] = x > 0 ? x : 0;
-  }
-  return true;
-}
-
 __device__ __forceinline__ bool dev_zero(const int64_t v[DR]) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
 
 __device__ __forceinline__ bool dev_requests(const DevPodX &x, int t, int64_t q[DR]) {
@@ -58,22 +45,45 @@ __device__ __forceinline__ bool dev_requests(const DevPodX &x, int t, int64_t q[
   return any;
 }
 
-__device__ __forceinline__ bool dev_has_type(const DevDev &dv, int32_t i, int t) {
-  for (int s = 0; s < dv.slots; s++)
-    if (dv.minor[dev_at(dv, i, t, s)] >= 0) return true;
-  return false;
+// A node's minors of one type, loaded once: every slot's minor, total and
+// free issue back to back (unrolled over KOORDHIP_DEV_SLOTS) instead of one
+// dependent round trip per slot and per plugin.
+struct DevRow {
+  int32_t minor[DS];
+  int64_t tot[DS][DR];
+  int64_t fr[DS][DR];
+};
+
+__device__ __forceinline__ void dev_load(const DevDev &dv, int32_t i, int t, DevRow &w) {
+  const size_t a0 = dev_at(dv, i, t, 0);
+#pragma unroll
+  for (int s = 0; s < DS; s++) {
+    const bool on = s < dv.slots;
+    w.minor[s] = on ? dv.minor[a0 + s] : -1;
+#pragma unroll
+    for (int r = 0; r < DR; r++) {
+      const int64_t tt = on ? dv.total[(a0 + s) * DR + r] : 0;
+      const int64_t x = tt - (on ? dv.used[(a0 + s) * DR + r] : 0);
+      w.tot[s][r] = tt;
+      w.fr[s][r] = x > 0 ? x : 0;
+    }
+  }
+}
+
+__device__ __forceinline__ bool dev_has_type(const DevRow &w) {
+  bool any = false;
+#pragma unroll
+  for (int s = 0; s < DS; s++) any |= w.minor[s] >= 0;
+  return any;
 }
 
 // fillGPUTotalMem (utils.go:211-233): memory <-> ratio from the node's GPU
 // memory (the first GPU with resources; one model per node, host-checked)
-__device__ __forceinline__ bool dev_fill_gpu(const DevDev &dv, int32_t i, int64_t q[DR]) {
+__device__ __forceinline__ bool dev_fill_gpu(const DevRow &w, int64_t q[DR]) {
   int64_t mem = -1;
-  for (int s = 0; s < dv.slots && mem < 0; s++) {
-    const size_t a = dev_at(dv, i, KOORDHIP_DEV_GPU, s);
-    if (dv.minor[a] < 0) continue;
-    const int64_t *t = dv.total + a * DR;
-    if (t[0] != 0 || t[1] != 0 || t[2] != 0) mem = t[2];
-  }
+#pragma unroll
+  for (int s = DS - 1; s >= 0; s--)
+    if (w.minor[s] >= 0 && (w.tot[s][0] != 0 || w.tot[s][1] != 0 || w.tot[s][2] != 0)) mem = w.tot[s][2];
   if (mem < 0) return false;
   if (q[2] >= 0) {
     const double f = (double)q[2] / (double)mem;  // memoryBytesToRatio, float64
@@ -130,106 +140,111 @@ __device__ __forceinline__ bool dev_present(const DevDev &dv, int32_t i) {
   return dv.slots > 0 && dv.present && dv.present[i];
 }
 
-// DeviceShare Filter: per requested type, `wanted` devices hold the per-device request
-__device__ __forceinline__ bool dev_filter(const DevDev &dv, const DevPodX &x, int32_t i) {
+// DeviceShare Filter (plugin.go:284-323: per requested type, `wanted`
+// devices hold the per-device request) and the raw Score (scoring.go:33-72,
+// before NormalizeScore; computed on infeasible nodes too, like the
+// reference's planes) in one pass over the node's device rows.  `nominated`:
+// a reservation PreScore nominated on the node (no device reservation state:
+// Score 0).  Returns the Filter verdict.
+__device__ __forceinline__ bool dev_eval(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
+                                         bool nominated, bool filter, bool score, int32_t *raw) {
+  *raw = 0;
   if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i)) return true;
-  for (int t = 0; t < DT; t++) {
-    int64_t q[DR], per[DR], tot[DR], f[DR];
-    if (!dev_requests(x, t, q)) continue;
-    if (!dev_has_type(dv, i, t)) return false;
-    if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(dv, i, q)) return false;
-    const int64_t w = dev_wanted(t, q, per);
-    int64_t cnt = 0;
-    for (int s = 0; s < dv.slots; s++) {
-      if (!dev_slot(dv, i, t, s, tot, f) || dev_zero(f)) continue;
-      cnt += dev_fits(per, f) ? 1 : 0;
-    }
-    if (cnt < w) return false;
-  }
-  return true;
-}
-
-// DeviceShare Score (raw, before NormalizeScore); `nominated`: a reservation
-// PreScore nominated on the node (no device reservation state: 0)
-__device__ __forceinline__ int32_t dev_score(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
-                                             bool nominated) {
-  if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i) || nominated) return 0;
+  bool ok = true;
   int64_t sum = 0;
   for (int t = 0; t < DT; t++) {
-    int64_t q[DR], tot[DR], f[DR];
-    if (!dev_requests(x, t, q) || !dev_has_type(dv, i, t)) continue;
-    if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(dv, i, q)) continue;
-    int64_t st[DR] = {0, 0, 0}, sf[DR] = {0, 0, 0};
-    for (int s = 0; s < dv.slots; s++) {
-      if (!dev_slot(dv, i, t, s, tot, f)) continue;
-#pragma unroll
-      for (int r = 0; r < DR; r++) {
-        st[r] += tot[r];
-        sf[r] += f[r];
-      }
+    int64_t q[DR];
+    if (!dev_requests(x, t, q)) continue;
+    DevRow w;
+    dev_load(dv, i, t, w);
+    if (!dev_has_type(w) || (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(w, q))) {
+      ok = false;
+      continue;
     }
+    if (filter) {
+      int64_t per[DR];
+      const int64_t want = dev_wanted(t, q, per);
+      int64_t cnt = 0;
 #pragma unroll
-    for (int r = 0; r < DR; r++) q[r] = q[r] > 0 ? q[r] : 0;
-    sum += dev_scorer(c, t, st, sf, q);
+      for (int s = 0; s < DS; s++)
+        cnt += (w.minor[s] >= 0 && !dev_zero(w.fr[s]) && dev_fits(per, w.fr[s])) ? 1 : 0;
+      ok &= cnt >= want;
+    }
+    if (score && !nominated) {
+      int64_t st[DR] = {0, 0, 0}, sf[DR] = {0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < DS; s++)
+        if (w.minor[s] >= 0)
+#pragma unroll
+          for (int r = 0; r < DR; r++) {
+            st[r] += w.tot[s][r];
+            sf[r] += w.fr[s][r];
+          }
+#pragma unroll
+      for (int r = 0; r < DR; r++) q[r] = q[r] > 0 ? q[r] : 0;
+      sum += dev_scorer(c, t, st, sf, q);
+    }
   }
-  return (int32_t)sum;
+  *raw = (int32_t)sum;
+  return ok || !filter;
 }
 
-// DeviceShare Reserve: per requested type the devices by (device score desc,
-// minor asc), the first `wanted` that hold the per-device request.  slots[t]:
-// bit s = dev slot s.  apply: add the per-device request to each one's used.
-// false: the Reserve fails (insufficient devices, or a nominated reservation
-// DeviceShare holds no state for).
+// DeviceShare Reserve (allocator.go:91-122): per requested type the devices
+// by (device score desc, minor asc), the first `wanted` that hold the
+// per-device request.  slots[t]: bit s = dev slot s; per[t]: the per-device
+// request dev_apply adds.  false: the Reserve fails (insufficient devices, or
+// a nominated reservation DeviceShare holds no state for).
 __device__ __forceinline__ bool dev_reserve(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
-                                            bool nominated, uint32_t slots[DT], bool apply) {
+                                            bool nominated, uint32_t slots[DT], int64_t per_t[DT][DR]) {
 #pragma unroll
-  for (int t = 0; t < DT; t++) slots[t] = 0u;
-  if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i)) return true;
-  if (nominated) return false;
-  int64_t per_t[DT][DR];
   for (int t = 0; t < DT; t++) {
-    int64_t q[DR], per[DR], tot[DR], f[DR];
+    slots[t] = 0u;
 #pragma unroll
     for (int r = 0; r < DR; r++) per_t[t][r] = 0;
+  }
+  if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i)) return true;
+  if (nominated) return false;
+  for (int t = 0; t < DT; t++) {
+    int64_t q[DR], per[DR];
     if (!dev_requests(x, t, q)) continue;
-    if (!dev_has_type(dv, i, t)) return false;
-    if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(dv, i, q)) return false;
-    const int64_t w = dev_wanted(t, q, per);
-    // selection: repeatedly the best unpicked fitting device (score desc, minor asc)
-    int64_t got = 0;
+    DevRow w;
+    dev_load(dv, i, t, w);
+    if (!dev_has_type(w)) return false;
+    if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(w, q)) return false;
+    const int64_t want = dev_wanted(t, q, per);
+    // every fitting device's score once, then the best `want` by (score desc, minor asc)
+    int64_t sc[DS];
+#pragma unroll
+    for (int s = 0; s < DS; s++)
+      sc[s] = (w.minor[s] >= 0 && !dev_zero(w.fr[s]) && dev_fits(per, w.fr[s])) ? dev_scorer(c, t, w.tot[s], w.fr[s], per)
+                                                                               : -1;
     uint32_t taken = 0u;
-    while (got < w) {
+    for (int64_t got = 0; got < want; got++) {
       int bs = -1;
-      int64_t bsc = -1;
-      int32_t bmin = 0;
-      for (int s = 0; s < dv.slots; s++) {
-        if ((taken >> s) & 1u) continue;
-        if (!dev_slot(dv, i, t, s, tot, f) || dev_zero(f) || !dev_fits(per, f)) continue;
-        const int64_t sc = dev_scorer(c, t, tot, f, per);
-        const int32_t m = dv.minor[dev_at(dv, i, t, s)];
-        if (bs < 0 || sc > bsc || (sc == bsc && m < bmin)) {
-          bs = s;
-          bsc = sc;
-          bmin = m;
-        }
+#pragma unroll
+      for (int s = 0; s < DS; s++) {
+        if (sc[s] < 0 || ((taken >> s) & 1u)) continue;
+        if (bs < 0 || sc[s] > sc[bs] || (sc[s] == sc[bs] && w.minor[s] < w.minor[bs])) bs = s;
       }
       if (bs < 0) return false;
       taken |= 1u << bs;
-      got++;
     }
     slots[t] = taken;
 #pragma unroll
     for (int r = 0; r < DR; r++) per_t[t][r] = per[r];
   }
-  if (apply)
-    for (int t = 0; t < DT; t++)
-      for (int s = 0; s < dv.slots; s++)
-        if ((slots[t] >> s) & 1u) {
-          const size_t a = dev_at(dv, i, t, s) * DR;
-#pragma unroll
-          for (int r = 0; r < DR; r++) dv.used[a + r] += per_t[t][r];
-        }
   return true;
+}
+
+__device__ __forceinline__ void dev_apply(const DevDev &dv, int32_t i, const uint32_t slots[DT],
+                                          const int64_t per_t[DT][DR]) {
+  for (int t = 0; t < DT; t++)
+    for (int s = 0; s < dv.slots; s++)
+      if ((slots[t] >> s) & 1u) {
+        const size_t a = dev_at(dv, i, t, s) * DR;
+#pragma unroll
+        for (int r = 0; r < DR; r++) dv.used[a + r] += per_t[t][r];
+      }
 }
 
 // NodeResourcesFit over the extended scalars the pod requests (upstream fitsRequest)

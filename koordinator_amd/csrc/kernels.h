@@ -2,8 +2,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "dev.hpp"
 #include "eval.hpp"
+
+namespace kh {
+struct DevPodX;  // dev.hpp (seq.hip, api.hip)
+}
 
 namespace kh {
 
@@ -96,7 +99,7 @@ const char *last_resolve_kernel();
 // plugin scores.
 hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                       int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
-                      uint32_t *out_dev, int32_t rs, hipStream_t s);
+                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, hipStream_t s);
 // parity: status bits (ORed into status: k_eval_full writes them first), the
 // normalized plugins' raw planes of scores ([np][NPLUGINS + NEXT][n]), and
 // the top-k of the normalized totals per pod; work: [np][4][n] int32

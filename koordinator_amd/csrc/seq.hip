@@ -10,12 +10,16 @@
 //
 //   phase A  every block evaluates its node slices (Filter of every plugin,
 //            the weighted sum of the per-node plugins, the raw normalized
-//            scores) into registers; per block: feasible count and the raw
-//            maxima over its feasible nodes, published as tagged granules
-//   phase B  every block reads all blocks' granules (the data is the flag:
-//            cdna_hip_programming.md Guideline 16 R2, no barrier), normalizes
-//            its nodes' raw scores by the global maxima, and publishes its best
-//            (total, lowest index) key the same way
+//            scores) into LDS; per block: feasible count, the raw maxima over
+//            its feasible nodes and its best (total, lowest index) key as if
+//            every maximum were 0, published as tagged granules (the data is
+//            the flag: cdna_hip_programming.md Guideline 16 R2, no barrier)
+//   phase B  only when some maximum is not 0 (a pod requesting devices, or
+//            with preferred terms / intolerable soft taints somewhere): every
+//            block normalizes its nodes' raw scores by the global maxima and
+//            publishes its best key the same way.  With all maxima 0 every
+//            normalized score is the same constant, so phase A's keys already
+//            rank the nodes: one hand-off per pod instead of two.
 //   commit   every block reads all keys: the winner w; the block owning w
 //            runs the Reserve of every plugin on w (DeviceShare's device
 //            choice, NodeNUMAResource's cpuset, Reservation's assume, the
@@ -23,7 +27,7 @@
 //            next pod.  Node w is only ever read by its owner block, so no
 //            other block waits for the commit.
 //
-// Granule ring: 2 parities x G blocks x 4 words; a block overwrites parity
+// Granule ring: 2 parities x G blocks x SEQ_GRAN words; a block overwrites parity
 // q's granules only after it has read every block's granules of the next
 // phase, which every block writes after it finished reading parity q.
 #include <hip/hip_runtime.h>
@@ -36,20 +40,28 @@ namespace kh {
 constexpr int SEQ_THREADS = 256;
 constexpr int SEQ_NPT = 8;  // nodes per thread held across the pod's phases (grid 256 x 256 x 8 >= 400k nodes)
 constexpr uint32_t SEQ_SPIN_LIMIT = 1u << 24;
+constexpr int SEQ_GRAN = 8;  // granule words per block and phase (6 used)
 
 struct SeqArgs {
   const DevPod *pods;
   const DevPodX *podx;  // NULL: no pod has a device / extended request
   int32_t n_pods;
   int32_t npt;          // node slices per thread
-  uint64_t *ga, *gb;    // granules [2][G][4]
+  uint64_t *ga, *gb;    // granules [2][G][SEQ_GRAN]
   uint32_t *tmo;        // spin timeout word (0 = ok)
   int32_t *out_node;
   uint64_t *out_cpus;   // [n_pods][NW] (NULL: no NodeNUMAResource)
   uint32_t *out_dev;    // [n_pods][DT] (NULL: no DeviceShare)
   uint32_t ext;         // bit e: normalized plugin e scores (DeviceShare, NodeAffinity, TaintToleration)
   int32_t rs;           // the Reservation plugin scores (its PreScore nominates)
+  uint64_t *dbg;        // KOORDHIP_STAMPS: block 0's per-phase cycle sums [0..4], owner commits [5] (NULL: off)
 };
+
+__device__ __forceinline__ uint64_t seq_stamp() {
+  uint64_t v;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+  return v;
+}
 
 __device__ __forceinline__ uint64_t seq_wave_max(uint64_t v) {
 #pragma unroll
@@ -68,8 +80,9 @@ __device__ __forceinline__ uint32_t ext_bits(const DevCfg &c) {
 // One node for one pod: the total of the per-node plugins (-1: some Filter
 // fails; with the Reservation plugin the ranking total of resv.hpp) and the
 // raw normalized scores.  Every column is read (the parity evaluator's rows,
-// like k_eval_full).
-__device__ __noinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x,
+// like k_eval_full).  Inlined once per kernel: a call keeps its frame (the
+// config and column descriptors, the NV row) in scratch, kilobytes per lane.
+__device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x,
                                             int32_t i, bool rs, int32_t raw[KOORDHIP_NEXT_PLUGINS],
                                             uint8_t *status) {
   NV v{};
@@ -90,10 +103,10 @@ __device__ __noinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, con
     t = eval_total(p, v, c);
   }
   const bool xf = !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x, i, d.n);
-  const bool df = !(c.filt & KOORDHIP_PLUGIN_DEVICESHARE) || dev_filter(d.dv, x, i);
+  const bool df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                           (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
   if (status) *status = (xf ? 0 : KOORDHIP_ST_XFIT_FAIL) | (df ? 0 : KOORDHIP_ST_DEVICE_FAIL);
   if (!xf || !df) t = -1;
-  raw[0] = (c.score & KOORDHIP_PLUGIN_DEVICESHARE) ? dev_score(c, d.dv, x, i, nominated) : 0;
   raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
   raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   return t;
@@ -156,8 +169,9 @@ __device__ int32_t seq_commit(const DevCfg &c, const DevNodes &d, const DevPod &
   const bool prescore = rs && nf > 1;
   const bool nominated = prescore && c.resv && resv_nominate(p, rv, mm) >= 0;
   uint32_t slots[DT] = {0u, 0u, 0u};
+  int64_t per[DT][DR];
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
-  if (dev && !dev_reserve(c, d.dv, x, w, nominated, slots, false)) return KOORDHIP_RESERVE_FAILED;
+  if (dev && !dev_reserve(c, d.dv, x, w, nominated, slots, per)) return KOORDHIP_RESERVE_FAILED;
   uint64_t m[NW] = {0, 0, 0, 0};
   if (numa_on(c) && numa_active(p, c)) {
     NumaRow r;
@@ -167,7 +181,7 @@ __device__ int32_t seq_commit(const DevCfg &c, const DevNodes &d, const DevPod &
     if (!numa_reserve<true>(d.nu.cls, r, p, m, pref)) return KOORDHIP_RESERVE_FAILED;
     store_numa_row(r, d, w);
   }
-  if (dev) (void)dev_reserve(c, d.dv, x, w, nominated, slots, true);
+  if (dev) dev_apply(d.dv, w, slots, per);
   if (c.resv) {  // Reservation Reserve: assumePod into the nominated reservation
     resv_assume(rv, p, m);
     store_resv(rv, d.rv, w);
@@ -186,164 +200,166 @@ __device__ int32_t seq_commit(const DevCfg &c, const DevNodes &d, const DevPod &
   return 0;
 }
 
+// Block-wide reduction of (sum, max, max, max) and a u64 max over the block's
+// threads; every thread gets the result.
+__device__ __forceinline__ void seq_block_reduce(int32_t v4[4], uint64_t &key, int32_t (*s_red)[8], uint64_t *s_key,
+                                                 int t) {
+  const int lane = t & 63, wv = t >> 6;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    v4[0] += __shfl_xor(v4[0], m);
+#pragma unroll
+    for (int e = 1; e < 4; e++) v4[e] = max(v4[e], __shfl_xor(v4[e], m));
+  }
+  key = seq_wave_max(key);
+  __syncthreads();  // the previous use of s_red / s_key is finished
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; e++) s_red[wv][e] = v4[e];
+    s_key[wv] = key;
+  }
+  __syncthreads();
+  v4[0] = 0;
+  v4[1] = v4[2] = v4[3] = 0;
+  key = 0;
+#pragma unroll
+  for (int w = 0; w < SEQ_THREADS / 64; w++) {
+    v4[0] += s_red[w][0];
+#pragma unroll
+    for (int e = 1; e < 4; e++) v4[e] = max(v4[e], s_red[w][e]);
+    key = s_key[w] > key ? s_key[w] : key;
+  }
+}
+
+// Every block's granules of one phase: (sum, max, max, max) of words 0..3 and
+// the u64 max of words 4..5; false when a spin timed out (every block stops).
+template <int NG>
+__device__ __forceinline__ bool seq_gather(const uint64_t *g, uint32_t epoch, int32_t G, int32_t v4[4], uint64_t &key,
+                                           int32_t (*s_red)[8], uint64_t *s_key, int32_t *s_stop, uint32_t *tmo,
+                                           int t) {
+  v4[0] = v4[1] = v4[2] = v4[3] = 0;
+  key = 0;
+  bool ok = true;
+  for (int32_t q = t; q < G; q += SEQ_THREADS) {
+    uint32_t gv[NG];
+    ok &= sweep<NG>(g + (size_t)q * SEQ_GRAN, epoch, gv, tmo);
+    v4[0] += (int32_t)gv[0];
+#pragma unroll
+    for (int e = 1; e < 4; e++) v4[e] = max(v4[e], (int32_t)gv[e]);
+    const uint64_t kk = ((uint64_t)gv[4] << 32) | gv[5];
+    key = kk > key ? kk : key;
+  }
+  if (t == 0) *s_stop = 0;
+  __syncthreads();
+  if (!ok) *s_stop = 1;
+  seq_block_reduce(v4, key, s_red, s_key, t);
+  return *s_stop == 0;
+}
+
 __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqArgs a) {
   __shared__ int32_t s_red[SEQ_THREADS / 64][8];
+  __shared__ int32_t s_tot[SEQ_NPT][SEQ_THREADS];
+  __shared__ int32_t s_raw[SEQ_NPT][KOORDHIP_NEXT_PLUGINS][SEQ_THREADS];
   __shared__ uint64_t s_key[SEQ_THREADS / 64];
-  __shared__ int32_t s_nf, s_stop;
-  __shared__ uint64_t s_best;
-  const int t = threadIdx.x, lane = __lane_id(), wv = t >> 6;
+  __shared__ int32_t s_stop;
+  const int t = threadIdx.x;
   const int32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t ext = a.ext;
+  const int32_t zero[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
   DevPodX none{};
   for (int q = 0; q < DT; q++) none.req[q][0] = none.req[q][1] = none.req[q][2] = q == 0 ? -1 : 0;
+  const bool dbg = a.dbg != nullptr && b == 0 && t == 0;
+  uint64_t ts = dbg ? seq_stamp() : 0, acc[5] = {0, 0, 0, 0, 0};
+  auto lap = [&](int q) {
+    if (dbg) {
+      const uint64_t u = seq_stamp();
+      acc[q] += u - ts;
+      ts = u;
+    }
+  };
   for (int32_t p = 0; p < a.n_pods; p++) {
     const DevPod pod = a.pods[p];
     const DevPodX x = a.podx ? a.podx[p] : none;
     const uint32_t eA = 2u * (uint32_t)p + 1u, eB = 2u * (uint32_t)p + 2u;
     const int par = p & 1;
-    // ---- phase A: this block's nodes
-    int32_t tot[SEQ_NPT], raw[SEQ_NPT][KOORDHIP_NEXT_PLUGINS];
-    int32_t nf = 0, mx[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < SEQ_NPT; k++) {
-      tot[k] = -1;
-      raw[k][0] = raw[k][1] = raw[k][2] = 0;
+    // ---- phase A: this block's nodes (totals and raw scores kept in LDS for
+    //      phase B: registers for SEQ_NPT slices would spill).  The block also
+    //      ranks its nodes as if every normalized maximum were 0, which is
+    //      exact whenever it is (then every normalized score is the same
+    //      constant): such pods need one hand-off, not two.
+    int32_t v4[4] = {0, 0, 0, 0};  // feasible count, raw maxima
+    uint64_t key0 = 0;
+#pragma unroll 1
+    for (int k = 0; k < a.npt; k++) {
+      int32_t tk = -1, rk[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
       const int32_t i = (k * G + b) * SEQ_THREADS + t;
-      if (k < a.npt && i < d.n) {
-        tot[k] = seq_eval(c, d, pod, x, i, a.rs != 0, raw[k], nullptr);
-        if (tot[k] >= 0) {
-          nf++;
+      if (i < d.n) {
+        tk = seq_eval(c, d, pod, x, i, a.rs != 0, rk, nullptr);
+        if (tk >= 0) {
+          v4[0]++;
 #pragma unroll
-          for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) mx[e] = max(mx[e], raw[k][e]);
+          for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) v4[1 + e] = max(v4[1 + e], rk[e]);
+          const uint64_t kk = make_key(tk + ext_total(c, ext, rk, zero), i);
+          key0 = kk > key0 ? kk : key0;
         }
       }
+      s_tot[k][t] = tk;
+#pragma unroll
+      for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) s_raw[k][e][t] = rk[e];
     }
-    int32_t gmx[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
-    int32_t nf_all = -1;
-    if (ext) {
-      // block reduce: feasible count, raw maxima
-      int32_t v4[4] = {nf, mx[0], mx[1], mx[2]};
+    seq_block_reduce(v4, key0, s_red, s_key, t);
+    if (t == 0) {
+      uint64_t *g = a.ga + ((size_t)par * G + b) * SEQ_GRAN;
 #pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        v4[0] += __shfl_xor(v4[0], m);
-#pragma unroll
-        for (int e = 1; e < 4; e++) v4[e] = max(v4[e], __shfl_xor(v4[e], m));
+      for (int e = 0; e < 4; e++) put_granule(g + e, eA, (uint32_t)v4[e]);
+      put_granule(g + 4, eA, (uint32_t)(key0 >> 32));
+      put_granule(g + 5, eA, (uint32_t)key0);
+    }
+    lap(0);
+    // ---- every block's granules: the feasible count, the raw maxima and the
+    //      best key under zero maxima
+    int32_t g4[4];
+    uint64_t win;
+    if (!seq_gather<6>(a.ga + (size_t)par * G * SEQ_GRAN, eA, G, g4, win, s_red, s_key, &s_stop, a.tmo, t)) return;
+    const int32_t nf_all = g4[0];
+    lap(1);
+    if (g4[1] | g4[2] | g4[3]) {
+      // ---- phase B: normalized totals, this block's best key
+      const int32_t gmx[KOORDHIP_NEXT_PLUGINS] = {g4[1], g4[2], g4[3]};
+      uint64_t best = 0;
+#pragma unroll 1
+      for (int k = 0; k < a.npt; k++) {
+        const int32_t tk = s_tot[k][t];
+        if (tk < 0) continue;
+        const int32_t i = (k * G + b) * SEQ_THREADS + t;
+        const int32_t rk[KOORDHIP_NEXT_PLUGINS] = {s_raw[k][0][t], s_raw[k][1][t], s_raw[k][2][t]};
+        const uint64_t key = make_key(tk + ext_total(c, ext, rk, gmx), i);
+        best = key > best ? key : best;
       }
-      if (lane == 0)
-        for (int e = 0; e < 4; e++) s_red[wv][e] = v4[e];
-      __syncthreads();
+      int32_t u4[4] = {0, 0, 0, 0};
+      seq_block_reduce(u4, best, s_red, s_key, t);
       if (t == 0) {
-        int32_t r4[4] = {0, 0, 0, 0};
-        for (int w = 0; w < SEQ_THREADS / 64; w++) {
-          r4[0] += s_red[w][0];
-          for (int e = 1; e < 4; e++) r4[e] = max(r4[e], s_red[w][e]);
-        }
-        uint64_t *g = a.ga + ((size_t)par * G + b) * 4;
-        for (int e = 0; e < 4; e++) put_granule(g + e, eA, (uint32_t)r4[e]);
-      }
-      // every block's granules: the global maxima and feasible count
-      int32_t r4[4] = {0, 0, 0, 0};
-      bool ok = true;
-      for (int32_t q = t; q < G; q += SEQ_THREADS) {
-        uint32_t gv[4];
-        ok &= sweep<4>(a.ga + ((size_t)par * G + q) * 4, eA, gv, a.tmo);
-        r4[0] += (int32_t)gv[0];
-        for (int e = 1; e < 4; e++) r4[e] = max(r4[e], (int32_t)gv[e]);
-      }
-      if (t == 0) s_stop = 0;
-      __syncthreads();
-      if (!ok) s_stop = 1;
+        uint64_t *g = a.gb + ((size_t)par * G + b) * SEQ_GRAN;
 #pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        r4[0] += __shfl_xor(r4[0], m);
-#pragma unroll
-        for (int e = 1; e < 4; e++) r4[e] = max(r4[e], __shfl_xor(r4[e], m));
+        for (int e = 0; e < 4; e++) put_granule(g + e, eB, 0u);
+        put_granule(g + 4, eB, (uint32_t)(best >> 32));
+        put_granule(g + 5, eB, (uint32_t)best);
       }
-      if (lane == 0)
-        for (int e = 0; e < 4; e++) s_red[wv][4 + e] = r4[e];
-      __syncthreads();
-      if (s_stop) return;
-      nf_all = 0;
-      for (int w = 0; w < SEQ_THREADS / 64; w++) {
-        nf_all += s_red[w][4];
-        for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) gmx[e] = max(gmx[e], s_red[w][5 + e]);
-      }
+      lap(2);
+      if (!seq_gather<6>(a.gb + (size_t)par * G * SEQ_GRAN, eB, G, u4, win, s_red, s_key, &s_stop, a.tmo, t)) return;
+      lap(3);
     }
-    // ---- phase B: normalized totals, this block's best key
-    uint64_t best = 0;
-#pragma unroll
-    for (int k = 0; k < SEQ_NPT; k++) {
-      if (tot[k] < 0) continue;
-      const int32_t i = (k * G + b) * SEQ_THREADS + t;
-      const uint64_t key = make_key(tot[k] + ext_total(c, ext, raw[k], gmx), i);
-      best = key > best ? key : best;
-    }
-    best = seq_wave_max(best);
-    int32_t nfw = nf;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) nfw += __shfl_xor(nfw, m);
-    if (lane == 0) {
-      s_key[wv] = best;
-      s_red[wv][0] = nfw;
-    }
-    __syncthreads();
-    if (t == 0) {
-      uint64_t bk = 0;
-      int32_t bn = 0;
-      for (int w = 0; w < SEQ_THREADS / 64; w++) {
-        bk = s_key[w] > bk ? s_key[w] : bk;
-        bn += s_red[w][0];
-      }
-      uint64_t *g = a.gb + ((size_t)par * G + b) * 4;
-      put_granule(g + 0, eB, (uint32_t)(bk >> 32));
-      put_granule(g + 1, eB, (uint32_t)bk);
-      put_granule(g + 2, eB, (uint32_t)bn);
-    }
-    // ---- every block's best: the winner
-    uint64_t kb = 0;
-    int32_t nb = 0;
-    bool ok = true;
-    for (int32_t q = t; q < G; q += SEQ_THREADS) {
-      uint32_t gv[3];
-      ok &= sweep<3>(a.gb + ((size_t)par * G + q) * 4, eB, gv, a.tmo);
-      const uint64_t kk = ((uint64_t)gv[0] << 32) | gv[1];
-      kb = kk > kb ? kk : kb;
-      nb += (int32_t)gv[2];
-    }
-    if (t == 0) s_stop = 0;
-    __syncthreads();
-    if (!ok) s_stop = 1;
-    kb = seq_wave_max(kb);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) nb += __shfl_xor(nb, m);
-    if (lane == 0) {
-      s_key[wv] = kb;
-      s_red[wv][1] = nb;
-    }
-    __syncthreads();
-    if (s_stop) return;
-    if (t == 0) {
-      uint64_t bk = 0;
-      int32_t nn = 0;
-      for (int w = 0; w < SEQ_THREADS / 64; w++) {
-        bk = s_key[w] > bk ? s_key[w] : bk;
-        nn += s_red[w][1];
-      }
-      s_best = bk;
-      s_nf = nn;
-    }
-    __syncthreads();
-    const uint64_t win = s_best;
+    // ---- the winner's owner block commits (its nodes are read by no other block)
     const int32_t wn = win ? key_node(win) : -1;
-    (void)nf_all;
     if (t == 0) {
       const bool mine = wn >= 0 ? ((wn / SEQ_THREADS) % G) == b : b == 0;
       if (mine) {
+        const uint64_t c0 = a.dbg ? seq_stamp() : 0;
         int32_t res = KOORDHIP_UNSCHEDULABLE;
         uint64_t cp[NW] = {0, 0, 0, 0};
         uint32_t dv[DT] = {0u, 0u, 0u};
         if (wn >= 0) {
-          const int32_t rc = seq_commit(c, d, pod, x, wn, s_nf, a.rs != 0, cp, dv);
+          const int32_t rc = seq_commit(c, d, pod, x, wn, nf_all, a.rs != 0, cp, dv);
           res = rc ? KOORDHIP_RESERVE_FAILED : wn;
           if (rc) {
             for (int q = 0; q < NW; q++) cp[q] = 0;
@@ -355,16 +371,20 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
           for (int q = 0; q < NW; q++) a.out_cpus[(size_t)p * NW + q] = cp[q];
         if (a.out_dev)
           for (int q = 0; q < DT; q++) a.out_dev[(size_t)p * DT + q] = dv[q];
+        if (a.dbg) atomicAdd((unsigned long long *)&a.dbg[5], (unsigned long long)(seq_stamp() - c0));
       }
     }
     __syncthreads();  // the owner's commit before its next evaluation of w
+    lap(4);
   }
+  if (dbg)
+    for (int q = 0; q < 5; q++) a.dbg[q] = acc[q];
 }
 
 // ---- parity evaluation (koordhip_eval_ext): per (pod, node) the status bits,
 // the raw score planes and the per-node total; then per pod the maxima and
 // the top-k of the normalized totals
-__global__ void k_seq_eval(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, const DevPodX *__restrict__ podx,
+__global__ __launch_bounds__(256) void k_seq_eval(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, const DevPodX *__restrict__ podx,
                            int32_t n_pods, int32_t rs, uint8_t *__restrict__ status, int32_t *__restrict__ scores,
                            int32_t *__restrict__ work) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
@@ -430,16 +450,17 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
 
 hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                       int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
-                      uint32_t *out_dev, int32_t rs, hipStream_t s) {
+                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   SeqArgs a{};
+  a.dbg = dbg;
   a.pods = pods;
   a.podx = podx;
   a.n_pods = n_pods;
   a.npt = (d.n + grid * SEQ_THREADS - 1) / (grid * SEQ_THREADS);
   if (a.npt > SEQ_NPT) return hipErrorInvalidValue;
   a.ga = granules;
-  a.gb = granules + (size_t)2 * grid * 4;
+  a.gb = granules + (size_t)2 * grid * SEQ_GRAN;
   a.tmo = tmo;
   a.out_node = out_node;
   a.out_cpus = out_cpus;

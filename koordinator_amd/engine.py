@@ -127,6 +127,14 @@ class PlacementEngine:
         self._staged = pods
         abi.check(self.lib, self.lib.koordhip_stage_pods(self._ctx, pods.ctypes.data, len(pods)))
 
+    def stage_pods_ext(self, pods: np.ndarray, ext: Optional[np.ndarray] = None):
+        """Stage pods with their koordhip_pod_ext records (the sequential cycle's place_staged)."""
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        x = None if ext is None else np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
+        self._staged = pods
+        abi.check(self.lib, self.lib.koordhip_stage_pods_ext(self._ctx, pods.ctypes.data,
+                                                             x.ctypes.data if x is not None else None, len(pods)))
+
     def place_staged(self):
         abi.check(self.lib, self.lib.koordhip_place_staged(self._ctx))
 
