@@ -16,8 +16,8 @@
 #include <vector>
 
 #include "../../include/koordhip.h"
-#include "dev.hpp"
 #include "kernels.h"
+#include "seq.h"
 
 namespace {
 
@@ -796,7 +796,15 @@ void shard(const koordhip_ctx *c, int32_t *lo, int32_t *hi) {
   // one-rank communicator only): evaluate shard 0 of W, as rank 0 of a
   // W-GPU job would; the placements then differ from the full table's
   if (c->comm && c->world == 1)
-    if (const char *w = std::getenv("KOORDHIP_SHARD_SIM")) *hi = (int32_t)((int64_t)c->n / std::max(1, std::atoi(w)));
+    if (const char *w = std::getenv("KOORDHIP_SHARD_SIM")) {
+      static bool warned = false;  // a diagnostic: say so, placements are not the full table's
+      if (!warned) {
+        std::fprintf(stderr, "[koordhip] KOORDHIP_SHARD_SIM=%s: evaluating shard 0 only (timing diagnostic; "
+                             "placements differ from the full table's)\n", w);
+        warned = true;
+      }
+      *hi = (int32_t)((int64_t)c->n / std::max(1, std::atoi(w)));
+    }
 }
 
 }  // namespace
@@ -1900,8 +1908,8 @@ int seq_place(koordhip_ctx *c) {
   c->last_evals = (int64_t)np * c->n;
   c->last_launches = 1;
   c->ev_used = 0;
-  c->eval_kernel = "kh::k_seq";
-  c->resolve_kernel = "kh::k_seq";
+  c->eval_kernel = kh::seq_kernel_name(c->dc);
+  c->resolve_kernel = c->eval_kernel;
   c->pipe_check = true;
   return 0;
 }

@@ -5,10 +5,6 @@
 #include "eval.hpp"
 
 namespace kh {
-struct DevPodX;  // dev.hpp (seq.hip, api.hip)
-}
-
-namespace kh {
 
 // LoadAware Filter inputs (device copies of koordhip_node_soa.laf_* / la_flags).
 struct PrepIn {
@@ -93,19 +89,6 @@ int side_mode(const DevCfg &c);
 const char *last_eval_kernel();
 const char *last_resolve_kernel();
 
-// seq.hip: the exact sequential cycle (normalized-score profiles).  grid =
-// resident blocks (one per CU); granules: 4 x 2 x grid x 4 u64 (zeroed before
-// the first launch of a call), tmo: one u32 (zeroed).  rs: the Reservation
-// plugin scores.
-hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
-                      int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
-                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, hipStream_t s);
-// parity: status bits (ORed into status: k_eval_full writes them first), the
-// normalized plugins' raw planes of scores ([np][NPLUGINS + NEXT][n]), and
-// the top-k of the normalized totals per pod; work: [np][4][n] int32
-hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
-                           int32_t rs, uint8_t *status, int32_t *scores, int32_t *work, int32_t k, uint64_t *topk,
-                           hipStream_t s);
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, int nm, int32_t lag);
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
                           int32_t r_begin, int32_t r_end, const uint64_t *lists0, int64_t list_buf, int32_t monotone,

@@ -1,0 +1,27 @@
+// seq.h -- launch wrappers of seq.hip (host side; api.hip and seq.hip only,
+// so DeviceShare changes do not rebuild kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dev.hpp"
+#include "kernels.h"
+
+namespace kh {
+
+// The exact sequential cycle (normalized-score profiles).  grid = resident
+// blocks (one per CU); granules: 2 phases x 2 parities x grid x 8 u64 (zeroed
+// before the first launch of a call), tmo: one u32 (zeroed).  rs: the
+// Reservation plugin scores.  dbg: KOORDHIP_STAMPS counters (NULL: off).
+hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
+                      int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
+                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, hipStream_t s);
+// parity: status bits (ORed into status: k_eval_full writes them first), the
+// normalized plugins' raw planes of scores ([np][NPLUGINS + NEXT][n]), and
+// the top-k of the normalized totals per pod; work: [np][4][n] int32
+hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
+                           int32_t rs, uint8_t *status, int32_t *scores, int32_t *work, int32_t k, uint64_t *topk,
+                           hipStream_t s);
+// the k_seq instantiation launch_seq runs for this config, as rocprofv3 names it
+const char *seq_kernel_name(const DevCfg &c);
+
+}  // namespace kh

@@ -32,8 +32,10 @@
 // phase, which every block writes after it finished reading parity q.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dev.hpp"
-#include "kernels.h"
+#include "seq.h"
 
 namespace kh {
 
@@ -77,27 +79,38 @@ __device__ __forceinline__ uint32_t ext_bits(const DevCfg &c) {
          ((c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? 4u : 0u);
 }
 
+// SM: the compiled side-row mode -- 0 none (Fit / LoadAware / static /
+// balanced), 1 + NodeNUMAResource (with the zone code), 2 + Reservation (the
+// several-slot rows, with NUMA when enabled).  The plain build keeps no side
+// row at all: a zero-initialised ~0.5 KB row per lane would live in scratch.
+__host__ __device__ constexpr int seq_mode(const DevCfg &c) {
+  return c.resv ? 2 : (((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) ? 1 : 0);
+}
+
 // One node for one pod: the total of the per-node plugins (-1: some Filter
 // fails; with the Reservation plugin the ranking total of resv.hpp) and the
 // raw normalized scores.  Every column is read (the parity evaluator's rows,
 // like k_eval_full).  Inlined once per kernel: a call keeps its frame (the
 // config and column descriptors, the NV row) in scratch, kilobytes per lane.
+template <int SM>
 __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x,
                                             int32_t i, bool rs, int32_t raw[KOORDHIP_NEXT_PLUGINS],
                                             uint8_t *status) {
   NV v{};
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
-  NumaRowR4 nr{};
-  load_numa<true>(nr, d, i, all);
   int32_t t;
   bool nominated = false;
-  if (c.resv) {
+  if constexpr (SM == 2) {
+    NumaRowR4 nr{};
+    load_numa<true>(nr, d, i, all);
     load_resv(nr, d.rv, i);
     t = c.resv_cpus ? eval_total_resv<KOORDHIP_RESV_SLOTS, true>(p, v, nr, d.nu.cls, c)
                     : eval_total_resv<KOORDHIP_RESV_SLOTS, false>(p, v, nr, d.nu.cls, c);
     if (rs && (x.flags & KOORDHIP_PODX_DEVICE)) nominated = resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
-  } else if (numa_on(c)) {
+  } else if constexpr (SM == 1) {
+    NumaRow nr{};
+    load_numa<true>(nr, d, i, all);
     t = eval_total_numa<true>(p, v, nr, d.nu.cls, c);
   } else {
     t = eval_total(p, v, c);
@@ -158,31 +171,36 @@ __device__ __forceinline__ bool sweep(const uint64_t *g, uint32_t epoch, uint32_
 // DeviceShare and the extended scalars); rc: 0, or KOORDHIP_RESERVE_FAILED
 // (nothing committed).  nf: the feasible node count (one: no PreScore, so no
 // reservation is nominated before the NodeNUMAResource / DeviceShare Reserve).
-__device__ int32_t seq_commit(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x, int32_t w,
-                              int32_t nf, bool rs, uint64_t *cpus_out, uint32_t *dev_out) {
-  NumaRowR4 rv{};
+template <int SM>
+__device__ __forceinline__ int32_t seq_commit(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x,
+                                           int32_t w, int32_t nf, bool rs, uint64_t *cpus_out, uint32_t *dev_out) {
+  using RV = typename std::conditional<SM == 2, NumaRowR4, NumaRow>::type;
+  RV rv;
   uint32_t mm = 0u;
-  if (c.resv) {
+  if constexpr (SM == 2) {
     load_resv(rv, d.rv, w);
     mm = resv_matched(rv, p);
   }
   const bool prescore = rs && nf > 1;
-  const bool nominated = prescore && c.resv && resv_nominate(p, rv, mm) >= 0;
+  bool nominated = false;
+  if constexpr (SM == 2) nominated = prescore && resv_nominate(p, rv, mm) >= 0;
   uint32_t slots[DT] = {0u, 0u, 0u};
   int64_t per[DT][DR];
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
   if (dev && !dev_reserve(c, d.dv, x, w, nominated, slots, per)) return KOORDHIP_RESERVE_FAILED;
   uint64_t m[NW] = {0, 0, 0, 0};
-  if (numa_on(c) && numa_active(p, c)) {
-    NumaRow r;
-    load_numa_row(r, d, w);
-    uint64_t pref[NW];
-    resv_pref_cpus(rv, p, (c.resv && prescore) ? mm : 0u, pref);
-    if (!numa_reserve<true>(d.nu.cls, r, p, m, pref)) return KOORDHIP_RESERVE_FAILED;
-    store_numa_row(r, d, w);
+  if constexpr (SM >= 1) {
+    if (numa_on(c) && numa_active(p, c)) {
+      NumaRow r;
+      load_numa_row(r, d, w);
+      uint64_t pref[NW] = {0, 0, 0, 0};
+      if constexpr (SM == 2) resv_pref_cpus(rv, p, prescore ? mm : 0u, pref);
+      if (!numa_reserve<true>(d.nu.cls, r, p, m, pref)) return KOORDHIP_RESERVE_FAILED;
+      store_numa_row(r, d, w);
+    }
   }
   if (dev) dev_apply(d.dv, w, slots, per);
-  if (c.resv) {  // Reservation Reserve: assumePod into the nominated reservation
+  if constexpr (SM == 2) {  // Reservation Reserve: assumePod into the nominated reservation
     resv_assume(rv, p, m);
     store_resv(rv, d.rv, w);
   }
@@ -256,6 +274,7 @@ __device__ __forceinline__ bool seq_gather(const uint64_t *g, uint32_t epoch, in
   return *s_stop == 0;
 }
 
+template <int SM>
 __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqArgs a) {
   __shared__ int32_t s_red[SEQ_THREADS / 64][8];
   __shared__ int32_t s_tot[SEQ_NPT][SEQ_THREADS];
@@ -294,7 +313,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
       int32_t tk = -1, rk[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
       const int32_t i = (k * G + b) * SEQ_THREADS + t;
       if (i < d.n) {
-        tk = seq_eval(c, d, pod, x, i, a.rs != 0, rk, nullptr);
+        tk = seq_eval<SM>(c, d, pod, x, i, a.rs != 0, rk, nullptr);
         if (tk >= 0) {
           v4[0]++;
 #pragma unroll
@@ -359,7 +378,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
         uint64_t cp[NW] = {0, 0, 0, 0};
         uint32_t dv[DT] = {0u, 0u, 0u};
         if (wn >= 0) {
-          const int32_t rc = seq_commit(c, d, pod, x, wn, nf_all, a.rs != 0, cp, dv);
+          const int32_t rc = seq_commit<SM>(c, d, pod, x, wn, nf_all, a.rs != 0, cp, dv);
           res = rc ? KOORDHIP_RESERVE_FAILED : wn;
           if (rc) {
             for (int q = 0; q < NW; q++) cp[q] = 0;
@@ -384,6 +403,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
 // ---- parity evaluation (koordhip_eval_ext): per (pod, node) the status bits,
 // the raw score planes and the per-node total; then per pod the maxima and
 // the top-k of the normalized totals
+template <int SM>
 __global__ __launch_bounds__(256) void k_seq_eval(DevCfg c, DevNodes d, const DevPod *__restrict__ pods, const DevPodX *__restrict__ podx,
                            int32_t n_pods, int32_t rs, uint8_t *__restrict__ status, int32_t *__restrict__ scores,
                            int32_t *__restrict__ work) {
@@ -398,7 +418,7 @@ __global__ __launch_bounds__(256) void k_seq_eval(DevCfg c, DevNodes d, const De
   }
   int32_t raw[KOORDHIP_NEXT_PLUGINS];
   uint8_t st = 0;
-  const int32_t t = seq_eval(c, d, pod, x, i, rs != 0, raw, &st);
+  const int32_t t = seq_eval<SM>(c, d, pod, x, i, rs != 0, raw, &st);
   const size_t n = (size_t)d.n;
   int32_t *wk = work + (size_t)p * 4 * n;
   wk[i] = t;
@@ -475,15 +495,26 @@ hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, co
   void *args[] = {&cc, &dd, &a};
   // every block must be resident (blocks read each other's granules): the
   // cooperative launch checks the grid against the occupancy
-  return hipLaunchCooperativeKernel((const void *)k_seq, dim3(grid), dim3(SEQ_THREADS), args, 0, s);
+  const int sm = seq_mode(c);
+  const void *f = sm == 2 ? (const void *)k_seq<2> : sm == 1 ? (const void *)k_seq<1> : (const void *)k_seq<0>;
+  return hipLaunchCooperativeKernel(f, dim3(grid), dim3(SEQ_THREADS), args, 0, s);
+}
+
+const char *seq_kernel_name(const DevCfg &c) {
+  static const char *names[3] = {"kh::k_seq<0>", "kh::k_seq<1>", "kh::k_seq<2>"};
+  return names[seq_mode(c)];
 }
 
 hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                            int32_t rs, uint8_t *status, int32_t *scores, int32_t *work, int32_t k, uint64_t *topk,
                            hipStream_t s) {
   if (n_pods <= 0 || d.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_seq_eval, dim3((d.n + 255) / 256, n_pods), dim3(256), 0, s, c, d, pods, podx, n_pods, rs,
-                     status, scores, work);
+  const dim3 g((d.n + 255) / 256, n_pods);
+  switch (seq_mode(c)) {
+    case 2: hipLaunchKernelGGL(k_seq_eval<2>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work); break;
+    case 1: hipLaunchKernelGGL(k_seq_eval<1>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work); break;
+    default: hipLaunchKernelGGL(k_seq_eval<0>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work);
+  }
   if (topk && k > 0) hipLaunchKernelGGL(k_seq_topk, dim3(n_pods), dim3(256), 0, s, c, d.n, work, k, topk);
   return hipGetLastError();
 }
