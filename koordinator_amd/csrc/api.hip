@@ -182,7 +182,8 @@ struct koordhip_ctx {
   int32_t podx_cap = 0;
   bool podx_staged = false;
   uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
-  uint64_t *d_seqg = nullptr;      // granules + timeout word of k_seq
+  uint64_t *d_seqg = nullptr;
+  void *d_seqdesc = nullptr;  // the sequential cycle's device copies of dc / d      // granules + timeout word of k_seq
   int32_t seq_grid = 0;
   int64_t last_launches = 0, last_evals = 0;
 };
@@ -1019,7 +1020,7 @@ int koordhip_destroy(koordhip_ctx *c) {
                   (void *)c->d_selpart[0], (void *)c->d_selcnt[0], (void *)c->d_selpart[1], (void *)c->d_selcnt[1],
                   (void *)c->d_etk_part[0], (void *)c->d_etk_part[1], (void *)c->d_etk_pcnt[0],
                   (void *)c->d_etk_pcnt[1], (void *)c->d_etk_sync[0], (void *)c->d_etk_sync[1], c->d_upd,
-                  (void *)c->d_podx, (void *)c->d_devout, (void *)c->d_seqg})
+                  (void *)c->d_podx, (void *)c->d_devout, (void *)c->d_seqg, c->d_seqdesc})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -1890,9 +1891,10 @@ int seq_place(koordhip_ctx *c) {
     HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 64 * sizeof(uint64_t), c->stream));
   }
   HIP_TRY(hipEventRecord(c->t0, c->stream));
+  if (!c->d_seqdesc) HIP_TRY(hipMalloc(&c->d_seqdesc, kh::seq_desc_bytes()));
   HIP_TRY(kh::launch_seq(c->dc, c->d, c->d_pods, c->podx_staged ? c->d_podx : nullptr, np, G, c->d_seqg, tmo,
                          c->d_out, c->d_cpus, dev ? c->d_devout : nullptr, rs, stamps ? c->d_dbg : nullptr,
-                         c->stream));
+                         c->d_seqdesc, c->stream));
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   if (stamps) {
     uint64_t h[6];

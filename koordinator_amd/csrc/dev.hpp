@@ -152,6 +152,7 @@ __device__ __forceinline__ bool dev_eval(const DevCfg &c, const DevDev &dv, cons
   if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i)) return true;
   bool ok = true;
   int64_t sum = 0;
+#pragma unroll 1
   for (int t = 0; t < DT; t++) {
     int64_t q[DR];
     if (!dev_requests(x, t, q)) continue;

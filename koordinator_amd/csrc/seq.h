@@ -12,9 +12,15 @@ namespace kh {
 // blocks (one per CU); granules: 2 phases x 2 parities x grid x 8 u64 (zeroed
 // before the first launch of a call), tmo: one u32 (zeroed).  rs: the
 // Reservation plugin scores.  dbg: KOORDHIP_STAMPS counters (NULL: off).
+// The host structs c and d must stay unchanged until the launch's copies of
+// them ran (they are the context's own).
 hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                       int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
-                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, hipStream_t s);
+                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, void *desc, hipStream_t s);
+// desc: a device buffer of seq_desc_bytes() the launch copies the config and
+// the column descriptors into (the commit reads them from there)
+constexpr size_t seq_desc_cfg_bytes() { return (sizeof(DevCfg) + 15) & ~(size_t)15; }
+constexpr size_t seq_desc_bytes() { return seq_desc_cfg_bytes() + sizeof(DevNodes); }
 // parity: status bits (ORed into status: k_eval_full writes them first), the
 // normalized plugins' raw planes of scores ([np][NPLUGINS + NEXT][n]), and
 // the top-k of the normalized totals per pod; work: [np][4][n] int32

@@ -57,6 +57,8 @@ struct SeqArgs {
   uint32_t ext;         // bit e: normalized plugin e scores (DeviceShare, NodeAffinity, TaintToleration)
   int32_t rs;           // the Reservation plugin scores (its PreScore nominates)
   uint64_t *dbg;        // KOORDHIP_STAMPS: block 0's per-phase cycle sums [0..4], owner commits [5] (NULL: off)
+  const DevCfg *gc;     // global copies of the kernel's config and column descriptors (the commit's)
+  const DevNodes *gd;
 };
 
 __device__ __forceinline__ uint64_t seq_stamp() {
@@ -172,8 +174,9 @@ __device__ __forceinline__ bool sweep(const uint64_t *g, uint32_t epoch, uint32_
 // (nothing committed).  nf: the feasible node count (one: no PreScore, so no
 // reservation is nominated before the NodeNUMAResource / DeviceShare Reserve).
 template <int SM>
-__device__ __forceinline__ int32_t seq_commit(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x,
-                                           int32_t w, int32_t nf, bool rs, uint64_t *cpus_out, uint32_t *dev_out) {
+__device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNodes &d, const DevPod &p,
+                                                   const DevPodX &x, int32_t w, int32_t nf, bool rs,
+                                                   uint64_t *cpus_out, uint32_t *dev_out) {
   using RV = typename std::conditional<SM == 2, NumaRowR4, NumaRow>::type;
   RV rv;
   uint32_t mm = 0u;
@@ -216,6 +219,37 @@ __device__ __forceinline__ int32_t seq_commit(const DevCfg &c, const DevNodes &d
   if (dev_out)
     for (int t = 0; t < DT; t++) dev_out[t] = slots[t];
   return 0;
+}
+
+// The owner's commit of pod p (out_node / out_cpus / out_dev written here).
+// Not inlined: one lane per pod runs it, and inlined its Reserve code (the
+// device choice, the cpuset replay) would push the per-pod loop out of the
+// instruction cache.  The config, the column descriptors and the pod come
+// through global pointers (reference arguments to kernel parameters make the
+// caller copy them into scratch).
+template <int SM>
+__device__ __noinline__ void seq_commit(const DevCfg *cp, const DevNodes *dp, const DevPod *pp, const DevPodX *px,
+                                        int32_t w, int32_t nf, bool rs, int32_t *out_node, uint64_t *out_cpus,
+                                        uint32_t *out_dev) {
+  DevPodX none{};
+  none.req[0][0] = none.req[0][1] = none.req[0][2] = -1;
+  const DevPodX &x = px ? *px : none;
+  uint64_t cpus[NW] = {0, 0, 0, 0};
+  uint32_t dv[DT] = {0u, 0u, 0u};
+  int32_t res = KOORDHIP_UNSCHEDULABLE;
+  if (w >= 0) {
+    const int32_t rc = seq_commit_body<SM>(*cp, *dp, *pp, x, w, nf, rs, cpus, dv);
+    res = rc ? KOORDHIP_RESERVE_FAILED : w;
+    if (rc) {
+      for (int q = 0; q < NW; q++) cpus[q] = 0;
+      for (int q = 0; q < DT; q++) dv[q] = 0u;
+    }
+  }
+  *out_node = res;
+  if (out_cpus)
+    for (int q = 0; q < NW; q++) out_cpus[q] = cpus[q];
+  if (out_dev)
+    for (int q = 0; q < DT; q++) out_dev[q] = dv[q];
 }
 
 // Block-wide reduction of (sum, max, max, max) and a u64 max over the block's
@@ -374,22 +408,9 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
       const bool mine = wn >= 0 ? ((wn / SEQ_THREADS) % G) == b : b == 0;
       if (mine) {
         const uint64_t c0 = a.dbg ? seq_stamp() : 0;
-        int32_t res = KOORDHIP_UNSCHEDULABLE;
-        uint64_t cp[NW] = {0, 0, 0, 0};
-        uint32_t dv[DT] = {0u, 0u, 0u};
-        if (wn >= 0) {
-          const int32_t rc = seq_commit<SM>(c, d, pod, x, wn, nf_all, a.rs != 0, cp, dv);
-          res = rc ? KOORDHIP_RESERVE_FAILED : wn;
-          if (rc) {
-            for (int q = 0; q < NW; q++) cp[q] = 0;
-            for (int q = 0; q < DT; q++) dv[q] = 0u;
-          }
-        }
-        a.out_node[p] = res;
-        if (a.out_cpus)
-          for (int q = 0; q < NW; q++) a.out_cpus[(size_t)p * NW + q] = cp[q];
-        if (a.out_dev)
-          for (int q = 0; q < DT; q++) a.out_dev[(size_t)p * DT + q] = dv[q];
+        seq_commit<SM>(a.gc, a.gd, a.pods + p, a.podx ? a.podx + p : nullptr, wn, nf_all, a.rs != 0, a.out_node + p,
+                       a.out_cpus ? a.out_cpus + (size_t)p * NW : nullptr,
+                       a.out_dev ? a.out_dev + (size_t)p * DT : nullptr);
         if (a.dbg) atomicAdd((unsigned long long *)&a.dbg[5], (unsigned long long)(seq_stamp() - c0));
       }
     }
@@ -470,10 +491,17 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
 
 hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                       int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
-                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, hipStream_t s) {
+                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, void *desc, hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   SeqArgs a{};
   a.dbg = dbg;
+  // the commit's copies of the config and the column descriptors (desc: 16-B aligned device buffer)
+  DevCfg *gc = static_cast<DevCfg *>(desc);
+  DevNodes *gd = reinterpret_cast<DevNodes *>(static_cast<char *>(desc) + seq_desc_cfg_bytes());
+  if (hipError_t e = hipMemcpyAsync(gc, &c, sizeof(DevCfg), hipMemcpyHostToDevice, s)) return e;
+  if (hipError_t e = hipMemcpyAsync(gd, &d, sizeof(DevNodes), hipMemcpyHostToDevice, s)) return e;
+  a.gc = gc;
+  a.gd = gd;
   a.pods = pods;
   a.podx = podx;
   a.n_pods = n_pods;

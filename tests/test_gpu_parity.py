@@ -298,3 +298,53 @@ def test_launch_modes_bit_exact(Engine, monkeypatch, mode, numa):
         got = e.place_stream(pods)
     ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods)
     assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
+
+
+# ----------------------------------------------------- bench.py --gpus N's per-rank setup
+@pytest.mark.parametrize("workload", ["config4", "config5"])
+def test_torch_nccl_group_beside_library_comm(Engine, workload):
+    """What every rank of `bench.py --gpus N` holds, on one GPU (world 1):
+    torch's nccl process group (RCCL, its own streams) beside the library's
+    communicator pair (`koordhip_comm_init` splits a second one for the second
+    evaluation stream) and its three CU-masked queues (the
+    hardware-queue budget).  The unique id travels by dist.broadcast as in
+    bench.py; placements equal the oracle's, and torch's collectives still
+    work after the persistent pipeline ran."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        resv = workload == "config5"
+        prof = shipped_profile(numa=resv, reservation=resv)
+        n, p = (3000, 3000) if resv else (4000, 6000)
+        table = synth.make_cluster(synth.ClusterSpec(n), prof)
+        if resv:
+            synth.add_numa(table, synth.NumaSpec(), prof)
+            synth.add_reservations(table, synth.ResvSpec())
+        pods = synth.make_pods(synth.StreamSpec(p, be_frac=0.3, resv_match_frac=0.2 if resv else 0.0), prof)
+        t = torch.tensor(list(Engine.comm_unique_id()), dtype=torch.uint8, device="cuda")
+        dist.broadcast(t, 0)
+        with Engine(prof, device=0) as e:
+            e.comm_init(bytes(t.cpu().tolist()), 1, 0)
+            e.load_snapshot(table)
+            e.checkpoint()
+            e.stage_pods(pods)
+            e.restore()
+            e.place_staged()
+            dist.barrier()
+            torch.cuda.synchronize()
+            e.synchronize()
+            got = e.fetch_placements(len(pods))
+        x = torch.ones(4, device="cuda")
+        dist.all_reduce(x)
+        assert x.tolist() == [1.0] * 4
+    finally:
+        dist.destroy_process_group()
+    ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods, threads=8)
+    assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
