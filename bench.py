@@ -452,7 +452,7 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
         "unschedulable": int((placements < 0).sum()),
         "device_pods_placed": int(((placements >= 0) & dev).sum()),
         "roofline": {"bound": "latency", "kernel": kn["resolve"],
-                     "limiter": "four grid-wide hand-offs per pod (not bandwidth); priced against HBM peak",
+                     "limiter": "latency: per pod one grid-wide hand-off (two for device pods) after the owner's commit and one evaluation chain (not bandwidth); priced against HBM peak",
                      "timing": "HIP events around the k_seq launch of the last timed step",
                      "achieved": round(gbs, 2) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 5) if gbs else None, "traffic": None,
