@@ -84,7 +84,16 @@ extern "C" {
 #define KOORDHIP_PLUGIN_AFFINITY_SCORE 128u  /* NodeAffinity Score: preferred terms (static_score[0]) */
 #define KOORDHIP_PLUGIN_TAINT_SCORE 256u     /* TaintToleration Score: intolerable PreferNoSchedule taints
                                                 (static_score[1], normalized reversed) */
-#define KOORDHIP_NEXT_PLUGINS 3              /* DeviceShare, NodeAffinity, TaintToleration */
+#define KOORDHIP_PLUGIN_PTS 512u             /* PodTopologySpread Filter (DoNotSchedule constraints) and Score
+                                                (ScheduleAnyway constraints, weight ext_weight[3]; its own
+                                                min-max NormalizeScore); pts_* columns, koordhip_pod_ext.pts_* */
+#define KOORDHIP_NEXT_PLUGINS 4              /* DeviceShare, NodeAffinity, TaintToleration, PodTopologySpread */
+/* PodTopologySpread envelope (k8s v1.24 podtopologyspread, not vendored): */
+#define KOORDHIP_PTS_KEYS 4      /* distinct topology keys of the snapshot's constraints */
+#define KOORDHIP_PTS_DOMAINS 64  /* values of a non-hostname key */
+#define KOORDHIP_PTS_CONS 8      /* distinct (label selector, namespace) of the snapshot's constraints */
+#define KOORDHIP_PTS_CLASSES 8   /* spread classes: (required node affinity, hard keys, soft keys) */
+#define KOORDHIP_PTS_POD 4       /* constraints per pod */
 /* NodeResourcesFit's extended scalar resources of device pods (koordinator.sh/
  * gpu-core, gpu-memory-ratio, gpu-memory, nvidia.com/gpu, ...): fitsRequest
  * checks each one the pod requests against Allocatable - Requested (upstream
@@ -202,6 +211,7 @@ typedef struct koordhip_numa_class {
 #define KOORDHIP_ST_STATIC_FAIL 16u /* NodeUnschedulable / NodeAffinity / TaintToleration */
 #define KOORDHIP_ST_DEVICE_FAIL 32u /* DeviceShare Filter (plugin.go:284-323) */
 #define KOORDHIP_ST_XFIT_FAIL 64u   /* NodeResourcesFit on an extended scalar resource (koordhip_pod_ext.xreq) */
+#define KOORDHIP_ST_PTS_FAIL 128u   /* PodTopologySpread Filter (a missing topology key, or the skew) */
 
 /* DeviceShare's device model (nodeDevice, device_cache.go:44-50): per node
  * and device type up to KOORDHIP_DEV_SLOTS minors, each with the Device CR's
@@ -244,12 +254,12 @@ typedef struct koordhip_config {
   int32_t reserved[5];
   /* ABI 9: the normalized-score plugins */
   int32_t ext_weight[KOORDHIP_NEXT_PLUGINS]; /* score weights: DeviceShare (scheduler-config.yaml:88-89: 1),
-                                               NodeAffinity, TaintToleration (1..100) */
+                                               NodeAffinity, TaintToleration, PodTopologySpread (1..100) */
   int32_t dev_most_allocated;  /* DeviceShareArgs.ScoringStrategy.Type == MostAllocated (scoring.go:125-132) */
   int32_t dev_res_weight[5];   /* DeviceShareArgs.ScoringStrategy.Resources weights (0 = not listed): gpu-core,
                                   gpu-memory-ratio, gpu-memory, rdma, fpga (defaults v1beta2/defaults.go:168-189:
                                   gpu-memory-ratio, rdma, fpga at 1) */
-  int32_t reserved2[3];
+  int32_t reserved2[2];
 } koordhip_config;
 
 /* Columnar node snapshot, all arrays of length n, little-endian, caller-owned
@@ -365,6 +375,27 @@ typedef struct koordhip_node_soa {
    * not tolerate) scores per (pod static class, node), [MAX_STATIC_CLASSES][n];
    * NULL = 0 */
   const uint16_t *static_score[2];
+  /* PodTopologySpread (KOORDHIP_PLUGIN_PTS): the topology keys of the
+   * snapshot's constraints (pts_keys <= KOORDHIP_PTS_KEYS; bit k of
+   * pts_hostname: key k is kubernetes.io/hostname, whose domain is the node
+   * itself), pts_dom [keys][n] = the node's domain for key k (0 ..
+   * pts_ndom[k] - 1 < KOORDHIP_PTS_DOMAINS; the node index for a hostname key;
+   * -1 = the node has no such label); the constraint table (pts_cons <=
+   * KOORDHIP_PTS_CONS distinct (label selector, namespace), pts_cons_key[c] =
+   * its key) with pts_cnt [cons][n] = the node's pods in that namespace the
+   * selector matches (countPodsMatchSelector; advanced by Reserve); pts_elig [n]
+   * bit 2s = the node matches spread class s's required node affinity and holds
+   * every DoNotSchedule key of the class, bit 2s + 1 = ... every ScheduleAnyway
+   * key (pts_classes <= KOORDHIP_PTS_CLASSES).  pts_keys 0: no columns. */
+  int32_t pts_keys;
+  uint32_t pts_hostname;
+  int32_t pts_ndom[KOORDHIP_PTS_KEYS];
+  int32_t pts_cons;
+  int32_t pts_classes;
+  int32_t pts_cons_key[KOORDHIP_PTS_CONS];
+  const int32_t *pts_dom;
+  const int32_t *pts_cnt;
+  const uint16_t *pts_elig;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -393,8 +424,24 @@ typedef struct koordhip_pod_ext {
   int64_t xreq[KOORDHIP_NXRES];  /* NodeResourcesFit extended scalar requests */
   uint32_t flags;                /* KOORDHIP_PODX_* */
   uint32_t xmask;                /* bit j: the pod's request map holds extended scalar j (xreq[j], even 0) */
+  /* PodTopologySpread: the pod's spec.topologySpreadConstraints in order
+   * (pts_n <= KOORDHIP_PTS_POD): pts_c[j] = its constraint table index,
+   * pts_fl[j] KOORDHIP_PTS_HARD (DoNotSchedule) / KOORDHIP_PTS_SELF (its
+   * selector matches the pod's own labels), pts_skew[j] = maxSkew; pts_class =
+   * the pod's spread class; pts_match bit c = table constraint c counts this
+   * pod once it is placed (its namespace and selector match). */
+  uint8_t pts_n;
+  uint8_t pts_class;
+  uint8_t pts_match;
+  uint8_t pts_pad;
+  uint8_t pts_c[KOORDHIP_PTS_POD];
+  uint8_t pts_fl[KOORDHIP_PTS_POD];
+  int32_t pts_skew[KOORDHIP_PTS_POD];
+  int32_t pts_reserved;
 } koordhip_pod_ext;
 #define KOORDHIP_PODX_DEVICE 1u  /* some device request (DeviceShare state.skip == false) */
+#define KOORDHIP_PTS_HARD 1u
+#define KOORDHIP_PTS_SELF 2u
 
 /* One top-k record of koordhip_eval. */
 typedef struct koordhip_topk {

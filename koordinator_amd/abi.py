@@ -18,10 +18,12 @@ NPLUGINS = 4
 PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_RESERVATION = 1, 2, 4, 8
 PLUGIN_NODE_STATIC, PLUGIN_BALANCED = 16, 32
 # normalized-score plugins (the exact sequential cycle, koordhip_place_stream_ext)
-PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE = 64, 128, 256
-NEXT_PLUGINS = 3
-EXT_PLUGIN_BITS = (PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE)
-NORMALIZED_PLUGINS = PLUGIN_DEVICESHARE | PLUGIN_AFFINITY_SCORE | PLUGIN_TAINT_SCORE
+PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE, PLUGIN_PTS = 64, 128, 256, 512
+NEXT_PLUGINS = 4
+EXT_PLUGIN_BITS = (PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE, PLUGIN_PTS)
+NORMALIZED_PLUGINS = PLUGIN_DEVICESHARE | PLUGIN_AFFINITY_SCORE | PLUGIN_TAINT_SCORE | PLUGIN_PTS
+PTS_KEYS, PTS_DOMAINS, PTS_CONS, PTS_CLASSES, PTS_POD = 4, 64, 8, 8, 4
+PTS_HARD, PTS_SELF = 1, 2
 NXRES = 8
 DEV_TYPES, DEV_SLOTS, DEV_RES = 3, 8, 3
 DEV_GPU, DEV_RDMA, DEV_FPGA = 0, 1, 2
@@ -66,7 +68,7 @@ def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> in
     return (required & 3) | ((preferred & 3) << 2) | ((exclusive & 3) << 4)
 
 ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL, ST_RESV_FAIL, ST_STATIC_FAIL = 1, 2, 4, 8, 16
-ST_DEVICE_FAIL, ST_XFIT_FAIL = 32, 64
+ST_DEVICE_FAIL, ST_XFIT_FAIL, ST_PTS_FAIL = 32, 64, 128
 UNSCHEDULABLE, RESERVE_FAILED = -1, -2
 E_INVAL, E_RESERVE = -1, -6
 UNIQUE_ID_BYTES = 128
@@ -104,10 +106,10 @@ class KoordhipConfig(C.Structure):
         ("numa_most_allocated", C.c_int32),
         ("reservation_weight", C.c_int32),
         ("reserved", C.c_int32 * 5),
-        ("ext_weight", C.c_int32 * 3),
+        ("ext_weight", C.c_int32 * NEXT_PLUGINS),
         ("dev_most_allocated", C.c_int32),
         ("dev_res_weight", C.c_int32 * 5),
-        ("reserved2", C.c_int32 * 3),
+        ("reserved2", C.c_int32 * 2),
     ]
 
 
@@ -162,6 +164,15 @@ class KoordhipNodeSoa(C.Structure):
         ("xalloc", _i64p),
         ("xrequested", _i64p),
         ("static_score", C.POINTER(C.c_uint16) * 2),
+        ("pts_keys", C.c_int32),
+        ("pts_hostname", C.c_uint32),
+        ("pts_ndom", C.c_int32 * PTS_KEYS),
+        ("pts_cons", C.c_int32),
+        ("pts_classes", C.c_int32),
+        ("pts_cons_key", C.c_int32 * PTS_CONS),
+        ("pts_dom", _i32p),
+        ("pts_cnt", _i32p),
+        ("pts_elig", C.POINTER(C.c_uint16)),
     ]
 
 
@@ -195,14 +206,22 @@ POD_DTYPE = np.dtype([
 ], align=True)
 assert POD_DTYPE.itemsize == 96
 TOPK_DTYPE = np.dtype([("node", "<i4"), ("score", "<i4")])
-# numpy twin of koordhip_pod_ext (144 bytes)
+# numpy twin of koordhip_pod_ext (176 bytes)
 POD_EXT_DTYPE = np.dtype([
     ("dev_req", "<i8", (DEV_TYPES, DEV_RES)),
     ("xreq", "<i8", (NXRES,)),
     ("flags", "<u4"),
     ("xmask", "<u4"),
+    ("pts_n", "u1"),
+    ("pts_class", "u1"),
+    ("pts_match", "u1"),
+    ("pts_pad", "u1"),
+    ("pts_c", "u1", (PTS_POD,)),
+    ("pts_fl", "u1", (PTS_POD,)),
+    ("pts_skew", "<i4", (PTS_POD,)),
+    ("pts_reserved", "<i4"),
 ], align=True)
-assert POD_EXT_DTYPE.itemsize == 144
+assert POD_EXT_DTYPE.itemsize == 176
 
 
 def pod_ext_array(n: int) -> np.ndarray:

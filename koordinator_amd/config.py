@@ -30,9 +30,10 @@ PLUGIN_TAINT_TOLERATION = "TaintToleration"
 PLUGIN_BALANCED = "NodeResourcesBalancedAllocation"
 STATIC_FILTERS = (PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
 PLUGIN_DEVICESHARE = "DeviceShare"
+PLUGIN_PTS = "PodTopologySpread"
 # Scores normalized over the pod's feasible nodes (DefaultNormalizeScore): the
 # sequential cycle; NodeAffinity / TaintToleration in `scores` are their Scores
-NORMALIZED_SCORES = (PLUGIN_DEVICESHARE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
+NORMALIZED_SCORES = (PLUGIN_DEVICESHARE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION, PLUGIN_PTS)
 
 
 class ArgsError(ValueError):
@@ -243,6 +244,18 @@ def with_normalized_scores(profile: Profile, affinity: int = 0, taint: int = 0) 
     return p
 
 
+def with_topology_spread(profile: Profile, weight: int = 2, filter: bool = True) -> Profile:
+    """The upstream PodTopologySpread plugin: Filter (DoNotSchedule constraints)
+    and Score (ScheduleAnyway; the upstream default profile weighs it 2)."""
+    p = copy.deepcopy(profile)
+    if filter and PLUGIN_PTS not in p.filters:
+        p.filters = tuple(p.filters) + (PLUGIN_PTS,)
+    if weight:
+        p.scores = dict(p.scores)
+        p.scores[PLUGIN_PTS] = weight
+    return p
+
+
 def to_c_config(profile: Profile, device: int = -1):
     """Lower a resolved profile to the koordhip_config ctypes struct."""
     from .abi import (KOORDHIP_ABI_VERSION, PLUGIN_BITS, KoordhipConfig)
@@ -256,10 +269,11 @@ def to_c_config(profile: Profile, device: int = -1):
     cfg.abi_version = KOORDHIP_ABI_VERSION
     from . import abi
     score_bits = {PLUGIN_NODE_AFFINITY: abi.PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_TOLERATION: abi.PLUGIN_TAINT_SCORE,
-                  PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE}
+                  PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE, PLUGIN_PTS: abi.PLUGIN_PTS}
+    own_filter_bits = {PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE, PLUGIN_PTS: abi.PLUGIN_PTS}
     cfg.filter_plugins = 0
     for x in p.filters:  # (the three static filters share one bit)
-        cfg.filter_plugins |= abi.PLUGIN_DEVICESHARE if x == PLUGIN_DEVICESHARE else PLUGIN_BITS[x]
+        cfg.filter_plugins |= own_filter_bits[x] if x in own_filter_bits else PLUGIN_BITS[x]
     cfg.score_plugins = 0
     for x in p.scores:
         cfg.score_plugins |= score_bits[x] if x in score_bits else PLUGIN_BITS[x]

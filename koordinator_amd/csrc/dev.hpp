@@ -26,6 +26,11 @@ struct DevPodX {
   int64_t xreq[KOORDHIP_NXRES];
   uint32_t flags;
   uint32_t xmask;
+  uint8_t pts_n, pts_class, pts_match, pts_pad;
+  uint8_t pts_c[KOORDHIP_PTS_POD];
+  uint8_t pts_fl[KOORDHIP_PTS_POD];
+  int32_t pts_skew[KOORDHIP_PTS_POD];
+  int32_t pts_reserved;
 };
 static_assert(sizeof(DevPodX) == sizeof(koordhip_pod_ext), "DevPodX mirrors koordhip_pod_ext");
 

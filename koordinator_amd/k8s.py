@@ -172,6 +172,8 @@ class Pod:
     tolerations: list = field(default_factory=list)
     # spec.affinity.nodeAffinity.preferredDuringScheduling...: [(weight, NodeSelectorTerm)]
     preferred_node_affinity: list = field(default_factory=list)
+    # spec.topologySpreadConstraints (topologyspread.TopologySpreadConstraint)
+    topology_spread_constraints: list = field(default_factory=list)
 
     @property
     def key(self) -> str:

@@ -197,8 +197,9 @@ def static_keyed(profile: Profile) -> bool:
 def sequential_profile(profile: Profile) -> bool:
     """DeviceShare or a normalized Score: the engine runs the sequential cycle
     and the snapshot carries the ABI 9 columns (NodeTable.enable_ext)."""
-    from .config import NORMALIZED_SCORES, PLUGIN_DEVICESHARE
-    return PLUGIN_DEVICESHARE in profile.filters or any(x in profile.scores for x in NORMALIZED_SCORES)
+    from .config import NORMALIZED_SCORES, PLUGIN_DEVICESHARE, PLUGIN_PTS
+    return (PLUGIN_DEVICESHARE in profile.filters or PLUGIN_PTS in profile.filters
+            or any(x in profile.scores for x in NORMALIZED_SCORES))
 
 
 def static_class_of(pod: k8s.Pod, profile: Profile, static_classes) -> int:

@@ -45,6 +45,23 @@ RESV_MUTABLE = ["resv_allocated0", "resv_allocated1", "resv_assigned"] + RESV_CP
 # every one is row-major per node here (as_soa transposes to the ABI's layouts).
 EXT_COLS = ["dev_present", "dev_minor", "dev_total", "dev_used", "xalloc", "xrequested", "static_score"]
 EXT_MUTABLE = ["dev_used", "xrequested"]
+# PodTopologySpread (sequential cycle): per node its domain per topology key
+# [n][PTS_KEYS] i32 (-1: no label), matching pods per constraint [n][PTS_CONS]
+# i32 (mutable), spread-class eligibility bits u16.  Present after enable_pts().
+PTS_COLS = ["pts_dom", "pts_cnt", "pts_elig"]
+PTS_MUTABLE = ["pts_cnt"]
+
+
+@dataclass
+class PtsMeta:
+    """koordhip_node_soa's PodTopologySpread scalars: the keys (bit k of hostname:
+    kubernetes.io/hostname), domains per key, the constraint table's keys, the
+    spread classes."""
+    keys: int = 0
+    hostname: int = 0
+    ndom: List[int] = field(default_factory=lambda: [0] * abi.PTS_KEYS)
+    cons_key: List[int] = field(default_factory=list)
+    classes: int = 0
 
 
 def slot_col(col: str, s: int) -> str:
@@ -83,6 +100,26 @@ class NodeTable:
     resv_slots: int = 1
     # DeviceShare minors per type per node held by the dev_* columns (0: none)
     dev_slots: int = 0
+    # PodTopologySpread tables (None: no pts_* columns)
+    pts: "PtsMeta" = None
+
+    @property
+    def has_pts(self) -> bool:
+        return self.pts is not None
+
+    def enable_pts(self, meta: "PtsMeta"):
+        """Add the PodTopologySpread columns (every node: no label, no pods, no class)."""
+        if not (0 < meta.keys <= abi.PTS_KEYS and len(meta.cons_key) <= abi.PTS_CONS
+                and meta.classes <= abi.PTS_CLASSES):
+            raise ValueError("PodTopologySpread tables outside the engine's envelope")
+        for k in range(meta.keys):
+            if not (meta.hostname >> k) & 1 and not 0 < meta.ndom[k] <= abi.PTS_DOMAINS:
+                raise ValueError(f"topology key {k}: 1..{abi.PTS_DOMAINS} domains")
+        self.pts = meta
+        self.cols["pts_dom"] = np.full((self.n, abi.PTS_KEYS), -1, np.int32)
+        self.cols["pts_cnt"] = np.zeros((self.n, abi.PTS_CONS), np.int32)
+        self.cols["pts_elig"] = np.zeros(self.n, np.uint16)
+        return self
 
     @property
     def has_ext(self) -> bool:
@@ -122,7 +159,7 @@ class NodeTable:
 
     def col_names(self) -> List[str]:
         return (ALL_COLS + [slot_col(c, s) for s in range(1, self.resv_slots) for c in RESV_COLS]
-                + (EXT_COLS if self.has_ext else []))
+                + (EXT_COLS if self.has_ext else []) + (PTS_COLS if self.has_pts else []))
 
     @classmethod
     def empty(cls, n: int) -> "NodeTable":
@@ -147,6 +184,7 @@ class NodeTable:
         t.numa_classes = self.numa_classes
         t.resv_slots = self.resv_slots
         t.dev_slots = self.dev_slots
+        t.pts = self.pts
         return t
 
     def copy(self) -> "NodeTable":
@@ -156,6 +194,7 @@ class NodeTable:
         t.numa_classes = self.numa_classes.copy()
         t.resv_slots = self.resv_slots
         t.dev_slots = self.dev_slots
+        t.pts = self.pts
         return t
 
     def as_soa(self) -> abi.KoordhipNodeSoa:
@@ -237,6 +276,23 @@ class NodeTable:
                     keep[f"ss{w}"] = np.ascontiguousarray(ss[:, w].T)      # [MAX_STATIC_CLASSES][n]
                     s.static_score[w] = keep[f"ss{w}"].ctypes.data_as(C.POINTER(C.c_uint16))
             s._keep_ext = keep
+        if self.has_pts:
+            m = self.pts
+            kp = {"dom": np.ascontiguousarray(self.cols["pts_dom"][:, :m.keys].T),          # [keys][n]
+                  "cnt": np.ascontiguousarray(self.cols["pts_cnt"][:, :max(1, len(m.cons_key))].T),  # [cons][n]
+                  "elig": np.ascontiguousarray(self.cols["pts_elig"])}
+            s.pts_keys = m.keys
+            s.pts_hostname = m.hostname
+            for k in range(abi.PTS_KEYS):
+                s.pts_ndom[k] = m.ndom[k] if k < m.keys else 0
+            s.pts_cons = len(m.cons_key)
+            s.pts_classes = m.classes
+            for c in range(abi.PTS_CONS):
+                s.pts_cons_key[c] = m.cons_key[c] if c < len(m.cons_key) else 0
+            s.pts_dom = kp["dom"].ctypes.data_as(C.POINTER(C.c_int32))
+            s.pts_cnt = kp["cnt"].ctypes.data_as(C.POINTER(C.c_int32))
+            s.pts_elig = kp["elig"].ctypes.data_as(C.POINTER(C.c_uint16))
+            s._keep_pts = kp
         return s
 
     def nbytes(self) -> int:

@@ -694,6 +694,80 @@ def make_device_ext(n: int, spec: DevStreamSpec) -> np.ndarray:
     return ext
 
 
+@dataclass
+class SpreadSpec:
+    """PodTopologySpread: zone / rack / hostname keys (a few nodes without a zone
+    or rack label), three apps with running pods, and pods of five spread
+    classes (hard zone; soft zone + hostname; hard hostname + soft rack; rack
+    affinity-restricted hard + soft zone; hard zone + hostname)."""
+    zones: int = 6
+    racks: int = 24
+    no_zone_frac: float = 0.03
+    no_rack_frac: float = 0.05
+    running_frac: float = 0.4     # nodes holding running pods of an app
+    pod_frac: float = 0.6         # pods with constraints
+    seed: int = SEED
+
+
+# the constraint table: (app, key) -- keys 0 zone, 1 rack, 2 hostname
+SPREAD_CONS = [(0, 0), (1, 0), (2, 0), (0, 1), (1, 1), (2, 1), (0, 2), (1, 2)]
+# per class: (hard key mask, soft key mask, [(key, hard, max_skew)])
+SPREAD_CLASSES = [
+    (0b001, 0b000, [(0, True, 1)]),
+    (0b000, 0b101, [(0, False, 1), (2, False, 2)]),
+    (0b100, 0b010, [(2, True, 2), (1, False, 1)]),
+    (0b010, 0b001, [(1, True, 3), (0, False, 2)]),
+    (0b101, 0b000, [(0, True, 2), (2, True, 1)]),
+]
+
+
+def add_spread(t: NodeTable, ext: np.ndarray, spec: SpreadSpec) -> NodeTable:
+    """The pts_* columns of a synthetic cluster and the pts_* fields of the
+    pods' koordhip_pod_ext records (class 3's required affinity: the nodes of
+    even zones)."""
+    from .snapshot import PtsMeta
+    n, sd = t.n, spec.seed + 13
+    t.enable_pts(PtsMeta(keys=3, hostname=0b100, ndom=[spec.zones, spec.racks, 0, 0],
+                         cons_key=[k for _, k in SPREAD_CONS], classes=len(SPREAD_CLASSES)))
+    zone = (splitmix64(sd, n, 1) % np.uint64(spec.zones)).astype(np.int32)
+    rack = (splitmix64(sd, n, 2) % np.uint64(spec.racks)).astype(np.int32)
+    zone[uniform(sd, n, 3) < spec.no_zone_frac] = -1
+    rack[uniform(sd, n, 4) < spec.no_rack_frac] = -1
+    dom = t["pts_dom"]
+    dom[:, 0], dom[:, 1], dom[:, 2] = zone, rack, np.arange(n, dtype=np.int32)
+    running = np.zeros((n, 3), np.int32)
+    for a in range(3):
+        on = uniform(sd, n, 10 + a) < spec.running_frac
+        running[:, a] = np.where(on, (splitmix64(sd, n, 20 + a) % np.uint64(4)).astype(np.int32) + 1, 0)
+    for c, (a, _) in enumerate(SPREAD_CONS):
+        t["pts_cnt"][:, c] = running[:, a]
+    has = lambda mask: np.all([dom[:, k] >= 0 for k in range(3) if (mask >> k) & 1] or [np.ones(n, bool)], axis=0)
+    elig = np.zeros(n, np.uint16)
+    for s_, (hard, soft, _) in enumerate(SPREAD_CLASSES):
+        aff = (zone >= 0) & (zone % 2 == 0) if s_ == 3 else np.ones(n, bool)
+        elig |= np.where(aff & has(hard), 1 << (2 * s_), 0).astype(np.uint16)
+        elig |= np.where(aff & has(soft), 1 << (2 * s_ + 1), 0).astype(np.uint16)
+    t["pts_elig"][:] = elig
+    m = len(ext)
+    sp = spec.seed + 17
+    on = uniform(sp, m, 1) < spec.pod_frac
+    app = (splitmix64(sp, m, 2) % np.uint64(3)).astype(np.int64)
+    cls = (splitmix64(sp, m, 3) % np.uint64(len(SPREAD_CLASSES))).astype(np.int64)
+    cls = np.where(app == 2, np.where(cls % 2 == 0, 0, 3), cls)   # app 2 has no hostname constraint
+    for j in np.flatnonzero(on):
+        a, s_ = int(app[j]), int(cls[j])
+        x = ext[j]
+        items = SPREAD_CLASSES[s_][2]
+        x["pts_n"] = len(items)
+        x["pts_class"] = s_
+        x["pts_match"] = sum(1 << c for c, (ca, _) in enumerate(SPREAD_CONS) if ca == a)
+        for q, (k, hard, skew) in enumerate(items):
+            x["pts_c"][q] = SPREAD_CONS.index((a, k))
+            x["pts_fl"][q] = (abi.PTS_HARD if hard else 0) | abi.PTS_SELF
+            x["pts_skew"][q] = skew
+    return t
+
+
 # Benchmark / parity configurations (BASELINE.json "configs")
 CONFIGS = {
     1: dict(nodes=500, pods=1000, be_frac=0.0),

@@ -46,6 +46,7 @@ class OrcState(C.Structure):
         ("dev_used", C.POINTER(C.c_int64)),
         ("xrequested", C.POINTER(C.c_int64)),
         ("dev_out", C.c_void_p),
+        ("pts_cnt", C.POINTER(C.c_int32)),
     ]
 
 
@@ -186,6 +187,13 @@ class Oracle:
               if self.table.dev_slots else np.zeros((n, abi.DEV_TYPES, S, abi.DEV_RES), np.int64))
         xr = np.ctypeslib.as_array(self.st.xrequested, shape=(abi.NXRES, n)).T.copy()
         return {"dev_used": du, "xrequested": xr}
+
+    def pts_counts(self) -> np.ndarray:
+        """PodTopologySpread matching pods per node and table constraint [n][cons]."""
+        m = self.table.pts
+        if m is None or not m.cons_key:
+            return np.zeros((self.n, 0), np.int32)
+        return np.ctypeslib.as_array(self.st.pts_cnt, shape=(len(m.cons_key), self.n)).T.copy()
 
     def dev_filter(self, ext_rec, node: int) -> bool:
         x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)

@@ -68,7 +68,31 @@ typedef struct orc_state {
   int64_t *dev_used;
   int64_t *xrequested;
   uint32_t *dev_out; /* optional [n_pods][TYPES] device slots of the last orc_place_stream_ext call */
+  /* PodTopologySpread: each table constraint's matching pods per node [cons][n] (pts_oracle.c) */
+  int32_t *pts_cnt;
 } orc_state;
+
+/* PodTopologySpread per-pod state (pts_oracle.c): PreFilter's pairs and
+ * minima per topology key, PreScore's ignored nodes, pairs and weights */
+typedef struct orc_pts {
+  int on, scored, nh, ns;
+  int hj[KOORDHIP_PTS_POD], sj[KOORDHIP_PTS_POD];
+  uint8_t *fpres[KOORDHIP_PTS_KEYS];
+  int64_t *fmatch[KOORDHIP_PTS_KEYS];
+  int64_t fmin[KOORDHIP_PTS_KEYS];
+  uint8_t *ignored;
+  uint8_t *spres[KOORDHIP_PTS_KEYS];
+  int64_t *scount[KOORDHIP_PTS_KEYS];
+  double weight[KOORDHIP_PTS_POD];
+} orc_pts;
+int orc_pts_active(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x);
+int orc_pts_prefilter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x, orc_pts *ps);
+int orc_pts_filter(const orc_state *st, const koordhip_pod_ext *x, const orc_pts *ps, int32_t i);
+int orc_pts_prescore(const orc_state *st, const koordhip_pod_ext *x, orc_pts *ps, const int32_t *feas, int32_t nf);
+int64_t orc_pts_score(const orc_state *st, const koordhip_pod_ext *x, const orc_pts *ps, int32_t i);
+void orc_pts_normalize(const orc_pts *ps, const int32_t *feas, int64_t *scores, int32_t nf);
+void orc_pts_commit(orc_state *st, const koordhip_pod_ext *x, int32_t i);
+void orc_pts_free(orc_pts *ps);
 
 int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n);
 void orc_state_free(orc_state *st);
