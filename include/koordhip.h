@@ -519,6 +519,9 @@ int koordhip_fetch_devices(koordhip_ctx *ctx, uint32_t *slots, int32_t n_pods);
 /* DeviceShare and extended-scalar mutable state: dev_used [n][TYPES][dev_slots][RES],
  * xrequested [NXRES][n] (either may be NULL). */
 int koordhip_read_devices(koordhip_ctx *ctx, int64_t *dev_used, int64_t *xrequested);
+/* PodTopologySpread: each table constraint's matching pods per node after the
+ * last place call, [pts_cons][n] (NodeInfo.AddPod of the placed pods). */
+int koordhip_read_pts(koordhip_ctx *ctx, int32_t *cnt);
 
 /* The same split in two so a caller can time the device part alone: stage
  * (host -> HBM copy) then place (HBM-resident pods, result kept on device

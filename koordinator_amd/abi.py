@@ -271,6 +271,7 @@ def load_library(path: str = LIB_PATH):
         "koordhip_eval_ext": (C.c_int, [vp, vp, vp, C.c_int32, _u8p, _i32p, vp, C.c_int32]),
         "koordhip_fetch_devices": (C.c_int, [vp, C.POINTER(C.c_uint32), C.c_int32]),
         "koordhip_read_devices": (C.c_int, [vp, _i64p, _i64p]),
+        "koordhip_read_pts": (C.c_int, [vp, _i32p]),
         "koordhip_stage_pods": (C.c_int, [vp, vp, C.c_int32]),
         "koordhip_stage_pods_ext": (C.c_int, [vp, vp, vp, C.c_int32]),
         "koordhip_place_staged": (C.c_int, [vp]),
@@ -308,7 +309,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_last_error", "koordhip_abi_version", "koordhip_create", "koordhip_destroy",
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_place_stream_ext", "koordhip_eval_ext", "koordhip_fetch_devices",
-    "koordhip_read_devices", "koordhip_stage_pods", "koordhip_stage_pods_ext", "koordhip_place_staged", "koordhip_fetch_placements",
+    "koordhip_read_devices", "koordhip_read_pts", "koordhip_stage_pods", "koordhip_stage_pods_ext", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
     "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
     "koordhip_read_resv_cpus", "koordhip_last_stats", "koordhip_last_kernel_stats",

@@ -183,7 +183,8 @@ struct koordhip_ctx {
   bool podx_staged = false;
   uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
   uint64_t *d_seqg = nullptr;
-  void *d_seqdesc = nullptr;  // the sequential cycle's device copies of dc / d      // granules + timeout word of k_seq
+  void *d_seqdesc = nullptr;  // the sequential cycle's device copies of dc / d
+  kh::PtsArgs pts{};          // PodTopologySpread columns (device pointers) and tables' shape      // granules + timeout word of k_seq
   int32_t seq_grid = 0;
   int64_t last_launches = 0, last_evals = 0;
 };
@@ -727,9 +728,9 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   dv = kh::DevDev{};
   const bool dev = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
   if (!c->seq) {
-    if (s->dev_slots > 0 || s->xalloc || s->static_score[0] || s->static_score[1])
-      return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score columns need DeviceShare or a normalized "
-                                   "Score plugin in the profile (the sequential cycle)");
+    if (s->dev_slots > 0 || s->xalloc || s->static_score[0] || s->static_score[1] || s->pts_keys > 0)
+      return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score / topology-spread columns need DeviceShare, "
+                                   "PodTopologySpread or a normalized Score plugin in the profile (the sequential cycle)");
     return 0;
   }
   int e = 0;
@@ -785,6 +786,50 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     if (!e) e = upload(c, ss, s->static_score[w], (size_t)n * KOORDHIP_MAX_STATIC_CLASSES);
     dv.sscore[w] = ss;
   }
+  // PodTopologySpread: the keys' domains, the constraint table's counts, the classes' eligibility
+  c->pts = kh::PtsArgs{};
+  const bool pts = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_PTS) != 0;
+  if (!e && pts && s->pts_keys > 0) {
+    if (s->pts_keys > KOORDHIP_PTS_KEYS || s->pts_cons < 0 || s->pts_cons > KOORDHIP_PTS_CONS || s->pts_classes < 0 ||
+        s->pts_classes > KOORDHIP_PTS_CLASSES || !s->pts_dom || !s->pts_elig || (s->pts_cons > 0 && !s->pts_cnt))
+      return fail(KOORDHIP_EINVAL, "PodTopologySpread tables outside KOORDHIP_PTS_* or a column missing");
+    for (int k = 0; k < s->pts_keys; k++)
+      if (!((s->pts_hostname >> k) & 1u) && (s->pts_ndom[k] < 1 || s->pts_ndom[k] > KOORDHIP_PTS_DOMAINS))
+        return fail(KOORDHIP_EINVAL, "PodTopologySpread: a non-hostname key needs 1..KOORDHIP_PTS_DOMAINS domains");
+    for (int cc = 0; cc < s->pts_cons; cc++)
+      if (s->pts_cons_key[cc] < 0 || s->pts_cons_key[cc] >= s->pts_keys)
+        return fail(KOORDHIP_EINVAL, "PodTopologySpread: a constraint's key is out of range");
+    for (int k = 0; k < s->pts_keys; k++)
+      for (int32_t i = 0; i < n; i++) {
+        const int32_t v = s->pts_dom[(size_t)k * n + i];
+        const int32_t hi = ((s->pts_hostname >> k) & 1u) ? n : s->pts_ndom[k];
+        if (v < -1 || v >= hi || (((s->pts_hostname >> k) & 1u) && v >= 0 && v != i))
+          return fail(KOORDHIP_EINVAL, "PodTopologySpread: pts_dom out of range (a hostname domain is the node)");
+      }
+    int32_t *pd = nullptr, *pc = nullptr;
+    uint16_t *pe = nullptr;
+    e = dev_alloc(c, &pd, (size_t)n * s->pts_keys);
+    if (!e) e = upload(c, pd, s->pts_dom, (size_t)n * s->pts_keys);
+    if (!e) e = dev_alloc(c, &pc, (size_t)n * std::max(1, s->pts_cons));
+    if (!e) e = upload(c, pc, s->pts_cons > 0 ? s->pts_cnt : nullptr, (size_t)n * std::max(1, s->pts_cons));
+    if (!e) e = dev_alloc(c, &pe, (size_t)n);
+    if (!e) e = upload(c, pe, s->pts_elig, (size_t)n);
+    kh::PtsArgs &pa = c->pts;
+    pa.dom = pd;
+    pa.cnt = pc;
+    pa.elig = pe;
+    pa.keys = s->pts_keys;
+    pa.cons = s->pts_cons;
+    pa.classes = s->pts_classes;
+    pa.host = s->pts_hostname;
+    pa.filt = (c->cfg.filter_plugins & KOORDHIP_PLUGIN_PTS) ? 1 : 0;
+    pa.score = (c->cfg.score_plugins & KOORDHIP_PLUGIN_PTS) ? 1 : 0;
+    for (int cc = 0; cc < KOORDHIP_PTS_CONS; cc++) pa.cons_key[cc] = cc < s->pts_cons ? s->pts_cons_key[cc] : 0;
+  }
+  c->pts.w = (c->cfg.score_plugins & KOORDHIP_PLUGIN_PTS) ? c->cfg.ext_weight[3] : 0;
+  // (a profile scoring PodTopologySpread on a snapshot without tables: every
+  // node scores 100, as for pods without constraints)
+  if (pts && !c->pts.dom) c->pts.score = (c->cfg.score_plugins & KOORDHIP_PLUGIN_PTS) ? 1 : 0;
   return e;
 }
 
@@ -820,15 +865,17 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   if (cfg->abi_version != KOORDHIP_ABI_VERSION) return fail(KOORDHIP_EINVAL, "abi_version mismatch");
   const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA |
                          KOORDHIP_PLUGIN_RESERVATION | KOORDHIP_PLUGIN_NODE_STATIC | KOORDHIP_PLUGIN_BALANCED |
-                         KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE;
+                         KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE |
+                         KOORDHIP_PLUGIN_PTS;
   if ((cfg->filter_plugins | cfg->score_plugins) & ~known) return fail(KOORDHIP_EINVAL, "unknown plugin bit");
   if (cfg->filter_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE))
     return fail(KOORDHIP_EINVAL, "the NodeAffinity / TaintToleration Score bits are Score plugins");
   for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) {
     static const uint32_t xb[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
-                                                       KOORDHIP_PLUGIN_TAINT_SCORE};
+                                                       KOORDHIP_PLUGIN_TAINT_SCORE, KOORDHIP_PLUGIN_PTS};
     if ((cfg->score_plugins & xb[e]) && (cfg->ext_weight[e] < 1 || cfg->ext_weight[e] > 100))
-      return fail(KOORDHIP_EINVAL, "DeviceShare / NodeAffinity / TaintToleration score weight must be in [1, 100]");
+      return fail(KOORDHIP_EINVAL,
+                  "DeviceShare / NodeAffinity / TaintToleration / PodTopologySpread score weight must be in [1, 100]");
   }
   for (int k = 0; k < 5; k++)
     if (cfg->dev_res_weight[k] < 0 || cfg->dev_res_weight[k] > 100)
@@ -890,7 +937,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.dev_most = cfg->dev_most_allocated ? 1 : 0;
   for (int k = 0; k < 5; k++) c->dc.dev_w[k] = cfg->dev_res_weight[k];
   // normalized scores couple a pod's nodes: the exact sequential cycle
-  c->seq = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) ||
+  c->seq = ((cfg->filter_plugins | cfg->score_plugins) & (KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_PTS)) ||
            (cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
@@ -928,6 +975,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     if (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) max_total += 100 * (int64_t)cfg->ext_weight[0];
     if (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) max_total += 100 * (int64_t)cfg->ext_weight[1];
     if (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) max_total += 100 * (int64_t)cfg->ext_weight[2];
+    if (cfg->score_plugins & KOORDHIP_PLUGIN_PTS) max_total += 100 * (int64_t)cfg->ext_weight[3];
     c->dc.resv_b1 = (int32_t)max_total + 1;
     if (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION) {
       // the ranking totals of resv.hpp: one normalised Reservation unit must
@@ -1331,7 +1379,28 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
         cols.push_back({const_cast<uint16_t *>(dv.sscore[w]) + (size_t)q * c->n, rows->static_score[w] + (size_t)q * m, 2,
                         false, "static_score"});
     }
-  } else if (rows->dev_slots > 0 || rows->xalloc || rows->static_score[0] || rows->static_score[1]) {
+    // PodTopologySpread rows: the same keys / constraint table as the loaded snapshot
+    if (rows->pts_keys > 0) {
+      const kh::PtsArgs &pa = c->pts;
+      if (!pa.dom || rows->pts_keys != pa.keys || rows->pts_cons != pa.cons || !rows->pts_dom || !rows->pts_elig ||
+          (pa.cons > 0 && !rows->pts_cnt))
+        return fail(KOORDHIP_EINVAL, "update rows: PodTopologySpread columns must match the loaded snapshot's tables");
+      for (int k = 0; k < pa.keys; k++) {
+        for (int32_t j = 0; j < m; j++) {
+          const int32_t v = rows->pts_dom[(size_t)k * m + j];
+          if (v < -1 || v >= (((pa.host >> k) & 1u) ? c->n : KOORDHIP_PTS_DOMAINS) ||
+              (((pa.host >> k) & 1u) && v >= 0 && v != idx[j]))
+            return fail(KOORDHIP_EINVAL, "update rows: pts_dom out of range");
+        }
+        cols.push_back({const_cast<int32_t *>(pa.dom) + (size_t)k * c->n, rows->pts_dom + (size_t)k * m, 4, false,
+                        "pts_dom"});
+      }
+      for (int cc = 0; cc < pa.cons; cc++)
+        cols.push_back({pa.cnt + (size_t)cc * c->n, rows->pts_cnt + (size_t)cc * m, 4, false, "pts_cnt"});
+      cols.push_back({const_cast<uint16_t *>(pa.elig), rows->pts_elig, 2, false, "pts_elig"});
+    }
+  } else if (rows->dev_slots > 0 || rows->xalloc || rows->static_score[0] || rows->static_score[1] ||
+             rows->pts_keys > 0) {
     return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score rows need DeviceShare or a normalized Score "
                                  "plugin in the profile");
   }
@@ -1619,7 +1688,25 @@ static int check_pod_ext(const koordhip_pod_ext *x, int32_t n, bool *any) {
     if ((e.flags & KOORDHIP_PODX_DEVICE) && e.dev_req[KOORDHIP_DEV_GPU][1] < 0 && e.dev_req[KOORDHIP_DEV_GPU][2] < 0 &&
         e.dev_req[KOORDHIP_DEV_GPU][0] > 0)
       return fail(KOORDHIP_EINVAL, "a GPU request needs gpu-memory-ratio or gpu-memory (ValidDeviceResourceCombinations)");
-    *any = *any || e.flags != 0 || e.xmask != 0;
+    if (e.pts_n > KOORDHIP_PTS_POD || e.pts_class >= KOORDHIP_PTS_CLASSES)
+      return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: more than KOORDHIP_PTS_POD constraints or a spread class out of range");
+    for (int j = 0; j < e.pts_n; j++)
+      if (e.pts_c[j] >= KOORDHIP_PTS_CONS || e.pts_skew[j] < 1 || (e.pts_fl[j] & ~(KOORDHIP_PTS_HARD | KOORDHIP_PTS_SELF)))
+        return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: a topology spread constraint out of range");
+    *any = *any || e.flags != 0 || e.xmask != 0 || e.pts_n != 0 || e.pts_match != 0;
+  }
+  return 0;
+}
+
+// the pods' topology spread constraints against the loaded snapshot's tables
+static int check_pod_pts(const koordhip_ctx *c, const koordhip_pod_ext *x, int32_t n) {
+  if (c->pts.keys <= 0) return 0;
+  for (int32_t j = 0; j < n; j++) {
+    if (x[j].pts_n && x[j].pts_class >= c->pts.classes)
+      return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: spread class beyond the snapshot's pts_classes");
+    for (int q = 0; q < x[j].pts_n; q++)
+      if (x[j].pts_c[q] >= c->pts.cons)
+        return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: constraint beyond the snapshot's pts_cons");
   }
   return 0;
 }
@@ -1629,6 +1716,7 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
   if (!ext || n_pods <= 0) return 0;
   bool any = false;
   if (int e = check_pod_ext(ext, n_pods, &any)) return e;
+  if (int e = check_pod_pts(c, ext, n_pods)) return e;
   if (!any) return 0;
   if (!c->seq) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   if (n_pods > c->podx_cap) {
@@ -1694,6 +1782,17 @@ int koordhip_read_devices(koordhip_ctx *c, int64_t *dev_used, int64_t *xrequeste
   return 0;
 }
 
+int koordhip_read_pts(koordhip_ctx *c, int32_t *cnt) {
+  if (!c || !cnt) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t nb = (size_t)c->n * std::max(0, c->pts.cons) * sizeof(int32_t);
+  if (!c->pts.cnt || !nb) return 0;
+  HIP_TRY(hipMemcpy(cnt, c->pts.cnt, nb, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods,
                       uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
@@ -1702,8 +1801,10 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
   if (topk && (k < 1 || k > kMaxBatch)) return fail(KOORDHIP_EINVAL, "k must be in [1, 64]");
   if (n_pods == 0) return 0;
   bool any = false;
-  if (ext)
+  if (ext) {
     if (int e = check_pod_ext(ext, n_pods, &any)) return e;
+    if (int e = check_pod_pts(c, ext, n_pods)) return e;
+  }
   if (!c->seq) {
     if (any) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
     // the per-node plugins only: koordhip_eval, its planes widened
@@ -1739,7 +1840,7 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
       hipMalloc(&dst, (size_t)per * std::max(n, 1)) != hipSuccess ||
       hipMalloc(&dsc4, (size_t)per * KOORDHIP_NPLUGINS * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
       hipMalloc(&dsc, (size_t)per * NPX * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
-      hipMalloc(&work, (size_t)per * 4 * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&work, (size_t)per * kh::SEQ_WORK_PLANES * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
       (topk && hipMalloc(&dk, (size_t)per * k * sizeof(uint64_t)) != hipSuccess)) {
     cleanup();
     return fail(KOORDHIP_ENOMEM, "eval buffers");
@@ -1757,7 +1858,8 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
     if (kh::launch_eval_full(c->dc, c->d, dp, np, dst, dsc4, c->stream) != hipSuccess ||
         hipMemcpy2DAsync(dsc, (size_t)NPX * n * sizeof(int32_t), dsc4, (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t),
                          (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t), np, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
-        kh::launch_seq_eval(c->dc, c->d, dp, dx, np, rs, dst, dsc, work, topk ? k : 0, dk, c->stream) != hipSuccess) {
+        kh::launch_seq_eval(c->dc, c->d, dp, dx, np, rs, dst, dsc, work, topk ? k : 0, dk, c->pts, c->stream) !=
+            hipSuccess) {
       e = fail(KOORDHIP_EDEVICE, "eval_ext launch");
       break;
     }
@@ -1874,7 +1976,7 @@ int seq_place(koordhip_ctx *c) {
     return fail(KOORDHIP_EINVAL, "the sequential cycle (DeviceShare / normalized Scores) runs on one GPU only");
   const int32_t G = c->n_cu;
   if ((int64_t)G * 256 * 8 < c->n) return fail(KOORDHIP_EINVAL, "too many nodes for the sequential cycle's grid");
-  const size_t gbytes = (size_t)2 * 2 * G * 8 * sizeof(uint64_t) + 64;  // [phase][parity][G][8] + the timeout word
+  const size_t gbytes = kh::seq_granule_bytes(G);
   if (!c->d_seqg) {
     HIP_TRY(hipMalloc(&c->d_seqg, gbytes));
     c->seq_grid = G;
@@ -1882,7 +1984,7 @@ int seq_place(koordhip_ctx *c) {
   const bool dev = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
   if (dev && !c->d_devout && c->pods_cap > 0)
     HIP_TRY(hipMalloc(&c->d_devout, (size_t)c->pods_cap * KOORDHIP_DEV_TYPES * sizeof(uint32_t)));
-  uint32_t *tmo = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(c->d_seqg) + gbytes - 64);
+  uint32_t *tmo = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(c->d_seqg) + kh::seq_tmo_offset(G));
   HIP_TRY(hipMemsetAsync(c->d_seqg, 0, gbytes, c->stream));
   const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
   const bool stamps = std::getenv("KOORDHIP_STAMPS") != nullptr;
@@ -1894,7 +1996,7 @@ int seq_place(koordhip_ctx *c) {
   if (!c->d_seqdesc) HIP_TRY(hipMalloc(&c->d_seqdesc, kh::seq_desc_bytes()));
   HIP_TRY(kh::launch_seq(c->dc, c->d, c->d_pods, c->podx_staged ? c->d_podx : nullptr, np, G, c->d_seqg, tmo,
                          c->d_out, c->d_cpus, dev ? c->d_devout : nullptr, rs, stamps ? c->d_dbg : nullptr,
-                         c->d_seqdesc, c->stream));
+                         c->d_seqdesc, c->pts, c->stream));
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   if (stamps) {
     uint64_t h[6];
@@ -2175,9 +2277,9 @@ int pipe_status(koordhip_ctx *c) {
   if (c->pipe_err) return fail(KOORDHIP_EDEVICE, kStall);
   if (c->seq && c->pipe_check && c->d_seqg) {  // the sequential cycle's spin timeout word
     c->pipe_check = false;
-    const size_t gbytes = (size_t)2 * 2 * c->seq_grid * 4 * sizeof(uint64_t) + 64;
     uint32_t tmo = 0;
-    HIP_TRY(hipMemcpy(&tmo, reinterpret_cast<char *>(c->d_seqg) + gbytes - 64, sizeof(tmo), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&tmo, reinterpret_cast<char *>(c->d_seqg) + kh::seq_tmo_offset(c->seq_grid), sizeof(tmo),
+                      hipMemcpyDeviceToHost));
     if (tmo) {
       c->pipe_err = true;
       return fail(KOORDHIP_EDEVICE, "sequential cycle stalled (watchdog): placements are incomplete");
@@ -2264,6 +2366,7 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
   if (c->d.dv.used)
     v.push_back({c->d.dv.used, n * KOORDHIP_DEV_TYPES * (size_t)c->d.dv.slots * KOORDHIP_DEV_RES * sizeof(int64_t)});
   if (c->d.dv.xreq) v.push_back({c->d.dv.xreq, n * KOORDHIP_NXRES * sizeof(int64_t)});
+  if (c->pts.cnt) v.push_back({c->pts.cnt, n * (size_t)std::max(1, c->pts.cons) * sizeof(int32_t)});
   if (c->dc.resv) {
     const size_t sl = (size_t)c->d.rv.slots;
     v.push_back({c->d.rv.rd[0], b * sl});

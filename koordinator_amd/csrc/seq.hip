@@ -35,6 +35,7 @@
 #include <type_traits>
 
 #include "dev.hpp"
+#include "pts.hpp"
 #include "seq.h"
 
 namespace kh {
@@ -42,7 +43,6 @@ namespace kh {
 constexpr int SEQ_THREADS = 256;
 constexpr int SEQ_NPT = 8;  // nodes per thread held across the pod's phases (grid 256 x 256 x 8 >= 400k nodes)
 constexpr uint32_t SEQ_SPIN_LIMIT = 1u << 24;
-constexpr int SEQ_GRAN = 8;  // granule words per block and phase (6 used)
 
 struct SeqArgs {
   const DevPod *pods;
@@ -59,6 +59,10 @@ struct SeqArgs {
   uint64_t *dbg;        // KOORDHIP_STAMPS: block 0's per-phase cycle sums [0..4], owner commits [5] (NULL: off)
   const DevCfg *gc;     // global copies of the kernel's config and column descriptors (the commit's)
   const DevNodes *gd;
+  // PodTopologySpread: the columns and the per-pod phases' granules: g0 the
+  // hostname minimum, gp the raw Score's min / max, gr the commit result
+  PtsArgs pts;
+  uint64_t *g0, *gp, *gr;
 };
 
 __device__ __forceinline__ uint64_t seq_stamp() {
@@ -124,6 +128,7 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   if (!xf || !df) t = -1;
   raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
   raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
+  raw[3] = 0;  // PodTopologySpread: its own phases (pts.hpp)
   return t;
 }
 
@@ -135,11 +140,12 @@ __device__ __forceinline__ int32_t norm_score(int32_t raw, int32_t mx, bool reve
   return reverse ? 100 - s : s;
 }
 
+// the max-normalized plugins (DeviceShare, NodeAffinity, TaintToleration reversed)
 __device__ __forceinline__ int32_t ext_total(const DevCfg &c, uint32_t ext, const int32_t raw[KOORDHIP_NEXT_PLUGINS],
                                              const int32_t mx[KOORDHIP_NEXT_PLUGINS]) {
   int32_t t = 0;
 #pragma unroll
-  for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+  for (int e = 0; e < 3; e++)
     if ((ext >> e) & 1u) t += c.w_ext[e] * norm_score(raw[e], mx[e], e == 2);
   return t;
 }
@@ -308,19 +314,60 @@ __device__ __forceinline__ bool seq_gather(const uint64_t *g, uint32_t epoch, in
   return *s_stop == 0;
 }
 
+// Every block's (min, max) granule pair of one phase
+__device__ __forceinline__ bool seq_gather_minmax(const uint64_t *g, uint32_t epoch, int32_t G, int32_t &mn,
+                                                  int32_t &mx, PtsLds &L, int32_t *s_stop, uint32_t *tmo, int t) {
+  int32_t a = INT32_MAX, b = 0;
+  bool ok = true;
+  for (int32_t q = t; q < G; q += SEQ_THREADS) {
+    uint32_t gv[2];
+    ok &= sweep<2>(g + (size_t)q * SEQ_GRAN, epoch, gv, tmo);
+    a = min(a, (int32_t)gv[0]);
+    b = max(b, (int32_t)gv[1]);
+  }
+  __syncthreads();  // the previous use of L.red is finished
+  if (t == 0) {
+    *s_stop = 0;
+    L.red[0] = INT32_MAX;
+    L.red[1] = 0;
+  }
+  __syncthreads();
+  if (!ok) *s_stop = 1;
+  atomicMin(&L.red[0], a);
+  atomicMax(&L.red[1], b);
+  __syncthreads();
+  mn = L.red[0];
+  mx = L.red[1];
+  __syncthreads();
+  return *s_stop == 0;
+}
+
+// Publish one block's (min, max) over L.red (reset to neutral first by the caller)
+__device__ __forceinline__ void seq_put_minmax(uint64_t *g, uint32_t epoch, const PtsLds &L, int t) {
+  __syncthreads();
+  if (t == 0) {
+    put_granule(g, epoch, (uint32_t)L.red[0]);
+    put_granule(g + 1, epoch, (uint32_t)L.red[1]);
+  }
+}
+
 template <int SM>
 __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqArgs a) {
   __shared__ int32_t s_red[SEQ_THREADS / 64][8];
   __shared__ int32_t s_tot[SEQ_NPT][SEQ_THREADS];
-  __shared__ int32_t s_raw[SEQ_NPT][KOORDHIP_NEXT_PLUGINS][SEQ_THREADS];
+  __shared__ int32_t s_raw[SEQ_NPT][KOORDHIP_NEXT_PLUGINS][SEQ_THREADS];  // [3]: PodTopologySpread raw, -1 ignored
   __shared__ uint64_t s_key[SEQ_THREADS / 64];
   __shared__ int32_t s_stop;
+  __shared__ PtsLds L;
   const int t = threadIdx.x;
   const int32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t ext = a.ext;
-  const int32_t zero[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
+  const int32_t zero[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0};
+  const PtsArgs &pa = a.pts;
+  const bool pts = pa.keys > 0;  // the snapshot has PodTopologySpread tables (and the plugin runs)
   DevPodX none{};
   for (int q = 0; q < DT; q++) none.req[q][0] = none.req[q][1] = none.req[q][2] = q == 0 ? -1 : 0;
+  if (pts) pts_init(pa, d.n, L, t, SEQ_THREADS);
   const bool dbg = a.dbg != nullptr && b == 0 && t == 0;
   uint64_t ts = dbg ? seq_stamp() : 0, acc[5] = {0, 0, 0, 0, 0};
   auto lap = [&](int q) {
@@ -333,26 +380,62 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
   for (int32_t p = 0; p < a.n_pods; p++) {
     const DevPod pod = a.pods[p];
     const DevPodX x = a.podx ? a.podx[p] : none;
-    const uint32_t eA = 2u * (uint32_t)p + 1u, eB = 2u * (uint32_t)p + 2u;
+    const uint32_t eA = 2u * (uint32_t)p + 1u, eB = 2u * (uint32_t)p + 2u, eP = (uint32_t)p + 1u;
     const int par = p & 1;
+    // ---- PodTopologySpread: the pod's pair counters from the replicas, and
+    //      for a DoNotSchedule hostname constraint the grid's minimum over
+    //      the hard-eligible nodes (its own hand-off)
+    const PtsPod q = pts ? pts_pod(pa, x) : PtsPod{};
+    const bool soft = q.on && q.ns > 0;
+    int32_t hmin = INT32_MAX;
+    if (q.on) {
+      pts_prep(pa, q, L, t);
+      if (q.hhost) {
+        int32_t m = INT32_MAX;
+        for (int k = 0; k < a.npt; k++) {
+          const int32_t i = (k * G + b) * SEQ_THREADS + t;
+          if (i >= d.n) continue;
+          for (int kk = 0; kk < PK; kk++)
+            if (((q.hkeys & pa.host) >> kk) & 1u) {
+              const int32_t v = pts_host_match(pa, q, kk, d.n, i);
+              if (v >= 0) m = min(m, v);
+            }
+        }
+        atomicMin(&L.red[0], m);
+        seq_put_minmax(a.g0 + ((size_t)par * G + b) * SEQ_GRAN, eP, L, t);
+        int32_t unused;
+        if (!seq_gather_minmax(a.g0 + (size_t)par * G * SEQ_GRAN, eP, G, hmin, unused, L, &s_stop, a.tmo, t)) return;
+        if (t == 0) {
+          L.red[0] = INT32_MAX;
+          L.red[1] = 0;
+        }
+        __syncthreads();
+      }
+    }
     // ---- phase A: this block's nodes (totals and raw scores kept in LDS for
     //      phase B: registers for SEQ_NPT slices would spill).  The block also
     //      ranks its nodes as if every normalized maximum were 0, which is
     //      exact whenever it is (then every normalized score is the same
     //      constant): such pods need one hand-off, not two.
+    // (PodTopologySpread Score without ScheduleAnyway constraints: 100 for every node)
+    const int32_t pts_const = (pa.score && !soft) ? 100 * pa.w : 0;
+    (void)pts;
     int32_t v4[4] = {0, 0, 0, 0};  // feasible count, raw maxima
     uint64_t key0 = 0;
 #pragma unroll 1
     for (int k = 0; k < a.npt; k++) {
-      int32_t tk = -1, rk[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
+      int32_t tk = -1, rk[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, -1};
       const int32_t i = (k * G + b) * SEQ_THREADS + t;
       if (i < d.n) {
         tk = seq_eval<SM>(c, d, pod, x, i, a.rs != 0, rk, nullptr);
+        rk[3] = -1;
+        if (tk >= 0 && q.on && q.nh > 0 && !pts_filter(pa, q, L, hmin, d.n, i)) tk = -1;
         if (tk >= 0) {
           v4[0]++;
 #pragma unroll
-          for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) v4[1 + e] = max(v4[1 + e], rk[e]);
-          const uint64_t kk = make_key(tk + ext_total(c, ext, rk, zero), i);
+          for (int e = 0; e < 3; e++) v4[1 + e] = max(v4[1 + e], rk[e]);
+          if (soft) rk[3] = pts_soft_mark(pa, q, L, d.n, i) ? 0 : -1;
+          const uint64_t kk = make_key(tk + ext_total(c, ext, rk, zero) + pts_const, i);
           key0 = kk > key0 ? kk : key0;
         }
       }
@@ -367,26 +450,91 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
       for (int e = 0; e < 4; e++) put_granule(g + e, eA, (uint32_t)v4[e]);
       put_granule(g + 4, eA, (uint32_t)(key0 >> 32));
       put_granule(g + 5, eA, (uint32_t)key0);
+      if (soft) {
+        put_granule(g + 6, eA, (uint32_t)L.nfni);
+#pragma unroll
+        for (int e = 0; e < 2 * PK; e++) put_granule(g + 7 + e, eA, (&L.smask[0][0])[e]);
+      }
     }
     lap(0);
     // ---- every block's granules: the feasible count, the raw maxima and the
-    //      best key under zero maxima
+    //      best key under zero maxima (+ PodTopologySpread's PreScore pairs)
     int32_t g4[4];
     uint64_t win;
-    if (!seq_gather<6>(a.ga + (size_t)par * G * SEQ_GRAN, eA, G, g4, win, s_red, s_key, &s_stop, a.tmo, t)) return;
+    if (soft) {
+      if (!seq_gather<7 + 2 * PK>(a.ga + (size_t)par * G * SEQ_GRAN, eA, G, g4, win, s_red, s_key, &s_stop, a.tmo, t))
+        return;
+    } else {
+      if (!seq_gather<6>(a.ga + (size_t)par * G * SEQ_GRAN, eA, G, g4, win, s_red, s_key, &s_stop, a.tmo, t)) return;
+    }
     const int32_t nf_all = g4[0];
     lap(1);
-    if (g4[1] | g4[2] | g4[3]) {
+    int32_t pmin = 0, pmax = 0;
+    if (soft) {
+      // ---- PodTopologySpread PreScore + Score: weights from the grid's pairs,
+      //      this block's raw scores, the grid's min / max over non-ignored nodes
+      uint32_t mask[PK][2];
+      int32_t nfni = 0;
+      {
+        // (the masks and count were reduced into s_red / s_key words by seq_gather's
+        // sweep of words 6.. -- re-read them here: every thread sweeps the granules once more)
+        for (int e = 0; e < PK; e++) mask[e][0] = mask[e][1] = 0u;
+        __syncthreads();
+        if (t == 0) {
+          L.nfni = 0;
+          for (int e = 0; e < 2 * PK; e++) (&L.smask[0][0])[e] = 0u;
+        }
+        __syncthreads();
+        for (int32_t g = t; g < G; g += SEQ_THREADS) {
+          const uint64_t *gg = a.ga + ((size_t)par * G + g) * SEQ_GRAN;
+          atomicAdd(&L.nfni, (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 6, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT));
+          for (int e = 0; e < 2 * PK; e++)
+            atomicOr(&(&L.smask[0][0])[e], (uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 7 + e,
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        __syncthreads();
+        nfni = L.nfni;
+        for (int e = 0; e < PK; e++) {
+          mask[e][0] = L.smask[e][0];
+          mask[e][1] = L.smask[e][1];
+        }
+        __syncthreads();
+        if (t == 0) {
+          L.red[0] = INT32_MAX;
+          L.red[1] = 0;
+        }
+        __syncthreads();
+      }
+      double w[PP];
+      pts_weights(pa, q, mask, nfni, w);
+      int32_t mn = INT32_MAX, mx = 0;
+#pragma unroll 1
+      for (int k = 0; k < a.npt; k++) {
+        const int32_t i = (k * G + b) * SEQ_THREADS + t;
+        if (s_tot[k][t] < 0 || s_raw[k][3][t] < 0) continue;
+        const int32_t r = pts_raw(pa, q, L, w, d.n, i);
+        s_raw[k][3][t] = r;
+        mn = min(mn, r);
+        mx = max(mx, r);
+      }
+      atomicMin(&L.red[0], mn);
+      atomicMax(&L.red[1], mx);
+      seq_put_minmax(a.gp + ((size_t)par * G + b) * SEQ_GRAN, eP, L, t);
+      if (!seq_gather_minmax(a.gp + (size_t)par * G * SEQ_GRAN, eP, G, pmin, pmax, L, &s_stop, a.tmo, t)) return;
+    }
+    if ((g4[1] | g4[2] | g4[3]) || soft) {
       // ---- phase B: normalized totals, this block's best key
-      const int32_t gmx[KOORDHIP_NEXT_PLUGINS] = {g4[1], g4[2], g4[3]};
+      const int32_t gmx[KOORDHIP_NEXT_PLUGINS] = {g4[1], g4[2], g4[3], 0};
       uint64_t best = 0;
 #pragma unroll 1
       for (int k = 0; k < a.npt; k++) {
         const int32_t tk = s_tot[k][t];
         if (tk < 0) continue;
         const int32_t i = (k * G + b) * SEQ_THREADS + t;
-        const int32_t rk[KOORDHIP_NEXT_PLUGINS] = {s_raw[k][0][t], s_raw[k][1][t], s_raw[k][2][t]};
-        const uint64_t key = make_key(tk + ext_total(c, ext, rk, gmx), i);
+        const int32_t rk[KOORDHIP_NEXT_PLUGINS] = {s_raw[k][0][t], s_raw[k][1][t], s_raw[k][2][t], 0};
+        const int32_t pt = soft ? pa.w * pts_norm(s_raw[k][3][t], pmin, pmax) : pts_const;
+        const uint64_t key = make_key(tk + ext_total(c, ext, rk, gmx) + pt, i);
         best = key > best ? key : best;
       }
       int32_t u4[4] = {0, 0, 0, 0};
@@ -404,6 +552,11 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     }
     // ---- the winner's owner block commits (its nodes are read by no other block)
     const int32_t wn = win ? key_node(win) : -1;
+    // PodTopologySpread: a placed pod counts for the table constraints it
+    // matches; a Reserve that may fail (devices, cpusets) tells the others
+    const uint32_t pmatch = (pts && wn >= 0) ? x.pts_match : 0u;
+    bool may_fail = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) && (x.flags & KOORDHIP_PODX_DEVICE);
+    if constexpr (SM >= 1) may_fail = may_fail || (numa_on(c) && numa_active(pod, c));
     if (t == 0) {
       const bool mine = wn >= 0 ? ((wn / SEQ_THREADS) % G) == b : b == 0;
       if (mine) {
@@ -411,14 +564,31 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
         seq_commit<SM>(a.gc, a.gd, a.pods + p, a.podx ? a.podx + p : nullptr, wn, nf_all, a.rs != 0, a.out_node + p,
                        a.out_cpus ? a.out_cpus + (size_t)p * NW : nullptr,
                        a.out_dev ? a.out_dev + (size_t)p * DT : nullptr);
+        if (pmatch) {
+          const bool done = __hip_atomic_load(a.out_node + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == wn;
+          if (done)
+            for (int cc = 0; cc < pa.cons; cc++)
+              if ((pmatch >> cc) & 1u) pa.cnt[(size_t)cc * d.n + wn] += 1;
+          if (may_fail) put_granule(a.gr + par, eP, done ? 1u : 0u);
+        }
         if (a.dbg) atomicAdd((unsigned long long *)&a.dbg[5], (unsigned long long)(seq_stamp() - c0));
+      }
+      if (pmatch) {
+        bool done = true;
+        if (may_fail) {
+          uint32_t v[1];
+          if (!sweep<1>(a.gr + par, eP, v, a.tmo)) s_stop = 1;
+          done = v[0] != 0;
+        }
+        if (done) pts_commit_tables(pa, L, pmatch, d.n, wn);
       }
     }
     __syncthreads();  // the owner's commit before its next evaluation of w
+    if (s_stop) return;
     lap(4);
   }
   if (dbg)
-    for (int q = 0; q < 5; q++) a.dbg[q] = acc[q];
+    for (int q2 = 0; q2 < 5; q2++) a.dbg[q2] = acc[q2];
 }
 
 // ---- parity evaluation (koordhip_eval_ext): per (pod, node) the status bits,
@@ -441,7 +611,7 @@ __global__ __launch_bounds__(256) void k_seq_eval(DevCfg c, DevNodes d, const De
   uint8_t st = 0;
   const int32_t t = seq_eval<SM>(c, d, pod, x, i, rs != 0, raw, &st);
   const size_t n = (size_t)d.n;
-  int32_t *wk = work + (size_t)p * 4 * n;
+  int32_t *wk = work + (size_t)p * SEQ_WORK_PLANES * n;
   wk[i] = t;
   for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) wk[(size_t)(e + 1) * n + i] = raw[e];
   if (status) status[(size_t)p * n + i] |= st;
@@ -451,23 +621,103 @@ __global__ __launch_bounds__(256) void k_seq_eval(DevCfg c, DevNodes d, const De
   }
 }
 
-__global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int32_t *__restrict__ work, int32_t k,
-                                                  uint64_t *__restrict__ out) {
-  __shared__ uint64_t s_k[4];
-  __shared__ int32_t s_m[4][KOORDHIP_NEXT_PLUGINS];
-  const int32_t p = blockIdx.x, t = threadIdx.x, lane = __lane_id(), wv = t >> 6;
-  const int32_t *wk = work + (size_t)p * 4 * n;
-  const uint32_t ext = ext_bits(c);
-  int32_t mx[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0};
+// PodTopologySpread for the parity evaluator: one workgroup per pod over
+// every node (its own replicas of the pair counters, from the columns):
+// the Filter's status bit and infeasible total, the raw Score plane (0 on
+// infeasible and ignored nodes) and work plane 4 (raw, -1 = not scored).
+__global__ __launch_bounds__(256) void k_pts_eval(PtsArgs pa, int32_t n, const DevPodX *__restrict__ podx,
+                                                  int32_t n_pods, uint8_t *__restrict__ status,
+                                                  int32_t *__restrict__ scores, int32_t *__restrict__ work) {
+  __shared__ PtsLds L;
+  const int32_t p = blockIdx.x, t = threadIdx.x;
+  if (p >= n_pods) return;
+  DevPodX x{};
+  if (podx) {
+    x = podx[p];
+  } else {
+    x.req[0][0] = x.req[0][1] = x.req[0][2] = -1;
+  }
+  const size_t NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
+  int32_t *wk = work + (size_t)p * SEQ_WORK_PLANES * n;
+  int32_t *w4 = wk + (size_t)4 * n;
+  int32_t *plane = scores ? scores + ((size_t)p * NPX + KOORDHIP_NPLUGINS + 3) * n : nullptr;
+  const PtsPod q = pts_pod(pa, x);
+  if (!q.on) {
+    for (int32_t i = t; i < n; i += 256) {
+      w4[i] = wk[i] >= 0 ? 0 : -1;
+      if (plane) plane[i] = 0;
+    }
+    return;
+  }
+  pts_init(pa, n, L, t, 256);
+  pts_prep(pa, q, L, t);
+  int32_t hmin = INT32_MAX;
+  if (q.hhost) {
+    int32_t m = INT32_MAX;
+    for (int32_t i = t; i < n; i += 256)
+      for (int k = 0; k < PK; k++)
+        if (((q.hkeys & pa.host) >> k) & 1u) {
+          const int32_t v = pts_host_match(pa, q, k, n, i);
+          if (v >= 0) m = min(m, v);
+        }
+    atomicMin(&L.red[0], m);
+    __syncthreads();
+    hmin = L.red[0];
+  }
   for (int32_t i = t; i < n; i += 256)
-    if (wk[i] >= 0)
-      for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) mx[e] = max(mx[e], wk[(size_t)(e + 1) * n + i]);
+    if (q.nh > 0 && !pts_filter(pa, q, L, hmin, n, i)) {
+      wk[i] = -1;
+      if (status) status[(size_t)p * n + i] |= KOORDHIP_ST_PTS_FAIL;
+    }
+  __syncthreads();
+  for (int32_t i = t; i < n; i += 256) {
+    w4[i] = wk[i] >= 0 ? ((q.ns == 0 || pts_soft_mark(pa, q, L, n, i)) ? 0 : -1) : -1;
+    if (plane) plane[i] = 0;
+  }
+  __syncthreads();
+  if (q.ns == 0) return;
+  uint32_t mask[PK][2];
+  for (int e = 0; e < PK; e++) {
+    mask[e][0] = L.smask[e][0];
+    mask[e][1] = L.smask[e][1];
+  }
+  double w[PP];
+  pts_weights(pa, q, mask, L.nfni, w);
+  for (int32_t i = t; i < n; i += 256)
+    if (w4[i] >= 0) {
+      const int32_t r = pts_raw(pa, q, L, w, n, i);
+      w4[i] = r;
+      if (plane) plane[i] = r;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int32_t *__restrict__ work, int32_t k,
+                                                  int32_t pts_w, uint64_t *__restrict__ out) {
+  __shared__ uint64_t s_k[4];
+  __shared__ int32_t s_m[4][KOORDHIP_NEXT_PLUGINS + 1];
+  const int32_t p = blockIdx.x, t = threadIdx.x, lane = __lane_id(), wv = t >> 6;
+  const int32_t *wk = work + (size_t)p * SEQ_WORK_PLANES * n;
+  const uint32_t ext = ext_bits(c);
+  int32_t mx[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0}, pmin = INT32_MAX;
+  for (int32_t i = t; i < n; i += 256)
+    if (wk[i] >= 0) {
+      for (int e = 0; e < 3; e++) mx[e] = max(mx[e], wk[(size_t)(e + 1) * n + i]);
+      const int32_t r = wk[(size_t)4 * n + i];
+      if (r >= 0) {
+        mx[3] = max(mx[3], r);
+        pmin = min(pmin, r);
+      }
+    }
   for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) {
     for (int m = 32; m >= 1; m >>= 1) mx[e] = max(mx[e], __shfl_xor(mx[e], m));
     if (lane == 0) s_m[wv][e] = mx[e];
   }
+  pmin = pts_wave_min(pmin);
+  if (lane == 0) s_m[wv][KOORDHIP_NEXT_PLUGINS] = pmin;
   __syncthreads();
   for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) mx[e] = max(max(s_m[0][e], s_m[1][e]), max(s_m[2][e], s_m[3][e]));
+  pmin = min(min(s_m[0][KOORDHIP_NEXT_PLUGINS], s_m[1][KOORDHIP_NEXT_PLUGINS]),
+             min(s_m[2][KOORDHIP_NEXT_PLUGINS], s_m[3][KOORDHIP_NEXT_PLUGINS]));
   uint64_t last = ~0ull;
   for (int32_t j = 0; j < k; j++) {
     uint64_t best = 0;
@@ -475,7 +725,8 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
       if (wk[i] < 0) continue;
       int32_t raw[KOORDHIP_NEXT_PLUGINS];
       for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) raw[e] = wk[(size_t)(e + 1) * n + i];
-      const uint64_t key = make_key(wk[i] + ext_total(c, ext, raw, mx), i);
+      const int32_t pt = pts_w ? pts_w * pts_norm(raw[3], pmin, mx[3]) : 0;
+      const uint64_t key = make_key(wk[i] + ext_total(c, ext, raw, mx) + pt, i);
       if (key < last && key > best) best = key;
     }
     best = seq_wave_max(best);
@@ -491,10 +742,12 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
 
 hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                       int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
-                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, void *desc, hipStream_t s) {
+                      uint32_t *out_dev, int32_t rs, uint64_t *dbg, void *desc, const PtsArgs &pts,
+                      hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   SeqArgs a{};
   a.dbg = dbg;
+  a.pts = pts;
   // the commit's copies of the config and the column descriptors (desc: 16-B aligned device buffer)
   DevCfg *gc = static_cast<DevCfg *>(desc);
   DevNodes *gd = reinterpret_cast<DevNodes *>(static_cast<char *>(desc) + seq_desc_cfg_bytes());
@@ -509,6 +762,9 @@ hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, co
   if (a.npt > SEQ_NPT) return hipErrorInvalidValue;
   a.ga = granules;
   a.gb = granules + (size_t)2 * grid * SEQ_GRAN;
+  a.g0 = granules + (size_t)4 * grid * SEQ_GRAN;
+  a.gp = granules + (size_t)6 * grid * SEQ_GRAN;
+  a.gr = granules + (size_t)8 * grid * SEQ_GRAN;
   a.tmo = tmo;
   a.out_node = out_node;
   a.out_cpus = out_cpus;
@@ -535,7 +791,7 @@ const char *seq_kernel_name(const DevCfg &c) {
 
 hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                            int32_t rs, uint8_t *status, int32_t *scores, int32_t *work, int32_t k, uint64_t *topk,
-                           hipStream_t s) {
+                           const PtsArgs &pts, hipStream_t s) {
   if (n_pods <= 0 || d.n <= 0) return hipSuccess;
   const dim3 g((d.n + 255) / 256, n_pods);
   switch (seq_mode(c)) {
@@ -543,7 +799,9 @@ hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pod
     case 1: hipLaunchKernelGGL(k_seq_eval<1>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work); break;
     default: hipLaunchKernelGGL(k_seq_eval<0>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work);
   }
-  if (topk && k > 0) hipLaunchKernelGGL(k_seq_topk, dim3(n_pods), dim3(256), 0, s, c, d.n, work, k, topk);
+  hipLaunchKernelGGL(k_pts_eval, dim3(n_pods), dim3(256), 0, s, pts, d.n, podx, n_pods, status, scores, work);
+  if (topk && k > 0)
+    hipLaunchKernelGGL(k_seq_topk, dim3(n_pods), dim3(256), 0, s, c, d.n, work, k, pts.score ? pts.w : 0, topk);
   return hipGetLastError();
 }
 

@@ -122,6 +122,15 @@ class PlacementEngine:
         abi.check(self.lib, self.lib.koordhip_read_devices(self._ctx, abi.ptr(used, C.c_int64), abi.ptr(xr, C.c_int64)))
         return {"dev_used": used, "xrequested": xr.T.copy()}
 
+    def read_pts(self) -> np.ndarray:
+        """PodTopologySpread matching pods per node and table constraint [n][cons]."""
+        m = self._table.pts if self._table is not None else None
+        C_ = len(m.cons_key) if m is not None else 0
+        out = np.zeros((C_, self.n), np.int32)
+        if C_:
+            abi.check(self.lib, self.lib.koordhip_read_pts(self._ctx, abi.ptr(out, C.c_int32)))
+        return out.T.copy()
+
     def stage_pods(self, pods: np.ndarray):
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         self._staged = pods

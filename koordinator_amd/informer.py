@@ -51,7 +51,7 @@ from . import abi, k8s
 from .config import Profile
 from . import numa as nm
 from . import reservation as rv
-from .marshal import AssignedPod, ClusterState, build_table, is_node_metric_expired, node_row
+from .marshal import AssignedPod, ClusterState, NewTopologyValue, build_table, is_node_metric_expired, node_row
 from .snapshot import NodeTable
 
 
@@ -129,7 +129,9 @@ class Informer:
         self._resv_rank: Dict[int, int] = {}
         self._resv_cpus_loaded = False                      # the snapshot carried resv_cpus columns
         from .nodefilters import StaticClasses
+        from .topologyspread import SpreadRegistry
         self.static_classes = StaticClasses()
+        self.cluster.spread = SpreadRegistry()
 
     # ---- full snapshot --------------------------------------------------------
     def table(self, now: float) -> NodeTable:
@@ -369,7 +371,21 @@ class Informer:
             for p in pods:
                 if self.static_classes.classify(pod_static(p)) >= self.static_classes.frozen:
                     self._reload = True
+        if self._spread_on():
+            for p in pods:
+                if not self.cluster.spread.covers(p):
+                    self._reload = True
         return self._reload
+
+    def _spread_on(self) -> bool:
+        from .config import PLUGIN_PTS
+        return PLUGIN_PTS in self.profile.filters or PLUGIN_PTS in self.profile.scores
+
+    def pod_ext_records(self, pods):
+        """koordhip_pod_ext records (DeviceShare, extended scalars, topology
+        spread constraints in the loaded snapshot's tables)."""
+        from .marshal import pod_ext_records
+        return pod_ext_records(pods, self.profile, self.cluster.spread)
 
     def pod_records(self, pods):
         """Pod records with the current owner groups' match masks and static classes."""
@@ -423,7 +439,11 @@ class Informer:
         labels = self._node_labels()
         for j, i in enumerate(idx):
             node = self.cluster.nodes[int(i)]
-            node_row(rows, j, node, self.cluster, self.profile, now, self.static_classes)
+            try:
+                node_row(rows, j, node, self.cluster, self.profile, now, self.static_classes, node_index=int(i))
+            except NewTopologyValue:
+                res.needs_reload = True              # a topology value the snapshot has no domain for
+                return np.zeros(0, np.int32), None, res
             r = placed.get(int(i))
             if r is None:
                 rv.clear_reservation_row(rows, j)

@@ -28,6 +28,10 @@ class MarshalError(ValueError):
     pass
 
 
+class NewTopologyValue(MarshalError):
+    """A node's topology label value has no domain in the loaded snapshot: rebuild it."""
+
+
 # ---------------------------------------------------------------------------
 # Pod side (PreFilter products)
 
@@ -307,6 +311,8 @@ class ClusterState:
     node_pods: Dict[str, List[k8s.Pod]] = field(default_factory=dict)  # NodeInfo.Pods per node
     assigned: Dict[str, List[AssignedPod]] = field(default_factory=dict)
     devices: Dict[str, object] = field(default_factory=dict)          # Device CRs by node (deviceshare.Device)
+    # PodTopologySpread: the registry of the pods to schedule (topologyspread.SpreadRegistry)
+    spread: object = None
 
 
 def estimate_node(node: k8s.Node) -> k8s.ResourceList:
@@ -449,10 +455,11 @@ def estimated_assigned_pod_used(cluster: ClusterState, node_name: str, nm: k8s.N
 
 
 def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, profile: Profile, now: float,
-             static_classes=None):
+             static_classes=None, node_index: Optional[int] = None):
     """Fill row i of `table` from the objects (Fit accounting + LoadAware state,
     and the static_allow bits of `static_classes` when the profile enables the
-    upstream static filters)."""
+    upstream static filters).  `node_index`: the node's row in the snapshot
+    when `table` holds a subset of its rows (an update_nodes delta)."""
     p = profile.resolved()
     args = p.loadaware
     t = table.cols
@@ -465,7 +472,7 @@ def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, pr
     else:
         t["static_allow"][i] = 0xFFFFFFFF
     if table.has_ext:
-        ext_row(table, i, node, cluster, profile, static_classes)
+        ext_row(table, i, node, cluster, profile, static_classes, node_index)
     # ---- Fit: Allocatable / Requested / NonZeroRequested / len(Pods)
     alloc = node.allocatable
     t["alloc0"][i] = alloc[k8s.CPU].milli_value() if k8s.CPU in alloc else 0
@@ -567,7 +574,8 @@ def node_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, pr
     t["la_flags"][i] = flags
 
 
-def ext_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, profile: Profile, static_classes=None):
+def ext_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, profile: Profile, static_classes=None,
+            node_index: Optional[int] = None):
     """Row i of the sequential cycle's columns: the node's Device CR and its
     pods' device allocations (dev_*), the extended scalars' Allocatable and
     Requested (xalloc / xrequested), the NodeAffinity / TaintToleration raw
@@ -586,12 +594,59 @@ def ext_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, pro
     for p in pods_on_node:
         for n, v in ds.fit_xreq(p).items():
             t["xrequested"][i, ds.XRES_INDEX[n]] += v
+    if table.has_pts:
+        pts_row(table, i, node, cluster, i if node_index is None else node_index)
     t["static_score"][i] = 0
     if static_scores_of(profile):
         from .nodefilters import static_scores
         if static_classes is None:
             raise MarshalError("the profile enables NodeAffinity / TaintToleration Scores: pass the StaticClasses")
         t["static_score"][i] = static_scores([node_static(node)], static_classes)[0]
+
+
+def pts_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, node_index: int):
+    """Row i of the PodTopologySpread columns: the node's domain per key (the
+    snapshot's domain index; a value it does not hold needs a rebuild; the
+    hostname domain is the node's snapshot row `node_index`), its matching pods
+    per table constraint, its spread-class eligibility."""
+    from . import topologyspread as ts
+    reg = cluster.spread
+    labels = node.labels or {}
+    dom = table["pts_dom"][i]
+    dom[:] = -1
+    for k, key in enumerate(reg.keys):
+        v = labels.get(key)
+        if v is None:
+            continue
+        if key == ts.HOSTNAME:
+            dom[k] = node_index
+            continue
+        d = reg.domains.values[k].get(v) if reg.domains is not None else None
+        if d is None:
+            raise NewTopologyValue(f"topology value {key}={v!r} is new to the snapshot: rebuild it")
+        dom[k] = d
+    cnt, elig = ts.node_pts(reg, node, cluster.node_pods.get(node.name, []))
+    table["pts_cnt"][i] = cnt
+    table["pts_elig"][i] = elig
+
+
+def pod_ext_records(pods, profile: Profile, spread=None) -> np.ndarray:
+    """koordhip_pod_ext records: DeviceShare requests, extended scalars and
+    (PodTopologySpread in the profile) the pods' spread constraints in the
+    registry's tables."""
+    from . import deviceshare as ds
+    from .config import PLUGIN_PTS
+    from .topologyspread import pod_pts_fields
+    pods = list(pods)
+    arr = ds.pod_ext_records(pods)
+    if PLUGIN_PTS in profile.filters or PLUGIN_PTS in profile.scores:
+        if spread is None:
+            raise MarshalError("the profile enables PodTopologySpread: pass the snapshot's SpreadRegistry")
+        for j, p in enumerate(pods):
+            if not spread.covers(p):
+                raise MarshalError(f"pod {p.key}: spread constraints first seen after the snapshot was built: rebuild it")
+            pod_pts_fields(arr[j], p, spread)
+    return arr
 
 
 def device_slots_of(cluster: ClusterState) -> int:
@@ -620,8 +675,20 @@ def build_table(cluster: ClusterState, profile: Profile, now: float, static_clas
     t = NodeTable.empty(len(cluster.nodes))
     t.names = [n.name for n in cluster.nodes]
     if sequential_profile(profile):
-        from .config import PLUGIN_DEVICESHARE
+        from .config import PLUGIN_DEVICESHARE, PLUGIN_PTS
         t.enable_ext(device_slots_of(cluster) if PLUGIN_DEVICESHARE in profile.filters else 0)
+        reg = cluster.spread
+        if (PLUGIN_PTS in profile.filters or PLUGIN_PTS in profile.scores) and reg is not None and reg.keys:
+            from . import topologyspread as ts
+            from .snapshot import PtsMeta
+            reg.domains = ts.DomainIndex(reg)
+            reg.domains.build(cluster.nodes)
+            ndom = [0 if key == ts.HOSTNAME else max(1, len(reg.domains.values[k])) for k, key in enumerate(reg.keys)]
+            t.enable_pts(PtsMeta(keys=len(reg.keys), hostname=sum(1 << k for k, key in enumerate(reg.keys)
+                                                                  if key == ts.HOSTNAME),
+                                 ndom=ndom + [0] * (abi.PTS_KEYS - len(ndom)),
+                                 cons_key=[k for _, _, k in reg.cons], classes=len(reg.classes)))
+            reg.freeze()
     for i, node in enumerate(cluster.nodes):
         node_row(t, i, node, cluster, profile, now, static_classes)
     if static_classes is not None:

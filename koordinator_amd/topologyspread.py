@@ -111,6 +111,7 @@ class SpreadRegistry:
         self.classes: List[Tuple[Tuple, int, int]] = []                 # (affinity key, hard key mask, soft key mask)
         self.class_affinity: List = []                                  # a pod of the class (its affinity)
         self.frozen = None                                              # (keys, cons, classes) covered by the snapshot
+        self.domains: Optional["DomainIndex"] = None                    # the snapshot's label value -> domain maps
 
     def _key(self, k: str) -> int:
         if k not in self.keys:
@@ -163,12 +164,12 @@ class SpreadRegistry:
 
     def covers(self, pod) -> bool:
         """The pod's keys, constraints and class were in the registry when the snapshot was built."""
+        r = self.register(pod)                      # (registered either way: the next snapshot covers it)
+        if r is None:
+            return True
         if self.frozen is None:
             return False
         nk, nc, ns = self.frozen
-        r = self.register(pod)
-        if r is None:
-            return True
         cls, items = r
         return cls < ns and all(c < nc for c, _, _ in items) and \
             all(self.cons[c][2] < nk for c, _, _ in items)
@@ -180,6 +181,15 @@ class SpreadRegistry:
             if ns == pod.namespace and sel is not None and sel.matches(pod.labels):
                 m |= 1 << c
         return m
+
+
+def registry_for(pods) -> SpreadRegistry:
+    """A registry holding the spread constraints of `pods` (the pods a snapshot
+    will schedule): set it as ClusterState.spread before marshal.build_table."""
+    reg = SpreadRegistry()
+    for p in pods:
+        reg.register(p)
+    return reg
 
 
 def pod_pts_fields(rec, pod, reg: SpreadRegistry):
