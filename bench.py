@@ -160,13 +160,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare"], default="config4",
+    ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare", "spread"], default="config4",
                     help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
                          "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods); "
                          "config5: 200k nodes, 10%% holding a Reservation matched by 20%% of the pods, "
                          "+ LoadAware + NodeNUMAResource; deviceshare: config 4's cluster with GPU / RDMA "
                          "devices and 20%% device pods, + DeviceShare (weight 1): the exact sequential cycle, "
-                         "one GPU")
+                         "one GPU; spread: config 4's cluster with zone / rack / hostname topology and 60%% of "
+                         "the pods in five PodTopologySpread classes, + PodTopologySpread (filter, weight 2): "
+                         "the exact sequential cycle, one GPU")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--be-frac", type=float, default=None)
@@ -195,13 +197,15 @@ def main():
 
     import torch
     from koordinator_amd import synth
-    from koordinator_amd.config import shipped_profile, to_c_config, with_deviceshare
+    from koordinator_amd.config import shipped_profile, to_c_config, with_deviceshare, with_topology_spread
     from koordinator_amd.engine import PlacementEngine
 
-    if args.workload == "deviceshare":
+    if args.workload in ("deviceshare", "spread"):
         if world > 1:
-            raise SystemExit("--workload deviceshare runs on one GPU (the sequential cycle is not node-sharded)")
-        return run_sequential(args, torch, synth, with_deviceshare(shipped_profile()), PlacementEngine)
+            raise SystemExit(f"--workload {args.workload} runs on one GPU (the sequential cycle is not node-sharded)")
+        prof = (with_deviceshare(shipped_profile()) if args.workload == "deviceshare"
+                else with_topology_spread(shipped_profile()))
+        return run_sequential(args, torch, synth, prof, PlacementEngine)
 
     dist = None
     if world > 1:
@@ -373,6 +377,7 @@ def main():
         out["cpu_baseline"] = cb
         out["speedup_vs_best_cpu_leg"] = round(value / cb["best_leg"]["pods_per_s"], 1)
     print(json.dumps(out), flush=True)
+    eng.close()                      # before interpreter teardown (the HIP runtime's own exit handlers)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
@@ -393,21 +398,33 @@ def seq_bytes_per_eval(pods: np.ndarray, ext: np.ndarray, cfg, dev_slots: int) -
     gres = (g > 0).sum(axis=1)
     rd = ext["dev_req"][:, abi.DEV_RDMA, 0] > 0
     per = 1 + dev_slots * (4 + 16 * gres) + rd * dev_slots * (4 + 16)
-    return b + np.where(dev, per, 0)
+    b = b + np.where(dev, per, 0)
+    # PodTopologySpread: pts_elig (2 B), the domain of each key the pod's
+    # constraints name and the node's count of each of its constraints (4 B each)
+    pn = ext["pts_n"].astype(np.int64)
+    nkeys = np.array([len(set(int(c) for c in x["pts_c"][:int(x["pts_n"])])) for x in ext], np.int64)
+    return b + np.where(pn > 0, 2 + 4 * nkeys + 4 * pn, 0)
 
 
 def run_sequential(args, torch, synth, prof, PlacementEngine):
-    """The DeviceShare workload: one persistent cooperative k_seq launch per
-    step (every node filtered and scored per pod, normalized over the
-    feasible nodes, the argmax committed before the next pod)."""
+    """The DeviceShare / spread workloads: one persistent cooperative k_seq
+    launch per step (every node filtered and scored per pod, normalized over
+    the feasible nodes, the argmax committed before the next pod)."""
     c = synth.CONFIGS[4]
     args.nodes = args.nodes or c["nodes"]
     args.pods = args.pods or 20000
     args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
+    spread = args.workload == "spread"
     table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
-    synth.add_devices(table, synth.DevSpec())
     pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac), prof)
-    ext = synth.make_device_ext(args.pods, synth.DevStreamSpec(frac=args.dev_frac))
+    if spread:
+        from koordinator_amd import abi
+        table.enable_ext(0)
+        ext = abi.pod_ext_array(args.pods)
+        synth.add_spread(table, ext, synth.SpreadSpec())
+    else:
+        synth.add_devices(table, synth.DevSpec())
+        ext = synth.make_device_ext(args.pods, synth.DevStreamSpec(frac=args.dev_frac))
     from koordinator_amd.config import to_c_config
     cfg = to_c_config(prof)
     eng = PlacementEngine(prof, device=0, profile_kernels=False)
@@ -438,21 +455,27 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     gbs = alg / seq_s / 1e9 if seq_s > 0 else None
     value = args.pods * args.steps / elapsed
     dev = (ext["flags"] & 1) != 0
+    if spread:
+        wl = (f"spread: {args.nodes} nodes (6 zones, 24 racks, hostname; 3 apps' running pods) x {args.pods} pods "
+              f"({int((ext['pts_n'] > 0).mean() * 100)}% in five PodTopologySpread classes), NodeResourcesFit + "
+              "LoadAwareScheduling + PodTopologySpread (filter, weight 2), the exact sequential cycle")
+    else:
+        wl = (f"deviceshare: {args.nodes} nodes (30% with 4/8 GPUs, half of those 2 RDMA NICs) x "
+              f"{args.pods} pods ({int(dev.mean() * 100)}% requesting GPUs), "
+              "NodeResourcesFit + LoadAwareScheduling + DeviceShare (weight 1, LeastAllocated), "
+              "the exact sequential cycle")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "pods/s",
         "evals_per_s": round(args.pods * args.nodes * args.steps / elapsed, 1),
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeded splitmix64 cluster + pod stream)",
-        "config": {"workload": f"deviceshare: {args.nodes} nodes (30% with 4/8 GPUs, half of those 2 RDMA NICs) x "
-                               f"{args.pods} pods ({int(dev.mean() * 100)}% requesting GPUs), "
-                               "NodeResourcesFit + LoadAwareScheduling + DeviceShare (weight 1, LeastAllocated), "
-                               "the exact sequential cycle",
-                   "nodes": args.nodes, "pods": args.pods, "parallelism": "single GPU (cooperative grid)"},
+        "config": {"workload": wl, "nodes": args.nodes, "pods": args.pods, "parallelism": "single GPU (cooperative grid)"},
         "unschedulable": int((placements < 0).sum()),
         "device_pods_placed": int(((placements >= 0) & dev).sum()),
+        "spread_pods_placed": int(((placements >= 0) & (ext["pts_n"] > 0)).sum()),
         "roofline": {"bound": "latency", "kernel": kn["resolve"],
-                     "limiter": "latency: per pod one grid-wide hand-off (two for device pods) after the owner's commit and one evaluation chain (not bandwidth); priced against HBM peak",
+                     "limiter": ("latency: per pod one grid-wide hand-off (two for device pods) after the owner's commit and one evaluation chain (not bandwidth); priced against HBM peak" if not spread else "latency: per pod the spread pre-pass (hostname minimum), one or two grid-wide hand-offs (soft scoring adds the raw min / max) and one evaluation chain (not bandwidth); priced against HBM peak"),
                      "timing": "HIP events around the k_seq launch of the last timed step",
                      "achieved": round(gbs, 2) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 5) if gbs else None, "traffic": None,
@@ -465,6 +488,7 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
         out["cpu_baseline"] = cb
         out["speedup_vs_best_cpu_leg"] = round(value / cb["best_leg"]["pods_per_s"], 1)
     print(json.dumps(out), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":
