@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 9
+#define KOORDHIP_ABI_VERSION 10
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -87,13 +87,21 @@ extern "C" {
 #define KOORDHIP_PLUGIN_PTS 512u             /* PodTopologySpread Filter (DoNotSchedule constraints) and Score
                                                 (ScheduleAnyway constraints, weight ext_weight[3]; its own
                                                 min-max NormalizeScore); pts_* columns, koordhip_pod_ext.pts_* */
-#define KOORDHIP_NEXT_PLUGINS 4              /* DeviceShare, NodeAffinity, TaintToleration, PodTopologySpread */
+#define KOORDHIP_PLUGIN_IPA 1024u            /* InterPodAffinity Filter (required affinity / anti-affinity, the
+                                                existing pods' required anti-affinity) and Score (preferred terms,
+                                                the existing pods' terms; weight ext_weight[4]; its own min-max
+                                                NormalizeScore); ipa_* columns, koordhip_pod_ext.ipa_* */
+#define KOORDHIP_NEXT_PLUGINS 5              /* DeviceShare, NodeAffinity, TaintToleration, PodTopologySpread,
+                                                InterPodAffinity */
 /* PodTopologySpread envelope (k8s v1.24 podtopologyspread, not vendored): */
 #define KOORDHIP_PTS_KEYS 4      /* distinct topology keys of the snapshot's constraints */
 #define KOORDHIP_PTS_DOMAINS 64  /* values of a non-hostname key */
 #define KOORDHIP_PTS_CONS 8      /* distinct (label selector, namespace) of the snapshot's constraints */
 #define KOORDHIP_PTS_CLASSES 8   /* spread classes: (required node affinity, hard keys, soft keys) */
 #define KOORDHIP_PTS_POD 4       /* constraints per pod */
+/* InterPodAffinity envelope (k8s v1.24 interpodaffinity, not vendored): the
+ * topology keys are the pts_* keys (shared with PodTopologySpread) */
+#define KOORDHIP_IPA_ENTRIES 32  /* count entries of the snapshot (ipa_cnt rows) */
 /* NodeResourcesFit's extended scalar resources of device pods (koordinator.sh/
  * gpu-core, gpu-memory-ratio, gpu-memory, nvidia.com/gpu, ...): fitsRequest
  * checks each one the pod requests against Allocatable - Requested (upstream
@@ -212,6 +220,7 @@ typedef struct koordhip_numa_class {
 #define KOORDHIP_ST_DEVICE_FAIL 32u /* DeviceShare Filter (plugin.go:284-323) */
 #define KOORDHIP_ST_XFIT_FAIL 64u   /* NodeResourcesFit on an extended scalar resource (koordhip_pod_ext.xreq) */
 #define KOORDHIP_ST_PTS_FAIL 128u   /* PodTopologySpread Filter (a missing topology key, or the skew) */
+#define KOORDHIP_ST_IPA_FAIL 256u   /* InterPodAffinity Filter (koordhip_eval_ext's 16-bit status only) */
 
 /* DeviceShare's device model (nodeDevice, device_cache.go:44-50): per node
  * and device type up to KOORDHIP_DEV_SLOTS minors, each with the Device CR's
@@ -254,12 +263,13 @@ typedef struct koordhip_config {
   int32_t reserved[5];
   /* ABI 9: the normalized-score plugins */
   int32_t ext_weight[KOORDHIP_NEXT_PLUGINS]; /* score weights: DeviceShare (scheduler-config.yaml:88-89: 1),
-                                               NodeAffinity, TaintToleration, PodTopologySpread (1..100) */
+                                               NodeAffinity, TaintToleration, PodTopologySpread,
+                                               InterPodAffinity (1..100) */
   int32_t dev_most_allocated;  /* DeviceShareArgs.ScoringStrategy.Type == MostAllocated (scoring.go:125-132) */
   int32_t dev_res_weight[5];   /* DeviceShareArgs.ScoringStrategy.Resources weights (0 = not listed): gpu-core,
                                   gpu-memory-ratio, gpu-memory, rdma, fpga (defaults v1beta2/defaults.go:168-189:
                                   gpu-memory-ratio, rdma, fpga at 1) */
-  int32_t reserved2[2];
+  int32_t reserved2[1];
 } koordhip_config;
 
 /* Columnar node snapshot, all arrays of length n, little-endian, caller-owned
@@ -396,6 +406,18 @@ typedef struct koordhip_node_soa {
   const int32_t *pts_dom;
   const int32_t *pts_cnt;
   const uint16_t *pts_elig;
+  /* InterPodAffinity (KOORDHIP_PLUGIN_IPA): count entries over the pts_* topology
+   * keys (ipa_ents <= KOORDHIP_IPA_ENTRIES, entry e on key ipa_ent_key[e]); ipa_cnt
+   * [ents][n] = the node's pods entry e counts (advanced by Reserve): a "match"
+   * entry counts the pods a term (or, for a pod's required affinity, all of its
+   * terms) matches, a "carry" entry the pods that carry an affinity term.  The
+   * pod-side masks and weights (koordhip_pod_ext.ipa_*) say which entries a pod
+   * reads and how; the domain sums over the nodes of a (key, value) pair are the
+   * reference's topologyPair counts.  ipa_ents 0: no columns. */
+  int32_t ipa_ents;
+  int32_t ipa_reserved;
+  int32_t ipa_ent_key[KOORDHIP_IPA_ENTRIES];
+  const int32_t *ipa_cnt;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -438,10 +460,28 @@ typedef struct koordhip_pod_ext {
   uint8_t pts_fl[KOORDHIP_PTS_POD];
   int32_t pts_skew[KOORDHIP_PTS_POD];
   int32_t pts_reserved;
+  /* InterPodAffinity, bit e = count entry e of the snapshot:
+   *   ipa_inc   entries that count this pod once it is placed (NodeInfo.AddPod)
+   *   ipa_aff   its required affinity terms' entry per topology key: a node
+   *             passes when it has every key and each pair counts > 0, or when
+   *             no pair counts anywhere and KOORDHIP_IPA_SELF (satisfyPodAffinity)
+   *   ipa_anti  its required anti-affinity terms' entries and the existing
+   *             pods' required anti-affinity terms that match it: a node fails
+   *             when one of them counts > 0 in the node's pair
+   *   ipa_score entries with a nonzero ipa_w: raw Score = sum of ipa_w[e] x the
+   *             pair count of e at the node (the reference's topologyScore) */
+  uint32_t ipa_inc;
+  uint32_t ipa_aff;
+  uint32_t ipa_anti;
+  uint32_t ipa_score;
+  uint32_t ipa_flags;
+  int32_t ipa_reserved;
+  int32_t ipa_w[KOORDHIP_IPA_ENTRIES];
 } koordhip_pod_ext;
 #define KOORDHIP_PODX_DEVICE 1u  /* some device request (DeviceShare state.skip == false) */
 #define KOORDHIP_PTS_HARD 1u
 #define KOORDHIP_PTS_SELF 2u
+#define KOORDHIP_IPA_SELF 1u     /* the pod matches all of its own required affinity terms */
 
 /* One top-k record of koordhip_eval. */
 typedef struct koordhip_topk {
@@ -492,11 +532,13 @@ int koordhip_eval(koordhip_ctx *ctx, const koordhip_pod *pods, int32_t n_pods, u
 
 /* ABI 9: the same with koordhip_pod_ext records (ext may be NULL: no device
  * requests), for every profile, including the normalized-score plugins.
+ * status: [n_pods][n] 16-bit KOORDHIP_ST_* bits (incl. KOORDHIP_ST_IPA_FAIL).
  * scores: [n_pods][KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS][n], planes
  * NPLUGINS.. the raw (un-normalized) DeviceShare / NodeAffinity /
- * TaintToleration scores; topk ranks the normalized weighted sums. */
+ * TaintToleration / PodTopologySpread (feasible nodes) / InterPodAffinity
+ * (every node) scores; topk ranks the normalized weighted sums. */
 int koordhip_eval_ext(koordhip_ctx *ctx, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods,
-                      uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
+                      uint16_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
 
 /* Greedy stream: pods attempted once, in order, each against the state left
  * by all earlier commits; winner = lowest-index max total score; the Reserve
@@ -522,6 +564,9 @@ int koordhip_read_devices(koordhip_ctx *ctx, int64_t *dev_used, int64_t *xreques
 /* PodTopologySpread: each table constraint's matching pods per node after the
  * last place call, [pts_cons][n] (NodeInfo.AddPod of the placed pods). */
 int koordhip_read_pts(koordhip_ctx *ctx, int32_t *cnt);
+/* InterPodAffinity: each count entry's pods per node after the last place
+ * call, [ipa_ents][n]. */
+int koordhip_read_ipa(koordhip_ctx *ctx, int32_t *cnt);
 
 /* The same split in two so a caller can time the device part alone: stage
  * (host -> HBM copy) then place (HBM-resident pods, result kept on device

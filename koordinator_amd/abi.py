@@ -11,19 +11,21 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 9
+KOORDHIP_ABI_VERSION = 10
 NRES = 5
 NPLUGINS = 4
 
 PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_RESERVATION = 1, 2, 4, 8
 PLUGIN_NODE_STATIC, PLUGIN_BALANCED = 16, 32
 # normalized-score plugins (the exact sequential cycle, koordhip_place_stream_ext)
-PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE, PLUGIN_PTS = 64, 128, 256, 512
-NEXT_PLUGINS = 4
-EXT_PLUGIN_BITS = (PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE, PLUGIN_PTS)
-NORMALIZED_PLUGINS = PLUGIN_DEVICESHARE | PLUGIN_AFFINITY_SCORE | PLUGIN_TAINT_SCORE | PLUGIN_PTS
+PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE, PLUGIN_PTS, PLUGIN_IPA = 64, 128, 256, 512, 1024
+NEXT_PLUGINS = 5
+EXT_PLUGIN_BITS = (PLUGIN_DEVICESHARE, PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_SCORE, PLUGIN_PTS, PLUGIN_IPA)
+NORMALIZED_PLUGINS = PLUGIN_DEVICESHARE | PLUGIN_AFFINITY_SCORE | PLUGIN_TAINT_SCORE | PLUGIN_PTS | PLUGIN_IPA
 PTS_KEYS, PTS_DOMAINS, PTS_CONS, PTS_CLASSES, PTS_POD = 4, 64, 8, 8, 4
 PTS_HARD, PTS_SELF = 1, 2
+IPA_ENTRIES = 32
+IPA_SELF = 1
 NXRES = 8
 DEV_TYPES, DEV_SLOTS, DEV_RES = 3, 8, 3
 DEV_GPU, DEV_RDMA, DEV_FPGA = 0, 1, 2
@@ -68,7 +70,7 @@ def numa_policy(required: int = 0, preferred: int = 0, exclusive: int = 0) -> in
     return (required & 3) | ((preferred & 3) << 2) | ((exclusive & 3) << 4)
 
 ST_FIT_FAIL, ST_LA_FAIL, ST_NUMA_FAIL, ST_RESV_FAIL, ST_STATIC_FAIL = 1, 2, 4, 8, 16
-ST_DEVICE_FAIL, ST_XFIT_FAIL, ST_PTS_FAIL = 32, 64, 128
+ST_DEVICE_FAIL, ST_XFIT_FAIL, ST_PTS_FAIL, ST_IPA_FAIL = 32, 64, 128, 256
 UNSCHEDULABLE, RESERVE_FAILED = -1, -2
 E_INVAL, E_RESERVE = -1, -6
 UNIQUE_ID_BYTES = 128
@@ -109,7 +111,7 @@ class KoordhipConfig(C.Structure):
         ("ext_weight", C.c_int32 * NEXT_PLUGINS),
         ("dev_most_allocated", C.c_int32),
         ("dev_res_weight", C.c_int32 * 5),
-        ("reserved2", C.c_int32 * 2),
+        ("reserved2", C.c_int32 * 1),
     ]
 
 
@@ -173,6 +175,10 @@ class KoordhipNodeSoa(C.Structure):
         ("pts_dom", _i32p),
         ("pts_cnt", _i32p),
         ("pts_elig", C.POINTER(C.c_uint16)),
+        ("ipa_ents", C.c_int32),
+        ("ipa_reserved", C.c_int32),
+        ("ipa_ent_key", C.c_int32 * IPA_ENTRIES),
+        ("ipa_cnt", _i32p),
     ]
 
 
@@ -220,8 +226,15 @@ POD_EXT_DTYPE = np.dtype([
     ("pts_fl", "u1", (PTS_POD,)),
     ("pts_skew", "<i4", (PTS_POD,)),
     ("pts_reserved", "<i4"),
+    ("ipa_inc", "<u4"),
+    ("ipa_aff", "<u4"),
+    ("ipa_anti", "<u4"),
+    ("ipa_score", "<u4"),
+    ("ipa_flags", "<u4"),
+    ("ipa_reserved", "<i4"),
+    ("ipa_w", "<i4", (IPA_ENTRIES,)),
 ], align=True)
-assert POD_EXT_DTYPE.itemsize == 176
+assert POD_EXT_DTYPE.itemsize == 328
 
 
 def pod_ext_array(n: int) -> np.ndarray:
@@ -268,10 +281,11 @@ def load_library(path: str = LIB_PATH):
         "koordhip_eval": (C.c_int, [vp, vp, C.c_int32, _u8p, _i32p, vp, C.c_int32]),
         "koordhip_place_stream": (C.c_int, [vp, vp, C.c_int32, _i32p]),
         "koordhip_place_stream_ext": (C.c_int, [vp, vp, vp, C.c_int32, _i32p]),
-        "koordhip_eval_ext": (C.c_int, [vp, vp, vp, C.c_int32, _u8p, _i32p, vp, C.c_int32]),
+        "koordhip_eval_ext": (C.c_int, [vp, vp, vp, C.c_int32, C.POINTER(C.c_uint16), _i32p, vp, C.c_int32]),
         "koordhip_fetch_devices": (C.c_int, [vp, C.POINTER(C.c_uint32), C.c_int32]),
         "koordhip_read_devices": (C.c_int, [vp, _i64p, _i64p]),
         "koordhip_read_pts": (C.c_int, [vp, _i32p]),
+        "koordhip_read_ipa": (C.c_int, [vp, _i32p]),
         "koordhip_stage_pods": (C.c_int, [vp, vp, C.c_int32]),
         "koordhip_stage_pods_ext": (C.c_int, [vp, vp, vp, C.c_int32]),
         "koordhip_place_staged": (C.c_int, [vp]),
@@ -309,7 +323,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_last_error", "koordhip_abi_version", "koordhip_create", "koordhip_destroy",
     "koordhip_load_snapshot", "koordhip_update_nodes", "koordhip_read_nodes", "koordhip_eval",
     "koordhip_place_stream", "koordhip_place_stream_ext", "koordhip_eval_ext", "koordhip_fetch_devices",
-    "koordhip_read_devices", "koordhip_read_pts", "koordhip_stage_pods", "koordhip_stage_pods_ext", "koordhip_place_staged", "koordhip_fetch_placements",
+    "koordhip_read_devices", "koordhip_read_pts", "koordhip_read_ipa", "koordhip_stage_pods", "koordhip_stage_pods_ext", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
     "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
     "koordhip_read_resv_cpus", "koordhip_last_stats", "koordhip_last_kernel_stats",

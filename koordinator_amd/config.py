@@ -31,9 +31,11 @@ PLUGIN_BALANCED = "NodeResourcesBalancedAllocation"
 STATIC_FILTERS = (PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
 PLUGIN_DEVICESHARE = "DeviceShare"
 PLUGIN_PTS = "PodTopologySpread"
-# Scores normalized over the pod's feasible nodes (DefaultNormalizeScore): the
-# sequential cycle; NodeAffinity / TaintToleration in `scores` are their Scores
-NORMALIZED_SCORES = (PLUGIN_DEVICESHARE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION, PLUGIN_PTS)
+PLUGIN_IPA = "InterPodAffinity"
+# Scores normalized over the pod's feasible nodes (DefaultNormalizeScore, or the
+# plugin's own min-max normalization): the sequential cycle; NodeAffinity /
+# TaintToleration in `scores` are their Scores
+NORMALIZED_SCORES = (PLUGIN_DEVICESHARE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION, PLUGIN_PTS, PLUGIN_IPA)
 
 
 class ArgsError(ValueError):
@@ -170,6 +172,19 @@ class DeviceShareArgs:
 
 
 @dataclass
+class InterPodAffinityArgs:
+    """InterPodAffinityArgs (upstream k8s v1.24 config/types.go), defaults
+    v1beta2 SetDefaults_InterPodAffinityArgs: HardPodAffinityWeight 1."""
+    hard_pod_affinity_weight: int = 1
+
+    def validate(self):
+        """ValidateInterPodAffinityArgs: 0..100."""
+        if not 0 <= self.hard_pod_affinity_weight <= 100:
+            raise ArgsError(f"hardPodAffinityWeight: Invalid value: {self.hard_pod_affinity_weight}: not in valid "
+                            "range [0-100]")
+
+
+@dataclass
 class Profile:
     """The scheduling profile restricted to the hot-path plugins."""
     filters: tuple = (PLUGIN_FIT, PLUGIN_LOADAWARE)
@@ -178,6 +193,7 @@ class Profile:
     loadaware: LoadAwareSchedulingArgs = field(default_factory=LoadAwareSchedulingArgs)
     numa: NodeNUMAResourceArgs = field(default_factory=NodeNUMAResourceArgs)
     deviceshare: DeviceShareArgs = field(default_factory=DeviceShareArgs)
+    interpodaffinity: InterPodAffinityArgs = field(default_factory=InterPodAffinityArgs)
     batch_pods: int = 0
 
     def resolved(self) -> "Profile":
@@ -256,6 +272,20 @@ def with_topology_spread(profile: Profile, weight: int = 2, filter: bool = True)
     return p
 
 
+def with_interpod_affinity(profile: Profile, weight: int = 1, filter: bool = True,
+                           hard_pod_affinity_weight: int = 1) -> Profile:
+    """The upstream InterPodAffinity plugin: Filter (required affinity /
+    anti-affinity) and Score (the upstream default profile weighs it 1)."""
+    p = copy.deepcopy(profile)
+    if filter and PLUGIN_IPA not in p.filters:
+        p.filters = tuple(p.filters) + (PLUGIN_IPA,)
+    if weight:
+        p.scores = dict(p.scores)
+        p.scores[PLUGIN_IPA] = weight
+    p.interpodaffinity = InterPodAffinityArgs(hard_pod_affinity_weight)
+    return p
+
+
 def to_c_config(profile: Profile, device: int = -1):
     """Lower a resolved profile to the koordhip_config ctypes struct."""
     from .abi import (KOORDHIP_ABI_VERSION, PLUGIN_BITS, KoordhipConfig)
@@ -269,8 +299,9 @@ def to_c_config(profile: Profile, device: int = -1):
     cfg.abi_version = KOORDHIP_ABI_VERSION
     from . import abi
     score_bits = {PLUGIN_NODE_AFFINITY: abi.PLUGIN_AFFINITY_SCORE, PLUGIN_TAINT_TOLERATION: abi.PLUGIN_TAINT_SCORE,
-                  PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE, PLUGIN_PTS: abi.PLUGIN_PTS}
-    own_filter_bits = {PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE, PLUGIN_PTS: abi.PLUGIN_PTS}
+                  PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE, PLUGIN_PTS: abi.PLUGIN_PTS, PLUGIN_IPA: abi.PLUGIN_IPA}
+    own_filter_bits = {PLUGIN_DEVICESHARE: abi.PLUGIN_DEVICESHARE, PLUGIN_PTS: abi.PLUGIN_PTS,
+                       PLUGIN_IPA: abi.PLUGIN_IPA}
     cfg.filter_plugins = 0
     for x in p.filters:  # (the three static filters share one bit)
         cfg.filter_plugins |= own_filter_bits[x] if x in own_filter_bits else PLUGIN_BITS[x]
@@ -289,6 +320,7 @@ def to_c_config(profile: Profile, device: int = -1):
             cfg.ext_weight[e] = w
     if PLUGIN_DEVICESHARE in p.filters or PLUGIN_DEVICESHARE in p.scores:
         p.deviceshare.validate()
+    p.interpodaffinity.validate()
     cfg.dev_most_allocated = 1 if p.deviceshare.scoring_type == "MostAllocated" else 0
     for k, r in enumerate(DeviceShareArgs.SCORER_RESOURCES):
         cfg.dev_res_weight[k] = p.deviceshare.resources.get(r, 0)

@@ -184,7 +184,9 @@ struct koordhip_ctx {
   uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
   uint64_t *d_seqg = nullptr;
   void *d_seqdesc = nullptr;  // the sequential cycle's device copies of dc / d
-  kh::PtsArgs pts{};          // PodTopologySpread columns (device pointers) and tables' shape      // granules + timeout word of k_seq
+  kh::PtsArgs pts{};          // PodTopologySpread columns (device pointers) and tables' shape
+  kh::IpaArgs ipa{};          // InterPodAffinity count entries (device pointers) and their keys
+  int64_t ipa_pods_bound = 0; // pods the snapshot's entries can count (for the raw Score's int32 bound)
   int32_t seq_grid = 0;
   int64_t last_launches = 0, last_evals = 0;
 };
@@ -728,7 +730,7 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   dv = kh::DevDev{};
   const bool dev = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
   if (!c->seq) {
-    if (s->dev_slots > 0 || s->xalloc || s->static_score[0] || s->static_score[1] || s->pts_keys > 0)
+    if (s->dev_slots > 0 || s->xalloc || s->static_score[0] || s->static_score[1] || s->pts_keys > 0 || s->ipa_ents > 0)
       return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score / topology-spread columns need DeviceShare, "
                                    "PodTopologySpread or a normalized Score plugin in the profile (the sequential cycle)");
     return 0;
@@ -788,8 +790,12 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   }
   // PodTopologySpread: the keys' domains, the constraint table's counts, the classes' eligibility
   c->pts = kh::PtsArgs{};
+  c->ipa = kh::IpaArgs{};
+  c->ipa_pods_bound = 0;
   const bool pts = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_PTS) != 0;
-  if (!e && pts && s->pts_keys > 0) {
+  const bool ipa = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_IPA) != 0;
+  // (the topology keys serve both plugins: loaded when either runs)
+  if (!e && (pts || ipa) && s->pts_keys > 0) {
     if (s->pts_keys > KOORDHIP_PTS_KEYS || s->pts_cons < 0 || s->pts_cons > KOORDHIP_PTS_CONS || s->pts_classes < 0 ||
         s->pts_classes > KOORDHIP_PTS_CLASSES || !s->pts_dom || !s->pts_elig || (s->pts_cons > 0 && !s->pts_cnt))
       return fail(KOORDHIP_EINVAL, "PodTopologySpread tables outside KOORDHIP_PTS_* or a column missing");
@@ -826,6 +832,40 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     pa.score = (c->cfg.score_plugins & KOORDHIP_PLUGIN_PTS) ? 1 : 0;
     for (int cc = 0; cc < KOORDHIP_PTS_CONS; cc++) pa.cons_key[cc] = cc < s->pts_cons ? s->pts_cons_key[cc] : 0;
   }
+  // InterPodAffinity: the count entries over those keys
+  if (!e && ipa && s->ipa_ents > 0) {
+    if (s->ipa_ents > KOORDHIP_IPA_ENTRIES || !s->ipa_cnt || !c->pts.dom)
+      return fail(KOORDHIP_EINVAL, "InterPodAffinity: more than KOORDHIP_IPA_ENTRIES entries, ipa_cnt missing, or no "
+                                   "topology keys (pts_keys / pts_dom)");
+    for (int q = 0; q < s->ipa_ents; q++)
+      if (s->ipa_ent_key[q] < 0 || s->ipa_ent_key[q] >= s->pts_keys)
+        return fail(KOORDHIP_EINVAL, "InterPodAffinity: an entry's key is out of range");
+    int64_t most = 0;  // the largest entry total: what a count can reach before the stream adds its pods
+    for (int q = 0; q < s->ipa_ents; q++) {
+      int64_t tot = 0;
+      for (int32_t i = 0; i < n; i++) {
+        const int32_t v = s->ipa_cnt[(size_t)q * n + i];
+        if (v < 0) return fail(KOORDHIP_EINVAL, "InterPodAffinity: a negative ipa_cnt");
+        tot += v;
+      }
+      most = std::max(most, tot);
+    }
+    c->ipa_pods_bound = most;
+    int32_t *ic = nullptr, *sums = nullptr;
+    e = dev_alloc(c, &ic, (size_t)n * s->ipa_ents);
+    if (!e) e = upload(c, ic, s->ipa_cnt, (size_t)n * s->ipa_ents);
+    if (!e) e = dev_alloc(c, &sums, (size_t)kh::IPA_SUMS);
+    kh::IpaArgs &ia = c->ipa;
+    ia.dom = c->pts.dom;
+    ia.cnt = ic;
+    ia.sums = sums;
+    ia.ents = s->ipa_ents;
+    ia.host = s->pts_hostname;
+    ia.filt = (c->cfg.filter_plugins & KOORDHIP_PLUGIN_IPA) ? 1 : 0;
+    ia.score = (c->cfg.score_plugins & KOORDHIP_PLUGIN_IPA) ? 1 : 0;
+    for (int q = 0; q < KOORDHIP_IPA_ENTRIES; q++) ia.ent_key[q] = q < s->ipa_ents ? s->ipa_ent_key[q] : 0;
+  }
+  c->ipa.w = (c->cfg.score_plugins & KOORDHIP_PLUGIN_IPA) ? c->cfg.ext_weight[4] : 0;
   c->pts.w = (c->cfg.score_plugins & KOORDHIP_PLUGIN_PTS) ? c->cfg.ext_weight[3] : 0;
   // (a profile scoring PodTopologySpread on a snapshot without tables: every
   // node scores 100, as for pods without constraints)
@@ -866,16 +906,17 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   const uint32_t known = KOORDHIP_PLUGIN_FIT | KOORDHIP_PLUGIN_LOADAWARE | KOORDHIP_PLUGIN_NUMA |
                          KOORDHIP_PLUGIN_RESERVATION | KOORDHIP_PLUGIN_NODE_STATIC | KOORDHIP_PLUGIN_BALANCED |
                          KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE |
-                         KOORDHIP_PLUGIN_PTS;
+                         KOORDHIP_PLUGIN_PTS | KOORDHIP_PLUGIN_IPA;
   if ((cfg->filter_plugins | cfg->score_plugins) & ~known) return fail(KOORDHIP_EINVAL, "unknown plugin bit");
   if (cfg->filter_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE))
     return fail(KOORDHIP_EINVAL, "the NodeAffinity / TaintToleration Score bits are Score plugins");
   for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) {
     static const uint32_t xb[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
-                                                       KOORDHIP_PLUGIN_TAINT_SCORE, KOORDHIP_PLUGIN_PTS};
+                                                       KOORDHIP_PLUGIN_TAINT_SCORE, KOORDHIP_PLUGIN_PTS,
+                                                       KOORDHIP_PLUGIN_IPA};
     if ((cfg->score_plugins & xb[e]) && (cfg->ext_weight[e] < 1 || cfg->ext_weight[e] > 100))
-      return fail(KOORDHIP_EINVAL,
-                  "DeviceShare / NodeAffinity / TaintToleration / PodTopologySpread score weight must be in [1, 100]");
+      return fail(KOORDHIP_EINVAL, "DeviceShare / NodeAffinity / TaintToleration / PodTopologySpread / "
+                                   "InterPodAffinity score weight must be in [1, 100]");
   }
   for (int k = 0; k < 5; k++)
     if (cfg->dev_res_weight[k] < 0 || cfg->dev_res_weight[k] > 100)
@@ -937,7 +978,8 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->dc.dev_most = cfg->dev_most_allocated ? 1 : 0;
   for (int k = 0; k < 5; k++) c->dc.dev_w[k] = cfg->dev_res_weight[k];
   // normalized scores couple a pod's nodes: the exact sequential cycle
-  c->seq = ((cfg->filter_plugins | cfg->score_plugins) & (KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_PTS)) ||
+  c->seq = ((cfg->filter_plugins | cfg->score_plugins) &
+            (KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_PTS | KOORDHIP_PLUGIN_IPA)) ||
            (cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
@@ -976,6 +1018,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
     if (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) max_total += 100 * (int64_t)cfg->ext_weight[1];
     if (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) max_total += 100 * (int64_t)cfg->ext_weight[2];
     if (cfg->score_plugins & KOORDHIP_PLUGIN_PTS) max_total += 100 * (int64_t)cfg->ext_weight[3];
+    if (cfg->score_plugins & KOORDHIP_PLUGIN_IPA) max_total += 100 * (int64_t)cfg->ext_weight[4];
     c->dc.resv_b1 = (int32_t)max_total + 1;
     if (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION) {
       // the ranking totals of resv.hpp: one normalised Reservation unit must
@@ -1399,8 +1442,16 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
         cols.push_back({pa.cnt + (size_t)cc * c->n, rows->pts_cnt + (size_t)cc * m, 4, false, "pts_cnt"});
       cols.push_back({const_cast<uint16_t *>(pa.elig), rows->pts_elig, 2, false, "pts_elig"});
     }
+    // InterPodAffinity rows: the loaded snapshot's entries
+    if (rows->ipa_ents > 0) {
+      const kh::IpaArgs &ia = c->ipa;
+      if (!ia.cnt || rows->ipa_ents != ia.ents || !rows->ipa_cnt)
+        return fail(KOORDHIP_EINVAL, "update rows: InterPodAffinity columns must match the loaded snapshot's entries");
+      for (int q = 0; q < ia.ents; q++)
+        cols.push_back({ia.cnt + (size_t)q * c->n, rows->ipa_cnt + (size_t)q * m, 4, false, "ipa_cnt"});
+    }
   } else if (rows->dev_slots > 0 || rows->xalloc || rows->static_score[0] || rows->static_score[1] ||
-             rows->pts_keys > 0) {
+             rows->pts_keys > 0 || rows->ipa_ents > 0) {
     return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score rows need DeviceShare or a normalized Score "
                                  "plugin in the profile");
   }
@@ -1572,7 +1623,11 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
     if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
     const size_t n = (size_t)c->n, NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
     std::vector<int32_t> sc(scores ? (size_t)n_pods * NPX * n : 0);
-    if (int e = koordhip_eval_ext(c, pods, nullptr, n_pods, status, scores ? sc.data() : nullptr, topk, k)) return e;
+    std::vector<uint16_t> st16(status ? (size_t)n_pods * n : 0);
+    if (int e = koordhip_eval_ext(c, pods, nullptr, n_pods, status ? st16.data() : nullptr,
+                                  scores ? sc.data() : nullptr, topk, k))
+      return e;
+    for (size_t q = 0; q < st16.size(); q++) status[q] = (uint8_t)st16[q];  // (no ext: no InterPodAffinity bit)
     if (scores)
       for (int32_t p = 0; p < n_pods; p++)
         std::memcpy(scores + (size_t)p * KOORDHIP_NPLUGINS * n, sc.data() + (size_t)p * NPX * n,
@@ -1693,13 +1748,34 @@ static int check_pod_ext(const koordhip_pod_ext *x, int32_t n, bool *any) {
     for (int j = 0; j < e.pts_n; j++)
       if (e.pts_c[j] >= KOORDHIP_PTS_CONS || e.pts_skew[j] < 1 || (e.pts_fl[j] & ~(KOORDHIP_PTS_HARD | KOORDHIP_PTS_SELF)))
         return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: a topology spread constraint out of range");
-    *any = *any || e.flags != 0 || e.xmask != 0 || e.pts_n != 0 || e.pts_match != 0;
+    if (e.ipa_flags & ~(uint32_t)KOORDHIP_IPA_SELF) return fail(KOORDHIP_EINVAL, "unknown koordhip_pod_ext.ipa_flags bit");
+    for (int q = 0; q < KOORDHIP_IPA_ENTRIES; q++)
+      if (((e.ipa_score >> q) & 1u) != (e.ipa_w[q] != 0 ? 1u : 0u))
+        return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: ipa_score must be exactly the entries with a nonzero ipa_w");
+    *any = *any || e.flags != 0 || e.xmask != 0 || e.pts_n != 0 || e.pts_match != 0 ||
+           (e.ipa_inc | e.ipa_aff | e.ipa_anti | e.ipa_score) != 0;
+  }
+  return 0;
+}
+
+// the pods' InterPodAffinity entries against the loaded snapshot's; the raw
+// Score must stay in int32 (sum of |w| x the most pods an entry can count)
+static int check_pod_ipa(const koordhip_ctx *c, const koordhip_pod_ext *x, int32_t n) {
+  const uint32_t valid = c->ipa.ents >= 32 ? ~0u : ((1u << std::max(0, c->ipa.ents)) - 1u);
+  for (int32_t j = 0; j < n; j++) {
+    if ((x[j].ipa_inc | x[j].ipa_aff | x[j].ipa_anti | x[j].ipa_score) & ~valid)
+      return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: an InterPodAffinity entry beyond the snapshot's ipa_ents");
+    int64_t wsum = 0;
+    for (int q = 0; q < KOORDHIP_IPA_ENTRIES; q++) wsum += std::abs((int64_t)x[j].ipa_w[q]);
+    if (wsum * (c->ipa_pods_bound + n) >= (1ll << 31))
+      return fail(KOORDHIP_EINVAL, "koordhip_pod_ext: InterPodAffinity weights x counts could overflow int32");
   }
   return 0;
 }
 
 // the pods' topology spread constraints against the loaded snapshot's tables
 static int check_pod_pts(const koordhip_ctx *c, const koordhip_pod_ext *x, int32_t n) {
+  if (int e = check_pod_ipa(c, x, n)) return e;
   if (c->pts.keys <= 0) return 0;
   for (int32_t j = 0; j < n; j++) {
     if (x[j].pts_n && x[j].pts_class >= c->pts.classes)
@@ -1782,6 +1858,17 @@ int koordhip_read_devices(koordhip_ctx *c, int64_t *dev_used, int64_t *xrequeste
   return 0;
 }
 
+int koordhip_read_ipa(koordhip_ctx *c, int32_t *cnt) {
+  if (!c || !cnt) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const size_t nb = (size_t)c->n * std::max(0, c->ipa.ents) * sizeof(int32_t);
+  if (!c->ipa.cnt || !nb) return 0;
+  HIP_TRY(hipMemcpy(cnt, c->ipa.cnt, nb, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int koordhip_read_pts(koordhip_ctx *c, int32_t *cnt) {
   if (!c || !cnt) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
@@ -1794,7 +1881,7 @@ int koordhip_read_pts(koordhip_ctx *c, int32_t *cnt) {
 }
 
 int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods,
-                      uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
+                      uint16_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
@@ -1811,7 +1898,10 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
     const int32_t n = c->n;
     const int NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
     std::vector<int32_t> sc(scores ? (size_t)n_pods * KOORDHIP_NPLUGINS * n : 0);
-    if (int e = koordhip_eval(c, pods, n_pods, status, scores ? sc.data() : nullptr, topk, k)) return e;
+    std::vector<uint8_t> st8(status ? (size_t)n_pods * n : 0);
+    if (int e = koordhip_eval(c, pods, n_pods, status ? st8.data() : nullptr, scores ? sc.data() : nullptr, topk, k))
+      return e;
+    for (size_t q = 0; q < st8.size(); q++) status[q] = st8[q];
     if (scores)
       for (int32_t p = 0; p < n_pods; p++) {
         std::memcpy(scores + (size_t)p * NPX * n, sc.data() + (size_t)p * KOORDHIP_NPLUGINS * n,
@@ -1826,11 +1916,11 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
   const int32_t per = std::max<int32_t>(1, std::min<int32_t>(kMaxBatch, (int32_t)((256ll << 20) / (48ll * std::max(n, 1)))));
   kh::DevPod *dp = nullptr;
   kh::DevPodX *dx = nullptr;
-  uint8_t *dst = nullptr;
+  uint8_t *dst = nullptr, *dist = nullptr;
   int32_t *dsc4 = nullptr, *dsc = nullptr, *work = nullptr;
   uint64_t *dk = nullptr;
   auto cleanup = [&]() {
-    for (void *p : {(void *)dp, (void *)dx, (void *)dst, (void *)dsc4, (void *)dsc, (void *)work, (void *)dk})
+    for (void *p : {(void *)dp, (void *)dx, (void *)dst, (void *)dist, (void *)dsc4, (void *)dsc, (void *)work, (void *)dk})
       if (p) (void)hipFree(p);
   };
   std::vector<kh::DevPod> hp;
@@ -1838,6 +1928,7 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
   if (hipMalloc(&dp, (size_t)per * sizeof(kh::DevPod)) != hipSuccess ||
       (ext && hipMalloc(&dx, (size_t)per * sizeof(kh::DevPodX)) != hipSuccess) ||
       hipMalloc(&dst, (size_t)per * std::max(n, 1)) != hipSuccess ||
+      hipMalloc(&dist, (size_t)per * std::max(n, 1)) != hipSuccess ||
       hipMalloc(&dsc4, (size_t)per * KOORDHIP_NPLUGINS * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
       hipMalloc(&dsc, (size_t)per * NPX * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
       hipMalloc(&work, (size_t)per * kh::SEQ_WORK_PLANES * std::max(n, 1) * sizeof(int32_t)) != hipSuccess ||
@@ -1847,6 +1938,7 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
   }
   const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
   std::vector<uint64_t> hk(topk ? (size_t)per * k : 0);
+  std::vector<uint8_t> h8(status ? (size_t)per * n : 0), hi8(status ? (size_t)per * n : 0);
   int e = 0;
   for (int32_t p0 = 0; p0 < n_pods && !e; p0 += per) {
     const int32_t np = std::min(per, n_pods - p0);
@@ -1855,11 +1947,12 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
       e = fail(KOORDHIP_EDEVICE, "copy pods");
       break;
     }
-    if (kh::launch_eval_full(c->dc, c->d, dp, np, dst, dsc4, c->stream) != hipSuccess ||
+    if (hipMemsetAsync(dist, 0, (size_t)np * n, c->stream) != hipSuccess ||
+        kh::launch_eval_full(c->dc, c->d, dp, np, dst, dsc4, c->stream) != hipSuccess ||
         hipMemcpy2DAsync(dsc, (size_t)NPX * n * sizeof(int32_t), dsc4, (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t),
                          (size_t)KOORDHIP_NPLUGINS * n * sizeof(int32_t), np, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
-        kh::launch_seq_eval(c->dc, c->d, dp, dx, np, rs, dst, dsc, work, topk ? k : 0, dk, c->pts, c->stream) !=
-            hipSuccess) {
+        kh::launch_seq_eval(c->dc, c->d, dp, dx, np, rs, dst, dist, dsc, work, topk ? k : 0, dk, c->pts, c->ipa,
+                            c->stream) != hipSuccess) {
       e = fail(KOORDHIP_EDEVICE, "eval_ext launch");
       break;
     }
@@ -1867,8 +1960,15 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
       e = fail(KOORDHIP_EDEVICE, "eval sync");
       break;
     }
-    if (status && hipMemcpy(status + (size_t)p0 * n, dst, (size_t)np * n, hipMemcpyDeviceToHost) != hipSuccess)
-      e = fail(KOORDHIP_EDEVICE, "copy status");
+    if (status) {
+      if (hipMemcpy(h8.data(), dst, (size_t)np * n, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(hi8.data(), dist, (size_t)np * n, hipMemcpyDeviceToHost) != hipSuccess) {
+        e = fail(KOORDHIP_EDEVICE, "copy status");
+      } else {
+        for (size_t q = 0; q < (size_t)np * n; q++)
+          status[(size_t)p0 * n + q] = (uint16_t)(h8[q] | (hi8[q] ? KOORDHIP_ST_IPA_FAIL : 0u));
+      }
+    }
     if (!e && scores &&
         hipMemcpy(scores + (size_t)p0 * NPX * n, dsc, (size_t)np * NPX * n * sizeof(int32_t), hipMemcpyDeviceToHost) !=
             hipSuccess)
@@ -1996,7 +2096,7 @@ int seq_place(koordhip_ctx *c) {
   if (!c->d_seqdesc) HIP_TRY(hipMalloc(&c->d_seqdesc, kh::seq_desc_bytes()));
   HIP_TRY(kh::launch_seq(c->dc, c->d, c->d_pods, c->podx_staged ? c->d_podx : nullptr, np, G, c->d_seqg, tmo,
                          c->d_out, c->d_cpus, dev ? c->d_devout : nullptr, rs, stamps ? c->d_dbg : nullptr,
-                         c->d_seqdesc, c->pts, c->stream));
+                         c->d_seqdesc, c->pts, c->ipa, c->stream));
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   if (stamps) {
     uint64_t h[6];
@@ -2367,6 +2467,7 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
     v.push_back({c->d.dv.used, n * KOORDHIP_DEV_TYPES * (size_t)c->d.dv.slots * KOORDHIP_DEV_RES * sizeof(int64_t)});
   if (c->d.dv.xreq) v.push_back({c->d.dv.xreq, n * KOORDHIP_NXRES * sizeof(int64_t)});
   if (c->pts.cnt) v.push_back({c->pts.cnt, n * (size_t)std::max(1, c->pts.cons) * sizeof(int32_t)});
+  if (c->ipa.cnt) v.push_back({c->ipa.cnt, n * (size_t)c->ipa.ents * sizeof(int32_t)});
   if (c->dc.resv) {
     const size_t sl = (size_t)c->d.rv.slots;
     v.push_back({c->d.rv.rd[0], b * sl});

@@ -31,6 +31,9 @@ struct DevPodX {
   uint8_t pts_fl[KOORDHIP_PTS_POD];
   int32_t pts_skew[KOORDHIP_PTS_POD];
   int32_t pts_reserved;
+  uint32_t ipa_inc, ipa_aff, ipa_anti, ipa_score, ipa_flags;
+  int32_t ipa_reserved;
+  int32_t ipa_w[KOORDHIP_IPA_ENTRIES];
 };
 static_assert(sizeof(DevPodX) == sizeof(koordhip_pod_ext), "DevPodX mirrors koordhip_pod_ext");
 

@@ -5,15 +5,19 @@
 
 #include "dev.hpp"
 #include "kernels.h"
+#include "ipa.hpp"
 #include "pts.hpp"
 
 namespace kh {
 
 // Granules: phases A, B, 0 (PodTopologySpread hostname minimum), P (its raw
 // Score min / max), each [2 parities][grid][SEQ_GRAN] u64, then the commit
-// result ring (2 words), then the spin timeout word on its own 64 B.
-constexpr int SEQ_GRAN = 16;
-constexpr int SEQ_WORK_PLANES = 5;  // koordhip_eval_ext's work rows: total, 3 raw, PodTopologySpread raw
+// result ring (2 words), then the spin timeout word on its own 64 B.  Phase A
+// uses words 0..5 (feasible count, raw maxima, best key), 6..14
+// (PodTopologySpread's soft pairs) and 15..16 (InterPodAffinity's raw min / max).
+constexpr int SEQ_GRAN = 32;
+constexpr int SEQ_WORK_PLANES = 6;  // koordhip_eval_ext's work rows: total, 3 raw, PodTopologySpread raw,
+                                    // InterPodAffinity raw
 constexpr size_t seq_granule_words(int grid) { return (size_t)8 * grid * SEQ_GRAN + 8; }
 constexpr size_t seq_tmo_offset(int grid) { return seq_granule_words(grid) * sizeof(uint64_t); }
 constexpr size_t seq_granule_bytes(int grid) { return seq_tmo_offset(grid) + 64; }
@@ -27,17 +31,18 @@ constexpr size_t seq_granule_bytes(int grid) { return seq_tmo_offset(grid) + 64;
 hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                       int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
                       uint32_t *out_dev, int32_t rs, uint64_t *dbg, void *desc, const PtsArgs &pts,
-                      hipStream_t s);
+                      const IpaArgs &ipa, hipStream_t s);
 // desc: a device buffer of seq_desc_bytes() the launch copies the config and
 // the column descriptors into (the commit reads them from there)
 constexpr size_t seq_desc_cfg_bytes() { return (sizeof(DevCfg) + 15) & ~(size_t)15; }
 constexpr size_t seq_desc_bytes() { return seq_desc_cfg_bytes() + sizeof(DevNodes); }
-// parity: status bits (ORed into status: k_eval_full writes them first), the
+// parity: status bits (ORed into status: k_eval_full writes them first;
+// InterPodAffinity's into ipa_status [np][n], 1 = its Filter fails), the
 // normalized plugins' raw planes of scores ([np][NPLUGINS + NEXT][n]), and
 // the top-k of the normalized totals per pod; work: [np][SEQ_WORK_PLANES][n] int32
 hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
-                           int32_t rs, uint8_t *status, int32_t *scores, int32_t *work, int32_t k, uint64_t *topk,
-                           const PtsArgs &pts, hipStream_t s);
+                           int32_t rs, uint8_t *status, uint8_t *ipa_status, int32_t *scores, int32_t *work, int32_t k,
+                           uint64_t *topk, const PtsArgs &pts, const IpaArgs &ipa, hipStream_t s);
 // the k_seq instantiation launch_seq runs for this config, as rocprofv3 names it
 const char *seq_kernel_name(const DevCfg &c);
 

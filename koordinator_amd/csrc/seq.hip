@@ -35,6 +35,7 @@
 #include <type_traits>
 
 #include "dev.hpp"
+#include "ipa.hpp"
 #include "pts.hpp"
 #include "seq.h"
 
@@ -63,6 +64,7 @@ struct SeqArgs {
   // hostname minimum, gp the raw Score's min / max, gr the commit result
   PtsArgs pts;
   uint64_t *g0, *gp, *gr;
+  IpaArgs ipa;  // InterPodAffinity: the count entries (ents 0: off)
 };
 
 __device__ __forceinline__ uint64_t seq_stamp() {
@@ -129,6 +131,7 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
   raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   raw[3] = 0;  // PodTopologySpread: its own phases (pts.hpp)
+  raw[4] = 0;  // InterPodAffinity: ipa.hpp
   return t;
 }
 
@@ -359,15 +362,19 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
   __shared__ uint64_t s_key[SEQ_THREADS / 64];
   __shared__ int32_t s_stop;
   __shared__ PtsLds L;
+  __shared__ IpaLds IL;
   const int t = threadIdx.x;
   const int32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t ext = a.ext;
-  const int32_t zero[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0};
+  const int32_t zero[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
   const PtsArgs &pa = a.pts;
   const bool pts = pa.keys > 0;  // the snapshot has PodTopologySpread tables (and the plugin runs)
+  const IpaArgs &ia = a.ipa;
+  const bool ipa = ia.ents > 0;  // the snapshot has InterPodAffinity entries (and the plugin runs)
   DevPodX none{};
   for (int q = 0; q < DT; q++) none.req[q][0] = none.req[q][1] = none.req[q][2] = q == 0 ? -1 : 0;
   if (pts) pts_init(pa, d.n, L, t, SEQ_THREADS);
+  if (ipa) ipa_load(ia, IL, t, SEQ_THREADS);
   const bool dbg = a.dbg != nullptr && b == 0 && t == 0;
   uint64_t ts = dbg ? seq_stamp() : 0, acc[5] = {0, 0, 0, 0, 0};
   auto lap = [&](int q) {
@@ -387,6 +394,12 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     //      the hard-eligible nodes (its own hand-off)
     const PtsPod q = pts ? pts_pod(pa, x) : PtsPod{};
     const bool soft = q.on && q.ns > 0;
+    // InterPodAffinity: Filter entries, and Score entries (weights read from
+    // the staged record: a register copy of 32 weights would spill)
+    const bool iaf = ipa && ia.filt && (x.ipa_aff | x.ipa_anti) != 0u;
+    const uint32_t isc = (ipa && ia.score && a.podx) ? x.ipa_score : 0u;
+    const int32_t *iw = isc ? a.podx[p].ipa_w : nullptr;
+    const bool wide = soft || isc != 0u;  // phase A publishes words 6..16 too
     int32_t hmin = INT32_MAX;
     if (q.on) {
       pts_prep(pa, q, L, t);
@@ -422,14 +435,21 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     (void)pts;
     int32_t v4[4] = {0, 0, 0, 0};  // feasible count, raw maxima
     uint64_t key0 = 0;
+    int32_t imn = INT32_MAX, imx = INT32_MIN;  // InterPodAffinity raw Score over this block's feasible nodes
 #pragma unroll 1
     for (int k = 0; k < a.npt; k++) {
-      int32_t tk = -1, rk[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, -1};
+      int32_t tk = -1, rk[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, -1, 0};
       const int32_t i = (k * G + b) * SEQ_THREADS + t;
       if (i < d.n) {
         tk = seq_eval<SM>(c, d, pod, x, i, a.rs != 0, rk, nullptr);
         rk[3] = -1;
         if (tk >= 0 && q.on && q.nh > 0 && !pts_filter(pa, q, L, hmin, d.n, i)) tk = -1;
+        if (tk >= 0 && iaf && !ipa_filter(ia, IL, x, d.n, i)) tk = -1;
+        if (tk >= 0 && isc) {
+          rk[4] = ipa_raw(ia, IL, isc, iw, d.n, i);
+          imn = min(imn, rk[4]);
+          imx = max(imx, rk[4]);
+        }
         if (tk >= 0) {
           v4[0]++;
 #pragma unroll
@@ -443,17 +463,28 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
 #pragma unroll
       for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) s_raw[k][e][t] = rk[e];
     }
-    seq_block_reduce(v4, key0, s_red, s_key, t);
+    if (isc) {
+      if (t == 0) {
+        IL.mm[0] = INT32_MAX;
+        IL.mm[1] = INT32_MIN;
+      }
+      __syncthreads();
+      atomicMin(&IL.mm[0], imn);
+      atomicMax(&IL.mm[1], imx);
+    }
+    seq_block_reduce(v4, key0, s_red, s_key, t);  // (its barriers order the atomics above)
     if (t == 0) {
       uint64_t *g = a.ga + ((size_t)par * G + b) * SEQ_GRAN;
 #pragma unroll
       for (int e = 0; e < 4; e++) put_granule(g + e, eA, (uint32_t)v4[e]);
       put_granule(g + 4, eA, (uint32_t)(key0 >> 32));
       put_granule(g + 5, eA, (uint32_t)key0);
-      if (soft) {
-        put_granule(g + 6, eA, (uint32_t)L.nfni);
+      if (wide) {
+        put_granule(g + 6, eA, soft ? (uint32_t)L.nfni : 0u);
 #pragma unroll
-        for (int e = 0; e < 2 * PK; e++) put_granule(g + 7 + e, eA, (&L.smask[0][0])[e]);
+        for (int e = 0; e < 2 * PK; e++) put_granule(g + 7 + e, eA, soft ? (&L.smask[0][0])[e] : 0u);
+        put_granule(g + 15, eA, isc ? (uint32_t)IL.mm[0] : 0u);
+        put_granule(g + 16, eA, isc ? (uint32_t)IL.mm[1] : 0u);
       }
     }
     lap(0);
@@ -461,14 +492,36 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     //      best key under zero maxima (+ PodTopologySpread's PreScore pairs)
     int32_t g4[4];
     uint64_t win;
-    if (soft) {
-      if (!seq_gather<7 + 2 * PK>(a.ga + (size_t)par * G * SEQ_GRAN, eA, G, g4, win, s_red, s_key, &s_stop, a.tmo, t))
+    if (wide) {
+      if (!seq_gather<17>(a.ga + (size_t)par * G * SEQ_GRAN, eA, G, g4, win, s_red, s_key, &s_stop, a.tmo, t))
         return;
     } else {
       if (!seq_gather<6>(a.ga + (size_t)par * G * SEQ_GRAN, eA, G, g4, win, s_red, s_key, &s_stop, a.tmo, t)) return;
     }
     const int32_t nf_all = g4[0];
     lap(1);
+    // InterPodAffinity: the grid's raw min / max over the feasible nodes
+    // (words 15, 16: their epochs were checked by the sweep above)
+    int32_t gimn = 0, gimx = 0;
+    if (isc) {
+      __syncthreads();
+      if (t == 0) {
+        IL.mm[0] = INT32_MAX;
+        IL.mm[1] = INT32_MIN;
+      }
+      __syncthreads();
+      for (int32_t g = t; g < G; g += SEQ_THREADS) {
+        const uint64_t *gg = a.ga + ((size_t)par * G + g) * SEQ_GRAN;
+        atomicMin(&IL.mm[0], (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 15, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT));
+        atomicMax(&IL.mm[1], (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 16, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT));
+      }
+      __syncthreads();
+      gimn = IL.mm[0];
+      gimx = IL.mm[1];
+    }
+    const bool inorm = isc && gimx > gimn;  // else every normalized InterPodAffinity score is 0
     int32_t pmin = 0, pmax = 0;
     if (soft) {
       // ---- PodTopologySpread PreScore + Score: weights from the grid's pairs,
@@ -523,7 +576,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
       seq_put_minmax(a.gp + ((size_t)par * G + b) * SEQ_GRAN, eP, L, t);
       if (!seq_gather_minmax(a.gp + (size_t)par * G * SEQ_GRAN, eP, G, pmin, pmax, L, &s_stop, a.tmo, t)) return;
     }
-    if ((g4[1] | g4[2] | g4[3]) || soft) {
+    if ((g4[1] | g4[2] | g4[3]) || soft || inorm) {
       // ---- phase B: normalized totals, this block's best key
       const int32_t gmx[KOORDHIP_NEXT_PLUGINS] = {g4[1], g4[2], g4[3], 0};
       uint64_t best = 0;
@@ -534,7 +587,8 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
         const int32_t i = (k * G + b) * SEQ_THREADS + t;
         const int32_t rk[KOORDHIP_NEXT_PLUGINS] = {s_raw[k][0][t], s_raw[k][1][t], s_raw[k][2][t], 0};
         const int32_t pt = soft ? pa.w * pts_norm(s_raw[k][3][t], pmin, pmax) : pts_const;
-        const uint64_t key = make_key(tk + ext_total(c, ext, rk, gmx) + pt, i);
+        const int32_t it = inorm ? ia.w * ipa_norm(s_raw[k][4][t], gimn, gimx) : 0;
+        const uint64_t key = make_key(tk + ext_total(c, ext, rk, gmx) + pt + it, i);
         best = key > best ? key : best;
       }
       int32_t u4[4] = {0, 0, 0, 0};
@@ -555,6 +609,8 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     // PodTopologySpread: a placed pod counts for the table constraints it
     // matches; a Reserve that may fail (devices, cpusets) tells the others
     const uint32_t pmatch = (pts && wn >= 0) ? x.pts_match : 0u;
+    // InterPodAffinity: the entries counting the placed pod
+    const uint32_t imatch = (ipa && wn >= 0) ? x.ipa_inc : 0u;
     bool may_fail = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) && (x.flags & KOORDHIP_PODX_DEVICE);
     if constexpr (SM >= 1) may_fail = may_fail || (numa_on(c) && numa_active(pod, c));
     if (t == 0) {
@@ -564,23 +620,28 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
         seq_commit<SM>(a.gc, a.gd, a.pods + p, a.podx ? a.podx + p : nullptr, wn, nf_all, a.rs != 0, a.out_node + p,
                        a.out_cpus ? a.out_cpus + (size_t)p * NW : nullptr,
                        a.out_dev ? a.out_dev + (size_t)p * DT : nullptr);
-        if (pmatch) {
+        if (pmatch | imatch) {
           const bool done = __hip_atomic_load(a.out_node + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == wn;
-          if (done)
+          if (done) {
             for (int cc = 0; cc < pa.cons; cc++)
               if ((pmatch >> cc) & 1u) pa.cnt[(size_t)cc * d.n + wn] += 1;
+            ipa_commit_cols(ia, imatch, d.n, wn);
+          }
           if (may_fail) put_granule(a.gr + par, eP, done ? 1u : 0u);
         }
         if (a.dbg) atomicAdd((unsigned long long *)&a.dbg[5], (unsigned long long)(seq_stamp() - c0));
       }
-      if (pmatch) {
+      if (pmatch | imatch) {
         bool done = true;
         if (may_fail) {
           uint32_t v[1];
           if (!sweep<1>(a.gr + par, eP, v, a.tmo)) s_stop = 1;
           done = v[0] != 0;
         }
-        if (done) pts_commit_tables(pa, L, pmatch, d.n, wn);
+        if (done) {
+          if (pmatch) pts_commit_tables(pa, L, pmatch, d.n, wn);
+          if (imatch) ipa_commit_tables(ia, IL, imatch, d.n, wn);
+        }
       }
     }
     __syncthreads();  // the owner's commit before its next evaluation of w
@@ -691,14 +752,63 @@ __global__ __launch_bounds__(256) void k_pts_eval(PtsArgs pa, int32_t n, const D
     }
 }
 
+// The launch's sums (one workgroup-local LDS table per block, then one global
+// add per nonzero cell).  sums must be zeroed before.
+__global__ __launch_bounds__(256) void k_ipa_sums(IpaArgs a, int32_t n) {
+  __shared__ int32_t s[IPA_SUMS];
+  for (int x = threadIdx.x; x < IPA_SUMS; x += blockDim.x) s[x] = 0;
+  __syncthreads();
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    for (int e = 0; e < a.ents; e++) {
+      const int32_t v = a.cnt[(size_t)e * n + i];
+      if (v == 0) continue;
+      const int k = a.ent_key[e];
+      const int32_t d = a.dom[(size_t)k * n + i];
+      if (d < 0) continue;
+      atomicAdd(&s[IE * PD + e], v);
+      if (!((a.host >> k) & 1u)) atomicAdd(&s[e * PD + d], v);
+    }
+  __syncthreads();
+  for (int x = threadIdx.x; x < IPA_SUMS; x += blockDim.x)
+    if (s[x]) atomicAdd(&a.sums[x], s[x]);
+}
+
+// InterPodAffinity for the parity evaluator: one workgroup per pod over every
+// node (the launch's sums from k_ipa_sums): the Filter's status plane and
+// infeasible total, the raw Score plane and work plane 5 (every node).
+__global__ __launch_bounds__(256) void k_ipa_eval(IpaArgs a, int32_t n, const DevPodX *__restrict__ podx,
+                                                  int32_t n_pods, uint8_t *__restrict__ ist,
+                                                  int32_t *__restrict__ scores, int32_t *__restrict__ work) {
+  __shared__ IpaLds L;
+  const int32_t p = blockIdx.x, t = threadIdx.x;
+  if (p >= n_pods || !podx) return;
+  const DevPodX &x = podx[p];
+  const size_t NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
+  int32_t *wk = work + (size_t)p * SEQ_WORK_PLANES * n;
+  int32_t *w5 = wk + (size_t)5 * n;
+  int32_t *plane = scores ? scores + ((size_t)p * NPX + KOORDHIP_NPLUGINS + 4) * n : nullptr;
+  ipa_load(a, L, t, 256);
+  const bool filt = a.filt && (x.ipa_aff | x.ipa_anti) != 0u;
+  const uint32_t sc = a.score ? x.ipa_score : 0u;
+  for (int32_t i = t; i < n; i += 256) {
+    if (filt && !ipa_filter(a, L, x, n, i)) {
+      wk[i] = -1;
+      if (ist) ist[(size_t)p * n + i] = 1;
+    }
+    const int32_t r = sc ? ipa_raw(a, L, sc, x.ipa_w, n, i) : 0;
+    w5[i] = r;
+    if (plane) plane[i] = r;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int32_t *__restrict__ work, int32_t k,
-                                                  int32_t pts_w, uint64_t *__restrict__ out) {
+                                                  int32_t pts_w, int32_t ipa_w, uint64_t *__restrict__ out) {
   __shared__ uint64_t s_k[4];
-  __shared__ int32_t s_m[4][KOORDHIP_NEXT_PLUGINS + 1];
+  __shared__ int32_t s_m[4][KOORDHIP_NEXT_PLUGINS + 2];
   const int32_t p = blockIdx.x, t = threadIdx.x, lane = __lane_id(), wv = t >> 6;
   const int32_t *wk = work + (size_t)p * SEQ_WORK_PLANES * n;
   const uint32_t ext = ext_bits(c);
-  int32_t mx[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0}, pmin = INT32_MAX;
+  int32_t mx[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, INT32_MIN}, pmin = INT32_MAX, imin = INT32_MAX;
   for (int32_t i = t; i < n; i += 256)
     if (wk[i] >= 0) {
       for (int e = 0; e < 3; e++) mx[e] = max(mx[e], wk[(size_t)(e + 1) * n + i]);
@@ -707,17 +817,26 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
         mx[3] = max(mx[3], r);
         pmin = min(pmin, r);
       }
+      const int32_t q = wk[(size_t)5 * n + i];
+      mx[4] = max(mx[4], q);
+      imin = min(imin, q);
     }
   for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) {
     for (int m = 32; m >= 1; m >>= 1) mx[e] = max(mx[e], __shfl_xor(mx[e], m));
     if (lane == 0) s_m[wv][e] = mx[e];
   }
   pmin = pts_wave_min(pmin);
-  if (lane == 0) s_m[wv][KOORDHIP_NEXT_PLUGINS] = pmin;
+  imin = pts_wave_min(imin);
+  if (lane == 0) {
+    s_m[wv][KOORDHIP_NEXT_PLUGINS] = pmin;
+    s_m[wv][KOORDHIP_NEXT_PLUGINS + 1] = imin;
+  }
   __syncthreads();
   for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) mx[e] = max(max(s_m[0][e], s_m[1][e]), max(s_m[2][e], s_m[3][e]));
   pmin = min(min(s_m[0][KOORDHIP_NEXT_PLUGINS], s_m[1][KOORDHIP_NEXT_PLUGINS]),
              min(s_m[2][KOORDHIP_NEXT_PLUGINS], s_m[3][KOORDHIP_NEXT_PLUGINS]));
+  imin = min(min(s_m[0][KOORDHIP_NEXT_PLUGINS + 1], s_m[1][KOORDHIP_NEXT_PLUGINS + 1]),
+             min(s_m[2][KOORDHIP_NEXT_PLUGINS + 1], s_m[3][KOORDHIP_NEXT_PLUGINS + 1]));
   uint64_t last = ~0ull;
   for (int32_t j = 0; j < k; j++) {
     uint64_t best = 0;
@@ -726,7 +845,8 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
       int32_t raw[KOORDHIP_NEXT_PLUGINS];
       for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) raw[e] = wk[(size_t)(e + 1) * n + i];
       const int32_t pt = pts_w ? pts_w * pts_norm(raw[3], pmin, mx[3]) : 0;
-      const uint64_t key = make_key(wk[i] + ext_total(c, ext, raw, mx) + pt, i);
+      const int32_t it = ipa_w ? ipa_w * ipa_norm(raw[4], imin, mx[4]) : 0;
+      const uint64_t key = make_key(wk[i] + ext_total(c, ext, raw, mx) + pt + it, i);
       if (key < last && key > best) best = key;
     }
     best = seq_wave_max(best);
@@ -743,11 +863,16 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
 hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                       int32_t grid, uint64_t *granules, uint32_t *tmo, int32_t *out_node, uint64_t *out_cpus,
                       uint32_t *out_dev, int32_t rs, uint64_t *dbg, void *desc, const PtsArgs &pts,
-                      hipStream_t s) {
+                      const IpaArgs &ipa, hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   SeqArgs a{};
   a.dbg = dbg;
   a.pts = pts;
+  a.ipa = ipa;
+  if (ipa.ents > 0) {  // this launch's domain sums of the count entries
+    if (hipError_t e = hipMemsetAsync(ipa.sums, 0, sizeof(int32_t) * IPA_SUMS, s)) return e;
+    hipLaunchKernelGGL(k_ipa_sums, dim3(std::min<int32_t>(1024, (d.n + 255) / 256)), dim3(256), 0, s, ipa, d.n);
+  }
   // the commit's copies of the config and the column descriptors (desc: 16-B aligned device buffer)
   DevCfg *gc = static_cast<DevCfg *>(desc);
   DevNodes *gd = reinterpret_cast<DevNodes *>(static_cast<char *>(desc) + seq_desc_cfg_bytes());
@@ -790,8 +915,8 @@ const char *seq_kernel_name(const DevCfg &c) {
 }
 
 hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
-                           int32_t rs, uint8_t *status, int32_t *scores, int32_t *work, int32_t k, uint64_t *topk,
-                           const PtsArgs &pts, hipStream_t s) {
+                           int32_t rs, uint8_t *status, uint8_t *ipa_status, int32_t *scores, int32_t *work, int32_t k,
+                           uint64_t *topk, const PtsArgs &pts, const IpaArgs &ipa, hipStream_t s) {
   if (n_pods <= 0 || d.n <= 0) return hipSuccess;
   const dim3 g((d.n + 255) / 256, n_pods);
   switch (seq_mode(c)) {
@@ -799,9 +924,16 @@ hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pod
     case 1: hipLaunchKernelGGL(k_seq_eval<1>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work); break;
     default: hipLaunchKernelGGL(k_seq_eval<0>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work);
   }
+  // InterPodAffinity's Filter before PodTopologySpread's PreScore reads the feasible set
+  if (ipa.ents > 0) {
+    if (hipError_t e = hipMemsetAsync(ipa.sums, 0, sizeof(int32_t) * IPA_SUMS, s)) return e;
+    hipLaunchKernelGGL(k_ipa_sums, dim3(std::min<int32_t>(1024, (d.n + 255) / 256)), dim3(256), 0, s, ipa, d.n);
+    hipLaunchKernelGGL(k_ipa_eval, dim3(n_pods), dim3(256), 0, s, ipa, d.n, podx, n_pods, ipa_status, scores, work);
+  }
   hipLaunchKernelGGL(k_pts_eval, dim3(n_pods), dim3(256), 0, s, pts, d.n, podx, n_pods, status, scores, work);
   if (topk && k > 0)
-    hipLaunchKernelGGL(k_seq_topk, dim3(n_pods), dim3(256), 0, s, c, d.n, work, k, pts.score ? pts.w : 0, topk);
+    hipLaunchKernelGGL(k_seq_topk, dim3(n_pods), dim3(256), 0, s, c, d.n, work, k, pts.score ? pts.w : 0,
+                       ipa.score ? ipa.w : 0, topk);
   return hipGetLastError();
 }
 

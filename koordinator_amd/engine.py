@@ -101,11 +101,11 @@ class PlacementEngine:
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         x = None if ext is None else np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
         p, n = len(pods), self.n
-        st = np.zeros((p, n), np.uint8) if status else None
+        st = np.zeros((p, n), np.uint16) if status else None
         sc = np.zeros((p, abi.NPLUGINS + abi.NEXT_PLUGINS, n), np.int32) if scores else None
         tk = np.zeros((p, k), abi.TOPK_DTYPE) if k else None
         abi.check(self.lib, self.lib.koordhip_eval_ext(
-            self._ctx, pods.ctypes.data, x.ctypes.data if x is not None else None, p, abi.ptr(st, C.c_uint8),
+            self._ctx, pods.ctypes.data, x.ctypes.data if x is not None else None, p, abi.ptr(st, C.c_uint16),
             abi.ptr(sc, C.c_int32), tk.ctypes.data if tk is not None else None, k))
         return {"status": st, "scores": sc, "topk": tk}
 
@@ -129,6 +129,15 @@ class PlacementEngine:
         out = np.zeros((C_, self.n), np.int32)
         if C_:
             abi.check(self.lib, self.lib.koordhip_read_pts(self._ctx, abi.ptr(out, C.c_int32)))
+        return out.T.copy()
+
+    def read_ipa(self) -> np.ndarray:
+        """InterPodAffinity count entries' pods per node [n][ents]."""
+        m = self._table.ipa if self._table is not None else None
+        E = len(m.ent_key) if m is not None else 0
+        out = np.zeros((E, self.n), np.int32)
+        if E:
+            abi.check(self.lib, self.lib.koordhip_read_ipa(self._ctx, abi.ptr(out, C.c_int32)))
         return out.T.copy()
 
     def stage_pods(self, pods: np.ndarray):

@@ -132,6 +132,9 @@ class Informer:
         from .topologyspread import SpreadRegistry
         self.static_classes = StaticClasses()
         self.cluster.spread = SpreadRegistry()
+        from .interpodaffinity import IpaRegistry
+        self.cluster.ipa = IpaRegistry(self.cluster.spread,
+                                       hard_weight=profile.interpodaffinity.hard_pod_affinity_weight)
 
     # ---- full snapshot --------------------------------------------------------
     def table(self, now: float) -> NodeTable:
@@ -375,17 +378,32 @@ class Informer:
             for p in pods:
                 if not self.cluster.spread.covers(p):
                     self._reload = True
+        if self._ipa_on():
+            for p in pods:
+                if not self.cluster.ipa.covers(p):
+                    self._reload = True
         return self._reload
 
     def _spread_on(self) -> bool:
         from .config import PLUGIN_PTS
         return PLUGIN_PTS in self.profile.filters or PLUGIN_PTS in self.profile.scores
 
+    def _ipa_on(self) -> bool:
+        from .config import PLUGIN_IPA
+        return PLUGIN_IPA in self.profile.filters or PLUGIN_IPA in self.profile.scores
+
+    def on_namespace(self, name: str, labels: Dict[str, str]):
+        """Namespace add / update: the labels affinity terms' namespaceSelectors read."""
+        if self.cluster.ipa.ns_labels.get(name) != dict(labels or {}):
+            self.cluster.ipa.ns_labels[name] = dict(labels or {})
+            if self._ipa_on():
+                self._reload = True
+
     def pod_ext_records(self, pods):
         """koordhip_pod_ext records (DeviceShare, extended scalars, topology
         spread constraints in the loaded snapshot's tables)."""
         from .marshal import pod_ext_records
-        return pod_ext_records(pods, self.profile, self.cluster.spread)
+        return pod_ext_records(pods, self.profile, self.cluster.spread, self.cluster.ipa)
 
     def pod_records(self, pods):
         """Pod records with the current owner groups' match masks and static classes."""

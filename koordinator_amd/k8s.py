@@ -174,6 +174,12 @@ class Pod:
     preferred_node_affinity: list = field(default_factory=list)
     # spec.topologySpreadConstraints (topologyspread.TopologySpreadConstraint)
     topology_spread_constraints: list = field(default_factory=list)
+    # spec.affinity.podAffinity / podAntiAffinity (interpodaffinity.PodAffinityTerm,
+    # WeightedPodAffinityTerm): required... and preferredDuringSchedulingIgnoredDuringExecution
+    pod_affinity_required: list = field(default_factory=list)
+    pod_affinity_preferred: list = field(default_factory=list)
+    pod_anti_affinity_required: list = field(default_factory=list)
+    pod_anti_affinity_preferred: list = field(default_factory=list)
 
     @property
     def key(self) -> str:

@@ -201,9 +201,13 @@ def static_keyed(profile: Profile) -> bool:
 def sequential_profile(profile: Profile) -> bool:
     """DeviceShare or a normalized Score: the engine runs the sequential cycle
     and the snapshot carries the ABI 9 columns (NodeTable.enable_ext)."""
-    from .config import NORMALIZED_SCORES, PLUGIN_DEVICESHARE, PLUGIN_PTS
-    return (PLUGIN_DEVICESHARE in profile.filters or PLUGIN_PTS in profile.filters
+    from .config import NORMALIZED_SCORES, PLUGIN_DEVICESHARE, PLUGIN_IPA, PLUGIN_PTS
+    return (PLUGIN_DEVICESHARE in profile.filters or PLUGIN_PTS in profile.filters or PLUGIN_IPA in profile.filters
             or any(x in profile.scores for x in NORMALIZED_SCORES))
+
+
+def _uses(profile: Profile, name: str) -> bool:
+    return name in profile.filters or name in profile.scores
 
 
 def static_class_of(pod: k8s.Pod, profile: Profile, static_classes) -> int:
@@ -311,8 +315,11 @@ class ClusterState:
     node_pods: Dict[str, List[k8s.Pod]] = field(default_factory=dict)  # NodeInfo.Pods per node
     assigned: Dict[str, List[AssignedPod]] = field(default_factory=dict)
     devices: Dict[str, object] = field(default_factory=dict)          # Device CRs by node (deviceshare.Device)
-    # PodTopologySpread: the registry of the pods to schedule (topologyspread.SpreadRegistry)
+    # PodTopologySpread: the registry of the pods to schedule (topologyspread.SpreadRegistry;
+    # its topology keys are InterPodAffinity's too)
     spread: object = None
+    # InterPodAffinity: the count entries (interpodaffinity.IpaRegistry over `spread`'s keys)
+    ipa: object = None
 
 
 def estimate_node(node: k8s.Node) -> k8s.ResourceList:
@@ -596,6 +603,8 @@ def ext_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, pro
             t["xrequested"][i, ds.XRES_INDEX[n]] += v
     if table.has_pts:
         pts_row(table, i, node, cluster, i if node_index is None else node_index)
+    if table.has_ipa:
+        ipa_row(table, i, node, cluster)
     t["static_score"][i] = 0
     if static_scores_of(profile):
         from .nodefilters import static_scores
@@ -625,27 +634,50 @@ def pts_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState, nod
         if d is None:
             raise NewTopologyValue(f"topology value {key}={v!r} is new to the snapshot: rebuild it")
         dom[k] = d
-    cnt, elig = ts.node_pts(reg, node, cluster.node_pods.get(node.name, []))
+    cnt, elig = ts.node_pts(reg, node, cluster.node_pods.get(node.name, [])) if reg.cons or reg.classes else (0, 0)
     table["pts_cnt"][i] = cnt
     table["pts_elig"][i] = elig
 
 
-def pod_ext_records(pods, profile: Profile, spread=None) -> np.ndarray:
-    """koordhip_pod_ext records: DeviceShare requests, extended scalars and
+def ipa_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState):
+    """Row i of the InterPodAffinity count column.  A running pod carrying a
+    term that a pod to schedule matches but the snapshot has no entry for
+    needs a rebuild."""
+    from .interpodaffinity import node_ipa
+    reg = cluster.ipa
+    pods_on_node = cluster.node_pods.get(node.name, [])
+    before = len(reg.entries)
+    for p in pods_on_node:
+        reg.register_existing(p)
+    if len(reg.entries) != before or (reg.frozen is not None and len(reg.entries) != reg.frozen):
+        raise NewTopologyValue(f"node {node.name}: a running pod carries an affinity term new to the snapshot")
+    table["ipa_cnt"][i] = node_ipa(reg, pods_on_node)
+
+
+def pod_ext_records(pods, profile: Profile, spread=None, ipa=None) -> np.ndarray:
+    """koordhip_pod_ext records: DeviceShare requests, extended scalars,
     (PodTopologySpread in the profile) the pods' spread constraints in the
-    registry's tables."""
+    registry's tables and (InterPodAffinity) their count-entry masks and weights."""
     from . import deviceshare as ds
     from .config import PLUGIN_PTS
     from .topologyspread import pod_pts_fields
+    from .config import PLUGIN_IPA
     pods = list(pods)
     arr = ds.pod_ext_records(pods)
-    if PLUGIN_PTS in profile.filters or PLUGIN_PTS in profile.scores:
+    if _uses(profile, PLUGIN_PTS):
         if spread is None:
             raise MarshalError("the profile enables PodTopologySpread: pass the snapshot's SpreadRegistry")
         for j, p in enumerate(pods):
             if not spread.covers(p):
                 raise MarshalError(f"pod {p.key}: spread constraints first seen after the snapshot was built: rebuild it")
             pod_pts_fields(arr[j], p, spread)
+    if _uses(profile, PLUGIN_IPA):
+        if ipa is None:
+            raise MarshalError("the profile enables InterPodAffinity: pass the snapshot's IpaRegistry")
+        for j, p in enumerate(pods):
+            if not ipa.covers(p):
+                raise MarshalError(f"pod {p.key}: affinity terms first seen after the snapshot was built: rebuild it")
+            ipa.pod_fields(arr[j], p)
     return arr
 
 
@@ -677,18 +709,32 @@ def build_table(cluster: ClusterState, profile: Profile, now: float, static_clas
     if sequential_profile(profile):
         from .config import PLUGIN_DEVICESHARE, PLUGIN_PTS
         t.enable_ext(device_slots_of(cluster) if PLUGIN_DEVICESHARE in profile.filters else 0)
+        from .config import PLUGIN_IPA
         reg = cluster.spread
-        if (PLUGIN_PTS in profile.filters or PLUGIN_PTS in profile.scores) and reg is not None and reg.keys:
+        ipa = cluster.ipa if _uses(profile, PLUGIN_IPA) else None
+        if ipa is not None:
+            if ipa.topo is not reg:
+                raise MarshalError("ClusterState.ipa must share ClusterState.spread's topology keys")
+            for pods_on_node in cluster.node_pods.values():
+                for p in pods_on_node:
+                    ipa.register_existing(p)
+        want = (_uses(profile, PLUGIN_PTS) and reg is not None and reg.keys) or (ipa is not None and ipa.entries)
+        if want:
             from . import topologyspread as ts
-            from .snapshot import PtsMeta
+            from .snapshot import IpaMeta, PtsMeta
             reg.domains = ts.DomainIndex(reg)
             reg.domains.build(cluster.nodes)
             ndom = [0 if key == ts.HOSTNAME else max(1, len(reg.domains.values[k])) for k, key in enumerate(reg.keys)]
+            pts_on = _uses(profile, PLUGIN_PTS)
             t.enable_pts(PtsMeta(keys=len(reg.keys), hostname=sum(1 << k for k, key in enumerate(reg.keys)
                                                                   if key == ts.HOSTNAME),
                                  ndom=ndom + [0] * (abi.PTS_KEYS - len(ndom)),
-                                 cons_key=[k for _, _, k in reg.cons], classes=len(reg.classes)))
+                                 cons_key=[k for _, _, k in reg.cons] if pts_on else [],
+                                 classes=len(reg.classes) if pts_on else 0))
             reg.freeze()
+            if ipa is not None and ipa.entries:
+                t.enable_ipa(IpaMeta(ent_key=ipa.ent_keys()))
+                ipa.freeze()
     for i, node in enumerate(cluster.nodes):
         node_row(t, i, node, cluster, profile, now, static_classes)
     if static_classes is not None:

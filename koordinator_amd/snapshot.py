@@ -50,6 +50,10 @@ EXT_MUTABLE = ["dev_used", "xrequested"]
 # i32 (mutable), spread-class eligibility bits u16.  Present after enable_pts().
 PTS_COLS = ["pts_dom", "pts_cnt", "pts_elig"]
 PTS_MUTABLE = ["pts_cnt"]
+# InterPodAffinity: per node the pods each count entry counts [n][IPA_ENTRIES]
+# i32 (mutable; the topology keys are the pts_* ones).  Present after enable_ipa().
+IPA_COLS = ["ipa_cnt"]
+IPA_MUTABLE = ["ipa_cnt"]
 
 
 @dataclass
@@ -62,6 +66,12 @@ class PtsMeta:
     ndom: List[int] = field(default_factory=lambda: [0] * abi.PTS_KEYS)
     cons_key: List[int] = field(default_factory=list)
     classes: int = 0
+
+
+@dataclass
+class IpaMeta:
+    """koordhip_node_soa's InterPodAffinity scalars: the count entries' topology keys."""
+    ent_key: List[int] = field(default_factory=list)
 
 
 def slot_col(col: str, s: int) -> str:
@@ -102,6 +112,22 @@ class NodeTable:
     dev_slots: int = 0
     # PodTopologySpread tables (None: no pts_* columns)
     pts: "PtsMeta" = None
+    # InterPodAffinity count entries (None: no ipa_* columns; needs the pts_* keys)
+    ipa: "IpaMeta" = None
+
+    @property
+    def has_ipa(self) -> bool:
+        return self.ipa is not None
+
+    def enable_ipa(self, meta: "IpaMeta"):
+        """Add the InterPodAffinity count column (every node: no pods counted)."""
+        if not self.has_pts:
+            raise ValueError("InterPodAffinity entries need the topology keys (enable_pts first)")
+        if not (0 < len(meta.ent_key) <= abi.IPA_ENTRIES and all(0 <= k < self.pts.keys for k in meta.ent_key)):
+            raise ValueError("InterPodAffinity entries outside the engine's envelope")
+        self.ipa = meta
+        self.cols["ipa_cnt"] = np.zeros((self.n, abi.IPA_ENTRIES), np.int32)
+        return self
 
     @property
     def has_pts(self) -> bool:
@@ -159,7 +185,8 @@ class NodeTable:
 
     def col_names(self) -> List[str]:
         return (ALL_COLS + [slot_col(c, s) for s in range(1, self.resv_slots) for c in RESV_COLS]
-                + (EXT_COLS if self.has_ext else []) + (PTS_COLS if self.has_pts else []))
+                + (EXT_COLS if self.has_ext else []) + (PTS_COLS if self.has_pts else [])
+                + (IPA_COLS if self.has_ipa else []))
 
     @classmethod
     def empty(cls, n: int) -> "NodeTable":
@@ -185,6 +212,7 @@ class NodeTable:
         t.resv_slots = self.resv_slots
         t.dev_slots = self.dev_slots
         t.pts = self.pts
+        t.ipa = self.ipa
         return t
 
     def copy(self) -> "NodeTable":
@@ -195,6 +223,7 @@ class NodeTable:
         t.resv_slots = self.resv_slots
         t.dev_slots = self.dev_slots
         t.pts = self.pts
+        t.ipa = self.ipa
         return t
 
     def as_soa(self) -> abi.KoordhipNodeSoa:
@@ -293,6 +322,14 @@ class NodeTable:
             s.pts_cnt = kp["cnt"].ctypes.data_as(C.POINTER(C.c_int32))
             s.pts_elig = kp["elig"].ctypes.data_as(C.POINTER(C.c_uint16))
             s._keep_pts = kp
+        if self.has_ipa:
+            ne = len(self.ipa.ent_key)
+            ki = np.ascontiguousarray(self.cols["ipa_cnt"][:, :ne].T)             # [ents][n]
+            s.ipa_ents = ne
+            for e in range(abi.IPA_ENTRIES):
+                s.ipa_ent_key[e] = self.ipa.ent_key[e] if e < ne else 0
+            s.ipa_cnt = ki.ctypes.data_as(C.POINTER(C.c_int32))
+            s._keep_ipa = ki
         return s
 
     def nbytes(self) -> int:

@@ -788,3 +788,73 @@ def config_workload(cfg_id: int, profile: Profile, n_nodes: int = None, n_pods: 
     pods = make_pods(StreamSpec(n_pods or c["pods"], be_frac=c["be_frac"], cpuset_frac=c.get("cpuset_frac", 0.0),
                                 resv_match_frac=c.get("resv_match_frac", 0.0)), profile)
     return table, pods
+
+
+@dataclass
+class IpaSpec:
+    """InterPodAffinity: zone / hostname topology (the PodTopologySpread keys
+    when the table has them), four apps with running pods, and pending pods of
+    those apps with the common term shapes -- app 0 spreads one pod per host
+    (required anti-affinity to itself), app 1 prefers zones running app 2
+    (weight 50), app 2 needs a zone running app 3 (required affinity; the
+    running app 2 pods carry it, so app 3 pods score hardPodAffinityWeight 1
+    there), app 3 avoids its own hosts (preferred anti-affinity, weight 30,
+    which its running pods carry too)."""
+    zones: int = 6
+    no_zone_frac: float = 0.03
+    running_frac: float = 0.3     # nodes holding running pods of an app
+    pod_frac: float = 0.6         # pending pods of one of the apps
+    seed: int = SEED
+
+
+# the count entries: (kind, app, key) with key 0 zone, 1 hostname
+IPA_ENTRIES = [("M", 0, 0), ("M", 0, 1), ("M", 1, 0), ("M", 1, 1), ("M", 2, 0), ("M", 2, 1), ("M", 3, 0), ("M", 3, 1),
+               ("C-anti", 0, 1), ("C-pref", 3, 1), ("C-aff", 2, 0)]
+
+
+def add_ipa(t: NodeTable, ext: np.ndarray, spec: IpaSpec) -> NodeTable:
+    """The ipa_* column and the pods' ipa_* fields (hand-encoded tables of the
+    shapes IpaSpec describes; test_ipa_objects.py checks the object path)."""
+    from .snapshot import IpaMeta, PtsMeta
+    n, sd = t.n, spec.seed + 23
+    if t.has_pts:   # the spread workload's keys: zone 0, hostname = the hostname bit
+        zk, hk = 0, int(t.pts.hostname).bit_length() - 1
+    else:
+        t.enable_pts(PtsMeta(keys=2, hostname=0b10, ndom=[spec.zones, 0, 0, 0], cons_key=[], classes=0))
+        zone = (splitmix64(sd, n, 1) % np.uint64(spec.zones)).astype(np.int32)
+        zone[uniform(sd, n, 3) < spec.no_zone_frac] = -1
+        t["pts_dom"][:, 0] = zone
+        t["pts_dom"][:, 1] = np.arange(n, dtype=np.int32)
+        zk, hk = 0, 1
+    key = {0: zk, 1: hk}
+    t.enable_ipa(IpaMeta(ent_key=[key[k] for _, _, k in IPA_ENTRIES]))
+    running = np.zeros((n, 4), np.int32)
+    for a in range(4):
+        on = uniform(sd, n, 10 + a) < spec.running_frac
+        running[:, a] = np.where(on, (splitmix64(sd, n, 20 + a) % np.uint64(3)).astype(np.int32) + 1, 0)
+    cnt = t["ipa_cnt"]
+    for e, (kind, a, _) in enumerate(IPA_ENTRIES):
+        cnt[:, e] = running[:, a]       # M: the app's pods; C: the app's pods carry the term
+    m = len(ext)
+    sp = spec.seed + 29
+    on = uniform(sp, m, 1) < spec.pod_frac
+    app = (splitmix64(sp, m, 2) % np.uint64(4)).astype(np.int64)
+    for j in np.flatnonzero(on):
+        x = ext[j]
+        a = int(app[j])
+        x["ipa_inc"] = (1 << (2 * a)) | (1 << (2 * a + 1))
+        if a == 0:
+            x["ipa_inc"] |= 1 << 8
+            x["ipa_anti"] = (1 << 1) | (1 << 8)
+        elif a == 1:
+            x["ipa_w"][4] = 50
+        elif a == 2:
+            x["ipa_inc"] |= 1 << 10
+            x["ipa_aff"] = 1 << 6
+        else:
+            x["ipa_inc"] |= 1 << 9
+            x["ipa_w"][7] = -30
+            x["ipa_w"][9] = -30
+            x["ipa_w"][10] = 1
+        x["ipa_score"] = sum(1 << e for e in range(abi.IPA_ENTRIES) if x["ipa_w"][e] != 0)
+    return t

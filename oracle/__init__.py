@@ -47,6 +47,7 @@ class OrcState(C.Structure):
         ("xrequested", C.POINTER(C.c_int64)),
         ("dev_out", C.c_void_p),
         ("pts_cnt", C.POINTER(C.c_int32)),
+        ("ipa_cnt", C.POINTER(C.c_int32)),
     ]
 
 
@@ -151,7 +152,7 @@ class Oracle:
     def eval_ext(self, pods: np.ndarray, ext=None, status=True, scores=True, k=0):
         """koordhip_eval_ext: raw planes of the normalized plugins too, topk by the normalized totals."""
         n, p = self.n, len(pods)
-        st = np.zeros((p, n), np.uint8) if status else None
+        st = np.zeros((p, n), np.uint16) if status else None
         sc = np.zeros((p, abi.NPLUGINS + abi.NEXT_PLUGINS, n), np.int32) if scores else None
         tk = np.zeros((p, k), abi.TOPK_DTYPE) if k else None
         pods = np.ascontiguousarray(pods)
@@ -194,6 +195,13 @@ class Oracle:
         if m is None or not m.cons_key:
             return np.zeros((self.n, 0), np.int32)
         return np.ctypeslib.as_array(self.st.pts_cnt, shape=(len(m.cons_key), self.n)).T.copy()
+
+    def ipa_counts(self) -> np.ndarray:
+        """InterPodAffinity count entries' pods per node [n][ents]."""
+        m = self.table.ipa
+        if m is None or not m.ent_key:
+            return np.zeros((self.n, 0), np.int32)
+        return np.ctypeslib.as_array(self.st.ipa_cnt, shape=(len(m.ent_key), self.n)).T.copy()
 
     def dev_filter(self, ext_rec, node: int) -> bool:
         x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)

@@ -148,6 +148,12 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
     if (!st->pts_cnt) return -1;
     if (soa->pts_cnt) memcpy(st->pts_cnt, soa->pts_cnt, sizeof(int32_t) * (size_t)soa->pts_cons * (size_t)n);
   }
+  if (soa->ipa_ents > 0) {
+    const size_t in = (size_t)soa->ipa_ents * (size_t)(n > 0 ? n : 1);
+    st->ipa_cnt = (int32_t *)calloc(in, sizeof(int32_t));
+    if (!st->ipa_cnt) return -1;
+    if (soa->ipa_cnt) memcpy(st->ipa_cnt, soa->ipa_cnt, sizeof(int32_t) * (size_t)soa->ipa_ents * (size_t)n);
+  }
   if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned || !st->dev_used ||
       !st->xrequested)
     return -1;
@@ -179,6 +185,7 @@ void orc_state_free(orc_state *st) {
   free(st->dev_used);
   free(st->xrequested);
   free(st->pts_cnt);
+  free(st->ipa_cnt);
   memset(st, 0, sizeof(*st));
 }
 
@@ -311,9 +318,10 @@ uint32_t orc_score_plugin_bit(int p) {
 /* ------------------------------------------------------------------------ */
 
 static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod,
-                        const koordhip_pod_ext *x, const orc_pts *ps, int32_t i) {
+                        const koordhip_pod_ext *x, const orc_pts *ps, const orc_ipa *ia, int32_t i) {
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NODE_STATIC) && !orc_static_filter(st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_PTS) && !orc_pts_filter(st, x, ps, i)) return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_IPA) && !orc_ipa_filter(st, x, ia, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_xfit_filter(st, x, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) return 0;
@@ -336,7 +344,8 @@ static int64_t orc_total(const koordhip_config *cfg, const orc_state *st, const 
 
 int64_t orc_bmax(const koordhip_config *cfg) {
   static const uint32_t ext[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
-                                                      KOORDHIP_PLUGIN_TAINT_SCORE, KOORDHIP_PLUGIN_PTS};
+                                                      KOORDHIP_PLUGIN_TAINT_SCORE, KOORDHIP_PLUGIN_PTS,
+                                                      KOORDHIP_PLUGIN_IPA};
   int64_t b = 0;
   for (int p = 0; p < KOORDHIP_NPLUGINS; p++)
     if (cfg->score_plugins & orc_score_plugin_bit(p)) b += 100 * cfg->plugin_weight[p];
@@ -391,7 +400,7 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
         row[3 * (size_t)n + i] =
             (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) ? (int32_t)orc_bal_score(cfg, st, pod, i) : 0;
       }
-      if (keys && orc_feasible(cfg, st, pod, NULL, NULL, i)) {
+      if (keys && orc_feasible(cfg, st, pod, NULL, NULL, NULL, i)) {
         int64_t t = orc_total(cfg, st, pod, i);
         if (rv) t = orc_resv_rank_total(cfg, st, pod, i, t);
         keys[nk++] = mkkey(t, i);
@@ -417,9 +426,10 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
 }
 
 int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, const koordhip_pod_ext *ext,
-                 int32_t n_pods, uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
+                 int32_t n_pods, uint16_t *status, int32_t *scores, koordhip_topk *topk, int32_t k) {
   static const uint32_t xb[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
-                                                     KOORDHIP_PLUGIN_TAINT_SCORE, 0u};
+                                                     KOORDHIP_PLUGIN_TAINT_SCORE, KOORDHIP_PLUGIN_PTS,
+                                                     KOORDHIP_PLUGIN_IPA};
   const int32_t n = st->n;
   const int NP = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
   const size_t nn = (size_t)(n > 0 ? n : 1);
@@ -427,26 +437,33 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
   int64_t *base = (int64_t *)malloc(sizeof(int64_t) * nn);
   int64_t *raw = (int64_t *)malloc(sizeof(int64_t) * KOORDHIP_NEXT_PLUGINS * nn);
   int64_t *ptsraw = (int64_t *)calloc(nn, sizeof(int64_t));
+  int64_t *ipraw = (int64_t *)calloc(nn, sizeof(int64_t));
   uint64_t *keys = (uint64_t *)malloc(sizeof(uint64_t) * nn);
   const int rv = orc_resv_on(cfg, st);
   const int rs = rv && (cfg->score_plugins & KOORDHIP_PLUGIN_RESERVATION);
   const int pts_score = (cfg->score_plugins & KOORDHIP_PLUGIN_PTS) != 0;
+  const int ipa_score = (cfg->score_plugins & KOORDHIP_PLUGIN_IPA) != 0;
   for (int32_t p = 0; p < n_pods; p++) {
     const koordhip_pod *pod = &pods[p];
     const koordhip_pod_ext *x = ext ? &ext[p] : NULL;
     orc_pts ps;
+    orc_ipa ia;
     if (orc_pts_prefilter(cfg, st, x, &ps)) return -1;
+    if (orc_ipa_prefilter(cfg, st, x, &ia)) return -1;
     if (rv) orc_resv_restore((orc_state *)st, pod, +1);
     int32_t nf = 0;
     for (int32_t i = 0; i < n; i++)
-      if (orc_feasible(cfg, st, pod, x, &ps, i)) feas[nf++] = i;
+      if (orc_feasible(cfg, st, pod, x, &ps, &ia, i)) feas[nf++] = i;
+    /* InterPodAffinity PreScore / Score: every node's raw score (its plane) */
+    if (ipa_score && orc_ipa_prescore(st, x, &ia)) return -1;
+    for (int32_t i = 0; i < n; i++) ipraw[i] = ipa_score ? orc_ipa_score(st, &ia, i) : 0;
     if (pts_score && orc_pts_prescore(st, x, &ps, feas, nf)) return -1;
     memset(ptsraw, 0, sizeof(int64_t) * nn);
     if (pts_score)
       for (int32_t j = 0; j < nf; j++) ptsraw[feas[j]] = orc_pts_score(st, x, &ps, feas[j]);
     for (int32_t i = 0; i < n; i++) {
       if (status) {
-        uint8_t b = 0;
+        uint16_t b = 0;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NODE_STATIC) && !orc_static_filter(st, pod, i))
           b |= KOORDHIP_ST_STATIC_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) b |= KOORDHIP_ST_FIT_FAIL;
@@ -458,6 +475,7 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
           b |= KOORDHIP_ST_RESV_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) b |= KOORDHIP_ST_DEVICE_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_PTS) && !orc_pts_filter(st, x, &ps, i)) b |= KOORDHIP_ST_PTS_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_IPA) && !orc_ipa_filter(st, x, &ia, i)) b |= KOORDHIP_ST_IPA_FAIL;
         status[(size_t)p * n + i] = b;
       }
       if (scores) {
@@ -478,6 +496,8 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
             (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) ? (int32_t)orc_static_score(st, pod, i, 1) : 0;
         /* PodTopologySpread: the raw Score of a feasible node (0 elsewhere and on ignored nodes) */
         row[7 * (size_t)n + i] = (int32_t)ptsraw[i];
+        /* InterPodAffinity: the raw Score of every node */
+        row[8 * (size_t)n + i] = (int32_t)ipraw[i];
       }
     }
     if (topk && k > 0) {
@@ -489,16 +509,17 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
         raw[(size_t)nf + j] = (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? orc_static_score(st, pod, i, 0) : 0;
         raw[2 * (size_t)nf + j] = (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) ? orc_static_score(st, pod, i, 1) : 0;
         raw[3 * (size_t)nf + j] = ptsraw[i];
+        raw[4 * (size_t)nf + j] = ipraw[i];
       }
-      for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+      for (int e = 0; e < 3; e++)
         if (cfg->score_plugins & xb[e]) orc_default_normalize(raw + (size_t)e * nf, nf, e == 2);
       if (pts_score) orc_pts_normalize(&ps, feas, raw + 3 * (size_t)nf, nf);
+      if (ipa_score) orc_ipa_normalize(raw + 4 * (size_t)nf, nf);
       for (int32_t j = 0; j < nf; j++) {
         const int32_t i = feas[j];
         int64_t t = base[j];
         for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
-          if (cfg->score_plugins & (e == 3 ? KOORDHIP_PLUGIN_PTS : xb[e]))
-            t += (int64_t)cfg->ext_weight[e] * raw[(size_t)e * nf + j];
+          if (cfg->score_plugins & xb[e]) t += (int64_t)cfg->ext_weight[e] * raw[(size_t)e * nf + j];
         if (rv) t = orc_resv_rank_total(cfg, st, pod, i, t);
         keys[j] = mkkey(t, i);
       }
@@ -516,11 +537,13 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
     }
     if (rv) orc_resv_restore((orc_state *)st, pod, -1);
     orc_pts_free(&ps);
+    orc_ipa_free(&ia);
   }
   free(feas);
   free(base);
   free(raw);
   free(ptsraw);
+  free(ipraw);
   free(keys);
   return 0;
 }
@@ -592,6 +615,7 @@ int orc_commit_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod
     for (int j = 0; j < KOORDHIP_NXRES; j++)
       if ((x->xmask >> j) & 1u) st->xrequested[(size_t)j * st->n + i] += x->xreq[j];
   orc_pts_commit(st, x, i); /* NodeInfo.AddPod: one more pod for the constraints it matches */
+  orc_ipa_commit(st, x, i); /* ... and for the InterPodAffinity entries that count it */
   return 0;
 }
 
@@ -721,13 +745,15 @@ typedef struct stream_ctx {
   int resv_score;         /* the Reservation plugin scores (its PreScore nominates) */
   int64_t *plugin_scores; /* [KOORDHIP_NPLUGINS][nfeasible] */
   orc_pts *pts;           /* PodTopologySpread PreFilter / PreScore state of the pod */
+  orc_ipa *ipa;           /* InterPodAffinity PreFilter / PreScore state of the pod */
 } stream_ctx;
 
 /* (upstream) findNodesThatPassFilters checkNode: RunFilterPlugins, append on success. */
 static void filter_piece(void *a, int32_t lo, int32_t hi) {
   stream_ctx *c = (stream_ctx *)a;
   for (int32_t i = lo; i < hi; i++)
-    if (orc_feasible(c->cfg, c->st, c->pod, c->ext, c->pts, i)) c->feasible[atomic_fetch_add(&c->nfeasible, 1)] = i;
+    if (orc_feasible(c->cfg, c->st, c->pod, c->ext, c->pts, c->ipa, i))
+      c->feasible[atomic_fetch_add(&c->nfeasible, 1)] = i;
 }
 
 /* (upstream) framework.RunScorePlugins: one Until over nodes, every score plugin per node. */
@@ -758,6 +784,8 @@ static void score_piece(void *a, int32_t lo, int32_t hi) {
     }
     if (c->cfg->score_plugins & KOORDHIP_PLUGIN_PTS)
       c->plugin_scores[(size_t)(KOORDHIP_NPLUGINS + 3) * nf + j] = orc_pts_score(c->st, c->ext, c->pts, i);
+    if (c->cfg->score_plugins & KOORDHIP_PLUGIN_IPA)
+      c->plugin_scores[(size_t)(KOORDHIP_NPLUGINS + 4) * nf + j] = orc_ipa_score(c->st, c->ipa, i);
   }
 }
 
@@ -769,7 +797,8 @@ int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_p
 void orc_set_dev_out(orc_state *st, uint32_t *devs) { st->dev_out = devs; }
 
 static const uint32_t k_ext_bits[KOORDHIP_NEXT_PLUGINS] = {KOORDHIP_PLUGIN_DEVICESHARE, KOORDHIP_PLUGIN_AFFINITY_SCORE,
-                                                           KOORDHIP_PLUGIN_TAINT_SCORE, 0u};
+                                                           KOORDHIP_PLUGIN_TAINT_SCORE, KOORDHIP_PLUGIN_PTS,
+                                                           KOORDHIP_PLUGIN_IPA};
 
 int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods,
                          const koordhip_pod_ext *ext, int32_t n_pods, int32_t *out_node, int32_t threads) {
@@ -789,13 +818,18 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
   orc_pts ps;
   memset(&ps, 0, sizeof(ps));
   c.pts = &ps;
+  orc_ipa ia;
+  memset(&ia, 0, sizeof(ia));
+  c.ipa = &ia;
   for (int32_t p = 0; p < n_pods; p++) {
     c.pod = &pods[p];
     c.ext = ext ? &ext[p] : NULL;
     uint32_t *devs = st->dev_out ? st->dev_out + (size_t)p * KOORDHIP_DEV_TYPES : NULL;
     if (devs) memset(devs, 0, sizeof(uint32_t) * KOORDHIP_DEV_TYPES);
     orc_pts_free(&ps);
+    orc_ipa_free(&ia);
     if (orc_pts_prefilter(cfg, st, c.ext, &ps)) return -1; /* PodTopologySpread PreFilter */
+    if (orc_ipa_prefilter(cfg, st, c.ext, &ia)) return -1; /* InterPodAffinity PreFilter */
     /* Reservation BeforePreFilter: the cycle's NodeInfos are the restored ones */
     if (rv) orc_resv_restore(st, &pods[p], +1);
     atomic_store(&c.nfeasible, 0);
@@ -809,14 +843,16 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
     }
     /* PodTopologySpread PreScore over the feasible list (before the Score Until) */
     if ((cfg->score_plugins & KOORDHIP_PLUGIN_PTS) && orc_pts_prescore(st, c.ext, &ps, c.feasible, nf)) return -1;
+    if ((cfg->score_plugins & KOORDHIP_PLUGIN_IPA) && orc_ipa_prescore(st, c.ext, &ia)) return -1;
     pool_until(&pl, nf, score_piece, &c);
     /* NormalizeScore of the normalized plugins (DefaultNormalizeScore over the
      * feasible list: DeviceShare scoring.go:78-80, upstream NodeAffinity, and
      * TaintToleration reversed), Reservation PreScore + Score + NormalizeScore */
     int64_t *xs = c.plugin_scores + (size_t)KOORDHIP_NPLUGINS * nf;
-    for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
+    for (int e = 0; e < 3; e++)
       if (cfg->score_plugins & k_ext_bits[e]) orc_default_normalize(xs + (size_t)e * nf, nf, e == 2);
     if (cfg->score_plugins & KOORDHIP_PLUGIN_PTS) orc_pts_normalize(&ps, c.feasible, xs + 3 * (size_t)nf, nf);
+    if (cfg->score_plugins & KOORDHIP_PLUGIN_IPA) orc_ipa_normalize(xs + 4 * (size_t)nf, nf);
     int64_t *norm = c.plugin_scores + (size_t)(KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS) * nf;
     if (rs) orc_resv_normalized(st, &pods[p], c.feasible, nf, norm);
     /* (upstream) prioritizeNodes: sum of score x weight; selectHost: max,
@@ -829,8 +865,7 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
                   cfg->plugin_weight[2] * c.plugin_scores[2 * (size_t)nf + j] +
                   cfg->plugin_weight[3] * c.plugin_scores[3 * (size_t)nf + j];
       for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++)
-        if (cfg->score_plugins & (e == 3 ? KOORDHIP_PLUGIN_PTS : k_ext_bits[e]))
-          t += (int64_t)cfg->ext_weight[e] * xs[(size_t)e * nf + j];
+        if (cfg->score_plugins & k_ext_bits[e]) t += (int64_t)cfg->ext_weight[e] * xs[(size_t)e * nf + j];
       if (rs) t += (int64_t)cfg->reservation_weight * norm[j];
       if (t > best || (t == best && i < best_node)) {
         best = t;
@@ -851,6 +886,7 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
     st->no_prescore = 0;
   }
   orc_pts_free(&ps);
+  orc_ipa_free(&ia);
   free(c.feasible);
   free(c.plugin_scores);
   pool_free(&pl);

@@ -70,6 +70,8 @@ typedef struct orc_state {
   uint32_t *dev_out; /* optional [n_pods][TYPES] device slots of the last orc_place_stream_ext call */
   /* PodTopologySpread: each table constraint's matching pods per node [cons][n] (pts_oracle.c) */
   int32_t *pts_cnt;
+  /* InterPodAffinity: each count entry's pods per node [ents][n] (ipa_oracle.c) */
+  int32_t *ipa_cnt;
 } orc_state;
 
 /* PodTopologySpread per-pod state (pts_oracle.c): PreFilter's pairs and
@@ -93,6 +95,24 @@ int64_t orc_pts_score(const orc_state *st, const koordhip_pod_ext *x, const orc_
 void orc_pts_normalize(const orc_pts *ps, const int32_t *feas, int64_t *scores, int32_t nf);
 void orc_pts_commit(orc_state *st, const koordhip_pod_ext *x, int32_t i);
 void orc_pts_free(orc_pts *ps);
+
+/* InterPodAffinity per-pod state (ipa_oracle.c): PreFilter's pair maps per
+ * topology key (affinityCounts; antiAffinityCounts + existingAntiAffinityCounts)
+ * and PreScore's topologyScore */
+typedef struct orc_ipa {
+  int on, filt, scored, aff_empty;
+  int64_t *aff[KOORDHIP_PTS_KEYS];
+  int64_t *anti[KOORDHIP_PTS_KEYS];
+  int64_t *score[KOORDHIP_PTS_KEYS];
+} orc_ipa;
+int orc_ipa_active(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x);
+int orc_ipa_prefilter(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x, orc_ipa *ia);
+int orc_ipa_filter(const orc_state *st, const koordhip_pod_ext *x, const orc_ipa *ia, int32_t i);
+int orc_ipa_prescore(const orc_state *st, const koordhip_pod_ext *x, orc_ipa *ia);
+int64_t orc_ipa_score(const orc_state *st, const orc_ipa *ia, int32_t i);
+void orc_ipa_normalize(int64_t *scores, int32_t nf);
+void orc_ipa_commit(orc_state *st, const koordhip_pod_ext *x, int32_t i);
+void orc_ipa_free(orc_ipa *ia);
 
 int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n);
 void orc_state_free(orc_state *st);
@@ -211,7 +231,7 @@ int orc_commit_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod
 /* koordhip_eval_ext: scores [n_pods][NPLUGINS + NEXT_PLUGINS][n] (raw), topk
  * by the ranking total with the normalized plugins' weighted scores added. */
 int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pods, const koordhip_pod_ext *ext,
-                 int32_t n_pods, uint8_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
+                 int32_t n_pods, uint16_t *status, int32_t *scores, koordhip_topk *topk, int32_t k);
 
 /* Greedy stream with the reference loop structure: per pod a parallel Filter
  * over all nodes, a parallel Score per plugin over the feasible nodes
