@@ -160,7 +160,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare", "spread"], default="config4",
+    ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare", "spread", "affinity"], default="config4",
                     help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
                          "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods); "
                          "config5: 200k nodes, 10%% holding a Reservation matched by 20%% of the pods, "
@@ -168,7 +168,9 @@ def main():
                          "devices and 20%% device pods, + DeviceShare (weight 1): the exact sequential cycle, "
                          "one GPU; spread: config 4's cluster with zone / rack / hostname topology and 60%% of "
                          "the pods in five PodTopologySpread classes, + PodTopologySpread (filter, weight 2): "
-                         "the exact sequential cycle, one GPU")
+                         "the exact sequential cycle, one GPU; affinity: config 4's cluster with zone / hostname "
+                         "topology, four apps' running pods and 60%% of the pods carrying pod affinity / "
+                         "anti-affinity terms, + InterPodAffinity (filter, weight 1): the exact sequential cycle")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--be-frac", type=float, default=None)
@@ -197,14 +199,16 @@ def main():
 
     import torch
     from koordinator_amd import synth
-    from koordinator_amd.config import shipped_profile, to_c_config, with_deviceshare, with_topology_spread
+    from koordinator_amd.config import (shipped_profile, to_c_config, with_deviceshare, with_interpod_affinity,
+                                        with_topology_spread)
     from koordinator_amd.engine import PlacementEngine
 
-    if args.workload in ("deviceshare", "spread"):
+    if args.workload in ("deviceshare", "spread", "affinity"):
         if world > 1:
             raise SystemExit(f"--workload {args.workload} runs on one GPU (the sequential cycle is not node-sharded)")
-        prof = (with_deviceshare(shipped_profile()) if args.workload == "deviceshare"
-                else with_topology_spread(shipped_profile()))
+        prof = {"deviceshare": lambda: with_deviceshare(shipped_profile()),
+                "spread": lambda: with_topology_spread(shipped_profile()),
+                "affinity": lambda: with_interpod_affinity(shipped_profile())}[args.workload]()
         return run_sequential(args, torch, synth, prof, PlacementEngine)
 
     dist = None
@@ -403,7 +407,12 @@ def seq_bytes_per_eval(pods: np.ndarray, ext: np.ndarray, cfg, dev_slots: int) -
     # constraints name and the node's count of each of its constraints (4 B each)
     pn = ext["pts_n"].astype(np.int64)
     nkeys = np.array([len(set(int(c) for c in x["pts_c"][:int(x["pts_n"])])) for x in ext], np.int64)
-    return b + np.where(pn > 0, 2 + 4 * nkeys + 4 * pn, 0)
+    b = b + np.where(pn > 0, 2 + 4 * nkeys + 4 * pn, 0)
+    # InterPodAffinity: per entry the pod's Filter / Score reads, the node's
+    # domain for the entry's key and (hostname entries) its own count: 8 B
+    m = (ext["ipa_aff"] | ext["ipa_anti"] | ext["ipa_score"]).astype(np.uint64)
+    ne = np.array([bin(int(v)).count("1") for v in m], np.int64)
+    return b + 8 * ne
 
 
 def run_sequential(args, torch, synth, prof, PlacementEngine):
@@ -415,13 +424,17 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     args.pods = args.pods or 20000
     args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
     spread = args.workload == "spread"
+    affinity = args.workload == "affinity"
     table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
     pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac), prof)
-    if spread:
+    if spread or affinity:
         from koordinator_amd import abi
         table.enable_ext(0)
         ext = abi.pod_ext_array(args.pods)
-        synth.add_spread(table, ext, synth.SpreadSpec())
+        if spread:
+            synth.add_spread(table, ext, synth.SpreadSpec())
+        else:
+            synth.add_ipa(table, ext, synth.IpaSpec())
     else:
         synth.add_devices(table, synth.DevSpec())
         ext = synth.make_device_ext(args.pods, synth.DevStreamSpec(frac=args.dev_frac))
@@ -455,7 +468,12 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     gbs = alg / seq_s / 1e9 if seq_s > 0 else None
     value = args.pods * args.steps / elapsed
     dev = (ext["flags"] & 1) != 0
-    if spread:
+    if affinity:
+        wl = (f"affinity: {args.nodes} nodes (6 zones, hostname; 4 apps' running pods) x {args.pods} pods "
+              f"({int(((ext['ipa_inc'] | ext['ipa_aff'] | ext['ipa_anti'] | ext['ipa_score']) != 0).mean() * 100)}% "
+              "carrying pod affinity / anti-affinity terms), NodeResourcesFit + LoadAwareScheduling + "
+              "InterPodAffinity (filter, weight 1), the exact sequential cycle")
+    elif spread:
         wl = (f"spread: {args.nodes} nodes (6 zones, 24 racks, hostname; 3 apps' running pods) x {args.pods} pods "
               f"({int((ext['pts_n'] > 0).mean() * 100)}% in five PodTopologySpread classes), NodeResourcesFit + "
               "LoadAwareScheduling + PodTopologySpread (filter, weight 2), the exact sequential cycle")
@@ -474,8 +492,9 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
         "unschedulable": int((placements < 0).sum()),
         "device_pods_placed": int(((placements >= 0) & dev).sum()),
         "spread_pods_placed": int(((placements >= 0) & (ext["pts_n"] > 0)).sum()),
+        "affinity_pods_placed": int(((placements >= 0) & ((ext["ipa_aff"] | ext["ipa_anti"] | ext["ipa_score"]) != 0)).sum()),
         "roofline": {"bound": "latency", "kernel": kn["resolve"],
-                     "limiter": ("latency: per pod one grid-wide hand-off (two for device pods) after the owner's commit and one evaluation chain (not bandwidth); priced against HBM peak" if not spread else "latency: per pod the spread pre-pass (hostname minimum), one or two grid-wide hand-offs (soft scoring adds the raw min / max) and one evaluation chain (not bandwidth); priced against HBM peak"),
+                     "limiter": ("latency: per pod one grid-wide hand-off (two for device pods) after the owner's commit and one evaluation chain (not bandwidth); priced against HBM peak" if not (spread or affinity) else "latency: per pod the spread pre-pass (hostname minimum), one or two grid-wide hand-offs (soft scoring adds the raw min / max) and one evaluation chain (not bandwidth); priced against HBM peak"),
                      "timing": "HIP events around the k_seq launch of the last timed step",
                      "achieved": round(gbs, 2) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 5) if gbs else None, "traffic": None,

@@ -153,6 +153,11 @@ __device__ __forceinline__ int32_t ext_total(const DevCfg &c, uint32_t ext, cons
   return t;
 }
 
+// The record of a pod without koordhip_pod_ext (no device request: gpu -1 =
+// key absent).  Pods read their record in place (global, wave-uniform: scalar
+// loads) -- a register copy of the 328-B record spills.
+__device__ const DevPodX kNoPodX = {{{-1, -1, -1}, {0, 0, 0}, {0, 0, 0}}};
+
 // R2 granules: {epoch, value}; one aligned 8-byte write-through store
 __device__ __forceinline__ void put_granule(uint64_t *g, uint32_t epoch, uint32_t v) {
   __hip_atomic_store(g, ((uint64_t)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -240,9 +245,7 @@ template <int SM>
 __device__ __noinline__ void seq_commit(const DevCfg *cp, const DevNodes *dp, const DevPod *pp, const DevPodX *px,
                                         int32_t w, int32_t nf, bool rs, int32_t *out_node, uint64_t *out_cpus,
                                         uint32_t *out_dev) {
-  DevPodX none{};
-  none.req[0][0] = none.req[0][1] = none.req[0][2] = -1;
-  const DevPodX &x = px ? *px : none;
+  const DevPodX &x = px ? *px : kNoPodX;
   uint64_t cpus[NW] = {0, 0, 0, 0};
   uint32_t dv[DT] = {0u, 0u, 0u};
   int32_t res = KOORDHIP_UNSCHEDULABLE;
@@ -371,8 +374,6 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
   const bool pts = pa.keys > 0;  // the snapshot has PodTopologySpread tables (and the plugin runs)
   const IpaArgs &ia = a.ipa;
   const bool ipa = ia.ents > 0;  // the snapshot has InterPodAffinity entries (and the plugin runs)
-  DevPodX none{};
-  for (int q = 0; q < DT; q++) none.req[q][0] = none.req[q][1] = none.req[q][2] = q == 0 ? -1 : 0;
   if (pts) pts_init(pa, d.n, L, t, SEQ_THREADS);
   if (ipa) ipa_load(ia, IL, t, SEQ_THREADS);
   const bool dbg = a.dbg != nullptr && b == 0 && t == 0;
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
   };
   for (int32_t p = 0; p < a.n_pods; p++) {
     const DevPod pod = a.pods[p];
-    const DevPodX x = a.podx ? a.podx[p] : none;
+    const DevPodX &x = a.podx ? a.podx[p] : kNoPodX;
     const uint32_t eA = 2u * (uint32_t)p + 1u, eB = 2u * (uint32_t)p + 2u, eP = (uint32_t)p + 1u;
     const int par = p & 1;
     // ---- PodTopologySpread: the pod's pair counters from the replicas, and
