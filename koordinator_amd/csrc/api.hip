@@ -1036,10 +1036,9 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
       delete c;
       return fail(KOORDHIP_EINVAL, "score weights too large: the ranking total must stay below 2^30");
     }
-    if (!c->eval_fused && max_total + 2 > 32768) {
-      delete c;
-      return fail(KOORDHIP_EINVAL, "KOORDHIP_EVAL_SPLIT takes ranking totals below 2^15 only");
-    }
+    // totals the split path's u16 score matrix cannot hold run the fused path,
+    // whose 32-bit keys take them (also when KOORDHIP_EVAL=split asked for the split one)
+    if (!c->eval_fused && max_total + 2 > 32768) c->eval_fused = true;
     int bits = 1;
     while ((1ll << bits) <= max_total + 1) bits++;
     c->score_bits = bits;

@@ -16,7 +16,7 @@ STAGES=${STAGES:-tests smoke bench stamps prof pmc}
 WORKLOADS=${WORKLOADS:-config4 config3 config5}
 mkdir -p gpurun_out
 has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
-steps_of() { case $1 in config4) echo "--steps 5 --warmup 2";; config3) echo "--steps 3 --warmup 1";; *) echo "--steps 2 --warmup 1";; esac; }
+steps_of() { case $1 in config4) echo "--steps 5 --warmup 2";; config3|deviceshare|spread|affinity) echo "--steps 3 --warmup 1";; *) echo "--steps 2 --warmup 1";; esac; }
 pods_pmc() { case $1 in config4) echo 30000;; config3) echo 10000;; *) echo 6000;; esac; }
 
 if has tests; then
@@ -36,9 +36,13 @@ for w in $WORKLOADS; do
     python3 - gpurun_out/bench_${R}_$w.json $w <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], d["eval_roofline"]["kernel"],
-      "eval us", d["eval_roofline"]["avg_launch_us"], "select us", d["select"]["avg_launch_us"],
-      "P", d["config"]["batch_pods"], "lag", d["config"]["pipeline_lag"], "unsched", d["unschedulable"])
+if "eval_roofline" in d:
+    print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], d["eval_roofline"]["kernel"],
+          "eval us", d["eval_roofline"]["avg_launch_us"], "select us", d["select"]["avg_launch_us"],
+          "P", d["config"]["batch_pods"], "lag", d["config"]["pipeline_lag"], "unsched", d["unschedulable"])
+else:  # the sequential cycle's workloads
+    print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], d["roofline"]["kernel"],
+          "us/pod", d["roofline"]["us_per_pod"], "unsched", d["unschedulable"])
 PY
   fi
   if has stamps; then

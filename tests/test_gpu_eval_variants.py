@@ -55,3 +55,19 @@ def test_gpu_numa_lag2_stream(Engine, monkeypatch):
         got = e.place_stream(pods)
         assert e.kernel_stats()["lag"] == 2
     assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
+
+
+def test_gpu_wide_totals_asked_split_run_fused(Engine, monkeypatch):
+    """BalancedAllocation weight 5 beside Reservation: ranking totals beyond the
+    split path's u16 matrix (2^15).  KOORDHIP_EVAL=split no longer fails the
+    create: the context runs the fused path (32-bit keys), bit-exact."""
+    from koordinator_amd.config import with_upstream
+    monkeypatch.setenv("KOORDHIP_EVAL", "split")
+    prof0, t, pods = _workload("resv", 3000, 2000)
+    prof = with_upstream(prof0, static_filters=(), balanced_weight=5)
+    ref = oracle.Oracle(to_c_config(prof), t).place_stream(pods, threads=8)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got = e.place_stream(pods)
+        assert "eval_topk" in e.kernel_names()["eval"]
+    assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
