@@ -2364,6 +2364,10 @@ int place_staged_impl(koordhip_ctx *c) {
     std::fprintf(stderr, "[koordhip stamps] general path split: list + X + c %llu cycles | pods with ready key tables %llu | "
                  "evaluation passes %llu\n",
                  (unsigned long long)h[55], (unsigned long long)h[56], (unsigned long long)h[57]);
+    std::fprintf(stderr, "[koordhip stamps] general commit split: row source %llu  Reserve delta %llu  voiding + "
+                 "outputs %llu cycles | winners already in M %llu\n",
+                 (unsigned long long)h[58], (unsigned long long)h[59], (unsigned long long)h[60],
+                 (unsigned long long)h[61]);
   }
   return 0;
 }

@@ -2103,6 +2103,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   // prologue phases 1 / 2 / 2b (cycles), phase-2 HBM row loads, general-path causes: conflicts, slow, voided by a general commit
   uint64_t c_p[3] = {0, 0, 0}, n_p2 = 0, n_conf = 0, n_slowc = 0, n_void = 0;
   uint64_t c_cand = 0, n_evpass = 0, n_tready = 0;  // general path: list + X + c cycles, evaluation passes, pods with ready tables
+  uint64_t c_gc[3] = {0, 0, 0}, n_ghit = 0;          // general commit: row source, Reserve delta, voiding + outputs; winners in M
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
   // Every loop keeps several global loads in flight per thread before its LDS
@@ -2631,6 +2632,15 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         lap(2);
         uint64_t cpus[NW] = {0, 0, 0, 0};
         int32_t result = KOORDHIP_UNSCHEDULABLE;
+        uint64_t t_gc = dbg ? stamp() : 0;
+        auto gclap = [&](int ph) {
+          if (dbg) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint64_t x = stamp();
+            c_gc[ph] += x - t_gc;
+            t_gc = x;
+          }
+        };
         if (best != 0) {
           const int32_t w = key_node(best);
           // w's M slot (a staged pod's, materialised now if lazy, or a general
@@ -2646,6 +2656,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             if (hit_g) rw = __builtin_ctzll(hit_g);
           }
           const bool hit = rw < nm;
+          if (dbg) n_ghit += hit;
           const NV *srow = &mrow[rw];
           const NR *snr = &mnr[rw];
           int32_t from_prev = -1;
@@ -2674,6 +2685,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               }
             }
           }
+          gclap(0);
           bool okr = true;
           if constexpr (NUMA) {
             if (numa_on(c) && numa_active(pod, c)) {
@@ -2737,6 +2749,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               }
               nm++;
             }
+            gclap(1);
             // later staged decisions that walked w are void
             bool met = false;
 #pragma unroll
@@ -2750,6 +2763,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         if (out_cpus && lane < NW)
           out_cpus[(size_t)(p0 + g) * NW + lane] =
               lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
+        gclap(2);
         lap(3);
         j = g + 1;
       }
@@ -2987,6 +3001,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[54], (unsigned long long)n_void);
     atomicAdd((unsigned long long *)&dbg[55], (unsigned long long)c_cand);
     atomicAdd((unsigned long long *)&dbg[56], (unsigned long long)n_tready);
+    atomicAdd((unsigned long long *)&dbg[58], (unsigned long long)c_gc[0]);
+    atomicAdd((unsigned long long *)&dbg[59], (unsigned long long)c_gc[1]);
+    atomicAdd((unsigned long long *)&dbg[60], (unsigned long long)c_gc[2]);
+    atomicAdd((unsigned long long *)&dbg[61], (unsigned long long)n_ghit);
   }
 }
 
