@@ -2098,13 +2098,14 @@ int seq_place(koordhip_ctx *c) {
                          c->d_seqdesc, c->pts, c->ipa, c->stream));
   HIP_TRY(hipEventRecord(c->t1, c->stream));
   if (stamps) {
-    uint64_t h[6];
+    uint64_t h[9];
     HIP_TRY(hipMemcpyAsync(h, c->d_dbg, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const double q = 1.0 / std::max(np, 1);
     std::fprintf(stderr, "[koordhip stamps] k_seq block 0 cycles per pod: evaluate %.0f  wait A %.0f  normalize+publish %.0f  "
-                 "wait B %.0f  commit barrier %.0f | owner commits %.0f\n", h[0] * q, h[1] * q, h[2] * q, h[3] * q,
-                 h[4] * q, h[5] * q);
+                 "wait B %.0f  commit barrier %.0f | owner commits %.0f | evaluate split: pod prep %.0f  node "
+                 "evaluation %.0f  reduce + publish %.0f\n", h[0] * q, h[1] * q, h[2] * q, h[3] * q,
+                 h[4] * q, h[5] * q, h[6] * q, h[7] * q, h[8] * q);
   }
   c->last_P = 1;
   c->last_lag = 0;

@@ -157,7 +157,9 @@ __device__ __forceinline__ bool dev_present(const DevDev &dv, int32_t i) {
 __device__ __forceinline__ bool dev_eval(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
                                          bool nominated, bool filter, bool score, int32_t *raw) {
   *raw = 0;
-  if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i)) return true;
+  if (!(x.flags & KOORDHIP_PODX_DEVICE) || dv.slots <= 0 || !dv.present) return true;
+  // the nodeDevice entry and the first requested type's rows in one round trip
+  const bool present = dv.present[i] != 0;
   bool ok = true;
   int64_t sum = 0;
 #pragma unroll 1
@@ -166,6 +168,7 @@ __device__ __forceinline__ bool dev_eval(const DevCfg &c, const DevDev &dv, cons
     if (!dev_requests(x, t, q)) continue;
     DevRow w;
     dev_load(dv, i, t, w);
+    if (!present) return true;
     if (!dev_has_type(w) || (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(w, q))) {
       ok = false;
       continue;
@@ -211,13 +214,17 @@ __device__ __forceinline__ bool dev_reserve(const DevCfg &c, const DevDev &dv, c
 #pragma unroll
     for (int r = 0; r < DR; r++) per_t[t][r] = 0;
   }
-  if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i)) return true;
-  if (nominated) return false;
+  if (!(x.flags & KOORDHIP_PODX_DEVICE) || dv.slots <= 0 || !dv.present) return true;
+  const bool present = dv.present[i] != 0;  // (issued with the first type's rows)
+  bool any = false;
   for (int t = 0; t < DT; t++) {
     int64_t q[DR], per[DR];
     if (!dev_requests(x, t, q)) continue;
+    any = true;
     DevRow w;
     dev_load(dv, i, t, w);
+    if (!present) return true;
+    if (nominated) return false;
     if (!dev_has_type(w)) return false;
     if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(w, q)) return false;
     const int64_t want = dev_wanted(t, q, per);
@@ -229,11 +236,19 @@ __device__ __forceinline__ bool dev_reserve(const DevCfg &c, const DevDev &dv, c
                                                                                : -1;
     uint32_t taken = 0u;
     for (int64_t got = 0; got < want; got++) {
+      // the best untaken slot by (score desc, minor asc); the running best's
+      // score and minor in registers (sc[bs] with a dynamic bs would live in scratch)
       int bs = -1;
+      int64_t bsc = -1;
+      int32_t bmi = 0;
 #pragma unroll
       for (int s = 0; s < DS; s++) {
         if (sc[s] < 0 || ((taken >> s) & 1u)) continue;
-        if (bs < 0 || sc[s] > sc[bs] || (sc[s] == sc[bs] && w.minor[s] < w.minor[bs])) bs = s;
+        if (bs < 0 || sc[s] > bsc || (sc[s] == bsc && w.minor[s] < bmi)) {
+          bs = s;
+          bsc = sc[s];
+          bmi = w.minor[s];
+        }
       }
       if (bs < 0) return false;
       taken |= 1u << bs;
@@ -242,29 +257,40 @@ __device__ __forceinline__ bool dev_reserve(const DevCfg &c, const DevDev &dv, c
 #pragma unroll
     for (int r = 0; r < DR; r++) per_t[t][r] = per[r];
   }
-  return true;
+  return any || !present || !nominated;
 }
 
 __device__ __forceinline__ void dev_apply(const DevDev &dv, int32_t i, const uint32_t slots[DT],
                                           const int64_t per_t[DT][DR]) {
-  for (int t = 0; t < DT; t++)
-    for (int s = 0; s < dv.slots; s++)
-      if ((slots[t] >> s) & 1u) {
-        const size_t a = dev_at(dv, i, t, s) * DR;
+  for (int t = 0; t < DT; t++) {
+    if (!slots[t]) continue;
+    // every taken slot's used values loaded before any store (one round trip)
+    int64_t u[DS][DR];
+    const size_t a0 = dev_at(dv, i, t, 0) * DR;
 #pragma unroll
-        for (int r = 0; r < DR; r++) dv.used[a + r] += per_t[t][r];
-      }
+    for (int s = 0; s < DS; s++)
+#pragma unroll
+      for (int r = 0; r < DR; r++) u[s][r] = ((slots[t] >> s) & 1u) ? dv.used[a0 + (size_t)s * DR + r] : 0;
+#pragma unroll
+    for (int s = 0; s < DS; s++)
+      if ((slots[t] >> s) & 1u)
+#pragma unroll
+        for (int r = 0; r < DR; r++) dv.used[a0 + (size_t)s * DR + r] = u[s][r] + per_t[t][r];
+  }
 }
 
 // NodeResourcesFit over the extended scalars the pod requests (upstream fitsRequest)
 __device__ __forceinline__ bool xfit_filter(const DevDev &dv, const DevPodX &x, int32_t i, int32_t n) {
   if (!x.xmask) return true;
+  // no early exit: every requested scalar's loads in flight together
+  bool ok = true;
+#pragma unroll
   for (int j = 0; j < KOORDHIP_NXRES; j++) {
     if (!((x.xmask >> j) & 1u)) continue;
     const int64_t a = dv.xalloc ? dv.xalloc[(size_t)j * n + i] : 0;
-    if (x.xreq[j] > a - dv.xreq[(size_t)j * n + i]) return false;
+    ok &= x.xreq[j] <= a - dv.xreq[(size_t)j * n + i];
   }
-  return true;
+  return ok;
 }
 
 __device__ __forceinline__ int32_t static_raw(const DevDev &dv, int which, int32_t cls, int32_t i, int32_t n) {

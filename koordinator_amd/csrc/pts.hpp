@@ -52,11 +52,14 @@ struct PtsLds {
   int32_t red[2];           // min / max scratch
 };
 
-// One pod's constraints, split by whenUnsatisfiable (wave-uniform)
+// One pod's constraints in its own order (wave-uniform).  Every loop over
+// them runs j = 0 .. PP-1 unrolled under the hard / soft masks: with static
+// indices the arrays stay in registers (a dynamically indexed array lives in
+// scratch, one memory round trip per access).
 struct PtsPod {
   int32_t cls, nh, ns;
-  int32_t hc[PP], hk[PP], hskew[PP], hself[PP];
-  int32_t sc[PP], sk[PP], sskew[PP];
+  int32_t c[PP], k[PP], skew[PP], self[PP];
+  uint32_t hard, soft;  // bit j: constraint j is a DoNotSchedule / ScheduleAnyway one the plugin evaluates
   uint32_t hkeys, skeys;
   bool on, hhost;
 };
@@ -66,22 +69,23 @@ __device__ __forceinline__ PtsPod pts_pod(const PtsArgs &pa, const DevPodX &x) {
   q.on = (pa.filt || pa.score) && pa.keys > 0 && x.pts_n > 0;
   if (!q.on) return q;
   q.cls = x.pts_class;
-  for (int j = 0; j < x.pts_n && j < PP; j++) {
+#pragma unroll
+  for (int j = 0; j < PP; j++) {
+    if (j >= x.pts_n) continue;
     const int c = x.pts_c[j], k = pa.cons_key[c];
+    q.c[j] = c;
+    q.k[j] = k;
+    q.skew[j] = x.pts_skew[j];
+    q.self[j] = (x.pts_fl[j] & KOORDHIP_PTS_SELF) ? 1 : 0;
     if (x.pts_fl[j] & KOORDHIP_PTS_HARD) {
       if (!pa.filt) continue;
-      q.hc[q.nh] = c;
-      q.hk[q.nh] = k;
-      q.hskew[q.nh] = x.pts_skew[j];
-      q.hself[q.nh] = (x.pts_fl[j] & KOORDHIP_PTS_SELF) ? 1 : 0;
+      q.hard |= 1u << j;
       q.hkeys |= 1u << k;
       q.hhost |= ((pa.host >> k) & 1u) != 0;
       q.nh++;
     } else {
       if (!pa.score) continue;
-      q.sc[q.ns] = c;
-      q.sk[q.ns] = k;
-      q.sskew[q.ns] = x.pts_skew[j];
+      q.soft |= 1u << j;
       q.skeys |= 1u << k;
       q.ns++;
     }
@@ -125,6 +129,31 @@ __device__ __forceinline__ int32_t pts_wave_min(int32_t v) {
   for (int m = 32; m >= 1; m >>= 1) v = min(v, __shfl_xor(v, m));
   return v;
 }
+__device__ __forceinline__ int32_t pts_wave_max(int32_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m));
+  return v;
+}
+__device__ __forceinline__ uint32_t pts_wave_or(uint32_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v |= __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ int32_t pts_wave_sum(int32_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+// A per-thread (min, max) folded into LDS: wave reductions, then one atomic
+// per wave (256 threads' atomics on one LDS word serialise)
+__device__ __forceinline__ void wave_fold_minmax(int32_t mn, int32_t mx, int32_t *dmin, int32_t *dmax) {
+  mn = pts_wave_min(mn);
+  mx = pts_wave_max(mx);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(dmin, mn);
+    atomicMax(dmax, mx);
+  }
+}
 
 // Per pod: the pair counters of its keys and the hard keys' minima (wave w =
 // key w, lane = domain; requires 256 threads), the phase-A accumulators reset.
@@ -133,16 +162,18 @@ __device__ __forceinline__ void pts_prep(const PtsArgs &pa, const PtsPod &q, Pts
   if (k < PK && !((pa.host >> k) & 1u)) {
     if ((q.hkeys >> k) & 1u) {
       int32_t m = 0;
-      for (int j = 0; j < q.nh; j++)
-        if (q.hk[j] == k) m += L.fsum[q.hc[j]][dd];
+#pragma unroll
+      for (int j = 0; j < PP; j++)
+        if (((q.hard >> j) & 1u) && q.k[j] == k) m += L.fsum[q.c[j]][dd];
       L.fmatch[k][dd] = m;
       const int32_t mn = pts_wave_min(pts_bit(L.fpres[q.cls][k], dd) ? m : INT32_MAX);
       if (dd == 0) L.fmin[k] = mn;
     }
     if ((q.skeys >> k) & 1u) {
       int32_t m = 0;
-      for (int j = 0; j < q.ns; j++)
-        if (q.sk[j] == k) m += L.ssum[q.cls][q.sc[j]][dd];
+#pragma unroll
+      for (int j = 0; j < PP; j++)
+        if (((q.soft >> j) & 1u) && q.k[j] == k) m += L.ssum[q.cls][q.c[j]][dd];
       L.smatch[k][dd] = m;
     }
   }
@@ -160,16 +191,19 @@ __device__ __forceinline__ void pts_prep(const PtsArgs &pa, const PtsPod &q, Pts
 __device__ __forceinline__ int32_t pts_host_match(const PtsArgs &pa, const PtsPod &q, int k, int32_t n, int32_t i) {
   if (!((pa.elig[i] >> (2 * q.cls)) & 1u)) return -1;
   int32_t m = 0;
-  for (int j = 0; j < q.nh; j++)
-    if (q.hk[j] == k) m += pa.cnt[(size_t)q.hc[j] * n + i];
+#pragma unroll
+  for (int j = 0; j < PP; j++)
+    if (((q.hard >> j) & 1u) && q.k[j] == k) m += pa.cnt[(size_t)q.c[j] * n + i];
   return m;
 }
 
 // Filter, filtering.go: every hard key on the node; matchNum + self - min <= maxSkew.
 __device__ __forceinline__ bool pts_filter(const PtsArgs &pa, const PtsPod &q, const PtsLds &L, int32_t hmin, int32_t n,
                                            int32_t i) {
-  for (int j = 0; j < q.nh; j++) {
-    const int k = q.hk[j];
+#pragma unroll
+  for (int j = 0; j < PP; j++) {
+    if (!((q.hard >> j) & 1u)) continue;
+    const int k = q.k[j];
     const int32_t d = pa.dom[(size_t)k * n + i];
     if (d < 0) return false;
     int64_t match, mn;
@@ -181,24 +215,50 @@ __device__ __forceinline__ bool pts_filter(const PtsArgs &pa, const PtsPod &q, c
       match = pts_bit(L.fpres[q.cls][k], d) ? L.fmatch[k][d] : 0;
       mn = L.fmin[k];
     }
-    if (match + q.hself[j] - mn > q.hskew[j]) return false;
+    if (match + q.self[j] - mn > q.skew[j]) return false;
   }
   return true;
 }
 
 // A feasible node: false = an IgnoredNode (lacks a soft key); else its
-// domains go into the workgroup's masks (PreScore's pairs) and count.
-__device__ __forceinline__ bool pts_soft_mark(const PtsArgs &pa, const PtsPod &q, PtsLds &L, int32_t n, int32_t i) {
-  for (int j = 0; j < q.ns; j++)
-    if (pa.dom[(size_t)q.sk[j] * n + i] < 0) return false;
-  for (int j = 0; j < q.ns; j++) {
-    const int k = q.sk[j];
+// domains go into the thread's masks (PreScore's pairs) and count, folded
+// into the workgroup's by pts_soft_fold.
+__device__ __forceinline__ bool pts_soft_mark(const PtsArgs &pa, const PtsPod &q, int32_t n, int32_t i,
+                                              uint32_t (&m)[PK][2], int32_t &cnt) {
+#pragma unroll
+  for (int j = 0; j < PP; j++)
+    if (((q.soft >> j) & 1u) && pa.dom[(size_t)q.k[j] * n + i] < 0) return false;
+#pragma unroll
+  for (int j = 0; j < PP; j++) {
+    if (!((q.soft >> j) & 1u)) continue;
+    const int k = q.k[j];
     if ((pa.host >> k) & 1u) continue;
     const int32_t d = pa.dom[(size_t)k * n + i];
-    atomicOr(&L.smask[k][d >> 5], 1u << (d & 31));
+#pragma unroll
+    for (int kk = 0; kk < PK; kk++)
+      if (kk == k) {
+        if (d < 32)
+          m[kk][0] |= 1u << d;
+        else
+          m[kk][1] |= 1u << (d - 32);
+      }
   }
-  atomicAdd(&L.nfni, 1);
+  cnt++;
   return true;
+}
+
+// the threads' soft masks and counts into L.smask / L.nfni (zeroed before)
+__device__ __forceinline__ void pts_soft_fold(PtsLds &L, const uint32_t (&m)[PK][2], int32_t cnt) {
+  const bool l0 = (threadIdx.x & 63) == 0;
+#pragma unroll
+  for (int k = 0; k < PK; k++)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t v = pts_wave_or(m[k][h]);
+      if (l0 && v) atomicOr(&L.smask[k][h], v);
+    }
+  cnt = pts_wave_sum(cnt);
+  if (l0 && cnt) atomicAdd(&L.nfni, cnt);
 }
 
 // topologyNormalizingWeight of each soft constraint from the grid's masks
@@ -207,13 +267,20 @@ __device__ __forceinline__ bool pts_soft_mark(const PtsArgs &pa, const PtsPod &q
 __device__ __forceinline__ void pts_weights(const PtsArgs &pa, const PtsPod &q, const uint32_t (&mask)[PK][2],
                                             int32_t nfni, double (&w)[PP]) {
   uint32_t seen = 0;
-  for (int j = 0; j < q.ns; j++) {
-    const int k = q.sk[j];
+#pragma unroll
+  for (int j = 0; j < PP; j++) {
+    w[j] = 0.0;
+    if (!((q.soft >> j) & 1u)) continue;
+    const int k = q.k[j];
     int64_t sz;
     if ((pa.host >> k) & 1u) {
       sz = nfni;
     } else {
-      sz = ((seen >> k) & 1u) ? 0 : (int64_t)(__popc(mask[k][0]) + __popc(mask[k][1]));
+      int32_t pc = 0;  // (static indices into mask: no scratch)
+#pragma unroll
+      for (int kk = 0; kk < PK; kk++)
+        if (kk == k) pc = __popc(mask[kk][0]) + __popc(mask[kk][1]);
+      sz = ((seen >> k) & 1u) ? 0 : (int64_t)pc;
       seen |= 1u << k;
     }
     w[j] = log((double)(sz + 2));
@@ -224,11 +291,13 @@ __device__ __forceinline__ void pts_weights(const PtsArgs &pa, const PtsPod &q, 
 __device__ __forceinline__ int32_t pts_raw(const PtsArgs &pa, const PtsPod &q, const PtsLds &L, const double (&w)[PP],
                                            int32_t n, int32_t i) {
   double s = 0.0;
-  for (int j = 0; j < q.ns; j++) {
-    const int k = q.sk[j];
+#pragma unroll
+  for (int j = 0; j < PP; j++) {
+    if (!((q.soft >> j) & 1u)) continue;
+    const int k = q.k[j];
     const int32_t d = pa.dom[(size_t)k * n + i];
-    const int64_t cnt = ((pa.host >> k) & 1u) ? (int64_t)pa.cnt[(size_t)q.sc[j] * n + i] : (int64_t)L.smatch[k][d];
-    s += (double)cnt * w[j] + (double)(q.sskew[j] - 1);
+    const int64_t cnt = ((pa.host >> k) & 1u) ? (int64_t)pa.cnt[(size_t)q.c[j] * n + i] : (int64_t)L.smatch[k][d];
+    s += (double)cnt * w[j] + (double)(q.skew[j] - 1);
   }
   return (int32_t)round(s);
 }

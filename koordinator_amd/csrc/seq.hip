@@ -204,6 +204,14 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   uint32_t slots[DT] = {0u, 0u, 0u};
   int64_t per[DT][DR];
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+  // the loads of every row the Reserve changes go out first (one round trip
+  // with the device rows' instead of one per structure): the Fit / LoadAware
+  // row and the extended scalars' Requested
+  NV v;
+  load_row(v, d, w);
+  int64_t xr[KOORDHIP_NXRES];
+#pragma unroll
+  for (int j = 0; j < KOORDHIP_NXRES; j++) xr[j] = ((x.xmask >> j) & 1u) ? d.dv.xreq[(size_t)j * d.n + w] : 0;
   if (dev && !dev_reserve(c, d.dv, x, w, nominated, slots, per)) return KOORDHIP_RESERVE_FAILED;
   uint64_t m[NW] = {0, 0, 0, 0};
   if constexpr (SM >= 1) {
@@ -221,13 +229,12 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
     resv_assume(rv, p, m);
     store_resv(rv, d.rv, w);
   }
-  NV v;
-  load_row(v, d, w);
   apply_delta(v, p, +1);
   store_row(v, d, w);
   if (x.xmask)
+#pragma unroll
     for (int j = 0; j < KOORDHIP_NXRES; j++)
-      if ((x.xmask >> j) & 1u) d.dv.xreq[(size_t)j * d.n + w] += x.xreq[j];
+      if ((x.xmask >> j) & 1u) d.dv.xreq[(size_t)j * d.n + w] = xr[j] + x.xreq[j];
   if (cpus_out)
     for (int q = 0; q < NW; q++) cpus_out[q] = m[q];
   if (dev_out)
@@ -339,8 +346,7 @@ __device__ __forceinline__ bool seq_gather_minmax(const uint64_t *g, uint32_t ep
   }
   __syncthreads();
   if (!ok) *s_stop = 1;
-  atomicMin(&L.red[0], a);
-  atomicMax(&L.red[1], b);
+  wave_fold_minmax(a, b, &L.red[0], &L.red[1]);
   __syncthreads();
   mn = L.red[0];
   mx = L.red[1];
@@ -357,8 +363,11 @@ __device__ __forceinline__ void seq_put_minmax(uint64_t *g, uint32_t epoch, cons
   }
 }
 
+// One workgroup per CU: one wave per SIMD, so the kernel may take the whole
+// register file (arch VGPRs + AGPRs as spill space) instead of scratch.
 template <int SM>
-__global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqArgs a) {
+__global__ __launch_bounds__(SEQ_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_seq(DevCfg c, DevNodes d,
+                                                                                              SeqArgs a) {
   __shared__ int32_t s_red[SEQ_THREADS / 64][8];
   __shared__ int32_t s_tot[SEQ_NPT][SEQ_THREADS];
   __shared__ int32_t s_raw[SEQ_NPT][KOORDHIP_NEXT_PLUGINS][SEQ_THREADS];  // [3]: PodTopologySpread raw, -1 ignored
@@ -377,7 +386,16 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
   if (pts) pts_init(pa, d.n, L, t, SEQ_THREADS);
   if (ipa) ipa_load(ia, IL, t, SEQ_THREADS);
   const bool dbg = a.dbg != nullptr && b == 0 && t == 0;
-  uint64_t ts = dbg ? seq_stamp() : 0, acc[5] = {0, 0, 0, 0, 0};
+  uint64_t ts = dbg ? seq_stamp() : 0, acc[5] = {0, 0, 0, 0, 0}, sub[3] = {0, 0, 0}, tsub = 0;
+  // phase A split (block 0, thread 0, its loads drained): pod prep, its node evaluation, reduce + publish
+  auto sublap = [&](int q) {
+    if (dbg) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t u = seq_stamp();
+      if (q > 0) sub[q - 1] += u - tsub;
+      tsub = u;
+    }
+  };
   auto lap = [&](int q) {
     if (dbg) {
       const uint64_t u = seq_stamp();
@@ -386,6 +404,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     }
   };
   for (int32_t p = 0; p < a.n_pods; p++) {
+    sublap(0);
     const DevPod pod = a.pods[p];
     const DevPodX &x = a.podx ? a.podx[p] : kNoPodX;
     const uint32_t eA = 2u * (uint32_t)p + 1u, eB = 2u * (uint32_t)p + 2u, eP = (uint32_t)p + 1u;
@@ -415,7 +434,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
               if (v >= 0) m = min(m, v);
             }
         }
-        atomicMin(&L.red[0], m);
+        wave_fold_minmax(m, 0, &L.red[0], &L.red[1]);
         seq_put_minmax(a.g0 + ((size_t)par * G + b) * SEQ_GRAN, eP, L, t);
         int32_t unused;
         if (!seq_gather_minmax(a.g0 + (size_t)par * G * SEQ_GRAN, eP, G, hmin, unused, L, &s_stop, a.tmo, t)) return;
@@ -437,6 +456,13 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     int32_t v4[4] = {0, 0, 0, 0};  // feasible count, raw maxima
     uint64_t key0 = 0;
     int32_t imn = INT32_MAX, imx = INT32_MIN;  // InterPodAffinity raw Score over this block's feasible nodes
+    uint32_t smk[PK][2] = {};                  // PodTopologySpread soft pairs of this thread's feasible nodes
+    int32_t snf = 0;
+    if (dbg) {
+      (void)pod.req[0];
+      (void)x.flags;
+    }
+    sublap(1);
 #pragma unroll 1
     for (int k = 0; k < a.npt; k++) {
       int32_t tk = -1, rk[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, -1, 0};
@@ -444,7 +470,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
       if (i < d.n) {
         tk = seq_eval<SM>(c, d, pod, x, i, a.rs != 0, rk, nullptr);
         rk[3] = -1;
-        if (tk >= 0 && q.on && q.nh > 0 && !pts_filter(pa, q, L, hmin, d.n, i)) tk = -1;
+        if (tk >= 0 && q.on && q.hard && !pts_filter(pa, q, L, hmin, d.n, i)) tk = -1;
         if (tk >= 0 && iaf && !ipa_filter(ia, IL, x, d.n, i)) tk = -1;
         if (tk >= 0 && isc) {
           rk[4] = ipa_raw(ia, IL, isc, iw, d.n, i);
@@ -455,7 +481,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
           v4[0]++;
 #pragma unroll
           for (int e = 0; e < 3; e++) v4[1 + e] = max(v4[1 + e], rk[e]);
-          if (soft) rk[3] = pts_soft_mark(pa, q, L, d.n, i) ? 0 : -1;
+          if (soft) rk[3] = pts_soft_mark(pa, q, d.n, i, smk, snf) ? 0 : -1;
           const uint64_t kk = make_key(tk + ext_total(c, ext, rk, zero) + pts_const, i);
           key0 = kk > key0 ? kk : key0;
         }
@@ -464,14 +490,15 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
 #pragma unroll
       for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) s_raw[k][e][t] = rk[e];
     }
+    sublap(2);
+    if (soft) pts_soft_fold(L, smk, snf);  // (L.smask / nfni zeroed by pts_prep; the reduce's barriers order it)
     if (isc) {
       if (t == 0) {
         IL.mm[0] = INT32_MAX;
         IL.mm[1] = INT32_MIN;
       }
       __syncthreads();
-      atomicMin(&IL.mm[0], imn);
-      atomicMax(&IL.mm[1], imx);
+      wave_fold_minmax(imn, imx, &IL.mm[0], &IL.mm[1]);
     }
     seq_block_reduce(v4, key0, s_red, s_key, t);  // (its barriers order the atomics above)
     if (t == 0) {
@@ -488,6 +515,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
         put_granule(g + 16, eA, isc ? (uint32_t)IL.mm[1] : 0u);
       }
     }
+    sublap(3);
     lap(0);
     // ---- every block's granules: the feasible count, the raw maxima and the
     //      best key under zero maxima (+ PodTopologySpread's PreScore pairs)
@@ -511,13 +539,15 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
         IL.mm[1] = INT32_MIN;
       }
       __syncthreads();
+      int32_t a15 = INT32_MAX, a16 = INT32_MIN;
       for (int32_t g = t; g < G; g += SEQ_THREADS) {
         const uint64_t *gg = a.ga + ((size_t)par * G + g) * SEQ_GRAN;
-        atomicMin(&IL.mm[0], (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 15, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT));
-        atomicMax(&IL.mm[1], (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 16, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT));
+        a15 = min(a15, (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 15, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT));
+        a16 = max(a16, (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 16, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT));
       }
+      wave_fold_minmax(a15, a16, &IL.mm[0], &IL.mm[1]);
       __syncthreads();
       gimn = IL.mm[0];
       gimx = IL.mm[1];
@@ -539,13 +569,19 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
           for (int e = 0; e < 2 * PK; e++) (&L.smask[0][0])[e] = 0u;
         }
         __syncthreads();
-        for (int32_t g = t; g < G; g += SEQ_THREADS) {
-          const uint64_t *gg = a.ga + ((size_t)par * G + g) * SEQ_GRAN;
-          atomicAdd(&L.nfni, (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 6, __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT));
-          for (int e = 0; e < 2 * PK; e++)
-            atomicOr(&(&L.smask[0][0])[e], (uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 7 + e,
-                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        {
+          uint32_t gm[PK][2] = {};
+          int32_t gc = 0;
+          for (int32_t g = t; g < G; g += SEQ_THREADS) {
+            const uint64_t *gg = a.ga + ((size_t)par * G + g) * SEQ_GRAN;
+            gc += (int32_t)(uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 6, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int e = 0; e < 2 * PK; e++)
+              gm[e >> 1][e & 1] |= (uint32_t)__hip_atomic_load(const_cast<uint64_t *>(gg) + 7 + e, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+          pts_soft_fold(L, gm, gc);
         }
         __syncthreads();
         nfni = L.nfni;
@@ -572,8 +608,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
         mn = min(mn, r);
         mx = max(mx, r);
       }
-      atomicMin(&L.red[0], mn);
-      atomicMax(&L.red[1], mx);
+      wave_fold_minmax(mn, mx, &L.red[0], &L.red[1]);
       seq_put_minmax(a.gp + ((size_t)par * G + b) * SEQ_GRAN, eP, L, t);
       if (!seq_gather_minmax(a.gp + (size_t)par * G * SEQ_GRAN, eP, G, pmin, pmax, L, &s_stop, a.tmo, t)) return;
     }
@@ -649,8 +684,10 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_seq(DevCfg c, DevNodes d, SeqAr
     if (s_stop) return;
     lap(4);
   }
-  if (dbg)
+  if (dbg) {
     for (int q2 = 0; q2 < 5; q2++) a.dbg[q2] = acc[q2];
+    for (int q2 = 0; q2 < 3; q2++) a.dbg[6 + q2] = sub[q2];
+  }
 }
 
 // ---- parity evaluation (koordhip_eval_ext): per (pod, node) the status bits,
@@ -722,7 +759,7 @@ __global__ __launch_bounds__(256) void k_pts_eval(PtsArgs pa, int32_t n, const D
           const int32_t v = pts_host_match(pa, q, k, n, i);
           if (v >= 0) m = min(m, v);
         }
-    atomicMin(&L.red[0], m);
+    wave_fold_minmax(m, 0, &L.red[0], &L.red[1]);
     __syncthreads();
     hmin = L.red[0];
   }
@@ -732,9 +769,14 @@ __global__ __launch_bounds__(256) void k_pts_eval(PtsArgs pa, int32_t n, const D
       if (status) status[(size_t)p * n + i] |= KOORDHIP_ST_PTS_FAIL;
     }
   __syncthreads();
-  for (int32_t i = t; i < n; i += 256) {
-    w4[i] = wk[i] >= 0 ? ((q.ns == 0 || pts_soft_mark(pa, q, L, n, i)) ? 0 : -1) : -1;
-    if (plane) plane[i] = 0;
+  {
+    uint32_t sm[PK][2] = {};
+    int32_t sc = 0;
+    for (int32_t i = t; i < n; i += 256) {
+      w4[i] = wk[i] >= 0 ? ((q.ns == 0 || pts_soft_mark(pa, q, n, i, sm, sc)) ? 0 : -1) : -1;
+      if (plane) plane[i] = 0;
+    }
+    pts_soft_fold(L, sm, sc);
   }
   __syncthreads();
   if (q.ns == 0) return;
