@@ -107,29 +107,37 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   NV v{};
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
+  // the reads that do not depend on the node row next, so their round trips
+  // overlap the row's: the extended scalars, the static Scores and (without
+  // the Reservation build, whose nomination needs the reservation rows) the
+  // device rows
+  const bool xf = !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x, i, d.n);
+  raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
+  raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   int32_t t;
-  bool nominated = false;
+  bool df = true;
   if constexpr (SM == 2) {
     NumaRowR4 nr{};
     load_numa<true>(nr, d, i, all);
     load_resv(nr, d.rv, i);
     t = c.resv_cpus ? eval_total_resv<KOORDHIP_RESV_SLOTS, true>(p, v, nr, d.nu.cls, c)
                     : eval_total_resv<KOORDHIP_RESV_SLOTS, false>(p, v, nr, d.nu.cls, c);
-    if (rs && (x.flags & KOORDHIP_PODX_DEVICE)) nominated = resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
-  } else if constexpr (SM == 1) {
-    NumaRow nr{};
-    load_numa<true>(nr, d, i, all);
-    t = eval_total_numa<true>(p, v, nr, d.nu.cls, c);
+    const bool nominated = rs && (x.flags & KOORDHIP_PODX_DEVICE) && resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
+    df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                  (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
   } else {
-    t = eval_total(p, v, c);
+    df = dev_eval(c, d.dv, x, i, false, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                  (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
+    if constexpr (SM == 1) {
+      NumaRow nr{};
+      load_numa<true>(nr, d, i, all);
+      t = eval_total_numa<true>(p, v, nr, d.nu.cls, c);
+    } else {
+      t = eval_total(p, v, c);
+    }
   }
-  const bool xf = !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x, i, d.n);
-  const bool df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
-                           (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
   if (status) *status = (xf ? 0 : KOORDHIP_ST_XFIT_FAIL) | (df ? 0 : KOORDHIP_ST_DEVICE_FAIL);
   if (!xf || !df) t = -1;
-  raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
-  raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   raw[3] = 0;  // PodTopologySpread: its own phases (pts.hpp)
   raw[4] = 0;  // InterPodAffinity: ipa.hpp
   return t;
