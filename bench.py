@@ -160,7 +160,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare", "spread", "affinity"], default="config4",
+    ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare", "spread", "affinity",
+                                                   "resvpolicy"], default="config4",
                     help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
                          "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods); "
                          "config5: 200k nodes, 10%% holding a Reservation matched by 20%% of the pods, "
@@ -170,7 +171,10 @@ def main():
                          "the pods in five PodTopologySpread classes, + PodTopologySpread (filter, weight 2): "
                          "the exact sequential cycle, one GPU; affinity: config 4's cluster with zone / hostname "
                          "topology, four apps' running pods and 60%% of the pods carrying pod affinity / "
-                         "anti-affinity terms, + InterPodAffinity (filter, weight 1): the exact sequential cycle")
+                         "anti-affinity terms, + InterPodAffinity (filter, weight 1): the exact sequential cycle; "
+                         "resvpolicy: config 5's profile and cluster with 30%% NUMA topology-policy nodes, up to 4 "
+                         "reservations per node (70%% holding cpusets, on policy nodes too) and 30%% cpuset pods: "
+                         "the exact sequential cycle")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--be-frac", type=float, default=None)
@@ -203,12 +207,13 @@ def main():
                                         with_topology_spread)
     from koordinator_amd.engine import PlacementEngine
 
-    if args.workload in ("deviceshare", "spread", "affinity"):
+    if args.workload in ("deviceshare", "spread", "affinity", "resvpolicy"):
         if world > 1:
             raise SystemExit(f"--workload {args.workload} runs on one GPU (the sequential cycle is not node-sharded)")
         prof = {"deviceshare": lambda: with_deviceshare(shipped_profile()),
                 "spread": lambda: with_topology_spread(shipped_profile()),
-                "affinity": lambda: with_interpod_affinity(shipped_profile())}[args.workload]()
+                "affinity": lambda: with_interpod_affinity(shipped_profile()),
+                "resvpolicy": lambda: shipped_profile(numa=True, reservation=True)}[args.workload]()
         return run_sequential(args, torch, synth, prof, PlacementEngine)
 
     dist = None
@@ -395,6 +400,8 @@ def seq_bytes_per_eval(pods: np.ndarray, ext: np.ndarray, cfg, dev_slots: int) -
     and RDMA slots (minor i32, total + used of the requested resources i64)."""
     from koordinator_amd import abi
     b = bytes_per_eval(pods, cfg).copy()
+    if ext is None:
+        return b
     xm = ext["xmask"].astype(np.int64)
     b += 16 * np.array([bin(int(x)).count("1") for x in xm], np.int64)
     dev = (ext["flags"] & abi.PODX_DEVICE) != 0
@@ -419,15 +426,23 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     """The DeviceShare / spread workloads: one persistent cooperative k_seq
     launch per step (every node filtered and scored per pod, normalized over
     the feasible nodes, the argmax committed before the next pod)."""
-    c = synth.CONFIGS[4]
+    resvpol = args.workload == "resvpolicy"
+    c = synth.CONFIGS[5 if resvpol else 4]
     args.nodes = args.nodes or c["nodes"]
     args.pods = args.pods or 20000
     args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
     spread = args.workload == "spread"
     affinity = args.workload == "affinity"
     table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
-    pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac), prof)
-    if spread or affinity:
+    pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac, cpuset_frac=0.3 if resvpol else 0.0,
+                                            resv_match_frac=c.get("resv_match_frac", 0.0)), prof)
+    if resvpol:
+        # the Reservation plugin on NUMA topology-policy nodes: such snapshots run in the sequential cycle
+        synth.add_numa(table, synth.NumaSpec(policy_frac=0.3), prof)
+        synth.add_reservations(table, synth.ResvSpec(slots=4, multi_frac=0.3))
+        synth.add_reserved_cpus(table, frac=0.7, policy_nodes=True)
+        ext = None
+    elif spread or affinity:
         from koordinator_amd import abi
         table.enable_ext(0)
         ext = abi.pod_ext_array(args.pods)
@@ -443,7 +458,10 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     eng = PlacementEngine(prof, device=0, profile_kernels=False)
     eng.load_snapshot(table)
     eng.checkpoint()
-    eng.stage_pods_ext(pods, ext)
+    if ext is None:
+        eng.stage_pods(pods)
+    else:
+        eng.stage_pods_ext(pods, ext)
 
     def step():
         eng.restore()
@@ -467,8 +485,18 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     alg = float(b.sum()) * args.nodes
     gbs = alg / seq_s / 1e9 if seq_s > 0 else None
     value = args.pods * args.steps / elapsed
+    if ext is None:
+        from koordinator_amd import abi
+        ext = abi.pod_ext_array(args.pods)   # (the counters below: no device / spread / affinity pods)
     dev = (ext["flags"] & 1) != 0
-    if affinity:
+    if resvpol:
+        pol = ((table["numa_flags"].astype(np.int64) >> 3) & 3) != 0
+        wl = (f"resvpolicy: {args.nodes} nodes ({int(pol.mean() * 100)}% with a NUMA topology policy; "
+              f"reservations on {int((table['resv_flags'] != 0).mean() * 100)}% of the nodes, up to 4 per node, "
+              f"70% holding cpusets) x {args.pods} pods (30% cpuset, {int(c['resv_match_frac'] * 100)}% matching "
+              "a reservation), NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource + Reservation, "
+              "the exact sequential cycle")
+    elif affinity:
         wl = (f"affinity: {args.nodes} nodes (6 zones, hostname; 4 apps' running pods) x {args.pods} pods "
               f"({int(((ext['ipa_inc'] | ext['ipa_aff'] | ext['ipa_anti'] | ext['ipa_score']) != 0).mean() * 100)}% "
               "carrying pod affinity / anti-affinity terms), NodeResourcesFit + LoadAwareScheduling + "
@@ -503,7 +531,7 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
                      "us_per_pod": round(seq_s * 1e6 / args.pods, 3)},
     }
     if not args.no_cpu_baseline:
-        cb = cpu_baseline(table, pods, cfg, args.cpu_budget, ext=ext)
+        cb = cpu_baseline(table, pods, cfg, args.cpu_budget, ext=None if resvpol else ext)
         out["cpu_baseline"] = cb
         out["speedup_vs_best_cpu_leg"] = round(value / cb["best_leg"]["pods_per_s"], 1)
     print(json.dumps(out), flush=True)

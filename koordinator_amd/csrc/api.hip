@@ -177,7 +177,9 @@ struct koordhip_ctx {
   double last_eval_ms = 0, last_total_ms = 0;
   std::string eval_kernel, resolve_kernel;  // template instantiations of the last place call's launches
   // the exact sequential cycle (normalized-score plugins: seq.hip)
-  bool seq = false;                // the profile enables DeviceShare or a normalized upstream Score
+  bool seq = false;                // the sequential cycle runs the placements (seq_profile, or a Reservation
+                                   // snapshot with NUMA topology-policy nodes)
+  bool seq_profile = false;        // the profile enables DeviceShare or a normalized upstream Score
   kh::DevPodX *d_podx = nullptr;   // staged koordhip_pod_ext records (NULL: none staged)
   int32_t podx_cap = 0;
   bool podx_staged = false;
@@ -631,8 +633,6 @@ int check_resv_cpus(const koordhip_node_soa *s, int32_t m, int32_t slots, const 
         return fail(KOORDHIP_EINVAL, "resv_cpus on an empty reservation slot");
       const int32_t cls = s->numa_class ? s->numa_class[i] : -1;
       if (cls < 0 || cls >= nclasses) return fail(KOORDHIP_EINVAL, "resv_cpus on a node without a CPU topology");
-      if (s->numa_flags && KOORDHIP_NODE_NUMA_POLICY(s->numa_flags[i]) != 0)
-        return fail(KOORDHIP_EINVAL, "resv_cpus on a NUMA topology-policy node");
       const int32_t ncpu = class_cpus[cls];
       for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) {
         const uint64_t x = s->resv_cpus[w][at];
@@ -729,7 +729,7 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   kh::DevDev &dv = c->d.dv;
   dv = kh::DevDev{};
   const bool dev = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
-  if (!c->seq) {
+  if (!c->seq_profile) {
     if (s->dev_slots > 0 || s->xalloc || s->static_score[0] || s->static_score[1] || s->pts_keys > 0 || s->ipa_ents > 0)
       return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score / topology-spread columns need DeviceShare, "
                                    "PodTopologySpread or a normalized Score plugin in the profile (the sequential cycle)");
@@ -981,6 +981,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
   c->seq = ((cfg->filter_plugins | cfg->score_plugins) &
             (KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_PTS | KOORDHIP_PLUGIN_IPA)) ||
            (cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
+  c->seq_profile = c->seq;
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
   c->side = c->numa || c->resv;
@@ -1216,8 +1217,10 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   if (!e) e = load_numa_columns(c, s, n);
   if (!e) e = load_resv_columns(c, s, n);
   if (!e) e = load_ext_columns(c, s, n);
-  if (!e && c->dc.resv && c->dc.zones)
-    e = fail(KOORDHIP_EINVAL, "the Reservation plugin with NUMA topology-policy nodes is not supported");
+  // the Reservation plugin on NUMA topology-policy nodes: the pipelined greedy's
+  // rows keep either the zones or the reserved CPUs, so such a snapshot runs in
+  // the sequential cycle (seq.hip: eval_total_resv<.., Z>)
+  c->seq = c->seq_profile || (c->dc.resv && c->dc.zones);
   if (e) {
     free_cols(c);
     return e;
@@ -1268,8 +1271,9 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     zrows = rows->numa_zone_alloc && rows->numa_zone_used;
     if (zpolicy && !c->d.nu.za)
       return fail(KOORDHIP_EINVAL, "a NUMA topology policy needs the zone columns at load_snapshot");
-    if (zpolicy && c->dc.resv)
-      return fail(KOORDHIP_EINVAL, "the Reservation plugin with NUMA topology-policy nodes is not supported");
+    if (zpolicy && c->dc.resv && !c->seq)
+      return fail(KOORDHIP_EINVAL, "a NUMA topology policy on a Reservation snapshot without one: load the snapshot "
+                                   "again (such snapshots run in the sequential cycle)");
     zrows = zrows && c->d.nu.za;
   }
   bool amp_rows = false, amp_any = false;
@@ -1385,7 +1389,7 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   }
   // ABI 9: DeviceShare device rows, extended scalars, static Scores (the
   // sequential cycle's columns; element = a node's whole device row)
-  if (c->seq) {
+  if (c->seq_profile) {
     kh::DevDev &dv = c->d.dv;
     if (rows->dev_slots > 0) {
       if (!dv.used || rows->dev_slots != dv.slots || !rows->dev_present || !rows->dev_minor || !rows->dev_total)
@@ -1793,7 +1797,7 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
   if (int e = check_pod_ext(ext, n_pods, &any)) return e;
   if (int e = check_pod_pts(c, ext, n_pods)) return e;
   if (!any) return 0;
-  if (!c->seq) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
+  if (!c->seq_profile) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   if (n_pods > c->podx_cap) {
     if (c->d_podx) HIP_TRY(hipFree(c->d_podx));
     c->d_podx = nullptr;
@@ -1891,8 +1895,9 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
     if (int e = check_pod_ext(ext, n_pods, &any)) return e;
     if (int e = check_pod_pts(c, ext, n_pods)) return e;
   }
+  if (any && !c->seq_profile)
+    return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   if (!c->seq) {
-    if (any) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
     // the per-node plugins only: koordhip_eval, its planes widened
     const int32_t n = c->n;
     const int NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;

@@ -469,43 +469,60 @@ __device__ __forceinline__ int32_t numa_score(const DevPod &p, const NV &v, cons
   double ac = v.a[KOORDHIP_RES_CPU], am = v.a[KOORDHIP_RES_MEM];
   double rc = v.r[KOORDHIP_RES_CPU], rm = v.r[KOORDHIP_RES_MEM];
   uint32_t mask = 0;
+  const bool hp = cs && P && any4(P);  // a nominated reservation's CPUs (the pod is a cpuset pod)
+  int taken_p = 0;                     // how many of them the pod takes
   if (Z && tp != 0) {  // the affinity stored by Filter's admit, then Allocate with it (:80-89)
     double av[2][ZMAX];
     zone_avail_all(r, C.nnuma, av);
     if (!zone_hint(C.nnuma, av, p, tp, &mask)) return 0;
     if (mask) {
+      // Score's getResourceOptions counts P as reusable zone resources (plugin.go:465-479)
+      double ru[ZMAX];
+#pragma unroll
+      for (int k = 0; k < ZMAX; k++) ru[k] = 0.0;
+      if (hp) {
+        zone_reusable(C, P, ru);
+        zone_avail_reus(r, C.nnuma, ru, av);
+      }
       double z[2][ZMAX];
       if (!zone_alloc(C.nnuma, av, p, mask, z)) return 0;
       if (cs) {
         uint64_t m[NW];
-        if (!(KOORDHIP_NUMA_REQUIRED(p.numa_policy) == KOORDHIP_CPUBIND_NONE ? zone_cpus_ok(C, r, p, z)
-                                                                              : zone_allocate(C, r, p, z, m)))
-          return 0;
+        if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) == KOORDHIP_CPUBIND_NONE) {
+          if (!zone_cpus_ok(C, r, p, z, hp ? P : nullptr, &taken_p)) return 0;
+        } else {
+          if (!zone_allocate(C, r, p, z, m, hp ? P : nullptr)) return 0;
+          if (hp) taken_p = popc_and(m, P);
+        }
       }
-      // calculateAllocatableAndRequested over the pod's zones (:134-152)
+      // calculateAllocatableAndRequested over the pod's zones (:134-152), the
+      // allocated amounts less the reusable ones
       ac = am = rc = rm = 0.0;
 #pragma unroll
       for (int k = 0; k < ZMAX; k++)
         if (zone_used(z, k)) {
           ac += r.za[k];
           am += r.za[ZMAX + k];
-          rc += r.zu[0][k];
+          rc += zone_cpu_allocated(r, k, ru);
           rm += r.zu[1][k];
         }
     }
   }
   double qc = p.req[KOORDHIP_RES_CPU];
-  if (cs && P && any4(P)) {  // (no topology policy: Reservation builds have no zones)
+  if (hp) {
     // Allocate with the preferred CPUs (free | P; P is allocated, so disjoint
     // from the free CPUs); calculateAllocatableAndRequested then counts the
-    // allocated CPUs less P's CPUs the pod did not take (:161-166): the pod
-    // takes min(need, |P|) of them
+    // allocated CPUs less P's CPUs the pod did not take (:161-166): without a
+    // hint the pod takes min(need, |P|) of them
     const int need = p.numa_cpus, np = popc4(P);
-    if (popc4(r.fr) + np < need) return 0;
-    if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE &&
-        !numa_allocate_pref(C, r, p, P[0], P[1], P[2], P[3]))
-      return 0;
-    rc = amplify((double)(r.cnt - (np - (need < np ? need : np))) * 1000.0, r.amp);
+    if (!mask) {
+      if (popc4(r.fr) + np < need) return 0;
+      if (KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE &&
+          !numa_allocate_pref(C, r, p, P[0], P[1], P[2], P[3]))
+        return 0;
+      taken_p = need < np ? need : np;
+    }
+    rc = amplify((double)(r.cnt - (np - taken_p)) * 1000.0, r.amp);
     qc = amplify(qc, r.amp);
   } else if (cs) {
     const bool proven = filtered && tp == 0 && KOORDHIP_NUMA_REQUIRED(p.numa_policy) != KOORDHIP_CPUBIND_NONE;
@@ -571,15 +588,26 @@ namespace kh {
 // ... with the Reservation plugin (NM == 3): the cycle's restore of the
 // node's reservation first (every plugin sees the restored NodeInfo), then
 // filterWithReservations and the ranking total of resv.hpp.
-// RC: some reservation holds CPUs (the NM 5 build)
-template <int S, bool RC = false>
+// RC: some reservation holds CPUs (the NM 5 build).  Z (the sequential cycle's
+// topology-policy snapshots; RC with S > 1): the zone row of node zi is read
+// into a copy of the row after the reserved CPUs (which share its bytes) are
+// taken, and the NodeNUMAResource Filter / Score run with the zone code.
+template <int S, bool RC = false, bool Z = false>
 __device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v, const NumaRowRS<S> &r,
-                                                   const DevNumaClass *classes, const DevCfg &c) {
+                                                   const DevNumaClass *classes, const DevCfg &c,
+                                                   const DevNodes *zd = nullptr, int32_t zi = 0) {
   NV w = v;
   uint32_t mm;
   const int nmatch = resv_restore(w, r, p, mm);
   int32_t t;
-  if constexpr (RC && S > 1) {
+  if constexpr (Z) {
+    static_assert(RC && S > 1, "the zone build is the several-slot reserved-CPU build");
+    uint64_t P[NW];
+    resv_pref_cpus(r, p, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P);
+    NumaRow q = r;
+    if (topo_policy(q.nflags) != 0) load_zones(q, *zd, zi);
+    t = eval_total_numa<true>(p, w, q, classes, c, P);
+  } else if constexpr (RC && S > 1) {
     // the NodeNUMAResource Score reads the reserved CPUs of the reservation
     // PreScore nominated on the node (scoring.go:86-166, plugin.go:503-524)
     uint64_t P[NW];
@@ -787,15 +815,30 @@ __device__ __attribute__((noinline)) bool numa_reserve(const DevNumaClass *class
     }
     numa_apply(r, p, cpus, +1, P);
   } else {
+    // the hint is Filter's (no reservation nominated yet); the allocation
+    // counts the nominated reservation's CPUs P as reusable zone resources and
+    // takes them first (getResourceOptions, plugin.go:455-501)
     uint32_t mask;
     double av[2][ZMAX];
     zone_avail_all(r, C.nnuma, av);
     if (!zone_hint(C.nnuma, av, p, tp, &mask)) return false;
+    const bool hp = cs && any4(P);
+    if (hp) {
+      double ru[ZMAX];
+      zone_reusable(C, P, ru);
+      zone_avail_reus(r, C.nnuma, ru, av);
+    }
     double z[2][ZMAX];
     if (mask && !zone_alloc(C.nnuma, av, p, mask, z)) return false;
     if (cs) {
-      if (!(mask ? zone_allocate_in(C, r, p, z, cpus) : numa_allocate_in<WAVE>(C, r, p, cpus))) return false;
-      numa_apply(r, p, cpus, +1);
+      if (mask) {
+        if (!zone_allocate_in(C, r, p, z, cpus, hp ? P : nullptr)) return false;
+      } else if (hp) {
+        if (!numa_allocate_pref_in<WAVE>(C, r, p, P, cpus)) return false;
+      } else if (!numa_allocate_in<WAVE>(C, r, p, cpus)) {
+        return false;
+      }
+      numa_apply(r, p, cpus, +1, P);
     }
     if (mask) {
 #pragma unroll

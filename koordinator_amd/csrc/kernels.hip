@@ -171,9 +171,13 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
   load_numa<true>(nr, d, i, all);
   int nmatch = 0;
   uint32_t mm = 0;
+  uint64_t P[NW] = {0, 0, 0, 0};  // the nominated reservation's reserved CPUs (scoring.go:82 -> plugin.go:503-524)
   if (c.resv) {  // the cycle's Reservation restore: every plugin sees the restored node
     load_resv(nr, d.rv, i);
     nmatch = resv_restore(v, nr, pod, mm);
+    resv_pref_cpus(nr, pod, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P);
+    // a topology-policy node's zone row shares the reserved CPUs' bytes: read it again
+    if (c.zones && topo_policy(nr.nflags) != 0) load_zones(nr, d, i);
   }
   if (status) {
     uint8_t b = 0;
@@ -192,8 +196,6 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
     int32_t *row = scores + (size_t)p * KOORDHIP_NPLUGINS * d.n;
     row[i] = (c.score & KOORDHIP_PLUGIN_FIT) ? fit_score(pod, v, c) : 0;
     row[(size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_LOADAWARE) ? la_score(pod, v, c) : 0;
-    uint64_t P[NW];  // the nominated reservation's reserved CPUs (scoring.go:82 -> plugin.go:503-524)
-    resv_pref_cpus(nr, pod, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P);
     row[2 * (size_t)d.n + i] =
         (c.score & KOORDHIP_PLUGIN_NUMA) ? numa_score<true>(pod, v, nr, d.nu.cls, c, false, P) : 0;
     row[3 * (size_t)d.n + i] = (c.score & KOORDHIP_PLUGIN_BALANCED) ? bal_score(pod, v) : 0;

@@ -871,6 +871,28 @@ __device__ __forceinline__ void zone_avail_all(const NumaRow &r, int M, double a
     }
 }
 
+// ... with getResourceOptions' reusableResources (plugin.go:469-479,
+// node_allocation.go:155-177): zone k's allocated cpu less ru[k] (the
+// nominated reservation's reserved CPUs in zone k x 1000), non-negative
+__device__ __forceinline__ double zone_cpu_allocated(const NumaRow &r, int k, const double ru[ZMAX]) {
+  const double u = r.zu[0][k] - ru[k];
+  return u > 0.0 ? u : 0.0;
+}
+__device__ __forceinline__ void zone_avail_reus(const NumaRow &r, int M, const double ru[ZMAX], double av[2][ZMAX]) {
+#pragma unroll
+  for (int k = 0; k < ZMAX; k++) {
+    const double ac = k < M ? r.za[k] - zone_cpu_allocated(r, k, ru) : 0.0;
+    const double am = k < M ? r.za[ZMAX + k] - r.zu[1][k] : 0.0;
+    av[0][k] = ac > 0.0 ? ac : 0.0;
+    av[1][k] = am > 0.0 ? am : 0.0;
+  }
+}
+// ru[k]: the reservation-preferred CPUs P in zone k x 1000 (no amplification on policy nodes)
+__device__ __forceinline__ void zone_reusable(const DevNumaClass &C, const uint64_t *P, double ru[ZMAX]) {
+#pragma unroll
+  for (int k = 0; k < ZMAX; k++) ru[k] = k < C.nnuma ? (double)popc_and(P, C.nm[k]) * 1000.0 : 0.0;
+}
+
 // bitmask.IsNarrowerThan order as one integer (masks < 256)
 __device__ __forceinline__ int narrow_key(uint32_t m) { return __popc(m) * 256 + (int)m; }
 
@@ -978,44 +1000,80 @@ __device__ __forceinline__ bool zone_used(const double z[2][ZMAX], int k) { retu
 // allocateCPUSet with allocated NUMA nodes (:264-295): zone k takes
 // min(|its available CPUs|, floor(cpu_k / 1000)) CPUs; the sum must be exact.
 // Preferred-only: takeCPUs never fails below |available| (closed form).
+// P: reservation-preferred CPUs (allocated, so disjoint from the free ones;
+// GetAvailableCPUs makes them available), NULL: none.  *taken_p: how many of
+// P the zones' takePreferredCPUs take (min(n_k, |P in zone k|) each).
 __device__ __forceinline__ bool zone_cpus_ok(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
-                                             const double z[2][ZMAX]) {
-  if (popc4(r.fr) < p.numa_cpus) return false;
-  int got = 0;
+                                             const double z[2][ZMAX], const uint64_t *P = nullptr,
+                                             int *taken_p = nullptr) {
+  uint64_t A[NW];
+  for (int w = 0; w < NW; w++) A[w] = r.fr[w] | (P ? P[w] : 0ull);
+  if (popc4(A) < p.numa_cpus) return false;
+  int got = 0, tp = 0;
   for (int k = 0; k < C.nnuma && k < ZMAX; k++)
-    if (zone_used(z, k)) got += min(popc_and(r.fr, C.nm[k]), (int)((long long)z[0][k] / 1000));
+    if (zone_used(z, k)) {
+      const int n = min(popc_and(A, C.nm[k]), (int)((long long)z[0][k] / 1000));
+      got += n;
+      if (P) tp += min(n, popc_and(P, C.nm[k]));
+    }
+  if (taken_p) *taken_p = tp;
   return got == p.numa_cpus;
 }
 
-// ... exact CPUs (Reserve, and Filter / Score under a required policy)
+// ... exact CPUs (Reserve, and Filter / Score under a required policy).
+// P (NULL: none): each zone's takePreferredCPUs (cpu_accumulator.go:29-85)
+// takes from P's CPUs in the zone first, then from the zone's others, both
+// over the allocateInfo P has left (numa_allocate_pref_in)
 __device__ __forceinline__ bool zone_allocate_in(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
-                                                 const double z[2][ZMAX], uint64_t *cpus) {
+                                                 const double z[2][ZMAX], uint64_t *cpus,
+                                                 const uint64_t *P = nullptr) {
   for (int w = 0; w < NW; w++) cpus[w] = 0;
-  if (popc4(r.fr) < p.numa_cpus) return false;
+  NumaRow q = r;
+  uint64_t PP[NW];
+  for (int w = 0; w < NW; w++) {
+    PP[w] = P ? P[w] : 0ull;
+    q.fr[w] |= PP[w];
+    q.ep[w] &= ~PP[w];
+    q.en[w] &= ~PP[w];
+  }
+  if (popc4(q.fr) < p.numa_cpus) return false;
   int got = 0;
   for (int k = 0; k < C.nnuma && k < ZMAX; k++) {
     if (!zone_used(z, k)) continue;
-    uint64_t A[NW], o[NW];
-    for (int w = 0; w < NW; w++) A[w] = r.fr[w] & C.nm[k][w];
-    const int n = min(popc4(A), (int)((long long)z[0][k] / 1000));
+    uint64_t A[NW], B[NW], o[NW];
+    for (int w = 0; w < NW; w++) {
+      A[w] = q.fr[w] & C.nm[k][w] & ~PP[w];
+      B[w] = PP[w] & C.nm[k][w];
+    }
+    const int n = min(popc4(A) + popc4(B), (int)((long long)z[0][k] / 1000));
     if (n <= 0) continue;
-    if (!acc_run(C, r, p, A, n, o)) return false;
-    for (int w = 0; w < NW; w++) cpus[w] |= o[w];
-    got += popc4(o);
+    const int n1 = min(n, popc4(B));
+    if (n1 > 0) {
+      if (!acc_run(C, q, p, B, n1, o)) return false;
+      for (int w = 0; w < NW; w++) cpus[w] |= o[w];
+      got += popc4(o);
+    }
+    if (n > n1) {
+      if (!acc_run(C, q, p, A, n - n1, o)) return false;
+      for (int w = 0; w < NW; w++) cpus[w] |= o[w];
+      got += popc4(o);
+    }
   }
   if (got != p.numa_cpus) return false;
   return required_ok(C, r, p, cpus);
 }
 
 __device__ __attribute__((noinline)) bool zone_allocate(const DevNumaClass &C, const NumaRow &r, const DevPod &p,
-                                                        const double z[2][ZMAX], uint64_t *cpus) {
+                                                        const double z[2][ZMAX], uint64_t *cpus,
+                                                        const uint64_t *P = nullptr) {
   const NumaRow rl = r;
   const DevPod pl = p;
   double zl[2][ZMAX];
   for (int q = 0; q < 2; q++)
     for (int k = 0; k < ZMAX; k++) zl[q][k] = z[q][k];
-  uint64_t o[NW];
-  const bool ok = zone_allocate_in(C, rl, pl, zl, o);
+  uint64_t o[NW], pl4[NW];
+  for (int w = 0; w < NW; w++) pl4[w] = P ? P[w] : 0ull;
+  const bool ok = zone_allocate_in(C, rl, pl, zl, o, P ? pl4 : nullptr);
   for (int w = 0; w < NW; w++) cpus[w] = o[w];
   return ok;
 }

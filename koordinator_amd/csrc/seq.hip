@@ -118,10 +118,11 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   bool df = true;
   if constexpr (SM == 2) {
     NumaRowR4 nr{};
-    load_numa<true>(nr, d, i, all);
+    load_numa<false>(nr, d, i, all);  // (the zone row shares the reserved CPUs' bytes: eval_total_resv<.., Z> reads it)
     load_resv(nr, d.rv, i);
-    t = c.resv_cpus ? eval_total_resv<KOORDHIP_RESV_SLOTS, true>(p, v, nr, d.nu.cls, c)
-                    : eval_total_resv<KOORDHIP_RESV_SLOTS, false>(p, v, nr, d.nu.cls, c);
+    t = c.zones       ? eval_total_resv<KOORDHIP_RESV_SLOTS, true, true>(p, v, nr, d.nu.cls, c, &d, i)
+        : c.resv_cpus ? eval_total_resv<KOORDHIP_RESV_SLOTS, true>(p, v, nr, d.nu.cls, c)
+                      : eval_total_resv<KOORDHIP_RESV_SLOTS, false>(p, v, nr, d.nu.cls, c);
     const bool nominated = rs && (x.flags & KOORDHIP_PODX_DEVICE) && resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
     df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);

@@ -502,8 +502,6 @@ def reserved_cpu_mask(table: NodeTable, i: int, r: Reservation) -> List[int]:
     cls = int(table["numa_class"][i])
     if not cpus or cls < 0 or cls >= len(table.numa_classes):
         return words
-    if (int(table["numa_flags"][i]) >> abi.NODE_NUMA_POLICY_SHIFT) & 3:
-        raise ReservationError(f"reservation {r.name}: reserved CPUs on a NUMA topology-policy node are not supported")
     rec = table.numa_classes[cls]
     pos_of = {int(rec["cpu_id"][p]): p for p in range(int(rec["num_cpus"]))}
     for c in cpus:

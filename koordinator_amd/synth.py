@@ -296,11 +296,13 @@ def add_reservations(t: NodeTable, spec: ResvSpec, seed: int = SEED) -> NodeTabl
 
 
 def add_reserved_cpus(t: NodeTable, frac: float = 0.6, partial_frac: float = 0.4, excl_frac: float = 0.3,
-                      seed: int = SEED) -> NodeTable:
-    """Give a `frac` share of the reservations on NUMA nodes (a CPU topology, no
-    topology policy) a cpuset: ~Allocatable cpu / 1000 CPUs of the node's free
-    ones, whole free cores first (the reserve pod's allocation in NodeAllocation,
-    some with an exclusive policy); on a `partial_frac` share of those with
+                      seed: int = SEED, policy_nodes: bool = False) -> NodeTable:
+    """Give a `frac` share of the reservations on NUMA nodes (a CPU topology; a
+    topology policy only with `policy_nodes`) a cpuset: ~Allocatable cpu / 1000
+    CPUs of the node's free ones, whole free cores first (the reserve pod's
+    allocation in NodeAllocation, some with an exclusive policy; on a policy
+    node its CPUs' zones also hold their count x 1000 of cpu in
+    NodeAllocation.allocatedResources); on a `partial_frac` share of those with
     assigned pods some of the CPUs went to the assigned pods (still allocated,
     no longer reserved: RestoreReservation, nodenumaresource/reservation.go:84-104).
     Call after add_numa and add_reservations."""
@@ -308,7 +310,8 @@ def add_reserved_cpus(t: NodeTable, frac: float = 0.6, partial_frac: float = 0.4
     rnd = splitmix64(s, n, 80)
     for i in range(n):
         cls = int(t["numa_class"][i])
-        if cls < 0 or (int(t["numa_flags"][i]) >> abi.NODE_NUMA_POLICY_SHIFT) & 3:
+        policy = (int(t["numa_flags"][i]) >> abi.NODE_NUMA_POLICY_SHIFT) & 3
+        if cls < 0 or (policy and not policy_nodes):
             continue
         rng = np.random.default_rng(int(rnd[i]))
         rec = t.numa_classes[cls]
@@ -339,6 +342,10 @@ def add_reserved_cpus(t: NodeTable, frac: float = 0.6, partial_frac: float = 0.4
                 elif ex == "NUMANodeLevel":
                     t[f"numa_excl_numa{w}"][i] |= np.uint64(m[w])
             t["numa_alloc_cnt"][i] += len(pick)
+            if policy:
+                node_of = rec["node_of"]
+                for p in pick:
+                    t["numa_zone_used"][i, 0, int(node_of[p])] += 1000
             if int(t[slot_col("resv_assigned", q)][i]) > 0 and rng.random() < partial_frac and len(pick) > 1:
                 gone = rng.choice(len(pick), size=int(rng.integers(1, len(pick) // 2 + 1)), replace=False)
                 for g in gone:

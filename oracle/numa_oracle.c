@@ -624,10 +624,18 @@ static int64_t zone_at(const int64_t *z, int32_t i, int r, int k) {
   return z[((size_t)i * 2 + (size_t)r) * KOORDHIP_NUMA_MAX_NODES + (size_t)k];
 }
 
-/* NodeAllocation.getAvailableNUMANodeResources (node_allocation.go:158-177):
- * allocatable - allocated, non-negative (no amplification, no reservation). */
-static int64_t zone_avail(const orc_state *st, int32_t i, int r, int k) {
-  const int64_t a = zone_at(st->soa->numa_zone_alloc, i, r, k) - zone_at(st->numa_zone_used, i, r, k);
+/* NodeAllocation.getAvailableNUMANodeResources (node_allocation.go:155-177)
+ * with getResourceOptions' reusableResources (plugin.go:465-479): zone k's
+ * allocated cpu less reus[k] (the nominated reservation's reserved CPUs in the
+ * zone x 1000; no amplification on policy nodes), non-negative; then
+ * allocatable - allocated, non-negative.  reus = NULL: none. */
+static int64_t zone_allocated(const orc_state *st, int32_t i, int r, int k, const int64_t *reus) {
+  int64_t u = zone_at(st->numa_zone_used, i, r, k);
+  if (r == 0 && reus) u -= reus[k];
+  return u > 0 ? u : 0;
+}
+static int64_t zone_avail(const orc_state *st, int32_t i, int r, int k, const int64_t *reus) {
+  const int64_t a = zone_at(st->soa->numa_zone_alloc, i, r, k) - zone_allocated(st, i, r, k, reus);
   return a > 0 ? a : 0;
 }
 
@@ -655,7 +663,7 @@ static int node_merge(const orc_state *st, const koordhip_pod *pod, int32_t i, i
         if (req[r] == 0) continue;
         int64_t sum = 0;
         for (int k = 0; k < M; k++)
-          if ((m >> k) & 1) sum += zone_avail(st, i, r, k);
+          if ((m >> k) & 1) sum += zone_avail(st, i, r, k, NULL);
         if (req[r] > sum) sat = 0;
       }
       if (!sat) continue;
@@ -682,14 +690,16 @@ static int node_merge(const orc_state *st, const koordhip_pod *pod, int32_t i, i
 }
 
 /* allocateResourcesByHint (resource_manager.go:166-227): the hinted zones in
- * ascending id take min(available, still requested) of cpu and memory. */
-static int alloc_by_hint(const orc_state *st, const koordhip_pod *pod, int32_t i, int M, uint64_t mask, int64_t *zones) {
+ * ascending id take min(available, still requested) of cpu and memory; the
+ * availability counts the reusable reservation CPUs (reus, NULL: none). */
+static int alloc_by_hint(const orc_state *st, const koordhip_pod *pod, int32_t i, int M, uint64_t mask, int64_t *zones,
+                         const int64_t *reus) {
   int64_t rem[2] = {pod->req[KOORDHIP_RES_CPU], pod->req[KOORDHIP_RES_MEM]};
   for (int q = 0; q < 2 * KOORDHIP_NUMA_MAX_NODES; q++) zones[q] = 0;
   for (int k = 0; k < M; k++) {
     if (!((mask >> k) & 1)) continue;
     for (int r = 0; r < 2; r++) {
-      const int64_t av = zone_avail(st, i, r, k);
+      const int64_t av = zone_avail(st, i, r, k, reus);
       const int64_t a = av < rem[r] ? av : rem[r];
       zones[r * KOORDHIP_NUMA_MAX_NODES + k] = a;
       rem[r] -= a;
@@ -713,7 +723,7 @@ int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t i,
   *nil = best.nil;
   if (!*admit) return 0;
   if (best.nil) return 1;
-  return alloc_by_hint(st, pod, i, M, best.mask, zones);
+  return alloc_by_hint(st, pod, i, M, best.mask, zones, NULL);
 }
 
 /* takePreferredCPUs (cpu_accumulator.go:29-85): the preferred CPUs among the
@@ -750,9 +760,9 @@ static int take_preferred(const koordhip_numa_class *t, const uint64_t *avail_in
  * zone holding a non-zero amount takes floor(cpu / 1000) CPUs from its own
  * available CPUs (:264-295).  pref: the reservation-preferred CPUs (NULL =
  * none): GetAvailableCPUs(preferredCPUs) drops their RefCount 1 -> 0, so they
- * join the available CPUs and leave allocateInfo (node_allocation.go:133-153;
- * Reservation builds have no topology-policy nodes, so pref comes with no
- * zones). */
+ * join the available CPUs and leave allocateInfo (node_allocation.go:133-153);
+ * both branches take them first through takePreferredCPUs (:277-287 per zone,
+ * :298-310 without a hint). */
 static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i, const int64_t *zones, uint64_t *out,
                         const uint64_t *pref) {
   const koordhip_node_soa *s = st->soa;
@@ -786,7 +796,7 @@ static int alloc_cpuset(const orc_state *st, const koordhip_pod *pod, int32_t i,
       const int64_t want = zones[k] / 1000;
       if (want < n) n = (int)want;
       if (n > 0) {
-        if (!orc_take_cpus(t, zav, ep, en, n, policy, excl, most, zo)) return 0;
+        if (!take_preferred(t, zav, pref, ep, en, n, policy, excl, most, zo)) return 0;
         for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) out[w] |= zo[w];
         got += popc(zo);
       }
@@ -816,17 +826,42 @@ int orc_numa_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, u
 }
 
 
-/* The whole Allocate of Filter's topology-manager admit / Reserve on a node
- * with a topology policy (manager.go:58-79 -> plugin Allocate, topology_hint.go:
- * 66-86): the merged hint's zones, then the cpuset inside them. */
+/* reusableResources (plugin.go:469-479): per zone, the reservation-preferred
+ * CPUs in it x 1000 (no amplification: policy nodes have none); NULL when pref
+ * holds no CPU. */
+static const int64_t *reusable_of(const orc_state *st, int32_t i, const uint64_t *pref, int64_t *reus) {
+  const koordhip_node_soa *s = st->soa;
+  if (!pref || !(pref[0] | pref[1] | pref[2] | pref[3])) return NULL;
+  const koordhip_numa_class *t = &s->numa_classes[s->numa_class[i]];
+  for (int k = 0; k < KOORDHIP_NUMA_MAX_NODES; k++) reus[k] = 0;
+  for (int p = 0; p < t->num_cpus; p++)
+    if (bit(pref, p) && t->node_of[p] < KOORDHIP_NUMA_MAX_NODES) reus[t->node_of[p]] += 1000;
+  return reus;
+}
+
+/* The whole Allocate of Filter's topology-manager admit / Score / Reserve on a
+ * node with a topology policy (manager.go:58-79 -> plugin Allocate,
+ * topology_hint.go:66-86): the merged hint's zones, then the cpuset inside
+ * them.  The hint is Filter's (the store's affinity, computed before PreScore
+ * nominates a reservation: no reusable resources); Score and Reserve then
+ * allocate with the nominated reservation's reserved CPUs (pref, NULL: none) as
+ * reusable zone resources and preferred CPUs (getResourceOptions,
+ * plugin.go:455-501). */
 static int policy_allocate(const orc_state *st, const koordhip_pod *pod, int32_t i, int64_t *zones, uint64_t *cpus,
-                           int *has_zones) {
+                           int *has_zones, const uint64_t *pref, int64_t *reus_out) {
   uint64_t mask;
   int32_t nil, admit;
+  int64_t reus[KOORDHIP_NUMA_MAX_NODES];
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
+  if (reus_out)
+    for (int k = 0; k < KOORDHIP_NUMA_MAX_NODES; k++) reus_out[k] = 0;
   if (!orc_numa_hint_alloc(st, pod, i, &mask, &nil, &admit, zones)) return 0;
   *has_zones = !nil;
-  if (pod->flags & KOORDHIP_POD_CPUSET) return alloc_cpuset(st, pod, i, nil ? NULL : zones, cpus, NULL);
+  const int64_t *ru = reusable_of(st, i, pref, reus);
+  if (ru && reus_out)
+    for (int k = 0; k < KOORDHIP_NUMA_MAX_NODES; k++) reus_out[k] = ru[k];
+  if (!nil && ru && !alloc_by_hint(st, pod, i, zones_of(st, i), mask, zones, ru)) return 0;
+  if (pod->flags & KOORDHIP_POD_CPUSET) return alloc_cpuset(st, pod, i, nil ? NULL : zones, cpus, pref);
   return 1;
 }
 
@@ -888,7 +923,7 @@ int orc_numa_filter(const koordhip_config *cfg, const orc_state *st, const koord
     int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES];
     uint64_t cpus[KOORDHIP_NUMA_WORDS];
     int hz;
-    return policy_allocate(st, pod, i, zones, cpus, &hz);
+    return policy_allocate(st, pod, i, zones, cpus, &hz, NULL, NULL);
   }
   return 1;
 }
@@ -928,7 +963,7 @@ int orc_numa_allocate_hint(const orc_state *st, const koordhip_pod *pod, int32_t
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) cpus[w] = 0;
   if (mask) {
     const int M = zones_of(st, i);
-    if (M == 0 || !alloc_by_hint(st, pod, i, M, mask, zones)) return 0; /* :167-169, :209-219 */
+    if (M == 0 || !alloc_by_hint(st, pod, i, M, mask, zones, NULL)) return 0; /* :167-169, :209-219 */
   }
   if (!(pod->flags & KOORDHIP_POD_CPUSET)) return 1;
   return alloc_cpuset(st, pod, i, mask ? zones : NULL, cpus, NULL);
@@ -956,20 +991,21 @@ int64_t orc_numa_score(const koordhip_config *cfg, const orc_state *st, const ko
   int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES];
   uint64_t cpus[KOORDHIP_NUMA_WORDS], pref[KOORDHIP_NUMA_WORDS];
   int hz = 0;
+  int64_t reus[KOORDHIP_NUMA_MAX_NODES];
   orc_resv_pref(cfg, st, pod, i, pref); /* getResourceOptions' preferredCPUs (plugin.go:465-495) */
   if (tp != KOORDHIP_NUMA_TOPO_NONE) {
-    if (!policy_allocate(st, pod, i, zones, cpus, &hz)) return 0; /* :86-89 */
+    if (!policy_allocate(st, pod, i, zones, cpus, &hz, pref, reus)) return 0; /* :86-89 */
   } else if (!alloc_cpuset(st, pod, i, NULL, cpus, pref)) {
     return 0;
   }
-  if (hz) { /* calculateAllocatableAndRequested over the pod's zones :134-152 */
+  if (hz) { /* calculateAllocatableAndRequested over the pod's zones :134-152 (allocated less the reusable CPUs) */
     acpu = amem = rcpu = rmem = 0;
     for (int k = 0; k < KOORDHIP_NUMA_MAX_NODES; k++) {
       if (zones[k] == 0 && zones[KOORDHIP_NUMA_MAX_NODES + k] == 0) continue;
       acpu += zone_at(s->numa_zone_alloc, i, 0, k);
       amem += zone_at(s->numa_zone_alloc, i, 1, k);
-      rcpu += zone_at(st->numa_zone_used, i, 0, k);
-      rmem += zone_at(st->numa_zone_used, i, 1, k);
+      rcpu += zone_allocated(st, i, 0, k, reus);
+      rmem += zone_allocated(st, i, 1, k, NULL);
     }
   }
   /* requested cpu := allocated cpuset size, amplified (:161-166); the cpuset
@@ -999,7 +1035,7 @@ int orc_numa_reserve(orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t
   int64_t zones[2 * KOORDHIP_NUMA_MAX_NODES] = {0};
   int hz = 0;
   if (node_policy(st, i) != KOORDHIP_NUMA_TOPO_NONE) {
-    if (!policy_allocate(st, pod, i, zones, out, &hz)) return 0;
+    if (!policy_allocate(st, pod, i, zones, out, &hz, pref, NULL)) return 0;
   } else if (!alloc_cpuset(st, pod, i, NULL, out, pref)) {
     return 0;
   }
