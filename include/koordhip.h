@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 10
+#define KOORDHIP_ABI_VERSION 11
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -159,7 +159,9 @@ extern "C" {
 #define KOORDHIP_RESV_GROUP_SHIFT 8    /* bits 8-13: owner group g, the pod matches iff bit g of koordhip_pod.resv_match */
 #define KOORDHIP_RESV_GROUP(f) (((f) >> KOORDHIP_RESV_GROUP_SHIFT) & 63u)
 #define KOORDHIP_RESV_MAX_ORDERS 1024  /* distinct reservation-order values (resv_order_rank < this) */
-#define KOORDHIP_RESV_SLOTS 4          /* Available reservations per node (koordhip_node_soa.resv_slots <= this) */
+#define KOORDHIP_RESV_SLOTS 4          /* Available reservations per node on the pipelined greedy */
+#define KOORDHIP_RESV_SLOTS_MAX 8      /* ... in a snapshot (koordhip_node_soa.resv_slots <= this); a snapshot with
+                                          more than KOORDHIP_RESV_SLOTS runs in the sequential cycle (ABI 11) */
 
 /* koordhip_pod.numa_policy, the NUMA PreFilter state (plugin.go:227-255):
  * bits 0-1 requiredCPUBindPolicy, 2-3 preferredCPUBindPolicy (= required when
@@ -344,8 +346,8 @@ typedef struct koordhip_node_soa {
    * nodeSelector, required affinity and tolerations); NULL = every class. */
   const uint32_t *static_allow;
   /* Reservation slots per node held by the resv_* columns: 0 or 1 = one
-   * reservation per node (columns of n values); S in [2, KOORDHIP_RESV_SLOTS]
-   * = up to S per node, every resv_* column then holds S x n values,
+   * reservation per node (columns of n values); S in [2, KOORDHIP_RESV_SLOTS_MAX]
+   * = up to S per node (S > KOORDHIP_RESV_SLOTS: the sequential cycle places), every resv_* column then holds S x n values,
    * slot-major (slot s of node i at [s * n + i]); a node's reservations fill
    * its slots from 0, unused slots have resv_flags 0.  koordhip_update_nodes
    * rows use the loaded snapshot's slot count. */

@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 10
+KOORDHIP_ABI_VERSION = 11
 NRES = 5
 NPLUGINS = 4
 
@@ -54,7 +54,8 @@ RESV_KEY_CPU, RESV_KEY_MEM = 16, 32
 RESV_POLICY_SHIFT, RESV_GROUP_SHIFT = 6, 8
 RESV_POLICY_DEFAULT, RESV_POLICY_ALIGNED, RESV_POLICY_RESTRICTED = 0, 1, 2
 RESV_MAX_GROUPS, RESV_MAX_ORDERS = 64, 1024
-RESV_SLOTS = 4   # Available reservations per node (koordhip_node_soa.resv_slots <= this)
+RESV_SLOTS = 4   # Available reservations per node on the pipelined greedy
+RESV_SLOTS_MAX = 8   # ... in a snapshot (koordhip_node_soa.resv_slots <= this; more than RESV_SLOTS: the sequential cycle)
 
 CPUBIND_NONE, CPUBIND_FULL_PCPUS, CPUBIND_SPREAD_BY_PCPUS = 0, 1, 2
 CPUEXCL_NONE, CPUEXCL_PCPU, CPUEXCL_NUMA = 0, 1, 2

@@ -651,8 +651,8 @@ int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   c->dc.resv = 0;
   c->dc.resv_slots = 1;
   if (!c->resv) return 0;
-  if (s->resv_slots < 0 || s->resv_slots > KOORDHIP_RESV_SLOTS)
-    return fail(KOORDHIP_EINVAL, "resv_slots out of [0, KOORDHIP_RESV_SLOTS]");
+  if (s->resv_slots < 0 || s->resv_slots > KOORDHIP_RESV_SLOTS_MAX)
+    return fail(KOORDHIP_EINVAL, "resv_slots out of [0, KOORDHIP_RESV_SLOTS_MAX]");
   // a snapshot without reservation columns gets zero columns: the Reservation
   // build (NM 3) still runs the plugin, e.g. a pod with a required reservation
   // affinity fails its Filter on every node (plugin.go:378-381)
@@ -1220,7 +1220,9 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   // the Reservation plugin on NUMA topology-policy nodes: the pipelined greedy's
   // rows keep either the zones or the reserved CPUs, so such a snapshot runs in
   // the sequential cycle (seq.hip: eval_total_resv<.., Z>)
-  c->seq = c->seq_profile || (c->dc.resv && c->dc.zones);
+  // (and more than KOORDHIP_RESV_SLOTS reservations per node: the pipelined
+  // rows hold at most that many)
+  c->seq = c->seq_profile || (c->dc.resv && (c->dc.zones || c->dc.resv_slots > KOORDHIP_RESV_SLOTS));
   if (e) {
     free_cols(c);
     return e;

@@ -167,7 +167,7 @@ __global__ void k_eval_full(DevCfg c, DevNodes d, const DevPod *__restrict__ pod
   NV v{};
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
-  NumaRowR4 nr{};
+  NumaRowR8 nr{};  // (every slot count: the sequential cycle's snapshots hold up to KOORDHIP_RESV_SLOTS_MAX)
   load_numa<true>(nr, d, i, all);
   int nmatch = 0;
   uint32_t mm = 0;
@@ -3018,7 +3018,7 @@ __global__ void k_commit(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, i
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const DevPod p = *pod;
   *rc = 0;
-  NumaRowR4 rv{};
+  NumaRowR8 rv{};
   if (c.resv) {
     load_resv(rv, d.rv, node);
     // Unreserve: whether the Reserve went into one of the node's reservations

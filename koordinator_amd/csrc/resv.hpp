@@ -42,14 +42,43 @@ static_assert(sizeof(ResvSlot) == 64, "reservation slot = 64 B");
 
 // A NUMA side row with the node's reservations (NM >= 3 builds).  The
 // several-slot rows (NM 4, which every snapshot with CPU-holding reservations
-// runs) keep each slot's reserved CPUs in NumaRow::rcm.
+// runs) keep each slot's reserved CPUs in NumaRow::rcm; the sequential cycle's
+// rows (KOORDHIP_RESV_SLOTS_MAX slots) keep those of the slots past
+// KOORDHIP_RESV_SLOTS in rcx (rcm_of).
+template <int S, bool X = (S > KOORDHIP_RESV_SLOTS)>
+struct NumaRowRS;
 template <int S>
-struct NumaRowRS : NumaRow {
+struct NumaRowRS<S, false> : NumaRow {
   static constexpr int kSlots = S;
   ResvSlot rs[S];
 };
+template <int S>
+struct NumaRowRS<S, true> : NumaRow {
+  static constexpr int kSlots = S;
+  ResvSlot rs[S];
+  uint64_t rcx[S - KOORDHIP_RESV_SLOTS][NW];
+};
 using NumaRowR = NumaRowRS<1>;
 using NumaRowR4 = NumaRowRS<KOORDHIP_RESV_SLOTS>;
+using NumaRowR8 = NumaRowRS<KOORDHIP_RESV_SLOTS_MAX>;
+
+// slot q's reserved CPUs (q: an unrolled, compile-time index)
+template <int S>
+__device__ __forceinline__ uint64_t *rcm_of(NumaRowRS<S> &r, int q) {
+  if constexpr (S > KOORDHIP_RESV_SLOTS) {
+    return q < KOORDHIP_RESV_SLOTS ? r.rcm[q] : r.rcx[q - KOORDHIP_RESV_SLOTS];
+  } else {
+    return r.rcm[q];
+  }
+}
+template <int S>
+__device__ __forceinline__ const uint64_t *rcm_of(const NumaRowRS<S> &r, int q) {
+  if constexpr (S > KOORDHIP_RESV_SLOTS) {
+    return q < KOORDHIP_RESV_SLOTS ? r.rcm[q] : r.rcx[q - KOORDHIP_RESV_SLOTS];
+  } else {
+    return r.rcm[q];
+  }
+}
 
 constexpr double RESV_NZ_CPU = 100.0;                         // (upstream) DefaultMilliCPURequest
 constexpr double RESV_NZ_MEM = 200.0 * 1024.0 * 1024.0;       // (upstream) DefaultMemoryRequest
@@ -78,7 +107,7 @@ __device__ __forceinline__ void load_resv(NumaRowRS<S> &r, const DevResv &d, int
     if constexpr (S > 1) {
       const bool on = d.rc[0] != nullptr && (x.rf & KOORDHIP_RESV_PRESENT);
 #pragma unroll
-      for (int w = 0; w < NW; w++) r.rcm[q][w] = on ? d.rc[w][at] : 0ull;
+      for (int w = 0; w < NW; w++) rcm_of(r, q)[w] = on ? d.rc[w][at] : 0ull;
     }
   }
 }
@@ -96,7 +125,7 @@ __device__ __forceinline__ void store_resv(const NumaRowRS<S> &r, const DevResv 
     if constexpr (S > 1) {
       if (d.rc[0])
 #pragma unroll
-        for (int w = 0; w < NW; w++) d.rc[w][at] = r.rcm[q][w];
+        for (int w = 0; w < NW; w++) d.rc[w][at] = rcm_of(r, q)[w];
     }
   }
 }
@@ -113,7 +142,7 @@ __device__ __forceinline__ void store_resv_wt(const NumaRowRS<S> &r, const DevRe
     if constexpr (S > 1) {
       if (d.rc[0])
 #pragma unroll
-        for (int w = 0; w < NW; w++) st_wt(&d.rc[w][at], r.rcm[q][w]);
+        for (int w = 0; w < NW; w++) st_wt(&d.rc[w][at], rcm_of(r, q)[w]);
     }
   }
 }
@@ -317,7 +346,7 @@ __device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p, co
   x.rn += 1;
   if constexpr (S > 1) {
 #pragma unroll
-    for (int w = 0; w < NW; w++) r.rcm[q][w] &= ~cpus[w];
+    for (int w = 0; w < NW; w++) rcm_of(r, q)[w] &= ~cpus[w];
   } else {
     (void)cpus;
   }
@@ -336,7 +365,7 @@ __device__ __forceinline__ void resv_pref_cpus(const NumaRowRS<S> &r, const DevP
     const int q = resv_nominate(p, r, mm);
     if (q < 0) return;
 #pragma unroll
-    for (int w = 0; w < NW; w++) P[w] = r.rcm[q][w];
+    for (int w = 0; w < NW; w++) P[w] = rcm_of(r, q)[w];
   } else {
     (void)r;
     (void)p;

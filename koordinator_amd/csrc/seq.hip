@@ -117,12 +117,12 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   int32_t t;
   bool df = true;
   if constexpr (SM == 2) {
-    NumaRowR4 nr{};
+    NumaRowR8 nr{};
     load_numa<false>(nr, d, i, all);  // (the zone row shares the reserved CPUs' bytes: eval_total_resv<.., Z> reads it)
     load_resv(nr, d.rv, i);
-    t = c.zones       ? eval_total_resv<KOORDHIP_RESV_SLOTS, true, true>(p, v, nr, d.nu.cls, c, &d, i)
-        : c.resv_cpus ? eval_total_resv<KOORDHIP_RESV_SLOTS, true>(p, v, nr, d.nu.cls, c)
-                      : eval_total_resv<KOORDHIP_RESV_SLOTS, false>(p, v, nr, d.nu.cls, c);
+    t = c.zones       ? eval_total_resv<KOORDHIP_RESV_SLOTS_MAX, true, true>(p, v, nr, d.nu.cls, c, &d, i)
+        : c.resv_cpus ? eval_total_resv<KOORDHIP_RESV_SLOTS_MAX, true>(p, v, nr, d.nu.cls, c)
+                      : eval_total_resv<KOORDHIP_RESV_SLOTS_MAX, false>(p, v, nr, d.nu.cls, c);
     const bool nominated = rs && (x.flags & KOORDHIP_PODX_DEVICE) && resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
     df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
@@ -200,7 +200,7 @@ template <int SM>
 __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNodes &d, const DevPod &p,
                                                    const DevPodX &x, int32_t w, int32_t nf, bool rs,
                                                    uint64_t *cpus_out, uint32_t *dev_out) {
-  using RV = typename std::conditional<SM == 2, NumaRowR4, NumaRow>::type;
+  using RV = typename std::conditional<SM == 2, NumaRowR8, NumaRow>::type;
   RV rv;
   uint32_t mm = 0u;
   if constexpr (SM == 2) {

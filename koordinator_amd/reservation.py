@@ -397,8 +397,8 @@ def available_by_node(node_index: Dict[str, int], reservations: Sequence[Reserva
         if not r.is_available() or r.node_name not in node_index:
             continue
         rs = placed.setdefault(node_index[r.node_name], [])
-        if len(rs) >= abi.RESV_SLOTS:
-            raise ReservationError(f"node {r.node_name}: more than {abi.RESV_SLOTS} Available reservations")
+        if len(rs) >= abi.RESV_SLOTS_MAX:
+            raise ReservationError(f"node {r.node_name}: more than {abi.RESV_SLOTS_MAX} Available reservations")
         rs.append(r)
     return placed
 

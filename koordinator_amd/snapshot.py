@@ -172,9 +172,9 @@ class NodeTable:
 
     def set_resv_slots(self, slots: int):
         """Hold up to `slots` reservations per node (new slots empty)."""
-        if not 1 <= slots <= abi.RESV_SLOTS:
-            raise ValueError(f"resv_slots must be in [1, {abi.RESV_SLOTS}]")
-        for s in range(1, abi.RESV_SLOTS):
+        if not 1 <= slots <= abi.RESV_SLOTS_MAX:
+            raise ValueError(f"resv_slots must be in [1, {abi.RESV_SLOTS_MAX}]")
+        for s in range(1, abi.RESV_SLOTS_MAX):
             for c in RESV_COLS:
                 name = slot_col(c, s)
                 if s < slots and name not in self.cols:

@@ -77,8 +77,9 @@ def test_reservation_columns():
 
 def test_reservations_fill_node_slots():
     """Several Available reservations on a node take its slots in the given
-    order (the nomination tie rule: lowest slot); more than KOORDHIP_RESV_SLOTS
-    are rejected."""
+    order (the nomination tie rule: lowest slot); more than
+    KOORDHIP_RESV_SLOTS_MAX are rejected (more than KOORDHIP_RESV_SLOTS run in
+    the sequential cycle)."""
     prof = G.resv_profile()
     rs = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": str(2 + i)})) for i in range(3)]
     t, _ = G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"}),
@@ -88,9 +89,12 @@ def test_reservations_fill_node_slots():
     assert all(int(t[slot_col("resv_flags", q)][1]) == 0 for q in range(3))
     soa = t.as_soa()
     assert soa.resv_slots == 3 and soa.resv_alloc[0][2] == 3000 and soa.resv_alloc[0][1] == 0   # slot-major [s * n + i]
-    rs5 = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": "1"})) for i in range(abi.RESV_SLOTS + 1)]
+    rs6 = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": "1"})) for i in range(6)]
+    t6, _ = G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"})], rs6, prof)
+    assert t6.resv_slots == 6 and int(t6[slot_col("resv_alloc0", 5)][0]) == 1000
+    rs9 = [rv.Reservation(f"r{i}", "n0", allocatable=G.rlist({"cpu": "1"})) for i in range(abi.RESV_SLOTS_MAX + 1)]
     with pytest.raises(rv.ReservationError):
-        G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"})], rs5, prof)
+        G.build_resv_nodes([("n0", {"cpu": "32", "memory": "64Gi", "pods": "110"})], rs9, prof)
 
 
 def test_reservation_weight_must_dominate():
