@@ -139,6 +139,15 @@ extern "C" {
 #define KOORDHIP_POD_NUMA_ERROR 128u  /* NUMA: PreFilter error (non-integral cpuset request, plugin.go:242-245) */
 #define KOORDHIP_POD_KEY_CPU 256u     /* "cpu" key present in PodRequestsAndLimits (Reservation nominate / score / Restricted) */
 #define KOORDHIP_POD_KEY_MEM 512u     /* "memory" key present */
+#define KOORDHIP_POD_RESERVE 2048u    /* a reserve pod (IsReservePod, util/reservation): the Reservation Filter checks
+                                         its reservation's nodeName (koordhip_pod_ext.reserve_node) and AllocatePolicy
+                                         against the node's Available reservations (plugin.go:326-362), no reservation
+                                         matches it (transformer.go:60,96; resv_match must be 0), its Reservation
+                                         Score is 0 (scoring.go:127-130) and its Reserve assumes a reservation that is
+                                         not Available yet (no slot, plugin.go:538-548).  A batch holding one runs in
+                                         the sequential cycle (ABI 11) */
+#define KOORDHIP_POD_RESERVE_POLICY_SHIFT 12  /* bits 12-13: the reserve pod's AllocatePolicy (KOORDHIP_RESV_POLICY codes) */
+#define KOORDHIP_POD_RESERVE_POLICY(f) (((f) >> KOORDHIP_POD_RESERVE_POLICY_SHIFT) & 3u)
 #define KOORDHIP_POD_RESV_AFFINITY 1024u /* a required reservation affinity (util/reservation/reservation.go:444-487): a node
                                             without a matched reservation fails the Reservation Filter (plugin.go:378-381) */
 
@@ -461,7 +470,8 @@ typedef struct koordhip_pod_ext {
   uint8_t pts_c[KOORDHIP_PTS_POD];
   uint8_t pts_fl[KOORDHIP_PTS_POD];
   int32_t pts_skew[KOORDHIP_PTS_POD];
-  int32_t pts_reserved;
+  int32_t reserve_node;  /* KOORDHIP_POD_RESERVE: 1 + the node index its reservation names
+                            (GetReservePodNodeName, plugin.go:335-339), 0 = any node */
   /* InterPodAffinity, bit e = count entry e of the snapshot:
    *   ipa_inc   entries that count this pod once it is placed (NodeInfo.AddPod)
    *   ipa_aff   its required affinity terms' entry per topology key: a node

@@ -48,6 +48,8 @@ POD_PROD, POD_DAEMONSET, POD_HAS_REQ, POD_REQ_BCPU, POD_REQ_BMEM = 1, 2, 4, 8, 1
 POD_CPUSET, POD_NUMA_SKIP, POD_NUMA_ERROR = 32, 64, 128
 POD_KEY_CPU, POD_KEY_MEM = 256, 512
 POD_RESV_AFFINITY = 1024
+POD_RESERVE = 2048                  # a reserve pod (IsReservePod): its reservation's nodeName / AllocatePolicy checks
+POD_RESERVE_POLICY_SHIFT = 12       # bits 12-13: the reserve pod's AllocatePolicy (RESV_POLICY_* codes)
 
 RESV_PRESENT, RESV_ALLOCATE_ONCE, RESV_UNSCHEDULABLE, RESV_ORDERED = 1, 2, 4, 8
 RESV_KEY_CPU, RESV_KEY_MEM = 16, 32
@@ -226,7 +228,7 @@ POD_EXT_DTYPE = np.dtype([
     ("pts_c", "u1", (PTS_POD,)),
     ("pts_fl", "u1", (PTS_POD,)),
     ("pts_skew", "<i4", (PTS_POD,)),
-    ("pts_reserved", "<i4"),
+    ("reserve_node", "<i4"),
     ("ipa_inc", "<u4"),
     ("ipa_aff", "<u4"),
     ("ipa_anti", "<u4"),

@@ -183,6 +183,7 @@ struct koordhip_ctx {
   kh::DevPodX *d_podx = nullptr;   // staged koordhip_pod_ext records (NULL: none staged)
   int32_t podx_cap = 0;
   bool podx_staged = false;
+  bool staged_reserve = false;     // the staged batch holds a reserve pod (KOORDHIP_POD_RESERVE): the sequential cycle
   uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
   uint64_t *d_seqg = nullptr;
   void *d_seqdesc = nullptr;  // the sequential cycle's device copies of dc / d
@@ -1621,10 +1622,15 @@ int koordhip_read_resv_cpus(koordhip_ctx *c, uint64_t *cpus) {
   return 0;
 }
 
+static int check_reserve_pods(const koordhip_ctx *c, const koordhip_pod *pods, int32_t n, bool *any);
+
 int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uint8_t *status, int32_t *scores,
                   koordhip_topk *topk, int32_t k) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
-  if (c->seq && n_pods > 0) {  // a normalized-score profile: the sequential cycle's evaluator, first planes
+  bool reserve = false;
+  if (pods)
+    if (int e = check_reserve_pods(c, pods, n_pods, &reserve)) return e;
+  if ((c->seq || reserve) && n_pods > 0) {  // the sequential cycle's evaluator (its first planes)
     if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
     const size_t n = (size_t)c->n, NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
     std::vector<int32_t> sc(scores ? (size_t)n_pods * NPX * n : 0);
@@ -1706,9 +1712,25 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
   return e;
 }
 
+// reserve pods (KOORDHIP_POD_RESERVE) in a batch: validated; true when the
+// Reservation plugin handles one (the batch then runs in the sequential cycle)
+static int check_reserve_pods(const koordhip_ctx *c, const koordhip_pod *pods, int32_t n, bool *any) {
+  *any = false;
+  for (int32_t j = 0; j < n; j++) {
+    if (!(pods[j].flags & KOORDHIP_POD_RESERVE)) continue;
+    if (pods[j].resv_match != 0 || (pods[j].flags & KOORDHIP_POD_RESV_AFFINITY))
+      return fail(KOORDHIP_EINVAL, "a reserve pod matches no reservation (resv_match 0, no reservation affinity)");
+    if (KOORDHIP_POD_RESERVE_POLICY(pods[j].flags) > 2) return fail(KOORDHIP_EINVAL, "reserve pod: unknown allocate policy");
+    *any = *any || c->dc.resv;
+  }
+  return 0;
+}
+
 int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
+  bool reserve = false;
+  if (int e = check_reserve_pods(c, pods, n_pods, &reserve)) return e;
   std::vector<kh::DevPod> hp;
   if (int e = to_dev_pods(pods, n_pods, hp)) return e;
   HIP_TRY(hipSetDevice(c->device));
@@ -1731,6 +1753,7 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->n_staged = n_pods;
   c->podx_staged = false;
+  c->staged_reserve = reserve;
   return 0;
 }
 
@@ -1795,11 +1818,17 @@ static int check_pod_pts(const koordhip_ctx *c, const koordhip_pod_ext *x, int32
 static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pods) {
   c->podx_staged = false;
   if (!ext || n_pods <= 0) return 0;
-  bool any = false;
+  bool any = false, rn = false;
   if (int e = check_pod_ext(ext, n_pods, &any)) return e;
   if (int e = check_pod_pts(c, ext, n_pods)) return e;
-  if (!any) return 0;
-  if (!c->seq_profile) return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
+  for (int32_t j = 0; j < n_pods; j++) {
+    if (ext[j].reserve_node < 0 || ext[j].reserve_node > c->n)
+      return fail(KOORDHIP_EINVAL, "koordhip_pod_ext.reserve_node out of [0, n]");
+    rn = rn || ext[j].reserve_node != 0;
+  }
+  if (any && !c->seq_profile)
+    return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
+  if (!any && !rn) return 0;
   if (n_pods > c->podx_cap) {
     if (c->d_podx) HIP_TRY(hipFree(c->d_podx));
     c->d_podx = nullptr;
@@ -1899,7 +1928,9 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
   }
   if (any && !c->seq_profile)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
-  if (!c->seq) {
+  bool reserve = false;
+  if (int e = check_reserve_pods(c, pods, n_pods, &reserve)) return e;
+  if (!c->seq && !reserve) {
     // the per-node plugins only: koordhip_eval, its planes widened
     const int32_t n = c->n;
     const int NPX = KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS;
@@ -2130,7 +2161,7 @@ int place_staged_impl(koordhip_ctx *c) {
   c->pipe_err = false;
   c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
-  if (c->seq) return seq_place(c);
+  if (c->seq || c->staged_reserve) return seq_place(c);
   if (c->podx_staged)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises

@@ -30,7 +30,7 @@ struct DevPodX {
   uint8_t pts_c[KOORDHIP_PTS_POD];
   uint8_t pts_fl[KOORDHIP_PTS_POD];
   int32_t pts_skew[KOORDHIP_PTS_POD];
-  int32_t pts_reserved;
+  int32_t reserve_node;  // KOORDHIP_POD_RESERVE: 1 + the node its reservation names, 0 = any
   uint32_t ipa_inc, ipa_aff, ipa_anti, ipa_score, ipa_flags;
   int32_t ipa_reserved;
   int32_t ipa_w[KOORDHIP_IPA_ENTRIES];

@@ -373,6 +373,25 @@ __device__ __forceinline__ void resv_pref_cpus(const NumaRowRS<S> &r, const DevP
   }
 }
 
+// The Reservation Filter of a reserve pod (plugin.go:326-362): its
+// reservation's nodeName (reserve_node - 1; 0 = none), and its AllocatePolicy
+// against every Available reservation of the node -- Default coexists only
+// with Default.
+template <int S>
+__device__ __forceinline__ bool reserve_pod_ok(const DevPod &p, int32_t reserve_node, const NumaRowRS<S> &r,
+                                               int32_t i) {
+  if (reserve_node > 0 && i != reserve_node - 1) return false;
+  const uint32_t pol = KOORDHIP_POD_RESERVE_POLICY(p.flags);
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < S; q++) {
+    const uint32_t rf = r.rs[q].rf;
+    const uint32_t rp = KOORDHIP_RESV_POLICY(rf);
+    ok &= !((rf & KOORDHIP_RESV_PRESENT) && (pol == 0u || rp == 0u) && pol != rp);
+  }
+  return ok;
+}
+
 // a slot of the node holds an Available reservation whose owner group `p` matches
 template <int S>
 __device__ __forceinline__ bool resv_matchable(const NumaRowRS<S> &r, const DevPod &p) {

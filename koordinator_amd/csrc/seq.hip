@@ -115,7 +115,7 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
   raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   int32_t t;
-  bool df = true;
+  bool df = true, rfail = false;
   if constexpr (SM == 2) {
     NumaRowR8 nr{};
     load_numa<false>(nr, d, i, all);  // (the zone row shares the reserved CPUs' bytes: eval_total_resv<.., Z> reads it)
@@ -126,6 +126,9 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
     const bool nominated = rs && (x.flags & KOORDHIP_PODX_DEVICE) && resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
     df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
+    if ((p.flags & KOORDHIP_POD_RESERVE) && (c.filt & KOORDHIP_PLUGIN_RESERVATION) &&
+        !reserve_pod_ok(p, x.reserve_node, nr, i))
+      rfail = true;
   } else {
     df = dev_eval(c, d.dv, x, i, false, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
@@ -137,8 +140,9 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
       t = eval_total(p, v, c);
     }
   }
-  if (status) *status = (xf ? 0 : KOORDHIP_ST_XFIT_FAIL) | (df ? 0 : KOORDHIP_ST_DEVICE_FAIL);
-  if (!xf || !df) t = -1;
+  if (status)
+    *status = (xf ? 0 : KOORDHIP_ST_XFIT_FAIL) | (df ? 0 : KOORDHIP_ST_DEVICE_FAIL) | (rfail ? KOORDHIP_ST_RESV_FAIL : 0);
+  if (!xf || !df || rfail) t = -1;
   raw[3] = 0;  // PodTopologySpread: its own phases (pts.hpp)
   raw[4] = 0;  // InterPodAffinity: ipa.hpp
   return t;

@@ -403,12 +403,12 @@ class Informer:
         """koordhip_pod_ext records (DeviceShare, extended scalars, topology
         spread constraints in the loaded snapshot's tables)."""
         from .marshal import pod_ext_records
-        return pod_ext_records(pods, self.profile, self.cluster.spread, self.cluster.ipa)
+        return pod_ext_records(pods, self.profile, self.cluster.spread, self.cluster.ipa, self.reservations, self._index)
 
     def pod_records(self, pods):
         """Pod records with the current owner groups' match masks and static classes."""
         from .marshal import pod_records
-        return pod_records(pods, self.profile, self.resv_index, self.static_classes)
+        return pod_records(pods, self.profile, self.resv_index, self.static_classes, self.reservations)
 
     # ---- deltas ----------------------------------------------------------------------------
     def _sync_assigned(self):

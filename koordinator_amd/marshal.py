@@ -14,7 +14,7 @@ from typing import Dict, Iterable, List, Optional, Set, Tuple
 import numpy as np
 
 from . import abi, numa, k8s
-from .config import LoadAwareSchedulingArgs, Profile
+from .config import PLUGIN_RESERVATION, LoadAwareSchedulingArgs, Profile
 from .snapshot import NodeTable, pod_array
 
 DEFAULT_MILLI_CPU_REQUEST = 250                 # estimator/default_estimator.go:35-38
@@ -227,12 +227,16 @@ def static_class_of(pod: k8s.Pod, profile: Profile, static_classes) -> int:
 
 
 def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None, resv_index=None,
-               static_classes=None) -> np.ndarray:
+               static_classes=None, reservations=None) -> np.ndarray:
     """One koordhip_pod record for `pod` (the per-pod PreFilter products);
     `resv_index` (reservation.ReservationIndex): the snapshot's reservation
     owner groups the pod is matched against; `static_classes`
     (nodefilters.StaticClasses): the snapshot's pod static classes (required
-    when the profile enables NodeUnschedulable / NodeAffinity / TaintToleration)."""
+    when the profile enables NodeUnschedulable / NodeAffinity / TaintToleration);
+    `reservations` (name -> reservation.Reservation): the reservations reserve
+    pods belong to (required for a reserve pod when the profile enables the
+    Reservation plugin; a pinned reserve pod's node goes in its
+    koordhip_pod_ext record, pod_ext_records)."""
     p = profile.resolved()
     rec = out if out is not None else pod_array(1)[0]
     req, present = fit_request(pod)
@@ -273,14 +277,19 @@ def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None,
     rec["numa_policy"] = pol
     rec["resv_match"] = resv_index.pod_mask(pod) if resv_index is not None else 0
     rec["static_class"] = static_class_of(pod, profile, static_classes)
+    if rv.is_reserve_pod(pod) and _uses(p, PLUGIN_RESERVATION):
+        if reservations is None:
+            raise MarshalError(f"reserve pod {pod.key}: pass the reservations (name -> Reservation)")
+        rv.reserve_pod_fields(rec, None, pod, reservations, {})
     return rec
 
 
-def pod_records(pods: Iterable[k8s.Pod], profile: Profile, resv_index=None, static_classes=None) -> np.ndarray:
+def pod_records(pods: Iterable[k8s.Pod], profile: Profile, resv_index=None, static_classes=None,
+                reservations=None) -> np.ndarray:
     pods = list(pods)
     arr = pod_array(len(pods))
     for i, p in enumerate(pods):
-        pod_record(p, profile, arr[i], resv_index, static_classes)
+        pod_record(p, profile, arr[i], resv_index, static_classes, reservations)
     return arr
 
 
@@ -654,10 +663,12 @@ def ipa_row(table: NodeTable, i: int, node: k8s.Node, cluster: ClusterState):
     table["ipa_cnt"][i] = node_ipa(reg, pods_on_node)
 
 
-def pod_ext_records(pods, profile: Profile, spread=None, ipa=None) -> np.ndarray:
+def pod_ext_records(pods, profile: Profile, spread=None, ipa=None, reservations=None, node_index=None) -> np.ndarray:
     """koordhip_pod_ext records: DeviceShare requests, extended scalars,
     (PodTopologySpread in the profile) the pods' spread constraints in the
-    registry's tables and (InterPodAffinity) their count-entry masks and weights."""
+    registry's tables, (InterPodAffinity) their count-entry masks and weights
+    and (the Reservation plugin) a pinned reserve pod's node (`node_index`:
+    node name -> snapshot row)."""
     from . import deviceshare as ds
     from .config import PLUGIN_PTS
     from .topologyspread import pod_pts_fields
@@ -678,6 +689,14 @@ def pod_ext_records(pods, profile: Profile, spread=None, ipa=None) -> np.ndarray
             if not ipa.covers(p):
                 raise MarshalError(f"pod {p.key}: affinity terms first seen after the snapshot was built: rebuild it")
             ipa.pod_fields(arr[j], p)
+    if _uses(profile, PLUGIN_RESERVATION):
+        from . import reservation as rv
+        for j, p in enumerate(pods):
+            if rv.is_reserve_pod(p):
+                if reservations is None or node_index is None:
+                    raise MarshalError(f"reserve pod {p.key}: pass the reservations and the node index")
+                scratch = pod_array(1)[0]
+                rv.reserve_pod_fields(scratch, arr[j], p, reservations, node_index)
     return arr
 
 

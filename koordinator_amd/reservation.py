@@ -291,6 +291,7 @@ class Reservation:
     cpus: List[int] = field(default_factory=list)
     assigned_cpus: List[int] = field(default_factory=list)
     cpu_exclusive: str = ""                                        # the reserve pod's preferredCPUExclusivePolicy
+    spec_node_name: str = ""                                       # Spec.Template.Spec.NodeName (a pinned reservation)
 
     def reserved_cpus(self) -> List[int]:
         """RestoreReservation's reservedCPUs of this reservation: its allocated
@@ -304,6 +305,56 @@ class Reservation:
     def reserve_pod(self) -> k8s.Pod:
         return k8s.Pod(name=f"reserve-{self.name}", containers=list(self.template) or
                        [k8s.Container(requests=dict(self.allocatable))])
+
+
+ANNOTATION_RESERVE_POD = "scheduling.koordinator.sh/reserve-pod"
+ANNOTATION_RESERVATION_NAME = "scheduling.koordinator.sh/reservation-name"
+ANNOTATION_RESERVATION_NODE = "scheduling.koordinator.sh/reservation-node"
+
+
+def is_reserve_pod(pod: k8s.Pod) -> bool:
+    """IsReservePod, util/reservation/reservation.go:172-174."""
+    return (pod.annotations or {}).get(ANNOTATION_RESERVE_POD) == "true"
+
+
+def new_reserve_pod(r: Reservation) -> k8s.Pod:
+    """NewReservePod (util/reservation/reservation.go:53-110) of a pending
+    reservation: the template's containers, the reservation's labels, the
+    reserve-pod / reservation-name annotations and, for a pinned reservation,
+    the reservation-node annotation (spec.nodeName cleared); priority 0 when
+    unset."""
+    ann = {ANNOTATION_RESERVE_POD: "true", ANNOTATION_RESERVATION_NAME: r.name}
+    if r.spec_node_name:
+        ann[ANNOTATION_RESERVATION_NODE] = r.spec_node_name
+    return k8s.Pod(name=reservation_key(r), uid=r.uid, labels=dict(r.labels), annotations=ann, priority=0,
+                   containers=list(r.template) or [k8s.Container(requests=dict(r.allocatable))])
+
+
+def reservation_key(r: Reservation) -> str:
+    """GetReservationKey: the UID when set, else the name."""
+    return r.uid or r.name
+
+
+def reserve_pod_fields(rec, ext_rec, pod: k8s.Pod, reservations: Dict[str, Reservation],
+                       node_index: Dict[str, int]) -> None:
+    """Mark a reserve pod's koordhip_pod record (KOORDHIP_POD_RESERVE, its
+    reservation's AllocatePolicy; no reservation matches it, transformer.go:60,96)
+    and its koordhip_pod_ext.reserve_node (the node its reservation names,
+    plugin.go:335-339; ext_rec None: the pod may not name one)."""
+    name = (pod.annotations or {}).get(ANNOTATION_RESERVATION_NAME, "")
+    r = reservations.get(name)
+    if r is None:                                    # rLister.Get fails: framework.Error (plugin.go:341-344)
+        raise ReservationError(f"reserve pod {pod.key}: reservation {name!r} not found")
+    if r.allocate_policy not in _POLICY_CODE:
+        raise ReservationError(f"reservation {r.name}: unknown allocate policy {r.allocate_policy!r}")
+    rec["flags"] = int(rec["flags"]) | abi.POD_RESERVE | (_POLICY_CODE[r.allocate_policy] << abi.POD_RESERVE_POLICY_SHIFT)
+    rec["flags"] = int(rec["flags"]) & ~abi.POD_RESV_AFFINITY
+    rec["resv_match"] = 0
+    node = (pod.annotations or {}).get(ANNOTATION_RESERVATION_NODE, "")
+    if node and ext_rec is not None:
+        if node not in node_index:       # (the reference finds no node; the record cannot say "none")
+            raise ReservationError(f"reserve pod {pod.key}: node {node!r} is not in the snapshot")
+        ext_rec["reserve_node"] = node_index[node] + 1
 
 
 def parse_order(labels: Dict[str, str]) -> int:

@@ -317,6 +317,14 @@ uint32_t orc_score_plugin_bit(int p) {
 /* Combined evaluation                                                       */
 /* ------------------------------------------------------------------------ */
 
+/* The Reservation plugin's Filter: a reserve pod's own checks, else
+ * filterWithReservations (a node without reservation columns fails only a
+ * required reservation affinity). */
+static int resv_pass(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i) {
+  if (pod->flags & KOORDHIP_POD_RESERVE) return orc_resv_reserve_pod_ok(st, pod, x, i);
+  return st->soa->resv_flags ? orc_resv_filter(st, pod, i) : !(pod->flags & KOORDHIP_POD_RESV_AFFINITY);
+}
+
 static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod,
                         const koordhip_pod_ext *x, const orc_pts *ps, const orc_ipa *ia, int32_t i) {
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NODE_STATIC) && !orc_static_filter(st, pod, i)) return 0;
@@ -327,9 +335,7 @@ static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const k
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) return 0;
-  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) &&
-      (st->soa->resv_flags ? !orc_resv_filter(st, pod, i) : (pod->flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
-    return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && !resv_pass(st, pod, x, i)) return 0;
   return 1;
 }
 
@@ -385,8 +391,7 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !fit_ok) b |= KOORDHIP_ST_FIT_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !la_ok) b |= KOORDHIP_ST_LA_FAIL;
         if (!numa_ok) b |= KOORDHIP_ST_NUMA_FAIL;
-        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) &&
-      (st->soa->resv_flags ? !orc_resv_filter(st, pod, i) : (pod->flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && !resv_pass(st, pod, NULL, i))
           b |= KOORDHIP_ST_RESV_FAIL;
         status[(size_t)p * n + i] = b;
       }
@@ -470,8 +475,7 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_xfit_filter(st, x, i)) b |= KOORDHIP_ST_XFIT_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) b |= KOORDHIP_ST_LA_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) b |= KOORDHIP_ST_NUMA_FAIL;
-        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) &&
-            (st->soa->resv_flags ? !orc_resv_filter(st, pod, i) : (pod->flags & KOORDHIP_POD_RESV_AFFINITY) != 0))
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && !resv_pass(st, pod, x, i))
           b |= KOORDHIP_ST_RESV_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) b |= KOORDHIP_ST_DEVICE_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_PTS) && !orc_pts_filter(st, x, &ps, i)) b |= KOORDHIP_ST_PTS_FAIL;

@@ -194,6 +194,8 @@ void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i, const ui
 /* getReservationReservedCPUs (nodenumaresource/plugin.go:503-524): the reserved
  * CPUs left in the reservation PreScore nominated on node i, for a cpuset pod;
  * zero when none */
+/* the Reservation Filter of a KOORDHIP_POD_RESERVE pod (x: its ext record or NULL) */
+int orc_resv_reserve_pod_ok(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i);
 void orc_resv_pref(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i, uint64_t *P);
 void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int32_t *feasible, int32_t nf,
                          int64_t *norm);

@@ -180,6 +180,24 @@ int orc_resv_filter(const orc_state *st, const koordhip_pod *pod, int32_t i) {
   return n_ar == 0;
 }
 
+/* The Reservation Filter of a reserve pod (plugin.go:326-362): its
+ * reservation's nodeName (x->reserve_node - 1, 0 / no record = none), then the
+ * allocate-policy conflict with every Available reservation on the node
+ * (:342-356: Default coexists only with Default); filterWithReservations is
+ * not run for it (:365-367).  1 = pass. */
+int orc_resv_reserve_pod_ok(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i) {
+  if (x && x->reserve_node > 0 && i != x->reserve_node - 1) return 0; /* ErrReasonNodeNotMatchReservation */
+  if (!st->soa->resv_flags) return 1;
+  const uint32_t pol = KOORDHIP_POD_RESERVE_POLICY(pod->flags);
+  for (int s = 0; s < orc_resv_slots(st); s++) {
+    const uint32_t rf = st->soa->resv_flags[at(st, s, i)];
+    if (!(rf & KOORDHIP_RESV_PRESENT)) continue;
+    const uint32_t rp = KOORDHIP_RESV_POLICY(rf);
+    if ((pol == 0 || rp == 0) && pol != rp) return 0; /* ErrReasonReservationAllocatePolicyConflict */
+  }
+  return 1;
+}
+
 /* FilterReservation (plugin.go:504-535) of slot x, a matched reservation */
 static int slot_passes(const orc_state *st, const koordhip_pod *pod, size_t x) {
   const uint32_t rf = st->soa->resv_flags[x];
