@@ -315,16 +315,33 @@ struct Acc {
   int most;  // 1: MostAllocated (ascending free), 0: LeastAllocated
 };
 
-__device__ __forceinline__ bool tbit(const uint64_t *m, int p) { return (m[p >> 6] >> (p & 63)) & 1ull; }
-__device__ __forceinline__ void sbit(uint64_t *m, int p) { m[p >> 6] |= 1ull << (p & 63); }
+// Bit p of a 4-word mask held in registers: the word is chosen by selects,
+// never by a dynamic index (which would move the whole array to scratch).
+__device__ __forceinline__ bool tbit(const uint64_t *m, int p) {
+  const int w = p >> 6;
+  const uint64_t x = w == 0 ? m[0] : (w == 1 ? m[1] : (w == 2 ? m[2] : m[3]));
+  return (x >> (p & 63)) & 1ull;
+}
+__device__ __forceinline__ void sbit(uint64_t *m, int p) {
+  const uint64_t b = 1ull << (p & 63);
+#pragma unroll
+  for (int w = 0; w < NW; w++) m[w] |= (w == (p >> 6)) ? b : 0ull;
+}
+__device__ __forceinline__ void cbit(uint64_t *m, int p) {
+  const uint64_t b = 1ull << (p & 63);
+#pragma unroll
+  for (int w = 0; w < NW; w++) m[w] &= (w == (p >> 6)) ? ~b : ~0ull;
+}
+// ... of a mask in memory (the class tables): one load
+__device__ __forceinline__ bool tbit_mem(const uint64_t *m, int p) { return (m[p >> 6] >> (p & 63)) & 1ull; }
 
 __device__ __forceinline__ void acc_take1(const DevNumaClass &C, Acc &a, int p) {
   sbit(a.R, p);
-  a.A[p >> 6] &= ~(1ull << (p & 63));
+  cbit(a.A, p);
   if (a.excl == (int)KOORDHIP_CPUEXCL_PCPU) sbit(a.XC, p - (p % C.cpc));
   if (a.excl == (int)KOORDHIP_CPUEXCL_NUMA)
     for (int k = 0; k < C.nnuma; k++)
-      if (tbit(C.nm[k], p)) a.XN |= 1u << k;
+      if (tbit_mem(C.nm[k], p)) a.XN |= 1u << k;
   a.need--;
 }
 
@@ -659,8 +676,9 @@ __device__ __forceinline__ bool acc_take_cpus(const DevNumaClass &C, Acc &a, int
       for (int i = 0; i < nu; i++) {
         for (int w = 0; w < NW; w++) T[w] = FA[w] & C.sm[uo[i]][w];
         bool stop = false;
-        for (int w = 0; w < NW && !stop; w++) {
-          uint64_t x = T[w];
+#pragma unroll
+        for (int w = 0; w < NW; w++) {  // (unrolled: T stays in registers)
+          uint64_t x = stop ? 0ull : T[w];
           while (x) {
             const int b = __builtin_ctzll(x);
             uint64_t core = (cpc == 1) ? (1ull << b) : (3ull << b);
