@@ -89,11 +89,15 @@ __device__ __forceinline__ uint32_t ext_bits(const DevCfg &c) {
 
 // SM: the compiled side-row mode -- 0 none (Fit / LoadAware / static /
 // balanced), 1 + NodeNUMAResource (with the zone code), 2 + Reservation (the
-// several-slot rows, with NUMA when enabled).  The plain build keeps no side
-// row at all: a zero-initialised ~0.5 KB row per lane would live in scratch.
+// 4-slot rows, with NUMA when enabled), 3 the same with the 8-slot rows
+// (more than KOORDHIP_RESV_SLOTS reservations on a node).  The plain build
+// keeps no side row at all: a zero-initialised ~0.5 KB row per lane would live
+// in scratch.
 __host__ __device__ constexpr int seq_mode(const DevCfg &c) {
-  return c.resv ? 2 : (((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) ? 1 : 0);
+  return c.resv ? (c.resv_slots > KOORDHIP_RESV_SLOTS ? 3 : 2) : (((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) ? 1 : 0);
 }
+template <int SM>
+using SeqResvRow = NumaRowRS<SM == 3 ? KOORDHIP_RESV_SLOTS_MAX : KOORDHIP_RESV_SLOTS>;
 
 // One node for one pod: the total of the per-node plugins (-1: some Filter
 // fails; with the Reservation plugin the ranking total of resv.hpp) and the
@@ -116,13 +120,14 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   int32_t t;
   bool df = true, rfail = false;
-  if constexpr (SM == 2) {
-    NumaRowR8 nr{};
+  if constexpr (SM >= 2) {
+    constexpr int S = SM == 3 ? KOORDHIP_RESV_SLOTS_MAX : KOORDHIP_RESV_SLOTS;
+    SeqResvRow<SM> nr{};
     load_numa<false>(nr, d, i, all);  // (the zone row shares the reserved CPUs' bytes: eval_total_resv<.., Z> reads it)
     load_resv(nr, d.rv, i);
-    t = c.zones       ? eval_total_resv<KOORDHIP_RESV_SLOTS_MAX, true, true>(p, v, nr, d.nu.cls, c, &d, i)
-        : c.resv_cpus ? eval_total_resv<KOORDHIP_RESV_SLOTS_MAX, true>(p, v, nr, d.nu.cls, c)
-                      : eval_total_resv<KOORDHIP_RESV_SLOTS_MAX, false>(p, v, nr, d.nu.cls, c);
+    t = c.zones       ? eval_total_resv<S, true, true>(p, v, nr, d.nu.cls, c, &d, i)
+        : c.resv_cpus ? eval_total_resv<S, true>(p, v, nr, d.nu.cls, c)
+                      : eval_total_resv<S, false>(p, v, nr, d.nu.cls, c);
     const bool nominated = rs && (x.flags & KOORDHIP_PODX_DEVICE) && resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
     df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
@@ -204,16 +209,16 @@ template <int SM>
 __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNodes &d, const DevPod &p,
                                                    const DevPodX &x, int32_t w, int32_t nf, bool rs,
                                                    uint64_t *cpus_out, uint32_t *dev_out) {
-  using RV = typename std::conditional<SM == 2, NumaRowR8, NumaRow>::type;
+  using RV = typename std::conditional<SM >= 2, SeqResvRow<SM>, NumaRow>::type;
   RV rv;
   uint32_t mm = 0u;
-  if constexpr (SM == 2) {
+  if constexpr (SM >= 2) {
     load_resv(rv, d.rv, w);
     mm = resv_matched(rv, p);
   }
   const bool prescore = rs && nf > 1;
   bool nominated = false;
-  if constexpr (SM == 2) nominated = prescore && resv_nominate(p, rv, mm) >= 0;
+  if constexpr (SM >= 2) nominated = prescore && resv_nominate(p, rv, mm) >= 0;
   uint32_t slots[DT] = {0u, 0u, 0u};
   int64_t per[DT][DR];
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
@@ -232,13 +237,13 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
       NumaRow r;
       load_numa_row(r, d, w);
       uint64_t pref[NW] = {0, 0, 0, 0};
-      if constexpr (SM == 2) resv_pref_cpus(rv, p, prescore ? mm : 0u, pref);
+      if constexpr (SM >= 2) resv_pref_cpus(rv, p, prescore ? mm : 0u, pref);
       if (!numa_reserve<true>(d.nu.cls, r, p, m, pref)) return KOORDHIP_RESERVE_FAILED;
       store_numa_row(r, d, w);
     }
   }
   if (dev) dev_apply(d.dv, w, slots, per);
-  if constexpr (SM == 2) {  // Reservation Reserve: assumePod into the nominated reservation
+  if constexpr (SM >= 2) {  // Reservation Reserve: assumePod into the nominated reservation
     resv_assume(rv, p, m);
     store_resv(rv, d.rv, w);
   }
@@ -961,12 +966,15 @@ hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, co
   // every block must be resident (blocks read each other's granules): the
   // cooperative launch checks the grid against the occupancy
   const int sm = seq_mode(c);
-  const void *f = sm == 2 ? (const void *)k_seq<2> : sm == 1 ? (const void *)k_seq<1> : (const void *)k_seq<0>;
+  const void *f = sm == 3   ? (const void *)k_seq<3>
+                  : sm == 2 ? (const void *)k_seq<2>
+                  : sm == 1 ? (const void *)k_seq<1>
+                            : (const void *)k_seq<0>;
   return hipLaunchCooperativeKernel(f, dim3(grid), dim3(SEQ_THREADS), args, 0, s);
 }
 
 const char *seq_kernel_name(const DevCfg &c) {
-  static const char *names[3] = {"kh::k_seq<0>", "kh::k_seq<1>", "kh::k_seq<2>"};
+  static const char *names[4] = {"kh::k_seq<0>", "kh::k_seq<1>", "kh::k_seq<2>", "kh::k_seq<3>"};
   return names[seq_mode(c)];
 }
 
@@ -976,6 +984,7 @@ hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pod
   if (n_pods <= 0 || d.n <= 0) return hipSuccess;
   const dim3 g((d.n + 255) / 256, n_pods);
   switch (seq_mode(c)) {
+    case 3: hipLaunchKernelGGL(k_seq_eval<3>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work); break;
     case 2: hipLaunchKernelGGL(k_seq_eval<2>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work); break;
     case 1: hipLaunchKernelGGL(k_seq_eval<1>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work); break;
     default: hipLaunchKernelGGL(k_seq_eval<0>, g, dim3(256), 0, s, c, d, pods, podx, n_pods, rs, status, scores, work);
