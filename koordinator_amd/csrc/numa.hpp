@@ -64,6 +64,7 @@ struct DevNumaClass {
 };
 
 static_assert(sizeof(DevNumaClass) % 16 == 0, "classes are staged in LDS as 16-B words");
+static_assert(offsetof(DevNumaClass, pos_by_id) % 16 == 0, "pos_by_id is read 16 entries per load");
 
 struct NumaRow {
   int32_t cls;     // -1: no CPU topology
@@ -437,53 +438,49 @@ __device__ __forceinline__ void acc_excluded(const DevNumaClass &C, const Acc &a
   }
 }
 
+// One lane: T |= the n positions of S with the smallest CPU ids.  pos_by_id
+// is read 16 entries per load (the loads are independent of the takes).
+__device__ __forceinline__ void lane_first_by_id(const DevNumaClass &C, const uint64_t *S, int n, uint64_t *T) {
+  for (int i = 0; i < C.ncpu && n > 0; i += 16) {
+    const uint4 q = *reinterpret_cast<const uint4 *>(C.pos_by_id + i);
+    const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const int p = (int)((wd[j >> 2] >> ((j & 3) * 8)) & 255u);
+      if (i + j < C.ncpu && n > 0 && tbit(S, p)) {
+        sbit(T, p);
+        n--;
+      }
+    }
+  }
+}
+
 // spread order of the CPUs of m listed in ascending CPU id (freeCPUsInNode /
 // freeCPUsInSocket + spreadCPUs): round t takes each core's t-th CPU by id,
 // rounds in id order; lists of <= cpc CPUs are kept in id order.  Takes n.
 // WAVE: the order is (round, id) with round 1 = the second CPU of a core whose
 // first is in m too -- positions ascend by id inside a core (build_numa_class
 // checks it), so that is the odd position of a core with both bits in m.
+// The same (round, id) order serves lists of <= cpc CPUs, which the
+// reference keeps in id order: inside a core positions ascend by id.
 template <bool WAVE = false>
 __device__ __forceinline__ void acc_take_spread_by_id(const DevNumaClass &C, Acc &a, const uint64_t *m, int n) {
+  if (n <= 0) return;
+  uint64_t S0[NW], S1[NW], T[NW];
+  for (int w = 0; w < NW; w++) {
+    S1[w] = C.cpc == 2 ? (m[w] & (m[w] << 1) & 0xAAAAAAAAAAAAAAAAull) : 0ull;
+    S0[w] = m[w] & ~S1[w];
+    T[w] = 0ull;
+  }
+  const int n0 = popc4(S0);
   if constexpr (WAVE) {
-    if (n <= 0) return;
-    uint64_t S0[NW], S1[NW], T[NW];
-    for (int w = 0; w < NW; w++) {
-      S1[w] = C.cpc == 2 ? (m[w] & (m[w] << 1) & 0xAAAAAAAAAAAAAAAAull) : 0ull;
-      S0[w] = m[w] & ~S1[w];
-      T[w] = 0ull;
-    }
-    const int n0 = popc4(S0);
     acc_first_by_id(C, S0, min(n, n0), T);
     if (n > n0) acc_first_by_id(C, S1, n - n0, T);
-    acc_take_mask(C, a, T);
-    return;
+  } else {
+    lane_first_by_id(C, S0, min(n, n0), T);
+    if (n > n0) lane_first_by_id(C, S1, n - n0, T);
   }
-  int len = popc4(m);
-  if (len <= C.cpc) {
-    for (int i = 0; i < C.ncpu && n > 0; i++) {
-      const int p = C.pos_by_id[i];
-      if (tbit(m, p)) {
-        acc_take1(C, a, p);
-        n--;
-      }
-    }
-    return;
-  }
-  uint64_t used[NW] = {0, 0, 0, 0};
-  for (int round = 0; round < C.cpc && n > 0; round++) {
-    uint64_t seen[NW] = {0, 0, 0, 0};  // cores already visited this round
-    for (int i = 0; i < C.ncpu && n > 0; i++) {
-      const int p = C.pos_by_id[i];
-      if (!tbit(m, p) || tbit(used, p)) continue;
-      const int lead = p - (p % C.cpc);
-      if (tbit(seen, lead)) continue;
-      sbit(seen, lead);
-      sbit(used, p);
-      acc_take1(C, a, p);
-      n--;
-    }
-  }
+  acc_take_mask(C, a, T);
 }
 
 // freeCPUs(filterExclusive) + spreadCPUs + one-by-one take (:218-229).
