@@ -30,11 +30,12 @@ NXRES = 8
 DEV_TYPES, DEV_SLOTS, DEV_RES = 3, 8, 3
 DEV_GPU, DEV_RDMA, DEV_FPGA = 0, 1, 2
 PODX_DEVICE = 1
-# upstream NodeUnschedulable / NodeAffinity / TaintToleration all map to the
-# host-resolved static filter bit
+# upstream NodeUnschedulable / NodeName / NodeAffinity / TaintToleration all map
+# to the host-resolved static filter bit
 PLUGIN_BITS = {"NodeResourcesFit": PLUGIN_FIT, "LoadAwareScheduling": PLUGIN_LOADAWARE,
                "NodeNUMAResource": PLUGIN_NUMA, "Reservation": PLUGIN_RESERVATION,
                "NodeUnschedulable": PLUGIN_NODE_STATIC, "NodeAffinity": PLUGIN_NODE_STATIC,
+               "NodeName": PLUGIN_NODE_STATIC,
                "TaintToleration": PLUGIN_NODE_STATIC, "NodeResourcesBalancedAllocation": PLUGIN_BALANCED}
 # plugin_weight[p] / score plane p
 SCORE_PLUGIN_BITS = (PLUGIN_FIT, PLUGIN_LOADAWARE, PLUGIN_NUMA, PLUGIN_BALANCED)

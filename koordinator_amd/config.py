@@ -28,7 +28,8 @@ PLUGIN_NODE_UNSCHEDULABLE = "NodeUnschedulable"
 PLUGIN_NODE_AFFINITY = "NodeAffinity"
 PLUGIN_TAINT_TOLERATION = "TaintToleration"
 PLUGIN_BALANCED = "NodeResourcesBalancedAllocation"
-STATIC_FILTERS = (PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
+PLUGIN_NODE_NAME = "NodeName"
+STATIC_FILTERS = (PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_NODE_NAME, PLUGIN_NODE_AFFINITY, PLUGIN_TAINT_TOLERATION)
 PLUGIN_DEVICESHARE = "DeviceShare"
 PLUGIN_PTS = "PodTopologySpread"
 PLUGIN_IPA = "InterPodAffinity"

@@ -372,7 +372,7 @@ class Informer:
             self._reload = True
         if static_keyed(self.profile):
             for p in pods:
-                if self.static_classes.classify(pod_static(p)) >= self.static_classes.frozen:
+                if self.static_classes.classify(pod_static(p, self.profile)) >= self.static_classes.frozen:
                     self._reload = True
         if self._spread_on():
             for p in pods:

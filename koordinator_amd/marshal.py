@@ -175,11 +175,15 @@ def node_static(node: k8s.Node):
                       name=node.name)
 
 
-def pod_static(pod: k8s.Pod):
-    """The pod fields the upstream static filters read (its static class key)."""
+def pod_static(pod: k8s.Pod, profile: Optional[Profile] = None):
+    """The pod fields the upstream static filters read (its static class key);
+    spec.nodeName only when `profile` enables the NodeName filter."""
+    from .config import PLUGIN_NODE_NAME
     from .nodefilters import PodStatic
+    name = pod.node_name if profile is not None and PLUGIN_NODE_NAME in profile.resolved().filters else ""
     return PodStatic(node_selector=dict(pod.node_selector or {}), required_terms=pod.required_node_affinity,
-                     tolerations=list(pod.tolerations), preferred_terms=list(pod.preferred_node_affinity or []))
+                     tolerations=list(pod.tolerations), preferred_terms=list(pod.preferred_node_affinity or []),
+                     node_name=name)
 
 
 def static_filters_of(profile: Profile) -> List[str]:
@@ -219,7 +223,7 @@ def static_class_of(pod: k8s.Pod, profile: Profile, static_classes) -> int:
         return 0
     if static_classes is None:
         raise MarshalError("the profile enables static node filters / Scores: pass the snapshot's StaticClasses")
-    c = static_classes.classify(pod_static(pod))
+    c = static_classes.classify(pod_static(pod, profile))
     if c >= getattr(static_classes, "frozen", abi.MAX_STATIC_CLASSES):
         raise MarshalError("pod static class first seen after the snapshot was built: rebuild it "
                            "(static_allow / static_score)")
@@ -300,7 +304,7 @@ def static_classes_for(pods: Iterable[k8s.Pod], profile: Profile):
     sc = StaticClasses()
     if static_keyed(profile):
         for pod in pods:
-            sc.classify(pod_static(pod))
+            sc.classify(pod_static(pod, profile))
     return sc
 
 

@@ -5,10 +5,10 @@ column, and the raw Scores of NodeAffinity
 into `static_score` (normalized over the feasible nodes on the device, in the
 sequential cycle).
 
-NodeUnschedulable, NodeAffinity (required part) and TaintToleration (Filter)
-read only the node's labels, taints and spec.unschedulable and the pod's
-nodeSelector, required node affinity and tolerations -- nothing a Reserve
-changes.  Pods sharing those three fields form one static class; a node's
+NodeUnschedulable, NodeName, NodeAffinity (required part) and TaintToleration
+(Filter) read only the node's name, labels, taints and spec.unschedulable and
+the pod's spec.nodeName, nodeSelector, required node affinity and tolerations
+-- nothing a Reserve changes.  Pods sharing those fields form one static class; a node's
 `static_allow` bit c says whether class c passes all enabled filters there, so
 the device Filter is one bit test per (pod, node).
 
@@ -24,7 +24,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import abi
-from .config import PLUGIN_NODE_AFFINITY, PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_TAINT_TOLERATION
+from .config import PLUGIN_NODE_AFFINITY, PLUGIN_NODE_NAME, PLUGIN_NODE_UNSCHEDULABLE, PLUGIN_TAINT_TOLERATION
 from .reservation import NodeSelectorRequirement, NodeSelectorTerm, _req_matches
 
 NO_SCHEDULE, PREFER_NO_SCHEDULE, NO_EXECUTE = "NoSchedule", "PreferNoSchedule", "NoExecute"
@@ -73,13 +73,14 @@ class PodStatic:
     tolerations: List[Toleration] = field(default_factory=list)
     # preferredDuringSchedulingIgnoredDuringExecution: (weight, NodeSelectorTerm)
     preferred_terms: List[Tuple[int, NodeSelectorTerm]] = field(default_factory=list)
+    node_name: str = ""                                       # spec.nodeName
 
     def key(self) -> Tuple:
         tk = lambda t: (tuple((r.key, r.operator, tuple(r.values)) for r in t.match_expressions),
                         tuple((r.key, r.operator, tuple(r.values)) for r in t.match_fields))
         terms = None if self.required_terms is None else tuple(tk(t) for t in self.required_terms)
         pref = tuple((int(w), tk(t)) for w, t in self.preferred_terms)
-        return (tuple(sorted(self.node_selector.items())), terms, tuple(self.tolerations), pref)
+        return (tuple(sorted(self.node_selector.items())), terms, tuple(self.tolerations), pref, self.node_name)
 
 
 def tolerates_all(tolerations: Sequence[Toleration], taints: Iterable[Taint], effects) -> bool:
@@ -95,6 +96,11 @@ def node_unschedulable_ok(pod: PodStatic, node: NodeStatic) -> bool:
     if not node.unschedulable:
         return True
     return any(tol.tolerates(Taint(TAINT_NODE_UNSCHEDULABLE, "", NO_SCHEDULE)) for tol in pod.tolerations)
+
+
+def node_name_ok(pod: PodStatic, node: NodeStatic) -> bool:
+    """(upstream) nodename/node_name.go Fits: no spec.nodeName, or the node's name."""
+    return not pod.node_name or pod.node_name == node.name
 
 
 def _term_matches(t: NodeSelectorTerm, node: NodeStatic) -> bool:
@@ -144,8 +150,8 @@ def taint_toleration_score(pod: PodStatic, node: NodeStatic) -> int:
     return sum(1 for t in node.taints if t.effect == PREFER_NO_SCHEDULE and not any(x.tolerates(t) for x in tols))
 
 
-_CHECKS = {PLUGIN_NODE_UNSCHEDULABLE: node_unschedulable_ok, PLUGIN_NODE_AFFINITY: node_affinity_ok,
-           PLUGIN_TAINT_TOLERATION: taint_toleration_ok}
+_CHECKS = {PLUGIN_NODE_UNSCHEDULABLE: node_unschedulable_ok, PLUGIN_NODE_NAME: node_name_ok,
+           PLUGIN_NODE_AFFINITY: node_affinity_ok, PLUGIN_TAINT_TOLERATION: taint_toleration_ok}
 
 
 class StaticClasses:

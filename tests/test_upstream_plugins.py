@@ -242,3 +242,22 @@ def test_static_class_key_includes_preferred_terms():
     b = cls.classify(PodStatic(preferred_terms=[(2, T([R("a", "Exists")]))]))
     c = cls.classify(PodStatic(preferred_terms=[(1, T([R("a", "Exists")]))]))
     assert a != b and a == c
+
+
+def test_node_name_filter():
+    """(upstream) nodename/node_name.go Fits: a pod naming a node passes only
+    that node; the name is part of the static class key only when the profile
+    enables NodeName (with_upstream does)."""
+    from koordinator_amd import k8s
+    from koordinator_amd.marshal import pod_static
+    nodes = [NodeStatic(name=f"n{i}") for i in range(5)]
+    cls = StaticClasses()
+    a = cls.classify(PodStatic(node_name="n3"))
+    b = cls.classify(PodStatic())
+    m = static_allow(nodes, cls, ["NodeName"])
+    assert [(int(x) >> a) & 1 for x in m] == [0, 0, 0, 1, 0]
+    assert all((int(x) >> b) & 1 for x in m)
+    pod = k8s.Pod(name="p", node_name="n3")
+    assert pod_static(pod, with_upstream(shipped_profile())).node_name == "n3"
+    assert pod_static(pod, shipped_profile()).node_name == ""
+    assert "NodeName" in with_upstream(shipped_profile()).filters
