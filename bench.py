@@ -161,7 +161,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare", "spread", "affinity",
-                                                   "resvpolicy"], default="config4",
+                                                   "resvpolicy", "config4ds"], default="config4",
                     help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
                          "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods); "
                          "config5: 200k nodes, 10%% holding a Reservation matched by 20%% of the pods, "
@@ -174,7 +174,8 @@ def main():
                          "anti-affinity terms, + InterPodAffinity (filter, weight 1): the exact sequential cycle; "
                          "resvpolicy: config 5's profile and cluster with 30%% NUMA topology-policy nodes, up to 4 "
                          "reservations per node (70%% holding cpusets, on policy nodes too) and 30%% cpuset pods: "
-                         "the exact sequential cycle")
+                         "the exact sequential cycle; config4ds: config 4 under the shipped profile with DeviceShare "
+                         "(weight 1) on a cluster with devices, no pod requesting one: the pipelined greedy")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--be-frac", type=float, default=None)
@@ -224,13 +225,17 @@ def main():
 
     resv = args.workload == "config5"
     numa = args.workload == "config3" or resv
-    c = synth.CONFIGS[{"config3": 3, "config4": 4, "config5": 5}[args.workload]]
+    c = synth.CONFIGS[{"config3": 3, "config4": 4, "config5": 5, "config4ds": 4}[args.workload]]
     args.nodes = args.nodes or c["nodes"]
     args.pods = args.pods or c["pods"]
     args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
     prof = shipped_profile(numa=numa, reservation=resv)
+    if args.workload == "config4ds":
+        prof = with_deviceshare(prof)
     prof.batch_pods = args.batch
     table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
+    if args.workload == "config4ds":
+        synth.add_devices(table, synth.DevSpec())
     if numa:
         synth.add_numa(table, synth.NumaSpec(), prof)
     if resv:
@@ -353,7 +358,9 @@ def main():
                                 "LSR/LSE cpuset, NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource"
                                 if numa else
                                 f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
-                                "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile"),
+                                "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile"
+                                + (" + DeviceShare (weight 1; 30% of the nodes with GPUs, no pod requesting one: "
+                                   "the pipelined greedy)" if args.workload == "config4ds" else "")),
                    "nodes": args.nodes, "pods": args.pods, "batch_pods": batch, "pipeline_lag": lag,
                    "parallelism": f"node-shard x{world}" + (" (one-rank RCCL exchange path)" if args.one_rank_comm and world == 1 else "")},
         "unschedulable": int((placements < 0).sum()),

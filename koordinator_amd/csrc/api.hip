@@ -180,10 +180,17 @@ struct koordhip_ctx {
   bool seq = false;                // the sequential cycle runs the placements (seq_profile, or a Reservation
                                    // snapshot with NUMA topology-policy nodes)
   bool seq_profile = false;        // the profile enables DeviceShare or a normalized upstream Score
+  bool seq_dev_only = false;       // ... and its only such plugin is DeviceShare: a batch without device /
+                                   // extended-scalar requests (PreFilter skip: Filter passes, Score 0, no
+                                   // Reserve, deviceshare/plugin.go:162-182, scoring.go:33-40) runs pipelined
+  bool seq_snap = false;           // the snapshot needs the sequential cycle (Reservation + topology-policy
+                                   // nodes, or more than KOORDHIP_RESV_SLOTS reservations on a node)
+  bool last_seq = false;           // the last place call ran the sequential cycle
   kh::DevPodX *d_podx = nullptr;   // staged koordhip_pod_ext records (NULL: none staged)
   int32_t podx_cap = 0;
   bool podx_staged = false;
   bool staged_reserve = false;     // the staged batch holds a reserve pod (KOORDHIP_POD_RESERVE): the sequential cycle
+  bool staged_ext = false;         // the staged batch's koordhip_pod_ext records carry requests / constraints
   uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
   uint64_t *d_seqg = nullptr;
   void *d_seqdesc = nullptr;  // the sequential cycle's device copies of dc / d
@@ -983,6 +990,9 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
             (KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_PTS | KOORDHIP_PLUGIN_IPA)) ||
            (cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
   c->seq_profile = c->seq;
+  c->seq_dev_only = c->seq_profile &&
+                    !((cfg->filter_plugins | cfg->score_plugins) & (KOORDHIP_PLUGIN_PTS | KOORDHIP_PLUGIN_IPA)) &&
+                    !(cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
   c->side = c->numa || c->resv;
@@ -1223,7 +1233,8 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   // the sequential cycle (seq.hip: eval_total_resv<.., Z>)
   // (and more than KOORDHIP_RESV_SLOTS reservations per node: the pipelined
   // rows hold at most that many)
-  c->seq = c->seq_profile || (c->dc.resv && (c->dc.zones || c->dc.resv_slots > KOORDHIP_RESV_SLOTS));
+  c->seq_snap = c->dc.resv && (c->dc.zones || c->dc.resv_slots > KOORDHIP_RESV_SLOTS);
+  c->seq = c->seq_profile || c->seq_snap;
   if (e) {
     free_cols(c);
     return e;
@@ -1518,6 +1529,7 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   }
   c->dc.la_alias = alias ? 1 : 0;
   if (zpolicy) c->dc.zones = 1;
+  if (zpolicy && c->dc.resv) c->seq_snap = true;
   if (amp_any) c->dc.amp = 1;
   HIP_TRY(kh::launch_prep_flags(pi, d, d_idx, m, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));  // the host image may be reused by the next call
@@ -1753,6 +1765,7 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->n_staged = n_pods;
   c->podx_staged = false;
+  c->staged_ext = false;
   c->staged_reserve = reserve;
   return 0;
 }
@@ -1828,6 +1841,7 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
   }
   if (any && !c->seq_profile)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
+  c->staged_ext = any;
   if (!any && !rn) return 0;
   if (n_pods > c->podx_cap) {
     if (c->d_podx) HIP_TRY(hipFree(c->d_podx));
@@ -2161,8 +2175,11 @@ int place_staged_impl(koordhip_ctx *c) {
   c->pipe_err = false;
   c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
-  if (c->seq || c->staged_reserve) return seq_place(c);
-  if (c->podx_staged)
+  // the sequential cycle: a snapshot or profile that needs it, a reserve pod in
+  // the batch, or a DeviceShare-only profile whose batch requests devices
+  c->last_seq = c->staged_reserve || c->seq_snap || (c->seq_profile && (!c->seq_dev_only || c->staged_ext));
+  if (c->last_seq) return seq_place(c);
+  if (c->podx_staged && c->staged_ext)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises
   // dispatches): every launch on one stream in dependency order, one resolve
@@ -2417,7 +2434,7 @@ int place_staged_impl(koordhip_ctx *c) {
 int pipe_status(koordhip_ctx *c) {
   static const char *kStall = "round pipeline stalled (watchdog): placements are incomplete";
   if (c->pipe_err) return fail(KOORDHIP_EDEVICE, kStall);
-  if (c->seq && c->pipe_check && c->d_seqg) {  // the sequential cycle's spin timeout word
+  if (c->last_seq && c->pipe_check && c->d_seqg) {  // the sequential cycle's spin timeout word
     c->pipe_check = false;
     uint32_t tmo = 0;
     HIP_TRY(hipMemcpy(&tmo, reinterpret_cast<char *>(c->d_seqg) + kh::seq_tmo_offset(c->seq_grid), sizeof(tmo),

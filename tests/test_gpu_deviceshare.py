@@ -196,3 +196,35 @@ def test_stream_static_filters_and_scores(numa):
     ok = got >= 0
     cls = pods["static_class"][ok].astype(np.uint32)
     assert (((t["static_allow"][got[ok]] >> cls) & 1) == 1).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("numa_resv", [False, True])
+def test_deviceshare_profile_batch_without_devices_runs_pipelined(numa_resv):
+    """The shipped profile enables DeviceShare; a batch in which no pod
+    requests a device (PreFilter skip for every pod: Filter passes, Score 0 on
+    every node so its normalisation is 0, no Reserve; deviceshare/plugin.go:
+    162-182, scoring.go:33-40) runs on the pipelined greedy, bit-exact with the
+    oracle's sequential cycle; the next batch with device pods runs the
+    sequential cycle on the state the first left."""
+    prof = with_deviceshare(shipped_profile(numa=numa_resv, reservation=numa_resv))
+    t = _cluster(4000, prof, numa=numa_resv, resv=numa_resv, seed=31)
+    pods, _ = _pods(1500, prof, seed=32, resv_match=0.2 if numa_resv else 0.0)
+    none = abi.pod_ext_array(len(pods))
+    pods2, ext2 = _pods(600, prof, seed=33, dev_frac=0.3)
+    o = oracle.Oracle(to_c_config(prof), t)
+    ref1 = o.place_stream_ext(pods, none)
+    ref2 = o.place_stream_ext(pods2, ext2)
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        got1 = e.place_stream_ext(pods, none)
+        k1 = e.kernel_names()["resolve"]
+        got2 = e.place_stream_ext(pods2, ext2)
+        k2 = e.kernel_names()["resolve"]
+        gst = e.read_nodes()
+    assert "k_resolve" in k1 and "k_seq" in k2, (k1, k2)
+    assert np.array_equal(got1, ref1), np.flatnonzero(got1 != ref1)[:10]
+    assert np.array_equal(got2, ref2), np.flatnonzero(got2 != ref2)[:10]
+    ost = o.state()
+    for k in ("requested", "npods"):
+        assert np.array_equal(gst[k], ost[k]), k
