@@ -180,9 +180,10 @@ struct koordhip_ctx {
   bool seq = false;                // the sequential cycle runs the placements (seq_profile, or a Reservation
                                    // snapshot with NUMA topology-policy nodes)
   bool seq_profile = false;        // the profile enables DeviceShare or a normalized upstream Score
-  bool seq_dev_only = false;       // ... and its only such plugin is DeviceShare: a batch without device /
-                                   // extended-scalar requests (PreFilter skip: Filter passes, Score 0, no
-                                   // Reserve, deviceshare/plugin.go:162-182, scoring.go:33-40) runs pipelined
+  bool seq_ext_only = false;       // ... and its such plugins read only koordhip_pod_ext (DeviceShare,
+                                   // PodTopologySpread, InterPodAffinity): a batch whose records are all empty
+                                   // (no device / extended-scalar request, no spread constraint or counted
+                                   // match, no affinity term or count entry) couples no nodes and runs pipelined
   bool seq_snap = false;           // the snapshot needs the sequential cycle (Reservation + topology-policy
                                    // nodes, or more than KOORDHIP_RESV_SLOTS reservations on a node)
   bool last_seq = false;           // the last place call ran the sequential cycle
@@ -990,9 +991,7 @@ int koordhip_create(const koordhip_config *cfg, koordhip_ctx **out) {
             (KOORDHIP_PLUGIN_DEVICESHARE | KOORDHIP_PLUGIN_PTS | KOORDHIP_PLUGIN_IPA)) ||
            (cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
   c->seq_profile = c->seq;
-  c->seq_dev_only = c->seq_profile &&
-                    !((cfg->filter_plugins | cfg->score_plugins) & (KOORDHIP_PLUGIN_PTS | KOORDHIP_PLUGIN_IPA)) &&
-                    !(cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
+  c->seq_ext_only = c->seq_profile && !(cfg->score_plugins & (KOORDHIP_PLUGIN_AFFINITY_SCORE | KOORDHIP_PLUGIN_TAINT_SCORE));
   c->numa = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_NUMA) != 0;
   c->resv = ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_RESERVATION) != 0;
   c->side = c->numa || c->resv;
@@ -2176,8 +2175,15 @@ int place_staged_impl(koordhip_ctx *c) {
   c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
   // the sequential cycle: a snapshot or profile that needs it, a reserve pod in
-  // the batch, or a DeviceShare-only profile whose batch requests devices
-  c->last_seq = c->staged_reserve || c->seq_snap || (c->seq_profile && (!c->seq_dev_only || c->staged_ext));
+  // the batch, or an ext-record profile whose batch carries ext content.  An
+  // empty record: DeviceShare's PreFilter skips the pod (Filter passes, Score 0,
+  // no Reserve: deviceshare/plugin.go:162-182, scoring.go:33-40);
+  // PodTopologySpread has no constraint (Filter passes; every Score 0, which
+  // NormalizeScore turns into the same 100 on every node) and the pod counts
+  // for none; InterPodAffinity has no term, no existing pod's term matches it
+  // (Filter passes, Score 0 everywhere, normalised to 0) and it counts for no
+  // entry -- nothing couples its nodes or changes the cycle's state.
+  c->last_seq = c->staged_reserve || c->seq_snap || (c->seq_profile && (!c->seq_ext_only || c->staged_ext));
   if (c->last_seq) return seq_place(c);
   if (c->podx_staged && c->staged_ext)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");

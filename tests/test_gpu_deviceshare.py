@@ -228,3 +228,34 @@ def test_deviceshare_profile_batch_without_devices_runs_pipelined(numa_resv):
     ost = o.state()
     for k in ("requested", "npods"):
         assert np.array_equal(gst[k], ost[k]), k
+
+
+@pytest.mark.gpu
+def test_spread_affinity_profile_batch_without_ext_runs_pipelined():
+    """PodTopologySpread + InterPodAffinity + DeviceShare in the profile: a
+    batch whose koordhip_pod_ext records are empty (no constraint, no term,
+    counted by no entry) couples no nodes and runs on the pipelined greedy; a
+    batch with spread / affinity pods then runs the sequential cycle on the state
+    the first left, both bit-exact with the oracle."""
+    from koordinator_amd.config import with_interpod_affinity, with_topology_spread
+    prof = with_interpod_affinity(with_topology_spread(with_deviceshare(shipped_profile())))
+    t = _cluster(3000, prof, seed=41)
+    pods = synth.make_pods(synth.StreamSpec(1200, be_frac=0.3, seed=42), prof)
+    none = abi.pod_ext_array(len(pods))
+    pods2 = synth.make_pods(synth.StreamSpec(500, be_frac=0.3, seed=43), prof)
+    ext2 = synth.make_device_ext(len(pods2), synth.DevStreamSpec(frac=0.2, seed=43))
+    synth.add_spread(t, ext2, synth.SpreadSpec())
+    synth.add_ipa(t, ext2, synth.IpaSpec())
+    o = oracle.Oracle(to_c_config(prof), t)
+    ref1 = o.place_stream_ext(pods, none)
+    ref2 = o.place_stream_ext(pods2, ext2)
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        got1 = e.place_stream_ext(pods, none)
+        k1 = e.kernel_names()["resolve"]
+        got2 = e.place_stream_ext(pods2, ext2)
+        k2 = e.kernel_names()["resolve"]
+    assert "k_resolve" in k1 and "k_seq" in k2, (k1, k2)
+    assert np.array_equal(got1, ref1), np.flatnonzero(got1 != ref1)[:10]
+    assert np.array_equal(got2, ref2), np.flatnonzero(got2 != ref2)[:10]
+    assert ((ext2["pts_n"] > 0) & (got2 >= 0)).sum() > 100
