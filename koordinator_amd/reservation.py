@@ -307,7 +307,6 @@ class Reservation:
                        [k8s.Container(requests=dict(self.allocatable))])
 
 
-ANNOTATION_RESERVE_POD = "scheduling.koordinator.sh/reserve-pod"
 ANNOTATION_RESERVATION_NAME = "scheduling.koordinator.sh/reservation-name"
 ANNOTATION_RESERVATION_NODE = "scheduling.koordinator.sh/reservation-node"
 
@@ -416,7 +415,7 @@ class ReservationIndex:
     def pod_mask(self, pod: k8s.Pod) -> int:
         """koordhip_pod.resv_match: bit g set iff the pod matches group g."""
         if (pod.annotations or {}).get(ANNOTATION_RESERVE_POD) == "true":
-            raise ReservationError("reserve pods are not scheduled by this engine")
+            return 0                # a reserve pod matches no reservation (transformer.go:60,96)
         aff = parse_reservation_affinity(pod.annotations or {})
         ai = None
         if aff is not None:

@@ -517,3 +517,46 @@ def test_reservation_cpuset_events_rows_equal_rebuild():
     inf.flush(eng, NOW)
     assert int(eng.table["numa_alloc_cnt"][1]) == cnt0
     assert not any(int(eng.table[f"resv_cpus{w}"][1]) for w in range(4))
+
+
+def test_reserve_pod_through_the_informer():
+    """A pending Reservation is scheduled as its reserve pod (NewReservePod):
+    the informer's pod records mark it (KOORDHIP_POD_RESERVE, its allocate
+    policy, no reservation match) and its ext record pins its node; the oracle
+    places it only on that node and no later pod of the batch matches it (it is
+    not Available yet).  Once the Reservation is Available on that node, a
+    reload's owner groups let a matching pod nominate it."""
+    import oracle
+    from koordinator_amd import abi
+    from koordinator_amd import reservation as rv
+    from koordinator_amd.config import to_c_config
+    prof = shipped_profile(reservation=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110)})
+             for i in range(8)]
+    inf = Informer(prof, nodes, NOW)
+    owner = rv.ReservationOwner(label_selector=rv.LabelSelector(match_labels={"app": "web"}))
+    r = rv.Reservation("r-web", phase="Pending", owners=[owner], spec_node_name="n5",
+                       allocatable={k8s.CPU: k8s.Q(4), k8s.MEMORY: k8s.Q(8 * GI)},
+                       allocate_policy=rv.POLICY_ALIGNED)
+    inf.on_reservation(r)
+    t = inf.table(NOW)
+    rp = rv.new_reserve_pod(r)
+    web = k8s.Pod(name="web-0", labels={"app": "web"},
+                  containers=[k8s.Container(requests={k8s.CPU: k8s.Q(1), k8s.MEMORY: k8s.Q(GI)})])
+    recs = inf.pod_records([rp, web])
+    ext = inf.pod_ext_records([rp, web])
+    assert recs["flags"][0] & abi.POD_RESERVE and recs["resv_match"][0] == 0
+    assert ext["reserve_node"][0] == 6 and ext["reserve_node"][1] == 0
+    o = oracle.Oracle(to_c_config(prof), t)
+    got = o.place_stream_ext(recs, ext)
+    assert got[0] == 5
+    assert o.resv_state()["assigned"].sum() == 0          # nothing matched the pending reservation
+    # the reservation is Available on n5 now: after a reload the web pod matches it
+    r2 = copy.deepcopy(r)
+    r2.phase, r2.node_name = "Available", "n5"
+    inf.on_reservation(r2)
+    t2 = inf.table(NOW)
+    recs2 = inf.pod_records([web])
+    assert recs2["resv_match"][0] != 0
+    o2 = oracle.Oracle(to_c_config(prof), t2)
+    assert o2.place_stream(recs2)[0] == 5                 # the reservation's node wins (weight 5000)
