@@ -147,6 +147,11 @@ extern "C" {
                                          not Available yet (no slot, plugin.go:538-548).  A batch holding one runs in
                                          the sequential cycle (ABI 11) */
 #define KOORDHIP_POD_RESERVE_POLICY_SHIFT 12  /* bits 12-13: the reserve pod's AllocatePolicy (KOORDHIP_RESV_POLICY codes) */
+#define KOORDHIP_POD_RESV_OPERATING 16384u /* a pod in the reservation operating mode (IsReservationOperatingMode,
+                                              apis/extension/operating_pod.go:51-53): the Reservation Filter checks
+                                              AllocatePolicy Aligned (bits 12-13 = 1) against the node's Available
+                                              reservations (plugin.go:332-357), then filterWithReservations as for
+                                              any pod; a batch holding one runs in the sequential cycle (ABI 11) */
 #define KOORDHIP_POD_RESERVE_POLICY(f) (((f) >> KOORDHIP_POD_RESERVE_POLICY_SHIFT) & 3u)
 #define KOORDHIP_POD_RESV_AFFINITY 1024u /* a required reservation affinity (util/reservation/reservation.go:444-487): a node
                                             without a matched reservation fails the Reservation Filter (plugin.go:378-381) */

@@ -51,6 +51,7 @@ POD_KEY_CPU, POD_KEY_MEM = 256, 512
 POD_RESV_AFFINITY = 1024
 POD_RESERVE = 2048                  # a reserve pod (IsReservePod): its reservation's nodeName / AllocatePolicy checks
 POD_RESERVE_POLICY_SHIFT = 12       # bits 12-13: the reserve pod's AllocatePolicy (RESV_POLICY_* codes)
+POD_RESV_OPERATING = 16384          # a reservation-operating-mode pod (AllocatePolicy Aligned in bits 12-13)
 
 RESV_PRESENT, RESV_ALLOCATE_ONCE, RESV_UNSCHEDULABLE, RESV_ORDERED = 1, 2, 4, 8
 RESV_KEY_CPU, RESV_KEY_MEM = 16, 32

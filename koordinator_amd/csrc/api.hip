@@ -1728,10 +1728,15 @@ int koordhip_eval(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, uin
 static int check_reserve_pods(const koordhip_ctx *c, const koordhip_pod *pods, int32_t n, bool *any) {
   *any = false;
   for (int32_t j = 0; j < n; j++) {
-    if (!(pods[j].flags & KOORDHIP_POD_RESERVE)) continue;
-    if (pods[j].resv_match != 0 || (pods[j].flags & KOORDHIP_POD_RESV_AFFINITY))
+    const uint32_t f = pods[j].flags;
+    if (!(f & (KOORDHIP_POD_RESERVE | KOORDHIP_POD_RESV_OPERATING))) continue;
+    if ((f & KOORDHIP_POD_RESERVE) && (f & KOORDHIP_POD_RESV_OPERATING))
+      return fail(KOORDHIP_EINVAL, "a pod is either a reserve pod or in the reservation operating mode");
+    if ((f & KOORDHIP_POD_RESERVE) && (pods[j].resv_match != 0 || (f & KOORDHIP_POD_RESV_AFFINITY)))
       return fail(KOORDHIP_EINVAL, "a reserve pod matches no reservation (resv_match 0, no reservation affinity)");
-    if (KOORDHIP_POD_RESERVE_POLICY(pods[j].flags) > 2) return fail(KOORDHIP_EINVAL, "reserve pod: unknown allocate policy");
+    if ((f & KOORDHIP_POD_RESV_OPERATING) && KOORDHIP_POD_RESERVE_POLICY(f) != 1u)
+      return fail(KOORDHIP_EINVAL, "a reservation-operating-mode pod checks AllocatePolicy Aligned (bits 12-13 = 1)");
+    if (KOORDHIP_POD_RESERVE_POLICY(f) > 2) return fail(KOORDHIP_EINVAL, "reserve pod: unknown allocate policy");
     *any = *any || c->dc.resv;
   }
   return 0;

@@ -131,8 +131,8 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
     const bool nominated = rs && (x.flags & KOORDHIP_PODX_DEVICE) && resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
     df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
-    if ((p.flags & KOORDHIP_POD_RESERVE) && (c.filt & KOORDHIP_PLUGIN_RESERVATION) &&
-        !reserve_pod_ok(p, x.reserve_node, nr, i))
+    if ((p.flags & (KOORDHIP_POD_RESERVE | KOORDHIP_POD_RESV_OPERATING)) && (c.filt & KOORDHIP_PLUGIN_RESERVATION) &&
+        !reserve_pod_ok(p, (p.flags & KOORDHIP_POD_RESERVE) ? x.reserve_node : 0, nr, i))
       rfail = true;
   } else {
     df = dev_eval(c, d.dv, x, i, false, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,

@@ -281,6 +281,9 @@ def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None,
     rec["numa_policy"] = pol
     rec["resv_match"] = resv_index.pod_mask(pod) if resv_index is not None else 0
     rec["static_class"] = static_class_of(pod, profile, static_classes)
+    if rv.is_reservation_operating_pod(pod) and not rv.is_reserve_pod(pod) and _uses(p, PLUGIN_RESERVATION):
+        # the Reservation Filter's Aligned policy check (reservation/plugin.go:332-357)
+        rec["flags"] = int(rec["flags"]) | abi.POD_RESV_OPERATING | (abi.RESV_POLICY_ALIGNED << abi.POD_RESERVE_POLICY_SHIFT)
     if rv.is_reserve_pod(pod) and _uses(p, PLUGIN_RESERVATION):
         if reservations is None:
             raise MarshalError(f"reserve pod {pod.key}: pass the reservations (name -> Reservation)")

@@ -356,6 +356,14 @@ def reserve_pod_fields(rec, ext_rec, pod: k8s.Pod, reservations: Dict[str, Reser
         ext_rec["reserve_node"] = node_index[node] + 1
 
 
+LABEL_POD_OPERATING_MODE = "scheduling.koordinator.sh/operating-mode"
+
+
+def is_reservation_operating_pod(pod: k8s.Pod) -> bool:
+    """IsReservationOperatingMode, apis/extension/operating_pod.go:51-53."""
+    return (pod.labels or {}).get(LABEL_POD_OPERATING_MODE) == "Reservation"
+
+
 def parse_order(labels: Dict[str, str]) -> int:
     """findMostPreferredReservationByOrder's label parse (scoring.go:160-167): 0 = unordered."""
     s = labels.get(LABEL_RESERVATION_ORDER, "")

@@ -322,6 +322,8 @@ uint32_t orc_score_plugin_bit(int p) {
  * required reservation affinity). */
 static int resv_pass(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i) {
   if (pod->flags & KOORDHIP_POD_RESERVE) return orc_resv_reserve_pod_ok(st, pod, x, i);
+  /* a reservation-operating-mode pod: the Aligned policy check first (plugin.go:332-357) */
+  if ((pod->flags & KOORDHIP_POD_RESV_OPERATING) && !orc_resv_reserve_pod_ok(st, pod, NULL, i)) return 0;
   return st->soa->resv_flags ? orc_resv_filter(st, pod, i) : !(pod->flags & KOORDHIP_POD_RESV_AFFINITY);
 }
 

@@ -156,3 +156,60 @@ def test_gpu_reserve_pods_without_ext_place_stream(Engine):
         e.load_snapshot(t)
         got = e.place_stream(rp)
     assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
+
+
+def _with_operating_pods(pods, frac=0.25, seed=8):
+    """A `frac` share of the stream in the reservation operating mode (the
+    Aligned policy check before filterWithReservations); they keep their
+    reservation matches."""
+    rng = np.random.default_rng(seed)
+    pods = pods.copy()
+    for j in range(len(pods)):
+        if rng.random() < frac and not int(pods["flags"][j]) & abi.POD_RESERVE:
+            pods["flags"][j] = int(pods["flags"][j]) | abi.POD_RESV_OPERATING | \
+                (abi.RESV_POLICY_ALIGNED << abi.POD_RESERVE_POLICY_SHIFT)
+    return pods
+
+
+def test_oracle_operating_mode_pods():
+    """An operating-mode pod fails a node holding a Default-policy Available
+    reservation (Aligned vs Default, plugin.go:342-356) and otherwise filters as
+    any pod."""
+    prof, t = _cluster(numa=False)
+    pods = synth.make_pods(synth.StreamSpec(60, seed=4, resv_match_frac=0.5, resv_groups=2), prof)
+    op = _with_operating_pods(pods, frac=1.0)
+    st_op = oracle.Oracle(to_c_config(prof), t).eval_ext(op, abi.pod_ext_array(len(op)))["status"]
+    st = oracle.Oracle(to_c_config(prof), t).eval_ext(pods, abi.pod_ext_array(len(pods)))["status"]
+    flags = np.concatenate([t["resv_flags"]] + [t[f"resv_flags@{q}"] for q in range(1, t.resv_slots)]).reshape(
+        t.resv_slots, t.n)
+    default_here = (((flags & abi.RESV_PRESENT) != 0) & (((flags >> abi.RESV_POLICY_SHIFT) & 3) == 0)).any(axis=0)
+    want = ((st & abi.ST_RESV_FAIL) != 0) | default_here[None, :]
+    assert np.array_equal((st_op & abi.ST_RESV_FAIL) != 0, want)
+    assert default_here.any()
+
+
+def test_operating_mode_pod_record():
+    from koordinator_amd import k8s
+    prof = shipped_profile(reservation=True)
+    pod = k8s.Pod(name="op", labels={rv.LABEL_POD_OPERATING_MODE: "Reservation"},
+                  containers=[k8s.Container(requests=G.rlist({"cpu": "1"}))])
+    rec = pod_records([pod], prof)[0]
+    assert rec["flags"] & abi.POD_RESV_OPERATING
+    assert (int(rec["flags"]) >> abi.POD_RESERVE_POLICY_SHIFT) & 3 == abi.RESV_POLICY_ALIGNED
+
+
+@pytest.mark.gpu
+def test_gpu_operating_mode_pods_stream(Engine):
+    prof, t = _cluster(n=2500, seed=17, numa=False)
+    pods = synth.make_pods(synth.StreamSpec(1500, seed=18, be_frac=0.2, resv_match_frac=0.4, resv_groups=2), prof)
+    rp, ext = _with_reserve_pods(pods, t.n, frac=0.1)
+    rp = _with_operating_pods(rp, frac=0.3)
+    o = oracle.Oracle(to_c_config(prof), t)
+    ref = o.place_stream_ext(rp, ext)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        got = e.place_stream_ext(rp, ext)
+        gr, rr = e.read_reservations(), o.resv_state()
+    assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
+    for k in ("allocated", "assigned"):
+        assert np.array_equal(gr[k], rr[k]), k
