@@ -119,26 +119,39 @@ __device__ __forceinline__ bool dev_fits(const int64_t per[DR], const int64_t f[
   return per[0] <= f[0] && per[1] <= f[1] && per[2] <= f[2];
 }
 
+// floor(a / b) for 0 <= a <= 100 b, 0 < b < 2^45: the quotient is at most 100,
+// so the f64 reciprocal estimate is within one of it and one exact fix-up step
+// (the remainder by fma) settles it -- int64 division without the 64-bit
+// software divide (the same device as eval.hpp lrs / mrs)
+__device__ __forceinline__ int64_t dev_pct_div(int64_t a, int64_t b) {
+  const double fa = (double)a, fb = (double)b;
+  int64_t q = (int64_t)(fa * __builtin_amdgcn_rcp(fb));
+  const double r = __builtin_fma(-(double)q, fb, fa);
+  q -= (r < 0.0);
+  q += (r >= fb);
+  return q;
+}
+
 // leastResourceScorer / mostResourceScorer over (total, free, request) of
 // type t's weighted resources (scoring.go:152-274)
 __device__ __forceinline__ int64_t dev_scorer(const DevCfg &c, int t, const int64_t tot[DR], const int64_t fr[DR],
                                               const int64_t req[DR]) {
-  int64_t num = 0, ws = 0;
+  int32_t num = 0, ws = 0;
 #pragma unroll
   for (int k = 0; k < 5; k++) {
     const int kt = k < 3 ? KOORDHIP_DEV_GPU : (k == 3 ? KOORDHIP_DEV_RDMA : KOORDHIP_DEV_FPGA);
     const int r = k < 3 ? k : 0;
-    const int64_t w = c.dev_w[k];
+    const int32_t w = c.dev_w[k];
     if (w <= 0 || kt != t || tot[r] == 0) continue;
     int64_t rq = tot[r] >= fr[r] ? tot[r] - fr[r] + req[r] : tot[r];
     int64_t sc;
     if (c.dev_most) {
       if (rq > tot[r]) rq = tot[r];
-      sc = rq * 100 / tot[r];
+      sc = dev_pct_div(rq * 100, tot[r]);
     } else {
-      sc = rq > tot[r] ? 0 : (tot[r] - rq) * 100 / tot[r];
+      sc = rq > tot[r] ? 0 : dev_pct_div((tot[r] - rq) * 100, tot[r]);
     }
-    num += sc * w;
+    num += (int32_t)sc * w;
     ws += w;
   }
   return ws ? num / ws : 0;
