@@ -25,6 +25,9 @@
  *   koordhip_commit         <- Reserve  load_aware.go:260-263 (podAssignCache.assign, pod_assign_cache.go:53-68),
  *                              (upstream) cache.AssumePod -> NodeInfo.AddPod
  *   koordhip_uncommit       <- Unreserve load_aware.go:265-267 (pod_assign_cache.go:70-80)
+ *   koordhip_commit_ext / koordhip_uncommit_ext
+ *                           <- the same plus DeviceShare Reserve / Unreserve deviceshare/plugin.go:368-426 and the
+ *                              (upstream) PodTopologySpread / InterPodAffinity AddPod / RemovePod of the pod
  *   reservation columns     <- Reservation BeforePreFilter restore reservation/transformer.go:48-293,
  *                              filterWithReservations plugin.go:373-494, PreScore/Score scoring.go:42-200,
  *                              NominateReservation nominator.go:32-85, Reserve -> reservationCache.assumePod
@@ -49,7 +52,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 11
+#define KOORDHIP_ABI_VERSION 12
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -153,6 +156,13 @@ extern "C" {
                                               reservations (plugin.go:332-357), then filterWithReservations as for
                                               any pod; a batch holding one runs in the sequential cycle (ABI 11) */
 #define KOORDHIP_POD_RESERVE_POLICY(f) (((f) >> KOORDHIP_POD_RESERVE_POLICY_SHIFT) & 3u)
+#define KOORDHIP_POD_CPUSET_QOS 32768u /* ABI 12: AllowUseCPUSet (nodenumaresource/util.go:42-49: koord-prod and
+                                          QoS LSE / LSR) -- such a pod gets the nominated reservation's reserved
+                                          CPUs restored (reservation.go:68-74) even when it binds none; on
+                                          topology-policy or CPU-amplified nodes that changes its zone / amplified
+                                          Score and Reserve (plugin.go:465-479), which the engine does not model
+                                          for non-binding pods: such a batch is refused (KOORDHIP_EINVAL) on a
+                                          snapshot with reservations holding CPUs on such nodes */
 #define KOORDHIP_POD_RESV_AFFINITY 1024u /* a required reservation affinity (util/reservation/reservation.go:444-487): a node
                                             without a matched reservation fails the Reservation Filter (plugin.go:378-381) */
 
@@ -611,6 +621,27 @@ int koordhip_restore(koordhip_ctx *ctx);
  * Unreserve of a cpuset pod takes the CPUs it was given. */
 int koordhip_commit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out);
 int koordhip_uncommit(koordhip_ctx *ctx, const koordhip_pod *pod, int32_t node, const uint64_t *cpus);
+
+/* ABI 12: Reserve / Unreserve of one pod WITH its koordhip_pod_ext record on
+ * one node -- the same Reserve the sequential cycle runs on its winner:
+ *   DeviceShare Reserve   <- deviceshare/plugin.go:368-405 (allocator.go:91-122: the
+ *                            device choice; deviceUsed += the per-device request)
+ *   DeviceShare Unreserve <- deviceshare/plugin.go:407-426 (deviceUsed -= it)
+ *   NodeResourcesFit      <- the extended scalars' Requested (xrequested) +/- xreq
+ *   PodTopologySpread / InterPodAffinity <- upstream AddPod / RemovePod of the
+ *                            placed pod: pts_cnt / ipa_cnt of the constraints and
+ *                            entries it counts for (pts_match, ipa_inc) +/- 1
+ * plus everything koordhip_commit does (Fit / LoadAware, NodeNUMAResource,
+ * Reservation).  Reserve assumes the cycle ran PreScore (more than one
+ * feasible node: a matched reservation is nominated).  dev_slots_out /
+ * dev_slots ([KOORDHIP_DEV_TYPES], bit s = device slot s of the type, as
+ * koordhip_fetch_devices): what Reserve took, what Unreserve returns.
+ * KOORDHIP_ERESERVE: Reserve failed and nothing was applied.  Unreserve is
+ * refused (KOORDHIP_EINVAL) where koordhip_uncommit is. */
+int koordhip_commit_ext(koordhip_ctx *ctx, const koordhip_pod *pod, const koordhip_pod_ext *ext, int32_t node,
+                        uint64_t *cpus_out, uint32_t *dev_slots_out);
+int koordhip_uncommit_ext(koordhip_ctx *ctx, const koordhip_pod *pod, const koordhip_pod_ext *ext, int32_t node,
+                          const uint64_t *cpus, const uint32_t *dev_slots);
 
 /* CPUs allocated to each pod of the last place call ([n_pods][KOORDHIP_NUMA_WORDS],
  * zero for non-cpuset pods): what PreBind writes into the resource-status

@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 11
+KOORDHIP_ABI_VERSION = 12
 NRES = 5
 NPLUGINS = 4
 
@@ -52,6 +52,7 @@ POD_RESV_AFFINITY = 1024
 POD_RESERVE = 2048                  # a reserve pod (IsReservePod): its reservation's nodeName / AllocatePolicy checks
 POD_RESERVE_POLICY_SHIFT = 12       # bits 12-13: the reserve pod's AllocatePolicy (RESV_POLICY_* codes)
 POD_RESV_OPERATING = 16384          # a reservation-operating-mode pod (AllocatePolicy Aligned in bits 12-13)
+POD_CPUSET_QOS = 32768              # AllowUseCPUSet: koord-prod and QoS LSE / LSR (nodenumaresource/util.go:42-49)
 
 RESV_PRESENT, RESV_ALLOCATE_ONCE, RESV_UNSCHEDULABLE, RESV_ORDERED = 1, 2, 4, 8
 RESV_KEY_CPU, RESV_KEY_MEM = 16, 32
@@ -300,6 +301,8 @@ def load_library(path: str = LIB_PATH):
         "koordhip_restore": (C.c_int, [vp]),
         "koordhip_commit": (C.c_int, [vp, vp, C.c_int32, _u64p]),
         "koordhip_uncommit": (C.c_int, [vp, vp, C.c_int32, _u64p]),
+        "koordhip_commit_ext": (C.c_int, [vp, vp, vp, C.c_int32, _u64p, C.POINTER(C.c_uint32)]),
+        "koordhip_uncommit_ext": (C.c_int, [vp, vp, vp, C.c_int32, _u64p, C.POINTER(C.c_uint32)]),
         "koordhip_fetch_cpusets": (C.c_int, [vp, _u64p, C.c_int32]),
         "koordhip_read_numa": (C.c_int, [vp, _u64p, _u64p, _u64p, _i32p]),
         "koordhip_read_numa_zones": (C.c_int, [vp, _i64p]),
@@ -330,6 +333,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_place_stream", "koordhip_place_stream_ext", "koordhip_eval_ext", "koordhip_fetch_devices",
     "koordhip_read_devices", "koordhip_read_pts", "koordhip_read_ipa", "koordhip_stage_pods", "koordhip_stage_pods_ext", "koordhip_place_staged", "koordhip_fetch_placements",
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
+    "koordhip_commit_ext", "koordhip_uncommit_ext",
     "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
     "koordhip_read_resv_cpus", "koordhip_last_stats", "koordhip_last_kernel_stats",
     "koordhip_set_profile_kernels", "koordhip_last_kernel_names",

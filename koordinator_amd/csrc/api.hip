@@ -153,6 +153,7 @@ struct koordhip_ctx {
   bool pipe_check = false;       // a place call ran: check PipeSync.err when it completes
   bool pipe_err = false;         // ... and it had stalled (sticky until the next place call)
   kh::DevPod *d_tmp_pod = nullptr;
+  kh::DevPodX *d_tmp_podx = nullptr;  // koordhip_commit_ext's record
   void *d_upd = nullptr;           // koordhip_update_nodes staging (grown, kept)
   size_t upd_cap = 0;
   std::vector<uint8_t> upd_host;   // its host image
@@ -190,6 +191,7 @@ struct koordhip_ctx {
   kh::DevPodX *d_podx = nullptr;   // staged koordhip_pod_ext records (NULL: none staged)
   int32_t podx_cap = 0;
   bool podx_staged = false;
+  bool staged_qos_nonbind = false;  // a staged pod KOORDHIP_POD_CPUSET_QOS rejects on some snapshots
   bool staged_reserve = false;     // the staged batch holds a reserve pod (KOORDHIP_POD_RESERVE): the sequential cycle
   bool staged_ext = false;         // the staged batch's koordhip_pod_ext records carry requests / constraints
   uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
@@ -749,6 +751,12 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     if (s->dev_slots > KOORDHIP_DEV_SLOTS || !s->dev_present || !s->dev_minor || !s->dev_total)
       return fail(KOORDHIP_EINVAL, "dev_slots > KOORDHIP_DEV_SLOTS or a device column missing");
     const size_t ns = (size_t)n * KOORDHIP_DEV_TYPES * s->dev_slots;
+    // the scorer's percent quotients (dev.hpp dev_pct_div: an f64 reciprocal and
+    // one exact fix-up) equal Go's int64 division only for operands below 2^45
+    for (size_t a = 0; a < ns * KOORDHIP_DEV_RES; a++)
+      if (s->dev_total[a] < 0 || s->dev_total[a] >= (1ll << 45) ||
+          (s->dev_used && (s->dev_used[a] < 0 || s->dev_used[a] >= (1ll << 45))))
+        return fail(KOORDHIP_EINVAL, "dev_total / dev_used out of [0, 2^45)");
     // a node holds one GPU model: every GPU with resources has the same memory
     // (fillGPUTotalMem reads the first one, utils.go:211-233)
     for (int32_t i = 0; i < n; i++) {
@@ -1116,7 +1124,7 @@ int koordhip_destroy(koordhip_ctx *c) {
   free_cols(c);
   for (void *p : c->ckpt) (void)hipFree(p);
   for (void *p : {(void *)c->d_pods, (void *)c->d_out, (void *)c->d_partial[0], (void *)c->d_partial[1], (void *)c->d_lists,
-                  (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_dbg,
+                  (void *)c->d_gather, (void *)c->d_final, (void *)c->d_tmp_pod, (void *)c->d_tmp_podx, (void *)c->d_dbg,
                   (void *)c->d_cpus, (void *)c->d_classes, (void *)c->d_rc, (void *)c->d_mod, (void *)c->d_desc,
                   (void *)c->d_selpart[0], (void *)c->d_selcnt[0], (void *)c->d_selpart[1], (void *)c->d_selcnt[1],
                   (void *)c->d_etk_part[0], (void *)c->d_etk_part[1], (void *)c->d_etk_pcnt[0],
@@ -1408,6 +1416,10 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
       if (!dv.used || rows->dev_slots != dv.slots || !rows->dev_present || !rows->dev_minor || !rows->dev_total)
         return fail(KOORDHIP_EINVAL, "update rows: device columns must match the loaded snapshot's dev_slots");
       const int32_t S = dv.slots;
+      for (size_t a = 0; a < (size_t)m * KOORDHIP_DEV_TYPES * S * KOORDHIP_DEV_RES; a++)
+        if (rows->dev_total[a] < 0 || rows->dev_total[a] >= (1ll << 45) ||
+            (rows->dev_used && (rows->dev_used[a] < 0 || rows->dev_used[a] >= (1ll << 45))))
+          return fail(KOORDHIP_EINVAL, "update rows: dev_total / dev_used out of [0, 2^45)");
       for (int32_t j = 0; j < m; j++) {
         int64_t mem = -1;
         for (int32_t q = 0; q < S; q++) {
@@ -1771,6 +1783,12 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
   c->podx_staged = false;
   c->staged_ext = false;
   c->staged_reserve = reserve;
+  // prod LSE / LSR pods that bind no CPUs but some reservation may match (see
+  // KOORDHIP_POD_CPUSET_QOS): checked against the snapshot at place time
+  c->staged_qos_nonbind = false;
+  for (int32_t j = 0; j < n_pods && !c->staged_qos_nonbind; j++)
+    c->staged_qos_nonbind = (pods[j].flags & KOORDHIP_POD_CPUSET_QOS) && pods[j].resv_match != 0 &&
+                            !(pods[j].flags & (KOORDHIP_POD_CPUSET | KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
   return 0;
 }
 
@@ -1860,6 +1878,12 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
 }
 
 int koordhip_stage_pods_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_pod_ext *ext, int32_t n_pods) {
+  // the nodeName pin (reserve_node) belongs to reserve pods only: elsewhere it
+  // would be silently ignored
+  if (pods && ext)
+    for (int32_t j = 0; j < n_pods; j++)
+      if (ext[j].reserve_node != 0 && !(pods[j].flags & KOORDHIP_POD_RESERVE))
+        return fail(KOORDHIP_EINVAL, "koordhip_pod_ext.reserve_node set on a pod without KOORDHIP_POD_RESERVE");
   if (int e = koordhip_stage_pods(c, pods, n_pods)) return e;
   return stage_ext(c, ext, n_pods);
 }
@@ -2188,8 +2212,22 @@ int place_staged_impl(koordhip_ctx *c) {
   // for none; InterPodAffinity has no term, no existing pod's term matches it
   // (Filter passes, Score 0 everywhere, normalised to 0) and it counts for no
   // entry -- nothing couples its nodes or changes the cycle's state.
+  // Upstream restores the nominated reservation's reserved CPUs for every
+  // AllowUseCPUSet pod (nodenumaresource/reservation.go:68-74), and on a
+  // topology-policy or CPU-amplified node they enter the zone / amplified
+  // Score and Reserve of a pod that binds none (plugin.go:465-479,
+  // scoring.go:95-120): not modelled for such pods -- refused, not diverged
+  if (c->staged_qos_nonbind && c->dc.resv_cpus && (c->dc.zones || c->dc.amp) &&
+      (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION))
+    return fail(KOORDHIP_EINVAL, "a prod LSE/LSR pod binding no CPUs that a reservation may match, on a snapshot with "
+                                 "reservations holding CPUs and topology-policy or CPU-amplified nodes: the reserved "
+                                 "CPUs' restore for such pods is not modelled (KOORDHIP_POD_CPUSET_QOS)");
   c->last_seq = c->staged_reserve || c->seq_snap || (c->seq_profile && (!c->seq_ext_only || c->staged_ext));
   if (c->last_seq) return seq_place(c);
+  // the pipelined greedy allocates no device: clear the slots a previous
+  // sequential batch left (koordhip_fetch_devices reads this buffer)
+  if (c->d_devout && c->n_staged > 0)
+    HIP_TRY(hipMemsetAsync(c->d_devout, 0, (size_t)c->n_staged * KOORDHIP_DEV_TYPES * sizeof(uint32_t), c->stream));
   if (c->podx_staged && c->staged_ext)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises
@@ -2607,6 +2645,68 @@ static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, i
 
 int koordhip_commit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, uint64_t *cpus_out) {
   return commit_impl(c, pod, node, +1, cpus_out);
+}
+
+static int commit_ext_impl(koordhip_ctx *c, const koordhip_pod *pod, const koordhip_pod_ext *ext, int32_t node, int sign,
+                           uint64_t *cpus_io, uint32_t *dev_io) {
+  if (!c || !pod || !ext) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (node < 0 || node >= c->n) return fail(KOORDHIP_EINVAL, "node index out of range");
+  bool any = false;
+  if (int e = check_pod_ext(ext, 1, &any)) return e;
+  if (int e = check_pod_pts(c, ext, 1)) return e;
+  if (any && !c->seq_profile)
+    return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
+  if (ext->reserve_node != 0 || (pod->flags & KOORDHIP_POD_RESERVE))
+    return fail(KOORDHIP_EINVAL, "a reserve pod's Reserve assumes its reservation: not on this entry point");
+  const bool cpuset = c->numa && (pod->flags & KOORDHIP_POD_CPUSET) &&
+                      !(pod->flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
+  if (sign < 0 && cpuset && !cpus_io) return fail(KOORDHIP_EINVAL, "Unreserve of a cpuset pod needs its cpus");
+  const bool dev = (ext->flags & KOORDHIP_PODX_DEVICE) &&
+                   ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE);
+  if (sign < 0 && dev && !dev_io) return fail(KOORDHIP_EINVAL, "Unreserve of a device pod needs its device slots");
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->d_tmp_podx) HIP_TRY(hipMalloc(&c->d_tmp_podx, sizeof(kh::DevPodX)));
+  // d_rc: status (byte 0), cpus (bytes 8..39), device slots (bytes 40..51)
+  uint64_t *d_cpus = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(c->d_rc) + sizeof(uint64_t));
+  uint32_t *d_dev = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(c->d_rc) + 40);
+  std::vector<kh::DevPod> hp;
+  if (int e = to_dev_pods(pod, 1, hp)) return e;
+  HIP_TRY(hipMemcpyAsync(c->d_tmp_pod, hp.data(), sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_tmp_podx, ext, sizeof(kh::DevPodX), hipMemcpyHostToDevice, c->stream));
+  uint64_t cz[KOORDHIP_NUMA_WORDS] = {0, 0, 0, 0};
+  uint32_t dz[KOORDHIP_DEV_TYPES] = {0u, 0u, 0u};
+  HIP_TRY(hipMemcpyAsync(d_cpus, (sign < 0 && cpus_io) ? cpus_io : cz, sizeof(cz), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_dev, (sign < 0 && dev_io) ? dev_io : dz, sizeof(dz), hipMemcpyHostToDevice, c->stream));
+  const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
+  HIP_TRY(kh::launch_commit_ext(c->dc, c->d, c->d_tmp_pod, c->d_tmp_podx, node, sign, rs, d_cpus, d_dev, c->d_rc,
+                                c->pts, c->ipa, c->stream));
+  int32_t rc = 0;
+  uint64_t got[KOORDHIP_NUMA_WORDS];
+  uint32_t gdev[KOORDHIP_DEV_TYPES];
+  HIP_TRY(hipMemcpyAsync(&rc, c->d_rc, sizeof(rc), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(got, d_cpus, sizeof(got), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(gdev, d_dev, sizeof(gdev), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (rc == KOORDHIP_EINVAL)
+    return fail(rc, "Unreserve not supported here: a NodeNUMAResource pod on a NUMA topology-policy node (its zone amounts "
+                    "are not passed back) or a pod its node's reservation matches (whether the Reserve took the "
+                    "reservation is not passed back)");
+  if (rc) return fail(rc, "Reserve failed: DeviceShare or NodeNUMAResource could not allocate");
+  if (sign > 0) {
+    if (cpus_io) std::memcpy(cpus_io, got, sizeof(got));
+    if (dev_io) std::memcpy(dev_io, gdev, sizeof(gdev));
+  }
+  return 0;
+}
+
+int koordhip_commit_ext(koordhip_ctx *c, const koordhip_pod *pod, const koordhip_pod_ext *ext, int32_t node,
+                        uint64_t *cpus_out, uint32_t *dev_slots_out) {
+  return commit_ext_impl(c, pod, ext, node, +1, cpus_out, dev_slots_out);
+}
+int koordhip_uncommit_ext(koordhip_ctx *c, const koordhip_pod *pod, const koordhip_pod_ext *ext, int32_t node,
+                          const uint64_t *cpus, const uint32_t *dev_slots) {
+  return commit_ext_impl(c, pod, ext, node, -1, const_cast<uint64_t *>(cpus), const_cast<uint32_t *>(dev_slots));
 }
 int koordhip_uncommit(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, const uint64_t *cpus) {
   return commit_impl(c, pod, node, -1, const_cast<uint64_t *>(cpus));

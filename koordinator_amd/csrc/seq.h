@@ -43,6 +43,13 @@ constexpr size_t seq_desc_bytes() { return seq_desc_cfg_bytes() + sizeof(DevNode
 hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,
                            int32_t rs, uint8_t *status, uint8_t *ipa_status, int32_t *scores, int32_t *work, int32_t k,
                            uint64_t *topk, const PtsArgs &pts, const IpaArgs &ipa, hipStream_t s);
+// Reserve (sign > 0) / Unreserve (sign < 0) of one pod with its ext record on
+// `node` (koordhip_commit_ext / koordhip_uncommit_ext); one device thread.  cpus
+// [NW], dev [DT]: Reserve's outputs, Unreserve's inputs; rc: 0 / KOORDHIP_ERESERVE
+// / KOORDHIP_EINVAL.  rs: the Reservation plugin scores (PreScore nominated).
+hipError_t launch_commit_ext(const DevCfg &c, const DevNodes &d, const DevPod *pod, const DevPodX *px, int32_t node,
+                             int32_t sign, int32_t rs, uint64_t *cpus, uint32_t *dev, int32_t *rc, const PtsArgs &pts,
+                             const IpaArgs &ipa, hipStream_t s);
 // the k_seq instantiation launch_seq runs for this config, as rocprofv3 names it
 const char *seq_kernel_name(const DevCfg &c);
 

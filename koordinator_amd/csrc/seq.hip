@@ -289,6 +289,107 @@ __device__ __noinline__ void seq_commit(const DevCfg *cp, const DevNodes *dp, co
     for (int q = 0; q < DT; q++) out_dev[q] = dv[q];
 }
 
+// Reserve (sign > 0) / Unreserve (sign < 0) of ONE pod with its
+// koordhip_pod_ext record on node w, from the host (koordhip_commit_ext /
+// koordhip_uncommit_ext): what the Go shim calls after it chose a node itself,
+// or when Permit / PreBind fails after Reserve.  Reserve is the sequential
+// cycle's commit (seq_commit_body: DeviceShare's device choice and deviceUsed,
+// plugin.go:368-405; NodeNUMAResource's cpuset; Reservation's assume; the Fit /
+// LoadAware delta; the extended scalars), with PreScore assumed to have run
+// (nf > 1), plus the PodTopologySpread / InterPodAffinity counts the placed pod
+// adds (upstream AddPod).  Unreserve undoes each of them from what Reserve
+// returned: the device slots (deviceshare plugin.go:407-426 -> allocator
+// Unreserve: each slot's per-device request, recomputed from the node's GPU
+// memory as Reserve computed it), the cpuset, the counts (RemovePod).  rc: 0,
+// KOORDHIP_ERESERVE (Reserve failed, nothing applied) or KOORDHIP_EINVAL
+// (an Unreserve the returned values cannot undo: see k_commit).
+template <int SM>
+__global__ void k_commit_ext(DevCfg c, DevNodes d, const DevPod *__restrict__ pod, const DevPodX *__restrict__ px,
+                             int32_t w, int32_t sign, int32_t rs, uint64_t *__restrict__ cpus, uint32_t *__restrict__ dev,
+                             int32_t *__restrict__ rc, PtsArgs pa, IpaArgs ia) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const DevPod p = *pod;
+  const DevPodX &x = *px;
+  *rc = 0;
+  const uint32_t pm = pa.cnt ? (uint32_t)x.pts_match : 0u;
+  const uint32_t im = ia.cnt ? x.ipa_inc : 0u;
+  if (sign > 0) {
+    const int32_t r = seq_commit_body<SM>(c, d, p, x, w, 2, rs != 0, cpus, dev);
+    if (r) {
+      *rc = KOORDHIP_ERESERVE;
+      return;
+    }
+    for (int cc = 0; cc < pa.cons; cc++)
+      if ((pm >> cc) & 1u) pa.cnt[(size_t)cc * d.n + w] += 1;
+    ipa_commit_cols(ia, im, d.n, w);
+    return;
+  }
+  // ---- Unreserve: refuse what the returned values cannot undo (k_commit's rules)
+  if constexpr (SM >= 2) {
+    SeqResvRow<SM> rv;
+    load_resv(rv, d.rv, w);
+    if (c.resv && resv_matchable(rv, p)) {
+      *rc = KOORDHIP_EINVAL;
+      return;
+    }
+  }
+  if constexpr (SM >= 1) {
+    if (numa_on(c) && numa_active(p, c)) {
+      NumaRow r;
+      load_numa_row(r, d, w);
+      if (topo_policy(r.nflags) != 0) {
+        *rc = KOORDHIP_EINVAL;
+        return;
+      }
+      if (is_cpuset(p)) {
+        uint64_t m[NW];
+        for (int q = 0; q < NW; q++) m[q] = cpus[q];
+        numa_apply(r, p, m, -1);
+        store_numa_row(r, d, w);
+      }
+    }
+  }
+  if (((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) && (x.flags & KOORDHIP_PODX_DEVICE) && d.dv.slots > 0) {
+    for (int t = 0; t < DT; t++) {
+      int64_t q[DR], per[DR];
+      if (!dev[t] || !dev_requests(x, t, q)) continue;
+      DevRow dr;
+      dev_load(d.dv, w, t, dr);
+      if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(dr, q)) continue;
+      (void)dev_wanted(t, q, per);
+      const size_t a0 = dev_at(d.dv, w, t, 0) * DR;
+      for (int s = 0; s < d.dv.slots; s++)
+        if ((dev[t] >> s) & 1u)
+          for (int r = 0; r < DR; r++) d.dv.used[a0 + (size_t)s * DR + r] -= per[r];
+    }
+  }
+  if (x.xmask)
+    for (int j = 0; j < KOORDHIP_NXRES; j++)
+      if ((x.xmask >> j) & 1u) d.dv.xreq[(size_t)j * d.n + w] -= x.xreq[j];
+  NV v;
+  load_row(v, d, w);
+  apply_delta(v, p, -1);
+  store_row(v, d, w);
+  for (int cc = 0; cc < pa.cons; cc++)
+    if ((pm >> cc) & 1u) pa.cnt[(size_t)cc * d.n + w] -= 1;
+  for (uint32_t inc = im; inc;) {
+    const int e = ipa_next(inc);
+    ia.cnt[(size_t)e * d.n + w] -= 1;
+  }
+}
+
+hipError_t launch_commit_ext(const DevCfg &c, const DevNodes &d, const DevPod *pod, const DevPodX *px, int32_t node,
+                             int32_t sign, int32_t rs, uint64_t *cpus, uint32_t *dev, int32_t *rc, const PtsArgs &pts,
+                             const IpaArgs &ipa, hipStream_t s) {
+  switch (seq_mode(c)) {
+    case 3: hipLaunchKernelGGL(k_commit_ext<3>, dim3(1), dim3(64), 0, s, c, d, pod, px, node, sign, rs, cpus, dev, rc, pts, ipa); break;
+    case 2: hipLaunchKernelGGL(k_commit_ext<2>, dim3(1), dim3(64), 0, s, c, d, pod, px, node, sign, rs, cpus, dev, rc, pts, ipa); break;
+    case 1: hipLaunchKernelGGL(k_commit_ext<1>, dim3(1), dim3(64), 0, s, c, d, pod, px, node, sign, rs, cpus, dev, rc, pts, ipa); break;
+    default: hipLaunchKernelGGL(k_commit_ext<0>, dim3(1), dim3(64), 0, s, c, d, pod, px, node, sign, rs, cpus, dev, rc, pts, ipa);
+  }
+  return hipGetLastError();
+}
+
 // Block-wide reduction of (sum, max, max, max) and a u64 max over the block's
 // threads; every thread gets the result.
 __device__ __forceinline__ void seq_block_reduce(int32_t v4[4], uint64_t &key, int32_t (*s_red)[8], uint64_t *s_key,
@@ -960,17 +1061,31 @@ hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, co
   if (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) a.ext |= 2u;
   if (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) a.ext |= 4u;
   a.rs = rs;
-  DevCfg cc = c;
-  DevNodes dd = d;
-  void *args[] = {&cc, &dd, &a};
-  // every block must be resident (blocks read each other's granules): the
-  // cooperative launch checks the grid against the occupancy
+  // Every block must be resident (blocks read each other's granules).  The
+  // occupancy is checked here and the kernel launched as an ordinary
+  // dispatch: nothing else runs on the device meanwhile (the pipelined
+  // path's persistent resolve is joined before any sequential batch), so the
+  // grid of one block per CU is resident.  (hipLaunchCooperativeKernel gave
+  // the same residency, but its cooperative queue is torn down by the HIP
+  // runtime at process exit, after a profiler's finalisation: every
+  // rocprofv3 trace of a k_seq workload died with SIGSEGV in exit().)
   const int sm = seq_mode(c);
   const void *f = sm == 3   ? (const void *)k_seq<3>
                   : sm == 2 ? (const void *)k_seq<2>
                   : sm == 1 ? (const void *)k_seq<1>
                             : (const void *)k_seq<0>;
-  return hipLaunchCooperativeKernel(f, dim3(grid), dim3(SEQ_THREADS), args, 0, s);
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  if (hipError_t e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) return e;
+  if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, SEQ_THREADS, 0)) return e;
+  if ((int64_t)per_cu * ncu < grid) return hipErrorCooperativeLaunchTooLarge;
+  switch (sm) {
+    case 3: hipLaunchKernelGGL(k_seq<3>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
+    case 2: hipLaunchKernelGGL(k_seq<2>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
+    case 1: hipLaunchKernelGGL(k_seq<1>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
+    default: hipLaunchKernelGGL(k_seq<0>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a);
+  }
+  return hipGetLastError();
 }
 
 const char *seq_kernel_name(const DevCfg &c) {

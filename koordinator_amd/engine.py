@@ -185,6 +185,26 @@ class PlacementEngine:
         abi.check(self.lib, self.lib.koordhip_uncommit(self._ctx, pod.ctypes.data, int(node),
                                                        abi.ptr(c, C.c_uint64)))
 
+    def commit_ext(self, pod, ext, node: int):
+        """Reserve of one pod with its koordhip_pod_ext record (DeviceShare, the
+        extended scalars, PodTopologySpread / InterPodAffinity counts besides
+        koordhip_commit's plugins): returns (cpus [NUMA_WORDS], device slots [DEV_TYPES])."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod), dtype=abi.POD_DTYPE)
+        x = np.ascontiguousarray(np.atleast_1d(ext), dtype=abi.POD_EXT_DTYPE)
+        cpus = np.zeros(abi.NUMA_WORDS, np.uint64)
+        dev = np.zeros(abi.DEV_TYPES, np.uint32)
+        abi.check(self.lib, self.lib.koordhip_commit_ext(self._ctx, pod.ctypes.data, x.ctypes.data, int(node),
+                                                         abi.ptr(cpus, C.c_uint64), abi.ptr(dev, C.c_uint32)))
+        return cpus, dev
+
+    def uncommit_ext(self, pod, ext, node: int, cpus=None, dev=None):
+        pod = np.ascontiguousarray(np.atleast_1d(pod), dtype=abi.POD_DTYPE)
+        x = np.ascontiguousarray(np.atleast_1d(ext), dtype=abi.POD_EXT_DTYPE)
+        c = None if cpus is None else np.ascontiguousarray(cpus, dtype=np.uint64)
+        d = None if dev is None else np.ascontiguousarray(dev, dtype=np.uint32)
+        abi.check(self.lib, self.lib.koordhip_uncommit_ext(self._ctx, pod.ctypes.data, x.ctypes.data, int(node),
+                                                           abi.ptr(c, C.c_uint64), abi.ptr(d, C.c_uint32)))
+
     def read_numa(self) -> dict:
         n = self.n
         fr = np.zeros((abi.NUMA_WORDS, n), np.uint64)

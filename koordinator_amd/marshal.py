@@ -276,7 +276,7 @@ def pod_record(pod: k8s.Pod, profile: Profile, out: Optional[np.ndarray] = None,
         nf, ncpus, pol = abi.POD_NUMA_ERROR, 0, 0
     from . import reservation as rv
     flags |= rv.pod_keys(pod)
-    rec["flags"] = flags | nf
+    rec["flags"] = flags | nf | (abi.POD_CPUSET_QOS if allow else 0)
     rec["numa_cpus"] = ncpus
     rec["numa_policy"] = pol
     rec["resv_match"] = resv_index.pod_mask(pod) if resv_index is not None else 0

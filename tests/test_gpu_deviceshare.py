@@ -231,6 +231,46 @@ def test_deviceshare_profile_batch_without_devices_runs_pipelined(numa_resv):
 
 
 @pytest.mark.gpu
+def test_fetch_devices_after_pipelined_batch_is_zero():
+    """A device batch runs the sequential cycle and fills the device slots;
+    the next batch, without device requests, runs pipelined and allocates no
+    device: koordhip_fetch_devices must then return zeros, not the previous
+    batch's slots (the bind loop would annotate phantom GPU minors)."""
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(2000, prof, seed=51)
+    pods1, ext1 = _pods(400, prof, seed=52, dev_frac=0.5)
+    pods2, _ = _pods(400, prof, seed=53)
+    none = abi.pod_ext_array(len(pods2))
+    o = oracle.Oracle(to_c_config(prof), t)
+    ref1, dref1 = o.place_stream_ext(pods1, ext1, devices=True)
+    ref2 = o.place_stream_ext(pods2, none)
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        got1 = e.place_stream_ext(pods1, ext1)
+        d1 = e.fetch_devices(len(pods1))
+        got2 = e.place_stream_ext(pods2, none)
+        assert "k_resolve" in e.kernel_names()["resolve"]
+        d2 = e.fetch_devices(len(pods2))
+    assert np.array_equal(got1, ref1) and np.array_equal(d1, dref1)
+    assert (d1 != 0).any()
+    assert np.array_equal(got2, ref2)
+    assert not d2.any(), np.flatnonzero(d2.any(axis=1))[:10]
+
+
+@pytest.mark.gpu
+def test_device_totals_beyond_exact_range_rejected():
+    """The device scorer divides by f64 reciprocal with one exact fix-up
+    (dev.hpp dev_pct_div), exact for operands below 2^45: larger dev_total /
+    dev_used are refused at load_snapshot, not silently mis-scored."""
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(200, prof, seed=61)
+    t["dev_total"][0, abi.DEV_GPU, 0, 2] = 1 << 46
+    with _engine(prof) as e:
+        with pytest.raises(abi.KoordhipError, match="2\\^45"):
+            e.load_snapshot(t)
+
+
+@pytest.mark.gpu
 def test_spread_affinity_profile_batch_without_ext_runs_pipelined():
     """PodTopologySpread + InterPodAffinity + DeviceShare in the profile: a
     batch whose koordhip_pod_ext records are empty (no constraint, no term,
@@ -259,3 +299,62 @@ def test_spread_affinity_profile_batch_without_ext_runs_pipelined():
     assert np.array_equal(got1, ref1), np.flatnonzero(got1 != ref1)[:10]
     assert np.array_equal(got2, ref2), np.flatnonzero(got2 != ref2)[:10]
     assert ((ext2["pts_n"] > 0) & (got2 >= 0)).sum() > 100
+
+
+def _state(e):
+    s = e.read_nodes()
+    d = e.read_devices()
+    return {"requested": s["requested"], "nz": s["nz"], "npods": s["npods"], "la_used": s["la_used"],
+            "dev_used": d["dev_used"], "xrequested": d["xrequested"], "pts": e.read_pts(), "ipa": e.read_ipa()}
+
+
+def _ostate(o):
+    s, d = o.state(), o.dev_state()
+    return {"requested": s["requested"], "nz": s["nz"], "npods": s["npods"], "la_used": s["la_used"],
+            "dev_used": d["dev_used"], "xrequested": d["xrequested"], "pts": o.pts_counts(), "ipa": o.ipa_counts()}
+
+
+@pytest.mark.gpu
+def test_commit_ext_uncommit_ext_then_stream():
+    """koordhip_commit_ext / koordhip_uncommit_ext (the Go shim's Reserve of a
+    node it chose, and the Unreserve after a failed Permit / PreBind) for
+    device pods with PodTopologySpread / InterPodAffinity records: each Reserve
+    equals the oracle cycle's Reserve of that pod on that node (node state,
+    deviceUsed, the extended scalars, the spread / affinity counts, the device
+    slots); Unreserve restores the state exactly, and a stream placed afterwards
+    equals the oracle's from the untouched snapshot."""
+    from koordinator_amd.config import with_interpod_affinity, with_topology_spread
+    prof = with_interpod_affinity(with_topology_spread(with_deviceshare(shipped_profile())))
+    t = _cluster(1500, prof, seed=71)
+    pods = synth.make_pods(synth.StreamSpec(300, be_frac=0.3, seed=72), prof)
+    ext = synth.make_device_ext(len(pods), synth.DevStreamSpec(frac=0.5, seed=72))
+    synth.add_spread(t, ext, synth.SpreadSpec())
+    synth.add_ipa(t, ext, synth.IpaSpec())
+    cfg = to_c_config(prof)
+    # pods with device requests and spread / affinity content
+    pick = [j for j in range(len(pods)) if ext["flags"][j] & abi.PODX_DEVICE and
+            (ext["pts_match"][j] or ext["ipa_inc"][j])][:6]
+    assert len(pick) >= 3
+    with _engine(prof) as e:
+        e.load_snapshot(t)
+        base = _state(e)
+        o0 = oracle.Oracle(cfg, t)
+        assert all(np.array_equal(base[k], v) for k, v in _ostate(o0).items())
+        for j in pick:
+            o = oracle.Oracle(cfg, t)   # the cycle's choice of node for this pod alone, and its Reserve
+            w, rdev = o.place_stream_ext(pods[j:j + 1], ext[j:j + 1], devices=True)
+            if w[0] < 0:
+                continue
+            cpus, dev = e.commit_ext(pods[j], ext[j], int(w[0]))
+            assert np.array_equal(dev, rdev[0]), (j, dev, rdev[0])
+            got, want = _state(e), _ostate(o)
+            for k in want:
+                assert np.array_equal(got[k], want[k]), (j, k)
+            e.uncommit_ext(pods[j], ext[j], int(w[0]), cpus, dev)
+            got = _state(e)
+            for k in base:
+                assert np.array_equal(got[k], base[k]), ("after uncommit", j, k)
+        rest = slice(100, 300)
+        ref = oracle.Oracle(cfg, t).place_stream_ext(pods[rest], ext[rest])
+        gotp = e.place_stream_ext(pods[rest], ext[rest])
+    assert np.array_equal(gotp, ref), np.flatnonzero(gotp != ref)[:10]

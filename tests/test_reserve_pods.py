@@ -213,3 +213,17 @@ def test_gpu_operating_mode_pods_stream(Engine):
     assert np.array_equal(ref, got), np.flatnonzero(ref != got)[:10]
     for k in ("allocated", "assigned"):
         assert np.array_equal(gr[k], rr[k]), k
+
+
+@pytest.mark.gpu
+def test_gpu_reserve_node_needs_reserve_pod(Engine):
+    """koordhip_pod_ext.reserve_node (the reservation's nodeName pin) on a pod
+    that is not a reserve pod is rejected loudly instead of being ignored."""
+    prof, t = _cluster(n=300, seed=21, numa=False)
+    pods = synth.make_pods(synth.StreamSpec(8, seed=22, be_frac=0.2), prof)
+    ext = abi.pod_ext_array(len(pods))
+    ext["reserve_node"][3] = 5
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(t)
+        with pytest.raises(abi.KoordhipError, match="reserve_node"):
+            e.stage_pods_ext(pods, ext)
