@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <condition_variable>
 #include <memory>
@@ -13,9 +14,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/koordhip.h"
+#include "cls.h"
 #include "kernels.h"
 #include "seq.h"
 
@@ -194,6 +197,32 @@ struct koordhip_ctx {
   bool staged_qos_nonbind = false;  // a staged pod KOORDHIP_POD_CPUSET_QOS rejects on some snapshots
   bool staged_reserve = false;     // the staged batch holds a reserve pod (KOORDHIP_POD_RESERVE): the sequential cycle
   bool staged_ext = false;         // the staged batch's koordhip_pod_ext records carry requests / constraints
+  // class-incremental lists (cls.hip): the staged pods' classes (byte-identical
+  // device records), the class buffers and the plan of the staged batch
+  std::vector<int32_t> pod_cls;    // class of each staged pod
+  std::vector<kh::DevPod> cls_rep; // each class's record
+  int32_t *d_pod_cls = nullptr;    // [pods_cap]
+  kh::DevPod *d_cls_pod = nullptr; // [cls_cap]
+  uint64_t *d_cls_buf = nullptr;   // [cls_cap][2][kClsCap]
+  kh::ClsMeta *d_cls_meta = nullptr;  // [cls_cap][2]
+  int32_t cls_cap = 0, cls_pod_cap = 0, pod_cls_cap = 0;
+  void *d_cls_S = nullptr;         // a build's score rows [kClsBuildRows][stride] and chunk maxima
+  size_t cls_S_cap = 0;
+  bool plan_ok = false;            // the plan below is the staged batch's for (plan_P, plan_lag)
+  int32_t plan_P = 0, plan_lag = 0;
+  struct ClsBuild {
+    int32_t u, er, tb, e0, ne;  // first use round, enqueue round, base round, entries [e0, e0 + ne)
+  };
+  std::vector<ClsBuild> plan_builds;
+  // per class its schedule (the rounds it appears in, bit 31: switch first to
+  // build plan_csm[] of the class), concatenated; per build entry the class /
+  // slot, the build number and the workgroup switches to wait for
+  std::vector<int32_t> plan_coff, plan_csched, plan_csm, plan_ent, plan_bm, plan_bw;
+  std::vector<kh::DevPod> plan_bpods;
+  int32_t *d_plan = nullptr;        // coff | csched | csm | ent | bm | bw | done[cls] | sw[cls]
+  kh::DevPod *d_plan_pods = nullptr;
+  size_t plan_cap = 0, plan_pods_cap = 0;
+  size_t plan_off[8] = {};          // element offsets of the arrays in d_plan
   uint32_t *d_devout = nullptr;    // [pods][DEV_TYPES] device slots of the last place call
   uint64_t *d_seqg = nullptr;
   void *d_seqdesc = nullptr;  // the sequential cycle's device copies of dc / d
@@ -1129,7 +1158,9 @@ int koordhip_destroy(koordhip_ctx *c) {
                   (void *)c->d_selpart[0], (void *)c->d_selcnt[0], (void *)c->d_selpart[1], (void *)c->d_selcnt[1],
                   (void *)c->d_etk_part[0], (void *)c->d_etk_part[1], (void *)c->d_etk_pcnt[0],
                   (void *)c->d_etk_pcnt[1], (void *)c->d_etk_sync[0], (void *)c->d_etk_sync[1], c->d_upd,
-                  (void *)c->d_podx, (void *)c->d_devout, (void *)c->d_seqg, c->d_seqdesc})
+                  (void *)c->d_podx, (void *)c->d_devout, (void *)c->d_seqg, c->d_seqdesc, (void *)c->d_pod_cls,
+                  (void *)c->d_cls_pod, (void *)c->d_cls_buf, (void *)c->d_cls_meta, c->d_cls_S,
+                  (void *)c->d_plan, (void *)c->d_plan_pods})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -1754,6 +1785,58 @@ static int check_reserve_pods(const koordhip_ctx *c, const koordhip_pod *pods, i
   return 0;
 }
 
+// The staged pods' classes for the class-incremental lists (cls.hip): pods
+// whose device records are byte-identical share a class.  More than
+// kClsMaxClasses classes: none (the pipelined greedy evaluates every pod).
+constexpr int32_t kClsMaxClasses = 1024;
+struct PodBytesHash {
+  size_t operator()(const std::array<uint64_t, 12> &a) const {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (uint64_t x : a) h = (h ^ x) * 0x100000001b3ull + (h >> 29);
+    return (size_t)h;
+  }
+};
+
+static int stage_classes(koordhip_ctx *c, const std::vector<kh::DevPod> &hp) {
+  static_assert(sizeof(kh::DevPod) == 12 * sizeof(uint64_t), "DevPod as 12 words");
+  const int32_t n = (int32_t)hp.size();
+  c->pod_cls.assign(n, 0);
+  c->cls_rep.clear();
+  c->plan_ok = false;
+  std::unordered_map<std::array<uint64_t, 12>, int32_t, PodBytesHash> m;
+  for (int32_t j = 0; j < n; j++) {
+    std::array<uint64_t, 12> k;
+    std::memcpy(k.data(), &hp[j], sizeof(kh::DevPod));
+    auto it = m.find(k);
+    if (it == m.end()) {
+      if ((int32_t)c->cls_rep.size() >= kClsMaxClasses) {
+        c->cls_rep.clear();  // too many classes for the class lists
+        return 0;
+      }
+      it = m.emplace(k, (int32_t)c->cls_rep.size()).first;
+      c->cls_rep.push_back(hp[j]);
+    }
+    c->pod_cls[j] = it->second;
+  }
+  if (n == 0) return 0;
+  const int32_t nc = (int32_t)c->cls_rep.size();
+  if (nc > c->cls_pod_cap) {
+    if (c->d_cls_pod) HIP_TRY(hipFree(c->d_cls_pod));
+    c->d_cls_pod = nullptr;
+    HIP_TRY(hipMalloc(&c->d_cls_pod, (size_t)nc * sizeof(kh::DevPod)));
+    c->cls_pod_cap = nc;
+  }
+  if (n > c->pod_cls_cap) {
+    if (c->d_pod_cls) HIP_TRY(hipFree(c->d_pod_cls));
+    c->d_pod_cls = nullptr;
+    HIP_TRY(hipMalloc(&c->d_pod_cls, (size_t)n * sizeof(int32_t)));
+    c->pod_cls_cap = n;
+  }
+  HIP_TRY(hipMemcpyAsync(c->d_cls_pod, c->cls_rep.data(), (size_t)nc * sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_pod_cls, c->pod_cls.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
 int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
@@ -1778,6 +1861,7 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
     c->pods_cap = n_pods;
   }
   if (n_pods) HIP_TRY(hipMemcpyAsync(c->d_pods, hp.data(), (size_t)n_pods * sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
+  if (int e = stage_classes(c, hp)) return e;
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->n_staged = n_pods;
   c->podx_staged = false;
@@ -2168,7 +2252,7 @@ int seq_place(koordhip_ctx *c) {
   const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
   const bool stamps = std::getenv("KOORDHIP_STAMPS") != nullptr;
   if (stamps) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 64 * sizeof(uint64_t)));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 96 * sizeof(uint64_t)));
     HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 64 * sizeof(uint64_t), c->stream));
   }
   HIP_TRY(hipEventRecord(c->t0, c->stream));
@@ -2195,6 +2279,183 @@ int seq_place(koordhip_ctx *c) {
   c->eval_kernel = kh::seq_kernel_name(c->dc);
   c->resolve_kernel = c->eval_kernel;
   c->pipe_check = true;
+  return 0;
+}
+
+// The class-incremental lists' plan of the staged batch for (P, lag): the
+// builds (batches by round) and each class's schedule.  A class is (re)built
+// when a round needs it and its current build is too old: lists of round u
+// apply the log rounds [tb, u - lag) of a build on the state after round
+// tb - 1, each round can move at most P of its keys out of the valid range, so
+// a build stays valid for amax = (kClsTarget - K) / P log rounds (at least K
+// valid keys remain).  A round that needs a build rebuilds, in the same batch,
+// every class whose build would expire within the next amax / 2 rounds (few
+// large batches: a build launch costs the same for 1 or 64 classes).  A
+// build for round u is enqueued kClsLead rounds ahead, on the state the lists
+// of round u - kClsLead see.  Class c's workgroup switches to the newest
+// build of c whose batch round is <= the round it is at (skipping builds it
+// never needed); a build overwrites the buffer slot of the class's build two
+// before it, so it waits until the workgroup copied the last build of that
+// slot it loads (bw, in switches; builds of a class alternate slots).
+constexpr int32_t kClsLead = 12;
+
+static int cls_plan(koordhip_ctx *c, int32_t P, int32_t lag, int32_t K) {
+  if (c->plan_ok && c->plan_P == P && c->plan_lag == lag) return 0;
+  const int32_t total = c->n_staged, rounds = (total + P - 1) / P, nc = (int32_t)c->cls_rep.size();
+  const int32_t amax = (kh::kClsTarget - K) / P, horizon = amax / 2;
+  c->plan_ok = false;
+  c->plan_builds.clear();
+  c->plan_ent.clear();
+  c->plan_bm.clear();
+  c->plan_bw.clear();
+  c->plan_bpods.clear();
+  std::vector<int32_t> valid(nc, -1), nb(nc, 0), seen(nc, -1);
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> builds(nc);  // per class (batch round, entry index)
+  std::vector<std::vector<int32_t>> apps(nc);                         // per class the rounds it appears in
+  for (int32_t u = 0; u < rounds; u++) {
+    const int32_t p0 = u * P, np = std::min(P, total - p0);
+    koordhip_ctx::ClsBuild b{u, std::max(0, u - kClsLead), 0, (int32_t)c->plan_ent.size(), 0};
+    b.tb = std::max(0, b.er - lag);
+    bool need = false;
+    for (int32_t j = 0; j < np && !need; j++) need = valid[c->pod_cls[p0 + j]] < u;
+    if (need)
+      for (int32_t cl = 0; cl < nc; cl++)
+        if (valid[cl] < u + horizon) {
+          valid[cl] = b.tb + lag + amax;
+          nb[cl]++;
+          builds[cl].push_back({u, (int32_t)c->plan_ent.size()});
+          c->plan_ent.push_back((cl << 1) | ((nb[cl] - 1) & 1));
+          c->plan_bm.push_back(nb[cl]);
+          c->plan_bw.push_back(0);
+          c->plan_bpods.push_back(c->cls_rep[cl]);
+          b.ne++;
+        }
+    if (b.ne) c->plan_builds.push_back(b);
+    for (int32_t j = 0; j < np; j++) {
+      const int32_t cl = c->pod_cls[p0 + j];
+      if (seen[cl] == u) continue;
+      seen[cl] = u;
+      apps[cl].push_back(u);
+    }
+  }
+  // schedules: switch at an appearance when a newer build's batch round has
+  // come; the switch count at which each loaded build was copied
+  c->plan_coff.assign(nc + 1, 0);
+  c->plan_csched.clear();
+  c->plan_csm.clear();
+  for (int32_t cl = 0; cl < nc; cl++) {
+    c->plan_coff[cl] = (int32_t)c->plan_csched.size();
+    const auto &bl = builds[cl];
+    std::vector<int32_t> loaded_at(bl.size() + 1, 0);  // build m -> the switch that copied it (0: never)
+    int32_t cur = 0, nsw = 0;
+    size_t bi = 0;
+    for (int32_t u : apps[cl]) {
+      while (bi < bl.size() && bl[bi].first <= u) bi++;
+      const int32_t latest = (int32_t)bi;  // builds 1 .. bi have batch rounds <= u
+      if (latest != cur) {
+        cur = latest;
+        loaded_at[cur] = ++nsw;
+        c->plan_csched.push_back(u | (int32_t)0x80000000);
+        c->plan_csm.push_back(cur);
+      } else {
+        c->plan_csched.push_back(u);
+        c->plan_csm.push_back(0);
+      }
+    }
+    for (size_t q = 0; q < bl.size(); q++) {
+      const int32_t m = (int32_t)q + 1;
+      int32_t w = 0;  // the newest loaded build of the same slot before m
+      for (int32_t x = m - 2; x >= 1 && !w; x -= 2) w = loaded_at[x];
+      c->plan_bw[bl[q].second] = w;
+    }
+  }
+  c->plan_coff[nc] = (int32_t)c->plan_csched.size();
+  // one device array for the schedule tables, the build tables and the sync words
+  const size_t sz[8] = {c->plan_coff.size(), c->plan_csched.size(), c->plan_csm.size(), c->plan_ent.size(),
+                        c->plan_bm.size(), c->plan_bw.size(), (size_t)nc, (size_t)nc + kh::kClsRoundRing};
+  size_t tot = 0;
+  for (int q = 0; q < 8; q++) {
+    c->plan_off[q] = tot;
+    tot += (sz[q] + 15) & ~(size_t)15;
+  }
+  if (tot > c->plan_cap) {
+    if (c->d_plan) HIP_TRY(hipFree(c->d_plan));
+    c->d_plan = nullptr;
+    HIP_TRY(hipMalloc(&c->d_plan, tot * sizeof(int32_t)));
+    c->plan_cap = tot;
+  }
+  const size_t np2 = std::max<size_t>(1, c->plan_bpods.size()) + 16;
+  if (np2 > c->plan_pods_cap) {
+    if (c->d_plan_pods) HIP_TRY(hipFree(c->d_plan_pods));
+    c->d_plan_pods = nullptr;
+    HIP_TRY(hipMalloc(&c->d_plan_pods, np2 * sizeof(kh::DevPod)));
+    c->plan_pods_cap = np2;
+  }
+  const std::vector<int32_t> *src[6] = {&c->plan_coff, &c->plan_csched, &c->plan_csm, &c->plan_ent, &c->plan_bm,
+                                        &c->plan_bw};
+  for (int q = 0; q < 6; q++)
+    if (!src[q]->empty())
+      HIP_TRY(hipMemcpyAsync(c->d_plan + c->plan_off[q], src[q]->data(), src[q]->size() * sizeof(int32_t),
+                             hipMemcpyHostToDevice, c->stream));
+  if (!c->plan_bpods.empty())
+    HIP_TRY(hipMemcpyAsync(c->d_plan_pods, c->plan_bpods.data(), c->plan_bpods.size() * sizeof(kh::DevPod),
+                           hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->plan_ok = true;
+  c->plan_P = P;
+  c->plan_lag = lag;
+  return 0;
+}
+
+// buffers and build scratch of the class lists (before the persistent
+// resolve is launched: an allocation later could wait behind it)
+static int cls_alloc(koordhip_ctx *c, int32_t n) {
+  const int32_t nc = (int32_t)c->cls_rep.size();
+  if (nc > c->cls_cap) {
+    if (c->d_cls_buf) HIP_TRY(hipFree(c->d_cls_buf));
+    if (c->d_cls_meta) HIP_TRY(hipFree(c->d_cls_meta));
+    c->d_cls_buf = nullptr;
+    c->d_cls_meta = nullptr;
+    HIP_TRY(hipMalloc(&c->d_cls_buf, (size_t)nc * 2 * kh::kClsCap * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&c->d_cls_meta, (size_t)nc * 2 * sizeof(kh::ClsMeta)));
+    c->cls_cap = nc;
+  }
+  const int64_t stride = ((int64_t)n + 63) & ~63ll;
+  const int32_t mstride = (kh::scan_chunks(c->partial_r, 0, n) + 63) & ~63;
+  const size_t sb = (size_t)kh::kClsBuildRows * (stride + mstride) * sizeof(uint16_t) + 64;
+  return ensure(c, &c->d_cls_S, &c->cls_S_cap, sb);
+}
+
+static kh::ClsSync cls_sync(koordhip_ctx *c, kh::PipeSync *sync) {
+  kh::ClsSync cs;
+  cs.sy = sync;
+  cs.done = c->d_plan + c->plan_off[6];
+  cs.sw = c->d_plan + c->plan_off[7];
+  cs.rcnt = cs.sw + ((c->cls_rep.size() + 15) & ~(size_t)15);
+  return cs;
+}
+
+// One build batch on the build stream: every class of the batch evaluated on
+// every node (k_scan), its buffer collected (k_cls_collect).
+static int cls_build(koordhip_ctx *c, const koordhip_ctx::ClsBuild &b, kh::PipeSync *sync, hipStream_t bs, bool timed) {
+  const int32_t n = c->n;
+  if (b.tb > 0) HIP_TRY(kh::launch_wait_resolved(sync, b.tb, bs));
+  const int64_t stride = ((int64_t)n + 63) & ~63ll;
+  const int32_t mstride = (kh::scan_chunks(c->partial_r, 0, n) + 63) & ~63;
+  uint16_t *S = reinterpret_cast<uint16_t *>(c->d_cls_S);
+  uint16_t *Mx = S + (size_t)kh::kClsBuildRows * stride;
+  const kh::ClsSync cs = cls_sync(c, sync);
+  for (int32_t j = 0; j < b.ne; j += kh::kClsBuildRows) {
+    const int32_t nb = std::min(kh::kClsBuildRows, b.ne - j);
+    int32_t tm = -1;
+    if (timed)
+      if (int e = timed_begin(c, TK_SELECT, bs, &tm)) return e;
+    HIP_TRY(kh::launch_scan(c->partial_r, c->dc, c->d, c->d_plan_pods + b.e0 + j, nb, 0, n, S, stride, Mx, mstride, 0, bs));
+    HIP_TRY(kh::launch_cls_collect(S, stride, n, c->d_plan + c->plan_off[3] + b.e0 + j,
+                                   c->d_plan + c->plan_off[4] + b.e0 + j, c->d_plan + c->plan_off[5] + b.e0 + j, nb,
+                                   b.tb, c->d_cls_buf, c->d_cls_meta, cs, c->d_dbg ? c->d_dbg + 64 : nullptr, bs));
+    if (int e = timed_end(c, tm, bs)) return e;
+  }
   return 0;
 }
 
@@ -2249,6 +2510,15 @@ int place_staged_impl(koordhip_ctx *c) {
   // (node-sharded: the rounds of the second stream exchange on comm2)
   const bool two = persistent && (!exch || c->comm2) && c->sel_split && wait_kernel &&
                    !std::getenv("KOORDHIP_ONE_EVAL_STREAM");
+  // class-incremental lists (cls.hip): the staged pods fall into few classes
+  // (byte-identical records); the second stream then runs the class builds
+  // (one persistent workgroup per class: every one resident, one per CU with
+  // half the CUs to spare for the resolve and the builds; not beside the
+  // KOORDHIP_CU_RESERVE A/B knob, whose masks were measured to stall 202
+  // class workgroups)
+  bool cls = two && !exch && !c->cls_rep.empty() && c->nbins <= 32768 && !std::getenv("KOORDHIP_CLS_OFF") &&
+             !c->cu_reserve && (int64_t)c->cls_rep.size() <= c->n_cu / 2 &&
+             kh::cls_run_lds(c->n, c->monotone) <= 150 * 1024;
   // Pipeline depth: round r's lists are evaluated on the state after round
   // r - 1 - lag.  Lag 2 (the default with the two evaluation streams) lets an
   // evaluation overlap two resolve rounds; the resolve then re-evaluates the
@@ -2268,6 +2538,7 @@ int place_staged_impl(koordhip_ctx *c) {
   const int nm = kh::side_mode(c->dc);
   while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, nm, lag) > 157 * 1024) P--;
   const int32_t K = (lag + 1) * P;
+  if (cls && (kh::kClsTarget - K) / P < 4 * kClsLead + 2) cls = false;
   c->last_P = P;
   c->last_lag = lag;
   const size_t lbytes = (size_t)kMaxBatch * 2 * kMaxBatch * sizeof(uint64_t);
@@ -2325,8 +2596,8 @@ int place_staged_impl(koordhip_ctx *c) {
   c->last_launches = 0;
   c->last_evals = 0;
   if (std::getenv("KOORDHIP_STAMPS")) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 64 * sizeof(uint64_t)));
-    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 64 * sizeof(uint64_t), c->stream));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 96 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 96 * sizeof(uint64_t), c->stream));
   }
   int32_t *mbuf = c->d_mod;  // M' handed between resolve launches
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
@@ -2359,7 +2630,16 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_eval2, hipEventDisableTiming));
   }
   if (two) HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
-  for (int slot = 0; slot < (two ? 2 : 1) && rounds > 0; slot++) {
+  if (cls && rounds > 0) {
+    if (int e = cls_plan(c, P, lag, K)) return e;
+    if (int e = cls_alloc(c, c->n)) return e;
+    // the build / switch counters start every call at zero; the build stream sees them
+    HIP_TRY(hipMemsetAsync(c->d_plan + c->plan_off[6], 0,
+                           (2 * ((c->cls_rep.size() + 15) & ~(size_t)15) + kh::kClsRoundRing) * sizeof(int32_t), c->stream));
+    HIP_TRY(hipEventRecord(c->ev_start, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+  }
+  for (int slot = 0; slot < (two ? 2 : 1) && rounds > 0 && !cls; slot++) {
     hipStream_t es = slot ? c->stream2 : c->stream;
     if (int e = eval_buffers(c, std::min(P, total), lo, hi, slot, es, K)) return e;
     // the per-pod hand-off words start every call at zero (Guideline 16: a
@@ -2376,7 +2656,24 @@ int place_staged_impl(koordhip_ctx *c) {
     c->resolve_kernel = kh::last_resolve_kernel();
     res_tm = tm;  // its end event is recorded after the round loop (nothing else runs on rstream)
   }
-  for (int32_t r = 0; r < rounds; r++) {
+  if (cls && rounds > 0) {
+    // ONE persistent workgroup per class for the whole stream (c->stream), the
+    // builds on the second stream, all enqueued now (each build waits for its
+    // state's round on the device)
+    int32_t tm = -1;
+    if (int e = timed_begin(c, TK_SCAN, c->stream, &tm)) return e;
+    HIP_TRY(kh::launch_cls_run(c->dc, c->d, c->d_cls_pod, (int32_t)c->cls_rep.size(), c->d_plan + c->plan_off[0],
+                               c->d_plan + c->plan_off[1], c->d_plan + c->plan_off[2], c->d_pod_cls, c->d_out, lag, P,
+                               total, c->d_cls_buf, c->d_cls_meta, K, c->monotone, c->d_lists, list_buf,
+                               cls_sync(c, sync), c->d_dbg ? c->d_dbg + 64 : nullptr, c->stream));
+    if (int e = timed_end(c, tm, c->stream)) return e;
+    for (const koordhip_ctx::ClsBuild &b : c->plan_builds)
+      if (int e = cls_build(c, b, sync, c->stream2, b.u % tstride == 0)) return e;
+    c->eval_kernel = kh::cls_run_kernel_name(c->dc);
+    c->last_launches = 1;
+    c->last_evals = (int64_t)total * c->n;  // every (pod, node) pair decided exactly (the lists' equivalent work)
+  }
+  for (int32_t r = 0; r < rounds && !cls; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
     const int par = r & 1;
     const int32_t cum = P * (r >> 1) + np;  // pods of the rounds of parity `par` up to r
@@ -2469,6 +2766,16 @@ int place_staged_impl(koordhip_ctx *c) {
     std::fprintf(stderr, "[koordhip stamps] general path split: list + X + c %llu cycles | pods with ready key tables %llu | "
                  "evaluation passes %llu\n",
                  (unsigned long long)h[55], (unsigned long long)h[56], (unsigned long long)h[57]);
+    if (cls) {
+      uint64_t q[32];
+      HIP_TRY(hipMemcpy(q, c->d_dbg + 64, sizeof(q), hipMemcpyDeviceToHost));
+      const double nl = (double)std::max<uint64_t>(q[7], 1), nc = (double)std::max<uint64_t>(q[15], 1);
+      std::fprintf(stderr, "[koordhip stamps] class lists, cycles per launch (workgroup 0, %llu launches): buffer %.0f  log %.0f  "
+                   "touched keys %.0f  compaction %.0f  sort %.0f  merge %.0f  outputs %.0f | builds (%llu): histogram %.0f  "
+                   "fine %.0f  emit %.0f  sort %.0f  write %.0f\n", (unsigned long long)q[7], q[0] / nl, q[1] / nl, q[2] / nl,
+                   q[3] / nl, q[4] / nl, q[5] / nl, q[6] / nl, (unsigned long long)q[15], q[8] / nc, q[9] / nc, q[10] / nc,
+                   q[11] / nc, q[12] / nc);
+    }
     std::fprintf(stderr, "[koordhip stamps] general commit split: row source %llu  Reserve delta %llu  voiding + "
                  "outputs %llu cycles | winners already in M %llu\n",
                  (unsigned long long)h[58], (unsigned long long)h[59], (unsigned long long)h[60],

@@ -24,6 +24,8 @@
 
 #include "eval.hpp"
 #include "kernels.h"
+#include "pipe.hpp"
+#include "rows.hpp"
 
 namespace kh {
 
@@ -91,11 +93,6 @@ __device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
   return ((uint64_t)mh << 32) | ml;
 }
 
-__device__ __forceinline__ uint64_t stamp() {
-  uint64_t t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
 
 // Wave max of an i32 (same DPP pattern), result uniform.
 __device__ __forceinline__ int32_t wave_max_i32_dpp(int32_t v) {
@@ -265,8 +262,6 @@ __device__ __forceinline__ int32_t block_exclusive_scan(int32_t v, int32_t *wsum
   return base + x - v;
 }
 
-struct PipeSync;
-__device__ void pipe_count_pod(PipeSync *sy, int32_t par);
 
 __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__restrict__ in, int64_t pod_stride,
                                                               int64_t list_stride, int32_t L, int32_t k,
@@ -437,9 +432,6 @@ __global__ __launch_bounds__(MERGE_THREADS) void k_topk_merge(const uint64_t *__
 #define SCAN_WPE3 4
 #endif
 constexpr int32_t kScanPodFastNodes = 65536;
-template <int NM>
-using side_row_t = typename std::conditional<NM >= 4, NumaRowR4,
-                                             typename std::conditional<NM == 3, NumaRowR, NumaRow>::type>::type;
 
 // NM: 0 = no NodeNUMAResource, 1 = NodeNUMAResource, 2 = ... with
 // topology-policy nodes (the zone code is compiled only here), 3 = with the
@@ -982,64 +974,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(const uint16_t *__restri
 }
 
 // ---------------------------------------------------------------------------
-// Device-side handshake between the evaluation stream and the persistent
-// resolve kernel (one per koordhip_place_staged call):
-//   sel[b]     pods of the rounds with parity b whose final lists are ready
-//              (cumulative; rounds alternate between two evaluation streams, so
-//              a later round may finish first) (k_select_split's
-//              merging workgroups add 1 each; k_signal_lists stores the count
-//              after a separate merge)
-//   res_round  rounds resolved + written back (k_resolve, release store)
-//   err        a side gave up waiting (watchdog): the call fails, nothing hangs
-struct PipeSync {
-  int32_t sel[2], res_round, err;
-};
-
-constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up
-
-__device__ __forceinline__ int32_t load_acquire(const int32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int32_t load_relaxed(const int32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Publish a flag after this wave's global stores (MI355X_MICROARCH.md
-// cross-XCD hand-off: wait for the stores, write the XCD L2 back, wait for
-// the write-back -- spelled out in asm because ROCm 7.2 can drop the wait
-// after buffer_wbl2 -- then a relaxed agent-scope flag store).
-__device__ __forceinline__ void store_release(int32_t *p, int32_t v) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One pod's final list is stored write-through (st_wt: every byte sc1, every
-// storing wave drained vmcnt and met at a barrier): count it into sel[par]
-// with a relaxed agent add, no release fence (Guideline 16 R1; the resolve's
-// wave acquires after its poll).
-__device__ void pipe_count_pod(PipeSync *sy, int32_t par) {
-  __hip_atomic_fetch_add(&sy->sel[par], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Spin (one thread) until *p >= v; false when the watchdog fires or the other
-// side reported an error.  Relaxed polls, ONE agent acquire after the match
-// (an acquire per poll costs 2-3x per hop, Guideline 16 Pitfall 5).
-__device__ bool wait_at_least(const int32_t *p, int32_t v, PipeSync *sy) {
-  const uint64_t t0 = stamp();
-  while (load_relaxed(p) < v) {
-    if (load_relaxed(&sy->err)) return false;
-    if (stamp() - t0 > PIPE_WATCHDOG) {
-      store_release(&sy->err, 1);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  return true;
-}
-
 // ---------------------------------------------------------------------------
 // k_select_split: the same exact top-k with G workgroups per pod.
 //
@@ -1922,36 +1856,6 @@ __device__ __forceinline__ uint64_t ktab_key(uint32_t v, int32_t nd) {
   return v ? ((uint64_t)v << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)nd) : 0ull;
 }
 
-template <int NM>
-__device__ __forceinline__ void load_side_row(side_row_t<NM> &r, const DevNodes &d, int32_t i) {
-  load_numa_row<NM == 2>(r, d, i);
-  if constexpr (NM >= 3) load_resv(r, d.rv, i);
-}
-template <int NM>
-__device__ __forceinline__ void store_side_row(const side_row_t<NM> &r, const DevNodes &d, int32_t i) {
-  store_numa_row<NM == 2>(r, d, i);
-  if constexpr (NM >= 3) store_resv(r, d.rv, i);
-}
-template <int NM>
-__device__ __forceinline__ void store_side_row_wt(const side_row_t<NM> &r, const DevNodes &d, int32_t i) {
-  store_numa_row_wt<NM == 2>(r, d, i);
-  if constexpr (NM >= 3) store_resv_wt(r, d.rv, i);
-}
-
-template <int NM>
-__device__ __forceinline__ int32_t eval_row(const DevPod &p, const NV &v, const side_row_t<NM> &nr,
-                                            const DevNumaClass *cls, const DevCfg &c) {
-  if constexpr (NM >= 3) {
-    return eval_total_resv<side_row_t<NM>::kSlots, NM == 5>(p, v, nr, cls, c);
-  } else if constexpr (NM != 0) {
-    return eval_total_numa<NM == 2>(p, v, nr, cls, c);
-  } else {
-    (void)nr;
-    (void)cls;
-    return eval_total(p, v, c);
-  }
-}
-
 // Evaluation stream, before k_scan of round r: rounds < r - 1 must be written back.
 __global__ void k_wait_resolved(PipeSync *sy, int32_t rounds) {
   if (threadIdx.x == 0) (void)wait_at_least(&sy->res_round, rounds, sy);
@@ -2497,7 +2401,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             pslot_r = slot;
           }
           if (mine) {
-            out_node[p0 + lane] = com ? sw : KOORDHIP_UNSCHEDULABLE;
+            // write-through: the class lists read the placements as the commit log
+            st_wt(&out_node[p0 + lane], (int32_t)(com ? sw : KOORDHIP_UNSCHEDULABLE));
             if (out_cpus) {
 #pragma unroll
               for (int q = 0; q < NW; q++) out_cpus[(size_t)(p0 + lane) * NW + q] = 0ull;
@@ -2761,7 +2666,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             ok &= ~voided;
           }
         }
-        if (lane == 0) out_node[p0 + g] = result;
+        if (lane == 0) st_wt(&out_node[p0 + g], result);
         if (out_cpus && lane < NW)
           out_cpus[(size_t)(p0 + g) * NW + lane] =
               lane == 0 ? cpus[0] : (lane == 1 ? cpus[1] : (lane == 2 ? cpus[2] : cpus[3]));
