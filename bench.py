@@ -334,6 +334,23 @@ def main():
     if traffic_src is not None and traffic_kernel != kn["eval"]:
         traffic, traffic_src = None, (f"none for {kn['eval']} (the committed PMC summary is of "
                                       f"{traffic_kernel or 'an unnamed kernel'})")
+    cls = kn["eval"].startswith("kh::k_cls_run")
+    if cls:
+        # class-incremental lists (cls.hip): one persistent workgroup per pod
+        # class for the whole step, builds (k_scan over the class records +
+        # k_cls_collect) in batches on the second stream
+        raw = np.ascontiguousarray(pods).view(np.uint8).reshape(len(pods), -1)
+        ncls = int(len(np.unique(raw, axis=0)))
+        bld_us = ks["select_ms"] * 1e3 / max(ks["select_launches"], 1)
+        eval_obj = {"bound": "latency", "kernel": kn["eval"],
+                    "mode": "class-incremental lists: one persistent workgroup per pod class keeps its best "
+                            f"{2048} keys in LDS and re-evaluates only the nodes the resolve committed since its "
+                            "last round (the commit log); the lists are exact top-k keys like k_scan + select's",
+                    "classes": ncls, "avg_launch_ms": round(ks["scan_ms"] / max(ks["scan_launches"], 1), 3),
+                    "timing": "HIP events around the persistent launch (the whole step)",
+                    "builds": {"kernels": "k_scan over the class records + k_cls_collect",
+                               "timed_batches": int(ks["select_launches"]), "avg_batch_us": round(bld_us, 3)},
+                    "traffic": None}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -372,7 +389,7 @@ def main():
                      "bytes_per_pod": b_pod, "avg_launch_ms": round(res_s * 1e3, 3),
                      "pods_per_launch": pods_per_launch,
                      "us_per_pod": round(res_s * 1e6 / max(pods_per_launch, 1), 4)},
-        "eval_roofline": {"bound": "hbm", "kernel": kn["eval"],
+        "eval_roofline": eval_obj if cls else {"bound": "hbm", "kernel": kn["eval"],
                           "achieved": round(scan_gbs, 1) if scan_gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(scan_gbs / HBM_PEAK_GBS, 4) if scan_gbs else None,
                           "traffic": traffic, "traffic_source": traffic_src,
@@ -381,9 +398,10 @@ def main():
                           "algorithmic_bytes_per_eval": round(float(b_eval.mean()), 2),
                           "algorithmic_GBps": round(evals_per_launch * float(b_eval.mean()) / (scan_us * 1e-6) / 1e9, 1)
                           if scan_us > 0 else None},
-        "select": {"kernel": "(in k_eval_topk)" if fused else "k_select_split",
-                   "avg_launch_us": round(ks["select_ms"] * 1e3 / max(ks["select_launches"], 1), 3)},
     }
+    if not cls:
+        out["select"] = {"kernel": "(in k_eval_topk)" if fused else "k_select_split",
+                         "avg_launch_us": round(ks["select_ms"] * 1e3 / max(ks["select_launches"], 1), 3)}
     if args.check:
         import oracle
         ref = oracle.Oracle(cfg, table).place_stream(pods, threads=min(16, os.cpu_count() or 1))

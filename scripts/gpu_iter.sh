@@ -19,8 +19,8 @@ for w in ${WORKLOADS:-config4 config5 config3}; do
 import json, sys
 try:
     d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-    print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], "eval us", d["eval_roofline"]["avg_launch_us"],
-          "select us", d["select"]["avg_launch_us"], "unsched", d["unschedulable"])
+    print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], "eval", d["eval_roofline"].get("avg_launch_us", d["eval_roofline"].get("avg_launch_ms")),
+          "select us", d.get("select", {}).get("avg_launch_us"), "unsched", d["unschedulable"])
 except Exception as e:
     print(sys.argv[2], "no result", e)
 PY

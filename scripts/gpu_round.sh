@@ -38,7 +38,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 if "eval_roofline" in d:
     print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], d["eval_roofline"]["kernel"],
-          "eval us", d["eval_roofline"]["avg_launch_us"], "select us", d["select"]["avg_launch_us"],
+          "eval", d["eval_roofline"]["kernel"], d["eval_roofline"].get("avg_launch_us", d["eval_roofline"].get("avg_launch_ms")), "select us", d.get("select", {}).get("avg_launch_us"),
           "P", d["config"]["batch_pods"], "lag", d["config"]["pipeline_lag"], "unsched", d["unschedulable"])
 else:  # the sequential cycle's workloads
     print(sys.argv[2], "pods/s", d["value"], "ms/step", d["ms_per_step"], d["roofline"]["kernel"],
