@@ -187,6 +187,11 @@ def main():
     ap.add_argument("--one-rank-comm", action="store_true",
                     help="N=1 only: attach a one-rank RCCL communicator, so every round takes the multi-GPU "
                          "exchange path (all-gather + merge) -- measures that pipeline on one GPU")
+    ap.add_argument("--mode", choices=["replicas", "shard"], default="replicas",
+                    help="N > 1: 'replicas' (default) -- every rank places its own copy of the stream on its own "
+                         "replica of the cluster (independent scheduler instances; weak scaling: the greedy's "
+                         "sequential Reserve chain does not shard, DESIGN.md section 6); 'shard' -- the node table "
+                         "sharded across the ranks, per-round top-k all-gathered over RCCL (strong scaling)")
     ap.add_argument("--probe-ranks", action="store_true",
                     help="print this rank's RANK / WORLD_SIZE and exit before any GPU work (launcher test)")
     args = ap.parse_args()
@@ -245,7 +250,8 @@ def main():
     cfg = to_c_config(prof)
 
     eng = PlacementEngine(prof, device=local_rank, profile_kernels=False)
-    if world > 1:
+    shard = world > 1 and args.mode == "shard"
+    if shard:
         uid = PlacementEngine.comm_unique_id() if rank == 0 else bytes(128)
         t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda")
         dist.broadcast(t, 0)
@@ -296,9 +302,9 @@ def main():
             dist.destroy_process_group()
         return
 
-    pods_total = args.pods * args.steps
+    pods_total = args.pods * args.steps * (world if world > 1 and not shard else 1)  # replicas: every rank's stream
     pods_profiled = args.pods
-    evals_total = args.pods * args.nodes * args.steps   # every pod is evaluated against every node
+    evals_total = pods_total * args.nodes   # every pod is evaluated against every node (of its replica)
     value = pods_total / elapsed
     batch = int(ks["round_pods"]) or eng.cfg.batch_pods or (16 if numa else 32)
     lag = int(ks["lag"]) or 1
@@ -361,7 +367,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if world == 1 or shard else "weak",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded splitmix64 cluster + pod stream, SURVEY.md §8(d))",
@@ -379,7 +385,8 @@ def main():
                                 + (" + DeviceShare (weight 1; 30% of the nodes with GPUs, no pod requesting one: "
                                    "the pipelined greedy)" if args.workload == "config4ds" else "")),
                    "nodes": args.nodes, "pods": args.pods, "batch_pods": batch, "pipeline_lag": lag,
-                   "parallelism": f"node-shard x{world}" + (" (one-rank RCCL exchange path)" if args.one_rank_comm and world == 1 else "")},
+                   "parallelism": (f"replicas x{world} (every rank: its own cluster replica and stream)" if world > 1 and not shard
+                                   else f"node-shard x{world}" + (" (one-rank RCCL exchange path)" if args.one_rank_comm and world == 1 else ""))},
         "unschedulable": int((placements < 0).sum()),
         "roofline": {"bound": "latency", "kernel": kn["resolve"],
                      "limiter": "latency: one workgroup's sequential greedy (not bandwidth); priced against HBM peak",
