@@ -161,7 +161,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=["config4", "config3", "config5", "deviceshare", "spread", "affinity",
-                                                   "resvpolicy", "config4ds"], default="config4",
+                                                   "resvpolicy", "config4ds", "config4dsmix"], default="config4",
                     help="config4: the headline (50k x 100k, Fit + LoadAware); config3: NodeNUMAResource "
                          "cpuset/NUMA-fit scoring (5k 2-socket nodes x 10k pods, 50%% LSR/LSE cpuset pods); "
                          "config5: 200k nodes, 10%% holding a Reservation matched by 20%% of the pods, "
@@ -180,7 +180,8 @@ def main():
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--be-frac", type=float, default=None)
     ap.add_argument("--batch", type=int, default=0)
-    ap.add_argument("--dev-frac", type=float, default=0.2, help="deviceshare workload: share of pods requesting GPUs")
+    ap.add_argument("--dev-frac", type=float, default=None,
+                    help="deviceshare / config4dsmix workloads: share of pods requesting GPUs (default 0.2 / 0.02)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--check", action="store_true", help="verify placements vs the oracle (slow)")
@@ -230,16 +231,17 @@ def main():
 
     resv = args.workload == "config5"
     numa = args.workload == "config3" or resv
-    c = synth.CONFIGS[{"config3": 3, "config4": 4, "config5": 5, "config4ds": 4}[args.workload]]
+    c = synth.CONFIGS[{"config3": 3, "config4": 4, "config5": 5, "config4ds": 4, "config4dsmix": 4}[args.workload]]
+    dsmix = args.workload == "config4dsmix"
     args.nodes = args.nodes or c["nodes"]
     args.pods = args.pods or c["pods"]
     args.be_frac = c["be_frac"] if args.be_frac is None else args.be_frac
     prof = shipped_profile(numa=numa, reservation=resv)
-    if args.workload == "config4ds":
+    if args.workload in ("config4ds", "config4dsmix"):
         prof = with_deviceshare(prof)
     prof.batch_pods = args.batch
     table = synth.make_cluster(synth.ClusterSpec(args.nodes), prof)
-    if args.workload == "config4ds":
+    if args.workload in ("config4ds", "config4dsmix"):
         synth.add_devices(table, synth.DevSpec())
     if numa:
         synth.add_numa(table, synth.NumaSpec(), prof)
@@ -247,6 +249,10 @@ def main():
         synth.add_reservations(table, synth.ResvSpec())
     pods = synth.make_pods(synth.StreamSpec(args.pods, be_frac=args.be_frac, cpuset_frac=c.get("cpuset_frac", 0.0),
                                             resv_match_frac=c.get("resv_match_frac", 0.0)), prof)
+    # config4dsmix: a few pods request GPUs (the reference's request forms,
+    # synth.make_device_ext); the rest carry empty records
+    ext = synth.make_device_ext(args.pods, synth.DevStreamSpec(frac=0.02 if args.dev_frac is None else args.dev_frac)) \
+        if dsmix else None
     cfg = to_c_config(prof)
 
     eng = PlacementEngine(prof, device=local_rank, profile_kernels=False)
@@ -260,7 +266,10 @@ def main():
         eng.comm_init(PlacementEngine.comm_unique_id(), 1, 0)
     eng.load_snapshot(table)
     eng.checkpoint()
-    eng.stage_pods(pods)
+    if ext is None:
+        eng.stage_pods(pods)
+    else:
+        eng.stage_pods_ext(pods, ext)
 
     def step():
         eng.restore()
@@ -383,7 +392,11 @@ def main():
                                 f"config4: {args.nodes} nodes x {args.pods} pods, {int(args.be_frac * 100)}% BE, "
                                 "NodeResourcesFit + LoadAwareScheduling, shipped scheduler-config.yaml profile"
                                 + (" + DeviceShare (weight 1; 30% of the nodes with GPUs, no pod requesting one: "
-                                   "the pipelined greedy)" if args.workload == "config4ds" else "")),
+                                   "the pipelined greedy)" if args.workload == "config4ds" else "")
+                                + (f" + DeviceShare (weight 1; 30% of the nodes with GPUs; "
+                                   f"{int((ext['flags'] != 0).sum())} pods ({(ext['flags'] != 0).mean() * 100:.1f}%) "
+                                   "requesting GPUs in the reference's four request forms, placed inside the pipelined "
+                                   "greedy by k_ext_worker)" if dsmix else "")),
                    "nodes": args.nodes, "pods": args.pods, "batch_pods": batch, "pipeline_lag": lag,
                    "parallelism": (f"replicas x{world} (every rank: its own cluster replica and stream)" if world > 1 and not shard
                                    else f"node-shard x{world}" + (" (one-rank RCCL exchange path)" if args.one_rank_comm and world == 1 else ""))},
@@ -409,12 +422,18 @@ def main():
     if not cls:
         out["select"] = {"kernel": "(in k_eval_topk)" if fused else "k_select_split",
                          "avg_launch_us": round(ks["select_ms"] * 1e3 / max(ks["select_launches"], 1), 3)}
+    if dsmix:
+        out["device_pods"] = {"pods": int((ext["flags"] != 0).sum()), "worker": "k_ext_worker<0>",
+                              "route": "pipelined (resolve hand-off)" if kn["resolve"].startswith("kh::k_resolve")
+                              else "sequential cycle"}
     if args.check:
         import oracle
-        ref = oracle.Oracle(cfg, table).place_stream(pods, threads=min(16, os.cpu_count() or 1))
+        orc = oracle.Oracle(cfg, table)
+        ref = orc.place_stream(pods, threads=min(16, os.cpu_count() or 1)) if ext is None else \
+            orc.place_stream_ext(pods, ext, threads=min(16, os.cpu_count() or 1))
         out["check"] = bool(np.array_equal(ref, placements))
     if world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(table, pods, cfg, args.cpu_budget)
+        cb = cpu_baseline(table, pods, cfg, args.cpu_budget, ext=ext)
         out["cpu_baseline"] = cb
         out["speedup_vs_best_cpu_leg"] = round(value / cb["best_leg"]["pods_per_s"], 1)
     print(json.dumps(out), flush=True)
@@ -484,7 +503,7 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
             synth.add_ipa(table, ext, synth.IpaSpec())
     else:
         synth.add_devices(table, synth.DevSpec())
-        ext = synth.make_device_ext(args.pods, synth.DevStreamSpec(frac=args.dev_frac))
+        ext = synth.make_device_ext(args.pods, synth.DevStreamSpec(frac=0.2 if args.dev_frac is None else args.dev_frac))
     from koordinator_amd.config import to_c_config
     cfg = to_c_config(prof)
     eng = PlacementEngine(prof, device=0, profile_kernels=False)

@@ -197,6 +197,18 @@ struct koordhip_ctx {
   bool staged_qos_nonbind = false;  // a staged pod KOORDHIP_POD_CPUSET_QOS rejects on some snapshots
   bool staged_reserve = false;     // the staged batch holds a reserve pod (KOORDHIP_POD_RESERVE): the sequential cycle
   bool staged_ext = false;         // the staged batch's koordhip_pod_ext records carry requests / constraints
+  // device pods inside the pipelined greedy (k_ext_worker, seq.hip): the
+  // staged pods whose records carry content, when that content is device /
+  // extended-scalar requests only (no spread constraint or count, no affinity
+  // entry); their DevPods carry KH_POD_EXT
+  bool staged_ext_dev = false;
+  std::vector<int32_t> ext_idx;
+  int32_t *d_ext_idx = nullptr;
+  int32_t ext_idx_cap = 0;
+  void *d_ext_scr = nullptr;        // k_ext_worker's table and arrival counter
+  hipStream_t xstream = nullptr;    // its stream (a dedicated queue: the worker spins on the resolve's flag)
+  hipEvent_t ev_ext = nullptr;
+  bool last_ext_pipe = false;       // the last place call placed device pods inside the pipeline
   // class-incremental lists (cls.hip): the staged pods' classes (byte-identical
   // device records), the class buffers and the plan of the staged batch
   std::vector<int32_t> pod_cls;    // class of each staged pod
@@ -311,6 +323,7 @@ int to_dev_pods(const koordhip_pod *src, int32_t n, std::vector<kh::DevPod> &out
     o.nz_mem = (double)p.nz_mem;
     o.est_cpu = (double)p.est_cpu;
     o.est_mem = (double)p.est_mem;
+    if (p.flags & kh::KH_POD_EXT) return fail(KOORDHIP_EINVAL, "koordhip_pod.flags bit 30 is reserved");
     o.flags = p.flags;
     o.numa_cpus = p.numa_cpus;
     o.numa_policy = p.numa_policy;
@@ -1160,7 +1173,7 @@ int koordhip_destroy(koordhip_ctx *c) {
                   (void *)c->d_etk_pcnt[1], (void *)c->d_etk_sync[0], (void *)c->d_etk_sync[1], c->d_upd,
                   (void *)c->d_podx, (void *)c->d_devout, (void *)c->d_seqg, c->d_seqdesc, (void *)c->d_pod_cls,
                   (void *)c->d_cls_pod, (void *)c->d_cls_buf, (void *)c->d_cls_meta, c->d_cls_S,
-                  (void *)c->d_plan, (void *)c->d_plan_pods})
+                  (void *)c->d_plan, (void *)c->d_plan_pods, (void *)c->d_ext_idx, c->d_ext_scr})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kRing; i++)
     if (c->ev_res[i]) (void)hipEventDestroy(c->ev_res[i]);
@@ -1174,6 +1187,11 @@ int koordhip_destroy(koordhip_ctx *c) {
     (void)hipStreamDestroy(c->stream2);
   }
   if (c->ev_eval2) (void)hipEventDestroy(c->ev_eval2);
+  if (c->xstream) {
+    (void)hipStreamSynchronize(c->xstream);
+    (void)hipStreamDestroy(c->xstream);
+  }
+  if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
@@ -1866,6 +1884,8 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
   c->n_staged = n_pods;
   c->podx_staged = false;
   c->staged_ext = false;
+  c->staged_ext_dev = false;
+  c->ext_idx.clear();
   c->staged_reserve = reserve;
   // prod LSE / LSR pods that bind no CPUs but some reservation may match (see
   // KOORDHIP_POD_CPUSET_QOS): checked against the snapshot at place time
@@ -1948,6 +1968,15 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
   if (any && !c->seq_profile)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   c->staged_ext = any;
+  // the pods with content; device / extended-scalar content only: they can be
+  // placed inside the pipelined greedy (KH_POD_EXT marks them)
+  bool devonly = any;
+  for (int32_t j = 0; j < n_pods && any; j++) {
+    const koordhip_pod_ext &e = ext[j];
+    const bool spread = e.pts_n != 0 || e.pts_match != 0 || (e.ipa_inc | e.ipa_aff | e.ipa_anti | e.ipa_score) != 0;
+    if (e.flags != 0 || e.xmask != 0 || spread) c->ext_idx.push_back(j);
+    devonly = devonly && !spread;
+  }
   if (!any && !rn) return 0;
   if (n_pods > c->podx_cap) {
     if (c->d_podx) HIP_TRY(hipFree(c->d_podx));
@@ -1956,6 +1985,18 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
     c->podx_cap = n_pods;
   }
   HIP_TRY(hipMemcpyAsync(c->d_podx, ext, (size_t)n_pods * sizeof(kh::DevPodX), hipMemcpyHostToDevice, c->stream));
+  if (devonly && !c->ext_idx.empty()) {
+    const int32_t ne = (int32_t)c->ext_idx.size();
+    if (ne > c->ext_idx_cap) {
+      if (c->d_ext_idx) HIP_TRY(hipFree(c->d_ext_idx));
+      c->d_ext_idx = nullptr;
+      HIP_TRY(hipMalloc(&c->d_ext_idx, (size_t)ne * sizeof(int32_t)));
+      c->ext_idx_cap = ne;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_ext_idx, c->ext_idx.data(), (size_t)ne * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(kh::launch_mark_ext(c->d_pods, c->d_ext_idx, ne, c->stream));
+    c->staged_ext_dev = true;
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->podx_staged = true;
   return 0;
@@ -2483,13 +2524,35 @@ int place_staged_impl(koordhip_ctx *c) {
     return fail(KOORDHIP_EINVAL, "a prod LSE/LSR pod binding no CPUs that a reservation may match, on a snapshot with "
                                  "reservations holding CPUs and topology-policy or CPU-amplified nodes: the reserved "
                                  "CPUs' restore for such pods is not modelled (KOORDHIP_POD_CPUSET_QOS)");
-  c->last_seq = c->staged_reserve || c->seq_snap || (c->seq_profile && (!c->seq_ext_only || c->staged_ext));
+  // Device pods among pods without ext content (DeviceShare as the only
+  // coupling plugin the records use, the plain plugin build, one GPU, the
+  // persistent pipeline): placed inside the pipelined greedy -- the resolve
+  // hands each one the exact state and k_ext_worker runs its reference cycle
+  // (seq.hip) -- instead of the whole batch in the sequential cycle.
+  // KOORDHIP_EXT_SEQ: the sequential cycle for such batches too (A/B).
+  const bool ext_pipe = c->seq_profile && c->seq_ext_only && c->staged_ext && c->staged_ext_dev && c->podx_staged &&
+                        !c->staged_reserve && !c->seq_snap && kh::side_mode(c->dc) == 0 && c->world == 1 &&
+                        !c->comm && !c->group && !std::getenv("KOORDHIP_SERIAL") && !std::getenv("KOORDHIP_ROUND_LAUNCH") &&
+                        !std::getenv("KOORDHIP_EXT_SEQ");
+  c->last_ext_pipe = ext_pipe;
+  c->last_seq = c->staged_reserve || c->seq_snap || (c->seq_profile && (!c->seq_ext_only || c->staged_ext) && !ext_pipe);
   if (c->last_seq) return seq_place(c);
-  // the pipelined greedy allocates no device: clear the slots a previous
-  // sequential batch left (koordhip_fetch_devices reads this buffer)
+  if (ext_pipe) {  // (allocations before the persistent launches: one later could wait behind them)
+    if (!c->d_devout && c->pods_cap > 0)
+      HIP_TRY(hipMalloc(&c->d_devout, (size_t)c->pods_cap * KOORDHIP_DEV_TYPES * sizeof(uint32_t)));
+    if (!c->d_ext_scr) HIP_TRY(hipMalloc(&c->d_ext_scr, kh::ext_worker_scratch_bytes()));
+    if (!c->xstream) {
+      const std::vector<uint32_t> all = full_cu_mask(c);
+      HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)all.size(), all.data()));
+      HIP_TRY(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming));
+    }
+  }
+  // the pipelined greedy allocates no device but the device pods' (k_ext_worker):
+  // clear the slots a previous sequential batch left (koordhip_fetch_devices
+  // reads this buffer)
   if (c->d_devout && c->n_staged > 0)
     HIP_TRY(hipMemsetAsync(c->d_devout, 0, (size_t)c->n_staged * KOORDHIP_DEV_TYPES * sizeof(uint32_t), c->stream));
-  if (c->podx_staged && c->staged_ext)
+  if (c->podx_staged && c->staged_ext && !ext_pipe)
     return fail(KOORDHIP_EINVAL, "device / extended-scalar pod requests need DeviceShare in the profile");
   // KOORDHIP_SERIAL (profiling under rocprofv3 --pmc, which serialises
   // dispatches): every launch on one stream in dependency order, one resolve
@@ -2651,10 +2714,25 @@ int place_staged_impl(koordhip_ctx *c) {
   if (persistent && rounds > 0) {
     int32_t tm = -1;
     if (int e = timed_begin(c, TK_RESOLVE, c->rstream, &tm)) return e;
-    HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, c->monotone, lag, sync,
+    // (monotone bit 1: the prologue's chained decisions, opt-in KOORDHIP_CHAIN: they
+    // take the staged-conflict pods off the general path -- config 4: 16.0k -> 0.4k
+    // general-path pods -- but the chain passes cost ~5k cycles a pod in the
+    // prologue and leave wave 0 waiting for wave 1's next-round loads: 75.1 vs
+    // 73.9 ms per step, profiles/r05h_chain_ab.txt)
+    const int32_t mono = c->monotone | ((c->monotone && std::getenv("KOORDHIP_CHAIN")) ? 2 : 0);
+    HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, mono, lag, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
     c->resolve_kernel = kh::last_resolve_kernel();
     res_tm = tm;  // its end event is recorded after the round loop (nothing else runs on rstream)
+  }
+  if (ext_pipe && rounds > 0) {
+    // the device pods' worker: one persistent launch on its own queue, after
+    // the call's PipeSync / device-slot resets (ev_start)
+    HIP_TRY(hipStreamWaitEvent(c->xstream, c->ev_start, 0));
+    HIP_TRY(kh::launch_ext_worker(c->dc, c->d, c->d_pods, c->d_podx, c->d_ext_idx, (int32_t)c->ext_idx.size(),
+                                  kh::ext_worker_grid(c->n_cu, c->n), c->d_ext_scr, c->d_out, c->d_devout, sync,
+                                  c->xstream));
+    HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
   }
   if (cls && rounds > 0) {
     // ONE persistent workgroup per class for the whole stream (c->stream), the
@@ -2716,6 +2794,7 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipEventRecord(c->ev_eval2, c->stream2));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_eval2, 0));
   }
+  if (ext_pipe && rounds > 0) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext, 0));
   if (!serial) {
     HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[0], 0));
@@ -2776,6 +2855,12 @@ int place_staged_impl(koordhip_ctx *c) {
                    q[3] / nl, q[4] / nl, q[5] / nl, q[6] / nl, (unsigned long long)q[15], q[8] / nc, q[9] / nc, q[10] / nc,
                    q[11] / nc, q[12] / nc);
     }
+    std::fprintf(stderr, "[koordhip stamps] chained decisions: %llu cycles, %llu pods resolved\n",
+                 (unsigned long long)h[62], (unsigned long long)h[63]);
+    if (ext_pipe)
+      std::fprintf(stderr, "[koordhip stamps] device pods (k_ext_worker): %llu, resolve cycles from the hand-off to the "
+                   "answer %llu (%.0f per pod)\n", (unsigned long long)h[31], (unsigned long long)h[30],
+                   h[31] ? (double)h[30] / h[31] : 0.0);
     std::fprintf(stderr, "[koordhip stamps] general commit split: row source %llu  Reserve delta %llu  voiding + "
                  "outputs %llu cycles | winners already in M %llu\n",
                  (unsigned long long)h[58], (unsigned long long)h[59], (unsigned long long)h[60],

@@ -1717,6 +1717,7 @@ constexpr int res_loaders() { return res_threads<NM>() >= 512 ? 3 : 1; }
 constexpr int RES_PRE = 128;    // prefetched rows of list heads (RES_PRE / round size per pod)
 constexpr int RES_HASH = 256;   // node -> M' slot (open addressing)
 constexpr int RES_WE = 8;       // list entries the prologue walks per pod
+constexpr int RES_CHAIN_PASSES = 3;  // passes of chained decisions per round
 constexpr int RES_LDS_MAX = 160 * 1024 - 3 * 1024;  // dynamic LDS cap (static LDS: M' nodes, hashes, flags)
 
 // An NV row as 8-byte words (the lane-parallel Reserve): words 0-4 a[], 5-9
@@ -1743,6 +1744,7 @@ __device__ __forceinline__ NV slot_row(const NV &src) {
 }
 
 struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
+  int32_t dep;  // per pod: the earlier pods whose staged commits its chained decision assumed (u64 masks)
   int32_t lists, pods, prev_rows, prev_numa, cur_rows, cur_numa, hash_node, hash_slot, pre_rows, pre_numa, pre_node,
       dec_key, dec_n, dec_src, dec_e, dec_c, moved, mhash, gbits, kpre, ktab, ready, classes, modmap, total;
   int32_t kwide;  // key-table entries are u32 (ranking totals above 16 bits), else u16
@@ -1796,6 +1798,8 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * RES_WE * 4;
   o.dec_c = at;  // per pod: bit 0 = its walk met an earlier pod's staged winner, bit 1 = general path only
   at += RES_MAXP_ROUND * 4;
+  o.dep = at;
+  at += RES_MAXP_ROUND * 8;
   o.moved = at;  // per M' slot: committed to again this round (its row moved into M)
   at += RES_MAXP_ROUND * 4;
   o.mhash = at;  // lazy staged rows: the pod of each M slot, the M slot of each pod
@@ -2010,6 +2014,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t c_p[3] = {0, 0, 0}, n_p2 = 0, n_conf = 0, n_slowc = 0, n_void = 0;
   uint64_t c_cand = 0, n_evpass = 0, n_tready = 0;  // general path: list + X + c cycles, evaluation passes, pods with ready tables
   uint64_t c_gc[3] = {0, 0, 0}, n_ghit = 0;          // general commit: row source, Reserve delta, voiding + outputs; winners in M
+  uint64_t c_chain = 0;                              // chained decisions: cycles (pods resolved: dbg[63])
+  uint64_t c_ext = 0, n_ext = 0;                     // device pods: cycles from the hand-off to the worker's answer, pods
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
   // Every loop keeps several global loads in flight per thread before its LDS
@@ -2238,6 +2244,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           // not monotone), a walk longer than RES_WE entries
           const uint32_t fl = lpod[l].flags;
           bool slow = !monotone || dn < 0;
+          // a device pod: its node comes from k_ext_worker (general path)
+          if constexpr (NM == 0) slow = slow || (fl & KH_POD_EXT) != 0u;
           if constexpr (NUMA) {
             // (with topology-policy nodes every NUMA pod: its zone hint can move
             // to emptier zones as a node fills, so its score is not monotone)
@@ -2288,6 +2296,166 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       }
     }
     __syncthreads();
+    // ---- 2c. chained decisions (monotone configurations, monotone bit 1): a
+    //          conflicting pod re-walks its list with the staged winners of the
+    //          earlier VALID pods as modified entries -- each evaluated on its
+    //          claimer's source row + the claimer's Reserve delta (the key
+    //          tables' kpre) -- up to the first unmodified entry (exact).  Its
+    //          decision then assumes those claimers' commits (dep: a claimer
+    //          voided later voids it too).  A pod whose new winner is a valid
+    //          claimer's node, or whose walk needs more than RES_WE entries,
+    //          stays on the general path.  Every pass re-checks the valid pods
+    //          against the valid claims (a pod resolved in a pass may meet a
+    //          winner resolved in the same pass) and repeats.
+    uint64_t *dep = reinterpret_cast<uint64_t *>(lds + ofs.dep);
+    for (int32_t x = t; x < n_pods; x += RES_THREADS) dep[x] = 0ull;
+    if (monotone & 2) {
+      const uint64_t t_c0 = (dbg && t == 0) ? stamp() : 0;
+      // the claims of the valid (dec_c == 0) pods: staged winner -> pod
+      auto claims = [&]() {
+        for (int32_t x = t; x < RES_HASH; x += RES_THREADS) {
+          ckey[x] = -1;
+          cval[x] = 64;
+        }
+        __syncthreads();
+        if (t < n_pods && dec_c[t] == 0 && dec_key[t] != 0ull) {
+          const int32_t sw = key_node(dec_key[t]);
+          uint32_t h = res_hash(sw);
+          for (;;) {
+            const int32_t prev = atomicCAS(&ckey[h], -1, sw);
+            if (prev == -1 || prev == sw) {
+              atomicMin(&cval[h], t);
+              break;
+            }
+            h = (h + 1) & (RES_HASH - 1);
+          }
+        }
+        __syncthreads();
+      };
+      auto claimer_of = [&](int32_t y) -> int32_t {
+        uint32_t q = res_hash(y);
+        for (;;) {
+          const int32_t xk = ckey[q];
+          if (xk == y) return cval[q];
+          if (xk < 0) return 64;
+          q = (q + 1) & (RES_HASH - 1);
+        }
+      };
+      for (int pass = 0; pass < RES_CHAIN_PASSES; pass++) {
+        claims();
+        if (t == 0) sh_done = 0;  // (reused as this pass's "a pod was resolved")
+        __syncthreads();
+        for (int32_t base = 0; base < n_pods * RES_WE; base += RES_THREADS) {
+          const int32_t x = base + t;
+          const int32_t l = x / RES_WE, q = x - l * RES_WE;
+          const bool live = l < n_pods && dec_c[l] == 1;  // uniform per 8-lane group
+          const uint64_t e = (live && q < kp) ? lk[l * kp + q] : 0ull;
+          const int32_t nd = e ? key_node(e) : -1;
+          const bool inm = e != 0 && xbit(modmap, nd);
+          const int32_t cl = e != 0 ? claimer_of(nd) : 64;
+          const bool clv = cl < l;
+          const bool mod = inm || clv;
+          const int gq = lane & ~(RES_WE - 1);
+          const uint32_t bx = (uint32_t)(__ballot(live && e != 0 && !mod) >> gq) & 0xFFu;
+          const uint32_t bz = (uint32_t)(__ballot(live && e == 0) >> gq) & 0xFFu;
+          const int f = bx ? __builtin_ctz(bx) : RES_WE, z = bz ? __builtin_ctz(bz) : RES_WE;
+          const bool general = f == RES_WE && z == RES_WE;
+          const bool walked = live && !general && (q < min(f, z) || (q == f && f < z));
+          uint64_t key = 0;
+          int32_t ms = -1;
+          if (walked) {
+            if (q < min(f, z)) {  // a modified entry: its key on the row it will have
+              NV v;
+              NR nr;
+              if (clv) {
+                const int32_t src = dec_src[cl];
+                v = src >= 0 ? pre[src] : prow[-src - 1];
+                if constexpr (NUMA) nr = src >= 0 ? prenr[src] : pnr[-src - 1];
+                apply_delta(v, lpod[cl], +1);
+              } else {
+                ms = prev_slot(nd);
+                v = slot_row(prow[ms]);
+                if constexpr (NUMA) nr = pnr[ms];
+              }
+              key = make_key(eval_row<NM>(lpod[l], v, nr, cls, c), nd);
+            } else {
+              key = e;
+            }
+          }
+          uint64_t mx = key, dm = (walked && clv) ? (1ull << cl) : 0ull;
+#pragma unroll
+          for (int m = 1; m < RES_WE; m <<= 1) {
+            const uint64_t o = shfl_xor_u64(mx, m);
+            mx = o > mx ? o : mx;
+            dm |= shfl_xor_u64(dm, m);
+          }
+          const bool win = walked && key == mx && mx != 0;
+          // the new winner is a valid claimer's node: two commits to one node (general path)
+          const bool rep = ((uint32_t)(__ballot(win && clv) >> gq) & 0xFFu) != 0u;
+          if (live && !general && !rep) {
+            dec_e[l * RES_WE + q] = walked ? nd : -1;
+            if (win) {  // the winner's row source, as in phase 2
+              int32_t src;
+              if (inm) {
+                src = -prev_slot(nd) - 1;
+              } else if (q < HP && pre_node[l * HP + q] == nd) {
+                src = l * HP + q;
+              } else {
+                src = l * HP;
+                NV v;
+                load_row(v, nodes(), nd);
+                pre[src] = v;
+                if constexpr (NUMA) {
+                  NR nr;
+                  load_side_row<NM>(nr, nodes(), nd);
+                  prenr[src] = nr;
+                }
+                pre_node[src] = nd;
+              }
+              dec_src[l] = src;
+            }
+            if (q == 0) {
+              dec_key[l] = mx;
+              dec_n[l] = f < z ? f + 1 : z;
+              if (mx == 0) dec_src[l] = 0;
+              dep[l] = dm;
+              dec_c[l] = 0;
+              sh_done = 1;
+              if (dbg) atomicAdd((unsigned long long *)&dbg[63], 1ull);
+            }
+          }
+        }
+        __syncthreads();
+        const bool resolved = sh_done != 0;
+        // re-check: a valid pod whose walk meets a valid claim it did not assume
+        claims();
+        for (int32_t x = t; x < n_pods * RES_WE; x += RES_THREADS) {
+          const int32_t l = x / RES_WE;
+          const int32_t y = dec_e[x];
+          if (y >= 0 && dec_c[l] == 0) {
+            const int32_t cl = claimer_of(y);
+            if (cl < l && !((dep[l] >> cl) & 1ull)) atomicOr(&dec_c[l], 1);
+          }
+        }
+        __syncthreads();
+        if (t < 64) {  // closure in pod order: a pod assuming an invalid pod's commit is invalid
+          const bool lv = lane < n_pods;
+          const uint64_t dl = lv ? dep[lane] : 0ull;
+          uint64_t valid = __ballot(lv && dec_c[lane] == 0);
+          for (;;) {
+            const uint64_t bad = __ballot(((valid >> lane) & 1ull) && (dl & ~valid) != 0ull);
+            if (!bad) break;
+            valid &= ~bad;
+            if ((bad >> lane) & 1ull) dec_c[lane] = 1;
+          }
+        }
+        __syncthreads();
+        if (!resolved) break;  // uniform
+      }
+      if (t == 0) sh_done = 0;  // (the helpers' stop flag again)
+      claims();                 // the loop's claimer(): the valid pods' winners
+      if (dbg && t == 0) c_chain += stamp() - t_c0;
+    }
     if (dbg && t == 0) {
       const uint64_t t_p3 = stamp();
       c_hash += t_a - t_entry;
@@ -2319,6 +2487,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         for (int q = 0; q < RES_WE; q++) se[q] = dec_e[lane * RES_WE + q];
       }
       const uint64_t prodmask = __ballot(live && (fl & KOORDHIP_POD_PROD));
+      const uint64_t mydep = live ? dep[lane] : 0ull;  // the staged commits this pod's chained decision assumed
       // general-path-only pods and conflicts: from the prologue (phase 2 / 2b)
       const int32_t dc = live ? dec_c[lane] : 2;
       const bool slow = (dc & 2) != 0;
@@ -2420,6 +2589,35 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         // ---- general path: pod g alone -- c, then every M and M' row's current key
         n_slow++;
         const DevPod pod = lpod[g];  // VGPR copy: SGPRs are the scarce register file here (uniform_pod measured slower)
+        // A device pod (KH_POD_EXT, plain build): k_ext_worker places it on the
+        // exact state -- every commit so far written back first (M rows,
+        // write-through, drained), then the hand-off; its node (or
+        // UNSCHEDULABLE / RESERVE_FAILED) comes back through out_node, and the
+        // Fit / LoadAware delta is committed below like any general-path pod's.
+        bool ext_pod = false;
+        int32_t ext_res = KOORDHIP_UNSCHEDULABLE;
+        if constexpr (NM == 0) ext_pod = (__builtin_amdgcn_readfirstlane(pod.flags) & KH_POD_EXT) != 0u;
+        if (ext_pod) {
+          const uint64_t t_x = dbg ? stamp() : 0;
+          while (lazy) materialize((int32_t)__builtin_ctzll(lazy));
+          if (lane < nm) {
+            const NV v = slot_row(mrow[lane]);
+            mrow[lane] = v;
+            store_row_wt(v, nodes(), my_node);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          int32_t xr = KOORDHIP_UNSCHEDULABLE;
+          if (lane == 0) {
+            __hip_atomic_store(&sy->ext_req, p0 + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wait_at_least(&sy->ext_done, p0 + g + 1, sy))
+              xr = __hip_atomic_load(&out_node[p0 + g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          ext_res = __builtin_amdgcn_readfirstlane(xr);
+          if (dbg) {
+            c_ext += stamp() - t_x;
+            n_ext++;
+          }
+        }
         const uint64_t *L = lk + (size_t)g * kp;
         const uint64_t e0 = lane < kp ? L[lane] : 0ull;
         const uint64_t e1 = (two && 64 + lane < kp) ? L[64 + lane] : 0ull;
@@ -2427,6 +2625,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         const bool x1 = e1 != 0 && xbit(modmap, key_node(e1));
         const uint64_t f0 = __ballot(e0 != 0 && !x0), f1 = __ballot(e1 != 0 && !x1);
         uint64_t best = f0 ? readlane_u64(e0, __builtin_ctzll(f0)) : (f1 ? readlane_u64(e1, __builtin_ctzll(f1)) : 0ull);
+        if (ext_pod) best = ext_res >= 0 ? make_key(0, ext_res) : 0ull;
         // (NM 5) how many nodes are feasible now: the list's entries outside X
         // are exact, the X rows are all evaluated below (these pods are never
         // monotone), and a list that was not full held every node feasible at
@@ -2440,7 +2639,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         // commit touched), else one evaluation on its current row -- a
         // materialised M slot (a general commit changed it), its staged
         // claimer's lazy row, or its M' row.
-        const bool mono_g = monotone && !((slowmask >> g) & 1ull);
+        const bool mono_g = monotone && !((slowmask >> g) & 1ull);  // (device pods are slow: no keys to take)
         if (dbg) c_cand += stamp() - ts;
         if (mono_g) {
           const bool tabs = have_tables && __hip_atomic_load(&ready[g], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
@@ -2505,7 +2704,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           c_g[0] += x - ts;
           ts = x;
         }
-        const int32_t nrows = mono_g ? 0 : nm + mp;
+        const int32_t nrows = (mono_g || ext_pod) ? 0 : nm + mp;
         const uint64_t t_rows = dbg ? stamp() : 0;
         if (nrows > 0)  // a pass over every M row: materialise the lazy ones first
           while (lazy) materialize((int32_t)__builtin_ctzll(lazy));
@@ -2538,7 +2737,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         }
         lap(2);
         uint64_t cpus[NW] = {0, 0, 0, 0};
-        int32_t result = KOORDHIP_UNSCHEDULABLE;
+        int32_t result = ext_pod ? ext_res : KOORDHIP_UNSCHEDULABLE;
         uint64_t t_gc = dbg ? stamp() : 0;
         auto gclap = [&](int ph) {
           if (dbg) {
@@ -2661,7 +2860,14 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             bool met = false;
 #pragma unroll
             for (int q = 0; q < RES_WE; q++) met = met || se[q] == w;
-            const uint64_t voided = __ballot(lane > g && met);
+            uint64_t voided = __ballot(lane > g && met);
+            // ... and the chained decisions that assumed a voided pod's commit
+            for (;;) {
+              const uint64_t nx = __ballot(lane > g && ((ok >> lane) & 1ull) && !((voided >> lane) & 1ull) &&
+                                           (mydep & voided) != 0ull);
+              if (!nx) break;
+              voided |= nx;
+            }
             if (dbg) n_void += __popcll(ok & voided);
             ok &= ~voided;
           }
@@ -2912,6 +3118,9 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[59], (unsigned long long)c_gc[1]);
     atomicAdd((unsigned long long *)&dbg[60], (unsigned long long)c_gc[2]);
     atomicAdd((unsigned long long *)&dbg[61], (unsigned long long)n_ghit);
+    atomicAdd((unsigned long long *)&dbg[62], (unsigned long long)c_chain);
+    atomicAdd((unsigned long long *)&dbg[30], (unsigned long long)c_ext);
+    atomicAdd((unsigned long long *)&dbg[31], (unsigned long long)n_ext);
   }
 }
 

@@ -21,8 +21,13 @@ static __device__ __forceinline__ uint64_t stamp() {
 //              after a separate merge)
 //   res_round  rounds resolved + written back (k_resolve, release store)
 //   err        a side gave up waiting (watchdog): the call fails, nothing hangs
+//   ext_req    device pods placed inside the pipeline (k_ext_worker, seq.hip):
+//              the resolve stores pod index + 1 once every earlier commit is
+//              written back (write-through, drained)
+//   ext_done   the worker stores pod index + 1 once that pod's placement and
+//              its DeviceShare Reserve are published (out_node write-through)
 struct PipeSync {
-  int32_t sel[2], res_round, err;
+  int32_t sel[2], res_round, err, ext_req, ext_done;
 };
 
 constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up

@@ -36,6 +36,7 @@
 
 #include "dev.hpp"
 #include "ipa.hpp"
+#include "pipe.hpp"
 #include "pts.hpp"
 #include "seq.h"
 
@@ -205,7 +206,9 @@ __device__ __forceinline__ bool sweep(const uint64_t *g, uint32_t epoch, uint32_
 // DeviceShare and the extended scalars); rc: 0, or KOORDHIP_RESERVE_FAILED
 // (nothing committed).  nf: the feasible node count (one: no PreScore, so no
 // reservation is nominated before the NodeNUMAResource / DeviceShare Reserve).
-template <int SM>
+// ROW false (k_ext_worker): the Fit / LoadAware row is the pipelined
+// resolve's, which applies that delta itself -- everything else here.
+template <int SM, bool ROW = true>
 __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNodes &d, const DevPod &p,
                                                    const DevPodX &x, int32_t w, int32_t nf, bool rs,
                                                    uint64_t *cpus_out, uint32_t *dev_out) {
@@ -226,7 +229,7 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   // with the device rows' instead of one per structure): the Fit / LoadAware
   // row and the extended scalars' Requested
   NV v;
-  load_row(v, d, w);
+  if constexpr (ROW) load_row(v, d, w);
   int64_t xr[KOORDHIP_NXRES];
 #pragma unroll
   for (int j = 0; j < KOORDHIP_NXRES; j++) xr[j] = ((x.xmask >> j) & 1u) ? d.dv.xreq[(size_t)j * d.n + w] : 0;
@@ -247,8 +250,10 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
     resv_assume(rv, p, m);
     store_resv(rv, d.rv, w);
   }
-  apply_delta(v, p, +1);
-  store_row(v, d, w);
+  if constexpr (ROW) {
+    apply_delta(v, p, +1);
+    store_row(v, d, w);
+  }
   if (x.xmask)
 #pragma unroll
     for (int j = 0; j < KOORDHIP_NXRES; j++)
@@ -419,6 +424,149 @@ __device__ __forceinline__ void seq_block_reduce(int32_t v4[4], uint64_t &key, i
     for (int e = 1; e < 4; e++) v4[e] = max(v4[e], s_red[w][e]);
     key = s_key[w] > key ? s_key[w] : key;
   }
+}
+
+// ---- device pods inside the pipelined greedy (koordhip_place_staged, a
+// DeviceShare profile whose staged batch holds a few device pods among pods
+// without ext content).  The pipelined resolve places every other pod; at a
+// device pod (KH_POD_EXT) it writes every commit so far back, stores
+// sync->ext_req = pod + 1 and waits.  This persistent grid then runs that
+// pod's reference cycle on the exact state: every node's Filter and
+// per-node total, DeviceShare's raw Score (0 .. 100 per requested type,
+// scoring.go:33-72) and the normalization over the feasible nodes
+// (DefaultNormalizeScore, scoring.go:78-80).  The normalized total of a node
+// is its per-node total + w * norm(raw), so the winner is among the best
+// (total, lowest index) node of each raw value: every workgroup folds its
+// nodes into a [EXT_RAW] table of such keys in LDS, merges it into the global
+// one with agent-scope atomic max, and the last workgroup to arrive takes the
+// maximum raw value, ranks the <= EXT_RAW candidates, runs DeviceShare's
+// Reserve (device choice + deviceUsed, the extended scalars; not the Fit /
+// LoadAware row, which the resolve commits in its own copy) and stores
+// out_node / out_dev write-through, then ext_done = pod + 1.  No grid-wide
+// barrier: the workgroups need not be co-resident.
+constexpr int EXT_RAW = 320;  // raw DeviceShare scores 0 .. 300 (three device types x 100)
+constexpr int EXT_THREADS = 256;
+
+template <int SM>
+__global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
+                                                            const DevPodX *__restrict__ podx,
+                                                            const int32_t *__restrict__ ext_idx, int32_t n_ext,
+                                                            uint64_t *__restrict__ tab, uint32_t *__restrict__ arrive,
+                                                            int32_t *__restrict__ out_node, uint32_t *__restrict__ out_dev,
+                                                            PipeSync *sy) {
+  __shared__ uint64_t lt[EXT_RAW];
+  __shared__ int32_t s_red[SEQ_THREADS / 64][8];
+  __shared__ uint64_t s_key[SEQ_THREADS / 64];
+  __shared__ int32_t s_go, s_last;
+  const int t = threadIdx.x;
+  const int32_t G = gridDim.x, b = blockIdx.x;
+  const int32_t wdev = (c.score & KOORDHIP_PLUGIN_DEVICESHARE) ? c.w_ext[0] : 0;
+  const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+  for (int32_t e = 0; e < n_ext; e++) {
+    const int32_t gp = ext_idx[e];
+    for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
+    if (t == 0) s_go = wait_at_least(&sy->ext_req, gp + 1, sy) ? 1 : 0;
+    __syncthreads();
+    if (!s_go) return;  // the pipeline gave up (block-uniform)
+    const DevPod &p = pods[gp];
+    const DevPodX &x = podx[gp];
+    for (int32_t i = b * EXT_THREADS + t; i < d.n; i += G * EXT_THREADS) {
+      int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
+      const int32_t tk = seq_eval<SM>(c, d, p, x, i, false, raw, nullptr);
+      if (tk >= 0) atomicMax(&lt[min(max(raw[0], 0), EXT_RAW - 1)], make_key(tk, i));
+    }
+    __syncthreads();
+    for (int r = t; r < EXT_RAW; r += EXT_THREADS)
+      if (lt[r]) __hip_atomic_fetch_max(&tab[r], lt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old + 1 == (uint32_t)G;
+      if (s_last) {
+        __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+    }
+    __syncthreads();
+    if (!s_last) continue;  // block-uniform
+    // ---- the last workgroup: maximum raw over the feasible nodes, then the winner
+    uint64_t v[2];
+    int32_t v4[4] = {0, -1, 0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int r = t + h * EXT_THREADS;
+      v[h] = r < EXT_RAW ? __hip_atomic_load(&tab[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      if (v[h]) v4[1] = r;
+      if (r < EXT_RAW) __hip_atomic_store(&tab[r], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next pod's
+    }
+    uint64_t kk = 0;
+    seq_block_reduce(v4, kk, s_red, s_key, t);
+    const int32_t mx = max(v4[1], 0);
+    uint64_t best = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+      if (v[h]) {
+        const uint64_t k2 = v[h] + ((uint64_t)(uint32_t)(wdev * norm_score(t + h * EXT_THREADS, mx, false)) << 32);
+        best = k2 > best ? k2 : best;
+      }
+    v4[0] = v4[1] = v4[2] = v4[3] = 0;
+    seq_block_reduce(v4, best, s_red, s_key, t);
+    if (t == 0) {
+      uint32_t slots[DT] = {0u, 0u, 0u};
+      int32_t res = KOORDHIP_UNSCHEDULABLE;
+      if (best) {
+        const int32_t w = key_node(best);
+        // (nf 2: SM 0 has no Reservation PreScore to skip)
+        res = seq_commit_body<SM, false>(c, d, p, x, w, 2, false, nullptr, dev ? slots : nullptr) ? KOORDHIP_RESERVE_FAILED
+                                                                                                     : w;
+        if (res < 0) slots[0] = slots[1] = slots[2] = 0u;
+      }
+      if (out_dev)
+        for (int q = 0; q < DT; q++) st_wt(&out_dev[(size_t)gp * DT + q], slots[q]);
+      st_wt(&out_node[gp], res);
+    }
+    // every lane's table reset and the commit's stores, then the hand-off
+    // (release: the device rows and extended scalars, plain stores, are read
+    // by the next device pod's workgroups on other XCDs)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) store_release(&sy->ext_done, gp + 1);
+  }
+}
+
+// pods[idx[j]].flags |= KH_POD_EXT
+__global__ void k_mark_ext(DevPod *pods, const int32_t *__restrict__ idx, int32_t n) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) pods[idx[j]].flags |= KH_POD_EXT;
+}
+
+hipError_t launch_mark_ext(DevPod *pods, const int32_t *idx, int32_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mark_ext, dim3((n + 255) / 256), dim3(256), 0, s, pods, idx, n);
+  return hipGetLastError();
+}
+
+int32_t ext_worker_grid(int32_t n_cu, int32_t n) {
+  // about two nodes per thread, at most half the CUs (the class lists' and
+  // the resolve's persistent workgroups hold the others' LDS)
+  const int32_t want = (n + 2 * EXT_THREADS - 1) / (2 * EXT_THREADS);
+  return std::max(1, std::min(want, std::max(1, n_cu / 2 - 2)));
+}
+
+size_t ext_worker_scratch_bytes() { return (size_t)EXT_RAW * sizeof(uint64_t) + 64; }
+
+hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx,
+                             const int32_t *ext_idx, int32_t n_ext, int32_t grid, void *scratch, int32_t *out_node,
+                             uint32_t *out_dev, PipeSync *sync, hipStream_t s) {
+  if (n_ext <= 0) return hipSuccess;
+  if (seq_mode(c) != 0) return hipErrorInvalidValue;  // the plain build only (the route checks it)
+  uint64_t *tab = static_cast<uint64_t *>(scratch);
+  uint32_t *arrive = reinterpret_cast<uint32_t *>(tab + EXT_RAW);
+  if (hipError_t e = hipMemsetAsync(scratch, 0, ext_worker_scratch_bytes(), s)) return e;
+  hipLaunchKernelGGL(k_ext_worker<0>, dim3(grid), dim3(EXT_THREADS), 0, s, c, d, pods, podx, ext_idx, n_ext, tab, arrive,
+                     out_node, out_dev, sync);
+  return hipGetLastError();
 }
 
 // Every block's granules of one phase: (sum, max, max, max) of words 0..3 and

@@ -47,10 +47,11 @@ def _engine(prof):
     return PlacementEngine(prof, device=0)
 
 
-def _compare_stream(prof, t, pods, ext, cpusets=False):
+def _compare_stream(prof, t, pods, ext, cpusets=False, names=False):
     with _engine(prof) as e:
         e.load_snapshot(t)
         got = e.place_stream_ext(pods, ext)
+        kn = e.kernel_names()
         gdev = e.fetch_devices(len(pods))
         gst = e.read_nodes()
         gdv = e.read_devices()
@@ -70,7 +71,7 @@ def _compare_stream(prof, t, pods, ext, cpusets=False):
     assert np.array_equal(gdv["xrequested"], ods["xrequested"])
     if cpusets:
         assert np.array_equal(gcs, rcs)
-    return got
+    return (got, kn) if names else got
 
 
 def test_eval_ext_parity_deviceshare():
@@ -86,14 +87,68 @@ def test_eval_ext_parity_deviceshare():
     assert np.array_equal(g["topk"], r["topk"])
 
 
+@pytest.mark.parametrize("route", ["pipelined", "sequential"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_stream_deviceshare_fit_loadaware(seed):
+def test_stream_deviceshare_fit_loadaware(seed, route, monkeypatch):
+    """Device pods among plain pods: placed inside the pipelined greedy (the
+    resolve hands each one to k_ext_worker on the exact state), or the whole
+    batch in the sequential cycle (KOORDHIP_EXT_SEQ) -- the same placements."""
+    if route == "sequential":
+        monkeypatch.setenv("KOORDHIP_EXT_SEQ", "1")
     prof = with_deviceshare(shipped_profile())
     t = _cluster(1500, prof, seed=synth.SEED + seed)
     pods, ext = _pods(2500, prof, seed=synth.SEED + seed)
-    got = _compare_stream(prof, t, pods, ext)
+    got, kn = _compare_stream(prof, t, pods, ext, names=True)
+    assert ("k_resolve" in kn["resolve"]) == (route == "pipelined"), kn
     dev = (ext["flags"] & abi.PODX_DEVICE) != 0
     assert (got[dev] >= 0).sum() > 50   # device pods do land (and take devices)
+
+
+@pytest.mark.parametrize("mode", ["default", "lag1_split", "one_stream"])
+def test_stream_device_pods_in_pipeline_low_fraction(mode, monkeypatch):
+    """config4dsmix's shape at test size: 2 % device pods among plain pods (the
+    class lists on), plus the lag-1 split-select and one-evaluation-stream
+    pipelines; placements, device slots, deviceUsed, the extended scalars and
+    the node rows bit-exact with the oracle."""
+    if mode == "lag1_split":
+        monkeypatch.setenv("KOORDHIP_LAG1", "1")
+        monkeypatch.setenv("KOORDHIP_CLS_OFF", "1")
+    elif mode == "one_stream":
+        monkeypatch.setenv("KOORDHIP_ONE_EVAL_STREAM", "1")
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(3000, prof, seed=synth.SEED + 11)
+    pods, ext = _pods(6000, prof, seed=synth.SEED + 11, dev_frac=0.02)
+    got, kn = _compare_stream(prof, t, pods, ext, names=True)
+    assert "k_resolve" in kn["resolve"], kn
+    dev = (ext["flags"] & abi.PODX_DEVICE) != 0
+    assert dev.sum() > 60 and (got[dev] >= 0).sum() > 30
+
+
+def test_stream_device_pods_in_pipeline_edge_cases():
+    """Every pod a device pod, runs of consecutive device pods, device pods at
+    round starts / ends, extended-scalar-only pods (xmask without a device
+    request) and device pods no node can take (UNSCHEDULABLE)."""
+    prof = with_deviceshare(shipped_profile())
+    t = _cluster(800, prof, seed=synth.SEED + 13, gpu_frac=0.2)
+    # all device pods: the worker places every pod
+    pods, ext = _pods(400, prof, seed=synth.SEED + 13, dev_frac=1.0)
+    _compare_stream(prof, t, pods, ext)
+    # runs and round boundaries (24-pod rounds), xmask-only pods, oversized requests
+    pods, ext = _pods(1200, prof, seed=synth.SEED + 14, dev_frac=0.0)
+    _, full = _pods(1200, prof, seed=synth.SEED + 15, dev_frac=1.0)
+    sel = np.zeros(1200, bool)
+    sel[[0, 23, 24, 25, 26, 47, 95, 96, 500]] = True
+    sel[600:640] = True                       # a run over two round boundaries
+    sel[np.arange(700, 1200, 37)] = True
+    ext[sel] = full[sel]
+    xonly = np.flatnonzero(sel)[::5]
+    ext["flags"][xonly] = 0                    # extended scalars only: the Fit of xrequested
+    ext["dev_req"][xonly] = 0
+    big = np.flatnonzero(sel)[1::7]
+    ext["dev_req"][big, abi.DEV_GPU, 0] = 800  # eight whole GPUs: fits only the 8-GPU nodes' free ones
+    ext["dev_req"][big, abi.DEV_GPU, 1] = 800
+    got, kn = _compare_stream(prof, t, pods, ext, names=True)
+    assert "k_resolve" in kn["resolve"], kn
 
 
 def test_stream_deviceshare_most_allocated():
