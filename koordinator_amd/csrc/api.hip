@@ -155,6 +155,7 @@ struct koordhip_ctx {
   hipEvent_t ev_res[kRing] = {}, ev_start = nullptr;
   bool pipe_check = false;       // a place call ran: check PipeSync.err when it completes
   bool pipe_err = false;         // ... and it had stalled (sticky until the next place call)
+  int32_t pipe_errc = 0;         // ... PipeSync.err's code (0: the sequential cycle's timeout)
   kh::DevPod *d_tmp_pod = nullptr;
   kh::DevPodX *d_tmp_podx = nullptr;  // koordhip_commit_ext's record
   void *d_upd = nullptr;           // koordhip_update_nodes staging (grown, kept)
@@ -202,12 +203,15 @@ struct koordhip_ctx {
   // extended-scalar requests only (no spread constraint or count, no affinity
   // entry); their DevPods carry KH_POD_EXT
   bool staged_ext_dev = false;
-  std::vector<int32_t> ext_idx;
+  std::vector<int32_t> ext_idx, ext_needc;
   int32_t *d_ext_idx = nullptr;
   int32_t ext_idx_cap = 0;
-  void *d_ext_scr = nullptr;        // k_ext_worker's table and arrival counter
-  hipStream_t xstream = nullptr;    // its stream (a dedicated queue: the worker spins on the resolve's flag)
-  hipEvent_t ev_ext = nullptr;
+  void *d_ext_scr = nullptr;        // k_ext_worker's table and per-pod chunk counters
+  size_t ext_scr_cap = 0;
+  hipStream_t xstream = nullptr;    // its stream (a dedicated queue: the worker spins on the resolve's flag;
+                                    // every fourth CU)
+  hipStream_t cstream = nullptr;    // the class lists' stream beside it (the other CUs)
+  hipEvent_t ev_ext = nullptr, ev_cls = nullptr;
   bool last_ext_pipe = false;       // the last place call placed device pods inside the pipeline
   // class-incremental lists (cls.hip): the staged pods' classes (byte-identical
   // device records), the class buffers and the plan of the staged batch
@@ -1187,11 +1191,13 @@ int koordhip_destroy(koordhip_ctx *c) {
     (void)hipStreamDestroy(c->stream2);
   }
   if (c->ev_eval2) (void)hipEventDestroy(c->ev_eval2);
-  if (c->xstream) {
-    (void)hipStreamSynchronize(c->xstream);
-    (void)hipStreamDestroy(c->xstream);
-  }
-  if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
+  for (hipStream_t x : {c->xstream, c->cstream})
+    if (x) {
+      (void)hipStreamSynchronize(x);
+      (void)hipStreamDestroy(x);
+    }
+  for (hipEvent_t e : {c->ev_ext, c->ev_cls})
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
@@ -1987,10 +1993,10 @@ static int stage_ext(koordhip_ctx *c, const koordhip_pod_ext *ext, int32_t n_pod
   HIP_TRY(hipMemcpyAsync(c->d_podx, ext, (size_t)n_pods * sizeof(kh::DevPodX), hipMemcpyHostToDevice, c->stream));
   if (devonly && !c->ext_idx.empty()) {
     const int32_t ne = (int32_t)c->ext_idx.size();
-    if (ne > c->ext_idx_cap) {
+    if (ne > c->ext_idx_cap) {  // [ext_idx | needc] (needc: per place call, for its P / lag)
       if (c->d_ext_idx) HIP_TRY(hipFree(c->d_ext_idx));
       c->d_ext_idx = nullptr;
-      HIP_TRY(hipMalloc(&c->d_ext_idx, (size_t)ne * sizeof(int32_t)));
+      HIP_TRY(hipMalloc(&c->d_ext_idx, (size_t)2 * ne * sizeof(int32_t)));
       c->ext_idx_cap = ne;
     }
     HIP_TRY(hipMemcpyAsync(c->d_ext_idx, c->ext_idx.data(), (size_t)ne * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
@@ -2503,6 +2509,7 @@ static int cls_build(koordhip_ctx *c, const koordhip_ctx::ClsBuild &b, kh::PipeS
 int place_staged_impl(koordhip_ctx *c) {
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
   c->pipe_err = false;
+  c->pipe_errc = 0;
   c->pipe_check = false;
   HIP_TRY(hipSetDevice(c->device));
   // the sequential cycle: a snapshot or profile that needs it, a reserve pod in
@@ -2540,11 +2547,29 @@ int place_staged_impl(koordhip_ctx *c) {
   if (ext_pipe) {  // (allocations before the persistent launches: one later could wait behind them)
     if (!c->d_devout && c->pods_cap > 0)
       HIP_TRY(hipMalloc(&c->d_devout, (size_t)c->pods_cap * KOORDHIP_DEV_TYPES * sizeof(uint32_t)));
-    if (!c->d_ext_scr) HIP_TRY(hipMalloc(&c->d_ext_scr, kh::ext_worker_scratch_bytes()));
+    const size_t xb = kh::ext_worker_scratch_bytes((int32_t)c->ext_idx.size(), c->n);
+    if (xb > c->ext_scr_cap) {
+      if (c->d_ext_scr) HIP_TRY(hipFree(c->d_ext_scr));
+      c->d_ext_scr = nullptr;
+      HIP_TRY(hipMalloc(&c->d_ext_scr, xb));
+      c->ext_scr_cap = xb;
+    }
     if (!c->xstream) {
+      // The worker's persistent workgroups and the class lists' must never
+      // starve each other of CUs (each waits on the other through the
+      // resolve): the worker runs on every fourth CU, the class lists on the
+      // others (the resolve and the builds anywhere)
       const std::vector<uint32_t> all = full_cu_mask(c);
-      HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)all.size(), all.data()));
+      std::vector<uint32_t> wm(all.size(), 0u), cm = all;
+      for (int32_t i = 3; i < c->n_cu; i += 4) {
+        wm[i >> 5] |= 1u << (i & 31);
+        cm[i >> 5] &= ~(1u << (i & 31));
+      }
+      if (std::getenv("KOORDHIP_EXT_NOMASK")) wm = cm = all;  // (A/B)
+      HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)wm.size(), wm.data()));
+      HIP_TRY(hipExtStreamCreateWithCUMask(&c->cstream, (uint32_t)cm.size(), cm.data()));
       HIP_TRY(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&c->ev_cls, hipEventDisableTiming));
     }
   }
   // the pipelined greedy allocates no device but the device pods' (k_ext_worker):
@@ -2729,22 +2754,42 @@ int place_staged_impl(koordhip_ctx *c) {
     // the device pods' worker: one persistent launch on its own queue, after
     // the call's PipeSync / device-slot resets (ev_start)
     HIP_TRY(hipStreamWaitEvent(c->xstream, c->ev_start, 0));
-    HIP_TRY(kh::launch_ext_worker(c->dc, c->d, c->d_pods, c->d_podx, c->d_ext_idx, (int32_t)c->ext_idx.size(),
-                                  kh::ext_worker_grid(c->n_cu, c->n), c->d_ext_scr, c->d_out, c->d_devout, sync,
-                                  c->xstream));
+    // needc[e]: the device pods of the rounds before round(e) - lag, whose
+    // device commits device pod e's pre-evaluation must see (later ones' nodes
+    // are in the resolve's X set at e's hand-off)
+    const int32_t ne = (int32_t)c->ext_idx.size();
+    c->ext_needc.assign(ne, 0);
+    for (int32_t e = 0, q = 0; e < ne; e++) {
+      const int32_t ue = c->ext_idx[e] / P;
+      while (q < e && c->ext_idx[q] / P < ue - lag) q++;
+      c->ext_needc[e] = q;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_ext_idx + ne, c->ext_needc.data(), (size_t)ne * sizeof(int32_t), hipMemcpyHostToDevice,
+                           c->xstream));
+    HIP_TRY(kh::launch_ext_worker(c->dc, c->d, c->d_pods, c->d_podx, c->d_ext_idx, c->d_ext_idx + ne, ne, P, lag,
+                                  c->n_cu, c->d_ext_scr, c->d_out, c->d_devout, sync,
+                                  c->d_dbg, c->xstream));
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
   }
   if (cls && rounds > 0) {
     // ONE persistent workgroup per class for the whole stream (c->stream), the
     // builds on the second stream, all enqueued now (each build waits for its
     // state's round on the device)
+    // (beside the device-pod worker: on the CUs it leaves, cstream)
+    const bool use_cs = ext_pipe && !std::getenv("KOORDHIP_EXT_NOCSTREAM");
+    hipStream_t cs = use_cs ? c->cstream : c->stream;
+    if (use_cs) HIP_TRY(hipStreamWaitEvent(cs, c->ev_start, 0));
     int32_t tm = -1;
-    if (int e = timed_begin(c, TK_SCAN, c->stream, &tm)) return e;
+    if (int e = timed_begin(c, TK_SCAN, cs, &tm)) return e;
     HIP_TRY(kh::launch_cls_run(c->dc, c->d, c->d_cls_pod, (int32_t)c->cls_rep.size(), c->d_plan + c->plan_off[0],
                                c->d_plan + c->plan_off[1], c->d_plan + c->plan_off[2], c->d_pod_cls, c->d_out, lag, P,
                                total, c->d_cls_buf, c->d_cls_meta, K, c->monotone, c->d_lists, list_buf,
-                               cls_sync(c, sync), c->d_dbg ? c->d_dbg + 64 : nullptr, c->stream));
-    if (int e = timed_end(c, tm, c->stream)) return e;
+                               cls_sync(c, sync), c->d_dbg ? c->d_dbg + 64 : nullptr, cs));
+    if (int e = timed_end(c, tm, cs)) return e;
+    if (use_cs) {
+      HIP_TRY(hipEventRecord(c->ev_cls, cs));
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_cls, 0));
+    }
     for (const koordhip_ctx::ClsBuild &b : c->plan_builds)
       if (int e = cls_build(c, b, sync, c->stream2, b.u % tstride == 0)) return e;
     c->eval_kernel = kh::cls_run_kernel_name(c->dc);
@@ -2857,10 +2902,19 @@ int place_staged_impl(koordhip_ctx *c) {
     }
     std::fprintf(stderr, "[koordhip stamps] chained decisions: %llu cycles, %llu pods resolved\n",
                  (unsigned long long)h[62], (unsigned long long)h[63]);
-    if (ext_pipe)
+    if (ext_pipe) {
+      uint64_t q[8], q8[2] = {0, 0};
+      HIP_TRY(hipMemcpy(q, c->d_dbg + 80, sizeof(q), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(q8, c->d_dbg + 88, sizeof(q8), hipMemcpyDeviceToHost));
+      const double np = (double)std::max<uint64_t>(q[6], 1);
       std::fprintf(stderr, "[koordhip stamps] device pods (k_ext_worker): %llu, resolve cycles from the hand-off to the "
-                   "answer %llu (%.0f per pod)\n", (unsigned long long)h[31], (unsigned long long)h[30],
-                   h[31] ? (double)h[30] / h[31] : 0.0);
+                   "answer %llu (%.0f per pod) | worker per pod: workgroup 0 waiting %.0f  evaluating %.0f  merge + "
+                   "arrival %.0f (chunks %.2f) | pre-evaluation workgroup: waiting %.0f  evaluating %.0f | last "
+                   "workgroup reduce %.0f  publish %.0f  device commit (after the hand-off) %.0f\n",
+                   (unsigned long long)h[31], (unsigned long long)h[30], h[31] ? (double)h[30] / h[31] : 0.0,
+                   q[0] / np, q[1] / np, q[2] / np, q[7] / np, (double)q8[1] / np, (double)q8[0] / np, q[3] / np,
+                   q[5] / np, q[4] / np);
+    }
     std::fprintf(stderr, "[koordhip stamps] general commit split: row source %llu  Reserve delta %llu  voiding + "
                  "outputs %llu cycles | winners already in M %llu\n",
                  (unsigned long long)h[58], (unsigned long long)h[59], (unsigned long long)h[60],
@@ -2872,9 +2926,18 @@ int place_staged_impl(koordhip_ctx *c) {
 // After a place call: did either side of the pipeline give up waiting?  The
 // error is sticky until the next place call: every later fetch / stats call
 // of this stream reports it.
+static const char *pipe_msg(int32_t err) {
+  switch (err) {
+    case 2: return "class lists underflowed (fewer than k keys above a build's boundary): placements are incomplete";
+    case 4: return "a device pod's DeviceShare Reserve failed where its Filter passed (k_ext_worker): placements are "
+                   "incomplete";
+    default: return "round pipeline stalled (watchdog): placements are incomplete";
+  }
+}
+
 int pipe_status(koordhip_ctx *c) {
   static const char *kStall = "round pipeline stalled (watchdog): placements are incomplete";
-  if (c->pipe_err) return fail(KOORDHIP_EDEVICE, kStall);
+  if (c->pipe_err) return fail(KOORDHIP_EDEVICE, c->pipe_errc ? pipe_msg(c->pipe_errc) : kStall);
   if (c->last_seq && c->pipe_check && c->d_seqg) {  // the sequential cycle's spin timeout word
     c->pipe_check = false;
     uint32_t tmo = 0;
@@ -2893,7 +2956,16 @@ int pipe_status(koordhip_ctx *c) {
   HIP_TRY(hipMemcpy(&err, reinterpret_cast<int32_t *>(sync) + kh::kPipeSyncErrWord, sizeof(err), hipMemcpyDeviceToHost));
   if (err) {
     c->pipe_err = true;
-    return fail(KOORDHIP_EDEVICE, kStall);
+    c->pipe_errc = err;
+    if (c->last_ext_pipe && c->d_ext_scr) {  // where the pipeline stood (device pods inside it)
+      int32_t sw[6] = {0, 0, 0, 0, 0, 0}, xd = 0;
+      HIP_TRY(hipMemcpy(sw, sync, sizeof(sw), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(&xd, static_cast<char *>(c->d_ext_scr) + kh::ext_worker_diag_offset((int32_t)c->ext_idx.size()),
+                        sizeof(xd), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[koordhip] pipeline error %d: sel %d/%d res_round %d ext_req %d ext_done %d | device-pod "
+                   "worker failed at device pod %d phase %d\n", err, sw[0], sw[1], sw[2], sw[4], sw[5], xd >> 4, xd & 15);
+    }
+    return fail(KOORDHIP_EDEVICE, pipe_msg(err));
   }
   return 0;
 }

@@ -273,6 +273,9 @@ __device__ __forceinline__ bool dev_reserve(const DevCfg &c, const DevDev &dv, c
   return any || !present || !nominated;
 }
 
+// WT: write-through stores (k_ext_worker: read next on other XCDs after a
+// relaxed hand-off, no L2 write-back fence)
+template <bool WT = false>
 __device__ __forceinline__ void dev_apply(const DevDev &dv, int32_t i, const uint32_t slots[DT],
                                           const int64_t per_t[DT][DR]) {
   for (int t = 0; t < DT; t++) {
@@ -288,7 +291,12 @@ __device__ __forceinline__ void dev_apply(const DevDev &dv, int32_t i, const uin
     for (int s = 0; s < DS; s++)
       if ((slots[t] >> s) & 1u)
 #pragma unroll
-        for (int r = 0; r < DR; r++) dv.used[a0 + (size_t)s * DR + r] = u[s][r] + per_t[t][r];
+        for (int r = 0; r < DR; r++) {
+          if constexpr (WT)
+            st_wt(&dv.used[a0 + (size_t)s * DR + r], (int64_t)(u[s][r] + per_t[t][r]));
+          else
+            dv.used[a0 + (size_t)s * DR + r] = u[s][r] + per_t[t][r];
+        }
   }
 }
 

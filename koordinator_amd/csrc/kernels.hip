@@ -2591,7 +2591,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         const DevPod pod = lpod[g];  // VGPR copy: SGPRs are the scarce register file here (uniform_pod measured slower)
         // A device pod (KH_POD_EXT, plain build): k_ext_worker places it on the
         // exact state -- every commit so far written back first (M rows,
-        // write-through, drained), then the hand-off; its node (or
+        // write-through, drained) and X exported, then the hand-off; its node (or
         // UNSCHEDULABLE / RESERVE_FAILED) comes back through out_node, and the
         // Fit / LoadAware delta is committed below like any general-path pod's.
         bool ext_pod = false;
@@ -2604,6 +2604,12 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             const NV v = slot_row(mrow[lane]);
             mrow[lane] = v;
             store_row_wt(v, nodes(), my_node);
+          }
+          {  // X = M' + this round's M so far: the nodes the worker evaluates again
+            int32_t *xl = pipe_xlist(sy);
+            if (lane < mp) st_wt(&xl[1 + lane], pnode[lane]);
+            if (lane < nm) st_wt(&xl[1 + mp + lane], my_node);
+            if (lane == 0) st_wt(&xl[0], mp + nm);
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           int32_t xr = KOORDHIP_UNSCHEDULABLE;

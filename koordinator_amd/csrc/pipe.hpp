@@ -29,6 +29,11 @@ static __device__ __forceinline__ uint64_t stamp() {
 struct PipeSync {
   int32_t sel[2], res_round, err, ext_req, ext_done;
 };
+// After the struct: the resolve's X set at a device-pod hand-off, {count,
+// nodes[kPipeXMax]} (M' and this round's M so far), stored write-through
+// before ext_req.
+constexpr int kPipeXMax = 128;
+static __device__ __forceinline__ int32_t *pipe_xlist(PipeSync *sy) { return reinterpret_cast<int32_t *>(sy + 1); }
 
 constexpr uint64_t PIPE_WATCHDOG = 8ull << 30;  // s_memtime ticks (~seconds) before a waiter gives up
 

@@ -245,7 +245,7 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
       store_numa_row(r, d, w);
     }
   }
-  if (dev) dev_apply(d.dv, w, slots, per);
+  if (dev) dev_apply<!ROW>(d.dv, w, slots, per);
   if constexpr (SM >= 2) {  // Reservation Reserve: assumePod into the nominated reservation
     resv_assume(rv, p, m);
     store_resv(rv, d.rv, w);
@@ -257,7 +257,12 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   if (x.xmask)
 #pragma unroll
     for (int j = 0; j < KOORDHIP_NXRES; j++)
-      if ((x.xmask >> j) & 1u) d.dv.xreq[(size_t)j * d.n + w] = xr[j] + x.xreq[j];
+      if ((x.xmask >> j) & 1u) {
+        if constexpr (ROW)
+          d.dv.xreq[(size_t)j * d.n + w] = xr[j] + x.xreq[j];
+        else
+          st_wt(&d.dv.xreq[(size_t)j * d.n + w], (int64_t)(xr[j] + x.xreq[j]));
+      }
   if (cpus_out)
     for (int q = 0; q < NW; q++) cpus_out[q] = m[q];
   if (dev_out)
@@ -429,68 +434,219 @@ __device__ __forceinline__ void seq_block_reduce(int32_t v4[4], uint64_t &key, i
 // ---- device pods inside the pipelined greedy (koordhip_place_staged, a
 // DeviceShare profile whose staged batch holds a few device pods among pods
 // without ext content).  The pipelined resolve places every other pod; at a
-// device pod (KH_POD_EXT) it writes every commit so far back, stores
-// sync->ext_req = pod + 1 and waits.  This persistent grid then runs that
-// pod's reference cycle on the exact state: every node's Filter and
-// per-node total, DeviceShare's raw Score (0 .. 100 per requested type,
+// device pod (KH_POD_EXT) it writes every commit so far back, exports its X
+// set (the nodes committed since the state the round's lists were evaluated
+// on: M' and this round's M, pipe_xlist) and stores sync->ext_req = pod + 1.
+// This persistent grid runs that pod's reference cycle: every node's Filter
+// and per-node total, DeviceShare's raw Score (0 .. 100 per requested type,
 // scoring.go:33-72) and the normalization over the feasible nodes
-// (DefaultNormalizeScore, scoring.go:78-80).  The normalized total of a node
-// is its per-node total + w * norm(raw), so the winner is among the best
-// (total, lowest index) node of each raw value: every workgroup folds its
-// nodes into a [EXT_RAW] table of such keys in LDS, merges it into the global
-// one with agent-scope atomic max, and the last workgroup to arrive takes the
-// maximum raw value, ranks the <= EXT_RAW candidates, runs DeviceShare's
-// Reserve (device choice + deviceUsed, the extended scalars; not the Fit /
-// LoadAware row, which the resolve commits in its own copy) and stores
-// out_node / out_dev write-through, then ext_done = pod + 1.  No grid-wide
-// barrier: the workgroups need not be co-resident.
+// (DefaultNormalizeScore, scoring.go:78-80).
+//   pre-evaluation, off the critical path: as soon as the pod's round u may
+//     be evaluated (res_round >= u - lag, and the device commits of the device
+//     pods of the rounds before that are published), every node's key
+//     make_key(total, i) (0: infeasible) and raw score into pk / pr;
+//   final, at the hand-off: only the X nodes are evaluated again (every other
+//     node's row is the pre-evaluation's); the normalized total of a node is
+//     its total + w * norm(raw), so the winner is among the best (total,
+//     lowest index) node of each raw value: every workgroup folds its chunk
+//     into a [EXT_RAW] table of such keys in LDS and merges it into the global
+//     one with agent-scope atomic max; the workgroup finishing the last chunk
+//     takes the maximum raw value, ranks the <= EXT_RAW candidates, stores
+//     out_node write-through and ext_done = pod + 1, and only then runs
+//     DeviceShare's Reserve (device choice + deviceUsed, the extended scalars;
+//     not the Fit / LoadAware row, which the resolve commits in its own copy)
+//     and publishes it (cdone) for the next device pod.
+// Node chunks are claimed from per-pod counters, not assigned: whichever
+// workgroups are resident share the work (none waits for a workgroup the GPU
+// has not started -- its CUs may be held by persistent kernels that wait on
+// this pod).
 constexpr int EXT_RAW = 320;  // raw DeviceShare scores 0 .. 300 (three device types x 100)
 constexpr int EXT_THREADS = 256;
+constexpr int32_t EXT_PCHUNK = EXT_THREADS;      // pre-evaluation chunk: one node per thread
+constexpr int EXT_FNPT = 4;                      // final chunk: four nodes per thread (two loads each)
+constexpr int32_t EXT_FCHUNK = EXT_THREADS * EXT_FNPT;
+constexpr int EXT_CW = 8;     // counter words per device pod: claimed / finished chunks of both phases
+constexpr int EXT_RING = 4;   // pre-evaluation buffers: device pods evaluated ahead of their hand-off
 
+// Workgroups [0, gf) run the final phases, [gf, grid) the pre-evaluations,
+// which run up to EXT_RING device pods ahead.
 template <int SM>
 __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
                                                             const DevPodX *__restrict__ podx,
-                                                            const int32_t *__restrict__ ext_idx, int32_t n_ext,
-                                                            uint64_t *__restrict__ tab, uint32_t *__restrict__ arrive,
-                                                            int32_t *__restrict__ out_node, uint32_t *__restrict__ out_dev,
-                                                            PipeSync *sy) {
+                                                            const int32_t *__restrict__ ext_idx,
+                                                            const int32_t *__restrict__ needc, int32_t n_ext, int32_t P,
+                                                            int32_t lag, int32_t gf, uint64_t *__restrict__ tab,
+                                                            uint32_t *__restrict__ cnt, uint64_t *__restrict__ pk,
+                                                            int32_t *__restrict__ pr, int32_t *__restrict__ out_node,
+                                                            uint32_t *__restrict__ out_dev, PipeSync *sy, uint64_t *dbg) {
   __shared__ uint64_t lt[EXT_RAW];
+  __shared__ uint32_t xm[EXT_FCHUNK / 32];  // the chunk's X nodes
   __shared__ int32_t s_red[SEQ_THREADS / 64][8];
   __shared__ uint64_t s_key[SEQ_THREADS / 64];
-  __shared__ int32_t s_go, s_last;
+  __shared__ int32_t s_go, s_last, s_ch;
   const int t = threadIdx.x;
-  const int32_t G = gridDim.x, b = blockIdx.x;
+  const int32_t b = blockIdx.x;
+  const int32_t ncp = (d.n + EXT_PCHUNK - 1) / EXT_PCHUNK, ncf = (d.n + EXT_FCHUNK - 1) / EXT_FCHUNK;
+  int32_t *cdone = reinterpret_cast<int32_t *>(cnt + (size_t)EXT_CW * n_ext);  // device commits published
+  const int32_t *xl = pipe_xlist(sy);
   const int32_t wdev = (c.score & KOORDHIP_PLUGIN_DEVICESHARE) ? c.w_ext[0] : 0;
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
-  for (int32_t e = 0; e < n_ext; e++) {
+  const size_t nn = (size_t)max(d.n, 1);
+  // dbg (KOORDHIP_STAMPS): final workgroup 0's cycles waiting for the hand-off,
+  // final phase, merge + arrival [80..82], its final chunks [87]; pre-evaluation
+  // workgroup gf's cycles waiting [89] and evaluating [88]; the last final
+  // workgroup's reduce, device commit (after the hand-off), publish [83..85],
+  // pods [86]
+  uint64_t c_w = 0, c_e = 0, c_m = 0, c_r = 0, c_c = 0, c_p = 0, n_l = 0, n_ch = 0, c_pre = 0, c_pw = 0;
+  // claim chunks of a phase until none is left; f(chunk) per claimed chunk
+  auto claim_all = [&](uint32_t *claim, int32_t nch, auto f) -> int32_t {
+    int32_t done = 0;
+    for (;;) {
+      if (t == 0) s_ch = (int32_t)__hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int32_t ch = s_ch;
+      __syncthreads();
+      if (ch >= nch) return done;  // block-uniform
+      done++;
+      f(ch);
+    }
+  };
+  // the pre-evaluation chunks of device pod e this workgroup can claim: every
+  // node's key (0: infeasible) and raw score into the pod's ring buffer, then
+  // the chunks counted as finished
+  auto pre_eval = [&](int32_t e) {
     const int32_t gp = ext_idx[e];
-    for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
-    if (t == 0) s_go = wait_at_least(&sy->ext_req, gp + 1, sy) ? 1 : 0;
-    __syncthreads();
-    if (!s_go) return;  // the pipeline gave up (block-uniform)
+    uint32_t *cw = cnt + (size_t)EXT_CW * e;
     const DevPod &p = pods[gp];
     const DevPodX &x = podx[gp];
-    for (int32_t i = b * EXT_THREADS + t; i < d.n; i += G * EXT_THREADS) {
-      int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
-      const int32_t tk = seq_eval<SM>(c, d, p, x, i, false, raw, nullptr);
-      if (tk >= 0) atomicMax(&lt[min(max(raw[0], 0), EXT_RAW - 1)], make_key(tk, i));
-    }
-    __syncthreads();
-    for (int r = t; r < EXT_RAW; r += EXT_THREADS)
-      if (lt[r]) __hip_atomic_fetch_max(&tab[r], lt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t *bk = pk + (size_t)(e % EXT_RING) * nn;
+    int32_t *br = pr + (size_t)(e % EXT_RING) * nn;
+    const int32_t pdone = claim_all(cw, ncp, [&](int32_t ch) {
+      const int32_t i = ch * EXT_PCHUNK + t;
+      if (i < d.n) {
+        int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
+        const int32_t tk = seq_eval<SM>(c, d, p, x, i, false, raw, nullptr);
+        st_wt(&bk[i], (uint64_t)(tk >= 0 ? make_key(tk, i) : 0ull));
+        st_wt(&br[i], (int32_t)min(max(raw[0], 0), EXT_RAW - 1));
+      }
+    });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old + 1 == (uint32_t)G;
-      if (s_last) {
-        __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (t == 0 && pdone) __hip_atomic_fetch_add(cw + 1, (uint32_t)pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (b >= gf) {
+    // ---- pre-evaluations: device pod e on the state round u's lists see, as
+    //      soon as that state is written back (X covers everything later), the
+    //      device commits of the device pods before it are published, and its
+    //      ring buffer's previous pod has had its final phase
+    for (int32_t e = 0; e < n_ext; e++) {
+      const int32_t gp = ext_idx[e], u = gp / P;
+      uint32_t *cw = cnt + (size_t)EXT_CW * e;  // {pre claimed, pre finished, final claimed, final finished}
+      const uint64_t tp0 = dbg ? stamp() : 0;
+      if (t == 0)
+        s_go = ((u <= lag || wait_at_least(&sy->res_round, u - lag, sy)) && wait_at_least(cdone, needc[e], sy) &&
+                (e < EXT_RING || wait_at_least(&sy->ext_done, ext_idx[e - EXT_RING] + 1, sy)))
+                   ? 1
+                   : 0;
+      __syncthreads();
+      if (!s_go) {  // the pipeline gave up (block-uniform); the host reports where
+        if (t == 0) atomicMax(cdone + 1, (e << 4) | 1);
+        break;
+      }
+      const uint64_t tp1 = dbg ? stamp() : 0;
+      pre_eval(e);
+      if (dbg && b == gf) {
+        c_pw += tp1 - tp0;
+        c_pre += stamp() - tp1;
       }
     }
+    if (dbg && t == 0 && b == gf) {
+      atomicAdd((unsigned long long *)&dbg[88], (unsigned long long)c_pre);
+      atomicAdd((unsigned long long *)&dbg[89], (unsigned long long)c_pw);
+    }
+    return;
+  }
+  __builtin_amdgcn_s_setprio(2);  // the resolve waits on the final phases: ahead of the evaluation side's waves
+  for (int32_t e = 0; e < n_ext; e++) {
+    const int32_t gp = ext_idx[e];
+    uint32_t *cw = cnt + (size_t)EXT_CW * e;
+    const DevPod &p = pods[gp];
+    const DevPodX &x = podx[gp];
+    const uint64_t *bk = pk + (size_t)(e % EXT_RING) * nn;
+    const int32_t *br = pr + (size_t)(e % EXT_RING) * nn;
+    // ---- final: at the hand-off, the previous device pod's device commit and
+    //      this pod's pre-evaluation published
+    for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
+    const uint64_t t0 = dbg ? stamp() : 0;
+    if (t == 0) s_go = (wait_at_least(&sy->ext_req, gp + 1, sy) && wait_at_least(cdone, e, sy)) ? 1 : 0;
     __syncthreads();
+    // the pre-evaluation chunks nobody has claimed yet (every condition of the
+    // pre-evaluation holds at the hand-off): the final workgroups never wait
+    // for a pre-evaluation workgroup the GPU has not started
+    if (s_go) pre_eval(e);
+    if (t == 0 && s_go) s_go = wait_at_least(reinterpret_cast<const int32_t *>(cw + 1), ncp, sy) ? 1 : 0;
+    __syncthreads();
+    if (!s_go) {
+      if (t == 0) atomicMax(cdone + 1, (e << 4) | 2);
+      break;
+    }
+    const uint64_t t1 = dbg ? stamp() : 0;
+    const int32_t nx = xl[0];
+    const int32_t done = claim_all(cw + 2, ncf, [&](int32_t ch) {
+      const int32_t c0 = ch * EXT_FCHUNK;
+      for (int32_t w = t; w < EXT_FCHUNK / 32; w += EXT_THREADS) xm[w] = 0u;
+      __syncthreads();
+      for (int32_t q = t; q < nx; q += EXT_THREADS) {
+        const int32_t y = xl[1 + q] - c0;
+        if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
+      }
+      __syncthreads();
+      uint64_t kv[EXT_FNPT];
+      int32_t rv[EXT_FNPT];
+#pragma unroll
+      for (int k = 0; k < EXT_FNPT; k++) {  // the pre-evaluated values, all loads in flight
+        const int32_t i = c0 + k * EXT_THREADS + t;
+        kv[k] = i < d.n ? __hip_atomic_load(&bk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        rv[k] = i < d.n ? __hip_atomic_load(&br[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      }
+#pragma unroll 1
+      for (int k = 0; k < EXT_FNPT; k++) {
+        const int32_t y = k * EXT_THREADS + t, i = c0 + y;
+        if (i < d.n && ((xm[y >> 5] >> (y & 31)) & 1u)) {  // committed since the pre-evaluation: evaluate again
+          int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
+          const int32_t tk = seq_eval<SM>(c, d, p, x, i, false, raw, nullptr);
+          kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
+          rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < EXT_FNPT; k++)
+        if (kv[k]) atomicMax(&lt[rv[k]], kv[k]);
+      __syncthreads();  // (xm reused by the next chunk)
+    });
+    const uint64_t t2 = dbg ? stamp() : 0;
+    if (done) {
+      for (int r = t; r < EXT_RAW; r += EXT_THREADS)
+        if (lt[r]) __hip_atomic_fetch_max(&tab[r], lt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(cw + 3, (uint32_t)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old + (uint32_t)done == (uint32_t)ncf;
+        if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+    } else if (t == 0) {
+      s_last = 0;
+    }
+    __syncthreads();
+    const uint64_t t3 = dbg ? stamp() : 0;
+    if (dbg && b == 0) {
+      c_w += t1 - t0;
+      c_e += t2 - t1;
+      c_m += t3 - t2;
+      n_ch += done;
+    }
     if (!s_last) continue;  // block-uniform
-    // ---- the last workgroup: maximum raw over the feasible nodes, then the winner
     uint64_t v[2];
     int32_t v4[4] = {0, -1, 0, 0};
 #pragma unroll
@@ -512,26 +668,53 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
       }
     v4[0] = v4[1] = v4[2] = v4[3] = 0;
     seq_block_reduce(v4, best, s_red, s_key, t);
+    const uint64_t t4 = dbg ? stamp() : 0;
+    // The node goes back to the resolve first: in the plain build the Reserve
+    // cannot fail where the Filter passed on the same state (the same device
+    // rows: dev_reserve takes the best `wanted` of the devices dev_eval counted,
+    // the extended scalars only add), so the resolve continues while this
+    // workgroup commits the devices; the next device pod's workgroups wait for
+    // that commit (cdone).  A Reserve that fails anyway stops the pipeline
+    // (sync->err = 4) instead of diverging.
+    if (t == 0) st_wt(&out_node[gp], best ? key_node(best) : (int32_t)KOORDHIP_UNSCHEDULABLE);
+    // every lane's table reset and out_node, drained, then the relaxed hand-off
+    // (Guideline 16 R1: no L2 write-back fence)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint64_t t5 = dbg ? stamp() : 0;
     if (t == 0) {
+      __hip_atomic_store(&sy->ext_done, gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       uint32_t slots[DT] = {0u, 0u, 0u};
-      int32_t res = KOORDHIP_UNSCHEDULABLE;
       if (best) {
-        const int32_t w = key_node(best);
         // (nf 2: SM 0 has no Reservation PreScore to skip)
-        res = seq_commit_body<SM, false>(c, d, p, x, w, 2, false, nullptr, dev ? slots : nullptr) ? KOORDHIP_RESERVE_FAILED
-                                                                                                     : w;
-        if (res < 0) slots[0] = slots[1] = slots[2] = 0u;
+        if (seq_commit_body<SM, false>(c, d, p, x, key_node(best), 2, false, nullptr, dev ? slots : nullptr))
+          __hip_atomic_store(&sy->err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (out_dev)
         for (int q = 0; q < DT; q++) st_wt(&out_dev[(size_t)gp * DT + q], slots[q]);
-      st_wt(&out_node[gp], res);
+      // the device rows and extended scalars (write-through: read next by the
+      // next device pod's workgroups on other XCDs), drained, then cdone
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cdone, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // every lane's table reset and the commit's stores, then the hand-off
-    // (release: the device rows and extended scalars, plain stores, are read
-    // by the next device pod's workgroups on other XCDs)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) store_release(&sy->ext_done, gp + 1);
+    if (dbg && t == 0) {
+      c_r += t4 - t3;
+      c_p += t5 - t4;
+      c_c += stamp() - t5;
+      n_l++;
+    }
+  }
+  if (dbg && t == 0) {
+    if (b == 0) {
+      atomicAdd((unsigned long long *)&dbg[80], (unsigned long long)c_w);
+      atomicAdd((unsigned long long *)&dbg[81], (unsigned long long)c_e);
+      atomicAdd((unsigned long long *)&dbg[82], (unsigned long long)c_m);
+      atomicAdd((unsigned long long *)&dbg[87], (unsigned long long)n_ch);
+    }
+    atomicAdd((unsigned long long *)&dbg[83], (unsigned long long)c_r);
+    atomicAdd((unsigned long long *)&dbg[84], (unsigned long long)c_c);
+    atomicAdd((unsigned long long *)&dbg[85], (unsigned long long)c_p);
+    atomicAdd((unsigned long long *)&dbg[86], (unsigned long long)n_l);
   }
 }
 
@@ -547,25 +730,46 @@ hipError_t launch_mark_ext(DevPod *pods, const int32_t *idx, int32_t n, hipStrea
   return hipGetLastError();
 }
 
-int32_t ext_worker_grid(int32_t n_cu, int32_t n) {
-  // about two nodes per thread, at most half the CUs (the class lists' and
-  // the resolve's persistent workgroups hold the others' LDS)
-  const int32_t want = (n + 2 * EXT_THREADS - 1) / (2 * EXT_THREADS);
-  return std::max(1, std::min(want, std::max(1, n_cu / 2 - 2)));
+// The worker's stream holds a quarter of the CUs (api.hip), two workgroups of
+// this kernel per CU (its VGPRs): final-phase workgroups about one chunk each,
+// at most half the slots; pre-evaluation workgroups on the rest (any subset
+// of either group makes progress: chunks are claimed)
+static int32_t ext_final_grid(int32_t n_cu, int32_t n) {
+  return std::max(1, std::min((n + EXT_FCHUNK - 1) / EXT_FCHUNK, std::max(1, n_cu / 4)));
+}
+static int32_t ext_worker_grid(int32_t n_cu, int32_t n) {
+  return ext_final_grid(n_cu, n) +
+         std::max(1, std::min((n + EXT_PCHUNK - 1) / EXT_PCHUNK, std::max(1, n_cu / 2 - ext_final_grid(n_cu, n))));
 }
 
-size_t ext_worker_scratch_bytes() { return (size_t)EXT_RAW * sizeof(uint64_t) + 64; }
+// the zeroed front (table, counters) and the pre-evaluation's per-node keys / raw scores
+static size_t ext_front_bytes(int32_t n_ext) {
+  return ((size_t)EXT_RAW * sizeof(uint64_t) + ((size_t)EXT_CW * std::max(n_ext, 1) + 2) * sizeof(uint32_t) + 255) &
+         ~(size_t)255;
+}
+size_t ext_worker_scratch_bytes(int32_t n_ext, int32_t n) {
+  return ext_front_bytes(n_ext) + (size_t)EXT_RING * std::max(n, 1) * (sizeof(uint64_t) + sizeof(int32_t)) + 64;
+}
+
+size_t ext_worker_diag_offset(int32_t n_ext) {
+  return (size_t)EXT_RAW * sizeof(uint64_t) + ((size_t)EXT_CW * std::max(n_ext, 1) + 1) * sizeof(uint32_t);
+}
 
 hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx,
-                             const int32_t *ext_idx, int32_t n_ext, int32_t grid, void *scratch, int32_t *out_node,
-                             uint32_t *out_dev, PipeSync *sync, hipStream_t s) {
+                             const int32_t *ext_idx, const int32_t *needc, int32_t n_ext, int32_t P, int32_t lag,
+                             int32_t n_cu, void *scratch, int32_t *out_node, uint32_t *out_dev, PipeSync *sync,
+                             uint64_t *dbg, hipStream_t s) {
   if (n_ext <= 0) return hipSuccess;
-  if (seq_mode(c) != 0) return hipErrorInvalidValue;  // the plain build only (the route checks it)
-  uint64_t *tab = static_cast<uint64_t *>(scratch);
-  uint32_t *arrive = reinterpret_cast<uint32_t *>(tab + EXT_RAW);
-  if (hipError_t e = hipMemsetAsync(scratch, 0, ext_worker_scratch_bytes(), s)) return e;
-  hipLaunchKernelGGL(k_ext_worker<0>, dim3(grid), dim3(EXT_THREADS), 0, s, c, d, pods, podx, ext_idx, n_ext, tab, arrive,
-                     out_node, out_dev, sync);
+  if (seq_mode(c) != 0 || P <= 0) return hipErrorInvalidValue;  // the plain build only (the route checks it)
+  char *base = static_cast<char *>(scratch);
+  uint64_t *tab = reinterpret_cast<uint64_t *>(base);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab + EXT_RAW);
+  uint64_t *pk = reinterpret_cast<uint64_t *>(base + ext_front_bytes(n_ext));
+  int32_t *pr = reinterpret_cast<int32_t *>(pk + (size_t)EXT_RING * std::max(d.n, 1));
+  const int32_t gf = ext_final_grid(n_cu, d.n), grid = ext_worker_grid(n_cu, d.n);
+  if (hipError_t e = hipMemsetAsync(scratch, 0, ext_front_bytes(n_ext), s)) return e;
+  hipLaunchKernelGGL(k_ext_worker<0>, dim3(grid), dim3(EXT_THREADS), 0, s, c, d, pods, podx, ext_idx, needc, n_ext, P,
+                     lag, gf, tab, cnt, pk, pr, out_node, out_dev, sync, dbg);
   return hipGetLastError();
 }
 
