@@ -210,8 +210,7 @@ struct koordhip_ctx {
   size_t ext_scr_cap = 0;
   hipStream_t xstream = nullptr;    // its stream (a dedicated queue: the worker spins on the resolve's flag;
                                     // every fourth CU)
-  hipStream_t cstream = nullptr;    // the class lists' stream beside it (the other CUs)
-  hipEvent_t ev_ext = nullptr, ev_cls = nullptr;
+  hipEvent_t ev_ext = nullptr;
   bool last_ext_pipe = false;       // the last place call placed device pods inside the pipeline
   // class-incremental lists (cls.hip): the staged pods' classes (byte-identical
   // device records), the class buffers and the plan of the staged batch
@@ -1191,13 +1190,11 @@ int koordhip_destroy(koordhip_ctx *c) {
     (void)hipStreamDestroy(c->stream2);
   }
   if (c->ev_eval2) (void)hipEventDestroy(c->ev_eval2);
-  for (hipStream_t x : {c->xstream, c->cstream})
-    if (x) {
-      (void)hipStreamSynchronize(x);
-      (void)hipStreamDestroy(x);
-    }
-  for (hipEvent_t e : {c->ev_ext, c->ev_cls})
-    if (e) (void)hipEventDestroy(e);
+  if (c->xstream) {
+    (void)hipStreamSynchronize(c->xstream);
+    (void)hipStreamDestroy(c->xstream);
+  }
+  if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
@@ -2419,7 +2416,7 @@ static int cls_plan(koordhip_ctx *c, int32_t P, int32_t lag, int32_t K) {
   c->plan_coff[nc] = (int32_t)c->plan_csched.size();
   // one device array for the schedule tables, the build tables and the sync words
   const size_t sz[8] = {c->plan_coff.size(), c->plan_csched.size(), c->plan_csm.size(), c->plan_ent.size(),
-                        c->plan_bm.size(), c->plan_bw.size(), (size_t)nc, (size_t)nc + kh::kClsRoundRing};
+                        c->plan_bm.size(), c->plan_bw.size(), (size_t)nc, (((size_t)nc + 15) & ~(size_t)15) + kh::kClsRoundRing + 1 + (size_t)nc};  // sw | rcnt ring, started, states
   size_t tot = 0;
   for (int q = 0; q < 8; q++) {
     c->plan_off[q] = tot;
@@ -2555,21 +2552,20 @@ int place_staged_impl(koordhip_ctx *c) {
       c->ext_scr_cap = xb;
     }
     if (!c->xstream) {
-      // The worker's persistent workgroups and the class lists' must never
-      // starve each other of CUs (each waits on the other through the
-      // resolve): the worker runs on every fourth CU, the class lists on the
-      // others (the resolve and the builds anywhere)
-      const std::vector<uint32_t> all = full_cu_mask(c);
-      std::vector<uint32_t> wm(all.size(), 0u), cm = all;
-      for (int32_t i = 3; i < c->n_cu; i += 4) {
-        wm[i >> 5] |= 1u << (i & 31);
-        cm[i >> 5] &= ~(1u << (i & 31));
+      // The worker's stream: a pooled HIP stream by default -- a fourth
+      // dedicated hardware queue beside the context's three measured
+      // time-sliced (steps 5-10x slower, watchdog stalls) -- else
+      // (KOORDHIP_EXT_DEDICATED, A/B) a dedicated queue on every fourth CU.
+      // The pipeline's other spinning kernels sit in dedicated queues, so the
+      // pooled queue it may share holds nothing it waits for.
+      if (std::getenv("KOORDHIP_EXT_DEDICATED")) {
+        std::vector<uint32_t> wm(full_cu_mask(c).size(), 0u);
+        for (int32_t i = 3; i < c->n_cu; i += 4) wm[i >> 5] |= 1u << (i & 31);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)wm.size(), wm.data()));
+      } else {
+        HIP_TRY(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
       }
-      if (std::getenv("KOORDHIP_EXT_NOMASK")) wm = cm = all;  // (A/B)
-      HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)wm.size(), wm.data()));
-      HIP_TRY(hipExtStreamCreateWithCUMask(&c->cstream, (uint32_t)cm.size(), cm.data()));
       HIP_TRY(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&c->ev_cls, hipEventDisableTiming));
     }
   }
   // the pipelined greedy allocates no device but the device pods' (k_ext_worker):
@@ -2723,7 +2719,8 @@ int place_staged_impl(koordhip_ctx *c) {
     if (int e = cls_alloc(c, c->n)) return e;
     // the build / switch counters start every call at zero; the build stream sees them
     HIP_TRY(hipMemsetAsync(c->d_plan + c->plan_off[6], 0,
-                           (2 * ((c->cls_rep.size() + 15) & ~(size_t)15) + kh::kClsRoundRing) * sizeof(int32_t), c->stream));
+                           (2 * ((c->cls_rep.size() + 15) & ~(size_t)15) + kh::kClsRoundRing + 1 + c->cls_rep.size()) *
+                               sizeof(int32_t), c->stream));
     HIP_TRY(hipEventRecord(c->ev_start, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
   }
@@ -2750,9 +2747,30 @@ int place_staged_impl(koordhip_ctx *c) {
     c->resolve_kernel = kh::last_resolve_kernel();
     res_tm = tm;  // its end event is recorded after the round loop (nothing else runs on rstream)
   }
+
+  if (cls && rounds > 0) {
+    // ONE persistent workgroup per class for the whole stream (c->stream), the
+    // builds on the second stream, all enqueued now (each build waits for its
+    // state's round on the device)
+    hipStream_t cs = c->stream;
+    int32_t tm = -1;
+    if (int e = timed_begin(c, TK_SCAN, cs, &tm)) return e;
+    HIP_TRY(kh::launch_cls_run(c->dc, c->d, c->d_cls_pod, (int32_t)c->cls_rep.size(), c->d_plan + c->plan_off[0],
+                               c->d_plan + c->plan_off[1], c->d_plan + c->plan_off[2], c->d_pod_cls, c->d_out, lag, P,
+                               total, c->d_cls_buf, c->d_cls_meta, K, c->monotone, c->d_lists, list_buf,
+                               cls_sync(c, sync), c->d_dbg ? c->d_dbg + 64 : nullptr, cs));
+    if (int e = timed_end(c, tm, cs)) return e;
+    for (const koordhip_ctx::ClsBuild &b : c->plan_builds)
+      if (int e = cls_build(c, b, sync, c->stream2, b.u % tstride == 0)) return e;
+    c->eval_kernel = kh::cls_run_kernel_name(c->dc);
+    c->last_launches = 1;
+    c->last_evals = (int64_t)total * c->n;  // every (pod, node) pair decided exactly (the lists' equivalent work)
+  }
   if (ext_pipe && rounds > 0) {
-    // the device pods' worker: one persistent launch on its own queue, after
-    // the call's PipeSync / device-slot resets (ev_start)
+    // the device pods' worker: one persistent launch on its own stream, after
+    // the call's PipeSync / device-slot resets (ev_start), and after the class
+    // lists' persistent launch (submitted first, its workgroups are placed
+    // first)
     HIP_TRY(hipStreamWaitEvent(c->xstream, c->ev_start, 0));
     // needc[e]: the device pods of the rounds before round(e) - lag, whose
     // device commits device pod e's pre-evaluation must see (later ones' nodes
@@ -2770,31 +2788,6 @@ int place_staged_impl(koordhip_ctx *c) {
                                   c->n_cu, c->d_ext_scr, c->d_out, c->d_devout, sync,
                                   c->d_dbg, c->xstream));
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
-  }
-  if (cls && rounds > 0) {
-    // ONE persistent workgroup per class for the whole stream (c->stream), the
-    // builds on the second stream, all enqueued now (each build waits for its
-    // state's round on the device)
-    // (beside the device-pod worker: on the CUs it leaves, cstream)
-    const bool use_cs = ext_pipe && !std::getenv("KOORDHIP_EXT_NOCSTREAM");
-    hipStream_t cs = use_cs ? c->cstream : c->stream;
-    if (use_cs) HIP_TRY(hipStreamWaitEvent(cs, c->ev_start, 0));
-    int32_t tm = -1;
-    if (int e = timed_begin(c, TK_SCAN, cs, &tm)) return e;
-    HIP_TRY(kh::launch_cls_run(c->dc, c->d, c->d_cls_pod, (int32_t)c->cls_rep.size(), c->d_plan + c->plan_off[0],
-                               c->d_plan + c->plan_off[1], c->d_plan + c->plan_off[2], c->d_pod_cls, c->d_out, lag, P,
-                               total, c->d_cls_buf, c->d_cls_meta, K, c->monotone, c->d_lists, list_buf,
-                               cls_sync(c, sync), c->d_dbg ? c->d_dbg + 64 : nullptr, cs));
-    if (int e = timed_end(c, tm, cs)) return e;
-    if (use_cs) {
-      HIP_TRY(hipEventRecord(c->ev_cls, cs));
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_cls, 0));
-    }
-    for (const koordhip_ctx::ClsBuild &b : c->plan_builds)
-      if (int e = cls_build(c, b, sync, c->stream2, b.u % tstride == 0)) return e;
-    c->eval_kernel = kh::cls_run_kernel_name(c->dc);
-    c->last_launches = 1;
-    c->last_evals = (int64_t)total * c->n;  // every (pod, node) pair decided exactly (the lists' equivalent work)
   }
   for (int32_t r = 0; r < rounds && !cls; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
@@ -2958,12 +2951,30 @@ int pipe_status(koordhip_ctx *c) {
     c->pipe_err = true;
     c->pipe_errc = err;
     if (c->last_ext_pipe && c->d_ext_scr) {  // where the pipeline stood (device pods inside it)
-      int32_t sw[6] = {0, 0, 0, 0, 0, 0}, xd = 0;
-      HIP_TRY(hipMemcpy(sw, sync, sizeof(sw), hipMemcpyDeviceToHost));
+      int32_t sy[96], xd = 0;
+      HIP_TRY(hipMemcpy(sy, sync, sizeof(sy), hipMemcpyDeviceToHost));
+      const int32_t sw[6] = {sy[0], sy[1], sy[2], sy[3], sy[kh::kPipeSyncExtReqWord], sy[kh::kPipeSyncExtDoneWord]};
       HIP_TRY(hipMemcpy(&xd, static_cast<char *>(c->d_ext_scr) + kh::ext_worker_diag_offset((int32_t)c->ext_idx.size()),
                         sizeof(xd), hipMemcpyDeviceToHost));
+      int32_t ws = 0, cstarted = -1;
+      HIP_TRY(hipMemcpy(&ws, static_cast<char *>(c->d_ext_scr) + kh::ext_worker_diag_offset((int32_t)c->ext_idx.size()) +
+                                 3 * sizeof(int32_t), sizeof(ws), hipMemcpyDeviceToHost));
+      if (c->d_plan && !c->cls_rep.empty()) {
+        const kh::ClsSync cs = cls_sync(c, sync);
+        HIP_TRY(hipMemcpy(&cstarted, cs.rcnt + kh::kClsRoundRing, sizeof(int32_t), hipMemcpyDeviceToHost));
+        std::vector<int32_t> st(c->cls_rep.size()), dn(c->cls_rep.size()), swv(c->cls_rep.size());
+        HIP_TRY(hipMemcpy(st.data(), cs.rcnt + kh::kClsRoundRing + 1, st.size() * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(dn.data(), cs.done, dn.size() * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(swv.data(), cs.sw, swv.size() * 4, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[koordhip] class workgroups (round << 4 | 1 build wait, 2 commit wait, 3 publish wait, 4 "
+                     "published; done; switches):");
+        for (size_t q = 0; q < st.size(); q++) std::fprintf(stderr, " %zu:%d/%d/%d", q, st[q], dn[q], swv[q]);
+        std::fprintf(stderr, "\n");
+      }
       std::fprintf(stderr, "[koordhip] pipeline error %d: sel %d/%d res_round %d ext_req %d ext_done %d | device-pod "
-                   "worker failed at device pod %d phase %d\n", err, sw[0], sw[1], sw[2], sw[4], sw[5], xd >> 4, xd & 15);
+                   "worker failed at device pod %d phase %d; worker workgroups started %d, class-list workgroups "
+                   "started %d of %zu\n", err, sw[0], sw[1], sw[2], sw[4], sw[5], xd >> 4, xd & 15, ws, cstarted,
+                   c->cls_rep.size());
     }
     return fail(KOORDHIP_EDEVICE, pipe_msg(err));
   }

@@ -384,6 +384,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
     lg[w] = 0u;
     if (!monotone) mb[w] = 0u;
   }
+  if (t == 0) atomicAdd(cs.rcnt + kClsRoundRing, 1);  // workgroups started (diagnostics: api.hip pipe_status)
   int32_t nsw = 0;  // switches to a new build so far
   for (int32_t ix = coff[cl]; ix < coff[cl + 1]; ix++) {
     const int32_t ent = csched[ix];
@@ -392,7 +393,10 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
     if (ent < 0) {  // ---- switch to build csm[ix]: wait for it, copy it into LDS
       const int32_t m = csm[ix];
       const int32_t slot = cl * 2 + ((m - 1) & 1);
-      if (t == 0) h.stop = cls_wait_ge(cs.done + cl, m, sy) ? 0 : 1;
+      if (t == 0) {
+        cs.rcnt[kClsRoundRing + 1 + cl] = (u << 4) | 1;  // (diagnostics: where each workgroup waits)
+        h.stop = cls_wait_ge(cs.done + cl, m, sy) ? 0 : 1;
+      }
       __syncthreads();
       if (h.stop) return;
       const ClsMeta mt = metas[slot];
@@ -431,6 +435,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
       h.stop = 0;
       // round u's lists reflect the commits of the rounds < u - lag (one agent
       // acquire after the poll, then the barrier, before any wave reads the log or a row)
+      cs.rcnt[kClsRoundRing + 1 + cl] = (u << 4) | 2;
       if (u > lag && !wait_at_least(&sy->res_round, u - lag, sy)) h.stop = 1;
     }
     __syncthreads();
@@ -624,12 +629,14 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
         const int32_t old = __hip_atomic_fetch_add(rc, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old + mine == np) {
           __hip_atomic_store(rc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          cs.rcnt[kClsRoundRing + 1 + cl] = (u << 4) | 3;
           if (!cls_wait_ge(&sy->sel[u & 1], P * (u >> 1), sy)) h.stop = 1;
           else __hip_atomic_fetch_add(&sy->sel[u & 1], np, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       h.cnt = ntot;
       h.base = max(base, u - lag);
+      cs.rcnt[kClsRoundRing + 1 + cl] = (u << 4) | 4;  // round u published
     }
     __syncthreads();
     if (under || h.over || h.stop) return;

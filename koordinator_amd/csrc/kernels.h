@@ -96,8 +96,9 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
                           int32_t trace, hipStream_t s);
 hipError_t launch_wait_resolved(PipeSync *sync, int32_t rounds, hipStream_t s);
 hipError_t launch_signal_lists(PipeSync *sync, int32_t par, int32_t pods, hipStream_t s);
-constexpr size_t kPipeSyncBytes = 24 + 4 * (1 + 128);  // PipeSync + the X list (pipe.hpp kPipeXMax)
-constexpr int kPipeSyncErrWord = 3;  // PipeSync {sel[2], res_round, err, ext_req, ext_done}: err's int32 index
+constexpr size_t kPipeSyncBytes = 384 + 4 * (1 + 128);  // PipeSync (three 128-B lines) + the X list (pipe.hpp kPipeXMax)
+constexpr int kPipeSyncErrWord = 3;  // PipeSync {sel[2], res_round, err, ...}: err's int32 index
+constexpr int kPipeSyncExtReqWord = 32, kPipeSyncExtDoneWord = 64;
 // single Reserve (sign +1, cpus <- allocated CPUs, *rc = KOORDHIP_ERESERVE on failure) / Unreserve (cpus given)
 hipError_t launch_commit(const DevCfg &c, const DevNodes &d, const DevPod *pod, int32_t node, int32_t sign,
                          uint64_t *cpus, int32_t *rc, hipStream_t s);

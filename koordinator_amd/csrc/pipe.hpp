@@ -26,9 +26,19 @@ static __device__ __forceinline__ uint64_t stamp() {
 //              written back (write-through, drained)
 //   ext_done   the worker stores pod index + 1 once that pod's placement and
 //              its DeviceShare Reserve are published (out_node write-through)
+// Every flag many waves poll has a 128-B line of its own: relaxed agent-scope
+// polls of one line from a few hundred workgroups serialise at its home and
+// delay every other waiter on it (the device-pod worker's idle workgroups
+// made a step 5x slower before ext_req / ext_done moved off sel / res_round).
 struct PipeSync {
-  int32_t sel[2], res_round, err, ext_req, ext_done;
+  int32_t sel[2], res_round, err;
+  int32_t pad0[28];
+  int32_t ext_req;
+  int32_t pad1[31];
+  int32_t ext_done;
+  int32_t pad2[31];
 };
+static_assert(sizeof(PipeSync) == 384, "PipeSync lines");
 // After the struct: the resolve's X set at a device-pod hand-off, {count,
 // nodes[kPipeXMax]} (M' and this round's M so far), stored write-through
 // before ext_req.
@@ -74,6 +84,22 @@ static __device__ bool wait_at_least(const int32_t *p, int32_t v, PipeSync *sy) 
       return false;
     }
     __builtin_amdgcn_s_sleep(4);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return true;
+}
+// The same for waiters off the critical path (the device-pod worker's idle
+// workgroups): longer sleeps, the error word read every 16th poll.
+static __device__ bool wait_at_least_idle(const int32_t *p, int32_t v, PipeSync *sy) {
+  const uint64_t t0 = stamp();
+  for (uint32_t k = 0; load_relaxed(p) < v; k++) {
+    if ((k & 15u) == 15u && load_relaxed(&sy->err)) return false;
+    if (stamp() - t0 > PIPE_WATCHDOG) {
+      store_release(&sy->err, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(32);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

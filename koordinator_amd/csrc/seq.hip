@@ -105,10 +105,14 @@ using SeqResvRow = NumaRowRS<SM == 3 ? KOORDHIP_RESV_SLOTS_MAX : KOORDHIP_RESV_S
 // raw normalized scores.  Every column is read (the parity evaluator's rows,
 // like k_eval_full).  Inlined once per kernel: a call keeps its frame (the
 // config and column descriptors, the NV row) in scratch, kilobytes per lane.
-template <int SM>
+// EARLY (k_ext_worker: no status, no raw planes of infeasible nodes): a node
+// whose extended scalars do not fit returns -1 before any other load.
+template <int SM, bool EARLY = false>
 __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x,
                                             int32_t i, bool rs, int32_t raw[KOORDHIP_NEXT_PLUGINS],
                                             uint8_t *status) {
+  if constexpr (EARLY)
+    if ((c.filt & KOORDHIP_PLUGIN_FIT) && !xfit_filter(d.dv, x, i, d.n)) return -1;
   NV v{};
   const Need all = need_all(c);
   load_node(v, d, i, all, c);
@@ -116,7 +120,7 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   // overlap the row's: the extended scalars, the static Scores and (without
   // the Reservation build, whose nomination needs the reservation rows) the
   // device rows
-  const bool xf = !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x, i, d.n);
+  const bool xf = EARLY || !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x, i, d.n);
   raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
   raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   int32_t t;
@@ -477,7 +481,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
                                                             const int32_t *__restrict__ needc, int32_t n_ext, int32_t P,
                                                             int32_t lag, int32_t gf, uint64_t *__restrict__ tab,
                                                             uint32_t *__restrict__ cnt, uint64_t *__restrict__ pk,
-                                                            int32_t *__restrict__ pr, int32_t *__restrict__ out_node,
+                                                            int32_t *__restrict__ pr, const int32_t *__restrict__ perm,
+                                                            int32_t *__restrict__ out_node,
                                                             uint32_t *__restrict__ out_dev, PipeSync *sy, uint64_t *dbg) {
   __shared__ uint64_t lt[EXT_RAW];
   __shared__ uint32_t xm[EXT_FCHUNK / 32];  // the chunk's X nodes
@@ -492,6 +497,7 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
   const int32_t wdev = (c.score & KOORDHIP_PLUGIN_DEVICESHARE) ? c.w_ext[0] : 0;
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
   const size_t nn = (size_t)max(d.n, 1);
+  if (t == 0) atomicAdd(cdone + 4, 1);  // workgroups started (diagnostics: api.hip pipe_status)
   // dbg (KOORDHIP_STAMPS): final workgroup 0's cycles waiting for the hand-off,
   // final phase, merge + arrival [80..82], its final chunks [87]; pre-evaluation
   // workgroup gf's cycles waiting [89] and evaluating [88]; the last final
@@ -522,10 +528,11 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
     uint64_t *bk = pk + (size_t)(e % EXT_RING) * nn;
     int32_t *br = pr + (size_t)(e % EXT_RING) * nn;
     const int32_t pdone = claim_all(cw, ncp, [&](int32_t ch) {
-      const int32_t i = ch * EXT_PCHUNK + t;
-      if (i < d.n) {
+      const int32_t j = ch * EXT_PCHUNK + t;
+      if (j < d.n) {
+        const int32_t i = perm[j];
         int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
-        const int32_t tk = seq_eval<SM>(c, d, p, x, i, false, raw, nullptr);
+        const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
         st_wt(&bk[i], (uint64_t)(tk >= 0 ? make_key(tk, i) : 0ull));
         st_wt(&br[i], (int32_t)min(max(raw[0], 0), EXT_RAW - 1));
       }
@@ -544,8 +551,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
       uint32_t *cw = cnt + (size_t)EXT_CW * e;  // {pre claimed, pre finished, final claimed, final finished}
       const uint64_t tp0 = dbg ? stamp() : 0;
       if (t == 0)
-        s_go = ((u <= lag || wait_at_least(&sy->res_round, u - lag, sy)) && wait_at_least(cdone, needc[e], sy) &&
-                (e < EXT_RING || wait_at_least(&sy->ext_done, ext_idx[e - EXT_RING] + 1, sy)))
+        s_go = ((u <= lag || wait_at_least_idle(&sy->res_round, u - lag, sy)) && wait_at_least_idle(cdone, needc[e], sy) &&
+                (e < EXT_RING || wait_at_least_idle(&sy->ext_done, ext_idx[e - EXT_RING] + 1, sy)))
                    ? 1
                    : 0;
       __syncthreads();
@@ -614,7 +621,7 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
         const int32_t y = k * EXT_THREADS + t, i = c0 + y;
         if (i < d.n && ((xm[y >> 5] >> (y & 31)) & 1u)) {  // committed since the pre-evaluation: evaluate again
           int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
-          const int32_t tk = seq_eval<SM>(c, d, p, x, i, false, raw, nullptr);
+          const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
           kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
           rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
         }
@@ -718,6 +725,35 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
   }
 }
 
+// The pre-evaluation's node order: nodes holding device scalars (any xalloc
+// > 0) first, the rest after (their extended-scalar Fit fails for a pod
+// requesting one: seq_eval<.., true> returns before their other loads, so
+// whole waves of them finish at once).  Order inside each part is free: the
+// pre-evaluation writes by node index.  cnt2: two zeroed counters.
+__global__ void k_ext_perm(DevDev dv, int32_t n, int32_t *__restrict__ perm, uint32_t *__restrict__ cnt2) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool has = false;
+  if (i < n && dv.xalloc)
+#pragma unroll
+    for (int j = 0; j < KOORDHIP_NXRES; j++) has = has || dv.xalloc[(size_t)j * n + i] > 0;
+  const uint64_t bh = __ballot(i < n && has), bo = __ballot(i < n && !has);
+  const int lane = threadIdx.x & 63;
+  uint32_t ah = 0, ao = 0;
+  if (lane == 0) {
+    if (bh) ah = atomicAdd(&cnt2[0], (uint32_t)__popcll(bh));
+    if (bo) ao = atomicAdd(&cnt2[1], (uint32_t)__popcll(bo));
+  }
+  ah = __shfl(ah, 0, 64);
+  ao = __shfl(ao, 0, 64);
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (i < n) {
+    if (has)
+      perm[ah + __popcll(bh & below)] = i;
+    else
+      perm[n - 1 - (int32_t)(ao + __popcll(bo & below))] = i;
+  }
+}
+
 // pods[idx[j]].flags |= KH_POD_EXT
 __global__ void k_mark_ext(DevPod *pods, const int32_t *__restrict__ idx, int32_t n) {
   const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -744,11 +780,12 @@ static int32_t ext_worker_grid(int32_t n_cu, int32_t n) {
 
 // the zeroed front (table, counters) and the pre-evaluation's per-node keys / raw scores
 static size_t ext_front_bytes(int32_t n_ext) {
-  return ((size_t)EXT_RAW * sizeof(uint64_t) + ((size_t)EXT_CW * std::max(n_ext, 1) + 2) * sizeof(uint32_t) + 255) &
+  return ((size_t)EXT_RAW * sizeof(uint64_t) + ((size_t)EXT_CW * std::max(n_ext, 1) + 5) * sizeof(uint32_t) + 255) &
          ~(size_t)255;
 }
 size_t ext_worker_scratch_bytes(int32_t n_ext, int32_t n) {
-  return ext_front_bytes(n_ext) + (size_t)EXT_RING * std::max(n, 1) * (sizeof(uint64_t) + sizeof(int32_t)) + 64;
+  return ext_front_bytes(n_ext) + (size_t)EXT_RING * std::max(n, 1) * (sizeof(uint64_t) + sizeof(int32_t)) +
+         (size_t)std::max(n, 1) * sizeof(int32_t) + 64;
 }
 
 size_t ext_worker_diag_offset(int32_t n_ext) {
@@ -766,10 +803,13 @@ hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *p
   uint32_t *cnt = reinterpret_cast<uint32_t *>(tab + EXT_RAW);
   uint64_t *pk = reinterpret_cast<uint64_t *>(base + ext_front_bytes(n_ext));
   int32_t *pr = reinterpret_cast<int32_t *>(pk + (size_t)EXT_RING * std::max(d.n, 1));
+  int32_t *perm = pr + (size_t)EXT_RING * std::max(d.n, 1);
+  uint32_t *pc = cnt + (size_t)EXT_CW * n_ext + 2;  // (after cdone and the failure word)
   const int32_t gf = ext_final_grid(n_cu, d.n), grid = ext_worker_grid(n_cu, d.n);
   if (hipError_t e = hipMemsetAsync(scratch, 0, ext_front_bytes(n_ext), s)) return e;
+  hipLaunchKernelGGL(k_ext_perm, dim3((d.n + 255) / 256), dim3(256), 0, s, d.dv, d.n, perm, pc);
   hipLaunchKernelGGL(k_ext_worker<0>, dim3(grid), dim3(EXT_THREADS), 0, s, c, d, pods, podx, ext_idx, needc, n_ext, P,
-                     lag, gf, tab, cnt, pk, pr, out_node, out_dev, sync, dbg);
+                     lag, gf, tab, cnt, pk, pr, perm, out_node, out_dev, sync, dbg);
   return hipGetLastError();
 }
 
