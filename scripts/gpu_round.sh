@@ -16,7 +16,7 @@ STAGES=${STAGES:-tests smoke bench stamps prof pmc}
 WORKLOADS=${WORKLOADS:-config4 config3 config5}
 mkdir -p gpurun_out
 has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
-steps_of() { case $1 in config4) echo "--steps 5 --warmup 2";; config3|deviceshare|spread|affinity) echo "--steps 3 --warmup 1";; resvpolicy) echo "--steps 1 --warmup 1";; *) echo "--steps 2 --warmup 1";; esac; }
+steps_of() { case $1 in config4|config4dsmix|config4ds) echo "--steps 5 --warmup 2";; config3|deviceshare|spread|affinity) echo "--steps 3 --warmup 1";; resvpolicy) echo "--steps 1 --warmup 1";; *) echo "--steps 2 --warmup 1";; esac; }
 pods_pmc() { case $1 in config4) echo 30000;; config3) echo 10000;; *) echo 6000;; esac; }
 
 if has tests; then
