@@ -2736,12 +2736,11 @@ int place_staged_impl(koordhip_ctx *c) {
   if (persistent && rounds > 0) {
     int32_t tm = -1;
     if (int e = timed_begin(c, TK_RESOLVE, c->rstream, &tm)) return e;
-    // (monotone bit 1: the prologue's chained decisions, opt-in KOORDHIP_CHAIN: they
-    // take the staged-conflict pods off the general path -- config 4: 16.0k -> 0.4k
-    // general-path pods -- but the chain passes cost ~5k cycles a pod in the
-    // prologue and leave wave 0 waiting for wave 1's next-round loads: 75.1 vs
-    // 73.9 ms per step, profiles/r05h_chain_ab.txt)
-    const int32_t mono = c->monotone | ((c->monotone && std::getenv("KOORDHIP_CHAIN")) ? 2 : 0);
+    // (monotone bit 1: the chained decisions, wave 0 at the start of each
+    // round's loop: they take the staged-conflict pods off the general path --
+    // config 4: 16.0k -> 0.4k general-path pods, 75.0 -> 62.5 ms per step,
+    // profiles/r05n_chain_ab.txt; KOORDHIP_CHAIN_OFF for A/B)
+    const int32_t mono = c->monotone | ((c->monotone && !std::getenv("KOORDHIP_CHAIN_OFF")) ? 2 : 0);
     HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, mono, lag, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
     c->resolve_kernel = kh::last_resolve_kernel();

@@ -1936,7 +1936,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   __shared__ int32_t pgen[RES_MAXP_ROUND];   // ... and the round that last did (lag 2)
   __shared__ int32_t seg_w[RES_MAXP_ROUND];  // staged winners by M slot (bulk commits)
   __shared__ int32_t ckey[RES_HASH], cval[RES_HASH];  // staged winner -> first pod (conflict detection)
-  __shared__ int32_t sh_mp, sh_stop, sh_done;
+  __shared__ int32_t sh_mp, sh_stop, sh_done, sh_chain;
   const int t = threadIdx.x, lane = lane_id();
   const int32_t words = (n_nodes + 31) >> 5;
   const int32_t HP = max(1, RES_PRE / P);  // prefetched list heads per pod
@@ -2157,7 +2157,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     const int32_t mp = sh_mp;
     if (!preloaded) load_round(r, p0, n_pods, lk, lpod, pre, prenr, pre_node, t, RES_THREADS);
     for (int32_t x = t; x < RES_HASH; x += RES_THREADS) hnode[x] = -1;
-    if (t == 0) sh_done = 0;
+    if (t == 0) {
+      sh_done = 0;
+      sh_chain = 0;
+    }
     __syncthreads();
     if (t < mp) {  // M' hash: node -> slot, linear probing, lock-free inserts
       const int32_t nd = pnode[t];
@@ -2296,166 +2299,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       }
     }
     __syncthreads();
-    // ---- 2c. chained decisions (monotone configurations, monotone bit 1): a
-    //          conflicting pod re-walks its list with the staged winners of the
-    //          earlier VALID pods as modified entries -- each evaluated on its
-    //          claimer's source row + the claimer's Reserve delta (the key
-    //          tables' kpre) -- up to the first unmodified entry (exact).  Its
-    //          decision then assumes those claimers' commits (dep: a claimer
-    //          voided later voids it too).  A pod whose new winner is a valid
-    //          claimer's node, or whose walk needs more than RES_WE entries,
-    //          stays on the general path.  Every pass re-checks the valid pods
-    //          against the valid claims (a pod resolved in a pass may meet a
-    //          winner resolved in the same pass) and repeats.
     uint64_t *dep = reinterpret_cast<uint64_t *>(lds + ofs.dep);
     for (int32_t x = t; x < n_pods; x += RES_THREADS) dep[x] = 0ull;
-    if (monotone & 2) {
-      const uint64_t t_c0 = (dbg && t == 0) ? stamp() : 0;
-      // the claims of the valid (dec_c == 0) pods: staged winner -> pod
-      auto claims = [&]() {
-        for (int32_t x = t; x < RES_HASH; x += RES_THREADS) {
-          ckey[x] = -1;
-          cval[x] = 64;
-        }
-        __syncthreads();
-        if (t < n_pods && dec_c[t] == 0 && dec_key[t] != 0ull) {
-          const int32_t sw = key_node(dec_key[t]);
-          uint32_t h = res_hash(sw);
-          for (;;) {
-            const int32_t prev = atomicCAS(&ckey[h], -1, sw);
-            if (prev == -1 || prev == sw) {
-              atomicMin(&cval[h], t);
-              break;
-            }
-            h = (h + 1) & (RES_HASH - 1);
-          }
-        }
-        __syncthreads();
-      };
-      auto claimer_of = [&](int32_t y) -> int32_t {
-        uint32_t q = res_hash(y);
-        for (;;) {
-          const int32_t xk = ckey[q];
-          if (xk == y) return cval[q];
-          if (xk < 0) return 64;
-          q = (q + 1) & (RES_HASH - 1);
-        }
-      };
-      for (int pass = 0; pass < RES_CHAIN_PASSES; pass++) {
-        claims();
-        if (t == 0) sh_done = 0;  // (reused as this pass's "a pod was resolved")
-        __syncthreads();
-        for (int32_t base = 0; base < n_pods * RES_WE; base += RES_THREADS) {
-          const int32_t x = base + t;
-          const int32_t l = x / RES_WE, q = x - l * RES_WE;
-          const bool live = l < n_pods && dec_c[l] == 1;  // uniform per 8-lane group
-          const uint64_t e = (live && q < kp) ? lk[l * kp + q] : 0ull;
-          const int32_t nd = e ? key_node(e) : -1;
-          const bool inm = e != 0 && xbit(modmap, nd);
-          const int32_t cl = e != 0 ? claimer_of(nd) : 64;
-          const bool clv = cl < l;
-          const bool mod = inm || clv;
-          const int gq = lane & ~(RES_WE - 1);
-          const uint32_t bx = (uint32_t)(__ballot(live && e != 0 && !mod) >> gq) & 0xFFu;
-          const uint32_t bz = (uint32_t)(__ballot(live && e == 0) >> gq) & 0xFFu;
-          const int f = bx ? __builtin_ctz(bx) : RES_WE, z = bz ? __builtin_ctz(bz) : RES_WE;
-          const bool general = f == RES_WE && z == RES_WE;
-          const bool walked = live && !general && (q < min(f, z) || (q == f && f < z));
-          uint64_t key = 0;
-          int32_t ms = -1;
-          if (walked) {
-            if (q < min(f, z)) {  // a modified entry: its key on the row it will have
-              NV v;
-              NR nr;
-              if (clv) {
-                const int32_t src = dec_src[cl];
-                v = src >= 0 ? pre[src] : prow[-src - 1];
-                if constexpr (NUMA) nr = src >= 0 ? prenr[src] : pnr[-src - 1];
-                apply_delta(v, lpod[cl], +1);
-              } else {
-                ms = prev_slot(nd);
-                v = slot_row(prow[ms]);
-                if constexpr (NUMA) nr = pnr[ms];
-              }
-              key = make_key(eval_row<NM>(lpod[l], v, nr, cls, c), nd);
-            } else {
-              key = e;
-            }
-          }
-          uint64_t mx = key, dm = (walked && clv) ? (1ull << cl) : 0ull;
-#pragma unroll
-          for (int m = 1; m < RES_WE; m <<= 1) {
-            const uint64_t o = shfl_xor_u64(mx, m);
-            mx = o > mx ? o : mx;
-            dm |= shfl_xor_u64(dm, m);
-          }
-          const bool win = walked && key == mx && mx != 0;
-          // the new winner is a valid claimer's node: two commits to one node (general path)
-          const bool rep = ((uint32_t)(__ballot(win && clv) >> gq) & 0xFFu) != 0u;
-          if (live && !general && !rep) {
-            dec_e[l * RES_WE + q] = walked ? nd : -1;
-            if (win) {  // the winner's row source, as in phase 2
-              int32_t src;
-              if (inm) {
-                src = -prev_slot(nd) - 1;
-              } else if (q < HP && pre_node[l * HP + q] == nd) {
-                src = l * HP + q;
-              } else {
-                src = l * HP;
-                NV v;
-                load_row(v, nodes(), nd);
-                pre[src] = v;
-                if constexpr (NUMA) {
-                  NR nr;
-                  load_side_row<NM>(nr, nodes(), nd);
-                  prenr[src] = nr;
-                }
-                pre_node[src] = nd;
-              }
-              dec_src[l] = src;
-            }
-            if (q == 0) {
-              dec_key[l] = mx;
-              dec_n[l] = f < z ? f + 1 : z;
-              if (mx == 0) dec_src[l] = 0;
-              dep[l] = dm;
-              dec_c[l] = 0;
-              sh_done = 1;
-              if (dbg) atomicAdd((unsigned long long *)&dbg[63], 1ull);
-            }
-          }
-        }
-        __syncthreads();
-        const bool resolved = sh_done != 0;
-        // re-check: a valid pod whose walk meets a valid claim it did not assume
-        claims();
-        for (int32_t x = t; x < n_pods * RES_WE; x += RES_THREADS) {
-          const int32_t l = x / RES_WE;
-          const int32_t y = dec_e[x];
-          if (y >= 0 && dec_c[l] == 0) {
-            const int32_t cl = claimer_of(y);
-            if (cl < l && !((dep[l] >> cl) & 1ull)) atomicOr(&dec_c[l], 1);
-          }
-        }
-        __syncthreads();
-        if (t < 64) {  // closure in pod order: a pod assuming an invalid pod's commit is invalid
-          const bool lv = lane < n_pods;
-          const uint64_t dl = lv ? dep[lane] : 0ull;
-          uint64_t valid = __ballot(lv && dec_c[lane] == 0);
-          for (;;) {
-            const uint64_t bad = __ballot(((valid >> lane) & 1ull) && (dl & ~valid) != 0ull);
-            if (!bad) break;
-            valid &= ~bad;
-            if ((bad >> lane) & 1ull) dec_c[lane] = 1;
-          }
-        }
-        __syncthreads();
-        if (!resolved) break;  // uniform
-      }
-      if (t == 0) sh_done = 0;  // (the helpers' stop flag again)
-      claims();                 // the loop's claimer(): the valid pods' winners
-      if (dbg && t == 0) c_chain += stamp() - t_c0;
-    }
     if (dbg && t == 0) {
       const uint64_t t_p3 = stamp();
       c_hash += t_a - t_entry;
@@ -2467,6 +2312,172 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     }
     if (t < 64) {  // ---- 3. the sequential greedy over the round (wave 0)
       __builtin_amdgcn_s_setprio(3);
+      // ---- 2c. chained decisions (monotone configurations, monotone bit 1),
+      //      wave 0 alone (no workgroup barrier: wave 1 loads the next round
+      //      meanwhile; the helper waves wait for sh_chain): a conflicting pod
+      //      re-walks its list with the staged winners of the earlier VALID
+      //      pods as modified entries -- each evaluated on its claimer's source
+      //      row + the claimer's Reserve delta -- up to the first unmodified
+      //      entry (exact).  Its decision then assumes those claimers' commits
+      //      (dep: a claimer voided later voids it too).  A pod whose new winner
+      //      is a valid claimer's node, or whose walk needs more than RES_WE
+      //      entries, stays on the general path.  Each pass re-checks the valid
+      //      pods against the valid claims and closes the dependencies in pod
+      //      order; up to RES_CHAIN_PASSES passes, eight pods per lane group.
+      if (monotone & 2) {
+        const uint64_t t_c0 = dbg ? stamp() : 0;
+        auto wsync = [&]() {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        };
+        // the claims of the valid (dec_c == 0) pods: staged winner -> first pod
+        auto claims = [&]() {
+          for (int32_t x = lane; x < RES_HASH; x += 64) {
+            ckey[x] = -1;
+            cval[x] = 64;
+          }
+          wsync();
+          if (lane < n_pods && dec_c[lane] == 0 && dec_key[lane] != 0ull) {
+            const int32_t sw2 = key_node(dec_key[lane]);
+            uint32_t h = res_hash(sw2);
+            for (;;) {
+              const int32_t prev = atomicCAS(&ckey[h], -1, sw2);
+              if (prev == -1 || prev == sw2) {
+                atomicMin(&cval[h], lane);
+                break;
+              }
+              h = (h + 1) & (RES_HASH - 1);
+            }
+          }
+          wsync();
+        };
+        auto claimer_of = [&](int32_t y) -> int32_t {
+          uint32_t q = res_hash(y);
+          for (;;) {
+            const int32_t xk = ckey[q];
+            if (xk == y) return cval[q];
+            if (xk < 0) return 64;
+            q = (q + 1) & (RES_HASH - 1);
+          }
+        };
+        for (int pass = 0; pass < RES_CHAIN_PASSES; pass++) {
+          claims();
+          uint64_t conf = __ballot(lane < n_pods && dec_c[lane] == 1);
+          if (!conf) break;
+          bool resolved = false;
+          while (conf) {  // eight conflicting pods at a time, eight lanes (entries) each
+            const int gq = lane >> 3, q = lane & 7;
+            uint64_t cm = conf;
+            for (int k = 0; k < gq && cm; k++) cm &= cm - 1ull;
+            const int32_t l = cm ? (int32_t)__builtin_ctzll(cm) : -1;
+            for (int k = 0; k < 8 && conf; k++) conf &= conf - 1ull;
+            const bool live = l >= 0;
+            const uint64_t e = (live && q < kp) ? lk[l * kp + q] : 0ull;
+            const int32_t nd = e ? key_node(e) : -1;
+            const bool inm = e != 0 && xbit(modmap, nd);
+            const int32_t cl = e != 0 ? claimer_of(nd) : 64;
+            const bool clv = live && cl < l;
+            const bool mod = inm || clv;
+            const int g8 = lane & ~7;
+            const uint32_t bx = (uint32_t)(__ballot(live && e != 0 && !mod) >> g8) & 0xFFu;
+            const uint32_t bz = (uint32_t)(__ballot(live && e == 0) >> g8) & 0xFFu;
+            const int f = bx ? __builtin_ctz(bx) : RES_WE, z = bz ? __builtin_ctz(bz) : RES_WE;
+            const bool general = f == RES_WE && z == RES_WE;
+            const bool walked = live && !general && (q < min(f, z) || (q == f && f < z));
+            uint64_t key = 0;
+            if (walked) {
+              if (q < min(f, z)) {  // a modified entry: its key on the row it will have
+                NV v;
+                NR nr;
+                if (clv) {
+                  const int32_t src = dec_src[cl];
+                  v = src >= 0 ? pre[src] : prow[-src - 1];
+                  if constexpr (NUMA) nr = src >= 0 ? prenr[src] : pnr[-src - 1];
+                  apply_delta(v, lpod[cl], +1);
+                } else {
+                  const int32_t ms = prev_slot(nd);
+                  v = slot_row(prow[ms]);
+                  if constexpr (NUMA) nr = pnr[ms];
+                }
+                key = make_key(eval_row<NM>(lpod[l], v, nr, cls, c), nd);
+              } else {
+                key = e;
+              }
+            }
+            uint64_t mx = key, dm = (walked && clv) ? (1ull << cl) : 0ull;
+#pragma unroll
+            for (int m = 1; m < RES_WE; m <<= 1) {
+              const uint64_t o = shfl_xor_u64(mx, m);
+              mx = o > mx ? o : mx;
+              dm |= shfl_xor_u64(dm, m);
+            }
+            const bool win = walked && key == mx && mx != 0;
+            // the new winner is a valid claimer's node: two commits to one node (general path)
+            const bool rep = ((uint32_t)(__ballot(win && clv) >> g8) & 0xFFu) != 0u;
+            const bool ok2 = live && !general && !rep;
+            if (ok2) {
+              dec_e[l * RES_WE + q] = walked ? nd : -1;
+              if (win) {  // the winner's row source, as in phase 2
+                int32_t src;
+                if (inm) {
+                  src = -prev_slot(nd) - 1;
+                } else if (q < HP && pre_node[l * HP + q] == nd) {
+                  src = l * HP + q;
+                } else {
+                  src = l * HP;
+                  NV v;
+                  load_row(v, nodes(), nd);
+                  pre[src] = v;
+                  if constexpr (NUMA) {
+                    NR nr;
+                    load_side_row<NM>(nr, nodes(), nd);
+                    prenr[src] = nr;
+                  }
+                  pre_node[src] = nd;
+                }
+                dec_src[l] = src;
+              }
+              if (q == 0) {
+                dec_key[l] = mx;
+                dec_n[l] = f < z ? f + 1 : z;
+                if (mx == 0) dec_src[l] = 0;
+                dep[l] = dm;
+                dec_c[l] = 0;
+                if (dbg) atomicAdd((unsigned long long *)&dbg[63], 1ull);
+              }
+            }
+            resolved = resolved || (__ballot(ok2) != 0ull);
+            wsync();
+          }
+          if (!resolved) break;
+          // re-check: a valid pod whose walk meets a valid claim it did not assume
+          claims();
+          for (int32_t x0 = 0; x0 < n_pods * RES_WE; x0 += 64) {
+            const int32_t x = x0 + lane, l2 = x / RES_WE;
+            const int32_t y = x < n_pods * RES_WE ? dec_e[x] : -1;
+            if (y >= 0 && dec_c[l2] == 0) {
+              const int32_t cl2 = claimer_of(y);
+              if (cl2 < l2 && !((dep[l2] >> cl2) & 1ull)) atomicOr(&dec_c[l2], 1);
+            }
+          }
+          wsync();
+          {  // closure in pod order: a pod assuming an invalid pod's commit is invalid
+            const bool lv = lane < n_pods;
+            const uint64_t dl = lv ? dep[lane] : 0ull;
+            uint64_t valid = __ballot(lv && dec_c[lane] == 0);
+            for (;;) {
+              const uint64_t bad = __ballot(((valid >> lane) & 1ull) && (dl & ~valid) != 0ull);
+              if (!bad) break;
+              valid &= ~bad;
+              if ((bad >> lane) & 1ull) dec_c[lane] = 1;
+            }
+          }
+          wsync();
+        }
+        claims();  // the loop's claimer(): the valid pods' winners
+        if (lane == 0) __hip_atomic_store(&sh_chain, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (dbg) c_chain += stamp() - t_c0;
+      }
       const uint64_t t_loop = dbg ? stamp() : 0;
       int32_t nm = 0;  // |M| (wave-uniform)
       my_node = -1;
@@ -3025,6 +3036,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       //      path, monotone): those pods are dealt round-robin to the waves.
       const int hw = __builtin_amdgcn_readfirstlane((t >> 6) - 1 - res_loaders<NM>()),
                 nh = RES_THREADS / 64 - 1 - res_loaders<NM>();
+      if (monotone & 2)  // wave 0's chained decisions first (they rewrite the staged decisions)
+        while (!__hip_atomic_load(&sh_chain, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) __builtin_amdgcn_s_sleep(1);
       uint64_t todo = __ballot(lane < n_pods && dec_c[lane] == 1);
       for (int32_t x = 0; x < hw && todo; x++) todo &= todo - 1ull;
       for (; have_tables && todo;) {
