@@ -2740,7 +2740,11 @@ int place_staged_impl(koordhip_ctx *c) {
     // round's loop: they take the staged-conflict pods off the general path --
     // config 4: 16.0k -> 0.4k general-path pods, 75.0 -> 62.5 ms per step,
     // profiles/r05n_chain_ab.txt; KOORDHIP_CHAIN_OFF for A/B)
-    const int32_t mono = c->monotone | ((c->monotone && !std::getenv("KOORDHIP_CHAIN_OFF")) ? 2 : 0);
+    // (bits 2-3: chain passes, 1 by default -- 1 / 2 / 3 passes measured 60.1 /
+    // 60.5 / 61.0 ms per step on config 4, r05o; KOORDHIP_CHAIN_PASSES for A/B)
+    const char *cp = std::getenv("KOORDHIP_CHAIN_PASSES");
+    const int32_t mono = c->monotone | ((c->monotone && !std::getenv("KOORDHIP_CHAIN_OFF")) ? 2 : 0) |
+                         (c->monotone ? (((cp ? std::atoi(cp) : 1) & 3) << 2) : 0);
     HIP_TRY(kh::launch_resolve(c->dc, c->d, c->d_desc, c->d_pods, total, P, K, 0, rounds, lists0, list_buf, mono, lag, sync,
                                mbuf, c->d_out, cpus, c->d_dbg, trace, c->rstream));
     c->resolve_kernel = kh::last_resolve_kernel();

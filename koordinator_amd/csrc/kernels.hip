@@ -2360,8 +2360,13 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             q = (q + 1) & (RES_HASH - 1);
           }
         };
-        for (int pass = 0; pass < RES_CHAIN_PASSES; pass++) {
-          claims();
+        // passes: monotone bits 2-3 (KOORDHIP_CHAIN_PASSES), else RES_CHAIN_PASSES;
+        // fresh: ckey / cval hold exactly the valid pods' claims
+        const int npass = ((monotone >> 2) & 3) ? ((monotone >> 2) & 3) : RES_CHAIN_PASSES;
+        bool fresh = false;
+        for (int pass = 0; pass < npass; pass++) {
+          if (!fresh) claims();
+          fresh = true;
           uint64_t conf = __ballot(lane < n_pods && dec_c[lane] == 1);
           if (!conf) break;
           bool resolved = false;
@@ -2452,13 +2457,17 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           if (!resolved) break;
           // re-check: a valid pod whose walk meets a valid claim it did not assume
           claims();
+          bool inv = false;
           for (int32_t x0 = 0; x0 < n_pods * RES_WE; x0 += 64) {
             const int32_t x = x0 + lane, l2 = x / RES_WE;
             const int32_t y = x < n_pods * RES_WE ? dec_e[x] : -1;
+            bool bad = false;
             if (y >= 0 && dec_c[l2] == 0) {
               const int32_t cl2 = claimer_of(y);
-              if (cl2 < l2 && !((dep[l2] >> cl2) & 1ull)) atomicOr(&dec_c[l2], 1);
+              bad = cl2 < l2 && !((dep[l2] >> cl2) & 1ull);
+              if (bad) atomicOr(&dec_c[l2], 1);
             }
+            inv = inv || __ballot(bad) != 0ull;
           }
           wsync();
           {  // closure in pod order: a pod assuming an invalid pod's commit is invalid
@@ -2468,13 +2477,15 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             for (;;) {
               const uint64_t bad = __ballot(((valid >> lane) & 1ull) && (dl & ~valid) != 0ull);
               if (!bad) break;
+              inv = true;
               valid &= ~bad;
               if ((bad >> lane) & 1ull) dec_c[lane] = 1;
             }
           }
           wsync();
+          fresh = !inv;  // (an invalidated pod's claim is still in the table)
         }
-        claims();  // the loop's claimer(): the valid pods' winners
+        if (!fresh) claims();  // the loop's claimer(): the valid pods' winners
         if (lane == 0) __hip_atomic_store(&sh_chain, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (dbg) c_chain += stamp() - t_c0;
       }
