@@ -226,6 +226,7 @@ class Informer:
         if pod.node_name:
             self._dirty.add(pod.node_name)
         self._touch_metric_refs(pod)
+        self._operating_pod(None, pod)
 
     def on_pod_update(self, old: Optional[k8s.Pod], pod: k8s.Pod, now: float):
         prev = self._pods_by_uid.get(pod.uid)
@@ -244,6 +245,7 @@ class Informer:
         if pod.node_name:
             self._dirty.add(pod.node_name)
         self._touch_metric_refs(pod)
+        self._operating_pod(prev, pod)
 
     def on_pod_delete(self, pod: k8s.Pod):
         prev = self._pods_by_uid.pop(pod.uid, pod)
@@ -254,6 +256,21 @@ class Informer:
         if prev.node_name:
             self._dirty.add(prev.node_name)
         self._touch_metric_refs(prev)
+        self._operating_pod(prev, None)
+
+    def _operating_pod(self, prev: Optional[k8s.Pod], pod: Optional[k8s.Pod]):
+        """A bound pod in the reservation operating mode is also an Available
+        reservation on its node (the reservation cache, pod_eventhandler.go:104-124,
+        cache.go:139-168): reservation_columns gives it a slot like a
+        Reservation's (rv.operating_pod_reservation)."""
+        r = rv.operating_pod_reservation(pod) if pod is not None else None
+        if prev is not None and rv.is_reservation_operating_pod(prev):
+            old = rv.operating_reservation_name(prev)
+            if r is None or r.name != old:
+                if old in self.reservations:
+                    self.on_reservation_delete(old)
+        if r is not None:
+            self.on_reservation(r)
 
     # ---- NodeMetric events -------------------------------------------------------------
     def on_node_metric(self, nm: k8s.NodeMetric):
@@ -330,7 +347,7 @@ class Informer:
         """The reserve pod's cpuset in NodeAllocation (ReservationToPodEventHandler ->
         podEventHandler, nodenumaresource/pod_eventhandler.go:40-50,94-144)."""
         uid = r.uid or f"reservation/{r.name}"
-        if not r.node_name:
+        if not r.node_name or r.pod is not None:  # (an operating-mode pod's cpuset is its own: _numa_pod)
             return
         alloc = self._alloc.setdefault(r.node_name, nm.NodeAllocation())
         opts = self._topo.get(r.node_name)

@@ -161,6 +161,8 @@ class Pod:
     node_name: str = ""
     qos_status: str = ""          # Status.QOSClass
     phase: str = "Running"
+    ready: bool = True            # the Ready condition (k8spodutil.IsPodReady)
+    deleting: bool = False        # metadata.deletionTimestamp set
     owner_refs: List[OwnerReference] = field(default_factory=list)
     api_version: str = "v1"
     # what the upstream static filters read (nodefilters.py): spec.nodeSelector,

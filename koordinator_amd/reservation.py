@@ -292,6 +292,11 @@ class Reservation:
     assigned_cpus: List[int] = field(default_factory=list)
     cpu_exclusive: str = ""                                        # the reserve pod's preferredCPUExclusivePolicy
     spec_node_name: str = ""                                       # Spec.Template.Spec.NodeName (a pinned reservation)
+    # a bound pod in the reservation operating mode (operating_pod_reservation):
+    # the pod is its own reserve pod; parse_error: its owners annotation did not
+    # parse (ReservationInfo.ParseError: it matches no pod)
+    pod: Optional[k8s.Pod] = None
+    parse_error: bool = False
 
     def reserved_cpus(self) -> List[int]:
         """RestoreReservation's reservedCPUs of this reservation: its allocated
@@ -303,6 +308,8 @@ class Reservation:
         return bool(self.node_name) and self.phase == "Available"
 
     def reserve_pod(self) -> k8s.Pod:
+        if self.pod is not None:
+            return self.pod
         return k8s.Pod(name=f"reserve-{self.name}", containers=list(self.template) or
                        [k8s.Container(requests=dict(self.allocatable))])
 
@@ -362,6 +369,73 @@ LABEL_POD_OPERATING_MODE = "scheduling.koordinator.sh/operating-mode"
 def is_reservation_operating_pod(pod: k8s.Pod) -> bool:
     """IsReservationOperatingMode, apis/extension/operating_pod.go:51-53."""
     return (pod.labels or {}).get(LABEL_POD_OPERATING_MODE) == "Reservation"
+
+
+ANNOTATION_RESERVATION_OWNERS = "scheduling.koordinator.sh/reservation-owners"
+ANNOTATION_RESERVATION_CURRENT_OWNER = "scheduling.koordinator.sh/reservation-current-owner"
+
+
+def _owner_from_json(o: dict) -> ReservationOwner:
+    def ref(d, cls, keys):
+        if d is None:
+            return None
+        return cls(**{k: d.get(j, "") for k, j in keys})
+    obj = ref(o.get("object"), ObjectRef, [("uid", "uid"), ("name", "name"), ("namespace", "namespace"),
+                                           ("api_version", "apiVersion")])
+    ctl = o.get("controller")
+    ctrl = None if ctl is None else ControllerRef(kind=ctl.get("kind", ""), name=ctl.get("name", ""),
+                                                  uid=ctl.get("uid", ""), api_version=ctl.get("apiVersion", ""),
+                                                  namespace=ctl.get("namespace", ""), controller=ctl.get("controller"))
+    ls = o.get("labelSelector")
+    sel = None
+    if ls is not None:
+        sel = LabelSelector(match_labels=dict(ls.get("matchLabels") or {}),
+                            match_expressions=[LabelSelectorRequirement(x.get("key", ""), x.get("operator", ""),
+                                                                        list(x.get("values") or []))
+                                               for x in ls.get("matchExpressions") or []])
+    return ReservationOwner(object=obj, controller=ctrl, label_selector=sel)
+
+
+def operating_reservation_name(pod: k8s.Pod) -> str:
+    return f"operating-pod/{pod.namespace}/{pod.name}"
+
+
+def operating_pod_reservation(pod: k8s.Pod) -> Optional[Reservation]:
+    """The reservation cache's entry for a bound pod in the reservation
+    operating mode (pod_eventhandler.go:104-124 -> cache.go:139-161,
+    NewReservationInfoFromPod, frameworkext/reservation_info.go:101-126):
+    Allocatable / ResourceNames = its PodRequestsAndLimits requests, owners from
+    its reservation-owners annotation (a parse error: it matches no pod), always
+    AllocateOnce (reservation_info.go:185-194), AllocatePolicy Aligned
+    (:196-204), Available while the pod runs and is Ready (:238-246),
+    unschedulable while terminating (:248-255), and its reservation-current-
+    owner annotation as an assigned pod (cache.go:152-160; with AllocateOnce
+    that takes it out of matching).  The pod itself is its reserve pod (a
+    NodeInfo pod already).  None for any other pod."""
+    if not is_reservation_operating_pod(pod) or not pod.node_name:
+        return None
+    reqs, _ = k8s.pod_requests_and_limits(pod)
+    ann = pod.annotations or {}
+    owners, perr = [], False
+    raw = ann.get(ANNOTATION_RESERVATION_OWNERS, "")
+    if raw:
+        try:
+            owners = [_owner_from_json(o) for o in json.loads(raw)]
+        except (ValueError, TypeError, AttributeError):
+            owners, perr = [], True
+    assigned = 0
+    cur = ann.get(ANNOTATION_RESERVATION_CURRENT_OWNER, "")
+    if cur:
+        try:
+            json.loads(cur)
+            assigned = 1
+        except ValueError:
+            assigned = 0              # (logged by the reference; no owner added)
+    return Reservation(name=operating_reservation_name(pod), node_name=pod.node_name,
+                       phase="Available" if (pod.phase == "Running" and pod.ready) else "Pending",
+                       uid=pod.uid, labels=dict(pod.labels or {}), owners=owners, allocatable=dict(reqs),
+                       allocated={}, assigned=assigned, allocate_once=True, allocate_policy=POLICY_ALIGNED,
+                       deleting=pod.deleting, pod=pod, parse_error=perr)
 
 
 def parse_order(labels: Dict[str, str]) -> int:
@@ -503,7 +577,7 @@ def _reservation_slot(table: NodeTable, i: int, q: int, r: Reservation, index: "
     extra = names - {k8s.CPU, k8s.MEMORY}
     if extra:
         raise ReservationError(f"reservation {r.name}: resources {sorted(extra)} are not supported")
-    parse_ok = True
+    parse_ok = not r.parse_error
     try:
         for o in r.owners:
             if o.label_selector is not None:

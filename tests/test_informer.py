@@ -560,3 +560,64 @@ def test_reserve_pod_through_the_informer():
     assert recs2["resv_match"][0] != 0
     o2 = oracle.Oracle(to_c_config(prof), t2)
     assert o2.place_stream(recs2)[0] == 5                 # the reservation's node wins (weight 5000)
+
+
+def test_operating_mode_pod_is_a_reservation():
+    """A bound pod in the reservation operating mode is also an Available
+    reservation on its node (pod_eventhandler.go:104-124, cache.go:139-168,
+    NewReservationInfoFromPod): its requests are the slot's Allocatable, its
+    reservation-owners annotation the owners, AllocateOnce and Aligned always;
+    Ready gates it, a current owner takes it out of matching, deleting the pod
+    removes the slot.  A matching pod nominates it and fits through the
+    restore where a non-matching one does not (oracle)."""
+    import json as _json
+    import oracle
+    from koordinator_amd import abi
+    from koordinator_amd import reservation as rv
+    from koordinator_amd.config import to_c_config
+    prof = shipped_profile(reservation=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(8), k8s.MEMORY: k8s.Q(16 * GI), k8s.PODS: k8s.Q(110)})
+             for i in range(4)]
+    inf = Informer(prof, nodes, NOW)
+    # every node but n2 is full; n2 holds the operating pod (6 cpu / 12 Gi) and a 1-cpu pod
+    for i in (0, 1, 3):
+        inf.on_pod_add(k8s.Pod(name=f"filler-{i}", uid=f"f{i}", node_name=f"n{i}", containers=[
+            k8s.Container(requests={k8s.CPU: k8s.Q(8), k8s.MEMORY: k8s.Q(16 * GI)})]), NOW)
+    owners = [{"labelSelector": {"matchLabels": {"app": "web"}}}]
+    op = k8s.Pod(name="op-0", uid="op0", node_name="n2",
+                 labels={rv.LABEL_POD_OPERATING_MODE: "Reservation"},
+                 annotations={rv.ANNOTATION_RESERVATION_OWNERS: _json.dumps(owners)},
+                 containers=[k8s.Container(requests={k8s.CPU: k8s.Q(6), k8s.MEMORY: k8s.Q(12 * GI)})])
+    inf.on_pod_add(op, NOW)
+    inf.on_pod_add(k8s.Pod(name="other", uid="o1", node_name="n2", containers=[
+        k8s.Container(requests={k8s.CPU: k8s.Q(1), k8s.MEMORY: k8s.Q(GI)})]), NOW)
+    t = inf.table(NOW)
+    f = int(t["resv_flags"][2])
+    assert f & abi.RESV_PRESENT and f & abi.RESV_ALLOCATE_ONCE
+    assert (f >> abi.RESV_POLICY_SHIFT) & 3 == abi.RESV_POLICY_ALIGNED
+    assert int(t["resv_alloc0"][2]) == 6000 and int(t["resv_alloc1"][2]) == 12 * GI
+    assert int(t["resv_assigned"][2]) == 0 and not any(int(t["resv_flags"][i]) for i in (0, 1, 3))
+    web = k8s.Pod(name="web-0", labels={"app": "web"},
+                  containers=[k8s.Container(requests={k8s.CPU: k8s.Q(4), k8s.MEMORY: k8s.Q(4 * GI)})])
+    db = k8s.Pod(name="db-0", labels={"app": "db"},
+                 containers=[k8s.Container(requests={k8s.CPU: k8s.Q(4), k8s.MEMORY: k8s.Q(4 * GI)})])
+    recs = inf.pod_records([web, db])
+    assert recs["resv_match"][0] != 0 and recs["resv_match"][1] == 0
+    got = oracle.Oracle(to_c_config(prof), t).place_stream(recs)
+    assert got[0] == 2 and got[1] < 0       # only the owner fits, into the operating pod's reservation
+    # a current owner: AllocateOnce with an assigned pod -> no longer matchable
+    op2 = copy.deepcopy(op)
+    op2.annotations[rv.ANNOTATION_RESERVATION_CURRENT_OWNER] = _json.dumps({"name": "web-9", "namespace": "default"})
+    inf.on_pod_update(op, op2, NOW)
+    t2 = inf.table(NOW)
+    assert int(t2["resv_assigned"][2]) == 1
+    assert oracle.Oracle(to_c_config(prof), t2).place_stream(inf.pod_records([web]))[0] < 0
+    # not Ready: not Available; deleted: no slot
+    op3 = copy.deepcopy(op)
+    op3.ready = False
+    inf.on_pod_update(op2, op3, NOW)
+    assert not int(inf.table(NOW)["resv_flags"][2])
+    inf.on_pod_update(op3, op, NOW)
+    assert int(inf.table(NOW)["resv_flags"][2]) & abi.RESV_PRESENT
+    inf.on_pod_delete(op)
+    assert not int(inf.table(NOW)["resv_flags"][2])
