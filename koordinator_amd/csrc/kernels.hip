@@ -1755,9 +1755,11 @@ struct ResLds {  // byte offsets into the dynamic LDS of k_resolve
 
 __host__ __device__ inline int32_t res_align(int32_t x) { return (x + 15) & ~15; }
 
+// chain: room for the chained decisions' dependency masks (the plain and NUMA
+// builds; the Reservation builds are never monotone, and their rows need the LDS)
 __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_t n_nodes, int32_t nrow,
                                           bool overlap = false, bool tables = true, int32_t lag = 1,
-                                          bool wide = false) {
+                                          bool wide = false, bool chain = true) {
   const bool numa = nrow > 0;  // nrow: bytes of a NUMA side row (0: none)
   ResLds o;
   int32_t at = 0;
@@ -1798,8 +1800,8 @@ __host__ __device__ inline ResLds res_lds(int32_t n_pods_max, int32_t kp, int32_
   at += RES_MAXP_ROUND * RES_WE * 4;
   o.dec_c = at;  // per pod: bit 0 = its walk met an earlier pod's staged winner, bit 1 = general path only
   at += RES_MAXP_ROUND * 4;
-  o.dep = at;
-  at += RES_MAXP_ROUND * 8;
+  o.dep = chain ? at : -1;
+  at += chain ? RES_MAXP_ROUND * 8 : 0;
   o.moved = at;  // per M' slot: committed to again this round (its row moved into M)
   at += RES_MAXP_ROUND * 4;
   o.mhash = at;  // lazy staged rows: the pod of each M slot, the M slot of each pod
@@ -1949,6 +1951,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     return *p;
   };
   const bool two = kp > 64;
+  const bool chain_on = (monotone & 2) && ofs.dep >= 0;  // the chained decisions (phase 2c)
   const uint64_t t_kernel = (dbg && t == 0) ? stamp() : 0;
   if (t == 0) {
     sh_mp = r_begin > 0 ? min(mbuf[0], P) : 0;
@@ -2299,8 +2302,9 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       }
     }
     __syncthreads();
-    uint64_t *dep = reinterpret_cast<uint64_t *>(lds + ofs.dep);
-    for (int32_t x = t; x < n_pods; x += RES_THREADS) dep[x] = 0ull;
+    uint64_t *dep = ofs.dep >= 0 ? reinterpret_cast<uint64_t *>(lds + ofs.dep) : nullptr;
+    if (dep)
+      for (int32_t x = t; x < n_pods; x += RES_THREADS) dep[x] = 0ull;
     if (dbg && t == 0) {
       const uint64_t t_p3 = stamp();
       c_hash += t_a - t_entry;
@@ -2324,7 +2328,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       //      entries, stays on the general path.  Each pass re-checks the valid
       //      pods against the valid claims and closes the dependencies in pod
       //      order; up to RES_CHAIN_PASSES passes, eight pods per lane group.
-      if (monotone & 2) {
+      if (chain_on) {
         const uint64_t t_c0 = dbg ? stamp() : 0;
         auto wsync = [&]() {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2509,7 +2513,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         for (int q = 0; q < RES_WE; q++) se[q] = dec_e[lane * RES_WE + q];
       }
       const uint64_t prodmask = __ballot(live && (fl & KOORDHIP_POD_PROD));
-      const uint64_t mydep = live ? dep[lane] : 0ull;  // the staged commits this pod's chained decision assumed
+      const uint64_t mydep = (dep && live) ? dep[lane] : 0ull;  // the staged commits this pod's chained decision assumed
       // general-path-only pods and conflicts: from the prologue (phase 2 / 2b)
       const int32_t dc = live ? dec_c[lane] : 2;
       const bool slow = (dc & 2) != 0;
@@ -3047,7 +3051,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
       //      path, monotone): those pods are dealt round-robin to the waves.
       const int hw = __builtin_amdgcn_readfirstlane((t >> 6) - 1 - res_loaders<NM>()),
                 nh = RES_THREADS / 64 - 1 - res_loaders<NM>();
-      if (monotone & 2)  // wave 0's chained decisions first (they rewrite the staged decisions)
+      if (chain_on)  // wave 0's chained decisions first (they rewrite the staged decisions)
         while (!__hip_atomic_load(&sh_chain, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) __builtin_amdgcn_s_sleep(1);
       uint64_t todo = __ballot(lane < n_pods && dec_c[lane] == 1);
       for (int32_t x = 0; x < hw && todo; x++) todo &= todo - 1ull;
@@ -3575,7 +3579,7 @@ static int32_t side_row_bytes(int nm) {
 
 int32_t resolve_lds_bytes(int32_t n_pods_max, int32_t k, int32_t n_nodes, int nm, int32_t lag) {
   const int32_t kp = list_stride(k);
-  return res_lds(n_pods_max, kp, n_nodes, side_row_bytes(nm), false, false, lag).total;
+  return res_lds(n_pods_max, kp, n_nodes, side_row_bytes(nm), false, false, lag, false, nm <= 2).total;
 }
 
 hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_desc, const DevPod *pods, int32_t total, int32_t P, int32_t k,
@@ -3596,10 +3600,11 @@ hipError_t launch_resolve(const DevCfg &c, const DevNodes &d, const DevNodes *d_
   const bool pre = r_end - r_begin > 1 && !std::getenv("KOORDHIP_NO_PRELOAD");
   const bool tab = !std::getenv("KOORDHIP_NO_KEY_TABLES");
   const bool wide = c.wide_keys != 0;
-  ResLds o = res_lds(P, kp, d.n, nrow, pre, tab, lag, wide);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag, wide);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag, wide);
-  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag, wide);
+  const bool chain = nm <= 2;
+  ResLds o = res_lds(P, kp, d.n, nrow, pre, tab, lag, wide, chain);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, tab, lag, wide, chain);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, pre, false, lag, wide, chain);
+  if (o.total > RES_LDS_MAX) o = res_lds(P, kp, d.n, nrow, false, false, lag, wide, chain);
   static bool attr[12] = {};
   const int ai = nm * 2 + (dbg ? 1 : 0);
   if (!attr[ai]) {
