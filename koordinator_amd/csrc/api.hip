@@ -2778,16 +2778,23 @@ int place_staged_impl(koordhip_ctx *c) {
     // needc[e]: the device pods of the rounds before round(e) - lag, whose
     // device commits device pod e's pre-evaluation must see (later ones' nodes
     // are in the resolve's X set at e's hand-off)
+    // lead: the pre-evaluation runs on the state after round(e) - lead - 1, i.e.
+    // `lead` rounds before the pod's round may start (the rounds between lag and
+    // lead add their commits, from the commit log, to the final phase's X).
+    // lag by default: config4dsmix measured 846k / 787k / 750k pods/s at lead 2 /
+    // 5 / 8 (r05q) -- the longer X re-evaluates more nodes at the hand-off
+    const char *ld = std::getenv("KOORDHIP_EXT_LEAD");
+    const int32_t lead = std::max(lag, ld ? std::atoi(ld) : lag);
     const int32_t ne = (int32_t)c->ext_idx.size();
     c->ext_needc.assign(ne, 0);
     for (int32_t e = 0, q = 0; e < ne; e++) {
       const int32_t ue = c->ext_idx[e] / P;
-      while (q < e && c->ext_idx[q] / P < ue - lag) q++;
+      while (q < e && c->ext_idx[q] / P < ue - lead) q++;
       c->ext_needc[e] = q;
     }
     HIP_TRY(hipMemcpyAsync(c->d_ext_idx + ne, c->ext_needc.data(), (size_t)ne * sizeof(int32_t), hipMemcpyHostToDevice,
                            c->xstream));
-    HIP_TRY(kh::launch_ext_worker(c->dc, c->d, c->d_pods, c->d_podx, c->d_ext_idx, c->d_ext_idx + ne, ne, P, lag,
+    HIP_TRY(kh::launch_ext_worker(c->dc, c->d, c->d_pods, c->d_podx, c->d_ext_idx, c->d_ext_idx + ne, ne, P, lag, lead,
                                   c->n_cu, c->d_ext_scr, c->d_out, c->d_devout, sync,
                                   c->d_dbg, c->xstream));
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));

@@ -53,9 +53,9 @@ hipError_t launch_commit_ext(const DevCfg &c, const DevNodes &d, const DevPod *p
 // Device pods inside the pipelined greedy (plain build, seq_mode 0): ONE
 // persistent launch per place call on its own stream; ext_idx[0 .. n_ext) the
 // staged indices of the KH_POD_EXT pods in stream order, needc[e] the device
-// pods of the rounds before round(e) - lag (whose device commits device pod e's
-// pre-evaluation must see).  Per pod: the pre-evaluation once the pod's round
-// may be evaluated, then at sync->ext_req the exact placement (the resolve's
+// pods of the rounds before round(e) - lead (whose device commits device pod e's
+// pre-evaluation must see; lead >= lag).  Per pod: the pre-evaluation on the state
+// after round(e) - lead - 1, then at sync->ext_req the exact placement (the resolve's
 // X nodes evaluated again, normalized DeviceShare Score), out_node and
 // sync->ext_done, then DeviceShare's Reserve without the Fit / LoadAware row and
 // out_dev.  scratch: ext_worker_scratch_bytes(n_ext, n) (its front zeroed here).
@@ -65,8 +65,8 @@ size_t ext_worker_scratch_bytes(int32_t n_ext, int32_t n);
 size_t ext_worker_diag_offset(int32_t n_ext);
 hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx,
                              const int32_t *ext_idx, const int32_t *needc, int32_t n_ext, int32_t P, int32_t lag,
-                             int32_t n_cu, void *scratch, int32_t *out_node, uint32_t *out_dev, PipeSync *sync,
-                             uint64_t *dbg, hipStream_t s);
+                             int32_t lead, int32_t n_cu, void *scratch, int32_t *out_node, uint32_t *out_dev,
+                             PipeSync *sync, uint64_t *dbg, hipStream_t s);
 hipError_t launch_mark_ext(DevPod *pods, const int32_t *idx, int32_t n, hipStream_t s);
 // the k_seq instantiation launch_seq runs for this config, as rocprofv3 names it
 const char *seq_kernel_name(const DevCfg &c);

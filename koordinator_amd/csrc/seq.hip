@@ -479,7 +479,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
                                                             const DevPodX *__restrict__ podx,
                                                             const int32_t *__restrict__ ext_idx,
                                                             const int32_t *__restrict__ needc, int32_t n_ext, int32_t P,
-                                                            int32_t lag, int32_t gf, uint64_t *__restrict__ tab,
+                                                            int32_t lag, int32_t lead, int32_t gf,
+                                                            uint64_t *__restrict__ tab,
                                                             uint32_t *__restrict__ cnt, uint64_t *__restrict__ pk,
                                                             int32_t *__restrict__ pr, const int32_t *__restrict__ perm,
                                                             int32_t *__restrict__ out_node,
@@ -551,7 +552,7 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
       uint32_t *cw = cnt + (size_t)EXT_CW * e;  // {pre claimed, pre finished, final claimed, final finished}
       const uint64_t tp0 = dbg ? stamp() : 0;
       if (t == 0)
-        s_go = ((u <= lag || wait_at_least_idle(&sy->res_round, u - lag, sy)) && wait_at_least_idle(cdone, needc[e], sy) &&
+        s_go = ((u <= lead || wait_at_least_idle(&sy->res_round, u - lead, sy)) && wait_at_least_idle(cdone, needc[e], sy) &&
                 (e < EXT_RING || wait_at_least_idle(&sy->ext_done, ext_idx[e - EXT_RING] + 1, sy)))
                    ? 1
                    : 0;
@@ -599,12 +600,21 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
     }
     const uint64_t t1 = dbg ? stamp() : 0;
     const int32_t nx = xl[0];
+    // the pre-evaluation saw the state after round u - lead - 1: the nodes
+    // committed since are the resolve's X (rounds u - lag .. u) and the commit
+    // log of rounds u - lead .. u - lag - 1 (out_node, written through, complete)
+    const int32_t u = gp / P;
+    const int32_t xlo = max(0, u - lead) * P, xhi = max(0, u - lag) * P;
     const int32_t done = claim_all(cw + 2, ncf, [&](int32_t ch) {
       const int32_t c0 = ch * EXT_FCHUNK;
       for (int32_t w = t; w < EXT_FCHUNK / 32; w += EXT_THREADS) xm[w] = 0u;
       __syncthreads();
       for (int32_t q = t; q < nx; q += EXT_THREADS) {
         const int32_t y = xl[1 + q] - c0;
+        if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
+      }
+      for (int32_t q = xlo + t; q < xhi; q += EXT_THREADS) {
+        const int32_t y = __hip_atomic_load(&out_node[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - c0;
         if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
       }
       __syncthreads();
@@ -794,9 +804,10 @@ size_t ext_worker_diag_offset(int32_t n_ext) {
 
 hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx,
                              const int32_t *ext_idx, const int32_t *needc, int32_t n_ext, int32_t P, int32_t lag,
-                             int32_t n_cu, void *scratch, int32_t *out_node, uint32_t *out_dev, PipeSync *sync,
-                             uint64_t *dbg, hipStream_t s) {
+                             int32_t lead, int32_t n_cu, void *scratch, int32_t *out_node, uint32_t *out_dev,
+                             PipeSync *sync, uint64_t *dbg, hipStream_t s) {
   if (n_ext <= 0) return hipSuccess;
+  if (lead < lag) return hipErrorInvalidValue;
   if (seq_mode(c) != 0 || P <= 0) return hipErrorInvalidValue;  // the plain build only (the route checks it)
   char *base = static_cast<char *>(scratch);
   uint64_t *tab = reinterpret_cast<uint64_t *>(base);
@@ -809,7 +820,7 @@ hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *p
   if (hipError_t e = hipMemsetAsync(scratch, 0, ext_front_bytes(n_ext), s)) return e;
   hipLaunchKernelGGL(k_ext_perm, dim3((d.n + 255) / 256), dim3(256), 0, s, d.dv, d.n, perm, pc);
   hipLaunchKernelGGL(k_ext_worker<0>, dim3(grid), dim3(EXT_THREADS), 0, s, c, d, pods, podx, ext_idx, needc, n_ext, P,
-                     lag, gf, tab, cnt, pk, pr, perm, out_node, out_dev, sync, dbg);
+                     lag, lead, gf, tab, cnt, pk, pr, perm, out_node, out_dev, sync, dbg);
   return hipGetLastError();
 }
 
