@@ -2903,8 +2903,14 @@ int place_staged_impl(koordhip_ctx *c) {
                    q[3] / nl, q[4] / nl, q[5] / nl, q[6] / nl, (unsigned long long)q[15], q[8] / nc, q[9] / nc, q[10] / nc,
                    q[11] / nc, q[12] / nc);
     }
-    std::fprintf(stderr, "[koordhip stamps] chained decisions: %llu cycles, %llu pods resolved\n",
-                 (unsigned long long)h[62], (unsigned long long)h[63]);
+    {
+      uint64_t q[4] = {0, 0, 0, 0};
+      HIP_TRY(hipMemcpy(q, c->d_dbg + 90, sizeof(q), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[koordhip stamps] chained decisions: %llu cycles, %llu pods resolved | claim tables %llu  "
+                   "re-walks %llu  re-check + closure %llu  final table %llu\n", (unsigned long long)h[62],
+                   (unsigned long long)h[63], (unsigned long long)q[0], (unsigned long long)q[1],
+                   (unsigned long long)q[2], (unsigned long long)q[3]);
+    }
     if (ext_pipe) {
       uint64_t q[8], q8[2] = {0, 0};
       HIP_TRY(hipMemcpy(q, c->d_dbg + 80, sizeof(q), hipMemcpyDeviceToHost));

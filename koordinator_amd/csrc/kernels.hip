@@ -1710,7 +1710,8 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
 template <int NM>
 constexpr int res_threads() { return NM ? 256 : 512; }
 // waves 1 .. RES_LOADERS load the next round while wave 0 resolves this one
-// (the rest build key tables): three of eight, one of four
+// (the rest build key tables): three of eight, one of four (seven of eight
+// measured no faster with the chained decisions, r05o)
 template <int NM>
 constexpr int res_loaders() { return res_threads<NM>() >= 512 ? 3 : 1; }
 
@@ -2018,6 +2019,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t c_cand = 0, n_evpass = 0, n_tready = 0;  // general path: list + X + c cycles, evaluation passes, pods with ready tables
   uint64_t c_gc[3] = {0, 0, 0}, n_ghit = 0;          // general commit: row source, Reserve delta, voiding + outputs; winners in M
   uint64_t c_chain = 0;                              // chained decisions: cycles (pods resolved: dbg[63])
+  uint64_t c_ch[4] = {0, 0, 0, 0};                   // ... split: claim tables, re-walks, re-check + closure, final table
   uint64_t c_ext = 0, n_ext = 0;                     // device pods: cycles from the hand-off to the worker's answer, pods
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
@@ -2368,9 +2370,18 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         // fresh: ckey / cval hold exactly the valid pods' claims
         const int npass = ((monotone >> 2) & 3) ? ((monotone >> 2) & 3) : RES_CHAIN_PASSES;
         bool fresh = false;
+        uint64_t tc = dbg ? stamp() : 0;
+        auto clap = [&](int ph) {
+          if (dbg) {
+            const uint64_t x = stamp();
+            c_ch[ph] += x - tc;
+            tc = x;
+          }
+        };
         for (int pass = 0; pass < npass; pass++) {
           if (!fresh) claims();
           fresh = true;
+          clap(0);
           uint64_t conf = __ballot(lane < n_pods && dec_c[lane] == 1);
           if (!conf) break;
           bool resolved = false;
@@ -2458,6 +2469,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             resolved = resolved || (__ballot(ok2) != 0ull);
             wsync();
           }
+          clap(1);
           if (!resolved) break;
           // re-check: a valid pod whose walk meets a valid claim it did not assume
           claims();
@@ -2488,8 +2500,10 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           }
           wsync();
           fresh = !inv;  // (an invalidated pod's claim is still in the table)
+          clap(2);
         }
         if (!fresh) claims();  // the loop's claimer(): the valid pods' winners
+        clap(3);
         if (lane == 0) __hip_atomic_store(&sh_chain, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (dbg) c_chain += stamp() - t_c0;
       }
@@ -3153,6 +3167,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[60], (unsigned long long)c_gc[2]);
     atomicAdd((unsigned long long *)&dbg[61], (unsigned long long)n_ghit);
     atomicAdd((unsigned long long *)&dbg[62], (unsigned long long)c_chain);
+    for (int q = 0; q < 4; q++) atomicAdd((unsigned long long *)&dbg[90 + q], (unsigned long long)c_ch[q]);
     atomicAdd((unsigned long long *)&dbg[30], (unsigned long long)c_ext);
     atomicAdd((unsigned long long *)&dbg[31], (unsigned long long)n_ext);
   }

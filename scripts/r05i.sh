@@ -17,3 +17,5 @@ KOORDHIP_EXT_SEQ=1 timeout -k 10 300 python bench.py --workload config4dsmix --s
 python -c "import json;d=json.load(open('gpurun_out/r05i_dsmix_seq.json'));print('dsmix sequential cycle', d['value'], d['ms_per_step'])"
 timeout -k 10 300 python bench.py --workload config4 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/r05i_c4.json 2> gpurun_out/r05i_c4.err || { tail -20 gpurun_out/r05i_c4.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/r05i_c4.json'));print('config4', d['value'], d['ms_per_step'])"
+timeout -k 10 300 python bench.py --workload deviceshare --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/r05i_ds.json 2> gpurun_out/r05i_ds.err || { tail -20 gpurun_out/r05i_ds.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/r05i_ds.json'));print('deviceshare', d['value'], d['ms_per_step'], d['config']['parallelism'])"
