@@ -2912,17 +2912,19 @@ int place_staged_impl(koordhip_ctx *c) {
                    (unsigned long long)q[2], (unsigned long long)q[3]);
     }
     if (ext_pipe) {
-      uint64_t q[8], q8[2] = {0, 0};
+      uint64_t q[8], q8[2] = {0, 0}, q94[2] = {0, 0};
       HIP_TRY(hipMemcpy(q, c->d_dbg + 80, sizeof(q), hipMemcpyDeviceToHost));
       HIP_TRY(hipMemcpy(q8, c->d_dbg + 88, sizeof(q8), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(q94, c->d_dbg + 94, sizeof(q94), hipMemcpyDeviceToHost));
       const double np = (double)std::max<uint64_t>(q[6], 1);
       std::fprintf(stderr, "[koordhip stamps] device pods (k_ext_worker): %llu, resolve cycles from the hand-off to the "
                    "answer %llu (%.0f per pod) | worker per pod: workgroup 0 waiting %.0f  evaluating %.0f  merge + "
                    "arrival %.0f (chunks %.2f) | pre-evaluation workgroup: waiting %.0f  evaluating %.0f | last "
-                   "workgroup reduce %.0f  publish %.0f  device commit (after the hand-off) %.0f\n",
+                   "workgroup reduce %.0f  publish %.0f  device commit (after the hand-off) %.0f | after the "
+                   "hand-off, workgroup 0 waits for the previous device commit %.0f, the pre-evaluation %.0f\n",
                    (unsigned long long)h[31], (unsigned long long)h[30], h[31] ? (double)h[30] / h[31] : 0.0,
                    q[0] / np, q[1] / np, q[2] / np, q[7] / np, (double)q8[1] / np, (double)q8[0] / np, q[3] / np,
-                   q[5] / np, q[4] / np);
+                   q[5] / np, q[4] / np, (double)q94[0] / np, (double)q94[1] / np);
     }
     std::fprintf(stderr, "[koordhip stamps] general commit split: row source %llu  Reserve delta %llu  voiding + "
                  "outputs %llu cycles | winners already in M %llu\n",

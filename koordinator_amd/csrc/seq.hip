@@ -504,7 +504,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
   // workgroup gf's cycles waiting [89] and evaluating [88]; the last final
   // workgroup's reduce, device commit (after the hand-off), publish [83..85],
   // pods [86]
-  uint64_t c_w = 0, c_e = 0, c_m = 0, c_r = 0, c_c = 0, c_p = 0, n_l = 0, n_ch = 0, c_pre = 0, c_pw = 0;
+  uint64_t c_w = 0, c_e = 0, c_m = 0, c_r = 0, c_c = 0, c_p = 0, n_l = 0, n_ch = 0, c_pre = 0, c_pw = 0, c_dc = 0,
+           c_pe = 0;
   // claim chunks of a phase until none is left; f(chunk) per claimed chunk
   auto claim_all = [&](uint32_t *claim, int32_t nch, auto f) -> int32_t {
     int32_t done = 0;
@@ -586,7 +587,13 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
     //      this pod's pre-evaluation published
     for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
     const uint64_t t0 = dbg ? stamp() : 0;
-    if (t == 0) s_go = (wait_at_least(&sy->ext_req, gp + 1, sy) && wait_at_least(cdone, e, sy)) ? 1 : 0;
+    uint64_t tw1 = 0, tw2 = 0;
+    if (t == 0) {
+      s_go = wait_at_least(&sy->ext_req, gp + 1, sy) ? 1 : 0;
+      tw1 = dbg ? stamp() : 0;
+      s_go = s_go && wait_at_least(cdone, e, sy);
+      tw2 = dbg ? stamp() : 0;
+    }
     __syncthreads();
     // the pre-evaluation chunks nobody has claimed yet (every condition of the
     // pre-evaluation holds at the hand-off): the final workgroups never wait
@@ -594,6 +601,10 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
     if (s_go) pre_eval(e);
     if (t == 0 && s_go) s_go = wait_at_least(reinterpret_cast<const int32_t *>(cw + 1), ncp, sy) ? 1 : 0;
     __syncthreads();
+    if (dbg && b == 0 && t == 0) {  // after the hand-off: the previous device commit, then the pre-evaluation
+      c_dc += tw2 - tw1;
+      c_pe += stamp() - tw2;
+    }
     if (!s_go) {
       if (t == 0) atomicMax(cdone + 1, (e << 4) | 2);
       break;
@@ -727,6 +738,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d
       atomicAdd((unsigned long long *)&dbg[81], (unsigned long long)c_e);
       atomicAdd((unsigned long long *)&dbg[82], (unsigned long long)c_m);
       atomicAdd((unsigned long long *)&dbg[87], (unsigned long long)n_ch);
+      atomicAdd((unsigned long long *)&dbg[94], (unsigned long long)c_dc);
+      atomicAdd((unsigned long long *)&dbg[95], (unsigned long long)c_pe);
     }
     atomicAdd((unsigned long long *)&dbg[83], (unsigned long long)c_r);
     atomicAdd((unsigned long long *)&dbg[84], (unsigned long long)c_c);
