@@ -311,8 +311,11 @@ int download_q(double *src, int64_t *dst, size_t count) {
   return 0;
 }
 
-// koordhip_pod (ABI) -> DevPod (device record)
-int to_dev_pods(const koordhip_pod *src, int32_t n, std::vector<kh::DevPod> &out) {
+// koordhip_pod (ABI) -> DevPod (device record).  ext (optional, the pods'
+// koordhip_pod_ext records) with `devshare` (DeviceShare in the profile): the
+// device pods get kh::KH_POD_DEVSHARE.
+int to_dev_pods(const koordhip_pod *src, int32_t n, std::vector<kh::DevPod> &out,
+                const koordhip_pod_ext *ext = nullptr, bool devshare = false) {
   out.resize(std::max(n, 0));
   for (int32_t j = 0; j < n; j++) {
     const koordhip_pod &p = src[j];
@@ -326,8 +329,10 @@ int to_dev_pods(const koordhip_pod *src, int32_t n, std::vector<kh::DevPod> &out
     o.nz_mem = (double)p.nz_mem;
     o.est_cpu = (double)p.est_cpu;
     o.est_mem = (double)p.est_mem;
-    if (p.flags & kh::KH_POD_EXT) return fail(KOORDHIP_EINVAL, "koordhip_pod.flags bit 30 is reserved");
+    if (p.flags & (kh::KH_POD_EXT | kh::KH_POD_DEVSHARE))
+      return fail(KOORDHIP_EINVAL, "koordhip_pod.flags bits 29-30 are reserved");
     o.flags = p.flags;
+    if (devshare && ext && (ext[j].flags & KOORDHIP_PODX_DEVICE)) o.flags |= kh::KH_POD_DEVSHARE;
     o.numa_cpus = p.numa_cpus;
     o.numa_policy = p.numa_policy;
     if (p.static_class < 0 || p.static_class >= KOORDHIP_MAX_STATIC_CLASSES)
@@ -1858,13 +1863,18 @@ static int stage_classes(koordhip_ctx *c, const std::vector<kh::DevPod> &hp) {
   return 0;
 }
 
-int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods) {
+static bool devshare_on(const koordhip_ctx *c) {
+  return ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+}
+
+// ext (optional): the pods' records, for kh::KH_POD_DEVSHARE (staged by stage_ext)
+static int stage_pods_impl(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, const koordhip_pod_ext *ext) {
   if (!c || (!pods && n_pods > 0)) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (n_pods < 0) return fail(KOORDHIP_EINVAL, "n_pods < 0");
   bool reserve = false;
   if (int e = check_reserve_pods(c, pods, n_pods, &reserve)) return e;
   std::vector<kh::DevPod> hp;
-  if (int e = to_dev_pods(pods, n_pods, hp)) return e;
+  if (int e = to_dev_pods(pods, n_pods, hp, ext, devshare_on(c))) return e;
   HIP_TRY(hipSetDevice(c->device));
   if (n_pods > c->pods_cap) {
     if (c->d_pods) HIP_TRY(hipFree(c->d_pods));
@@ -1897,6 +1907,10 @@ int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pod
     c->staged_qos_nonbind = (pods[j].flags & KOORDHIP_POD_CPUSET_QOS) && pods[j].resv_match != 0 &&
                             !(pods[j].flags & (KOORDHIP_POD_CPUSET | KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));
   return 0;
+}
+
+int koordhip_stage_pods(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods) {
+  return stage_pods_impl(c, pods, n_pods, nullptr);
 }
 
 // DeviceShare PreFilter products (PreparePod, deviceshare/plugin.go:162-182) validated
@@ -2012,7 +2026,7 @@ int koordhip_stage_pods_ext(koordhip_ctx *c, const koordhip_pod *pods, const koo
     for (int32_t j = 0; j < n_pods; j++)
       if (ext[j].reserve_node != 0 && !(pods[j].flags & KOORDHIP_POD_RESERVE))
         return fail(KOORDHIP_EINVAL, "koordhip_pod_ext.reserve_node set on a pod without KOORDHIP_POD_RESERVE");
-  if (int e = koordhip_stage_pods(c, pods, n_pods)) return e;
+  if (int e = stage_pods_impl(c, pods, n_pods, ext)) return e;
   return stage_ext(c, ext, n_pods);
 }
 
@@ -2131,7 +2145,7 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
       if (p) (void)hipFree(p);
   };
   std::vector<kh::DevPod> hp;
-  if (int ce = to_dev_pods(pods, n_pods, hp)) return ce;
+  if (int ce = to_dev_pods(pods, n_pods, hp, ext, devshare_on(c))) return ce;
   if (hipMalloc(&dp, (size_t)per * sizeof(kh::DevPod)) != hipSuccess ||
       (ext && hipMalloc(&dx, (size_t)per * sizeof(kh::DevPodX)) != hipSuccess) ||
       hipMalloc(&dst, (size_t)per * std::max(n, 1)) != hipSuccess ||
@@ -3164,7 +3178,7 @@ static int commit_ext_impl(koordhip_ctx *c, const koordhip_pod *pod, const koord
   uint64_t *d_cpus = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(c->d_rc) + sizeof(uint64_t));
   uint32_t *d_dev = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(c->d_rc) + 40);
   std::vector<kh::DevPod> hp;
-  if (int e = to_dev_pods(pod, 1, hp)) return e;
+  if (int e = to_dev_pods(pod, 1, hp, ext, devshare_on(c))) return e;
   HIP_TRY(hipMemcpyAsync(c->d_tmp_pod, hp.data(), sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_tmp_podx, ext, sizeof(kh::DevPodX), hipMemcpyHostToDevice, c->stream));
   uint64_t cz[KOORDHIP_NUMA_WORDS] = {0, 0, 0, 0};

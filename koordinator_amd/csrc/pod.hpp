@@ -30,4 +30,12 @@ static_assert(sizeof(DevPod) == 96, "DevPod is 96 bytes");
 // hands it the exact state and takes its node back.
 constexpr uint32_t KH_POD_EXT = 1u << 30;
 
+// Engine-internal flag bit (set by the host from the pod's koordhip_pod_ext;
+// to_dev_pods rejects it from callers): DeviceShare is in the profile and the
+// pod requests devices, so DeviceShare's FilterReservation takes part in the
+// reservation nomination (deviceshare/plugin.go:325-356) -- it fails every
+// reservation holding no devices, and none does in the engine's envelope, so
+// such a pod is nominated into no reservation (resv_nominate, resv.hpp).
+constexpr uint32_t KH_POD_DEVSHARE = 1u << 29;
+
 }  // namespace kh

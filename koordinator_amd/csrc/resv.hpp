@@ -285,9 +285,13 @@ __device__ __forceinline__ int32_t resv_score(const DevPod &p, const ResvSlot &r
 }
 
 // NominateReservation: among the matched candidates the smallest order label,
-// else the highest scoreReservation; ties -> the lowest slot.  -1: none.
+// else the highest scoreReservation; ties -> the lowest slot.  -1: none.  A
+// device pod under DeviceShare (KH_POD_DEVSHARE) passes DeviceShare's
+// FilterReservation on no reservation (none holds devices here: the restore
+// state has no entry for it, deviceshare/plugin.go:337-346), so it has none.
 template <int S>
 __device__ __forceinline__ int resv_nominate(const DevPod &p, const NumaRowRS<S> &r, uint32_t mm) {
+  if (p.flags & KH_POD_DEVSHARE) return -1;
   int best = -1, brk = 0;
   bool ord = false;
   int32_t bsc = -1;

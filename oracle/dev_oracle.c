@@ -17,10 +17,12 @@
  *
  * Reservations holding devices are outside the engine's envelope (the host
  * rejects them): RestoreReservation (reservation.go:119-170) then keeps no
- * reservation for DeviceShare, so Filter / Score / Reserve see the node alone,
- * except for a reservation the Reservation plugin nominated on the node: Score
- * returns 0 there (scoreWithNominatedReservation :409-431, allocIndex -1) and
- * Reserve fails (allocateWithNominatedReservation :379-393).
+ * reservation for DeviceShare, so Filter / Score / Reserve see the node alone.
+ * No reservation is nominated for a device pod either: DeviceShare's
+ * FilterReservation fails every reservation that holds no devices (see
+ * orc_resv_nominate), so the `nominated` branches below (Score 0,
+ * scoreWithNominatedReservation :409-431; Reserve failing,
+ * allocateWithNominatedReservation :379-393) are not reached from a stream.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -51,6 +53,13 @@ static int has_type(const orc_state *st, int32_t i, int t) {
   for (int s = 0; s < st->soa->dev_slots; s++)
     if (dminor(st, i, t, s) >= 0) return 1;
   return 0;
+}
+
+koordhip_pod orc_devshare_pod(const koordhip_config *cfg, const koordhip_pod *pod, const koordhip_pod_ext *x) {
+  koordhip_pod p = *pod;
+  if (x && (x->flags & KOORDHIP_PODX_DEVICE) && ((cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE))
+    p.flags |= ORC_POD_DEVSHARE;
+  return p;
 }
 
 int orc_dev_node_present(const orc_state *st, int32_t i) {

@@ -451,8 +451,9 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
   const int pts_score = (cfg->score_plugins & KOORDHIP_PLUGIN_PTS) != 0;
   const int ipa_score = (cfg->score_plugins & KOORDHIP_PLUGIN_IPA) != 0;
   for (int32_t p = 0; p < n_pods; p++) {
-    const koordhip_pod *pod = &pods[p];
     const koordhip_pod_ext *x = ext ? &ext[p] : NULL;
+    const koordhip_pod pp = orc_devshare_pod(cfg, &pods[p], x);
+    const koordhip_pod *pod = &pp;
     orc_pts ps;
     orc_ipa ia;
     if (orc_pts_prefilter(cfg, st, x, &ps)) return -1;
@@ -611,6 +612,8 @@ int orc_commit_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod
                    int32_t i, uint64_t *cpus, int nominated, uint32_t *devs) {
   uint32_t slots[KOORDHIP_DEV_TYPES] = {0, 0, 0};
   const int dev = (cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE;
+  const koordhip_pod pp = orc_devshare_pod(cfg, pod, x);
+  pod = &pp;
   if (dev && orc_dev_reserve(cfg, st, x, i, nominated, slots, 0)) return KOORDHIP_ERESERVE;
   const int rc = orc_commit(cfg, st, pod, i, +1, cpus);
   if (rc) return rc;
@@ -828,8 +831,9 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
   memset(&ia, 0, sizeof(ia));
   c.ipa = &ia;
   for (int32_t p = 0; p < n_pods; p++) {
-    c.pod = &pods[p];
     c.ext = ext ? &ext[p] : NULL;
+    const koordhip_pod pp = orc_devshare_pod(cfg, &pods[p], c.ext);
+    c.pod = &pp;
     uint32_t *devs = st->dev_out ? st->dev_out + (size_t)p * KOORDHIP_DEV_TYPES : NULL;
     if (devs) memset(devs, 0, sizeof(uint32_t) * KOORDHIP_DEV_TYPES);
     orc_pts_free(&ps);
@@ -837,12 +841,12 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
     if (orc_pts_prefilter(cfg, st, c.ext, &ps)) return -1; /* PodTopologySpread PreFilter */
     if (orc_ipa_prefilter(cfg, st, c.ext, &ia)) return -1; /* InterPodAffinity PreFilter */
     /* Reservation BeforePreFilter: the cycle's NodeInfos are the restored ones */
-    if (rv) orc_resv_restore(st, &pods[p], +1);
+    if (rv) orc_resv_restore(st, c.pod, +1);
     atomic_store(&c.nfeasible, 0);
     pool_until(&pl, n, filter_piece, &c);
     int32_t nf = atomic_load(&c.nfeasible);
     if (nf == 0) {
-      if (rv) orc_resv_restore(st, &pods[p], -1);
+      if (rv) orc_resv_restore(st, c.pod, -1);
       out_node[p] = KOORDHIP_UNSCHEDULABLE;
       if (st->cpuset_out) memset(st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS, 0, 8 * KOORDHIP_NUMA_WORDS);
       continue;
@@ -860,7 +864,7 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
     if (cfg->score_plugins & KOORDHIP_PLUGIN_PTS) orc_pts_normalize(&ps, c.feasible, xs + 3 * (size_t)nf, nf);
     if (cfg->score_plugins & KOORDHIP_PLUGIN_IPA) orc_ipa_normalize(xs + 4 * (size_t)nf, nf);
     int64_t *norm = c.plugin_scores + (size_t)(KOORDHIP_NPLUGINS + KOORDHIP_NEXT_PLUGINS) * nf;
-    if (rs) orc_resv_normalized(st, &pods[p], c.feasible, nf, norm);
+    if (rs) orc_resv_normalized(st, c.pod, c.feasible, nf, norm);
     /* (upstream) prioritizeNodes: sum of score x weight; selectHost: max,
      * reservoir-random tie-break REPLACED by lowest node index (BASELINE.json). */
     int64_t best = -1;
@@ -882,12 +886,12 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
     (void)best_j;
     /* One feasible node: (upstream) schedulePod returns it without
      * prioritizeNodes, so PreScore nominates no reservation */
-    const int nominated = rs && nf > 1 && orc_resv_nominated(st, &pods[p], best_node);
-    if (rv) orc_resv_restore(st, &pods[p], -1);
+    const int nominated = rs && nf > 1 && orc_resv_nominated(st, c.pod, best_node);
+    if (rv) orc_resv_restore(st, c.pod, -1);
     uint64_t *cs = st->cpuset_out ? st->cpuset_out + (size_t)p * KOORDHIP_NUMA_WORDS : NULL;
     /* Reserve (+ AssumePod); a failed Reserve leaves no state and is not retried. */
     st->no_prescore = nf == 1;
-    out_node[p] = orc_commit_ext(cfg, st, &pods[p], c.ext, best_node, cs, nominated, devs) ? KOORDHIP_RESERVE_FAILED
+    out_node[p] = orc_commit_ext(cfg, st, c.pod, c.ext, best_node, cs, nominated, devs) ? KOORDHIP_RESERVE_FAILED
                                                                                             : best_node;
     st->no_prescore = 0;
   }

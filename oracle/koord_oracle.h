@@ -181,6 +181,12 @@ int orc_numa_hint_alloc(const orc_state *st, const koordhip_pod *pod, int32_t no
 int orc_resv_on(const koordhip_config *cfg, const orc_state *st);
 int orc_resv_slots(const orc_state *st); /* reservation slots per node (resv_* columns hold slots x n) */
 int orc_resv_nominate(const orc_state *st, const koordhip_pod *pod, int32_t i); /* nominated slot, -1 none */
+/* Oracle-internal pod flag bit (never from the ABI): DeviceShare is in the
+ * profile and the pod requests devices (PreparePod: not skip), so DeviceShare's
+ * FilterReservation takes part in the nomination (deviceshare/plugin.go:325-356). */
+#define ORC_POD_DEVSHARE (1u << 29)
+/* `pod` with ORC_POD_DEVSHARE set when it applies (x: its ext record or NULL) */
+koordhip_pod orc_devshare_pod(const koordhip_config *cfg, const koordhip_pod *pod, const koordhip_pod_ext *x);
 int orc_resv_node_present(const orc_state *st, int32_t i);
 int orc_resv_node_matchable(const orc_state *st, const koordhip_pod *pod, int32_t i);
 void orc_resv_classify(const orc_state *st, const koordhip_pod *pod, int32_t i, int *matched, int *unmatched);

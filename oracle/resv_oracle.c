@@ -227,12 +227,22 @@ static int64_t slot_score(const orc_state *st, const koordhip_pod *pod, size_t x
 
 /* NominateReservation (nominator.go:32-85) on node i: the slot of the
  * reservation nominated for `pod`, -1 for none.  Candidates: the matched
- * reservations passing FilterReservation; the smallest order label among them
- * (findMostPreferredReservationByOrder), else the highest scoreReservation
- * (prioritizeReservations: the Reservation plugin is the only
- * ReservationScorePlugin here); ties: the lowest slot. */
+ * reservations passing RunReservationFilterPlugins (nominator.go:47-54); the
+ * smallest order label among them (findMostPreferredReservationByOrder), else
+ * the highest scoreReservation (prioritizeReservations); ties: the lowest slot.
+ *
+ * The reservation filter plugins are the Reservation plugin's FilterReservation
+ * (slot_passes) and DeviceShare's (deviceshare/plugin.go:325-356): for a pod
+ * requesting devices that one looks the reservation up among the node's
+ * RestoreReservation state, which keeps only reservations holding devices
+ * (reservation.go:134-161, `len(allocatable) == 0` -> skipped); a reservation
+ * holding none fails it (allocIndex -1 -> an error status, :337-346).  No
+ * reservation holds devices in the engine's envelope, so a device pod is never
+ * nominated (and DeviceShare's ScoreReservation, 0 for every candidate left,
+ * changes no ranking). */
 int orc_resv_nominate(const orc_state *st, const koordhip_pod *pod, int32_t i) {
   if (!st->soa->resv_flags) return -1;
+  if (pod->flags & ORC_POD_DEVSHARE) return -1;
   int best = -1, best_rank = 0, ord = 0;
   int64_t best_sc = -1;
   for (int s = 0; s < orc_resv_slots(st); s++) {
