@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 12
+#define KOORDHIP_ABI_VERSION 13
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -444,6 +444,20 @@ typedef struct koordhip_node_soa {
   int32_t ipa_reserved;
   int32_t ipa_ent_key[KOORDHIP_IPA_ENTRIES];
   const int32_t *ipa_cnt;
+  /* ABI 13: DeviceShare with a reservation holding devices (the reservation
+   * restore, deviceshare/reservation.go:119-170; Filter / FilterReservation /
+   * Score / ScoreReservation / Reserve through tryAllocateFromReservation
+   * :181-283 and the nominated reservation :365-443).  resv_dev_slot [n]: the
+   * reservation slot (0 .. max(resv_slots, 1) - 1) of node i's one reservation
+   * holding devices, -1 = none (at most one per node: the host rejects more).
+   * resv_dev [n][2][TYPES][dev_slots][RES]: [0] that reservation's allocatable
+   * (its reserve pod's device allocation, nd.getUsed(reservePod)) and [1] its
+   * allocated (its AssignedPods' allocations on those minors,
+   * appendAllocatedByHints :145-151; advanced by Reserve).  Both allocations
+   * are also in dev_used, as in the reference's deviceUsed.  NULL = none.  The
+   * sequential cycle places batches on such snapshots. */
+  const int32_t *resv_dev_slot;
+  const int64_t *resv_dev;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -545,6 +559,9 @@ int koordhip_read_numa_zones(koordhip_ctx *ctx, int64_t *zone_used);
 int koordhip_read_reservations(koordhip_ctx *ctx, int64_t *allocated, int32_t *assigned);
 /* ... and the reservations' remaining reserved CPUs [WORDS][S n] (zeros when no loaded reservation holds CPUs). */
 int koordhip_read_resv_cpus(koordhip_ctx *ctx, uint64_t *cpus);
+/* ABI 13: the loaded resv_dev column [n][2][TYPES][dev_slots][RES] (its
+ * allocated half advanced by Reserve); zeros without one. */
+int koordhip_read_resv_devices(koordhip_ctx *ctx, int64_t *resv_dev);
 
 /* Parity/debug mode, no commit: for n_pods pods against the current state.
  *   status : optional, [n_pods][n] KOORDHIP_ST_* bits (every plugin evaluated)

@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 12
+KOORDHIP_ABI_VERSION = 13
 NRES = 5
 NPLUGINS = 4
 
@@ -185,6 +185,8 @@ class KoordhipNodeSoa(C.Structure):
         ("ipa_reserved", C.c_int32),
         ("ipa_ent_key", C.c_int32 * IPA_ENTRIES),
         ("ipa_cnt", _i32p),
+        ("resv_dev_slot", _i32p),
+        ("resv_dev", _i64p),
     ]
 
 
@@ -308,6 +310,7 @@ def load_library(path: str = LIB_PATH):
         "koordhip_read_numa_zones": (C.c_int, [vp, _i64p]),
         "koordhip_read_reservations": (C.c_int, [vp, _i64p, _i32p]),
         "koordhip_read_resv_cpus": (C.c_int, [vp, _u64p]),
+        "koordhip_read_resv_devices": (C.c_int, [vp, _i64p]),
         "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_last_kernel_stats": (C.c_int, [vp, C.POINTER(KoordhipKernelStats)]),
@@ -335,7 +338,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
     "koordhip_commit_ext", "koordhip_uncommit_ext",
     "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
-    "koordhip_read_resv_cpus", "koordhip_last_stats", "koordhip_last_kernel_stats",
+    "koordhip_read_resv_cpus", "koordhip_read_resv_devices", "koordhip_last_stats", "koordhip_last_kernel_stats",
     "koordhip_set_profile_kernels", "koordhip_last_kernel_names",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]

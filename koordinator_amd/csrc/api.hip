@@ -837,6 +837,49 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     dv.minor = mi;
     dv.total = tt;
     dv.used = us;
+    // DeviceShare's reservation restore (deviceshare/reservation.go:119-170):
+    // each node's one reservation holding devices
+    if (!e && s->resv_dev_slot && s->resv_dev) {
+      const int32_t S = s->resv_slots > 1 ? s->resv_slots : 1;
+      if (!s->resv_flags) return fail(KOORDHIP_EINVAL, "resv_dev without reservation columns");
+      const size_t per = (size_t)KOORDHIP_DEV_TYPES * s->dev_slots * KOORDHIP_DEV_RES;
+      for (int32_t i = 0; i < n; i++) {
+        const int32_t h = s->resv_dev_slot[i];
+        if (h < -1 || h >= S) return fail(KOORDHIP_EINVAL, "resv_dev_slot out of [-1, resv_slots)");
+        const int64_t *row = s->resv_dev + (size_t)i * 2 * per;
+        bool any = false;
+        for (size_t a = 0; a < 2 * per; a++) {
+          if (row[a] < 0 || row[a] >= (1ll << 45)) return fail(KOORDHIP_EINVAL, "resv_dev out of [0, 2^45)");
+          any = any || (a < per && row[a] != 0);
+        }
+        if (h < 0) {
+          for (size_t a = 0; a < 2 * per; a++)
+            if (row[a]) return fail(KOORDHIP_EINVAL, "resv_dev values on a node without a device-holding reservation");
+          continue;
+        }
+        if (!(s->resv_flags[(size_t)h * n + i] & KOORDHIP_RESV_PRESENT))
+          return fail(KOORDHIP_EINVAL, "resv_dev_slot names an empty reservation slot");
+        if (!any) return fail(KOORDHIP_EINVAL, "a device-holding reservation with no devices (use resv_dev_slot -1)");
+        // its minors are the node's; its allocated lies on them
+        for (int t = 0; t < KOORDHIP_DEV_TYPES; t++)
+          for (int32_t q = 0; q < s->dev_slots; q++) {
+            const int64_t *A = row + ((size_t)t * s->dev_slots + q) * KOORDHIP_DEV_RES;
+            const int64_t *D = A + per;
+            const bool a = A[0] || A[1] || A[2], d = D[0] || D[1] || D[2];
+            if ((a || d) && s->dev_minor[((size_t)i * KOORDHIP_DEV_TYPES + t) * s->dev_slots + q] < 0)
+              return fail(KOORDHIP_EINVAL, "resv_dev on an empty device slot");
+            if (d && !a) return fail(KOORDHIP_EINVAL, "resv_dev allocated outside the reservation's minors");
+          }
+      }
+      int32_t *rs = nullptr;
+      int64_t *rd = nullptr;
+      e = dev_alloc(c, &rs, n);
+      if (!e) e = upload(c, rs, s->resv_dev_slot, n);
+      if (!e) e = dev_alloc(c, &rd, (size_t)n * 2 * per);
+      if (!e) e = upload(c, rd, s->resv_dev, (size_t)n * 2 * per);
+      dv.rslot = rs;
+      dv.rdev = rd;
+    }
   }
   int64_t *xa = nullptr, *xr = nullptr;
   if (!e && s->xalloc) {
@@ -1327,6 +1370,8 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
       return fail(KOORDHIP_EINVAL, "duplicate row index (a row would mix fields of two updates)");
   }
+  if (rows->resv_dev_slot || rows->resv_dev)
+    return fail(KOORDHIP_EINVAL, "update rows: device-holding reservations change with a snapshot load only");
   const bool numa_rows = c->numa && rows->numa_class;
   if (numa_rows) {
     for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
@@ -1699,6 +1744,21 @@ int koordhip_read_resv_cpus(koordhip_ctx *c, uint64_t *cpus) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
     HIP_TRY(hipMemcpy(cpus + (size_t)w * n, c->d.rv.rc[w], n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int koordhip_read_resv_devices(koordhip_ctx *c, int64_t *resv_dev) {
+  if (!c || !resv_dev) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  const size_t nd = (size_t)c->n * 2 * KOORDHIP_DEV_TYPES * (size_t)std::max(c->d.dv.slots, 0) * KOORDHIP_DEV_RES;
+  if (nd == 0) return 0;
+  if (!c->d.dv.rdev) {
+    std::memset(resv_dev, 0, nd * sizeof(int64_t));
+    return 0;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(resv_dev, c->d.dv.rdev, nd * sizeof(int64_t), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -2549,7 +2609,7 @@ int place_staged_impl(koordhip_ctx *c) {
   // (seq.hip) -- instead of the whole batch in the sequential cycle.
   // KOORDHIP_EXT_SEQ: the sequential cycle for such batches too (A/B).
   const bool ext_pipe = c->seq_profile && c->seq_ext_only && c->staged_ext && c->staged_ext_dev && c->podx_staged &&
-                        !c->staged_reserve && !c->seq_snap && kh::side_mode(c->dc) == 0 && c->world == 1 &&
+                        !c->staged_reserve && !c->seq_snap && !c->d.dv.rslot && kh::side_mode(c->dc) == 0 && c->world == 1 &&
                         !c->comm && !c->group && !std::getenv("KOORDHIP_SERIAL") && !std::getenv("KOORDHIP_ROUND_LAUNCH") &&
                         !std::getenv("KOORDHIP_EXT_SEQ");
   c->last_ext_pipe = ext_pipe;
@@ -3081,6 +3141,8 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
   if (c->d.dv.used)
     v.push_back({c->d.dv.used, n * KOORDHIP_DEV_TYPES * (size_t)c->d.dv.slots * KOORDHIP_DEV_RES * sizeof(int64_t)});
   if (c->d.dv.xreq) v.push_back({c->d.dv.xreq, n * KOORDHIP_NXRES * sizeof(int64_t)});
+  if (c->d.dv.rdev)
+    v.push_back({c->d.dv.rdev, n * 2 * KOORDHIP_DEV_TYPES * (size_t)c->d.dv.slots * KOORDHIP_DEV_RES * sizeof(int64_t)});
   if (c->pts.cnt) v.push_back({c->pts.cnt, n * (size_t)std::max(1, c->pts.cons) * sizeof(int32_t)});
   if (c->ipa.cnt) v.push_back({c->ipa.cnt, n * (size_t)c->ipa.ents * sizeof(int32_t)});
   if (c->dc.resv) {

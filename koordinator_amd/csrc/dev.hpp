@@ -300,6 +300,256 @@ __device__ __forceinline__ void dev_apply(const DevDev &dv, int32_t i, const uin
   }
 }
 
+// ---- DeviceShare with the node's reservation holding devices ------------
+// (deviceshare/reservation.go:119-443; oracle/dev_oracle.c restates the same
+// rules).  One such reservation per node (host-checked), slot h; for the pod
+// its restore class (1 matched, 2 unmatched with assigned pods) and
+// AllocatePolicy.  Per minor: remained Rm = max0(A - D); the preemptible amount
+// P of a free mode -- RC_NODE: (class 2) A - Rm, (class 1) A; RC_ALIGNED:
+// (class 1) D + Rm -- and the free resources max0(total - max0(used - P));
+// RC_REQUIRED: Rm itself on a type calcRequiredDeviceResources names.  Rare
+// (a device pod on a node whose reservation holds devices), so these run out
+// of line: the common device path keeps its registers.
+struct DevRC {
+  int32_t h;    // reservation slot holding devices, -1 none
+  int32_t cls;  // its class for the pod
+  int32_t pol;  // its AllocatePolicy
+  uint32_t rq;  // bit t: calcRequiredDeviceResources names type t
+};
+enum { RC_NODE = 0, RC_ALIGNED = 1, RC_REQUIRED = 2 };
+
+__device__ __forceinline__ size_t rdev_at(const DevDev &dv, int32_t i, int half, int t, int s) {
+  return ((((size_t)i * 2 + (size_t)half) * DT + (size_t)t) * (size_t)dv.slots + (size_t)s) * DR;
+}
+
+// calcRequiredDeviceResources (reservation.go:344-363): the types it names --
+// those with a minor left in Rm, or (Rm empty) every type the reservation holds
+__device__ __noinline__ uint32_t rc_required_types(const DevDev &dv, int32_t i) {
+  uint32_t left = 0u, held = 0u;
+  for (int t = 0; t < DT; t++)
+    for (int s = 0; s < dv.slots; s++) {
+      const size_t a = rdev_at(dv, i, 0, t, s), d = rdev_at(dv, i, 1, t, s);
+      for (int r = 0; r < DR; r++) {
+        const int64_t av = dv.rdev[a + r], dd = dv.rdev[d + r];
+        held |= (av != 0 ? 1u : 0u) << t;
+        left |= (av - dd > 0 ? 1u : 0u) << t;
+      }
+    }
+  return left ? left : held;
+}
+
+// the free resources of dev slot s of type t in `mode`; *hint: the slot is one
+// of the reservation's minors (A nonzero)
+__device__ __forceinline__ void rc_free_slot(const DevDev &dv, int32_t i, const DevRC &rc, int mode, int t, int s,
+                                             int64_t f[DR], bool *hint) {
+  const size_t a = rdev_at(dv, i, 0, t, s), d = rdev_at(dv, i, 1, t, s), u = dev_at(dv, i, t, s) * DR;
+  int64_t A[DR], D[DR], Rm[DR];
+  bool h = false;
+#pragma unroll
+  for (int r = 0; r < DR; r++) {
+    A[r] = dv.rdev[a + r];
+    D[r] = dv.rdev[d + r];
+    Rm[r] = A[r] - D[r] > 0 ? A[r] - D[r] : 0;
+    h |= A[r] != 0;
+  }
+  *hint = h;
+  if (mode == RC_REQUIRED && ((rc.rq >> t) & 1u)) {
+#pragma unroll
+    for (int r = 0; r < DR; r++) f[r] = Rm[r];
+    return;
+  }
+  if (mode == RC_REQUIRED) mode = RC_ALIGNED;
+#pragma unroll
+  for (int r = 0; r < DR; r++) {
+    int64_t p = 0;
+    if (rc.cls == 2) p += A[r] - Rm[r];
+    if (rc.cls == 1) p += mode == RC_NODE ? A[r] : D[r] + Rm[r];
+    const int64_t uu = dv.used[u + r] - p > 0 ? dv.used[u + r] - p : 0;
+    const int64_t tt = dv.total[u + r];
+    f[r] = tt - uu > 0 ? tt - uu : 0;
+  }
+}
+
+// tryAllocateDevice over the pod's types with the reservation's hints
+// (device_cache.go:272-365): `req` keeps to its minors (a type it holds none of
+// is not restricted), `pref` orders them first, then the scorer's score
+// (`scorer`; else 0) desc, minor asc; `want` fitting non-zero devices per type.
+__device__ __noinline__ bool rc_allocate(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
+                                         const DevRC &rc, bool req, bool pref, int mode, bool scorer,
+                                         uint32_t slots[DT], int64_t per_t[DT][DR]) {
+  for (int t = 0; t < DT; t++) {
+    slots[t] = 0u;
+    for (int r = 0; r < DR; r++) per_t[t][r] = 0;
+  }
+  for (int t = 0; t < DT; t++) {
+    int64_t q[DR], per[DR];
+    if (!dev_requests(x, t, q)) continue;
+    DevRow w;
+    dev_load(dv, i, t, w);
+    if (!dev_has_type(w)) return false;
+    if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(w, q)) return false;
+    const int64_t want = dev_wanted(t, q, per);
+    uint32_t hm = 0u;
+    int64_t sc[DS];
+    for (int s = 0; s < DS; s++) {
+      sc[s] = -1;
+      if (s >= dv.slots || w.minor[s] < 0) continue;
+      int64_t f[DR];
+      bool h;
+      rc_free_slot(dv, i, rc, mode, t, s, f, &h);
+      hm |= (h ? 1u : 0u) << s;
+      if (!dev_zero(f) && dev_fits(per, f)) sc[s] = scorer ? dev_scorer(c, t, w.tot[s], f, per) : 0;
+    }
+    uint32_t taken = 0u;
+    for (int64_t got = 0; got < want; got++) {
+      int bs = -1;
+      int64_t bsc = -1;
+      int32_t bmi = 0;
+      bool bpf = false;
+      for (int s = 0; s < DS; s++) {
+        if (sc[s] < 0 || ((taken >> s) & 1u)) continue;
+        if (req && hm && !((hm >> s) & 1u)) continue;
+        const bool pf = pref && ((hm >> s) & 1u);
+        if (bs < 0 || (pf && !bpf) || (pf == bpf && (sc[s] > bsc || (sc[s] == bsc && w.minor[s] < bmi)))) {
+          bs = s;
+          bsc = sc[s];
+          bmi = w.minor[s];
+          bpf = pf;
+        }
+      }
+      if (bs < 0) return false;
+      taken |= 1u << bs;
+    }
+    slots[t] = taken;
+    for (int r = 0; r < DR; r++) per_t[t][r] = per[r];
+  }
+  return true;
+}
+
+// tryAllocateFromReservation (reservation.go:181-283) over the matched
+// reservation holding devices: 1 allocated, 0 none (fall back to the node),
+// -1 Unschedulable (Aligned / Restricted that cannot hold the pod).
+// fromResv: requiredFromReservation (FilterReservation).
+__device__ __forceinline__ int rc_from_reservation(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
+                                                   const DevRC &rc, bool fromResv, bool scorer, uint32_t slots[DT],
+                                                   int64_t per_t[DT][DR]) {
+  if (rc.h < 0 || rc.cls != 1) return 0;
+  if (rc.pol == 0) return rc_allocate(c, dv, x, i, rc, fromResv, true, RC_NODE, scorer, slots, per_t) ? 1 : 0;
+  if (rc.pol == 1) return rc_allocate(c, dv, x, i, rc, true, true, RC_ALIGNED, scorer, slots, per_t) ? 1 : -1;
+  if (!rc_allocate(c, dv, x, i, rc, true, true, RC_ALIGNED, false, slots, per_t)) return -1;
+  return rc_allocate(c, dv, x, i, rc, true, true, RC_REQUIRED, scorer, slots, per_t) ? 1 : -1;
+}
+
+// the node's reservation holding devices for a device pod (rc.h -1: none or
+// no restore).  `klass`: the restore class of slot q (resv_class).
+__device__ __forceinline__ DevRC rc_of(const DevCfg &c, const DevDev &dv, int32_t i, int32_t h, int32_t klass,
+                                       uint32_t rf) {
+  DevRC rc{-1, 0, 0, 0u};
+  if (!dv.rslot || !c.resv || h < 0) return rc;
+  rc.h = h;
+  rc.cls = klass;
+  rc.pol = (int32_t)KOORDHIP_RESV_POLICY(rf);
+  rc.rq = (rc.cls == 1 && rc.pol == 2) ? rc_required_types(dv, i) : 0u;
+  return rc;
+}
+
+// DeviceShare FilterReservation (plugin.go:325-356) of the matched reservation holding devices
+__device__ __noinline__ bool rc_filter_reservation(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
+                                                   const DevRC &rc) {
+  if (!dev_present(dv, i)) return true;
+  uint32_t slots[DT];
+  int64_t per[DT][DR];
+  return rc_from_reservation(c, dv, x, i, rc, true, false, slots, per) > 0;
+}
+
+// scoreNode per requested type over the free devices of `mode`
+__device__ __noinline__ int64_t rc_score(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
+                                         const DevRC &rc, int mode) {
+  int64_t sum = 0;
+  for (int t = 0; t < DT; t++) {
+    int64_t q[DR];
+    if (!dev_requests(x, t, q)) continue;
+    DevRow w;
+    dev_load(dv, i, t, w);
+    if (!dev_has_type(w) || (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(w, q))) continue;
+    int64_t st[DR] = {0, 0, 0}, sf[DR] = {0, 0, 0};
+    for (int s = 0; s < DS; s++) {
+      if (s >= dv.slots || w.minor[s] < 0) continue;
+      int64_t f[DR];
+      bool h;
+      rc_free_slot(dv, i, rc, mode, t, s, f, &h);
+      for (int r = 0; r < DR; r++) {
+        st[r] += w.tot[s][r];
+        sf[r] += f[r];
+      }
+    }
+    for (int r = 0; r < DR; r++) q[r] = q[r] > 0 ? q[r] : 0;
+    sum += dev_scorer(c, t, st, sf, q);
+  }
+  return sum;
+}
+
+// DeviceShare Filter and raw Score on a node whose reservation holds devices
+// (plugin.go:284-323, scoring.go:33-72 with scoreWithNominatedReservation);
+// `nomq`: the reservation slot PreScore nominated (-1 none)
+__device__ __noinline__ bool rc_eval(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i, const DevRC &rc,
+                                     int32_t nomq, bool filter, bool score, int32_t *raw) {
+  *raw = 0;
+  if (!dev_present(dv, i)) return true;
+  bool ok = true;
+  if (filter) {
+    uint32_t slots[DT];
+    int64_t per[DT][DR];
+    const int r = rc_from_reservation(c, dv, x, i, rc, false, false, slots, per);
+    ok = r != 0 ? r > 0 : rc_allocate(c, dv, x, i, rc, false, false, RC_NODE, false, slots, per);
+  }
+  if (score) {
+    if (nomq >= 0)
+      *raw = (nomq == rc.h && rc.cls == 1)
+                 ? (int32_t)rc_score(c, dv, x, i, rc, rc.pol == 0 ? RC_NODE : (rc.pol == 1 ? RC_ALIGNED : RC_REQUIRED))
+                 : 0;
+    else
+      *raw = (int32_t)rc_score(c, dv, x, i, rc, RC_NODE);
+  }
+  return ok || !filter;
+}
+
+// DeviceShare Reserve on such a node (plugin.go:368-405): the nominated
+// reservation's allocation (`nomq`, -1 none), else the node's
+__device__ __noinline__ bool rc_reserve(const DevCfg &c, const DevDev &dv, const DevPodX &x, int32_t i,
+                                        const DevRC &rc, int32_t nomq, uint32_t slots[DT], int64_t per_t[DT][DR]) {
+  for (int t = 0; t < DT; t++) {
+    slots[t] = 0u;
+    for (int r = 0; r < DR; r++) per_t[t][r] = 0;
+  }
+  if (!(x.flags & KOORDHIP_PODX_DEVICE) || !dev_present(dv, i)) return true;
+  int r = 0;
+  if (nomq >= 0) {
+    if (nomq != rc.h || rc.cls != 1) return false;
+    r = rc_from_reservation(c, dv, x, i, rc, false, true, slots, per_t);
+    if (r < 0) return false;
+  }
+  return r > 0 || rc_allocate(c, dv, x, i, rc, false, false, RC_NODE, true, slots, per_t);
+}
+
+// the assumed pod's allocation on the reservation's minors joins its allocated
+template <bool WT = false>
+__device__ __noinline__ void rc_apply_allocated(const DevDev &dv, int32_t i, const uint32_t slots[DT],
+                                                const int64_t per_t[DT][DR]) {
+  for (int t = 0; t < DT; t++)
+    for (int s = 0; s < dv.slots; s++) {
+      if (!((slots[t] >> s) & 1u)) continue;
+      const size_t a = rdev_at(dv, i, 0, t, s), d = rdev_at(dv, i, 1, t, s);
+      if (dv.rdev[a] == 0 && dv.rdev[a + 1] == 0 && dv.rdev[a + 2] == 0) continue;  // not its minor
+      for (int r = 0; r < DR; r++) {
+        if constexpr (WT)
+          st_wt(&dv.rdev[d + r], (int64_t)(dv.rdev[d + r] + per_t[t][r]));
+        else
+          dv.rdev[d + r] += per_t[t][r];
+      }
+    }
+}
+
 // NodeResourcesFit over the extended scalars the pod requests (upstream fitsRequest)
 __device__ __forceinline__ bool xfit_filter(const DevDev &dv, const DevPodX &x, int32_t i, int32_t n) {
   if (!x.xmask) return true;

@@ -82,6 +82,11 @@ struct DevDev {
   const int64_t *xalloc;      // [NXRES][n] (NULL: 0)
   int64_t *xreq;              // [NXRES][n] Requested of the extended scalars
   const uint16_t *sscore[2];  // [MAX_STATIC_CLASSES][n] NodeAffinity / TaintToleration raw scores (NULL: 0)
+  // the node's one reservation holding devices (koordhip_node_soa.resv_dev_*;
+  // NULL: none): its slot [n] (-1 none) and [n][2][TYPES][slots][RES] its
+  // allocatable / allocated (the allocated half advanced by Reserve)
+  const int32_t *rslot;
+  int64_t *rdev;
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are

@@ -36,7 +36,8 @@ struct ResvSlot {
   int32_t rn;                  // len(AssignedPods)
   uint32_t rf;                 // KOORDHIP_RESV_* (0: empty slot)
   int32_t rk;                  // order rank
-  int32_t rpad;
+  int32_t rdev;                // (per pod) DeviceShare's FilterReservation passes: the slot can be a device pod's
+                               // nomination (set by the caller after load_resv; 0 = not)
 };
 static_assert(sizeof(ResvSlot) == 64, "reservation slot = 64 B");
 
@@ -92,6 +93,7 @@ __device__ __forceinline__ void load_resv(NumaRowRS<S> &r, const DevResv &d, int
     x.rf = q < d.slots ? d.flags[at] : 0u;
     x.rn = 0;
     x.rk = 0;
+    x.rdev = 0;
 #pragma unroll
     for (int k = 0; k < 2; k++) x.ra[k] = x.rd[k] = x.rz[k] = 0.0;
     if (x.rf & KOORDHIP_RESV_PRESENT) {
@@ -286,18 +288,20 @@ __device__ __forceinline__ int32_t resv_score(const DevPod &p, const ResvSlot &r
 
 // NominateReservation: among the matched candidates the smallest order label,
 // else the highest scoreReservation; ties -> the lowest slot.  -1: none.  A
-// device pod under DeviceShare (KH_POD_DEVSHARE) passes DeviceShare's
-// FilterReservation on no reservation (none holds devices here: the restore
-// state has no entry for it, deviceshare/plugin.go:337-346), so it has none.
+// device pod under DeviceShare (KH_POD_DEVSHARE) must also pass DeviceShare's
+// FilterReservation (deviceshare/plugin.go:325-356): only the node's
+// reservation holding devices can (ResvSlot::rdev, set by the caller); a
+// reservation holding none has no restore entry and fails it (:337-346).
 template <int S>
 __device__ __forceinline__ int resv_nominate(const DevPod &p, const NumaRowRS<S> &r, uint32_t mm) {
-  if (p.flags & KH_POD_DEVSHARE) return -1;
+  const bool devshare = (p.flags & KH_POD_DEVSHARE) != 0;
   int best = -1, brk = 0;
   bool ord = false;
   int32_t bsc = -1;
 #pragma unroll
   for (int q = 0; q < S; q++) {
     if (!((mm >> q) & 1u) || !resv_candidate(p, r.rs[q])) continue;
+    if (devshare && !r.rs[q].rdev) continue;
     const ResvSlot &x = r.rs[q];
     if (x.rf & KOORDHIP_RESV_ORDERED) {
       if (!ord || x.rk < brk) {

@@ -100,6 +100,33 @@ __host__ __device__ constexpr int seq_mode(const DevCfg &c) {
 template <int SM>
 using SeqResvRow = NumaRowRS<SM == 3 ? KOORDHIP_RESV_SLOTS_MAX : KOORDHIP_RESV_SLOTS>;
 
+// The node's reservation holding devices, for a device pod under DeviceShare
+// (KH_POD_DEVSHARE): its DevRC (dev.hpp; h -1: none) and DeviceShare's
+// FilterReservation of it, recorded in its slot's rdev -- the nomination's only
+// possible candidate for the pod (resv_nominate).
+template <int S>
+__device__ __forceinline__ DevRC seq_dev_resv(const DevCfg &c, const DevDev &dv, const DevPod &p, const DevPodX &x,
+                                              NumaRowRS<S> &r, int32_t i) {
+  DevRC rc{-1, 0, 0, 0u};
+  if (!dv.rslot || !c.resv || !(p.flags & KH_POD_DEVSHARE)) return rc;
+  const int32_t h = dv.rslot[i];
+  if (h < 0 || h >= S) return rc;
+  int32_t cls = 0;
+  uint32_t rf = 0u;
+#pragma unroll
+  for (int q = 0; q < S; q++)
+    if (q == h) {
+      cls = resv_class(r.rs[q], p);
+      rf = r.rs[q].rf;
+    }
+  rc = rc_of(c, dv, i, h, cls, rf);
+  if (rc.h >= 0 && rc.cls == 1 && rc_filter_reservation(c, dv, x, i, rc))
+#pragma unroll
+    for (int q = 0; q < S; q++)
+      if (q == h) r.rs[q].rdev = 1;
+  return rc;
+}
+
 // One node for one pod: the total of the per-node plugins (-1: some Filter
 // fails; with the Reservation plugin the ranking total of resv.hpp) and the
 // raw normalized scores.  Every column is read (the parity evaluator's rows,
@@ -130,12 +157,17 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
     SeqResvRow<SM> nr{};
     load_numa<false>(nr, d, i, all);  // (the zone row shares the reserved CPUs' bytes: eval_total_resv<.., Z> reads it)
     load_resv(nr, d.rv, i);
+    const DevRC rc = seq_dev_resv(c, d.dv, p, x, nr, i);
     t = c.zones       ? eval_total_resv<S, true, true>(p, v, nr, d.nu.cls, c, &d, i)
         : c.resv_cpus ? eval_total_resv<S, true>(p, v, nr, d.nu.cls, c)
                       : eval_total_resv<S, false>(p, v, nr, d.nu.cls, c);
-    const bool nominated = rs && (x.flags & KOORDHIP_PODX_DEVICE) && resv_nominate(p, nr, resv_matched(nr, p)) >= 0;
-    df = dev_eval(c, d.dv, x, i, nominated, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
-                  (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
+    const int32_t nq = (rs && (x.flags & KOORDHIP_PODX_DEVICE)) ? resv_nominate(p, nr, resv_matched(nr, p)) : -1;
+    if (rc.h >= 0)
+      df = rc_eval(c, d.dv, x, i, rc, nq, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
+    else
+      df = dev_eval(c, d.dv, x, i, nq >= 0, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                    (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
     if ((p.flags & (KOORDHIP_POD_RESERVE | KOORDHIP_POD_RESV_OPERATING)) && (c.filt & KOORDHIP_PLUGIN_RESERVATION) &&
         !reserve_pod_ok(p, (p.flags & KOORDHIP_POD_RESERVE) ? x.reserve_node : 0, nr, i))
       rfail = true;
@@ -174,6 +206,16 @@ __device__ __forceinline__ int32_t ext_total(const DevCfg &c, uint32_t ext, cons
   for (int e = 0; e < 3; e++)
     if ((ext >> e) & 1u) t += c.w_ext[e] * norm_score(raw[e], mx[e], e == 2);
   return t;
+}
+
+// tk plus the normalized plugins' `extra`, except in the Reservation ranking
+// total's preferred tier (a node whose matched reservations carry an order
+// label, resv.hpp): the reference's preferred node takes the normalized
+// Reservation score 100 x its weight and wins outright, the tier ranks by the
+// order alone -- extra added there would reorder two ordered nodes
+// (orc_resv_rank_total ignores it the same way)
+__device__ __forceinline__ int32_t rank_add(const DevCfg &c, int32_t tk, int32_t extra) {
+  return (c.resv && (c.score & KOORDHIP_PLUGIN_RESERVATION) && tk >= 101 * c.resv_b1) ? tk : tk + extra;
 }
 
 // The record of a pod without koordhip_pod_ext (no device request: gpu -1 =
@@ -219,13 +261,21 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   using RV = typename std::conditional<SM >= 2, SeqResvRow<SM>, NumaRow>::type;
   RV rv;
   uint32_t mm = 0u;
+  DevRC rc{-1, 0, 0, 0u};
   if constexpr (SM >= 2) {
     load_resv(rv, d.rv, w);
     mm = resv_matched(rv, p);
+    rc = seq_dev_resv(c, d.dv, p, x, rv, w);
   }
   const bool prescore = rs && nf > 1;
-  bool nominated = false;
-  if constexpr (SM >= 2) nominated = prescore && resv_nominate(p, rv, mm) >= 0;
+  // the reservation PreScore nominated (DeviceShare Reserve reads it) and the
+  // one the Reservation Reserve assumes the pod into, both on the state
+  // before any Reserve
+  int32_t nq = -1, qa = -1;
+  if constexpr (SM >= 2) {
+    qa = resv_nominate(p, rv, mm);
+    nq = prescore ? qa : -1;
+  }
   uint32_t slots[DT] = {0u, 0u, 0u};
   int64_t per[DT][DR];
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
@@ -237,7 +287,8 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   int64_t xr[KOORDHIP_NXRES];
 #pragma unroll
   for (int j = 0; j < KOORDHIP_NXRES; j++) xr[j] = ((x.xmask >> j) & 1u) ? d.dv.xreq[(size_t)j * d.n + w] : 0;
-  if (dev && !dev_reserve(c, d.dv, x, w, nominated, slots, per)) return KOORDHIP_RESERVE_FAILED;
+  if (dev && !(rc.h >= 0 ? rc_reserve(c, d.dv, x, w, rc, nq, slots, per) : dev_reserve(c, d.dv, x, w, nq >= 0, slots, per)))
+    return KOORDHIP_RESERVE_FAILED;
   uint64_t m[NW] = {0, 0, 0, 0};
   if constexpr (SM >= 1) {
     if (numa_on(c) && numa_active(p, c)) {
@@ -249,7 +300,10 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
       store_numa_row(r, d, w);
     }
   }
-  if (dev) dev_apply<!ROW>(d.dv, w, slots, per);
+  if (dev) {
+    dev_apply<!ROW>(d.dv, w, slots, per);
+    if (rc.h >= 0 && qa == rc.h) rc_apply_allocated<!ROW>(d.dv, w, slots, per);
+  }
   if constexpr (SM >= 2) {  // Reservation Reserve: assumePod into the nominated reservation
     resv_assume(rv, p, m);
     store_resv(rv, d.rv, w);
@@ -1017,7 +1071,7 @@ __global__ __launch_bounds__(SEQ_THREADS) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
           for (int e = 0; e < 3; e++) v4[1 + e] = max(v4[1 + e], rk[e]);
           if (soft) rk[3] = pts_soft_mark(pa, q, d.n, i, smk, snf) ? 0 : -1;
-          const uint64_t kk = make_key(tk + ext_total(c, ext, rk, zero) + pts_const, i);
+          const uint64_t kk = make_key(rank_add(c, tk, ext_total(c, ext, rk, zero) + pts_const), i);
           key0 = kk > key0 ? kk : key0;
         }
       }
@@ -1159,7 +1213,7 @@ __global__ __launch_bounds__(SEQ_THREADS) __attribute__((amdgpu_waves_per_eu(1, 
         const int32_t rk[KOORDHIP_NEXT_PLUGINS] = {s_raw[k][0][t], s_raw[k][1][t], s_raw[k][2][t], 0};
         const int32_t pt = soft ? pa.w * pts_norm(s_raw[k][3][t], pmin, pmax) : pts_const;
         const int32_t it = inorm ? ia.w * ipa_norm(s_raw[k][4][t], gimn, gimx) : 0;
-        const uint64_t key = make_key(tk + ext_total(c, ext, rk, gmx) + pt + it, i);
+        const uint64_t key = make_key(rank_add(c, tk, ext_total(c, ext, rk, gmx) + pt + it), i);
         best = key > best ? key : best;
       }
       int32_t u4[4] = {0, 0, 0, 0};
@@ -1424,7 +1478,7 @@ __global__ __launch_bounds__(256) void k_seq_topk(DevCfg c, int32_t n, const int
       for (int e = 0; e < KOORDHIP_NEXT_PLUGINS; e++) raw[e] = wk[(size_t)(e + 1) * n + i];
       const int32_t pt = pts_w ? pts_w * pts_norm(raw[3], pmin, mx[3]) : 0;
       const int32_t it = ipa_w ? ipa_w * ipa_norm(raw[4], imin, mx[4]) : 0;
-      const uint64_t key = make_key(wk[i] + ext_total(c, ext, raw, mx) + pt + it, i);
+      const uint64_t key = make_key(rank_add(c, wk[i], ext_total(c, ext, raw, mx) + pt + it), i);
       if (key < last && key > best) best = key;
     }
     best = seq_wave_max(best);

@@ -122,6 +122,14 @@ class PlacementEngine:
         abi.check(self.lib, self.lib.koordhip_read_devices(self._ctx, abi.ptr(used, C.c_int64), abi.ptr(xr, C.c_int64)))
         return {"dev_used": used, "xrequested": xr.T.copy()}
 
+    def read_resv_devices(self) -> np.ndarray:
+        """The device-holding reservations' column [n][2][TYPES][dev_slots][RES]
+        (allocatable, allocated; the allocated half advanced by Reserve)."""
+        S = max(1, self._table.dev_slots if self._table is not None else 0)
+        out = np.zeros((self.n, 2, abi.DEV_TYPES, S, abi.DEV_RES), np.int64)
+        abi.check(self.lib, self.lib.koordhip_read_resv_devices(self._ctx, abi.ptr(out, C.c_int64)))
+        return out
+
     def read_pts(self) -> np.ndarray:
         """PodTopologySpread matching pods per node and table constraint [n][cons]."""
         m = self._table.pts if self._table is not None else None

@@ -54,6 +54,12 @@ PTS_MUTABLE = ["pts_cnt"]
 # i32 (mutable; the topology keys are the pts_* ones).  Present after enable_ipa().
 IPA_COLS = ["ipa_cnt"]
 IPA_MUTABLE = ["ipa_cnt"]
+# DeviceShare with a reservation holding devices (ABI 13): per node the slot of
+# its one such reservation [n] i32 (-1: none) and that reservation's device
+# allocatable / allocated [n][2][TYPES][dev_slots][RES] i64 (the allocated half
+# mutable).  Present after enable_resv_dev().
+RESV_DEV_COLS = ["resv_dev_slot", "resv_dev"]
+RESV_DEV_MUTABLE = ["resv_dev"]
 
 
 @dataclass
@@ -170,6 +176,19 @@ class NodeTable:
         self.cols["static_score"] = np.zeros((n, 2, abi.MAX_STATIC_CLASSES), np.uint16)
         return self
 
+    @property
+    def has_resv_dev(self) -> bool:
+        return "resv_dev_slot" in self.cols
+
+    def enable_resv_dev(self):
+        """Add the device-holding reservation columns (no node has one);
+        needs the device columns (enable_ext with dev_slots > 0)."""
+        if not self.has_ext or self.dev_slots <= 0:
+            raise ValueError("device-holding reservations need the device columns (enable_ext(dev_slots > 0))")
+        self.cols["resv_dev_slot"] = np.full(self.n, -1, np.int32)
+        self.cols["resv_dev"] = np.zeros((self.n, 2, abi.DEV_TYPES, self.dev_slots, abi.DEV_RES), np.int64)
+        return self
+
     def set_resv_slots(self, slots: int):
         """Hold up to `slots` reservations per node (new slots empty)."""
         if not 1 <= slots <= abi.RESV_SLOTS_MAX:
@@ -186,7 +205,7 @@ class NodeTable:
     def col_names(self) -> List[str]:
         return (ALL_COLS + [slot_col(c, s) for s in range(1, self.resv_slots) for c in RESV_COLS]
                 + (EXT_COLS if self.has_ext else []) + (PTS_COLS if self.has_pts else [])
-                + (IPA_COLS if self.has_ipa else []))
+                + (IPA_COLS if self.has_ipa else []) + (RESV_DEV_COLS if self.has_resv_dev else []))
 
     @classmethod
     def empty(cls, n: int) -> "NodeTable":
@@ -304,6 +323,11 @@ class NodeTable:
                 if ss[:, w].any():
                     keep[f"ss{w}"] = np.ascontiguousarray(ss[:, w].T)      # [MAX_STATIC_CLASSES][n]
                     s.static_score[w] = keep[f"ss{w}"].ctypes.data_as(C.POINTER(C.c_uint16))
+            if self.has_resv_dev and (self.cols["resv_dev_slot"] >= 0).any():
+                keep["resv_dev_slot"] = np.ascontiguousarray(self.cols["resv_dev_slot"], dtype=np.int32)
+                keep["resv_dev"] = np.ascontiguousarray(self.cols["resv_dev"], dtype=np.int64)
+                s.resv_dev_slot = keep["resv_dev_slot"].ctypes.data_as(C.POINTER(C.c_int32))
+                s.resv_dev = keep["resv_dev"].ctypes.data_as(C.POINTER(C.c_int64))
             s._keep_ext = keep
         if self.has_pts:
             m = self.pts

@@ -48,6 +48,9 @@ class OrcState(C.Structure):
         ("dev_out", C.c_void_p),
         ("pts_cnt", C.POINTER(C.c_int32)),
         ("ipa_cnt", C.POINTER(C.c_int32)),
+        ("resv_dev", C.POINTER(C.c_int64)),
+        ("cur_ext", C.c_void_p),
+        ("resv_restore", C.c_int32),
     ]
 
 
@@ -105,14 +108,16 @@ def lib():
         L.orc_eval_ext.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, vp, C.c_int32,
                                    vp, vp, vp, C.c_int32]
         L.orc_set_dev_out.argtypes = [C.POINTER(OrcState), vp]
-        L.orc_dev_filter.argtypes = [C.POINTER(OrcState), vp, C.c_int32]
+        L.orc_dev_filter.argtypes = [C.POINTER(OrcState), vp, vp, C.c_int32]
         L.orc_dev_filter.restype = C.c_int
-        L.orc_dev_score.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32, C.c_int]
+        L.orc_dev_score.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, vp, C.c_int32, C.c_int]
         L.orc_dev_score.restype = C.c_int64
-        L.orc_dev_reserve.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, C.c_int32, C.c_int, vp,
+        L.orc_dev_reserve.argtypes = [C.POINTER(abi.KoordhipConfig), C.POINTER(OrcState), vp, vp, C.c_int32, C.c_int, vp,
                                       C.c_int]
         L.orc_dev_reserve.restype = C.c_int
         L.orc_default_normalize.argtypes = [vp, C.c_int32, C.c_int]
+        L.orc_dev_try_from_reservation.argtypes = [C.POINTER(OrcState), vp, vp, C.c_int32, C.c_int, vp]
+        L.orc_dev_try_from_reservation.restype = C.c_int
         _lib = L
     return _lib
 
@@ -181,6 +186,25 @@ class Oracle:
         res = (out,) + ((cs,) if cpusets else ()) + ((dv,) if devices else ())
         return res if len(res) > 1 else out
 
+    def resv_dev_state(self) -> np.ndarray:
+        """The device-holding reservations' column [n][2][TYPES][dev_slots][RES] (zeros without one)."""
+        S = max(1, self.table.dev_slots)
+        shape = (self.n, 2, abi.DEV_TYPES, S, abi.DEV_RES)
+        if not self.st.resv_dev:
+            return np.zeros(shape, np.int64)
+        return np.ctypeslib.as_array(self.st.resv_dev, shape=shape).copy()
+
+    def dev_try_from_reservation(self, pod, ext_rec, node: int, from_resv: bool = False):
+        """tryAllocateFromReservation over node's matched reservation holding
+        devices: (1 allocated / 0 none / -1 Unschedulable, slots [TYPES])."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod))
+        x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)
+        sl = np.zeros(abi.DEV_TYPES, np.uint32)
+        self.st.resv_restore = 1
+        r = lib().orc_dev_try_from_reservation(C.byref(self.st), pod.ctypes.data, x.ctypes.data, node,
+                                               int(from_resv), sl.ctypes.data)
+        return int(r), sl
+
     def dev_state(self) -> dict:
         """DeviceShare deviceUsed [n][TYPES][S][RES] and the extended scalars' Requested [n][NXRES]."""
         n, S = self.n, max(1, self.table.dev_slots)
@@ -205,17 +229,17 @@ class Oracle:
 
     def dev_filter(self, ext_rec, node: int) -> bool:
         x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)
-        return bool(lib().orc_dev_filter(C.byref(self.st), x.ctypes.data, node))
+        return bool(lib().orc_dev_filter(C.byref(self.st), None, x.ctypes.data, node))
 
     def dev_score(self, ext_rec, node: int, nominated: bool = False) -> int:
         x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)
-        return int(lib().orc_dev_score(C.byref(self.cfg), C.byref(self.st), x.ctypes.data, node, int(nominated)))
+        return int(lib().orc_dev_score(C.byref(self.cfg), C.byref(self.st), None, x.ctypes.data, node, int(nominated)))
 
     def dev_reserve(self, ext_rec, node: int, nominated: bool = False, apply: bool = True):
         """(ok, slots [TYPES])"""
         x = np.ascontiguousarray(np.atleast_1d(ext_rec), dtype=abi.POD_EXT_DTYPE)
         sl = np.zeros(abi.DEV_TYPES, np.uint32)
-        rc = lib().orc_dev_reserve(C.byref(self.cfg), C.byref(self.st), x.ctypes.data, node, int(nominated),
+        rc = lib().orc_dev_reserve(C.byref(self.cfg), C.byref(self.st), None, x.ctypes.data, node, int(nominated),
                                    sl.ctypes.data, int(apply))
         return rc == 0, sl
 

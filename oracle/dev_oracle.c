@@ -39,15 +39,6 @@ static int32_t dminor(const orc_state *st, int32_t i, int t, int s) {
   return st->soa->dev_minor[((size_t)i * T + (size_t)t) * (size_t)st->soa->dev_slots + (size_t)s];
 }
 
-/* resetDeviceFree, device_cache.go:185-202 (SubtractWithNonNegativeResult) */
-static void dev_free(const orc_state *st, int32_t i, int t, int s, int64_t f[R]) {
-  const int64_t *tot = st->soa->dev_total + dix(st, i, t, s);
-  const int64_t *used = st->dev_used + dix(st, i, t, s);
-  for (int r = 0; r < R; r++) {
-    const int64_t x = tot[r] - used[r];
-    f[r] = x > 0 ? x : 0;
-  }
-}
 static int is_zero(const int64_t v[R]) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
 static int has_type(const orc_state *st, int32_t i, int t) {
   for (int s = 0; s < st->soa->dev_slots; s++)
@@ -158,42 +149,231 @@ static int64_t dev_scorer(const koordhip_config *cfg, int t, const int64_t tot[R
   return wsum ? num / wsum : 0;
 }
 
-/* DeviceShare Filter, plugin.go:284-323 -> tryAllocateDevice (device_cache.go:
- * 272-314) with no scorer: per requested type, the node needs its devices
- * (:286-289), the GPU memory fill (:291-295) and `wanted` devices whose free
- * resources hold the per-device request, unhealthy (zero) ones skipped
- * (tryAllocateByDeviceType :316-365).  1 = passes. */
-int orc_dev_filter(const orc_state *st, const koordhip_pod_ext *x, int32_t i) {
-  if (!x || !(x->flags & KOORDHIP_PODX_DEVICE)) return 1; /* state.skip */
-  if (!orc_dev_node_present(st, i)) return 1;           /* nodeDeviceInfo == nil: :298-301 */
+/* ---- the node's reservation holding devices (reservation.go:119-170) ----
+ * At most one per node (host-checked): slot h = resv_dev_slot[i], its
+ * allocatable A (the reserve pod's devices) and allocated D (its AssignedPods'
+ * on A's minors), per type and dev slot.  For the pod being scheduled the
+ * restore keeps it as matched (class 1) or as unmatched with assigned pods
+ * (class 2, transformer.go:86-103); per minor:
+ *   remained Rm = SubtractWithNonNegativeResult(A, D) (subtractAllocated :84-92)
+ *   mergedUnmatchedUsed   = A - Rm           (class 2, :86-93)
+ *   mergedMatchedAllocatable = A, mergedMatchedAllocated = D   (class 1, :95-105)
+ * The free devices of a preemptible map P (calcFreeWithPreemptible,
+ * device_cache.go:456-481): total - SubtractWithNonNegativeResult(used, P),
+ * clamped at 0 -- with P = 0 the plain free. */
+typedef struct dev_rc {
+  int h;   /* slot of the reservation holding devices; -1: none (or no restore) */
+  int cls; /* its class for the pod: 1 matched, 2 unmatched with assigned pods, 0 neither */
+  int pol; /* its AllocatePolicy: 0 Default, 1 Aligned, 2 Restricted */
+  const int64_t *A, *D; /* [TYPES][dev_slots][RES] */
+} dev_rc;
+
+enum { FREE_NODE = 0, FREE_ALIGNED = 1, FREE_REQUIRED = 2 };
+
+int orc_dev_resv_slot(const orc_state *st, int32_t i) {
+  if (!st->resv_dev || !st->soa->resv_dev_slot || !st->resv_restore) return -1;
+  return st->soa->resv_dev_slot[i];
+}
+
+static size_t rdix(const orc_state *st, int32_t i, int half, int t, int s) {
+  return ((((size_t)i * 2 + (size_t)half) * T + (size_t)t) * (size_t)st->soa->dev_slots + (size_t)s) * R;
+}
+
+static dev_rc dev_rc_of(const orc_state *st, const koordhip_pod *pod, int32_t i) {
+  dev_rc rc = {-1, 0, 0, NULL, NULL};
+  const int h = pod ? orc_dev_resv_slot(st, i) : -1;
+  if (h < 0) return rc;
+  rc.h = h;
+  rc.cls = orc_resv_slot_class(st, pod, h, i);
+  rc.pol = (int)KOORDHIP_RESV_POLICY(st->soa->resv_flags[(size_t)h * st->n + i]);
+  rc.A = st->resv_dev + rdix(st, i, 0, 0, 0);
+  rc.D = st->resv_dev + rdix(st, i, 1, 0, 0);
+  return rc;
+}
+
+static const int64_t *rc_at(const orc_state *st, const int64_t *base, int t, int s) {
+  return base + ((size_t)t * (size_t)st->soa->dev_slots + (size_t)s) * R;
+}
+/* the reservation's remained on (t, s) */
+static void rc_remained(const orc_state *st, const dev_rc *rc, int t, int s, int64_t rm[R]) {
+  const int64_t *a = rc_at(st, rc->A, t, s), *d = rc_at(st, rc->D, t, s);
+  for (int r = 0; r < R; r++) rm[r] = a[r] - d[r] > 0 ? a[r] - d[r] : 0;
+}
+/* newDeviceMinorMap(allocatable): the reservation's minors of type t (dev slot bits) */
+static uint32_t rc_hints(const orc_state *st, const dev_rc *rc, int t) {
+  uint32_t m = 0;
+  if (rc->h < 0) return 0;
+  for (int s = 0; s < st->soa->dev_slots; s++)
+    if (!is_zero(rc_at(st, rc->A, t, s))) m |= 1u << s;
+  return m;
+}
+/* calcRequiredDeviceResources (reservation.go:344-363) for type t: 1 when it
+ * names type t -- Rm has a minor of type t, or Rm is empty altogether and the
+ * reservation holds type t (then every one of its minors with nothing left) */
+static int rc_required(const orc_state *st, const dev_rc *rc, int t) {
+  int any_t = 0, any = 0;
+  for (int u = 0; u < T; u++)
+    for (int s = 0; s < st->soa->dev_slots; s++) {
+      int64_t rm[R];
+      rc_remained(st, rc, u, s, rm);
+      if (!is_zero(rm)) {
+        any = 1;
+        if (u == t) any_t = 1;
+      }
+    }
+  return any_t || (!any && rc_hints(st, rc, t) != 0);
+}
+
+/* the preemptible amount on (t, s) of free mode `mode` (FREE_NODE: basic +
+ * mergedMatchedAllocatable; FREE_ALIGNED: basic + mergedMatchedAllocated +
+ * the reservation's remained, tryAllocateFromReservation :220-253) */
+static void rc_preempt(const orc_state *st, const dev_rc *rc, int mode, int t, int s, int64_t p[R]) {
+  for (int r = 0; r < R; r++) p[r] = 0;
+  if (rc->h < 0) return;
+  const int64_t *a = rc_at(st, rc->A, t, s), *d = rc_at(st, rc->D, t, s);
+  int64_t rm[R];
+  rc_remained(st, rc, t, s, rm);
+  for (int r = 0; r < R; r++) {
+    if (rc->cls == 2) p[r] += a[r] - rm[r]; /* mergedUnmatchedUsed */
+    if (rc->cls == 1) p[r] += mode == FREE_NODE ? a[r] : d[r] + rm[r];
+  }
+}
+
+/* the free resources of (t, s) in mode `mode` (FREE_REQUIRED: the remained
+ * when calcRequiredDeviceResources names type t, tryAllocateByDeviceType
+ * :330-335; else the aligned free) */
+static void rc_free(const orc_state *st, const dev_rc *rc, int mode, int32_t i, int t, int s, int64_t f[R]) {
+  if (mode == FREE_REQUIRED) {
+    if (rc_required(st, rc, t)) {
+      rc_remained(st, rc, t, s, f);
+      return;
+    }
+    mode = FREE_ALIGNED;
+  }
+  int64_t p[R];
+  rc_preempt(st, rc, mode, t, s, p);
+  const int64_t *tot = st->soa->dev_total + dix(st, i, t, s);
+  const int64_t *used = st->dev_used + dix(st, i, t, s);
+  for (int r = 0; r < R; r++) {
+    const int64_t u = used[r] - p[r] > 0 ? used[r] - p[r] : 0;
+    f[r] = tot[r] - u > 0 ? tot[r] - u : 0;
+  }
+}
+
+typedef struct dev_pick {
+  int32_t s, minor, pref;
+  int64_t score;
+} dev_pick;
+
+static int pick_cmp(const void *a, const void *b) {
+  const dev_pick *x = (const dev_pick *)a, *y = (const dev_pick *)b;
+  if (x->pref != y->pref) return x->pref ? -1 : 1;
+  if (x->score != y->score) return x->score > y->score ? -1 : 1;
+  return x->minor < y->minor ? -1 : (x->minor > y->minor ? 1 : 0);
+}
+
+/* tryAllocateDevice (device_cache.go:272-314) over the pod's requested types:
+ * per type the node needs devices (:286-289), the GPU memory fill (:291-295),
+ * `wanted` devices (calcDeviceWanted) among the free ones of `mode` ordered by
+ * sortDeviceResourcesByMinor (device_resources.go:177-195: preferred minors --
+ * the reservation's, `pref` -- first, then scoreDevices' score desc, minor
+ * asc; no `scorer`: score 0), skipping minors outside the reservation's when
+ * `req` (required, :337-339; a type the reservation holds none of is not
+ * restricted) and zero ones (:341-343).  1 = allocated (slots[t], per_t[t]). */
+static int dev_allocate(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x, int32_t i,
+                        const dev_rc *rc, int req, int pref, int mode, int scorer, uint32_t *slots,
+                        int64_t per_t[T][R]) {
+  for (int t = 0; t < T; t++) slots[t] = 0;
   for (int t = 0; t < T; t++) {
     int64_t q[R], per[R], f[R];
     if (!dev_requests(x, t, q)) continue;
     if (!has_type(st, i, t)) return 0;
     if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(st, i, q)) return 0;
     const int64_t w = dev_wanted(t, q, per);
-    int64_t cnt = 0;
+    const uint32_t hm = rc_hints(st, rc, t);
+    dev_pick pk[KOORDHIP_DEV_SLOTS];
+    int np = 0;
     for (int s = 0; s < st->soa->dev_slots; s++) {
-      if (dminor(st, i, t, s) < 0) continue;
-      dev_free(st, i, t, s, f);
-      if (is_zero(f)) continue;
-      if (dev_fits(per, f)) cnt++;
+      const int32_t m = dminor(st, i, t, s);
+      if (m < 0) continue;
+      rc_free(st, rc, mode, i, t, s, f);
+      pk[np].s = s;
+      pk[np].minor = m;
+      pk[np].pref = pref && ((hm >> s) & 1u);
+      pk[np].score = scorer ? dev_scorer(cfg, t, st->soa->dev_total + dix(st, i, t, s), f, per) : 0;
+      np++;
     }
-    if (cnt < w) return 0;
+    qsort(pk, (size_t)np, sizeof(dev_pick), pick_cmp);
+    int64_t got = 0;
+    for (int j = 0; j < np && got < w; j++) {
+      if (req && hm && !((hm >> pk[j].s) & 1u)) continue;
+      rc_free(st, rc, mode, i, t, pk[j].s, f);
+      if (is_zero(f) || !dev_fits(per, f)) continue;
+      slots[t] |= 1u << pk[j].s;
+      got++;
+    }
+    if (got < w) return 0;
+    if (per_t) memcpy(per_t[t], per, sizeof(per));
   }
   return 1;
 }
 
-/* DeviceShare Score, scoring.go:33-72 -> nodeDevice.score (device_cache.go:
- * 397-452): per requested type, scoreNode over the sums of the node's device
- * totals and frees with the (GPU-filled) pod request; the types add up.
- * `nominated`: the Reservation plugin nominated a reservation on the node
- * (no DeviceShare reservation state: the score is 0, :54-59 / reservation.go:
- * 409-431). */
-int64_t orc_dev_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x, int32_t i,
-                      int nominated) {
-  if (!x || !(x->flags & KOORDHIP_PODX_DEVICE)) return 0;
-  if (!orc_dev_node_present(st, i) || nominated) return 0;
+/* tryAllocateFromReservation (reservation.go:181-283) over the node's matched
+ * reservation holding devices: 1 allocated (slots), 0 none (the caller falls
+ * back to the node), -1 Unschedulable (an Aligned / Restricted reservation
+ * that cannot hold the pod, :278-281).  fromResv: requiredFromReservation
+ * (FilterReservation): a Default reservation then also restricts to its minors. */
+static int dev_from_reservation(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x,
+                                int32_t i, const dev_rc *rc, int fromResv, int scorer, uint32_t *slots,
+                                int64_t per_t[T][R]) {
+  if (rc->h < 0 || rc->cls != 1) return 0;
+  if (rc->pol == 0) /* Default: preemptible = basic + mergedMatchedAllocatable, preferred its minors */
+    return dev_allocate(cfg, st, x, i, rc, fromResv, 1, FREE_NODE, scorer, slots, per_t) ? 1 : 0;
+  if (rc->pol == 1) /* Aligned: required = preferred = its minors */
+    return dev_allocate(cfg, st, x, i, rc, 1, 1, FREE_ALIGNED, scorer, slots, per_t) ? 1 : -1;
+  /* Restricted: the node fits (no scorer), then the reservation's remained holds it */
+  if (!dev_allocate(cfg, st, x, i, rc, 1, 1, FREE_ALIGNED, 0, slots, per_t)) return -1;
+  return dev_allocate(cfg, st, x, i, rc, 1, 1, FREE_REQUIRED, scorer, slots, per_t) ? 1 : -1;
+}
+
+/* tryAllocateFromReservation of the node's reservation holding devices for
+ * `pod` (no scorer): 1 / 0 / -1 as dev_from_reservation (KAT entry point). */
+int orc_dev_try_from_reservation(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i,
+                                 int fromResv, uint32_t *slots) {
+  const dev_rc rc = dev_rc_of(st, pod, i);
+  return dev_from_reservation(NULL, st, x, i, &rc, fromResv, 0, slots, NULL);
+}
+
+/* DeviceShare Filter, plugin.go:284-323: tryAllocateFromReservation over the
+ * matched reservation holding devices, else the node with the matched
+ * reservations' allocatable preemptible (no scorer).  1 = passes. */
+int orc_dev_filter(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i) {
+  if (!x || !(x->flags & KOORDHIP_PODX_DEVICE)) return 1; /* state.skip */
+  if (!orc_dev_node_present(st, i)) return 1;           /* nodeDeviceInfo == nil: :298-301 */
+  const dev_rc rc = dev_rc_of(st, pod, i);
+  uint32_t slots[T];
+  const int r = dev_from_reservation(NULL, st, x, i, &rc, 0, 0, slots, NULL);
+  if (r != 0) return r > 0;
+  return dev_allocate(NULL, st, x, i, &rc, 0, 0, FREE_NODE, 0, slots, NULL);
+}
+
+/* DeviceShare FilterReservation (plugin.go:325-356) of the node's reservation
+ * holding devices, for a matched one: tryAllocateFromReservation with
+ * requiredFromReservation.  1 = passes. */
+int orc_dev_filter_reservation(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i) {
+  if (!x || !(x->flags & KOORDHIP_PODX_DEVICE)) return 1;
+  const dev_rc rc = dev_rc_of(st, pod, i);
+  if (rc.h < 0 || rc.cls != 1) return 0; /* not in the restore's matched: allocIndex -1 */
+  if (!orc_dev_node_present(st, i)) return 1; /* :349-352 */
+  uint32_t slots[T];
+  return dev_from_reservation(NULL, st, x, i, &rc, 1, 0, slots, NULL) > 0;
+}
+
+/* scoreNode of type t over the free devices of `mode` (scoring.go:179-209;
+ * nodeDevice.scoreByDeviceType device_cache.go:425-452): sums of the node's
+ * totals and of the frees, the (GPU-filled) pod request */
+static int64_t dev_score_mode(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x, int32_t i,
+                              const dev_rc *rc, int mode) {
   int64_t sum = 0;
   for (int t = 0; t < T; t++) {
     int64_t q[R];
@@ -204,7 +384,7 @@ int64_t orc_dev_score(const koordhip_config *cfg, const orc_state *st, const koo
     for (int s = 0; s < st->soa->dev_slots; s++) {
       if (dminor(st, i, t, s) < 0) continue;
       const int64_t *tt = st->soa->dev_total + dix(st, i, t, s);
-      dev_free(st, i, t, s, f);
+      rc_free(st, rc, mode, i, t, s, f);
       for (int r = 0; r < R; r++) {
         tot[r] += tt[r];
         fr[r] += f[r];
@@ -217,68 +397,79 @@ int64_t orc_dev_score(const koordhip_config *cfg, const orc_state *st, const koo
   return sum;
 }
 
-typedef struct dev_pick {
-  int32_t s, minor;
-  int64_t score;
-} dev_pick;
-
-static int pick_cmp(const void *a, const void *b) {
-  const dev_pick *x = (const dev_pick *)a, *y = (const dev_pick *)b;
-  if (x->score != y->score) return x->score > y->score ? -1 : 1;
-  return x->minor < y->minor ? -1 : (x->minor > y->minor ? 1 : 0);
+/* DeviceShare Score, scoring.go:33-72 -> nodeDevice.score (device_cache.go:
+ * 397-452): per requested type, scoreNode; the types add up.  `nominated`: the
+ * Reservation plugin's PreScore nominated a reservation on the node: the
+ * device-holding one is scored by its policy (scoreWithReservation,
+ * reservation.go:286-342), any other gives 0 (:409-431, allocIndex -1). */
+int64_t orc_dev_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod,
+                      const koordhip_pod_ext *x, int32_t i, int nominated) {
+  if (!x || !(x->flags & KOORDHIP_PODX_DEVICE)) return 0;
+  if (!orc_dev_node_present(st, i)) return 0;
+  const dev_rc rc = dev_rc_of(st, pod, i);
+  if (nominated) {
+    const int q = pod ? orc_resv_nominate(st, pod, i) : -1;
+    if (q < 0 || q != rc.h || rc.cls != 1) return 0;
+    return dev_score_mode(cfg, st, x, i, &rc, rc.pol == 0 ? FREE_NODE : (rc.pol == 1 ? FREE_ALIGNED : FREE_REQUIRED));
+  }
+  return dev_score_mode(cfg, st, x, i, &rc, FREE_NODE);
 }
 
-/* DeviceShare Reserve, plugin.go:368-405 -> the default allocator's Allocate
- * with the plugin's scorer (allocator.go:91-102) and Reserve (:116-118): per
- * requested type the devices ordered by scoreDevices (device_resources.go:
- * 161-175) and sortDeviceResourcesByMinor (:177-195: score desc, minor asc; no
- * preferred minors), the first `wanted` that hold the per-device request;
- * updateCacheUsed adds it to each.  Returns 0 (allocation in slots[t], bit s =
- * dev slot s) or -1 (insufficient devices / a nominated reservation: the
- * Reserve fails and nothing is committed).  apply = 0: nothing changes. */
-int orc_dev_reserve(const koordhip_config *cfg, orc_state *st, const koordhip_pod_ext *x, int32_t i, int nominated,
-                    uint32_t *slots, int apply) {
+/* DeviceShare Reserve, plugin.go:368-405: the nominated reservation's
+ * allocation (allocateWithNominatedReservation :365-407 -> tryAllocateFrom-
+ * Reservation with the scorer), else the node's (the default allocator's
+ * Allocate with the plugin's scorer, allocator.go:91-102); Reserve adds it to
+ * deviceUsed (updateCacheUsed, allocator.go:116-118).  With the pod assumed
+ * into the device-holding reservation (the Reservation Reserve, `assumed`
+ * below) the next cycle's restore counts the allocation on its minors as its
+ * allocated (appendAllocatedByHints, reservation.go:145-151).  Returns 0
+ * (allocation in slots[t], bit s = dev slot s) or -1 (nothing committed). */
+int orc_dev_reserve(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x,
+                    int32_t i, int nominated, uint32_t *slots, int apply) {
   for (int t = 0; t < T; t++) slots[t] = 0;
   if (!x || !(x->flags & KOORDHIP_PODX_DEVICE)) return 0;
   if (!orc_dev_node_present(st, i)) return 0; /* :377-380 */
-  if (nominated) return -1;                   /* allocateWithNominatedReservation: missing nominated reservation */
+  const dev_rc rc = dev_rc_of(st, pod, i);
   int64_t per_t[T][R];
-  for (int t = 0; t < T; t++) {
-    int64_t q[R], per[R], f[R];
-    if (!dev_requests(x, t, q)) continue;
-    if (!has_type(st, i, t)) return -1;
-    if (t == KOORDHIP_DEV_GPU && !dev_fill_gpu(st, i, q)) return -1;
-    const int64_t w = dev_wanted(t, q, per);
-    dev_pick pk[KOORDHIP_DEV_SLOTS];
-    int np = 0;
-    for (int s = 0; s < st->soa->dev_slots; s++) {
-      const int32_t m = dminor(st, i, t, s);
-      if (m < 0) continue;
-      dev_free(st, i, t, s, f);
-      pk[np].s = s;
-      pk[np].minor = m;
-      pk[np].score = dev_scorer(cfg, t, st->soa->dev_total + dix(st, i, t, s), f, per);
-      np++;
-    }
-    qsort(pk, (size_t)np, sizeof(dev_pick), pick_cmp);
-    int64_t got = 0;
-    for (int j = 0; j < np && got < w; j++) {
-      dev_free(st, i, t, pk[j].s, f);
-      if (is_zero(f) || !dev_fits(per, f)) continue;
-      slots[t] |= 1u << pk[j].s;
-      got++;
-    }
-    if (got < w) return -1;
-    memcpy(per_t[t], per, sizeof(per));
+  memset(per_t, 0, sizeof(per_t));
+  int r = 0;
+  if (nominated) {
+    const int q = pod ? orc_resv_nominate(st, pod, i) : -1;
+    if (q < 0 || q != rc.h || rc.cls != 1) return -1; /* missing nominated reservation :391-393 */
+    r = dev_from_reservation(cfg, st, x, i, &rc, 0, 1, slots, per_t);
+    if (r < 0) return -1;
   }
-  if (!apply) return 0;
-  for (int t = 0; t < T; t++)
+  if (r == 0 && !dev_allocate(cfg, st, x, i, &rc, 0, 0, FREE_NODE, 1, slots, per_t)) return -1;
+  if (apply) orc_dev_apply(st, x, i, slots, -1);
+  return 0;
+}
+
+/* updateCacheUsed of an allocation (slots from orc_dev_reserve): deviceUsed
+ * += the per-device request; `assumed` = the slot of the reservation the
+ * Reservation Reserve assumed the pod into (-1 none): when it is the node's
+ * device-holding one, its allocated grows on its minors. */
+void orc_dev_apply(orc_state *st, const koordhip_pod_ext *x, int32_t i, const uint32_t *slots, int assumed) {
+  const int h = orc_dev_resv_slot(st, i);
+  for (int t = 0; t < T; t++) {
+    if (!slots[t]) continue;
+    int64_t q[R], per[R];
+    (void)dev_requests(x, t, q);
+    if (t == KOORDHIP_DEV_GPU) (void)dev_fill_gpu(st, i, q);
+    (void)dev_wanted(t, q, per);
+    uint32_t hm = 0u;
+    if (h >= 0 && assumed == h)
+      for (int s = 0; s < st->soa->dev_slots; s++)
+        if (!is_zero(st->resv_dev + rdix(st, i, 0, t, s))) hm |= 1u << s;
     for (int s = 0; s < st->soa->dev_slots; s++)
       if ((slots[t] >> s) & 1u) {
         int64_t *u = st->dev_used + dix(st, i, t, s);
-        for (int r = 0; r < R; r++) u[r] += per_t[t][r];
+        for (int r = 0; r < R; r++) u[r] += per[r];
+        if ((hm >> s) & 1u) {
+          int64_t *d = st->resv_dev + rdix(st, i, 1, t, s);
+          for (int r = 0; r < R; r++) d[r] += per[r];
+        }
       }
-  return 0;
+  }
 }
 
 /* (upstream, UPSTREAM-ASSUMED) noderesources fitsRequest over the pod's

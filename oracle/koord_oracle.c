@@ -154,6 +154,10 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
     if (!st->ipa_cnt) return -1;
     if (soa->ipa_cnt) memcpy(st->ipa_cnt, soa->ipa_cnt, sizeof(int32_t) * (size_t)soa->ipa_ents * (size_t)n);
   }
+  if (soa->resv_dev && soa->resv_dev_slot && soa->dev_slots > 0) {
+    st->resv_dev = dup64(soa->resv_dev, n * 2 * KOORDHIP_DEV_TYPES * soa->dev_slots * KOORDHIP_DEV_RES);
+    if (!st->resv_dev) return -1;
+  }
   if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned || !st->dev_used ||
       !st->xrequested)
     return -1;
@@ -186,6 +190,7 @@ void orc_state_free(orc_state *st) {
   free(st->xrequested);
   free(st->pts_cnt);
   free(st->ipa_cnt);
+  free(st->resv_dev);
   memset(st, 0, sizeof(*st));
 }
 
@@ -334,7 +339,7 @@ static int orc_feasible(const koordhip_config *cfg, const orc_state *st, const k
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_IPA) && !orc_ipa_filter(st, x, ia, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_fit_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_FIT) && !orc_xfit_filter(st, x, i)) return 0;
-  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) return 0;
+  if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, pod, x, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_LOADAWARE) && !orc_la_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) return 0;
   if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && !resv_pass(st, pod, x, i)) return 0;
@@ -454,6 +459,8 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
     const koordhip_pod_ext *x = ext ? &ext[p] : NULL;
     const koordhip_pod pp = orc_devshare_pod(cfg, &pods[p], x);
     const koordhip_pod *pod = &pp;
+    ((orc_state *)st)->cur_ext = x;
+    ((orc_state *)st)->resv_restore = rv;
     orc_pts ps;
     orc_ipa ia;
     if (orc_pts_prefilter(cfg, st, x, &ps)) return -1;
@@ -480,7 +487,7 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_NUMA) && !orc_numa_filter(cfg, st, pod, i)) b |= KOORDHIP_ST_NUMA_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_RESERVATION) && !resv_pass(st, pod, x, i))
           b |= KOORDHIP_ST_RESV_FAIL;
-        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, x, i)) b |= KOORDHIP_ST_DEVICE_FAIL;
+        if ((cfg->filter_plugins & KOORDHIP_PLUGIN_DEVICESHARE) && !orc_dev_filter(st, pod, x, i)) b |= KOORDHIP_ST_DEVICE_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_PTS) && !orc_pts_filter(st, x, &ps, i)) b |= KOORDHIP_ST_PTS_FAIL;
         if ((cfg->filter_plugins & KOORDHIP_PLUGIN_IPA) && !orc_ipa_filter(st, x, &ia, i)) b |= KOORDHIP_ST_IPA_FAIL;
         status[(size_t)p * n + i] = b;
@@ -496,7 +503,7 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
         row[3 * (size_t)n + i] =
             (cfg->score_plugins & KOORDHIP_PLUGIN_BALANCED) ? (int32_t)orc_bal_score(cfg, st, pod, i) : 0;
         row[4 * (size_t)n + i] =
-            (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? (int32_t)orc_dev_score(cfg, st, x, i, nom) : 0;
+            (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? (int32_t)orc_dev_score(cfg, st, pod, x, i, nom) : 0;
         row[5 * (size_t)n + i] =
             (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? (int32_t)orc_static_score(st, pod, i, 0) : 0;
         row[6 * (size_t)n + i] =
@@ -512,7 +519,7 @@ int orc_eval_ext(const koordhip_config *cfg, const orc_state *st, const koordhip
         const int32_t i = feas[j];
         const int nom = rs && orc_resv_nominated(st, pod, i);
         base[j] = orc_total(cfg, st, pod, i);
-        raw[j] = (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? orc_dev_score(cfg, st, x, i, nom) : 0;
+        raw[j] = (cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? orc_dev_score(cfg, st, pod, x, i, nom) : 0;
         raw[(size_t)nf + j] = (cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? orc_static_score(st, pod, i, 0) : 0;
         raw[2 * (size_t)nf + j] = (cfg->score_plugins & KOORDHIP_PLUGIN_TAINT_SCORE) ? orc_static_score(st, pod, i, 1) : 0;
         raw[3 * (size_t)nf + j] = ptsraw[i];
@@ -614,10 +621,15 @@ int orc_commit_ext(const koordhip_config *cfg, orc_state *st, const koordhip_pod
   const int dev = (cfg->filter_plugins | cfg->score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE;
   const koordhip_pod pp = orc_devshare_pod(cfg, pod, x);
   pod = &pp;
-  if (dev && orc_dev_reserve(cfg, st, x, i, nominated, slots, 0)) return KOORDHIP_ERESERVE;
+  st->cur_ext = x;
+  st->resv_restore = orc_resv_on(cfg, st);
+  /* the reservation the Reservation Reserve will assume the pod into, decided
+   * on the state before any Reserve */
+  const int assumed = (st->resv_restore && orc_resv_node_present(st, i)) ? orc_resv_nominate(st, pod, i) : -1;
+  if (dev && orc_dev_reserve(cfg, st, pod, x, i, nominated, slots, 0)) return KOORDHIP_ERESERVE;
   const int rc = orc_commit(cfg, st, pod, i, +1, cpus);
   if (rc) return rc;
-  if (dev) (void)orc_dev_reserve(cfg, st, x, i, nominated, slots, 1);
+  if (dev) orc_dev_apply(st, x, i, slots, assumed);
   if (devs)
     for (int t = 0; t < KOORDHIP_DEV_TYPES; t++) devs[t] = slots[t];
   if (x)
@@ -785,7 +797,7 @@ static void score_piece(void *a, int32_t lo, int32_t hi) {
                                  KOORDHIP_PLUGIN_TAINT_SCORE)) {
       int64_t *x = c->plugin_scores + (size_t)KOORDHIP_NPLUGINS * nf;
       const int nom = c->resv_score && orc_resv_nominated(c->st, c->pod, i);
-      x[j] = (c->cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? orc_dev_score(c->cfg, c->st, c->ext, i, nom) : 0;
+      x[j] = (c->cfg->score_plugins & KOORDHIP_PLUGIN_DEVICESHARE) ? orc_dev_score(c->cfg, c->st, c->pod, c->ext, i, nom) : 0;
       x[(size_t)nf + j] =
           (c->cfg->score_plugins & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? orc_static_score(c->st, c->pod, i, 0) : 0;
       x[2 * (size_t)nf + j] =
@@ -834,6 +846,8 @@ int orc_place_stream_ext(const koordhip_config *cfg, orc_state *st, const koordh
     c.ext = ext ? &ext[p] : NULL;
     const koordhip_pod pp = orc_devshare_pod(cfg, &pods[p], c.ext);
     c.pod = &pp;
+    st->cur_ext = c.ext;
+    st->resv_restore = rv;
     uint32_t *devs = st->dev_out ? st->dev_out + (size_t)p * KOORDHIP_DEV_TYPES : NULL;
     if (devs) memset(devs, 0, sizeof(uint32_t) * KOORDHIP_DEV_TYPES);
     orc_pts_free(&ps);

@@ -72,6 +72,15 @@ typedef struct orc_state {
   int32_t *pts_cnt;
   /* InterPodAffinity: each count entry's pods per node [ents][n] (ipa_oracle.c) */
   int32_t *ipa_cnt;
+  /* DeviceShare: the resv_dev column of the snapshot's device-holding
+   * reservations, its allocated half advanced by Reserve (NULL: none) */
+  int64_t *resv_dev;
+  /* the koordhip_pod_ext record of the pod being scheduled (NULL: none): the
+   * nomination's DeviceShare FilterReservation reads it */
+  const koordhip_pod_ext *cur_ext;
+  /* the Reservation plugin's BeforePreFilter runs (orc_resv_on): the
+   * DeviceShare reservation restore exists */
+  int32_t resv_restore;
 } orc_state;
 
 /* PodTopologySpread per-pod state (pts_oracle.c): PreFilter's pairs and
@@ -208,14 +217,25 @@ void orc_resv_normalized(const orc_state *st, const koordhip_pod *pod, const int
 int64_t orc_resv_rank_total(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod, int32_t i,
                             int64_t b);
 
-/* DeviceShare, extended scalars, upstream normalized Scores (dev_oracle.c). */
+/* DeviceShare, extended scalars, upstream normalized Scores (dev_oracle.c).
+ * pod (NULL: no reservation context) is the pod being scheduled. */
 int orc_dev_node_present(const orc_state *st, int32_t i);
-int orc_dev_filter(const orc_state *st, const koordhip_pod_ext *x, int32_t i);
-int64_t orc_dev_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod_ext *x, int32_t i,
-                      int nominated);
-/* apply = 0: the allocation only (nothing changes) */
-int orc_dev_reserve(const koordhip_config *cfg, orc_state *st, const koordhip_pod_ext *x, int32_t i, int nominated,
-                    uint32_t *slots, int apply);
+int orc_dev_filter(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i);
+int64_t orc_dev_score(const koordhip_config *cfg, const orc_state *st, const koordhip_pod *pod,
+                      const koordhip_pod_ext *x, int32_t i, int nominated);
+/* apply = 0: the allocation only (nothing changes); apply with `assumed`
+ * (the Reservation Reserve assumed the pod into the node's device-holding
+ * reservation) also advances that reservation's allocated devices */
+int orc_dev_reserve(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x,
+                    int32_t i, int nominated, uint32_t *slots, int apply);
+int orc_dev_try_from_reservation(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i,
+                                 int fromResv, uint32_t *slots);
+void orc_dev_apply(orc_state *st, const koordhip_pod_ext *x, int32_t i, const uint32_t *slots, int assumed);
+/* the slot of node i's reservation holding devices, -1 none */
+int orc_dev_resv_slot(const orc_state *st, int32_t i);
+/* DeviceShare FilterReservation of that reservation (plugin.go:325-356) */
+int orc_dev_filter_reservation(const orc_state *st, const koordhip_pod *pod, const koordhip_pod_ext *x, int32_t i);
+int orc_resv_slot_class(const orc_state *st, const koordhip_pod *pod, int s, int32_t i);
 int orc_xfit_filter(const orc_state *st, const koordhip_pod_ext *x, int32_t i);
 int64_t orc_static_score(const orc_state *st, const koordhip_pod *pod, int32_t i, int which);
 void orc_default_normalize(int64_t *scores, int32_t nf, int reverse);

@@ -65,6 +65,10 @@ static int slot_class(const orc_state *st, const koordhip_pod *pod, size_t x) {
   return assigned > 0 ? 2 : 0;                                                     /* :100-101 */
 }
 
+int orc_resv_slot_class(const orc_state *st, const koordhip_pod *pod, int s, int32_t i) {
+  return st->soa->resv_flags ? slot_class(st, pod, at(st, s, i)) : 0;
+}
+
 void orc_resv_classify(const orc_state *st, const koordhip_pod *pod, int32_t i, int *matched, int *unmatched) {
   *matched = *unmatched = 0;
   if (!st->soa->resv_flags) return;
@@ -236,18 +240,25 @@ static int64_t slot_score(const orc_state *st, const koordhip_pod *pod, size_t x
  * requesting devices that one looks the reservation up among the node's
  * RestoreReservation state, which keeps only reservations holding devices
  * (reservation.go:134-161, `len(allocatable) == 0` -> skipped); a reservation
- * holding none fails it (allocIndex -1 -> an error status, :337-346).  No
- * reservation holds devices in the engine's envelope, so a device pod is never
- * nominated (and DeviceShare's ScoreReservation, 0 for every candidate left,
- * changes no ranking). */
+ * holding none fails it (allocIndex -1 -> an error status, :337-346), the
+ * node's one reservation holding devices passes it when
+ * tryAllocateFromReservation(requiredFromReservation) allocates
+ * (orc_dev_filter_reservation).  With at most that one candidate left,
+ * DeviceShare's ScoreReservation (normalized over the candidates) changes no
+ * ranking. */
 int orc_resv_nominate(const orc_state *st, const koordhip_pod *pod, int32_t i) {
   if (!st->soa->resv_flags) return -1;
-  if (pod->flags & ORC_POD_DEVSHARE) return -1;
+  const int devshare = (pod->flags & ORC_POD_DEVSHARE) != 0;
+  const int dslot = devshare ? orc_dev_resv_slot(st, i) : -1;
+  if (devshare && (dslot < 0 || slot_class(st, pod, at(st, dslot, i)) != 1 ||
+                   !orc_dev_filter_reservation(st, pod, st->cur_ext, i)))
+    return -1;
   int best = -1, best_rank = 0, ord = 0;
   int64_t best_sc = -1;
   for (int s = 0; s < orc_resv_slots(st); s++) {
     const size_t x = at(st, s, i);
     if (slot_class(st, pod, x) != 1 || !slot_passes(st, pod, x)) continue;
+    if (devshare && s != dslot) continue;
     const uint32_t rf = st->soa->resv_flags[x];
     if (rf & KOORDHIP_RESV_ORDERED) {
       const int rk = st->soa->resv_order_rank[x];
