@@ -196,6 +196,7 @@ struct koordhip_ctx {
   int32_t podx_cap = 0;
   bool podx_staged = false;
   bool staged_qos_nonbind = false;  // a staged pod KOORDHIP_POD_CPUSET_QOS rejects on some snapshots
+  bool staged_dsr = false;          // the staged device pods carry kh::KH_POD_DEVSHARE (reservations were loaded)
   bool staged_reserve = false;     // the staged batch holds a reserve pod (KOORDHIP_POD_RESERVE): the sequential cycle
   bool staged_ext = false;         // the staged batch's koordhip_pod_ext records carry requests / constraints
   // device pods inside the pipelined greedy (k_ext_worker, seq.hip): the
@@ -1926,6 +1927,10 @@ static int stage_classes(koordhip_ctx *c, const std::vector<kh::DevPod> &hp) {
 static bool devshare_on(const koordhip_ctx *c) {
   return ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
 }
+// kh::KH_POD_DEVSHARE only matters to the reservation nomination: without
+// reservations it stays off, so device pods keep sharing pod classes with
+// byte-identical plain pods (the class lists of the pipelined greedy)
+static bool devshare_resv_on(const koordhip_ctx *c) { return devshare_on(c) && c->dc.resv; }
 
 // ext (optional): the pods' records, for kh::KH_POD_DEVSHARE (staged by stage_ext)
 static int stage_pods_impl(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_pods, const koordhip_pod_ext *ext) {
@@ -1934,7 +1939,7 @@ static int stage_pods_impl(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_
   bool reserve = false;
   if (int e = check_reserve_pods(c, pods, n_pods, &reserve)) return e;
   std::vector<kh::DevPod> hp;
-  if (int e = to_dev_pods(pods, n_pods, hp, ext, devshare_on(c))) return e;
+  if (int e = to_dev_pods(pods, n_pods, hp, ext, devshare_resv_on(c))) return e;
   HIP_TRY(hipSetDevice(c->device));
   if (n_pods > c->pods_cap) {
     if (c->d_pods) HIP_TRY(hipFree(c->d_pods));
@@ -1955,6 +1960,7 @@ static int stage_pods_impl(koordhip_ctx *c, const koordhip_pod *pods, int32_t n_
   if (int e = stage_classes(c, hp)) return e;
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->n_staged = n_pods;
+  c->staged_dsr = devshare_resv_on(c);
   c->podx_staged = false;
   c->staged_ext = false;
   c->staged_ext_dev = false;
@@ -2205,7 +2211,7 @@ int koordhip_eval_ext(koordhip_ctx *c, const koordhip_pod *pods, const koordhip_
       if (p) (void)hipFree(p);
   };
   std::vector<kh::DevPod> hp;
-  if (int ce = to_dev_pods(pods, n_pods, hp, ext, devshare_on(c))) return ce;
+  if (int ce = to_dev_pods(pods, n_pods, hp, ext, devshare_resv_on(c))) return ce;
   if (hipMalloc(&dp, (size_t)per * sizeof(kh::DevPod)) != hipSuccess ||
       (ext && hipMalloc(&dx, (size_t)per * sizeof(kh::DevPodX)) != hipSuccess) ||
       hipMalloc(&dst, (size_t)per * std::max(n, 1)) != hipSuccess ||
@@ -2340,6 +2346,8 @@ extern "C" {
 
 int koordhip_place_staged(koordhip_ctx *c) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
+  if (c->n_staged > 0 && c->staged_dsr != devshare_resv_on(c))
+    return fail(KOORDHIP_ESTATE, "the pods were staged under a snapshot with(out) reservations; stage them again");
   const int e = place_staged_impl(c);
   if (e && c->group) c->group->abort();
   return e;
@@ -3240,7 +3248,7 @@ static int commit_ext_impl(koordhip_ctx *c, const koordhip_pod *pod, const koord
   uint64_t *d_cpus = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(c->d_rc) + sizeof(uint64_t));
   uint32_t *d_dev = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(c->d_rc) + 40);
   std::vector<kh::DevPod> hp;
-  if (int e = to_dev_pods(pod, 1, hp, ext, devshare_on(c))) return e;
+  if (int e = to_dev_pods(pod, 1, hp, ext, devshare_resv_on(c))) return e;
   HIP_TRY(hipMemcpyAsync(c->d_tmp_pod, hp.data(), sizeof(kh::DevPod), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_tmp_podx, ext, sizeof(kh::DevPodX), hipMemcpyHostToDevice, c->stream));
   uint64_t cz[KOORDHIP_NUMA_WORDS] = {0, 0, 0, 0};
