@@ -654,6 +654,49 @@ def add_devices(t: NodeTable, spec: DevSpec, seed: int = SEED) -> NodeTable:
 
 
 @dataclass
+class DevResvSpec:
+    """Reservations holding devices (after add_reservations and add_devices):
+    on a GPU node with an Available reservation in slot 0, with probability
+    `frac` the reservation's reserve pod holds one or two of its GPUs (25, 50 or
+    100 % of each) and its assigned pods a share of that (0, 1/4 or 1/2); the
+    reservation's AllocatePolicy is drawn from `policy` (Default, Aligned,
+    Restricted)."""
+    frac: float = 0.8
+    policy: tuple = (0.5, 0.25, 0.25)
+
+
+def add_device_reservations(t: NodeTable, spec: DevResvSpec = DevResvSpec(), seed: int = SEED) -> NodeTable:
+    """The resv_dev_* columns: both allocations join dev_used, as in the
+    nodeDevice cache (the reserve pod and its assigned pods are pods of the node)."""
+    G = abi.DEV_GPU
+    rng = np.random.default_rng(seed + 1000)
+    t.enable_resv_dev()
+    pol = rng.choice(3, size=t.n, p=list(spec.policy))
+    for i in range(t.n):
+        if not (t["resv_flags"][i] & abi.RESV_PRESENT) or not t["dev_present"][i]:
+            continue
+        gpus = [s for s in range(t.dev_slots) if t["dev_minor"][i, G, s] >= 0 and t["dev_total"][i, G, s].any()]
+        if not gpus or rng.random() >= spec.frac:
+            continue
+        for s in rng.choice(gpus, size=min(len(gpus), int(rng.integers(1, 3))), replace=False):
+            tot = t["dev_total"][i, G, s]
+            frac = int(rng.choice([25, 50, 100]))
+            a = np.array([tot[0] * frac // 100, frac, tot[2] * frac // 100], np.int64)
+            a = np.minimum(a, np.maximum(tot - t["dev_used"][i, G, s], 0))
+            d = np.minimum(a * int(rng.choice([0, 0, 1, 2])) // 4, a)
+            if not a.any():
+                continue
+            t["resv_dev"][i, 0, G, s] = a
+            t["resv_dev"][i, 1, G, s] = d
+            t["dev_used"][i, G, s] += a + d
+        if t["resv_dev"][i, 0].any():
+            t["resv_dev_slot"][i] = 0
+            f = int(t["resv_flags"][i]) & ~(3 << abi.RESV_POLICY_SHIFT)
+            t["resv_flags"][i] = f | (int(pol[i]) << abi.RESV_POLICY_SHIFT)
+    return t
+
+
+@dataclass
 class DevStreamSpec:
     """Device pods of a stream (their koordhip_pod_ext records): a share of the
     pods request GPUs in the reference's request forms -- koordinator.sh/gpu

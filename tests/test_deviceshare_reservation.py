@@ -153,10 +153,9 @@ def test_try_allocate_from_reservation_kat(case):
         assert r == 1 and int(slots[abi.DEV_GPU]) == 1 << want
 
 
-def _dev_resv_cluster(n, seed, policy_frac=(0.5, 0.25, 0.25)):
-    """A DeviceShare + Reservation (+ NUMA) cluster whose reservations on GPU
-    nodes hold devices: the reserve pod's allocation (A, one or two GPUs, part
-    or whole) and its assigned pods' share of it (D <= A) are in dev_used."""
+def _dev_resv_cluster(n, seed):
+    """A DeviceShare + Reservation + NodeNUMAResource cluster whose reservations
+    on GPU nodes hold devices (synth.add_device_reservations)."""
     from koordinator_amd.config import shipped_profile
     from koordinator_amd import synth
     prof = with_deviceshare(shipped_profile(numa=True, reservation=True))
@@ -164,33 +163,7 @@ def _dev_resv_cluster(n, seed, policy_frac=(0.5, 0.25, 0.25)):
     synth.add_numa(t, synth.NumaSpec(), prof, seed=seed)
     synth.add_reservations(t, synth.ResvSpec(node_frac=0.6), seed=seed)
     synth.add_devices(t, synth.DevSpec(gpu_frac=0.6), seed=seed)
-    rng = np.random.default_rng(seed + 1000)
-    t.enable_resv_dev()
-    pol = rng.choice(3, size=n, p=policy_frac)
-    for i in range(n):
-        if not (t["resv_flags"][i] & abi.RESV_PRESENT) or not t["dev_present"][i]:
-            continue
-        gpus = [s for s in range(t.dev_slots) if t["dev_minor"][i, abi.DEV_GPU, s] >= 0
-                and t["dev_total"][i, abi.DEV_GPU, s].any()]
-        if not gpus or rng.random() < 0.2:
-            continue
-        t["resv_flags"][i] = (int(t["resv_flags"][i]) & ~(3 << abi.RESV_POLICY_SHIFT)) | (int(pol[i]) << abi.RESV_POLICY_SHIFT)
-        t["resv_dev_slot"][i] = 0
-        for s in rng.choice(gpus, size=min(len(gpus), int(rng.integers(1, 3))), replace=False):
-            tot = t["dev_total"][i, abi.DEV_GPU, s]
-            frac = int(rng.choice([25, 50, 100]))
-            a = np.array([tot[0] * frac // 100, frac, tot[2] * frac // 100], np.int64)
-            d = a * int(rng.choice([0, 0, 1, 2])) // 4
-            free = tot - t["dev_used"][i, abi.DEV_GPU, s]
-            a = np.minimum(a, np.maximum(free, 0))
-            d = np.minimum(d, a)
-            if not a.any():
-                continue
-            t["resv_dev"][i, 0, abi.DEV_GPU, s] = a
-            t["resv_dev"][i, 1, abi.DEV_GPU, s] = d
-            t["dev_used"][i, abi.DEV_GPU, s] += a + d
-        if not t["resv_dev"][i, 0].any():
-            t["resv_dev_slot"][i] = -1
+    synth.add_device_reservations(t, synth.DevResvSpec(), seed=seed)
     return prof, t
 
 
