@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define KOORDHIP_ABI_VERSION 13
+#define KOORDHIP_ABI_VERSION 14
 
 /* ---- error codes ------------------------------------------------------- */
 #define KOORDHIP_OK 0
@@ -458,6 +458,26 @@ typedef struct koordhip_node_soa {
    * sequential cycle places batches on such snapshots. */
   const int32_t *resv_dev_slot;
   const int64_t *resv_dev;
+  /* ABI 14: the NodeResourcesFit extended scalars of that reservation
+   * (koordinator.sh/gpu-core, nvidia.com/gpu, ...; the KOORDHIP_NXRES slots of
+   * xalloc): resv_xalloc [NXRES][n] = its Allocatable's scalars (the reserve
+   * pod's scalar requests; a scalar it lists must be > 0: the host rejects a
+   * zero-valued key), resv_xallocated [NXRES][n] = its Allocated's (its
+   * AssignedPods' scalar requests masked to those keys, reservation_info.go:
+   * 297-306; advanced by Reserve).  0 on nodes whose resv_dev_slot is -1.  They
+   * enter every rule the reference applies to a reservation's ResourceList:
+   * the restore of NodeInfo.Requested's scalars (RemovePod of the reserve pod
+   * for a matched reservation, -Allocatable + SubtractWithNonNegativeResult(
+   * Allocatable, Allocated) for an unmatched one with assigned pods,
+   * transformer.go:227-293), filterWithReservations' fitsNode over the pod's
+   * scalars (plugin.go:445-494), Restricted's LessThanOrEqual (:420-432),
+   * FilterReservation's intersection (:504-535), scoreReservation's
+   * MostAllocated over RemoveZeros(Allocatable) (scoring.go:177-200) and the
+   * Reserve's AddAssignedPod.  NULL = none.  A snapshot with a non-zero value
+   * places every batch in the sequential cycle (koordhip_eval refuses it: use
+   * koordhip_eval_ext). */
+  const int64_t *resv_xalloc;
+  const int64_t *resv_xallocated;
 } koordhip_node_soa;
 
 /* One pod of the stream, the host-side PreFilter product (96 bytes). */
@@ -562,6 +582,9 @@ int koordhip_read_resv_cpus(koordhip_ctx *ctx, uint64_t *cpus);
 /* ABI 13: the loaded resv_dev column [n][2][TYPES][dev_slots][RES] (its
  * allocated half advanced by Reserve); zeros without one. */
 int koordhip_read_resv_devices(koordhip_ctx *ctx, int64_t *resv_dev);
+/* ABI 14: the loaded resv_xallocated column [NXRES][n] (advanced by Reserve);
+ * zeros without one. */
+int koordhip_read_resv_scalars(koordhip_ctx *ctx, int64_t *resv_xallocated);
 
 /* Parity/debug mode, no commit: for n_pods pods against the current state.
  *   status : optional, [n_pods][n] KOORDHIP_ST_* bits (every plugin evaluated)

@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-KOORDHIP_ABI_VERSION = 13
+KOORDHIP_ABI_VERSION = 14
 NRES = 5
 NPLUGINS = 4
 
@@ -187,6 +187,8 @@ class KoordhipNodeSoa(C.Structure):
         ("ipa_cnt", _i32p),
         ("resv_dev_slot", _i32p),
         ("resv_dev", _i64p),
+        ("resv_xalloc", _i64p),
+        ("resv_xallocated", _i64p),
     ]
 
 
@@ -311,6 +313,7 @@ def load_library(path: str = LIB_PATH):
         "koordhip_read_reservations": (C.c_int, [vp, _i64p, _i32p]),
         "koordhip_read_resv_cpus": (C.c_int, [vp, _u64p]),
         "koordhip_read_resv_devices": (C.c_int, [vp, _i64p]),
+        "koordhip_read_resv_scalars": (C.c_int, [vp, _i64p]),
         "koordhip_last_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
         "koordhip_last_kernel_stats": (C.c_int, [vp, C.POINTER(KoordhipKernelStats)]),
@@ -338,7 +341,7 @@ EXPORTED_SYMBOLS = [
     "koordhip_synchronize", "koordhip_checkpoint", "koordhip_restore", "koordhip_commit", "koordhip_uncommit",
     "koordhip_commit_ext", "koordhip_uncommit_ext",
     "koordhip_fetch_cpusets", "koordhip_read_numa", "koordhip_read_numa_zones", "koordhip_read_reservations",
-    "koordhip_read_resv_cpus", "koordhip_read_resv_devices", "koordhip_last_stats", "koordhip_last_kernel_stats",
+    "koordhip_read_resv_cpus", "koordhip_read_resv_devices", "koordhip_read_resv_scalars", "koordhip_last_stats", "koordhip_last_kernel_stats",
     "koordhip_set_profile_kernels", "koordhip_last_kernel_names",
     "koordhip_comm_unique_id", "koordhip_comm_init", "koordhip_comm_init_local",
 ]

@@ -189,6 +189,7 @@ struct koordhip_ctx {
                                    // PodTopologySpread, InterPodAffinity): a batch whose records are all empty
                                    // (no device / extended-scalar request, no spread constraint or counted
                                    // match, no affinity term or count entry) couples no nodes and runs pipelined
+  bool resv_x = false;             // a device-holding reservation lists extended scalars (ABI 14 resv_xalloc)
   bool seq_snap = false;           // the snapshot needs the sequential cycle (Reservation + topology-policy
                                    // nodes, or more than KOORDHIP_RESV_SLOTS reservations on a node)
   bool last_seq = false;           // the last place call ran the sequential cycle
@@ -785,12 +786,67 @@ int load_resv_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   return e;
 }
 
+// The device-holding reservation columns of a snapshot or of update rows (m
+// rows, slot-major reservation columns of stride m): each node's one such
+// reservation names an Available slot, holds devices only on the node's minors,
+// its allocated only on its own minors; values in [0, 2^45).
+int check_resv_dev(const koordhip_node_soa *s, int32_t n) {
+  const int32_t S = s->resv_slots > 1 ? s->resv_slots : 1;
+  if (!s->resv_flags) return fail(KOORDHIP_EINVAL, "resv_dev without reservation columns");
+  const size_t per = (size_t)KOORDHIP_DEV_TYPES * s->dev_slots * KOORDHIP_DEV_RES;
+  for (int32_t i = 0; i < n; i++) {
+    const int32_t h = s->resv_dev_slot[i];
+    if (h < -1 || h >= S) return fail(KOORDHIP_EINVAL, "resv_dev_slot out of [-1, resv_slots)");
+    const int64_t *row = s->resv_dev + (size_t)i * 2 * per;
+    bool any = false;
+    for (size_t a = 0; a < 2 * per; a++) {
+      if (row[a] < 0 || row[a] >= (1ll << 45)) return fail(KOORDHIP_EINVAL, "resv_dev out of [0, 2^45)");
+      any = any || (a < per && row[a] != 0);
+    }
+    if (h < 0) {
+      for (size_t a = 0; a < 2 * per; a++)
+        if (row[a]) return fail(KOORDHIP_EINVAL, "resv_dev values on a node without a device-holding reservation");
+      continue;
+    }
+    if (!(s->resv_flags[(size_t)h * n + i] & KOORDHIP_RESV_PRESENT))
+      return fail(KOORDHIP_EINVAL, "resv_dev_slot names an empty reservation slot");
+    if (!any) return fail(KOORDHIP_EINVAL, "a device-holding reservation with no devices (use resv_dev_slot -1)");
+    // its minors are the node's; its allocated lies on them
+    for (int t = 0; t < KOORDHIP_DEV_TYPES; t++)
+      for (int32_t q = 0; q < s->dev_slots; q++) {
+        const int64_t *A = row + ((size_t)t * s->dev_slots + q) * KOORDHIP_DEV_RES;
+        const int64_t *D = A + per;
+        const bool a = A[0] || A[1] || A[2], d = D[0] || D[1] || D[2];
+        if ((a || d) && s->dev_minor[((size_t)i * KOORDHIP_DEV_TYPES + t) * s->dev_slots + q] < 0)
+          return fail(KOORDHIP_EINVAL, "resv_dev on an empty device slot");
+        if (d && !a) return fail(KOORDHIP_EINVAL, "resv_dev allocated outside the reservation's minors");
+      }
+  }
+  return 0;
+}
+
+// ABI 14: the extended scalars of the device-holding reservations, [NXRES][m]
+// rows of a snapshot or of update rows: values in [0, 2^45) (the scorer's
+// 100 x quotient stays exact), none on a node without such a reservation.
+int check_resv_scalars(const int64_t *xa, const int64_t *xd, const int32_t *slot, int32_t m) {
+  for (int j = 0; j < KOORDHIP_NXRES; j++)
+    for (int32_t i = 0; i < m; i++) {
+      const int64_t a = xa[(size_t)j * m + i], d = xd ? xd[(size_t)j * m + i] : 0;
+      if (a < 0 || a >= (1ll << 45) || d < 0 || d >= (1ll << 45))
+        return fail(KOORDHIP_EINVAL, "resv_xalloc / resv_xallocated out of [0, 2^45)");
+      if ((a || d) && (!slot || slot[i] < 0))
+        return fail(KOORDHIP_EINVAL, "resv_xalloc / resv_xallocated on a node without a device-holding reservation");
+    }
+  return 0;
+}
+
 // ABI 9 columns of the sequential cycle: DeviceShare devices, extended
 // scalars, static Scores (int64 on device: the device code is integer).
 int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
   kh::DevDev &dv = c->d.dv;
   dv = kh::DevDev{};
   const bool dev = ((c->cfg.filter_plugins | c->cfg.score_plugins) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+  c->resv_x = false;
   if (!c->seq_profile) {
     if (s->dev_slots > 0 || s->xalloc || s->static_score[0] || s->static_score[1] || s->pts_keys > 0 || s->ipa_ents > 0)
       return fail(KOORDHIP_EINVAL, "device / extended-scalar / static-score / topology-spread columns need DeviceShare, "
@@ -841,37 +897,8 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
     // DeviceShare's reservation restore (deviceshare/reservation.go:119-170):
     // each node's one reservation holding devices
     if (!e && s->resv_dev_slot && s->resv_dev) {
-      const int32_t S = s->resv_slots > 1 ? s->resv_slots : 1;
-      if (!s->resv_flags) return fail(KOORDHIP_EINVAL, "resv_dev without reservation columns");
+      if (int ce = check_resv_dev(s, n)) return ce;
       const size_t per = (size_t)KOORDHIP_DEV_TYPES * s->dev_slots * KOORDHIP_DEV_RES;
-      for (int32_t i = 0; i < n; i++) {
-        const int32_t h = s->resv_dev_slot[i];
-        if (h < -1 || h >= S) return fail(KOORDHIP_EINVAL, "resv_dev_slot out of [-1, resv_slots)");
-        const int64_t *row = s->resv_dev + (size_t)i * 2 * per;
-        bool any = false;
-        for (size_t a = 0; a < 2 * per; a++) {
-          if (row[a] < 0 || row[a] >= (1ll << 45)) return fail(KOORDHIP_EINVAL, "resv_dev out of [0, 2^45)");
-          any = any || (a < per && row[a] != 0);
-        }
-        if (h < 0) {
-          for (size_t a = 0; a < 2 * per; a++)
-            if (row[a]) return fail(KOORDHIP_EINVAL, "resv_dev values on a node without a device-holding reservation");
-          continue;
-        }
-        if (!(s->resv_flags[(size_t)h * n + i] & KOORDHIP_RESV_PRESENT))
-          return fail(KOORDHIP_EINVAL, "resv_dev_slot names an empty reservation slot");
-        if (!any) return fail(KOORDHIP_EINVAL, "a device-holding reservation with no devices (use resv_dev_slot -1)");
-        // its minors are the node's; its allocated lies on them
-        for (int t = 0; t < KOORDHIP_DEV_TYPES; t++)
-          for (int32_t q = 0; q < s->dev_slots; q++) {
-            const int64_t *A = row + ((size_t)t * s->dev_slots + q) * KOORDHIP_DEV_RES;
-            const int64_t *D = A + per;
-            const bool a = A[0] || A[1] || A[2], d = D[0] || D[1] || D[2];
-            if ((a || d) && s->dev_minor[((size_t)i * KOORDHIP_DEV_TYPES + t) * s->dev_slots + q] < 0)
-              return fail(KOORDHIP_EINVAL, "resv_dev on an empty device slot");
-            if (d && !a) return fail(KOORDHIP_EINVAL, "resv_dev allocated outside the reservation's minors");
-          }
-      }
       int32_t *rs = nullptr;
       int64_t *rd = nullptr;
       e = dev_alloc(c, &rs, n);
@@ -880,8 +907,23 @@ int load_ext_columns(koordhip_ctx *c, const koordhip_node_soa *s, int32_t n) {
       if (!e) e = upload(c, rd, s->resv_dev, (size_t)n * 2 * per);
       dv.rslot = rs;
       dv.rdev = rd;
+      // ABI 14: that reservation's extended scalars (Allocatable, Allocated)
+      if (!e && s->resv_xalloc) {
+        if (int xe = check_resv_scalars(s->resv_xalloc, s->resv_xallocated, s->resv_dev_slot, n)) return xe;
+        int64_t *xa = nullptr, *xd = nullptr;
+        e = dev_alloc(c, &xa, (size_t)n * KOORDHIP_NXRES);
+        if (!e) e = upload(c, xa, s->resv_xalloc, (size_t)n * KOORDHIP_NXRES);
+        if (!e) e = dev_alloc(c, &xd, (size_t)n * KOORDHIP_NXRES);
+        if (!e) e = upload(c, xd, s->resv_xallocated, (size_t)n * KOORDHIP_NXRES);  // NULL: zeros
+        dv.rxa = xa;
+        dv.rxd = xd;
+        for (size_t a = 0; a < (size_t)n * KOORDHIP_NXRES && !c->resv_x; a++) c->resv_x = s->resv_xalloc[a] != 0;
+      }
     }
   }
+  if (!e && s->resv_xalloc && !dv.rxa)
+    return fail(KOORDHIP_EINVAL, "resv_xalloc needs DeviceShare and the device-holding reservation columns "
+                                 "(resv_dev_slot, resv_dev)");
   int64_t *xa = nullptr, *xr = nullptr;
   if (!e && s->xalloc) {
     e = dev_alloc(c, &xa, (size_t)n * KOORDHIP_NXRES);
@@ -1341,7 +1383,10 @@ int koordhip_load_snapshot(koordhip_ctx *c, const koordhip_node_soa *s, int32_t 
   // the sequential cycle (seq.hip: eval_total_resv<.., Z>)
   // (and more than KOORDHIP_RESV_SLOTS reservations per node: the pipelined
   // rows hold at most that many)
-  c->seq_snap = c->dc.resv && (c->dc.zones || c->dc.resv_slots > KOORDHIP_RESV_SLOTS);
+  // (and device-holding reservations listing extended scalars: their
+  // scoreReservation / FilterReservation / fitsNode terms live only in the
+  // sequential cycle's rules, resv.hpp ResvXS)
+  c->seq_snap = c->dc.resv && (c->dc.zones || c->dc.resv_slots > KOORDHIP_RESV_SLOTS || c->resv_x);
   c->seq = c->seq_profile || c->seq_snap;
   if (e) {
     free_cols(c);
@@ -1371,8 +1416,33 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
     if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
       return fail(KOORDHIP_EINVAL, "duplicate row index (a row would mix fields of two updates)");
   }
-  if (rows->resv_dev_slot || rows->resv_dev)
-    return fail(KOORDHIP_EINVAL, "update rows: device-holding reservations change with a snapshot load only");
+  // device-holding reservations (ABI 13 / 14): a row carrying the reservation
+  // columns replaces ALL of the node's reservation state, its device-holding
+  // reservation included -- rows without resv_dev_slot / resv_dev (and
+  // resv_xalloc) hold none, so the node's slot, device allocation and scalars
+  // are cleared (a different reservation moving into the slot cannot inherit
+  // them).  Rows without reservation columns leave all of it alone.
+  const bool rdev_rows = rows->resv_dev_slot || rows->resv_dev || rows->resv_xalloc || rows->resv_xallocated;
+  if (rdev_rows) {
+    if (!c->d.dv.rslot)
+      return fail(KOORDHIP_EINVAL, "update rows: device-holding reservations need the resv_dev columns at load_snapshot");
+    if (!rows->resv_flags) return fail(KOORDHIP_EINVAL, "update rows: resv_dev columns come with the reservation columns");
+    if (!rows->resv_dev_slot || !rows->resv_dev || (rows->resv_xallocated && !rows->resv_xalloc))
+      return fail(KOORDHIP_EINVAL, "update rows: resv_dev_slot and resv_dev together (resv_xallocated with resv_xalloc)");
+    if (rows->dev_slots != c->d.dv.slots || !rows->dev_minor)
+      return fail(KOORDHIP_EINVAL, "update rows: a device-holding reservation row needs the node's device columns");
+    if (std::max(1, rows->resv_slots) != c->d.rv.slots)
+      return fail(KOORDHIP_EINVAL, "update rows: resv_slots differs from the loaded snapshot's");
+    if (int e = check_resv_dev(rows, m)) return e;
+    if (rows->resv_xalloc) {
+      if (int e = check_resv_scalars(rows->resv_xalloc, rows->resv_xallocated, rows->resv_dev_slot, m)) return e;
+      bool anyx = false;
+      for (size_t a = 0; a < (size_t)m * KOORDHIP_NXRES && !anyx; a++) anyx = rows->resv_xalloc[a] != 0;
+      if (anyx && !c->d.dv.rxa)
+        return fail(KOORDHIP_EINVAL, "update rows: reservations listing extended scalars need the resv_xalloc column at "
+                                     "load_snapshot");
+    }
+  }
   const bool numa_rows = c->numa && rows->numa_class;
   if (numa_rows) {
     for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++)
@@ -1511,6 +1581,33 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
           cols.push_back({rv.rc[w] + q * dn, rc_rows[w] + q * sm, 8, false, "resv_cpus"});
     }
   }
+  // the device-holding reservation of every row with reservation columns (none: cleared)
+  std::vector<int32_t> no_rslot;
+  std::vector<int64_t> no_rdev, no_rx;
+  bool rows_x = false;
+  if (resv_rows && c->d.dv.rslot) {
+    kh::DevDev &dv = c->d.dv;
+    const int32_t rb = 2 * KOORDHIP_DEV_TYPES * dv.slots * KOORDHIP_DEV_RES;
+    if (!rdev_rows) {
+      no_rslot.assign((size_t)m, -1);
+      no_rdev.assign((size_t)m * rb, 0);
+    }
+    cols.push_back({const_cast<int32_t *>(dv.rslot), rdev_rows ? rows->resv_dev_slot : no_rslot.data(), 4, false,
+                    "resv_dev_slot"});
+    cols.push_back({dv.rdev, rdev_rows ? rows->resv_dev : no_rdev.data(), rb * 8, false, "resv_dev"});
+    if (dv.rxa) {
+      const bool given = rdev_rows && rows->resv_xalloc;
+      if (!given || !rows->resv_xallocated) no_rx.assign((size_t)m * KOORDHIP_NXRES, 0);
+      for (int j = 0; j < KOORDHIP_NXRES; j++) {
+        cols.push_back({const_cast<int64_t *>(dv.rxa) + (size_t)j * c->n,
+                        (given ? rows->resv_xalloc : no_rx.data()) + (size_t)j * m, 8, false, "resv_xalloc"});
+        cols.push_back({dv.rxd + (size_t)j * c->n,
+                        ((given && rows->resv_xallocated) ? rows->resv_xallocated : no_rx.data()) + (size_t)j * m, 8,
+                        false, "resv_xallocated"});
+      }
+      for (size_t a = 0; given && a < (size_t)m * KOORDHIP_NXRES && !rows_x; a++) rows_x = rows->resv_xalloc[a] != 0;
+    }
+  }
   // ABI 9: DeviceShare device rows, extended scalars, static Scores (the
   // sequential cycle's columns; element = a node's whole device row)
   if (c->seq_profile) {
@@ -1644,6 +1741,11 @@ int koordhip_update_nodes(koordhip_ctx *c, const int32_t *idx, const koordhip_no
   c->dc.la_alias = alias ? 1 : 0;
   if (zpolicy) c->dc.zones = 1;
   if (zpolicy && c->dc.resv) c->seq_snap = true;
+  if (rows_x && !c->resv_x) {  // reservations listing extended scalars from now on: the sequential cycle places
+    c->resv_x = true;
+    c->seq_snap = true;
+    c->seq = true;
+  }
   if (amp_any) c->dc.amp = 1;
   HIP_TRY(kh::launch_prep_flags(pi, d, d_idx, m, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));  // the host image may be reused by the next call
@@ -1760,6 +1862,20 @@ int koordhip_read_resv_devices(koordhip_ctx *c, int64_t *resv_dev) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(resv_dev, c->d.dv.rdev, nd * sizeof(int64_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int koordhip_read_resv_scalars(koordhip_ctx *c, int64_t *resv_xallocated) {
+  if (!c || !resv_xallocated) return fail(KOORDHIP_EINVAL, "NULL argument");
+  if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  const size_t nx = (size_t)c->n * KOORDHIP_NXRES;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (!c->d.dv.rxd) {
+    std::memset(resv_xallocated, 0, nx * sizeof(int64_t));
+    return 0;
+  }
+  HIP_TRY(hipMemcpy(resv_xallocated, c->d.dv.rxd, nx * sizeof(int64_t), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -3149,6 +3265,7 @@ static std::vector<std::pair<void *, size_t>> mutable_cols(koordhip_ctx *c) {
   if (c->d.dv.used)
     v.push_back({c->d.dv.used, n * KOORDHIP_DEV_TYPES * (size_t)c->d.dv.slots * KOORDHIP_DEV_RES * sizeof(int64_t)});
   if (c->d.dv.xreq) v.push_back({c->d.dv.xreq, n * KOORDHIP_NXRES * sizeof(int64_t)});
+  if (c->d.dv.rxd) v.push_back({c->d.dv.rxd, n * KOORDHIP_NXRES * sizeof(int64_t)});
   if (c->d.dv.rdev)
     v.push_back({c->d.dv.rdev, n * 2 * KOORDHIP_DEV_TYPES * (size_t)c->d.dv.slots * KOORDHIP_DEV_RES * sizeof(int64_t)});
   if (c->pts.cnt) v.push_back({c->pts.cnt, n * (size_t)std::max(1, c->pts.cons) * sizeof(int32_t)});
@@ -3191,9 +3308,21 @@ int koordhip_restore(koordhip_ctx *c) {
   return 0;
 }
 
+static int commit_ext_impl(koordhip_ctx *c, const koordhip_pod *pod, const koordhip_pod_ext *ext, int32_t node, int sign,
+                           uint64_t *cpus_io, uint32_t *dev_io);
+
 static int commit_impl(koordhip_ctx *c, const koordhip_pod *pod, int32_t node, int sign, uint64_t *cpus_io) {
   if (!c || !pod) return fail(KOORDHIP_EINVAL, "NULL argument");
   if (!c->loaded) return fail(KOORDHIP_ESTATE, "no snapshot loaded");
+  if (c->resv_x) {
+    // reservations listing extended scalars: the nomination's scoreReservation
+    // counts them (resv.hpp ResvXS) -- the sequential cycle's Reserve, with an
+    // empty koordhip_pod_ext record (no device request: gpu keys absent)
+    koordhip_pod_ext none;
+    std::memset(&none, 0, sizeof(none));
+    for (int r = 0; r < KOORDHIP_DEV_RES; r++) none.dev_req[KOORDHIP_DEV_GPU][r] = -1;
+    return commit_ext_impl(c, pod, &none, node, sign, cpus_io, nullptr);
+  }
   if (node < 0 || node >= c->n) return fail(KOORDHIP_EINVAL, "node index out of range");
   const bool cpuset = c->numa && (pod->flags & KOORDHIP_POD_CPUSET) &&
                       !(pod->flags & (KOORDHIP_POD_NUMA_SKIP | KOORDHIP_POD_NUMA_ERROR));

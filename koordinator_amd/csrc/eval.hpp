@@ -87,6 +87,11 @@ struct DevDev {
   // allocatable / allocated (the allocated half advanced by Reserve)
   const int32_t *rslot;
   int64_t *rdev;
+  // ABI 14: that reservation's extended scalars [NXRES][n], its Allocatable
+  // (the reserve pod's scalar requests) and Allocated (advanced by Reserve);
+  // NULL: none (the sequential cycle's Reservation rules read them, resv.hpp ResvXS)
+  const int64_t *rxa;
+  int64_t *rxd;
 };
 
 // Columnar node state in HBM.  Static columns are const; the mutable ones are
@@ -600,15 +605,16 @@ namespace kh {
 template <int S, bool RC = false, bool Z = false>
 __device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v, const NumaRowRS<S> &r,
                                                    const DevNumaClass *classes, const DevCfg &c,
-                                                   const DevNodes *zd = nullptr, int32_t zi = 0) {
+                                                   const DevNodes *zd = nullptr, int32_t zi = 0,
+                                                   ResvXS rx = no_rx()) {
   NV w = v;
   uint32_t mm;
-  const int nmatch = resv_restore(w, r, p, mm);
+  const int nmatch = resv_restore(w, r, p, mm, rx);
   int32_t t;
   if constexpr (Z) {
     static_assert(RC && S > 1, "the zone build is the several-slot reserved-CPU build");
     uint64_t P[NW];
-    resv_pref_cpus(r, p, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P);
+    resv_pref_cpus(r, p, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P, rx);
     NumaRow q = r;
     if (topo_policy(q.nflags) != 0) load_zones(q, *zd, zi);
     t = eval_total_numa<true>(p, w, q, classes, c, P);
@@ -616,7 +622,7 @@ __device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v,
     // the NodeNUMAResource Score reads the reserved CPUs of the reservation
     // PreScore nominated on the node (scoring.go:86-166, plugin.go:503-524)
     uint64_t P[NW];
-    resv_pref_cpus(r, p, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P);
+    resv_pref_cpus(r, p, (c.score & KOORDHIP_PLUGIN_RESERVATION) ? mm : 0u, P, rx);
     t = eval_total_numa<false>(p, w, r, classes, c, P);
   } else {
     t = eval_total_numa<false>(p, w, r, classes, c);
@@ -624,12 +630,12 @@ __device__ __forceinline__ int32_t eval_total_resv(const DevPod &p, const NV &v,
   if (t < 0) return t;
   if (nmatch == 0)  // a required reservation affinity needs a matched reservation on the node (plugin.go:378-381)
     return ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && (p.flags & KOORDHIP_POD_RESV_AFFINITY)) ? -1 : t;
-  if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !resv_filter(p, w, r, mm, nmatch)) return -1;
+  if ((c.filt & KOORDHIP_PLUGIN_RESERVATION) && !resv_filter(p, w, r, mm, nmatch, rx)) return -1;
   if (c.score & KOORDHIP_PLUGIN_RESERVATION) {
     const int rk = resv_node_rank(r, mm);
     if (rk >= 0) return 101 * c.resv_b1 + (KOORDHIP_RESV_MAX_ORDERS - 1 - rk);
-    const int q = resv_nominate(p, r, mm);
-    if (q >= 0) t += resv_score(p, r.rs[q]) * c.resv_b1;
+    const int q = resv_nominate(p, r, mm, rx);
+    if (q >= 0) t += resv_score(p, r.rs[q], q == rx.h, rx) * c.resv_b1;
   }
   return t;
 }

@@ -160,6 +160,33 @@ __device__ __forceinline__ double rem_of(const ResvSlot &r, int k) {
   return rkey(r.rf, k) && x > 0.0 ? x : 0.0;  // SubtractWithNonNegativeResult(Allocatable, Allocated)
 }
 
+// ABI 14 (the sequential cycle): the node's reservation holding devices
+// (slot h) may list NodeResourcesFit extended scalars in its Allocatable.  They
+// are more keys of that reservation's ResourceLists, so every rule below sees
+// them -- as the facts one out-of-line pass over the scalars (seq.hip
+// resv_scalars) derives for the (pod, node):
+//   RX_REM    SubtractWithNonNegativeResult(Allocatable, Allocated) has a
+//             non-zero scalar (an unmatched reservation's remainder pod comes
+//             back even when its cpu / memory remainder is zero, transformer.go:262-276)
+//   RX_FIT_H  fitsNode's scalar part with rInfo = h (rRemained = h's remainder)
+//   RX_FIT_O  ... with any other matched rInfo (rRemained 0); both with
+//             podRequested = the scalars after the unmatched restore and
+//             allRAllocated = h's Allocated when h is matched (plugin.go:445-494)
+//   RX_LE     Restricted's LessThanOrEqual(podRequests, rRemained) over the scalars (:420-432)
+//   RX_INTER  FilterReservation's intersection holds a scalar; RX_NZ: one with a remainder (:504-535)
+//   RX_XFIT   NodeResourcesFit over the pod's scalars on the restored Requested
+//   xs / xw   scoreReservation's scalar terms: the sum of 100 (request + Allocated) /
+//             Allocatable over RemoveZeros(Allocatable)'s scalars and their count (scoring.go:177-200)
+// h = -1: no such reservation (every hook is a no-op: the pipelined builds
+// never see one -- such snapshots run in the sequential cycle).
+enum : uint32_t { RX_REM = 1u, RX_FIT_H = 2u, RX_FIT_O = 4u, RX_LE = 8u, RX_INTER = 16u, RX_NZ = 32u, RX_XFIT = 64u };
+struct ResvXS {
+  int32_t h;
+  uint32_t f;
+  int32_t xs, xw;
+};
+__device__ __forceinline__ ResvXS no_rx() { return ResvXS{-1, 0u, 0, 0}; }
+
 // transformer.go:86-103: 1 = matched, 2 = unmatched with assigned pods, 0 = untouched
 __device__ __forceinline__ int resv_class(const ResvSlot &r, const DevPod &p) {
   if (!(r.rf & KOORDHIP_RESV_PRESENT)) return 0;
@@ -174,7 +201,8 @@ __device__ __forceinline__ int resv_class(const ResvSlot &r, const DevPod &p) {
 // depend on the order), then the Fit over-commit bits of the result.  Returns
 // the matched count; mm: the matched slots.
 template <int S>
-__device__ __forceinline__ int resv_restore(NV &v, const NumaRowRS<S> &r, const DevPod &p, uint32_t &mm) {
+__device__ __forceinline__ int resv_restore(NV &v, const NumaRowRS<S> &r, const DevPod &p, uint32_t &mm,
+                                            ResvXS rx = no_rx()) {
   int nmatch = 0;
   bool touched = false;
   mm = 0;
@@ -194,7 +222,7 @@ __device__ __forceinline__ int resv_restore(NV &v, const NumaRowRS<S> &r, const 
       mm |= 1u << q;
     } else {
       const double rc = rem_of(x, 0), rm = rem_of(x, 1);
-      if (rc > 0.0 || rm > 0.0) {  // a pod requesting the remainder comes back
+      if (rc > 0.0 || rm > 0.0 || (q == rx.h && (rx.f & RX_REM))) {  // a pod requesting the remainder comes back
         v.r[KOORDHIP_RES_CPU] += rc;
         v.r[KOORDHIP_RES_MEM] += rm;
         v.nz_cpu += rkey(x.rf, 0) ? rc : RESV_NZ_CPU;
@@ -219,7 +247,7 @@ __device__ __forceinline__ int resv_restore(NV &v, const NumaRowRS<S> &r, const 
 // (Default ones are insufficient only with preemptible resources).
 template <int S>
 __device__ __forceinline__ bool resv_filter(const DevPod &p, const NV &v, const NumaRowRS<S> &r, uint32_t mm,
-                                            int nmatch) {
+                                            int nmatch, ResvXS rx = no_rx()) {
   double podreq[2] = {v.r[KOORDHIP_RES_CPU], v.r[KOORDHIP_RES_MEM]}, rall[2] = {0.0, 0.0};
 #pragma unroll
   for (int q = 0; q < S; q++)
@@ -247,11 +275,12 @@ __device__ __forceinline__ bool resv_filter(const DevPod &p, const NV &v, const 
         fits &= !(p.req[KOORDHIP_RES_BCPU] > v.a[KOORDHIP_RES_BCPU] - v.r[KOORDHIP_RES_BCPU]);
       if (p.flags & KOORDHIP_POD_REQ_BMEM)
         fits &= !(p.req[KOORDHIP_RES_BMEM] > v.a[KOORDHIP_RES_BMEM] - v.r[KOORDHIP_RES_BMEM]);
+      if (rx.h >= 0) fits &= (rx.f & (q == rx.h ? RX_FIT_H : RX_FIT_O)) != 0u;  // the extended scalars
     }
     if (pol == 1) {  // Aligned
       pass |= fits;
     } else {  // Restricted: LessThanOrEqual(podRequests, rRemained)
-      bool le = true;
+      bool le = !(q == rx.h && !(rx.f & RX_LE));
 #pragma unroll
       for (int k = 0; k < 2; k++) le &= !(rkey(x.rf, k) && pkey(p, k) && p.req[k] > rem_of(x, k));
       pass |= le && fits;
@@ -261,8 +290,8 @@ __device__ __forceinline__ bool resv_filter(const DevPod &p, const NV &v, const 
 }
 
 // FilterReservation of a matched reservation: a nomination candidate
-__device__ __forceinline__ bool resv_candidate(const DevPod &p, const ResvSlot &r) {
-  bool inter = false, nonzero = false;
+__device__ __forceinline__ bool resv_candidate(const DevPod &p, const ResvSlot &r, bool xh = false, uint32_t xf = 0u) {
+  bool inter = xh && (xf & RX_INTER), nonzero = xh && (xf & RX_NZ);
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const bool both = rkey(r.rf, k) && pkey(p, k);
@@ -273,7 +302,7 @@ __device__ __forceinline__ bool resv_candidate(const DevPod &p, const ResvSlot &
 }
 
 // scoreReservation: MostAllocated (weights 1) over the non-zero Allocatable
-__device__ __forceinline__ int32_t resv_score(const DevPod &p, const ResvSlot &r) {
+__device__ __forceinline__ int32_t resv_score(const DevPod &p, const ResvSlot &r, bool xh = false, ResvXS rx = no_rx()) {
   int32_t s = 0, w = 0;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -283,6 +312,7 @@ __device__ __forceinline__ int32_t resv_score(const DevPod &p, const ResvSlot &r
     w += on ? 1 : 0;
     s += (on && req <= cap) ? mrs(req, cap) : 0;  // 100 * req / cap, req <= cap
   }
+  if (xh && rx.xw > 0) return (s + rx.xs) / (w + rx.xw);  // (the extended scalars of RemoveZeros(Allocatable))
   return w == 2 ? (s >> 1) : s;
 }
 
@@ -293,14 +323,14 @@ __device__ __forceinline__ int32_t resv_score(const DevPod &p, const ResvSlot &r
 // reservation holding devices can (ResvSlot::rdev, set by the caller); a
 // reservation holding none has no restore entry and fails it (:337-346).
 template <int S>
-__device__ __forceinline__ int resv_nominate(const DevPod &p, const NumaRowRS<S> &r, uint32_t mm) {
+__device__ __forceinline__ int resv_nominate(const DevPod &p, const NumaRowRS<S> &r, uint32_t mm, ResvXS rx = no_rx()) {
   const bool devshare = (p.flags & KH_POD_DEVSHARE) != 0;
   int best = -1, brk = 0;
   bool ord = false;
   int32_t bsc = -1;
 #pragma unroll
   for (int q = 0; q < S; q++) {
-    if (!((mm >> q) & 1u) || !resv_candidate(p, r.rs[q])) continue;
+    if (!((mm >> q) & 1u) || !resv_candidate(p, r.rs[q], q == rx.h, rx.f)) continue;
     if (devshare && !r.rs[q].rdev) continue;
     const ResvSlot &x = r.rs[q];
     if (x.rf & KOORDHIP_RESV_ORDERED) {
@@ -310,7 +340,7 @@ __device__ __forceinline__ int resv_nominate(const DevPod &p, const NumaRowRS<S>
         ord = true;
       }
     } else if (!ord) {
-      const int32_t sc = resv_score(p, x);
+      const int32_t sc = resv_score(p, x, q == rx.h, rx);
       if (sc > bsc) {
         best = q;
         bsc = sc;
@@ -344,9 +374,9 @@ __device__ __forceinline__ int resv_node_rank(const NumaRowRS<S> &r, uint32_t mm
 // reserved CPUs (the next cycle's RestoreReservation subtracts the assigned
 // pods' cpusets, reservation.go:90-97).
 template <int S>
-__device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p, const uint64_t *cpus) {
-  const int q = resv_nominate(p, r, resv_matched(r, p));
-  if (q < 0) return;
+__device__ __forceinline__ int resv_assume(NumaRowRS<S> &r, const DevPod &p, const uint64_t *cpus, ResvXS rx = no_rx()) {
+  const int q = resv_nominate(p, r, resv_matched(r, p), rx);
+  if (q < 0) return q;
   ResvSlot &x = r.rs[q];
 #pragma unroll
   for (int k = 0; k < 2; k++)
@@ -358,6 +388,7 @@ __device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p, co
   } else {
     (void)cpus;
   }
+  return q;
 }
 
 // The reservation-preferred CPUs of a pod on the node (getReservationReservedCPUs,
@@ -365,12 +396,13 @@ __device__ __forceinline__ void resv_assume(NumaRowRS<S> &r, const DevPod &p, co
 // reservation, for a pod AllowUseCPUSet lets restore them (PreRestoreReservation
 // :68-74; only cpuset pods -- requestCPUBind -- read them).  Zero: none.
 template <int S>
-__device__ __forceinline__ void resv_pref_cpus(const NumaRowRS<S> &r, const DevPod &p, uint32_t mm, uint64_t *P) {
+__device__ __forceinline__ void resv_pref_cpus(const NumaRowRS<S> &r, const DevPod &p, uint32_t mm, uint64_t *P,
+                                               ResvXS rx = no_rx()) {
 #pragma unroll
   for (int w = 0; w < NW; w++) P[w] = 0ull;
   if constexpr (S > 1) {
     if (!(p.flags & KOORDHIP_POD_CPUSET) || (p.flags & KOORDHIP_POD_NUMA_SKIP) || mm == 0u) return;
-    const int q = resv_nominate(p, r, mm);
+    const int q = resv_nominate(p, r, mm, rx);
     if (q < 0) return;
 #pragma unroll
     for (int w = 0; w < NW; w++) P[w] = rcm_of(r, q)[w];
@@ -378,6 +410,7 @@ __device__ __forceinline__ void resv_pref_cpus(const NumaRowRS<S> &r, const DevP
     (void)r;
     (void)p;
     (void)mm;
+    (void)rx;
   }
 }
 

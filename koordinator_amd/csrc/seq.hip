@@ -127,6 +127,58 @@ __device__ __forceinline__ DevRC seq_dev_resv(const DevCfg &c, const DevDev &dv,
   return rc;
 }
 
+// ABI 14: resv.hpp's ResvXS for pod (p, x) on node i, whose reservation
+// holding devices is slot h with restore class `cls` (1 matched, 2 unmatched
+// with assigned pods, 0 neither), from its extended scalars (Allocatable A,
+// Allocated D, remainder max0(A - D); a listed key has A > 0) and the node's
+// scalar Allocatable / Requested.  Rare (a node whose reservation lists
+// extended scalars), so out of line: the common path keeps its registers.
+__device__ __noinline__ ResvXS resv_scalars(const DevDev &dv, const DevPodX &x, int32_t i, int32_t n, int32_t h,
+                                            int cls) {
+  ResvXS rx{h, RX_FIT_H | RX_FIT_O | RX_LE | RX_XFIT, 0, 0};
+  for (int j = 0; j < KOORDHIP_NXRES; j++) {
+    const size_t at = (size_t)j * n + i;
+    const int64_t A = dv.rxa[at], D = dv.rxd[at];
+    const int64_t rem = A - D > 0 ? A - D : 0;
+    const bool key = (x.xmask >> j) & 1u;
+    const int64_t px = key ? x.xreq[j] : 0;
+    if (rem > 0) rx.f |= RX_REM;
+    if (A != 0) {  // RemoveZeros(Allocatable) / ResourceNames
+      rx.xw++;
+      const int64_t req = px + D;  // scoreReservation: PodRequestsAndLimits + Allocated
+      if (req <= A) rx.xs += (int32_t)(100 * req / A);
+      if (key) {
+        rx.f |= RX_INTER | (rem > 0 ? RX_NZ : 0u);
+        if (px > rem) rx.f &= ~RX_LE;
+      }
+    }
+    if (!key) continue;
+    const int64_t alloc = dv.xalloc ? dv.xalloc[at] : 0, xr = dv.xreq[at];
+    // NodeResourcesFit on the restored NodeInfo: the reserve pod leaves, an
+    // unmatched reservation's remainder comes back (transformer.go:227-293)
+    if (px > alloc - (xr - (cls != 0 ? A : 0) + (cls == 2 ? rem : 0))) rx.f &= ~RX_XFIT;
+    // fitsNode: podRequested after the unmatched restore, allRAllocated = D when matched
+    const int64_t preq = xr + (cls == 2 ? rem - A : 0), rall = cls == 1 ? D : 0;
+    if (px > alloc - (preq - rem - rall)) rx.f &= ~RX_FIT_H;
+    if (px > alloc - (preq - rall)) rx.f &= ~RX_FIT_O;
+  }
+  return rx;
+}
+
+// the ResvXS of node i's reservation holding devices for the pod (h -1: none)
+template <int S>
+__device__ __forceinline__ ResvXS seq_resv_x(const DevNodes &d, const DevPod &p, const DevPodX &x,
+                                             const NumaRowRS<S> &r, int32_t i) {
+  if (!d.dv.rxa) return no_rx();
+  const int32_t h = d.dv.rslot[i];
+  if (h < 0 || h >= S) return no_rx();
+  int cls = 0;
+#pragma unroll
+  for (int q = 0; q < S; q++)
+    if (q == h) cls = resv_class(r.rs[q], p);
+  return resv_scalars(d.dv, x, i, d.n, h, cls);
+}
+
 // One node for one pod: the total of the per-node plugins (-1: some Filter
 // fails; with the Reservation plugin the ranking total of resv.hpp) and the
 // raw normalized scores.  Every column is read (the parity evaluator's rows,
@@ -147,7 +199,7 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   // overlap the row's: the extended scalars, the static Scores and (without
   // the Reservation build, whose nomination needs the reservation rows) the
   // device rows
-  const bool xf = EARLY || !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x, i, d.n);
+  bool xfr = EARLY || !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x, i, d.n);
   raw[1] = (c.score & KOORDHIP_PLUGIN_AFFINITY_SCORE) ? static_raw(d.dv, 0, p.sclass, i, d.n) : 0;
   raw[2] = (c.score & KOORDHIP_PLUGIN_TAINT_SCORE) ? static_raw(d.dv, 1, p.sclass, i, d.n) : 0;
   int32_t t;
@@ -158,10 +210,12 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
     load_numa<false>(nr, d, i, all);  // (the zone row shares the reserved CPUs' bytes: eval_total_resv<.., Z> reads it)
     load_resv(nr, d.rv, i);
     const DevRC rc = seq_dev_resv(c, d.dv, p, x, nr, i);
-    t = c.zones       ? eval_total_resv<S, true, true>(p, v, nr, d.nu.cls, c, &d, i)
-        : c.resv_cpus ? eval_total_resv<S, true>(p, v, nr, d.nu.cls, c)
-                      : eval_total_resv<S, false>(p, v, nr, d.nu.cls, c);
-    const int32_t nq = (rs && (x.flags & KOORDHIP_PODX_DEVICE)) ? resv_nominate(p, nr, resv_matched(nr, p)) : -1;
+    const ResvXS rx = seq_resv_x(d, p, x, nr, i);
+    if (rx.h >= 0 && (c.filt & KOORDHIP_PLUGIN_FIT)) xfr = (rx.f & RX_XFIT) != 0u;  // on the restored scalars
+    t = c.zones       ? eval_total_resv<S, true, true>(p, v, nr, d.nu.cls, c, &d, i, rx)
+        : c.resv_cpus ? eval_total_resv<S, true>(p, v, nr, d.nu.cls, c, nullptr, 0, rx)
+                      : eval_total_resv<S, false>(p, v, nr, d.nu.cls, c, nullptr, 0, rx);
+    const int32_t nq = (rs && (x.flags & KOORDHIP_PODX_DEVICE)) ? resv_nominate(p, nr, resv_matched(nr, p), rx) : -1;
     if (rc.h >= 0)
       df = rc_eval(c, d.dv, x, i, rc, nq, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
                    (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
@@ -182,6 +236,7 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
       t = eval_total(p, v, c);
     }
   }
+  const bool xf = xfr;
   if (status)
     *status = (xf ? 0 : KOORDHIP_ST_XFIT_FAIL) | (df ? 0 : KOORDHIP_ST_DEVICE_FAIL) | (rfail ? KOORDHIP_ST_RESV_FAIL : 0);
   if (!xf || !df || rfail) t = -1;
@@ -262,10 +317,12 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   RV rv;
   uint32_t mm = 0u;
   DevRC rc{-1, 0, 0, 0u};
+  ResvXS rx = no_rx();
   if constexpr (SM >= 2) {
     load_resv(rv, d.rv, w);
     mm = resv_matched(rv, p);
     rc = seq_dev_resv(c, d.dv, p, x, rv, w);
+    rx = seq_resv_x(d, p, x, rv, w);
   }
   const bool prescore = rs && nf > 1;
   // the reservation PreScore nominated (DeviceShare Reserve reads it) and the
@@ -273,7 +330,7 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   // before any Reserve
   int32_t nq = -1, qa = -1;
   if constexpr (SM >= 2) {
-    qa = resv_nominate(p, rv, mm);
+    qa = resv_nominate(p, rv, mm, rx);
     nq = prescore ? qa : -1;
   }
   uint32_t slots[DT] = {0u, 0u, 0u};
@@ -295,7 +352,7 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
       NumaRow r;
       load_numa_row(r, d, w);
       uint64_t pref[NW] = {0, 0, 0, 0};
-      if constexpr (SM >= 2) resv_pref_cpus(rv, p, prescore ? mm : 0u, pref);
+      if constexpr (SM >= 2) resv_pref_cpus(rv, p, prescore ? mm : 0u, pref, rx);
       if (!numa_reserve<true>(d.nu.cls, r, p, m, pref)) return KOORDHIP_RESERVE_FAILED;
       store_numa_row(r, d, w);
     }
@@ -305,8 +362,13 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
     if (rc.h >= 0 && qa == rc.h) rc_apply_allocated<!ROW>(d.dv, w, slots, per);
   }
   if constexpr (SM >= 2) {  // Reservation Reserve: assumePod into the nominated reservation
-    resv_assume(rv, p, m);
+    const int qz = resv_assume(rv, p, m, rx);
     store_resv(rv, d.rv, w);
+    if (qz >= 0 && qz == rx.h && x.xmask)  // ... its extended scalars' Allocated (masked to its keys)
+      for (int j = 0; j < KOORDHIP_NXRES; j++) {
+        const size_t at = (size_t)j * d.n + w;
+        if (((x.xmask >> j) & 1u) && d.dv.rxa[at] != 0) d.dv.rxd[at] += x.xreq[j];
+      }
   }
   if constexpr (ROW) {
     apply_delta(v, p, +1);

@@ -130,6 +130,13 @@ class PlacementEngine:
         abi.check(self.lib, self.lib.koordhip_read_resv_devices(self._ctx, abi.ptr(out, C.c_int64)))
         return out
 
+    def read_resv_scalars(self) -> np.ndarray:
+        """The device-holding reservations' extended-scalar Allocated [n][NXRES]
+        (advanced by Reserve; zeros without the resv_xalloc column)."""
+        out = np.zeros((abi.NXRES, self.n), np.int64)
+        abi.check(self.lib, self.lib.koordhip_read_resv_scalars(self._ctx, abi.ptr(out, C.c_int64)))
+        return out.T.copy()
+
     def read_pts(self) -> np.ndarray:
         """PodTopologySpread matching pods per node and table constraint [n][cons]."""
         m = self._table.pts if self._table is not None else None

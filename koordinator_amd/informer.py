@@ -128,6 +128,23 @@ class Informer:
         self.resv_index = rv.ReservationIndex()
         self._resv_rank: Dict[int, int] = {}
         self._resv_cpus_loaded = False                      # the snapshot carried resv_cpus columns
+        # NodeInfo's reserve pods of the Available reservations (the scheduler
+        # cache holds them, frameworkext/eventhandlers/reservation_handler.go:
+        # 250-281): reservation name -> the pod in cluster.node_pods
+        self._resv_pods: Dict[str, k8s.Pod] = {}
+        # AssignedPods from the pods' reservation-allocated annotation
+        # (reservation/pod_eventhandler.go:95-131): reservation uid or name -> pod uid -> pod
+        self._assigned: Dict[str, Dict[str, k8s.Pod]] = {}
+        self._assigned_of: Dict[str, str] = {}              # pod uid -> the key it is assigned under
+        # operating-mode pods: the reservation cache keeps their ReservationInfo
+        # across updates (cache.go:139-161: UpdatePod refreshes the Allocatable
+        # only; AddAssignedPod is cumulative): pod uid -> (owners, parse error,
+        # the current owners seen: key -> (namespace, name, uid))
+        self._op_state: Dict[str, tuple] = {}
+        # bound operating-mode pods the engine cannot hold as a reservation slot
+        # (unsupported resources, more than RESV_SLOTS_MAX on a node): they stay
+        # plain NodeInfo pods; pod key -> reason
+        self.outside_envelope: Dict[str, str] = {}
         from .nodefilters import StaticClasses
         from .topologyspread import SpreadRegistry
         self.static_classes = StaticClasses()
@@ -148,11 +165,13 @@ class Informer:
             t.numa_classes = self._classes.records()
         elif self._table is not None:
             _keep_numa(t, self._table)
-        self._resv_rank = rv.order_ranks(rv.available_by_node(self._index, list(self.reservations.values())).values())
+        live = self._live_reservations()
+        self._resv_rank = rv.order_ranks(rv.available_by_node(self._index, live, []).values())
         # owner groups from the live reservations only (the registered affinities stay)
         self.resv_index = rv.ReservationIndex(affinities=list(self.resv_index.affinities))
-        rv.reservation_columns(t, self._index, list(self.reservations.values()), self.resv_index,
-                               self._node_labels())
+        over: list = []
+        rv.reservation_columns(t, self._index, live, self.resv_index, self._node_labels(), over)
+        self._note_overflow(over)
         self._resv_cpus_loaded = _has_resv_cpus(t)
         self._table = t
         self._dirty.clear()
@@ -226,6 +245,7 @@ class Informer:
         if pod.node_name:
             self._dirty.add(pod.node_name)
         self._touch_metric_refs(pod)
+        self._track_assigned(pod, True)
         self._operating_pod(None, pod)
 
     def on_pod_update(self, old: Optional[k8s.Pod], pod: k8s.Pod, now: float):
@@ -245,6 +265,7 @@ class Informer:
         if pod.node_name:
             self._dirty.add(pod.node_name)
         self._touch_metric_refs(pod)
+        self._track_assigned(pod, True)
         self._operating_pod(prev, pod)
 
     def on_pod_delete(self, pod: k8s.Pod):
@@ -256,21 +277,137 @@ class Informer:
         if prev.node_name:
             self._dirty.add(prev.node_name)
         self._touch_metric_refs(prev)
+        self._track_assigned(prev, False)
         self._operating_pod(prev, None)
+
+    def _track_assigned(self, pod: k8s.Pod, present: bool):
+        """The reservation cache's AssignedPods (reservation/pod_eventhandler.go:
+        95-131, cache.go:201-232): a bound, non-terminated pod whose
+        reservation-allocated annotation names a reservation is one of its
+        assigned pods; terminated or deleted, it leaves."""
+        old = self._assigned_of.pop(pod.uid, None)
+        if old is not None:
+            m = self._assigned.get(old, {})
+            m.pop(pod.uid, None)
+            if not m:
+                self._assigned.pop(old, None)
+            self._dirty_reservation(old)
+        ra = rv.reservation_allocated(pod) if present else None
+        if ra is None or not pod.node_name or k8s.is_terminated(pod):
+            return
+        key = ra[0] or ra[1]
+        if not key:
+            return
+        self._assigned.setdefault(key, {})[pod.uid] = pod
+        self._assigned_of[pod.uid] = key
+        self._dirty_reservation(key)
+
+    def _dirty_reservation(self, key: str):
+        for r in self.reservations.values():
+            if key in (r.uid, r.name) and r.node_name:
+                self._dirty.add(r.node_name)
+
+    def _devices_on(self) -> bool:
+        from .config import PLUGIN_DEVICESHARE
+        return PLUGIN_DEVICESHARE in self.profile.filters or PLUGIN_DEVICESHARE in self.profile.scores
 
     def _operating_pod(self, prev: Optional[k8s.Pod], pod: Optional[k8s.Pod]):
         """A bound pod in the reservation operating mode is also an Available
         reservation on its node (the reservation cache, pod_eventhandler.go:104-124,
         cache.go:139-168): reservation_columns gives it a slot like a
-        Reservation's (rv.operating_pod_reservation)."""
-        r = rv.operating_pod_reservation(pod) if pod is not None else None
+        Reservation's (rv.operating_pod_reservation).  Its ReservationInfo
+        outlives updates (cache.go:139-161): the owners parsed when it was first
+        added stay, its current owners accumulate as assigned pods; a terminated
+        or deleted pod removes it (pod_eventhandler.go:91-93, 136-141).  One the
+        engine cannot hold (resources outside the envelope) stays a plain pod,
+        counted in `outside_envelope`."""
+        gone = pod is None or k8s.is_terminated(pod)
+        r = rv.operating_pod_reservation(pod) if not gone else None
         if prev is not None and rv.is_reservation_operating_pod(prev):
             old = rv.operating_reservation_name(prev)
             if r is None or r.name != old:
                 if old in self.reservations:
                     self.on_reservation_delete(old)
-        if r is not None:
-            self.on_reservation(r)
+        if r is None:
+            if prev is not None:
+                self._op_state.pop(prev.uid, None)
+                self.outside_envelope.pop(prev.key, None)
+            if pod is not None:
+                self._op_state.pop(pod.uid, None)
+            return
+        st = self._op_state.get(pod.uid)
+        if st is None:
+            st = (r.owners, r.parse_error, {})
+            self._op_state[pod.uid] = st
+        owners, perr, seen = st
+        cur = rv.current_owner(pod)
+        if cur is not None:
+            seen.setdefault(cur[2] or f"{cur[0]}/{cur[1]}", cur)   # AddAssignedPod (a repeated UID is skipped)
+        r.owners, r.parse_error, r.assigned = owners, perr, len(seen)
+        why = rv.reservation_unsupported(r, self._devices_on())
+        if why is not None:
+            self.outside_envelope[pod.key] = why
+            if r.name in self.reservations:
+                self.on_reservation_delete(r.name)
+            return
+        self.outside_envelope.pop(pod.key, None)
+        self.on_reservation(r)
+
+    def _note_overflow(self, over: list):
+        for r in over:
+            if r.pod is not None:
+                self.outside_envelope[r.pod.key] = f"more than {abi.RESV_SLOTS_MAX} reservations on node {r.node_name}"
+
+    def _pod_named(self, namespace: str, name: str) -> Optional[k8s.Pod]:
+        return self.cluster.pods.get(f"{namespace or 'default'}/{name}") or self.cluster.pods.get(f"{namespace}/{name}")
+
+    def _live_reservations(self) -> List[rv.Reservation]:
+        """The reservations as the reservation cache holds them now: a
+        Reservation with pods assigned through their reservation-allocated
+        annotation takes its assigned count, Allocated (their requests masked to
+        its ResourceNames, reservation_info.go:297-306), their cpusets and device
+        allocations from those pods; an operating-mode pod's current owners
+        supply their cpusets and device allocations (nd.getUsed / the
+        NodeAllocation of the owner, when it is a pod of the cluster).  Otherwise
+        the Reservation's own fields stand."""
+        import dataclasses
+        from . import deviceshare as ds
+        out = []
+        for r in self.reservations.values():
+            pods = []
+            if r.pod is not None:
+                st = self._op_state.get(r.pod.uid)
+                for (ns, nmn, _uid) in (st[2].values() if st else ()):
+                    q = self._pod_named(ns, nmn)
+                    if q is not None and q.node_name == r.node_name:
+                        pods.append(q)
+                cpus = (nm.pod_allocation(r.pod.annotations or {}) or ([], "", []))[0]
+                r = dataclasses.replace(r, cpus=list(cpus))
+            else:
+                pods = list(self._assigned.get(r.uid, {}).values()) + \
+                    ([] if r.uid else list(self._assigned.get(r.name, {}).values()))
+                if not pods:
+                    out.append(r)
+                    continue
+                names = set(r.allocatable)
+                alloc: k8s.ResourceList = {}
+                for q in pods:
+                    reqs, _ = k8s.pod_requests_and_limits(q)
+                    for n, v in reqs.items():
+                        if n in names:
+                            alloc[n] = alloc[n] + v if n in alloc else v
+                r = dataclasses.replace(r, assigned=len(pods), allocated=alloc)
+            acpus, adev = [], []
+            for q in pods:
+                a = nm.pod_allocation(q.annotations or {})
+                if a is not None:
+                    acpus.extend(a[0])
+                d = ds.parse_device_allocated(q.annotations or {})
+                if d:
+                    adev.append(d)
+            out.append(dataclasses.replace(r, assigned_cpus=sorted(set(acpus)) or list(r.assigned_cpus),
+                                           assigned_devices=adev or list(r.assigned_devices)))
+        return out
 
     # ---- NodeMetric events -------------------------------------------------------------
     def on_node_metric(self, nm: k8s.NodeMetric):
@@ -357,6 +494,23 @@ class Informer:
             alloc.release(uid)
         self._dirty.add(r.node_name)
 
+    def _nodeinfo_reserve_pod(self, r: rv.Reservation, present: bool):
+        """An Available Reservation's reserve pod is a pod of its node's NodeInfo
+        (addReservationToSchedulerCache, frameworkext/eventhandlers/
+        reservation_handler.go:250-281; NewReservePod carries its labels and
+        annotations) and of the nodeDevice cache (ReservationToPodEventHandler,
+        deviceshare/pod_handler.go:43-45).  An operating-mode pod is its own."""
+        old = self._resv_pods.pop(r.name, None)
+        if old is not None:
+            self.cluster.node_pods[old.node_name] = [p for p in self.cluster.node_pods.get(old.node_name, [])
+                                                     if p is not old]
+            self._dirty.add(old.node_name)
+        if present and r.pod is None and r.is_available():
+            p = r.reserve_pod()
+            self._resv_pods[r.name] = p
+            self.cluster.node_pods.setdefault(r.node_name, []).append(p)
+            self._dirty.add(r.node_name)
+
     def on_reservation(self, r: rv.Reservation):
         """Add or update."""
         old = self.reservations.get(r.name)
@@ -364,6 +518,7 @@ class Informer:
             self._numa_reservation(old, False)
         self.reservations[r.name] = r
         self._numa_reservation(r, True)
+        self._nodeinfo_reserve_pod(r, True)
         for nn in ({old.node_name} if old is not None else set()) | {r.node_name}:
             if nn:
                 self._dirty.add(nn)
@@ -375,6 +530,7 @@ class Informer:
         old = self.reservations.pop(name, None)
         if old is not None:
             self._numa_reservation(old, False)
+            self._nodeinfo_reserve_pod(old, False)
         if old is not None and old.node_name:
             self._dirty.add(old.node_name)
 
@@ -460,7 +616,9 @@ class Informer:
         self._sync_assigned()
         idx = np.array(sorted(self._index[n] for n in dirty), np.int32)
         rows = self._table.rows(idx)
-        placed = rv.available_by_node(self._index, list(self.reservations.values()))
+        over: list = []
+        placed = rv.available_by_node(self._index, self._live_reservations(), over)
+        self._note_overflow(over)
         if self.nrts or self._classes is not None:
             try:
                 for j, i in enumerate(idx):

@@ -735,6 +735,8 @@ def build_table(cluster: ClusterState, profile: Profile, now: float, static_clas
     if sequential_profile(profile):
         from .config import PLUGIN_DEVICESHARE, PLUGIN_PTS
         t.enable_ext(device_slots_of(cluster) if PLUGIN_DEVICESHARE in profile.filters else 0)
+        if PLUGIN_DEVICESHARE in profile.filters and _uses(profile, PLUGIN_RESERVATION):
+            t.enable_resv_dev()     # reservations holding devices (reservation.device_reservation_row)
         from .config import PLUGIN_IPA
         reg = cluster.spread
         ipa = cluster.ipa if _uses(profile, PLUGIN_IPA) else None

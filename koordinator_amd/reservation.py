@@ -297,6 +297,13 @@ class Reservation:
     # parse (ReservationInfo.ParseError: it matches no pod)
     pod: Optional[k8s.Pod] = None
     parse_error: bool = False
+    # metadata.annotations: NewReservePod copies them onto the reserve pod
+    # (util/reservation/reservation.go:75-80), so the device-allocated one is the
+    # reserve pod's DeviceShare allocation (deviceshare/reservation.go:139-141)
+    annotations: Dict[str, str] = field(default_factory=dict)
+    # each AssignedPod's device allocation on the node (its device-allocated
+    # annotation: nd.getUsed of the assigned pod, reservation.go:145-151)
+    assigned_devices: List[dict] = field(default_factory=list)
 
     def reserved_cpus(self) -> List[int]:
         """RestoreReservation's reservedCPUs of this reservation: its allocated
@@ -310,8 +317,15 @@ class Reservation:
     def reserve_pod(self) -> k8s.Pod:
         if self.pod is not None:
             return self.pod
-        return k8s.Pod(name=f"reserve-{self.name}", containers=list(self.template) or
-                       [k8s.Container(requests=dict(self.allocatable))])
+        return k8s.Pod(name=f"reserve-{self.name}", uid=self.uid, annotations=dict(self.annotations or {}),
+                       labels=dict(self.labels or {}), node_name=self.node_name,
+                       containers=list(self.template) or [k8s.Container(requests=dict(self.allocatable))])
+
+    def device_allocation(self) -> dict:
+        """The reserve pod's DeviceShare allocation {type: [(minor, {resource: value})]}
+        (its device-allocated annotation; an operating-mode pod's own)."""
+        from .deviceshare import parse_device_allocated
+        return parse_device_allocated(self.pod.annotations if self.pod is not None else self.annotations)
 
 
 ANNOTATION_RESERVATION_NAME = "scheduling.koordinator.sh/reservation-name"
@@ -329,7 +343,8 @@ def new_reserve_pod(r: Reservation) -> k8s.Pod:
     reserve-pod / reservation-name annotations and, for a pinned reservation,
     the reservation-node annotation (spec.nodeName cleared); priority 0 when
     unset."""
-    ann = {ANNOTATION_RESERVE_POD: "true", ANNOTATION_RESERVATION_NAME: r.name}
+    ann = dict(r.annotations or {})
+    ann.update({ANNOTATION_RESERVE_POD: "true", ANNOTATION_RESERVATION_NAME: r.name})
     if r.spec_node_name:
         ann[ANNOTATION_RESERVATION_NODE] = r.spec_node_name
     return k8s.Pod(name=reservation_key(r), uid=r.uid, labels=dict(r.labels), annotations=ann, priority=0,
@@ -371,6 +386,7 @@ def is_reservation_operating_pod(pod: k8s.Pod) -> bool:
     return (pod.labels or {}).get(LABEL_POD_OPERATING_MODE) == "Reservation"
 
 
+ANNOTATION_RESERVATION_ALLOCATED = "scheduling.koordinator.sh/reservation-allocated"   # apis/extension/reservation.go:37
 ANNOTATION_RESERVATION_OWNERS = "scheduling.koordinator.sh/reservation-owners"
 ANNOTATION_RESERVATION_CURRENT_OWNER = "scheduling.koordinator.sh/reservation-current-owner"
 
@@ -394,6 +410,33 @@ def _owner_from_json(o: dict) -> ReservationOwner:
                                                                         list(x.get("values") or []))
                                                for x in ls.get("matchExpressions") or []])
     return ReservationOwner(object=obj, controller=ctrl, label_selector=sel)
+
+
+def reservation_allocated(pod: k8s.Pod) -> Optional[Tuple[str, str]]:
+    """GetReservationAllocated: the (uid, name) of the reservation a pod was
+    assumed into (its reservation-allocated annotation), None without one or on
+    a parse error."""
+    raw = (pod.annotations or {}).get(ANNOTATION_RESERVATION_ALLOCATED, "")
+    if not raw:
+        return None
+    try:
+        a = json.loads(raw)
+        return str(a.get("uid", "") or ""), str(a.get("name", "") or "")
+    except (ValueError, TypeError, AttributeError):
+        return None
+
+
+def current_owner(pod: k8s.Pod) -> Optional[Tuple[str, str, str]]:
+    """GetReservationCurrentOwner: (namespace, name, uid) of the pod the
+    operating-mode pod serves, None without one or on a parse error."""
+    raw = (pod.annotations or {}).get(ANNOTATION_RESERVATION_CURRENT_OWNER, "")
+    if not raw:
+        return None
+    try:
+        o = json.loads(raw)
+        return str(o.get("namespace", "") or ""), str(o.get("name", "") or ""), str(o.get("uid", "") or "")
+    except (ValueError, TypeError, AttributeError):
+        return None
 
 
 def operating_reservation_name(pod: k8s.Pod) -> str:
@@ -519,20 +562,41 @@ def _q2(rl: k8s.ResourceList, name: str) -> int:
     return q.milli_value() if name == k8s.CPU else q.value()
 
 
-def available_by_node(node_index: Dict[str, int], reservations: Sequence[Reservation]) -> Dict[int, List[Reservation]]:
+def available_by_node(node_index: Dict[str, int], reservations: Sequence[Reservation],
+                      overflow: Optional[list] = None) -> Dict[int, List[Reservation]]:
     """The reservation cache's Available reservations by node row (cache.go:236-252),
     each node's in the given order: its reservation slots.  The reference keeps
     them in a map and breaks nomination ties by its iteration order; here the
-    lowest slot wins (include/koordhip.h KOORDHIP_RESV_SLOTS)."""
+    lowest slot wins (include/koordhip.h KOORDHIP_RESV_SLOTS).  More than
+    RESV_SLOTS_MAX on a node raise -- except, with `overflow` given, bound
+    operating-mode pods past the limit, which stay plain NodeInfo pods and are
+    appended to `overflow` (outside the engine's envelope, counted by the caller)."""
     placed: Dict[int, List[Reservation]] = {}
     for r in reservations:
         if not r.is_available() or r.node_name not in node_index:
             continue
         rs = placed.setdefault(node_index[r.node_name], [])
         if len(rs) >= abi.RESV_SLOTS_MAX:
+            if overflow is not None and r.pod is not None:
+                overflow.append(r)
+                continue
             raise ReservationError(f"node {r.node_name}: more than {abi.RESV_SLOTS_MAX} Available reservations")
         rs.append(r)
     return placed
+
+
+def reservation_unsupported(r: Reservation, devices: bool) -> Optional[str]:
+    """Why the engine cannot hold `r` as a reservation slot (None: it can):
+    Allocatable keys other than cpu / memory and -- with DeviceShare's device
+    columns (`devices`) -- the device scalars."""
+    from .deviceshare import XRES_INDEX
+    allowed = {k8s.CPU, k8s.MEMORY} | (set(XRES_INDEX) if devices else set())
+    extra = set(r.allocatable) - allowed
+    if extra:
+        return f"resources {sorted(extra)}"
+    if any(r.allocatable[n].value() <= 0 for n in set(r.allocatable) & set(XRES_INDEX)):
+        return "a zero-valued extended resource"
+    return None
 
 
 def slots_needed(placed: Dict[int, List[Reservation]]) -> int:
@@ -553,6 +617,10 @@ def clear_reservation_row(table: NodeTable, i):
     for q in range(table.resv_slots):
         for c in RESV_COLUMNS:
             table[slot_col(c, q)][i] = 0
+    if table.has_resv_dev:
+        table["resv_dev_slot"][i] = -1
+        for c in ("resv_dev", "resv_xalloc", "resv_xallocated"):
+            table[c][i] = 0
 
 
 def reservation_row(table: NodeTable, i: int, r, index: "ReservationIndex", rank: Dict[int, int],
@@ -566,17 +634,80 @@ def reservation_row(table: NodeTable, i: int, r, index: "ReservationIndex", rank
     clear_reservation_row(table, i)
     for q, x in enumerate(rs):
         _reservation_slot(table, i, q, x, index, rank, node_labels)
+    device_reservation_row(table, i, rs)
+
+
+def device_reservation_row(table: NodeTable, i: int, rs: List[Reservation]):
+    """Row i of the device-holding reservation columns (resv_dev_slot, resv_dev,
+    resv_xalloc, resv_xallocated) for node i's reservations `rs` in slot order:
+    DeviceShare's RestoreReservation state (deviceshare/reservation.go:119-170)
+    -- the reserve pod's device allocation as the reservation's allocatable, its
+    AssignedPods' allocations on those minors as its allocated
+    (appendAllocatedByHints) -- and the reservation's NodeResourcesFit extended
+    scalars (Allocatable; Allocated masked to its keys).  The engine holds one
+    such reservation per node; a reservation listing extended scalars must hold
+    devices (its scalars ride on that slot)."""
+    from .deviceshare import TYPE_INDEX, TYPE_RESOURCES, XRES_INDEX
+    held = [(q, r) for q, r in enumerate(rs) if r.device_allocation() or set(r.allocatable) & set(XRES_INDEX)]
+    if not table.has_resv_dev:
+        if held:
+            raise ReservationError(f"reservation {held[0][1].name}: a reservation holding devices needs the "
+                                   "device-holding reservation columns (DeviceShare with devices; NodeTable.enable_resv_dev)")
+        return
+    table["resv_dev_slot"][i] = -1
+    table["resv_dev"][i] = 0
+    table["resv_xalloc"][i] = 0
+    table["resv_xallocated"][i] = 0
+    if not held:
+        return
+    if len(held) > 1:
+        raise ReservationError(f"node {i}: more than one reservation holding devices (the engine holds one per node)")
+    q, r = held[0]
+    alloc = r.device_allocation()
+    if not alloc:
+        raise ReservationError(f"reservation {r.name}: extended resources in its Allocatable but no device allocation")
+    slot_of = {(typ, int(table["dev_minor"][i, t, s])): s for typ, t in TYPE_INDEX.items()
+               for s in range(table.dev_slots) if table["dev_minor"][i, t, s] >= 0}
+    A = table["resv_dev"][i, 0]
+    D = table["resv_dev"][i, 1]
+    for typ, items in alloc.items():
+        for minor, res in items:
+            s = slot_of.get((typ, minor))
+            if s is None:
+                raise ReservationError(f"reservation {r.name}: device {typ}/{minor} is not on its node")
+            for k, n in enumerate(TYPE_RESOURCES[typ]):
+                A[TYPE_INDEX[typ], s, k] += res.get(n, 0)
+    for pa in r.assigned_devices:         # appendAllocatedByHints: only the reservation's minors
+        for typ, items in pa.items():
+            for minor, res in items:
+                s = slot_of.get((typ, minor))
+                if s is None or not A[TYPE_INDEX[typ], s].any():
+                    continue
+                for k, n in enumerate(TYPE_RESOURCES[typ]):
+                    D[TYPE_INDEX[typ], s, k] += res.get(n, 0)
+    if not A.any():
+        raise ReservationError(f"reservation {r.name}: its device allocation holds no resources")
+    table["resv_dev_slot"][i] = q
+    for n in set(r.allocatable) & set(XRES_INDEX):
+        j = XRES_INDEX[n]
+        table["resv_xalloc"][i, j] = r.allocatable[n].value()
+        table["resv_xallocated"][i, j] = r.allocated[n].value() if n in r.allocated else 0
 
 
 def _reservation_slot(table: NodeTable, i: int, q: int, r: Reservation, index: "ReservationIndex",
                       rank: Dict[int, int], node_labels: Optional[Dict[str, str]]):
     from .marshal import nonzero_request, fit_request
 
+    from .deviceshare import XRES_INDEX, fit_xreq
     col = lambda c: table[slot_col(c, q)]
     names = set(r.allocatable)
-    extra = names - {k8s.CPU, k8s.MEMORY}
+    xnames = names & set(XRES_INDEX)
+    extra = names - {k8s.CPU, k8s.MEMORY} - xnames
     if extra:
         raise ReservationError(f"reservation {r.name}: resources {sorted(extra)} are not supported")
+    for n in sorted(xnames):
+        if r.allocatable[n].value() <= 0:     # (a zero-valued key: Restricted's LessThanOrEqual still reads it)
+            raise ReservationError(f"reservation {r.name}: a zero-valued extended resource {n!r} in its Allocatable")
     parse_ok = not r.parse_error
     try:
         for o in r.owners:
@@ -586,9 +717,12 @@ def _reservation_slot(table: NodeTable, i: int, q: int, r: Reservation, index: "
         parse_ok = False                                  # ReservationInfo.ParseError
     pod = r.reserve_pod()
     req, present = fit_request(pod)
-    if present - {k8s.CPU, k8s.MEMORY} or any(req[k] for k in range(abi.NRES) if k not in (abi.RES_CPU, abi.RES_MEM)):
-        raise ReservationError(f"reservation {r.name}: the reserve pod requests resources other than cpu/memory")
-    if req[abi.RES_CPU] != _q2(r.allocatable, k8s.CPU) or req[abi.RES_MEM] != _q2(r.allocatable, k8s.MEMORY):
+    if present - {k8s.CPU, k8s.MEMORY} - set(XRES_INDEX) or \
+            any(req[k] for k in range(abi.NRES) if k not in (abi.RES_CPU, abi.RES_MEM)):
+        raise ReservationError(f"reservation {r.name}: the reserve pod requests resources other than cpu, memory and "
+                               "device scalars")
+    if req[abi.RES_CPU] != _q2(r.allocatable, k8s.CPU) or req[abi.RES_MEM] != _q2(r.allocatable, k8s.MEMORY) or \
+            fit_xreq(pod) != {n: r.allocatable[n].value() for n in xnames}:
         raise ReservationError(f"reservation {r.name}: allocatable differs from the reserve pod's requests")
     f = abi.RESV_PRESENT if parse_ok else 0
     if r.allocate_once is None or r.allocate_once:
@@ -650,12 +784,13 @@ def reserved_cpu_mask(table: NodeTable, i: int, r: Reservation) -> List[int]:
 
 def reservation_columns(table: NodeTable, node_index: Dict[str, int], reservations: Sequence[Reservation],
                         index: Optional[ReservationIndex] = None,
-                        node_labels: Optional[Dict[str, Dict[str, str]]] = None) -> ReservationIndex:
+                        node_labels: Optional[Dict[str, Dict[str, str]]] = None,
+                        overflow: Optional[list] = None) -> ReservationIndex:
     """Fill the resv_* columns of `table` (the reservation cache's view,
     cache.go:236-252) and return the owner groups for the pod masks
     (node_labels: node name -> labels, for reservation affinities)."""
     index = index or ReservationIndex()
-    placed = available_by_node(node_index, reservations)
+    placed = available_by_node(node_index, reservations, overflow)
     table.set_resv_slots(max(table.resv_slots, slots_needed(placed)))
     clear_reservation_row(table, slice(None))
     rank = order_ranks(placed.values())

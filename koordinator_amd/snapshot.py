@@ -58,8 +58,11 @@ IPA_MUTABLE = ["ipa_cnt"]
 # its one such reservation [n] i32 (-1: none) and that reservation's device
 # allocatable / allocated [n][2][TYPES][dev_slots][RES] i64 (the allocated half
 # mutable).  Present after enable_resv_dev().
-RESV_DEV_COLS = ["resv_dev_slot", "resv_dev"]
-RESV_DEV_MUTABLE = ["resv_dev"]
+RESV_DEV_COLS = ["resv_dev_slot", "resv_dev", "resv_xalloc", "resv_xallocated"]
+RESV_DEV_MUTABLE = ["resv_dev", "resv_xallocated"]
+# (ABI 14: that reservation's NodeResourcesFit extended scalars [n][NXRES] i64,
+# its Allocatable -- the reserve pod's scalar requests -- and Allocated, the
+# latter mutable)
 
 
 @dataclass
@@ -187,6 +190,8 @@ class NodeTable:
             raise ValueError("device-holding reservations need the device columns (enable_ext(dev_slots > 0))")
         self.cols["resv_dev_slot"] = np.full(self.n, -1, np.int32)
         self.cols["resv_dev"] = np.zeros((self.n, 2, abi.DEV_TYPES, self.dev_slots, abi.DEV_RES), np.int64)
+        self.cols["resv_xalloc"] = np.zeros((self.n, abi.NXRES), np.int64)
+        self.cols["resv_xallocated"] = np.zeros((self.n, abi.NXRES), np.int64)
         return self
 
     def set_resv_slots(self, slots: int):
@@ -328,6 +333,11 @@ class NodeTable:
                 keep["resv_dev"] = np.ascontiguousarray(self.cols["resv_dev"], dtype=np.int64)
                 s.resv_dev_slot = keep["resv_dev_slot"].ctypes.data_as(C.POINTER(C.c_int32))
                 s.resv_dev = keep["resv_dev"].ctypes.data_as(C.POINTER(C.c_int64))
+                if self.cols["resv_xalloc"].any():      # NULL: no reservation holds extended scalars
+                    keep["resv_xalloc"] = np.ascontiguousarray(self.cols["resv_xalloc"].T)          # [NXRES][n]
+                    keep["resv_xallocated"] = np.ascontiguousarray(self.cols["resv_xallocated"].T)
+                    s.resv_xalloc = keep["resv_xalloc"].ctypes.data_as(C.POINTER(C.c_int64))
+                    s.resv_xallocated = keep["resv_xallocated"].ctypes.data_as(C.POINTER(C.c_int64))
             s._keep_ext = keep
         if self.has_pts:
             m = self.pts

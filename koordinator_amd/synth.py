@@ -663,11 +663,17 @@ class DevResvSpec:
     Restricted)."""
     frac: float = 0.8
     policy: tuple = (0.5, 0.25, 0.25)
+    # the reserve pod requests its GPUs in the koordinator.sh/gpu-core +
+    # gpu-memory-ratio form: those scalars are the reservation's extended
+    # Allocatable (resv_xalloc), its assigned pods' share its Allocated
+    # (resv_xallocated), and both sit in the node's Requested (xrequested)
+    scalars: bool = True
 
 
 def add_device_reservations(t: NodeTable, spec: DevResvSpec = DevResvSpec(), seed: int = SEED) -> NodeTable:
     """The resv_dev_* columns: both allocations join dev_used, as in the
     nodeDevice cache (the reserve pod and its assigned pods are pods of the node)."""
+    from .deviceshare import GPU_CORE, GPU_MEMORY_RATIO, XRES_INDEX
     G = abi.DEV_GPU
     rng = np.random.default_rng(seed + 1000)
     t.enable_resv_dev()
@@ -691,6 +697,13 @@ def add_device_reservations(t: NodeTable, spec: DevResvSpec = DevResvSpec(), see
             t["dev_used"][i, G, s] += a + d
         if t["resv_dev"][i, 0].any():
             t["resv_dev_slot"][i] = 0
+            if spec.scalars:
+                A, D = t["resv_dev"][i, 0, G], t["resv_dev"][i, 1, G]
+                for k, name in ((0, GPU_CORE), (1, GPU_MEMORY_RATIO)):
+                    j = XRES_INDEX[name]
+                    t["resv_xalloc"][i, j] = int(A[:, k].sum())
+                    t["resv_xallocated"][i, j] = int(D[:, k].sum())
+                    t["xrequested"][i, j] += int(A[:, k].sum()) + int(D[:, k].sum())
             f = int(t["resv_flags"][i]) & ~(3 << abi.RESV_POLICY_SHIFT)
             t["resv_flags"][i] = f | (int(pol[i]) << abi.RESV_POLICY_SHIFT)
     return t

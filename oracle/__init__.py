@@ -49,6 +49,7 @@ class OrcState(C.Structure):
         ("pts_cnt", C.POINTER(C.c_int32)),
         ("ipa_cnt", C.POINTER(C.c_int32)),
         ("resv_dev", C.POINTER(C.c_int64)),
+        ("resv_xallocated", C.POINTER(C.c_int64)),
         ("cur_ext", C.c_void_p),
         ("resv_restore", C.c_int32),
     ]
@@ -165,6 +166,7 @@ class Oracle:
         lib().orc_eval_ext(C.byref(self.cfg), C.byref(self.st), pods.ctypes.data, x.ctypes.data if x is not None else None,
                            p, st.ctypes.data if st is not None else None, sc.ctypes.data if sc is not None else None,
                            tk.ctypes.data if tk is not None else None, k)
+        self.st.cur_ext = None              # (the records die with this call)
         return {"status": st, "scores": sc, "topk": tk}
 
     def place_stream_ext(self, pods: np.ndarray, ext=None, threads: int = 1, cpusets: bool = False,
@@ -181,6 +183,7 @@ class Oracle:
                                         x.ctypes.data if x is not None else None, len(pods), out.ctypes.data, threads)
         lib().orc_set_cpuset_out(C.byref(self.st), None)
         lib().orc_set_dev_out(C.byref(self.st), None)
+        self.st.cur_ext = None
         if rc != 0:
             raise RuntimeError("orc_place_stream_ext failed")
         res = (out,) + ((cs,) if cpusets else ()) + ((dv,) if devices else ())
@@ -193,6 +196,13 @@ class Oracle:
         if not self.st.resv_dev:
             return np.zeros(shape, np.int64)
         return np.ctypeslib.as_array(self.st.resv_dev, shape=shape).copy()
+
+    def resv_scalar_state(self) -> np.ndarray:
+        """The device-holding reservations' extended-scalar Allocated, [n][NXRES]
+        (zeros without the resv_xalloc column)."""
+        if not self.st.resv_xallocated:
+            return np.zeros((self.n, abi.NXRES), np.int64)
+        return np.ctypeslib.as_array(self.st.resv_xallocated, shape=(abi.NXRES, self.n)).T.copy()
 
     def dev_try_from_reservation(self, pod, ext_rec, node: int, from_resv: bool = False):
         """tryAllocateFromReservation over node's matched reservation holding
@@ -309,6 +319,7 @@ class Oracle:
 
     def resv_restore_delta(self, pod: np.ndarray, node: int):
         """(requested delta [cpu, mem], non-zero delta [cpu, mem], pod-count delta) of the restore."""
+        self.st.cur_ext = None    # a plain record: no scalar requests (no stale ext pointer)
         pod = np.ascontiguousarray(np.atleast_1d(pod))
         dr, dn, dp = np.zeros(2, np.int64), np.zeros(2, np.int64), np.zeros(1, np.int32)
         lib().orc_resv_restore_delta(C.byref(self.st), pod.ctypes.data, node, dr.ctypes.data, dn.ctypes.data,
@@ -317,6 +328,7 @@ class Oracle:
 
     def resv_filter(self, pod: np.ndarray, node: int) -> bool:
         """filterWithReservations of (pod, node) inside the pod's cycle (restore applied)."""
+        self.st.cur_ext = None    # a plain record: no scalar requests (no stale ext pointer)
         pod = np.ascontiguousarray(np.atleast_1d(pod))
         lib().orc_resv_restore(C.byref(self.st), pod.ctypes.data, 1)
         ok = lib().orc_resv_filter(C.byref(self.st), pod.ctypes.data, node)
@@ -324,20 +336,24 @@ class Oracle:
         return bool(ok)
 
     def resv_nominated(self, pod: np.ndarray, node: int) -> bool:
+        self.st.cur_ext = None    # a plain record: no scalar requests (no stale ext pointer)
         pod = np.ascontiguousarray(np.atleast_1d(pod))
         return bool(lib().orc_resv_nominated(C.byref(self.st), pod.ctypes.data, node))
 
     def resv_nominate(self, pod: np.ndarray, node: int) -> int:
         """NominateReservation on `node`: the nominated reservation's slot, -1 for none."""
+        self.st.cur_ext = None    # a plain record: no scalar requests (no stale ext pointer)
         pod = np.ascontiguousarray(np.atleast_1d(pod))
         return int(lib().orc_resv_nominate(C.byref(self.st), pod.ctypes.data, node))
 
     def resv_score(self, pod: np.ndarray, node: int) -> int:
+        self.st.cur_ext = None    # a plain record: no scalar requests (no stale ext pointer)
         pod = np.ascontiguousarray(np.atleast_1d(pod))
         return int(lib().orc_resv_score(C.byref(self.st), pod.ctypes.data, node))
 
     def resv_normalized(self, pod: np.ndarray, feasible) -> np.ndarray:
         """PreScore + Score + DefaultNormalizeScore of the Reservation plugin over `feasible`."""
+        self.st.cur_ext = None    # a plain record: no scalar requests (no stale ext pointer)
         pod = np.ascontiguousarray(np.atleast_1d(pod))
         f = np.ascontiguousarray(feasible, np.int32)
         out = np.zeros(len(f), np.int64)

@@ -158,6 +158,10 @@ int orc_state_init(orc_state *st, const koordhip_node_soa *soa, int32_t n) {
     st->resv_dev = dup64(soa->resv_dev, n * 2 * KOORDHIP_DEV_TYPES * soa->dev_slots * KOORDHIP_DEV_RES);
     if (!st->resv_dev) return -1;
   }
+  if (soa->resv_xalloc && soa->resv_dev_slot) {
+    st->resv_xallocated = dup64(soa->resv_xallocated, n * KOORDHIP_NXRES);
+    if (!st->resv_xallocated) return -1;
+  }
   if (!st->flags || !st->npods || !st->numa_alloc_cnt || !st->numa_zone_used || !st->resv_assigned || !st->dev_used ||
       !st->xrequested)
     return -1;
@@ -191,6 +195,7 @@ void orc_state_free(orc_state *st) {
   free(st->pts_cnt);
   free(st->ipa_cnt);
   free(st->resv_dev);
+  free(st->resv_xallocated);
   memset(st, 0, sizeof(*st));
 }
 
@@ -382,6 +387,7 @@ int orc_eval(const koordhip_config *cfg, const orc_state *st, const koordhip_pod
   const int32_t n = st->n;
   uint64_t *keys = (topk && k > 0) ? (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1)) : NULL;
   const int rv = orc_resv_on(cfg, st);
+  ((orc_state *)st)->cur_ext = NULL; /* plain records: no scalar requests */
   for (int32_t p = 0; p < n_pods; p++) {
     const koordhip_pod *pod = &pods[p];
     int32_t nk = 0;
@@ -812,6 +818,7 @@ static void score_piece(void *a, int32_t lo, int32_t hi) {
 
 int orc_place_stream(const koordhip_config *cfg, orc_state *st, const koordhip_pod *pods, int32_t n_pods,
                      int32_t *out_node, int32_t threads) {
+  st->cur_ext = NULL;
   return orc_place_stream_ext(cfg, st, pods, NULL, n_pods, out_node, threads);
 }
 

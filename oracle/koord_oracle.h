@@ -75,6 +75,10 @@ typedef struct orc_state {
   /* DeviceShare: the resv_dev column of the snapshot's device-holding
    * reservations, its allocated half advanced by Reserve (NULL: none) */
   int64_t *resv_dev;
+  /* ABI 14: the extended scalars' Allocated of each node's device-holding
+   * reservation [NXRES][n] (the resv_xallocated column, advanced by Reserve;
+   * NULL: no snapshot column) */
+  int64_t *resv_xallocated;
   /* the koordhip_pod_ext record of the pod being scheduled (NULL: none): the
    * nomination's DeviceShare FilterReservation reads it */
   const koordhip_pod_ext *cur_ext;

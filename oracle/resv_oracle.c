@@ -53,6 +53,24 @@ static int64_t rem_of(const orc_state *st, size_t x, int r) {
   return has_key(st->soa->resv_flags[x], r) ? max0(st->soa->resv_alloc[r][x] - st->resv_allocated[r][x]) : 0;
 }
 
+/* ---- ABI 14: the extended scalars of the node's reservation holding devices
+ * (slot h = resv_dev_slot[i]): more keys of that reservation's Allocatable
+ * (resv_xalloc; a listed key is > 0) and Allocated (st->resv_xallocated), so
+ * every ResourceList rule of this file sees them as it sees cpu / memory.  The
+ * pod's scalar requests are its koordhip_pod_ext record's (st->cur_ext; NULL:
+ * none). */
+static int xslot(const orc_state *st, int32_t i) {
+  if (!st->soa->resv_xalloc || !st->soa->resv_dev_slot || !st->resv_xallocated) return -1;
+  return st->soa->resv_dev_slot[i];
+}
+static int64_t xa(const orc_state *st, int j, int32_t i) { return st->soa->resv_xalloc[(size_t)j * st->n + i]; }
+static int64_t xrem(const orc_state *st, int j, int32_t i) {
+  return max0(xa(st, j, i) - st->resv_xallocated[(size_t)j * st->n + i]);
+}
+/* the pod requests scalar j (the key is in its request map) */
+static int xkey(const orc_state *st, int j) { return st->cur_ext && ((st->cur_ext->xmask >> j) & 1u); }
+static int64_t xreq(const orc_state *st, int j) { return xkey(st, j) ? st->cur_ext->xreq[j] : 0; }
+
 /* transformer.go:86-103: 1 = matched, 2 = unmatched with assigned pods, 0 =
  * untouched, for slot x (isReservedPod is false: reserve pods are not streamed). */
 static int slot_class(const orc_state *st, const koordhip_pod *pod, size_t x) {
@@ -102,10 +120,14 @@ void orc_resv_restore_delta(const orc_state *st, const koordhip_pod *pod, int32_
       *dpods -= 1; /* RemovePod */
       continue;
     }
-    /* unmatched: a pod requesting SubtractWithNonNegativeResult(Allocatable, Allocated) comes back unless IsZero */
+    /* unmatched: a pod requesting SubtractWithNonNegativeResult(Allocatable, Allocated) comes back unless IsZero
+     * (its scalars too, on the device-holding reservation) */
     const uint32_t rf = so->resv_flags[x];
     const int64_t rem0 = rem_of(st, x, 0), rem1 = rem_of(st, x, 1);
-    if (rem0 == 0 && rem1 == 0) continue;
+    int xany = 0;
+    if (s == xslot(st, i))
+      for (int j = 0; j < KOORDHIP_NXRES; j++) xany |= xrem(st, j, i) != 0;
+    if (rem0 == 0 && rem1 == 0 && !xany) continue;
     for (int r = 0; r < 2; r++) {
       const int64_t rem = r ? rem1 : rem0;
       dreq[r] += rem;
@@ -126,6 +148,13 @@ void orc_resv_restore(orc_state *st, const koordhip_pod *pod, int sign) {
     st->nz_cpu_m[i] += sign * dnz[0];
     st->nz_mem[i] += sign * dnz[1];
     st->npods[i] += sign * dp;
+    /* NodeResourcesFit's extended scalars (updateNodeInfoRequested's ScalarResources loop, :285-290, and
+     * RemovePod): the device-holding reservation's Allocatable leaves, its remainder comes back when unmatched */
+    const int h = xslot(st, i);
+    const int c = h >= 0 ? slot_class(st, pod, at(st, h, i)) : 0;
+    if (c)
+      for (int j = 0; j < KOORDHIP_NXRES; j++)
+        st->xrequested[(size_t)j * st->n + i] += sign * (-xa(st, j, i) + (c == 2 ? xrem(st, j, i) : 0));
   }
 }
 
@@ -173,11 +202,28 @@ int orc_resv_filter(const orc_state *st, const koordhip_pod *pod, int32_t i) {
           pod->req[KOORDHIP_RES_BMEM] > so->alloc[KOORDHIP_RES_BMEM][i] - st->requested[KOORDHIP_RES_BMEM][i])
         fits = 0;
     }
+    /* fitsNode over the pod's scalars: Allocatable - (podRequested - rRemained - allRAllocated), podRequested
+     * = the scalars' Requested after the unmatched restore (the matched one undone), on the device-holding
+     * reservation h (rRemained: this reservation's, h's only when x is h; allRAllocated: h's when matched) */
+    const int h = xslot(st, i);
+    if (fits && (pod->flags & KOORDHIP_POD_HAS_REQ) && st->cur_ext)
+      for (int j = 0; j < KOORDHIP_NXRES && fits; j++) {
+        if (!xkey(st, j)) continue;
+        const int hm = h >= 0 && slot_class(st, pod, at(st, h, i)) == 1;
+        const int64_t alloc = so->xalloc ? so->xalloc[(size_t)j * st->n + i] : 0;
+        const int64_t preq = st->xrequested[(size_t)j * st->n + i] + (hm ? xa(st, j, i) : 0);
+        const int64_t rrem = (h >= 0 && s == h) ? xrem(st, j, i) : 0;
+        const int64_t rall_x = hm ? st->resv_xallocated[(size_t)j * st->n + i] : 0;
+        if (xreq(st, j) > alloc - (preq - rrem - rall_x)) fits = 0;
+      }
     if (policy == 1 && fits) return 1; /* Aligned :415-419 */
     if (policy == 2) {                  /* Restricted :420-432: LessThanOrEqual(podRequests, rRemained) */
       int le = 1;
       for (int r = 0; r < 2; r++)
         if (has_key(so->resv_flags[x], r) && pod_key(pod, r) && pod->req[r] > rem_of(st, x, r)) le = 0;
+      if (h >= 0 && s == h)
+        for (int j = 0; j < KOORDHIP_NXRES; j++)
+          if (xa(st, j, i) != 0 && xkey(st, j) && xreq(st, j) > xrem(st, j, i)) le = 0;
       if (le && fits) return 1;
     }
   }
@@ -203,7 +249,8 @@ int orc_resv_reserve_pod_ok(const orc_state *st, const koordhip_pod *pod, const 
 }
 
 /* FilterReservation (plugin.go:504-535) of slot x, a matched reservation */
-static int slot_passes(const orc_state *st, const koordhip_pod *pod, size_t x) {
+static int slot_passes(const orc_state *st, const koordhip_pod *pod, int s, int32_t i) {
+  const size_t x = at(st, s, i);
   const uint32_t rf = st->soa->resv_flags[x];
   int inter = 0, nonzero = 0;
   for (int r = 0; r < 2; r++) {
@@ -211,12 +258,19 @@ static int slot_passes(const orc_state *st, const koordhip_pod *pod, size_t x) {
     inter = 1;
     if (rem_of(st, x, r) != 0) nonzero = 1;
   }
+  if (s == xslot(st, i))
+    for (int j = 0; j < KOORDHIP_NXRES; j++) {
+      if (!(xa(st, j, i) != 0 && xkey(st, j))) continue;
+      inter = 1;
+      if (xrem(st, j, i) != 0) nonzero = 1;
+    }
   return inter && nonzero;
 }
 
 /* scoreReservation (scoring.go:177-200) of slot x: MostAllocated over
  * RemoveZeros(Allocatable) of podRequests + Allocated. */
-static int64_t slot_score(const orc_state *st, const koordhip_pod *pod, size_t x) {
+static int64_t slot_score(const orc_state *st, const koordhip_pod *pod, int slot, int32_t i) {
+  const size_t x = at(st, slot, i);
   const uint32_t rf = st->soa->resv_flags[x];
   int64_t s = 0, w = 0;
   for (int r = 0; r < 2; r++) {
@@ -226,6 +280,14 @@ static int64_t slot_score(const orc_state *st, const koordhip_pod *pod, size_t x
     const int64_t req = (pod_key(pod, r) ? pod->req[r] : 0) + st->resv_allocated[r][x];
     if (req <= cap) s += 100 * req / cap; /* MaxNodeScore * MilliValue / MilliValue */
   }
+  if (slot == xslot(st, i)) /* the scalars of RemoveZeros(Allocatable), requested = the pod's + Allocated */
+    for (int j = 0; j < KOORDHIP_NXRES; j++) {
+      const int64_t cap = xa(st, j, i);
+      if (cap == 0) continue;
+      w++;
+      const int64_t req = xreq(st, j) + st->resv_xallocated[(size_t)j * st->n + i];
+      if (req <= cap) s += 100 * req / cap;
+    }
   return w ? s / w : 0;
 }
 
@@ -257,7 +319,7 @@ int orc_resv_nominate(const orc_state *st, const koordhip_pod *pod, int32_t i) {
   int64_t best_sc = -1;
   for (int s = 0; s < orc_resv_slots(st); s++) {
     const size_t x = at(st, s, i);
-    if (slot_class(st, pod, x) != 1 || !slot_passes(st, pod, x)) continue;
+    if (slot_class(st, pod, x) != 1 || !slot_passes(st, pod, s, i)) continue;
     if (devshare && s != dslot) continue;
     const uint32_t rf = st->soa->resv_flags[x];
     if (rf & KOORDHIP_RESV_ORDERED) {
@@ -268,7 +330,7 @@ int orc_resv_nominate(const orc_state *st, const koordhip_pod *pod, int32_t i) {
         ord = 1;
       }
     } else if (!ord) {
-      const int64_t sc = slot_score(st, pod, x);
+      const int64_t sc = slot_score(st, pod, s, i);
       if (sc > best_sc) {
         best = s;
         best_sc = sc;
@@ -286,7 +348,7 @@ int orc_resv_nominated(const orc_state *st, const koordhip_pod *pod, int32_t i) 
  * nominated reservation's scoreReservation, 0 without one. */
 int64_t orc_resv_score(const orc_state *st, const koordhip_pod *pod, int32_t i) {
   const int s = orc_resv_nominate(st, pod, i);
-  return s < 0 ? 0 : slot_score(st, pod, at(st, s, i));
+  return s < 0 ? 0 : slot_score(st, pod, s, i);
 }
 
 /* PreScore's node order (scoring.go:58-67): the smallest order label among the
@@ -315,6 +377,9 @@ void orc_resv_assume(orc_state *st, const koordhip_pod *pod, int32_t i, const ui
   for (int r = 0; r < 2; r++)
     if (has_key(rf, r) && pod_key(pod, r)) st->resv_allocated[r][x] += pod->req[r];
   st->resv_assigned[x] += 1;
+  if (s == xslot(st, i)) /* ... and the pod's scalars masked to its keys */
+    for (int j = 0; j < KOORDHIP_NXRES; j++)
+      if (xa(st, j, i) != 0 && xkey(st, j)) st->resv_xallocated[(size_t)j * st->n + i] += xreq(st, j);
   if (cpus && st->resv_cpus[0])
     for (int w = 0; w < KOORDHIP_NUMA_WORDS; w++) st->resv_cpus[w][x] &= ~cpus[w];
 }

@@ -621,3 +621,57 @@ def test_operating_mode_pod_is_a_reservation():
     assert int(inf.table(NOW)["resv_flags"][2]) & abi.RESV_PRESENT
     inf.on_pod_delete(op)
     assert not int(inf.table(NOW)["resv_flags"][2])
+
+
+def test_operating_mode_pods_outside_the_envelope_stay_plain_pods():
+    """a bound operating-mode pod whose requests the engine
+    cannot hold as a reservation slot (ephemeral-storage, or nvidia.com/gpu
+    without DeviceShare's device columns) stays a plain NodeInfo pod, counted in
+    `outside_envelope` -- table() and delta() do not raise; more than
+    RESV_SLOTS_MAX operating pods on one node likewise (the extra ones stay
+    plain).  Its owners parsed on the first add stay and its current owners
+    accumulate (cache.go:139-161); a terminated pod leaves the cache."""
+    import json as _json
+    from koordinator_amd import abi
+    from koordinator_amd import reservation as rv
+    prof = shipped_profile(reservation=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(64), k8s.MEMORY: k8s.Q(128 * GI), k8s.PODS: k8s.Q(110),
+                                                 k8s.EPHEMERAL: k8s.Q(100 * GI)}) for i in range(2)]
+    inf = Informer(prof, nodes, NOW)
+    op = lambda name, req, ann=None: k8s.Pod(name=name, uid=name, node_name="n0",
+                                             labels={rv.LABEL_POD_OPERATING_MODE: "Reservation"},
+                                             annotations=dict(ann or {}),
+                                             containers=[k8s.Container(requests=req)])
+    gpu = op("op-gpu", {k8s.CPU: k8s.Q(1), "nvidia.com/gpu": k8s.Q(1)})
+    eph = op("op-eph", {k8s.CPU: k8s.Q(1), k8s.EPHEMERAL: k8s.Q(GI)})
+    inf.on_pod_add(gpu, NOW)
+    inf.on_pod_add(eph, NOW)
+    t = inf.table(NOW)                              # no raise
+    assert not int(t["resv_flags"][0]) & abi.RESV_PRESENT
+    assert set(inf.outside_envelope) == {gpu.key, eph.key}
+    assert int(t["npods"][0]) == 2                  # still NodeInfo pods
+    # nine supported operating pods on one node: eight slots, the ninth plain
+    owners = _json.dumps([{"labelSelector": {"matchLabels": {"app": "web"}}}])
+    for k in range(9):
+        inf.on_pod_add(op(f"op-{k}", {k8s.CPU: k8s.Q(1), k8s.MEMORY: k8s.Q(GI)},
+                          {rv.ANNOTATION_RESERVATION_OWNERS: owners}), NOW)
+    t = inf.table(NOW)
+    assert t.resv_slots == abi.RESV_SLOTS_MAX and len(inf.outside_envelope) == 3
+    res = inf.flush(_TableEngine(t), NOW)           # a delta does not raise either
+    assert not res.needs_reload
+    # sticky owners: an edit of the owners annotation does not change the groups the slot matches
+    p0 = next(p for p in inf.cluster.node_pods["n0"] if p.name == "op-0")
+    edited = copy.deepcopy(p0)
+    edited.annotations[rv.ANNOTATION_RESERVATION_OWNERS] = _json.dumps([{"labelSelector": {"matchLabels": {"app": "db"}}}])
+    edited.annotations[rv.ANNOTATION_RESERVATION_CURRENT_OWNER] = _json.dumps({"name": "web-1", "namespace": "default"})
+    inf.on_pod_update(p0, edited, NOW)
+    r = inf.reservations[rv.operating_reservation_name(edited)]
+    assert r.owners[0].label_selector.match_labels == {"app": "web"} and r.assigned == 1
+    cleared = copy.deepcopy(edited)
+    del cleared.annotations[rv.ANNOTATION_RESERVATION_CURRENT_OWNER]
+    inf.on_pod_update(edited, cleared, NOW)         # AddAssignedPod is cumulative: still assigned
+    assert inf.reservations[rv.operating_reservation_name(cleared)].assigned == 1
+    done = copy.deepcopy(cleared)
+    done.phase = "Succeeded"
+    inf.on_pod_update(cleared, done, NOW)           # terminated: out of the cache
+    assert rv.operating_reservation_name(done) not in inf.reservations
