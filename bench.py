@@ -133,12 +133,48 @@ def pmc_traffic(workload="config4"):
     if not os.path.exists(p) and workload == "config4":
         p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
-        return None, None, None
+        return None, None, None, {}
     try:
         d = json.load(open(p))
-        return d.get("hbm_bytes_per_launch"), d.get("source"), d.get("kernel")
+        return d.get("hbm_bytes_per_launch"), d.get("source"), d.get("kernel"), d.get("kernels", {})
     except (OSError, ValueError):
-        return None, None, None
+        return None, None, None, {}
+
+
+def latency_leg(eng, pods, ext=None, reps=200):
+    """The per-cycle drop-in path (the shim's
+    PreFilter calls koordhip_eval for the one pod of a scheduling cycle and
+    reads the per-node status / per-plugin score arrays; batch admission calls
+    koordhip_place_stream): host-to-host wall time per call on the loaded
+    snapshot, median and p99 of `reps` calls after 10 warm-up calls -- the
+    pod upload, the launches, the synchronisation and the result copies
+    included.  place_stream commits its pods (the state is restored after)."""
+    import numpy as _np
+
+    def timed(fn):
+        for _ in range(10):
+            fn()
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            fn()
+            ts.append((time.perf_counter() - t) * 1e6)
+        ts = _np.sort(_np.array(ts))
+        return {"median_us": round(float(_np.median(ts)), 1), "p99_us": round(float(ts[int(len(ts) * 0.99) - 1]), 1),
+                "calls": reps}
+
+    one, many = pods[:1], pods[:64]
+    out = {"nodes": int(eng.n), "method": "time.perf_counter around each C-ABI call (host to host), after 10 warm-up calls",
+           "eval_1pod_status_scores": timed(lambda: eng.eval(one, status=True, scores=True)),
+           "eval_1pod_status_only": timed(lambda: eng.eval(one, status=True, scores=False))}
+    if ext is None:
+        out["place_stream_1pod"] = timed(lambda: eng.place_stream(one))
+        out["place_stream_64pods"] = timed(lambda: eng.place_stream(many))
+    else:
+        out["place_stream_1pod"] = timed(lambda: eng.place_stream_ext(one, ext[:1]))
+        out["place_stream_64pods"] = timed(lambda: eng.place_stream_ext(many, ext[:64]))
+    eng.restore()
+    return out
 
 
 def launch_ranks(n: int) -> int:
@@ -188,11 +224,16 @@ def main():
     ap.add_argument("--one-rank-comm", action="store_true",
                     help="N=1 only: attach a one-rank RCCL communicator, so every round takes the multi-GPU "
                          "exchange path (all-gather + merge) -- measures that pipeline on one GPU")
-    ap.add_argument("--mode", choices=["replicas", "shard"], default="replicas",
-                    help="N > 1: 'replicas' (default) -- every rank places its own copy of the stream on its own "
-                         "replica of the cluster (independent scheduler instances; weak scaling: the greedy's "
-                         "sequential Reserve chain does not shard, DESIGN.md section 6); 'shard' -- the node table "
-                         "sharded across the ranks, per-round top-k all-gathered over RCCL (strong scaling)")
+    ap.add_argument("--mode", choices=["replicas", "shard"], default="shard",
+                    help="N > 1: 'shard' (default, north_star's partition: ONE cluster's schedule) -- the node "
+                         "table sharded across the ranks with the per-round top-k all-gathered over RCCL, or, "
+                         "where the class-incremental lists cover the batch, every rank on the full replica "
+                         "without an exchange (the library's fallback: never slower than one GPU; DESIGN.md "
+                         "section 6); 'replicas' (opt-in) -- independent replicas, not one cluster: every rank "
+                         "places its own copy of the stream on its own copy of the cluster")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the per-cycle latency leg (koordhip_eval of 1 pod, koordhip_place_stream of 1 / "
+                         "64 pods on the loaded snapshot)")
     ap.add_argument("--probe-ranks", action="store_true",
                     help="print this rank's RANK / WORLD_SIZE and exit before any GPU work (launcher test)")
     args = ap.parse_args()
@@ -266,10 +307,12 @@ def main():
         eng.comm_init(PlacementEngine.comm_unique_id(), 1, 0)
     eng.load_snapshot(table)
     eng.checkpoint()
+    t_st = time.perf_counter()
     if ext is None:
         eng.stage_pods(pods)
     else:
         eng.stage_pods_ext(pods, ext)
+    stage_pods_ms = (time.perf_counter() - t_st) * 1e3
 
     def step():
         eng.restore()
@@ -299,11 +342,16 @@ def main():
     ks = eng.kernel_stats()
     kn = eng.kernel_names()
     eng.set_profile_kernels(False)
+    executed = float(ks["executed_evals"])   # this rank's, per step
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        te = torch.tensor([executed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(te, op=dist.ReduceOp.SUM)   # every rank's evaluations (a local rank runs the full table)
+        executed = float(te.item())
     placements = eng.fetch_placements(len(pods))
+    lat = latency_leg(eng, pods, ext) if (world == 1 and not args.no_latency) else None
 
     if rank != 0:
         if dist is not None:
@@ -313,7 +361,13 @@ def main():
 
     pods_total = args.pods * args.steps * (world if world > 1 and not shard else 1)  # replicas: every rank's stream
     pods_profiled = args.pods
-    evals_total = pods_total * args.nodes   # every pod is evaluated against every node (of its replica)
+    # equivalent evaluations: every (pod, node) pair of the schedule decided
+    # exactly (what a full Filter + Score pass per pod computes); executed: the
+    # (pod, node) evaluations the kernels actually ran (class-list builds +
+    # commit-log re-evaluations + the device pods' evaluations), all ranks
+    evals_total = pods_total * args.nodes
+    executed_total = executed * args.steps * (world if world > 1 and not shard else 1)
+    local = shard and world > 1 and (int(ks["flags"]) & 1) != 0
     value = pods_total / elapsed
     batch = int(ks["round_pods"]) or eng.cfg.batch_pods or (16 if numa else 32)
     lag = int(ks["lag"]) or 1
@@ -345,7 +399,7 @@ def main():
     fused = ks["select_launches"] == 0
     phys = col_bytes if fused else col_bytes + pods_per_round * args.nodes * 2 + pods_per_round * args.nodes / 64 * 2
     scan_gbs = phys / (scan_us * 1e-6) / 1e9 if scan_us > 0 else None
-    traffic, traffic_src, traffic_kernel = pmc_traffic(args.workload)
+    traffic, traffic_src, traffic_kernel, pmc_kernels = pmc_traffic(args.workload)
     if traffic_src is not None and traffic_kernel != kn["eval"]:
         traffic, traffic_src = None, (f"none for {kn['eval']} (the committed PMC summary is of "
                                       f"{traffic_kernel or 'an unnamed kernel'})")
@@ -364,13 +418,23 @@ def main():
                     "classes": ncls, "avg_launch_ms": round(ks["scan_ms"] / max(ks["scan_launches"], 1), 3),
                     "timing": "HIP events around the persistent launch (the whole step)",
                     "builds": {"kernels": "k_scan over the class records + k_cls_collect",
-                               "timed_batches": int(ks["select_launches"]), "avg_batch_us": round(bld_us, 3)},
-                    "traffic": None}
+                               "timed_batches": int(ks["select_launches"]), "avg_batch_us": round(bld_us, 3),
+                               "traffic": {k: v["hbm_bytes_per_launch"] for k, v in pmc_kernels.items()
+                                           if "class build" in k or "k_cls_collect" in k} or None},
+                    "executed_evals_per_step": int(ks["executed_evals"]),
+                    "traffic": traffic, "traffic_source": traffic_src,
+                    "traffic_note": "HBM bytes of one k_cls_run launch (the whole stream's class workgroups) "
+                                    "from the PMC replay (scripts/pmc_summary.py), of the stream size it was "
+                                    "collected on"}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "pods/s",
-        "evals_per_s": round(evals_total / elapsed, 1),
+        "equivalent_evals_per_s": round(evals_total / elapsed, 1),
+        "executed_evals_per_s": round(executed_total / elapsed, 1),
+        "evals_note": "equivalent: every (pod, node) pair decided exactly; executed: the evaluations the kernels ran",
+        "stage_ms": round(stage_pods_ms + ks["plan_us"] / 1e3, 3),
+        "stage_split_ms": {"stage_pods": round(stage_pods_ms, 3), "cls_plan": round(ks["plan_us"] / 1e3, 3)},
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -396,11 +460,15 @@ def main():
                                 + (f" + DeviceShare (weight 1; 30% of the nodes with GPUs; "
                                    f"{int((ext['flags'] != 0).sum())} pods ({(ext['flags'] != 0).mean() * 100:.1f}%) "
                                    "requesting GPUs in the reference's four request forms, placed inside the pipelined "
-                                   "greedy by k_ext_worker)" if dsmix else "")),
+                                   "greedy by k_ext_pre / k_ext_final)" if dsmix else "")),
                    "nodes": args.nodes, "pods": args.pods, "batch_pods": batch, "pipeline_lag": lag,
-                   "parallelism": (f"replicas x{world} (every rank: its own cluster replica and stream)" if world > 1 and not shard
+                   "parallelism": (f"independent replicas x{world}, not one cluster (every rank: its own cluster "
+                                   "copy and stream)" if world > 1 and not shard
+                                   else f"node-shard x{world}: every rank on the full replica, no exchange (class "
+                                   "lists; the library's fallback, one cluster's schedule)" if local
                                    else f"node-shard x{world}" + (" (one-rank RCCL exchange path)" if args.one_rank_comm and world == 1 else ""))},
         "unschedulable": int((placements < 0).sum()),
+        "latency": lat,
         "roofline": {"bound": "latency", "kernel": kn["resolve"],
                      "limiter": "latency: one workgroup's sequential greedy (not bandwidth); priced against HBM peak",
                      "timing": "the timed step (persistent launch)" if persistent else "HIP events per launch",
@@ -423,7 +491,8 @@ def main():
         out["select"] = {"kernel": "(in k_eval_topk)" if fused else "k_select_split",
                          "avg_launch_us": round(ks["select_ms"] * 1e3 / max(ks["select_launches"], 1), 3)}
     if dsmix:
-        out["device_pods"] = {"pods": int((ext["flags"] != 0).sum()), "worker": "k_ext_worker<0>",
+        out["device_pods_traffic"] = {k: v["hbm_bytes_per_launch"] for k, v in pmc_kernels.items() if "k_ext_" in k} or None
+        out["device_pods"] = {"pods": int((ext["flags"] != 0).sum()), "kernels": "k_ext_pre<0> + k_ext_final<0>",
                               "route": "pipelined (resolve hand-off)" if kn["resolve"].startswith("kh::k_resolve")
                               else "sequential cycle"}
     if args.check:
@@ -509,10 +578,12 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     eng = PlacementEngine(prof, device=0, profile_kernels=False)
     eng.load_snapshot(table)
     eng.checkpoint()
+    t_st = time.perf_counter()
     if ext is None:
         eng.stage_pods(pods)
     else:
         eng.stage_pods_ext(pods, ext)
+    stage_pods_ms = (time.perf_counter() - t_st) * 1e3
 
     def step():
         eng.restore()
@@ -533,7 +604,7 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
     placements = eng.fetch_placements(len(pods))
     seq_s = ks["total_ms"] * 1e-3
     # a DeviceShare batch of device pods among plain ones runs on the pipelined
-    # greedy (k_resolve + k_ext_worker); everything else here in k_seq
+    # greedy (k_resolve + k_ext_pre / k_ext_final); everything else here in k_seq
     pipelined = kn["resolve"].startswith("kh::k_resolve")
     b = seq_bytes_per_eval(pods, ext, cfg, table.dev_slots)
     alg = float(b.sum()) * args.nodes
@@ -563,23 +634,26 @@ def run_sequential(args, torch, synth, prof, PlacementEngine):
         wl = (f"deviceshare: {args.nodes} nodes (30% with 4/8 GPUs, half of those 2 RDMA NICs) x "
               f"{args.pods} pods ({int(dev.mean() * 100)}% requesting GPUs), "
               "NodeResourcesFit + LoadAwareScheduling + DeviceShare (weight 1, LeastAllocated), "
-              + ("the pipelined greedy with the device pods placed exactly by k_ext_worker"
+              + ("the pipelined greedy with the device pods placed exactly by k_ext_pre / k_ext_final"
                  if pipelined else "the exact sequential cycle"))
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "pods/s",
-        "evals_per_s": round(args.pods * args.nodes * args.steps / elapsed, 1),
+        "equivalent_evals_per_s": round(args.pods * args.nodes * args.steps / elapsed, 1),
+        "executed_evals_per_s": round(float(ks["executed_evals"]) * args.steps / elapsed, 1),
+        "evals_note": "equivalent: every (pod, node) pair decided exactly; executed: the evaluations the kernels ran",
+        "stage_ms": round(stage_pods_ms, 3),
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeded splitmix64 cluster + pod stream)",
         "config": {"workload": wl, "nodes": args.nodes, "pods": args.pods,
-                   "parallelism": "single GPU" + (" (pipelined greedy + device-pod worker)" if pipelined
+                   "parallelism": "single GPU" + (" (pipelined greedy + device-pod kernels)" if pipelined
                                                   else " (cooperative grid)")},
         "unschedulable": int((placements < 0).sum()),
         "device_pods_placed": int(((placements >= 0) & dev).sum()),
         "spread_pods_placed": int(((placements >= 0) & (ext["pts_n"] > 0)).sum()),
         "affinity_pods_placed": int(((placements >= 0) & ((ext["ipa_aff"] | ext["ipa_anti"] | ext["ipa_score"]) != 0)).sum()),
         "roofline": {"bound": "latency", "kernel": kn["resolve"],
-                     "limiter": ("latency: the persistent resolve's sequential greedy, and per device pod one hand-off to k_ext_worker (write-back, evaluation of every node, last-arriver winner + device Reserve) and back (not bandwidth); priced against HBM peak" if pipelined else "latency: per pod one grid-wide hand-off (two for device pods) after the owner's commit and one evaluation chain (not bandwidth); priced against HBM peak" if not (spread or affinity) else "latency: per pod the spread pre-pass (hostname minimum), one or two grid-wide hand-offs (soft scoring adds the raw min / max) and one evaluation chain (not bandwidth); priced against HBM peak"),
+                     "limiter": ("latency: the persistent resolve's sequential greedy, and per device pod one hand-off to k_ext_final (write-back, re-evaluation of the nodes changed since the pre-evaluation, last-arriver winner + device Reserve) and back (not bandwidth); priced against HBM peak" if pipelined else "latency: per pod one grid-wide hand-off (two for device pods) after the owner's commit and one evaluation chain (not bandwidth); priced against HBM peak" if not (spread or affinity) else "latency: per pod the spread pre-pass (hostname minimum), one or two grid-wide hand-offs (soft scoring adds the raw min / max) and one evaluation chain (not bandwidth); priced against HBM peak"),
                      "timing": "HIP events around the place call of the last timed step",
                      "achieved": round(gbs, 2) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 5) if gbs else None, "traffic": None,

@@ -714,8 +714,13 @@ typedef struct koordhip_kernel_stats {
   int64_t rounds;    /* pipelined rounds */
   int64_t round_pods; /* pods per round (batch_pods, LDS-clamped) */
   int64_t lag;        /* pipeline depth: round r's lists see the state after round r - 1 - lag */
-  int64_t reserved[2];
+  int64_t executed_evals; /* (pod, node) evaluations actually run: class-list builds + incremental
+                            * re-evaluations + device pods' pre-evaluations and final re-evaluations
+                            * (evals is the equivalent work: every pair decided exactly) */
+  int32_t plan_us;        /* host time of the class-list plan of the call */
+  int32_t flags;          /* KOORDHIP_KSTAT_LOCAL: a sharded rank ran the full table (no exchange) */
 } koordhip_kernel_stats;
+#define KOORDHIP_KSTAT_LOCAL 1
 int koordhip_last_kernel_stats(koordhip_ctx *ctx, koordhip_kernel_stats *out);
 /* Turn the per-launch event timing on / off for later place calls (the
  * events cost a few microseconds per round: bench.py times its steps with it

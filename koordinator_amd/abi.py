@@ -93,7 +93,11 @@ class KoordhipKernelStats(C.Structure):
                 ("select_ms", C.c_double), ("select_launches", C.c_int64),
                 ("resolve_ms", C.c_double), ("resolve_launches", C.c_int64),
                 ("total_ms", C.c_double), ("evals", C.c_int64), ("pods", C.c_int64), ("rounds", C.c_int64),
-                ("round_pods", C.c_int64), ("lag", C.c_int64), ("reserved", C.c_int64 * 2)]
+                ("round_pods", C.c_int64), ("lag", C.c_int64), ("executed_evals", C.c_int64),
+                ("plan_us", C.c_int32), ("flags", C.c_int32)]
+
+
+KSTAT_LOCAL = 1
 
 
 class KoordhipConfig(C.Structure):

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -200,20 +201,21 @@ struct koordhip_ctx {
   bool staged_dsr = false;          // the staged device pods carry kh::KH_POD_DEVSHARE (reservations were loaded)
   bool staged_reserve = false;     // the staged batch holds a reserve pod (KOORDHIP_POD_RESERVE): the sequential cycle
   bool staged_ext = false;         // the staged batch's koordhip_pod_ext records carry requests / constraints
-  // device pods inside the pipelined greedy (k_ext_worker, seq.hip): the
+  // device pods inside the pipelined greedy (k_ext_pre / k_ext_final, seq.hip): the
   // staged pods whose records carry content, when that content is device /
   // extended-scalar requests only (no spread constraint or count, no affinity
   // entry); their DevPods carry KH_POD_EXT
   bool staged_ext_dev = false;
-  std::vector<int32_t> ext_idx, ext_needc;
+  std::vector<int32_t> ext_idx;
   int32_t *d_ext_idx = nullptr;
   int32_t ext_idx_cap = 0;
-  void *d_ext_scr = nullptr;        // k_ext_worker's table and per-pod chunk counters
+  void *d_ext_scr = nullptr;        // the device-pod launches' table, arrival counters, pre-evaluation ring
   size_t ext_scr_cap = 0;
-  hipStream_t xstream = nullptr;    // its stream (a dedicated queue: the worker spins on the resolve's flag;
-                                    // every fourth CU)
-  hipEvent_t ev_ext = nullptr;
+  hipStream_t xstream = nullptr;    // their streams (pooled: transient launches, one-workgroup waits):
+  hipStream_t xstream2 = nullptr;   // the pre-evaluations, the finals
+  hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr;
   bool last_ext_pipe = false;       // the last place call placed device pods inside the pipeline
+  bool last_local = false;          // ... ran a node-sharded rank on the full table (class lists, no exchange)
   // class-incremental lists (cls.hip): the staged pods' classes (byte-identical
   // device records), the class buffers and the plan of the staged batch
   std::vector<int32_t> pod_cls;    // class of each staged pod
@@ -248,6 +250,11 @@ struct koordhip_ctx {
   int64_t ipa_pods_bound = 0; // pods the snapshot's entries can count (for the raw Score's int32 bound)
   int32_t seq_grid = 0;
   int64_t last_launches = 0, last_evals = 0;
+  // executed evaluations of the last call: the host-known part (builds, device
+  // pods' pre-evaluations) plus the device counters read by kernel_stats
+  int64_t last_exec = 0, last_ext_exec = 0;
+  const uint32_t *last_evc = nullptr, *last_reev = nullptr;
+  int32_t last_plan_us = 0;  // the class-list plan of the staged batch (0: none made)
 };
 
 namespace {
@@ -1281,11 +1288,13 @@ int koordhip_destroy(koordhip_ctx *c) {
     (void)hipStreamDestroy(c->stream2);
   }
   if (c->ev_eval2) (void)hipEventDestroy(c->ev_eval2);
-  if (c->xstream) {
-    (void)hipStreamSynchronize(c->xstream);
-    (void)hipStreamDestroy(c->xstream);
-  }
+  for (hipStream_t xs : {c->xstream, c->xstream2})
+    if (xs) {
+      (void)hipStreamSynchronize(xs);
+      (void)hipStreamDestroy(xs);
+    }
   if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
+  if (c->ev_ext2) (void)hipEventDestroy(c->ev_ext2);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
@@ -2006,6 +2015,7 @@ static int stage_classes(koordhip_ctx *c, const std::vector<kh::DevPod> &hp) {
   c->pod_cls.assign(n, 0);
   c->cls_rep.clear();
   c->plan_ok = false;
+  c->last_plan_us = 0;
   std::unordered_map<std::array<uint64_t, 12>, int32_t, PodBytesHash> m;
   for (int32_t j = 0; j < n; j++) {
     std::array<uint64_t, 12> k;
@@ -2448,6 +2458,7 @@ int group_agree(koordhip_ctx *c) {
 }
 
 int place_staged_impl(koordhip_ctx *c);
+int pmc_replay(koordhip_ctx *c);
 
 // every CU of the device as a hipExtStreamCreateWithCUMask mask
 std::vector<uint32_t> full_cu_mask(const koordhip_ctx *c) {
@@ -2464,8 +2475,9 @@ int koordhip_place_staged(koordhip_ctx *c) {
   if (!c) return fail(KOORDHIP_EINVAL, "ctx is NULL");
   if (c->n_staged > 0 && c->staged_dsr != devshare_resv_on(c))
     return fail(KOORDHIP_ESTATE, "the pods were staged under a snapshot with(out) reservations; stage them again");
-  const int e = place_staged_impl(c);
+  int e = place_staged_impl(c);
   if (e && c->group) c->group->abort();
+  if (!e && std::getenv("KOORDHIP_PMC_REPLAY") && std::getenv("KOORDHIP_SERIAL")) e = pmc_replay(c);
   return e;
 }
 
@@ -2518,7 +2530,7 @@ int seq_place(koordhip_ctx *c) {
   c->last_evals = (int64_t)np * c->n;
   c->last_launches = 1;
   c->ev_used = 0;
-  c->eval_kernel = kh::seq_kernel_name(c->dc);
+  c->eval_kernel = kh::seq_kernel_name(c->dc, c->d);
   c->resolve_kernel = c->eval_kernel;
   c->pipe_check = true;
   return 0;
@@ -2543,6 +2555,7 @@ constexpr int32_t kClsLead = 12;
 
 static int cls_plan(koordhip_ctx *c, int32_t P, int32_t lag, int32_t K) {
   if (c->plan_ok && c->plan_P == P && c->plan_lag == lag) return 0;
+  const auto tp0 = std::chrono::steady_clock::now();
   const int32_t total = c->n_staged, rounds = (total + P - 1) / P, nc = (int32_t)c->cls_rep.size();
   const int32_t amax = (kh::kClsTarget - K) / P, horizon = amax / 2;
   c->plan_ok = false;
@@ -2614,7 +2627,7 @@ static int cls_plan(koordhip_ctx *c, int32_t P, int32_t lag, int32_t K) {
   c->plan_coff[nc] = (int32_t)c->plan_csched.size();
   // one device array for the schedule tables, the build tables and the sync words
   const size_t sz[8] = {c->plan_coff.size(), c->plan_csched.size(), c->plan_csm.size(), c->plan_ent.size(),
-                        c->plan_bm.size(), c->plan_bw.size(), (size_t)nc, (((size_t)nc + 15) & ~(size_t)15) + kh::kClsRoundRing + 1 + (size_t)nc};  // sw | rcnt ring, started, states
+                        c->plan_bm.size(), c->plan_bw.size(), (size_t)nc, (((size_t)nc + 15) & ~(size_t)15) + kh::kClsRoundRing + 1 + (size_t)nc + 1};  // sw | rcnt ring, started, states, evc
   size_t tot = 0;
   for (int q = 0; q < 8; q++) {
     c->plan_off[q] = tot;
@@ -2646,6 +2659,8 @@ static int cls_plan(koordhip_ctx *c, int32_t P, int32_t lag, int32_t K) {
   c->plan_ok = true;
   c->plan_P = P;
   c->plan_lag = lag;
+  // (kernel stats: the host time of the staged batch's plan, made by its first place call)
+  c->last_plan_us = (int32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - tp0).count();
   return 0;
 }
 
@@ -2674,6 +2689,7 @@ static kh::ClsSync cls_sync(koordhip_ctx *c, kh::PipeSync *sync) {
   cs.done = c->d_plan + c->plan_off[6];
   cs.sw = c->d_plan + c->plan_off[7];
   cs.rcnt = cs.sw + ((c->cls_rep.size() + 15) & ~(size_t)15);
+  cs.evc = reinterpret_cast<uint32_t *>(cs.rcnt + kh::kClsRoundRing + 1 + c->cls_rep.size());
   return cs;
 }
 
@@ -2698,6 +2714,102 @@ static int cls_build(koordhip_ctx *c, const koordhip_ctx::ClsBuild &b, kh::PipeS
                                    b.tb, c->d_cls_buf, c->d_cls_meta, cs, c->d_dbg ? c->d_dbg + 64 : nullptr, bs));
     if (int e = timed_end(c, tm, bs)) return e;
   }
+  return 0;
+}
+
+// KOORDHIP_PMC_REPLAY (with KOORDHIP_SERIAL; for rocprofv3 --pmc, which
+// serialises every dispatch, so the pipeline's persistent kernels cannot run
+// beside each other): after a completed call, the class lists' builds
+// (k_scan + k_cls_collect) and class workgroups (k_cls_run), and the device
+// pods' pre-evaluations and finals, launched again one after another on the
+// checkpointed snapshot state over the call's own commit log, with every wait
+// satisfied in advance -- the pipeline's launches and grids, for their HBM
+// counters (the state is the snapshot's, not each round's: the evaluations
+// read the same columns, the class buffers change less).  The call's
+// placements are kept; the node state is the checkpoint's plus the replayed
+// device commits (the caller restores).  Diagnostics only.
+int pmc_replay(koordhip_ctx *c) {
+  if (c->last_seq && !(c->seq_profile && c->seq_ext_only && c->staged_ext_dev)) return 0;
+  if (!c->d_mod || c->n_staged <= 0) return 0;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int e = koordhip_restore(c)) return e;
+  const int32_t total = c->n_staged;
+  int32_t P = c->batch;
+  int32_t lag = ((!c->side || c->resv) && !std::getenv("KOORDHIP_LAG1")) ? 2 : 1;
+  if (lag == 2 && (3 * P > kh::kResolveMaxK || 2 * P > kMaxBatch)) lag = 1;
+  const int nm = kh::side_mode(c->dc);
+  while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, nm, lag) > 157 * 1024) P--;
+  const int32_t K = (lag + 1) * P, rounds = (total + P - 1) / P;
+  const bool cls = !c->last_seq && !c->cls_rep.empty() && c->nbins <= 32768 && c->world == 1 &&
+                   (int64_t)c->cls_rep.size() <= c->n_cu / 2 && kh::cls_run_lds(c->n, c->monotone) <= 150 * 1024 &&
+                   (kh::kClsTarget - K) / P >= 4 * kClsLead + 2;
+  const bool ext = c->seq_profile && c->seq_ext_only && c->staged_ext && c->staged_ext_dev && c->podx_staged &&
+                   !c->staged_reserve && !c->seq_snap && !c->d.dv.rslot && nm == 0 && c->world == 1 &&
+                   !c->ext_idx.empty();
+  int32_t *saved = nullptr;
+  HIP_TRY(hipMalloc(&saved, (size_t)total * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(saved, c->d_out, (size_t)total * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+  kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
+  HIP_TRY(hipMemsetAsync(sync, 0, kh::kPipeSyncBytes, c->stream));
+  const int32_t big = 0x3fffffff;
+  const int32_t head[3] = {big, big, rounds};  // sel[0], sel[1], res_round: every round published and resolved
+  HIP_TRY(hipMemcpyAsync(sync, head, sizeof(head), hipMemcpyHostToDevice, c->stream));
+  int32_t nscan = 0;
+  if (cls) {
+    if (int e = cls_plan(c, P, lag, K)) return e;
+    if (int e = cls_alloc(c, c->n)) return e;
+    const kh::ClsSync cs = cls_sync(c, sync);
+    const size_t nc = c->cls_rep.size();
+    HIP_TRY(hipMemsetAsync(c->d_plan + c->plan_off[6], 0,
+                           (2 * ((nc + 15) & ~(size_t)15) + kh::kClsRoundRing + 1 + nc + 1) * sizeof(int32_t), c->stream));
+    // every build's slot free and every build published before anything waits
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(cs.done), big, nc, c->stream));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(cs.sw), big, nc, c->stream));
+    for (const koordhip_ctx::ClsBuild &b : c->plan_builds) {
+      if (int e = cls_build(c, b, sync, c->stream, false)) return e;
+      nscan += (b.ne + kh::kClsBuildRows - 1) / kh::kClsBuildRows;
+    }
+    HIP_TRY(kh::launch_cls_run(c->dc, c->d, c->d_cls_pod, (int32_t)nc, c->d_plan + c->plan_off[0],
+                               c->d_plan + c->plan_off[1], c->d_plan + c->plan_off[2], c->d_pod_cls, c->d_out, lag, P,
+                               total, c->d_cls_buf, c->d_cls_meta, K, c->monotone, c->d_lists,
+                               (int64_t)((size_t)kMaxBatch * 2 * kMaxBatch), cs, nullptr, c->stream));
+  }
+  const int32_t ne = (int32_t)c->ext_idx.size();
+  if (ext) {
+    if (!c->d_devout && c->pods_cap > 0)
+      HIP_TRY(hipMalloc(&c->d_devout, (size_t)c->pods_cap * KOORDHIP_DEV_TYPES * sizeof(uint32_t)));
+    const size_t xb = kh::ext_scratch_bytes(ne, c->n);
+    if (xb > c->ext_scr_cap) {
+      if (c->d_ext_scr) HIP_TRY(hipFree(c->d_ext_scr));
+      c->d_ext_scr = nullptr;
+      HIP_TRY(hipMalloc(&c->d_ext_scr, xb));
+      c->ext_scr_cap = xb;
+    }
+    const char *ld = std::getenv("KOORDHIP_EXT_LEAD");
+    const int32_t lead = std::max(lag, ld ? std::atoi(ld) : lag);
+    HIP_TRY(kh::launch_ext_begin(c->d, ne, c->d_ext_scr, c->stream));
+    for (int32_t e = 0; e < ne; e++) {
+      const int32_t gp = c->ext_idx[e], u = gp / P;
+      HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(reinterpret_cast<int32_t *>(sync) +
+                                                                  kh::kPipeSyncExtReqWord),
+                                gp + 1, 1, c->stream));
+      HIP_TRY(kh::launch_ext_pre(c->dc, c->d, c->d_pods, c->d_podx, e, gp, u - lead, e, ne, c->d_ext_scr, sync,
+                                 c->stream));
+      HIP_TRY(kh::launch_ext_final(c->dc, c->d, c->d_pods, c->d_podx, e, gp, std::max(0, u - lead) * P,
+                                   std::max(0, u - lag) * P, ne, c->d_ext_scr, c->d_out, c->d_devout, sync, nullptr,
+                                   c->stream));
+    }
+  }
+  HIP_TRY(hipMemcpyAsync(c->d_out, saved, (size_t)total * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipFree(saved));
+  int32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, reinterpret_cast<int32_t *>(sync) + kh::kPipeSyncErrWord, sizeof(err), hipMemcpyDeviceToHost));
+  std::fprintf(stderr, "[koordhip pmc replay] P %d lag %d: class lists %s (%zu builds, %d k_scan + k_cls_collect "
+               "launches, 1 k_cls_run of %zu workgroups), device pods %d (k_ext_pre + k_ext_final each)%s\n", P, lag,
+               cls ? "replayed" : "not used", cls ? c->plan_builds.size() : (size_t)0, nscan,
+               cls ? c->cls_rep.size() : (size_t)0, ext ? ne : 0, err ? ": ERROR (a replayed kernel gave up)" : "");
+  if (err) return fail(KOORDHIP_EDEVICE, "PMC replay: a replayed kernel reported an error");
   return 0;
 }
 
@@ -2729,7 +2841,7 @@ int place_staged_impl(koordhip_ctx *c) {
   // Device pods among pods without ext content (DeviceShare as the only
   // coupling plugin the records use, the plain plugin build, one GPU, the
   // persistent pipeline): placed inside the pipelined greedy -- the resolve
-  // hands each one the exact state and k_ext_worker runs its reference cycle
+  // hands each one the exact state and k_ext_pre / k_ext_final run its reference cycle
   // (seq.hip) -- instead of the whole batch in the sequential cycle.
   // KOORDHIP_EXT_SEQ: the sequential cycle for such batches too (A/B).
   const bool ext_pipe = c->seq_profile && c->seq_ext_only && c->staged_ext && c->staged_ext_dev && c->podx_staged &&
@@ -2742,7 +2854,7 @@ int place_staged_impl(koordhip_ctx *c) {
   if (ext_pipe) {  // (allocations before the persistent launches: one later could wait behind them)
     if (!c->d_devout && c->pods_cap > 0)
       HIP_TRY(hipMalloc(&c->d_devout, (size_t)c->pods_cap * KOORDHIP_DEV_TYPES * sizeof(uint32_t)));
-    const size_t xb = kh::ext_worker_scratch_bytes((int32_t)c->ext_idx.size(), c->n);
+    const size_t xb = kh::ext_scratch_bytes((int32_t)c->ext_idx.size(), c->n);
     if (xb > c->ext_scr_cap) {
       if (c->d_ext_scr) HIP_TRY(hipFree(c->d_ext_scr));
       c->d_ext_scr = nullptr;
@@ -2750,23 +2862,16 @@ int place_staged_impl(koordhip_ctx *c) {
       c->ext_scr_cap = xb;
     }
     if (!c->xstream) {
-      // The worker's stream: a pooled HIP stream by default -- a fourth
-      // dedicated hardware queue beside the context's three measured
-      // time-sliced (steps 5-10x slower, watchdog stalls) -- else
-      // (KOORDHIP_EXT_DEDICATED, A/B) a dedicated queue on every fourth CU.
-      // The pipeline's other spinning kernels sit in dedicated queues, so the
-      // pooled queue it may share holds nothing it waits for.
-      if (std::getenv("KOORDHIP_EXT_DEDICATED")) {
-        std::vector<uint32_t> wm(full_cu_mask(c).size(), 0u);
-        for (int32_t i = 3; i < c->n_cu; i += 4) wm[i >> 5] |= 1u << (i & 31);
-        HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)wm.size(), wm.data()));
-      } else {
-        HIP_TRY(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-      }
+      // The device pods' streams: transient launches only (a one-workgroup
+      // wait launch before each), so they hold no workgroup that waits while
+      // others need its CU; pooled HIP streams (no more dedicated queues)
+      HIP_TRY(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+      HIP_TRY(hipStreamCreateWithFlags(&c->xstream2, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming));
     }
   }
-  // the pipelined greedy allocates no device but the device pods' (k_ext_worker):
+  // the pipelined greedy allocates no device but the device pods' (k_ext_final):
   // clear the slots a previous sequential batch left (koordhip_fetch_devices
   // reads this buffer)
   if (c->d_devout && c->n_staged > 0)
@@ -2788,7 +2893,18 @@ int place_staged_impl(koordhip_ctx *c) {
   // counts finished lists per round parity).
   // exchanged: node-sharded, or a one-rank RCCL communicator (the exchange
   // path end to end on one GPU: all-gather, merge, per-round signal)
-  const bool exch = c->world > 1 || c->comm != nullptr;
+  // A node-sharded rank (world > 1) whose batch the class-incremental lists
+  // cover evaluates the full table itself: every rank holds the full replica
+  // and resolves every pod anyway, and sharding divides only the evaluation,
+  // which the class lists already took off the critical path -- through the
+  // per-round all-gather world > 1 would run slower than one GPU (DESIGN.md
+  // section 6).  KOORDHIP_SHARD_FORCE keeps the exchange (A/B).
+  const bool cls_fit = !c->cls_rep.empty() && c->nbins <= 32768 && !std::getenv("KOORDHIP_CLS_OFF") && !c->cu_reserve &&
+                       (int64_t)c->cls_rep.size() <= c->n_cu / 2 && kh::cls_run_lds(c->n, c->monotone) <= 150 * 1024;
+  const bool local = c->world > 1 && !c->group && persistent && c->sel_split && wait_kernel && cls_fit &&
+                     !std::getenv("KOORDHIP_SHARD_FORCE");
+  c->last_local = local;
+  const bool exch = (c->world > 1 || c->comm != nullptr) && !local;
   // (node-sharded: the rounds of the second stream exchange on comm2)
   const bool two = persistent && (!exch || c->comm2) && c->sel_split && wait_kernel &&
                    !std::getenv("KOORDHIP_ONE_EVAL_STREAM");
@@ -2873,10 +2989,13 @@ int place_staged_impl(koordhip_ctx *c) {
     c->ev_kind.resize(c->ev.size() / 2);
   }
   int32_t lo = 0, hi = c->n;
-  shard(c, &lo, &hi);
+  if (!local) shard(c, &lo, &hi);
   c->ev_used = 0;
   c->last_launches = 0;
   c->last_evals = 0;
+  c->last_exec = -1;  // -1: equal to last_evals (every pair evaluated once)
+  c->last_ext_exec = 0;
+  c->last_evc = c->last_reev = nullptr;
   if (std::getenv("KOORDHIP_STAMPS")) {
     if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 96 * sizeof(uint64_t)));
     HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 96 * sizeof(uint64_t), c->stream));
@@ -2917,7 +3036,7 @@ int place_staged_impl(koordhip_ctx *c) {
     if (int e = cls_alloc(c, c->n)) return e;
     // the build / switch counters start every call at zero; the build stream sees them
     HIP_TRY(hipMemsetAsync(c->d_plan + c->plan_off[6], 0,
-                           (2 * ((c->cls_rep.size() + 15) & ~(size_t)15) + kh::kClsRoundRing + 1 + c->cls_rep.size()) *
+                           (2 * ((c->cls_rep.size() + 15) & ~(size_t)15) + kh::kClsRoundRing + 1 + c->cls_rep.size() + 1) *
                                sizeof(int32_t), c->stream));
     HIP_TRY(hipEventRecord(c->ev_start, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
@@ -2966,36 +3085,58 @@ int place_staged_impl(koordhip_ctx *c) {
     c->eval_kernel = kh::cls_run_kernel_name(c->dc);
     c->last_launches = 1;
     c->last_evals = (int64_t)total * c->n;  // every (pod, node) pair decided exactly (the lists' equivalent work)
+    // executed: each build evaluates its classes over every node, the class
+    // workgroups count their incremental re-evaluations on the device
+    c->last_exec = 0;
+    for (const koordhip_ctx::ClsBuild &b : c->plan_builds) c->last_exec += (int64_t)b.ne * c->n;
+    c->last_evc = cls_sync(c, sync).evc;
   }
   if (ext_pipe && rounds > 0) {
-    // the device pods' worker: one persistent launch on its own stream, after
-    // the call's PipeSync / device-slot resets (ev_start), and after the class
-    // lists' persistent launch (submitted first, its workgroups are placed
-    // first)
+    // The device pods: per pod e (round u) a pre-evaluation once the resolve
+    // finished round u - lead (and the device commits of the device pods of
+    // the rounds before that are published), and the exact placement at its
+    // hand-off -- transient launches, the pre-evaluations on xstream, the
+    // finals (with the device Reserve) on xstream2, each behind a
+    // one-workgroup wait on device flags, after the call's PipeSync /
+    // device-slot resets (ev_start).  Two streams let pre-evaluation e + 1 run
+    // while final e waits for its hand-off.  They are submitted in an order
+    // whose every wait the launches before it satisfy, so they cannot deadlock
+    // even where the two streams share one hardware queue: final(e) waits for
+    // the hand-off of e (round u: the lists of rounds <= u and the finals of
+    // the device pods before e, all earlier) and pre(e); pre(e) waits for
+    // rounds < u - lead (the finals of the device pods of those rounds come
+    // before it: a final of round u' precedes a pre whose wait round exceeds
+    // u') and follows final(e - RING), whose ring buffer it reuses.  lead: the
+    // rounds between lag and lead add their commits, from the commit log, to
+    // the final's re-evaluated set.
     HIP_TRY(hipStreamWaitEvent(c->xstream, c->ev_start, 0));
-    // needc[e]: the device pods of the rounds before round(e) - lag, whose
-    // device commits device pod e's pre-evaluation must see (later ones' nodes
-    // are in the resolve's X set at e's hand-off)
-    // lead: the pre-evaluation runs on the state after round(e) - lead - 1, i.e.
-    // `lead` rounds before the pod's round may start (the rounds between lag and
-    // lead add their commits, from the commit log, to the final phase's X).
-    // lag by default: config4dsmix measured 846k / 787k / 750k pods/s at lead 2 /
-    // 5 / 8 (r05q) -- the longer X re-evaluates more nodes at the hand-off
+    HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_start, 0));
     const char *ld = std::getenv("KOORDHIP_EXT_LEAD");
     const int32_t lead = std::max(lag, ld ? std::atoi(ld) : lag);
-    const int32_t ne = (int32_t)c->ext_idx.size();
-    c->ext_needc.assign(ne, 0);
-    for (int32_t e = 0, q = 0; e < ne; e++) {
-      const int32_t ue = c->ext_idx[e] / P;
-      while (q < e && c->ext_idx[q] / P < ue - lead) q++;
-      c->ext_needc[e] = q;
-    }
-    HIP_TRY(hipMemcpyAsync(c->d_ext_idx + ne, c->ext_needc.data(), (size_t)ne * sizeof(int32_t), hipMemcpyHostToDevice,
-                           c->xstream));
-    HIP_TRY(kh::launch_ext_worker(c->dc, c->d, c->d_pods, c->d_podx, c->d_ext_idx, c->d_ext_idx + ne, ne, P, lag, lead,
-                                  c->n_cu, c->d_ext_scr, c->d_out, c->d_devout, sync,
-                                  c->d_dbg, c->xstream));
+    const int32_t ne = (int32_t)c->ext_idx.size(), R = kh::ext_ring();
+    HIP_TRY(kh::launch_ext_begin(c->d, ne, c->d_ext_scr, c->xstream));
+    c->last_ext_exec = (int64_t)ne * c->n;  // the pre-evaluations; the finals' re-evaluations on the device
+    c->last_reev = kh::ext_reevals(c->d_ext_scr, ne, c->n);
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
+    HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_ext, 0));  // (the zeroed flags)
+    auto u_of = [&](int32_t e) { return c->ext_idx[e] / P; };
+    for (int32_t ip = 0, ifn = 0, needc = 0; ifn < ne;) {
+      const bool can_pre = ip < ne && ifn >= ip - R + 1;
+      if (can_pre && (ip <= ifn || u_of(ip) - lead < u_of(ifn))) {
+        while (needc < ip && u_of(needc) < u_of(ip) - lead) needc++;  // device pods of the rounds < u - lead
+        HIP_TRY(kh::launch_ext_pre(c->dc, c->d, c->d_pods, c->d_podx, ip, c->ext_idx[ip], u_of(ip) - lead, needc, ne,
+                                   c->d_ext_scr, sync, c->xstream));
+        ip++;
+      } else {
+        const int32_t u = u_of(ifn);
+        HIP_TRY(kh::launch_ext_final(c->dc, c->d, c->d_pods, c->d_podx, ifn, c->ext_idx[ifn], std::max(0, u - lead) * P,
+                                     std::max(0, u - lag) * P, ne, c->d_ext_scr, c->d_out, c->d_devout, sync, c->d_dbg,
+                                     c->xstream2));
+        ifn++;
+      }
+    }
+    HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
+    HIP_TRY(hipEventRecord(c->ev_ext2, c->xstream2));
   }
   for (int32_t r = 0; r < rounds && !cls; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
@@ -3040,7 +3181,10 @@ int place_staged_impl(koordhip_ctx *c) {
     HIP_TRY(hipEventRecord(c->ev_eval2, c->stream2));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_eval2, 0));
   }
-  if (ext_pipe && rounds > 0) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext, 0));
+  if (ext_pipe && rounds > 0) {
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext, 0));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext2, 0));
+  }
   if (!serial) {
     HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res[0], 0));
@@ -3110,19 +3254,14 @@ int place_staged_impl(koordhip_ctx *c) {
                    (unsigned long long)q[2], (unsigned long long)q[3]);
     }
     if (ext_pipe) {
-      uint64_t q[8], q8[2] = {0, 0}, q94[2] = {0, 0};
+      uint64_t q[8];
       HIP_TRY(hipMemcpy(q, c->d_dbg + 80, sizeof(q), hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(q8, c->d_dbg + 88, sizeof(q8), hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(q94, c->d_dbg + 94, sizeof(q94), hipMemcpyDeviceToHost));
       const double np = (double)std::max<uint64_t>(q[6], 1);
-      std::fprintf(stderr, "[koordhip stamps] device pods (k_ext_worker): %llu, resolve cycles from the hand-off to the "
-                   "answer %llu (%.0f per pod) | worker per pod: workgroup 0 waiting %.0f  evaluating %.0f  merge + "
-                   "arrival %.0f (chunks %.2f) | pre-evaluation workgroup: waiting %.0f  evaluating %.0f | last "
-                   "workgroup reduce %.0f  publish %.0f  device commit (after the hand-off) %.0f | after the "
-                   "hand-off, workgroup 0 waits for the previous device commit %.0f, the pre-evaluation %.0f\n",
+      std::fprintf(stderr, "[koordhip stamps] device pods (k_ext_pre / k_ext_final): %llu, resolve cycles from the "
+                   "hand-off to the answer %llu (%.0f per pod) | final launch per pod: workgroup 0 evaluate + fold "
+                   "%.0f | last workgroup: decide + publish %.0f  device commit %.0f\n",
                    (unsigned long long)h[31], (unsigned long long)h[30], h[31] ? (double)h[30] / h[31] : 0.0,
-                   q[0] / np, q[1] / np, q[2] / np, q[7] / np, (double)q8[1] / np, (double)q8[0] / np, q[3] / np,
-                   q[5] / np, q[4] / np, (double)q94[0] / np, (double)q94[1] / np);
+                   q[0] / np, q[3] / np, q[4] / np);
     }
     std::fprintf(stderr, "[koordhip stamps] general commit split: row source %llu  Reserve delta %llu  voiding + "
                  "outputs %llu cycles | winners already in M %llu\n",
@@ -3138,7 +3277,7 @@ int place_staged_impl(koordhip_ctx *c) {
 static const char *pipe_msg(int32_t err) {
   switch (err) {
     case 2: return "class lists underflowed (fewer than k keys above a build's boundary): placements are incomplete";
-    case 4: return "a device pod's DeviceShare Reserve failed where its Filter passed (k_ext_worker): placements are "
+    case 4: return "a device pod's DeviceShare Reserve failed where its Filter passed (k_ext_final): placements are "
                    "incomplete";
     default: return "round pipeline stalled (watchdog): placements are incomplete";
   }
@@ -3166,15 +3305,10 @@ int pipe_status(koordhip_ctx *c) {
   if (err) {
     c->pipe_err = true;
     c->pipe_errc = err;
-    if (c->last_ext_pipe && c->d_ext_scr) {  // where the pipeline stood (device pods inside it)
-      int32_t sy[96], xd = 0;
+    if (c->last_ext_pipe || (c->d_plan && !c->cls_rep.empty())) {  // where the pipeline stood
+      int32_t sy[96], cstarted = -1;
       HIP_TRY(hipMemcpy(sy, sync, sizeof(sy), hipMemcpyDeviceToHost));
       const int32_t sw[6] = {sy[0], sy[1], sy[2], sy[3], sy[kh::kPipeSyncExtReqWord], sy[kh::kPipeSyncExtDoneWord]};
-      HIP_TRY(hipMemcpy(&xd, static_cast<char *>(c->d_ext_scr) + kh::ext_worker_diag_offset((int32_t)c->ext_idx.size()),
-                        sizeof(xd), hipMemcpyDeviceToHost));
-      int32_t ws = 0, cstarted = -1;
-      HIP_TRY(hipMemcpy(&ws, static_cast<char *>(c->d_ext_scr) + kh::ext_worker_diag_offset((int32_t)c->ext_idx.size()) +
-                                 3 * sizeof(int32_t), sizeof(ws), hipMemcpyDeviceToHost));
       if (c->d_plan && !c->cls_rep.empty()) {
         const kh::ClsSync cs = cls_sync(c, sync);
         HIP_TRY(hipMemcpy(&cstarted, cs.rcnt + kh::kClsRoundRing, sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -3187,10 +3321,8 @@ int pipe_status(koordhip_ctx *c) {
         for (size_t q = 0; q < st.size(); q++) std::fprintf(stderr, " %zu:%d/%d/%d", q, st[q], dn[q], swv[q]);
         std::fprintf(stderr, "\n");
       }
-      std::fprintf(stderr, "[koordhip] pipeline error %d: sel %d/%d res_round %d ext_req %d ext_done %d | device-pod "
-                   "worker failed at device pod %d phase %d; worker workgroups started %d, class-list workgroups "
-                   "started %d of %zu\n", err, sw[0], sw[1], sw[2], sw[4], sw[5], xd >> 4, xd & 15, ws, cstarted,
-                   c->cls_rep.size());
+      std::fprintf(stderr, "[koordhip] pipeline error %d: sel %d/%d res_round %d ext_req %d ext_done %d | class-list "
+                   "workgroups started %d of %zu\n", err, sw[0], sw[1], sw[2], sw[4], sw[5], cstarted, c->cls_rep.size());
     }
     return fail(KOORDHIP_EDEVICE, pipe_msg(err));
   }
@@ -3467,6 +3599,16 @@ int koordhip_last_kernel_stats(koordhip_ctx *c, koordhip_kernel_stats *out) {
   out->rounds = (c->n_staged + c->last_P - 1) / std::max(c->last_P, 1);
   out->round_pods = c->last_P;
   out->lag = c->last_lag;
+  int64_t ex = (c->last_exec < 0 ? c->last_evals : c->last_exec) + c->last_ext_exec;
+  for (const uint32_t *p : {c->last_evc, c->last_reev})
+    if (p) {
+      uint32_t v = 0;
+      HIP_TRY(hipMemcpy(&v, p, sizeof(v), hipMemcpyDeviceToHost));
+      ex += v;
+    }
+  out->executed_evals = ex;
+  out->plan_us = c->last_plan_us;
+  out->flags = c->last_local ? KOORDHIP_KSTAT_LOCAL : 0;
   return 0;
 }
 

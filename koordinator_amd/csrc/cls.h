@@ -35,6 +35,7 @@ struct ClsSync {
   int32_t *done;
   int32_t *sw;
   int32_t *rcnt;  // [kClsRoundRing]: the listed pods of round u at u % kClsRoundRing (zero between rounds)
+  uint32_t *evc;  // (pod class, node) evaluations the lists re-ran from the commit log (per call; bench accounting)
 };
 constexpr int32_t kClsRoundRing = 16;  // rounds in flight between the class lists and the resolve (<= lag + 2)
 

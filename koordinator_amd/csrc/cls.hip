@@ -386,6 +386,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
   }
   if (t == 0) atomicAdd(cs.rcnt + kClsRoundRing, 1);  // workgroups started (diagnostics: api.hip pipe_status)
   int32_t nsw = 0;  // switches to a new build so far
+  uint32_t nev = 0;  // evaluations from the commit log (counted into cs.evc at the end)
   for (int32_t ix = coff[cl]; ix < coff[cl + 1]; ix++) {
     const int32_t ent = csched[ix];
     const int32_t u = ent & 0x7FFFFFFF;
@@ -496,6 +497,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
           bk[j] = eval_key(key_node(bk[j]));
           chg[j] = 1;
         }
+        nev += (uint32_t)ntouch * (t == 0);
         moved = ntouch > 0 ? 1 : 0;
       }
       // ---- (non-monotone) committed nodes outside the buffer whose key rose above the boundary
@@ -506,6 +508,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
             const int32_t y = w * 32 + __builtin_ctz(bits);
             bits &= bits - 1u;
             const uint64_t key = eval_key(y);
+            nev++;
             if (key > bnd) {
               const int32_t pos = cnt + atomicAdd(&h.ins, 1);
               moved = 1;
@@ -643,6 +646,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_cls_run(DevCfg c, DevNodes d, c
     st.lap(6);
     if (dbg && cl == 0 && t == 0) atomicAdd((unsigned long long *)&dbg[7], 1ull);
   }
+  if (nev) atomicAdd(cs.evc, nev);
 }
 
 hipError_t launch_cls_collect(const uint16_t *S, int64_t s_stride, int32_t n, const int32_t *ent, const int32_t *bm,

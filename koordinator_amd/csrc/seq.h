@@ -50,25 +50,31 @@ hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pod
 hipError_t launch_commit_ext(const DevCfg &c, const DevNodes &d, const DevPod *pod, const DevPodX *px, int32_t node,
                              int32_t sign, int32_t rs, uint64_t *cpus, uint32_t *dev, int32_t *rc, const PtsArgs &pts,
                              const IpaArgs &ipa, hipStream_t s);
-// Device pods inside the pipelined greedy (plain build, seq_mode 0): ONE
-// persistent launch per place call on its own stream; ext_idx[0 .. n_ext) the
-// staged indices of the KH_POD_EXT pods in stream order, needc[e] the device
-// pods of the rounds before round(e) - lead (whose device commits device pod e's
-// pre-evaluation must see; lead >= lag).  Per pod: the pre-evaluation on the state
-// after round(e) - lead - 1, then at sync->ext_req the exact placement (the resolve's
-// X nodes evaluated again, normalized DeviceShare Score), out_node and
-// sync->ext_done, then DeviceShare's Reserve without the Fit / LoadAware row and
-// out_dev.  scratch: ext_worker_scratch_bytes(n_ext, n) (its front zeroed here).
-size_t ext_worker_scratch_bytes(int32_t n_ext, int32_t n);
-// byte offset in scratch of the worker's failure word ((device pod << 4) | phase:
-// 1 pre-evaluation wait, 2 hand-off wait; 0 = none)
-size_t ext_worker_diag_offset(int32_t n_ext);
-hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx,
-                             const int32_t *ext_idx, const int32_t *needc, int32_t n_ext, int32_t P, int32_t lag,
-                             int32_t lead, int32_t n_cu, void *scratch, int32_t *out_node, uint32_t *out_dev,
-                             PipeSync *sync, uint64_t *dbg, hipStream_t s);
+// Device pods inside the pipelined greedy (plain build, seq_mode 0): per place
+// call launch_ext_begin once, then per device pod e (staged index gp, round u)
+// launch_ext_pre (a wait for the resolve's rounds < `rounds` = u - lead, the
+// device commits of the first `needc` device pods and the final of e - ext_ring(),
+// whose ring buffer it reuses; then the pre-evaluation of every node) and
+// launch_ext_final (a wait for sync->ext_req = gp + 1 and pre-evaluation e, then
+// the exact placement over the pre-evaluated values with the X nodes and the
+// commit-log rounds [xlo, xhi) evaluated again; out_node, sync->ext_done,
+// DeviceShare's Reserve without the Fit / LoadAware row, out_dev).  Every wait
+// is one workgroup on device flags; submitted in an order whose waits the
+// launches before them satisfy (api.hip), they stay deadlock-free on one stream
+// or two.  scratch: ext_scratch_bytes(n_ext, n).
+size_t ext_scratch_bytes(int32_t n_ext, int32_t n);
+int32_t ext_ring();
+hipError_t launch_ext_begin(const DevNodes &d, int32_t n_ext, void *scratch, hipStream_t s);
+// the device word counting the finals' re-evaluated nodes of the call (zeroed by launch_ext_begin)
+const uint32_t *ext_reevals(const void *scratch, int32_t n_ext, int32_t n);
+hipError_t launch_ext_pre(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t e,
+                          int32_t gp, int32_t rounds, int32_t needc, int32_t n_ext, void *scratch, PipeSync *sync,
+                          hipStream_t s);
+hipError_t launch_ext_final(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t e,
+                            int32_t gp, int32_t xlo, int32_t xhi, int32_t n_ext, void *scratch, int32_t *out_node,
+                            uint32_t *out_dev, PipeSync *sync, uint64_t *dbg, hipStream_t s);
 hipError_t launch_mark_ext(DevPod *pods, const int32_t *idx, int32_t n, hipStream_t s);
 // the k_seq instantiation launch_seq runs for this config, as rocprofv3 names it
-const char *seq_kernel_name(const DevCfg &c);
+const char *seq_kernel_name(const DevCfg &c, const DevNodes &d);
 
 }  // namespace kh

@@ -32,6 +32,7 @@
 // phase, which every block writes after it finished reading parity q.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "dev.hpp"
@@ -97,8 +98,22 @@ __device__ __forceinline__ uint32_t ext_bits(const DevCfg &c) {
 __host__ __device__ constexpr int seq_mode(const DevCfg &c) {
   return c.resv ? (c.resv_slots > KOORDHIP_RESV_SLOTS ? 3 : 2) : (((c.filt | c.score) & KOORDHIP_PLUGIN_NUMA) ? 1 : 0);
 }
+// k_seq's instantiation: the Reservation builds without DeviceShare and
+// without a reservation holding devices or extended scalars take 4 / 5
+static inline int seq_launch_mode(const DevCfg &c, const DevNodes &d) {
+  const int sm = seq_mode(c);
+  const bool nodev = !((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) && !d.dv.rslot && !d.dv.rxa;
+  return (sm >= 2 && nodev) ? sm + 2 : sm;
+}
+// k_seq only: SM 4 / 5 = SM 2 / 3 without DeviceShare and without a
+// reservation holding devices (the device and device-reservation code compiled
+// out: the Reservation + NodeNUMAResource profiles keep their registers)
 template <int SM>
-using SeqResvRow = NumaRowRS<SM == 3 ? KOORDHIP_RESV_SLOTS_MAX : KOORDHIP_RESV_SLOTS>;
+constexpr int kSeqSlots = (SM == 3 || SM == 5) ? KOORDHIP_RESV_SLOTS_MAX : KOORDHIP_RESV_SLOTS;
+template <int SM>
+constexpr bool kSeqDev = SM < 4;
+template <int SM>
+using SeqResvRow = NumaRowRS<kSeqSlots<SM>>;
 
 // The node's reservation holding devices, for a device pod under DeviceShare
 // (KH_POD_DEVSHARE): its DevRC (dev.hpp; h -1: none) and DeviceShare's
@@ -184,7 +199,7 @@ __device__ __forceinline__ ResvXS seq_resv_x(const DevNodes &d, const DevPod &p,
 // raw normalized scores.  Every column is read (the parity evaluator's rows,
 // like k_eval_full).  Inlined once per kernel: a call keeps its frame (the
 // config and column descriptors, the NV row) in scratch, kilobytes per lane.
-// EARLY (k_ext_worker: no status, no raw planes of infeasible nodes): a node
+// EARLY (k_ext_pre / k_ext_final: no status, no raw planes of infeasible nodes): a node
 // whose extended scalars do not fit returns -1 before any other load.
 template <int SM, bool EARLY = false>
 __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, const DevPod &p, const DevPodX &x,
@@ -205,23 +220,29 @@ __device__ __forceinline__ int32_t seq_eval(const DevCfg &c, const DevNodes &d, 
   int32_t t;
   bool df = true, rfail = false;
   if constexpr (SM >= 2) {
-    constexpr int S = SM == 3 ? KOORDHIP_RESV_SLOTS_MAX : KOORDHIP_RESV_SLOTS;
+    constexpr int S = kSeqSlots<SM>;
     SeqResvRow<SM> nr{};
     load_numa<false>(nr, d, i, all);  // (the zone row shares the reserved CPUs' bytes: eval_total_resv<.., Z> reads it)
     load_resv(nr, d.rv, i);
-    const DevRC rc = seq_dev_resv(c, d.dv, p, x, nr, i);
-    const ResvXS rx = seq_resv_x(d, p, x, nr, i);
-    if (rx.h >= 0 && (c.filt & KOORDHIP_PLUGIN_FIT)) xfr = (rx.f & RX_XFIT) != 0u;  // on the restored scalars
+    DevRC rc{-1, 0, 0, 0u};
+    ResvXS rx = no_rx();
+    if constexpr (kSeqDev<SM>) {
+      rc = seq_dev_resv(c, d.dv, p, x, nr, i);
+      rx = seq_resv_x(d, p, x, nr, i);
+      if (rx.h >= 0 && (c.filt & KOORDHIP_PLUGIN_FIT)) xfr = (rx.f & RX_XFIT) != 0u;  // on the restored scalars
+    }
     t = c.zones       ? eval_total_resv<S, true, true>(p, v, nr, d.nu.cls, c, &d, i, rx)
         : c.resv_cpus ? eval_total_resv<S, true>(p, v, nr, d.nu.cls, c, nullptr, 0, rx)
                       : eval_total_resv<S, false>(p, v, nr, d.nu.cls, c, nullptr, 0, rx);
-    const int32_t nq = (rs && (x.flags & KOORDHIP_PODX_DEVICE)) ? resv_nominate(p, nr, resv_matched(nr, p), rx) : -1;
-    if (rc.h >= 0)
-      df = rc_eval(c, d.dv, x, i, rc, nq, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
-                   (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
-    else
-      df = dev_eval(c, d.dv, x, i, nq >= 0, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
-                    (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
+    if constexpr (kSeqDev<SM>) {
+      const int32_t nq = (rs && (x.flags & KOORDHIP_PODX_DEVICE)) ? resv_nominate(p, nr, resv_matched(nr, p), rx) : -1;
+      if (rc.h >= 0)
+        df = rc_eval(c, d.dv, x, i, rc, nq, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                     (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
+      else
+        df = dev_eval(c, d.dv, x, i, nq >= 0, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                      (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw[0]);
+    }
     if ((p.flags & (KOORDHIP_POD_RESERVE | KOORDHIP_POD_RESV_OPERATING)) && (c.filt & KOORDHIP_PLUGIN_RESERVATION) &&
         !reserve_pod_ok(p, (p.flags & KOORDHIP_POD_RESERVE) ? x.reserve_node : 0, nr, i))
       rfail = true;
@@ -307,7 +328,7 @@ __device__ __forceinline__ bool sweep(const uint64_t *g, uint32_t epoch, uint32_
 // DeviceShare and the extended scalars); rc: 0, or KOORDHIP_RESERVE_FAILED
 // (nothing committed).  nf: the feasible node count (one: no PreScore, so no
 // reservation is nominated before the NodeNUMAResource / DeviceShare Reserve).
-// ROW false (k_ext_worker): the Fit / LoadAware row is the pipelined
+// ROW false (k_ext_final): the Fit / LoadAware row is the pipelined
 // resolve's, which applies that delta itself -- everything else here.
 template <int SM, bool ROW = true>
 __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNodes &d, const DevPod &p,
@@ -321,8 +342,10 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   if constexpr (SM >= 2) {
     load_resv(rv, d.rv, w);
     mm = resv_matched(rv, p);
-    rc = seq_dev_resv(c, d.dv, p, x, rv, w);
-    rx = seq_resv_x(d, p, x, rv, w);
+    if constexpr (kSeqDev<SM>) {
+      rc = seq_dev_resv(c, d.dv, p, x, rv, w);
+      rx = seq_resv_x(d, p, x, rv, w);
+    }
   }
   const bool prescore = rs && nf > 1;
   // the reservation PreScore nominated (DeviceShare Reserve reads it) and the
@@ -335,7 +358,7 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   }
   uint32_t slots[DT] = {0u, 0u, 0u};
   int64_t per[DT][DR];
-  const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+  const bool dev = kSeqDev<SM> && ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
   // the loads of every row the Reserve changes go out first (one round trip
   // with the device rows' instead of one per structure): the Fit / LoadAware
   // row and the extended scalars' Requested
@@ -344,8 +367,9 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
   int64_t xr[KOORDHIP_NXRES];
 #pragma unroll
   for (int j = 0; j < KOORDHIP_NXRES; j++) xr[j] = ((x.xmask >> j) & 1u) ? d.dv.xreq[(size_t)j * d.n + w] : 0;
-  if (dev && !(rc.h >= 0 ? rc_reserve(c, d.dv, x, w, rc, nq, slots, per) : dev_reserve(c, d.dv, x, w, nq >= 0, slots, per)))
-    return KOORDHIP_RESERVE_FAILED;
+  if constexpr (kSeqDev<SM>)
+    if (dev && !(rc.h >= 0 ? rc_reserve(c, d.dv, x, w, rc, nq, slots, per) : dev_reserve(c, d.dv, x, w, nq >= 0, slots, per)))
+      return KOORDHIP_RESERVE_FAILED;
   uint64_t m[NW] = {0, 0, 0, 0};
   if constexpr (SM >= 1) {
     if (numa_on(c) && numa_active(p, c)) {
@@ -357,14 +381,15 @@ __device__ __forceinline__ int32_t seq_commit_body(const DevCfg &c, const DevNod
       store_numa_row(r, d, w);
     }
   }
-  if (dev) {
-    dev_apply<!ROW>(d.dv, w, slots, per);
-    if (rc.h >= 0 && qa == rc.h) rc_apply_allocated<!ROW>(d.dv, w, slots, per);
-  }
+  if constexpr (kSeqDev<SM>)
+    if (dev) {
+      dev_apply<!ROW>(d.dv, w, slots, per);
+      if (rc.h >= 0 && qa == rc.h) rc_apply_allocated<!ROW>(d.dv, w, slots, per);
+    }
   if constexpr (SM >= 2) {  // Reservation Reserve: assumePod into the nominated reservation
     const int qz = resv_assume(rv, p, m, rx);
     store_resv(rv, d.rv, w);
-    if (qz >= 0 && qz == rx.h && x.xmask)  // ... its extended scalars' Allocated (masked to its keys)
+    if (kSeqDev<SM> && qz >= 0 && qz == rx.h && x.xmask)  // ... its extended scalars' Allocated (masked to its keys)
       for (int j = 0; j < KOORDHIP_NXRES; j++) {
         const size_t at = (size_t)j * d.n + w;
         if (((x.xmask >> j) & 1u) && d.dv.rxa[at] != 0) d.dv.rxd[at] += x.xreq[j];
@@ -557,311 +582,408 @@ __device__ __forceinline__ void seq_block_reduce(int32_t v4[4], uint64_t &key, i
 // device pod (KH_POD_EXT) it writes every commit so far back, exports its X
 // set (the nodes committed since the state the round's lists were evaluated
 // on: M' and this round's M, pipe_xlist) and stores sync->ext_req = pod + 1.
-// This persistent grid runs that pod's reference cycle: every node's Filter
-// and per-node total, DeviceShare's raw Score (0 .. 100 per requested type,
-// scoring.go:33-72) and the normalization over the feasible nodes
-// (DefaultNormalizeScore, scoring.go:78-80).
-//   pre-evaluation, off the critical path: as soon as the pod's round u may
-//     be evaluated (res_round >= u - lag, and the device commits of the device
-//     pods of the rounds before that are published), every node's key
-//     make_key(total, i) (0: infeasible) and raw score into pk / pr;
-//   final, at the hand-off: only the X nodes are evaluated again (every other
-//     node's row is the pre-evaluation's); the normalized total of a node is
-//     its total + w * norm(raw), so the winner is among the best (total,
-//     lowest index) node of each raw value: every workgroup folds its chunk
-//     into a [EXT_RAW] table of such keys in LDS and merges it into the global
-//     one with agent-scope atomic max; the workgroup finishing the last chunk
-//     takes the maximum raw value, ranks the <= EXT_RAW candidates, stores
-//     out_node write-through and ext_done = pod + 1, and only then runs
-//     DeviceShare's Reserve (device choice + deviceUsed, the extended scalars;
-//     not the Fit / LoadAware row, which the resolve commits in its own copy)
-//     and publishes it (cdone) for the next device pod.
-// Node chunks are claimed from per-pod counters, not assigned: whichever
-// workgroups are resident share the work (none waits for a workgroup the GPU
-// has not started -- its CUs may be held by persistent kernels that wait on
-// this pod).
+// Two TRANSIENT launches per device pod run that pod's reference cycle: every
+// node's Filter and per-node total, DeviceShare's raw Score (0 .. 100 per
+// requested type, scoring.go:33-72) and the normalization over the feasible
+// nodes (DefaultNormalizeScore, scoring.go:78-80):
+//   k_ext_pre    (after the resolve finished round u - lead: the state every
+//                later commit is in X or the commit log of) every node's key
+//                make_key(total, i) (0: infeasible) and raw score into pk / pr;
+//   k_ext_final  (after the hand-off) only the X nodes and the log nodes are
+//                evaluated again (every other node's value is the
+//                pre-evaluation's); the normalized total of a node is its total
+//                + w * norm(raw), so the winner is among the best (total,
+//                lowest index) node of each raw value: every workgroup folds its
+//                chunk into a [EXT_RAW] table of such keys in LDS and merges it
+//                into the global one with agent-scope atomic max; the last
+//                arriving workgroup takes the maximum raw value, ranks the
+//                <= EXT_RAW candidates, stores out_node write-through and
+//                ext_done = pod + 1, then runs DeviceShare's Reserve (device
+//                choice + deviceUsed, the extended scalars; not the Fit /
+//                LoadAware row, which the resolve commits in its own copy).
+// Both sit on ONE stream in an order whose every wait is satisfiable by the
+// launches before it (api.hip), each behind a one-workgroup wait launch: no
+// workgroup of theirs waits for another kernel while it holds a CU, so the
+// pipeline's only persistent workgroups are the resolve's and the class
+// lists' (round 5's persistent worker grid -- 128 workgroups of one per CU --
+// left some XCD no CU for a class build's 1024-thread collect workgroup, which
+// is dealt to a fixed XCD: the build stream stalled behind it, the class lists
+// and the resolve behind the build; profiles/r05q_ext_lead.txt,
+// gpurun_out/r05j_dsmix.err).
 constexpr int EXT_RAW = 320;  // raw DeviceShare scores 0 .. 300 (three device types x 100)
 constexpr int EXT_THREADS = 256;
 constexpr int32_t EXT_PCHUNK = EXT_THREADS;      // pre-evaluation chunk: one node per thread
 constexpr int EXT_FNPT = 4;                      // final chunk: four nodes per thread (two loads each)
 constexpr int32_t EXT_FCHUNK = EXT_THREADS * EXT_FNPT;
-constexpr int EXT_CW = 8;     // counter words per device pod: claimed / finished chunks of both phases
 constexpr int EXT_RING = 4;   // pre-evaluation buffers: device pods evaluated ahead of their hand-off
 
-// Workgroups [0, gf) run the final phases, [gf, grid) the pre-evaluations,
-// which run up to EXT_RING device pods ahead.
+// DeviceShare's Reserve of a device pod on node w without the Fit / LoadAware
+// row (seq_commit_body<0, false>: dev_reserve, allocator.go:91-122, then
+// deviceUsed and the extended scalars' Requested), by ONE wave: lane l < DT x
+// DS holds dev slot l % DS of type l / DS (every row in one load round trip;
+// one lane's dependent loads cost ~40k cycles), the `wanted` best fitting
+// devices of a type by (score desc, minor asc) -- minors are unique on a node,
+// so that order is strict and each lane's rank among its type's lanes decides
+// -- and lanes 32 .. 39 the extended scalars.  The same allocation as
+// dev_reserve; false (nothing applied) where it fails.  All 64 lanes call it.
+__device__ __noinline__ bool ext_commit_wave(const DevCfg &c, const DevNodes &d, const DevPodX &x, int32_t w,
+                                             uint32_t slots[DT]) {
+  const int lane = threadIdx.x & 63;
+  const DevDev &dv = d.dv;
+  const bool devp = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) && (x.flags & KOORDHIP_PODX_DEVICE) &&
+                    dv.slots > 0 && dv.present;
+  const int t = lane / DS, s = lane % DS;
+  int64_t qt[DR] = {0, 0, 0};
+  const bool req = t < DT && devp && dev_requests(x, t, qt);
+  const bool mine = req && s < dv.slots;
+  int32_t mi = -1;
+  int64_t tot[DR] = {0, 0, 0}, usd[DR] = {0, 0, 0}, fr[DR] = {0, 0, 0};
+  size_t a0 = 0;
+  const bool present = devp && dv.present[w] != 0;
+  if (mine) {
+    a0 = dev_at(dv, w, t, s) * DR;
+    mi = dv.minor[a0 / DR];
+#pragma unroll
+    for (int r = 0; r < DR; r++) {
+      tot[r] = dv.total[a0 + r];
+      usd[r] = dv.used[a0 + r];
+      fr[r] = tot[r] - usd[r] > 0 ? tot[r] - usd[r] : 0;
+    }
+  }
+  const int j = lane - 32;
+  const bool xl = j >= 0 && j < KOORDHIP_NXRES && ((x.xmask >> j) & 1u);
+  const int64_t xr = xl ? dv.xreq[(size_t)j * d.n + w] : 0;
+  bool ok = true, any = false;
+  uint64_t take = 0ull;
+  int64_t myper[DR] = {0, 0, 0};
+  for (int u = 0; u < DT && present; u++) {
+    int64_t q[DR];
+    if (!dev_requests(x, u, q)) continue;
+    any = true;
+    const uint64_t has = __ballot(t == u && mine && mi >= 0);
+    if (!has) {
+      ok = false;  // dev_has_type
+      break;
+    }
+    if (u == KOORDHIP_DEV_GPU) {  // fillGPUTotalMem: the lowest slot with resources
+      const uint64_t wr = __ballot(t == u && mine && mi >= 0 && (tot[0] != 0 || tot[1] != 0 || tot[2] != 0));
+      if (!wr) {
+        ok = false;
+        break;
+      }
+      const int64_t mem = __shfl(tot[2], __builtin_ctzll(wr), 64);
+      if (q[2] >= 0) {
+        const double f = (double)q[2] / (double)mem;  // memoryBytesToRatio, float64
+        q[1] = (int64_t)(f * 100.0);
+      } else {
+        q[2] = (q[1] > 0 ? q[1] : 0) * mem / 100;  // memoryRatioToBytes
+      }
+      if (q[0] < 0) q[0] = 0;
+    }
+    int64_t per[DR];
+    const int64_t want = dev_wanted(u, q, per);
+    const bool fit = t == u && mine && mi >= 0 && !dev_zero(fr) && dev_fits(per, fr);
+    const int64_t sc = fit ? dev_scorer(c, u, tot, fr, per) : -1;
+    int32_t rank = 0;
+#pragma unroll
+    for (int k = 0; k < DS; k++) {
+      const int64_t os = __shfl(sc, u * DS + k, 64);
+      const int32_t om = __shfl(mi, u * DS + k, 64);
+      rank += (os >= 0 && (os > sc || (os == sc && om < mi))) ? 1 : 0;
+    }
+    const uint64_t fits = __ballot(fit);
+    if ((int64_t)__popcll(fits) < want) {
+      ok = false;
+      break;
+    }
+    const bool mine_taken = fit && rank < want;
+    take |= __ballot(mine_taken);
+    if (t == u)
+#pragma unroll
+      for (int r = 0; r < DR; r++) myper[r] = per[r];
+  }
+  (void)any;
+  if (!ok) return false;
+  if (((take >> lane) & 1ull) && mine)
+#pragma unroll
+    for (int r = 0; r < DR; r++) st_wt(&dv.used[a0 + r], (int64_t)(usd[r] + myper[r]));
+  if (xl) st_wt(&dv.xreq[(size_t)j * d.n + w], (int64_t)(xr + x.xreq[j]));
+#pragma unroll
+  for (int u = 0; u < DT; u++) slots[u] = (uint32_t)((take >> (u * DS)) & ((1ull << DS) - 1ull));
+  return true;
+}
+
+// flags (ExtScr::fl), each on a 128-B line of its own (pipe.hpp: many pollers
+// of one line delay its writer): pre-evaluations finished, finals finished
+// (their ring buffer read), device commits published, the gates the first
+// workgroup of a spinning pre-evaluation / final opens for the others; relaxed
+// agent-scope words, each stored after the data it covers was written through
+// and drained (Guideline 16 R1).  EXT_PERM: the permutation's two counters;
+// EXT_REEV: the finals' re-evaluated nodes of the call.
+enum {
+  EXT_PREDONE = 0,
+  EXT_FDONE = 32,
+  EXT_CDONE = 64,
+  EXT_PERM = 96,
+  EXT_REEV = 100,
+  EXT_GPRE = 128,
+  EXT_GFIN = 160,
+  EXT_GFA = 192,
+  EXT_FLAGS = 224
+};
+
+// A gate waiter (every workgroup of a spinning grid but the first): polls its
+// own line only, the pipeline's error word every 64th poll (pipe.hpp: a poller
+// of the error word polls the line of sel / res_round, which the resolve and
+// the class workgroups use)
+static __device__ bool wait_gate(const int32_t *p, int32_t v, PipeSync *sy) {
+  const uint64_t t0 = stamp();
+  for (uint32_t k = 0; load_relaxed(p) < v; k++) {
+    if ((k & 63u) == 63u) {
+      if (load_relaxed(&sy->err)) return false;
+      if (stamp() - t0 > PIPE_WATCHDOG) {
+        store_release(&sy->err, 1);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return true;
+}
+
 template <int SM>
-__global__ __launch_bounds__(EXT_THREADS) void k_ext_worker(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
-                                                            const DevPodX *__restrict__ podx,
-                                                            const int32_t *__restrict__ ext_idx,
-                                                            const int32_t *__restrict__ needc, int32_t n_ext, int32_t P,
-                                                            int32_t lag, int32_t lead, int32_t gf,
-                                                            uint64_t *__restrict__ tab,
-                                                            uint32_t *__restrict__ cnt, uint64_t *__restrict__ pk,
-                                                            int32_t *__restrict__ pr, const int32_t *__restrict__ perm,
-                                                            int32_t *__restrict__ out_node,
-                                                            uint32_t *__restrict__ out_dev, PipeSync *sy, uint64_t *dbg) {
+__global__ __launch_bounds__(EXT_THREADS) void k_ext_pre(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
+                                                         const DevPodX *__restrict__ podx, int32_t e, int32_t gp,
+                                                         uint64_t *__restrict__ bk, int32_t *__restrict__ br,
+                                                         const int32_t *__restrict__ perm, uint32_t *__restrict__ parr,
+                                                         int32_t *__restrict__ fl, PipeSync *sy, int32_t rounds,
+                                                         int32_t needc, int32_t fdone, int32_t spin) {
+  if (spin) {  // the waits of k_wait_ext_pre inside the grid (no launch boundary after them)
+    __shared__ int32_t s_ok;
+    if (threadIdx.x == 0) {
+      bool ok;
+      if (blockIdx.x == 0) {  // one poller of the pipeline's lines, then the gate
+        ok = rounds <= 0 || wait_at_least(&sy->res_round, rounds, sy);
+        ok = ok && (needc <= 0 || wait_at_least(&fl[EXT_CDONE], needc, sy));
+        ok = ok && (fdone <= 0 || wait_at_least(&fl[EXT_FDONE], fdone, sy));
+        if (ok) __hip_atomic_store(&fl[EXT_GPRE], e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        ok = wait_gate(&fl[EXT_GPRE], e + 1, sy);
+      }
+      s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+  }
+  if (__hip_atomic_load(&sy->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // the pipeline gave up
+  const int32_t j = (int32_t)blockIdx.x * EXT_PCHUNK + (int32_t)threadIdx.x;
+  if (j < d.n) {
+    const int32_t i = perm[j];
+    int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
+    const int32_t tk = seq_eval<SM, true>(c, d, pods[gp], podx[gp], i, false, raw, nullptr);
+    st_wt(&bk[i], (uint64_t)(tk >= 0 ? make_key(tk, i) : 0ull));
+    st_wt(&br[i], (int32_t)min(max(raw[0], 0), EXT_RAW - 1));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(parr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x)
+    __hip_atomic_store(&fl[EXT_PREDONE], e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// tab: [EXT_RAW] u64 (zero between pods: the last workgroup resets it), arrive:
+// this pod's arrival counter (zeroed per call).  The X nodes: pipe_xlist; the
+// log nodes: out_node of rounds [xlo, xhi) (the pre-evaluation's state is after
+// round u - lead - 1, the resolve's X covers rounds u - lag .. u).
+template <int SM>
+__global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d, const DevPod *__restrict__ pods,
+                                                           const DevPodX *__restrict__ podx, int32_t gp, int32_t xlo,
+                                                           int32_t xhi, uint64_t *__restrict__ tab,
+                                                           uint32_t *__restrict__ arrive,
+                                                           uint64_t *__restrict__ bk,
+                                                           int32_t *__restrict__ br, int32_t *__restrict__ out_node,
+                                                           uint32_t *__restrict__ out_dev, int32_t e,
+                                                           int32_t *__restrict__ fl, PipeSync *sy, uint64_t *dbg,
+                                                           int32_t spin) {
   __shared__ uint64_t lt[EXT_RAW];
   __shared__ uint32_t xm[EXT_FCHUNK / 32];  // the chunk's X nodes
   __shared__ int32_t s_red[SEQ_THREADS / 64][8];
   __shared__ uint64_t s_key[SEQ_THREADS / 64];
-  __shared__ int32_t s_go, s_last, s_ch;
+  __shared__ int32_t s_last;
+  __shared__ uint32_t s_nre;
+  __shared__ int32_t s_ok[2];
   const int t = threadIdx.x;
-  const int32_t b = blockIdx.x;
-  const int32_t ncp = (d.n + EXT_PCHUNK - 1) / EXT_PCHUNK, ncf = (d.n + EXT_FCHUNK - 1) / EXT_FCHUNK;
-  int32_t *cdone = reinterpret_cast<int32_t *>(cnt + (size_t)EXT_CW * n_ext);  // device commits published
+  const int32_t c0 = (int32_t)blockIdx.x * EXT_FCHUNK;
+  // spin: the grid is resident before the hand-off (launched behind the
+  // previous final) -- the pre-evaluation is awaited and its values loaded
+  // first, then the hand-off, so no launch boundary sits between the
+  // resolve's request and the fold
+  if (spin) {  // the first workgroup polls the flags and opens the gates
+    if (t == 0) {
+      if (blockIdx.x == 0) {
+        s_ok[0] = wait_at_least(&fl[EXT_PREDONE], e + 1, sy);
+        if (s_ok[0]) __hip_atomic_store(&fl[EXT_GFA], e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        s_ok[0] = wait_gate(&fl[EXT_GFA], e + 1, sy);
+      }
+    }
+    __syncthreads();
+    if (!s_ok[0]) return;
+  }
+  uint64_t kv[EXT_FNPT];
+  int32_t rv[EXT_FNPT];
+#pragma unroll
+  for (int k = 0; k < EXT_FNPT; k++) {  // the pre-evaluated values, all loads in flight
+    const int32_t i = c0 + k * EXT_THREADS + t;
+    kv[k] = i < d.n ? __hip_atomic_load(&bk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    rv[k] = i < d.n ? __hip_atomic_load(&br[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  }
+  if (spin) {
+    if (t == 0) {
+      if (blockIdx.x == 0) {
+        s_ok[1] = wait_at_least(&sy->ext_req, gp + 1, sy);
+        if (s_ok[1]) __hip_atomic_store(&fl[EXT_GFIN], gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        s_ok[1] = wait_gate(&fl[EXT_GFIN], gp + 1, sy);
+      }
+    }
+    __syncthreads();
+    if (!s_ok[1]) return;
+  }
+  // the hand-off happened and the pre-evaluation is published (the waits
+  // above or the wait launch before this one), unless the pipeline gave up
+  if (__hip_atomic_load(&sy->ext_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp + 1 ||
+      __hip_atomic_load(&fl[EXT_PREDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e + 1 ||
+      __hip_atomic_load(&sy->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return;  // (grid-uniform)
+  const uint64_t t0 = (dbg && blockIdx.x == 0) ? stamp() : 0;
+  const DevPod &p = pods[gp];
+  const DevPodX &x = podx[gp];
   const int32_t *xl = pipe_xlist(sy);
   const int32_t wdev = (c.score & KOORDHIP_PLUGIN_DEVICESHARE) ? c.w_ext[0] : 0;
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
-  const size_t nn = (size_t)max(d.n, 1);
-  if (t == 0) atomicAdd(cdone + 4, 1);  // workgroups started (diagnostics: api.hip pipe_status)
-  // dbg (KOORDHIP_STAMPS): final workgroup 0's cycles waiting for the hand-off,
-  // final phase, merge + arrival [80..82], its final chunks [87]; pre-evaluation
-  // workgroup gf's cycles waiting [89] and evaluating [88]; the last final
-  // workgroup's reduce, device commit (after the hand-off), publish [83..85],
-  // pods [86]
-  uint64_t c_w = 0, c_e = 0, c_m = 0, c_r = 0, c_c = 0, c_p = 0, n_l = 0, n_ch = 0, c_pre = 0, c_pw = 0, c_dc = 0,
-           c_pe = 0;
-  // claim chunks of a phase until none is left; f(chunk) per claimed chunk
-  auto claim_all = [&](uint32_t *claim, int32_t nch, auto f) -> int32_t {
-    int32_t done = 0;
-    for (;;) {
-      if (t == 0) s_ch = (int32_t)__hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const int32_t ch = s_ch;
-      __syncthreads();
-      if (ch >= nch) return done;  // block-uniform
-      done++;
-      f(ch);
-    }
-  };
-  // the pre-evaluation chunks of device pod e this workgroup can claim: every
-  // node's key (0: infeasible) and raw score into the pod's ring buffer, then
-  // the chunks counted as finished
-  auto pre_eval = [&](int32_t e) {
-    const int32_t gp = ext_idx[e];
-    uint32_t *cw = cnt + (size_t)EXT_CW * e;
-    const DevPod &p = pods[gp];
-    const DevPodX &x = podx[gp];
-    uint64_t *bk = pk + (size_t)(e % EXT_RING) * nn;
-    int32_t *br = pr + (size_t)(e % EXT_RING) * nn;
-    const int32_t pdone = claim_all(cw, ncp, [&](int32_t ch) {
-      const int32_t j = ch * EXT_PCHUNK + t;
-      if (j < d.n) {
-        const int32_t i = perm[j];
-        int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
-        const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
-        st_wt(&bk[i], (uint64_t)(tk >= 0 ? make_key(tk, i) : 0ull));
-        st_wt(&br[i], (int32_t)min(max(raw[0], 0), EXT_RAW - 1));
-      }
-    });
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0 && pdone) __hip_atomic_fetch_add(cw + 1, (uint32_t)pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  if (b >= gf) {
-    // ---- pre-evaluations: device pod e on the state round u's lists see, as
-    //      soon as that state is written back (X covers everything later), the
-    //      device commits of the device pods before it are published, and its
-    //      ring buffer's previous pod has had its final phase
-    for (int32_t e = 0; e < n_ext; e++) {
-      const int32_t gp = ext_idx[e], u = gp / P;
-      uint32_t *cw = cnt + (size_t)EXT_CW * e;  // {pre claimed, pre finished, final claimed, final finished}
-      const uint64_t tp0 = dbg ? stamp() : 0;
-      if (t == 0)
-        s_go = ((u <= lead || wait_at_least_idle(&sy->res_round, u - lead, sy)) && wait_at_least_idle(cdone, needc[e], sy) &&
-                (e < EXT_RING || wait_at_least_idle(&sy->ext_done, ext_idx[e - EXT_RING] + 1, sy)))
-                   ? 1
-                   : 0;
-      __syncthreads();
-      if (!s_go) {  // the pipeline gave up (block-uniform); the host reports where
-        if (t == 0) atomicMax(cdone + 1, (e << 4) | 1);
-        break;
-      }
-      const uint64_t tp1 = dbg ? stamp() : 0;
-      pre_eval(e);
-      if (dbg && b == gf) {
-        c_pw += tp1 - tp0;
-        c_pre += stamp() - tp1;
-      }
-    }
-    if (dbg && t == 0 && b == gf) {
-      atomicAdd((unsigned long long *)&dbg[88], (unsigned long long)c_pre);
-      atomicAdd((unsigned long long *)&dbg[89], (unsigned long long)c_pw);
-    }
-    return;
+  for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
+  for (int32_t w = t; w < EXT_FCHUNK / 32; w += EXT_THREADS) xm[w] = 0u;
+  if (t == 0) s_nre = 0u;
+  __syncthreads();
+  const int32_t nx = xl[0];
+  for (int32_t q = t; q < nx; q += EXT_THREADS) {
+    const int32_t y = xl[1 + q] - c0;
+    if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
   }
-  __builtin_amdgcn_s_setprio(2);  // the resolve waits on the final phases: ahead of the evaluation side's waves
-  for (int32_t e = 0; e < n_ext; e++) {
-    const int32_t gp = ext_idx[e];
-    uint32_t *cw = cnt + (size_t)EXT_CW * e;
-    const DevPod &p = pods[gp];
-    const DevPodX &x = podx[gp];
-    const uint64_t *bk = pk + (size_t)(e % EXT_RING) * nn;
-    const int32_t *br = pr + (size_t)(e % EXT_RING) * nn;
-    // ---- final: at the hand-off, the previous device pod's device commit and
-    //      this pod's pre-evaluation published
-    for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
-    const uint64_t t0 = dbg ? stamp() : 0;
-    uint64_t tw1 = 0, tw2 = 0;
-    if (t == 0) {
-      s_go = wait_at_least(&sy->ext_req, gp + 1, sy) ? 1 : 0;
-      tw1 = dbg ? stamp() : 0;
-      s_go = s_go && wait_at_least(cdone, e, sy);
-      tw2 = dbg ? stamp() : 0;
-    }
-    __syncthreads();
-    // the pre-evaluation chunks nobody has claimed yet (every condition of the
-    // pre-evaluation holds at the hand-off): the final workgroups never wait
-    // for a pre-evaluation workgroup the GPU has not started
-    if (s_go) pre_eval(e);
-    if (t == 0 && s_go) s_go = wait_at_least(reinterpret_cast<const int32_t *>(cw + 1), ncp, sy) ? 1 : 0;
-    __syncthreads();
-    if (dbg && b == 0 && t == 0) {  // after the hand-off: the previous device commit, then the pre-evaluation
-      c_dc += tw2 - tw1;
-      c_pe += stamp() - tw2;
-    }
-    if (!s_go) {
-      if (t == 0) atomicMax(cdone + 1, (e << 4) | 2);
-      break;
-    }
-    const uint64_t t1 = dbg ? stamp() : 0;
-    const int32_t nx = xl[0];
-    // the pre-evaluation saw the state after round u - lead - 1: the nodes
-    // committed since are the resolve's X (rounds u - lag .. u) and the commit
-    // log of rounds u - lead .. u - lag - 1 (out_node, written through, complete)
-    const int32_t u = gp / P;
-    const int32_t xlo = max(0, u - lead) * P, xhi = max(0, u - lag) * P;
-    const int32_t done = claim_all(cw + 2, ncf, [&](int32_t ch) {
-      const int32_t c0 = ch * EXT_FCHUNK;
-      for (int32_t w = t; w < EXT_FCHUNK / 32; w += EXT_THREADS) xm[w] = 0u;
-      __syncthreads();
-      for (int32_t q = t; q < nx; q += EXT_THREADS) {
-        const int32_t y = xl[1 + q] - c0;
-        if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
-      }
-      for (int32_t q = xlo + t; q < xhi; q += EXT_THREADS) {
-        const int32_t y = __hip_atomic_load(&out_node[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - c0;
-        if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
-      }
-      __syncthreads();
-      uint64_t kv[EXT_FNPT];
-      int32_t rv[EXT_FNPT];
-#pragma unroll
-      for (int k = 0; k < EXT_FNPT; k++) {  // the pre-evaluated values, all loads in flight
-        const int32_t i = c0 + k * EXT_THREADS + t;
-        kv[k] = i < d.n ? __hip_atomic_load(&bk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        rv[k] = i < d.n ? __hip_atomic_load(&br[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-      }
+  for (int32_t q = xlo + t; q < xhi; q += EXT_THREADS) {
+    const int32_t y = __hip_atomic_load(&out_node[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - c0;
+    if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
+  }
+  __syncthreads();
 #pragma unroll 1
-      for (int k = 0; k < EXT_FNPT; k++) {
-        const int32_t y = k * EXT_THREADS + t, i = c0 + y;
-        if (i < d.n && ((xm[y >> 5] >> (y & 31)) & 1u)) {  // committed since the pre-evaluation: evaluate again
-          int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
-          const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
-          kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
-          rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < EXT_FNPT; k++)
-        if (kv[k]) atomicMax(&lt[rv[k]], kv[k]);
-      __syncthreads();  // (xm reused by the next chunk)
-    });
-    const uint64_t t2 = dbg ? stamp() : 0;
-    if (done) {
-      for (int r = t; r < EXT_RAW; r += EXT_THREADS)
-        if (lt[r]) __hip_atomic_fetch_max(&tab[r], lt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(cw + 3, (uint32_t)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old + (uint32_t)done == (uint32_t)ncf;
-        if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-    } else if (t == 0) {
-      s_last = 0;
+  for (int k = 0; k < EXT_FNPT; k++) {
+    const int32_t y = k * EXT_THREADS + t, i = c0 + y;
+    if (i < d.n && ((xm[y >> 5] >> (y & 31)) & 1u)) {  // committed since the pre-evaluation: evaluate again
+      int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
+      const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
+      kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
+      rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
+      atomicAdd(&s_nre, 1u);
     }
-    __syncthreads();
-    const uint64_t t3 = dbg ? stamp() : 0;
-    if (dbg && b == 0) {
-      c_w += t1 - t0;
-      c_e += t2 - t1;
-      c_m += t3 - t2;
-      n_ch += done;
-    }
-    if (!s_last) continue;  // block-uniform
-    uint64_t v[2];
-    int32_t v4[4] = {0, -1, 0, 0};
+  }
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int r = t + h * EXT_THREADS;
-      v[h] = r < EXT_RAW ? __hip_atomic_load(&tab[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-      if (v[h]) v4[1] = r;
-      if (r < EXT_RAW) __hip_atomic_store(&tab[r], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next pod's
-    }
-    uint64_t kk = 0;
-    seq_block_reduce(v4, kk, s_red, s_key, t);
-    const int32_t mx = max(v4[1], 0);
-    uint64_t best = 0;
+  for (int k = 0; k < EXT_FNPT; k++)
+    if (kv[k]) atomicMax(&lt[rv[k]], kv[k]);
+  __syncthreads();
+  for (int r = t; r < EXT_RAW; r += EXT_THREADS)
+    if (lt[r]) __hip_atomic_fetch_max(&tab[r], lt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0 && s_nre)  // executed evaluations (the call's re-evaluated nodes)
+    __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(&fl[EXT_REEV]), s_nre, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old + 1u == gridDim.x;
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!s_last) return;  // block-uniform
+  const uint64_t t1 = dbg ? stamp() : 0;
+  uint64_t v[2];
+  int32_t v4[4] = {0, -1, 0, 0};
 #pragma unroll
-    for (int h = 0; h < 2; h++)
-      if (v[h]) {
-        const uint64_t k2 = v[h] + ((uint64_t)(uint32_t)(wdev * norm_score(t + h * EXT_THREADS, mx, false)) << 32);
-        best = k2 > best ? k2 : best;
-      }
-    v4[0] = v4[1] = v4[2] = v4[3] = 0;
-    seq_block_reduce(v4, best, s_red, s_key, t);
-    const uint64_t t4 = dbg ? stamp() : 0;
-    // The node goes back to the resolve first: in the plain build the Reserve
-    // cannot fail where the Filter passed on the same state (the same device
-    // rows: dev_reserve takes the best `wanted` of the devices dev_eval counted,
-    // the extended scalars only add), so the resolve continues while this
-    // workgroup commits the devices; the next device pod's workgroups wait for
-    // that commit (cdone).  A Reserve that fails anyway stops the pipeline
-    // (sync->err = 4) instead of diverging.
-    if (t == 0) st_wt(&out_node[gp], best ? key_node(best) : (int32_t)KOORDHIP_UNSCHEDULABLE);
-    // every lane's table reset and out_node, drained, then the relaxed hand-off
-    // (Guideline 16 R1: no L2 write-back fence)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const uint64_t t5 = dbg ? stamp() : 0;
+  for (int h = 0; h < 2; h++) {
+    const int r = t + h * EXT_THREADS;
+    v[h] = r < EXT_RAW ? __hip_atomic_load(&tab[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    if (v[h]) v4[1] = r;
+    if (r < EXT_RAW) __hip_atomic_store(&tab[r], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next pod's
+  }
+  uint64_t kk = 0;
+  seq_block_reduce(v4, kk, s_red, s_key, t);
+  const int32_t mx = max(v4[1], 0);
+  uint64_t best = 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+    if (v[h]) {
+      const uint64_t k2 = v[h] + ((uint64_t)(uint32_t)(wdev * norm_score(t + h * EXT_THREADS, mx, false)) << 32);
+      best = k2 > best ? k2 : best;
+    }
+  v4[0] = v4[1] = v4[2] = v4[3] = 0;
+  seq_block_reduce(v4, best, s_red, s_key, t);
+  // The node goes back to the resolve first: in the plain build the Reserve
+  // cannot fail where the Filter passed on the same state (the same device
+  // rows: dev_reserve takes the best `wanted` of the devices dev_eval counted,
+  // the extended scalars only add), so the resolve continues while this
+  // workgroup commits the devices; the next device pod's launches come after
+  // this one on the stream.  A Reserve that fails anyway stops the pipeline
+  // (sync->err = 4) instead of diverging.
+  if (t == 0) st_wt(&out_node[gp], best ? key_node(best) : (int32_t)KOORDHIP_UNSCHEDULABLE);
+  // every lane's table reset and out_node, drained, then the relaxed hand-off
+  // (Guideline 16 R1: no L2 write-back fence)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_store(&sy->ext_done, gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&fl[EXT_FDONE], e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // its ring buffer is read
+  }
+  const uint64_t t2 = dbg ? stamp() : 0;
+  if (t < 64) {  // wave 0: the device Reserve (every lane)
+    uint32_t slots[DT] = {0u, 0u, 0u};
+    const bool okc = !best || ext_commit_wave(c, d, x, key_node(best), slots);
     if (t == 0) {
-      __hip_atomic_store(&sy->ext_done, gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t slots[DT] = {0u, 0u, 0u};
-      if (best) {
-        // (nf 2: SM 0 has no Reservation PreScore to skip)
-        if (seq_commit_body<SM, false>(c, d, p, x, key_node(best), 2, false, nullptr, dev ? slots : nullptr))
-          __hip_atomic_store(&sy->err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (!okc) __hip_atomic_store(&sy->err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (out_dev)
-        for (int q = 0; q < DT; q++) st_wt(&out_dev[(size_t)gp * DT + q], slots[q]);
-      // the device rows and extended scalars (write-through: read next by the
-      // next device pod's workgroups on other XCDs), drained, then cdone
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(cdone, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int q = 0; q < DT; q++) st_wt(&out_dev[(size_t)gp * DT + q], okc ? slots[q] : 0u);
     }
-    if (dbg && t == 0) {
-      c_r += t4 - t3;
-      c_p += t5 - t4;
-      c_c += stamp() - t5;
-      n_l++;
+    // the device rows and extended scalars (write-through), drained, then cdone
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_store(&fl[EXT_CDONE], e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dbg) {  // [80] evaluate + fold (workgroup 0), [83] decide + publish, [84] device commit, [86] pods
+      atomicAdd((unsigned long long *)&dbg[83], (unsigned long long)(t2 - t1));
+      atomicAdd((unsigned long long *)&dbg[84], (unsigned long long)(stamp() - t2));
+      atomicAdd((unsigned long long *)&dbg[86], 1ull);
     }
   }
-  if (dbg && t == 0) {
-    if (b == 0) {
-      atomicAdd((unsigned long long *)&dbg[80], (unsigned long long)c_w);
-      atomicAdd((unsigned long long *)&dbg[81], (unsigned long long)c_e);
-      atomicAdd((unsigned long long *)&dbg[82], (unsigned long long)c_m);
-      atomicAdd((unsigned long long *)&dbg[87], (unsigned long long)n_ch);
-      atomicAdd((unsigned long long *)&dbg[94], (unsigned long long)c_dc);
-      atomicAdd((unsigned long long *)&dbg[95], (unsigned long long)c_pe);
-    }
-    atomicAdd((unsigned long long *)&dbg[83], (unsigned long long)c_r);
-    atomicAdd((unsigned long long *)&dbg[84], (unsigned long long)c_c);
-    atomicAdd((unsigned long long *)&dbg[85], (unsigned long long)c_p);
-    atomicAdd((unsigned long long *)&dbg[86], (unsigned long long)n_l);
-  }
+  if (dbg && blockIdx.x == 0 && t == 0) atomicAdd((unsigned long long *)&dbg[80], (unsigned long long)(t1 - t0));
+}
+
+// one thread waits until a pre-evaluation may start: the resolve finished
+// round `rounds` - 1 (rounds > 0), the device commits of the first `needc`
+// device pods are published, the final `fdone` - 1 read its ring buffer
+__global__ void k_wait_ext_pre(PipeSync *sy, int32_t *fl, int32_t rounds, int32_t needc, int32_t fdone) {
+  if (threadIdx.x != 0) return;
+  bool ok = rounds <= 0 || wait_at_least(&sy->res_round, rounds, sy);
+  ok = ok && (needc <= 0 || wait_at_least(&fl[EXT_CDONE], needc, sy));
+  ok = ok && (fdone <= 0 || wait_at_least(&fl[EXT_FDONE], fdone, sy));
+  (void)ok;
+}
+// ... and until a final may start: the resolve's hand-off of device pod gp
+// (ext_req = gp + 1) and the pod's pre-evaluation (e + 1 finished)
+__global__ void k_wait_ext_final(PipeSync *sy, int32_t *fl, int32_t want, int32_t pre) {
+  if (threadIdx.x != 0) return;
+  if (wait_at_least(&sy->ext_req, want, sy)) (void)wait_at_least(&fl[EXT_PREDONE], pre, sy);
 }
 
 // The pre-evaluation's node order: nodes holding device scalars (any xalloc
@@ -905,51 +1027,94 @@ hipError_t launch_mark_ext(DevPod *pods, const int32_t *idx, int32_t n, hipStrea
   return hipGetLastError();
 }
 
-// The worker's stream holds a quarter of the CUs (api.hip), two workgroups of
-// this kernel per CU (its VGPRs): final-phase workgroups about one chunk each,
-// at most half the slots; pre-evaluation workgroups on the rest (any subset
-// of either group makes progress: chunks are claimed)
-static int32_t ext_final_grid(int32_t n_cu, int32_t n) {
-  return std::max(1, std::min((n + EXT_FCHUNK - 1) / EXT_FCHUNK, std::max(1, n_cu / 4)));
+// scratch: [EXT_RAW] table, per device pod the final's and the pre-evaluation's
+// arrival counters, the flags (the zeroed front), then the RING
+// pre-evaluation buffers (keys u64, raw i32 per node) and the node permutation
+static size_t ext_fl_off(int32_t n_ext) {
+  return ((size_t)EXT_RAW * sizeof(uint64_t) + (size_t)2 * std::max(n_ext, 1) * sizeof(uint32_t) + 127) &
+         ~(size_t)127;
 }
-static int32_t ext_worker_grid(int32_t n_cu, int32_t n) {
-  return ext_final_grid(n_cu, n) +
-         std::max(1, std::min((n + EXT_PCHUNK - 1) / EXT_PCHUNK, std::max(1, n_cu / 2 - ext_final_grid(n_cu, n))));
-}
-
-// the zeroed front (table, counters) and the pre-evaluation's per-node keys / raw scores
 static size_t ext_front_bytes(int32_t n_ext) {
-  return ((size_t)EXT_RAW * sizeof(uint64_t) + ((size_t)EXT_CW * std::max(n_ext, 1) + 5) * sizeof(uint32_t) + 255) &
-         ~(size_t)255;
+  return (ext_fl_off(n_ext) + (size_t)EXT_FLAGS * sizeof(int32_t) + 255) & ~(size_t)255;
 }
-size_t ext_worker_scratch_bytes(int32_t n_ext, int32_t n) {
+size_t ext_scratch_bytes(int32_t n_ext, int32_t n) {
   return ext_front_bytes(n_ext) + (size_t)EXT_RING * std::max(n, 1) * (sizeof(uint64_t) + sizeof(int32_t)) +
          (size_t)std::max(n, 1) * sizeof(int32_t) + 64;
 }
+int32_t ext_ring() { return EXT_RING; }
 
-size_t ext_worker_diag_offset(int32_t n_ext) {
-  return (size_t)EXT_RAW * sizeof(uint64_t) + ((size_t)EXT_CW * std::max(n_ext, 1) + 1) * sizeof(uint32_t);
+struct ExtScr {
+  uint64_t *tab;
+  uint32_t *arrive, *parr;
+  int32_t *fl;  // [EXT_FLAGS] (the enum above), 128-B aligned
+  uint64_t *pk;
+  int32_t *pr;
+  int32_t *perm;
+};
+static ExtScr ext_scr(void *scratch, int32_t n_ext, int32_t n) {
+  char *base = static_cast<char *>(scratch);
+  ExtScr x;
+  x.tab = reinterpret_cast<uint64_t *>(base);
+  x.arrive = reinterpret_cast<uint32_t *>(x.tab + EXT_RAW);
+  x.parr = x.arrive + std::max(n_ext, 1);
+  x.fl = reinterpret_cast<int32_t *>(base + ext_fl_off(n_ext));
+  x.pk = reinterpret_cast<uint64_t *>(base + ext_front_bytes(n_ext));
+  x.pr = reinterpret_cast<int32_t *>(x.pk + (size_t)EXT_RING * std::max(n, 1));
+  x.perm = x.pr + (size_t)EXT_RING * std::max(n, 1);
+  return x;
 }
 
-hipError_t launch_ext_worker(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx,
-                             const int32_t *ext_idx, const int32_t *needc, int32_t n_ext, int32_t P, int32_t lag,
-                             int32_t lead, int32_t n_cu, void *scratch, int32_t *out_node, uint32_t *out_dev,
-                             PipeSync *sync, uint64_t *dbg, hipStream_t s) {
-  if (n_ext <= 0) return hipSuccess;
-  if (lead < lag) return hipErrorInvalidValue;
-  if (seq_mode(c) != 0 || P <= 0) return hipErrorInvalidValue;  // the plain build only (the route checks it)
-  char *base = static_cast<char *>(scratch);
-  uint64_t *tab = reinterpret_cast<uint64_t *>(base);
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab + EXT_RAW);
-  uint64_t *pk = reinterpret_cast<uint64_t *>(base + ext_front_bytes(n_ext));
-  int32_t *pr = reinterpret_cast<int32_t *>(pk + (size_t)EXT_RING * std::max(d.n, 1));
-  int32_t *perm = pr + (size_t)EXT_RING * std::max(d.n, 1);
-  uint32_t *pc = cnt + (size_t)EXT_CW * n_ext + 2;  // (after cdone and the failure word)
-  const int32_t gf = ext_final_grid(n_cu, d.n), grid = ext_worker_grid(n_cu, d.n);
+// The finals spin in their own grid (launched behind the previous final, so
+// resident before the hand-off: no launch boundary between the resolve's
+// request and the fold); the pre-evaluations wait in a one-workgroup launch
+// ahead of each (off the critical path, and a grid of a few hundred spinning
+// workgroups would hold CUs the builds need).  KOORDHIP_EXT_WAITK: the finals
+// behind wait launches too (A/B); KOORDHIP_EXT_PRESPIN: the pre-evaluations
+// spin too (A/B).  0 / 1 / 2: none / finals / both.
+static int32_t ext_spin() {
+  static const int32_t v = std::getenv("KOORDHIP_EXT_WAITK") ? 0 : std::getenv("KOORDHIP_EXT_PRESPIN") ? 2 : 1;
+  return v;
+}
+
+const uint32_t *ext_reevals(const void *scratch, int32_t n_ext, int32_t n) {
+  const ExtScr x = ext_scr(const_cast<void *>(scratch), n_ext, n);
+  return reinterpret_cast<const uint32_t *>(x.fl + EXT_REEV);
+}
+
+hipError_t launch_ext_begin(const DevNodes &d, int32_t n_ext, void *scratch, hipStream_t s) {
+  const ExtScr x = ext_scr(scratch, n_ext, d.n);
   if (hipError_t e = hipMemsetAsync(scratch, 0, ext_front_bytes(n_ext), s)) return e;
-  hipLaunchKernelGGL(k_ext_perm, dim3((d.n + 255) / 256), dim3(256), 0, s, d.dv, d.n, perm, pc);
-  hipLaunchKernelGGL(k_ext_worker<0>, dim3(grid), dim3(EXT_THREADS), 0, s, c, d, pods, podx, ext_idx, needc, n_ext, P,
-                     lag, lead, gf, tab, cnt, pk, pr, perm, out_node, out_dev, sync, dbg);
+  hipLaunchKernelGGL(k_ext_perm, dim3((d.n + 255) / 256), dim3(256), 0, s, d.dv, d.n, x.perm,
+                     reinterpret_cast<uint32_t *>(x.fl + EXT_PERM));
+  return hipGetLastError();
+}
+
+hipError_t launch_ext_pre(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t e,
+                          int32_t gp, int32_t rounds, int32_t needc, int32_t n_ext, void *scratch, PipeSync *sync,
+                          hipStream_t s) {
+  if (seq_mode(c) != 0) return hipErrorInvalidValue;  // the plain build only (the route checks it)
+  const ExtScr x = ext_scr(scratch, n_ext, d.n);
+  const size_t nn = (size_t)std::max(d.n, 1);
+  const int32_t spin = ext_spin() > 1;  // (pre-evaluations spin only with KOORDHIP_EXT_PRESPIN)
+  if (!spin && (rounds > 0 || needc > 0 || e >= EXT_RING))
+    hipLaunchKernelGGL(k_wait_ext_pre, dim3(1), dim3(64), 0, s, sync, x.fl, rounds, needc, e - EXT_RING + 1);
+  hipLaunchKernelGGL(k_ext_pre<0>, dim3((d.n + EXT_PCHUNK - 1) / EXT_PCHUNK), dim3(EXT_THREADS), 0, s, c, d, pods, podx,
+                     e, gp, x.pk + (size_t)(e % EXT_RING) * nn, x.pr + (size_t)(e % EXT_RING) * nn, x.perm, x.parr + e,
+                     x.fl, sync, rounds, needc, e - EXT_RING + 1, spin);
+  return hipGetLastError();
+}
+
+hipError_t launch_ext_final(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t e,
+                            int32_t gp, int32_t xlo, int32_t xhi, int32_t n_ext, void *scratch, int32_t *out_node,
+                            uint32_t *out_dev, PipeSync *sync, uint64_t *dbg, hipStream_t s) {
+  if (seq_mode(c) != 0) return hipErrorInvalidValue;
+  const ExtScr x = ext_scr(scratch, n_ext, d.n);
+  const size_t nn = (size_t)std::max(d.n, 1);
+  const int32_t spin = ext_spin() > 0;
+  if (!spin) hipLaunchKernelGGL(k_wait_ext_final, dim3(1), dim3(64), 0, s, sync, x.fl, gp + 1, e + 1);
+  hipLaunchKernelGGL(k_ext_final<0>, dim3((d.n + EXT_FCHUNK - 1) / EXT_FCHUNK), dim3(EXT_THREADS), 0, s, c, d, pods,
+                     podx, gp, xlo, xhi, x.tab, x.arrive + e, x.pk + (size_t)(e % EXT_RING) * nn,
+                     x.pr + (size_t)(e % EXT_RING) * nn, out_node, out_dev, e, x.fl, sync, dbg, spin);
   return hipGetLastError();
 }
 
@@ -1601,8 +1766,10 @@ hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, co
   // the same residency, but its cooperative queue is torn down by the HIP
   // runtime at process exit, after a profiler's finalisation: every
   // rocprofv3 trace of a k_seq workload died with SIGSEGV in exit().)
-  const int sm = seq_mode(c);
-  const void *f = sm == 3   ? (const void *)k_seq<3>
+  const int sm = seq_launch_mode(c, d);
+  const void *f = sm == 5   ? (const void *)k_seq<5>
+                  : sm == 4 ? (const void *)k_seq<4>
+                  : sm == 3 ? (const void *)k_seq<3>
                   : sm == 2 ? (const void *)k_seq<2>
                   : sm == 1 ? (const void *)k_seq<1>
                             : (const void *)k_seq<0>;
@@ -1612,6 +1779,8 @@ hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, co
   if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, SEQ_THREADS, 0)) return e;
   if ((int64_t)per_cu * ncu < grid) return hipErrorCooperativeLaunchTooLarge;
   switch (sm) {
+    case 5: hipLaunchKernelGGL(k_seq<5>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
+    case 4: hipLaunchKernelGGL(k_seq<4>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
     case 3: hipLaunchKernelGGL(k_seq<3>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
     case 2: hipLaunchKernelGGL(k_seq<2>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
     case 1: hipLaunchKernelGGL(k_seq<1>, dim3(grid), dim3(SEQ_THREADS), 0, s, c, d, a); break;
@@ -1620,9 +1789,10 @@ hipError_t launch_seq(const DevCfg &c, const DevNodes &d, const DevPod *pods, co
   return hipGetLastError();
 }
 
-const char *seq_kernel_name(const DevCfg &c) {
-  static const char *names[4] = {"kh::k_seq<0>", "kh::k_seq<1>", "kh::k_seq<2>", "kh::k_seq<3>"};
-  return names[seq_mode(c)];
+const char *seq_kernel_name(const DevCfg &c, const DevNodes &d) {
+  static const char *names[6] = {"kh::k_seq<0>", "kh::k_seq<1>", "kh::k_seq<2>",
+                                 "kh::k_seq<3>", "kh::k_seq<4>", "kh::k_seq<5>"};
+  return names[seq_launch_mode(c, d)];
 }
 
 hipError_t launch_seq_eval(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t n_pods,

@@ -8,7 +8,8 @@
 #   quick   bench lines without the CPU baseline (iteration)
 #   stamps  KOORDHIP_STAMPS resolve / select cycle stamps per workload
 #   prof    rocprofv3 --kernel-trace --stats per workload
-#   pmc     FETCH_SIZE / WRITE_SIZE passes per workload (KOORDHIP_SERIAL: no persistent resolve)
+#   pmc     FETCH_SIZE / WRITE_SIZE passes per workload (KOORDHIP_SERIAL: no persistent resolve;
+#           KOORDHIP_PMC_REPLAY: the class lists' and device pods' launches replayed after each call)
 # Every GPU step has its own time limit; the first failure stops the script.
 set -u
 R=${ROUND:-r04x}
@@ -17,7 +18,7 @@ WORKLOADS=${WORKLOADS:-config4 config3 config5}
 mkdir -p gpurun_out
 has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
 steps_of() { case $1 in config4|config4dsmix|config4ds) echo "--steps 5 --warmup 2";; config3|deviceshare|spread|affinity) echo "--steps 3 --warmup 1";; resvpolicy) echo "--steps 1 --warmup 1";; *) echo "--steps 2 --warmup 1";; esac; }
-pods_pmc() { case $1 in config4) echo 30000;; config3) echo 10000;; *) echo 6000;; esac; }
+pods_pmc() { case $1 in config4|config4dsmix) echo 100000;; config3) echo 10000;; *) echo 6000;; esac; }
 
 if has tests; then
   FILES=${TESTS_FILES:-tests}
@@ -54,7 +55,7 @@ PY
     bash scripts/profile.sh ${R}_$w --workload $w --steps 1 --warmup 1 ${BENCH_ARGS:-} || exit 1
   fi
   if has pmc; then
-    KOORDHIP_SERIAL=1 bash scripts/pmc.sh pmc_${R}_$w --workload $w --steps 1 --warmup 0 --pods $(pods_pmc $w) ${BENCH_ARGS:-} || exit 1
+    KOORDHIP_SERIAL=1 KOORDHIP_PMC_REPLAY=1 bash scripts/pmc.sh pmc_${R}_$w --workload $w --steps 1 --warmup 0 --pods $(pods_pmc $w) ${BENCH_ARGS:-} || exit 1
   fi
 done
 exit 0

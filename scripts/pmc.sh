@@ -8,6 +8,6 @@ export TMPDIR=/tmp
 for ctr in FETCH_SIZE WRITE_SIZE; do
   mkdir -p gpurun_out/$name/$ctr
   timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/$name/$ctr -o run \
-    -- python3 bench.py --no-cpu-baseline "$@" > gpurun_out/$name/$ctr/bench.log 2>&1 || { echo "pmc $ctr failed rc=$?"; exit 1; }
+    -- python3 bench.py --no-cpu-baseline --no-latency "$@" > gpurun_out/$name/$ctr/bench.log 2>&1 || { echo "pmc $ctr failed rc=$?"; exit 1; }
 done
 echo "pmc ok" >&2
