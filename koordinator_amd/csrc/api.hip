@@ -2506,7 +2506,7 @@ int seq_place(koordhip_ctx *c) {
   const int32_t rs = (c->dc.resv && (c->cfg.score_plugins & KOORDHIP_PLUGIN_RESERVATION)) ? 1 : 0;
   const bool stamps = std::getenv("KOORDHIP_STAMPS") != nullptr;
   if (stamps) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 96 * sizeof(uint64_t)));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 128 * sizeof(uint64_t)));
     HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 64 * sizeof(uint64_t), c->stream));
   }
   HIP_TRY(hipEventRecord(c->t0, c->stream));
@@ -2730,8 +2730,14 @@ static int cls_build(koordhip_ctx *c, const koordhip_ctx::ClsBuild &b, kh::PipeS
 // device commits (the caller restores).  Diagnostics only.
 int pmc_replay(koordhip_ctx *c) {
   if (c->last_seq && !(c->seq_profile && c->seq_ext_only && c->staged_ext_dev)) return 0;
-  if (!c->d_mod || c->n_staged <= 0) return 0;
+  if (c->n_staged <= 0) return 0;
   HIP_TRY(hipStreamSynchronize(c->stream));
+  // (a context that has only run the sequential cycle has no pipeline buffers: temporary ones)
+  const size_t lbytes = (size_t)kMaxBatch * 2 * kMaxBatch * sizeof(uint64_t);
+  int32_t *mod = c->d_mod;
+  uint64_t *lists = c->d_lists;
+  if (!mod) HIP_TRY(hipMalloc(&mod, (1 + kMaxBatch) * sizeof(int32_t) + kh::kPipeSyncBytes));
+  if (!lists) HIP_TRY(hipMalloc(&lists, 4 * lbytes));
   if (int e = koordhip_restore(c)) return e;
   const int32_t total = c->n_staged;
   int32_t P = c->batch;
@@ -2740,16 +2746,16 @@ int pmc_replay(koordhip_ctx *c) {
   const int nm = kh::side_mode(c->dc);
   while (P > 1 && kh::resolve_lds_bytes(P, (lag + 1) * P, c->n, nm, lag) > 157 * 1024) P--;
   const int32_t K = (lag + 1) * P, rounds = (total + P - 1) / P;
-  const bool cls = !c->last_seq && !c->cls_rep.empty() && c->nbins <= 32768 && c->world == 1 &&
-                   (int64_t)c->cls_rep.size() <= c->n_cu / 2 && kh::cls_run_lds(c->n, c->monotone) <= 150 * 1024 &&
-                   (kh::kClsTarget - K) / P >= 4 * kClsLead + 2;
   const bool ext = c->seq_profile && c->seq_ext_only && c->staged_ext && c->staged_ext_dev && c->podx_staged &&
                    !c->staged_reserve && !c->seq_snap && !c->d.dv.rslot && nm == 0 && c->world == 1 &&
                    !c->ext_idx.empty();
+  const bool cls = (!c->last_seq || ext) && !c->cls_rep.empty() && c->nbins <= 32768 && c->world == 1 &&
+                   (int64_t)c->cls_rep.size() <= c->n_cu / 2 && kh::cls_run_lds(c->n, c->monotone) <= 150 * 1024 &&
+                   (kh::kClsTarget - K) / P >= 4 * kClsLead + 2;
   int32_t *saved = nullptr;
   HIP_TRY(hipMalloc(&saved, (size_t)total * sizeof(int32_t)));
   HIP_TRY(hipMemcpyAsync(saved, c->d_out, (size_t)total * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
-  kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
+  kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(mod + 1 + kMaxBatch);
   HIP_TRY(hipMemsetAsync(sync, 0, kh::kPipeSyncBytes, c->stream));
   const int32_t big = 0x3fffffff;
   const int32_t head[3] = {big, big, rounds};  // sel[0], sel[1], res_round: every round published and resolved
@@ -2771,7 +2777,7 @@ int pmc_replay(koordhip_ctx *c) {
     }
     HIP_TRY(kh::launch_cls_run(c->dc, c->d, c->d_cls_pod, (int32_t)nc, c->d_plan + c->plan_off[0],
                                c->d_plan + c->plan_off[1], c->d_plan + c->plan_off[2], c->d_pod_cls, c->d_out, lag, P,
-                               total, c->d_cls_buf, c->d_cls_meta, K, c->monotone, c->d_lists,
+                               total, c->d_cls_buf, c->d_cls_meta, K, c->monotone, lists,
                                (int64_t)((size_t)kMaxBatch * 2 * kMaxBatch), cs, nullptr, c->stream));
   }
   const int32_t ne = (int32_t)c->ext_idx.size();
@@ -2805,6 +2811,8 @@ int pmc_replay(koordhip_ctx *c) {
   HIP_TRY(hipFree(saved));
   int32_t err = 0;
   HIP_TRY(hipMemcpy(&err, reinterpret_cast<int32_t *>(sync) + kh::kPipeSyncErrWord, sizeof(err), hipMemcpyDeviceToHost));
+  if (mod != c->d_mod) HIP_TRY(hipFree(mod));
+  if (lists != c->d_lists) HIP_TRY(hipFree(lists));
   std::fprintf(stderr, "[koordhip pmc replay] P %d lag %d: class lists %s (%zu builds, %d k_scan + k_cls_collect "
                "launches, 1 k_cls_run of %zu workgroups), device pods %d (k_ext_pre + k_ext_final each)%s\n", P, lag,
                cls ? "replayed" : "not used", cls ? c->plan_builds.size() : (size_t)0, nscan,
@@ -2997,8 +3005,8 @@ int place_staged_impl(koordhip_ctx *c) {
   c->last_ext_exec = 0;
   c->last_evc = c->last_reev = nullptr;
   if (std::getenv("KOORDHIP_STAMPS")) {
-    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 96 * sizeof(uint64_t)));
-    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 96 * sizeof(uint64_t), c->stream));
+    if (!c->d_dbg) HIP_TRY(hipMalloc(&c->d_dbg, 128 * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(c->d_dbg, 0, 128 * sizeof(uint64_t), c->stream));
   }
   int32_t *mbuf = c->d_mod;  // M' handed between resolve launches
   kh::PipeSync *sync = reinterpret_cast<kh::PipeSync *>(c->d_mod + 1 + kMaxBatch);
@@ -3262,6 +3270,18 @@ int place_staged_impl(koordhip_ctx *c) {
                    "%.0f | last workgroup: decide + publish %.0f  device commit %.0f\n",
                    (unsigned long long)h[31], (unsigned long long)h[30], h[31] ? (double)h[30] / h[31] : 0.0,
                    q[0] / np, q[3] / np, q[4] / np);
+      uint64_t r[12];
+      HIP_TRY(hipMemcpy(r, c->d_dbg + 96, sizeof(r), hipMemcpyDeviceToHost));
+      const double nb = (double)std::max<uint64_t>(r[10], 1);
+      std::fprintf(stderr, "[koordhip stamps] device-pod finals, us: request seen -> last workgroup arrived %.2f per pod | "
+                   "per workgroup: -> gate seen %.2f  X marked %.2f  re-evaluated %.2f  folded + arrived %.2f\n",
+                   r[5] * 0.01 / np, r[6] * 0.01 / nb, r[7] * 0.01 / nb, r[8] * 0.01 / nb, r[9] * 0.01 / nb);
+      // (s_memrealtime: 100 MHz, one clock for every CU)
+      std::fprintf(stderr, "[koordhip stamps] device-pod hand-offs, us per pod: the request seen -> published %.2f | "
+                   "requests already set when the final's first workgroup started: %llu of %llu | pre-evaluation "
+                   "published after the request: %llu pods, waited %.2f us each\n",
+                   r[2] * 0.01 / np, (unsigned long long)r[0], (unsigned long long)q[6], (unsigned long long)r[1],
+                   r[1] ? r[3] * 0.01 / r[1] : 0.0);
     }
     std::fprintf(stderr, "[koordhip stamps] general commit split: row source %llu  Reserve delta %llu  voiding + "
                  "outputs %llu cycles | winners already in M %llu\n",

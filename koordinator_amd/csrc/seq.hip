@@ -736,6 +736,12 @@ enum {
 // own line only, the pipeline's error word every 64th poll (pipe.hpp: a poller
 // of the error word polls the line of sel / res_round, which the resolve and
 // the class workgroups use)
+static __device__ __forceinline__ uint64_t realtime() {  // 100 MHz, one clock for every CU
+  uint64_t t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 static __device__ bool wait_gate(const int32_t *p, int32_t v, PipeSync *sy) {
   const uint64_t t0 = stamp();
   for (uint32_t k = 0; load_relaxed(p) < v; k++) {
@@ -823,7 +829,17 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   if (spin) {  // the first workgroup polls the flags and opens the gates
     if (t == 0) {
       if (blockIdx.x == 0) {
+        // hand-off timeline (s_memrealtime, dbg[96..100]): [96] finals whose request was set before
+        // their grid started, [97] / [99] pods whose pre-evaluation was published after the request
+        // and the time waited for it, [98] request seen -> published, [100] the current request seen
+        const bool req0 = dbg && load_relaxed(&sy->ext_req) >= gp + 1;
+        const uint64_t ta = dbg ? realtime() : 0;
+        if (req0) atomicAdd((unsigned long long *)&dbg[96], 1ull);
         s_ok[0] = wait_at_least(&fl[EXT_PREDONE], e + 1, sy);
+        if (dbg && s_ok[0] && (req0 || load_relaxed(&sy->ext_req) >= gp + 1) && realtime() - ta > 20) {
+          atomicAdd((unsigned long long *)&dbg[97], 1ull);
+          atomicAdd((unsigned long long *)&dbg[99], (unsigned long long)(realtime() - ta));
+        }
         if (s_ok[0]) __hip_atomic_store(&fl[EXT_GFA], e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         s_ok[0] = wait_gate(&fl[EXT_GFA], e + 1, sy);
@@ -844,6 +860,7 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     if (t == 0) {
       if (blockIdx.x == 0) {
         s_ok[1] = wait_at_least(&sy->ext_req, gp + 1, sy);
+        if (dbg) __hip_atomic_store(&dbg[100], realtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (s_ok[1]) __hip_atomic_store(&fl[EXT_GFIN], gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         s_ok[1] = wait_gate(&fl[EXT_GFIN], gp + 1, sy);
@@ -852,6 +869,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     __syncthreads();
     if (!s_ok[1]) return;
   }
+  uint64_t tg = 0, tm = 0, te = 0;  // (dbg: this workgroup's phase times, s_memrealtime)
+  if (dbg && t == 0) tg = realtime();
   // the hand-off happened and the pre-evaluation is published (the waits
   // above or the wait launch before this one), unless the pipeline gave up
   if (__hip_atomic_load(&sy->ext_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp + 1 ||
@@ -878,16 +897,25 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
   }
   __syncthreads();
+  if (dbg && t == 0) tm = realtime();
 #pragma unroll 1
   for (int k = 0; k < EXT_FNPT; k++) {
     const int32_t y = k * EXT_THREADS + t, i = c0 + y;
-    if (i < d.n && ((xm[y >> 5] >> (y & 31)) & 1u)) {  // committed since the pre-evaluation: evaluate again
+    // committed since the pre-evaluation: evaluate again -- unless the node was
+    // infeasible then (every Filter of the plain build is monotone in the
+    // commits of the batch -- Fit / LoadAware requests, DeviceShare's device
+    // usage and the extended scalars only grow -- so it still is)
+    if (i < d.n && kv[k] != 0ull && ((xm[y >> 5] >> (y & 31)) & 1u)) {
       int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
       const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
       kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
       rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
       atomicAdd(&s_nre, 1u);
     }
+  }
+  if (dbg) {
+    __syncthreads();
+    if (t == 0) te = realtime();
   }
 #pragma unroll
   for (int k = 0; k < EXT_FNPT; k++)
@@ -904,6 +932,15 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     const uint32_t old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = old + 1u == gridDim.x;
     if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (dbg && spin) {  // [102..105] per workgroup: request seen -> gate seen -> X marked -> re-evaluated -> arrived
+      const uint64_t ts = __hip_atomic_load(&dbg[100], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ta = realtime();
+      atomicAdd((unsigned long long *)&dbg[102], (unsigned long long)(tg > ts ? tg - ts : 0));
+      atomicAdd((unsigned long long *)&dbg[103], (unsigned long long)(tm - tg));
+      atomicAdd((unsigned long long *)&dbg[104], (unsigned long long)(te - tm));
+      atomicAdd((unsigned long long *)&dbg[105], (unsigned long long)(ta - te));
+      atomicAdd((unsigned long long *)&dbg[106], 1ull);
+      if (s_last) atomicAdd((unsigned long long *)&dbg[101], (unsigned long long)(ta - ts));
+    }
   }
   __syncthreads();
   if (!s_last) return;  // block-uniform
@@ -943,6 +980,10 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   __syncthreads();
   if (t == 0) {
     __hip_atomic_store(&sy->ext_done, gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dbg && spin) {  // [98] request seen -> published; [99] / [100] pods whose pre-evaluation came later
+      const uint64_t ts = __hip_atomic_load(&dbg[100], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd((unsigned long long *)&dbg[98], (unsigned long long)(realtime() - ts));
+    }
     __hip_atomic_store(&fl[EXT_FDONE], e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // its ring buffer is read
   }
   const uint64_t t2 = dbg ? stamp() : 0;

@@ -26,9 +26,9 @@ except Exception as e:
 PY
     [ $rc -eq 0 ] || { tail -20 gpurun_out/iter_${w}_${v}.err; exit $rc; }
     if [ "${STAMPS:-0}" = 1 ]; then
-      env $v KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
+      env $v KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline --no-latency ${BENCH_ARGS:-} \
         > /dev/null 2> gpurun_out/iter_stamps_${w}_${v}.err || exit 1
-      grep "stamps\] \(resolve\|round\|prologue\)" gpurun_out/iter_stamps_${w}_${v}.err | tail -4 | cut -c1-300
+      grep "stamps\] \(resolve cycles\|round\|device\)" gpurun_out/iter_stamps_${w}_${v}.err | tail -4 | cut -c1-400
     fi
   done
 done

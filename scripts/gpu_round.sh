@@ -47,7 +47,7 @@ else:  # the sequential cycle's workloads
 PY
   fi
   if has stamps; then
-    KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
+    KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline --no-latency ${BENCH_ARGS:-} \
       > gpurun_out/stamps_${R}_$w.json 2> gpurun_out/stamps_${R}_$w.err || { tail -20 gpurun_out/stamps_${R}_$w.err; exit 1; }
     grep "stamps\] resolve cycles" gpurun_out/stamps_${R}_$w.err | tail -1 | cut -c1-250
   fi
