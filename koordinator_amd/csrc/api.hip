@@ -212,8 +212,8 @@ struct koordhip_ctx {
   void *d_ext_scr = nullptr;        // the device-pod launches' table, arrival counters, pre-evaluation ring
   size_t ext_scr_cap = 0;
   hipStream_t xstream = nullptr;    // their streams (pooled: transient launches, one-workgroup waits):
-  hipStream_t xstream2 = nullptr;   // the pre-evaluations, the finals
-  hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr;
+  hipStream_t xstream2 = nullptr, xstream3 = nullptr;  // the pre-evaluations, the finals (alternating)
+  hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;
   bool last_ext_pipe = false;       // the last place call placed device pods inside the pipeline
   bool last_local = false;          // ... ran a node-sharded rank on the full table (class lists, no exchange)
   // class-incremental lists (cls.hip): the staged pods' classes (byte-identical
@@ -1288,13 +1288,14 @@ int koordhip_destroy(koordhip_ctx *c) {
     (void)hipStreamDestroy(c->stream2);
   }
   if (c->ev_eval2) (void)hipEventDestroy(c->ev_eval2);
-  for (hipStream_t xs : {c->xstream, c->xstream2})
+  for (hipStream_t xs : {c->xstream, c->xstream2, c->xstream3})
     if (xs) {
       (void)hipStreamSynchronize(xs);
       (void)hipStreamDestroy(xs);
     }
   if (c->ev_ext) (void)hipEventDestroy(c->ev_ext);
   if (c->ev_ext2) (void)hipEventDestroy(c->ev_ext2);
+  if (c->ev_ext3) (void)hipEventDestroy(c->ev_ext3);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->t0) (void)hipEventDestroy(c->t0);
   if (c->t1) (void)hipEventDestroy(c->t1);
@@ -2814,8 +2815,8 @@ int pmc_replay(koordhip_ctx *c) {
   if (mod != c->d_mod) HIP_TRY(hipFree(mod));
   if (lists != c->d_lists) HIP_TRY(hipFree(lists));
   std::fprintf(stderr, "[koordhip pmc replay] P %d lag %d: class lists %s (%zu builds, %d k_scan + k_cls_collect "
-               "launches, 1 k_cls_run of %zu workgroups), device pods %d (k_ext_pre + k_ext_final each)%s\n", P, lag,
-               cls ? "replayed" : "not used", cls ? c->plan_builds.size() : (size_t)0, nscan,
+               "launches, %d k_cls_run of %zu workgroups), device pods %d (k_ext_pre + k_ext_final each)%s\n", P, lag,
+               cls ? "replayed" : "not used", cls ? c->plan_builds.size() : (size_t)0, nscan, cls ? 1 : 0,
                cls ? c->cls_rep.size() : (size_t)0, ext ? ne : 0, err ? ": ERROR (a replayed kernel gave up)" : "");
   if (err) return fail(KOORDHIP_EDEVICE, "PMC replay: a replayed kernel reported an error");
   return 0;
@@ -2875,8 +2876,10 @@ int place_staged_impl(koordhip_ctx *c) {
       // others need its CU; pooled HIP streams (no more dedicated queues)
       HIP_TRY(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
       HIP_TRY(hipStreamCreateWithFlags(&c->xstream2, hipStreamNonBlocking));
+      HIP_TRY(hipStreamCreateWithFlags(&c->xstream3, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming));
     }
   }
   // the pipelined greedy allocates no device but the device pods' (k_ext_final):
@@ -2909,7 +2912,10 @@ int place_staged_impl(koordhip_ctx *c) {
   // section 6).  KOORDHIP_SHARD_FORCE keeps the exchange (A/B).
   const bool cls_fit = !c->cls_rep.empty() && c->nbins <= 32768 && !std::getenv("KOORDHIP_CLS_OFF") && !c->cu_reserve &&
                        (int64_t)c->cls_rep.size() <= c->n_cu / 2 && kh::cls_run_lds(c->n, c->monotone) <= 150 * 1024;
-  const bool local = c->world > 1 && !c->group && persistent && c->sel_split && wait_kernel && cls_fit &&
+  // (KOORDHIP_SHARD_LOCAL_SIM: a lone one-GPU context takes that decision as
+  // if it were a rank of a sharded job -- the path's one-GPU test)
+  const bool local_sim = c->world == 1 && !c->comm && std::getenv("KOORDHIP_SHARD_LOCAL_SIM") != nullptr;
+  const bool local = (c->world > 1 || local_sim) && !c->group && persistent && c->sel_split && wait_kernel && cls_fit &&
                      !std::getenv("KOORDHIP_SHARD_FORCE");
   c->last_local = local;
   const bool exch = (c->world > 1 || c->comm != nullptr) && !local;
@@ -3103,11 +3109,18 @@ int place_staged_impl(koordhip_ctx *c) {
     // The device pods: per pod e (round u) a pre-evaluation once the resolve
     // finished round u - lead (and the device commits of the device pods of
     // the rounds before that are published), and the exact placement at its
-    // hand-off -- transient launches, the pre-evaluations on xstream, the
-    // finals (with the device Reserve) on xstream2, each behind a
-    // one-workgroup wait on device flags, after the call's PipeSync /
-    // device-slot resets (ev_start).  Two streams let pre-evaluation e + 1 run
-    // while final e waits for its hand-off.  They are submitted in an order
+    // hand-off -- transient launches, the pre-evaluations on xstream behind a
+    // one-workgroup wait on device flags, the finals (with the device
+    // Reserve) on xstream2, each spinning in its own grid (seq.hip ext_spin:
+    // launched behind the previous final, so resident before its hand-off
+    // unless two device pods come close together), after the call's PipeSync
+    // / device-slot resets (ev_start).  Separate streams let pre-evaluation
+    // e + 1 run while final e waits for its hand-off.  (Finals alternating
+    // over a third pooled stream removed the late launches but measured 169 ms
+    // per step instead of 122 on config4dsmix: pooled streams share HIP's
+    // hardware queues, so a pre-evaluation queued behind a spinning final
+    // waited ~140 us; xstream3 is kept only for KOORDHIP_EXT_ALT A/B.)
+    // They are submitted in an order
     // whose every wait the launches before it satisfy, so they cannot deadlock
     // even where the two streams share one hardware queue: final(e) waits for
     // the hand-off of e (round u: the lists of rounds <= u and the finals of
@@ -3119,14 +3132,17 @@ int place_staged_impl(koordhip_ctx *c) {
     // the final's re-evaluated set.
     HIP_TRY(hipStreamWaitEvent(c->xstream, c->ev_start, 0));
     HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_start, 0));
+    HIP_TRY(hipStreamWaitEvent(c->xstream3, c->ev_start, 0));
     const char *ld = std::getenv("KOORDHIP_EXT_LEAD");
     const int32_t lead = std::max(lag, ld ? std::atoi(ld) : lag);
     const int32_t ne = (int32_t)c->ext_idx.size(), R = kh::ext_ring();
+    const bool alt = std::getenv("KOORDHIP_EXT_ALT") != nullptr;
     HIP_TRY(kh::launch_ext_begin(c->d, ne, c->d_ext_scr, c->xstream));
     c->last_ext_exec = (int64_t)ne * c->n;  // the pre-evaluations; the finals' re-evaluations on the device
     c->last_reev = kh::ext_reevals(c->d_ext_scr, ne, c->n);
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
     HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_ext, 0));  // (the zeroed flags)
+    HIP_TRY(hipStreamWaitEvent(c->xstream3, c->ev_ext, 0));
     auto u_of = [&](int32_t e) { return c->ext_idx[e] / P; };
     for (int32_t ip = 0, ifn = 0, needc = 0; ifn < ne;) {
       const bool can_pre = ip < ne && ifn >= ip - R + 1;
@@ -3139,12 +3155,13 @@ int place_staged_impl(koordhip_ctx *c) {
         const int32_t u = u_of(ifn);
         HIP_TRY(kh::launch_ext_final(c->dc, c->d, c->d_pods, c->d_podx, ifn, c->ext_idx[ifn], std::max(0, u - lead) * P,
                                      std::max(0, u - lag) * P, ne, c->d_ext_scr, c->d_out, c->d_devout, sync, c->d_dbg,
-                                     c->xstream2));
+                                     (alt && (ifn & 1)) ? c->xstream3 : c->xstream2));
         ifn++;
       }
     }
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
     HIP_TRY(hipEventRecord(c->ev_ext2, c->xstream2));
+    HIP_TRY(hipEventRecord(c->ev_ext3, c->xstream3));
   }
   for (int32_t r = 0; r < rounds && !cls; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
@@ -3192,6 +3209,7 @@ int place_staged_impl(koordhip_ctx *c) {
   if (ext_pipe && rounds > 0) {
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext, 0));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext2, 0));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext3, 0));
   }
   if (!serial) {
     HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));

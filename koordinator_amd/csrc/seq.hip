@@ -859,7 +859,9 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   if (spin) {
     if (t == 0) {
       if (blockIdx.x == 0) {
-        s_ok[1] = wait_at_least(&sy->ext_req, gp + 1, sy);
+        // the hand-off, and the previous device pod's Reserve published (the
+        // finals alternate between two streams: final e - 1 may still commit)
+        s_ok[1] = wait_at_least(&sy->ext_req, gp + 1, sy) && (e == 0 || wait_at_least(&fl[EXT_CDONE], e, sy));
         if (dbg) __hip_atomic_store(&dbg[100], realtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (s_ok[1]) __hip_atomic_store(&fl[EXT_GFIN], gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
@@ -1024,7 +1026,8 @@ __global__ void k_wait_ext_pre(PipeSync *sy, int32_t *fl, int32_t rounds, int32_
 // (ext_req = gp + 1) and the pod's pre-evaluation (e + 1 finished)
 __global__ void k_wait_ext_final(PipeSync *sy, int32_t *fl, int32_t want, int32_t pre) {
   if (threadIdx.x != 0) return;
-  if (wait_at_least(&sy->ext_req, want, sy)) (void)wait_at_least(&fl[EXT_PREDONE], pre, sy);
+  if (wait_at_least(&sy->ext_req, want, sy) && wait_at_least(&fl[EXT_PREDONE], pre, sy))
+    (void)(pre <= 1 || wait_at_least(&fl[EXT_CDONE], pre - 1, sy));  // (the previous device pod's Reserve)
 }
 
 // The pre-evaluation's node order: nodes holding device scalars (any xalloc

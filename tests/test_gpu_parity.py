@@ -300,6 +300,30 @@ def test_launch_modes_bit_exact(Engine, monkeypatch, mode, numa):
     assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
 
 
+# ------------------------------------------- node-sharded rank on class lists
+@pytest.mark.gpu
+def test_shard_local_fallback_bit_exact(Engine, monkeypatch):
+    """A rank of a node-sharded job whose batch the class-incremental lists
+    cover evaluates the full replica without the per-round exchange (api.hip
+    `local`: never slower than one GPU, DESIGN.md section 6);
+    KOORDHIP_SHARD_LOCAL_SIM takes that decision on one GPU.  The kernel stats
+    report it (KSTAT_LOCAL) and the placements equal the oracle's."""
+    from koordinator_amd import abi
+    monkeypatch.setenv("KOORDHIP_SHARD_LOCAL_SIM", "1")
+    prof = shipped_profile()
+    table = synth.make_cluster(synth.ClusterSpec(3000), prof)
+    pods = synth.make_pods(synth.StreamSpec(4000, be_frac=0.3), prof)
+    with Engine(prof, device=0) as e:
+        e.load_snapshot(table)
+        got = e.place_stream(pods)
+        ks = e.kernel_stats()
+        names = e.kernel_names()
+    assert int(ks["flags"]) & abi.KSTAT_LOCAL, ks
+    assert names["eval"].startswith("kh::k_cls_run"), names
+    ref = oracle.Oracle(to_c_config(prof), table).place_stream(pods)
+    assert np.array_equal(got, ref), int(np.flatnonzero(got != ref)[0])
+
+
 # ----------------------------------------------------- bench.py --gpus N's per-rank setup
 @pytest.mark.parametrize("workload", ["config4", "config5"])
 def test_torch_nccl_group_beside_library_comm(Engine, workload):
