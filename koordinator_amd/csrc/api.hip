@@ -2804,7 +2804,7 @@ int pmc_replay(koordhip_ctx *c) {
                                  c->stream));
       HIP_TRY(kh::launch_ext_final(c->dc, c->d, c->d_pods, c->d_podx, e, gp, std::max(0, u - lead) * P,
                                    std::max(0, u - lag) * P, ne, c->d_ext_scr, c->d_out, c->d_devout, sync, nullptr,
-                                   c->stream));
+                                   c->d_ext_idx, e, c->stream));
     }
   }
   HIP_TRY(hipMemcpyAsync(c->d_out, saved, (size_t)total * sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
@@ -2871,15 +2871,31 @@ int place_staged_impl(koordhip_ctx *c) {
       c->ext_scr_cap = xb;
     }
     if (!c->xstream) {
-      // The device pods' streams: transient launches only (a one-workgroup
-      // wait launch before each), so they hold no workgroup that waits while
-      // others need its CU; pooled HIP streams (no more dedicated queues)
-      HIP_TRY(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-      HIP_TRY(hipStreamCreateWithFlags(&c->xstream2, hipStreamNonBlocking));
-      HIP_TRY(hipStreamCreateWithFlags(&c->xstream3, hipStreamNonBlocking));
+      // The device pods' streams: transient launches only (the pre-evaluations
+      // behind one-workgroup waits on xstream, the finals spinning in their
+      // own small grid between the previous final and their hand-off on
+      // xstream2), two pooled streams created back to back (HIP deals pooled
+      // streams over its queues in turn, so they get two).  Measured on
+      // config4dsmix at lead 2: 114.2 ms per step; one stream for both
+      // (KOORDHIP_EXT_ONE, A/B) 130.2 -- a pre-evaluation enqueued ahead of a
+      // final keeps it from being resident before its hand-off (1,067 of 1,957
+      // finals late); two CU-masked streams (KOORDHIP_EXT_DEDICATED, A/B) 114.2
+      // but they add two hardware queues to the pipeline's three, and a lead-5
+      // run stalled into the watchdog.
+      if (std::getenv("KOORDHIP_EXT_DEDICATED")) {
+        const std::vector<uint32_t> all = full_cu_mask(c);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream, (uint32_t)all.size(), all.data()));
+        HIP_TRY(hipExtStreamCreateWithCUMask(&c->xstream2, (uint32_t)all.size(), all.data()));
+      } else {
+        HIP_TRY(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+        if (!std::getenv("KOORDHIP_EXT_ONE")) HIP_TRY(hipStreamCreateWithFlags(&c->xstream2, hipStreamNonBlocking));
+      }
+      if (std::getenv("KOORDHIP_EXT_ALT")) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->xstream3, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming));
+      }
       HIP_TRY(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming));
     }
   }
   // the pipelined greedy allocates no device but the device pods' (k_ext_final):
@@ -3109,45 +3125,42 @@ int place_staged_impl(koordhip_ctx *c) {
     // The device pods: per pod e (round u) a pre-evaluation once the resolve
     // finished round u - lead (and the device commits of the device pods of
     // the rounds before that are published), and the exact placement at its
-    // hand-off -- transient launches, the pre-evaluations on xstream behind a
-    // one-workgroup wait on device flags, the finals (with the device
-    // Reserve) on xstream2, each spinning in its own grid (seq.hip ext_spin:
-    // launched behind the previous final, so resident before its hand-off
-    // unless two device pods come close together), after the call's PipeSync
-    // / device-slot resets (ev_start).  Separate streams let pre-evaluation
-    // e + 1 run while final e waits for its hand-off.  (Finals alternating
-    // over a third pooled stream removed the late launches but measured 169 ms
-    // per step instead of 122 on config4dsmix: pooled streams share HIP's
-    // hardware queues, so a pre-evaluation queued behind a spinning final
-    // waited ~140 us; xstream3 is kept only for KOORDHIP_EXT_ALT A/B.)
-    // They are submitted in an order
-    // whose every wait the launches before it satisfy, so they cannot deadlock
-    // even where the two streams share one hardware queue: final(e) waits for
-    // the hand-off of e (round u: the lists of rounds <= u and the finals of
-    // the device pods before e, all earlier) and pre(e); pre(e) waits for
-    // rounds < u - lead (the finals of the device pods of those rounds come
-    // before it: a final of round u' precedes a pre whose wait round exceeds
-    // u') and follows final(e - RING), whose ring buffer it reuses.  lead: the
-    // rounds between lag and lead add their commits, from the commit log, to
-    // the final's re-evaluated set.
+    // hand-off -- transient launches (streams: see their creation): the
+    // pre-evaluations behind a one-workgroup wait on device flags on xstream,
+    // the finals (with the device Reserve) on xstream2, spinning in their own grid
+    // (seq.hip ext_spin: resident before the hand-off unless two device pods
+    // come close together), after the call's PipeSync / device-slot resets
+    // (ev_start).  They are submitted in an order whose every wait the
+    // launches before it satisfy, so they cannot deadlock even where the two
+    // streams share one in-order queue:
+    // final(e) waits for the hand-off of e (round u: the lists of rounds <= u
+    // and the finals of the device pods before e, all earlier), pre(e) and the
+    // previous pod's Reserve; pre(e) waits for rounds < u - lead (the finals of
+    // the device pods of those rounds come before it: a final of round u'
+    // precedes a pre whose wait round exceeds u') and follows final(e - RING),
+    // whose ring buffer it reuses.  lead: the rounds between lag and lead add
+    // their commits, from the commit log, to the final's re-evaluated set.
     HIP_TRY(hipStreamWaitEvent(c->xstream, c->ev_start, 0));
-    HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_start, 0));
-    HIP_TRY(hipStreamWaitEvent(c->xstream3, c->ev_start, 0));
+    hipStream_t xs2 = c->xstream2 ? c->xstream2 : c->xstream;  // the finals' stream
+    if (c->xstream2) HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_start, 0));
+    if (c->xstream3) HIP_TRY(hipStreamWaitEvent(c->xstream3, c->ev_start, 0));
     const char *ld = std::getenv("KOORDHIP_EXT_LEAD");
     const int32_t lead = std::max(lag, ld ? std::atoi(ld) : lag);
     const int32_t ne = (int32_t)c->ext_idx.size(), R = kh::ext_ring();
-    const bool alt = std::getenv("KOORDHIP_EXT_ALT") != nullptr;
+    const bool alt = c->xstream3 != nullptr;  // (KOORDHIP_EXT_ALT at the streams' creation)
     HIP_TRY(kh::launch_ext_begin(c->d, ne, c->d_ext_scr, c->xstream));
     c->last_ext_exec = (int64_t)ne * c->n;  // the pre-evaluations; the finals' re-evaluations on the device
     c->last_reev = kh::ext_reevals(c->d_ext_scr, ne, c->n);
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
-    HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_ext, 0));  // (the zeroed flags)
-    HIP_TRY(hipStreamWaitEvent(c->xstream3, c->ev_ext, 0));
+    if (c->xstream2) HIP_TRY(hipStreamWaitEvent(c->xstream2, c->ev_ext, 0));  // (the zeroed flags)
+    if (c->xstream3) HIP_TRY(hipStreamWaitEvent(c->xstream3, c->ev_ext, 0));
     auto u_of = [&](int32_t e) { return c->ext_idx[e] / P; };
+    std::vector<int32_t> pre_needc(ne, 0);  // per device pod the device commits its pre-evaluation waited for
     for (int32_t ip = 0, ifn = 0, needc = 0; ifn < ne;) {
       const bool can_pre = ip < ne && ifn >= ip - R + 1;
       if (can_pre && (ip <= ifn || u_of(ip) - lead < u_of(ifn))) {
         while (needc < ip && u_of(needc) < u_of(ip) - lead) needc++;  // device pods of the rounds < u - lead
+        pre_needc[ip] = needc;
         HIP_TRY(kh::launch_ext_pre(c->dc, c->d, c->d_pods, c->d_podx, ip, c->ext_idx[ip], u_of(ip) - lead, needc, ne,
                                    c->d_ext_scr, sync, c->xstream));
         ip++;
@@ -3155,13 +3168,13 @@ int place_staged_impl(koordhip_ctx *c) {
         const int32_t u = u_of(ifn);
         HIP_TRY(kh::launch_ext_final(c->dc, c->d, c->d_pods, c->d_podx, ifn, c->ext_idx[ifn], std::max(0, u - lead) * P,
                                      std::max(0, u - lag) * P, ne, c->d_ext_scr, c->d_out, c->d_devout, sync, c->d_dbg,
-                                     (alt && (ifn & 1)) ? c->xstream3 : c->xstream2));
+                                     c->d_ext_idx, pre_needc[ifn], (alt && (ifn & 1)) ? c->xstream3 : xs2));
         ifn++;
       }
     }
     HIP_TRY(hipEventRecord(c->ev_ext, c->xstream));
-    HIP_TRY(hipEventRecord(c->ev_ext2, c->xstream2));
-    HIP_TRY(hipEventRecord(c->ev_ext3, c->xstream3));
+    if (c->xstream2) HIP_TRY(hipEventRecord(c->ev_ext2, c->xstream2));
+    if (c->xstream3) HIP_TRY(hipEventRecord(c->ev_ext3, c->xstream3));
   }
   for (int32_t r = 0; r < rounds && !cls; r++) {
     const int32_t p0 = r * P, np = std::min(P, total - p0);
@@ -3208,8 +3221,8 @@ int place_staged_impl(koordhip_ctx *c) {
   }
   if (ext_pipe && rounds > 0) {
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext, 0));
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext2, 0));
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext3, 0));
+    if (c->xstream2) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext2, 0));
+    if (c->xstream3) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_ext3, 0));
   }
   if (!serial) {
     HIP_TRY(hipEventRecord(c->ev_res[0], c->rstream));
@@ -3272,8 +3285,12 @@ int place_staged_impl(koordhip_ctx *c) {
                    q[11] / nc, q[12] / nc);
     }
     {
-      uint64_t q[4] = {0, 0, 0, 0};
+      uint64_t q[4] = {0, 0, 0, 0}, rw[3] = {0, 0, 0};
       HIP_TRY(hipMemcpy(q, c->d_dbg + 90, sizeof(q), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(rw, c->d_dbg + 107, sizeof(rw), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[koordhip stamps] chain re-walks: walk + keys %llu  winners' rows %llu cycles | winner rows "
+                   "loaded from HBM %llu\n", (unsigned long long)rw[0], (unsigned long long)rw[1],
+                   (unsigned long long)rw[2]);
       std::fprintf(stderr, "[koordhip stamps] chained decisions: %llu cycles, %llu pods resolved | claim tables %llu  "
                    "re-walks %llu  re-check + closure %llu  final table %llu\n", (unsigned long long)h[62],
                    (unsigned long long)h[63], (unsigned long long)q[0], (unsigned long long)q[1],

@@ -2020,6 +2020,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t c_gc[3] = {0, 0, 0}, n_ghit = 0;          // general commit: row source, Reserve delta, voiding + outputs; winners in M
   uint64_t c_chain = 0;                              // chained decisions: cycles (pods resolved: dbg[63])
   uint64_t c_ch[4] = {0, 0, 0, 0};                   // ... split: claim tables, re-walks, re-check + closure, final table
+  uint64_t c_rw[2] = {0, 0}, n_chbm = 0;             // ... re-walks: walk + keys, winners' rows; chain HBM row loads
   uint64_t c_ext = 0, n_ext = 0;                     // device pods: cycles from the hand-off to the worker's answer, pods
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
@@ -2386,6 +2387,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           if (!conf) break;
           bool resolved = false;
           while (conf) {  // eight conflicting pods at a time, eight lanes (entries) each
+            const uint64_t t_g = dbg ? stamp() : 0;
+            bool hbm = false;
             const int gq = lane >> 3, q = lane & 7;
             uint64_t cm = conf;
             for (int k = 0; k < gq && cm; k++) cm &= cm - 1ull;
@@ -2431,6 +2434,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               mx = o > mx ? o : mx;
               dm |= shfl_xor_u64(dm, m);
             }
+            const uint64_t t_k = dbg ? stamp() : 0;
             const bool win = walked && key == mx && mx != 0;
             // the new winner is a valid claimer's node: two commits to one node (general path)
             const bool rep = ((uint32_t)(__ballot(win && clv) >> g8) & 0xFFu) != 0u;
@@ -2445,6 +2449,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                   src = l * HP + q;
                 } else {
                   src = l * HP;
+                  hbm = true;
                   NV v;
                   load_row(v, nodes(), nd);
                   pre[src] = v;
@@ -2468,6 +2473,12 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             }
             resolved = resolved || (__ballot(ok2) != 0ull);
             wsync();
+            if (dbg) {
+              const uint64_t t_s = stamp();
+              c_rw[0] += t_k - t_g;
+              c_rw[1] += t_s - t_k;
+              n_chbm += __popcll(__ballot(hbm));
+            }
           }
           clap(1);
           if (!resolved) break;
@@ -3168,6 +3179,9 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[61], (unsigned long long)n_ghit);
     atomicAdd((unsigned long long *)&dbg[62], (unsigned long long)c_chain);
     for (int q = 0; q < 4; q++) atomicAdd((unsigned long long *)&dbg[90 + q], (unsigned long long)c_ch[q]);
+    atomicAdd((unsigned long long *)&dbg[107], (unsigned long long)c_rw[0]);
+    atomicAdd((unsigned long long *)&dbg[108], (unsigned long long)c_rw[1]);
+    atomicAdd((unsigned long long *)&dbg[109], (unsigned long long)n_chbm);
     atomicAdd((unsigned long long *)&dbg[30], (unsigned long long)c_ext);
     atomicAdd((unsigned long long *)&dbg[31], (unsigned long long)n_ext);
   }

@@ -70,9 +70,13 @@ const uint32_t *ext_reevals(const void *scratch, int32_t n_ext, int32_t n);
 hipError_t launch_ext_pre(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t e,
                           int32_t gp, int32_t rounds, int32_t needc, int32_t n_ext, void *scratch, PipeSync *sync,
                           hipStream_t s);
+// (ext_idx: the device pods' staged indices on the device; dlo: the `needc`
+// pre-evaluation e waited for -- the device pods [dlo, e) may have committed
+// after it read their nodes, which the final then evaluates in full)
 hipError_t launch_ext_final(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t e,
                             int32_t gp, int32_t xlo, int32_t xhi, int32_t n_ext, void *scratch, int32_t *out_node,
-                            uint32_t *out_dev, PipeSync *sync, uint64_t *dbg, hipStream_t s);
+                            uint32_t *out_dev, PipeSync *sync, uint64_t *dbg, const int32_t *ext_idx, int32_t dlo,
+                            hipStream_t s);
 hipError_t launch_mark_ext(DevPod *pods, const int32_t *idx, int32_t n, hipStream_t s);
 // the k_seq instantiation launch_seq runs for this config, as rocprofv3 names it
 const char *seq_kernel_name(const DevCfg &c, const DevNodes &d);

@@ -616,6 +616,7 @@ constexpr int32_t EXT_PCHUNK = EXT_THREADS;      // pre-evaluation chunk: one no
 constexpr int EXT_FNPT = 4;                      // final chunk: four nodes per thread (two loads each)
 constexpr int32_t EXT_FCHUNK = EXT_THREADS * EXT_FNPT;
 constexpr int EXT_RING = 4;   // pre-evaluation buffers: device pods evaluated ahead of their hand-off
+constexpr int EXT_DMAX = 32;  // device pods a final tracks as possibly missed by its pre-evaluation
 
 // DeviceShare's Reserve of a device pod on node w without the Fit / LoadAware
 // row (seq_commit_body<0, false>: dev_reserve, allocator.go:91-122, then
@@ -812,7 +813,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
                                                            int32_t *__restrict__ br, int32_t *__restrict__ out_node,
                                                            uint32_t *__restrict__ out_dev, int32_t e,
                                                            int32_t *__restrict__ fl, PipeSync *sy, uint64_t *dbg,
-                                                           int32_t spin) {
+                                                           int32_t spin, const int32_t *__restrict__ ext_idx,
+                                                           int32_t dlo) {
   __shared__ uint64_t lt[EXT_RAW];
   __shared__ uint32_t xm[EXT_FCHUNK / 32];  // the chunk's X nodes
   __shared__ int32_t s_red[SEQ_THREADS / 64][8];
@@ -820,6 +822,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   __shared__ int32_t s_last;
   __shared__ uint32_t s_nre;
   __shared__ int32_t s_ok[2];
+  __shared__ int32_t s_dn[EXT_DMAX];  // the nodes of the device pods [dlo, e): committed maybe after the pre-evaluation read
+  __shared__ int32_t s_nd;
   const int t = threadIdx.x;
   const int32_t c0 = (int32_t)blockIdx.x * EXT_FCHUNK;
   // spin: the grid is resident before the hand-off (launched behind the
@@ -887,7 +891,12 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
   for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
   for (int32_t w = t; w < EXT_FCHUNK / 32; w += EXT_THREADS) xm[w] = 0u;
-  if (t == 0) s_nre = 0u;
+  if (t == 0) {
+    s_nre = 0u;
+    s_nd = e - dlo <= EXT_DMAX ? e - dlo : -1;  // (-1: too many, every re-evaluation in full)
+  }
+  if (t < e - dlo && t < EXT_DMAX)  // (published before this pod's hand-off)
+    s_dn[t] = __hip_atomic_load(&out_node[ext_idx[dlo + t]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const int32_t nx = xl[0];
   for (int32_t q = t; q < nx; q += EXT_THREADS) {
@@ -907,11 +916,27 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     // infeasible then (every Filter of the plain build is monotone in the
     // commits of the batch -- Fit / LoadAware requests, DeviceShare's device
     // usage and the extended scalars only grow -- so it still is)
+    //
+    // A node no device pod committed to since the pre-evaluation read it keeps
+    // its device rows and extended scalars (only device pods change them):
+    // its DeviceShare Filter / raw score and extended-scalar Fit stand, and
+    // only the row part -- seq_eval's eval_total over the Fit / LoadAware row,
+    // one row load -- is evaluated again.  The nodes of the device pods the
+    // pre-evaluation may have missed (s_dn) are evaluated in full.
     if (i < d.n && kv[k] != 0ull && ((xm[y >> 5] >> (y & 31)) & 1u)) {
-      int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
-      const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
-      kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
-      rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
+      bool full = s_nd < 0;
+      for (int32_t j = 0; j < s_nd; j++) full = full || s_dn[j] == i;
+      if (full) {
+        int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
+        const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
+        kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
+        rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
+      } else {
+        NV v{};
+        load_node(v, d, i, need_all(c), c);
+        const int32_t tk = eval_total(p, v, c);
+        kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
+      }
       atomicAdd(&s_nre, 1u);
     }
   }
@@ -1150,7 +1175,8 @@ hipError_t launch_ext_pre(const DevCfg &c, const DevNodes &d, const DevPod *pods
 
 hipError_t launch_ext_final(const DevCfg &c, const DevNodes &d, const DevPod *pods, const DevPodX *podx, int32_t e,
                             int32_t gp, int32_t xlo, int32_t xhi, int32_t n_ext, void *scratch, int32_t *out_node,
-                            uint32_t *out_dev, PipeSync *sync, uint64_t *dbg, hipStream_t s) {
+                            uint32_t *out_dev, PipeSync *sync, uint64_t *dbg, const int32_t *ext_idx, int32_t dlo,
+                            hipStream_t s) {
   if (seq_mode(c) != 0) return hipErrorInvalidValue;
   const ExtScr x = ext_scr(scratch, n_ext, d.n);
   const size_t nn = (size_t)std::max(d.n, 1);
@@ -1158,7 +1184,8 @@ hipError_t launch_ext_final(const DevCfg &c, const DevNodes &d, const DevPod *po
   if (!spin) hipLaunchKernelGGL(k_wait_ext_final, dim3(1), dim3(64), 0, s, sync, x.fl, gp + 1, e + 1);
   hipLaunchKernelGGL(k_ext_final<0>, dim3((d.n + EXT_FCHUNK - 1) / EXT_FCHUNK), dim3(EXT_THREADS), 0, s, c, d, pods,
                      podx, gp, xlo, xhi, x.tab, x.arrive + e, x.pk + (size_t)(e % EXT_RING) * nn,
-                     x.pr + (size_t)(e % EXT_RING) * nn, out_node, out_dev, e, x.fl, sync, dbg, spin);
+                     x.pr + (size_t)(e % EXT_RING) * nn, out_node, out_dev, e, x.fl, sync, dbg, spin, ext_idx,
+                     std::min(std::max(dlo, 0), e));
   return hipGetLastError();
 }
 
