@@ -3305,8 +3305,10 @@ int place_staged_impl(koordhip_ctx *c) {
                    "%.0f | last workgroup: decide + publish %.0f  device commit %.0f\n",
                    (unsigned long long)h[31], (unsigned long long)h[30], h[31] ? (double)h[30] / h[31] : 0.0,
                    q[0] / np, q[3] / np, q[4] / np);
-      uint64_t r[12];
+      uint64_t r[16];
       HIP_TRY(hipMemcpy(r, c->d_dbg + 96, sizeof(r), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[koordhip stamps] device-pod finals: workgroups with a full (device) re-evaluation %llu, "
+                   "their re-evaluation %.2f us each\n", (unsigned long long)r[14], r[14] ? r[15] * 0.01 / r[14] : 0.0);
       const double nb = (double)std::max<uint64_t>(r[10], 1);
       std::fprintf(stderr, "[koordhip stamps] device-pod finals, us: request seen -> last workgroup arrived %.2f per pod | "
                    "per workgroup: -> gate seen %.2f  X marked %.2f  re-evaluated %.2f  folded + arrived %.2f\n",

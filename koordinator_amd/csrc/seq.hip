@@ -860,6 +860,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     kv[k] = i < d.n ? __hip_atomic_load(&bk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     rv[k] = i < d.n ? __hip_atomic_load(&br[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   }
+  // the staged indices of the device pods [dlo, e) (static: before the hand-off)
+  const int32_t gi = (t < e - dlo && t < EXT_DMAX) ? ext_idx[dlo + t] : -1;
   if (spin) {
     if (t == 0) {
       if (blockIdx.x == 0) {
@@ -889,18 +891,23 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   const int32_t *xl = pipe_xlist(sy);
   const int32_t wdev = (c.score & KOORDHIP_PLUGIN_DEVICESHARE) ? c.w_ext[0] : 0;
   const bool dev = ((c.filt | c.score) & KOORDHIP_PLUGIN_DEVICESHARE) != 0;
+  // one round trip for X's count and nodes (read speculatively: X <= kPipeXMax
+  // < EXT_THREADS nodes) and the nodes of the device pods [dlo, e) (published
+  // before this pod's hand-off)
+  static_assert(kPipeXMax <= EXT_THREADS, "one X node per thread");
+  const int32_t nx = xl[0];
+  const int32_t xv = t < kPipeXMax ? xl[1 + t] : -1;
+  const int32_t dn = gi >= 0 ? __hip_atomic_load(&out_node[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
   for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
   for (int32_t w = t; w < EXT_FCHUNK / 32; w += EXT_THREADS) xm[w] = 0u;
   if (t == 0) {
     s_nre = 0u;
     s_nd = e - dlo <= EXT_DMAX ? e - dlo : -1;  // (-1: too many, every re-evaluation in full)
   }
-  if (t < e - dlo && t < EXT_DMAX)  // (published before this pod's hand-off)
-    s_dn[t] = __hip_atomic_load(&out_node[ext_idx[dlo + t]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  const int32_t nx = xl[0];
-  for (int32_t q = t; q < nx; q += EXT_THREADS) {
-    const int32_t y = xl[1 + q] - c0;
+  if (gi >= 0) s_dn[t] = dn;
+  if (t < nx) {
+    const int32_t y = xv - c0;
     if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
   }
   for (int32_t q = xlo + t; q < xhi; q += EXT_THREADS) {
@@ -909,6 +916,7 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   }
   __syncthreads();
   if (dbg && t == 0) tm = realtime();
+  int32_t s_fullw = 0;  // (dbg: this thread evaluated a node in full)
 #pragma unroll 1
   for (int k = 0; k < EXT_FNPT; k++) {
     const int32_t y = k * EXT_THREADS + t, i = c0 + y;
@@ -927,6 +935,7 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
       bool full = s_nd < 0;
       for (int32_t j = 0; j < s_nd; j++) full = full || s_dn[j] == i;
       if (full) {
+        s_fullw = 1;
         int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
         const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
         kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
@@ -944,6 +953,7 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     __syncthreads();
     if (t == 0) te = realtime();
   }
+  const bool anyfull = dbg && __syncthreads_or(s_fullw) != 0;
 #pragma unroll
   for (int k = 0; k < EXT_FNPT; k++)
     if (kv[k]) atomicMax(&lt[rv[k]], kv[k]);
@@ -966,6 +976,10 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
       atomicAdd((unsigned long long *)&dbg[104], (unsigned long long)(te - tm));
       atomicAdd((unsigned long long *)&dbg[105], (unsigned long long)(ta - te));
       atomicAdd((unsigned long long *)&dbg[106], 1ull);
+      if (anyfull) {  // [110] / [111] workgroups with a full re-evaluation, their re-evaluation time
+        atomicAdd((unsigned long long *)&dbg[110], 1ull);
+        atomicAdd((unsigned long long *)&dbg[111], (unsigned long long)(te - tm));
+      }
       if (s_last) atomicAdd((unsigned long long *)&dbg[101], (unsigned long long)(ta - ts));
     }
   }
