@@ -623,6 +623,45 @@ def test_operating_mode_pod_is_a_reservation():
     assert not int(inf.table(NOW)["resv_flags"][2])
 
 
+def test_operating_mode_pod_cpuset_is_the_slot_reserved_cpus():
+    """an operating-mode pod holding a cpuset (its
+    resource-status allocation) is a reservation whose reserved CPUs are that
+    cpuset, less the CPUs of the pods it admitted (its current owners'
+    allocations) -- nodenumaresource/reservation.go:76-113 -- so a matching
+    cpuset pod takes them first."""
+    import json as _json
+    from koordinator_amd import numa as nm
+    from koordinator_amd import reservation as rv
+    rng = np.random.default_rng(5)
+    prof = shipped_profile(numa=True, reservation=True)
+    nodes = [k8s.Node(name=f"n{i}", allocatable={k8s.CPU: k8s.Q(32), k8s.MEMORY: k8s.Q(64 * GI), k8s.PODS: k8s.Q(110)})
+             for i in range(3)]
+    inf = Informer(prof, nodes, NOW)
+    for n in nodes:
+        inf.on_nrt(_nrt(rng, n.name))
+    owners = [{"labelSelector": {"matchLabels": {"app": "web"}}}]
+    op = k8s.Pod(name="op-0", uid="op0", node_name="n1",
+                 labels={rv.LABEL_POD_OPERATING_MODE: "Reservation"},
+                 annotations={rv.ANNOTATION_RESERVATION_OWNERS: _json.dumps(owners),
+                              nm.ANNOTATION_RESOURCE_STATUS: _json.dumps({"cpuset": "4-7"})},
+                 containers=[k8s.Container(requests={k8s.CPU: k8s.Q(4), k8s.MEMORY: k8s.Q(4 * GI)})])
+    inf.on_pod_add(op, NOW)
+    t = inf.table(NOW)
+    topo = nm.linux_topology(2, 1, 8, 2)
+    assert int(t["resv_flags"][1]) and [int(t[f"resv_cpus{w}"][1]) for w in range(4)] == \
+        [int(x) for x in topo.mask([4, 5, 6, 7])]
+    # a current owner holding CPUs 4-5 of them: the slot keeps 6-7
+    web = k8s.Pod(name="web-1", uid="w1", node_name="n1", labels={"app": "web"},
+                  annotations={nm.ANNOTATION_RESOURCE_STATUS: _json.dumps({"cpuset": "4-5"})},
+                  containers=[k8s.Container(requests={k8s.CPU: k8s.Q(2), k8s.MEMORY: k8s.Q(GI)})])
+    inf.on_pod_add(web, NOW)
+    op2 = copy.deepcopy(op)
+    op2.annotations[rv.ANNOTATION_RESERVATION_CURRENT_OWNER] = _json.dumps({"name": "web-1", "namespace": "default"})
+    inf.on_pod_update(op, op2, NOW)
+    t2 = inf.table(NOW)
+    assert [int(t2[f"resv_cpus{w}"][1]) for w in range(4)] == [int(x) for x in topo.mask([6, 7])]
+
+
 def test_operating_mode_pods_outside_the_envelope_stay_plain_pods():
     """a bound operating-mode pod whose requests the engine
     cannot hold as a reservation slot (ephemeral-storage, or nvidia.com/gpu
