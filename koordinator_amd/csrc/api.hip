@@ -3285,11 +3285,12 @@ int place_staged_impl(koordhip_ctx *c) {
                    q[11] / nc, q[12] / nc);
     }
     {
-      uint64_t q[4] = {0, 0, 0, 0}, rw[3] = {0, 0, 0};
+      uint64_t q[4] = {0, 0, 0, 0}, rw[7] = {0, 0, 0, 0, 0, 0, 0};
       HIP_TRY(hipMemcpy(q, c->d_dbg + 90, sizeof(q), hipMemcpyDeviceToHost));
       HIP_TRY(hipMemcpy(rw, c->d_dbg + 107, sizeof(rw), hipMemcpyDeviceToHost));
-      std::fprintf(stderr, "[koordhip stamps] chain re-walks: walk + keys %llu  winners' rows %llu cycles | winner rows "
-                   "loaded from HBM %llu\n", (unsigned long long)rw[0], (unsigned long long)rw[1],
+      std::fprintf(stderr, "[koordhip stamps] chain re-walks: walk + keys %llu (entries + claims %llu, row + evaluation "
+                   "%llu)  winners' rows %llu cycles | winner rows loaded from HBM %llu\n", (unsigned long long)rw[0],
+                   (unsigned long long)rw[5], (unsigned long long)rw[6], (unsigned long long)rw[1],
                    (unsigned long long)rw[2]);
       std::fprintf(stderr, "[koordhip stamps] chained decisions: %llu cycles, %llu pods resolved | claim tables %llu  "
                    "re-walks %llu  re-check + closure %llu  final table %llu\n", (unsigned long long)h[62],

@@ -1940,6 +1940,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   __shared__ int32_t seg_w[RES_MAXP_ROUND];  // staged winners by M slot (bulk commits)
   __shared__ int32_t ckey[RES_HASH], cval[RES_HASH];  // staged winner -> first pod (conflict detection)
   __shared__ int32_t sh_mp, sh_stop, sh_done, sh_chain;
+  __shared__ uint64_t sh_rsv;  // the chained decisions: pods resolved in the current pass
   const int t = threadIdx.x, lane = lane_id();
   const int32_t words = (n_nodes + 31) >> 5;
   const int32_t HP = max(1, RES_PRE / P);  // prefetched list heads per pod
@@ -2020,7 +2021,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
   uint64_t c_gc[3] = {0, 0, 0}, n_ghit = 0;          // general commit: row source, Reserve delta, voiding + outputs; winners in M
   uint64_t c_chain = 0;                              // chained decisions: cycles (pods resolved: dbg[63])
   uint64_t c_ch[4] = {0, 0, 0, 0};                   // ... split: claim tables, re-walks, re-check + closure, final table
-  uint64_t c_rw[2] = {0, 0}, n_chbm = 0;             // ... re-walks: walk + keys, winners' rows; chain HBM row loads
+  uint64_t c_rw[4] = {0, 0, 0, 0}, n_chbm = 0;             // ... re-walks: walk + keys, winners' rows; chain HBM row loads
   uint64_t c_ext = 0, n_ext = 0;                     // device pods: cycles from the hand-off to the worker's answer, pods
   // ---- a round's global reads: lists -> LDS (stride kp, zero padded), pod
   //      records, and the rows of each pod's first HP list entries (slot HP j + q)
@@ -2386,6 +2387,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           uint64_t conf = __ballot(lane < n_pods && dec_c[lane] == 1);
           if (!conf) break;
           bool resolved = false;
+          if (lane == 0) sh_rsv = 0ull;
+          wsync();
           while (conf) {  // eight conflicting pods at a time, eight lanes (entries) each
             const uint64_t t_g = dbg ? stamp() : 0;
             bool hbm = false;
@@ -2407,6 +2410,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             const int f = bx ? __builtin_ctz(bx) : RES_WE, z = bz ? __builtin_ctz(bz) : RES_WE;
             const bool general = f == RES_WE && z == RES_WE;
             const bool walked = live && !general && (q < min(f, z) || (q == f && f < z));
+            const uint64_t t_wk = dbg ? stamp() : 0;
             uint64_t key = 0;
             if (walked) {
               if (q < min(f, z)) {  // a modified entry: its key on the row it will have
@@ -2426,6 +2430,12 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
               } else {
                 key = e;
               }
+            }
+            if (dbg) {  // (every lane's key done)
+              asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+              const uint64_t t_ev = stamp();
+              c_rw[2] += t_wk - t_g;
+              c_rw[3] += t_ev - t_wk;
             }
             uint64_t mx = key, dm = (walked && clv) ? (1ull << cl) : 0ull;
 #pragma unroll
@@ -2468,6 +2478,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
                 if (mx == 0) dec_src[l] = 0;
                 dep[l] = dm;
                 dec_c[l] = 0;
+                atomicOr((unsigned long long *)&sh_rsv, (unsigned long long)(1ull << l));
                 if (dbg) atomicAdd((unsigned long long *)&dbg[63], 1ull);
               }
             }
@@ -2482,21 +2493,26 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           }
           clap(1);
           if (!resolved) break;
-          // re-check: a valid pod whose walk meets a valid claim it did not assume
-          claims();
+          // re-check: a valid pod whose walk meets the new winner of a pod
+          // resolved in this pass that it did not assume -- the only claims
+          // that changed: every other valid walk met no earlier claim in 2b,
+          // and a re-walk assumed every valid claimer it met.  (Where two pods
+          // resolved in one pass took one node, both are checked, not only the
+          // first: at most an extra general-path pod, never another placement.)
           bool inv = false;
-          for (int32_t x0 = 0; x0 < n_pods * RES_WE; x0 += 64) {
-            const int32_t x = x0 + lane, l2 = x / RES_WE;
-            const int32_t y = x < n_pods * RES_WE ? dec_e[x] : -1;
-            bool bad = false;
-            if (y >= 0 && dec_c[l2] == 0) {
-              const int32_t cl2 = claimer_of(y);
-              bad = cl2 < l2 && !((dep[l2] >> cl2) & 1ull);
+          for (uint64_t rm = sh_rsv; rm; rm &= rm - 1ull) {
+            const int32_t r = (int32_t)__builtin_ctzll(rm);
+            const uint64_t kr = dec_key[r];
+            if (kr == 0ull) continue;
+            const int32_t wr = key_node(kr);
+            for (int32_t x0 = (r + 1) * RES_WE; x0 < n_pods * RES_WE; x0 += 64) {
+              const int32_t x = x0 + lane, l2 = x / RES_WE;
+              const bool bad = x < n_pods * RES_WE && dec_e[x] == wr && dec_c[l2] == 0 && !((dep[l2] >> r) & 1ull);
               if (bad) atomicOr(&dec_c[l2], 1);
+              inv = inv || __ballot(bad) != 0ull;
             }
-            inv = inv || __ballot(bad) != 0ull;
+            wsync();
           }
-          wsync();
           {  // closure in pod order: a pod assuming an invalid pod's commit is invalid
             const bool lv = lane < n_pods;
             const uint64_t dl = lv ? dep[lane] : 0ull;
@@ -2510,7 +2526,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
             }
           }
           wsync();
-          fresh = !inv;  // (an invalidated pod's claim is still in the table)
+          fresh = false;  // (the resolved pods' new claims are not in the table)
           clap(2);
         }
         if (!fresh) claims();  // the loop's claimer(): the valid pods' winners
@@ -3182,6 +3198,8 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
     atomicAdd((unsigned long long *)&dbg[107], (unsigned long long)c_rw[0]);
     atomicAdd((unsigned long long *)&dbg[108], (unsigned long long)c_rw[1]);
     atomicAdd((unsigned long long *)&dbg[109], (unsigned long long)n_chbm);
+    atomicAdd((unsigned long long *)&dbg[112], (unsigned long long)c_rw[2]);
+    atomicAdd((unsigned long long *)&dbg[113], (unsigned long long)c_rw[3]);
     atomicAdd((unsigned long long *)&dbg[30], (unsigned long long)c_ext);
     atomicAdd((unsigned long long *)&dbg[31], (unsigned long long)n_ext);
   }
