@@ -2364,9 +2364,31 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           for (;;) {
             const int32_t xk = ckey[q];
             if (xk == y) return cval[q];
-            if (xk < 0) return 64;
+            if (xk == -1) return 64;  // (-2: a removed claim, probe on)
             q = (q + 1) & (RES_HASH - 1);
           }
+        };
+        // the first pass's claims from 2b's table (every non-slow pod's staged
+        // winner -> its first claimer): drop the nodes whose first claimer
+        // conflicts -- every later claimer of such a node met that claim on its
+        // own walk (its winner is a walked entry), so it conflicts too, and the
+        // table then holds exactly the valid pods' claims (a tombstone, -2,
+        // keeps the probe chains)
+        auto drop_conflicting = [&]() {
+          if (lane < n_pods && dec_c[lane] == 1 && dec_key[lane] != 0ull) {
+            const int32_t y = key_node(dec_key[lane]);
+            uint32_t q = res_hash(y);
+            for (;;) {
+              const int32_t xk = ckey[q];
+              if (xk == y) {
+                if (cval[q] == lane) ckey[q] = -2;
+                break;
+              }
+              if (xk == -1) break;
+              q = (q + 1) & (RES_HASH - 1);
+            }
+          }
+          wsync();
         };
         // passes: monotone bits 2-3 (KOORDHIP_CHAIN_PASSES), else RES_CHAIN_PASSES;
         // fresh: ckey / cval hold exactly the valid pods' claims
@@ -2381,7 +2403,12 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           }
         };
         for (int pass = 0; pass < npass; pass++) {
-          if (!fresh) claims();
+          if (!fresh) {
+            if (pass == 0)
+              drop_conflicting();
+            else
+              claims();
+          }
           fresh = true;
           clap(0);
           uint64_t conf = __ballot(lane < n_pods && dec_c[lane] == 1);
@@ -2604,7 +2631,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         for (;;) {
           const int32_t xk = ckey[q];
           if (xk == y) return cval[q];
-          if (xk < 0) return 64;
+          if (xk == -1) return 64;  // (-2: a claim the chained decisions dropped)
           q = (q + 1) & (RES_HASH - 1);
         }
       };
