@@ -823,7 +823,8 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   __shared__ uint32_t s_nre;
   __shared__ int32_t s_ok[2];
   __shared__ int32_t s_dn[EXT_DMAX];  // the nodes of the device pods [dlo, e): committed maybe after the pre-evaluation read
-  __shared__ int32_t s_nd;
+  __shared__ int32_t s_dok[EXT_DMAX], s_draw[EXT_DMAX];  // ... their DeviceShare / extended-scalar part for this pod
+  __shared__ int32_t s_nd, s_cd;
   const int t = threadIdx.x;
   const int32_t c0 = (int32_t)blockIdx.x * EXT_FCHUNK;
   // spin: the grid is resident before the hand-off (launched behind the
@@ -860,8 +861,35 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     kv[k] = i < d.n ? __hip_atomic_load(&bk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     rv[k] = i < d.n ? __hip_atomic_load(&br[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   }
-  // the staged indices of the device pods [dlo, e) (static: before the hand-off)
+  // The device pods [dlo, e) -- committed maybe after the pre-evaluation read
+  // their nodes -- have all committed before this final runs (the finals of a
+  // stream run in order; the wait covers KOORDHIP_EXT_ALT's second stream):
+  // their nodes' device rows and extended scalars are final until this pod's
+  // own Reserve, so the DeviceShare Filter / raw score and the extended-scalar
+  // Fit of those nodes are evaluated now, while the hand-off is pending
+  // (measured: ~12 us of dependent loads on the critical path otherwise)
   const int32_t gi = (t < e - dlo && t < EXT_DMAX) ? ext_idx[dlo + t] : -1;
+  if (t == 0) {
+    s_nre = 0u;
+    s_nd = e - dlo <= EXT_DMAX ? e - dlo : -1;  // (-1: too many, every re-evaluation in full)
+    s_cd = e == 0 || wait_gate(&fl[EXT_CDONE], e, sy);
+  }
+  __syncthreads();
+  if (!s_cd) return;  // the pipeline gave up
+  if (gi >= 0) s_dn[t] = __hip_atomic_load(&out_node[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (t < s_nd) {
+    const int32_t y = s_dn[t];
+    if (y >= c0 && y < c0 + EXT_FCHUNK && y < d.n) {
+      const DevPodX &x0 = podx[gp];
+      const bool xf = !(c.filt & KOORDHIP_PLUGIN_FIT) || xfit_filter(d.dv, x0, y, d.n);
+      int32_t raw0 = 0;
+      const bool df = dev_eval(c, d.dv, x0, y, false, (c.filt & KOORDHIP_PLUGIN_DEVICESHARE) != 0,
+                               (c.score & KOORDHIP_PLUGIN_DEVICESHARE) != 0, &raw0);
+      s_dok[t] = (xf && df) ? 1 : 0;
+      s_draw[t] = min(max(raw0, 0), EXT_RAW - 1);
+    }
+  }
   if (spin) {
     if (t == 0) {
       if (blockIdx.x == 0) {
@@ -897,15 +925,9 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
   static_assert(kPipeXMax <= EXT_THREADS, "one X node per thread");
   const int32_t nx = xl[0];
   const int32_t xv = t < kPipeXMax ? xl[1 + t] : -1;
-  const int32_t dn = gi >= 0 ? __hip_atomic_load(&out_node[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
   for (int r = t; r < EXT_RAW; r += EXT_THREADS) lt[r] = 0ull;
   for (int32_t w = t; w < EXT_FCHUNK / 32; w += EXT_THREADS) xm[w] = 0u;
-  if (t == 0) {
-    s_nre = 0u;
-    s_nd = e - dlo <= EXT_DMAX ? e - dlo : -1;  // (-1: too many, every re-evaluation in full)
-  }
   __syncthreads();
-  if (gi >= 0) s_dn[t] = dn;
   if (t < nx) {
     const int32_t y = xv - c0;
     if (y >= 0 && y < EXT_FCHUNK) atomicOr(&xm[y >> 5], 1u << (y & 31));
@@ -929,21 +951,27 @@ __global__ __launch_bounds__(EXT_THREADS) void k_ext_final(DevCfg c, DevNodes d,
     // its device rows and extended scalars (only device pods change them):
     // its DeviceShare Filter / raw score and extended-scalar Fit stand, and
     // only the row part -- seq_eval's eval_total over the Fit / LoadAware row,
-    // one row load -- is evaluated again.  The nodes of the device pods the
-    // pre-evaluation may have missed (s_dn) are evaluated in full.
+    // one row load -- is evaluated again; the nodes of the device pods the
+    // pre-evaluation may have missed (s_dn) take the part evaluated above.
     if (i < d.n && kv[k] != 0ull && ((xm[y >> 5] >> (y & 31)) & 1u)) {
-      bool full = s_nd < 0;
-      for (int32_t j = 0; j < s_nd; j++) full = full || s_dn[j] == i;
-      if (full) {
+      if (s_nd < 0) {
         s_fullw = 1;
         int32_t raw[KOORDHIP_NEXT_PLUGINS] = {0, 0, 0, 0, 0};
         const int32_t tk = seq_eval<SM, true>(c, d, p, x, i, false, raw, nullptr);
         kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
         rv[k] = min(max(raw[0], 0), EXT_RAW - 1);
       } else {
+        int32_t jd = -1;
+        for (int32_t j = 0; j < s_nd; j++)
+          if (s_dn[j] == i) jd = j;
         NV v{};
         load_node(v, d, i, need_all(c), c);
-        const int32_t tk = eval_total(p, v, c);
+        int32_t tk = eval_total(p, v, c);
+        if (jd >= 0) {
+          s_fullw = 1;
+          if (!s_dok[jd]) tk = -1;
+          rv[k] = s_draw[jd];
+        }
         kv[k] = tk >= 0 ? make_key(tk, i) : 0ull;
       }
       atomicAdd(&s_nre, 1u);
