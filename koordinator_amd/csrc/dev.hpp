@@ -273,7 +273,7 @@ __device__ __forceinline__ bool dev_reserve(const DevCfg &c, const DevDev &dv, c
   return any || !present || !nominated;
 }
 
-// WT: write-through stores (k_ext_worker: read next on other XCDs after a
+// WT: write-through stores (k_ext_final: read next on other XCDs after a
 // relaxed hand-off, no L2 write-back fence)
 template <bool WT = false>
 __device__ __forceinline__ void dev_apply(const DevDev &dv, int32_t i, const uint32_t slots[DT],

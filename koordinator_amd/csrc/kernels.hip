@@ -2254,7 +2254,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
           // not monotone), a walk longer than RES_WE entries
           const uint32_t fl = lpod[l].flags;
           bool slow = !monotone || dn < 0;
-          // a device pod: its node comes from k_ext_worker (general path)
+          // a device pod: its node comes from k_ext_final (general path)
           if constexpr (NM == 0) slow = slow || (fl & KH_POD_EXT) != 0u;
           if constexpr (NUMA) {
             // (with topology-policy nodes every NUMA pod: its zone hint can move
@@ -2683,7 +2683,7 @@ __global__ __launch_bounds__(res_threads<NM>()) void k_resolve(DevCfg c, const D
         // ---- general path: pod g alone -- c, then every M and M' row's current key
         n_slow++;
         const DevPod pod = lpod[g];  // VGPR copy: SGPRs are the scarce register file here (uniform_pod measured slower)
-        // A device pod (KH_POD_EXT, plain build): k_ext_worker places it on the
+        // A device pod (KH_POD_EXT, plain build): k_ext_final places it on the
         // exact state -- every commit so far written back first (M rows,
         // write-through, drained) and X exported, then the hand-off; its node (or
         // UNSCHEDULABLE / RESERVE_FAILED) comes back through out_node, and the

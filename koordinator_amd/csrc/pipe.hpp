@@ -21,15 +21,17 @@ static __device__ __forceinline__ uint64_t stamp() {
 //              after a separate merge)
 //   res_round  rounds resolved + written back (k_resolve, release store)
 //   err        a side gave up waiting (watchdog): the call fails, nothing hangs
-//   ext_req    device pods placed inside the pipeline (k_ext_worker, seq.hip):
+//   ext_req    device pods placed inside the pipeline (k_ext_final, seq.hip):
 //              the resolve stores pod index + 1 once every earlier commit is
 //              written back (write-through, drained)
-//   ext_done   the worker stores pod index + 1 once that pod's placement and
-//              its DeviceShare Reserve are published (out_node write-through)
+//   ext_done   k_ext_final stores pod index + 1 once that pod's placement is
+//              published (out_node write-through); its DeviceShare Reserve
+//              follows, published in the ext flags (cdone)
 // Every flag many waves poll has a 128-B line of its own: relaxed agent-scope
 // polls of one line from a few hundred workgroups serialise at its home and
-// delay every other waiter on it (the device-pod worker's idle workgroups
-// made a step 5x slower before ext_req / ext_done moved off sel / res_round).
+// delay every other waiter on it (round 5's persistent device-pod worker's
+// idle workgroups made a step 5x slower before ext_req / ext_done moved off
+// sel / res_round).
 struct PipeSync {
   int32_t sel[2], res_round, err;
   int32_t pad0[28];
@@ -89,7 +91,7 @@ static __device__ bool wait_at_least(const int32_t *p, int32_t v, PipeSync *sy) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   return true;
 }
-// The same for waiters off the critical path (the device-pod worker's idle
+// The same for waiters off the critical path (idle
 // workgroups): longer sleeps, the error word read every 16th poll.
 static __device__ bool wait_at_least_idle(const int32_t *p, int32_t v, PipeSync *sy) {
   const uint64_t t0 = stamp();

@@ -26,7 +26,7 @@ static_assert(sizeof(DevPod) == 96, "DevPod is 96 bytes");
 
 // Engine-internal flag bit (never from the host API: to_dev_pods rejects it):
 // a pod whose koordhip_pod_ext record requests devices / extended scalars,
-// placed inside the pipelined greedy by k_ext_worker (seq.hip) -- the resolve
+// placed inside the pipelined greedy by k_ext_pre / k_ext_final (seq.hip) -- the resolve
 // hands it the exact state and takes its node back.
 constexpr uint32_t KH_POD_EXT = 1u << 30;
 
