@@ -12,10 +12,11 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
 fi
 for w in ${WORKLOADS:-config4 config5 config3}; do
   for v in ${VARIANTS:-X=1}; do
+    tag=$(echo "$v" | tr '/' '_')
     env $v timeout -k 10 300 python bench.py --workload $w --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
-      > gpurun_out/iter_${w}_${v}.json 2> gpurun_out/iter_${w}_${v}.err
+      > gpurun_out/iter_${w}_${tag}.json 2> gpurun_out/iter_${w}_${tag}.err
     rc=$?
-    python3 - gpurun_out/iter_${w}_${v}.json "$w $v" <<'PY'
+    python3 - gpurun_out/iter_${w}_${tag}.json "$w $v" <<'PY'
 import json, sys
 try:
     d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
@@ -24,11 +25,11 @@ try:
 except Exception as e:
     print(sys.argv[2], "no result", e)
 PY
-    [ $rc -eq 0 ] || { tail -20 gpurun_out/iter_${w}_${v}.err; exit $rc; }
+    [ $rc -eq 0 ] || { tail -20 gpurun_out/iter_${w}_${tag}.err; exit $rc; }
     if [ "${STAMPS:-0}" = 1 ]; then
       env $v KOORDHIP_STAMPS=1 timeout -k 10 300 python bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline --no-latency ${BENCH_ARGS:-} \
-        > /dev/null 2> gpurun_out/iter_stamps_${w}_${v}.err || exit 1
-      grep "stamps\] \(resolve cycles\|round\|device\)" gpurun_out/iter_stamps_${w}_${v}.err | tail -4 | cut -c1-400
+        > /dev/null 2> gpurun_out/iter_stamps_${w}_${tag}.err || exit 1
+      grep "stamps\] \(resolve cycles\|round\|device\)" gpurun_out/iter_stamps_${w}_${tag}.err | tail -4 | cut -c1-400
     fi
   done
 done
