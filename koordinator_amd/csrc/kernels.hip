@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "eval.hpp"
+#include "karg.hpp"
 #include "kernels.h"
 #include "pipe.hpp"
 #include "rows.hpp"
@@ -1322,7 +1323,6 @@ struct EtkHdr {
   int32_t wsum[ETK_WAVES];            // block scans
   int32_t rmax[ETK_WAVES], rcnt[ETK_WAVES];
   int32_t cnt_gt, last, sel_b, sel_above;
-  int32_t rl_n;                       // the one-reservation build's deferred nodes (ETK_RCOMPACT)
 };
 constexpr int32_t ETK_HDR = (int32_t)((sizeof(EtkHdr) + 15) & ~(size_t)15);
 
@@ -1421,26 +1421,10 @@ __device__ __forceinline__ uint32_t etk_kth(F each, uint32_t top, int32_t nnz, i
 // (the evaluation phase is bound by the column loads' latency); the slice
 // selections then run pod after pod, and the workgroup merges every pod whose
 // last slice it was.
-// The evaluation reads ~50 column pointers of DevNodes and the DevCfg fields:
-// more wave-uniform values than a wave's 102 SGPRs, so the compiler parks them
-// in VGPR lanes and spends one v_readlane per use (42 % of the NM 3 loop's
-// VALU instructions).  kernarg_fresh returns the kernel argument at `off` of
-// the kernarg segment through a pointer the compiler cannot follow across the
-// asm, so every evaluation re-reads what it needs with scalar loads (the
-// scalar cache holds the segment) instead of keeping it live.
-// (k_eval_topk's arguments: DevCfg at 0, DevNodes right after it.)
+// (karg.hpp) k_eval_topk re-reads DevCfg / DevNodes per evaluation; 0: keep the by-value copies
 #ifndef ETK_KARG
 #define ETK_KARG 1
 #endif
-template <class T>
-__device__ __forceinline__ const T &kernarg_fresh(size_t off) {
-  const __attribute__((address_space(4))) char *k =
-      (const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(k));
-  return *(const T *)(k + off);
-}
-static_assert(sizeof(DevCfg) % alignof(DevNodes) == 0, "DevNodes follows DevCfg in the kernarg segment");
-constexpr size_t ETK_KARG_NODES = sizeof(DevCfg);
 
 // compile-time A/B knobs (make variant): the NUMA / Reservation builds' waves
 // per SIMD and evaluations in flight per thread
@@ -1449,15 +1433,6 @@ constexpr size_t ETK_KARG_NODES = sizeof(DevCfg);
 #endif
 #ifndef ETK_R3
 #define ETK_R3 4
-#endif
-// The one-reservation build (NM 3) evaluates the nodes holding no reservation
-// first, without the Reservation plugin's restore / filter / nomination (for
-// them eval_total_resv is the NUMA total plus the reservation-affinity check),
-// and parks the slice's reservation-holding nodes in an LDS list the workgroup
-// then evaluates densely: with ~10 % of the nodes holding one, nearly every
-// 64-node wave would otherwise run the Reservation branch.
-#ifndef ETK_RCOMPACT
-#define ETK_RCOMPACT 1
 #endif
 template <int NM, int VT, int R, int G>
 __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM == 5 ? 2 : (NM >= 3 ? ETK_WPE3 : 1)))) void k_eval_topk(
@@ -1506,14 +1481,6 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
     else need_or(need, pod_needs(gpod[g], c));
   }
   const int32_t c0 = lo + s * SL;
-  constexpr bool RCOMPACT = NM == 3 && ETK_RCOMPACT;
-  // (RCOMPACT) the deferred nodes' slice offsets, after the topology classes
-  uint16_t *rl = reinterpret_cast<uint16_t *>(
-      etk_lds + ETK_HDR + VBYTES + (d.nu.ncls <= NUMA_LDS_CLASSES ? d.nu.ncls * (int32_t)sizeof(DevNumaClass) : 0));
-  if constexpr (RCOMPACT) {
-    if (t == 0) h.rl_n = 0;
-    __syncthreads();
-  }
   // ---- evaluate: R nodes in flight per thread, each row evaluated for the G
   //      pods, values parked in LDS (pod g's at vals[g * SL ...])
   uint32_t vmax[G];
@@ -1530,24 +1497,10 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
       for (int g = 0; g < G; g++) sv[r][g] = 0u;
       if (i < hi) {
         const DevCfg &c = ETK_KARG ? kernarg_fresh<DevCfg>(0) : c_arg;
-        const DevNodes &d = ETK_KARG ? kernarg_fresh<DevNodes>(ETK_KARG_NODES) : d_arg;
+        const DevNodes &d = ETK_KARG ? kernarg_fresh<DevNodes>(KARG_NODES) : d_arg;
         NV v;
         load_node(v, d, i, need, c);
-        if constexpr (RCOMPACT) {
-          NumaRow nr;
-          load_numa<false>(nr, d, i, need);
-          const uint32_t rf = d.rv.slots > 0 ? d.rv.flags[i] : 0u;
-          if (rf & KOORDHIP_RESV_PRESENT) {
-            rl[atomicAdd(&h.rl_n, 1)] = (uint16_t)((q0 + r) * ETK_THREADS + t);
-          } else {
-            const bool aff = (c.filt & KOORDHIP_PLUGIN_RESERVATION) != 0;
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-              const int32_t x = eval_total_numa<false>(gpod[g], v, nr, cls, c);
-              sv[r][g] = (x >= 0 && aff && (gpod[g].flags & KOORDHIP_POD_RESV_AFFINITY)) ? 0u : (uint32_t)(x + 1);
-            }
-          }
-        } else if constexpr (NM >= 3) {
+        if constexpr (NM >= 3) {
           side_row_t<NM> nr;
           load_numa<false>(nr, d, i, need);
           load_resv(nr, d.rv, i);
@@ -1573,28 +1526,6 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
         vmax[g] = max(vmax[g], sv[r][g]);
         vnz[g] += sv[r][g] != 0u;
       }
-  }
-  if constexpr (RCOMPACT) {  // the deferred reservation-holding nodes, dense
-    __syncthreads();
-    const int32_t m = h.rl_n;
-#pragma unroll 1
-    for (int32_t j = t; j < m; j += ETK_THREADS) {
-      const int32_t o = rl[j], i = c0 + o;
-      const DevCfg &c = ETK_KARG ? kernarg_fresh<DevCfg>(0) : c_arg;
-      const DevNodes &d = ETK_KARG ? kernarg_fresh<DevNodes>(ETK_KARG_NODES) : d_arg;
-      NV v;
-      load_node(v, d, i, need, c);
-      side_row_t<NM> nr;
-      load_numa<false>(nr, d, i, need);
-      load_resv(nr, d.rv, i);
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        const uint32_t x = (uint32_t)(eval_total_resv<side_row_t<NM>::kSlots, false>(gpod[g], v, nr, cls, c) + 1);
-        vals[g * SL + o] = x;
-        vmax[g] = max(vmax[g], x);
-        vnz[g] += x != 0u;
-      }
-    }
   }
   uint32_t lastmask = 0;  // (thread 0) pods whose last slice this workgroup is
 #pragma unroll 1
@@ -3655,8 +3586,7 @@ hipError_t launch_eval_topk(const DevCfg &c, const DevNodes &d, const DevPod *po
   const int32_t stage_cap = (int32_t)std::min<int64_t>((int64_t)nslices * k, ETK_MERGE_KEYS);
   const size_t vbytes = (size_t)std::max<int32_t>(G * sl * 4, stage_cap * 8);
   const size_t lds = (size_t)ETK_HDR + vbytes +
-                     ((nm != 0 && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0) +
-                     ((nm == 3 && ETK_RCOMPACT) ? (size_t)sl * 2 : 0);  // the deferred-node list
+                     ((nm != 0 && d.nu.ncls <= NUMA_LDS_CLASSES) ? (size_t)d.nu.ncls * sizeof(DevNumaClass) : 0);
   const int32_t spx = (nslices + 7) / 8;
   const int32_t blocks = 8 * spx * ((n_pods + G - 1) / G);
   static bool attr[6][3][5] = {};
