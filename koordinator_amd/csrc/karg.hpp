@@ -10,6 +10,11 @@
 // scalar cache holds the segment) instead of keeping it live.  Offsets follow
 // the kernel's explicit argument order (each argument at its natural
 // alignment; DevCfg first and DevNodes right after it, asserted below).
+// Call it in wave-uniform control flow only: inside a divergent branch (a
+// per-lane node guard) the multi-slot Reservation builds read wrong values
+// (test_reservation_slots' streams), outside it they are bit-exact.  The
+// pod record stays in SGPRs: re-reading it per evaluation put its scalar
+// loads on every evaluation's critical path (config 5 230k -> 168k pods/s).
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -1489,6 +1489,9 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
   for (int g = 0; g < G; g++) vmax[g] = 0u, vnz[g] = 0;
 #pragma unroll 1
   for (int q0 = 0; q0 < VT; q0 += R) {
+    // (karg.hpp) re-read per R evaluations, outside the divergent node guard
+    const DevCfg &cq = ETK_KARG ? kernarg_fresh<DevCfg>(0) : c_arg;
+    const DevNodes &dq = ETK_KARG ? kernarg_fresh<DevNodes>(KARG_NODES) : d_arg;
     uint32_t sv[R][G];
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -1496,8 +1499,8 @@ __global__ __launch_bounds__(ETK_THREADS) __attribute__((amdgpu_waves_per_eu(NM 
 #pragma unroll
       for (int g = 0; g < G; g++) sv[r][g] = 0u;
       if (i < hi) {
-        const DevCfg &c = ETK_KARG ? kernarg_fresh<DevCfg>(0) : c_arg;
-        const DevNodes &d = ETK_KARG ? kernarg_fresh<DevNodes>(KARG_NODES) : d_arg;
+        const DevCfg &c = cq;
+        const DevNodes &d = dq;
         NV v;
         load_node(v, d, i, need, c);
         if constexpr (NM >= 3) {
